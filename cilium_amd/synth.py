@@ -1,0 +1,324 @@
+"""Synthetic tables and header streams for the BASELINE.json configurations.
+
+The reference has no traffic generator for the verdict path; SURVEY.md §8d
+defines the workloads (C1..C5).  Everything here is plain numpy and seeded,
+so the golden-vector script (oracle/gen_golden.py), the parity tests and
+bench.py all see byte-identical inputs for a given seed.
+
+Byte conventions follow the reference datapath:
+  * IPv4 addresses are `__be32` as the BPF program loads them: the four
+    network-order bytes read as a little-endian u32 (so 10.0.0.1 -> 0x0100000a).
+  * Ports are `__be16` raw (network-order bytes read little-endian), the form
+    stored in PolicyKey.DestPort (pkg/maps/policymap/policymap.go:64-69).
+  * For ICMP the "sport" word carries the first two ICMP bytes (type, code),
+    "dport" the checksum — exactly what ct_lookup4 reads
+    (bpf/lib/conntrack.h:496-526).
+"""
+from __future__ import annotations
+
+import dataclasses
+import numpy as np
+
+# reserved identities, bpf/node_config.h
+HOST_ID, WORLD_ID, CLUSTER_ID, HEALTH_ID, INIT_ID = 1, 2, 3, 4, 5
+# header flag bits (cfc.h CFC_HF_*)
+HF_FRAG = 1          # ipv4_is_fragment(): frag_off & htons(0xBFFF)
+HF_TCP_CLOSE = 2     # TCP RST or FIN set (conntrack.h:533)
+IPPROTO_ICMP, IPPROTO_TCP, IPPROTO_UDP, IPPROTO_ICMPV6 = 1, 6, 17, 58
+
+IPCACHE_DT = np.dtype([("family", "u1"), ("plen", "u1"), ("addr", "u1", 16),
+                       ("label", "<u4"), ("tunnel", "<u4")])
+ENDPOINT_DT = np.dtype([("family", "u1"), ("addr", "u1", 16),
+                        ("ifindex", "<u4"), ("lxc_id", "<u2"),
+                        ("flags", "<u4")])
+POLICY_DT = np.dtype([("identity", "<u4"), ("dport", "<u2"), ("proto", "u1"),
+                      ("egress", "u1"), ("proxy_port", "<u2")])
+PREFILTER_DT = np.dtype([("family", "u1"), ("plen", "u1"),
+                         ("addr", "u1", 16), ("dyn", "u1")])
+
+
+def htons(x):
+    x = np.asarray(x, dtype=np.uint32)
+    return (((x & 0xFF) << 8) | ((x >> 8) & 0xFF)).astype(np.uint16)
+
+
+def ntohs(x):
+    return htons(x)
+
+
+def ip4(s: str) -> int:
+    """'10.0.0.1' -> be32 raw (little-endian load of network bytes)."""
+    b = bytes(int(p) for p in s.split("."))
+    return int.from_bytes(b, "little")
+
+
+def be32_to_bytes(a: np.ndarray) -> np.ndarray:
+    return np.ascontiguousarray(a.astype("<u4")).view(np.uint8).reshape(-1, 4)
+
+
+def mask_be32(plen: np.ndarray) -> np.ndarray:
+    """Network-order prefix mask as a be32-raw u32 (GET_PREFIX, ipv6.h:136)."""
+    plen = np.asarray(plen, dtype=np.uint64)
+    host = np.where(plen == 0, 0, (0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF)
+    return byteswap32(host.astype(np.uint32))
+
+
+def byteswap32(x):
+    x = np.asarray(x, dtype=np.uint32)
+    return (((x & 0xFF) << 24) | ((x & 0xFF00) << 8) | ((x >> 8) & 0xFF00)
+            | (x >> 24)).astype(np.uint32)
+
+
+@dataclasses.dataclass
+class Tables:
+    ipcache: np.ndarray                      # IPCACHE_DT
+    endpoints: np.ndarray                    # ENDPOINT_DT
+    policy: dict                             # lxc_id -> POLICY_DT array
+    prefilter: np.ndarray                    # PREFILTER_DT
+    seclabel: dict                           # lxc_id -> u32 (endpoint SECLABEL)
+
+
+@dataclasses.dataclass
+class Headers:
+    family: int                              # 4 or 6 (whole batch)
+    saddr: np.ndarray                        # v4: (n,) <u4 be32 raw; v6: (n,16) u8
+    daddr: np.ndarray
+    sport: np.ndarray                        # (n,) <u2 be16 raw
+    dport: np.ndarray
+    proto: np.ndarray                        # (n,) u1
+    flags: np.ndarray                        # (n,) u1 HF_*
+    length: np.ndarray                       # (n,) <u2 skb->len
+    mark: np.ndarray                         # (n,) <u4 skb->mark
+
+    def __len__(self):
+        return len(self.proto)
+
+    def slice(self, a, b):
+        return Headers(self.family, self.saddr[a:b], self.daddr[a:b],
+                       self.sport[a:b], self.dport[a:b], self.proto[a:b],
+                       self.flags[a:b], self.length[a:b], self.mark[a:b])
+
+
+def _v4_entries(addr_be32, plen, label):
+    n = len(addr_be32)
+    e = np.zeros(n, IPCACHE_DT)
+    e["family"] = 1
+    e["plen"] = plen
+    e["addr"][:, :4] = be32_to_bytes(addr_be32)
+    e["label"] = label
+    return e
+
+
+def gen_ipcache_v4(rng, n, label_base=256, label_mod=16384,
+                   lengths=((8, .01), (12, .02), (16, .07), (20, .10),
+                            (24, .40), (28, .10), (32, .30))):
+    """C2 ipcache: n unique IPv4 prefixes, length mix of SURVEY.md §8d."""
+    ls = np.array([l for l, _ in lengths])
+    ps = np.array([p for _, p in lengths], dtype=np.float64)
+    ps /= ps.sum()
+    out_a, out_l = [], []
+    seen = set()
+    need = n
+    while need > 0:
+        m = int(need * 1.3) + 16
+        plen = rng.choice(ls, size=m, p=ps).astype(np.uint32)
+        host = rng.integers(0, 1 << 32, size=m, dtype=np.uint64).astype(np.uint32)
+        # keep away from 64.48.32.16 (LXC_IPV4) /8 and the 10/8 endpoint space
+        top = host >> 24
+        ok = (top != 10) & (top != 64) & (top != 0) & (top < 224)
+        plen, host = plen[ok], host[ok]
+        hmask = np.where(plen == 0, 0,
+                         (np.uint64(0xFFFFFFFF) << (32 - plen.astype(np.uint64)))
+                         & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+        host &= hmask
+        for h, l in zip(host.tolist(), plen.tolist()):
+            if (h, l) in seen:
+                continue
+            seen.add((h, l))
+            out_a.append(h)
+            out_l.append(l)
+            need -= 1
+            if need == 0:
+                break
+    host = np.array(out_a, dtype=np.uint32)
+    plen = np.array(out_l, dtype=np.uint8)
+    label = (label_base + (np.arange(n) % label_mod)).astype(np.uint32)
+    return _v4_entries(byteswap32(host), plen, label)
+
+
+def endpoint_v4(addr_be32, ifindex, lxc_id, flags=0):
+    e = np.zeros(1, ENDPOINT_DT)
+    e["family"] = 1
+    e["addr"][0, :4] = be32_to_bytes(np.array([addr_be32], np.uint32))[0]
+    e["ifindex"] = ifindex
+    e["lxc_id"] = lxc_id
+    e["flags"] = flags
+    return e
+
+
+PORT_SET = np.array([22, 25, 53, 80, 110, 123, 143, 389, 443, 445, 465, 587,
+                     636, 853, 993, 995, 1433, 1521, 2049, 2379, 3000, 3306,
+                     5000, 5432, 5672, 6379, 6443, 8000, 8080, 8443, 9090,
+                     9200], dtype=np.uint32)
+PROXY_PORTS = np.array([10001, 10002, 10003, 10004], dtype=np.uint32)
+
+
+def gen_policy(rng, n, identities, ports=PORT_SET, l3_frac=0.5,
+               wildcard=8, proxy_frac=0.05, both_dirs=True):
+    """C2 policymap: n unique keys (half L3 {id,0,0,dir}, half L4
+    {id,port,proto,dir}), a few wildcard-port keys {0,port,proto,dir} and
+    some proxy redirects."""
+    keys = set()
+    rows = []
+    identities = np.asarray(identities, dtype=np.uint32)
+    # wildcard-port entries first (policy.h:85-96 fallback)
+    for _ in range(wildcard):
+        p = int(rng.choice(ports))
+        pr = int(rng.choice([IPPROTO_TCP, IPPROTO_UDP]))
+        d = int(rng.integers(0, 2)) if both_dirs else 0
+        k = (0, int(htons(p)), pr, d)
+        if k not in keys:
+            keys.add(k)
+            rows.append(k + (0,))
+    while len(rows) < n:
+        ident = int(rng.choice(identities))
+        d = int(rng.integers(0, 2)) if both_dirs else 0
+        if rng.random() < l3_frac:
+            k = (ident, 0, 0, d)
+        else:
+            p = int(rng.choice(ports))
+            pr = IPPROTO_TCP if rng.random() < 0.75 else IPPROTO_UDP
+            k = (ident, int(htons(p)), pr, d)
+        if k in keys:
+            continue
+        keys.add(k)
+        proxy = 0
+        if k[1] != 0 and rng.random() < proxy_frac:
+            proxy = int(htons(int(rng.choice(PROXY_PORTS))))
+        rows.append(k + (proxy,))
+    out = np.zeros(len(rows), POLICY_DT)
+    a = np.array(rows, dtype=np.int64)
+    out["identity"], out["dport"], out["proto"] = a[:, 0], a[:, 1], a[:, 2]
+    out["egress"], out["proxy_port"] = a[:, 3], a[:, 4]
+    return out
+
+
+def _addr_in_prefix_v4(rng, ipc, idx):
+    """Random address inside prefix idx (be32 raw)."""
+    base = byteswap32(ipc["addr"][idx, :4].copy().view("<u4").ravel())
+    plen = ipc["plen"][idx].astype(np.uint64)
+    hostbits = (rng.integers(0, 1 << 32, size=len(idx), dtype=np.uint64)
+                & ((np.uint64(1) << (np.uint64(32) - plen)) - np.uint64(1)))
+    return byteswap32((base.astype(np.uint64) | hostbits).astype(np.uint32))
+
+
+def gen_headers_v4(rng, n, ipc, dst_addrs, in_prefix=0.9, local_frac=0.97,
+                   ports=PORT_SET, frag=0.01, mark_host=0.03, mark_proxy=0.02,
+                   other_proto=0.005, proxy_ident=None, src_fixed=None):
+    """IPv4 header batch.  src: `in_prefix` inside a random ipcache prefix,
+    rest uniform (WORLD); dst: a local endpoint with prob `local_frac`."""
+    if src_fixed is not None:
+        saddr = np.full(n, src_fixed, np.uint32)
+    else:
+        pick = rng.integers(0, len(ipc), size=n)
+        saddr = _addr_in_prefix_v4(rng, ipc, pick)
+        uni = rng.random(n) >= in_prefix
+        saddr[uni] = rng.integers(0, 1 << 32, size=int(uni.sum()),
+                                  dtype=np.uint64).astype(np.uint32)
+    dst_addrs = np.asarray(dst_addrs, dtype=np.uint32)
+    daddr = dst_addrs[rng.integers(0, len(dst_addrs), size=n)]
+    nonlocal_ = rng.random(n) >= local_frac
+    daddr[nonlocal_] = rng.integers(0, 1 << 32, size=int(nonlocal_.sum()),
+                                    dtype=np.uint64).astype(np.uint32)
+    r = rng.random(n)
+    proto = np.where(r < 0.70, IPPROTO_TCP,
+                     np.where(r < 0.95, IPPROTO_UDP, IPPROTO_ICMP)).astype(np.uint8)
+    oth = rng.random(n) < other_proto
+    proto[oth] = rng.choice(np.array([47, 132, 50], np.uint8), size=int(oth.sum()))
+    # ports: 60% from the policy port set, 40% uniform
+    dp = np.where(rng.random(n) < 0.6, rng.choice(ports, size=n),
+                  rng.integers(1, 65536, size=n)).astype(np.uint32)
+    sp = rng.integers(32768, 65536, size=n).astype(np.uint32)
+    sport, dport = htons(sp), htons(dp)
+    icmp = proto == IPPROTO_ICMP
+    itype = rng.choice(np.array([0, 8, 8, 8, 3, 11, 13], np.uint32),
+                       size=int(icmp.sum()))
+    sport[icmp] = itype.astype(np.uint16)          # bytes [type, code=0]
+    dport[icmp] = rng.integers(0, 65536, size=int(icmp.sum())).astype(np.uint16)
+    flags = np.zeros(n, np.uint8)
+    flags[rng.random(n) < frag] |= HF_FRAG
+    tcp = proto == IPPROTO_TCP
+    flags[tcp & (rng.random(n) < 0.02)] |= HF_TCP_CLOSE
+    minlen = np.where(proto == IPPROTO_TCP, 54,
+                      np.where(proto == IPPROTO_UDP, 42, 42)).astype(np.uint32)
+    length = np.maximum(rng.integers(60, 1501, size=n), minlen).astype(np.uint16)
+    mark = np.zeros(n, np.uint32)
+    rm = rng.random(n)
+    mark[rm < mark_host] = 0xC00                              # MARK_MAGIC_HOST
+    if proxy_ident is not None and len(proxy_ident):
+        sel = (rm >= mark_host) & (rm < mark_host + mark_proxy)
+        ids = rng.choice(np.asarray(proxy_ident, np.uint32), size=int(sel.sum()))
+        magic = np.where(rng.random(int(sel.sum())) < 0.5, 0xA00, 0xB00)
+        # identity = ((mark & 0xFF) << 16) | mark >> 16  (common.h get_identity_via_proxy)
+        mark[sel] = ((ids & 0xFFFF) << 16) | ((ids >> 16) & 0xFF) | magic
+    return Headers(4, saddr, daddr, sport, dport, proto, flags, length, mark)
+
+
+def ensure_no_reverse(h: Headers):
+    """Drop headers whose reverse 5-tuple appeared earlier (CT_REPLY would
+    change the verdict: SURVEY.md §8c 'Streams must avoid intra-batch
+    reverse packets').  Returns a boolean keep-mask."""
+    fwd = {}
+    keep = np.ones(len(h), bool)
+    s, d = h.saddr.tolist(), h.daddr.tolist()
+    sp, dp, pr = h.sport.tolist(), h.dport.tolist(), h.proto.tolist()
+    for i in range(len(h)):
+        if (d[i], s[i], dp[i], sp[i], pr[i]) in fwd:
+            keep[i] = False
+            continue
+        fwd[(s[i], d[i], sp[i], dp[i], pr[i])] = 1
+    return keep
+
+
+# ---------------------------------------------------------------- configs
+LXC_IPV4 = ip4("64.48.32.16")       # bpf/lxc_config.h LXC_IPV4 0x10203040
+EP_LXC_ID = 0x1010                  # bpf/lxc_config.h LXC_ID
+EP_SECLABEL = 2                     # bpf/node_config.h SECLABEL
+
+
+def config_c2(seed=2, n_prefixes=100_000, n_policy=16384, n_endpoints=1):
+    """C2 tables: 100k IPv4 prefixes + 16k-entry policymap for one endpoint
+    (SURVEY.md §8d).  Endpoint 0 is the reference's own LXC (64.48.32.16,
+    LXC_ID 0x1010); a host endpoint (ENDPOINT_F_HOST) is added too."""
+    rng = np.random.default_rng(seed)
+    ipc = gen_ipcache_v4(rng, n_prefixes)
+    eps = [endpoint_v4(LXC_IPV4, 100, EP_LXC_ID)]
+    for i in range(1, n_endpoints):
+        eps.append(endpoint_v4(ip4(f"10.1.{i >> 8}.{i & 255}"), 100 + i,
+                               EP_LXC_ID + i))
+    eps.append(endpoint_v4(ip4("10.0.255.254"), 0, 0xFFF0, flags=1))  # host
+    eps = np.concatenate(eps)
+    idents = np.unique(ipc["label"])
+    pol = {}
+    for e in eps:
+        if e["flags"] & 1:
+            continue
+        pol[int(e["lxc_id"])] = gen_policy(rng, n_policy, idents)
+    pf = np.zeros(0, PREFILTER_DT)
+    seclabel = {int(e["lxc_id"]): EP_SECLABEL for e in eps}
+    return Tables(ipc, eps, pol, pf, seclabel)
+
+
+def local_v4_addrs(t: Tables):
+    e = t.endpoints[t.endpoints["family"] == 1]
+    return e["addr"][:, :4].copy().view("<u4").ravel()
+
+
+def proxy_identities(t: Tables):
+    return np.unique(t.ipcache["label"])[:64]
+
+
+def headers_c2(t: Tables, n, seed=2, **kw):
+    rng = np.random.default_rng(seed + 1000)
+    return gen_headers_v4(rng, n, t.ipcache, local_v4_addrs(t),
+                          proxy_ident=proxy_identities(t), **kw)

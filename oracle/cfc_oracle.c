@@ -1,0 +1,688 @@
+/*
+ * cfc_oracle.c — CPU restatement of the reference verdict path.
+ * TEST INFRASTRUCTURE ONLY (see cfc_oracle.h).
+ *
+ * Tables are kept the simple way: exact-match hash tables, and longest-prefix
+ * match done as one hash table per prefix length probed from the longest
+ * present length down — the same scheme as the reference's hashed-prefix
+ * fallback LPM_LOOKUP_FN (bpf/lib/eps.h:88-108).  The kernel LPM trie the
+ * reference uses (kernel/bpf/lpm_trie.c) returns the same longest match.
+ */
+#define _GNU_SOURCE
+#include "cfc_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* bpf/node_config.h */
+#define HOST_ID 1u
+#define WORLD_ID 2u
+#define CLUSTER_ID 3u
+#define HEALTH_ID 4u
+#define IPV4_CLUSTER_MASK 0xff0000u
+#define IPV4_CLUSTER_RANGE 0x100000u
+/* bpf/lib/common.h:237-269 */
+#define DROP_INVALID_SIP -132
+#define DROP_POLICY -133
+#define DROP_CT_UNKNOWN_PROTO -137
+#define DROP_FRAG_NOSUPPORT -157
+/* UAPI */
+#define TC_ACT_OK 0
+#define TC_ACT_SHOT 2
+#define TC_ACT_REDIRECT 7
+#define XDP_DROP 1
+#define XDP_PASS 2
+#define METRIC_INGRESS 1
+#define METRIC_EGRESS 2
+#define CT_EGRESS 0
+#define CT_INGRESS 1
+#define HF_FRAG 1
+#define ENDPOINT_F_HOST 1u
+#define MARK_MAGIC_HOST_MASK 0xF00u
+#define MARK_MAGIC_PROXY_INGRESS 0xA00u
+#define MARK_MAGIC_PROXY_EGRESS 0xB00u
+#define MARK_MAGIC_HOST 0xC00u
+
+/* ------------------------------------------------------------ hash table */
+typedef struct {
+    uint32_t ksz, cap, n;
+    uint8_t *keys;
+    uint32_t *vals;
+    uint8_t *used;
+} htab;
+
+static uint64_t hbytes(const uint8_t *k, uint32_t n)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t i = 0; i < n; i++) {
+        h ^= k[i];
+        h *= 1099511628211ull;
+    }
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    return h;
+}
+
+static void ht_init(htab *h, uint32_t ksz)
+{
+    memset(h, 0, sizeof(*h));
+    h->ksz = ksz;
+}
+
+static void ht_free(htab *h)
+{
+    free(h->keys);
+    free(h->vals);
+    free(h->used);
+    memset(h, 0, sizeof(*h));
+}
+
+static void ht_put(htab *h, const uint8_t *k, uint32_t v);
+
+static void ht_grow(htab *h)
+{
+    htab o = *h;
+    h->cap = o.cap ? o.cap * 2 : 64;
+    h->n = 0;
+    h->keys = calloc((size_t)h->cap, h->ksz);
+    h->vals = calloc((size_t)h->cap, sizeof(uint32_t));
+    h->used = calloc((size_t)h->cap, 1);
+    for (uint32_t i = 0; i < o.cap; i++)
+        if (o.used[i])
+            ht_put(h, o.keys + (size_t)i * o.ksz, o.vals[i]);
+    free(o.keys);
+    free(o.vals);
+    free(o.used);
+}
+
+static int64_t ht_find(const htab *h, const uint8_t *k)
+{
+    if (!h->cap)
+        return -1;
+    uint32_t m = h->cap - 1, i = (uint32_t)hbytes(k, h->ksz) & m;
+    while (h->used[i]) {
+        if (!memcmp(h->keys + (size_t)i * h->ksz, k, h->ksz))
+            return i;
+        i = (i + 1) & m;
+    }
+    return -1;
+}
+
+static void ht_put(htab *h, const uint8_t *k, uint32_t v)
+{
+    int64_t s = ht_find(h, k);
+    if (s >= 0) {
+        h->vals[s] = v;
+        return;
+    }
+    if ((h->n + 1) * 2 > h->cap)
+        ht_grow(h);
+    uint32_t m = h->cap - 1, i = (uint32_t)hbytes(k, h->ksz) & m;
+    while (h->used[i])
+        i = (i + 1) & m;
+    h->used[i] = 1;
+    memcpy(h->keys + (size_t)i * h->ksz, k, h->ksz);
+    h->vals[i] = v;
+    h->n++;
+}
+
+static int ht_get(const htab *h, const uint8_t *k, uint32_t *v)
+{
+    int64_t s = ht_find(h, k);
+    if (s < 0)
+        return 0;
+    *v = h->vals[s];
+    return 1;
+}
+
+/* ------------------------------------------------------------ LPM */
+typedef struct {
+    int alen;            /* address bytes: 4 or 16 */
+    htab len[129];
+    int lens[129];       /* present prefix lengths, descending */
+    int nlens;
+} lpm;
+
+static void lpm_init(lpm *l, int alen)
+{
+    memset(l, 0, sizeof(*l));
+    l->alen = alen;
+    for (int i = 0; i <= alen * 8; i++)
+        ht_init(&l->len[i], (uint32_t)alen);
+}
+
+static void lpm_free(lpm *l)
+{
+    for (int i = 0; i <= l->alen * 8; i++)
+        ht_free(&l->len[i]);
+}
+
+/* ipv6_addr_clear_suffix / GET_PREFIX (bpf/lib/ipv6.h:136-150) */
+static void mask_addr(uint8_t *out, const uint8_t *a, int alen, int plen)
+{
+    for (int i = 0; i < alen; i++) {
+        int b = plen - 8 * i;
+        uint8_t m = b >= 8 ? 0xFF : b <= 0 ? 0 : (uint8_t)(0xFF << (8 - b));
+        out[i] = a[i] & m;
+    }
+}
+
+static void lpm_add(lpm *l, int plen, const uint8_t *addr, uint32_t val)
+{
+    uint8_t k[16];
+    mask_addr(k, addr, l->alen, plen);
+    if (!l->len[plen].n) {
+        int i = l->nlens++;
+        while (i > 0 && l->lens[i - 1] < plen) {
+            l->lens[i] = l->lens[i - 1];
+            i--;
+        }
+        l->lens[i] = plen;
+    }
+    ht_put(&l->len[plen], k, val);
+}
+
+static int lpm_lookup(const lpm *l, const uint8_t *addr, uint32_t *val)
+{
+    uint8_t k[16];
+    for (int i = 0; i < l->nlens; i++) {
+        int p = l->lens[i];
+        mask_addr(k, addr, l->alen, p);
+        if (ht_get(&l->len[p], k, val))
+            return 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------ tables */
+typedef struct {
+    uint8_t key[8];      /* struct policy_key (common.h:180-186) raw bytes */
+    uint16_t proxy_port; /* struct policy_entry.proxy_port, be16 raw */
+    uint64_t packets, bytes;
+} pentry;
+
+typedef struct {
+    htab idx;            /* key -> index into ents */
+    pentry *ents;
+    uint32_t n, cap;
+} pmap;
+
+typedef struct {
+    uint32_t ifindex, flags;
+    uint16_t lxc_id;
+} epinfo;
+
+struct cfo {
+    lpm ipc4, ipc6;
+    htab lxc;            /* 20-byte endpoint_key -> index into eps */
+    epinfo *eps;
+    uint32_t neps, capeps;
+    pmap *pol[65536];
+    uint32_t seclabel[65536];
+    uint8_t has_seclabel[65536];
+    htab pf4_fix, pf6_fix; /* lpm_v{4,6}_key bytes (prefixlen + addr) */
+    lpm pf4_dyn, pf6_dyn;
+    uint64_t metrics[256][4][2];
+};
+
+cfo_t *cfo_new(void)
+{
+    cfo_t *o = calloc(1, sizeof(*o));
+    lpm_init(&o->ipc4, 4);
+    lpm_init(&o->ipc6, 16);
+    lpm_init(&o->pf4_dyn, 4);
+    lpm_init(&o->pf6_dyn, 16);
+    ht_init(&o->lxc, 20);
+    ht_init(&o->pf4_fix, 8);
+    ht_init(&o->pf6_fix, 20);
+    return o;
+}
+
+void cfo_free(cfo_t *o)
+{
+    if (!o)
+        return;
+    lpm_free(&o->ipc4);
+    lpm_free(&o->ipc6);
+    lpm_free(&o->pf4_dyn);
+    lpm_free(&o->pf6_dyn);
+    ht_free(&o->lxc);
+    ht_free(&o->pf4_fix);
+    ht_free(&o->pf6_fix);
+    for (int i = 0; i < 65536; i++)
+        if (o->pol[i]) {
+            ht_free(&o->pol[i]->idx);
+            free(o->pol[i]->ents);
+            free(o->pol[i]);
+        }
+    free(o->eps);
+    free(o);
+}
+
+int cfo_ipcache_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
+                    uint32_t label)
+{
+    if (family == 1 && plen >= 0 && plen <= 32)
+        lpm_add(&o->ipc4, plen, addr, label);
+    else if (family == 2 && plen >= 0 && plen <= 128)
+        lpm_add(&o->ipc6, plen, addr, label);
+    else
+        return -22;
+    return 0;
+}
+
+static void ep_key(uint8_t k[20], int family, const uint8_t *addr)
+{
+    memset(k, 0, 20);
+    memcpy(k, addr, family == 1 ? 4 : 16);
+    k[16] = (uint8_t)family;
+}
+
+int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
+                     uint32_t ifindex, uint16_t lxc_id, uint32_t flags)
+{
+    uint8_t k[20];
+    ep_key(k, family, addr);
+    if (o->neps == o->capeps) {
+        o->capeps = o->capeps ? o->capeps * 2 : 16;
+        o->eps = realloc(o->eps, o->capeps * sizeof(epinfo));
+    }
+    o->eps[o->neps] = (epinfo){ifindex, flags, lxc_id};
+    ht_put(&o->lxc, k, o->neps++);
+    return 0;
+}
+
+int cfo_seclabel_set(cfo_t *o, uint16_t lxc_id, uint32_t seclabel)
+{
+    o->seclabel[lxc_id] = seclabel;
+    o->has_seclabel[lxc_id] = 1;
+    return 0;
+}
+
+static void pkey(uint8_t k[8], uint32_t id, uint16_t dport, uint8_t proto,
+                 uint8_t egress)
+{
+    memcpy(k, &id, 4);
+    memcpy(k + 4, &dport, 2);
+    k[6] = proto;
+    k[7] = egress;
+}
+
+int cfo_policy_add(cfo_t *o, uint16_t lxc_id, uint32_t identity,
+                   uint16_t dport_be, uint8_t proto, uint8_t egress,
+                   uint16_t proxy_port_be)
+{
+    pmap *m = o->pol[lxc_id];
+    if (!m) {
+        m = o->pol[lxc_id] = calloc(1, sizeof(pmap));
+        ht_init(&m->idx, 8);
+    }
+    uint8_t k[8];
+    pkey(k, identity, dport_be, proto, egress);
+    uint32_t i;
+    if (!ht_get(&m->idx, k, &i)) {
+        if (m->n == m->cap) {
+            m->cap = m->cap ? m->cap * 2 : 64;
+            m->ents = realloc(m->ents, m->cap * sizeof(pentry));
+        }
+        i = m->n++;
+        ht_put(&m->idx, k, i);
+    }
+    memcpy(m->ents[i].key, k, 8);
+    m->ents[i].proxy_port = proxy_port_be;
+    m->ents[i].packets = m->ents[i].bytes = 0;
+    return 0;
+}
+
+int cfo_prefilter_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
+                      int dyn)
+{
+    int alen = family == 1 ? 4 : 16;
+    if (dyn) {
+        lpm_add(family == 1 ? &o->pf4_dyn : &o->pf6_dyn, plen, addr, 1);
+    } else {
+        uint8_t k[20];
+        uint32_t pl = (uint32_t)plen;
+        memcpy(k, &pl, 4);
+        memcpy(k + 4, addr, alen);
+        ht_put(family == 1 ? &o->pf4_fix : &o->pf6_fix, k, 1);
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------ datapath */
+static inline void add64(uint64_t *p, uint64_t v)
+{
+    __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+}
+
+/* update_metrics (bpf/lib/metrics.h:43-61); reason = -DROP_* or 0 */
+static void metric(cfo_t *o, int reason, int dir, uint32_t len)
+{
+    uint8_t r = (uint8_t)(-reason);
+    add64(&o->metrics[r][dir][0], 1);
+    add64(&o->metrics[r][dir][1], len);
+}
+
+static const epinfo *lxc_lookup(const cfo_t *o, int family,
+                                const uint8_t *addr)
+{
+    uint8_t k[20];
+    uint32_t i;
+    ep_key(k, family, addr);
+    return ht_get(&o->lxc, k, &i) ? &o->eps[i] : NULL;
+}
+
+static pentry *pol_lookup(pmap *m, uint32_t id, uint16_t dport, uint8_t proto,
+                          uint8_t egress)
+{
+    if (!m)
+        return NULL;
+    uint8_t k[8];
+    uint32_t i;
+    pkey(k, id, dport, proto, egress);
+    return ht_get(&m->idx, k, &i) ? &m->ents[i] : NULL;
+}
+
+static void hit(pentry *e, uint32_t len)
+{
+    add64(&e->packets, 1);
+    add64(&e->bytes, len);
+}
+
+/* __policy_can_access (bpf/lib/policy.h:46-110).  cb[CB_POLICY] is always 0
+ * here: policy_clear_mark() runs first on every path we model
+ * (bpf_lxc.c:916, :626). */
+static int policy_can_access(pmap *m, uint32_t identity, uint16_t dport,
+                             uint8_t proto, int dir, int frag, uint32_t len)
+{
+    uint8_t egress = !dir;
+    pentry *e;
+    if (!frag) {
+        e = pol_lookup(m, identity, dport, proto, egress);
+        if (e) {
+            hit(e, len);
+            return e->proxy_port;
+        }
+    }
+    e = pol_lookup(m, identity, 0, 0, egress);
+    if (e) {
+        hit(e, len);
+        return TC_ACT_OK;
+    }
+    if (!frag) {
+        e = pol_lookup(m, 0, dport, proto, egress);
+        if (e) {
+            hit(e, len);
+            return e->proxy_port;
+        }
+    }
+    return frag ? DROP_FRAG_NOSUPPORT : DROP_POLICY;
+}
+
+/* Policy port of a CT_NEW packet as ct_lookup4 leaves tuple->dport
+ * (bpf/lib/conntrack.h:496-584): TCP/UDP ports are loaded swapped, the
+ * reverse lookup misses, ipv4_ct_tuple_reverse() swaps them back.
+ * Returns 0 and sets *dp, or DROP_CT_UNKNOWN_PROTO. */
+static int ct_new_dport(uint8_t proto, uint16_t sport, uint16_t dport,
+                        uint16_t *dp)
+{
+    switch (proto) {
+    case 1: { /* IPPROTO_ICMP */
+        uint8_t type = (uint8_t)(sport & 0xFF);
+        uint16_t t_sport = 0, t_dport = 0;
+        if (type == 0)          /* ICMP_ECHOREPLY: tuple->dport = ICMP_ECHO */
+            t_dport = 8;
+        else if (type == 8)     /* ICMP_ECHO: tuple->sport = type */
+            t_sport = type;
+        (void)t_dport;
+        *dp = t_sport;          /* after reverse: dport <- sport */
+        return 0;
+    }
+    case 6:
+    case 17:
+        *dp = dport;
+        return 0;
+    default:
+        return DROP_CT_UNKNOWN_PROTO;
+    }
+}
+
+typedef struct {
+    int32_t action, verdict;
+    uint32_t identity;
+} res_t;
+
+/* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
+ * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src. */
+static res_t lxc_ingress_v4(cfo_t *o, const epinfo *ep, uint32_t src,
+                            uint8_t proto, uint16_t sport, uint16_t dport,
+                            int frag, uint32_t len, int skip_proxy)
+{
+    res_t r = {TC_ACT_SHOT, 0, src};
+    uint16_t pdport;
+    int ret = ct_new_dport(proto, sport, dport, &pdport);
+    if (ret < 0) {
+        r.verdict = ret;
+        metric(o, ret, METRIC_INGRESS, len);
+        return r;
+    }
+    int verdict = policy_can_access(o->pol[ep->lxc_id], src, pdport, proto,
+                                    CT_INGRESS, frag, len);
+    if (verdict < 0) { /* policy_can_access_ingress -> DROP_POLICY */
+        r.verdict = DROP_POLICY;
+        metric(o, DROP_POLICY, METRIC_INGRESS, len);
+        return r;
+    }
+    if (skip_proxy)
+        verdict = 0;
+    if (verdict > 0) { /* redirect_to_proxy: cb[CB_IFINDEX] = HOST_IFINDEX */
+        r.action = TC_ACT_REDIRECT;
+        r.verdict = verdict;
+        return r;
+    }
+    metric(o, 0, METRIC_INGRESS, len); /* send_trace_notify(TRACE_TO_LXC) */
+    r.action = ep->ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+    r.verdict = 0;
+    return r;
+}
+
+/* from_netdev (FROM_HOST) -> handle_ipv4 (bpf_netdev.c:128-153, 357-453) */
+static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
+                               uint8_t proto, uint16_t sport, uint16_t dport,
+                               int frag, uint32_t len, uint32_t mark)
+{
+    uint32_t identity, magic = mark & MARK_MAGIC_HOST_MASK;
+    int skip_proxy = 0;
+    if (magic == MARK_MAGIC_PROXY_INGRESS || magic == MARK_MAGIC_PROXY_EGRESS) {
+        identity = ((mark & 0xFF) << 16) | (mark >> 16);
+        skip_proxy = magic == MARK_MAGIC_PROXY_INGRESS;
+    } else if (magic == MARK_MAGIC_HOST) {
+        identity = HOST_ID;
+    } else {
+        identity = WORLD_ID;
+    }
+    if (identity < HEALTH_ID) { /* identity_is_reserved, policy.h:41-44 */
+        uint32_t label;
+        if (lpm_lookup(&o->ipc4, (const uint8_t *)&saddr, &label) && label &&
+            label != CLUSTER_ID && label != HOST_ID)
+            identity = label;
+    }
+    res_t r = {TC_ACT_OK, 0, identity};
+    const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
+    if (!ep || (ep->flags & ENDPOINT_F_HOST))
+        return r; /* to the stack (tunnel endpoints out of scope) */
+    return lxc_ingress_v4(o, ep, identity, proto, sport, dport, frag, len,
+                          skip_proxy);
+}
+
+/* handle_ipv4_from_lxc (bpf_lxc.c:440-692) for endpoint lxc */
+static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
+                           uint32_t daddr, uint8_t proto, uint16_t sport,
+                           uint16_t dport, int frag, uint32_t len)
+{
+    res_t r = {TC_ACT_SHOT, 0, 0};
+    const epinfo *self = lxc_lookup(o, 1, (const uint8_t *)&saddr);
+    if (!self || self->lxc_id != lxc) { /* is_valid_lxc_src_ipv4, lxc.h:55 */
+        r.verdict = DROP_INVALID_SIP;
+        metric(o, DROP_INVALID_SIP, METRIC_EGRESS, len);
+        return r;
+    }
+    uint16_t pdport;
+    int ret = ct_new_dport(proto, sport, dport, &pdport);
+    if (ret < 0) {
+        r.verdict = ret;
+        metric(o, ret, METRIC_EGRESS, len);
+        return r;
+    }
+    uint32_t label = 0, dst;
+    if (lpm_lookup(&o->ipc4, (const uint8_t *)&daddr, &label) && label)
+        dst = label;
+    else if ((daddr & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE)
+        dst = CLUSTER_ID;
+    else
+        dst = WORLD_ID;
+    r.identity = dst;
+    int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
+                                    CT_EGRESS, 0, len);
+    if (verdict < 0) {
+        r.verdict = DROP_POLICY;
+        metric(o, DROP_POLICY, METRIC_EGRESS, len);
+        return r;
+    }
+    if (verdict > 0) { /* proxy: redirect(HOST_IFINDEX), TRACE_TO_PROXY */
+        r.action = TC_ACT_REDIRECT;
+        r.verdict = verdict;
+        return r;
+    }
+    const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
+    if (ep) {
+        if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST */
+            metric(o, 0, METRIC_EGRESS, len);
+            r.action = TC_ACT_REDIRECT;
+            return r;
+        }
+        /* ipv4_local_delivery (l3.h:103-131): egress forward metric, then
+         * the destination's policy program with src = SECLABEL */
+        metric(o, 0, METRIC_EGRESS, len);
+        res_t d = lxc_ingress_v4(o, ep, o->seclabel[lxc], proto, sport, dport,
+                                 frag, len, 0);
+        d.identity = dst;
+        return d;
+    }
+    metric(o, 0, METRIC_EGRESS, len); /* pass_to_stack: TRACE_TO_STACK */
+    r.action = TC_ACT_OK;
+    return r;
+}
+
+/* check_v4 (bpf_xdp.c:97-121) */
+static int xdp_v4(cfo_t *o, uint32_t saddr, uint32_t daddr)
+{
+    uint32_t v;
+    if (lpm_lookup(&o->pf4_dyn, (const uint8_t *)&saddr, &v))
+        return XDP_DROP;
+    uint8_t k[8];
+    uint32_t pl = 32;
+    memcpy(k, &pl, 4);
+    memcpy(k + 4, &saddr, 4);
+    if (ht_get(&o->pf4_fix, k, &v))
+        return XDP_DROP;
+    return lxc_lookup(o, 1, (const uint8_t *)&daddr) ? XDP_PASS : XDP_DROP;
+}
+
+void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint32_t *saddr, const uint32_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *mark,
+                     int32_t *action, int32_t *verdict, uint32_t *identity,
+                     int nthreads)
+{
+    if (nthreads <= 0)
+        nthreads = 1;
+#pragma omp parallel for schedule(static, 4096) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        res_t r;
+        if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
+            int x = xdp_v4(o, saddr[i], daddr[i]);
+            if (mode == CFO_MODE_XDP || x == XDP_DROP) {
+                action[i] = x;
+                verdict[i] = x == XDP_PASS ? 0 : -1;
+                identity[i] = 0;
+                continue;
+            }
+        }
+        if (mode == CFO_MODE_EGRESS)
+            r = lxc_egress_v4(o, ep_lxc, saddr[i], daddr[i], proto[i],
+                              sport[i], dport[i], flags[i] & HF_FRAG, len[i]);
+        else
+            r = netdev_ingress_v4(o, saddr[i], daddr[i], proto[i], sport[i],
+                                  dport[i], flags[i] & HF_FRAG, len[i],
+                                  mark ? mark[i] : 0);
+        action[i] = r.action;
+        verdict[i] = r.verdict;
+        identity[i] = r.identity;
+    }
+}
+
+static int cmp_rows7(const void *a, const void *b)
+{
+    const uint64_t *x = a, *y = b;
+    for (int i = 0; i < 7; i++)
+        if (x[i] != y[i])
+            return x[i] < y[i] ? -1 : 1;
+    return 0;
+}
+
+size_t cfo_policy_dump(cfo_t *o, uint16_t lxc_id, uint64_t *rows, size_t cap)
+{
+    pmap *m = o->pol[lxc_id];
+    if (!m)
+        return 0;
+    if (rows && cap >= m->n) {
+        for (uint32_t i = 0; i < m->n; i++) {
+            pentry *e = &m->ents[i];
+            uint32_t id;
+            uint16_t dp;
+            memcpy(&id, e->key, 4);
+            memcpy(&dp, e->key + 4, 2);
+            uint64_t *r = rows + 7 * (size_t)i;
+            r[0] = id;
+            r[1] = dp;
+            r[2] = e->key[6];
+            r[3] = e->key[7];
+            r[4] = e->proxy_port;
+            r[5] = e->packets;
+            r[6] = e->bytes;
+        }
+        qsort(rows, m->n, 7 * sizeof(uint64_t), cmp_rows7);
+    }
+    return m->n;
+}
+
+size_t cfo_metrics_dump(cfo_t *o, uint64_t *rows, size_t cap)
+{
+    size_t n = 0;
+    for (int r = 0; r < 256; r++)
+        for (int d = 0; d < 4; d++)
+            if (o->metrics[r][d][0]) {
+                if (rows && n < cap) {
+                    rows[4 * n] = (uint64_t)r;
+                    rows[4 * n + 1] = (uint64_t)d;
+                    rows[4 * n + 2] = o->metrics[r][d][0];
+                    rows[4 * n + 3] = o->metrics[r][d][1];
+                }
+                n++;
+            }
+    return n;
+}
+
+void cfo_counters_reset(cfo_t *o)
+{
+    memset(o->metrics, 0, sizeof(o->metrics));
+    for (int i = 0; i < 65536; i++)
+        if (o->pol[i])
+            for (uint32_t j = 0; j < o->pol[i]->n; j++)
+                o->pol[i]->ents[j].packets = o->pol[i]->ents[j].bytes = 0;
+}

@@ -1,0 +1,68 @@
+/*
+ * cfc_oracle — CPU restatement of the reference verdict path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the checker the GPU engine is compared
+ * against (tests/, __graft_entry__.smoke(), bench.py's cpu_baseline leg).
+ * It is never linked into or called by the product (cilium_amd/libcfc.so).
+ *
+ * Pinned against golden vectors produced by the reference's own BPF programs
+ * run with BPF_PROG_TEST_RUN (oracle/gen_golden.py -> tests/golden/).
+ *
+ * Conventions are the reference datapath's: addresses/ports are raw
+ * network-order bytes loaded little-endian (be32/be16 "raw"), identities are
+ * host-order u32, verdicts follow bpf/lib/policy.h (<0 drop reason, 0 allow,
+ * >0 proxy port as stored in policy_entry.proxy_port).
+ */
+#ifndef CFC_ORACLE_H
+#define CFC_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct cfo cfo_t;
+
+enum { CFO_MODE_INGRESS = 0, CFO_MODE_EGRESS = 1, CFO_MODE_XDP = 2,
+       CFO_MODE_FULL = 3 };
+
+cfo_t *cfo_new(void);
+void cfo_free(cfo_t *o);
+
+/* family: 1 = IPv4, 2 = IPv6 (ENDPOINT_KEY_IPV4/6, common.h:139-140) */
+int cfo_ipcache_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
+                    uint32_t label);
+int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
+                     uint32_t ifindex, uint16_t lxc_id, uint32_t flags);
+int cfo_seclabel_set(cfo_t *o, uint16_t lxc_id, uint32_t seclabel);
+int cfo_policy_add(cfo_t *o, uint16_t lxc_id, uint32_t identity,
+                   uint16_t dport_be, uint8_t proto, uint8_t egress,
+                   uint16_t proxy_port_be);
+int cfo_prefilter_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
+                      int dyn);
+
+/* Classify n IPv4 headers (SoA).  mark may be NULL.  Outputs: action = the
+ * return code of the last reference program run (TC_ACT_* or XDP_*),
+ * verdict (policy.h convention; -1 = XDP prefilter drop), identity (ingress:
+ * source security identity used for policy; egress: destination identity).
+ * Counters accumulate in the oracle's policy entries and metrics table. */
+void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint32_t *saddr, const uint32_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *mark,
+                     int32_t *action, int32_t *verdict, uint32_t *identity,
+                     int nthreads);
+
+/* rows of 7 u64: identity, dport, proto, egress, proxy_port, packets, bytes
+ * (sorted); returns the number of rows (writes at most cap). */
+size_t cfo_policy_dump(cfo_t *o, uint16_t lxc_id, uint64_t *rows, size_t cap);
+/* rows of 4 u64: reason, dir, count, bytes (sorted, non-zero only) */
+size_t cfo_metrics_dump(cfo_t *o, uint64_t *rows, size_t cap);
+void cfo_counters_reset(cfo_t *o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,472 @@
+"""Generate golden vectors by running the reference BPF datapath.
+
+TEST INFRASTRUCTURE ONLY.  Runs in the build container (root, kernel with
+BPF_PROG_TEST_RUN); writes small fixtures to tests/golden/*.npz which the
+CPU oracle and the GPU parity tests are checked against.
+
+Reference programs driven (compiled by oracle/Makefile from the reference):
+  ingress : bpf_netdev.o "from-netdev" (FROM_HOST, netdev_config.h)
+            -> tail 2/7 handle_ipv4 (bpf_netdev.c:357-453: ipcache src
+            identity, cilium_lxc lookup) -> ipv4_local_delivery (l3.h:103)
+            -> cilium_policy[lxc_id] = bpf_lxc.o "1/0x1010" handle_policy
+            (bpf_lxc.c:1039) -> tail 2/11 ipv4_policy (bpf_lxc.c:898-1015)
+            -> __policy_can_access (policy.h:46-110)
+  egress  : bpf_lxc.o "from-container" (bpf_lxc.c:718) -> tail 2/7
+            handle_ipv4_from_lxc (bpf_lxc.c:440-692)
+  xdp     : bpf_xdp.o "from-netdev" (bpf_xdp.c:158-184)
+  full    : xdp, then ingress for XDP_PASS packets.
+
+Per header we record the program's return code, skb->cb[] and the rewritten
+L4 destination port; after the stream, every policymap's packets/bytes and
+the cilium_metrics map (summed over CPUs).  From those the expected
+(action, verdict, identity) triple is derived (see `_derive_*`).
+
+Usage: python3 oracle/gen_golden.py [scenario ...]
+"""
+import os
+import struct
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+from cilium_amd import synth as S  # noqa: E402
+import bpf_harness as H            # noqa: E402
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+LXC_MAC = bytes([0xaa, 0xbb, 0xcc, 0xdd, 0xee, 0xff])    # lxc_config.h
+NODE_MAC = bytes([0xde, 0xad, 0xbe, 0xef, 0xc0, 0xde])   # lxc/node_config.h
+HOST_IFINDEX = 1                                         # node_config.h
+TC_ACT_OK, TC_ACT_SHOT, TC_ACT_REDIRECT = 0, 2, 7
+XDP_DROP, XDP_PASS = 1, 2
+
+MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
+MODES = {"ingress": MODE_INGRESS, "egress": MODE_EGRESS, "xdp": MODE_XDP,
+         "full": MODE_FULL}
+
+
+# ------------------------------------------------------------ packets
+def build_packet_v4(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
+    proto = int(h.proto[i])
+    L = int(h.length[i])
+    frag = 0x2000 if (h.flags[i] & S.HF_FRAG) else 0      # MF, offset 0
+    ip = struct.pack(">BBHHHBBH", 0x45, 0, L - 14, i & 0xFFFF, frag, 64,
+                     proto, 0)
+    ip += struct.pack("<II", int(h.saddr[i]), int(h.daddr[i]))
+    sp, dp = int(h.sport[i]), int(h.dport[i])
+    if proto == S.IPPROTO_TCP:
+        fl = 0x11 if (h.flags[i] & S.HF_TCP_CLOSE) else 0x02
+        l4 = struct.pack("<HH", sp, dp) + struct.pack(">IIBBHHH", 1, 0, 0x50,
+                                                       fl, 1024, 0, 0)
+    elif proto == S.IPPROTO_UDP:
+        l4 = struct.pack("<HH", sp, dp) + struct.pack(">HH", L - 34, 0)
+    else:   # ICMP (type/code in sport word, csum in dport word) and others
+        l4 = struct.pack("<HH", sp, dp) + b"\x00" * 4
+    pkt = eth_dst + eth_src + b"\x08\x00" + ip + l4
+    assert len(pkt) <= L, (len(pkt), L)
+    return pkt + bytes(L - len(pkt))
+
+
+# ------------------------------------------------------------ datapath
+def u32(x):
+    return struct.pack("<I", x)
+
+
+def ipcache_key(e):
+    # struct ipcache_key: lpm prefixlen = 32 static bits + plen (eps.h:49-52)
+    return struct.pack("<IHBB", 32 + int(e["plen"]), 0, 0,
+                       int(e["family"])) + bytes(e["addr"])
+
+
+def endpoint_key(e):
+    return bytes(e["addr"]) + struct.pack("<BBH", int(e["family"]), 0, 0)
+
+
+def endpoint_value(e):
+    # struct endpoint_info (common.h:165-173), 48 bytes
+    return struct.pack("<IHHI4xQQ16x", int(e["ifindex"]), 0, int(e["lxc_id"]),
+                       int(e["flags"]), 0, 0)
+
+
+def policy_key(r):
+    return struct.pack("<IHBB", int(r["identity"]), int(r["dport"]),
+                       int(r["proto"]), int(r["egress"]))
+
+
+class RefDatapath:
+    def __init__(self, t: S.Tables):
+        n_ipc = max(512000, len(t.ipcache) + 16)
+        n_pf = max(1024, len(t.prefilter) + 16)
+        self.L = L = H.Loader({"cilium_ipcache": n_ipc, "v4_fix": n_pf,
+                               "v4_dyn": n_pf, "v6_fix": n_pf, "v6_dyn": n_pf,
+                               "cilium_policy_foo": 16384 * 2})
+        self.t = t
+        SC = H.PROG_SCHED_CLS
+        nd = {"cilium_calls_111": "calls_nd"}
+        self.netdev = L.load("bpf_netdev.o", "from-netdev", SC, nd)
+        nd_v4 = L.load("bpf_netdev.o", "2/7", SC, nd)
+        L.maps["calls_nd"].update(u32(7), u32(nd_v4))
+        self.ep_prog = {}
+        self.policy_map = {}
+        for k, e in enumerate(t.endpoints):
+            if int(e["flags"]) & 1:
+                continue
+            lxc = int(e["lxc_id"])
+            rn = {"cilium_calls_111": f"calls_lxc{k}",
+                  "cilium_policy_foo": f"policy{k}"}
+            for ct in ("cilium_ct_tcp4_111", "cilium_ct_any4_111",
+                       "cilium_ct_tcp6_111", "cilium_ct_any6_111"):
+                rn[ct] = f"{ct}_{k}"
+            pol = L.load("bpf_lxc.o", "1/0x1010", SC, rn)
+            calls = {}
+            for sec, idx in (("2/11", 11), ("2/7", 7)):
+                calls[idx] = L.load("bpf_lxc.o", sec, SC, rn)
+            egress = L.load("bpf_lxc.o", "from-container", SC, rn)
+            for idx, fd in calls.items():
+                L.maps[f"calls_lxc{k}"].update(u32(idx), u32(fd))
+            L.maps["cilium_policy"].update(u32(lxc), u32(pol))
+            self.ep_prog[lxc] = egress
+            pm = L.maps[f"policy{k}"]
+            self.policy_map[lxc] = pm
+            for r in t.policy.get(lxc, []):
+                pm.update(policy_key(r), struct.pack("<H6xQQ",
+                                                     int(r["proxy_port"]), 0, 0))
+        self.xdp = L.load("bpf_xdp.o", "from-netdev", H.PROG_XDP)
+        for e in t.ipcache:
+            L.maps["cilium_ipcache"].update(
+                ipcache_key(e), struct.pack("<II", int(e["label"]),
+                                            int(e["tunnel"])))
+        for e in t.endpoints:
+            L.maps["cilium_lxc"].update(endpoint_key(e), endpoint_value(e))
+        for p in t.prefilter:
+            fam = int(p["family"])
+            an = 4 if fam == 1 else 16
+            name = ("v4_" if fam == 1 else "v6_") + ("dyn" if p["dyn"] else "fix")
+            key = struct.pack("<I", int(p["plen"])) + bytes(p["addr"][:an])
+            L.maps[name].update(key, b"\x01")
+
+    def close(self):
+        self.L.close()
+
+    # ------------------------------------------------------- counters
+    def policy_counters(self):
+        out = {}
+        for lxc, pm in self.policy_map.items():
+            rows = []
+            for k in pm.keys():
+                v = pm.lookup(k)
+                ident, dport, proto, eg = struct.unpack("<IHBB", k)
+                pp, pk, by = struct.unpack("<H6xQQ", v)
+                rows.append((ident, dport, proto, eg, pp, pk, by))
+            rows.sort()
+            out[lxc] = np.array(rows, dtype=np.uint64).reshape(-1, 7)
+        return out
+
+    def metrics(self):
+        m = self.L.maps.get("cilium_metrics")
+        rows = []
+        if m is None:
+            return np.zeros((0, 4), np.uint64)
+        ncpu = H.ncpus_possible()
+        for k in m.keys():
+            v = m.lookup(k)
+            cnt = sum(struct.unpack_from("<Q", v, 16 * c)[0] for c in range(ncpu))
+            byt = sum(struct.unpack_from("<Q", v, 16 * c + 8)[0]
+                      for c in range(ncpu))
+            reason, dirb = k[0], k[1] & 3
+            rows.append((reason, dirb, cnt, byt))
+        rows.sort()
+        return np.array(rows, dtype=np.uint64).reshape(-1, 4)
+
+
+# ------------------------------------------------------------ run + derive
+def _dport_out(pkt_out):
+    return struct.unpack_from("<H", pkt_out, 14 + 20 + 2)[0]
+
+
+def _derive_ingress(h, i, ret, cb, pkt_out):
+    """-> action, verdict, identity, id_mask"""
+    if ret == TC_ACT_SHOT:
+        # send_drop_notify(skb, src_label, SECLABEL, LXC_ID, ...):
+        # cb[1] = src << 16 | dst & 0xFFFF, cb[2] = reason (drop.h:94-102)
+        return ret, cb[2], (cb[1] >> 16) & 0xFFFF, 0xFFFF
+    if ret == TC_ACT_REDIRECT:
+        # proxy redirect rewrote the dport (lxc.h:118) and set
+        # cb[CB_IFINDEX] = HOST_IFINDEX (bpf_lxc.c:1004)
+        v = _dport_out(pkt_out) if cb[1] == HOST_IFINDEX else 0
+        return ret, v, cb[0] & 0xFFFFFFFF, 0xFFFFFFFF
+    # TC_ACT_OK: non-local / host endpoint: identity not observable
+    return ret, 0, 0, 0
+
+
+def _derive_egress(h, i, ret, cb, pkt_out):
+    if ret == TC_ACT_SHOT:
+        if cb[3] == 0:
+            # egress-stage drop: send_drop_notify(SECLABEL, dstID, 0, ...)
+            return ret, cb[2], cb[1] & 0xFFFF, 0xFFFF
+        # dropped by the destination endpoint's ingress policy
+        return ret, cb[2], 0, 0
+    if ret == TC_ACT_REDIRECT:
+        dp = _dport_out(pkt_out)
+        v = dp if dp != int(h.dport[i]) else 0
+        return ret, v, 0, 0
+    return ret, 0, 0, 0
+
+
+def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
+    n = len(h)
+    action = np.zeros(n, np.int32)
+    verdict = np.zeros(n, np.int32)
+    ident = np.zeros(n, np.uint32)
+    idmask = np.zeros(n, np.uint32)
+    for i in range(n):
+        if mode in (MODE_XDP, MODE_FULL):
+            ret = H.test_run_xdp(dp.xdp, build_packet_v4(h, i))
+            if mode == MODE_XDP or ret == XDP_DROP:
+                action[i] = ret
+                verdict[i] = 0 if ret == XDP_PASS else -1
+                continue
+        if mode in (MODE_INGRESS, MODE_FULL):
+            ret, cb, po = H.test_run_skb(dp.netdev, build_packet_v4(h, i),
+                                         mark=int(h.mark[i]))
+            r = _derive_ingress(h, i, ret, cb, po)
+        else:
+            ret, cb, po = H.test_run_skb(
+                dp.ep_prog[ep_lxc], build_packet_v4(h, i, LXC_MAC, NODE_MAC))
+            r = _derive_egress(h, i, ret, cb, po)
+        action[i], verdict[i], ident[i], idmask[i] = r
+    return action, verdict, ident, idmask
+
+
+def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
+    action, verdict, ident, idmask = res
+    d = dict(mode=np.int32(mode), ep_lxc=np.int32(ep_lxc or 0),
+             ipcache=t.ipcache, endpoints=t.endpoints, prefilter=t.prefilter,
+             seclabel=np.array(sorted(t.seclabel.items()), np.uint32).reshape(-1, 2),
+             h_family=np.int32(h.family), h_saddr=h.saddr, h_daddr=h.daddr,
+             h_sport=h.sport, h_dport=h.dport, h_proto=h.proto,
+             h_flags=h.flags, h_length=h.length, h_mark=h.mark,
+             x_action=action, x_verdict=verdict, x_identity=ident,
+             x_idmask=idmask, x_metrics=dp.metrics())
+    for lxc, pol in t.policy.items():
+        d[f"policy_{lxc}"] = pol
+    for lxc, c in dp.policy_counters().items():
+        d[f"x_counters_{lxc}"] = c
+    os.makedirs(GOLDEN, exist_ok=True)
+    path = os.path.join(GOLDEN, f"{name}.npz")
+    np.savez_compressed(path, **d)
+    return path
+
+
+# ------------------------------------------------------------ scenarios
+def sc_c2_ingress(n=20000, seed=2, n_prefixes=100_000, n_policy=16384):
+    t = S.config_c2(seed, n_prefixes=n_prefixes, n_policy=n_policy)
+    h = S.headers_c2(t, int(n * 1.02), seed=seed)
+    h = _keep(h, S.ensure_no_reverse(h))
+    h = h.slice(0, n)
+    return t, h, MODE_INGRESS, None
+
+
+def sc_small_ingress(n=20000, seed=1):
+    """C1-sized: a few hundred prefixes, ~100 identities, 3 endpoints with
+    small policies (examples/policies scale)."""
+    rng = np.random.default_rng(seed)
+    ipc = S.gen_ipcache_v4(rng, 300, label_base=256, label_mod=100)
+    eps = np.concatenate([S.endpoint_v4(S.LXC_IPV4, 100, S.EP_LXC_ID),
+                          S.endpoint_v4(S.ip4("10.0.1.2"), 101, 0x2020),
+                          S.endpoint_v4(S.ip4("10.0.1.3"), 0, 0x3030),
+                          S.endpoint_v4(S.ip4("10.0.255.254"), 0, 0xFFF0, 1)])
+    idents = np.unique(ipc["label"])
+    pol = {S.EP_LXC_ID: S.gen_policy(rng, 50, idents, wildcard=3,
+                                     proxy_frac=0.2),
+           0x2020: S.gen_policy(rng, 40, idents, wildcard=2, l3_frac=0.2),
+           0x3030: np.zeros(0, S.POLICY_DT)}
+    t = S.Tables(ipc, eps, pol, np.zeros(0, S.PREFILTER_DT),
+                 {int(e["lxc_id"]): S.EP_SECLABEL for e in eps})
+    h = S.gen_headers_v4(rng, int(n * 1.02), ipc, S.local_v4_addrs(t),
+                         local_frac=0.9, frag=0.05, mark_host=0.05,
+                         mark_proxy=0.05, other_proto=0.02,
+                         proxy_ident=np.concatenate([idents[:8], [1, 2, 3, 4, 5, 70000]]))
+    h = _keep(h, S.ensure_no_reverse(h)).slice(0, n)
+    return t, h, MODE_INGRESS, None
+
+
+def sc_edge_ingress(seed=7):
+    """Hand-picked fallback cases: L4 hit, L3 fallback, wildcard port,
+    fragments (L3 only), proxy, ICMP echo -> port 2048 quirk, unknown proto,
+    identity override rules (label 0/HOST/CLUSTER ignored), marks."""
+    ipc = np.concatenate([
+        S._v4_entries(np.array([S.ip4("172.16.0.0")], np.uint32), [12], [1000]),
+        S._v4_entries(np.array([S.ip4("172.16.5.0")], np.uint32), [24], [1001]),
+        S._v4_entries(np.array([S.ip4("172.16.5.128")], np.uint32), [25], [0]),
+        S._v4_entries(np.array([S.ip4("172.16.6.0")], np.uint32), [24], [S.HOST_ID]),
+        S._v4_entries(np.array([S.ip4("172.16.7.0")], np.uint32), [24], [S.CLUSTER_ID]),
+        S._v4_entries(np.array([S.ip4("172.16.8.8")], np.uint32), [32], [4242]),
+        S._v4_entries(np.array([S.ip4("0.0.0.0")], np.uint32), [0], [7]),
+        S._v4_entries(np.array([S.ip4("192.168.0.0")], np.uint32), [16], [0x80000001]),
+    ])
+    eps = np.concatenate([S.endpoint_v4(S.LXC_IPV4, 100, S.EP_LXC_ID),
+                          S.endpoint_v4(S.ip4("10.0.255.254"), 0, 0xFFF0, 1)])
+    ht = lambda p: int(S.htons(p))   # noqa: E731
+    rows = [(1000, ht(80), 6, 0, 0), (1000, ht(53), 17, 0, 0),
+            (1001, 0, 0, 0, 0), (4242, ht(443), 6, 0, ht(10001)),
+            (0, ht(8080), 6, 0, 0), (0, ht(9090), 6, 0, ht(10002)),
+            (7, 0, 0, 0, 0), (1000, 8, 1, 0, 0), (1000, 0, 1, 0, 0),
+            (S.WORLD_ID, ht(22), 6, 0, 0), (S.HOST_ID, 0, 0, 0, 0),
+            (0x80000001, ht(80), 6, 0, 0), (1000, ht(80), 6, 1, 0),
+            (70000, 0, 0, 0, 0), (1001, ht(80), 6, 0, ht(10003))]
+    pol = np.zeros(len(rows), S.POLICY_DT)
+    a = np.array(rows, dtype=np.int64)
+    pol["identity"], pol["dport"], pol["proto"] = a[:, 0], a[:, 1], a[:, 2]
+    pol["egress"], pol["proxy_port"] = a[:, 3], a[:, 4]
+    t = S.Tables(ipc, eps, {S.EP_LXC_ID: pol}, np.zeros(0, S.PREFILTER_DT),
+                 {S.EP_LXC_ID: S.EP_SECLABEL, 0xFFF0: S.EP_SECLABEL})
+    srcs = ["172.16.1.1", "172.16.5.9", "172.16.5.200", "172.16.6.1",
+            "172.16.7.1", "172.16.8.8", "8.8.8.8", "192.168.3.4", "0.0.0.0"]
+    dsts = ["64.48.32.16", "10.0.255.254", "9.9.9.9"]
+    cases = []
+    for s in srcs:
+        for d in dsts:
+            for proto, sp, dp in ((6, 40000, 80), (6, 40001, 443), (6, 40002, 8080),
+                                  (6, 40003, 9090), (6, 40004, 22), (17, 40005, 53),
+                                  (17, 40006, 80), (1, 8, 0x1234), (1, 0, 7),
+                                  (1, 3, 0), (1, 11, 0), (47, 0, 0), (132, 1, 2)):
+                for fl in (0, S.HF_FRAG, S.HF_TCP_CLOSE):
+                    for mark in (0, 0xC00, 0xA00 | (4242 & 0xFFFF) << 16,
+                                 0xB00 | (70000 & 0xFFFF) << 16 | (70000 >> 16),
+                                 0xB00 | (3 << 16)):
+                        cases.append((s, d, proto, sp, dp, fl, mark))
+    n = len(cases)
+    rng = np.random.default_rng(seed)
+    h = S.Headers(4, np.array([S.ip4(c[0]) for c in cases], np.uint32),
+                  np.array([S.ip4(c[1]) for c in cases], np.uint32),
+                  np.array([c[3] if c[2] == 1 else ht(c[3]) for c in cases], np.uint16),
+                  np.array([c[4] if c[2] == 1 else ht(c[4]) for c in cases], np.uint16),
+                  np.array([c[2] for c in cases], np.uint8),
+                  np.array([c[5] for c in cases], np.uint8),
+                  rng.integers(60, 200, size=n).astype(np.uint16),
+                  np.array([c[6] for c in cases], np.uint32))
+    # make source ports distinct per case so no two headers form a reverse pair
+    tcpudp = (h.proto == 6) | (h.proto == 17)
+    h.sport[tcpudp] = S.htons(20000 + np.arange(n)[tcpudp] % 40000)
+    return t, h, MODE_INGRESS, None
+
+
+def sc_c2_egress(n=20000, seed=3):
+    t = S.config_c2(seed, n_prefixes=100_000, n_policy=16384, n_endpoints=2)
+    rng = np.random.default_rng(seed + 7)
+    h = S.gen_headers_v4(rng, n, t.ipcache, S.local_v4_addrs(t),
+                         local_frac=0.05, mark_host=0, mark_proxy=0,
+                         src_fixed=S.LXC_IPV4)
+    # swap roles: destination addresses come from the ipcache (in_prefix),
+    # sources are the endpoint; 2% spoofed sources (DROP_INVALID_SIP)
+    dst = S._addr_in_prefix_v4(rng, t.ipcache,
+                               rng.integers(0, len(t.ipcache), size=n))
+    loc = S.local_v4_addrs(t)
+    r = rng.random(n)
+    h.daddr = np.where(r < 0.85, dst, np.where(
+        r < 0.95, loc[rng.integers(0, len(loc), size=n)],
+        rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32))
+    ).astype(np.uint32)
+    # cluster range 0x100000 mask 0xff0000: some 16.x destinations -> CLUSTER_ID
+    cl = rng.random(n) < 0.02
+    h.daddr[cl] = (h.daddr[cl] & np.uint32(0xFF00FFFF)) | np.uint32(0x100000)
+    spoof = rng.random(n) < 0.02
+    h.saddr[spoof] = S.ip4("64.48.32.17")
+    h = _keep(h, S.ensure_no_reverse(h))
+    return t, h, MODE_EGRESS, S.EP_LXC_ID
+
+
+def _prefilter_v4(rng, ipc, n_fix, n_dyn):
+    pf = np.zeros(n_fix + n_dyn, S.PREFILTER_DT)
+    pf["family"] = 1
+    fix = rng.integers(1 << 24, 224 << 24, size=n_fix, dtype=np.uint64).astype(np.uint32)
+    pf["plen"][:n_fix] = 32
+    pf["addr"][:n_fix, :4] = S.be32_to_bytes(S.byteswap32(fix))
+    dl = rng.choice(np.array([8, 12, 16, 20, 24, 28, 31, 32]), size=n_dyn)
+    dh = rng.integers(1 << 24, 224 << 24, size=n_dyn, dtype=np.uint64).astype(np.uint32)
+    dh &= (np.uint64(0xFFFFFFFF) << (32 - dl.astype(np.uint64))).astype(np.uint32)
+    pf["plen"][n_fix:] = dl
+    pf["addr"][n_fix:, :4] = S.be32_to_bytes(S.byteswap32(dh))
+    pf["dyn"][n_fix:] = 1
+    # unique keys
+    _, u = np.unique(np.stack([pf["dyn"], pf["plen"],
+                               pf["addr"][:, :4].copy().view("<u4").ravel()], 1),
+                     axis=0, return_index=True)
+    return pf[np.sort(u)]
+
+
+def sc_xdp(n=20000, seed=4, mode=MODE_XDP):
+    t = S.config_c2(seed, n_prefixes=20_000, n_policy=4096)
+    rng = np.random.default_rng(seed + 11)
+    t.prefilter = _prefilter_v4(rng, t.ipcache, 5000, 300)
+    h = S.headers_c2(t, n, seed=seed, local_frac=0.85)
+    r = rng.random(n)
+    fix = t.prefilter[t.prefilter["dyn"] == 0]
+    dyn = t.prefilter[t.prefilter["dyn"] == 1]
+    fa = fix["addr"][:, :4].copy().view("<u4").ravel()
+    sel = r < 0.25
+    h.saddr[sel] = fa[rng.integers(0, len(fa), size=int(sel.sum()))]
+    sel2 = (r >= 0.25) & (r < 0.4)
+    di = rng.integers(0, len(dyn), size=int(sel2.sum()))
+    base = S.byteswap32(dyn["addr"][di, :4].copy().view("<u4").ravel()).astype(np.uint64)
+    pl = dyn["plen"][di].astype(np.uint64)
+    hb = rng.integers(0, 1 << 32, size=len(di), dtype=np.uint64) & ((np.uint64(1) << (np.uint64(32) - pl)) - np.uint64(1))
+    h.saddr[sel2] = S.byteswap32((base | hb).astype(np.uint32))
+    h = _keep(h, S.ensure_no_reverse(h))
+    return t, h, mode, None
+
+
+def sc_empty(n=2000, seed=5):
+    """Empty ipcache / policymap / prefilter: everything WORLD, DROP_POLICY."""
+    t = S.Tables(np.zeros(0, S.IPCACHE_DT),
+                 S.endpoint_v4(S.LXC_IPV4, 100, S.EP_LXC_ID),
+                 {S.EP_LXC_ID: np.zeros(0, S.POLICY_DT)},
+                 np.zeros(0, S.PREFILTER_DT), {S.EP_LXC_ID: S.EP_SECLABEL})
+    rng = np.random.default_rng(seed)
+    ipc = S.gen_ipcache_v4(rng, 100)
+    h = S.gen_headers_v4(rng, n, ipc, S.local_v4_addrs(t))
+    h = _keep(h, S.ensure_no_reverse(h))
+    return t, h, MODE_INGRESS, None
+
+
+def _keep(h, m):
+    return S.Headers(h.family, h.saddr[m], h.daddr[m], h.sport[m], h.dport[m],
+                     h.proto[m], h.flags[m], h.length[m], h.mark[m])
+
+
+SCENARIOS = {
+    "edge_ingress_v4": sc_edge_ingress,
+    "small_ingress_v4": sc_small_ingress,
+    "c2_ingress_v4": sc_c2_ingress,
+    "c2_egress_v4": sc_c2_egress,
+    "xdp_v4": sc_xdp,
+    "full_v4": lambda: sc_xdp(seed=6, mode=MODE_FULL),
+    "empty_ingress_v4": sc_empty,
+}
+
+
+def main(names):
+    for name in names or SCENARIOS:
+        t0 = time.time()
+        t, h, mode, ep = SCENARIOS[name]()
+        dp = RefDatapath(t)
+        try:
+            res = run(dp, h, mode, ep)
+            path = save(name, t, h, mode, ep, res, dp)
+        finally:
+            dp.close()
+        act = res[0]
+        print(f"{name}: {len(h)} headers, mode {mode}, actions "
+              f"{dict(zip(*np.unique(act, return_counts=True)))}, "
+              f"{os.path.getsize(path) // 1024} KiB, {time.time() - t0:.1f}s")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,128 @@
+"""ctypes front-end of the C restatement (liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the checker — never by cilium_amd/.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        vp, u8p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8)
+        L.cfo_new.restype = vp
+        L.cfo_free.argtypes = [vp]
+        L.cfo_ipcache_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, u8p,
+                                      ctypes.c_uint32]
+        L.cfo_endpoint_add.argtypes = [vp, ctypes.c_int, u8p, ctypes.c_uint32,
+                                       ctypes.c_uint16, ctypes.c_uint32]
+        L.cfo_seclabel_set.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32]
+        L.cfo_policy_add.argtypes = [vp, ctypes.c_uint16, ctypes.c_uint32,
+                                     ctypes.c_uint16, ctypes.c_uint8,
+                                     ctypes.c_uint8, ctypes.c_uint16]
+        L.cfo_prefilter_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, u8p,
+                                        ctypes.c_int]
+        L.cfo_classify_v4.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
+                                      ctypes.c_size_t] + [vp] * 11 + [ctypes.c_int]
+        L.cfo_policy_dump.restype = ctypes.c_size_t
+        L.cfo_policy_dump.argtypes = [vp, ctypes.c_uint16, vp, ctypes.c_size_t]
+        L.cfo_metrics_dump.restype = ctypes.c_size_t
+        L.cfo_metrics_dump.argtypes = [vp, vp, ctypes.c_size_t]
+        L.cfo_counters_reset.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _u8p(a):
+    a = np.ascontiguousarray(a, dtype=np.uint8)
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), a
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class Oracle:
+    def __init__(self, tables=None):
+        self.L = lib()
+        self.h = self.L.cfo_new()
+        self.lxc_ids = []
+        if tables is not None:
+            self.load(tables)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.cfo_free(self.h)
+            self.h = None
+
+    def load(self, t):
+        L, h = self.L, self.h
+        for e in t.ipcache:
+            p, keep = _u8p(e["addr"])
+            L.cfo_ipcache_add(h, int(e["family"]), int(e["plen"]), p,
+                              int(e["label"]))
+        for e in t.endpoints:
+            p, keep = _u8p(e["addr"])
+            L.cfo_endpoint_add(h, int(e["family"]), p, int(e["ifindex"]),
+                               int(e["lxc_id"]), int(e["flags"]))
+        for lxc, lab in t.seclabel.items():
+            L.cfo_seclabel_set(h, int(lxc), int(lab))
+        for lxc, pol in t.policy.items():
+            self.lxc_ids.append(int(lxc))
+            for r in pol:
+                L.cfo_policy_add(h, int(lxc), int(r["identity"]), int(r["dport"]),
+                                 int(r["proto"]), int(r["egress"]),
+                                 int(r["proxy_port"]))
+        for p in t.prefilter:
+            a, keep = _u8p(p["addr"])
+            L.cfo_prefilter_add(h, int(p["family"]), int(p["plen"]), a,
+                                int(p["dyn"]))
+
+    def classify(self, hdr, mode, ep_lxc=0, nthreads=1):
+        n = len(hdr)
+        act = np.zeros(n, np.int32)
+        ver = np.zeros(n, np.int32)
+        ide = np.zeros(n, np.uint32)
+        c = np.ascontiguousarray
+        arrs = [c(hdr.saddr, np.uint32), c(hdr.daddr, np.uint32),
+                c(hdr.sport, np.uint16), c(hdr.dport, np.uint16),
+                c(hdr.proto, np.uint8), c(hdr.flags, np.uint8),
+                c(hdr.length, np.uint16), c(hdr.mark, np.uint32)]
+        assert hdr.family == 4, "IPv6 oracle path not built yet"
+        self.L.cfo_classify_v4(self.h, mode, ep_lxc, n,
+                               *[_p(a) for a in arrs], _p(act), _p(ver),
+                               _p(ide), nthreads)
+        return act, ver, ide
+
+    def policy_counters(self, lxc):
+        n = self.L.cfo_policy_dump(self.h, lxc, None, 0)
+        rows = np.zeros((n, 7), np.uint64)
+        self.L.cfo_policy_dump(self.h, lxc, _p(rows), n)
+        return rows
+
+    def metrics(self):
+        n = self.L.cfo_metrics_dump(self.h, None, 0)
+        rows = np.zeros((n, 4), np.uint64)
+        self.L.cfo_metrics_dump(self.h, _p(rows), n)
+        return rows
+
+    def reset_counters(self):
+        self.L.cfo_counters_reset(self.h)
