@@ -1,0 +1,200 @@
+"""Benchmark: classified headers/s (Mpps, whole node) of the MI355X verdict
+engine at the C2 configuration (100k-prefix IPv4 ipcache + 16k-entry
+policymap, 64M-header batches; BASELINE.json configs[1]).
+
+A step = one cfc_classify_v4 launch over one resident 64M-header batch in
+FULL mode: XDP prefilter (25k-entry /32 deny-list) -> ipcache LPM -> endpoint
+-> policymap with L3/wildcard fallbacks -> verdicts + counters.  With
+--gpus N (torchrun, one rank per GPU) each rank classifies its own 64M shard
+of the stream (weak scaling, tables replicated) and the counters are
+all-reduced over RCCL once at the end of the timed region.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+S_IN, S_OUT = 16, 8        # SoA bytes per header in (saddr,daddr,ports,meta) / out
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--headers", type=int, default=64 << 20)
+    ap.add_argument("--mode", default="full",
+                    choices=["ingress", "egress", "xdp", "full"])
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000,
+                    help="headers timed on the host-core oracle (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--seed", type=int, default=2)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from cilium_amd import synth as S
+    from cilium_amd.datapath import Datapath, HeaderBatchV4, Verdicts
+    from cilium_amd.distributed import allreduce_counters, env_rank
+    from cilium_amd.loader import load_tables
+
+    rank, local_rank, world = env_rank()
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    mode = {"ingress": 0, "egress": 1, "xdp": 2, "full": 3}[args.mode]
+    ep_lxc = S.EP_LXC_ID if mode == 1 else 0
+
+    t0 = time.time()
+    tables = S.config_c2_bench(args.seed)
+    dp = Datapath(local_rank)
+    load_tables(dp, tables)
+    st = dp.stats()
+    log(f"[rank {rank}] tables loaded+committed in {time.time() - t0:.1f}s: {st}")
+
+    n = args.headers
+    # each rank owns its shard of the stream: seed differs per rank
+    s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
+    if mode == 1:
+        s.fill_(S.LXC_IPV4 - (1 << 32) if S.LXC_IPV4 >= 1 << 31 else S.LXC_IPV4)
+    batch = HeaderBatchV4(s, d, p, m, None)
+    out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
+                   torch.empty(n, dtype=torch.int32, device=dev), None)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] batch of {n} headers generated ({(n * S_IN) >> 20} MiB)")
+
+    for _ in range(args.warmup):
+        dp.classify_v4(batch, mode, ep_lxc, out=out)
+    torch.cuda.synchronize()
+    dp.counters_clear()
+
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        dp.classify_v4(batch, mode, ep_lxc, out=out)
+        evs[i][1].record(stream)
+    if world > 1:
+        allreduce_counters(dp)   # the only collective: counter SUM over RCCL
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - w0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1:
+        tw = torch.tensor([wall], device=dev, dtype=torch.float64)
+        dist.all_reduce(tw, op=dist.ReduceOp.MAX)
+        wall = float(tw.item())
+    if world == 1:
+        dp.counters_sync()
+    total = n * world * args.steps
+    mpps = total / wall / 1e6
+    log(f"[rank {rank}] {args.steps} steps in {wall * 1e3:.2f} ms, kernel avg "
+        f"{kern_ms:.3f} ms/launch, {mpps:.0f} Mpps")
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    # ---- algorithmic bytes per header from the oracle's lookup counts (L),
+    #      and the host-core baseline + a parity check on the same sample
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    samp = args.cpu_sample if (world == 1 and not args.no_cpu) else 200_000
+    samp = min(samp, n)
+    hs = S.unpack_v4(s[:samp].cpu().numpy(), d[:samp].cpu().numpy(),
+                     p[:samp].cpu().numpy(), m[:samp].cpu().numpy())
+    orc = O.Oracle(tables)
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    c0 = time.perf_counter()
+    oa, ov, oi, lk = orc.classify(hs, mode, ep_lxc, nthreads=cores,
+                                  want_lookups=True)
+    cpu_s = time.perf_counter() - c0
+    # the timed region's last launch wrote `out` for this same batch
+    parity = bool(np.array_equal(out.verdict[:samp].cpu().numpy(), ov) and
+                  np.array_equal(out.identity[:samp].cpu().numpy().view(np.uint32), oi))
+    mean_l = float(lk.mean())
+    b_hdr = S_IN + S_OUT + 64.0 * mean_l
+    achieved = n * b_hdr / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            pm = json.load(open(tf))
+            if pm.get("headers") == n and pm.get("mode") == args.mode:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    res = {
+        "metric": "classified headers/sec (Mpps, whole node) at 100k-prefix "
+                  "ipcache + 16k-ID policy",
+        "value": round(mpps, 1),
+        "unit": "Mpps",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded C2 generator, SURVEY.md §8d)",
+        "config": {
+            "workload": "C2: 100k IPv4 /8-/32 ipcache prefixes + 16384-entry "
+                        "policymap + 25k /32 prefilter deny-list, "
+                        f"{n}-header batch per GPU, mode {args.mode}",
+            "headers_per_step_per_gpu": n,
+            "ipcache_prefixes": st["ipcache_v4_prefixes"],
+            "policy_entries": st["policy_entries"],
+            "prefilter_v4_fix": st["prefilter_v4_fix"],
+            "mode": args.mode,
+            "parallelism": f"header-stream shards x{world}, tables replicated",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "bytes_per_header": round(b_hdr, 2),
+            "mean_lookups_per_header": round(mean_l, 4),
+            "kernel_ms_per_launch": round(kern_ms, 4),
+        },
+        "cpu_baseline": None if (world > 1 or args.no_cpu) else {
+            "value": round(samp / cpu_s / 1e6, 3),
+            "unit": "Mpps",
+            "cores": cores,
+            "kind": "port",
+            "sample": f"first {samp} headers of the same stream through the C "
+                      f"restatement (oracle/cfc_oracle.c), {cores} OpenMP threads",
+        },
+        "parity_sample_ok": parity,
+    }
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

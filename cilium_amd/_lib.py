@@ -1,0 +1,94 @@
+"""ctypes binding of libcfc.so (include/cfc.h).
+
+The shared library is the product: there is no Python or CPU fallback for the
+datapath.  If it is missing this module raises at import of the binding.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcfc.so")
+
+CFC_DEVICE_NONE = -1
+MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
+HF_FRAG, HF_TCP_CLOSE = 0x100, 0x200
+DROP_PREFILTER = -1
+
+# every symbol include/cfc.h declares
+EXPORTS = (
+    "cfc_open", "cfc_close", "cfc_abi_version", "cfc_map_open",
+    "cfc_map_close", "cfc_map_update", "cfc_map_lookup", "cfc_map_delete",
+    "cfc_map_get_next_key", "cfc_num_possible_cpus", "cfc_endpoint_config",
+    "cfc_commit", "cfc_classify_v4", "cfc_counters_device",
+    "cfc_counters_sync", "cfc_counters_clear", "cfc_counters_export",
+    "cfc_counters_import", "cfc_get_stats", "cfc_strerror",
+)
+
+
+class CfcError(OSError):
+    pass
+
+
+class HdrV4(ctypes.Structure):
+    _fields_ = [("saddr", ctypes.c_void_p), ("daddr", ctypes.c_void_p),
+                ("ports", ctypes.c_void_p), ("meta", ctypes.c_void_p),
+                ("mark", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+
+
+class Out(ctypes.Structure):
+    _fields_ = [("verdict", ctypes.c_void_p), ("identity", ctypes.c_void_p),
+                ("action", ctypes.c_void_p)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("epoch", ctypes.c_uint64), ("device_bytes", ctypes.c_uint64),
+                ("ipcache_v4_prefixes", ctypes.c_uint32),
+                ("lpm4_tbl8_groups", ctypes.c_uint32),
+                ("policy_entries", ctypes.c_uint32),
+                ("endpoints", ctypes.c_uint32),
+                ("prefilter_v4_fix", ctypes.c_uint32),
+                ("prefilter_v4_dyn", ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CfcError(2, f"{LIB_PATH} is not built (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    pint = ctypes.POINTER(ctypes.c_int)
+    L.cfc_open.argtypes = [i32, ctypes.POINTER(vp)]
+    L.cfc_close.argtypes = [vp]
+    L.cfc_close.restype = None
+    L.cfc_map_open.argtypes = [vp, ctypes.c_char_p, u32, u32, u32, u32, u32,
+                               pint, pint]
+    L.cfc_map_close.argtypes = [vp, i32]
+    L.cfc_map_update.argtypes = [vp, i32, vp, vp, u64]
+    L.cfc_map_lookup.argtypes = [vp, i32, vp, vp]
+    L.cfc_map_delete.argtypes = [vp, i32, vp]
+    L.cfc_map_get_next_key.argtypes = [vp, i32, vp, vp]
+    L.cfc_endpoint_config.argtypes = [vp, ctypes.c_uint16, u32]
+    L.cfc_commit.argtypes = [vp, vp]
+    L.cfc_classify_v4.argtypes = [vp, ctypes.POINTER(HdrV4), ctypes.POINTER(Out),
+                                  i32, ctypes.c_uint16, vp]
+    L.cfc_counters_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
+    L.cfc_counters_sync.argtypes = [vp, vp]
+    L.cfc_counters_clear.argtypes = [vp, vp]
+    L.cfc_counters_export.argtypes = [vp, vp, u64, vp]
+    L.cfc_counters_import.argtypes = [vp, vp, u64, vp]
+    L.cfc_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.cfc_strerror.argtypes = [i32]
+    L.cfc_strerror.restype = ctypes.c_char_p
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    if rc < 0:
+        raise CfcError(-rc, f"{what}: {os.strerror(-rc)}")
+    return rc

@@ -1,0 +1,597 @@
+// C ABI of libcfc.so (include/cfc.h): context, BPF-map emulation, epoch
+// publication of the flattened tables, classify dispatch and counters.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cfc.h"
+#include "classify.hpp"
+#include "flatten.hpp"
+#include "maps.hpp"
+
+using namespace cfc;
+
+namespace {
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { reset(); }
+    void reset()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    int upload(const void *src, size_t n, hipStream_t s)
+    {
+        reset();
+        if (!n)
+            return 0;
+        if (hipMalloc(&p, n) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        bytes = n;
+        if (hipMemcpyAsync(p, src, n, hipMemcpyHostToDevice, s) != hipSuccess)
+            return -EIO;
+        return 0;
+    }
+};
+
+template <class T>
+static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
+{
+    return b.upload(v.data(), v.size() * sizeof(T), s);
+}
+
+struct Epoch {
+    uint64_t id = 0;
+    DevBuf tbl24, tbl8, ovf, pf24, pf8, pffix, lxc4, eps, pol;
+    DevTables T{};
+    std::unordered_map<int, PolLoc> pol_loc;
+    std::vector<std::pair<Map *, std::string>> ctr_owner;
+    cfc_stats st{};
+};
+
+}  // namespace
+
+struct cfc_ctx {
+    int device = 0;
+    int num_cus = 256;
+    std::recursive_mutex mu;
+    std::map<std::string, std::unique_ptr<Map>> maps;   // by path
+    std::map<int, Map *> fds;
+    int next_fd = 3;
+    std::vector<uint32_t> seclabel = std::vector<uint32_t>(65536, 0);
+    uint64_t seclabel_gen = 0;
+
+    std::unique_ptr<Epoch> epoch;
+    uint64_t epoch_seq = 0;
+    uint64_t built_sig = ~0ull;   // signature of the maps the epoch was built from
+
+    // counters: [n_ctr][2] u64 then metrics
+    uint64_t *ctr = nullptr;
+    size_t ctr_u64 = 0;
+    bool ctr_pending = false;
+    hipStream_t last_stream = nullptr;
+    hipEvent_t last_done = nullptr;
+    uint32_t *ws = nullptr;
+    size_t ws_bytes = 0;
+    Map *metrics = nullptr;
+};
+
+namespace {
+
+uint64_t tables_sig(cfc_ctx *c)
+{
+    uint64_t s = 1469598103934665603ull ^ c->seclabel_gen;
+    for (auto &kv : c->maps) {
+        if (kv.second->role == ROLE_NONE || kv.second->role == ROLE_METRICS)
+            continue;
+        s = (s ^ (uint64_t)(uintptr_t)kv.second.get()) * 1099511628211ull;
+        s = (s ^ kv.second->gen) * 1099511628211ull;
+        s = (s ^ kv.second->kv.size()) * 1099511628211ull;
+    }
+    return s;
+}
+
+int fold_counters(cfc_ctx *c, hipStream_t s)
+{
+    if (!c->ctr_pending || !c->epoch)
+        return 0;
+    std::vector<uint64_t> h(c->ctr_u64);
+    if (hipMemcpyAsync(h.data(), c->ctr, c->ctr_u64 * 8, hipMemcpyDeviceToHost,
+                       s) != hipSuccess)
+        return -EIO;
+    if (hipMemsetAsync(c->ctr, 0, c->ctr_u64 * 8, s) != hipSuccess)
+        return -EIO;
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    Epoch &E = *c->epoch;
+    size_t nctr = E.ctr_owner.size();
+    for (size_t i = 0; i < nctr; i++) {
+        uint64_t pk = h[2 * i], by = h[2 * i + 1];
+        if (!pk && !by)
+            continue;
+        Map *m = E.ctr_owner[i].first;
+        auto it = m->kv.find(E.ctr_owner[i].second);
+        if (it == m->kv.end())
+            continue;   // entry deleted since: the kernel's update is lost too
+        uint64_t v[2];
+        memcpy(v, &it->second.val[8], 16);
+        v[0] += pk;
+        v[1] += by;
+        memcpy(&it->second.val[8], v, 16);
+    }
+    const uint64_t *met = h.data() + 2 * nctr;
+    for (int r = 0; r < METRIC_REASONS; r++)
+        for (int d = 0; d < METRIC_DIRS; d++) {
+            uint64_t cnt = met[(r * METRIC_DIRS + d) * 2];
+            uint64_t byt = met[(r * METRIC_DIRS + d) * 2 + 1];
+            if (!cnt && !byt)
+                continue;
+            // struct metrics_key {u8 reason; u8 dir:2; u16 reserved[3]}
+            uint8_t key[8] = {(uint8_t)r, (uint8_t)d, 0, 0, 0, 0, 0, 0};
+            Map *mm = c->metrics;
+            std::string nk((const char *)key, 8);
+            auto it = mm->kv.find(nk);
+            uint64_t v[2] = {0, 0};
+            if (it != mm->kv.end())
+                memcpy(v, it->second.val.data(), 16);
+            v[0] += cnt;
+            v[1] += byt;
+            if (it == mm->kv.end() && mm->kv.size() >= mm->max_entries)
+                continue;   // map_update_elem fails in update_metrics too
+            Map::Entry &e = mm->kv[nk];
+            e.key = nk;
+            e.val.assign((const char *)v, 16);
+            mm->gen++;
+        }
+    c->ctr_pending = false;
+    return 0;
+}
+
+int commit_locked(cfc_ctx *c, hipStream_t s)
+{
+    uint64_t sig = tables_sig(c);
+    if (c->epoch && sig == c->built_sig)
+        return 0;
+    int rc = fold_counters(c, s);
+    if (rc)
+        return rc;
+    std::vector<Map *> ms;
+    for (auto &kv : c->maps)
+        ms.push_back(kv.second.get());
+    HostImage img;
+    build_image(ms, c->seclabel.data(), &img);
+
+    auto E = std::make_unique<Epoch>();
+    E->id = ++c->epoch_seq;
+    if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
+        (rc = upload_vec(E->ovf, img.lbl_ovf, s)) || (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
+        (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
+        (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->eps, img.eps, s)) ||
+        (rc = upload_vec(E->pol, img.pol, s)))
+        return rc;
+    DevTables &T = E->T;
+    T.tbl24 = (const uint32_t *)E->tbl24.p;
+    T.tbl8 = (const uint32_t *)E->tbl8.p;
+    T.lbl_ovf = (const uint32_t *)E->ovf.p;
+    T.pf_tbl24 = (const uint32_t *)E->pf24.p;
+    T.pf_tbl8 = (const uint32_t *)E->pf8.p;
+    T.pf_fix = (const uint32_t *)E->pffix.p;
+    T.pf_fix_mask = img.pf_fix_mask;
+    T.lxc4 = (const Lxc4Slot *)E->lxc4.p;
+    T.lxc4_mask = img.lxc4_mask;
+    T.n_eps = (uint32_t)img.eps.size();
+    T.eps = (const EpRec *)E->eps.p;
+    T.pol = (const PolSlot *)E->pol.p;
+    T.n_ctr = (uint32_t)img.ctr_owner.size();
+    E->pol_loc = img.pol_loc;
+    E->ctr_owner = img.ctr_owner;
+    E->st.epoch = E->id;
+    E->st.device_bytes = img.device_bytes();
+    E->st.ipcache_v4_prefixes = img.n_prefix4;
+    E->st.lpm4_tbl8_groups = (uint32_t)(img.tbl8.size() / 256);
+    E->st.policy_entries = T.n_ctr;
+    E->st.endpoints = T.n_eps;
+    E->st.prefilter_v4_fix = img.n_pf_fix;
+    E->st.prefilter_v4_dyn = img.n_pf_dyn;
+
+    // counters for the new entry layout (old ones were folded above)
+    size_t need = 2ull * T.n_ctr + METRIC_U64;
+    if (need != c->ctr_u64) {
+        if (c->ctr)
+            (void)hipFree(c->ctr);
+        c->ctr = nullptr;
+        if (hipMalloc((void **)&c->ctr, need * 8) != hipSuccess)
+            return -ENOMEM;
+        c->ctr_u64 = need;
+    }
+    if (hipMemsetAsync(c->ctr, 0, need * 8, s) != hipSuccess)
+        return -EIO;
+    // the host images must outlive the copies, and in-flight launches on
+    // other streams may still read the previous epoch: drain the device
+    if (hipDeviceSynchronize() != hipSuccess)
+        return -EIO;
+    c->epoch = std::move(E);
+    c->built_sig = sig;
+    return 0;
+}
+
+Map *get_map(cfc_ctx *c, int fd)
+{
+    auto it = c->fds.find(fd);
+    return it == c->fds.end() ? nullptr : it->second;
+}
+
+bool role_geometry_ok(Role r, uint32_t type, uint32_t ks, uint32_t vs)
+{
+    switch (r) {
+    case ROLE_IPCACHE: return type == MT_LPM_TRIE && ks == 24 && vs == 8;
+    case ROLE_LXC: return (type == MT_HASH) && ks == 20 && vs == 48;
+    case ROLE_POLICY: return type == MT_HASH && ks == 8 && vs == 24;
+    case ROLE_METRICS: return type == MT_PERCPU_HASH && ks == 8 && vs == 16;
+    case ROLE_PF4_FIX: return type == MT_HASH && ks == 8 && vs == 1;
+    case ROLE_PF4_DYN: return type == MT_LPM_TRIE && ks == 8 && vs == 1;
+    case ROLE_PF6_FIX: return type == MT_HASH && ks == 20 && vs == 1;
+    case ROLE_PF6_DYN: return type == MT_LPM_TRIE && ks == 20 && vs == 1;
+    default: return true;
+    }
+}
+
+// a write to a counter-bearing map must see the counts of every packet
+// classified before it (the kernel bumps them in place in the reference)
+int before_counter_write(cfc_ctx *c, Map *m)
+{
+    if (m->role == ROLE_POLICY || m->role == ROLE_METRICS)
+        return fold_counters(c, c->last_stream);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfc_abi_version(void) { return CFC_ABI_VERSION; }
+int cfc_num_possible_cpus(void) { return 1; }
+
+int cfc_open(int device, cfc_ctx **out)
+{
+    if (!out)
+        return -EINVAL;
+    if (device != CFC_DEVICE_NONE) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+            return -ENODEV;
+        if (device < 0 || device >= ndev)
+            return -ENODEV;
+        if (hipSetDevice(device) != hipSuccess)
+            return -ENODEV;
+    }
+    auto *c = new cfc_ctx();
+    c->device = device;
+    if (device != CFC_DEVICE_NONE) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, device) == hipSuccess &&
+            p.multiProcessorCount > 0)
+            c->num_cus = p.multiProcessorCount;
+        (void)hipEventCreateWithFlags(&c->last_done, hipEventDisableTiming);
+    }
+    // the datapath owns cilium_metrics (bpf/lib/maps.h:35-41)
+    auto m = std::make_unique<Map>();
+    m->name = "cilium_metrics";
+    m->role = ROLE_METRICS;
+    m->type = MT_PERCPU_HASH;
+    m->ksz = 8;
+    m->vsz = 16;
+    m->max_entries = 65536;  // METRICS_MAP_SIZE, node_config.h
+    c->metrics = m.get();
+    c->maps["cilium_metrics"] = std::move(m);
+    *out = c;
+    return 0;
+}
+
+void cfc_close(cfc_ctx *c)
+{
+    if (!c)
+        return;
+    if (c->device != CFC_DEVICE_NONE) {
+        (void)hipSetDevice(c->device);
+        (void)hipDeviceSynchronize();
+    }
+    c->epoch.reset();
+    if (c->ctr)
+        (void)hipFree(c->ctr);
+    if (c->ws)
+        (void)hipFree(c->ws);
+    if (c->last_done)
+        (void)hipEventDestroy(c->last_done);
+    delete c;
+}
+
+int cfc_map_open(cfc_ctx *c, const char *path, uint32_t type, uint32_t ks,
+                 uint32_t vs, uint32_t max_entries, uint32_t flags, int *fd,
+                 int *created)
+{
+    if (!c || !path || !fd)
+        return -EINVAL;
+    if (type != MT_HASH && type != MT_PERCPU_HASH && type != MT_LRU_HASH &&
+        type != MT_LPM_TRIE)
+        return -EINVAL;
+    if (!ks || !vs || !max_entries || (type == MT_LPM_TRIE && ks <= 4))
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    std::string p(path);
+    std::string base = p.substr(p.find_last_of('/') + 1);
+    int lxc = -1;
+    Role r = role_for(p, &lxc);
+    if (!role_geometry_ok(r, type, ks, vs))
+        return -EINVAL;
+    std::string key = r == ROLE_NONE ? p : base;
+    auto it = c->maps.find(key);
+    int was_created = 0;
+    Map *m;
+    if (it != c->maps.end()) {
+        m = it->second.get();
+        // objCheck (pkg/bpf/bpf.go:306): same geometry or refuse
+        if (m->type != type || m->ksz != ks || m->vsz != vs ||
+            (m->role != ROLE_METRICS && m->max_entries != max_entries))
+            return -EINVAL;
+    } else {
+        auto nm = std::make_unique<Map>();
+        nm->name = key;
+        nm->role = r;
+        nm->policy_lxc = lxc;
+        nm->type = type;
+        nm->ksz = ks;
+        nm->vsz = vs;
+        nm->max_entries = max_entries;
+        nm->flags = flags;
+        m = nm.get();
+        c->maps[key] = std::move(nm);
+        was_created = 1;
+    }
+    *fd = c->next_fd++;
+    c->fds[*fd] = m;
+    if (created)
+        *created = was_created;
+    return 0;
+}
+
+int cfc_map_close(cfc_ctx *c, int fd)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    return c->fds.erase(fd) ? 0 : -EBADF;
+}
+
+int cfc_map_update(cfc_ctx *c, int fd, const void *key, const void *value,
+                   uint64_t flags)
+{
+    if (!c || !key || !value)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Map *m = get_map(c, fd);
+    if (!m)
+        return -EBADF;
+    int rc = before_counter_write(c, m);
+    return rc ? rc : m->update(key, value, flags);
+}
+
+int cfc_map_lookup(cfc_ctx *c, int fd, const void *key, void *value)
+{
+    if (!c || !key || !value)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Map *m = get_map(c, fd);
+    return m ? m->lookup(key, value) : -EBADF;
+}
+
+int cfc_map_delete(cfc_ctx *c, int fd, const void *key)
+{
+    if (!c || !key)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Map *m = get_map(c, fd);
+    if (!m)
+        return -EBADF;
+    int rc = before_counter_write(c, m);
+    return rc ? rc : m->erase(key);
+}
+
+int cfc_map_get_next_key(cfc_ctx *c, int fd, const void *key, void *next)
+{
+    if (!c || !next)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Map *m = get_map(c, fd);
+    return m ? m->next_key(key, next) : -EBADF;
+}
+
+int cfc_endpoint_config(cfc_ctx *c, uint16_t lxc_id, uint32_t seclabel)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->seclabel[lxc_id] != seclabel) {
+        c->seclabel[lxc_id] = seclabel;
+        c->seclabel_gen++;
+    }
+    return 0;
+}
+
+int cfc_commit(cfc_ctx *c, void *stream)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    return commit_locked(c, (hipStream_t)stream);
+}
+
+int cfc_classify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream)
+{
+    if (!c || !in || !out || !out->verdict || !out->identity)
+        return -EINVAL;
+    if (in->n && (!in->saddr || !in->daddr || !in->ports || !in->meta))
+        return -EINVAL;
+    if (mode < CFC_MODE_INGRESS || mode > CFC_MODE_FULL)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    int rc = commit_locked(c, s);
+    if (rc)
+        return rc;
+    Epoch &E = *c->epoch;
+    EgressArgs ea{ep_lxc, c->seclabel[ep_lxc], 0, 0};
+    if (mode == CFC_MODE_EGRESS) {
+        auto it = E.pol_loc.find(ep_lxc);
+        if (it == E.pol_loc.end())
+            return -ENOENT;  // no endpoint program (policy map) for ep_lxc
+        ea.pol_base = it->second.base;
+        ea.pol_mask = it->second.mask;
+    }
+    size_t need = classify_workspace_bytes(in->n, E.T.n_ctr, c->num_cus);
+    if (need > c->ws_bytes) {
+        if (c->ws) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(c->ws);
+        }
+        c->ws = nullptr;
+        c->ws_bytes = 0;
+        if (hipMalloc((void **)&c->ws, need) != hipSuccess)
+            return -ENOMEM;
+        c->ws_bytes = need;
+    }
+    // the workspace is shared: order this launch after the previous one
+    if (c->ctr_pending && c->last_stream != s)
+        (void)hipStreamWaitEvent(s, c->last_done, 0);
+    rc = launch_classify_v4(E.T, *in, *out, mode, ea, c->ctr,
+                            c->ctr + 2ull * E.T.n_ctr, c->ws, c->num_cus, s);
+    if (rc)
+        return rc;
+    (void)hipEventRecord(c->last_done, s);
+    c->last_stream = s;
+    c->ctr_pending = true;
+    return 0;
+}
+
+int cfc_counters_device(cfc_ctx *c, uint64_t **dev, uint64_t *n)
+{
+    if (!c || !dev || !n)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    int rc = commit_locked(c, c->last_stream);
+    if (rc)
+        return rc;
+    *dev = c->ctr;
+    *n = c->ctr_u64;
+    c->ctr_pending = true;  // the caller may write (all-reduce) into it
+    return 0;
+}
+
+int cfc_counters_sync(cfc_ctx *c, void *stream)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    return fold_counters(c, (hipStream_t)stream);
+}
+
+int cfc_counters_clear(cfc_ctx *c, void *stream)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    if (c->ctr && hipMemsetAsync(c->ctr, 0, c->ctr_u64 * 8,
+                                 (hipStream_t)stream) != hipSuccess)
+        return -EIO;
+    c->ctr_pending = false;
+    return 0;
+}
+
+int cfc_counters_export(cfc_ctx *c, uint64_t *dst, uint64_t n, void *stream)
+{
+    if (!c || !dst)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    int rc = commit_locked(c, (hipStream_t)stream);
+    if (rc)
+        return rc;
+    if (n != c->ctr_u64)
+        return -EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (c->ctr_pending && c->last_stream != s)
+        (void)hipStreamWaitEvent(s, c->last_done, 0);
+    if (hipMemcpyAsync(dst, c->ctr, n * 8, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        hipMemsetAsync(c->ctr, 0, n * 8, s) != hipSuccess)
+        return -EIO;
+    (void)hipEventRecord(c->last_done, s);
+    c->last_stream = s;
+    return 0;
+}
+
+int cfc_counters_import(cfc_ctx *c, const uint64_t *src, uint64_t n,
+                        void *stream)
+{
+    if (!c || !src)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    if (!c->epoch || n != c->ctr_u64)
+        return -EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (c->last_stream != s)
+        (void)hipStreamWaitEvent(s, c->last_done, 0);
+    int rc = launch_add_u64(c->ctr, src, n, s);
+    if (rc)
+        return rc;
+    (void)hipEventRecord(c->last_done, s);
+    c->last_stream = s;
+    c->ctr_pending = true;
+    return 0;
+}
+
+int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
+{
+    if (!c || !st)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (!c->epoch)
+        return -ENOENT;
+    *st = c->epoch->st;
+    return 0;
+}
+
+const char *cfc_strerror(int err)
+{
+    return strerror(err < 0 ? -err : err);
+}
+
+}  // extern "C"

@@ -1,0 +1,266 @@
+#include "flatten.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+
+namespace cfc {
+
+static uint32_t pow2_at_least(uint64_t x)
+{
+    uint32_t p = 1;
+    while (p < x)
+        p <<= 1;
+    return p;
+}
+
+uint64_t HostImage::device_bytes() const
+{
+    return 4ull * (tbl24.size() + tbl8.size() + lbl_ovf.size() +
+                   pf_tbl24.size() + pf_tbl8.size() + pf_fix.size()) +
+           sizeof(Lxc4Slot) * lxc4.size() + sizeof(EpRec) * eps.size() +
+           sizeof(PolSlot) * pol.size();
+}
+
+// DIR-24-8: every prefix <= /24 fills its tbl24 range in ascending length
+// order (longer prefixes overwrite), then every /25../32 expands its /24 into
+// a 256-entry tbl8 group seeded with the covering value.
+void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
+                   std::vector<uint32_t> *tbl8)
+{
+    std::stable_sort(pfx.begin(), pfx.end(),
+                     [](const Pfx4 &a, const Pfx4 &b) { return a.plen < b.plen; });
+    tbl24->assign(1u << 24, 0);
+    tbl8->clear();
+    uint32_t *t24 = tbl24->data();
+    for (const Pfx4 &p : pfx) {
+        if (p.plen > 24)
+            break;
+        uint32_t start = p.plen ? (p.addr >> 8) & ~((1u << (24 - p.plen)) - 1) : 0;
+        std::fill(t24 + start, t24 + start + (1u << (24 - p.plen)), p.leaf);
+    }
+    for (const Pfx4 &p : pfx) {
+        if (p.plen <= 24)
+            continue;
+        uint32_t idx = p.addr >> 8;
+        if (!(t24[idx] & LPM_GROUP)) {
+            uint32_t g = (uint32_t)(tbl8->size() >> 8);
+            tbl8->resize(tbl8->size() + 256, t24[idx]);
+            t24[idx] = LPM_GROUP | g;
+        }
+        uint32_t g = t24[idx] & ~LPM_GROUP;
+        uint32_t lo = p.addr & 0xFF & ~((1u << (32 - p.plen)) - 1);
+        uint32_t *grp = tbl8->data() + ((size_t)g << 8);
+        std::fill(grp + lo, grp + lo + (1u << (32 - p.plen)), p.leaf);
+    }
+}
+
+static uint32_t leaf_for(uint32_t label, std::vector<uint32_t> *ovf)
+{
+    if (label < LPM_INDIRECT)
+        return label;
+    ovf->push_back(label);
+    return LPM_INDIRECT | (uint32_t)(ovf->size() - 1);
+}
+
+static inline uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// Effective IPv4 prefixes of the ipcache LPM map.  A datapath v4 lookup key
+// is {prefixlen 64, pad 0,0, family 1, addr, zeros} (eps.h:70-80); a stored
+// entry with total prefixlen P matches iff P <= 64 and its first P bits agree,
+// so entries with P <= 32 whose static bits agree act as v4 /0.  Among
+// entries collapsing onto the same v4 prefix the longest P wins (trie).
+static void ipcache_v4(const Map *m, std::vector<Pfx4> *out,
+                       std::vector<uint32_t> *ovf)
+{
+    static const uint8_t stat4[4] = {0, 0, 0, 1};
+    std::map<std::pair<uint32_t, int>, std::pair<uint32_t, uint32_t>> best;
+    for (const auto &kv : m->kv) {
+        const uint8_t *k = (const uint8_t *)kv.first.data();  // normalised
+        uint32_t P;
+        memcpy(&P, k, 4);
+        if (P > 64)
+            continue;
+        bool ok = true;
+        for (uint32_t bit = 0; bit < std::min<uint32_t>(P, 32); bit++) {
+            uint32_t byte = bit >> 3, sh = 7 - (bit & 7);
+            if (((k[4 + byte] >> sh) & 1) != ((stat4[byte] >> sh) & 1)) {
+                ok = false;
+                break;
+            }
+        }
+        if (!ok)
+            continue;
+        int plen = P > 32 ? (int)(P - 32) : 0;
+        uint32_t a;
+        memcpy(&a, k + 8, 4);  // already masked by norm()
+        uint32_t label;
+        memcpy(&label, kv.second.val.data(), 4);
+        auto key = std::make_pair(bswap(a), plen);
+        auto it = best.find(key);
+        if (it == best.end() || it->second.first < P)
+            best[key] = {P, label};
+    }
+    for (const auto &b : best)
+        out->push_back({b.first.first, (uint8_t)b.first.second,
+                        leaf_for(b.second.second, ovf)});
+}
+
+void build_image(const std::vector<Map *> &maps, const uint32_t *seclabel,
+                 HostImage *img)
+{
+    *img = HostImage();
+    const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,
+              *pf4dyn = nullptr;
+    std::map<int, Map *> pols;
+    for (Map *m : maps) {
+        switch (m->role) {
+        case ROLE_IPCACHE: ipc = m; break;
+        case ROLE_LXC: lxc = m; break;
+        case ROLE_PF4_FIX: pf4fix = m; break;
+        case ROLE_PF4_DYN: pf4dyn = m; break;
+        case ROLE_POLICY: pols[m->policy_lxc] = m; break;
+        default: break;
+        }
+    }
+
+    // ---- ipcache v4
+    if (ipc) {
+        std::vector<Pfx4> pfx;
+        ipcache_v4(ipc, &pfx, &img->lbl_ovf);
+        img->n_prefix4 = (uint32_t)pfx.size();
+        if (!pfx.empty())
+            build_dir24_8(pfx, &img->tbl24, &img->tbl8);
+    }
+
+    // ---- prefilter
+    if (pf4dyn && pf4dyn->ksz == 8) {
+        std::vector<Pfx4> pfx;
+        for (const auto &kv : pf4dyn->kv) {
+            const uint8_t *k = (const uint8_t *)kv.first.data();
+            uint32_t P, a;
+            memcpy(&P, k, 4);
+            memcpy(&a, k + 4, 4);
+            pfx.push_back({bswap(a), (uint8_t)P, 1u});
+        }
+        img->n_pf_dyn = (uint32_t)pfx.size();
+        if (!pfx.empty())
+            build_dir24_8(pfx, &img->pf_tbl24, &img->pf_tbl8);
+    }
+    if (pf4fix && pf4fix->ksz == 8) {
+        std::vector<uint32_t> addrs;
+        for (const auto &kv : pf4fix->kv) {
+            const uint8_t *k = (const uint8_t *)kv.first.data();
+            uint32_t P, a;
+            memcpy(&P, k, 4);
+            memcpy(&a, k + 4, 4);
+            if (P == 32)  // check_v4 looks up {prefixlen 32, saddr} exactly
+                addrs.push_back(a);
+        }
+        img->n_pf_fix = (uint32_t)addrs.size();
+        if (!addrs.empty()) {
+            uint32_t nb = pow2_at_least((addrs.size() * 2 + PF_SLOTS - 1) / PF_SLOTS);
+            img->pf_fix.assign((size_t)nb * 16, 0);
+            img->pf_fix_mask = nb - 1;
+            for (uint32_t a : addrs) {
+                uint32_t b = hash32(a, nb - 1);
+                while (img->pf_fix[(size_t)b * 16 + 15] == PF_SLOTS)
+                    b = (b + 1) & (nb - 1);
+                uint32_t *bk = &img->pf_fix[(size_t)b * 16];
+                bk[bk[15]++] = a;
+            }
+        }
+    }
+
+    // ---- policy tables (deterministic: ascending lxc id, key order)
+    for (auto &pm : pols) {
+        Map *m = pm.second;
+        PolLoc loc;
+        loc.present = 1;
+        uint32_t n = (uint32_t)m->kv.size();
+        uint32_t nb = pow2_at_least(std::max<uint64_t>(1, (n * 2 + POL_SLOTS - 1) / POL_SLOTS));
+        if (nb < 2 && n)
+            nb = 2;
+        loc.base = (uint32_t)(img->pol.size() / POL_SLOTS);
+        loc.mask = nb - 1;
+        PolSlot empty{};
+        empty.ctr = EMPTY;
+        img->pol.resize(img->pol.size() + (size_t)nb * POL_SLOTS, empty);
+        PolSlot *tab = img->pol.data() + (size_t)loc.base * POL_SLOTS;
+        for (const auto &kv : m->kv) {
+            uint64_t key;
+            memcpy(&key, kv.first.data(), 8);
+            uint16_t proxy;
+            memcpy(&proxy, kv.second.val.data(), 2);
+            uint32_t b = hash64(key, loc.mask);
+            for (;;) {
+                PolSlot *bk = tab + (size_t)b * POL_SLOTS;
+                int s = 0;
+                while (s < POL_SLOTS && bk[s].ctr != EMPTY)
+                    s++;
+                if (s < POL_SLOTS) {
+                    bk[s].key = key;
+                    bk[s].proxy_port = proxy;
+                    bk[s].ctr = (uint32_t)img->ctr_owner.size();
+                    img->ctr_owner.emplace_back(m, kv.first);
+                    break;
+                }
+                b = (b + 1) & loc.mask;
+            }
+        }
+        img->pol_loc[pm.first] = loc;
+    }
+
+    // ---- endpoints (cilium_lxc): IPv4 keys {ip4, 0 x12, family 1, 0, 0}
+    if (lxc && lxc->ksz == 20 && lxc->vsz >= 12) {
+        std::vector<std::pair<uint32_t, uint32_t>> v4;  // addr, ep index
+        for (const auto &kv : lxc->kv) {
+            const uint8_t *k = (const uint8_t *)kv.first.data();
+            const uint8_t *v = (const uint8_t *)kv.second.val.data();
+            EpRec r{};
+            memcpy(&r.ifindex, v, 4);
+            uint16_t id;
+            memcpy(&id, v + 6, 2);
+            r.lxc_id = id;
+            memcpy(&r.flags, v + 8, 4);
+            r.seclabel = seclabel[id];
+            auto it = img->pol_loc.find(id);
+            if (it != img->pol_loc.end()) {
+                r.pol_base = it->second.base;
+                r.pol_mask = it->second.mask;
+                r.has_policy = 1;
+            }
+            bool is_v4 = k[16] == 1 && k[17] == 0 && k[18] == 0 && k[19] == 0;
+            for (int i = 4; i < 16 && is_v4; i++)
+                is_v4 = k[i] == 0;
+            if (!is_v4)
+                continue;  // IPv6 endpoints: next step of the build
+            uint32_t a;
+            memcpy(&a, k, 4);
+            v4.emplace_back(a, (uint32_t)img->eps.size());
+            img->eps.push_back(r);
+        }
+        if (!v4.empty()) {
+            uint32_t nb = pow2_at_least((v4.size() * 2 + LXC_SLOTS - 1) / LXC_SLOTS);
+            Lxc4Slot empty{0, EMPTY};
+            img->lxc4.assign((size_t)nb * LXC_SLOTS, empty);
+            img->lxc4_mask = nb - 1;
+            for (auto &e : v4) {
+                uint32_t b = hash32(e.first, nb - 1);
+                for (;;) {
+                    Lxc4Slot *bk = &img->lxc4[(size_t)b * LXC_SLOTS];
+                    int s = 0;
+                    while (s < LXC_SLOTS && bk[s].ep != EMPTY)
+                        s++;
+                    if (s < LXC_SLOTS) {
+                        bk[s] = {e.first, e.second};
+                        break;
+                    }
+                    b = (b + 1) & (nb - 1);
+                }
+            }
+        }
+    }
+}
+
+}  // namespace cfc

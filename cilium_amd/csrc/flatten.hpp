@@ -1,0 +1,51 @@
+// Flattening of the host maps into the device layouts of layout.h.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "layout.h"
+#include "maps.hpp"
+
+namespace cfc {
+
+struct PolLoc {
+    uint32_t base = 0, mask = 0, present = 0;
+};
+
+struct HostImage {
+    // IPv4 ipcache, DIR-24-8
+    std::vector<uint32_t> tbl24, tbl8, lbl_ovf;
+    uint32_t n_prefix4 = 0;
+    // prefilter
+    std::vector<uint32_t> pf_tbl24, pf_tbl8;
+    uint32_t n_pf_dyn = 0;
+    std::vector<uint32_t> pf_fix;
+    uint32_t pf_fix_mask = 0, n_pf_fix = 0;
+    // endpoints
+    std::vector<Lxc4Slot> lxc4;
+    uint32_t lxc4_mask = 0;
+    std::vector<EpRec> eps;
+    // policy
+    std::vector<PolSlot> pol;
+    std::unordered_map<int, PolLoc> pol_loc;       // lxc_id -> table
+    std::vector<std::pair<Map *, std::string>> ctr_owner;  // ctr -> entry
+    uint64_t device_bytes() const;
+};
+
+// maps: every map of the context.  seclabel: per-lxc SECLABEL.
+void build_image(const std::vector<Map *> &maps, const uint32_t *seclabel,
+                 HostImage *img);
+
+// exposed for host-side unit tests of the DIR-24-8 builder
+struct Pfx4 {
+    uint32_t addr;   // host byte order
+    uint8_t plen;
+    uint32_t leaf;   // encoded LPM leaf
+};
+void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
+                   std::vector<uint32_t> *tbl8);
+
+}  // namespace cfc

@@ -1,0 +1,63 @@
+// Host mirror of the BPF maps behind the C ABI.
+//
+// Semantics follow the kernel map types the reference uses through pkg/bpf
+// (pkg/bpf/bpf.go:108-252): HASH (kernel/bpf/hashtab.c: -E2BIG when full,
+// BPF_NOEXIST/-EEXIST, BPF_EXIST/-ENOENT), LRU_HASH (evicts instead of
+// failing), PERCPU_HASH (one CPU slot here), LPM_TRIE (kernel/bpf/lpm_trie.c:
+// key = u32 prefixlen + data, -ENOSPC when full, lookups are longest-prefix
+// matches bounded by the key's prefixlen, data bits past prefixlen ignored).
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+
+namespace cfc {
+
+enum MapType : uint32_t {
+    MT_HASH = 1,
+    MT_PERCPU_HASH = 5,
+    MT_LRU_HASH = 9,
+    MT_LPM_TRIE = 11,
+};
+
+enum Role {
+    ROLE_NONE = 0,
+    ROLE_IPCACHE,   // cilium_ipcache
+    ROLE_LXC,       // cilium_lxc
+    ROLE_POLICY,    // cilium_policy_<lxc_id>
+    ROLE_METRICS,   // cilium_metrics
+    ROLE_PF4_FIX,   // cilium_cidr_v4_fix
+    ROLE_PF4_DYN,   // cilium_cidr_v4_dyn
+    ROLE_PF6_FIX,   // cilium_cidr_v6_fix
+    ROLE_PF6_DYN,   // cilium_cidr_v6_dyn
+};
+
+struct Map {
+    std::string name;
+    Role role = ROLE_NONE;
+    int policy_lxc = -1;
+    uint32_t type = 0, ksz = 0, vsz = 0, max_entries = 0, flags = 0;
+    uint64_t gen = 0;   // bumped on every mutation
+
+    struct Entry {
+        std::string key;  // key bytes as last written
+        std::string val;
+    };
+    // ordered by normalised key -> deterministic iteration and flattening
+    std::map<std::string, Entry> kv;
+
+    bool lpm() const { return type == MT_LPM_TRIE; }
+    uint32_t value_bytes() const;  // per-CPU rounded for PERCPU maps
+    // normalised key: raw for hashes; prefixlen + masked data for LPM.
+    // Returns false for an invalid LPM key (prefixlen too large).
+    bool norm(const uint8_t *k, std::string *out) const;
+
+    int update(const void *key, const void *value, uint64_t flags);
+    int lookup(const void *key, void *value) const;
+    int erase(const void *key);
+    int next_key(const void *key, void *next) const;
+};
+
+Role role_for(const std::string &path, int *policy_lxc);
+
+}  // namespace cfc

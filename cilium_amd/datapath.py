@@ -1,0 +1,215 @@
+"""Datapath: one libcfc context (one GPU) seen from Python.
+
+Two halves, as in include/cfc.h:
+  * the pkg/bpf-shaped map API (`open_or_create_map`, `update_element`, ...)
+    that pkg/maps/* mirrors in this package build on;
+  * `classify_v4`, the batched replacement of the reference's per-packet
+    programs, over torch tensors resident on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+
+from . import _lib as L
+
+
+@dataclasses.dataclass
+class HeaderBatchV4:
+    """Device SoA batch (all torch int32 tensors on the same GPU)."""
+    saddr: "torch.Tensor"
+    daddr: "torch.Tensor"
+    ports: "torch.Tensor"     # sport | dport << 16 (be16 raw each)
+    meta: "torch.Tensor"      # proto | flags << 8 | len << 16
+    mark: "torch.Tensor | None" = None
+
+    def __len__(self):
+        return int(self.saddr.numel())
+
+
+@dataclasses.dataclass
+class Verdicts:
+    verdict: "torch.Tensor"   # int32
+    identity: "torch.Tensor"  # int32 (u32 bits)
+    action: "torch.Tensor | None"  # uint8
+
+
+def pack_v4(h, device="cuda"):
+    """synth.Headers (numpy) -> HeaderBatchV4 on `device`."""
+    import numpy as np
+    import torch
+    ports = (h.sport.astype(np.uint32) | (h.dport.astype(np.uint32) << 16))
+    meta = (h.proto.astype(np.uint32) | (h.flags.astype(np.uint32) << 8)
+            | (h.length.astype(np.uint32) << 16))
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32)
+                                .view(np.int32)).to(device)
+    return HeaderBatchV4(t(h.saddr), t(h.daddr), t(ports), t(meta),
+                         t(h.mark) if h.mark is not None else None)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    if isinstance(stream, int):
+        return ctypes.c_void_p(stream)
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+class Datapath:
+    def __init__(self, device: int = 0):
+        self.L = L.lib()
+        self.device = device
+        self.h = ctypes.c_void_p()
+        L.check(self.L.cfc_open(device, ctypes.byref(self.h)), "cfc_open")
+        self._vsz = {}
+        self._ksz = {}
+
+    def close(self):
+        if self.h:
+            self.L.cfc_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------ pkg/bpf mirror
+    def open_or_create_map(self, path, map_type, key_size, value_size,
+                           max_entries, flags=0):
+        """bpf.OpenOrCreateMap (pkg/bpf/bpf.go:371) -> (fd, is_new)."""
+        fd, created = ctypes.c_int(), ctypes.c_int()
+        L.check(self.L.cfc_map_open(self.h, path.encode(), map_type, key_size,
+                                    value_size, max_entries, flags,
+                                    ctypes.byref(fd), ctypes.byref(created)),
+                f"open map {path}")
+        self._ksz[fd.value] = key_size
+        self._vsz[fd.value] = value_size if map_type != 5 else ((value_size + 7) & ~7)
+        return fd.value, bool(created.value)
+
+    def update_element(self, fd, key: bytes, value: bytes, flags=0):
+        """bpf.UpdateElement (pkg/bpf/bpf.go:153)."""
+        L.check(self.L.cfc_map_update(self.h, fd, key, value, flags),
+                "update element")
+
+    def lookup_element(self, fd, key: bytes):
+        """bpf.LookupElement (pkg/bpf/bpf.go:177) -> value bytes or None."""
+        buf = ctypes.create_string_buffer(self._vsz[fd])
+        rc = self.L.cfc_map_lookup(self.h, fd, key, buf)
+        if rc == -2:  # ENOENT
+            return None
+        L.check(rc, "lookup element")
+        return buf.raw
+
+    def delete_element(self, fd, key: bytes):
+        """bpf.DeleteElement (pkg/bpf/bpf.go:214)."""
+        L.check(self.L.cfc_map_delete(self.h, fd, key), "delete element")
+
+    def get_next_key(self, fd, key: bytes | None):
+        """bpf.GetNextKey (pkg/bpf/bpf.go:225) -> next key or None at end."""
+        buf = ctypes.create_string_buffer(self._ksz[fd])
+        rc = self.L.cfc_map_get_next_key(self.h, fd, key, buf)
+        if rc == -2:
+            return None
+        L.check(rc, "get next key")
+        return buf.raw
+
+    def keys(self, fd):
+        out, k = [], None
+        while True:
+            k = self.get_next_key(fd, k)
+            if k is None:
+                return out
+            out.append(k)
+
+    def obj_close(self, fd):
+        L.check(self.L.cfc_map_close(self.h, fd), "close map")
+
+    def endpoint_config(self, lxc_id, seclabel):
+        L.check(self.L.cfc_endpoint_config(self.h, lxc_id, seclabel),
+                "endpoint config")
+
+    # ------------------------------------------------ datapath
+    def _stream(self, stream):
+        if self.device == L.CFC_DEVICE_NONE:
+            return ctypes.c_void_p()
+        return _stream_handle(stream)
+
+    def commit(self, stream=None):
+        L.check(self.L.cfc_commit(self.h, self._stream(stream)),"commit")
+
+    def classify_v4(self, batch: HeaderBatchV4, mode=L.MODE_INGRESS, ep_lxc=0,
+                    out: Verdicts | None = None, want_action=True,
+                    stream=None) -> Verdicts:
+        import torch
+        n = len(batch)
+        dev = batch.saddr.device
+        if out is None:
+            out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
+                           torch.empty(n, dtype=torch.int32, device=dev),
+                           torch.empty(n, dtype=torch.uint8, device=dev)
+                           if want_action else None)
+        for t in (batch.saddr, batch.daddr, batch.ports, batch.meta):
+            assert t.is_cuda and t.is_contiguous() and t.numel() == n
+            assert t.dtype == torch.int32
+        if batch.mark is not None:
+            assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
+        hdr = L.HdrV4(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+                      _ptr(batch.meta), _ptr(batch.mark), n)
+        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action))
+        L.check(self.L.cfc_classify_v4(self.h, ctypes.byref(hdr),
+                                       ctypes.byref(o), mode, ep_lxc,
+                                       self._stream(stream)),"classify")
+        return out
+
+    def counters_sync(self, stream=None):
+        L.check(self.L.cfc_counters_sync(self.h, self._stream(stream)),
+                "counters sync")
+
+    def counters_clear(self, stream=None):
+        L.check(self.L.cfc_counters_clear(self.h, self._stream(stream)),
+                "counters clear")
+
+    def counters_export(self, t, stream=None):
+        """Move the device counter block into int64 tensor `t` (zeroing it)."""
+        L.check(self.L.cfc_counters_export(self.h, _ptr(t), t.numel(),
+                                           self._stream(stream)), "export")
+
+    def counters_import(self, t, stream=None):
+        """Add int64 tensor `t` (e.g. an all-reduced block) into the counters."""
+        L.check(self.L.cfc_counters_import(self.h, _ptr(t), t.numel(),
+                                           self._stream(stream)), "import")
+
+    def counters_device(self):
+        """(device pointer, number of u64) of the live counter block."""
+        p, n = ctypes.c_void_p(), ctypes.c_uint64()
+        L.check(self.L.cfc_counters_device(self.h, ctypes.byref(p),
+                                           ctypes.byref(n)), "counters device")
+        return p.value, n.value
+
+    def stats(self):
+        st = L.Stats()
+        L.check(self.L.cfc_get_stats(self.h, ctypes.byref(st)), "stats")
+        return {f: getattr(st, f) for f, _ in L.Stats._fields_}
+
+
+def host_only():
+    """A context with the map API only (no GPU): control-plane tooling."""
+    return Datapath(L.CFC_DEVICE_NONE)
+
+
+def errno_name(e: OSError):
+    import errno
+    return errno.errorcode.get(e.errno, str(e.errno))
+
+
+__all__ = ["Datapath", "HeaderBatchV4", "Verdicts", "pack_v4", "host_only",
+           "errno_name"]

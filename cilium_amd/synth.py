@@ -322,3 +322,98 @@ def headers_c2(t: Tables, n, seed=2, **kw):
     rng = np.random.default_rng(seed + 1000)
     return gen_headers_v4(rng, n, t.ipcache, local_v4_addrs(t),
                           proxy_ident=proxy_identities(t), **kw)
+
+
+# ------------------------------------------------------- device generator
+def gen_batch_v4_torch(t: Tables, n, seed, device, in_prefix=0.9,
+                       local_frac=0.97, deny_frac=0.02, frag=0.01):
+    """C2/C4 header batch generated directly on the GPU in the packed SoA
+    form of cfc_hdr_v4 (saddr, daddr, ports, meta), same distribution as
+    gen_headers_v4: 90% sources inside a random ipcache
+    prefix, the rest uniform; 97% destinations on a local endpoint; TCP 70% /
+    UDP 25% / ICMP 5% (+0.5% other protocols); 60% of dports from the policy
+    port set; 1% fragments; len U[60,1500].  `deny_frac` of the sources are
+    taken from the prefilter's /32 deny set when one is configured."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    i64 = torch.int64
+
+    def rint(lo, hi, size=n):
+        return torch.randint(lo, hi, (size,), generator=g, device=device, dtype=i64)
+
+    def rnd(size=n):
+        return torch.rand((size,), generator=g, device=device)
+
+    def bswap(x):
+        return (((x & 0xFF) << 24) | ((x & 0xFF00) << 8) | ((x >> 8) & 0xFF00)
+                | ((x >> 24) & 0xFF))
+
+    ipc = t.ipcache[t.ipcache["family"] == 1]
+    base = torch.from_numpy(byteswap32(ipc["addr"][:, :4].copy().view("<u4")
+                                       .ravel()).astype(np.int64)).to(device)
+    plen = torch.from_numpy(ipc["plen"].astype(np.int64)).to(device)
+    pick = rint(0, len(ipc))
+    host = base[pick] | (rint(0, 1 << 32) & ((1 << (32 - plen[pick])) - 1))
+    host = torch.where(rnd() < in_prefix, host, rint(0, 1 << 32))
+    pf = t.prefilter
+    fix = pf[(pf["family"] == 1) & (pf["dyn"] == 0) & (pf["plen"] == 32)] if len(pf) else pf
+    if len(fix) and deny_frac > 0:
+        deny = torch.from_numpy(byteswap32(fix["addr"][:, :4].copy().view("<u4")
+                                           .ravel()).astype(np.int64)).to(device)
+        host = torch.where(rnd() < deny_frac, deny[rint(0, len(fix))], host)
+    saddr = bswap(host)
+    eps = t.endpoints[(t.endpoints["family"] == 1) & ((t.endpoints["flags"] & 1) == 0)]
+    loc = torch.from_numpy(eps["addr"][:, :4].copy().view("<u4").ravel()
+                           .astype(np.int64)).to(device)
+    daddr = torch.where(rnd() < local_frac, loc[rint(0, len(loc))],
+                        rint(0, 1 << 32))
+    r = rnd()
+    proto = torch.where(r < 0.70, 6, torch.where(r < 0.95, 17, 1))
+    proto = torch.where(rnd() < 0.005, 47, proto)
+    ports_set = torch.from_numpy(PORT_SET.astype(np.int64)).to(device)
+    dp = torch.where(rnd() < 0.6, ports_set[rint(0, len(PORT_SET))], rint(1, 65536))
+    sp = rint(32768, 65536)
+
+    def hs(x):
+        return ((x & 0xFF) << 8) | ((x >> 8) & 0xFF)
+    ports = hs(sp) | (hs(dp) << 16)
+    itype = torch.tensor([0, 8, 8, 8, 3, 11, 13], device=device, dtype=i64)[rint(0, 7)]
+    ports = torch.where(proto == 1, itype | (rint(0, 65536) << 16), ports)
+    flags = (rnd() < frag).to(i64) * HF_FRAG
+    flags |= ((proto == 6) & (rnd() < 0.02)).to(i64) * HF_TCP_CLOSE
+    minlen = torch.where(proto == 6, 54, 42)
+    length = torch.maximum(rint(60, 1501), minlen)
+    meta = proto | (flags << 8) | (length << 16)
+
+    def i32(x):
+        return (x & 0xFFFFFFFF).to(torch.int64).sub_(
+            ((x & 0xFFFFFFFF) >= (1 << 31)).to(i64) << 32).to(torch.int32)
+    return i32(saddr), i32(daddr), i32(ports), i32(meta)
+
+
+def unpack_v4(saddr, daddr, ports, meta, mark=None) -> Headers:
+    """Packed numpy int32/uint32 SoA -> Headers (for the oracle)."""
+    u = lambda a: np.ascontiguousarray(a).view(np.uint32)   # noqa: E731
+    s, d, p, m = u(saddr), u(daddr), u(ports), u(meta)
+    return Headers(4, s, d, (p & 0xFFFF).astype(np.uint16),
+                   (p >> 16).astype(np.uint16), (m & 0xFF).astype(np.uint8),
+                   ((m >> 8) & 0xFF).astype(np.uint8),
+                   (m >> 16).astype(np.uint16),
+                   u(mark) if mark is not None else np.zeros(len(s), np.uint32))
+
+
+def config_c2_bench(seed=2, n_prefilter=25_000):
+    """The bench tables: C2 (100k prefixes, 16k-entry policymap) plus a
+    production-shaped prefilter (fixed /32 deny-list only, dyn disabled as
+    in pkg/policy/prefilter.go:282-289)."""
+    t = config_c2(seed)
+    rng = np.random.default_rng(seed + 500)
+    host = np.unique(rng.integers(1 << 24, 224 << 24, size=n_prefilter,
+                                  dtype=np.uint64).astype(np.uint32))
+    pf = np.zeros(len(host), PREFILTER_DT)
+    pf["family"] = 1
+    pf["plen"] = 32
+    pf["addr"][:, :4] = be32_to_bytes(byteswap32(host))
+    t.prefilter = pf
+    return t

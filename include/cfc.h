@@ -1,0 +1,191 @@
+/*
+ * cfc.h — C ABI of the MI355X flow-classification engine (libcfc.so).
+ *
+ * This is the drop-in boundary for Cilium's datapath verdict path.  The
+ * map-population half mirrors pkg/bpf's fd-based BPF map API one call for
+ * one call, with the reference's key/value byte layouts, so pkg/maps/
+ * {policymap,ipcache,lxcmap,cidrmap,metricsmap} and pkg/policy/prefilter.go
+ * work unchanged on top of a thin cgo shim.  The datapath
+ * half replaces the per-packet BPF programs (bpf_xdp.c, bpf_netdev.c,
+ * bpf_lxc.c) by one batched call over SoA header arrays resident in HBM.
+ *
+ * Conventions
+ *  - every function returns 0 or a negative errno (-ENOENT, -EEXIST,
+ *    -E2BIG, -ENOSPC, -EINVAL, -ENOMEM, -EBADF, -ENODEV); nothing aborts.
+ *  - key/value buffers are caller-owned and copied (pkg/bpf/bpf.go:153-252).
+ *  - all mutators and cfc_classify are thread-safe; a table change becomes
+ *    visible to the next cfc_classify (auto-commit) or at cfc_commit().
+ *    Work already queued on a stream keeps reading the previous epoch.
+ *  - addresses/ports are raw network-order bytes loaded little-endian
+ *    ("be32"/"be16" raw), identities are host-order u32.
+ */
+#ifndef CFC_H
+#define CFC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFC_ABI_VERSION 1
+
+typedef struct cfc_ctx cfc_ctx;
+
+/* ------------------------------------------------------------------ context */
+/* One context per GPU (device ordinal).  Tables are replicated per context.
+ * device = CFC_DEVICE_NONE opens a host-only context: the map API works
+ * (control-plane tooling, tests without a GPU); cfc_commit, cfc_classify_*
+ * and the counter calls return -ENODEV.  There is no CPU datapath. */
+#define CFC_DEVICE_NONE (-1)
+int cfc_open(int device, cfc_ctx **out);
+void cfc_close(cfc_ctx *ctx);
+int cfc_abi_version(void);
+
+/* ------------------------------------------------------------- BPF map API */
+/* Map types use the kernel's numbering (pkg/bpf/bpf.go:39-59). */
+#define CFC_MAP_TYPE_HASH 1
+#define CFC_MAP_TYPE_PERCPU_HASH 5
+#define CFC_MAP_TYPE_LRU_HASH 9
+#define CFC_MAP_TYPE_LPM_TRIE 11
+
+/* Update flags (pkg/bpf/bpf.go BPF_ANY/BPF_NOEXIST/BPF_EXIST). */
+#define CFC_ANY 0
+#define CFC_NOEXIST 1
+#define CFC_EXIST 2
+
+/*
+ * Replaces bpf.OpenOrCreateMap(path, mapType, keySize, valueSize,
+ * maxEntries, flags) (pkg/bpf/bpf.go:371) and bpf.CreateMap (:108).
+ * The basename of `path` selects the datapath role, as the pin path does in
+ * the reference:
+ *   cilium_ipcache          LPM_TRIE key 24 (struct ipcache_key) value 8
+ *   cilium_lxc              HASH key 20 (struct endpoint_key) value 48
+ *   cilium_policy_<id>      HASH key 8 (struct policy_key) value 24; the
+ *                           policy of endpoint LXC_ID <id> (decimal)
+ *   cilium_metrics          PERCPU_HASH key 8 value 16 (one "CPU": the GPU)
+ *   cilium_cidr_v4_fix|v4_dyn|v6_fix|v6_dyn   prefilter (pkg/maps/cidrmap)
+ *                           HASH or LPM_TRIE, key 4+addr bytes, value 1
+ * Any other name is a plain map with no datapath role.  Opening an existing
+ * path with the same geometry returns a new handle to it (*created = 0);
+ * a geometry mismatch returns -EINVAL (pkg/bpf/bpf.go:306 objCheck).
+ */
+int cfc_map_open(cfc_ctx *ctx, const char *path, uint32_t map_type,
+                 uint32_t key_size, uint32_t value_size,
+                 uint32_t max_entries, uint32_t flags, int *fd,
+                 int *created);
+/* bpf.ObjClose (pkg/bpf/bpf.go:299).  The map itself persists (pinned). */
+int cfc_map_close(cfc_ctx *ctx, int fd);
+/* bpf.UpdateElement (pkg/bpf/bpf.go:153) */
+int cfc_map_update(cfc_ctx *ctx, int fd, const void *key, const void *value,
+                   uint64_t flags);
+/* bpf.LookupElement (pkg/bpf/bpf.go:177).  LPM maps do longest-prefix
+ * match like the kernel trie.  Policy-map values carry the packet/byte
+ * counters as of the last cfc_counters_sync(). */
+int cfc_map_lookup(cfc_ctx *ctx, int fd, const void *key, void *value);
+/* bpf.DeleteElement (pkg/bpf/bpf.go:214) */
+int cfc_map_delete(cfc_ctx *ctx, int fd, const void *key);
+/* bpf.GetNextKey (pkg/bpf/bpf.go:225); key == NULL (or absent) -> first. */
+int cfc_map_get_next_key(cfc_ctx *ctx, int fd, const void *key,
+                         void *next_key);
+/* Number of per-CPU value slots of PERCPU maps (always 1). */
+int cfc_num_possible_cpus(void);
+
+/* Per-endpoint datapath constants that the reference compiles into each
+ * endpoint program from lxc_config.h (written by pkg/endpoint/bpf.go:86-190):
+ * SECLABEL, the endpoint's security identity used as the source identity
+ * of its egress traffic. */
+int cfc_endpoint_config(cfc_ctx *ctx, uint16_t lxc_id, uint32_t seclabel);
+
+/* Flatten the host tables into device layouts and publish them as the new
+ * epoch.  Enqueued on `stream` (hipStream_t, NULL = default stream). */
+int cfc_commit(cfc_ctx *ctx, void *stream);
+
+/* ---------------------------------------------------------------- datapath */
+/* Which reference program chain a batch runs through. */
+#define CFC_MODE_INGRESS 0 /* bpf_netdev from-netdev (FROM_HOST) -> local
+                              delivery -> bpf_lxc ipv4_policy */
+#define CFC_MODE_EGRESS 1  /* bpf_lxc from-container of endpoint ep_lxc */
+#define CFC_MODE_XDP 2     /* bpf_xdp prefilter only */
+#define CFC_MODE_FULL 3    /* XDP prefilter, then INGRESS for XDP_PASS */
+
+/* header meta word bits (cfc_hdr_v4.meta) */
+#define CFC_HF_FRAG 0x100u      /* ipv4_is_fragment() (ipv4.h:50-61) */
+#define CFC_HF_TCP_CLOSE 0x200u /* TCP RST|FIN (conntrack.h:533) */
+
+/* Device-resident SoA batch of IPv4 headers; all pointers are device
+ * pointers with n elements.  `ports` is the first 32-bit word of the L4
+ * header exactly as ct_lookup4 loads it (sport be16 in bits 0-15, dport be16
+ * in bits 16-31; for ICMP: type | code << 8 | csum << 16).  `meta` packs
+ * proto (bits 0-7), CFC_HF_* flags (bits 8-15) and skb->len (bits 16-31).
+ * `mark` (skb->mark, FROM_HOST identity) may be NULL = 0. */
+typedef struct {
+    const uint32_t *saddr;
+    const uint32_t *daddr;
+    const uint32_t *ports;
+    const uint32_t *meta;
+    const uint32_t *mark;
+    uint64_t n;
+} cfc_hdr_v4;
+
+/* Outputs (device pointers, n elements; action may be NULL).
+ *  verdict : bpf/lib/policy.h convention — <0 drop reason (DROP_*, or
+ *            CFC_DROP_PREFILTER for an XDP prefilter drop), 0 forwarded,
+ *            >0 proxy port (policy_entry.proxy_port, be16 raw).
+ *  identity: INGRESS/FULL: source security identity the policy used;
+ *            EGRESS: destination identity; XDP: 0.
+ *  action  : return code of the last reference program that ran
+ *            (TC_ACT_OK 0 / TC_ACT_SHOT 2 / TC_ACT_REDIRECT 7, or XDP_DROP 1 /
+ *            XDP_PASS 2 in XDP mode and for prefilter drops in FULL mode). */
+#define CFC_DROP_PREFILTER (-1)
+typedef struct {
+    int32_t *verdict;
+    uint32_t *identity;
+    uint8_t *action;
+} cfc_out;
+
+/* Classify a batch (asynchronous on `stream`).  Policy-entry and metrics
+ * counters accumulate on the device until cfc_counters_sync(). */
+int cfc_classify_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream);
+
+/* ---------------------------------------------------------------- counters */
+/* The device counter block is a flat u64 array: 2 u64 (packets, bytes) per
+ * policy entry in the committed epoch's entry order, then 256 reasons x 4
+ * directions x 2 u64 for cilium_metrics.  It is identical in layout on
+ * every rank holding the same tables, so it can be all-reduced in place
+ * (RCCL) before cfc_counters_sync(). */
+int cfc_counters_device(cfc_ctx *ctx, uint64_t **dev_ptr, uint64_t *n_u64);
+/* Fold the device counters into the host maps (policy entry packets/bytes,
+ * cilium_metrics) and zero them.  Synchronises `stream`. */
+int cfc_counters_sync(cfc_ctx *ctx, void *stream);
+/* Zero the device counters without folding (e.g. on non-root ranks after
+ * an all-reduce whose result was folded elsewhere). */
+int cfc_counters_clear(cfc_ctx *ctx, void *stream);
+/* Copy the counter block into caller device memory `dst` (n_u64 u64, as
+ * reported by cfc_counters_device) and zero it — the send side of a
+ * counter all-reduce.  cfc_counters_import adds `src` back in. */
+int cfc_counters_export(cfc_ctx *ctx, uint64_t *dst, uint64_t n_u64,
+                        void *stream);
+int cfc_counters_import(cfc_ctx *ctx, const uint64_t *src, uint64_t n_u64,
+                        void *stream);
+
+/* ------------------------------------------------------------- diagnostics */
+typedef struct {
+    uint64_t epoch;
+    uint64_t device_bytes;      /* bytes of device tables in this epoch */
+    uint32_t ipcache_v4_prefixes;
+    uint32_t lpm4_tbl8_groups;
+    uint32_t policy_entries;
+    uint32_t endpoints;
+    uint32_t prefilter_v4_fix;
+    uint32_t prefilter_v4_dyn;
+} cfc_stats;
+int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
+const char *cfc_strerror(int err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFC_H */

@@ -25,6 +25,7 @@
 #define DROP_INVALID_SIP -132
 #define DROP_POLICY -133
 #define DROP_CT_UNKNOWN_PROTO -137
+#define DROP_MISSED_TAIL_CALL -140
 #define DROP_FRAG_NOSUPPORT -157
 /* UAPI */
 #define TC_ACT_OK 0
@@ -374,9 +375,14 @@ static const epinfo *lxc_lookup(const cfo_t *o, int family,
     return ht_get(&o->lxc, k, &i) ? &o->eps[i] : NULL;
 }
 
+/* map_lookup_elem() calls the reference executes for the current header
+ * (SURVEY.md §8d "L"): prefilter, endpoint, ipcache and policy lookups. */
+static _Thread_local uint32_t tl_lookups;
+
 static pentry *pol_lookup(pmap *m, uint32_t id, uint16_t dport, uint8_t proto,
                           uint8_t egress)
 {
+    tl_lookups++;
     if (!m)
         return NULL;
     uint8_t k[8];
@@ -458,9 +464,18 @@ typedef struct {
  * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src. */
 static res_t lxc_ingress_v4(cfo_t *o, const epinfo *ep, uint32_t src,
                             uint8_t proto, uint16_t sport, uint16_t dport,
-                            int frag, uint32_t len, int skip_proxy)
+                            int frag, uint32_t len, int skip_proxy,
+                            int dir_missed)
 {
     res_t r = {TC_ACT_SHOT, 0, src};
+    if (!o->pol[ep->lxc_id]) {
+        /* no endpoint program behind cilium_policy[lxc_id]: the tail call
+         * in ipv4_local_delivery (l3.h:130) falls through and the caller
+         * drops with DROP_MISSED_TAIL_CALL */
+        r.verdict = DROP_MISSED_TAIL_CALL;
+        metric(o, DROP_MISSED_TAIL_CALL, dir_missed, len);
+        return r;
+    }
     uint16_t pdport;
     int ret = ct_new_dport(proto, sport, dport, &pdport);
     if (ret < 0) {
@@ -505,16 +520,18 @@ static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
     }
     if (identity < HEALTH_ID) { /* identity_is_reserved, policy.h:41-44 */
         uint32_t label;
+        tl_lookups++;
         if (lpm_lookup(&o->ipc4, (const uint8_t *)&saddr, &label) && label &&
             label != CLUSTER_ID && label != HOST_ID)
             identity = label;
     }
     res_t r = {TC_ACT_OK, 0, identity};
+    tl_lookups++;
     const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
     if (!ep || (ep->flags & ENDPOINT_F_HOST))
         return r; /* to the stack (tunnel endpoints out of scope) */
     return lxc_ingress_v4(o, ep, identity, proto, sport, dport, frag, len,
-                          skip_proxy);
+                          skip_proxy, METRIC_INGRESS);
 }
 
 /* handle_ipv4_from_lxc (bpf_lxc.c:440-692) for endpoint lxc */
@@ -537,6 +554,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         return r;
     }
     uint32_t label = 0, dst;
+    tl_lookups++;
     if (lpm_lookup(&o->ipc4, (const uint8_t *)&daddr, &label) && label)
         dst = label;
     else if ((daddr & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE)
@@ -556,6 +574,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         r.verdict = verdict;
         return r;
     }
+    tl_lookups++;
     const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
     if (ep) {
         if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST */
@@ -567,7 +586,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
          * the destination's policy program with src = SECLABEL */
         metric(o, 0, METRIC_EGRESS, len);
         res_t d = lxc_ingress_v4(o, ep, o->seclabel[lxc], proto, sport, dport,
-                                 frag, len, 0);
+                                 frag, len, 0, METRIC_EGRESS);
         d.identity = dst;
         return d;
     }
@@ -580,14 +599,21 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
 static int xdp_v4(cfo_t *o, uint32_t saddr, uint32_t daddr)
 {
     uint32_t v;
+    /* the dyn (LPM) lookup only exists when CIDR4_LPM_PREFILTER is compiled
+     * in; production keeps it off (prefilter.go:282-289): count it only
+     * when that map holds entries */
+    if (o->pf4_dyn.nlens)
+        tl_lookups++;
     if (lpm_lookup(&o->pf4_dyn, (const uint8_t *)&saddr, &v))
         return XDP_DROP;
     uint8_t k[8];
     uint32_t pl = 32;
     memcpy(k, &pl, 4);
     memcpy(k + 4, &saddr, 4);
+    tl_lookups++;
     if (ht_get(&o->pf4_fix, k, &v))
         return XDP_DROP;
+    tl_lookups++;
     return lxc_lookup(o, 1, (const uint8_t *)&daddr) ? XDP_PASS : XDP_DROP;
 }
 
@@ -597,19 +623,22 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
-                     int nthreads)
+                     uint8_t *lookups, int nthreads)
 {
     if (nthreads <= 0)
         nthreads = 1;
 #pragma omp parallel for schedule(static, 4096) num_threads(nthreads)
     for (size_t i = 0; i < n; i++) {
         res_t r;
+        tl_lookups = 0;
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v4(o, saddr[i], daddr[i]);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
                 action[i] = x;
                 verdict[i] = x == XDP_PASS ? 0 : -1;
                 identity[i] = 0;
+                if (lookups)
+                    lookups[i] = (uint8_t)tl_lookups;
                 continue;
             }
         }
@@ -623,7 +652,18 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         action[i] = r.action;
         verdict[i] = r.verdict;
         identity[i] = r.identity;
+        if (lookups)
+            lookups[i] = (uint8_t)tl_lookups;
     }
+}
+
+int cfo_policy_create(cfo_t *o, uint16_t lxc_id)
+{
+    if (!o->pol[lxc_id]) {
+        o->pol[lxc_id] = calloc(1, sizeof(pmap));
+        ht_init(&o->pol[lxc_id]->idx, 8);
+    }
+    return 0;
 }
 
 static int cmp_rows7(const void *a, const void *b)

@@ -36,6 +36,9 @@ int cfo_ipcache_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
 int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
                      uint32_t ifindex, uint16_t lxc_id, uint32_t flags);
 int cfo_seclabel_set(cfo_t *o, uint16_t lxc_id, uint32_t seclabel);
+/* An endpoint program (and its policymap) exists for lxc_id.  Endpoints in
+ * cilium_lxc without one drop with DROP_MISSED_TAIL_CALL. */
+int cfo_policy_create(cfo_t *o, uint16_t lxc_id);
 int cfo_policy_add(cfo_t *o, uint16_t lxc_id, uint32_t identity,
                    uint16_t dport_be, uint8_t proto, uint8_t egress,
                    uint16_t proxy_port_be);
@@ -46,14 +49,17 @@ int cfo_prefilter_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
  * return code of the last reference program run (TC_ACT_* or XDP_*),
  * verdict (policy.h convention; -1 = XDP prefilter drop), identity (ingress:
  * source security identity used for policy; egress: destination identity).
- * Counters accumulate in the oracle's policy entries and metrics table. */
+ * Counters accumulate in the oracle's policy entries and metrics table.
+ * lookups (may be NULL) receives, per header, the number of map lookups
+ * the reference executes (prefilter, endpoint, ipcache, policy): the L of
+ * SURVEY.md §8d's algorithmic-bytes formula. */
 void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint32_t *saddr, const uint32_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
-                     int nthreads);
+                     uint8_t *lookups, int nthreads);
 
 /* rows of 7 u64: identity, dport, proto, egress, proxy_port, packets, bytes
  * (sorted); returns the number of rows (writes at most cap). */

@@ -115,9 +115,9 @@ class RefDatapath:
         self.ep_prog = {}
         self.policy_map = {}
         for k, e in enumerate(t.endpoints):
-            if int(e["flags"]) & 1:
-                continue
             lxc = int(e["lxc_id"])
+            if int(e["flags"]) & 1 or lxc not in t.policy:
+                continue   # host entry, or an endpoint without a program
             rn = {"cilium_calls_111": f"calls_lxc{k}",
                   "cilium_policy_foo": f"policy{k}"}
             for ct in ("cilium_ct_tcp4_111", "cilium_ct_any4_111",
@@ -194,7 +194,10 @@ def _derive_ingress(h, i, ret, cb, pkt_out):
     """-> action, verdict, identity, id_mask"""
     if ret == TC_ACT_SHOT:
         # send_drop_notify(skb, src_label, SECLABEL, LXC_ID, ...):
-        # cb[1] = src << 16 | dst & 0xFFFF, cb[2] = reason (drop.h:94-102)
+        # cb[1] = src << 16 | dst & 0xFFFF, cb[2] = reason (drop.h:94-102).
+        # A missed tail call is reported by the netdev program with src 0.
+        if cb[2] == -140:
+            return ret, cb[2], 0, 0
         return ret, cb[2], (cb[1] >> 16) & 0xFFFF, 0xFFFF
     if ret == TC_ACT_REDIRECT:
         # proxy redirect rewrote the dport (lxc.h:118) and set
@@ -281,6 +284,7 @@ def sc_small_ingress(n=20000, seed=1):
     eps = np.concatenate([S.endpoint_v4(S.LXC_IPV4, 100, S.EP_LXC_ID),
                           S.endpoint_v4(S.ip4("10.0.1.2"), 101, 0x2020),
                           S.endpoint_v4(S.ip4("10.0.1.3"), 0, 0x3030),
+                          S.endpoint_v4(S.ip4("10.0.1.4"), 104, 0x4040),  # no program
                           S.endpoint_v4(S.ip4("10.0.255.254"), 0, 0xFFF0, 1)])
     idents = np.unique(ipc["label"])
     pol = {S.EP_LXC_ID: S.gen_policy(rng, 50, idents, wildcard=3,

@@ -41,7 +41,8 @@ def lib():
         L.cfo_prefilter_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, u8p,
                                         ctypes.c_int]
         L.cfo_classify_v4.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
-                                      ctypes.c_size_t] + [vp] * 11 + [ctypes.c_int]
+                                      ctypes.c_size_t] + [vp] * 12 + [ctypes.c_int]
+        L.cfo_policy_create.argtypes = [vp, ctypes.c_uint16]
         L.cfo_policy_dump.restype = ctypes.c_size_t
         L.cfo_policy_dump.argtypes = [vp, ctypes.c_uint16, vp, ctypes.c_size_t]
         L.cfo_metrics_dump.restype = ctypes.c_size_t
@@ -87,6 +88,7 @@ class Oracle:
             L.cfo_seclabel_set(h, int(lxc), int(lab))
         for lxc, pol in t.policy.items():
             self.lxc_ids.append(int(lxc))
+            L.cfo_policy_create(h, int(lxc))
             for r in pol:
                 L.cfo_policy_add(h, int(lxc), int(r["identity"]), int(r["dport"]),
                                  int(r["proto"]), int(r["egress"]),
@@ -96,11 +98,12 @@ class Oracle:
             L.cfo_prefilter_add(h, int(p["family"]), int(p["plen"]), a,
                                 int(p["dyn"]))
 
-    def classify(self, hdr, mode, ep_lxc=0, nthreads=1):
+    def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False):
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
         ide = np.zeros(n, np.uint32)
+        lk = np.zeros(n, np.uint8) if want_lookups else None
         c = np.ascontiguousarray
         arrs = [c(hdr.saddr, np.uint32), c(hdr.daddr, np.uint32),
                 c(hdr.sport, np.uint16), c(hdr.dport, np.uint16),
@@ -109,7 +112,9 @@ class Oracle:
         assert hdr.family == 4, "IPv6 oracle path not built yet"
         self.L.cfo_classify_v4(self.h, mode, ep_lxc, n,
                                *[_p(a) for a in arrs], _p(act), _p(ver),
-                               _p(ide), nthreads)
+                               _p(ide), _p(lk), nthreads)
+        if want_lookups:
+            return act, ver, ide, lk
         return act, ver, ide
 
     def policy_counters(self, lxc):

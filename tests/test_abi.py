@@ -1,0 +1,171 @@
+"""The C ABI library: loads, exports every symbol include/cfc.h declares, and
+its map half behaves like the kernel BPF maps pkg/bpf drives (host-only
+context, no GPU needed)."""
+import ctypes
+import errno
+import os
+import re
+import struct
+
+import pytest
+
+import cilium_amd as C
+from cilium_amd import _lib, cidrmap, ipcache, lxcmap, metricsmap, policymap
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "cfc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\**\s*(cfc_\w+)\s*\(",
+                                 txt, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    fns = header_functions()
+    assert len(fns) >= 18
+    for f in fns:
+        assert hasattr(L, f), f
+    assert sorted(_lib.EXPORTS) == fns
+    assert L.cfc_abi_version() == 1
+    assert L.cfc_num_possible_cpus() == 1
+
+
+def test_no_gpu_means_no_datapath():
+    dp = C.host_only()
+    with pytest.raises(OSError) as e:
+        dp.commit()
+    assert e.value.errno == errno.ENODEV
+
+
+def errno_of(fn):
+    with pytest.raises(OSError) as e:
+        fn()
+    return e.value.errno
+
+
+def test_hash_map_semantics():
+    dp = C.host_only()
+    fd, new = dp.open_or_create_map("/sys/fs/bpf/tc/globals/test_hash", 1, 4, 8, 2)
+    assert new
+    k1, k2, k3 = (struct.pack("<I", i) for i in (1, 2, 3))
+    dp.update_element(fd, k1, b"a" * 8)
+    assert errno_of(lambda: dp.update_element(fd, k1, b"b" * 8, 1)) == errno.EEXIST
+    assert errno_of(lambda: dp.update_element(fd, k2, b"b" * 8, 2)) == errno.ENOENT
+    dp.update_element(fd, k2, b"b" * 8, 1)
+    assert errno_of(lambda: dp.update_element(fd, k3, b"c" * 8)) == errno.E2BIG
+    dp.update_element(fd, k1, b"z" * 8, 2)                 # replace in place
+    assert dp.lookup_element(fd, k1) == b"z" * 8
+    assert dp.lookup_element(fd, k3) is None
+    assert sorted(dp.keys(fd)) == [k1, k2]
+    assert dp.get_next_key(fd, k3) in (k1, k2)              # unknown -> first
+    dp.delete_element(fd, k1)
+    assert errno_of(lambda: dp.delete_element(fd, k1)) == errno.ENOENT
+    # reopen with a different geometry: objCheck refuses (bpf.go:306)
+    assert errno_of(lambda: dp.open_or_create_map(
+        "/sys/fs/bpf/tc/globals/test_hash", 1, 4, 16, 2)) == errno.EINVAL
+    fd2, new2 = dp.open_or_create_map("/sys/fs/bpf/tc/globals/test_hash", 1, 4, 8, 2)
+    assert not new2 and dp.lookup_element(fd2, k2) == b"b" * 8
+    dp.obj_close(fd2)
+    assert errno_of(lambda: dp.obj_close(fd2)) == errno.EBADF
+
+
+def test_lpm_map_semantics():
+    dp = C.host_only()
+    fd, _ = dp.open_or_create_map("lpm_test", 11, 8, 1, 3, 1)
+
+    def key(cidr):
+        a, p = cidr.split("/")
+        return struct.pack("<I", int(p)) + bytes(int(x) for x in a.split("."))
+    dp.update_element(fd, key("10.0.0.0/8"), b"\x08")
+    dp.update_element(fd, key("10.1.0.0/16"), b"\x10")
+    dp.update_element(fd, key("10.1.2.3/16"), b"\x11")    # same prefix: replace
+    assert len(dp.keys(fd)) == 2
+    assert dp.lookup_element(fd, key("10.1.9.9/32")) == b"\x11"
+    assert dp.lookup_element(fd, key("10.2.9.9/32")) == b"\x08"
+    assert dp.lookup_element(fd, key("10.1.9.9/12")) == b"\x08"  # bounded by key len
+    assert dp.lookup_element(fd, key("11.0.0.1/32")) is None
+    assert errno_of(lambda: dp.update_element(fd, key("1.2.3.4/33"), b"\x00")) == errno.EINVAL
+    dp.update_element(fd, key("0.0.0.0/0"), b"\x00")
+    assert errno_of(lambda: dp.update_element(fd, key("9.0.0.0/8"), b"\x00")) == errno.ENOSPC
+    assert dp.lookup_element(fd, key("11.0.0.1/32")) == b"\x00"
+    assert errno_of(lambda: dp.delete_element(fd, key("10.0.0.0/9"))) == errno.ENOENT
+
+
+def test_role_geometry_is_checked():
+    dp = C.host_only()
+    assert errno_of(lambda: dp.open_or_create_map("cilium_policy_7", 1, 8, 16, 10)) == errno.EINVAL
+    assert errno_of(lambda: dp.open_or_create_map("cilium_ipcache", 1, 24, 8, 10)) == errno.EINVAL
+    dp.open_or_create_map("cilium_policy_7", 1, 8, 24, 16384)
+
+
+def test_policymap_mirror():
+    dp = C.host_only()
+    pm, new = policymap.OpenMap(dp, policymap.path_for(4112))
+    assert new
+    pm.Allow(1000, 80, 6, policymap.Ingress, 0)
+    pm.Allow(1000, 0, 0, policymap.Ingress)
+    pm.Allow(0, 53, 17, policymap.Egress, 10001)
+    assert pm.Exists(1000, 80, 6, 0) and not pm.Exists(1000, 81, 6, 0)
+    d = {x.Key.ToHost(): x.PolicyEntry for x in pm.DumpToSlice()}
+    k = policymap.PolicyKey(0, 53, 17, 1)
+    assert d[k].ProxyPort == 0x1127        # htons(10001), network order
+    # raw layout: identity LE, port network order, proto, direction
+    raw = policymap.PolicyKey(1000, 80, 6, 0).ToNetwork().pack()
+    assert raw == struct.pack("<I", 1000) + b"\x00\x50" + b"\x06\x00"
+    pm.Delete(1000, 80, 6, 0)
+    assert not pm.Exists(1000, 80, 6, 0)
+    pm.Flush()
+    assert pm.DumpToSlice() == []
+
+
+def test_ipcache_and_lxc_mirrors():
+    dp = C.host_only()
+    m = ipcache.Map(dp)
+    m.Update(ipcache.NewKey("10.0.0.0/8"), ipcache.RemoteEndpointInfo(42))
+    m.Update(ipcache.NewKey("10.1.0.0/16"), ipcache.RemoteEndpointInfo(43))
+    m.Update(ipcache.NewKey("f00d::/64"), ipcache.RemoteEndpointInfo(44))
+    assert m.Lookup(ipcache.NewKey("10.1.2.3/32")).SecurityIdentity == 43
+    assert m.Lookup(ipcache.NewKey("10.9.2.3/32")).SecurityIdentity == 42
+    assert m.Lookup(ipcache.NewKey("f00d::1/128")).SecurityIdentity == 44
+    assert m.Lookup(ipcache.NewKey("11.0.0.1/32")) is None
+    k = ipcache.NewKey("10.1.0.0/16")
+    assert k.Prefixlen == 48 and k.pack()[:8] == struct.pack("<IHBB", 48, 0, 0, 1)
+    assert sorted(x.String() for x in m.Dump()) == ["10.0.0.0/8", "10.1.0.0/16",
+                                                     "f00d::/64"]
+    lx = lxcmap.LXCMap(dp)
+    lx.WriteEndpoint([lxcmap.NewEndpointKey("10.0.0.1"),
+                      lxcmap.NewEndpointKey("f00d::1")],
+                     lxcmap.EndpointInfo(IfIndex=5, LxcID=0x1010))
+    lx.AddHostEntry("10.0.255.254")
+    assert lx.Lookup("f00d::1").LxcID == 0x1010
+    assert lx.Lookup("10.0.255.254").IsHost()
+    assert len(lxcmap.EndpointInfo().pack()) == 48
+
+
+def test_prefilter_revisions_and_rollback():
+    dp = C.host_only()
+    pf = cidrmap.PreFilter(dp)
+    pf.Insert(1, ["1.2.3.4/32", "::1/128"])
+    cidrs, rev = pf.Dump()
+    assert rev == 2 and sorted(cidrs) == ["1.2.3.4/32", "::1/128"]
+    with pytest.raises(ValueError):
+        pf.Insert(1, ["5.5.5.5/32"])                     # stale revision
+    with pytest.raises(ValueError):
+        pf.Insert(2, ["6.6.6.6/32", "7.7.7.0/24"])       # dyn map disabled
+    assert sorted(pf.Dump()[0]) == ["1.2.3.4/32", "::1/128"]   # rolled back
+    with pytest.raises(ValueError):
+        pf.Delete(2, ["1.2.3.4/32", "8.8.8.8/32"])       # all-or-nothing
+    pf.Delete(2, ["1.2.3.4/32"])
+    assert pf.Dump() == (["::1/128"], 3)
+
+
+def test_metrics_map_owned_by_datapath():
+    dp = C.host_only()
+    fd = metricsmap.open_map(dp)
+    assert metricsmap.dump(dp, fd) == {}
+    # geometry of the datapath-owned map is fixed
+    with pytest.raises(OSError):
+        dp.open_or_create_map("cilium_metrics", 1, 8, 16, 65536)
