@@ -1,26 +1,39 @@
 // Batched verdict kernels for gfx950 (MI355X).
 //
-// One thread classifies one header at a time; a 1024-thread workgroup owns a
-// contiguous slice of the batch, so each loop iteration reads 4 KiB of every
-// SoA input array coalesced and writes the outputs coalesced.  The lookups
-// are dependent random accesses (DIR-24-8 tbl24/tbl8 in the Infinity Cache,
-// the endpoint and policy buckets in L2): this is HBM/latency-bound integer
-// work with no contraction, so there is no MFMA here.
+// Shape.  A 1024-thread workgroup owns a contiguous slice of <= 65536 headers
+// of the SoA batch; each loop iteration reads 4 KiB of every input array
+// coalesced (non-temporal: the 1-GiB stream must not evict the lookup tables
+// from the 256-MiB Infinity Cache) and writes the outputs the same way.
 //
-// Counters follow the reference's exact integer sums.  Per-entry packets and
-// bytes (policy.h:68-69,80-81,92-93) and cilium_metrics (metrics.h:43-61)
-// are accumulated in LDS as u32 (a wrap carries 2^32 straight to the global
-// u64), written once per workgroup as a partial slab, and summed per entry by
-// a second kernel — no per-header global atomics.
+// Latency.  The lookups are dependent random accesses — DIR-24-8 tbl24/tbl8
+// (Infinity Cache), the endpoint / prefilter / policy buckets (L2).  The
+// kernel is bound by how many of them are in flight, so each header's chain
+// is cut to four memory round trips by issuing every lookup as soon as its
+// inputs exist:
+//   1. inputs
+//   2. tbl24[src|dst], endpoint bucket[dst], prefilter bucket[src]  (together)
+//   3. tbl8 (if the /24 is split), endpoint record
+//   4. the three policy buckets of __policy_can_access (L4, L3, wildcard-port)
+//      loaded speculatively together, resolved in the reference's order.
+// Overflowing buckets (never at the load factors flatten.cpp builds) fall
+// back to a probing loop.  There is no contraction here, hence no MFMA.
+//
+// Counters.  The reference bumps policy_entry packets/bytes
+// (policy.h:68-69,80-81,92-93) and cilium_metrics (metrics.h:43-61) per
+// packet.  Here they are exact u32 sums in LDS (a workgroup sees at most
+// 65536 headers, so neither packets nor bytes can wrap), written once per
+// workgroup as a partial slab and summed per entry by k_reduce_partials.
+// Metrics keys are few and hot (most packets of a batch share one drop
+// reason), so they are aggregated across the wave before the LDS atomic.
 //
 // Reference semantics restated here (file:line in /root/reference):
-//   netdev_ingress  bpf_netdev.c:128-153 (FROM_HOST identity from mark),
-//                   :357-453 handle_ipv4 (ipcache src identity, lxc lookup)
-//   lxc_ingress     bpf_lxc.c:898-1028 ipv4_policy + tail_ipv4_policy
-//   lxc_egress      bpf_lxc.c:440-704 handle_ipv4_from_lxc
-//   policy_access   bpf/lib/policy.h:46-146
-//   ct_new_dport    bpf/lib/conntrack.h:467-590 (ports of a CT_NEW tuple)
-//   xdp_v4          bpf_xdp.c:88-121
+//   ingress   bpf_netdev.c:128-153 (FROM_HOST identity from skb->mark),
+//             :357-453 handle_ipv4, l3.h:103-131 ipv4_local_delivery,
+//             bpf_lxc.c:898-1028 ipv4_policy + tail_ipv4_policy
+//   egress    bpf_lxc.c:440-704 handle_ipv4_from_lxc
+//   policy    bpf/lib/policy.h:46-146
+//   ct ports  bpf/lib/conntrack.h:467-590 (tuple->dport of a CT_NEW lookup)
+//   xdp       bpf_xdp.c:88-121
 #include "classify.hpp"
 
 namespace cfc {
@@ -30,130 +43,137 @@ namespace {
 constexpr uint32_t HOST_ID = 1, WORLD_ID = 2, CLUSTER_ID = 3, HEALTH_ID = 4;
 constexpr uint32_t IPV4_CLUSTER_MASK = 0xff0000u, IPV4_CLUSTER_RANGE = 0x100000u;
 constexpr int DROP_INVALID_SIP = -132, DROP_POLICY = -133,
-              DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140,
-              DROP_FRAG_NOSUPPORT = -157;
+              DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140;
 constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
 constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
 constexpr uint32_t ENDPOINT_F_HOST = 1;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint64_t MAX_PER_BLOCK = 65536;   // keeps u32 LDS sums exact
 
-struct Counters {
-    uint32_t *s_met;   // LDS metrics [256][4][2] u32
-    uint32_t *s_ctr;   // LDS policy counters [n_ctr][2] u32, or null
-    uint64_t *g_ctr;
-    uint64_t *g_met;
-
-    __device__ static void add_carry(uint32_t *s, uint64_t *g, uint32_t v)
-    {
-        uint32_t old = atomicAdd(s, v);
-        if (old + v < old)
-            atomicAdd((unsigned long long *)g, 1ull << 32);
-    }
-    __device__ void hit(uint32_t idx, uint32_t len) const
-    {
-        if (s_ctr) {
-            add_carry(&s_ctr[2 * idx], &g_ctr[2 * idx], 1u);
-            add_carry(&s_ctr[2 * idx + 1], &g_ctr[2 * idx + 1], len);
-        } else {
-            atomicAdd((unsigned long long *)&g_ctr[2 * idx], 1ull);
-            atomicAdd((unsigned long long *)&g_ctr[2 * idx + 1],
-                      (unsigned long long)len);
-        }
-    }
-    // update_metrics(len, dir, -reason); reason is DROP_* (<0) or 0
-    __device__ void metric(int reason, int dir, uint32_t len) const
-    {
-        uint32_t j = (((uint32_t)(uint8_t)(-reason)) * METRIC_DIRS + dir) * 2;
-        add_carry(&s_met[j], &g_met[j], 1u);
-        add_carry(&s_met[j + 1], &g_met[j + 1], len);
-    }
-};
-
-__device__ __forceinline__ uint32_t lpm4(const uint32_t *tbl24,
-                                         const uint32_t *tbl8,
-                                         const uint32_t *ovf, uint32_t addr_be)
+template <class T>
+__device__ __forceinline__ T ld_nt(const T *p)
 {
-    if (!tbl24)
-        return 0;
-    uint32_t h = __builtin_bswap32(addr_be);
-    uint32_t e = tbl24[h >> 8];
-    if (e & LPM_GROUP)
-        e = tbl8[((e & ~LPM_GROUP) << 8) | (h & 0xFF)];
-    if (e & LPM_INDIRECT)
-        e = ovf[e & LPM_PAYLOAD];
-    return e;
+    return __builtin_nontemporal_load(p);
+}
+template <class T>
+__device__ __forceinline__ void st_nt(T v, T *p)
+{
+    __builtin_nontemporal_store(v, p);
 }
 
-__device__ __forceinline__ int lxc4_find(const DevTables &T, uint32_t addr)
+struct B64 {   // one 64-byte bucket
+    uint4 q[4];
+};
+__device__ __forceinline__ B64 ldb(const void *p)
+{
+    const uint4 *b = reinterpret_cast<const uint4 *>(p);
+    B64 r;
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        r.q[i] = b[i];
+    return r;
+}
+
+// ---- lookups on a loaded bucket: 1 hit, 0 definite miss, -1 keep probing
+__device__ __forceinline__ int lxc_scan(const B64 &B, uint32_t addr, int *ep)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint4 v = B.q[i];
+        if (v.y == EMPTY)
+            return 0;
+        if (v.x == addr) {
+            *ep = (int)v.y;
+            return 1;
+        }
+        if (v.w == EMPTY)
+            return 0;
+        if (v.z == addr) {
+            *ep = (int)v.w;
+            return 1;
+        }
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int pf_scan(const B64 &B, uint32_t addr)
+{
+    const uint32_t a[16] = {B.q[0].x, B.q[0].y, B.q[0].z, B.q[0].w,
+                            B.q[1].x, B.q[1].y, B.q[1].z, B.q[1].w,
+                            B.q[2].x, B.q[2].y, B.q[2].z, B.q[2].w,
+                            B.q[3].x, B.q[3].y, B.q[3].z, B.q[3].w};
+    const uint32_t cnt = a[15];
+    bool hit = false;
+#pragma unroll
+    for (int i = 0; i < PF_SLOTS; i++)
+        hit |= ((uint32_t)i < cnt) & (a[i] == addr);
+    return hit ? 1 : (cnt < (uint32_t)PF_SLOTS ? 0 : -1);
+}
+
+__device__ __forceinline__ int pol_scan(const B64 &B, uint64_t key,
+                                        uint32_t *ctr, uint32_t *proxy)
+{
+#pragma unroll
+    for (int s = 0; s < POL_SLOTS; s++) {
+        const uint4 v = B.q[s];
+        if (v.w == EMPTY)
+            return 0;
+        if ((((uint64_t)v.y << 32) | v.x) == key) {
+            *ctr = v.w;
+            *proxy = v.z & 0xFFFF;
+            return 1;
+        }
+    }
+    return -1;
+}
+
+// ---- probing continuations (cold paths)
+__device__ inline int lxc_probe_from(const DevTables &T, uint32_t addr,
+                                           uint32_t b)
+{
+    for (;;) {
+        b = (b + 1) & T.lxc4_mask;
+        int ep = -1;
+        int r = lxc_scan(ldb(T.lxc4 + (size_t)b * LXC_SLOTS), addr, &ep);
+        if (r >= 0)
+            return r ? ep : -1;
+    }
+}
+
+__device__ inline bool pf_probe_from(const DevTables &T, uint32_t addr,
+                                           uint32_t b)
+{
+    for (;;) {
+        b = (b + 1) & T.pf_fix_mask;
+        int r = pf_scan(ldb(T.pf_fix + (size_t)b * 16), addr);
+        if (r >= 0)
+            return r == 1;
+    }
+}
+
+__device__ inline uint32_t pol_probe_from(const PolSlot *pol,
+                                                uint32_t base, uint32_t mask,
+                                                uint64_t key, uint32_t b,
+                                                uint32_t *proxy)
+{
+    for (;;) {
+        b = (b + 1) & mask;
+        uint32_t c = NONE;
+        int r = pol_scan(ldb(pol + (size_t)(base + b) * POL_SLOTS), key, &c, proxy);
+        if (r >= 0)
+            return r ? c : NONE;
+    }
+}
+
+__device__ __forceinline__ int lxc_find(const DevTables &T, uint32_t addr)
 {
     if (!T.lxc4)
         return -1;
     uint32_t b = hash32(addr, T.lxc4_mask);
-    for (;;) {
-        const uint4 *bk = reinterpret_cast<const uint4 *>(T.lxc4 + (size_t)b * LXC_SLOTS);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint4 v = bk[q];
-            if (v.y == EMPTY)
-                return -1;
-            if (v.x == addr)
-                return (int)v.y;
-            if (v.w == EMPTY)
-                return -1;
-            if (v.z == addr)
-                return (int)v.w;
-        }
-        b = (b + 1) & T.lxc4_mask;
-    }
-}
-
-__device__ __forceinline__ bool pf_fix_hit(const DevTables &T, uint32_t addr)
-{
-    if (!T.pf_fix)
-        return false;
-    uint32_t b = hash32(addr, T.pf_fix_mask);
-    for (;;) {
-        const uint4 *bk = reinterpret_cast<const uint4 *>(T.pf_fix + (size_t)b * 16);
-        uint4 q[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            q[i] = bk[i];
-        uint32_t cnt = q[3].w;
-        const uint32_t a[15] = {q[0].x, q[0].y, q[0].z, q[0].w, q[1].x, q[1].y,
-                                q[1].z, q[1].w, q[2].x, q[2].y, q[2].z, q[2].w,
-                                q[3].x, q[3].y, q[3].z};
-        bool hit = false;
-#pragma unroll
-        for (int i = 0; i < 15; i++)
-            hit |= (i < (int)cnt) & (a[i] == addr);
-        if (hit)
-            return true;
-        if (cnt < (uint32_t)PF_SLOTS)
-            return false;
-        b = (b + 1) & T.pf_fix_mask;
-    }
-}
-
-// policy hash probe: returns counter index or EMPTY; *proxy = proxy_port
-__device__ __forceinline__ uint32_t pol_find(const PolSlot *pol, uint32_t base,
-                                             uint32_t mask, uint64_t key,
-                                             uint32_t *proxy)
-{
-    uint32_t b = hash64(key, mask);
-    for (;;) {
-        const uint4 *bk = reinterpret_cast<const uint4 *>(pol + (size_t)(base + b) * POL_SLOTS);
-#pragma unroll
-        for (int s = 0; s < POL_SLOTS; s++) {
-            uint4 v = bk[s];
-            if (v.w == EMPTY)
-                return EMPTY;
-            if ((((uint64_t)v.y << 32) | v.x) == key) {
-                *proxy = v.z & 0xFFFF;
-                return v.w;
-            }
-        }
-        b = (b + 1) & mask;
-    }
+    int ep = -1;
+    int r = lxc_scan(ldb(T.lxc4 + (size_t)b * LXC_SLOTS), addr, &ep);
+    return r > 0 ? ep : (r == 0 ? -1 : lxc_probe_from(T, addr, b));
 }
 
 __device__ __forceinline__ uint64_t pkey(uint32_t id, uint32_t dport,
@@ -163,39 +183,10 @@ __device__ __forceinline__ uint64_t pkey(uint32_t id, uint32_t dport,
            ((uint64_t)egress << 56);
 }
 
-// __policy_can_access (policy.h:46-110) with cb[CB_POLICY] == 0
-__device__ __forceinline__ int policy_access(const DevTables &T, uint32_t base,
-                                             uint32_t mask, uint32_t id,
-                                             uint32_t dport, uint32_t proto,
-                                             uint32_t egress, bool frag,
-                                             uint32_t len, const Counters &C)
-{
-    uint32_t proxy = 0, c;
-    if (!frag) {
-        c = pol_find(T.pol, base, mask, pkey(id, dport, proto, egress), &proxy);
-        if (c != EMPTY) {
-            C.hit(c, len);
-            return (int)proxy;
-        }
-    }
-    c = pol_find(T.pol, base, mask, pkey(id, 0, 0, egress), &proxy);
-    if (c != EMPTY) {
-        C.hit(c, len);
-        return TC_ACT_OK;
-    }
-    if (!frag) {
-        c = pol_find(T.pol, base, mask, pkey(0, dport, proto, egress), &proxy);
-        if (c != EMPTY) {
-            C.hit(c, len);
-            return (int)proxy;
-        }
-    }
-    return frag ? DROP_FRAG_NOSUPPORT : DROP_POLICY;
-}
-
 // tuple->dport of a CT_NEW lookup (conntrack.h:496-584): TCP/UDP ports are
 // loaded swapped and swapped back by ipv4_ct_tuple_reverse(); ICMP echo puts
-// its type (8) in tuple->sport, which becomes the dport; other ICMP -> 0.
+// its type (8) in tuple->sport, which becomes the dport; other ICMP -> 0;
+// any other protocol -> DROP_CT_UNKNOWN_PROTO.
 __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
                                              uint32_t *dport)
 {
@@ -203,156 +194,122 @@ __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
         *dport = ports >> 16;
         return true;
     }
-    if (proto == 1) {
-        *dport = (ports & 0xFF) == 8 ? 8u : 0u;
-        return true;
-    }
-    return false;
+    *dport = (ports & 0xFF) == 8 ? 8u : 0u;
+    return proto == 1;
 }
 
-struct Res {
-    int act, ver;
-    uint32_t id;
+// __policy_can_access (policy.h:46-110), cb[CB_POLICY] == 0: the three keys'
+// buckets are loaded together, the first match in the reference's order
+// wins.  Returns the verdict (<0 drop) and the matched counter (or NONE).
+struct PolicyProbe {
+    uint64_t k[3];
+    uint32_t b[3];
+    B64 bk[3];
 };
 
-// ipv4_policy (bpf_lxc.c:898-1015) of endpoint r, src label `src`
-__device__ __forceinline__ void lxc_ingress(const DevTables &T, const EpRec &r,
-                                            uint32_t src, uint32_t proto,
-                                            uint32_t ports, bool frag,
-                                            uint32_t len, bool skip_proxy,
-                                            int dir_missed, const Counters &C,
-                                            Res &o)
+__device__ __forceinline__ void policy_issue(const DevTables &T, uint32_t base,
+                                             uint32_t mask, uint32_t id,
+                                             uint32_t dport, uint32_t proto,
+                                             uint32_t egress, PolicyProbe &P)
 {
-    if (!r.has_policy) {  // cilium_policy[lxc_id] tail call missed (l3.h:130)
-        o.act = TC_ACT_SHOT;
-        o.ver = DROP_MISSED_TAIL_CALL;
-        C.metric(DROP_MISSED_TAIL_CALL, dir_missed, len);
-        return;
+    P.k[0] = pkey(id, dport, proto, egress);   // L4
+    P.k[1] = pkey(id, 0, 0, egress);           // L3
+    P.k[2] = pkey(0, dport, proto, egress);    // wildcard port
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        P.b[j] = hash64(P.k[j], mask);
+        P.bk[j] = ldb(T.pol + (size_t)(base + P.b[j]) * POL_SLOTS);
     }
-    uint32_t dport;
-    if (!ct_new_dport(proto, ports, &dport)) {
-        o.act = TC_ACT_SHOT;
-        o.ver = DROP_CT_UNKNOWN_PROTO;
-        C.metric(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS, len);
-        return;
-    }
-    int v = policy_access(T, r.pol_base, r.pol_mask, src, dport, proto, 0,
-                          frag, len, C);
-    if (v < 0) {
-        o.act = TC_ACT_SHOT;
-        o.ver = DROP_POLICY;
-        C.metric(DROP_POLICY, METRIC_INGRESS, len);
-        return;
-    }
-    if (skip_proxy)
-        v = 0;
-    if (v > 0) {  // redirect_to_proxy -> redirect(HOST_IFINDEX)
-        o.act = TC_ACT_REDIRECT;
-        o.ver = v;
-        return;
-    }
-    C.metric(0, METRIC_INGRESS, len);  // send_trace_notify(TRACE_TO_LXC)
-    o.act = r.ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
-    o.ver = 0;
 }
 
-__device__ __forceinline__ void netdev_ingress(const DevTables &T,
-                                               uint32_t saddr, uint32_t daddr,
-                                               uint32_t ports, uint32_t meta,
-                                               uint32_t mark, const Counters &C,
-                                               Res &o)
+__device__ __forceinline__ int policy_resolve(const DevTables &T, uint32_t base,
+                                              uint32_t mask, bool frag,
+                                              const PolicyProbe &P,
+                                              uint32_t *ctr)
 {
-    uint32_t magic = mark & 0xF00u, identity;
-    bool skip_proxy = false;
-    if (magic == 0xA00u || magic == 0xB00u) {  // proxy: identity in mark
-        identity = ((mark & 0xFF) << 16) | (mark >> 16);
-        skip_proxy = magic == 0xA00u;
+    uint32_t proxy = 0, c = NONE;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        if (frag && j != 1)   // fragments: L3 key only (policy.h:61,85)
+            continue;
+        int r = pol_scan(P.bk[j], P.k[j], &c, &proxy);
+        if (r < 0)
+            c = pol_probe_from(T.pol, base, mask, P.k[j], P.b[j], &proxy);
+        if (r > 0 || (r < 0 && c != NONE)) {
+            *ctr = c;
+            return j == 1 ? TC_ACT_OK : (int)proxy;
+        }
+    }
+    *ctr = NONE;
+    return DROP_POLICY;   // (DROP_FRAG_NOSUPPORT also becomes DROP_POLICY)
+}
+
+__device__ __forceinline__ int policy_access(const DevTables &T, uint32_t base,
+                                             uint32_t mask, uint32_t id,
+                                             uint32_t dport, uint32_t proto,
+                                             uint32_t egress, bool frag,
+                                             uint32_t *ctr)
+{
+    PolicyProbe P;
+    policy_issue(T, base, mask, id, dport, proto, egress, P);
+    return policy_resolve(T, base, mask, frag, P, ctr);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o);
+    return v;
+}
+
+// update_metrics for every lane of the wave at once: key = index into the
+// metrics block ([reason][dir][count,bytes]) or NONE.  Must be reached by
+// the whole wave (uniform control flow).
+__device__ __forceinline__ void metrics_wave(uint32_t *s_met, uint64_t *g_met,
+                                             uint32_t key, uint32_t len)
+{
+    uint64_t pending = __ballot(key != NONE);
+    const int lane = threadIdx.x & 63;
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t lk = __shfl(key, leader);
+        const bool mine = key == lk;
+        const uint64_t m = __ballot(mine);
+        const uint32_t sum = wave_sum(mine ? len : 0u);
+        if (lane == leader) {
+            if (s_met) {
+                atomicAdd(&s_met[lk], (uint32_t)__popcll(m));
+                atomicAdd(&s_met[lk + 1], sum);
+            } else {
+                atomicAdd((unsigned long long *)&g_met[lk],
+                          (unsigned long long)__popcll(m));
+                atomicAdd((unsigned long long *)&g_met[lk + 1],
+                          (unsigned long long)sum);
+            }
+        }
+        pending &= ~m;
+    }
+}
+
+__device__ __forceinline__ uint32_t mkey(int reason, int dir)
+{
+    return ((uint32_t)(uint8_t)(-reason) * METRIC_DIRS + (uint32_t)dir) * 2;
+}
+
+template <bool LDS>
+__device__ __forceinline__ void count_hit(uint32_t *s_ctr, uint64_t *g_ctr,
+                                          uint32_t c, uint32_t len)
+{
+    if (c == NONE)
+        return;
+    if (LDS) {
+        atomicAdd(&s_ctr[2 * c], 1u);
+        atomicAdd(&s_ctr[2 * c + 1], len);
     } else {
-        identity = magic == 0xC00u ? HOST_ID : WORLD_ID;
+        atomicAdd((unsigned long long *)&g_ctr[2 * c], 1ull);
+        atomicAdd((unsigned long long *)&g_ctr[2 * c + 1], (unsigned long long)len);
     }
-    if (identity < HEALTH_ID) {  // identity_is_reserved
-        uint32_t l = lpm4(T.tbl24, T.tbl8, T.lbl_ovf, saddr);
-        if (l && l != CLUSTER_ID && l != HOST_ID)
-            identity = l;
-    }
-    o.id = identity;
-    o.act = TC_ACT_OK;
-    o.ver = 0;
-    int e = lxc4_find(T, daddr);
-    if (e < 0)
-        return;
-    EpRec r = T.eps[e];
-    if (r.flags & ENDPOINT_F_HOST)
-        return;
-    lxc_ingress(T, r, identity, meta & 0xFF, ports, (meta & CFC_HF_FRAG) != 0,
-                meta >> 16, skip_proxy, METRIC_INGRESS, C, o);
-}
-
-__device__ __forceinline__ void lxc_egress(const DevTables &T,
-                                           const EgressArgs &E, uint32_t saddr,
-                                           uint32_t daddr, uint32_t ports,
-                                           uint32_t meta, const Counters &C,
-                                           Res &o)
-{
-    uint32_t len = meta >> 16, proto = meta & 0xFF;
-    o.id = 0;
-    o.act = TC_ACT_SHOT;
-    int se = lxc4_find(T, saddr);
-    if (se < 0 || T.eps[se].lxc_id != E.lxc_id) {  // is_valid_lxc_src_ipv4
-        o.ver = DROP_INVALID_SIP;
-        C.metric(DROP_INVALID_SIP, METRIC_EGRESS, len);
-        return;
-    }
-    uint32_t dport;
-    if (!ct_new_dport(proto, ports, &dport)) {
-        o.ver = DROP_CT_UNKNOWN_PROTO;
-        C.metric(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS, len);
-        return;
-    }
-    uint32_t l = lpm4(T.tbl24, T.tbl8, T.lbl_ovf, daddr);
-    uint32_t dst = l ? l
-                     : ((daddr & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE ? CLUSTER_ID
-                                                                          : WORLD_ID);
-    o.id = dst;
-    int v = policy_access(T, E.pol_base, E.pol_mask, dst, dport, proto, 1,
-                          false, len, C);
-    if (v < 0) {
-        o.ver = DROP_POLICY;
-        C.metric(DROP_POLICY, METRIC_EGRESS, len);
-        return;
-    }
-    o.ver = v;
-    if (v > 0) {  // proxy redirect (bpf_lxc.c:582-604)
-        o.act = TC_ACT_REDIRECT;
-        return;
-    }
-    int e = lxc4_find(T, daddr);
-    C.metric(0, METRIC_EGRESS, len);  // to_host / local delivery / to_stack
-    if (e < 0) {
-        o.act = TC_ACT_OK;
-        return;
-    }
-    EpRec r = T.eps[e];
-    if (r.flags & ENDPOINT_F_HOST) {
-        o.act = TC_ACT_REDIRECT;
-        return;
-    }
-    Res d;
-    lxc_ingress(T, r, E.seclabel, proto, ports, (meta & CFC_HF_FRAG) != 0,
-                len, false, METRIC_EGRESS, C, d);
-    o.act = d.act;
-    o.ver = d.ver;
-}
-
-// check_v4 (bpf_xdp.c:97-121): dyn LPM, then fixed /32 set, then endpoint
-__device__ __forceinline__ bool xdp_pass(const DevTables &T, uint32_t saddr,
-                                         uint32_t daddr)
-{
-    if (lpm4(T.pf_tbl24, T.pf_tbl8, nullptr, saddr))
-        return false;
-    if (pf_fix_hit(T, saddr))
-        return false;
-    return lxc4_find(T, daddr) >= 0;
 }
 
 template <int MODE, bool LDS>
@@ -365,33 +322,221 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
     for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64 + n_ctr2; j += BLOCK)
         smem[j] = 0;
     __syncthreads();
-    Counters C{smem, LDS ? smem + METRIC_U64 : nullptr, g_ctr, g_met};
+    uint32_t *s_met = smem;
+    uint32_t *s_ctr = smem + METRIC_U64;
+
+    constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
+    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
+    constexpr bool LPM = MODE != CFC_MODE_XDP;
 
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
     const uint64_t end = min(in.n, start + per_block);
-    for (uint64_t i = start + threadIdx.x; i < end; i += BLOCK) {
-        const uint32_t saddr = in.saddr[i], daddr = in.daddr[i];
-        const uint32_t ports = in.ports[i], meta = in.meta[i];
-        const uint32_t mark = in.mark ? in.mark[i] : 0u;
-        Res o{TC_ACT_OK, 0, 0};
-        if (MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL) {
-            bool pass = xdp_pass(T, saddr, daddr);
-            if (MODE == CFC_MODE_XDP || !pass) {
-                o.act = pass ? XDP_PASS : XDP_DROP;
-                o.ver = pass ? 0 : CFC_DROP_PREFILTER;
-                o.id = 0;
-            } else {
-                netdev_ingress(T, saddr, daddr, ports, meta, mark, C, o);
-            }
-        } else if (MODE == CFC_MODE_EGRESS) {
-            lxc_egress(T, E, saddr, daddr, ports, meta, C, o);
-        } else {
-            netdev_ingress(T, saddr, daddr, ports, meta, mark, C, o);
+    // trip count is uniform across the workgroup (metrics_wave needs whole waves)
+    for (uint64_t base = start; base < end; base += BLOCK) {
+        const uint64_t i = base + threadIdx.x;
+        const bool valid = i < end;
+        uint32_t sa = 0, da = 0, pt = 0, mt = 0, mk = 0;
+        if (valid) {
+            sa = ld_nt(in.saddr + i);
+            da = ld_nt(in.daddr + i);
+            pt = ld_nt(in.ports + i);
+            mt = ld_nt(in.meta + i);
+            if (in.mark)
+                mk = ld_nt(in.mark + i);
         }
-        out.verdict[i] = o.ver;
-        out.identity[i] = o.id;
-        if (out.action)
-            out.action[i] = (uint8_t)o.act;
+        const uint32_t proto = mt & 0xFF, len = mt >> 16;
+        const bool frag = (mt & CFC_HF_FRAG) != 0;
+
+        // ---- round 2: every lookup that only needs the header
+        uint32_t e24 = 0, pfd = 0;
+        B64 lx{}, pf{}, ls{};
+        const uint32_t la = EGR ? da : sa;
+        const uint32_t lh = __builtin_bswap32(la);
+        const uint32_t hsh = __builtin_bswap32(sa);
+        uint32_t lxb = 0, pfb = 0, lsb = 0;
+        if (valid) {
+            if (LPM && T.tbl24)
+                e24 = T.tbl24[lh >> 8];
+            if (XDP && T.pf_tbl24)
+                pfd = T.pf_tbl24[hsh >> 8];
+            if (T.lxc4) {
+                lxb = hash32(da, T.lxc4_mask);
+                lx = ldb(T.lxc4 + (size_t)lxb * LXC_SLOTS);
+                if (EGR) {
+                    lsb = hash32(sa, T.lxc4_mask);
+                    ls = ldb(T.lxc4 + (size_t)lsb * LXC_SLOTS);
+                }
+            }
+            if (XDP && T.pf_fix) {
+                pfb = hash32(sa, T.pf_fix_mask);
+                pf = ldb(T.pf_fix + (size_t)pfb * 16);
+            }
+        }
+
+        // ---- round 3: second-level LPM, endpoint records
+        if (e24 & LPM_GROUP)
+            e24 = T.tbl8[((e24 & ~LPM_GROUP) << 8) | (lh & 0xFF)];
+        if (e24 & LPM_INDIRECT)
+            e24 = T.lbl_ovf[e24 & LPM_PAYLOAD];
+        if (pfd & LPM_GROUP)
+            pfd = T.pf_tbl8[((pfd & ~LPM_GROUP) << 8) | (hsh & 0xFF)];
+        int ep = -1, es = -1;
+        if (valid && T.lxc4) {
+            int r = lxc_scan(lx, da, &ep);
+            if (r < 0)
+                ep = lxc_probe_from(T, da, lxb);
+            if (EGR) {
+                r = lxc_scan(ls, sa, &es);
+                if (r < 0)
+                    es = lxc_probe_from(T, sa, lsb);
+            }
+        }
+        EpRec rec{};
+        if (ep >= 0)
+            rec = T.eps[ep];
+        uint32_t src_lxc = NONE;
+        if (EGR && es >= 0)
+            src_lxc = T.eps[es].lxc_id;
+
+        int act = TC_ACT_OK, ver = 0;
+        uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
+        bool xdp_drop = false;
+        if (XDP && valid) {
+            bool deny = pfd != 0;
+            if (!deny && T.pf_fix) {
+                int r = pf_scan(pf, sa);
+                deny = r > 0 || (r < 0 && pf_probe_from(T, sa, pfb));
+            }
+            xdp_drop = deny || ep < 0;
+            if (MODE == CFC_MODE_XDP || xdp_drop) {
+                act = xdp_drop ? XDP_DROP : XDP_PASS;
+                ver = xdp_drop ? CFC_DROP_PREFILTER : 0;
+            }
+        }
+
+        // ---- round 4: identity, then the three policy buckets together
+        bool need_pol = false, skip_proxy = false;
+        uint32_t pbase = 0, pmask = 0, egress_bit = 0, dport = 0, src = 0;
+        if (valid && MODE != CFC_MODE_XDP && !xdp_drop) {
+            const bool known = ct_new_dport(proto, pt, &dport);
+            if (!EGR) {
+                // handle_identity_from_host (bpf_netdev.c:128-153)
+                const uint32_t magic = mk & 0xF00u;
+                if (magic == 0xA00u || magic == 0xB00u) {
+                    ident = ((mk & 0xFF) << 16) | (mk >> 16);
+                    skip_proxy = magic == 0xA00u;
+                } else {
+                    ident = magic == 0xC00u ? HOST_ID : WORLD_ID;
+                }
+                // handle_ipv4 (:375-398): reserved identities take the ipcache's
+                if (ident < HEALTH_ID && e24 && e24 != CLUSTER_ID && e24 != HOST_ID)
+                    ident = e24;
+                if (ep >= 0 && !(rec.flags & ENDPOINT_F_HOST)) {
+                    if (!rec.has_policy) {
+                        act = TC_ACT_SHOT;
+                        ver = DROP_MISSED_TAIL_CALL;
+                        met0 = mkey(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
+                    } else if (!known) {
+                        act = TC_ACT_SHOT;
+                        ver = DROP_CT_UNKNOWN_PROTO;
+                        met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
+                    } else {
+                        need_pol = true;
+                        pbase = rec.pol_base;
+                        pmask = rec.pol_mask;
+                        src = ident;
+                    }
+                }
+            } else {
+                act = TC_ACT_SHOT;
+                if (src_lxc != E.lxc_id) {   // is_valid_lxc_src_ipv4 (lxc.h:55)
+                    ver = DROP_INVALID_SIP;
+                    met0 = mkey(DROP_INVALID_SIP, METRIC_EGRESS);
+                } else if (!known) {
+                    ver = DROP_CT_UNKNOWN_PROTO;
+                    met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
+                } else {
+                    // destination identity (bpf_lxc.c:516-532)
+                    ident = e24 ? e24
+                                : ((da & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE
+                                       ? CLUSTER_ID
+                                       : WORLD_ID);
+                    need_pol = true;
+                    pbase = E.pol_base;
+                    pmask = E.pol_mask;
+                    egress_bit = 1;
+                    src = ident;
+                }
+            }
+        }
+        PolicyProbe P;
+        if (need_pol)
+            policy_issue(T, pbase, pmask, src, dport, proto, egress_bit, P);
+
+        if (need_pol) {
+            int v = policy_resolve(T, pbase, pmask, frag && !EGR, P, &ctr0);
+            const int mdir = EGR ? METRIC_EGRESS : METRIC_INGRESS;
+            if (v < 0) {
+                act = TC_ACT_SHOT;
+                ver = DROP_POLICY;
+                met0 = mkey(DROP_POLICY, mdir);
+            } else if (!EGR) {
+                if (skip_proxy)
+                    v = 0;
+                if (v > 0) {           // redirect_to_proxy
+                    act = TC_ACT_REDIRECT;
+                    ver = v;
+                } else {               // TRACE_TO_LXC
+                    met0 = mkey(0, METRIC_INGRESS);
+                    act = rec.ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+                    ver = 0;
+                }
+            } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
+                act = TC_ACT_REDIRECT;
+                ver = v;
+            } else {
+                met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
+                ver = 0;
+                if (ep < 0) {
+                    act = TC_ACT_OK;
+                } else if (rec.flags & ENDPOINT_F_HOST) {
+                    act = TC_ACT_REDIRECT;
+                } else if (!rec.has_policy) {
+                    act = TC_ACT_SHOT;
+                    ver = DROP_MISSED_TAIL_CALL;
+                    met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
+                } else {
+                    // local delivery: the destination's ipv4_policy with
+                    // src = SECLABEL of the sending endpoint
+                    int w = policy_access(T, rec.pol_base, rec.pol_mask,
+                                          E.seclabel, dport, proto, 0, frag,
+                                          &ctr1);
+                    if (w < 0) {
+                        act = TC_ACT_SHOT;
+                        ver = DROP_POLICY;
+                        met1 = mkey(DROP_POLICY, METRIC_INGRESS);
+                    } else if (w > 0) {
+                        act = TC_ACT_REDIRECT;
+                        ver = w;
+                    } else {
+                        met1 = mkey(0, METRIC_INGRESS);
+                        act = rec.ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+                    }
+                }
+            }
+        }
+
+        if (valid) {
+            st_nt(ver, out.verdict + i);
+            st_nt(ident, out.identity + i);
+            if (out.action)
+                out.action[i] = (uint8_t)act;
+            count_hit<LDS>(s_ctr, g_ctr, ctr0, len);
+            count_hit<LDS>(s_ctr, g_ctr, ctr1, len);
+        }
+        metrics_wave(s_met, nullptr, met0, len);
+        if (EGR)
+            metrics_wave(s_met, nullptr, met1, len);
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64; j += BLOCK) {
@@ -402,7 +547,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
     if (LDS) {
         uint32_t *dst = partial + (size_t)blockIdx.x * n_ctr2;
         for (uint32_t j = threadIdx.x; j < n_ctr2; j += BLOCK)
-            dst[j] = smem[METRIC_U64 + j];
+            st_nt(smem[METRIC_U64 + j], dst + j);
     }
 }
 
@@ -417,9 +562,18 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const uint32_t *partial
         return;
     uint64_t s = 0;
     for (uint32_t b = 0; b < nblk; b++)
-        s += partial[(size_t)b * n2 + j];
+        s += ld_nt(partial + (size_t)b * n2 + j);
     if (s)
         atomicAdd((unsigned long long *)&g_ctr[j], (unsigned long long)s);
+}
+
+__global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
+                                                 const uint64_t *src,
+                                                 uint64_t n)
+{
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n)
+        dst[i] += src[i];
 }
 
 template <int MODE, bool LDS>
@@ -433,8 +587,8 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
-                            hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(4ull * (METRIC_U64 + 2ull * LDS_CTR_MAX)));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(4ull * (METRIC_U64 + 2ull * LDS_CTR_MAX)));
         attr_set = true;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), lds, s, T, in, out, E,
@@ -446,26 +600,20 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
     }
 }
 
-uint32_t grid_for(uint64_t n, int num_cus, bool lds)
+// Workgroups of <= MAX_PER_BLOCK headers; at least one per CU when the
+// batch allows it.
+void geometry(uint64_t n, int num_cus, uint32_t *grid, uint64_t *per_block)
 {
-    uint64_t want = (n + BLOCK - 1) / BLOCK;
-    uint64_t cap = lds ? (uint64_t)num_cus : (uint64_t)num_cus * 2;
-    if (want < 1)
-        want = 1;
-    return (uint32_t)(want < cap ? want : cap);
+    uint64_t pb = (n + (uint64_t)num_cus - 1) / (uint64_t)num_cus;
+    pb = (pb + BLOCK - 1) / BLOCK * BLOCK;
+    if (pb < BLOCK)
+        pb = BLOCK;
+    if (pb > MAX_PER_BLOCK)
+        pb = MAX_PER_BLOCK;
+    *per_block = pb;
+    *grid = (uint32_t)((n + pb - 1) / pb);
 }
 
-}  // namespace
-
-namespace {
-__global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
-                                                 const uint64_t *src,
-                                                 uint64_t n)
-{
-    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n)
-        dst[i] += src[i];
-}
 }  // namespace
 
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
@@ -480,10 +628,12 @@ int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
 
 size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int num_cus)
 {
-    bool lds = n_ctr <= LDS_CTR_MAX;
-    if (!lds)
+    if (n_ctr > LDS_CTR_MAX || n == 0)
         return 0;
-    return 4ull * 2 * n_ctr * grid_for(n, num_cus, true);
+    uint32_t grid;
+    uint64_t pb;
+    geometry(n, num_cus, &grid, &pb);
+    return 4ull * 2 * n_ctr * grid;
 }
 
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
@@ -494,8 +644,9 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
     if (in.n == 0)
         return 0;
     bool lds = T.n_ctr <= LDS_CTR_MAX;
-    uint32_t grid = grid_for(in.n, num_cus, lds);
-    uint64_t per_block = (in.n + grid - 1) / grid;
+    uint32_t grid;
+    uint64_t per_block;
+    geometry(in.n, num_cus, &grid, &per_block);
 #define CFC_LAUNCH(M)                                                         \
     (lds ? launch_mode<M, true>(T, in, out, E, g_ctr, g_met, ws, grid,        \
                                 per_block, s)                                 \
