@@ -54,7 +54,7 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 
 struct Epoch {
     uint64_t id = 0;
-    DevBuf tbl24, tbl8, ovf, pf24, pf8, pffix, lxc4, eps, pol;
+    DevBuf tbl24, tbl8, ovf, pf24, pf8, pffix, lxc4, pol;
     DevTables T{};
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
@@ -171,15 +171,14 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     for (auto &kv : c->maps)
         ms.push_back(kv.second.get());
     HostImage img;
-    build_image(ms, c->seclabel.data(), &img);
+    build_image(ms, &img);
 
     auto E = std::make_unique<Epoch>();
     E->id = ++c->epoch_seq;
     if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
         (rc = upload_vec(E->ovf, img.lbl_ovf, s)) || (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
         (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
-        (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->eps, img.eps, s)) ||
-        (rc = upload_vec(E->pol, img.pol, s)))
+        (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)))
         return rc;
     DevTables &T = E->T;
     T.tbl24 = (const uint32_t *)E->tbl24.p;
@@ -189,10 +188,9 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     T.pf_tbl8 = (const uint32_t *)E->pf8.p;
     T.pf_fix = (const uint32_t *)E->pffix.p;
     T.pf_fix_mask = img.pf_fix_mask;
-    T.lxc4 = (const Lxc4Slot *)E->lxc4.p;
+    T.pf_fix_zero = img.pf_fix_zero;
+    T.lxc4 = (const LxcSlot *)E->lxc4.p;
     T.lxc4_mask = img.lxc4_mask;
-    T.n_eps = (uint32_t)img.eps.size();
-    T.eps = (const EpRec *)E->eps.p;
     T.pol = (const PolSlot *)E->pol.p;
     T.n_ctr = (uint32_t)img.ctr_owner.size();
     E->pol_loc = img.pol_loc;
@@ -202,7 +200,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->st.ipcache_v4_prefixes = img.n_prefix4;
     E->st.lpm4_tbl8_groups = (uint32_t)(img.tbl8.size() / 256);
     E->st.policy_entries = T.n_ctr;
-    E->st.endpoints = T.n_eps;
+    E->st.endpoints = img.n_eps;
     E->st.prefilter_v4_fix = img.n_pf_fix;
     E->st.prefilter_v4_dyn = img.n_pf_dyn;
 

@@ -47,7 +47,6 @@ constexpr int DROP_INVALID_SIP = -132, DROP_POLICY = -133,
 constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
 constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
-constexpr uint32_t ENDPOINT_F_HOST = 1;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint64_t MAX_PER_BLOCK = 65536;   // keeps u32 LDS sums exact
 
@@ -62,118 +61,41 @@ __device__ __forceinline__ void st_nt(T v, T *p)
     __builtin_nontemporal_store(v, p);
 }
 
-struct B64 {   // one 64-byte bucket
-    uint4 q[4];
-};
-__device__ __forceinline__ B64 ldb(const void *p)
+__device__ __forceinline__ uint4 ld16(const void *p)
 {
-    const uint4 *b = reinterpret_cast<const uint4 *>(p);
-    B64 r;
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-        r.q[i] = b[i];
-    return r;
+    return *reinterpret_cast<const uint4 *>(p);
 }
 
-// ---- lookups on a loaded bucket: 1 hit, 0 definite miss, -1 keep probing
-__device__ __forceinline__ int lxc_scan(const B64 &B, uint32_t addr, int *ep)
-{
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const uint4 v = B.q[i];
-        if (v.y == EMPTY)
-            return 0;
-        if (v.x == addr) {
-            *ep = (int)v.y;
-            return 1;
-        }
-        if (v.w == EMPTY)
-            return 0;
-        if (v.z == addr) {
-            *ep = (int)v.w;
-            return 1;
-        }
-    }
-    return -1;
-}
-
-__device__ __forceinline__ int pf_scan(const B64 &B, uint32_t addr)
-{
-    const uint32_t a[16] = {B.q[0].x, B.q[0].y, B.q[0].z, B.q[0].w,
-                            B.q[1].x, B.q[1].y, B.q[1].z, B.q[1].w,
-                            B.q[2].x, B.q[2].y, B.q[2].z, B.q[2].w,
-                            B.q[3].x, B.q[3].y, B.q[3].z, B.q[3].w};
-    const uint32_t cnt = a[15];
-    bool hit = false;
-#pragma unroll
-    for (int i = 0; i < PF_SLOTS; i++)
-        hit |= ((uint32_t)i < cnt) & (a[i] == addr);
-    return hit ? 1 : (cnt < (uint32_t)PF_SLOTS ? 0 : -1);
-}
-
-__device__ __forceinline__ int pol_scan(const B64 &B, uint64_t key,
-                                        uint32_t *ctr, uint32_t *proxy)
-{
-#pragma unroll
-    for (int s = 0; s < POL_SLOTS; s++) {
-        const uint4 v = B.q[s];
-        if (v.w == EMPTY)
-            return 0;
-        if ((((uint64_t)v.y << 32) | v.x) == key) {
-            *ctr = v.w;
-            *proxy = v.z & 0xFFFF;
-            return 1;
-        }
-    }
-    return -1;
-}
-
-// ---- probing continuations (cold paths)
-__device__ inline int lxc_probe_from(const DevTables &T, uint32_t addr,
-                                           uint32_t b)
+// ---- endpoint lookup: 16-byte slots, linear probing (layout.h)
+// resolve from the first loaded slot; returns the slot (info VALID) or a
+// zero slot for a miss
+__device__ __forceinline__ uint4 lxc_resolve(const DevTables &T, uint32_t addr,
+                                             uint32_t s, uint4 v)
 {
     for (;;) {
-        b = (b + 1) & T.lxc4_mask;
-        int ep = -1;
-        int r = lxc_scan(ldb(T.lxc4 + (size_t)b * LXC_SLOTS), addr, &ep);
-        if (r >= 0)
-            return r ? ep : -1;
+        if (!(v.w & LXC_VALID))
+            return make_uint4(0, 0, 0, 0);
+        if (v.x == addr)
+            return v;
+        s = (s + 1) & T.lxc4_mask;
+        v = ld16(T.lxc4 + s);
     }
 }
 
-__device__ inline bool pf_probe_from(const DevTables &T, uint32_t addr,
-                                           uint32_t b)
+// ---- prefilter /32 set: 16-byte buckets of 4 addresses, 0 = free
+__device__ __forceinline__ bool pf_resolve(const DevTables &T, uint32_t addr,
+                                           uint32_t b, uint4 v)
 {
+    if (addr == 0)
+        return T.pf_fix_zero != 0;
     for (;;) {
+        if (v.x == addr || v.y == addr || v.z == addr || v.w == addr)
+            return true;
+        if (!v.x || !v.y || !v.z || !v.w)
+            return false;
         b = (b + 1) & T.pf_fix_mask;
-        int r = pf_scan(ldb(T.pf_fix + (size_t)b * 16), addr);
-        if (r >= 0)
-            return r == 1;
+        v = ld16(T.pf_fix + (size_t)b * PF_SLOTS);
     }
-}
-
-__device__ inline uint32_t pol_probe_from(const PolSlot *pol,
-                                                uint32_t base, uint32_t mask,
-                                                uint64_t key, uint32_t b,
-                                                uint32_t *proxy)
-{
-    for (;;) {
-        b = (b + 1) & mask;
-        uint32_t c = NONE;
-        int r = pol_scan(ldb(pol + (size_t)(base + b) * POL_SLOTS), key, &c, proxy);
-        if (r >= 0)
-            return r ? c : NONE;
-    }
-}
-
-__device__ __forceinline__ int lxc_find(const DevTables &T, uint32_t addr)
-{
-    if (!T.lxc4)
-        return -1;
-    uint32_t b = hash32(addr, T.lxc4_mask);
-    int ep = -1;
-    int r = lxc_scan(ldb(T.lxc4 + (size_t)b * LXC_SLOTS), addr, &ep);
-    return r > 0 ? ep : (r == 0 ? -1 : lxc_probe_from(T, addr, b));
 }
 
 __device__ __forceinline__ uint64_t pkey(uint32_t id, uint32_t dport,
@@ -198,13 +120,14 @@ __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
     return proto == 1;
 }
 
-// __policy_can_access (policy.h:46-110), cb[CB_POLICY] == 0: the three keys'
-// buckets are loaded together, the first match in the reference's order
-// wins.  Returns the verdict (<0 drop) and the matched counter (or NONE).
+// __policy_can_access (policy.h:46-110), cb[CB_POLICY] == 0: the first
+// slot of each of the three keys (L4, L3, wildcard port) is loaded at once,
+// then the keys are resolved in the reference's order.  Returns the verdict
+// (<0 drop) and the matched counter (or NONE).
 struct PolicyProbe {
     uint64_t k[3];
-    uint32_t b[3];
-    B64 bk[3];
+    uint32_t s[3];
+    uint4 v[3];
 };
 
 __device__ __forceinline__ void policy_issue(const DevTables &T, uint32_t base,
@@ -217,8 +140,8 @@ __device__ __forceinline__ void policy_issue(const DevTables &T, uint32_t base,
     P.k[2] = pkey(0, dport, proto, egress);    // wildcard port
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        P.b[j] = hash64(P.k[j], mask);
-        P.bk[j] = ldb(T.pol + (size_t)(base + P.b[j]) * POL_SLOTS);
+        P.s[j] = hash64(P.k[j], mask);
+        P.v[j] = ld16(T.pol + base + P.s[j]);
     }
 }
 
@@ -227,17 +150,22 @@ __device__ __forceinline__ int policy_resolve(const DevTables &T, uint32_t base,
                                               const PolicyProbe &P,
                                               uint32_t *ctr)
 {
-    uint32_t proxy = 0, c = NONE;
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         if (frag && j != 1)   // fragments: L3 key only (policy.h:61,85)
             continue;
-        int r = pol_scan(P.bk[j], P.k[j], &c, &proxy);
-        if (r < 0)
-            c = pol_probe_from(T.pol, base, mask, P.k[j], P.b[j], &proxy);
-        if (r > 0 || (r < 0 && c != NONE)) {
-            *ctr = c;
-            return j == 1 ? TC_ACT_OK : (int)proxy;
+        uint4 v = P.v[j];
+        uint32_t s = P.s[j];
+        for (;;) {
+            const uint64_t key = ((uint64_t)v.y << 32) | v.x;
+            if (key == P.k[j]) {
+                *ctr = v.w;
+                return j == 1 ? TC_ACT_OK : (int)(v.z & 0xFFFF);
+            }
+            if (key == POL_EMPTY)
+                break;
+            s = (s + 1) & mask;
+            v = ld16(T.pol + base + s);
         }
     }
     *ctr = NONE;
@@ -349,65 +277,55 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
 
         // ---- round 2: every lookup that only needs the header
         uint32_t e24 = 0, pfd = 0;
-        B64 lx{}, pf{}, ls{};
+        uint4 lx = make_uint4(0, 0, 0, 0), pf = lx, ls = lx;
         const uint32_t la = EGR ? da : sa;
         const uint32_t lh = __builtin_bswap32(la);
         const uint32_t hsh = __builtin_bswap32(sa);
-        uint32_t lxb = 0, pfb = 0, lsb = 0;
+        uint32_t lxs = 0, pfb = 0, lss = 0;
         if (valid) {
             if (LPM && T.tbl24)
                 e24 = T.tbl24[lh >> 8];
             if (XDP && T.pf_tbl24)
                 pfd = T.pf_tbl24[hsh >> 8];
             if (T.lxc4) {
-                lxb = hash32(da, T.lxc4_mask);
-                lx = ldb(T.lxc4 + (size_t)lxb * LXC_SLOTS);
+                lxs = hash32(da, T.lxc4_mask);
+                lx = ld16(T.lxc4 + lxs);
                 if (EGR) {
-                    lsb = hash32(sa, T.lxc4_mask);
-                    ls = ldb(T.lxc4 + (size_t)lsb * LXC_SLOTS);
+                    lss = hash32(sa, T.lxc4_mask);
+                    ls = ld16(T.lxc4 + lss);
                 }
             }
             if (XDP && T.pf_fix) {
                 pfb = hash32(sa, T.pf_fix_mask);
-                pf = ldb(T.pf_fix + (size_t)pfb * 16);
+                pf = ld16(T.pf_fix + (size_t)pfb * PF_SLOTS);
             }
         }
 
-        // ---- round 3: second-level LPM, endpoint records
+        // ---- round 3: second-level LPM, endpoint slot resolution
         if (e24 & LPM_GROUP)
             e24 = T.tbl8[((e24 & ~LPM_GROUP) << 8) | (lh & 0xFF)];
         if (e24 & LPM_INDIRECT)
             e24 = T.lbl_ovf[e24 & LPM_PAYLOAD];
         if (pfd & LPM_GROUP)
             pfd = T.pf_tbl8[((pfd & ~LPM_GROUP) << 8) | (hsh & 0xFF)];
-        int ep = -1, es = -1;
+        // rec: {addr, pol_base, pol_mask, info}; info == 0 -> not local
+        uint4 rec = make_uint4(0, 0, 0, 0), srec = rec;
         if (valid && T.lxc4) {
-            int r = lxc_scan(lx, da, &ep);
-            if (r < 0)
-                ep = lxc_probe_from(T, da, lxb);
-            if (EGR) {
-                r = lxc_scan(ls, sa, &es);
-                if (r < 0)
-                    es = lxc_probe_from(T, sa, lsb);
-            }
+            rec = lxc_resolve(T, da, lxs, lx);
+            if (EGR)
+                srec = lxc_resolve(T, sa, lss, ls);
         }
-        EpRec rec{};
-        if (ep >= 0)
-            rec = T.eps[ep];
-        uint32_t src_lxc = NONE;
-        if (EGR && es >= 0)
-            src_lxc = T.eps[es].lxc_id;
+        const bool local = (rec.w & LXC_VALID) != 0;
+        const uint32_t src_lxc = (srec.w & LXC_VALID) ? (srec.w & 0xFFFF) : NONE;
 
         int act = TC_ACT_OK, ver = 0;
         uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
         bool xdp_drop = false;
         if (XDP && valid) {
             bool deny = pfd != 0;
-            if (!deny && T.pf_fix) {
-                int r = pf_scan(pf, sa);
-                deny = r > 0 || (r < 0 && pf_probe_from(T, sa, pfb));
-            }
-            xdp_drop = deny || ep < 0;
+            if (!deny && (T.pf_fix || T.pf_fix_zero))
+                deny = pf_resolve(T, sa, pfb, pf);
+            xdp_drop = deny || !local;
             if (MODE == CFC_MODE_XDP || xdp_drop) {
                 act = xdp_drop ? XDP_DROP : XDP_PASS;
                 ver = xdp_drop ? CFC_DROP_PREFILTER : 0;
@@ -431,8 +349,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
                 // handle_ipv4 (:375-398): reserved identities take the ipcache's
                 if (ident < HEALTH_ID && e24 && e24 != CLUSTER_ID && e24 != HOST_ID)
                     ident = e24;
-                if (ep >= 0 && !(rec.flags & ENDPOINT_F_HOST)) {
-                    if (!rec.has_policy) {
+                if (local && !(rec.w & LXC_HOST)) {
+                    if (!(rec.w & LXC_HAS_POLICY)) {
                         act = TC_ACT_SHOT;
                         ver = DROP_MISSED_TAIL_CALL;
                         met0 = mkey(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
@@ -442,8 +360,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
                         met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
                     } else {
                         need_pol = true;
-                        pbase = rec.pol_base;
-                        pmask = rec.pol_mask;
+                        pbase = rec.y;
+                        pmask = rec.z;
                         src = ident;
                     }
                 }
@@ -488,7 +406,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
                     ver = v;
                 } else {               // TRACE_TO_LXC
                     met0 = mkey(0, METRIC_INGRESS);
-                    act = rec.ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+                    act = (rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
                     ver = 0;
                 }
             } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
@@ -497,18 +415,18 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
             } else {
                 met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
                 ver = 0;
-                if (ep < 0) {
+                if (!local) {
                     act = TC_ACT_OK;
-                } else if (rec.flags & ENDPOINT_F_HOST) {
+                } else if (rec.w & LXC_HOST) {
                     act = TC_ACT_REDIRECT;
-                } else if (!rec.has_policy) {
+                } else if (!(rec.w & LXC_HAS_POLICY)) {
                     act = TC_ACT_SHOT;
                     ver = DROP_MISSED_TAIL_CALL;
                     met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
                 } else {
                     // local delivery: the destination's ipv4_policy with
                     // src = SECLABEL of the sending endpoint
-                    int w = policy_access(T, rec.pol_base, rec.pol_mask,
+                    int w = policy_access(T, rec.y, rec.z,
                                           E.seclabel, dport, proto, 0, frag,
                                           &ctr1);
                     if (w < 0) {
@@ -520,7 +438,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
                         ver = w;
                     } else {
                         met1 = mkey(0, METRIC_INGRESS);
-                        act = rec.ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
+                        act = (rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
                     }
                 }
             }
@@ -552,6 +470,8 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
 }
 
 // Sum the per-workgroup partial slabs per counter (column sums, coalesced).
+// blockIdx.x: 256 columns, blockIdx.y: REDUCE_ROWS partial rows.
+constexpr uint32_t REDUCE_ROWS = 32;
 __global__ __launch_bounds__(256) void k_reduce_partials(const uint32_t *partial,
                                                          uint32_t nblk,
                                                          uint32_t n2,
@@ -560,8 +480,10 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const uint32_t *partial
     uint32_t j = blockIdx.x * 256 + threadIdx.x;
     if (j >= n2)
         return;
+    uint32_t b0 = blockIdx.y * REDUCE_ROWS;
+    uint32_t b1 = min(nblk, b0 + REDUCE_ROWS);
     uint64_t s = 0;
-    for (uint32_t b = 0; b < nblk; b++)
+    for (uint32_t b = b0; b < b1; b++)
         s += ld_nt(partial + (size_t)b * n2 + j);
     if (s)
         atomicAdd((unsigned long long *)&g_ctr[j], (unsigned long long)s);
@@ -595,8 +517,9 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                        g_ctr, g_met, ws, per_block);
     if (LDS && T.n_ctr) {
         uint32_t n2 = 2 * T.n_ctr;
-        hipLaunchKernelGGL(k_reduce_partials, dim3((n2 + 255) / 256), dim3(256),
-                           0, s, ws, grid, n2, g_ctr);
+        hipLaunchKernelGGL(k_reduce_partials,
+                           dim3((n2 + 255) / 256, (grid + REDUCE_ROWS - 1) / REDUCE_ROWS),
+                           dim3(256), 0, s, ws, grid, n2, g_ctr);
     }
 }
 

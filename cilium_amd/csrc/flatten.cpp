@@ -18,8 +18,7 @@ uint64_t HostImage::device_bytes() const
 {
     return 4ull * (tbl24.size() + tbl8.size() + lbl_ovf.size() +
                    pf_tbl24.size() + pf_tbl8.size() + pf_fix.size()) +
-           sizeof(Lxc4Slot) * lxc4.size() + sizeof(EpRec) * eps.size() +
-           sizeof(PolSlot) * pol.size();
+           sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size();
 }
 
 // DIR-24-8: every prefix <= /24 fills its tbl24 range in ascending length
@@ -106,8 +105,7 @@ static void ipcache_v4(const Map *m, std::vector<Pfx4> *out,
                         leaf_for(b.second.second, ovf)});
 }
 
-void build_image(const std::vector<Map *> &maps, const uint32_t *seclabel,
-                 HostImage *img)
+void build_image(const std::vector<Map *> &maps, HostImage *img)
 {
     *img = HostImage();
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,
@@ -154,110 +152,110 @@ void build_image(const std::vector<Map *> &maps, const uint32_t *seclabel,
             uint32_t P, a;
             memcpy(&P, k, 4);
             memcpy(&a, k + 4, 4);
-            if (P == 32)  // check_v4 looks up {prefixlen 32, saddr} exactly
+            if (P != 32)   // check_v4 looks up {prefixlen 32, saddr} exactly
+                continue;
+            if (a == 0)
+                img->pf_fix_zero = 1;   // 0 marks free slots
+            else
                 addrs.push_back(a);
         }
-        img->n_pf_fix = (uint32_t)addrs.size();
+        img->n_pf_fix = (uint32_t)addrs.size() + img->pf_fix_zero;
         if (!addrs.empty()) {
-            uint32_t nb = pow2_at_least((addrs.size() * 2 + PF_SLOTS - 1) / PF_SLOTS);
-            img->pf_fix.assign((size_t)nb * 16, 0);
+            // load factor <= 25%: 4-address buckets, one per expected address
+            uint32_t nb = pow2_at_least(addrs.size());
+            img->pf_fix.assign((size_t)nb * PF_SLOTS, 0);
             img->pf_fix_mask = nb - 1;
             for (uint32_t a : addrs) {
                 uint32_t b = hash32(a, nb - 1);
-                while (img->pf_fix[(size_t)b * 16 + 15] == PF_SLOTS)
+                for (;;) {
+                    uint32_t *bk = &img->pf_fix[(size_t)b * PF_SLOTS];
+                    int s = 0;
+                    while (s < PF_SLOTS && bk[s])
+                        s++;
+                    if (s < PF_SLOTS) {
+                        bk[s] = a;
+                        break;
+                    }
                     b = (b + 1) & (nb - 1);
-                uint32_t *bk = &img->pf_fix[(size_t)b * 16];
-                bk[bk[15]++] = a;
+                }
             }
         }
     }
 
-    // ---- policy tables (deterministic: ascending lxc id, key order)
+    // ---- policy tables (deterministic: ascending lxc id, key order);
+    //      linear probing over 16-byte slots at load factor <= 25%
     for (auto &pm : pols) {
         Map *m = pm.second;
         PolLoc loc;
         loc.present = 1;
-        uint32_t n = (uint32_t)m->kv.size();
-        uint32_t nb = pow2_at_least(std::max<uint64_t>(1, (n * 2 + POL_SLOTS - 1) / POL_SLOTS));
-        if (nb < 2 && n)
-            nb = 2;
-        loc.base = (uint32_t)(img->pol.size() / POL_SLOTS);
-        loc.mask = nb - 1;
+        uint32_t n = 0;
+        for (const auto &kv : m->kv)
+            n += ((uint8_t)kv.first[7] & 0xFE) == 0;
+        uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 4ull * n));
+        loc.base = (uint32_t)img->pol.size();
+        loc.mask = ns - 1;
         PolSlot empty{};
+        empty.key = POL_EMPTY;
         empty.ctr = EMPTY;
-        img->pol.resize(img->pol.size() + (size_t)nb * POL_SLOTS, empty);
-        PolSlot *tab = img->pol.data() + (size_t)loc.base * POL_SLOTS;
+        img->pol.resize(img->pol.size() + ns, empty);
+        PolSlot *tab = img->pol.data() + loc.base;
         for (const auto &kv : m->kv) {
             uint64_t key;
             memcpy(&key, kv.first.data(), 8);
+            if (((uint8_t)kv.first[7] & 0xFE) != 0)
+                continue;   // pad bits set: no datapath lookup can match it
             uint16_t proxy;
             memcpy(&proxy, kv.second.val.data(), 2);
-            uint32_t b = hash64(key, loc.mask);
-            for (;;) {
-                PolSlot *bk = tab + (size_t)b * POL_SLOTS;
-                int s = 0;
-                while (s < POL_SLOTS && bk[s].ctr != EMPTY)
-                    s++;
-                if (s < POL_SLOTS) {
-                    bk[s].key = key;
-                    bk[s].proxy_port = proxy;
-                    bk[s].ctr = (uint32_t)img->ctr_owner.size();
-                    img->ctr_owner.emplace_back(m, kv.first);
-                    break;
-                }
-                b = (b + 1) & loc.mask;
-            }
+            uint32_t s = hash64(key, loc.mask);
+            while (tab[s].key != POL_EMPTY)
+                s = (s + 1) & loc.mask;
+            tab[s].key = key;
+            tab[s].proxy_port = proxy;
+            tab[s].ctr = (uint32_t)img->ctr_owner.size();
+            img->ctr_owner.emplace_back(m, kv.first);
         }
         img->pol_loc[pm.first] = loc;
     }
 
-    // ---- endpoints (cilium_lxc): IPv4 keys {ip4, 0 x12, family 1, 0, 0}
+    // ---- endpoints (cilium_lxc): IPv4 keys {ip4, 0 x12, family 1, 0, 0},
+    //      the endpoint record inlined in the slot
     if (lxc && lxc->ksz == 20 && lxc->vsz >= 12) {
-        std::vector<std::pair<uint32_t, uint32_t>> v4;  // addr, ep index
+        std::vector<LxcSlot> v4;
         for (const auto &kv : lxc->kv) {
             const uint8_t *k = (const uint8_t *)kv.first.data();
             const uint8_t *v = (const uint8_t *)kv.second.val.data();
-            EpRec r{};
-            memcpy(&r.ifindex, v, 4);
-            uint16_t id;
-            memcpy(&id, v + 6, 2);
-            r.lxc_id = id;
-            memcpy(&r.flags, v + 8, 4);
-            r.seclabel = seclabel[id];
-            auto it = img->pol_loc.find(id);
-            if (it != img->pol_loc.end()) {
-                r.pol_base = it->second.base;
-                r.pol_mask = it->second.mask;
-                r.has_policy = 1;
-            }
             bool is_v4 = k[16] == 1 && k[17] == 0 && k[18] == 0 && k[19] == 0;
             for (int i = 4; i < 16 && is_v4; i++)
                 is_v4 = k[i] == 0;
             if (!is_v4)
                 continue;  // IPv6 endpoints: next step of the build
-            uint32_t a;
-            memcpy(&a, k, 4);
-            v4.emplace_back(a, (uint32_t)img->eps.size());
-            img->eps.push_back(r);
+            LxcSlot r{};
+            memcpy(&r.addr, k, 4);
+            uint32_t ifindex, flags;
+            uint16_t id;
+            memcpy(&ifindex, v, 4);
+            memcpy(&id, v + 6, 2);
+            memcpy(&flags, v + 8, 4);
+            r.info = id | LXC_VALID | ((flags & 1) ? LXC_HOST : 0) |
+                     (ifindex ? LXC_IFINDEX : 0);
+            auto it = img->pol_loc.find(id);
+            if (it != img->pol_loc.end()) {
+                r.pol_base = it->second.base;
+                r.pol_mask = it->second.mask;
+                r.info |= LXC_HAS_POLICY;
+            }
+            v4.push_back(r);
         }
+        img->n_eps = (uint32_t)v4.size();
         if (!v4.empty()) {
-            uint32_t nb = pow2_at_least((v4.size() * 2 + LXC_SLOTS - 1) / LXC_SLOTS);
-            Lxc4Slot empty{0, EMPTY};
-            img->lxc4.assign((size_t)nb * LXC_SLOTS, empty);
-            img->lxc4_mask = nb - 1;
-            for (auto &e : v4) {
-                uint32_t b = hash32(e.first, nb - 1);
-                for (;;) {
-                    Lxc4Slot *bk = &img->lxc4[(size_t)b * LXC_SLOTS];
-                    int s = 0;
-                    while (s < LXC_SLOTS && bk[s].ep != EMPTY)
-                        s++;
-                    if (s < LXC_SLOTS) {
-                        bk[s] = {e.first, e.second};
-                        break;
-                    }
-                    b = (b + 1) & (nb - 1);
-                }
+            uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 4ull * v4.size()));
+            img->lxc4.assign(ns, LxcSlot{});
+            img->lxc4_mask = ns - 1;
+            for (const LxcSlot &e : v4) {
+                uint32_t s = hash32(e.addr, ns - 1);
+                while (img->lxc4[s].info & LXC_VALID)
+                    s = (s + 1) & (ns - 1);
+                img->lxc4[s] = e;
             }
         }
     }

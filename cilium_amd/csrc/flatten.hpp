@@ -23,11 +23,10 @@ struct HostImage {
     std::vector<uint32_t> pf_tbl24, pf_tbl8;
     uint32_t n_pf_dyn = 0;
     std::vector<uint32_t> pf_fix;
-    uint32_t pf_fix_mask = 0, n_pf_fix = 0;
+    uint32_t pf_fix_mask = 0, pf_fix_zero = 0, n_pf_fix = 0;
     // endpoints
-    std::vector<Lxc4Slot> lxc4;
-    uint32_t lxc4_mask = 0;
-    std::vector<EpRec> eps;
+    std::vector<LxcSlot> lxc4;
+    uint32_t lxc4_mask = 0, n_eps = 0;
     // policy
     std::vector<PolSlot> pol;
     std::unordered_map<int, PolLoc> pol_loc;       // lxc_id -> table
@@ -35,9 +34,8 @@ struct HostImage {
     uint64_t device_bytes() const;
 };
 
-// maps: every map of the context.  seclabel: per-lxc SECLABEL.
-void build_image(const std::vector<Map *> &maps, const uint32_t *seclabel,
-                 HostImage *img);
+// maps: every map of the context.
+void build_image(const std::vector<Map *> &maps, HostImage *img);
 
 // exposed for host-side unit tests of the DIR-24-8 builder
 struct Pfx4 {

@@ -2,16 +2,22 @@
 // HIP kernels (classify.hip).  Everything here is plain data: the kernels get
 // one DevTables by value per launch.
 //
-// HBM layout of one epoch (all read-only while classifying):
-//   lpm4      DIR-24-8 IPv4 ipcache: tbl24 (2^24 x u32 = 64 MiB, sits in the
-//             256 MiB Infinity Cache) + 256-entry tbl8 groups for /25-/32.
-//   pf4_dyn   same structure for the prefilter LPM deny-list (only if used)
-//   pf4_fix   exact /32 deny set: 64-B buckets of 15 addresses + count
-//   lxc4      local endpoints by IPv4: 64-B buckets of 8 {addr, ep index}
-//   eps       endpoint records (32 B)
-//   pol       all endpoints' policy hash tables: 64-B buckets of 4 slots
+// Every probe is ONE 16-byte load per lane (global_load_dwordx4): on gfx950
+// the per-CU address unit (TA) spends a cycle per distinct cache line a wave
+// instruction touches, so a random-access kernel is bound by the number of
+// divergent load instructions, not by bytes.  Tables are therefore sized for
+// short probe sequences (load factor <= 25%) rather than for compactness —
+// they are small next to 288 GB of HBM3E and stay L2/Infinity-Cache resident.
+//
+// HBM layout of one epoch (read-only while classifying):
+//   lpm4      DIR-24-8 IPv4 ipcache: tbl24 (2^24 x u32 = 64 MiB, resident in
+//             the 256 MiB Infinity Cache) + 256-entry tbl8 groups for /25-/32
+//   pf4_dyn   same structure for the prefilter LPM deny-list (when used)
+//   pf4_fix   exact /32 deny set: 16-B buckets of 4 addresses (0 = empty)
+//   lxc4      local endpoints by IPv4: 16-B slots with the endpoint record
+//   pol       every endpoint's policy table: 16-B slots
 //             {key u64, proxy u16, pad, counter index u32}
-//   lbl_ovf   identities >= 2^30 (rare) referenced indirectly from LPM leaves
+//   lbl_ovf   identities >= 2^30 (rare) referenced from LPM leaves
 // Counters (read-write): u64 packets/bytes per policy entry + metrics.
 #pragma once
 #include <stdint.h>
@@ -30,37 +36,37 @@ constexpr uint32_t LPM_GROUP = 0x80000000u;
 constexpr uint32_t LPM_INDIRECT = 0x40000000u;
 constexpr uint32_t LPM_PAYLOAD = 0x3FFFFFFFu;
 
-// ---- 64-byte bucket hash tables --------------------------------------------
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 
-struct alignas(16) PolSlot {       // 16 B; 4 per 64-B bucket
+// ---- policy: open addressing, linear probing over 16-byte slots -------------
+// The datapath only ever looks up keys whose pad bits (byte 7, bits 1-7) are
+// zero (policy.h:53-59), so an all-ones key marks a free slot and stored keys
+// with pad bits set — which no lookup can match — are left out of the table.
+constexpr uint64_t POL_EMPTY = ~0ull;
+struct alignas(16) PolSlot {
     uint64_t key;                  // struct policy_key raw bytes (LE load)
     uint16_t proxy_port;           // policy_entry.proxy_port (be16 raw)
     uint16_t pad;
-    uint32_t ctr;                  // counter index, EMPTY = free slot
+    uint32_t ctr;                  // counter index
 };
-constexpr int POL_SLOTS = 4;
 
-struct Lxc4Slot {                  // 8 B; 8 per bucket
+// ---- endpoints (cilium_lxc), IPv4 keys: 16-byte slots, linear probing -------
+// info: bits 0-15 lxc_id, then flags
+constexpr uint32_t LXC_HOST = 1u << 16;       // ENDPOINT_F_HOST
+constexpr uint32_t LXC_HAS_POLICY = 1u << 17; // an endpoint program exists
+constexpr uint32_t LXC_IFINDEX = 1u << 18;    // ifindex != 0 (redirect)
+constexpr uint32_t LXC_VALID = 1u << 31;      // 0 = free slot
+struct alignas(16) LxcSlot {
     uint32_t addr;                 // be32 raw
-    uint32_t ep;                   // index into eps, EMPTY = free slot
-};
-constexpr int LXC_SLOTS = 8;
-
-constexpr int PF_SLOTS = 15;       // pf4_fix bucket: u32 addr[15] + u32 count
-
-struct alignas(16) EpRec {         // 32 B
-    uint32_t lxc_id;
-    uint32_t ifindex;
-    uint32_t flags;                // ENDPOINT_F_HOST = 1
-    uint32_t seclabel;             // SECLABEL of the endpoint program
-    uint32_t pol_base;             // first bucket of its policy table
-    uint32_t pol_mask;             // buckets - 1 (power of two), 0 = empty table
-    uint32_t has_policy;
-    uint32_t pad;
+    uint32_t pol_base;             // first slot of its policy table
+    uint32_t pol_mask;             // slots - 1 (power of two)
+    uint32_t info;
 };
 
-// Hashes: multiplicative (Fibonacci) hashing of the raw key, top bits.
+// ---- prefilter /32 set: 16-byte buckets of 4 addresses, 0 = empty -----------
+constexpr int PF_SLOTS = 4;
+
+// Hashes of the raw keys.
 __host__ __device__ inline uint32_t hash64(uint64_t k, uint32_t mask)
 {
     k ^= k >> 29;
@@ -75,22 +81,18 @@ __host__ __device__ inline uint32_t hash32(uint32_t k, uint32_t mask)
 }
 
 struct DevTables {
-    const uint32_t *tbl24;         // may be null when no v4 ipcache prefixes
+    const uint32_t *tbl24;         // null when no v4 ipcache prefixes
     const uint32_t *tbl8;
     const uint32_t *lbl_ovf;
-    uint32_t lpm4_default;         // tbl24 == null: value of a /0 prefix (or 0)
     const uint32_t *pf_tbl24;      // null when the dyn prefilter is empty
     const uint32_t *pf_tbl8;
-    const uint32_t *pf_fix;        // buckets of 16 u32, null when empty
-    uint32_t pf_fix_mask;
-    uint32_t pf_dyn_default;       // pf_tbl24 == null: 1 if a /0 deny exists
-    const Lxc4Slot *lxc4;          // buckets of LXC_SLOTS slots
-    uint32_t lxc4_mask;
-    uint32_t n_eps;
-    const EpRec *eps;
-    const PolSlot *pol;            // buckets of POL_SLOTS slots
+    const uint32_t *pf_fix;        // buckets of 4 u32, null when empty
+    const LxcSlot *lxc4;           // null when no IPv4 endpoints
+    const PolSlot *pol;
+    uint32_t pf_fix_mask;          // buckets - 1
+    uint32_t pf_fix_zero;          // 0.0.0.0/32 is in the deny set
+    uint32_t lxc4_mask;            // slots - 1
     uint32_t n_ctr;                // policy entries (counter slots)
-    uint32_t pad;
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]
