@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcfc.so")
+# CFC_LIB selects an alternative in-tree build (kernel A/B experiments)
+LIB_PATH = os.path.join(HERE, os.environ.get("CFC_LIB", "libcfc.so"))
 
 CFC_DEVICE_NONE = -1
 MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3

@@ -49,6 +49,9 @@ constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr uint64_t MAX_PER_BLOCK = 65536;   // keeps u32 LDS sums exact
+#ifndef CFC_UNROLL
+#define CFC_UNROLL 2   // headers in flight per thread
+#endif
 
 template <class T>
 __device__ __forceinline__ T ld_nt(const T *p)
@@ -240,7 +243,233 @@ __device__ __forceinline__ void count_hit(uint32_t *s_ctr, uint64_t *g_ctr,
     }
 }
 
-template <int MODE, bool LDS>
+// Per-header state carried through the lookup rounds.
+struct Hdr {
+    uint32_t sa, da, pt, mt, mk;
+    bool valid;
+    uint32_t e24, pfd, lh, hsh, lxs, lss, pfb;
+    uint4 lx, ls, pf, rec;
+    uint32_t src_lxc;
+    int act, ver;
+    uint32_t ident, met0, met1, ctr0, ctr1;
+    bool xdp_drop, need_pol, skip_proxy;
+    uint32_t pbase, pmask, egress_bit, dport;
+    PolicyProbe P;
+};
+
+// round 1: the header (non-temporal streaming loads)
+template <int MODE>
+__device__ __forceinline__ void r1_load(const cfc_hdr_v4 &in, uint64_t i,
+                                        uint64_t end, Hdr &h)
+{
+    h.valid = i < end;
+    h.sa = h.da = h.pt = h.mt = h.mk = 0;
+    if (h.valid) {
+        h.sa = ld_nt(in.saddr + i);
+        h.da = ld_nt(in.daddr + i);
+        h.pt = ld_nt(in.ports + i);
+        h.mt = ld_nt(in.meta + i);
+        if (in.mark)
+            h.mk = ld_nt(in.mark + i);
+    }
+}
+
+// round 2: every lookup that only needs the header
+template <int MODE>
+__device__ __forceinline__ void r2_issue(const DevTables &T, Hdr &h)
+{
+    constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
+    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
+    constexpr bool LPM = MODE != CFC_MODE_XDP;
+    h.e24 = h.pfd = 0;
+    h.lx = h.ls = h.pf = make_uint4(0, 0, 0, 0);
+    h.lh = __builtin_bswap32(EGR ? h.da : h.sa);
+    h.hsh = __builtin_bswap32(h.sa);
+    h.lxs = h.lss = h.pfb = 0;
+    if (!h.valid)
+        return;
+    if (LPM && T.tbl24)
+        h.e24 = T.tbl24[h.lh >> 8];
+    if (XDP && T.pf_tbl24)
+        h.pfd = T.pf_tbl24[h.hsh >> 8];
+    if (T.lxc4) {
+        h.lxs = hash32(h.da, T.lxc4_mask);
+        h.lx = ld16(T.lxc4 + h.lxs);
+        if (EGR) {
+            h.lss = hash32(h.sa, T.lxc4_mask);
+            h.ls = ld16(T.lxc4 + h.lss);
+        }
+    }
+    if (XDP && T.pf_fix) {
+        h.pfb = hash32(h.sa, T.pf_fix_mask);
+        h.pf = ld16(T.pf_fix + (size_t)h.pfb * PF_SLOTS);
+    }
+}
+
+// round 3: second-level LPM, endpoint resolution, prefilter verdict,
+// identity, and the first slot of the three policy keys
+template <int MODE>
+__device__ __forceinline__ void r3_identity(const DevTables &T,
+                                            const EgressArgs &E, Hdr &h)
+{
+    constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
+    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
+    if (h.e24 & LPM_GROUP)
+        h.e24 = T.tbl8[((h.e24 & ~LPM_GROUP) << 8) | (h.lh & 0xFF)];
+    if (h.e24 & LPM_INDIRECT)
+        h.e24 = T.lbl_ovf[h.e24 & LPM_PAYLOAD];
+    if (h.pfd & LPM_GROUP)
+        h.pfd = T.pf_tbl8[((h.pfd & ~LPM_GROUP) << 8) | (h.hsh & 0xFF)];
+    // rec: {addr, pol_base, pol_mask, info}; info == 0 -> not local
+    h.rec = make_uint4(0, 0, 0, 0);
+    uint4 srec = h.rec;
+    if (h.valid && T.lxc4) {
+        h.rec = lxc_resolve(T, h.da, h.lxs, h.lx);
+        if (EGR)
+            srec = lxc_resolve(T, h.sa, h.lss, h.ls);
+    }
+    const bool local = (h.rec.w & LXC_VALID) != 0;
+    h.src_lxc = (srec.w & LXC_VALID) ? (srec.w & 0xFFFF) : NONE;
+
+    h.act = TC_ACT_OK;
+    h.ver = 0;
+    h.ident = 0;
+    h.met0 = h.met1 = h.ctr0 = h.ctr1 = NONE;
+    h.xdp_drop = false;
+    if (XDP && h.valid) {
+        bool deny = h.pfd != 0;
+        if (!deny && (T.pf_fix || T.pf_fix_zero))
+            deny = pf_resolve(T, h.sa, h.pfb, h.pf);
+        h.xdp_drop = deny || !local;
+        if (MODE == CFC_MODE_XDP || h.xdp_drop) {
+            h.act = h.xdp_drop ? XDP_DROP : XDP_PASS;
+            h.ver = h.xdp_drop ? CFC_DROP_PREFILTER : 0;
+        }
+    }
+
+    h.need_pol = h.skip_proxy = false;
+    h.pbase = h.pmask = h.egress_bit = h.dport = 0;
+    if (!h.valid || MODE == CFC_MODE_XDP || h.xdp_drop)
+        return;
+    const uint32_t proto = h.mt & 0xFF;
+    const bool known = ct_new_dport(proto, h.pt, &h.dport);
+    if (!EGR) {
+        // handle_identity_from_host (bpf_netdev.c:128-153)
+        const uint32_t magic = h.mk & 0xF00u;
+        if (magic == 0xA00u || magic == 0xB00u) {
+            h.ident = ((h.mk & 0xFF) << 16) | (h.mk >> 16);
+            h.skip_proxy = magic == 0xA00u;
+        } else {
+            h.ident = magic == 0xC00u ? HOST_ID : WORLD_ID;
+        }
+        // handle_ipv4 (:375-398): reserved identities take the ipcache's
+        if (h.ident < HEALTH_ID && h.e24 && h.e24 != CLUSTER_ID && h.e24 != HOST_ID)
+            h.ident = h.e24;
+        if (local && !(h.rec.w & LXC_HOST)) {
+            if (!(h.rec.w & LXC_HAS_POLICY)) {
+                h.act = TC_ACT_SHOT;
+                h.ver = DROP_MISSED_TAIL_CALL;
+                h.met0 = mkey(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
+            } else if (!known) {
+                h.act = TC_ACT_SHOT;
+                h.ver = DROP_CT_UNKNOWN_PROTO;
+                h.met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
+            } else {
+                h.need_pol = true;
+                h.pbase = h.rec.y;
+                h.pmask = h.rec.z;
+            }
+        }
+    } else {
+        h.act = TC_ACT_SHOT;
+        if (h.src_lxc != E.lxc_id) {   // is_valid_lxc_src_ipv4 (lxc.h:55)
+            h.ver = DROP_INVALID_SIP;
+            h.met0 = mkey(DROP_INVALID_SIP, METRIC_EGRESS);
+        } else if (!known) {
+            h.ver = DROP_CT_UNKNOWN_PROTO;
+            h.met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
+        } else {
+            // destination identity (bpf_lxc.c:516-532)
+            h.ident = h.e24 ? h.e24
+                            : ((h.da & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE
+                                   ? CLUSTER_ID
+                                   : WORLD_ID);
+            h.need_pol = true;
+            h.pbase = E.pol_base;
+            h.pmask = E.pol_mask;
+            h.egress_bit = 1;
+        }
+    }
+    if (h.need_pol)
+        policy_issue(T, h.pbase, h.pmask, h.ident, h.dport, proto,
+                     h.egress_bit, h.P);
+}
+
+// round 4: resolve the policy verdict, compose the program result
+template <int MODE>
+__device__ __forceinline__ void r4_verdict(const DevTables &T,
+                                           const EgressArgs &E, Hdr &h)
+{
+    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
+    if (!h.need_pol)
+        return;
+    const bool frag = (h.mt & CFC_HF_FRAG) != 0;
+    const uint32_t proto = h.mt & 0xFF;
+    int v = policy_resolve(T, h.pbase, h.pmask, frag && !EGR, h.P, &h.ctr0);
+    const int mdir = EGR ? METRIC_EGRESS : METRIC_INGRESS;
+    if (v < 0) {
+        h.act = TC_ACT_SHOT;
+        h.ver = DROP_POLICY;
+        h.met0 = mkey(DROP_POLICY, mdir);
+    } else if (!EGR) {
+        if (h.skip_proxy)
+            v = 0;
+        if (v > 0) {           // redirect_to_proxy
+            h.act = TC_ACT_REDIRECT;
+            h.ver = v;
+        } else {               // TRACE_TO_LXC
+            h.met0 = mkey(0, METRIC_INGRESS);
+            h.act = (h.rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
+            h.ver = 0;
+        }
+    } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
+        h.act = TC_ACT_REDIRECT;
+        h.ver = v;
+    } else {
+        h.met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
+        h.ver = 0;
+        if (!(h.rec.w & LXC_VALID)) {
+            h.act = TC_ACT_OK;
+        } else if (h.rec.w & LXC_HOST) {
+            h.act = TC_ACT_REDIRECT;
+        } else if (!(h.rec.w & LXC_HAS_POLICY)) {
+            h.act = TC_ACT_SHOT;
+            h.ver = DROP_MISSED_TAIL_CALL;
+            h.met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
+        } else {
+            // local delivery: the destination's ipv4_policy with
+            // src = SECLABEL of the sending endpoint
+            int w = policy_access(T, h.rec.y, h.rec.z, E.seclabel, h.dport,
+                                  proto, 0, frag, &h.ctr1);
+            if (w < 0) {
+                h.act = TC_ACT_SHOT;
+                h.ver = DROP_POLICY;
+                h.met1 = mkey(DROP_POLICY, METRIC_INGRESS);
+            } else if (w > 0) {
+                h.act = TC_ACT_REDIRECT;
+                h.ver = w;
+            } else {
+                h.met1 = mkey(0, METRIC_INGRESS);
+                h.act = (h.rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
+            }
+        }
+    }
+}
+
+// U headers per thread go through the rounds side by side, so each thread
+// keeps U independent lookup chains in flight (occupancy is capped at one
+// workgroup per CU by the LDS counter slab).
+template <int MODE, bool LDS, int U>
 __global__ __launch_bounds__(BLOCK) void k_classify_v4(
     DevTables T, cfc_hdr_v4 in, cfc_out out, EgressArgs E, uint64_t *g_ctr,
     uint64_t *g_met, uint32_t *partial, uint64_t per_block)
@@ -253,208 +482,40 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
     uint32_t *s_met = smem;
     uint32_t *s_ctr = smem + METRIC_U64;
 
-    constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
-    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
-    constexpr bool LPM = MODE != CFC_MODE_XDP;
-
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
     const uint64_t end = min(in.n, start + per_block);
-    // trip count is uniform across the workgroup (metrics_wave needs whole waves)
-    for (uint64_t base = start; base < end; base += BLOCK) {
-        const uint64_t i = base + threadIdx.x;
-        const bool valid = i < end;
-        uint32_t sa = 0, da = 0, pt = 0, mt = 0, mk = 0;
-        if (valid) {
-            sa = ld_nt(in.saddr + i);
-            da = ld_nt(in.daddr + i);
-            pt = ld_nt(in.ports + i);
-            mt = ld_nt(in.meta + i);
-            if (in.mark)
-                mk = ld_nt(in.mark + i);
-        }
-        const uint32_t proto = mt & 0xFF, len = mt >> 16;
-        const bool frag = (mt & CFC_HF_FRAG) != 0;
-
-        // ---- round 2: every lookup that only needs the header
-        uint32_t e24 = 0, pfd = 0;
-        uint4 lx = make_uint4(0, 0, 0, 0), pf = lx, ls = lx;
-        const uint32_t la = EGR ? da : sa;
-        const uint32_t lh = __builtin_bswap32(la);
-        const uint32_t hsh = __builtin_bswap32(sa);
-        uint32_t lxs = 0, pfb = 0, lss = 0;
-        if (valid) {
-            if (LPM && T.tbl24)
-                e24 = T.tbl24[lh >> 8];
-            if (XDP && T.pf_tbl24)
-                pfd = T.pf_tbl24[hsh >> 8];
-            if (T.lxc4) {
-                lxs = hash32(da, T.lxc4_mask);
-                lx = ld16(T.lxc4 + lxs);
-                if (EGR) {
-                    lss = hash32(sa, T.lxc4_mask);
-                    ls = ld16(T.lxc4 + lss);
-                }
+    // the trip count is uniform across the workgroup (metrics_wave needs
+    // whole waves)
+    for (uint64_t base = start; base < end; base += (uint64_t)BLOCK * U) {
+        Hdr h[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            r1_load<MODE>(in, base + (uint64_t)u * BLOCK + threadIdx.x, end, h[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            r2_issue<MODE>(T, h[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            r3_identity<MODE>(T, E, h[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            r4_verdict<MODE>(T, E, h[u]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
+            const uint32_t len = h[u].mt >> 16;
+            if (h[u].valid) {
+                st_nt(h[u].ver, out.verdict + i);
+                st_nt(h[u].ident, out.identity + i);
+                if (out.action)
+                    out.action[i] = (uint8_t)h[u].act;
+                count_hit<LDS>(s_ctr, g_ctr, h[u].ctr0, len);
+                count_hit<LDS>(s_ctr, g_ctr, h[u].ctr1, len);
             }
-            if (XDP && T.pf_fix) {
-                pfb = hash32(sa, T.pf_fix_mask);
-                pf = ld16(T.pf_fix + (size_t)pfb * PF_SLOTS);
-            }
+            metrics_wave(s_met, nullptr, h[u].met0, len);
+            if (MODE == CFC_MODE_EGRESS)
+                metrics_wave(s_met, nullptr, h[u].met1, len);
         }
-
-        // ---- round 3: second-level LPM, endpoint slot resolution
-        if (e24 & LPM_GROUP)
-            e24 = T.tbl8[((e24 & ~LPM_GROUP) << 8) | (lh & 0xFF)];
-        if (e24 & LPM_INDIRECT)
-            e24 = T.lbl_ovf[e24 & LPM_PAYLOAD];
-        if (pfd & LPM_GROUP)
-            pfd = T.pf_tbl8[((pfd & ~LPM_GROUP) << 8) | (hsh & 0xFF)];
-        // rec: {addr, pol_base, pol_mask, info}; info == 0 -> not local
-        uint4 rec = make_uint4(0, 0, 0, 0), srec = rec;
-        if (valid && T.lxc4) {
-            rec = lxc_resolve(T, da, lxs, lx);
-            if (EGR)
-                srec = lxc_resolve(T, sa, lss, ls);
-        }
-        const bool local = (rec.w & LXC_VALID) != 0;
-        const uint32_t src_lxc = (srec.w & LXC_VALID) ? (srec.w & 0xFFFF) : NONE;
-
-        int act = TC_ACT_OK, ver = 0;
-        uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
-        bool xdp_drop = false;
-        if (XDP && valid) {
-            bool deny = pfd != 0;
-            if (!deny && (T.pf_fix || T.pf_fix_zero))
-                deny = pf_resolve(T, sa, pfb, pf);
-            xdp_drop = deny || !local;
-            if (MODE == CFC_MODE_XDP || xdp_drop) {
-                act = xdp_drop ? XDP_DROP : XDP_PASS;
-                ver = xdp_drop ? CFC_DROP_PREFILTER : 0;
-            }
-        }
-
-        // ---- round 4: identity, then the three policy buckets together
-        bool need_pol = false, skip_proxy = false;
-        uint32_t pbase = 0, pmask = 0, egress_bit = 0, dport = 0, src = 0;
-        if (valid && MODE != CFC_MODE_XDP && !xdp_drop) {
-            const bool known = ct_new_dport(proto, pt, &dport);
-            if (!EGR) {
-                // handle_identity_from_host (bpf_netdev.c:128-153)
-                const uint32_t magic = mk & 0xF00u;
-                if (magic == 0xA00u || magic == 0xB00u) {
-                    ident = ((mk & 0xFF) << 16) | (mk >> 16);
-                    skip_proxy = magic == 0xA00u;
-                } else {
-                    ident = magic == 0xC00u ? HOST_ID : WORLD_ID;
-                }
-                // handle_ipv4 (:375-398): reserved identities take the ipcache's
-                if (ident < HEALTH_ID && e24 && e24 != CLUSTER_ID && e24 != HOST_ID)
-                    ident = e24;
-                if (local && !(rec.w & LXC_HOST)) {
-                    if (!(rec.w & LXC_HAS_POLICY)) {
-                        act = TC_ACT_SHOT;
-                        ver = DROP_MISSED_TAIL_CALL;
-                        met0 = mkey(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
-                    } else if (!known) {
-                        act = TC_ACT_SHOT;
-                        ver = DROP_CT_UNKNOWN_PROTO;
-                        met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
-                    } else {
-                        need_pol = true;
-                        pbase = rec.y;
-                        pmask = rec.z;
-                        src = ident;
-                    }
-                }
-            } else {
-                act = TC_ACT_SHOT;
-                if (src_lxc != E.lxc_id) {   // is_valid_lxc_src_ipv4 (lxc.h:55)
-                    ver = DROP_INVALID_SIP;
-                    met0 = mkey(DROP_INVALID_SIP, METRIC_EGRESS);
-                } else if (!known) {
-                    ver = DROP_CT_UNKNOWN_PROTO;
-                    met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
-                } else {
-                    // destination identity (bpf_lxc.c:516-532)
-                    ident = e24 ? e24
-                                : ((da & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE
-                                       ? CLUSTER_ID
-                                       : WORLD_ID);
-                    need_pol = true;
-                    pbase = E.pol_base;
-                    pmask = E.pol_mask;
-                    egress_bit = 1;
-                    src = ident;
-                }
-            }
-        }
-        PolicyProbe P;
-        if (need_pol)
-            policy_issue(T, pbase, pmask, src, dport, proto, egress_bit, P);
-
-        if (need_pol) {
-            int v = policy_resolve(T, pbase, pmask, frag && !EGR, P, &ctr0);
-            const int mdir = EGR ? METRIC_EGRESS : METRIC_INGRESS;
-            if (v < 0) {
-                act = TC_ACT_SHOT;
-                ver = DROP_POLICY;
-                met0 = mkey(DROP_POLICY, mdir);
-            } else if (!EGR) {
-                if (skip_proxy)
-                    v = 0;
-                if (v > 0) {           // redirect_to_proxy
-                    act = TC_ACT_REDIRECT;
-                    ver = v;
-                } else {               // TRACE_TO_LXC
-                    met0 = mkey(0, METRIC_INGRESS);
-                    act = (rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
-                    ver = 0;
-                }
-            } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
-                act = TC_ACT_REDIRECT;
-                ver = v;
-            } else {
-                met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
-                ver = 0;
-                if (!local) {
-                    act = TC_ACT_OK;
-                } else if (rec.w & LXC_HOST) {
-                    act = TC_ACT_REDIRECT;
-                } else if (!(rec.w & LXC_HAS_POLICY)) {
-                    act = TC_ACT_SHOT;
-                    ver = DROP_MISSED_TAIL_CALL;
-                    met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
-                } else {
-                    // local delivery: the destination's ipv4_policy with
-                    // src = SECLABEL of the sending endpoint
-                    int w = policy_access(T, rec.y, rec.z,
-                                          E.seclabel, dport, proto, 0, frag,
-                                          &ctr1);
-                    if (w < 0) {
-                        act = TC_ACT_SHOT;
-                        ver = DROP_POLICY;
-                        met1 = mkey(DROP_POLICY, METRIC_INGRESS);
-                    } else if (w > 0) {
-                        act = TC_ACT_REDIRECT;
-                        ver = w;
-                    } else {
-                        met1 = mkey(0, METRIC_INGRESS);
-                        act = (rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
-                    }
-                }
-            }
-        }
-
-        if (valid) {
-            st_nt(ver, out.verdict + i);
-            st_nt(ident, out.identity + i);
-            if (out.action)
-                out.action[i] = (uint8_t)act;
-            count_hit<LDS>(s_ctr, g_ctr, ctr0, len);
-            count_hit<LDS>(s_ctr, g_ctr, ctr1, len);
-        }
-        metrics_wave(s_met, nullptr, met0, len);
-        if (EGR)
-            metrics_wave(s_met, nullptr, met1, len);
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64; j += BLOCK) {
@@ -505,7 +566,7 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                  hipStream_t s)
 {
     size_t lds = 4ull * (METRIC_U64 + (LDS ? 2ull * T.n_ctr : 0));
-    auto kern = k_classify_v4<MODE, LDS>;
+    auto kern = k_classify_v4<MODE, LDS, CFC_UNROLL>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
