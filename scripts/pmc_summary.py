@@ -4,7 +4,12 @@ kernel, plus HBM traffic per launch corrected as MI355X_MICROARCH.md's HBM
 section prescribes (FETCH_SIZE reads 1/2 of wide coalesced streaming reads
 on gfx950; the random 4-64 B lookups are reported as measured).
 
-usage: python3 scripts/pmc_summary.py OUTDIR [kernel-substring]
+usage: python3 scripts/pmc_summary.py OUTDIR [kernel-substring] [--traffic HEADERS MODE STREAM_BYTES_PER_HDR]
+
+With --traffic, also writes profiles/pmc_traffic.json, which bench.py reports
+as roofline.traffic when its batch size and mode match: HBM-side bytes per
+launch = FETCH_SIZE (x1 for the random lookups, +1x the streamed SoA input
+bytes, which FETCH_SIZE counts at half on gfx950) + WRITE_SIZE.
 """
 import csv
 import glob
@@ -14,7 +19,7 @@ import sys
 from collections import defaultdict
 
 
-def main(out, kname="k_classify_v4"):
+def main(out, kname="k_classify_v4", traffic=None):
     res = {"kernels": {}, "counters": {}}
     ks = glob.glob(os.path.join(out, "kt", "*kernel_stats.csv"))
     if ks:
@@ -40,8 +45,27 @@ def main(out, kname="k_classify_v4"):
                 res[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
         res["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if traffic and "hbm_fetch_bytes_per_launch" in res:
+        n, mode, sb = int(traffic[0]), traffic[1], float(traffic[2])
+        fix = 0.5 * n * sb
+        res["hbm_bytes_per_launch"] = (res["hbm_fetch_bytes_per_launch"] + fix
+                                       + res["hbm_write_bytes_per_launch"])
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        with open(os.path.join(root, "profiles", "pmc_traffic.json"), "w") as f:
+            json.dump({"headers": n, "mode": mode, "source": out,
+                       "stream_read_bytes_per_header": sb,
+                       "fetch_size_bytes": res["hbm_fetch_bytes_per_launch"],
+                       "write_size_bytes": res["hbm_write_bytes_per_launch"],
+                       "hbm_bytes_per_launch": res["hbm_bytes_per_launch"]},
+                      f, indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    a = sys.argv[1:]
+    tr = None
+    if "--traffic" in a:
+        i = a.index("--traffic")
+        tr = a[i + 1:i + 4]
+        a = a[:i] + a[i + 4:]
+    main(*a, traffic=tr)
