@@ -1,0 +1,91 @@
+"""Multi-rank path on CPU (gloo, world_size 2): the header stream is sharded
+contiguously, every rank classifies its shard against replicated tables, and
+the u64 counter blocks are SUM-all-reduced (cilium_amd/distributed.py,
+SURVEY.md §8e).  The oracle stands in for each rank's engine here; the GPU
+side of the same exchange (cfc_counters_export/import) runs in
+tests/test_gpu_parity.py and bench.py --gpus N."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from cilium_amd import synth as S
+from cilium_amd.distributed import allreduce_block, shard_range
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_range_partitions_the_stream():
+    for n in (0, 1, 7, 1000, 1 << 20):
+        for world in (1, 2, 3, 8):
+            got = [shard_range(n, r, world) for r in range(world)]
+            assert got[0][0] == 0 and got[-1][1] == n
+            for (a, b), (c, d) in zip(got, got[1:]):
+                assert b == c and a <= b
+            sizes = [b - a for a, b in got]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = S.config_c2(2, n_prefixes=5000, n_policy=1024, n_endpoints=2)
+        h = S.headers_c2(t, 40_000, seed=11)
+        a, b = shard_range(len(h), rank, world)
+        o = O.Oracle(t)
+        _, ver, ide = o.classify(h.slice(a, b), 0, 0)
+        lxc = sorted(t.policy)[0]
+        pc = o.policy_counters(lxc)             # rows: ..., packets, bytes
+        blk = np.concatenate([pc[:, 5], pc[:, 6]]).astype(np.uint64)
+        # u64 counters travel as int64 (two's complement == mod 2^64)
+        tb = torch.from_numpy(blk.view(np.int64).copy())
+        allreduce_block(tb)
+        # wrap-around stays exact: add 2^64-1 on rank 0, +1 on rank 1
+        w = torch.tensor([-1 if rank == 0 else 1], dtype=torch.int64)
+        allreduce_block(w)
+        q.put((rank, ver, ide, tb.numpy().view(np.uint64), int(w.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_shards_and_counter_allreduce():
+    import oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    # the concatenated shard verdicts are the whole stream's
+    t = S.config_c2(2, n_prefixes=5000, n_policy=1024, n_endpoints=2)
+    h = S.headers_c2(t, 40_000, seed=11)
+    o = O.Oracle(t)
+    _, ver, ide = o.classify(h, 0, 0)
+    np.testing.assert_array_equal(np.concatenate([r[1] for r in res]), ver)
+    np.testing.assert_array_equal(np.concatenate([r[2] for r in res]), ide)
+    # the all-reduced counter block equals the single-rank totals
+    pc = o.policy_counters(sorted(t.policy)[0])
+    want = np.concatenate([pc[:, 5], pc[:, 6]]).astype(np.uint64)
+    for r in res:
+        np.testing.assert_array_equal(r[3], want)
+        assert r[4] == 0
