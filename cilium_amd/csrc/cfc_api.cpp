@@ -54,7 +54,7 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 
 struct Epoch {
     uint64_t id = 0;
-    DevBuf tbl24, tbl8, ovf, pf24, pf8, pffix, lxc4, pol;
+    DevBuf tbl24, tbl8, ovf, pf24, pf8, pffix, lxc4, pol, pfbloom, polbloom;
     DevTables T{};
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
@@ -178,7 +178,9 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
         (rc = upload_vec(E->ovf, img.lbl_ovf, s)) || (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
         (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
-        (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)))
+        (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)) ||
+        (rc = upload_vec(E->pfbloom, img.pf_bloom, s)) ||
+        (rc = upload_vec(E->polbloom, img.pol_bloom, s)))
         return rc;
     DevTables &T = E->T;
     T.tbl24 = (const uint32_t *)E->tbl24.p;
@@ -191,7 +193,12 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     T.pf_fix_zero = img.pf_fix_zero;
     T.lxc4 = (const LxcSlot *)E->lxc4.p;
     T.lxc4_mask = img.lxc4_mask;
+    T.lxc4_lds = img.lxc4.size() <= LXC_LDS_MAX_SLOTS;
     T.pol = (const PolSlot *)E->pol.p;
+    T.pf_bloom = (const uint32_t *)E->pfbloom.p;
+    T.pf_bloom_words = (uint32_t)img.pf_bloom.size();
+    T.pol_bloom = (const uint32_t *)E->polbloom.p;
+    T.pol_bloom_words = (uint32_t)img.pol_bloom.size();
     T.n_ctr = (uint32_t)img.ctr_owner.size();
     E->pol_loc = img.pol_loc;
     E->ctr_owner = img.ctr_owner;
@@ -465,7 +472,7 @@ int cfc_classify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
     }
-    size_t need = classify_workspace_bytes(in->n, E.T.n_ctr, c->num_cus);
+    size_t need = classify_workspace_bytes(in->n, E.T.n_ctr, mode);
     if (need > c->ws_bytes) {
         if (c->ws) {
             (void)hipDeviceSynchronize();

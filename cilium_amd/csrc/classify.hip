@@ -1,30 +1,38 @@
 // Batched verdict kernels for gfx950 (MI355X).
 //
-// Shape.  A 1024-thread workgroup owns a contiguous slice of <= 65536 headers
-// of the SoA batch; each loop iteration reads 4 KiB of every input array
-// coalesced (non-temporal: the 1-GiB stream must not evict the lookup tables
-// from the 256-MiB Infinity Cache) and writes the outputs the same way.
+// Two kernels per batch:
+//   k_classify_v4  every lookup of the verdict path; writes verdict,
+//                  identity, action and, per header, the index of the
+//                  policy entry whose counters the reference would bump
+//                  (policy.h:68-69,80-81,92-93).
+//   k_count        the policy-entry packets/bytes: an exact u32 histogram
+//                  of those indices in LDS per <= 64512 headers, written as
+//                  a partial slab and summed per entry by k_reduce_partials.
 //
-// Latency.  The lookups are dependent random accesses — DIR-24-8 tbl24/tbl8
-// (Infinity Cache), the endpoint / prefilter / policy buckets (L2).  The
-// kernel is bound by how many of them are in flight, so each header's chain
-// is cut to four memory round trips by issuing every lookup as soon as its
-// inputs exist:
+// Why two.  The classify kernel is bound by random accesses that miss the
+// CU: tbl24/tbl8 in the Infinity Cache (~57 G lines/s chip-wide measured,
+// profiles/ubench), endpoint / prefilter / policy buckets in L2 (~267 G/s).
+// Moving the counter histogram out frees its LDS for structures that turn
+// those accesses into LDS reads:
+//   * the endpoint table (cilium_lxc) itself when it is small;
+//   * a blocked Bloom filter over the prefilter's /32 deny set: an address
+//     is probed in L2 only when the filter says "maybe";
+//   * a blocked Bloom filter over every policy key: of __policy_can_access's
+//     three keys (L4, L3, wildcard port) only those that may exist are
+//     probed, in the reference's order — usually none (DROP_POLICY) or one.
+// A filter never answers "absent" for a present key, so verdicts stay
+// exact; a false positive costs one probe that misses.
+//
+// Shape.  One 1024-thread workgroup per CU owns a contiguous slice of the
+// SoA batch; every loop iteration streams 4 KiB of each input array
+// (non-temporal: the 1-GiB stream must not evict tbl24 from the 256-MiB
+// Infinity Cache).  U headers per thread go through four rounds side by
+// side so U independent lookup chains are in flight per lane:
 //   1. inputs
-//   2. tbl24[src|dst], endpoint bucket[dst], prefilter bucket[src]  (together)
-//   3. tbl8 (if the /24 is split), endpoint record
-//   4. the three policy buckets of __policy_can_access (L4, L3, wildcard-port)
-//      loaded speculatively together, resolved in the reference's order.
-// Overflowing buckets (never at the load factors flatten.cpp builds) fall
-// back to a probing loop.  There is no contraction here, hence no MFMA.
-//
-// Counters.  The reference bumps policy_entry packets/bytes
-// (policy.h:68-69,80-81,92-93) and cilium_metrics (metrics.h:43-61) per
-// packet.  Here they are exact u32 sums in LDS (a workgroup sees at most
-// 65536 headers, so neither packets nor bytes can wrap), written once per
-// workgroup as a partial slab and summed per entry by k_reduce_partials.
-// Metrics keys are few and hot (most packets of a batch share one drop
-// reason), so they are aggregated across the wave before the LDS atomic.
+//   2. tbl24[src|dst]; endpoint slot (LDS); prefilter bucket if "maybe"
+//   3. tbl8 (split /24s); identity; the first policy key that may exist
+//   4. resolve the policy probe (further keys only after a false positive)
+// There is no contraction here, hence no MFMA.
 //
 // Reference semantics restated here (file:line in /root/reference):
 //   ingress   bpf_netdev.c:128-153 (FROM_HOST identity from skb->mark),
@@ -34,6 +42,7 @@
 //   policy    bpf/lib/policy.h:46-146
 //   ct ports  bpf/lib/conntrack.h:467-590 (tuple->dport of a CT_NEW lookup)
 //   xdp       bpf_xdp.c:88-121
+//   metrics   bpf/lib/metrics.h:43-61
 #include "classify.hpp"
 
 namespace cfc {
@@ -48,7 +57,8 @@ constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
 constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-constexpr uint64_t MAX_PER_BLOCK = 65536;   // keeps u32 LDS sums exact
+// k_count: u32 LDS sums stay exact (65535 headers x 65535 bytes < 2^32)
+constexpr uint64_t COUNT_PER_BLOCK = 63 * BLOCK;
 #ifndef CFC_UNROLL
 #define CFC_UNROLL 2   // headers in flight per thread
 #endif
@@ -69,11 +79,37 @@ __device__ __forceinline__ uint4 ld16(const void *p)
     return *reinterpret_cast<const uint4 *>(p);
 }
 
-// ---- endpoint lookup: 16-byte slots, linear probing (layout.h)
-// resolve from the first loaded slot; returns the slot (info VALID) or a
-// zero slot for a miss
-__device__ __forceinline__ uint4 lxc_resolve(const DevTables &T, uint32_t addr,
-                                             uint32_t s, uint4 v)
+// Workgroup-shared state: LDS copies of the small tables.  Accessed through
+// the extern __shared__ symbol with dword offsets (not through pointers kept
+// in a struct, which would lose the LDS address space and turn every read
+// into a flat load).
+extern __shared__ uint4 cfc_smem[];
+
+struct Lds {
+    bool lxc, pfb, polb;          // which tables are in LDS
+    uint32_t lxc_off;             // uint4 index of the endpoint slots
+    uint32_t pfb_off, polb_off;   // dword index of the Bloom filters
+    uint32_t pfb_mask, polb_mask;
+};
+
+__device__ __forceinline__ unsigned long long *lds_met()
+{
+    return reinterpret_cast<unsigned long long *>(cfc_smem);
+}
+__device__ __forceinline__ uint32_t lds_word(uint32_t off)
+{
+    return reinterpret_cast<const uint32_t *>(cfc_smem)[off];
+}
+
+// ---- endpoint lookup: 16-byte slots, linear probing (layout.h).
+// Returns the slot (info VALID) or a zero slot for a miss.
+__device__ __forceinline__ uint4 lxc_slot(const DevTables &T, const Lds &S,
+                                          uint32_t s)
+{
+    return S.lxc ? cfc_smem[S.lxc_off + s] : ld16(T.lxc4 + s);
+}
+__device__ __forceinline__ uint4 lxc_resolve(const DevTables &T, const Lds &S,
+                                             uint32_t addr, uint32_t s, uint4 v)
 {
     for (;;) {
         if (!(v.w & LXC_VALID))
@@ -81,7 +117,7 @@ __device__ __forceinline__ uint4 lxc_resolve(const DevTables &T, uint32_t addr,
         if (v.x == addr)
             return v;
         s = (s + 1) & T.lxc4_mask;
-        v = ld16(T.lxc4 + s);
+        v = lxc_slot(T, S, s);
     }
 }
 
@@ -89,8 +125,6 @@ __device__ __forceinline__ uint4 lxc_resolve(const DevTables &T, uint32_t addr,
 __device__ __forceinline__ bool pf_resolve(const DevTables &T, uint32_t addr,
                                            uint32_t b, uint4 v)
 {
-    if (addr == 0)
-        return T.pf_fix_zero != 0;
     for (;;) {
         if (v.x == addr || v.y == addr || v.z == addr || v.w == addr)
             return true;
@@ -99,6 +133,13 @@ __device__ __forceinline__ bool pf_resolve(const DevTables &T, uint32_t addr,
         b = (b + 1) & T.pf_fix_mask;
         v = ld16(T.pf_fix + (size_t)b * PF_SLOTS);
     }
+}
+
+__device__ __forceinline__ bool bloom_maybe(uint32_t off, uint32_t mask,
+                                            uint64_t h)
+{
+    const uint32_t b = bloom_bits(h);
+    return (lds_word(off + ((uint32_t)h & mask)) & b) == b;
 }
 
 __device__ __forceinline__ uint64_t pkey(uint32_t id, uint32_t dport,
@@ -123,67 +164,113 @@ __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
     return proto == 1;
 }
 
-// __policy_can_access (policy.h:46-110), cb[CB_POLICY] == 0: the first
-// slot of each of the three keys (L4, L3, wildcard port) is loaded at once,
-// then the keys are resolved in the reference's order.  Returns the verdict
-// (<0 drop) and the matched counter (or NONE).
+// __policy_can_access (policy.h:46-110) with cb[CB_POLICY] == 0, split in
+// two halves so the first probe overlaps other headers' lookups:
+// policy_issue() filters the three keys and loads the first slot of the
+// first key that may exist; policy_resolve() walks the keys in the
+// reference's order (L4, L3, wildcard port; fragments: L3 only).
 struct PolicyProbe {
-    uint64_t k[3];
-    uint32_t s[3];
-    uint4 v[3];
+    uint32_t id, pp;    // identity; dport | proto << 16
+    uint32_t eg;        // egress << 24
+    uint32_t maybe;     // bit j: key j may exist (and applies)
+    uint32_t j, s;      // key and slot of the issued probe (j = 3: none)
+    uint4 v;
+    // key j by masking, not by selecting among stored keys: the compiler
+    // turns a 3-way select on a per-lane index into a scratch-memory table
+    __device__ __forceinline__ uint64_t key(uint32_t i) const
+    {
+        const uint32_t lo = id & (0u - (uint32_t)(i != 2));
+        const uint32_t hi = (pp & (0u - (uint32_t)(i != 1))) | eg;
+        return ((uint64_t)hi << 32) | lo;
+    }
 };
 
-__device__ __forceinline__ void policy_issue(const DevTables &T, uint32_t base,
-                                             uint32_t mask, uint32_t id,
-                                             uint32_t dport, uint32_t proto,
-                                             uint32_t egress, PolicyProbe &P)
+__device__ __forceinline__ void policy_probe_key(const DevTables &T,
+                                                 uint32_t base, uint32_t mask,
+                                                 PolicyProbe &P)
 {
-    P.k[0] = pkey(id, dport, proto, egress);   // L4
-    P.k[1] = pkey(id, 0, 0, egress);           // L3
-    P.k[2] = pkey(0, dport, proto, egress);    // wildcard port
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        P.s[j] = hash64(P.k[j], mask);
-        P.v[j] = ld16(T.pol + base + P.s[j]);
+    P.j = P.maybe ? __builtin_ctz(P.maybe) : 3;
+    if (P.j < 3) {
+        P.s = hash64(P.key(P.j), mask);
+        P.v = ld16(T.pol + base + P.s);
     }
 }
 
-__device__ __forceinline__ int policy_resolve(const DevTables &T, uint32_t base,
-                                              uint32_t mask, bool frag,
-                                              const PolicyProbe &P,
-                                              uint32_t *ctr)
+__device__ __forceinline__ void policy_issue(const DevTables &T, const Lds &S,
+                                             uint32_t base, uint32_t mask,
+                                             uint32_t id, uint32_t dport,
+                                             uint32_t proto, uint32_t egress,
+                                             bool frag, PolicyProbe &P)
 {
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        if (frag && j != 1)   // fragments: L3 key only (policy.h:61,85)
-            continue;
-        uint4 v = P.v[j];
-        uint32_t s = P.s[j];
+    // keys 0: L4 {id, dport, proto}, 1: L3 {id, 0, 0}, 2: wildcard port
+    // {0, dport, proto}, all with the direction bit
+    P.id = id;
+    P.pp = dport | (proto << 16);
+    P.eg = egress << 24;
+    P.maybe = frag ? 2u : 7u;                // policy.h:61,85
+    if (S.polb) {
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.key(0))))
+            P.maybe &= ~1u;
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.key(1))))
+            P.maybe &= ~2u;
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.key(2))))
+            P.maybe &= ~4u;
+    }
+    policy_probe_key(T, base, mask, P);
+}
+
+// Returns the verdict (<0 drop) and the matched counter (or NONE).  Works
+// on register copies of the probe state (writing through a pointer into the
+// per-header state array would keep that array out of registers).
+struct PolicyResult {
+    int verdict;
+    uint32_t ctr;
+};
+__device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
+                                                       uint32_t base,
+                                                       uint32_t mask,
+                                                       const PolicyProbe &P0)
+{
+    uint32_t maybe = P0.maybe, j = P0.j, s = P0.s;
+    uint4 v = P0.v;
+    uint32_t ctr = NONE;
+    int verdict = DROP_POLICY;   // (DROP_FRAG_NOSUPPORT also -> DROP_POLICY)
+    while (j < 3) {
+        const uint64_t want = P0.key(j);
+        bool hit = false;
         for (;;) {
             const uint64_t key = ((uint64_t)v.y << 32) | v.x;
-            if (key == P.k[j]) {
-                *ctr = v.w;
-                return j == 1 ? TC_ACT_OK : (int)(v.z & 0xFFFF);
+            if (key == want) {
+                hit = true;
+                break;
             }
             if (key == POL_EMPTY)
                 break;
             s = (s + 1) & mask;
             v = ld16(T.pol + base + s);
         }
+        if (hit) {
+            ctr = v.w;
+            verdict = j == 1 ? TC_ACT_OK : (int)(v.z & 0xFFFF);
+            break;
+        }
+        maybe &= ~(1u << j);   // a false positive of the filter
+        j = maybe ? __builtin_ctz(maybe) : 3;
+        if (j < 3) {
+            s = hash64(P0.key(j), mask);
+            v = ld16(T.pol + base + s);
+        }
     }
-    *ctr = NONE;
-    return DROP_POLICY;   // (DROP_FRAG_NOSUPPORT also becomes DROP_POLICY)
+    return PolicyResult{verdict, ctr};
 }
 
-__device__ __forceinline__ int policy_access(const DevTables &T, uint32_t base,
-                                             uint32_t mask, uint32_t id,
-                                             uint32_t dport, uint32_t proto,
-                                             uint32_t egress, bool frag,
-                                             uint32_t *ctr)
+__device__ __forceinline__ PolicyResult policy_access(
+    const DevTables &T, const Lds &S, uint32_t base, uint32_t mask, uint32_t id,
+    uint32_t dport, uint32_t proto, uint32_t egress, bool frag)
 {
     PolicyProbe P;
-    policy_issue(T, base, mask, id, dport, proto, egress, P);
-    return policy_resolve(T, base, mask, frag, P, ctr);
+    policy_issue(T, S, base, mask, id, dport, proto, egress, frag, P);
+    return policy_resolve(T, base, mask, P);
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
@@ -196,8 +283,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 
 // update_metrics for every lane of the wave at once: key = index into the
 // metrics block ([reason][dir][count,bytes]) or NONE.  Must be reached by
-// the whole wave (uniform control flow).
-__device__ __forceinline__ void metrics_wave(uint32_t *s_met, uint64_t *g_met,
+// the whole wave (uniform control flow).  Keys are few and hot, so lanes
+// with the same key are summed across the wave before one LDS atomic.
+__device__ __forceinline__ void metrics_wave(unsigned long long *s_met,
                                              uint32_t key, uint32_t len)
 {
     uint64_t pending = __ballot(key != NONE);
@@ -209,15 +297,8 @@ __device__ __forceinline__ void metrics_wave(uint32_t *s_met, uint64_t *g_met,
         const uint64_t m = __ballot(mine);
         const uint32_t sum = wave_sum(mine ? len : 0u);
         if (lane == leader) {
-            if (s_met) {
-                atomicAdd(&s_met[lk], (uint32_t)__popcll(m));
-                atomicAdd(&s_met[lk + 1], sum);
-            } else {
-                atomicAdd((unsigned long long *)&g_met[lk],
-                          (unsigned long long)__popcll(m));
-                atomicAdd((unsigned long long *)&g_met[lk + 1],
-                          (unsigned long long)sum);
-            }
+            atomicAdd(&s_met[lk], (unsigned long long)__popcll(m));
+            atomicAdd(&s_met[lk + 1], (unsigned long long)sum);
         }
         pending &= ~m;
     }
@@ -228,27 +309,13 @@ __device__ __forceinline__ uint32_t mkey(int reason, int dir)
     return ((uint32_t)(uint8_t)(-reason) * METRIC_DIRS + (uint32_t)dir) * 2;
 }
 
-template <bool LDS>
-__device__ __forceinline__ void count_hit(uint32_t *s_ctr, uint64_t *g_ctr,
-                                          uint32_t c, uint32_t len)
-{
-    if (c == NONE)
-        return;
-    if (LDS) {
-        atomicAdd(&s_ctr[2 * c], 1u);
-        atomicAdd(&s_ctr[2 * c + 1], len);
-    } else {
-        atomicAdd((unsigned long long *)&g_ctr[2 * c], 1ull);
-        atomicAdd((unsigned long long *)&g_ctr[2 * c + 1], (unsigned long long)len);
-    }
-}
-
 // Per-header state carried through the lookup rounds.
 struct Hdr {
     uint32_t sa, da, pt, mt, mk;
     bool valid;
     uint32_t e24, pfd, lh, hsh, lxs, lss, pfb;
     uint4 lx, ls, pf, rec;
+    bool pf_maybe;
     uint32_t src_lxc;
     int act, ver;
     uint32_t ident, met0, met1, ctr0, ctr1;
@@ -258,7 +325,6 @@ struct Hdr {
 };
 
 // round 1: the header (non-temporal streaming loads)
-template <int MODE>
 __device__ __forceinline__ void r1_load(const cfc_hdr_v4 &in, uint64_t i,
                                         uint64_t end, Hdr &h)
 {
@@ -276,7 +342,8 @@ __device__ __forceinline__ void r1_load(const cfc_hdr_v4 &in, uint64_t i,
 
 // round 2: every lookup that only needs the header
 template <int MODE>
-__device__ __forceinline__ void r2_issue(const DevTables &T, Hdr &h)
+__device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
+                                         Hdr &h)
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
@@ -286,6 +353,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, Hdr &h)
     h.lh = __builtin_bswap32(EGR ? h.da : h.sa);
     h.hsh = __builtin_bswap32(h.sa);
     h.lxs = h.lss = h.pfb = 0;
+    h.pf_maybe = false;
     if (!h.valid)
         return;
     if (LPM && T.tbl24)
@@ -294,22 +362,25 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, Hdr &h)
         h.pfd = T.pf_tbl24[h.hsh >> 8];
     if (T.lxc4) {
         h.lxs = hash32(h.da, T.lxc4_mask);
-        h.lx = ld16(T.lxc4 + h.lxs);
+        h.lx = lxc_slot(T, S, h.lxs);
         if (EGR) {
             h.lss = hash32(h.sa, T.lxc4_mask);
-            h.ls = ld16(T.lxc4 + h.lss);
+            h.ls = lxc_slot(T, S, h.lss);
         }
     }
-    if (XDP && T.pf_fix) {
-        h.pfb = hash32(h.sa, T.pf_fix_mask);
-        h.pf = ld16(T.pf_fix + (size_t)h.pfb * PF_SLOTS);
+    if (XDP && T.pf_fix && h.sa) {
+        h.pf_maybe = !S.pfb || bloom_maybe(S.pfb_off, S.pfb_mask, pf_bloom_hash(h.sa));
+        if (h.pf_maybe) {
+            h.pfb = hash32(h.sa, T.pf_fix_mask);
+            h.pf = ld16(T.pf_fix + (size_t)h.pfb * PF_SLOTS);
+        }
     }
 }
 
 // round 3: second-level LPM, endpoint resolution, prefilter verdict,
-// identity, and the first slot of the three policy keys
+// identity, and the first policy key that may exist
 template <int MODE>
-__device__ __forceinline__ void r3_identity(const DevTables &T,
+__device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
                                             const EgressArgs &E, Hdr &h)
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
@@ -324,9 +395,9 @@ __device__ __forceinline__ void r3_identity(const DevTables &T,
     h.rec = make_uint4(0, 0, 0, 0);
     uint4 srec = h.rec;
     if (h.valid && T.lxc4) {
-        h.rec = lxc_resolve(T, h.da, h.lxs, h.lx);
+        h.rec = lxc_resolve(T, S, h.da, h.lxs, h.lx);
         if (EGR)
-            srec = lxc_resolve(T, h.sa, h.lss, h.ls);
+            srec = lxc_resolve(T, S, h.sa, h.lss, h.ls);
     }
     const bool local = (h.rec.w & LXC_VALID) != 0;
     h.src_lxc = (srec.w & LXC_VALID) ? (srec.w & 0xFFFF) : NONE;
@@ -338,8 +409,9 @@ __device__ __forceinline__ void r3_identity(const DevTables &T,
     h.xdp_drop = false;
     if (XDP && h.valid) {
         bool deny = h.pfd != 0;
-        if (!deny && (T.pf_fix || T.pf_fix_zero))
-            deny = pf_resolve(T, h.sa, h.pfb, h.pf);
+        if (!deny)
+            deny = h.sa ? (h.pf_maybe && pf_resolve(T, h.sa, h.pfb, h.pf))
+                        : T.pf_fix_zero != 0;
         h.xdp_drop = deny || !local;
         if (MODE == CFC_MODE_XDP || h.xdp_drop) {
             h.act = h.xdp_drop ? XDP_DROP : XDP_PASS;
@@ -400,14 +472,22 @@ __device__ __forceinline__ void r3_identity(const DevTables &T,
             h.egress_bit = 1;
         }
     }
-    if (h.need_pol)
-        policy_issue(T, h.pbase, h.pmask, h.ident, h.dport, proto,
-                     h.egress_bit, h.P);
+    if (h.need_pol) {
+        // ingress fragments look up the L3 key only (policy.h:61,85); the
+        // egress path passes is_fragment = false (policy.h:153-154)
+        const bool frag = !EGR && (h.mt & CFC_HF_FRAG);
+        policy_issue(T, S, h.pbase, h.pmask, h.ident, h.dport, proto,
+                     h.egress_bit, frag, h.P);
+    }
 }
 
-// round 4: resolve the policy verdict, compose the program result
+// round 4: resolve the policy verdict, compose the program result.
+// The outcome is built in locals and written back once: conditional stores
+// to different fields of `h` get merged by the compiler into one store
+// through a selected field address, which pushes the whole per-header state
+// array into scratch memory.
 template <int MODE>
-__device__ __forceinline__ void r4_verdict(const DevTables &T,
+__device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                                            const EgressArgs &E, Hdr &h)
 {
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
@@ -415,72 +495,117 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T,
         return;
     const bool frag = (h.mt & CFC_HF_FRAG) != 0;
     const uint32_t proto = h.mt & 0xFF;
-    int v = policy_resolve(T, h.pbase, h.pmask, frag && !EGR, h.P, &h.ctr0);
+    const PolicyResult pr = policy_resolve(T, h.pbase, h.pmask, h.P);
     const int mdir = EGR ? METRIC_EGRESS : METRIC_INGRESS;
+    const bool ifx = (h.rec.w & LXC_IFINDEX) != 0;
+    int v = pr.verdict;
+    int act, ver;
+    uint32_t met0 = NONE, met1 = NONE, ctr1 = NONE;
     if (v < 0) {
-        h.act = TC_ACT_SHOT;
-        h.ver = DROP_POLICY;
-        h.met0 = mkey(DROP_POLICY, mdir);
+        act = TC_ACT_SHOT;
+        ver = DROP_POLICY;
+        met0 = mkey(DROP_POLICY, mdir);
     } else if (!EGR) {
         if (h.skip_proxy)
             v = 0;
-        if (v > 0) {           // redirect_to_proxy
-            h.act = TC_ACT_REDIRECT;
-            h.ver = v;
-        } else {               // TRACE_TO_LXC
-            h.met0 = mkey(0, METRIC_INGRESS);
-            h.act = (h.rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
-            h.ver = 0;
-        }
+        // redirect_to_proxy, or TRACE_TO_LXC + delivery
+        act = (v > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+        ver = v;
+        met0 = v > 0 ? NONE : mkey(0, METRIC_INGRESS);
     } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
-        h.act = TC_ACT_REDIRECT;
-        h.ver = v;
+        act = TC_ACT_REDIRECT;
+        ver = v;
     } else {
-        h.met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
-        h.ver = 0;
+        met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
+        ver = 0;
         if (!(h.rec.w & LXC_VALID)) {
-            h.act = TC_ACT_OK;
+            act = TC_ACT_OK;
         } else if (h.rec.w & LXC_HOST) {
-            h.act = TC_ACT_REDIRECT;
+            act = TC_ACT_REDIRECT;
         } else if (!(h.rec.w & LXC_HAS_POLICY)) {
-            h.act = TC_ACT_SHOT;
-            h.ver = DROP_MISSED_TAIL_CALL;
-            h.met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
+            act = TC_ACT_SHOT;
+            ver = DROP_MISSED_TAIL_CALL;
+            met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
         } else {
             // local delivery: the destination's ipv4_policy with
             // src = SECLABEL of the sending endpoint
-            int w = policy_access(T, h.rec.y, h.rec.z, E.seclabel, h.dport,
-                                  proto, 0, frag, &h.ctr1);
+            const PolicyResult pw = policy_access(T, S, h.rec.y, h.rec.z,
+                                                  E.seclabel, h.dport, proto,
+                                                  0, frag);
+            const int w = pw.verdict;
+            ctr1 = pw.ctr;
             if (w < 0) {
-                h.act = TC_ACT_SHOT;
-                h.ver = DROP_POLICY;
-                h.met1 = mkey(DROP_POLICY, METRIC_INGRESS);
-            } else if (w > 0) {
-                h.act = TC_ACT_REDIRECT;
-                h.ver = w;
+                act = TC_ACT_SHOT;
+                ver = DROP_POLICY;
+                met1 = mkey(DROP_POLICY, METRIC_INGRESS);
             } else {
-                h.met1 = mkey(0, METRIC_INGRESS);
-                h.act = (h.rec.w & LXC_IFINDEX) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                act = (w > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                ver = w;
+                met1 = w > 0 ? NONE : mkey(0, METRIC_INGRESS);
             }
         }
     }
+    h.act = act;
+    h.ver = ver;
+    h.met0 = met0;
+    h.met1 = met1;
+    h.ctr0 = pr.ctr;
+    h.ctr1 = ctr1;
 }
 
-// U headers per thread go through the rounds side by side, so each thread
-// keeps U independent lookup chains in flight (occupancy is capped at one
-// workgroup per CU by the LDS counter slab).
-template <int MODE, bool LDS, int U>
-__global__ __launch_bounds__(BLOCK) void k_classify_v4(
-    DevTables T, cfc_hdr_v4 in, cfc_out out, EgressArgs E, uint64_t *g_ctr,
-    uint64_t *g_met, uint32_t *partial, uint64_t per_block)
+// LDS image of one launch: the metrics block, then the tables copied in.
+struct LdsPlan {
+    uint32_t lxc_slots, pf_words, pol_words;
+    __host__ __device__ size_t bytes() const
+    {
+        return 8ull * METRIC_U64 + 16ull * lxc_slots + 4ull * pf_words +
+               4ull * pol_words;
+    }
+};
+
+__host__ LdsPlan lds_plan(const DevTables &T)
 {
-    extern __shared__ uint32_t smem[];
-    const uint32_t n_ctr2 = LDS ? 2 * T.n_ctr : 0;
-    for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64 + n_ctr2; j += BLOCK)
-        smem[j] = 0;
+    LdsPlan p;
+    p.lxc_slots = (T.lxc4 && T.lxc4_lds) ? T.lxc4_mask + 1 : 0;
+    p.pf_words = T.pf_bloom ? T.pf_bloom_words : 0;
+    p.pol_words = T.pol_bloom ? T.pol_bloom_words : 0;
+    return p;
+}
+
+template <class W>
+__device__ __forceinline__ void lds_copy(W *dst, const W *src, uint32_t n)
+{
+    for (uint32_t j = threadIdx.x; j < n; j += BLOCK)
+        dst[j] = src[j];
+}
+
+template <int MODE, int U>
+__global__ __launch_bounds__(BLOCK) void k_classify_v4(
+    DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
+    uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
+{
+    // LDS image (uint4 units): metrics | endpoint slots | pf Bloom | pol Bloom
+    unsigned long long *s_met = lds_met();
+    Lds S;
+    S.lxc_off = METRIC_U64 / 2;
+    const uint32_t pf4 = S.lxc_off + L.lxc_slots;      // uint4 index
+    const uint32_t pol4 = pf4 + L.pf_words / 4;
+    S.pfb_off = 4 * pf4;
+    S.polb_off = 4 * pol4;
+    S.lxc = L.lxc_slots != 0;
+    S.pfb = L.pf_words != 0;
+    S.polb = L.pol_words != 0;
+    S.pfb_mask = L.pf_words - 1;
+    S.polb_mask = L.pol_words - 1;
+    for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64; j += BLOCK)
+        s_met[j] = 0;
+    lds_copy(cfc_smem + S.lxc_off, reinterpret_cast<const uint4 *>(T.lxc4),
+             L.lxc_slots);
+    lds_copy(cfc_smem + pf4, reinterpret_cast<const uint4 *>(T.pf_bloom),
+             L.pf_words / 4);
+    lds_copy(cfc_smem + pol4, reinterpret_cast<const uint4 *>(T.pol_bloom),
+             L.pol_words / 4);
     __syncthreads();
-    uint32_t *s_met = smem;
-    uint32_t *s_ctr = smem + METRIC_U64;
 
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
     const uint64_t end = min(in.n, start + per_block);
@@ -490,16 +615,16 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
         Hdr h[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r1_load<MODE>(in, base + (uint64_t)u * BLOCK + threadIdx.x, end, h[u]);
+            r1_load(in, base + (uint64_t)u * BLOCK + threadIdx.x, end, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r2_issue<MODE>(T, h[u]);
+            r2_issue<MODE>(T, S, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r3_identity<MODE>(T, E, h[u]);
+            r3_identity<MODE>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r4_verdict<MODE>(T, E, h[u]);
+            r4_verdict<MODE>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
@@ -509,24 +634,64 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
                 st_nt(h[u].ident, out.identity + i);
                 if (out.action)
                     out.action[i] = (uint8_t)h[u].act;
-                count_hit<LDS>(s_ctr, g_ctr, h[u].ctr0, len);
-                count_hit<LDS>(s_ctr, g_ctr, h[u].ctr1, len);
+                if (MODE != CFC_MODE_XDP) {
+                    st_nt(h[u].ctr0, ctr_idx + i);
+                    if (MODE == CFC_MODE_EGRESS)
+                        st_nt(h[u].ctr1, ctr_idx + in.n + i);
+                }
             }
-            metrics_wave(s_met, nullptr, h[u].met0, len);
+            metrics_wave(s_met, h[u].met0, len);
             if (MODE == CFC_MODE_EGRESS)
-                metrics_wave(s_met, nullptr, h[u].met1, len);
+                metrics_wave(s_met, h[u].met1, len);
         }
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64; j += BLOCK) {
-        uint32_t v = smem[j];
+        unsigned long long v = s_met[j];
         if (v)
-            atomicAdd((unsigned long long *)&g_met[j], (unsigned long long)v);
+            atomicAdd((unsigned long long *)&g_met[j], v);
+    }
+}
+
+// Policy-entry counters from the per-header entry indices: an LDS
+// histogram per <= COUNT_PER_BLOCK headers (ctr index i < n_hdr pairs with
+// meta[i], i >= n_hdr — egress local delivery — with meta[i - n_hdr]).
+template <bool LDS>
+__global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
+                                                 const uint32_t *meta,
+                                                 uint64_t n, uint64_t n_hdr,
+                                                 uint32_t n_ctr,
+                                                 uint32_t *partial,
+                                                 uint64_t *g_ctr)
+{
+    uint32_t *s_ctr = reinterpret_cast<uint32_t *>(cfc_smem);
+    const uint32_t n2 = 2 * n_ctr;
+    if (LDS) {
+        for (uint32_t j = threadIdx.x; j < n2; j += BLOCK)
+            s_ctr[j] = 0;
+        __syncthreads();
+    }
+    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
+    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    for (uint64_t i = start + threadIdx.x; i < end; i += BLOCK) {
+        const uint32_t c = ld_nt(ctr_idx + i);
+        if (c == NONE)
+            continue;
+        const uint32_t len = meta[i < n_hdr ? i : i - n_hdr] >> 16;
+        if (LDS) {
+            atomicAdd(&s_ctr[2 * c], 1u);
+            atomicAdd(&s_ctr[2 * c + 1], len);
+        } else {
+            atomicAdd((unsigned long long *)&g_ctr[2 * c], 1ull);
+            atomicAdd((unsigned long long *)&g_ctr[2 * c + 1],
+                      (unsigned long long)len);
+        }
     }
     if (LDS) {
-        uint32_t *dst = partial + (size_t)blockIdx.x * n_ctr2;
-        for (uint32_t j = threadIdx.x; j < n_ctr2; j += BLOCK)
-            st_nt(smem[METRIC_U64 + j], dst + j);
+        __syncthreads();
+        uint32_t *dst = partial + (size_t)blockIdx.x * n2;
+        for (uint32_t j = threadIdx.x; j < n2; j += BLOCK)
+            st_nt(s_ctr[j], dst + j);
     }
 }
 
@@ -559,46 +724,27 @@ __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
         dst[i] += src[i];
 }
 
-template <int MODE, bool LDS>
+template <int MODE>
 void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
-                 const EgressArgs &E, uint64_t *g_ctr, uint64_t *g_met,
-                 uint32_t *ws, uint32_t grid, uint64_t per_block,
-                 hipStream_t s)
+                 const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
+                 uint32_t grid, uint64_t per_block, hipStream_t s)
 {
-    size_t lds = 4ull * (METRIC_U64 + (LDS ? 2ull * T.n_ctr : 0));
-    auto kern = k_classify_v4<MODE, LDS, CFC_UNROLL>;
+    const LdsPlan L = lds_plan(T);
+    auto kern = k_classify_v4<MODE, CFC_UNROLL>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)(4ull * (METRIC_U64 + 2ull * LDS_CTR_MAX)));
+                                  LDS_BYTES_MAX);
         attr_set = true;
     }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), lds, s, T, in, out, E,
-                       g_ctr, g_met, ws, per_block);
-    if (LDS && T.n_ctr) {
-        uint32_t n2 = 2 * T.n_ctr;
-        hipLaunchKernelGGL(k_reduce_partials,
-                           dim3((n2 + 255) / 256, (grid + REDUCE_ROWS - 1) / REDUCE_ROWS),
-                           dim3(256), 0, s, ws, grid, n2, g_ctr);
-    }
-}
-
-// Workgroups of <= MAX_PER_BLOCK headers; at least one per CU when the
-// batch allows it.
-void geometry(uint64_t n, int num_cus, uint32_t *grid, uint64_t *per_block)
-{
-    uint64_t pb = (n + (uint64_t)num_cus - 1) / (uint64_t)num_cus;
-    pb = (pb + BLOCK - 1) / BLOCK * BLOCK;
-    if (pb < BLOCK)
-        pb = BLOCK;
-    if (pb > MAX_PER_BLOCK)
-        pb = MAX_PER_BLOCK;
-    *per_block = pb;
-    *grid = (uint32_t)((n + pb - 1) / pb);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
+                       out, E, ctr_idx, g_met, per_block);
 }
 
 }  // namespace
+
+size_t classify_lds_bytes(const DevTables &T) { return lds_plan(T).bytes(); }
 
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
                    hipStream_t s)
@@ -610,14 +756,17 @@ int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int num_cus)
+size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode)
 {
-    if (n_ctr > LDS_CTR_MAX || n == 0)
+    if (n == 0 || mode == CFC_MODE_XDP)
         return 0;
-    uint32_t grid;
-    uint64_t pb;
-    geometry(n, num_cus, &grid, &pb);
-    return 4ull * 2 * n_ctr * grid;
+    const uint64_t m = mode == CFC_MODE_EGRESS ? 2 * n : n;
+    size_t bytes = 4ull * m;                        // entry index per header
+    if (n_ctr && n_ctr <= LDS_CTR_MAX) {
+        const uint64_t nblk = (m + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK;
+        bytes += 4ull * 2 * n_ctr * nblk;           // partial slabs
+    }
+    return bytes;
 }
 
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
@@ -627,23 +776,52 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 {
     if (in.n == 0)
         return 0;
-    bool lds = T.n_ctr <= LDS_CTR_MAX;
-    uint32_t grid;
-    uint64_t per_block;
-    geometry(in.n, num_cus, &grid, &per_block);
-#define CFC_LAUNCH(M)                                                         \
-    (lds ? launch_mode<M, true>(T, in, out, E, g_ctr, g_met, ws, grid,        \
-                                per_block, s)                                 \
-         : launch_mode<M, false>(T, in, out, E, g_ctr, g_met, ws, grid,       \
-                                 per_block, s))
+    if (classify_lds_bytes(T) > LDS_BYTES_MAX)
+        return -22;
+    // one workgroup per CU (the LDS image allows no more), a contiguous
+    // slice each, rounded to whole loop iterations
+    const uint64_t step = (uint64_t)BLOCK * CFC_UNROLL;
+    uint64_t per_block = (in.n + (uint64_t)num_cus - 1) / (uint64_t)num_cus;
+    per_block = (per_block + step - 1) / step * step;
+    const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
     switch (mode) {
-    case CFC_MODE_INGRESS: CFC_LAUNCH(CFC_MODE_INGRESS); break;
-    case CFC_MODE_EGRESS: CFC_LAUNCH(CFC_MODE_EGRESS); break;
-    case CFC_MODE_XDP: CFC_LAUNCH(CFC_MODE_XDP); break;
-    case CFC_MODE_FULL: CFC_LAUNCH(CFC_MODE_FULL); break;
+    case CFC_MODE_INGRESS:
+        launch_mode<CFC_MODE_INGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    case CFC_MODE_EGRESS:
+        launch_mode<CFC_MODE_EGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    case CFC_MODE_XDP:
+        launch_mode<CFC_MODE_XDP>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    case CFC_MODE_FULL:
+        launch_mode<CFC_MODE_FULL>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
     default: return -22;
     }
-#undef CFC_LAUNCH
+    if (mode != CFC_MODE_XDP && T.n_ctr) {
+        const uint64_t m = mode == CFC_MODE_EGRESS ? 2 * in.n : in.n;
+        const uint32_t nblk = (uint32_t)((m + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        if (T.n_ctr <= LDS_CTR_MAX) {
+            static bool attr_set = false;
+            if (!attr_set) {
+                (void)hipFuncSetAttribute((const void *)k_count<true>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          LDS_BYTES_MAX);
+                attr_set = true;
+            }
+            uint32_t *partial = ws + m;
+            const uint32_t n2 = 2 * T.n_ctr;
+            hipLaunchKernelGGL(k_count<true>, dim3(nblk), dim3(BLOCK), 4ull * n2,
+                               s, ws, in.meta, m, in.n, T.n_ctr, partial, g_ctr);
+            hipLaunchKernelGGL(k_reduce_partials,
+                               dim3((n2 + 255) / 256, (nblk + REDUCE_ROWS - 1) / REDUCE_ROWS),
+                               dim3(256), 0, s, partial, nblk, n2, g_ctr);
+        } else {
+            hipLaunchKernelGGL(k_count<false>, dim3(nblk), dim3(BLOCK), 0, s, ws,
+                               in.meta, m, in.n, T.n_ctr, nullptr, g_ctr);
+        }
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -5;
 }

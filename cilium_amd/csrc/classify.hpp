@@ -17,13 +17,18 @@ struct EgressArgs {
     uint32_t pol_mask;
 };
 
-// LDS-privatised policy counters are used when 2*n_ctr u32 fit next to the
-// metrics block in the 160 KiB LDS (one 1024-thread block per CU).
+// The counter kernel keeps policy counters in LDS when 2*n_ctr u32 fit in
+// the 160 KiB LDS (one 1024-thread block per CU); beyond, global atomics.
 constexpr uint32_t LDS_CTR_MAX = 18432;
 constexpr int BLOCK = 1024;
+constexpr int LDS_BYTES_MAX = 160 * 1024;
 
-// Bytes of workspace (u32 partial counters) a launch over n headers needs.
-size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int num_cus);
+// Bytes of workspace a launch over n headers needs: the matched policy-entry
+// index per header (two per header in EGRESS mode) + the counter kernel's
+// partial slabs.
+size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode);
+// LDS image of the classify kernel for these tables (must be <= 160 KiB).
+size_t classify_lds_bytes(const DevTables &T);
 
 // dst[i] += src[i] for n u64 (counter import)
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,

@@ -17,7 +17,8 @@ static uint32_t pow2_at_least(uint64_t x)
 uint64_t HostImage::device_bytes() const
 {
     return 4ull * (tbl24.size() + tbl8.size() + lbl_ovf.size() +
-                   pf_tbl24.size() + pf_tbl8.size() + pf_fix.size()) +
+                   pf_tbl24.size() + pf_tbl8.size() + pf_fix.size() +
+                   pf_bloom.size() + pol_bloom.size()) +
            sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size();
 }
 
@@ -52,6 +53,17 @@ void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
         uint32_t *grp = tbl8->data() + ((size_t)g << 8);
         std::fill(grp + lo, grp + lo + (1u << (32 - p.plen)), p.leaf);
     }
+}
+
+// Blocked Bloom filter with ~`per_word` keys per 32-bit word, capped.
+static void bloom_size(std::vector<uint32_t> *b, size_t keys, uint32_t max_words)
+{
+    uint32_t w = pow2_at_least(std::max<size_t>(64, keys));
+    b->assign(std::min(w, max_words), 0u);
+}
+static inline void bloom_add(std::vector<uint32_t> *b, uint64_t h)
+{
+    (*b)[h & (b->size() - 1)] |= bloom_bits(h);
 }
 
 static uint32_t leaf_for(uint32_t label, std::vector<uint32_t> *ovf)
@@ -161,6 +173,11 @@ void build_image(const std::vector<Map *> &maps, HostImage *img)
         }
         img->n_pf_fix = (uint32_t)addrs.size() + img->pf_fix_zero;
         if (!addrs.empty()) {
+            // ~1 key per 4 bits of filter at most: 25k deny addresses in
+            // 32 KiB give ~1.5% false positives
+            bloom_size(&img->pf_bloom, 2 * addrs.size(), PF_BLOOM_MAX_WORDS);
+            for (uint32_t a : addrs)
+                bloom_add(&img->pf_bloom, pf_bloom_hash(a));
             // load factor <= 25%: 4-address buckets, one per expected address
             uint32_t nb = pow2_at_least(addrs.size());
             img->pf_fix.assign((size_t)nb * PF_SLOTS, 0);
@@ -184,6 +201,11 @@ void build_image(const std::vector<Map *> &maps, HostImage *img)
 
     // ---- policy tables (deterministic: ascending lxc id, key order);
     //      linear probing over 16-byte slots at load factor <= 25%
+    size_t n_pol_keys = 0;
+    for (auto &pm : pols)
+        n_pol_keys += pm.second->kv.size();
+    if (n_pol_keys)
+        bloom_size(&img->pol_bloom, n_pol_keys, POL_BLOOM_MAX_WORDS);
     for (auto &pm : pols) {
         Map *m = pm.second;
         PolLoc loc;
@@ -210,6 +232,7 @@ void build_image(const std::vector<Map *> &maps, HostImage *img)
             while (tab[s].key != POL_EMPTY)
                 s = (s + 1) & loc.mask;
             tab[s].key = key;
+            bloom_add(&img->pol_bloom, pol_bloom_hash(loc.base, key));
             tab[s].proxy_port = proxy;
             tab[s].ctr = (uint32_t)img->ctr_owner.size();
             img->ctr_owner.emplace_back(m, kv.first);

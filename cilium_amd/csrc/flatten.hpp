@@ -27,8 +27,10 @@ struct HostImage {
     // endpoints
     std::vector<LxcSlot> lxc4;
     uint32_t lxc4_mask = 0, n_eps = 0;
+    std::vector<uint32_t> pf_bloom;                 // words (pow2) or empty
     // policy
     std::vector<PolSlot> pol;
+    std::vector<uint32_t> pol_bloom;
     std::unordered_map<int, PolLoc> pol_loc;       // lxc_id -> table
     std::vector<std::pair<Map *, std::string>> ctr_owner;  // ctr -> entry
     uint64_t device_bytes() const;

@@ -18,6 +18,8 @@
 //   pol       every endpoint's policy table: 16-B slots
 //             {key u64, proxy u16, pad, counter index u32}
 //   lbl_ovf   identities >= 2^30 (rare) referenced from LPM leaves
+//   pf_bloom  blocked Bloom filter over pf4_fix   } copied into LDS by
+//   pol_bloom blocked Bloom filter over all pol   } every workgroup
 // Counters (read-write): u64 packets/bytes per policy entry + metrics.
 #pragma once
 #include <stdint.h>
@@ -80,6 +82,38 @@ __host__ __device__ inline uint32_t hash32(uint32_t k, uint32_t mask)
     return (uint32_t)(x >> 32) & mask;
 }
 
+// ---- blocked Bloom filters (LDS-resident while classifying) ----------------
+// One 32-bit word per key, three bits set in it: a query is one ds_read_b32.
+// They only ever answer "absent" or "maybe"; a "maybe" is resolved by the
+// exact table, so a false positive costs one extra probe and never a wrong
+// verdict.
+__host__ __device__ inline uint64_t mix64(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return k;
+}
+__host__ __device__ inline uint32_t bloom_bits(uint64_t h)
+{
+    return (1u << ((h >> 32) & 31)) | (1u << ((h >> 40) & 31)) |
+           (1u << ((h >> 48) & 31));
+}
+// policy keys are filtered per endpoint table (its first slot)
+__host__ __device__ inline uint64_t pol_bloom_hash(uint32_t base, uint64_t key)
+{
+    return mix64(key ^ ((uint64_t)base * 0x9E3779B97F4A7C15ull));
+}
+__host__ __device__ inline uint64_t pf_bloom_hash(uint32_t addr)
+{
+    return mix64((uint64_t)addr | 0x5bd1e99500000000ull);
+}
+constexpr uint32_t POL_BLOOM_MAX_WORDS = 16384;   // 64 KiB
+constexpr uint32_t PF_BLOOM_MAX_WORDS = 8192;     // 32 KiB
+constexpr uint32_t LXC_LDS_MAX_SLOTS = 1024;      // 16 KiB of endpoint slots
+
 struct DevTables {
     const uint32_t *tbl24;         // null when no v4 ipcache prefixes
     const uint32_t *tbl8;
@@ -89,13 +123,19 @@ struct DevTables {
     const uint32_t *pf_fix;        // buckets of 4 u32, null when empty
     const LxcSlot *lxc4;           // null when no IPv4 endpoints
     const PolSlot *pol;
+    const uint32_t *pf_bloom;      // Bloom filter over pf_fix, or null
+    const uint32_t *pol_bloom;     // Bloom filter over every policy key
     uint32_t pf_fix_mask;          // buckets - 1
     uint32_t pf_fix_zero;          // 0.0.0.0/32 is in the deny set
     uint32_t lxc4_mask;            // slots - 1
     uint32_t n_ctr;                // policy entries (counter slots)
+    uint32_t pf_bloom_words;       // power of two, 0 = no filter
+    uint32_t pol_bloom_words;      // power of two, 0 = no filter
+    uint32_t lxc4_lds;             // 1: the endpoint table is copied to LDS
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]
+// (policy-entry counters live in their own block: [n_ctr][packets, bytes])
 constexpr int METRIC_REASONS = 256;
 constexpr int METRIC_DIRS = 4;
 constexpr int METRIC_U64 = METRIC_REASONS * METRIC_DIRS * 2;
