@@ -42,11 +42,14 @@ def main():
                     help="headers timed on the host-core oracle (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "hashed"],
+                    help="IPv4 ipcache device layout (cfc_set_option CFC_OPT_LPM4)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     from cilium_amd import synth as S
+    from cilium_amd import _lib as LL
     from cilium_amd.datapath import Datapath, HeaderBatchV4, Verdicts
     from cilium_amd.distributed import allreduce_counters, env_rank
     from cilium_amd.loader import load_tables
@@ -63,6 +66,8 @@ def main():
     t0 = time.time()
     tables = S.config_c2_bench(args.seed)
     dp = Datapath(local_rank)
+    dp.set_option(LL.OPT_LPM4, {"auto": LL.LPM4_AUTO, "dir24_8": LL.LPM4_DIR24_8,
+                                "hashed": LL.LPM4_HASHED}[args.lpm4])
     load_tables(dp, tables)
     st = dp.stats()
     log(f"[rank {rank}] tables loaded+committed in {time.time() - t0:.1f}s: {st}")
@@ -82,6 +87,10 @@ def main():
         dp.classify_v4(batch, mode, ep_lxc, out=out)
     torch.cuda.synchronize()
     dp.counters_clear()
+    # HIP events recorded by the library on the launch stream around the
+    # classify kernel and the counter kernels of every timed call
+    dp.set_option(LL.OPT_TIMING, 1)
+    dp.timing_collect()
 
     stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -100,7 +109,11 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - w0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    tm = dp.timing_collect()
+    assert tm["launches"] == args.steps, tm
+    kern_ms = tm["classify_ms"] / tm["launches"]    # k_classify_v4 alone
+    count_ms = tm["count_ms"] / tm["launches"]      # k_count + k_reduce_partials
     if world > 1:
         tw = torch.tensor([wall], device=dev, dtype=torch.float64)
         dist.all_reduce(tw, op=dist.ReduceOp.MAX)
@@ -109,8 +122,9 @@ def main():
         dp.counters_sync()
     total = n * world * args.steps
     mpps = total / wall / 1e6
-    log(f"[rank {rank}] {args.steps} steps in {wall * 1e3:.2f} ms, kernel avg "
-        f"{kern_ms:.3f} ms/launch, {mpps:.0f} Mpps")
+    log(f"[rank {rank}] {args.steps} steps in {wall * 1e3:.2f} ms; per call "
+        f"{call_ms:.3f} ms = classify {kern_ms:.3f} + counters {count_ms:.3f}; "
+        f"{mpps:.0f} Mpps")
 
     if rank != 0:
         dist.destroy_process_group()
@@ -141,7 +155,9 @@ def main():
     if os.path.exists(tf):
         try:
             pm = json.load(open(tf))
-            if pm.get("headers") == n and pm.get("mode") == args.mode:
+            layout = {1: "dir24_8", 2: "hashed"}.get(st["lpm4_layout"], "none")
+            if (pm.get("headers") == n and pm.get("mode") == args.mode
+                    and pm.get("lpm4_layout") == layout):
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -168,9 +184,11 @@ def main():
             "policy_entries": st["policy_entries"],
             "prefilter_v4_fix": st["prefilter_v4_fix"],
             "mode": args.mode,
+            "lpm4_layout": {1: "dir24_8", 2: "hashed"}.get(st["lpm4_layout"], "none"),
             "parallelism": f"header-stream shards x{world}, tables replicated",
         },
         "roofline": {
+            "kernel": "k_classify_v4",
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
@@ -180,6 +198,8 @@ def main():
             "bytes_per_header": round(b_hdr, 2),
             "mean_lookups_per_header": round(mean_l, 4),
             "kernel_ms_per_launch": round(kern_ms, 4),
+            "count_kernels_ms_per_launch": round(count_ms, 4),
+            "call_ms_per_launch": round(call_ms, 4),
         },
         "cpu_baseline": None if (world > 1 or args.no_cpu) else {
             "value": round(samp / cpu_s / 1e6, 3),

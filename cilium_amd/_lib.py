@@ -14,6 +14,8 @@ CFC_DEVICE_NONE = -1
 MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
 HF_FRAG, HF_TCP_CLOSE = 0x100, 0x200
 DROP_PREFILTER = -1
+OPT_LPM4, OPT_TIMING = 1, 2
+LPM4_AUTO, LPM4_DIR24_8, LPM4_HASHED = 0, 1, 2
 
 # every symbol include/cfc.h declares
 EXPORTS = (
@@ -23,6 +25,7 @@ EXPORTS = (
     "cfc_commit", "cfc_classify_v4", "cfc_counters_device",
     "cfc_counters_sync", "cfc_counters_clear", "cfc_counters_export",
     "cfc_counters_import", "cfc_get_stats", "cfc_strerror",
+    "cfc_set_option", "cfc_timing_collect",
 )
 
 
@@ -48,7 +51,14 @@ class Stats(ctypes.Structure):
                 ("policy_entries", ctypes.c_uint32),
                 ("endpoints", ctypes.c_uint32),
                 ("prefilter_v4_fix", ctypes.c_uint32),
-                ("prefilter_v4_dyn", ctypes.c_uint32)]
+                ("prefilter_v4_dyn", ctypes.c_uint32),
+                ("lpm4_layout", ctypes.c_uint32),
+                ("lpm4_probe_slots", ctypes.c_uint32)]
+
+
+class Timing(ctypes.Structure):
+    _fields_ = [("launches", ctypes.c_uint64), ("classify_ms", ctypes.c_double),
+                ("count_ms", ctypes.c_double)]
 
 
 _lib = None
@@ -83,6 +93,8 @@ def lib():
     L.cfc_counters_export.argtypes = [vp, vp, u64, vp]
     L.cfc_counters_import.argtypes = [vp, vp, u64, vp]
     L.cfc_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.cfc_set_option.argtypes = [vp, i32, ctypes.c_int64]
+    L.cfc_timing_collect.argtypes = [vp, ctypes.POINTER(Timing)]
     L.cfc_strerror.argtypes = [i32]
     L.cfc_strerror.restype = ctypes.c_char_p
     _lib = L

@@ -54,7 +54,8 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 
 struct Epoch {
     uint64_t id = 0;
-    DevBuf tbl24, tbl8, ovf, pf24, pf8, pffix, lxc4, pol, pfbloom, polbloom;
+    DevBuf tbl24, tbl8, ovf, dir16, lh4, pf24, pf8, pffix, lxc4, pol, pfbloom,
+        polbloom;
     DevTables T{};
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
@@ -72,6 +73,7 @@ struct cfc_ctx {
     int next_fd = 3;
     std::vector<uint32_t> seclabel = std::vector<uint32_t>(65536, 0);
     uint64_t seclabel_gen = 0;
+    BuildOpts opts;
 
     std::unique_ptr<Epoch> epoch;
     uint64_t epoch_seq = 0;
@@ -86,6 +88,11 @@ struct cfc_ctx {
     uint32_t *ws = nullptr;
     size_t ws_bytes = 0;
     Map *metrics = nullptr;
+
+    // CFC_OPT_TIMING: events of the launches since the last collect
+    bool timing = false;
+    std::vector<LaunchTiming> tpool;
+    size_t tused = 0;
 };
 
 namespace {
@@ -93,6 +100,7 @@ namespace {
 uint64_t tables_sig(cfc_ctx *c)
 {
     uint64_t s = 1469598103934665603ull ^ c->seclabel_gen;
+    s = (s ^ (uint64_t)c->opts.lpm4) * 1099511628211ull;
     for (auto &kv : c->maps) {
         if (kv.second->role == ROLE_NONE || kv.second->role == ROLE_METRICS)
             continue;
@@ -171,18 +179,23 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     for (auto &kv : c->maps)
         ms.push_back(kv.second.get());
     HostImage img;
-    build_image(ms, &img);
+    build_image(ms, c->opts, &img);
 
     auto E = std::make_unique<Epoch>();
     E->id = ++c->epoch_seq;
     if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
-        (rc = upload_vec(E->ovf, img.lbl_ovf, s)) || (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
+        (rc = upload_vec(E->ovf, img.lbl_ovf, s)) ||
+        (rc = upload_vec(E->dir16, img.dir16, s)) || (rc = upload_vec(E->lh4, img.lh4, s)) ||
+        (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
         (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
         (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)) ||
         (rc = upload_vec(E->pfbloom, img.pf_bloom, s)) ||
         (rc = upload_vec(E->polbloom, img.pol_bloom, s)))
         return rc;
     DevTables &T = E->T;
+    T.dir16 = (const uint64_t *)E->dir16.p;
+    T.lh4 = (const uint64_t *)E->lh4.p;
+    T.lh4_mask = img.lh4_mask;
     T.tbl24 = (const uint32_t *)E->tbl24.p;
     T.tbl8 = (const uint32_t *)E->tbl8.p;
     T.lbl_ovf = (const uint32_t *)E->ovf.p;
@@ -210,6 +223,8 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->st.endpoints = img.n_eps;
     E->st.prefilter_v4_fix = img.n_pf_fix;
     E->st.prefilter_v4_dyn = img.n_pf_dyn;
+    E->st.lpm4_layout = (uint32_t)img.lpm4_layout;
+    E->st.lpm4_probe_slots = (uint32_t)img.lh4.size();
 
     // counters for the new entry layout (old ones were folded above)
     size_t need = 2ull * T.n_ctr + METRIC_U64;
@@ -260,6 +275,30 @@ int before_counter_write(cfc_ctx *c, Map *m)
     if (m->role == ROLE_POLICY || m->role == ROLE_METRICS)
         return fold_counters(c, c->last_stream);
     return 0;
+}
+
+// the next set of timing events (grown on demand, reused after a collect)
+const LaunchTiming *next_timing(cfc_ctx *c)
+{
+    if (!c->timing)
+        return nullptr;
+    if (c->tused == c->tpool.size()) {
+        LaunchTiming t;
+        for (auto &e : t.ev)
+            if (hipEventCreate(&e) != hipSuccess)
+                return nullptr;
+        c->tpool.push_back(t);
+    }
+    return &c->tpool[c->tused++];
+}
+
+void free_timing(cfc_ctx *c)
+{
+    for (auto &t : c->tpool)
+        for (auto &e : t.ev)
+            (void)hipEventDestroy(e);
+    c->tpool.clear();
+    c->tused = 0;
 }
 
 }  // namespace
@@ -314,6 +353,7 @@ void cfc_close(cfc_ctx *c)
         (void)hipDeviceSynchronize();
     }
     c->epoch.reset();
+    free_timing(c);
     if (c->ctr)
         (void)hipFree(c->ctr);
     if (c->ws)
@@ -321,6 +361,52 @@ void cfc_close(cfc_ctx *c)
     if (c->last_done)
         (void)hipEventDestroy(c->last_done);
     delete c;
+}
+
+int cfc_set_option(cfc_ctx *c, int option, int64_t value)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    switch (option) {
+    case CFC_OPT_LPM4:
+        if (value < CFC_LPM4_AUTO || value > CFC_LPM4_HASHED)
+            return -EINVAL;
+        c->opts.lpm4 = (int)value;   // the next commit rebuilds (tables_sig)
+        return 0;
+    case CFC_OPT_TIMING:
+        if (value != 0 && value != 1)
+            return -EINVAL;
+        if (c->device == CFC_DEVICE_NONE)
+            return -ENODEV;
+        c->timing = value != 0;
+        return 0;
+    default:
+        return -EINVAL;
+    }
+}
+
+int cfc_timing_collect(cfc_ctx *c, cfc_timing *out)
+{
+    if (!c || !out)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    memset(out, 0, sizeof(*out));
+    for (size_t i = 0; i < c->tused; i++) {
+        const LaunchTiming &t = c->tpool[i];
+        float a = 0, b = 0;
+        if (hipEventSynchronize(t.ev[2]) != hipSuccess ||
+            hipEventElapsedTime(&a, t.ev[0], t.ev[1]) != hipSuccess ||
+            hipEventElapsedTime(&b, t.ev[1], t.ev[2]) != hipSuccess)
+            return -EIO;
+        out->launches++;
+        out->classify_ms += a;
+        out->count_ms += b;
+    }
+    c->tused = 0;
+    return 0;
 }
 
 int cfc_map_open(cfc_ctx *c, const char *path, uint32_t type, uint32_t ks,
@@ -488,7 +574,8 @@ int cfc_classify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
     if (c->ctr_pending && c->last_stream != s)
         (void)hipStreamWaitEvent(s, c->last_done, 0);
     rc = launch_classify_v4(E.T, *in, *out, mode, ea, c->ctr,
-                            c->ctr + 2ull * E.T.n_ctr, c->ws, c->num_cus, s);
+                            c->ctr + 2ull * E.T.n_ctr, c->ws, c->num_cus, s,
+                            in->n ? next_timing(c) : nullptr);
     if (rc)
         return rc;
     (void)hipEventRecord(c->last_done, s);

@@ -5,15 +5,17 @@
 //                  identity, action and, per header, the index of the
 //                  policy entry whose counters the reference would bump
 //                  (policy.h:68-69,80-81,92-93).
-//   k_count        the policy-entry packets/bytes: an exact u32 histogram
-//                  of those indices in LDS per <= 64512 headers, written as
-//                  a partial slab and summed per entry by k_reduce_partials.
+//   k_count        the policy-entry packets/bytes: an exact histogram of
+//                  those indices in LDS per <= 64512 headers (one packed
+//                  u64 {packets << 32 | bytes} atomic per header), written
+//                  as a partial slab and summed per entry by
+//                  k_reduce_partials.
 //
 // Why two.  The classify kernel is bound by random accesses that miss the
-// CU: tbl24/tbl8 in the Infinity Cache (~57 G lines/s chip-wide measured,
-// profiles/ubench), endpoint / prefilter / policy buckets in L2 (~267 G/s).
-// Moving the counter histogram out frees its LDS for structures that turn
-// those accesses into LDS reads:
+// CU: the ipcache in L2 or the Infinity Cache (~267 / ~57 G lines/s
+// chip-wide measured, profiles/ubench), endpoint / prefilter / policy
+// buckets in L2.  Moving the counter histogram out frees its LDS for
+// structures that turn those accesses into LDS reads:
 //   * the endpoint table (cilium_lxc) itself when it is small;
 //   * a blocked Bloom filter over the prefilter's /32 deny set: an address
 //     is probed in L2 only when the filter says "maybe";
@@ -23,14 +25,21 @@
 // A filter never answers "absent" for a present key, so verdicts stay
 // exact; a false positive costs one probe that misses.
 //
+// IPv4 LPM.  Two layouts (layout.h), chosen per epoch by the flattener:
+//   hashed     dir16[a >> 16] (512 KiB) then the probe table (<= 4 MiB) for
+//              the lengths 17..32 present in that /16, longest first — both
+//              L2-resident;
+//   DIR-24-8   tbl24 (64 MiB, Infinity Cache) then tbl8 for split /24s —
+//              for ipcaches too large for the hashed table.
+//
 // Shape.  One 1024-thread workgroup per CU owns a contiguous slice of the
 // SoA batch; every loop iteration streams 4 KiB of each input array
-// (non-temporal: the 1-GiB stream must not evict tbl24 from the 256-MiB
-// Infinity Cache).  U headers per thread go through four rounds side by
-// side so U independent lookup chains are in flight per lane:
+// (non-temporal: the 1-GiB stream must not evict the tables).  U headers per
+// thread go through four rounds side by side so U independent lookup chains
+// are in flight per lane:
 //   1. inputs
-//   2. tbl24[src|dst]; endpoint slot (LDS); prefilter bucket if "maybe"
-//   3. tbl8 (split /24s); identity; the first policy key that may exist
+//   2. dir16 | tbl24; endpoint slot (LDS); prefilter bucket if "maybe"
+//   3. the LPM probes | tbl8; identity; the first policy key that may exist
 //   4. resolve the policy probe (further keys only after a false positive)
 // There is no contraction here, hence no MFMA.
 //
@@ -57,7 +66,8 @@ constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
 constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
-// k_count: u32 LDS sums stay exact (65535 headers x 65535 bytes < 2^32)
+// k_count: the packed u32 byte sums stay exact (64512 headers x 65535
+// bytes < 2^32, so they never carry into the packet count)
 constexpr uint64_t COUNT_PER_BLOCK = 63 * BLOCK;
 #ifndef CFC_UNROLL
 #define CFC_UNROLL 2   // headers in flight per thread
@@ -99,6 +109,33 @@ __device__ __forceinline__ unsigned long long *lds_met()
 __device__ __forceinline__ uint32_t lds_word(uint32_t off)
 {
     return reinterpret_cast<const uint32_t *>(cfc_smem)[off];
+}
+
+// ---- hashed IPv4 LPM (layout.h): probe the /16's lengths longest first;
+// the first hit is the longest match, else the /16's own leaf.  Returns the
+// label (0 = no match).
+__device__ __forceinline__ uint32_t lh_lookup(const DevTables &T, uint32_t a,
+                                              uint64_t d16)
+{
+    uint32_t lens = (uint32_t)(d16 >> 32);
+    while (lens) {
+        const uint32_t b = 31 - __builtin_clz(lens);     // length 17 + b
+        const uint32_t key = a & (0xFFFFFFFFu << (15 - b));
+        uint32_t s = lh_hash(key, 17 + b, T.lh4_mask);
+        for (;;) {
+            const uint2 v = *reinterpret_cast<const uint2 *>(T.lh4 + s);
+            if (!(v.y & LH_VALID))
+                break;
+            if (v.x == key && ((v.y >> 27) & 15) == b) {
+                const uint32_t l = v.y & (LH_INDIRECT | LH_PAYLOAD);
+                return (l & LH_INDIRECT) ? T.lbl_ovf[l & LH_PAYLOAD] : l;
+            }
+            s = (s + 1) & T.lh4_mask;
+        }
+        lens &= ~(1u << b);
+    }
+    const uint32_t leaf = (uint32_t)d16;
+    return (leaf & LPM_INDIRECT) ? T.lbl_ovf[leaf & LPM_PAYLOAD] : leaf;
 }
 
 // ---- endpoint lookup: 16-byte slots, linear probing (layout.h).
@@ -313,6 +350,7 @@ __device__ __forceinline__ uint32_t mkey(int reason, int dir)
 struct Hdr {
     uint32_t sa, da, pt, mt, mk;
     bool valid;
+    uint64_t d16;
     uint32_t e24, pfd, lh, hsh, lxs, lss, pfb;
     uint4 lx, ls, pf, rec;
     bool pf_maybe;
@@ -348,6 +386,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     constexpr bool LPM = MODE != CFC_MODE_XDP;
+    h.d16 = 0;
     h.e24 = h.pfd = 0;
     h.lx = h.ls = h.pf = make_uint4(0, 0, 0, 0);
     h.lh = __builtin_bswap32(EGR ? h.da : h.sa);
@@ -356,8 +395,12 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.pf_maybe = false;
     if (!h.valid)
         return;
-    if (LPM && T.tbl24)
-        h.e24 = T.tbl24[h.lh >> 8];
+    if (LPM) {
+        if (T.dir16)
+            h.d16 = T.dir16[h.lh >> 16];
+        else if (T.tbl24)
+            h.e24 = T.tbl24[h.lh >> 8];
+    }
     if (XDP && T.pf_tbl24)
         h.pfd = T.pf_tbl24[h.hsh >> 8];
     if (T.lxc4) {
@@ -385,10 +428,15 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
-    if (h.e24 & LPM_GROUP)
-        h.e24 = T.tbl8[((h.e24 & ~LPM_GROUP) << 8) | (h.lh & 0xFF)];
-    if (h.e24 & LPM_INDIRECT)
-        h.e24 = T.lbl_ovf[h.e24 & LPM_PAYLOAD];
+    constexpr bool LPM = MODE != CFC_MODE_XDP;
+    if (LPM && T.dir16) {
+        h.e24 = lh_lookup(T, h.lh, h.d16);
+    } else {
+        if (h.e24 & LPM_GROUP)
+            h.e24 = T.tbl8[((h.e24 & ~LPM_GROUP) << 8) | (h.lh & 0xFF)];
+        if (h.e24 & LPM_INDIRECT)
+            h.e24 = T.lbl_ovf[h.e24 & LPM_PAYLOAD];
+    }
     if (h.pfd & LPM_GROUP)
         h.pfd = T.pf_tbl8[((h.pfd & ~LPM_GROUP) << 8) | (h.hsh & 0xFF)];
     // rec: {addr, pol_base, pol_mask, info}; info == 0 -> not local
@@ -656,18 +704,18 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
 // Policy-entry counters from the per-header entry indices: an LDS
 // histogram per <= COUNT_PER_BLOCK headers (ctr index i < n_hdr pairs with
 // meta[i], i >= n_hdr — egress local delivery — with meta[i - n_hdr]).
+// One u64 LDS atomic per header adds {1 << 32 | len}.
 template <bool LDS>
 __global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
                                                  const uint32_t *meta,
                                                  uint64_t n, uint64_t n_hdr,
                                                  uint32_t n_ctr,
-                                                 uint32_t *partial,
+                                                 uint64_t *partial,
                                                  uint64_t *g_ctr)
 {
-    uint32_t *s_ctr = reinterpret_cast<uint32_t *>(cfc_smem);
-    const uint32_t n2 = 2 * n_ctr;
+    unsigned long long *s_ctr = reinterpret_cast<unsigned long long *>(cfc_smem);
     if (LDS) {
-        for (uint32_t j = threadIdx.x; j < n2; j += BLOCK)
+        for (uint32_t j = threadIdx.x; j < n_ctr; j += BLOCK)
             s_ctr[j] = 0;
         __syncthreads();
     }
@@ -679,8 +727,7 @@ __global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
             continue;
         const uint32_t len = meta[i < n_hdr ? i : i - n_hdr] >> 16;
         if (LDS) {
-            atomicAdd(&s_ctr[2 * c], 1u);
-            atomicAdd(&s_ctr[2 * c + 1], len);
+            atomicAdd(&s_ctr[c], (1ull << 32) | len);
         } else {
             atomicAdd((unsigned long long *)&g_ctr[2 * c], 1ull);
             atomicAdd((unsigned long long *)&g_ctr[2 * c + 1],
@@ -689,30 +736,35 @@ __global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
     }
     if (LDS) {
         __syncthreads();
-        uint32_t *dst = partial + (size_t)blockIdx.x * n2;
-        for (uint32_t j = threadIdx.x; j < n2; j += BLOCK)
-            st_nt(s_ctr[j], dst + j);
+        uint64_t *dst = partial + (size_t)blockIdx.x * n_ctr;
+        for (uint32_t j = threadIdx.x; j < n_ctr; j += BLOCK)
+            st_nt((uint64_t)s_ctr[j], dst + j);
     }
 }
 
 // Sum the per-workgroup partial slabs per counter (column sums, coalesced).
-// blockIdx.x: 256 columns, blockIdx.y: REDUCE_ROWS partial rows.
+// blockIdx.x: 256 entries, blockIdx.y: REDUCE_ROWS partial rows.
 constexpr uint32_t REDUCE_ROWS = 32;
-__global__ __launch_bounds__(256) void k_reduce_partials(const uint32_t *partial,
+__global__ __launch_bounds__(256) void k_reduce_partials(const uint64_t *partial,
                                                          uint32_t nblk,
-                                                         uint32_t n2,
+                                                         uint32_t n_ctr,
                                                          uint64_t *g_ctr)
 {
     uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= n2)
+    if (j >= n_ctr)
         return;
     uint32_t b0 = blockIdx.y * REDUCE_ROWS;
     uint32_t b1 = min(nblk, b0 + REDUCE_ROWS);
-    uint64_t s = 0;
-    for (uint32_t b = b0; b < b1; b++)
-        s += ld_nt(partial + (size_t)b * n2 + j);
-    if (s)
-        atomicAdd((unsigned long long *)&g_ctr[j], (unsigned long long)s);
+    uint64_t pk = 0, by = 0;
+    for (uint32_t b = b0; b < b1; b++) {
+        const uint64_t v = ld_nt(partial + (size_t)b * n_ctr + j);
+        pk += v >> 32;
+        by += v & 0xFFFFFFFFull;
+    }
+    if (pk) {
+        atomicAdd((unsigned long long *)&g_ctr[2 * j], (unsigned long long)pk);
+        atomicAdd((unsigned long long *)&g_ctr[2 * j + 1], (unsigned long long)by);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
@@ -742,6 +794,9 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                        out, E, ctr_idx, g_met, per_block);
 }
 
+// u32 index of the partial slabs in the workspace (8-byte aligned)
+uint64_t partial_off(uint64_t m) { return (m + 1) & ~1ull; }
+
 }  // namespace
 
 size_t classify_lds_bytes(const DevTables &T) { return lds_plan(T).bytes(); }
@@ -761,10 +816,10 @@ size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode)
     if (n == 0 || mode == CFC_MODE_XDP)
         return 0;
     const uint64_t m = mode == CFC_MODE_EGRESS ? 2 * n : n;
-    size_t bytes = 4ull * m;                        // entry index per header
+    size_t bytes = 4ull * partial_off(m);            // entry index per header
     if (n_ctr && n_ctr <= LDS_CTR_MAX) {
         const uint64_t nblk = (m + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK;
-        bytes += 4ull * 2 * n_ctr * nblk;           // partial slabs
+        bytes += 8ull * n_ctr * nblk;                // partial slabs
     }
     return bytes;
 }
@@ -772,7 +827,7 @@ size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode)
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,
                        uint64_t *g_ctr, uint64_t *g_met, uint32_t *ws,
-                       int num_cus, hipStream_t s)
+                       int num_cus, hipStream_t s, const LaunchTiming *tm)
 {
     if (in.n == 0)
         return 0;
@@ -784,6 +839,8 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
     uint64_t per_block = (in.n + (uint64_t)num_cus - 1) / (uint64_t)num_cus;
     per_block = (per_block + step - 1) / step * step;
     const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
+    if (tm)
+        (void)hipEventRecord(tm->ev[0], s);
     switch (mode) {
     case CFC_MODE_INGRESS:
         launch_mode<CFC_MODE_INGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
@@ -799,6 +856,8 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
         break;
     default: return -22;
     }
+    if (tm)
+        (void)hipEventRecord(tm->ev[1], s);
     if (mode != CFC_MODE_XDP && T.n_ctr) {
         const uint64_t m = mode == CFC_MODE_EGRESS ? 2 * in.n : in.n;
         const uint32_t nblk = (uint32_t)((m + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
@@ -810,18 +869,19 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                                           LDS_BYTES_MAX);
                 attr_set = true;
             }
-            uint32_t *partial = ws + m;
-            const uint32_t n2 = 2 * T.n_ctr;
-            hipLaunchKernelGGL(k_count<true>, dim3(nblk), dim3(BLOCK), 4ull * n2,
+            uint64_t *partial = reinterpret_cast<uint64_t *>(ws + partial_off(m));
+            hipLaunchKernelGGL(k_count<true>, dim3(nblk), dim3(BLOCK), 8ull * T.n_ctr,
                                s, ws, in.meta, m, in.n, T.n_ctr, partial, g_ctr);
             hipLaunchKernelGGL(k_reduce_partials,
-                               dim3((n2 + 255) / 256, (nblk + REDUCE_ROWS - 1) / REDUCE_ROWS),
-                               dim3(256), 0, s, partial, nblk, n2, g_ctr);
+                               dim3((T.n_ctr + 255) / 256, (nblk + REDUCE_ROWS - 1) / REDUCE_ROWS),
+                               dim3(256), 0, s, partial, nblk, T.n_ctr, g_ctr);
         } else {
             hipLaunchKernelGGL(k_count<false>, dim3(nblk), dim3(BLOCK), 0, s, ws,
                                in.meta, m, in.n, T.n_ctr, nullptr, g_ctr);
         }
     }
+    if (tm)
+        (void)hipEventRecord(tm->ev[2], s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -5;
 }

@@ -17,11 +17,19 @@ struct EgressArgs {
     uint32_t pol_mask;
 };
 
-// The counter kernel keeps policy counters in LDS when 2*n_ctr u32 fit in
-// the 160 KiB LDS (one 1024-thread block per CU); beyond, global atomics.
+// The counter kernel keeps one packed u64 per policy entry in LDS when
+// n_ctr of them fit in the 160 KiB LDS (one 1024-thread block per CU);
+// beyond, global atomics.
 constexpr uint32_t LDS_CTR_MAX = 18432;
 constexpr int BLOCK = 1024;
 constexpr int LDS_BYTES_MAX = 160 * 1024;
+
+// Optional per-call timing (CFC_OPT_TIMING): events recorded on the launch
+// stream before the classify kernel, after it, and after the counter
+// kernels.
+struct LaunchTiming {
+    hipEvent_t ev[3];
+};
 
 // Bytes of workspace a launch over n headers needs: the matched policy-entry
 // index per header (two per header in EGRESS mode) + the counter kernel's
@@ -37,6 +45,7 @@ int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,
                        uint64_t *g_ctr, uint64_t *g_met, uint32_t *workspace,
-                       int num_cus, hipStream_t stream);
+                       int num_cus, hipStream_t stream,
+                       const LaunchTiming *timing = nullptr);
 
 }  // namespace cfc

@@ -19,6 +19,7 @@ uint64_t HostImage::device_bytes() const
     return 4ull * (tbl24.size() + tbl8.size() + lbl_ovf.size() +
                    pf_tbl24.size() + pf_tbl8.size() + pf_fix.size() +
                    pf_bloom.size() + pol_bloom.size()) +
+           8ull * (dir16.size() + lh4.size()) +
            sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size();
 }
 
@@ -52,6 +53,57 @@ void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
         uint32_t lo = p.addr & 0xFF & ~((1u << (32 - p.plen)) - 1);
         uint32_t *grp = tbl8->data() + ((size_t)g << 8);
         std::fill(grp + lo, grp + lo + (1u << (32 - p.plen)), p.leaf);
+    }
+}
+
+static size_t lh4_slots(size_t n_long)
+{
+    return pow2_at_least(std::max<uint64_t>(16, 2ull * n_long));
+}
+
+// Hashed layout (layout.h): prefixes <= /16 are expanded into dir16's low
+// words in ascending length order; every longer prefix sets its length bit
+// in its /16's high word and gets one slot of the probe table (load <= 50%).
+void build_lh4(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
+               std::vector<uint64_t> *dir16, std::vector<uint64_t> *lh4,
+               uint32_t *mask)
+{
+    std::stable_sort(pfx.begin(), pfx.end(),
+                     [](const Pfx4 &a, const Pfx4 &b) { return a.plen < b.plen; });
+    dir16->assign(1u << 16, 0);
+    uint64_t *d = dir16->data();
+    size_t n_long = 0;
+    for (const Pfx4 &p : pfx) {
+        if (p.plen <= 16) {
+            uint32_t start = p.plen ? (p.addr >> 16) & ~((1u << (16 - p.plen)) - 1) : 0;
+            for (uint32_t j = start; j < start + (1u << (16 - p.plen)); j++)
+                d[j] = (d[j] & 0xFFFFFFFF00000000ull) | p.leaf;
+        } else {
+            d[p.addr >> 16] |= (uint64_t)(1u << (p.plen - 17)) << 32;
+            n_long++;
+        }
+    }
+    const uint32_t ns = (uint32_t)lh4_slots(n_long);
+    lh4->assign(ns, 0);
+    *mask = ns - 1;
+    uint64_t *t = lh4->data();
+    for (const Pfx4 &p : pfx) {
+        if (p.plen <= 16)
+            continue;
+        uint32_t l26;
+        if (p.leaf & LPM_INDIRECT) {
+            l26 = LH_INDIRECT | (p.leaf & LPM_PAYLOAD);
+        } else if (p.leaf > LH_PAYLOAD) {
+            ovf->push_back(p.leaf);
+            l26 = LH_INDIRECT | (uint32_t)(ovf->size() - 1);
+        } else {
+            l26 = p.leaf;
+        }
+        uint32_t s = lh_hash(p.addr, p.plen, ns - 1);
+        while (t[s] >> 63)
+            s = (s + 1) & (ns - 1);
+        t[s] = ((uint64_t)(LH_VALID | (uint32_t)(p.plen - 17) << 27 | l26) << 32) |
+               p.addr;
     }
 }
 
@@ -117,7 +169,8 @@ static void ipcache_v4(const Map *m, std::vector<Pfx4> *out,
                         leaf_for(b.second.second, ovf)});
 }
 
-void build_image(const std::vector<Map *> &maps, HostImage *img)
+void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
+                 HostImage *img)
 {
     *img = HostImage();
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,
@@ -134,13 +187,30 @@ void build_image(const std::vector<Map *> &maps, HostImage *img)
         }
     }
 
-    // ---- ipcache v4
+    // ---- ipcache v4: the hashed layout while its probe table fits one
+    //      XCD's L2 (or when forced), DIR-24-8 otherwise
     if (ipc) {
         std::vector<Pfx4> pfx;
         ipcache_v4(ipc, &pfx, &img->lbl_ovf);
         img->n_prefix4 = (uint32_t)pfx.size();
-        if (!pfx.empty())
-            build_dir24_8(pfx, &img->tbl24, &img->tbl8);
+        if (!pfx.empty()) {
+            size_t n_long = 0;
+            for (const Pfx4 &p : pfx)
+                n_long += p.plen > 16;
+            // measured at C2 (profiles/bench_r01_v5*.json): the hashed
+            // layout's extra probes cost more than its L2 residency gains,
+            // so AUTO stays on DIR-24-8
+            const bool hashed = opt.lpm4 == LPM4_HASHED;
+            (void)n_long;
+            if (hashed) {
+                build_lh4(pfx, &img->lbl_ovf, &img->dir16, &img->lh4,
+                          &img->lh4_mask);
+                img->lpm4_layout = LPM4_HASHED;
+            } else {
+                build_dir24_8(pfx, &img->tbl24, &img->tbl8);
+                img->lpm4_layout = LPM4_DIR24_8;
+            }
+        }
     }
 
     // ---- prefilter
@@ -200,7 +270,9 @@ void build_image(const std::vector<Map *> &maps, HostImage *img)
     }
 
     // ---- policy tables (deterministic: ascending lxc id, key order);
-    //      linear probing over 16-byte slots at load factor <= 25%
+    //      linear probing over 16-byte slots at load factor <= 50% (the
+    //      Bloom filter screens out most lookups of absent keys, so probe
+    //      sequences mostly end in a hit)
     size_t n_pol_keys = 0;
     for (auto &pm : pols)
         n_pol_keys += pm.second->kv.size();
@@ -213,7 +285,7 @@ void build_image(const std::vector<Map *> &maps, HostImage *img)
         uint32_t n = 0;
         for (const auto &kv : m->kv)
             n += ((uint8_t)kv.first[7] & 0xFE) == 0;
-        uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 4ull * n));
+        uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 2ull * n));
         loc.base = (uint32_t)img->pol.size();
         loc.mask = ns - 1;
         PolSlot empty{};

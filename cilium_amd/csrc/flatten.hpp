@@ -15,19 +15,31 @@ struct PolLoc {
     uint32_t base = 0, mask = 0, present = 0;
 };
 
+// IPv4 ipcache layouts (cfc_set_option CFC_OPT_LPM4)
+enum Lpm4Layout { LPM4_AUTO = 0, LPM4_DIR24_8 = 1, LPM4_HASHED = 2 };
+// AUTO picks the hashed layout while its probe table stays <= 4 MiB
+constexpr size_t LH4_MAX_BYTES = 4u << 20;
+
+struct BuildOpts {
+    int lpm4 = LPM4_AUTO;
+};
+
 struct HostImage {
-    // IPv4 ipcache, DIR-24-8
+    // IPv4 ipcache: DIR-24-8 (tbl24/tbl8) or hashed (dir16/lh4)
     std::vector<uint32_t> tbl24, tbl8, lbl_ovf;
+    std::vector<uint64_t> dir16, lh4;
+    uint32_t lh4_mask = 0;
+    int lpm4_layout = 0;           // LPM4_DIR24_8 / LPM4_HASHED, 0 = empty
     uint32_t n_prefix4 = 0;
     // prefilter
     std::vector<uint32_t> pf_tbl24, pf_tbl8;
     uint32_t n_pf_dyn = 0;
     std::vector<uint32_t> pf_fix;
     uint32_t pf_fix_mask = 0, pf_fix_zero = 0, n_pf_fix = 0;
+    std::vector<uint32_t> pf_bloom;                 // words (pow2) or empty
     // endpoints
     std::vector<LxcSlot> lxc4;
     uint32_t lxc4_mask = 0, n_eps = 0;
-    std::vector<uint32_t> pf_bloom;                 // words (pow2) or empty
     // policy
     std::vector<PolSlot> pol;
     std::vector<uint32_t> pol_bloom;
@@ -37,9 +49,10 @@ struct HostImage {
 };
 
 // maps: every map of the context.
-void build_image(const std::vector<Map *> &maps, HostImage *img);
+void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
+                 HostImage *img);
 
-// exposed for host-side unit tests of the DIR-24-8 builder
+// exposed for host-side unit tests of the LPM builders
 struct Pfx4 {
     uint32_t addr;   // host byte order
     uint8_t plen;
@@ -47,5 +60,9 @@ struct Pfx4 {
 };
 void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
                    std::vector<uint32_t> *tbl8);
+// hashed layout; direct labels >= 2^26 get lbl_ovf entries
+void build_lh4(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
+               std::vector<uint64_t> *dir16, std::vector<uint64_t> *lh4,
+               uint32_t *mask);
 
 }  // namespace cfc

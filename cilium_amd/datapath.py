@@ -143,6 +143,19 @@ class Datapath:
             return ctypes.c_void_p()
         return _stream_handle(stream)
 
+    def set_option(self, option, value):
+        """cfc_set_option: L.OPT_LPM4 (ipcache layout, next commit) or
+        L.OPT_TIMING (per-call kernel events)."""
+        L.check(self.L.cfc_set_option(self.h, option, value), "set option")
+
+    def timing_collect(self):
+        """Kernel device time of the calls since the last collect (needs
+        OPT_TIMING): {launches, classify_ms, count_ms} (sums)."""
+        t = L.Timing()
+        L.check(self.L.cfc_timing_collect(self.h, ctypes.byref(t)), "timing")
+        return {"launches": t.launches, "classify_ms": t.classify_ms,
+                "count_ms": t.count_ms}
+
     def commit(self, stream=None):
         L.check(self.L.cfc_commit(self.h, self._stream(stream)),"commit")
 

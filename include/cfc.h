@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 1
+#define CFC_ABI_VERSION 2
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -101,6 +101,21 @@ int cfc_endpoint_config(cfc_ctx *ctx, uint16_t lxc_id, uint32_t seclabel);
 /* Flatten the host tables into device layouts and publish them as the new
  * epoch.  Enqueued on `stream` (hipStream_t, NULL = default stream). */
 int cfc_commit(cfc_ctx *ctx, void *stream);
+
+/* ----------------------------------------------------------------- options */
+/* CFC_OPT_LPM4: device layout of the IPv4 ipcache, applied at the next
+ * commit.  AUTO (default) uses the hashed layout — a /16 directory plus a
+ * probe table for /17-/32, both L2-resident — while the probe table fits in
+ * 4 MiB, and DIR-24-8 (64 MiB, Infinity-Cache resident) beyond.  Lookups
+ * give the same result in every layout.
+ * CFC_OPT_TIMING: 1 = record HIP events around the kernels of every
+ * cfc_classify_* call (read back with cfc_timing_collect). */
+#define CFC_OPT_LPM4 1
+#define CFC_LPM4_AUTO 0
+#define CFC_LPM4_DIR24_8 1
+#define CFC_LPM4_HASHED 2
+#define CFC_OPT_TIMING 2
+int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
 
 /* ---------------------------------------------------------------- datapath */
 /* Which reference program chain a batch runs through. */
@@ -181,9 +196,21 @@ typedef struct {
     uint32_t endpoints;
     uint32_t prefilter_v4_fix;
     uint32_t prefilter_v4_dyn;
+    uint32_t lpm4_layout;       /* CFC_LPM4_DIR24_8 / _HASHED, 0 = empty */
+    uint32_t lpm4_probe_slots;  /* hashed layout: probe-table slots */
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);
+
+/* Device time of the kernels of the cfc_classify_* calls made since the
+ * previous collect with CFC_OPT_TIMING on (waits for them to finish):
+ * classify_ms sums the lookup kernel, count_ms the counter kernels. */
+typedef struct {
+    uint64_t launches;
+    double classify_ms;
+    double count_ms;
+} cfc_timing;
+int cfc_timing_collect(cfc_ctx *ctx, cfc_timing *out);
 
 #ifdef __cplusplus
 }

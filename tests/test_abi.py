@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(_lib.EXPORTS) == fns
-    assert L.cfc_abi_version() == 1
+    assert L.cfc_abi_version() == 2
     assert L.cfc_num_possible_cpus() == 1
 
 
@@ -38,6 +38,18 @@ def test_no_gpu_means_no_datapath():
     with pytest.raises(OSError) as e:
         dp.commit()
     assert e.value.errno == errno.ENODEV
+
+
+def test_options_on_host_only_context():
+    """The ipcache layout is a table option (it applies at the next commit);
+    timing needs a device."""
+    dp = C.host_only()
+    for v in (_lib.LPM4_AUTO, _lib.LPM4_DIR24_8, _lib.LPM4_HASHED):
+        dp.set_option(_lib.OPT_LPM4, v)
+    assert errno_of(lambda: dp.set_option(_lib.OPT_LPM4, 3)) == errno.EINVAL
+    assert errno_of(lambda: dp.set_option(99, 0)) == errno.EINVAL
+    assert errno_of(lambda: dp.set_option(_lib.OPT_TIMING, 1)) == errno.ENODEV
+    assert errno_of(dp.timing_collect) == errno.ENODEV
 
 
 def errno_of(fn):

@@ -9,6 +9,7 @@ import pytest
 import golden_io as G
 import oracle as O
 from cilium_amd import synth as S
+from cilium_amd import _lib as L
 from cilium_amd import metricsmap
 from cilium_amd.datapath import Datapath, pack_v4
 from cilium_amd.loader import load_tables, policy_rows
@@ -23,9 +24,15 @@ def torch():
     return torch
 
 
-def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1):
+LAYOUTS = {"dir24_8": L.LPM4_DIR24_8, "hashed": L.LPM4_HASHED}
+
+
+def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     dp = Datapath(0)
+    dp.set_option(L.OPT_LPM4, lpm4)
     pms = load_tables(dp, t)
+    if lpm4 != L.LPM4_AUTO and len(t.ipcache):
+        assert dp.stats()["lpm4_layout"] == lpm4
     b = pack_v4(h)
     n = len(h)
     act = np.empty(n, np.int32)
@@ -50,11 +57,13 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1):
     return act, ver, ide, counters, metrics
 
 
+@pytest.mark.parametrize("layout", sorted(LAYOUTS))
 @pytest.mark.parametrize("name", G.names())
-def test_golden(torch, name):
+def test_golden(torch, name, layout):
     g = G.Golden(name)
     act, ver, ide, counters, metrics = run_gpu(torch, g.tables, g.headers,
-                                               g.mode, g.ep_lxc)
+                                               g.mode, g.ep_lxc,
+                                               lpm4=LAYOUTS[layout])
     bad = G.mismatches(g, act, ver, ide)
     assert len(bad) == 0, f"{len(bad)} differ; first {bad[:8]}"
     for lxc, exp in g.counters.items():
@@ -68,8 +77,9 @@ def test_golden(torch, name):
     np.testing.assert_array_equal(ide, oi)
 
 
-def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1):
-    act, ver, ide, counters, metrics = run_gpu(torch, t, h, mode, ep_lxc, chunks)
+def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
+    act, ver, ide, counters, metrics = run_gpu(torch, t, h, mode, ep_lxc, chunks,
+                                               lpm4)
     o = O.Oracle(t)
     oa, ov, oi = o.classify(h, mode, ep_lxc, nthreads=16)
     for name, a, b in (("action", act, oa), ("verdict", ver, ov),
@@ -90,6 +100,19 @@ def test_c2_full_tables_vs_oracle(torch, mode):
     h = S.headers_c2(t, 4_000_000, seed=21)
     act, ver = compare_with_oracle(torch, t, h, mode, chunks=3)
     assert len(np.unique(act)) >= 2
+
+
+def test_c2_layouts_and_auto_choice(torch):
+    """The layout AUTO picks at C2 scale, and the other one forced, give the
+    same bits."""
+    t = S.config_c2(2)
+    dp = Datapath(0)
+    load_tables(dp, t)
+    st = dp.stats()
+    dp.close()
+    assert st["lpm4_layout"] == L.LPM4_DIR24_8
+    h = S.headers_c2(t, 1_000_000, seed=23)
+    compare_with_oracle(torch, t, h, 0, lpm4=L.LPM4_HASHED)
 
 
 def _prefilter(t):
@@ -123,7 +146,8 @@ def test_many_endpoints_global_counter_path(torch):
     compare_with_oracle(torch, t, h, 0)
 
 
-def test_wide_labels_and_edge_tables(torch):
+@pytest.mark.parametrize("layout", sorted(LAYOUTS))
+def test_wide_labels_and_edge_tables(torch, layout):
     """identities >= 2^30 (indirect LPM leaves), /0 and /32 prefixes,
     labels HOST/CLUSTER/0 that the ingress override ignores."""
     rng = np.random.default_rng(11)
@@ -132,6 +156,7 @@ def test_wide_labels_and_edge_tables(torch):
     ipc["label"][100:120] = S.HOST_ID
     ipc["label"][120:140] = S.CLUSTER_ID
     ipc["label"][140:160] = 0
+    ipc["label"][160:180] = (1 << 26) + np.arange(20)   # > the lh4 leaf field
     ipc = np.concatenate([ipc, S._v4_entries(np.array([0], np.uint32), [0], [77])])
     t = S.Tables(ipc, S.config_c2(1, n_prefixes=10, n_policy=10).endpoints, {},
                  np.zeros(0, S.PREFILTER_DT), {S.EP_LXC_ID: 2})
@@ -139,7 +164,7 @@ def test_wide_labels_and_edge_tables(torch):
     t.policy = {S.EP_LXC_ID: S.gen_policy(rng, 3000, idents, proxy_frac=0.1)}
     h = S.gen_headers_v4(rng, 500_000, ipc, S.local_v4_addrs(t),
                          proxy_ident=idents[:50], frag=0.05, other_proto=0.02)
-    compare_with_oracle(torch, t, h, 0)
+    compare_with_oracle(torch, t, h, 0, lpm4=LAYOUTS[layout])
 
 
 def test_empty_tables(torch):
