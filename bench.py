@@ -42,7 +42,7 @@ def main():
                     help="headers timed on the host-core oracle (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=2)
-    ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "hashed"],
+    ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "trie"],
                     help="IPv4 ipcache device layout (cfc_set_option CFC_OPT_LPM4)")
     args = ap.parse_args()
 
@@ -67,7 +67,7 @@ def main():
     tables = S.config_c2_bench(args.seed)
     dp = Datapath(local_rank)
     dp.set_option(LL.OPT_LPM4, {"auto": LL.LPM4_AUTO, "dir24_8": LL.LPM4_DIR24_8,
-                                "hashed": LL.LPM4_HASHED}[args.lpm4])
+                                "trie": LL.LPM4_TRIE}[args.lpm4])
     load_tables(dp, tables)
     st = dp.stats()
     log(f"[rank {rank}] tables loaded+committed in {time.time() - t0:.1f}s: {st}")
@@ -155,7 +155,7 @@ def main():
     if os.path.exists(tf):
         try:
             pm = json.load(open(tf))
-            layout = {1: "dir24_8", 2: "hashed"}.get(st["lpm4_layout"], "none")
+            layout = {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none")
             if (pm.get("headers") == n and pm.get("mode") == args.mode
                     and pm.get("lpm4_layout") == layout):
                 traffic = pm.get("hbm_bytes_per_launch")
@@ -184,7 +184,7 @@ def main():
             "policy_entries": st["policy_entries"],
             "prefilter_v4_fix": st["prefilter_v4_fix"],
             "mode": args.mode,
-            "lpm4_layout": {1: "dir24_8", 2: "hashed"}.get(st["lpm4_layout"], "none"),
+            "lpm4_layout": {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none"),
             "parallelism": f"header-stream shards x{world}, tables replicated",
         },
         "roofline": {

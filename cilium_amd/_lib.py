@@ -15,7 +15,7 @@ MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
 HF_FRAG, HF_TCP_CLOSE = 0x100, 0x200
 DROP_PREFILTER = -1
 OPT_LPM4, OPT_TIMING = 1, 2
-LPM4_AUTO, LPM4_DIR24_8, LPM4_HASHED = 0, 1, 2
+LPM4_AUTO, LPM4_DIR24_8, LPM4_TRIE = 0, 1, 2
 
 # every symbol include/cfc.h declares
 EXPORTS = (
@@ -53,7 +53,7 @@ class Stats(ctypes.Structure):
                 ("prefilter_v4_fix", ctypes.c_uint32),
                 ("prefilter_v4_dyn", ctypes.c_uint32),
                 ("lpm4_layout", ctypes.c_uint32),
-                ("lpm4_probe_slots", ctypes.c_uint32)]
+                ("lpm4_kib", ctypes.c_uint32)]
 
 
 class Timing(ctypes.Structure):

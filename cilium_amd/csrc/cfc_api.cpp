@@ -54,7 +54,7 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 
 struct Epoch {
     uint64_t id = 0;
-    DevBuf tbl24, tbl8, ovf, dir16, lh4, pf24, pf8, pffix, lxc4, pol, pfbloom,
+    DevBuf tbl24, tbl8, ovf, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
         polbloom;
     DevTables T{};
     std::unordered_map<int, PolLoc> pol_loc;
@@ -185,7 +185,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->id = ++c->epoch_seq;
     if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
         (rc = upload_vec(E->ovf, img.lbl_ovf, s)) ||
-        (rc = upload_vec(E->dir16, img.dir16, s)) || (rc = upload_vec(E->lh4, img.lh4, s)) ||
+        (rc = upload_vec(E->l4c, img.l4c, s)) || (rc = upload_vec(E->l4l, img.l4l, s)) ||
         (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
         (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
         (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)) ||
@@ -193,9 +193,8 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
         (rc = upload_vec(E->polbloom, img.pol_bloom, s)))
         return rc;
     DevTables &T = E->T;
-    T.dir16 = (const uint64_t *)E->dir16.p;
-    T.lh4 = (const uint64_t *)E->lh4.p;
-    T.lh4_mask = img.lh4_mask;
+    T.l4c = (const uint32_t *)E->l4c.p;
+    T.l4l = (const uint64_t *)E->l4l.p;
     T.tbl24 = (const uint32_t *)E->tbl24.p;
     T.tbl8 = (const uint32_t *)E->tbl8.p;
     T.lbl_ovf = (const uint32_t *)E->ovf.p;
@@ -224,7 +223,9 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->st.prefilter_v4_fix = img.n_pf_fix;
     E->st.prefilter_v4_dyn = img.n_pf_dyn;
     E->st.lpm4_layout = (uint32_t)img.lpm4_layout;
-    E->st.lpm4_probe_slots = (uint32_t)img.lh4.size();
+    E->st.lpm4_kib = (uint32_t)((4ull * (img.l4c.size() + img.tbl24.size() +
+                                        img.tbl8.size()) +
+                                 8ull * img.l4l.size() + 1023) / 1024);
 
     // counters for the new entry layout (old ones were folded above)
     size_t need = 2ull * T.n_ctr + METRIC_U64;
@@ -370,7 +371,7 @@ int cfc_set_option(cfc_ctx *c, int option, int64_t value)
     std::lock_guard<std::recursive_mutex> g(c->mu);
     switch (option) {
     case CFC_OPT_LPM4:
-        if (value < CFC_LPM4_AUTO || value > CFC_LPM4_HASHED)
+        if (value < CFC_LPM4_AUTO || value > CFC_LPM4_TRIE)
             return -EINVAL;
         c->opts.lpm4 = (int)value;   // the next commit rebuilds (tables_sig)
         return 0;

@@ -26,11 +26,10 @@
 // exact; a false positive costs one probe that misses.
 //
 // IPv4 LPM.  Two layouts (layout.h), chosen per epoch by the flattener:
-//   hashed     dir16[a >> 16] (512 KiB) then the probe table (<= 4 MiB) for
-//              the lengths 17..32 present in that /16, longest first — both
-//              L2-resident;
-//   DIR-24-8   tbl24 (64 MiB, Infinity Cache) then tbl8 for split /24s —
-//              for ipcaches too large for the hashed table.
+//   compact    the /16 directory word, then (usually) one 16-byte load of
+//              that node's prefix list, longest first — about 1-2 MiB in
+//              all, L2-resident;
+//   DIR-24-8   tbl24 (64 MiB, Infinity Cache) then tbl8 for split /24s.
 //
 // Shape.  One 1024-thread workgroup per CU owns a contiguous slice of the
 // SoA batch; every loop iteration streams 4 KiB of each input array
@@ -38,8 +37,10 @@
 // thread go through four rounds side by side so U independent lookup chains
 // are in flight per lane:
 //   1. inputs
-//   2. dir16 | tbl24; endpoint slot (LDS); prefilter bucket if "maybe"
-//   3. the LPM probes | tbl8; identity; the first policy key that may exist
+//   2. directory word | tbl24; endpoint slot (LDS); prefilter bucket if
+//      "maybe"
+//   3. the node's prefix list | tbl8; identity; the first policy key that
+//      may exist
 //   4. resolve the policy probe (further keys only after a false positive)
 // There is no contraction here, hence no MFMA.
 //
@@ -111,31 +112,39 @@ __device__ __forceinline__ uint32_t lds_word(uint32_t off)
     return reinterpret_cast<const uint32_t *>(cfc_smem)[off];
 }
 
-// ---- hashed IPv4 LPM (layout.h): probe the /16's lengths longest first;
-// the first hit is the longest match, else the /16's own leaf.  Returns the
-// label (0 = no match).
-__device__ __forceinline__ uint32_t lh_lookup(const DevTables &T, uint32_t a,
-                                              uint64_t d16)
+// ---- compact IPv4 LPM (layout.h): walk from the /16 directory word `e`
+// through chunks to a leaf or a prefix list; the first list entry that
+// matches is the longest prefix.  Returns the label (0 = no match).
+__device__ __forceinline__ uint32_t l4_leaf(const DevTables &T, uint32_t e)
 {
-    uint32_t lens = (uint32_t)(d16 >> 32);
-    while (lens) {
-        const uint32_t b = 31 - __builtin_clz(lens);     // length 17 + b
-        const uint32_t key = a & (0xFFFFFFFFu << (15 - b));
-        uint32_t s = lh_hash(key, 17 + b, T.lh4_mask);
-        for (;;) {
-            const uint2 v = *reinterpret_cast<const uint2 *>(T.lh4 + s);
-            if (!(v.y & LH_VALID))
-                break;
-            if (v.x == key && ((v.y >> 27) & 15) == b) {
-                const uint32_t l = v.y & (LH_INDIRECT | LH_PAYLOAD);
-                return (l & LH_INDIRECT) ? T.lbl_ovf[l & LH_PAYLOAD] : l;
-            }
-            s = (s + 1) & T.lh4_mask;
+    return (e & LPM_INDIRECT) ? T.lbl_ovf[e & LPM_PAYLOAD] : e;
+}
+__device__ __forceinline__ uint32_t l4_list_leaf(const DevTables &T, uint32_t hi)
+{
+    const uint32_t l = hi & (LL_INDIRECT | LL_PAYLOAD);
+    return (l & LL_INDIRECT) ? T.lbl_ovf[l & LL_PAYLOAD] : l;
+}
+__device__ __forceinline__ uint32_t l4_lookup(const DevTables &T, uint32_t a,
+                                              uint32_t e)
+{
+    uint32_t shift = 16;   // address bits below the current node
+    while (e & L4_PTR) {
+        const uint32_t cnt = (e >> 24) & 127, off = e & L4_OFF;
+        if (cnt == 0) {
+            shift -= 8;
+            e = T.l4c[off + ((a >> shift) & 255)];
+            continue;
         }
-        lens &= ~(1u << b);
+        for (uint32_t i = 0; i < cnt; i += 2) {
+            const uint4 v = ld16(T.l4l + off + i);
+            if (l4_match(a, v.x, v.y))
+                return l4_list_leaf(T, v.y);
+            if (l4_match(a, v.z, v.w))
+                return l4_list_leaf(T, v.w);
+        }
+        return 0;   // not reached: a list ends with its node's own prefix
     }
-    const uint32_t leaf = (uint32_t)d16;
-    return (leaf & LPM_INDIRECT) ? T.lbl_ovf[leaf & LPM_PAYLOAD] : leaf;
+    return l4_leaf(T, e);
 }
 
 // ---- endpoint lookup: 16-byte slots, linear probing (layout.h).
@@ -350,7 +359,7 @@ __device__ __forceinline__ uint32_t mkey(int reason, int dir)
 struct Hdr {
     uint32_t sa, da, pt, mt, mk;
     bool valid;
-    uint64_t d16;
+    uint32_t l4e;
     uint32_t e24, pfd, lh, hsh, lxs, lss, pfb;
     uint4 lx, ls, pf, rec;
     bool pf_maybe;
@@ -386,7 +395,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     constexpr bool LPM = MODE != CFC_MODE_XDP;
-    h.d16 = 0;
+    h.l4e = 0;
     h.e24 = h.pfd = 0;
     h.lx = h.ls = h.pf = make_uint4(0, 0, 0, 0);
     h.lh = __builtin_bswap32(EGR ? h.da : h.sa);
@@ -396,8 +405,8 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     if (!h.valid)
         return;
     if (LPM) {
-        if (T.dir16)
-            h.d16 = T.dir16[h.lh >> 16];
+        if (T.l4c)
+            h.l4e = T.l4c[h.lh >> 16];
         else if (T.tbl24)
             h.e24 = T.tbl24[h.lh >> 8];
     }
@@ -429,8 +438,8 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     constexpr bool LPM = MODE != CFC_MODE_XDP;
-    if (LPM && T.dir16) {
-        h.e24 = lh_lookup(T, h.lh, h.d16);
+    if (LPM && T.l4c) {
+        h.e24 = l4_lookup(T, h.lh, h.l4e);
     } else {
         if (h.e24 & LPM_GROUP)
             h.e24 = T.tbl8[((h.e24 & ~LPM_GROUP) << 8) | (h.lh & 0xFF)];

@@ -19,7 +19,7 @@ uint64_t HostImage::device_bytes() const
     return 4ull * (tbl24.size() + tbl8.size() + lbl_ovf.size() +
                    pf_tbl24.size() + pf_tbl8.size() + pf_fix.size() +
                    pf_bloom.size() + pol_bloom.size()) +
-           8ull * (dir16.size() + lh4.size()) +
+           4ull * l4c.size() + 8ull * l4l.size() +
            sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size();
 }
 
@@ -56,55 +56,106 @@ void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
     }
 }
 
-static size_t lh4_slots(size_t n_long)
-{
-    return pow2_at_least(std::max<uint64_t>(16, 2ull * n_long));
-}
+namespace {
 
-// Hashed layout (layout.h): prefixes <= /16 are expanded into dir16's low
-// words in ascending length order; every longer prefix sets its length bit
-// in its /16's high word and gets one slot of the probe table (load <= 50%).
-void build_lh4(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
-               std::vector<uint64_t> *dir16, std::vector<uint64_t> *lh4,
-               uint32_t *mask)
+// Builder of the compact multibit layout (layout.h).
+struct L4Trie {
+    std::vector<uint32_t> *c, *ovf;
+    std::vector<uint64_t> *l;
+    bool ok = true;
+
+    // list-entry leaf: 26 payload bits, wider labels through lbl_ovf
+    uint32_t list_leaf(uint32_t leaf)
+    {
+        if (leaf & LPM_INDIRECT)
+            return LL_INDIRECT | (leaf & LPM_PAYLOAD);
+        if (leaf > LL_PAYLOAD) {
+            ovf->push_back(leaf);
+            return LL_INDIRECT | (uint32_t)(ovf->size() - 1);
+        }
+        return leaf;
+    }
+    uint64_t entry(uint32_t addr, int len, uint32_t leaf)
+    {
+        return ((uint64_t)(((uint32_t)len & 31) << 27 | list_leaf(leaf)) << 32) | addr;
+    }
+
+    // The node for the range `base`/`lvl` whose own covering leaf is `def`;
+    // `longp` holds the prefixes longer than lvl inside the range.
+    uint32_t node(std::vector<Pfx4> &longp, uint32_t base, int lvl, uint32_t def)
+    {
+        if (longp.empty())
+            return def;
+        if (longp.size() + 1 < L4_LIST_MAX) {
+            std::stable_sort(longp.begin(), longp.end(),
+                             [](const Pfx4 &a, const Pfx4 &b) { return a.plen > b.plen; });
+            const size_t off = l->size();   // always even
+            for (const Pfx4 &p : longp)
+                l->push_back(entry(p.addr, p.plen, p.leaf));
+            l->push_back(entry(base, lvl, def));
+            if (l->size() & 1)
+                l->push_back(l->back());
+            if (off > L4_OFF)
+                ok = false;
+            return L4_PTR | (uint32_t)(l->size() - off) << 24 | (uint32_t)(off & L4_OFF);
+        }
+        // split: a chunk for the next 8 bits
+        const int nl = lvl + 8;
+        const uint32_t sh = 32 - nl;
+        const size_t off = c->size();
+        c->resize(off + 256, 0);
+        uint32_t defs[256];
+        std::fill(defs, defs + 256, def);
+        std::vector<std::vector<Pfx4>> sub(256);
+        std::stable_sort(longp.begin(), longp.end(),
+                         [](const Pfx4 &a, const Pfx4 &b) { return a.plen < b.plen; });
+        for (const Pfx4 &p : longp) {
+            const uint32_t j = (p.addr >> sh) & 255;
+            if (p.plen <= nl) {
+                const uint32_t span = 1u << (nl - p.plen);
+                std::fill(defs + (j & ~(span - 1)), defs + (j & ~(span - 1)) + span, p.leaf);
+            } else {
+                sub[j].push_back(p);
+            }
+        }
+        for (uint32_t j = 0; j < 256; j++) {
+            const uint32_t e = node(sub[j], base | (j << sh), nl, defs[j]);
+            (*c)[off + j] = e;
+        }
+        if (off > L4_OFF)
+            ok = false;
+        return L4_PTR | (uint32_t)off;
+    }
+};
+
+}  // namespace
+
+bool build_l4trie(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
+                  std::vector<uint32_t> *l4c, std::vector<uint64_t> *l4l)
 {
     std::stable_sort(pfx.begin(), pfx.end(),
                      [](const Pfx4 &a, const Pfx4 &b) { return a.plen < b.plen; });
-    dir16->assign(1u << 16, 0);
-    uint64_t *d = dir16->data();
-    size_t n_long = 0;
+    l4c->assign(1u << 16, 0);
+    l4l->clear();
+    // /0../16: paint the directory's covering leaves, shortest first
     for (const Pfx4 &p : pfx) {
-        if (p.plen <= 16) {
-            uint32_t start = p.plen ? (p.addr >> 16) & ~((1u << (16 - p.plen)) - 1) : 0;
-            for (uint32_t j = start; j < start + (1u << (16 - p.plen)); j++)
-                d[j] = (d[j] & 0xFFFFFFFF00000000ull) | p.leaf;
-        } else {
-            d[p.addr >> 16] |= (uint64_t)(1u << (p.plen - 17)) << 32;
-            n_long++;
-        }
+        if (p.plen > 16)
+            break;
+        const uint32_t start = p.plen ? (p.addr >> 16) & ~((1u << (16 - p.plen)) - 1) : 0;
+        std::fill(l4c->begin() + start, l4c->begin() + start + (1u << (16 - p.plen)),
+                  p.leaf);
     }
-    const uint32_t ns = (uint32_t)lh4_slots(n_long);
-    lh4->assign(ns, 0);
-    *mask = ns - 1;
-    uint64_t *t = lh4->data();
-    for (const Pfx4 &p : pfx) {
-        if (p.plen <= 16)
-            continue;
-        uint32_t l26;
-        if (p.leaf & LPM_INDIRECT) {
-            l26 = LH_INDIRECT | (p.leaf & LPM_PAYLOAD);
-        } else if (p.leaf > LH_PAYLOAD) {
-            ovf->push_back(p.leaf);
-            l26 = LH_INDIRECT | (uint32_t)(ovf->size() - 1);
-        } else {
-            l26 = p.leaf;
-        }
-        uint32_t s = lh_hash(p.addr, p.plen, ns - 1);
-        while (t[s] >> 63)
-            s = (s + 1) & (ns - 1);
-        t[s] = ((uint64_t)(LH_VALID | (uint32_t)(p.plen - 17) << 27 | l26) << 32) |
-               p.addr;
+    std::map<uint32_t, std::vector<Pfx4>> by16;
+    for (const Pfx4 &p : pfx)
+        if (p.plen > 16)
+            by16[p.addr >> 16].push_back(p);
+    L4Trie b{l4c, ovf, l4l};
+    for (auto &g : by16) {
+        const uint32_t def = (*l4c)[g.first];
+        const uint32_t e = b.node(g.second, g.first << 16, 16, def);
+        (*l4c)[g.first] = e;
     }
+    return b.ok;
 }
 
 // Blocked Bloom filter with ~`per_word` keys per 32-bit word, capped.
@@ -187,25 +238,23 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         }
     }
 
-    // ---- ipcache v4: the hashed layout while its probe table fits one
-    //      XCD's L2 (or when forced), DIR-24-8 otherwise
+    // ---- ipcache v4: the compact multibit layout unless forced (or its
+    //      offsets overflow), DIR-24-8 otherwise
     if (ipc) {
         std::vector<Pfx4> pfx;
         ipcache_v4(ipc, &pfx, &img->lbl_ovf);
         img->n_prefix4 = (uint32_t)pfx.size();
         if (!pfx.empty()) {
-            size_t n_long = 0;
-            for (const Pfx4 &p : pfx)
-                n_long += p.plen > 16;
-            // measured at C2 (profiles/bench_r01_v5*.json): the hashed
-            // layout's extra probes cost more than its L2 residency gains,
-            // so AUTO stays on DIR-24-8
-            const bool hashed = opt.lpm4 == LPM4_HASHED;
-            (void)n_long;
-            if (hashed) {
-                build_lh4(pfx, &img->lbl_ovf, &img->dir16, &img->lh4,
-                          &img->lh4_mask);
-                img->lpm4_layout = LPM4_HASHED;
+            const size_t n_ovf = img->lbl_ovf.size();
+            bool trie = opt.lpm4 != LPM4_DIR24_8;
+            if (trie && !build_l4trie(pfx, &img->lbl_ovf, &img->l4c, &img->l4l)) {
+                img->l4c.clear();
+                img->l4l.clear();
+                img->lbl_ovf.resize(n_ovf);
+                trie = false;
+            }
+            if (trie) {
+                img->lpm4_layout = LPM4_TRIE;
             } else {
                 build_dir24_8(pfx, &img->tbl24, &img->tbl8);
                 img->lpm4_layout = LPM4_DIR24_8;

@@ -16,20 +16,18 @@ struct PolLoc {
 };
 
 // IPv4 ipcache layouts (cfc_set_option CFC_OPT_LPM4)
-enum Lpm4Layout { LPM4_AUTO = 0, LPM4_DIR24_8 = 1, LPM4_HASHED = 2 };
-// AUTO picks the hashed layout while its probe table stays <= 4 MiB
-constexpr size_t LH4_MAX_BYTES = 4u << 20;
+enum Lpm4Layout { LPM4_AUTO = 0, LPM4_DIR24_8 = 1, LPM4_TRIE = 2 };
 
 struct BuildOpts {
     int lpm4 = LPM4_AUTO;
 };
 
 struct HostImage {
-    // IPv4 ipcache: DIR-24-8 (tbl24/tbl8) or hashed (dir16/lh4)
+    // IPv4 ipcache: compact multibit (l4c/l4l) or DIR-24-8 (tbl24/tbl8)
     std::vector<uint32_t> tbl24, tbl8, lbl_ovf;
-    std::vector<uint64_t> dir16, lh4;
-    uint32_t lh4_mask = 0;
-    int lpm4_layout = 0;           // LPM4_DIR24_8 / LPM4_HASHED, 0 = empty
+    std::vector<uint32_t> l4c;
+    std::vector<uint64_t> l4l;
+    int lpm4_layout = 0;           // LPM4_DIR24_8 / LPM4_TRIE, 0 = empty
     uint32_t n_prefix4 = 0;
     // prefilter
     std::vector<uint32_t> pf_tbl24, pf_tbl8;
@@ -60,9 +58,9 @@ struct Pfx4 {
 };
 void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
                    std::vector<uint32_t> *tbl8);
-// hashed layout; direct labels >= 2^26 get lbl_ovf entries
-void build_lh4(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
-               std::vector<uint64_t> *dir16, std::vector<uint64_t> *lh4,
-               uint32_t *mask);
+// compact multibit layout (layout.h); labels too wide for a list entry get
+// lbl_ovf entries.  False when an offset would not fit its 24 bits.
+bool build_l4trie(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
+                  std::vector<uint32_t> *l4c, std::vector<uint64_t> *l4l);
 
 }  // namespace cfc

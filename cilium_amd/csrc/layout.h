@@ -10,8 +10,9 @@
 // they are small next to 288 GB of HBM3E and stay L2/Infinity-Cache resident.
 //
 // HBM layout of one epoch (read-only while classifying):
-//   lpm4      DIR-24-8 IPv4 ipcache: tbl24 (2^24 x u32 = 64 MiB, resident in
-//             the 256 MiB Infinity Cache) + 256-entry tbl8 groups for /25-/32
+//   lpm4      IPv4 ipcache: the compact multibit layout (l4c nodes + l4l
+//             prefix lists, L2-resident), or DIR-24-8: tbl24 (2^24 x u32 =
+//             64 MiB, Infinity Cache) + 256-entry tbl8 groups for /25-/32
 //   pf4_dyn   same structure for the prefilter LPM deny-list (when used)
 //   pf4_fix   exact /32 deny set: 16-B buckets of 4 addresses (0 = empty)
 //   lxc4      local endpoints by IPv4: 16-B slots with the endpoint record
@@ -40,32 +41,34 @@ constexpr uint32_t LPM_PAYLOAD = 0x3FFFFFFFu;
 
 constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 
-// ---- IPv4 LPM, hashed layout (sized for one XCD's 4 MiB L2) ---------------
+// ---- IPv4 LPM, compact multibit layout (default) --------------------------
 // DIR-24-8 costs ~1.3 Infinity-Cache accesses per lookup (tbl24 is 64 MiB).
-// When the ipcache is small enough, lookups instead go to two L2-resident
-// structures:
-//   dir16[a >> 16] (u64)  lo: leaf of the longest prefix <= /16 covering
-//                         this /16 (encoding above, 0 = none); hi: bit L-17
-//                         set for each length L in 17..32 that has a prefix
-//                         inside this /16 (512 KiB)
-//   lh4 (u64 slots)       every prefix of length >= 17, open addressing with
-//                         linear probing at load <= 50%:
-//                         lo = prefix address (host order, masked),
-//                         hi = LH_VALID | (L-17) << 27 | leaf26
-// A lookup probes the lengths of its /16 longest first (usually one or two
-// probes) and falls back to the /16's own leaf.  leaf26 is the label, or
-// LH_INDIRECT | index into lbl_ovf for labels >= 2^26.
-constexpr uint32_t LH_VALID = 0x80000000u;
-constexpr uint32_t LH_INDIRECT = 1u << 26;
-constexpr uint32_t LH_PAYLOAD = (1u << 26) - 1;
-__host__ __device__ inline uint32_t lh_hash(uint32_t key, uint32_t len,
-                                            uint32_t mask)
+// The compact layout keeps the whole ipcache in about 1-2 MiB, resident in
+// every XCD's 4 MiB L2:
+//   l4c (u32 nodes)  l4c[0..65535] is the /16 directory; 256-entry chunks
+//                    for the next 8 bits follow.  A node is
+//      bit31 clear              a leaf (LPM leaf encoding above; 0 = none)
+//      bit31 set, cnt == 0      a chunk at l4c[off] for the next 8 bits
+//      bit31 set, cnt  > 0      a list of cnt prefixes at l4l[off]
+//                    (off = bits 0-23, cnt = bits 24-30)
+//   l4l (u64)        per-node prefix lists, longest first, ending with the
+//                    node's own covering prefix (which always matches), padded
+//                    to an even length so that one 16-byte load reads two:
+//                    lo = prefix address (host order, masked),
+//                    hi = (len & 31) << 27 | leaf27 (LL_INDIRECT -> lbl_ovf)
+// A node lists its prefixes while it has fewer than L4_LIST_MAX, and is
+// split into a chunk beyond; a lookup is the directory word plus, usually,
+// one 16-byte list load.
+constexpr uint32_t L4_PTR = 0x80000000u;
+constexpr uint32_t L4_OFF = 0xFFFFFFu;
+constexpr uint32_t L4_LIST_MAX = 16;
+constexpr uint32_t LL_INDIRECT = 1u << 26;
+constexpr uint32_t LL_PAYLOAD = (1u << 26) - 1;
+__host__ __device__ inline bool l4_match(uint32_t a, uint32_t addr, uint32_t hi)
 {
-    uint64_t k = ((uint64_t)len << 32) | key;
-    k ^= k >> 29;
-    k *= 0xbf58476d1ce4e5b9ull;
-    k ^= k >> 32;
-    return (uint32_t)k & mask;
+    const uint32_t len = hi >> 27;   // 0 stands for 32
+    const uint32_t m = len ? 0xFFFFFFFFu << (32 - len) : 0xFFFFFFFFu;
+    return (a & m) == addr;
 }
 
 // ---- policy: open addressing, linear probing over 16-byte slots -------------
@@ -143,10 +146,9 @@ constexpr uint32_t PF_BLOOM_MAX_WORDS = 8192;     // 32 KiB
 constexpr uint32_t LXC_LDS_MAX_SLOTS = 1024;      // 16 KiB of endpoint slots
 
 struct DevTables {
-    const uint64_t *dir16;         // hashed IPv4 LPM layout, or null
-    const uint64_t *lh4;
-    uint32_t lh4_mask;
-    const uint32_t *tbl24;         // DIR-24-8 layout (null: none or hashed)
+    const uint32_t *l4c;           // compact IPv4 LPM nodes, or null
+    const uint64_t *l4l;           // its prefix lists
+    const uint32_t *tbl24;         // DIR-24-8 layout (null: none or compact)
     const uint32_t *tbl8;
     const uint32_t *lbl_ovf;
     const uint32_t *pf_tbl24;      // null when the dyn prefilter is empty

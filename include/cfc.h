@@ -104,16 +104,17 @@ int cfc_commit(cfc_ctx *ctx, void *stream);
 
 /* ----------------------------------------------------------------- options */
 /* CFC_OPT_LPM4: device layout of the IPv4 ipcache, applied at the next
- * commit.  AUTO (default) uses the hashed layout — a /16 directory plus a
- * probe table for /17-/32, both L2-resident — while the probe table fits in
- * 4 MiB, and DIR-24-8 (64 MiB, Infinity-Cache resident) beyond.  Lookups
- * give the same result in every layout.
+ * commit.  AUTO (default) and TRIE use the compact multibit layout — a /16
+ * directory, 8-bit chunks and short per-node prefix lists, a few MiB and
+ * L2-resident; DIR-24-8 is the classic 64 MiB table (Infinity-Cache
+ * resident), also used when the compact layout's offsets would overflow.
+ * Lookups give the same result in every layout.
  * CFC_OPT_TIMING: 1 = record HIP events around the kernels of every
  * cfc_classify_* call (read back with cfc_timing_collect). */
 #define CFC_OPT_LPM4 1
 #define CFC_LPM4_AUTO 0
 #define CFC_LPM4_DIR24_8 1
-#define CFC_LPM4_HASHED 2
+#define CFC_LPM4_TRIE 2
 #define CFC_OPT_TIMING 2
 int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
 
@@ -196,8 +197,8 @@ typedef struct {
     uint32_t endpoints;
     uint32_t prefilter_v4_fix;
     uint32_t prefilter_v4_dyn;
-    uint32_t lpm4_layout;       /* CFC_LPM4_DIR24_8 / _HASHED, 0 = empty */
-    uint32_t lpm4_probe_slots;  /* hashed layout: probe-table slots */
+    uint32_t lpm4_layout;       /* CFC_LPM4_DIR24_8 / _TRIE, 0 = empty */
+    uint32_t lpm4_kib;          /* device KiB of the IPv4 ipcache layout */
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

@@ -44,7 +44,7 @@ def test_options_on_host_only_context():
     """The ipcache layout is a table option (it applies at the next commit);
     timing needs a device."""
     dp = C.host_only()
-    for v in (_lib.LPM4_AUTO, _lib.LPM4_DIR24_8, _lib.LPM4_HASHED):
+    for v in (_lib.LPM4_AUTO, _lib.LPM4_DIR24_8, _lib.LPM4_TRIE):
         dp.set_option(_lib.OPT_LPM4, v)
     assert errno_of(lambda: dp.set_option(_lib.OPT_LPM4, 3)) == errno.EINVAL
     assert errno_of(lambda: dp.set_option(99, 0)) == errno.EINVAL

@@ -24,7 +24,7 @@ def torch():
     return torch
 
 
-LAYOUTS = {"dir24_8": L.LPM4_DIR24_8, "hashed": L.LPM4_HASHED}
+LAYOUTS = {"dir24_8": L.LPM4_DIR24_8, "trie": L.LPM4_TRIE}
 
 
 def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
@@ -110,9 +110,10 @@ def test_c2_layouts_and_auto_choice(torch):
     load_tables(dp, t)
     st = dp.stats()
     dp.close()
-    assert st["lpm4_layout"] == L.LPM4_DIR24_8
+    assert st["lpm4_layout"] == L.LPM4_TRIE
+    assert st["lpm4_kib"] <= 4096
     h = S.headers_c2(t, 1_000_000, seed=23)
-    compare_with_oracle(torch, t, h, 0, lpm4=L.LPM4_HASHED)
+    compare_with_oracle(torch, t, h, 0, lpm4=L.LPM4_DIR24_8)
 
 
 def _prefilter(t):
@@ -156,7 +157,7 @@ def test_wide_labels_and_edge_tables(torch, layout):
     ipc["label"][100:120] = S.HOST_ID
     ipc["label"][120:140] = S.CLUSTER_ID
     ipc["label"][140:160] = 0
-    ipc["label"][160:180] = (1 << 26) + np.arange(20)   # > the lh4 leaf field
+    ipc["label"][160:180] = (1 << 26) + np.arange(20)   # > a list entry's leaf field
     ipc = np.concatenate([ipc, S._v4_entries(np.array([0], np.uint32), [0], [77])])
     t = S.Tables(ipc, S.config_c2(1, n_prefixes=10, n_policy=10).endpoints, {},
                  np.zeros(0, S.PREFILTER_DT), {S.EP_LXC_ID: 2})
