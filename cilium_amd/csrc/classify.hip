@@ -70,9 +70,37 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 // k_count: the packed u32 byte sums stay exact (64512 headers x 65535
 // bytes < 2^32, so they never carry into the packet count)
 constexpr uint64_t COUNT_PER_BLOCK = 63 * BLOCK;
+// workspace: entry indices [n] (egress: a second array at ctr_stride(n)),
+// then the partial slabs; both arrays 16-byte aligned for k_count
+__host__ __device__ constexpr uint64_t ctr_stride(uint64_t n) { return (n + 3) & ~3ull; }
 #ifndef CFC_UNROLL
-#define CFC_UNROLL 2   // headers in flight per thread
+#define CFC_UNROLL 1   // headers in flight per thread
 #endif
+#ifndef CFC_WG_PER_CU
+#define CFC_WG_PER_CU 2   // 1024-thread workgroups resident per CU
+#endif
+constexpr int WAVES_PER_SIMD = 4 * CFC_WG_PER_CU;
+constexpr size_t LDS_PER_WG = LDS_BYTES_MAX / CFC_WG_PER_CU;
+
+// update_metrics keys (reason, direction) a mode can produce.  A header
+// carries the index of its key, or NONE; every thread counts its headers per
+// key in registers, and the workgroup sums them in LDS at the end.
+constexpr int LDS_MET_U64 = 16;   // 2 x 7 keys, rounded to uint4 units
+template <int MODE>
+constexpr int met_n()
+{
+    return MODE == CFC_MODE_EGRESS ? 7 : MODE == CFC_MODE_XDP ? 0 : 4;
+}
+// reason (as the positive DROP_* magnitude) and direction of key k
+template <int MODE>
+__host__ __device__ constexpr uint32_t met_reason_dir(int k)
+{
+    constexpr uint32_t eg[7][2] = {{0, 2}, {132, 2}, {133, 2}, {137, 2},
+                                   {140, 2}, {0, 1}, {133, 1}};
+    constexpr uint32_t in[4][2] = {{0, 1}, {133, 1}, {137, 1}, {140, 1}};
+    return MODE == CFC_MODE_EGRESS ? eg[k][0] * METRIC_DIRS + eg[k][1]
+                                   : in[k][0] * METRIC_DIRS + in[k][1];
+}
 
 template <class T>
 __device__ __forceinline__ T ld_nt(const T *p)
@@ -83,6 +111,14 @@ template <class T>
 __device__ __forceinline__ void st_nt(T v, T *p)
 {
     __builtin_nontemporal_store(v, p);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte non-temporal load (p 16-byte aligned)
+__device__ __forceinline__ uint4 ld_nt4(const uint32_t *p)
+{
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
 
 __device__ __forceinline__ uint4 ld16(const void *p)
@@ -182,7 +218,7 @@ __device__ __forceinline__ bool pf_resolve(const DevTables &T, uint32_t addr,
 }
 
 __device__ __forceinline__ bool bloom_maybe(uint32_t off, uint32_t mask,
-                                            uint64_t h)
+                                            uint32_t h)
 {
     const uint32_t b = bloom_bits(h);
     return (lds_word(off + ((uint32_t)h & mask)) & b) == b;
@@ -223,11 +259,21 @@ struct PolicyProbe {
     uint4 v;
     // key j by masking, not by selecting among stored keys: the compiler
     // turns a 3-way select on a per-lane index into a scratch-memory table
+    __device__ __forceinline__ uint32_t lo(uint32_t i) const
+    {
+        return id & (0u - (uint32_t)(i != 2));
+    }
+    __device__ __forceinline__ uint32_t hi(uint32_t i) const
+    {
+        return (pp & (0u - (uint32_t)(i != 1))) | eg;
+    }
     __device__ __forceinline__ uint64_t key(uint32_t i) const
     {
-        const uint32_t lo = id & (0u - (uint32_t)(i != 2));
-        const uint32_t hi = (pp & (0u - (uint32_t)(i != 1))) | eg;
-        return ((uint64_t)hi << 32) | lo;
+        return ((uint64_t)hi(i) << 32) | lo(i);
+    }
+    __device__ __forceinline__ uint32_t pre(uint32_t i) const
+    {
+        return pol_key_pre(lo(i), hi(i));
     }
 };
 
@@ -237,7 +283,7 @@ __device__ __forceinline__ void policy_probe_key(const DevTables &T,
 {
     P.j = P.maybe ? __builtin_ctz(P.maybe) : 3;
     if (P.j < 3) {
-        P.s = hash64(P.key(P.j), mask);
+        P.s = pol_slot(P.pre(P.j), mask);
         P.v = ld16(T.pol + base + P.s);
     }
 }
@@ -255,11 +301,11 @@ __device__ __forceinline__ void policy_issue(const DevTables &T, const Lds &S,
     P.eg = egress << 24;
     P.maybe = frag ? 2u : 7u;                // policy.h:61,85
     if (S.polb) {
-        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.key(0))))
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(0))))
             P.maybe &= ~1u;
-        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.key(1))))
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(1))))
             P.maybe &= ~2u;
-        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.key(2))))
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(2))))
             P.maybe &= ~4u;
     }
     policy_probe_key(T, base, mask, P);
@@ -303,7 +349,7 @@ __device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
         maybe &= ~(1u << j);   // a false positive of the filter
         j = maybe ? __builtin_ctz(maybe) : 3;
         if (j < 3) {
-            s = hash64(P0.key(j), mask);
+            s = pol_slot(P0.pre(j), mask);
             v = ld16(T.pol + base + s);
         }
     }
@@ -319,41 +365,71 @@ __device__ __forceinline__ PolicyResult policy_access(
     return policy_resolve(T, base, mask, P);
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o);
-    return v;
-}
 
-// update_metrics for every lane of the wave at once: key = index into the
-// metrics block ([reason][dir][count,bytes]) or NONE.  Must be reached by
-// the whole wave (uniform control flow).  Keys are few and hot, so lanes
-// with the same key are summed across the wave before one LDS atomic.
-__device__ __forceinline__ void metrics_wave(unsigned long long *s_met,
-                                             uint32_t key, uint32_t len)
+
+// key index of (reason, dir) in this mode's table (met_reason_dir)
+template <int MODE>
+__device__ __forceinline__ uint32_t mkey(int reason, int dir)
 {
-    uint64_t pending = __ballot(key != NONE);
-    const int lane = threadIdx.x & 63;
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const uint32_t lk = __shfl(key, leader);
-        const bool mine = key == lk;
-        const uint64_t m = __ballot(mine);
-        const uint32_t sum = wave_sum(mine ? len : 0u);
-        if (lane == leader) {
-            atomicAdd(&s_met[lk], (unsigned long long)__popcll(m));
-            atomicAdd(&s_met[lk + 1], (unsigned long long)sum);
+    if (MODE == CFC_MODE_EGRESS) {
+        if (dir == METRIC_INGRESS)
+            return reason == 0 ? 5u : 6u;
+        switch (reason) {
+        case 0: return 0;
+        case -132: return 1;
+        case -133: return 2;
+        case -137: return 3;
+        default: return 4;   // -140
         }
-        pending &= ~m;
+    }
+    switch (reason) {
+    case 0: return 0;
+    case -133: return 1;
+    case -137: return 2;
+    default: return 3;       // -140
     }
 }
 
-__device__ __forceinline__ uint32_t mkey(int reason, int dir)
-{
-    return ((uint32_t)(uint8_t)(-reason) * METRIC_DIRS + (uint32_t)dir) * 2;
-}
+// Per-thread update_metrics counts (bytes in u32: a thread sees at most
+// 65536 headers between flushes, 65536 x 65535 < 2^32).
+template <int N>
+struct MetAcc {
+    uint32_t cnt[N > 0 ? N : 1], byt[N > 0 ? N : 1];
+    __device__ __forceinline__ void clear()
+    {
+#pragma unroll
+        for (int k = 0; k < N; k++)
+            cnt[k] = byt[k] = 0;
+    }
+    __device__ __forceinline__ void add(uint32_t key, uint32_t len)
+    {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const bool m = key == (uint32_t)k;
+            cnt[k] += m;
+            byt[k] += m ? len : 0u;
+        }
+    }
+    // whole-wave sums into the LDS histogram (uniform control flow)
+    __device__ __forceinline__ void flush(unsigned long long *s_met)
+    {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            uint32_t c = cnt[k];
+            uint64_t b = byt[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                c += __shfl_xor(c, o);
+                b += __shfl_xor(b, o);
+            }
+            if ((threadIdx.x & 63) == 0 && c) {
+                atomicAdd(&s_met[2 * k], (unsigned long long)c);
+                atomicAdd(&s_met[2 * k + 1], (unsigned long long)b);
+            }
+        }
+        clear();
+    }
+};
 
 // Per-header state carried through the lookup rounds.
 struct Hdr {
@@ -498,11 +574,11 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
             if (!(h.rec.w & LXC_HAS_POLICY)) {
                 h.act = TC_ACT_SHOT;
                 h.ver = DROP_MISSED_TAIL_CALL;
-                h.met0 = mkey(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
+                h.met0 = mkey<MODE>(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
             } else if (!known) {
                 h.act = TC_ACT_SHOT;
                 h.ver = DROP_CT_UNKNOWN_PROTO;
-                h.met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
+                h.met0 = mkey<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
             } else {
                 h.need_pol = true;
                 h.pbase = h.rec.y;
@@ -513,10 +589,10 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
         h.act = TC_ACT_SHOT;
         if (h.src_lxc != E.lxc_id) {   // is_valid_lxc_src_ipv4 (lxc.h:55)
             h.ver = DROP_INVALID_SIP;
-            h.met0 = mkey(DROP_INVALID_SIP, METRIC_EGRESS);
+            h.met0 = mkey<MODE>(DROP_INVALID_SIP, METRIC_EGRESS);
         } else if (!known) {
             h.ver = DROP_CT_UNKNOWN_PROTO;
-            h.met0 = mkey(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
+            h.met0 = mkey<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
         } else {
             // destination identity (bpf_lxc.c:516-532)
             h.ident = h.e24 ? h.e24
@@ -561,19 +637,19 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     if (v < 0) {
         act = TC_ACT_SHOT;
         ver = DROP_POLICY;
-        met0 = mkey(DROP_POLICY, mdir);
+        met0 = mkey<MODE>(DROP_POLICY, mdir);
     } else if (!EGR) {
         if (h.skip_proxy)
             v = 0;
         // redirect_to_proxy, or TRACE_TO_LXC + delivery
         act = (v > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
         ver = v;
-        met0 = v > 0 ? NONE : mkey(0, METRIC_INGRESS);
+        met0 = v > 0 ? NONE : mkey<MODE>(0, METRIC_INGRESS);
     } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
         act = TC_ACT_REDIRECT;
         ver = v;
     } else {
-        met0 = mkey(0, METRIC_EGRESS);   // to_host/local/to_stack
+        met0 = mkey<MODE>(0, METRIC_EGRESS);   // to_host/local/to_stack
         ver = 0;
         if (!(h.rec.w & LXC_VALID)) {
             act = TC_ACT_OK;
@@ -582,7 +658,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
         } else if (!(h.rec.w & LXC_HAS_POLICY)) {
             act = TC_ACT_SHOT;
             ver = DROP_MISSED_TAIL_CALL;
-            met1 = mkey(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
+            met1 = mkey<MODE>(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
         } else {
             // local delivery: the destination's ipv4_policy with
             // src = SECLABEL of the sending endpoint
@@ -594,11 +670,11 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
             if (w < 0) {
                 act = TC_ACT_SHOT;
                 ver = DROP_POLICY;
-                met1 = mkey(DROP_POLICY, METRIC_INGRESS);
+                met1 = mkey<MODE>(DROP_POLICY, METRIC_INGRESS);
             } else {
                 act = (w > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
                 ver = w;
-                met1 = w > 0 ? NONE : mkey(0, METRIC_INGRESS);
+                met1 = w > 0 ? NONE : mkey<MODE>(0, METRIC_INGRESS);
             }
         }
     }
@@ -615,7 +691,7 @@ struct LdsPlan {
     uint32_t lxc_slots, pf_words, pol_words;
     __host__ __device__ size_t bytes() const
     {
-        return 8ull * METRIC_U64 + 16ull * lxc_slots + 4ull * pf_words +
+        return 8ull * LDS_MET_U64 + 16ull * lxc_slots + 4ull * pf_words +
                4ull * pol_words;
     }
 };
@@ -637,14 +713,14 @@ __device__ __forceinline__ void lds_copy(W *dst, const W *src, uint32_t n)
 }
 
 template <int MODE, int U>
-__global__ __launch_bounds__(BLOCK) void k_classify_v4(
+__global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
     uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
 {
     // LDS image (uint4 units): metrics | endpoint slots | pf Bloom | pol Bloom
     unsigned long long *s_met = lds_met();
     Lds S;
-    S.lxc_off = METRIC_U64 / 2;
+    S.lxc_off = LDS_MET_U64 / 2;
     const uint32_t pf4 = S.lxc_off + L.lxc_slots;      // uint4 index
     const uint32_t pol4 = pf4 + L.pf_words / 4;
     S.pfb_off = 4 * pf4;
@@ -654,7 +730,7 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
     S.polb = L.pol_words != 0;
     S.pfb_mask = L.pf_words - 1;
     S.polb_mask = L.pol_words - 1;
-    for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64; j += BLOCK)
+    for (uint32_t j = threadIdx.x; j < (uint32_t)LDS_MET_U64; j += BLOCK)
         s_met[j] = 0;
     lds_copy(cfc_smem + S.lxc_off, reinterpret_cast<const uint4 *>(T.lxc4),
              L.lxc_slots);
@@ -666,8 +742,11 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
 
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
     const uint64_t end = min(in.n, start + per_block);
-    // the trip count is uniform across the workgroup (metrics_wave needs
-    // whole waves)
+    // the trip count is uniform across the workgroup (the metrics flush
+    // needs whole waves)
+    MetAcc<met_n<MODE>()> acc;
+    acc.clear();
+    uint32_t iter = 0;
     for (uint64_t base = start; base < end; base += (uint64_t)BLOCK * U) {
         Hdr h[U];
 #pragma unroll
@@ -694,31 +773,38 @@ __global__ __launch_bounds__(BLOCK) void k_classify_v4(
                 if (MODE != CFC_MODE_XDP) {
                     st_nt(h[u].ctr0, ctr_idx + i);
                     if (MODE == CFC_MODE_EGRESS)
-                        st_nt(h[u].ctr1, ctr_idx + in.n + i);
+                        st_nt(h[u].ctr1, ctr_idx + ctr_stride(in.n) + i);
                 }
             }
-            metrics_wave(s_met, h[u].met0, len);
+            acc.add(h[u].met0, len);
             if (MODE == CFC_MODE_EGRESS)
-                metrics_wave(s_met, h[u].met1, len);
+                acc.add(h[u].met1, len);
+        }
+        if (++iter == 65536 / (2 * U)) {
+            acc.flush(s_met);
+            iter = 0;
         }
     }
+    acc.flush(s_met);
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < (uint32_t)METRIC_U64; j += BLOCK) {
-        unsigned long long v = s_met[j];
+    for (uint32_t j = threadIdx.x; j < 2u * met_n<MODE>(); j += BLOCK) {
+        const unsigned long long v = s_met[j];
         if (v)
-            atomicAdd((unsigned long long *)&g_met[j], v);
+            atomicAdd((unsigned long long *)&g_met[met_reason_dir<MODE>(j >> 1) * 2 + (j & 1)],
+                      v);
     }
 }
 
 // Policy-entry counters from the per-header entry indices: an LDS
-// histogram per <= COUNT_PER_BLOCK headers (ctr index i < n_hdr pairs with
-// meta[i], i >= n_hdr — egress local delivery — with meta[i - n_hdr]).
-// One u64 LDS atomic per header adds {1 << 32 | len}.
+// histogram per <= COUNT_PER_BLOCK headers.  blockIdx.y selects the index
+// array (1: egress local delivery, at ctr_idx + stride), both paired with
+// meta[i].  Four headers per thread and iteration (16-byte loads, four
+// independent LDS atomics); one u64 atomic per header adds {1 << 32 | len}.
 template <bool LDS>
 __global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
+                                                 uint64_t stride,
                                                  const uint32_t *meta,
-                                                 uint64_t n, uint64_t n_hdr,
-                                                 uint32_t n_ctr,
+                                                 uint64_t n, uint32_t n_ctr,
                                                  uint64_t *partial,
                                                  uint64_t *g_ctr)
 {
@@ -728,13 +814,11 @@ __global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
             s_ctr[j] = 0;
         __syncthreads();
     }
-    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
-    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
-    for (uint64_t i = start + threadIdx.x; i < end; i += BLOCK) {
-        const uint32_t c = ld_nt(ctr_idx + i);
+    const uint32_t *idx = ctr_idx + blockIdx.y * stride;   // 16-B aligned
+    auto add = [&](uint32_t c, uint32_t m) {
         if (c == NONE)
-            continue;
-        const uint32_t len = meta[i < n_hdr ? i : i - n_hdr] >> 16;
+            return;
+        const uint32_t len = m >> 16;
         if (LDS) {
             atomicAdd(&s_ctr[c], (1ull << 32) | len);
         } else {
@@ -742,10 +826,32 @@ __global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
             atomicAdd((unsigned long long *)&g_ctr[2 * c + 1],
                       (unsigned long long)len);
         }
+    };
+    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
+    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    const uint64_t end4 = start + ((end - start) & ~3ull);
+    for (uint64_t i = start + 4 * threadIdx.x; i < end4; i += 4 * BLOCK) {
+        const uint4 c = ld_nt4(idx + i);
+        uint4 m;
+        if ((reinterpret_cast<uintptr_t>(meta + i) & 15) == 0) {
+            m = ld_nt4(meta + i);
+        } else {
+            m.x = meta[i];
+            m.y = meta[i + 1];
+            m.z = meta[i + 2];
+            m.w = meta[i + 3];
+        }
+        add(c.x, m.x);
+        add(c.y, m.y);
+        add(c.z, m.z);
+        add(c.w, m.w);
     }
+    for (uint64_t i = end4 + threadIdx.x; i < end; i += BLOCK)
+        add(idx[i], meta[i]);
     if (LDS) {
         __syncthreads();
-        uint64_t *dst = partial + (size_t)blockIdx.x * n_ctr;
+        const size_t row = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+        uint64_t *dst = partial + row * n_ctr;
         for (uint32_t j = threadIdx.x; j < n_ctr; j += BLOCK)
             st_nt((uint64_t)s_ctr[j], dst + j);
     }
@@ -796,15 +902,17 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES_MAX);
+                                  (int)LDS_PER_WG);
         attr_set = true;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
                        out, E, ctr_idx, g_met, per_block);
 }
 
-// u32 index of the partial slabs in the workspace (8-byte aligned)
-uint64_t partial_off(uint64_t m) { return (m + 1) & ~1ull; }
+uint64_t partial_off(uint64_t n, int mode)
+{
+    return (mode == CFC_MODE_EGRESS ? 2 : 1) * ctr_stride(n);
+}
 
 }  // namespace
 
@@ -824,11 +932,11 @@ size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode)
 {
     if (n == 0 || mode == CFC_MODE_XDP)
         return 0;
-    const uint64_t m = mode == CFC_MODE_EGRESS ? 2 * n : n;
-    size_t bytes = 4ull * partial_off(m);            // entry index per header
+    const uint64_t halves = mode == CFC_MODE_EGRESS ? 2 : 1;
+    size_t bytes = 4ull * partial_off(n, mode);      // entry index per header
     if (n_ctr && n_ctr <= LDS_CTR_MAX) {
-        const uint64_t nblk = (m + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK;
-        bytes += 8ull * n_ctr * nblk;                // partial slabs
+        const uint64_t nblk = (n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK;
+        bytes += 8ull * n_ctr * nblk * halves;       // partial slabs
     }
     return bytes;
 }
@@ -840,12 +948,13 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 {
     if (in.n == 0)
         return 0;
-    if (classify_lds_bytes(T) > LDS_BYTES_MAX)
+    if (classify_lds_bytes(T) > LDS_PER_WG)
         return -22;
-    // one workgroup per CU (the LDS image allows no more), a contiguous
-    // slice each, rounded to whole loop iterations
+    // CFC_WG_PER_CU workgroups per CU (the LDS image allows no more), a
+    // contiguous slice each, rounded to whole loop iterations
     const uint64_t step = (uint64_t)BLOCK * CFC_UNROLL;
-    uint64_t per_block = (in.n + (uint64_t)num_cus - 1) / (uint64_t)num_cus;
+    const uint64_t nwg = (uint64_t)num_cus * CFC_WG_PER_CU;
+    uint64_t per_block = (in.n + nwg - 1) / nwg;
     per_block = (per_block + step - 1) / step * step;
     const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
     if (tm)
@@ -868,8 +977,10 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
     if (mode != CFC_MODE_XDP && T.n_ctr) {
-        const uint64_t m = mode == CFC_MODE_EGRESS ? 2 * in.n : in.n;
-        const uint32_t nblk = (uint32_t)((m + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        const uint32_t halves = mode == CFC_MODE_EGRESS ? 2 : 1;
+        const uint32_t nblk = (uint32_t)((in.n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        const dim3 grid_c(nblk, halves);
+        const uint64_t stride = ctr_stride(in.n);
         if (T.n_ctr <= LDS_CTR_MAX) {
             static bool attr_set = false;
             if (!attr_set) {
@@ -878,15 +989,16 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                                           LDS_BYTES_MAX);
                 attr_set = true;
             }
-            uint64_t *partial = reinterpret_cast<uint64_t *>(ws + partial_off(m));
-            hipLaunchKernelGGL(k_count<true>, dim3(nblk), dim3(BLOCK), 8ull * T.n_ctr,
-                               s, ws, in.meta, m, in.n, T.n_ctr, partial, g_ctr);
+            uint64_t *partial = reinterpret_cast<uint64_t *>(ws + partial_off(in.n, mode));
+            const uint32_t rows = nblk * halves;
+            hipLaunchKernelGGL(k_count<true>, grid_c, dim3(BLOCK), 8ull * T.n_ctr,
+                               s, ws, stride, in.meta, in.n, T.n_ctr, partial, g_ctr);
             hipLaunchKernelGGL(k_reduce_partials,
-                               dim3((T.n_ctr + 255) / 256, (nblk + REDUCE_ROWS - 1) / REDUCE_ROWS),
-                               dim3(256), 0, s, partial, nblk, T.n_ctr, g_ctr);
+                               dim3((T.n_ctr + 255) / 256, (rows + REDUCE_ROWS - 1) / REDUCE_ROWS),
+                               dim3(256), 0, s, partial, rows, T.n_ctr, g_ctr);
         } else {
-            hipLaunchKernelGGL(k_count<false>, dim3(nblk), dim3(BLOCK), 0, s, ws,
-                               in.meta, m, in.n, T.n_ctr, nullptr, g_ctr);
+            hipLaunchKernelGGL(k_count<false>, grid_c, dim3(BLOCK), 0, s, ws, stride,
+                               in.meta, in.n, T.n_ctr, nullptr, g_ctr);
         }
     }
     if (tm)

@@ -164,7 +164,7 @@ static void bloom_size(std::vector<uint32_t> *b, size_t keys, uint32_t max_words
     uint32_t w = pow2_at_least(std::max<size_t>(64, keys));
     b->assign(std::min(w, max_words), 0u);
 }
-static inline void bloom_add(std::vector<uint32_t> *b, uint64_t h)
+static inline void bloom_add(std::vector<uint32_t> *b, uint32_t h)
 {
     (*b)[h & (b->size() - 1)] |= bloom_bits(h);
 }
@@ -349,11 +349,12 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
                 continue;   // pad bits set: no datapath lookup can match it
             uint16_t proxy;
             memcpy(&proxy, kv.second.val.data(), 2);
-            uint32_t s = hash64(key, loc.mask);
+            const uint32_t pre = pol_key_pre((uint32_t)key, (uint32_t)(key >> 32));
+            uint32_t s = pol_slot(pre, loc.mask);
             while (tab[s].key != POL_EMPTY)
                 s = (s + 1) & loc.mask;
             tab[s].key = key;
-            bloom_add(&img->pol_bloom, pol_bloom_hash(loc.base, key));
+            bloom_add(&img->pol_bloom, pol_bloom_hash(loc.base, pre));
             tab[s].proxy_port = proxy;
             tab[s].ctr = (uint32_t)img->ctr_owner.size();
             img->ctr_owner.emplace_back(m, kv.first);

@@ -99,51 +99,57 @@ struct alignas(16) LxcSlot {
 // ---- prefilter /32 set: 16-byte buckets of 4 addresses, 0 = empty -----------
 constexpr int PF_SLOTS = 4;
 
-// Hashes of the raw keys.
-__host__ __device__ inline uint32_t hash64(uint64_t k, uint32_t mask)
+// Hashes of the raw keys: 32-bit multiply / xor-shift mixes (a 64-bit
+// multiply costs several VALU instructions on the GPU).
+__host__ __device__ inline uint32_t fmix32(uint32_t h)
 {
-    k ^= k >> 29;
-    k *= 0xbf58476d1ce4e5b9ull;
-    k ^= k >> 32;
-    return (uint32_t)k & mask;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
 }
 __host__ __device__ inline uint32_t hash32(uint32_t k, uint32_t mask)
 {
     uint64_t x = (uint64_t)k * 0x9E3779B97F4A7C15ull;
     return (uint32_t)(x >> 32) & mask;
 }
+// struct policy_key as a u64 (lo = identity, hi = dport | nexthdr << 16 |
+// egress << 24), folded to 32 bits; the table slot and the Bloom filter
+// word both derive from it
+__host__ __device__ inline uint32_t pol_key_pre(uint32_t lo, uint32_t hi)
+{
+    return lo * 0x9E3779B1u + hi * 0x7FEB352Du;
+}
+__host__ __device__ inline uint32_t pol_slot(uint32_t pre, uint32_t mask)
+{
+    return fmix32(pre) & mask;
+}
 
 // ---- blocked Bloom filters (LDS-resident while classifying) ----------------
 // One 32-bit word per key, three bits set in it: a query is one ds_read_b32.
 // They only ever answer "absent" or "maybe"; a "maybe" is resolved by the
 // exact table, so a false positive costs one extra probe and never a wrong
-// verdict.
-__host__ __device__ inline uint64_t mix64(uint64_t k)
+// verdict.  The word is h & (words - 1) (at most 13 bits), the bits come
+// from bits 17-31 of h.
+__host__ __device__ inline uint32_t bloom_bits(uint32_t h)
 {
-    k ^= k >> 33;
-    k *= 0xff51afd7ed558ccdull;
-    k ^= k >> 33;
-    k *= 0xc4ceb9fe1a85ec53ull;
-    k ^= k >> 33;
-    return k;
-}
-__host__ __device__ inline uint32_t bloom_bits(uint64_t h)
-{
-    return (1u << ((h >> 32) & 31)) | (1u << ((h >> 40) & 31)) |
-           (1u << ((h >> 48) & 31));
+    return (1u << ((h >> 17) & 31)) | (1u << ((h >> 22) & 31)) | (1u << (h >> 27));
 }
 // policy keys are filtered per endpoint table (its first slot)
-__host__ __device__ inline uint64_t pol_bloom_hash(uint32_t base, uint64_t key)
+__host__ __device__ inline uint32_t pol_bloom_hash(uint32_t base, uint32_t pre)
 {
-    return mix64(key ^ ((uint64_t)base * 0x9E3779B97F4A7C15ull));
+    return fmix32(pre ^ (base * 0x846CA68Bu + 0x5bd1e995u));
 }
-__host__ __device__ inline uint64_t pf_bloom_hash(uint32_t addr)
+__host__ __device__ inline uint32_t pf_bloom_hash(uint32_t addr)
 {
-    return mix64((uint64_t)addr | 0x5bd1e99500000000ull);
+    return fmix32(addr ^ 0x5bd1e995u);
 }
-constexpr uint32_t POL_BLOOM_MAX_WORDS = 16384;   // 64 KiB
+// (sized so that two 1024-thread workgroups fit one CU's 160 KiB of LDS)
+constexpr uint32_t POL_BLOOM_MAX_WORDS = 8192;    // 32 KiB
 constexpr uint32_t PF_BLOOM_MAX_WORDS = 8192;     // 32 KiB
-constexpr uint32_t LXC_LDS_MAX_SLOTS = 1024;      // 16 KiB of endpoint slots
+constexpr uint32_t LXC_LDS_MAX_SLOTS = 512;       // 8 KiB of endpoint slots
 
 struct DevTables {
     const uint32_t *l4c;           // compact IPv4 LPM nodes, or null
