@@ -447,20 +447,20 @@ struct Hdr {
     PolicyProbe P;
 };
 
-// round 1: the header (non-temporal streaming loads)
+// round 1: the header (non-temporal streaming loads).  Lanes past the end
+// of the slice take the slice's last header: they compute exactly what its
+// own lane computes and store the same values to the same places, so no
+// round needs a validity branch; only the metrics count them out.
 __device__ __forceinline__ void r1_load(const cfc_hdr_v4 &in, uint64_t i,
                                         uint64_t end, Hdr &h)
 {
     h.valid = i < end;
-    h.sa = h.da = h.pt = h.mt = h.mk = 0;
-    if (h.valid) {
-        h.sa = ld_nt(in.saddr + i);
-        h.da = ld_nt(in.daddr + i);
-        h.pt = ld_nt(in.ports + i);
-        h.mt = ld_nt(in.meta + i);
-        if (in.mark)
-            h.mk = ld_nt(in.mark + i);
-    }
+    i = h.valid ? i : end - 1;
+    h.sa = ld_nt(in.saddr + i);
+    h.da = ld_nt(in.daddr + i);
+    h.pt = ld_nt(in.ports + i);
+    h.mt = ld_nt(in.meta + i);
+    h.mk = in.mark ? ld_nt(in.mark + i) : 0u;
 }
 
 // round 2: every lookup that only needs the header
@@ -478,8 +478,6 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.hsh = __builtin_bswap32(h.sa);
     h.lxs = h.lss = h.pfb = 0;
     h.pf_maybe = false;
-    if (!h.valid)
-        return;
     if (LPM) {
         if (T.l4c)
             h.l4e = T.l4c[h.lh >> 16];
@@ -527,7 +525,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     // rec: {addr, pol_base, pol_mask, info}; info == 0 -> not local
     h.rec = make_uint4(0, 0, 0, 0);
     uint4 srec = h.rec;
-    if (h.valid && T.lxc4) {
+    if (T.lxc4) {
         h.rec = lxc_resolve(T, S, h.da, h.lxs, h.lx);
         if (EGR)
             srec = lxc_resolve(T, S, h.sa, h.lss, h.ls);
@@ -540,7 +538,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     h.ident = 0;
     h.met0 = h.met1 = h.ctr0 = h.ctr1 = NONE;
     h.xdp_drop = false;
-    if (XDP && h.valid) {
+    if (XDP) {
         bool deny = h.pfd != 0;
         if (!deny)
             deny = h.sa ? (h.pf_maybe && pf_resolve(T, h.sa, h.pfb, h.pf))
@@ -554,7 +552,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
 
     h.need_pol = h.skip_proxy = false;
     h.pbase = h.pmask = h.egress_bit = h.dport = 0;
-    if (!h.valid || MODE == CFC_MODE_XDP || h.xdp_drop)
+    if (MODE == CFC_MODE_XDP || h.xdp_drop)
         return;
     const uint32_t proto = h.mt & 0xFF;
     const bool known = ct_new_dport(proto, h.pt, &h.dport);
@@ -765,20 +763,21 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
         for (int u = 0; u < U; u++) {
             const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
             const uint32_t len = h[u].mt >> 16;
-            if (h[u].valid) {
-                st_nt(h[u].ver, out.verdict + i);
-                st_nt(h[u].ident, out.identity + i);
+            {   // (lanes past the end rewrite the last header's values)
+                const uint64_t o = h[u].valid ? i : end - 1;
+                st_nt(h[u].ver, out.verdict + o);
+                st_nt(h[u].ident, out.identity + o);
                 if (out.action)
-                    out.action[i] = (uint8_t)h[u].act;
+                    out.action[o] = (uint8_t)h[u].act;
                 if (MODE != CFC_MODE_XDP) {
-                    st_nt(h[u].ctr0, ctr_idx + i);
+                    st_nt(h[u].ctr0, ctr_idx + o);
                     if (MODE == CFC_MODE_EGRESS)
-                        st_nt(h[u].ctr1, ctr_idx + ctr_stride(in.n) + i);
+                        st_nt(h[u].ctr1, ctr_idx + ctr_stride(in.n) + o);
                 }
             }
-            acc.add(h[u].met0, len);
+            acc.add(h[u].valid ? h[u].met0 : NONE, len);
             if (MODE == CFC_MODE_EGRESS)
-                acc.add(h[u].met1, len);
+                acc.add(h[u].valid ? h[u].met1 : NONE, len);
         }
         if (++iter == 65536 / (2 * U)) {
             acc.flush(s_met);
