@@ -24,6 +24,7 @@ HOST_ID, WORLD_ID, CLUSTER_ID, HEALTH_ID, INIT_ID = 1, 2, 3, 4, 5
 # header flag bits (cfc.h CFC_HF_*)
 HF_FRAG = 1          # ipv4_is_fragment(): frag_off & htons(0xBFFF)
 HF_TCP_CLOSE = 2     # TCP RST or FIN set (conntrack.h:533)
+HF_EXTHDR = 4        # IPv6: extension headers precede `proto`
 IPPROTO_ICMP, IPPROTO_TCP, IPPROTO_UDP, IPPROTO_ICMPV6 = 1, 6, 17, 58
 
 IPCACHE_DT = np.dtype([("family", "u1"), ("plen", "u1"), ("addr", "u1", 16),
@@ -144,6 +145,193 @@ def gen_ipcache_v4(rng, n, label_base=256, label_mod=16384,
     plen = np.array(out_l, dtype=np.uint8)
     label = (label_base + (np.arange(n) % label_mod)).astype(np.uint32)
     return _v4_entries(byteswap32(host), plen, label)
+
+
+# ------------------------------------------------------------------ IPv6
+def ip6(s: str) -> np.ndarray:
+    """'beef::1' -> 16 network-order bytes."""
+    import ipaddress
+    return np.frombuffer(ipaddress.IPv6Address(s).packed, np.uint8).copy()
+
+
+LXC_IPV6 = np.array([0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x01, 0x01, 0x65,
+                     0x82, 0xbc], np.uint8)        # bpf/lxc_config.h LXC_IP
+ROUTER_IPV6 = np.array([0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 0],
+                       np.uint8)                   # bpf/node_config.h ROUTER_IP
+
+
+def mask_v6(addrs: np.ndarray, plen) -> np.ndarray:
+    """Clear the bits past plen of (m,16) network-order addresses
+    (ipv6_addr_clear_suffix, ipv6.h:140-150)."""
+    addrs = np.asarray(addrs, np.uint8).reshape(-1, 16)
+    plen = np.broadcast_to(np.asarray(plen, np.int64), (len(addrs),))
+    bit = np.arange(16)[None, :] * 8
+    keep = np.clip(plen[:, None] - bit, 0, 8)
+    m = (0xFF << (8 - keep)) & 0xFF
+    return (addrs & m.astype(np.uint8)).astype(np.uint8)
+
+
+def _v6_entries(addrs, plen, label):
+    n = len(addrs)
+    e = np.zeros(n, IPCACHE_DT)
+    e["family"] = 2
+    e["plen"] = plen
+    e["addr"] = mask_v6(addrs, plen)
+    e["label"] = label
+    return e
+
+
+def gen_ipcache_v6(rng, n, label_base=256, label_mod=16384,
+                   lengths=((32, .02), (40, .03), (48, .30), (56, .20),
+                            (64, .25), (96, .05), (128, .15))):
+    """C3 ipcache: n unique IPv6 prefixes, mass at /48, /56, /64 and /128
+    (SURVEY.md §8d), inside 2000::/4 and away from the node's beef::/16."""
+    ls = np.array([l for l, _ in lengths])
+    ps = np.array([p for _, p in lengths], dtype=np.float64)
+    ps /= ps.sum()
+    out_a, out_l, seen = [], [], set()
+    need = n
+    while need > 0:
+        m = int(need * 1.2) + 16
+        plen = rng.choice(ls, size=m, p=ps)
+        a = rng.integers(0, 256, size=(m, 16), dtype=np.uint16).astype(np.uint8)
+        a[:, 0] = 0x20 | (a[:, 0] & 0x0F)
+        a = mask_v6(a, plen)
+        for row, l in zip(a, plen.tolist()):
+            k = (row.tobytes(), l)
+            if k in seen:
+                continue
+            seen.add(k)
+            out_a.append(row)
+            out_l.append(l)
+            need -= 1
+            if need == 0:
+                break
+    addrs = np.stack(out_a)
+    label = (label_base + (np.arange(n) % label_mod)).astype(np.uint32)
+    return _v6_entries(addrs, np.array(out_l, np.uint8), label)
+
+
+def endpoint_v6(addr16, ifindex, lxc_id, flags=0):
+    e = np.zeros(1, ENDPOINT_DT)
+    e["family"] = 2
+    e["addr"][0] = np.asarray(addr16, np.uint8)
+    e["ifindex"] = ifindex
+    e["lxc_id"] = lxc_id
+    e["flags"] = flags
+    return e
+
+
+def _addr_in_prefix_v6(rng, ipc, idx):
+    base = ipc["addr"][idx]
+    plen = ipc["plen"][idx].astype(np.int64)
+    rnd = rng.integers(0, 256, size=(len(idx), 16), dtype=np.uint16).astype(np.uint8)
+    host = rnd & ~mask_v6(np.full((len(idx), 16), 0xFF, np.uint8), plen)
+    return (base | host).astype(np.uint8)
+
+
+ICMP6_TYPES = np.array([128, 128, 129, 1, 3, 136], np.uint32)
+
+
+def gen_headers_v6(rng, n, ipc, dst_addrs, in_prefix=0.9, local_frac=0.97,
+                   ports=None, ext=0.01, exthdr_drop=0.005,
+                   mark_host=0.03, mark_proxy=0.02, other_proto=0.005,
+                   proxy_ident=None, src_fixed=None, icmp_types=ICMP6_TYPES):
+    """IPv6 header batch, the C3 analogue of gen_headers_v4.  `proto` is the
+    next header ipv6_hdrlen() stops at: a fraction `exthdr_drop` stops at
+    FRAGMENT (44) or NONE (59), which the datapath drops."""
+    ports = PORT_SET if ports is None else ports
+    if src_fixed is not None:
+        saddr = np.tile(np.asarray(src_fixed, np.uint8), (n, 1))
+    else:
+        pick = rng.integers(0, len(ipc), size=n)
+        saddr = _addr_in_prefix_v6(rng, ipc, pick)
+        uni = rng.random(n) >= in_prefix
+        saddr[uni] = rng.integers(0, 256, size=(int(uni.sum()), 16),
+                                  dtype=np.uint16).astype(np.uint8)
+    dst_addrs = np.asarray(dst_addrs, np.uint8).reshape(-1, 16)
+    daddr = dst_addrs[rng.integers(0, len(dst_addrs), size=n)].copy()
+    nonlocal_ = rng.random(n) >= local_frac
+    daddr[nonlocal_] = rng.integers(0, 256, size=(int(nonlocal_.sum()), 16),
+                                    dtype=np.uint16).astype(np.uint8)
+    r = rng.random(n)
+    proto = np.where(r < 0.70, IPPROTO_TCP,
+                     np.where(r < 0.95, IPPROTO_UDP, IPPROTO_ICMPV6)).astype(np.uint8)
+    oth = rng.random(n) < other_proto
+    proto[oth] = rng.choice(np.array([47, 132, 50], np.uint8), size=int(oth.sum()))
+    dr = rng.random(n) < exthdr_drop
+    proto[dr] = rng.choice(np.array([44, 59], np.uint8), size=int(dr.sum()))
+    dp = np.where(rng.random(n) < 0.6, rng.choice(ports, size=n),
+                  rng.integers(1, 65536, size=n)).astype(np.uint32)
+    sp = rng.integers(32768, 65536, size=n).astype(np.uint32)
+    sport, dport = htons(sp), htons(dp)
+    icmp = proto == IPPROTO_ICMPV6
+    sport[icmp] = rng.choice(np.asarray(icmp_types, np.uint32),
+                             size=int(icmp.sum())).astype(np.uint16)
+    dport[icmp] = rng.integers(0, 65536, size=int(icmp.sum())).astype(np.uint16)
+    flags = np.zeros(n, np.uint8)
+    flags[rng.random(n) < ext] |= HF_EXTHDR
+    tcp = proto == IPPROTO_TCP
+    flags[tcp & (rng.random(n) < 0.02)] |= HF_TCP_CLOSE
+    length = rng.integers(100, 1501, size=n).astype(np.uint16)
+    mark = np.zeros(n, np.uint32)
+    rm = rng.random(n)
+    mark[rm < mark_host] = 0xC00
+    if proxy_ident is not None and len(proxy_ident):
+        sel = (rm >= mark_host) & (rm < mark_host + mark_proxy)
+        ids = rng.choice(np.asarray(proxy_ident, np.uint32), size=int(sel.sum()))
+        magic = np.where(rng.random(int(sel.sum())) < 0.5, 0xA00, 0xB00)
+        mark[sel] = ((ids & 0xFFFF) << 16) | ((ids >> 16) & 0xFF) | magic
+    return Headers(6, saddr, daddr, sport, dport, proto, flags, length, mark)
+
+
+def local_v6_addrs(t: Tables):
+    e = t.endpoints[t.endpoints["family"] == 2]
+    return e["addr"].copy()
+
+
+def config_c3(seed=3, n_prefixes=1_000_000, n_v4_prefixes=100_000,
+              n_policy=16384, n_endpoints=1, n_prefilter=50_000):
+    """C3 (dual stack): 1M IPv6 /32-/128 ipcache prefixes next to C2's IPv4
+    ones, endpoints with both addresses, and a 50k-entry prefilter (half v4
+    /32, half v6 /128 exact entries)."""
+    t = config_c2(seed, n_prefixes=n_v4_prefixes, n_policy=n_policy,
+                  n_endpoints=n_endpoints)
+    rng = np.random.default_rng(seed + 77)
+    ipc6 = gen_ipcache_v6(rng, n_prefixes)
+    t.ipcache = np.concatenate([t.ipcache, ipc6])
+    eps = [endpoint_v6(LXC_IPV6, 100, EP_LXC_ID)]
+    for i in range(1, n_endpoints):
+        a = LXC_IPV6.copy()
+        a[12:] = [0, 0, i >> 8, i & 255]
+        eps.append(endpoint_v6(a, 100 + i, EP_LXC_ID + i))
+    host = LXC_IPV6.copy()
+    host[12:] = [0xff, 0xff, 0xff, 0xfe]
+    eps.append(endpoint_v6(host, 0, 0xFFF0, flags=1))
+    t.endpoints = np.concatenate([t.endpoints] + eps)
+    half = n_prefilter // 2
+    pf = np.zeros(n_prefilter, PREFILTER_DT)
+    v4 = np.unique(rng.integers(1 << 24, 224 << 24, size=half,
+                                dtype=np.uint64).astype(np.uint32))
+    pf = pf[:len(v4) + (n_prefilter - half)]
+    pf["family"][:len(v4)] = 1
+    pf["plen"][:len(v4)] = 32
+    pf["addr"][:len(v4), :4] = be32_to_bytes(byteswap32(v4))
+    a6 = rng.integers(0, 256, size=(n_prefilter - half, 16),
+                      dtype=np.uint16).astype(np.uint8)
+    a6[:, 0] = 0x20 | (a6[:, 0] & 0x0F)
+    pf["family"][len(v4):] = 2
+    pf["plen"][len(v4):] = 128
+    pf["addr"][len(v4):] = a6
+    t.prefilter = pf
+    return t
+
+
+def headers_c3(t: Tables, n, seed=3, **kw):
+    rng = np.random.default_rng(seed + 3000)
+    ipc6 = t.ipcache[t.ipcache["family"] == 2]
+    return gen_headers_v6(rng, n, ipc6, local_v6_addrs(t),
+                          proxy_ident=proxy_identities(t), **kw)
 
 
 def endpoint_v4(addr_be32, ifindex, lxc_id, flags=0):
@@ -270,7 +458,11 @@ def ensure_no_reverse(h: Headers):
     reverse packets').  Returns a boolean keep-mask."""
     fwd = {}
     keep = np.ones(len(h), bool)
-    s, d = h.saddr.tolist(), h.daddr.tolist()
+    if h.saddr.ndim == 2:    # IPv6: (n, 16) bytes
+        s = [bytes(a) for a in h.saddr]
+        d = [bytes(a) for a in h.daddr]
+    else:
+        s, d = h.saddr.tolist(), h.daddr.tolist()
     sp, dp, pr = h.sport.tolist(), h.dport.tolist(), h.proto.tolist()
     for i in range(len(h)):
         if (d[i], s[i], dp[i], sp[i], pr[i]) in fwd:

@@ -460,12 +460,17 @@ typedef struct {
     uint32_t identity;
 } res_t;
 
+static int ct6_new_dport(uint8_t proto, uint16_t sport, uint16_t dport,
+                         uint16_t *dp);
+
 /* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
- * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src. */
-static res_t lxc_ingress_v4(cfo_t *o, const epinfo *ep, uint32_t src,
-                            uint8_t proto, uint16_t sport, uint16_t dport,
-                            int frag, uint32_t len, int skip_proxy,
-                            int dir_missed)
+ * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src; with
+ * v6 set, ipv6_policy (:753-882) + tail_ipv6_policy (:884-895), which differ
+ * only in the CT port derivation and pass is_fragment = false. */
+static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src,
+                         uint8_t proto, uint16_t sport, uint16_t dport,
+                         int frag, uint32_t len, int skip_proxy,
+                         int dir_missed, int v6)
 {
     res_t r = {TC_ACT_SHOT, 0, src};
     if (!o->pol[ep->lxc_id]) {
@@ -477,7 +482,8 @@ static res_t lxc_ingress_v4(cfo_t *o, const epinfo *ep, uint32_t src,
         return r;
     }
     uint16_t pdport;
-    int ret = ct_new_dport(proto, sport, dport, &pdport);
+    int ret = v6 ? ct6_new_dport(proto, sport, dport, &pdport)
+                 : ct_new_dport(proto, sport, dport, &pdport);
     if (ret < 0) {
         r.verdict = ret;
         metric(o, ret, METRIC_INGRESS, len);
@@ -503,21 +509,25 @@ static res_t lxc_ingress_v4(cfo_t *o, const epinfo *ep, uint32_t src,
     return r;
 }
 
+/* handle_identity_from_host (bpf_netdev.c:128-153) */
+static uint32_t identity_from_mark(uint32_t mark, int *skip_proxy)
+{
+    uint32_t magic = mark & MARK_MAGIC_HOST_MASK;
+    *skip_proxy = 0;
+    if (magic == MARK_MAGIC_PROXY_INGRESS || magic == MARK_MAGIC_PROXY_EGRESS) {
+        *skip_proxy = magic == MARK_MAGIC_PROXY_INGRESS;
+        return ((mark & 0xFF) << 16) | (mark >> 16);
+    }
+    return magic == MARK_MAGIC_HOST ? HOST_ID : WORLD_ID;
+}
+
 /* from_netdev (FROM_HOST) -> handle_ipv4 (bpf_netdev.c:128-153, 357-453) */
 static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
                                uint8_t proto, uint16_t sport, uint16_t dport,
                                int frag, uint32_t len, uint32_t mark)
 {
-    uint32_t identity, magic = mark & MARK_MAGIC_HOST_MASK;
-    int skip_proxy = 0;
-    if (magic == MARK_MAGIC_PROXY_INGRESS || magic == MARK_MAGIC_PROXY_EGRESS) {
-        identity = ((mark & 0xFF) << 16) | (mark >> 16);
-        skip_proxy = magic == MARK_MAGIC_PROXY_INGRESS;
-    } else if (magic == MARK_MAGIC_HOST) {
-        identity = HOST_ID;
-    } else {
-        identity = WORLD_ID;
-    }
+    int skip_proxy;
+    uint32_t identity = identity_from_mark(mark, &skip_proxy);
     if (identity < HEALTH_ID) { /* identity_is_reserved, policy.h:41-44 */
         uint32_t label;
         tl_lookups++;
@@ -530,8 +540,8 @@ static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
     const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
     if (!ep || (ep->flags & ENDPOINT_F_HOST))
         return r; /* to the stack (tunnel endpoints out of scope) */
-    return lxc_ingress_v4(o, ep, identity, proto, sport, dport, frag, len,
-                          skip_proxy, METRIC_INGRESS);
+    return lxc_ingress(o, ep, identity, proto, sport, dport, frag, len,
+                       skip_proxy, METRIC_INGRESS, 0);
 }
 
 /* handle_ipv4_from_lxc (bpf_lxc.c:440-692) for endpoint lxc */
@@ -585,8 +595,8 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         /* ipv4_local_delivery (l3.h:103-131): egress forward metric, then
          * the destination's policy program with src = SECLABEL */
         metric(o, 0, METRIC_EGRESS, len);
-        res_t d = lxc_ingress_v4(o, ep, o->seclabel[lxc], proto, sport, dport,
-                                 frag, len, 0, METRIC_EGRESS);
+        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], proto, sport, dport,
+                              frag, len, 0, METRIC_EGRESS, 0);
         d.identity = dst;
         return d;
     }
@@ -649,6 +659,218 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             r = netdev_ingress_v4(o, saddr[i], daddr[i], proto[i], sport[i],
                                   dport[i], flags[i] & HF_FRAG, len[i],
                                   mark ? mark[i] : 0);
+        action[i] = r.action;
+        verdict[i] = r.verdict;
+        identity[i] = r.identity;
+        if (lookups)
+            lookups[i] = (uint8_t)tl_lookups;
+    }
+}
+
+/* ------------------------------------------------------------ IPv6 */
+#define DROP_INVALID_EXTHDR -156
+#define IPPROTO_ICMPV6 58
+#define NEXTHDR_FRAGMENT 44
+#define NEXTHDR_NONE 59
+#define HF_EXTHDR 4
+#define VERDICT_PUNT -2
+/* node_config.h:30 ROUTER_IP */
+static const uint8_t ROUTER_IP6[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0,
+                                       0, 0, 0, 1, 0, 1, 0, 0};
+
+/* tuple->dport of a CT_NEW ct_lookup6 (conntrack.h:339-400): TCP/UDP ports
+ * loaded swapped and swapped back by ipv6_ct_tuple_reverse(); an ICMPv6
+ * echo request puts its type (128) in tuple->sport, which becomes the dport;
+ * other ICMPv6 -> 0; anything else -> DROP_CT_UNKNOWN_PROTO. */
+static int ct6_new_dport(uint8_t proto, uint16_t sport, uint16_t dport,
+                         uint16_t *dp)
+{
+    switch (proto) {
+    case IPPROTO_ICMPV6:
+        *dp = (sport & 0xFF) == 128 ? 128 : 0;
+        return 0;
+    case 6:
+    case 17:
+        *dp = dport;
+        return 0;
+    default:
+        return DROP_CT_UNKNOWN_PROTO;
+    }
+}
+
+/* ipv6_hdrlen (ipv6.h:61-98): the header's proto is the next header the
+ * extension-header walk stops at; NONE and FRAGMENT end in a drop. */
+static int exthdr_drop(uint8_t proto)
+{
+    return proto == NEXTHDR_NONE ? DROP_INVALID_EXTHDR
+           : proto == NEXTHDR_FRAGMENT ? DROP_FRAG_NOSUPPORT : 0;
+}
+
+/* icmp6_handle (icmp6.h:390-412) answers neighbour solicitations and echo
+ * requests to the router itself; those headers are reported as punted.  It
+ * reads the type right after the fixed header, so behind extension headers
+ * it sees the next-header byte and never triggers. */
+static int icmp6_punt(uint8_t proto, uint8_t flags, uint16_t sport,
+                      const uint8_t *daddr)
+{
+    if (proto != IPPROTO_ICMPV6 || (flags & HF_EXTHDR))
+        return 0;
+    uint8_t type = (uint8_t)(sport & 0xFF);
+    return type == 135 || (type == 128 && !memcmp(daddr, ROUTER_IP6, 16));
+}
+
+/* from_netdev (FROM_HOST) -> handle_ipv6 (bpf_netdev.c:172-275, 494-503) */
+static res_t netdev_ingress_v6(cfo_t *o, const uint8_t *saddr,
+                               const uint8_t *daddr, uint8_t proto,
+                               uint16_t sport, uint16_t dport, uint8_t flags,
+                               uint32_t len, uint32_t mark)
+{
+    int skip_proxy;
+    uint32_t identity = identity_from_mark(mark, &skip_proxy);
+    res_t r = {TC_ACT_SHOT, 0, 0};
+    int ret = exthdr_drop(proto);
+    if (ret) { /* send_drop_notify_error(skb, ret, TC_ACT_SHOT, INGRESS) */
+        r.verdict = ret;
+        metric(o, ret, METRIC_INGRESS, len);
+        return r;
+    }
+    if (icmp6_punt(proto, flags, sport, daddr)) {
+        r.action = TC_ACT_OK;
+        r.verdict = VERDICT_PUNT;
+        return r;
+    }
+    if (identity < HEALTH_ID) { /* :203-213, no HOST_ID exclusion for v6 */
+        uint32_t label;
+        tl_lookups++;
+        if (lpm_lookup(&o->ipc6, saddr, &label) && label && label != CLUSTER_ID)
+            identity = label;
+    }
+    r.action = TC_ACT_OK;
+    r.identity = identity;
+    tl_lookups++;
+    const epinfo *ep = lxc_lookup(o, 2, daddr);
+    if (!ep || (ep->flags & ENDPOINT_F_HOST))
+        return r;
+    return lxc_ingress(o, ep, identity, proto, sport, dport, 0, len,
+                       skip_proxy, METRIC_INGRESS, 1);
+}
+
+/* from-container -> handle_ipv6 -> ipv6_l3_from_lxc (bpf_lxc.c:112-436) */
+static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
+                           const uint8_t *daddr, uint8_t proto, uint16_t sport,
+                           uint16_t dport, uint8_t flags, uint32_t len)
+{
+    res_t r = {TC_ACT_SHOT, 0, 0};
+    if (icmp6_punt(proto, flags, sport, daddr)) { /* :411-419 */
+        r.action = TC_ACT_OK;
+        r.verdict = VERDICT_PUNT;
+        return r;
+    }
+    const epinfo *self = lxc_lookup(o, 2, saddr);
+    if (!self || self->lxc_id != lxc) { /* is_valid_lxc_src_ip, lxc.h:46 */
+        r.verdict = DROP_INVALID_SIP;
+        metric(o, DROP_INVALID_SIP, METRIC_EGRESS, len);
+        return r;
+    }
+    int ret = exthdr_drop(proto);
+    if (!ret) {
+        uint16_t pdport;
+        ret = ct6_new_dport(proto, sport, dport, &pdport);
+        if (!ret) {
+            uint32_t label = 0, dst;
+            tl_lookups++;
+            if (lpm_lookup(&o->ipc6, daddr, &label) && label)
+                dst = label;
+            else if (!memcmp(daddr, ROUTER_IP6, 8)) /* ipv6_match_prefix_64 */
+                dst = CLUSTER_ID;
+            else
+                dst = WORLD_ID;
+            r.identity = dst;
+            int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
+                                            CT_EGRESS, 0, len);
+            if (verdict < 0) {
+                r.verdict = DROP_POLICY;
+                metric(o, DROP_POLICY, METRIC_EGRESS, len);
+                return r;
+            }
+            if (verdict > 0) {
+                r.action = TC_ACT_REDIRECT;
+                r.verdict = verdict;
+                return r;
+            }
+            tl_lookups++;
+            const epinfo *ep = lxc_lookup(o, 2, daddr);
+            metric(o, 0, METRIC_EGRESS, len); /* to_host / local / to_stack */
+            if (ep) {
+                if (ep->flags & ENDPOINT_F_HOST) {
+                    r.action = TC_ACT_REDIRECT;
+                    return r;
+                }
+                res_t d = lxc_ingress(o, ep, o->seclabel[lxc], proto, sport,
+                                      dport, 0, len, 0, METRIC_EGRESS, 1);
+                d.identity = dst;
+                return d;
+            }
+            r.action = TC_ACT_OK;
+            return r;
+        }
+    }
+    r.verdict = ret;
+    metric(o, ret, METRIC_EGRESS, len);
+    return r;
+}
+
+/* check_v6 (bpf_xdp.c:132-156) */
+static int xdp_v6(cfo_t *o, const uint8_t *saddr, const uint8_t *daddr)
+{
+    uint32_t v;
+    if (o->pf6_dyn.nlens)
+        tl_lookups++;
+    if (lpm_lookup(&o->pf6_dyn, saddr, &v))
+        return XDP_DROP;
+    uint8_t k[20];
+    uint32_t pl = 128;
+    memcpy(k, &pl, 4);
+    memcpy(k + 4, saddr, 16);
+    tl_lookups++;
+    if (ht_get(&o->pf6_fix, k, &v))
+        return XDP_DROP;
+    tl_lookups++;
+    return lxc_lookup(o, 2, daddr) ? XDP_PASS : XDP_DROP;
+}
+
+void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint8_t *saddr, const uint8_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *mark,
+                     int32_t *action, int32_t *verdict, uint32_t *identity,
+                     uint8_t *lookups, int nthreads)
+{
+    if (nthreads <= 0)
+        nthreads = 1;
+#pragma omp parallel for schedule(static, 4096) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        res_t r;
+        const uint8_t *sa = saddr + 16 * i, *da = daddr + 16 * i;
+        tl_lookups = 0;
+        if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
+            int x = xdp_v6(o, sa, da);
+            if (mode == CFO_MODE_XDP || x == XDP_DROP) {
+                action[i] = x;
+                verdict[i] = x == XDP_PASS ? 0 : -1;
+                identity[i] = 0;
+                if (lookups)
+                    lookups[i] = (uint8_t)tl_lookups;
+                continue;
+            }
+        }
+        if (mode == CFO_MODE_EGRESS)
+            r = lxc_egress_v6(o, ep_lxc, sa, da, proto[i], sport[i], dport[i],
+                              flags[i], len[i]);
+        else
+            r = netdev_ingress_v6(o, sa, da, proto[i], sport[i], dport[i],
+                                  flags[i], len[i], mark ? mark[i] : 0);
         action[i] = r.action;
         verdict[i] = r.verdict;
         identity[i] = r.identity;

@@ -61,6 +61,19 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
                      uint8_t *lookups, int nthreads);
 
+/* The same for IPv6: saddr/daddr are n x 16 raw address bytes; proto is the
+ * next header ipv6_hdrlen() stops at (44 / 59 drop); flags bit 2 (4) marks
+ * extension headers in front of it.  ICMPv6 neighbour solicitations and echo
+ * requests to ROUTER_IP, which the datapath answers itself
+ * (icmp6.h:390-412), come back as verdict -2 (punted). */
+void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint8_t *saddr, const uint8_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *mark,
+                     int32_t *action, int32_t *verdict, uint32_t *identity,
+                     uint8_t *lookups, int nthreads);
+
 /* rows of 7 u64: identity, dport, proto, egress, proxy_port, packets, bytes
  * (sorted); returns the number of rows (writes at most cap). */
 size_t cfo_policy_dump(cfo_t *o, uint16_t lxc_id, uint64_t *rows, size_t cap);

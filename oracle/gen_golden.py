@@ -73,6 +73,40 @@ def build_packet_v4(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
     return pkt + bytes(L - len(pkt))
 
 
+def build_packet_v6(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
+    """Ethernet + IPv6 (+ one 8-byte destination-options header when
+    HF_EXTHDR) + L4; `proto` is the next header after the extension headers
+    (44 / 59 produce the fragment / no-next-header drops)."""
+    proto = int(h.proto[i])
+    L = int(h.length[i])
+    ext = bool(h.flags[i] & S.HF_EXTHDR)
+    sp, dp = int(h.sport[i]), int(h.dport[i])
+    if proto == S.IPPROTO_TCP:
+        fl = 0x11 if (h.flags[i] & S.HF_TCP_CLOSE) else 0x02
+        l4 = struct.pack("<HH", sp, dp) + struct.pack(">IIBBHHH", 1, 0, 0x50,
+                                                       fl, 1024, 0, 0)
+    elif proto == S.IPPROTO_UDP:
+        l4 = struct.pack("<HH", sp, dp) + struct.pack(">HH", 8, 0)
+    elif proto == 59:
+        l4 = b""
+    else:   # ICMPv6 (type/code in the sport word, csum in dport), others
+        l4 = struct.pack("<HH", sp, dp) + b"\x00" * 4
+    eh = bytes([proto, 0, 1, 4, 0, 0, 0, 0]) if ext else b""   # PadN option
+    payload = eh + l4
+    first = 60 if ext else proto
+    ip = struct.pack(">IHBB", 0x60000000, L - 54, first, 64)
+    ip += bytes(h.saddr[i]) + bytes(h.daddr[i])
+    pkt = eth_dst + eth_src + b"\x86\xdd" + ip + payload
+    assert len(pkt) <= L, (len(pkt), L)
+    return pkt + bytes(L - len(pkt))
+
+
+def l4_offset(h, i):
+    if h.family == 4:
+        return 14 + 20
+    return 14 + 40 + (8 if h.flags[i] & S.HF_EXTHDR else 0)
+
+
 # ------------------------------------------------------------ datapath
 def u32(x):
     return struct.pack("<I", x)
@@ -116,8 +150,9 @@ class RefDatapath:
         self.policy_map = {}
         for k, e in enumerate(t.endpoints):
             lxc = int(e["lxc_id"])
-            if int(e["flags"]) & 1 or lxc not in t.policy:
-                continue   # host entry, or an endpoint without a program
+            if int(e["flags"]) & 1 or lxc not in t.policy or lxc in self.ep_prog:
+                continue   # host entry, an endpoint without a program, or
+                           # the second address of a dual-stack endpoint
             rn = {"cilium_calls_111": f"calls_lxc{k}",
                   "cilium_policy_foo": f"policy{k}"}
             for ct in ("cilium_ct_tcp4_111", "cilium_ct_any4_111",
@@ -125,7 +160,7 @@ class RefDatapath:
                 rn[ct] = f"{ct}_{k}"
             pol = L.load("bpf_lxc.o", "1/0x1010", SC, rn)
             calls = {}
-            for sec, idx in (("2/11", 11), ("2/7", 7)):
+            for sec, idx in (("2/11", 11), ("2/7", 7), ("2/12", 12), ("2/10", 10)):
                 calls[idx] = L.load("bpf_lxc.o", sec, SC, rn)
             egress = L.load("bpf_lxc.o", "from-container", SC, rn)
             for idx, fd in calls.items():
@@ -186,8 +221,8 @@ class RefDatapath:
 
 
 # ------------------------------------------------------------ run + derive
-def _dport_out(pkt_out):
-    return struct.unpack_from("<H", pkt_out, 14 + 20 + 2)[0]
+def _dport_out(pkt_out, off=14 + 20):
+    return struct.unpack_from("<H", pkt_out, off + 2)[0]
 
 
 def _derive_ingress(h, i, ret, cb, pkt_out):
@@ -196,13 +231,15 @@ def _derive_ingress(h, i, ret, cb, pkt_out):
         # send_drop_notify(skb, src_label, SECLABEL, LXC_ID, ...):
         # cb[1] = src << 16 | dst & 0xFFFF, cb[2] = reason (drop.h:94-102).
         # A missed tail call is reported by the netdev program with src 0.
-        if cb[2] == -140:
+        if cb[2] in (-140, -156, -157):
+            # errors of the netdev program itself (send_drop_notify_error:
+            # no identities recorded)
             return ret, cb[2], 0, 0
         return ret, cb[2], (cb[1] >> 16) & 0xFFFF, 0xFFFF
     if ret == TC_ACT_REDIRECT:
         # proxy redirect rewrote the dport (lxc.h:118) and set
         # cb[CB_IFINDEX] = HOST_IFINDEX (bpf_lxc.c:1004)
-        v = _dport_out(pkt_out) if cb[1] == HOST_IFINDEX else 0
+        v = _dport_out(pkt_out, l4_offset(h, i)) if cb[1] == HOST_IFINDEX else 0
         return ret, v, cb[0] & 0xFFFFFFFF, 0xFFFFFFFF
     # TC_ACT_OK: non-local / host endpoint: identity not observable
     return ret, 0, 0, 0
@@ -216,7 +253,7 @@ def _derive_egress(h, i, ret, cb, pkt_out):
         # dropped by the destination endpoint's ingress policy
         return ret, cb[2], 0, 0
     if ret == TC_ACT_REDIRECT:
-        dp = _dport_out(pkt_out)
+        dp = _dport_out(pkt_out, l4_offset(h, i))
         v = dp if dp != int(h.dport[i]) else 0
         return ret, v, 0, 0
     return ret, 0, 0, 0
@@ -228,20 +265,21 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     verdict = np.zeros(n, np.int32)
     ident = np.zeros(n, np.uint32)
     idmask = np.zeros(n, np.uint32)
+    build = build_packet_v4 if h.family == 4 else build_packet_v6
     for i in range(n):
         if mode in (MODE_XDP, MODE_FULL):
-            ret = H.test_run_xdp(dp.xdp, build_packet_v4(h, i))
+            ret = H.test_run_xdp(dp.xdp, build(h, i))
             if mode == MODE_XDP or ret == XDP_DROP:
                 action[i] = ret
                 verdict[i] = 0 if ret == XDP_PASS else -1
                 continue
         if mode in (MODE_INGRESS, MODE_FULL):
-            ret, cb, po = H.test_run_skb(dp.netdev, build_packet_v4(h, i),
+            ret, cb, po = H.test_run_skb(dp.netdev, build(h, i),
                                          mark=int(h.mark[i]))
             r = _derive_ingress(h, i, ret, cb, po)
         else:
             ret, cb, po = H.test_run_skb(
-                dp.ep_prog[ep_lxc], build_packet_v4(h, i, LXC_MAC, NODE_MAC))
+                dp.ep_prog[ep_lxc], build(h, i, LXC_MAC, NODE_MAC))
             r = _derive_egress(h, i, ret, cb, po)
         action[i], verdict[i], ident[i], idmask[i] = r
     return action, verdict, ident, idmask
@@ -440,6 +478,166 @@ def sc_empty(n=2000, seed=5):
     return t, h, MODE_INGRESS, None
 
 
+# ------------------------------------------------------------ IPv6 scenarios
+def _v6(*specs):
+    """[(addr string, plen, label), ...] -> ipcache entries"""
+    return np.concatenate([S._v6_entries(S.ip6(a)[None, :], [l], [lab])
+                           for a, l, lab in specs])
+
+
+def sc_edge_ingress_v6(seed=8):
+    """The IPv6 fallback cases: L4 / L3 / wildcard-port hits, ICMPv6 (echo
+    request -> port 128, other types -> 0), extension headers, the
+    FRAGMENT / NONE next-header drops, unknown protocols, the identity
+    override rule (label 0/CLUSTER ignored) and the marks."""
+    ipc = _v6(("2001:db8::", 32, 1000), ("2001:db8:5::", 48, 1001),
+              ("2001:db8:5:8000::", 49, 0), ("2001:db8:6::", 48, S.HOST_ID),
+              ("2001:db8:7::", 48, S.CLUSTER_ID), ("2001:db8:8::8", 128, 4242),
+              ("::", 0, 7), ("fd00::", 16, 0x80000001),
+              ("2001:db8:9::", 64, 70000))
+    host = S.LXC_IPV6.copy()
+    host[12:] = [0xff, 0xff, 0xff, 0xfe]
+    eps = np.concatenate([S.endpoint_v6(S.LXC_IPV6, 100, S.EP_LXC_ID),
+                          S.endpoint_v6(host, 0, 0xFFF0, 1)])
+    ht = lambda p: int(S.htons(p))   # noqa: E731
+    rows = [(1000, ht(80), 6, 0, 0), (1000, ht(53), 17, 0, 0),
+            (1001, 0, 0, 0, 0), (4242, ht(443), 6, 0, ht(10001)),
+            (0, ht(8080), 6, 0, 0), (0, ht(9090), 6, 0, ht(10002)),
+            (7, 0, 0, 0, 0), (1000, 128, 58, 0, 0), (1001, 0x8000, 58, 0, 0),
+            (4242, 0, 58, 0, 0), (S.WORLD_ID, ht(22), 6, 0, 0),
+            (S.HOST_ID, 0, 0, 0, 0), (0x80000001, ht(80), 6, 0, 0),
+            (1000, ht(80), 6, 1, 0), (70000, ht(22), 6, 0, ht(10003)),
+            (1001, ht(80), 6, 0, ht(10003)), (1000, 0, 132, 0, 0)]
+    pol = np.zeros(len(rows), S.POLICY_DT)
+    a = np.array(rows, dtype=np.int64)
+    pol["identity"], pol["dport"], pol["proto"] = a[:, 0], a[:, 1], a[:, 2]
+    pol["egress"], pol["proxy_port"] = a[:, 3], a[:, 4]
+    t = S.Tables(ipc, eps, {S.EP_LXC_ID: pol}, np.zeros(0, S.PREFILTER_DT),
+                 {S.EP_LXC_ID: S.EP_SECLABEL, 0xFFF0: S.EP_SECLABEL})
+    srcs = ["2001:db8:1::1", "2001:db8:5::9", "2001:db8:5:8000::1",
+            "2001:db8:6::1", "2001:db8:7::1", "2001:db8:8::8", "3fff::1",
+            "fd00:1::4", "2001:db8:9::77", "::"]
+    dsts = [S.LXC_IPV6, host, S.ip6("2001:db8:ffff::1")]
+    cases = []
+    for si, sa in enumerate(srcs):
+        for d in dsts:
+            for proto, sp, dp in ((6, 40000, 80), (6, 40001, 443), (6, 40002, 8080),
+                                  (6, 40003, 9090), (6, 40004, 22), (17, 40005, 53),
+                                  (17, 40006, 80), (58, 128, 0x1234),
+                                  (58, 129, 0x77), (58, 1, 0), (58, 3, 0),
+                                  (58, 136, 0), (47, 0, 0), (132, 1, 2),
+                                  (44, 0, 0), (59, 0, 0)):
+                for fl in (0, S.HF_EXTHDR, S.HF_TCP_CLOSE):
+                    for mark in (0, 0xC00, 0xA00 | (4242 & 0xFFFF) << 16,
+                                 0xB00 | (70000 & 0xFFFF) << 16 | (70000 >> 16),
+                                 0xB00 | (3 << 16)):
+                        cases.append((S.ip6(sa), d, proto, sp, dp, fl, mark))
+    n = len(cases)
+    rng = np.random.default_rng(seed)
+    raw = lambda c: c[2] in (58, 44, 59, 47)   # noqa: E731  (no port swap)
+    h = S.Headers(6, np.stack([c[0] for c in cases]).astype(np.uint8),
+                  np.stack([np.asarray(c[1], np.uint8) for c in cases]),
+                  np.array([c[3] if raw(c) else ht(c[3]) for c in cases], np.uint16),
+                  np.array([c[4] if raw(c) else ht(c[4]) for c in cases], np.uint16),
+                  np.array([c[2] for c in cases], np.uint8),
+                  np.array([c[5] for c in cases], np.uint8),
+                  rng.integers(100, 300, size=n).astype(np.uint16),
+                  np.array([c[6] for c in cases], np.uint32))
+    tcpudp = (h.proto == 6) | (h.proto == 17)
+    h.sport[tcpudp] = S.htons(20000 + np.arange(n)[tcpudp] % 40000)
+    return t, h, MODE_INGRESS, None
+
+
+def sc_c3_ingress(n=20000, seed=3):
+    t = S.config_c3(seed, n_prefixes=100_000, n_v4_prefixes=20_000,
+                    n_policy=16384, n_prefilter=0)
+    h = S.headers_c3(t, int(n * 1.02), seed=seed, ext=0.05, exthdr_drop=0.01,
+                     local_frac=0.9)
+    h = _keep(h, S.ensure_no_reverse(h)).slice(0, n)
+    return t, h, MODE_INGRESS, None
+
+
+def sc_c3_egress(n=20000, seed=9):
+    t = S.config_c3(seed, n_prefixes=100_000, n_v4_prefixes=20_000,
+                    n_policy=16384, n_endpoints=2, n_prefilter=0)
+    rng = np.random.default_rng(seed + 7)
+    ipc6 = t.ipcache[t.ipcache["family"] == 2]
+    loc = S.local_v6_addrs(t)
+    h = S.gen_headers_v6(rng, n, ipc6, loc, local_frac=1.0, mark_host=0,
+                         mark_proxy=0, src_fixed=S.LXC_IPV6, ext=0.05)
+    dst = S._addr_in_prefix_v6(rng, ipc6, rng.integers(0, len(ipc6), size=n))
+    r = rng.random(n)
+    sel_loc = (r >= 0.85) & (r < 0.93)
+    sel_rnd = r >= 0.93
+    d = dst.copy()
+    d[sel_loc] = loc[rng.integers(0, len(loc), size=int(sel_loc.sum()))]
+    d[sel_rnd] = rng.integers(0, 256, size=(int(sel_rnd.sum()), 16),
+                              dtype=np.uint16).astype(np.uint8)
+    # inside the router's /64 (match_prefix_64 -> CLUSTER_ID), never the
+    # router address itself (echo requests to it are answered, not routed)
+    cl = rng.random(n) < 0.03
+    d[cl, :8] = S.ROUTER_IPV6[:8]
+    d[cl, 8] = 0x80 | d[cl, 8]
+    h.daddr = d
+    spoof = rng.random(n) < 0.02
+    h.saddr[spoof] = S.ip6("2001:db8::dead")
+    h = _keep(h, S.ensure_no_reverse(h) & _no_related(h))
+    return t, h, MODE_EGRESS, S.EP_LXC_ID
+
+
+def _no_related(h):
+    """Drop ICMPv6 error messages (types 1-4) between an address pair that
+    already carried ICMPv6: ct_lookup6 looks them up as TUPLE_F_RELATED
+    (conntrack.h) and an earlier packet's entry would then skip policy —
+    state the per-batch oracle does not model."""
+    keep = np.ones(len(h), bool)
+    seen = set()
+    for i in range(len(h)):
+        if int(h.proto[i]) != S.IPPROTO_ICMPV6:
+            continue
+        pair = frozenset((bytes(h.saddr[i]), bytes(h.daddr[i])))
+        if 1 <= (int(h.sport[i]) & 0xFF) <= 4 and pair in seen:
+            keep[i] = False
+        seen.add(pair)
+    return keep
+
+
+def _prefilter_v6(rng, n_fix, n_dyn):
+    pf = np.zeros(n_fix + n_dyn, S.PREFILTER_DT)
+    pf["family"] = 2
+    a = rng.integers(0, 256, size=(n_fix + n_dyn, 16), dtype=np.uint16).astype(np.uint8)
+    a[:, 0] = 0x20 | (a[:, 0] & 0x0F)
+    pl = np.full(n_fix + n_dyn, 128)
+    pl[n_fix:] = rng.choice(np.array([16, 24, 32, 48, 56, 64, 96, 127, 128]),
+                            size=n_dyn)
+    pf["plen"] = pl
+    pf["addr"] = S.mask_v6(a, pl)
+    pf["dyn"][n_fix:] = 1
+    _, u = np.unique(np.concatenate([pf["dyn"][:, None], pf["plen"][:, None],
+                                     pf["addr"]], 1), axis=0, return_index=True)
+    return pf[np.sort(u)]
+
+
+def sc_xdp_v6(n=20000, seed=10, mode=MODE_XDP):
+    t = S.config_c3(seed, n_prefixes=20_000, n_v4_prefixes=5_000,
+                    n_policy=4096, n_prefilter=0)
+    rng = np.random.default_rng(seed + 11)
+    t.prefilter = np.concatenate([_prefilter_v4(rng, t.ipcache[t.ipcache["family"] == 1],
+                                                500, 50),
+                                  _prefilter_v6(rng, 5000, 300)])
+    h = S.headers_c3(t, n, seed=seed, local_frac=0.85, ext=0.05)
+    r = rng.random(n)
+    pf6 = t.prefilter[t.prefilter["family"] == 2]
+    fix, dyn = pf6[pf6["dyn"] == 0], pf6[pf6["dyn"] == 1]
+    sel = r < 0.25
+    h.saddr[sel] = fix["addr"][rng.integers(0, len(fix), size=int(sel.sum()))]
+    sel2 = (r >= 0.25) & (r < 0.4)
+    di = rng.integers(0, len(dyn), size=int(sel2.sum()))
+    h.saddr[sel2] = S._addr_in_prefix_v6(rng, dyn, di)
+    h = _keep(h, S.ensure_no_reverse(h))
+    return t, h, mode, None
+
+
 def _keep(h, m):
     return S.Headers(h.family, h.saddr[m], h.daddr[m], h.sport[m], h.dport[m],
                      h.proto[m], h.flags[m], h.length[m], h.mark[m])
@@ -453,6 +651,11 @@ SCENARIOS = {
     "xdp_v4": sc_xdp,
     "full_v4": lambda: sc_xdp(seed=6, mode=MODE_FULL),
     "empty_ingress_v4": sc_empty,
+    "edge_ingress_v6": sc_edge_ingress_v6,
+    "c3_ingress_v6": sc_c3_ingress,
+    "c3_egress_v6": sc_c3_egress,
+    "xdp_v6": sc_xdp_v6,
+    "full_v6": lambda: sc_xdp_v6(seed=12, mode=MODE_FULL),
 }
 
 

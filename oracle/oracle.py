@@ -42,6 +42,8 @@ def lib():
                                         ctypes.c_int]
         L.cfo_classify_v4.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
                                       ctypes.c_size_t] + [vp] * 12 + [ctypes.c_int]
+        L.cfo_classify_v6.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
+                                      ctypes.c_size_t] + [vp] * 12 + [ctypes.c_int]
         L.cfo_policy_create.argtypes = [vp, ctypes.c_uint16]
         L.cfo_policy_dump.restype = ctypes.c_size_t
         L.cfo_policy_dump.argtypes = [vp, ctypes.c_uint16, vp, ctypes.c_size_t]
@@ -105,14 +107,16 @@ class Oracle:
         ide = np.zeros(n, np.uint32)
         lk = np.zeros(n, np.uint8) if want_lookups else None
         c = np.ascontiguousarray
-        arrs = [c(hdr.saddr, np.uint32), c(hdr.daddr, np.uint32),
+        at = np.uint32 if hdr.family == 4 else np.uint8
+        arrs = [c(hdr.saddr, at), c(hdr.daddr, at),
                 c(hdr.sport, np.uint16), c(hdr.dport, np.uint16),
                 c(hdr.proto, np.uint8), c(hdr.flags, np.uint8),
                 c(hdr.length, np.uint16), c(hdr.mark, np.uint32)]
-        assert hdr.family == 4, "IPv6 oracle path not built yet"
-        self.L.cfo_classify_v4(self.h, mode, ep_lxc, n,
-                               *[_p(a) for a in arrs], _p(act), _p(ver),
-                               _p(ide), _p(lk), nthreads)
+        if hdr.family == 6:
+            assert arrs[0].shape == (n, 16) and arrs[1].shape == (n, 16)
+        fn = self.L.cfo_classify_v4 if hdr.family == 4 else self.L.cfo_classify_v6
+        fn(self.h, mode, ep_lxc, n, *[_p(a) for a in arrs], _p(act), _p(ver),
+           _p(ide), _p(lk), nthreads)
         if want_lookups:
             return act, ver, ide, lk
         return act, ver, ide

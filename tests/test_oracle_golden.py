@@ -11,7 +11,8 @@ NAMES = G.names()
 
 
 def test_have_goldens():
-    assert len(NAMES) >= 7, NAMES
+    assert len(NAMES) >= 12, NAMES
+    assert any(n.endswith("_v6") for n in NAMES)
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -35,5 +36,5 @@ def test_goldens_cover_every_outcome():
         seen |= {(int(a), int(v) if v <= 0 else 1)
                  for a, v in zip(g.action, g.verdict)}
     for want in [(7, 0), (7, 1), (0, 0), (2, -133), (2, -137), (2, -132),
-                 (1, -1), (2, 0)]:
+                 (1, -1), (2, 0), (2, -156), (2, -157)]:
         assert want in seen, want
