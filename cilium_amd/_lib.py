@@ -12,8 +12,8 @@ LIB_PATH = os.path.join(HERE, os.environ.get("CFC_LIB", "libcfc.so"))
 
 CFC_DEVICE_NONE = -1
 MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
-HF_FRAG, HF_TCP_CLOSE = 0x100, 0x200
-DROP_PREFILTER = -1
+HF_FRAG, HF_TCP_CLOSE, HF_EXTHDR = 0x100, 0x200, 0x400
+DROP_PREFILTER, VERDICT_PUNT = -1, -2
 OPT_LPM4, OPT_TIMING = 1, 2
 LPM4_AUTO, LPM4_DIR24_8, LPM4_TRIE = 0, 1, 2
 
@@ -25,7 +25,7 @@ EXPORTS = (
     "cfc_commit", "cfc_classify_v4", "cfc_counters_device",
     "cfc_counters_sync", "cfc_counters_clear", "cfc_counters_export",
     "cfc_counters_import", "cfc_get_stats", "cfc_strerror",
-    "cfc_set_option", "cfc_timing_collect",
+    "cfc_set_option", "cfc_timing_collect", "cfc_classify_v6",
 )
 
 
@@ -37,6 +37,10 @@ class HdrV4(ctypes.Structure):
     _fields_ = [("saddr", ctypes.c_void_p), ("daddr", ctypes.c_void_p),
                 ("ports", ctypes.c_void_p), ("meta", ctypes.c_void_p),
                 ("mark", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+
+
+class HdrV6(ctypes.Structure):
+    _fields_ = HdrV4._fields_
 
 
 class Out(ctypes.Structure):
@@ -53,7 +57,14 @@ class Stats(ctypes.Structure):
                 ("prefilter_v4_fix", ctypes.c_uint32),
                 ("prefilter_v4_dyn", ctypes.c_uint32),
                 ("lpm4_layout", ctypes.c_uint32),
-                ("lpm4_kib", ctypes.c_uint32)]
+                ("lpm4_kib", ctypes.c_uint32),
+                ("ipcache_v6_prefixes", ctypes.c_uint32),
+                ("lpm6_lengths", ctypes.c_uint32),
+                ("lpm6_groups", ctypes.c_uint32),
+                ("lpm6_kib", ctypes.c_uint32),
+                ("endpoints_v6", ctypes.c_uint32),
+                ("prefilter_v6_fix", ctypes.c_uint32),
+                ("prefilter_v6_dyn", ctypes.c_uint32)]
 
 
 class Timing(ctypes.Structure):
@@ -86,6 +97,8 @@ def lib():
     L.cfc_endpoint_config.argtypes = [vp, ctypes.c_uint16, u32]
     L.cfc_commit.argtypes = [vp, vp]
     L.cfc_classify_v4.argtypes = [vp, ctypes.POINTER(HdrV4), ctypes.POINTER(Out),
+                                  i32, ctypes.c_uint16, vp]
+    L.cfc_classify_v6.argtypes = [vp, ctypes.POINTER(HdrV6), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
     L.cfc_counters_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
     L.cfc_counters_sync.argtypes = [vp, vp]

@@ -55,7 +55,8 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 struct Epoch {
     uint64_t id = 0;
     DevBuf tbl24, tbl8, ovf, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
-        polbloom;
+        polbloom, lxc6;
+    DevBuf l6[3][3];   // ipc6 / pf6_fix / pf6_dyn: slots, bloom, lens
     DevTables T{};
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
@@ -167,6 +168,22 @@ int fold_counters(cfc_ctx *c, hipStream_t s)
     return 0;
 }
 
+int upload_lpm6(DevBuf *b, const Lpm6Host &h, Lpm6 *d, hipStream_t s)
+{
+    int rc;
+    if ((rc = upload_vec(b[0], h.slots, s)) || (rc = upload_vec(b[1], h.bloom, s)) ||
+        (rc = upload_vec(b[2], h.lens, s)))
+        return rc;
+    d->slots = (const L6Slot *)b[0].p;
+    d->bloom = (const uint64_t *)b[1].p;
+    d->lens = (const uint32_t *)b[2].p;
+    d->mask = h.slots.empty() ? 0 : (uint32_t)h.slots.size() - 1;
+    d->bloom_mask = h.bloom.empty() ? 0 : (uint32_t)h.bloom.size() - 1;
+    d->nlen = (uint32_t)h.lens.size();
+    d->def_label = h.def_label;
+    return 0;
+}
+
 int commit_locked(cfc_ctx *c, hipStream_t s)
 {
     uint64_t sig = tables_sig(c);
@@ -190,9 +207,16 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
         (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
         (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)) ||
         (rc = upload_vec(E->pfbloom, img.pf_bloom, s)) ||
-        (rc = upload_vec(E->polbloom, img.pol_bloom, s)))
+        (rc = upload_vec(E->polbloom, img.pol_bloom, s)) ||
+        (rc = upload_vec(E->lxc6, img.lxc6, s)) ||
+        (rc = upload_lpm6(E->l6[0], img.ipc6, &E->T.ipc6, s)) ||
+        (rc = upload_lpm6(E->l6[1], img.pf6_fix, &E->T.pf6_fix, s)) ||
+        (rc = upload_lpm6(E->l6[2], img.pf6_dyn, &E->T.pf6_dyn, s)))
         return rc;
     DevTables &T = E->T;
+    T.lxc6 = (const Lxc6Slot *)E->lxc6.p;
+    T.lxc6_mask = img.lxc6_mask;
+    T.lxc6_lds = img.lxc6.size() <= LXC6_LDS_MAX_SLOTS;
     T.l4c = (const uint32_t *)E->l4c.p;
     T.l4l = (const uint64_t *)E->l4l.p;
     T.tbl24 = (const uint32_t *)E->tbl24.p;
@@ -226,6 +250,13 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->st.lpm4_kib = (uint32_t)((4ull * (img.l4c.size() + img.tbl24.size() +
                                         img.tbl8.size()) +
                                  8ull * img.l4l.size() + 1023) / 1024);
+    E->st.ipcache_v6_prefixes = img.ipc6.n;
+    E->st.lpm6_lengths = (uint32_t)img.ipc6.lens.size();
+    E->st.lpm6_groups = img.ipc6.groups;
+    E->st.lpm6_kib = (uint32_t)((img.ipc6.bytes() + 1023) / 1024);
+    E->st.endpoints_v6 = img.n_eps6;
+    E->st.prefilter_v6_fix = img.pf6_fix.n;
+    E->st.prefilter_v6_dyn = img.pf6_dyn.n;
 
     // counters for the new entry layout (old ones were folded above)
     size_t need = 2ull * T.n_ctr + METRIC_U64;
@@ -533,8 +564,14 @@ int cfc_commit(cfc_ctx *c, void *stream)
     return commit_locked(c, (hipStream_t)stream);
 }
 
-int cfc_classify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
-                    int mode, uint16_t ep_lxc, void *stream)
+}  // extern "C"
+
+namespace {
+
+// cfc_classify_v4 / _v6: validation, auto-commit, workspace, launch
+template <class Hdr, class Launch>
+int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
+             uint16_t ep_lxc, void *stream, Launch launch)
 {
     if (!c || !in || !out || !out->verdict || !out->identity)
         return -EINVAL;
@@ -574,15 +611,30 @@ int cfc_classify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
     // the workspace is shared: order this launch after the previous one
     if (c->ctr_pending && c->last_stream != s)
         (void)hipStreamWaitEvent(s, c->last_done, 0);
-    rc = launch_classify_v4(E.T, *in, *out, mode, ea, c->ctr,
-                            c->ctr + 2ull * E.T.n_ctr, c->ws, c->num_cus, s,
-                            in->n ? next_timing(c) : nullptr);
+    rc = launch(E.T, *in, *out, mode, ea, c->ctr, c->ctr + 2ull * E.T.n_ctr,
+                c->ws, c->num_cus, s, in->n ? next_timing(c) : nullptr);
     if (rc)
         return rc;
     (void)hipEventRecord(c->last_done, s);
     c->last_stream = s;
     c->ctr_pending = true;
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfc_classify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream)
+{
+    return classify(c, in, out, mode, ep_lxc, stream, launch_classify_v4);
+}
+
+int cfc_classify_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream)
+{
+    return classify(c, in, out, mode, ep_lxc, stream, launch_classify_v6);
 }
 
 int cfc_counters_device(cfc_ctx *c, uint64_t **dev, uint64_t *n)

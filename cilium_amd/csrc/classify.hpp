@@ -48,4 +48,16 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                        int num_cus, hipStream_t stream,
                        const LaunchTiming *timing = nullptr);
 
+// The policy-entry counter kernels over the per-header entry indices the
+// classify kernel left in the workspace (both families).
+void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
+                     int mode, uint32_t *workspace, uint64_t *g_ctr,
+                     hipStream_t stream);
+
+int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
+                       const cfc_out &out, int mode, const EgressArgs &E,
+                       uint64_t *g_ctr, uint64_t *g_met, uint32_t *workspace,
+                       int num_cus, hipStream_t stream,
+                       const LaunchTiming *timing = nullptr);
+
 }  // namespace cfc

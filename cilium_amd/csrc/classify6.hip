@@ -1,0 +1,452 @@
+// IPv6 verdict kernel for gfx950 (MI355X): k_classify_v6.
+//
+// Same contract as k_classify_v4 (classify.hip): one pass over a SoA batch
+// writes verdict, identity, action and the policy-entry index per header;
+// the shared counter kernels (launch_counters) turn the indices into
+// packets/bytes.  What differs is the address work:
+//   * the ipcache is a 1M-prefix IPv6 LPM (layout.h Lpm6): lengths are
+//     probed longest first, each group of lengths screened by one 8-byte
+//     Bloom word (L2-resident), so a lookup is usually one Bloom load plus
+//     one 32-byte slot (Infinity Cache);
+//   * endpoints are 32-byte slots keyed by the full address, copied to LDS
+//     when the table is small;
+//   * the prefilter's exact /128 set and its LPM deny list are Lpm6 tables.
+// The per-header work is straight-line: the lookup chain of one header is
+// short and the 32 resident waves per CU keep enough of them in flight.
+//
+// Reference semantics restated here (file:line in /root/reference):
+//   ingress   bpf_netdev.c:128-153 (identity from skb->mark), :172-275
+//             handle_ipv6 (ipv6_hdrlen drops, icmp6_handle, ipcache
+//             override unless CLUSTER_ID), l3.h ipv6_local_delivery,
+//             bpf_lxc.c:753-895 ipv6_policy + tail_ipv6_policy
+//   egress    bpf_lxc.c:112-436 ipv6_l3_from_lxc / handle_ipv6 (icmp6
+//             punt, is_valid_lxc_src_ip, dst identity with the router /64
+//             as CLUSTER_ID)
+//   ct ports  conntrack.h ct_lookup6 (ICMPv6 echo request -> 128)
+//   xdp       bpf_xdp.c:132-156 check_v6
+#include "kern_common.hpp"
+
+namespace cfc {
+
+namespace {
+
+constexpr int DROP_INVALID_EXTHDR = -156, DROP_FRAG_NOSUPPORT = -157;
+constexpr int VERDICT_PUNT = CFC_VERDICT_PUNT;
+// node_config.h ROUTER_IP beef::1:0:1:0:0 as host-order words
+constexpr uint32_t ROUTER6_W0 = 0xBEEF0000u, ROUTER6_W1 = 0u,
+                   ROUTER6_W2 = 0x00000001u, ROUTER6_W3 = 0x00010000u;
+
+// update_metrics keys (reason, direction) per mode
+constexpr int LDS_MET6_U64 = 18;   // 2 x 9 keys
+template <int MODE>
+constexpr int met6_n()
+{
+    return MODE == CFC_MODE_EGRESS ? 9 : MODE == CFC_MODE_XDP ? 0 : 6;
+}
+template <int MODE>
+__host__ __device__ constexpr uint32_t met6_reason_dir(int k)
+{
+    constexpr uint32_t eg[9][2] = {{0, 2},   {132, 2}, {133, 2}, {137, 2}, {140, 2},
+                                   {156, 2}, {157, 2}, {0, 1},   {133, 1}};
+    constexpr uint32_t in[6][2] = {{0, 1},   {133, 1}, {137, 1},
+                                   {140, 1}, {156, 1}, {157, 1}};
+    return MODE == CFC_MODE_EGRESS ? eg[k][0] * METRIC_DIRS + eg[k][1]
+                                   : in[k][0] * METRIC_DIRS + in[k][1];
+}
+template <int MODE>
+__device__ __forceinline__ uint32_t mkey6(int reason, int dir)
+{
+    if (MODE == CFC_MODE_EGRESS) {
+        if (dir == METRIC_INGRESS)
+            return reason == 0 ? 7u : 8u;
+        switch (reason) {
+        case 0: return 0;
+        case -132: return 1;
+        case -133: return 2;
+        case -137: return 3;
+        case -140: return 4;
+        case -156: return 5;
+        default: return 6;   // -157
+        }
+    }
+    switch (reason) {
+    case 0: return 0;
+    case -133: return 1;
+    case -137: return 2;
+    case -140: return 3;
+    case -156: return 4;
+    default: return 5;       // -157
+    }
+}
+
+__device__ __forceinline__ uint4 bswap4(uint4 v)
+{
+    return make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y),
+                      __builtin_bswap32(v.z), __builtin_bswap32(v.w));
+}
+
+// ---- IPv6 LPM (layout.h Lpm6): the label of the longest prefix holding the
+// host-order address a (a matched label 0 shadows shorter prefixes, as the
+// reference's trie does), def_label when none
+__device__ __forceinline__ uint32_t lpm6_lookup(const Lpm6 &P, uint4 a)
+{
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+    uint64_t bw = 0;
+    for (uint32_t j = 0; j < P.nlen; j++) {
+        const uint32_t e = P.lens[j];   // uniform
+        const uint32_t len = e & 255;
+        if (e & L6_GROUP_FIRST)
+            bw = P.bloom[l6_group_hash(w, (e >> 8) & 255) & P.bloom_mask];
+        const uint32_t m0 = a.x & l6_word_mask(len, 0), m1 = a.y & l6_word_mask(len, 1),
+                       m2 = a.z & l6_word_mask(len, 2), m3 = a.w & l6_word_mask(len, 3);
+        const uint32_t h = l6_hash(m0, m1, m2, m3, len);
+        const uint64_t b = l6_bloom_bits(h);
+        if ((bw & b) != b)
+            continue;
+        for (uint32_t s = h & P.mask;; s = (s + 1) & P.mask) {
+            const uint4 k = ld16(&P.slots[s].w[0]);
+            const uint4 v = ld16(&P.slots[s].label);   // {label, len, 0, 0}
+            if (v.y == len && k.x == m0 && k.y == m1 && k.z == m2 && k.w == m3)
+                return v.x;
+            if (!v.y)
+                break;
+        }
+    }
+    return P.def_label;
+}
+
+// ---- endpoints: {pol_base, pol_mask, info, 0} of the slot holding the raw
+// address, zeros when it is not local
+__device__ __forceinline__ uint4 lxc6_find(const DevTables &T, bool lds,
+                                           uint32_t lds_off, uint4 raw)
+{
+    if (!T.lxc6)
+        return make_uint4(0, 0, 0, 0);
+    uint32_t s = l6_hash(raw.x, raw.y, raw.z, raw.w, L6_LXC_TAG) & T.lxc6_mask;
+    for (;;) {
+        uint4 k, v;
+        if (lds) {
+            k = cfc_smem[lds_off + 2 * s];
+            v = cfc_smem[lds_off + 2 * s + 1];
+        } else {
+            k = ld16(&T.lxc6[s].a[0]);
+            v = ld16(&T.lxc6[s].pol_base);
+        }
+        if (!(v.z & LXC_VALID))
+            return make_uint4(0, 0, 0, 0);
+        if (k.x == raw.x && k.y == raw.y && k.z == raw.z && k.w == raw.w)
+            return v;
+        s = (s + 1) & T.lxc6_mask;
+    }
+}
+
+// tuple->dport of a CT_NEW ct_lookup6: TCP/UDP dport, ICMPv6 echo request
+// -> 128 (its type), other ICMPv6 -> 0, anything else DROP_CT_UNKNOWN_PROTO
+__device__ __forceinline__ bool ct6_new_dport(uint32_t proto, uint32_t ports,
+                                              uint32_t *dport)
+{
+    if (proto == 6 || proto == 17) {
+        *dport = ports >> 16;
+        return true;
+    }
+    *dport = (ports & 0xFF) == 128 ? 128u : 0u;
+    return proto == 58;
+}
+
+// icmp6_handle (icmp6.h:390-412): neighbour solicitations and echo requests
+// to the router are answered, not classified.  It reads the type right after
+// the fixed header, so with extension headers it never triggers.
+__device__ __forceinline__ bool icmp6_punt(uint32_t proto, uint32_t meta,
+                                           uint32_t ports, uint4 da)
+{
+    if (proto != 58 || (meta & CFC_HF_EXTHDR))
+        return false;
+    const uint32_t type = ports & 0xFF;
+    return type == 135 || (type == 128 && da.x == ROUTER6_W0 && da.y == ROUTER6_W1 &&
+                           da.z == ROUTER6_W2 && da.w == ROUTER6_W3);
+}
+
+struct LdsPlan6 {
+    uint32_t lxc_slots, pol_words;
+    __host__ __device__ size_t bytes() const
+    {
+        return 8ull * LDS_MET6_U64 + 32ull * lxc_slots + 4ull * pol_words;
+    }
+};
+
+__host__ LdsPlan6 lds_plan6(const DevTables &T)
+{
+    LdsPlan6 p;
+    p.lxc_slots = (T.lxc6 && T.lxc6_lds) ? T.lxc6_mask + 1 : 0;
+    p.pol_words = T.pol_bloom ? T.pol_bloom_words : 0;
+    return p;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
+    DevTables T, LdsPlan6 L, cfc_hdr_v6 in, cfc_out out, EgressArgs E,
+    uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
+{
+    constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
+    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
+    // LDS image (uint4 units): metrics | endpoint slots | pol Bloom
+    unsigned long long *s_met = lds_met();
+    const uint32_t lxc_off = LDS_MET6_U64 / 2;
+    const uint32_t pol4 = lxc_off + 2 * L.lxc_slots;
+    const bool lxc_lds = L.lxc_slots != 0;
+    Lds S;
+    S.lxc = false;
+    S.pfb = false;
+    S.polb = L.pol_words != 0;
+    S.polb_off = 4 * pol4;
+    S.polb_mask = L.pol_words - 1;
+    for (uint32_t j = threadIdx.x; j < (uint32_t)LDS_MET6_U64; j += BLOCK)
+        s_met[j] = 0;
+    lds_copy(cfc_smem + lxc_off, reinterpret_cast<const uint4 *>(T.lxc6),
+             2 * L.lxc_slots);
+    lds_copy(cfc_smem + pol4, reinterpret_cast<const uint4 *>(T.pol_bloom),
+             L.pol_words / 4);
+    __syncthreads();
+
+    const uint64_t start = (uint64_t)blockIdx.x * per_block;
+    const uint64_t end = min(in.n, start + per_block);
+    const uint32_t *sa_in = reinterpret_cast<const uint32_t *>(in.saddr);
+    const uint32_t *da_in = reinterpret_cast<const uint32_t *>(in.daddr);
+    MetAcc<met6_n<MODE>()> acc;
+    acc.clear();
+    uint32_t iter = 0;
+    for (uint64_t base = start; base < end; base += BLOCK) {
+        // lanes past the end redo the slice's last header (see r1_load)
+        const bool valid = base + threadIdx.x < end;
+        const uint64_t i = valid ? base + threadIdx.x : end - 1;
+        const uint4 sa_raw = ld_nt4(sa_in + 4 * i);
+        const uint4 da_raw = ld_nt4(da_in + 4 * i);
+        const uint32_t pt = ld_nt(in.ports + i);
+        const uint32_t mt = ld_nt(in.meta + i);
+        const uint32_t mk = in.mark ? ld_nt(in.mark + i) : 0u;
+        const uint4 sa = bswap4(sa_raw), da = bswap4(da_raw);
+        const uint32_t proto = mt & 0xFF;
+
+        int act = TC_ACT_OK, ver = 0;
+        uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
+        const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
+        const bool local = (drec.z & LXC_VALID) != 0;
+        bool done = false;
+        if (XDP) {
+            bool deny = lpm6_lookup(T.pf6_dyn, sa) != 0;
+            if (!deny)
+                deny = lpm6_lookup(T.pf6_fix, sa) != 0;
+            const bool drop = deny || !local;
+            if (MODE == CFC_MODE_XDP || drop) {
+                act = drop ? XDP_DROP : XDP_PASS;
+                ver = drop ? CFC_DROP_PREFILTER : 0;
+                done = true;
+            }
+        }
+        if (!done) {
+            uint32_t dport;
+            const bool known = ct6_new_dport(proto, pt, &dport);
+            const int xd = proto == 59 ? DROP_INVALID_EXTHDR
+                         : proto == 44 ? DROP_FRAG_NOSUPPORT : 0;
+            const bool punt = icmp6_punt(proto, mt, pt, da);
+            const bool ifx = (drec.z & LXC_IFINDEX) != 0;
+            if (!EGR) {
+                // handle_identity_from_host (bpf_netdev.c:128-153)
+                const uint32_t magic = mk & 0xF00u;
+                bool skip_proxy = false;
+                if (magic == 0xA00u || magic == 0xB00u) {
+                    ident = ((mk & 0xFF) << 16) | (mk >> 16);
+                    skip_proxy = magic == 0xA00u;
+                } else {
+                    ident = magic == 0xC00u ? HOST_ID : WORLD_ID;
+                }
+                if (xd) {   // send_drop_notify_error: no identity recorded
+                    act = TC_ACT_SHOT;
+                    ver = xd;
+                    ident = 0;
+                    met0 = mkey6<MODE>(xd, METRIC_INGRESS);
+                } else if (punt) {
+                    ver = VERDICT_PUNT;
+                    ident = 0;
+                } else {
+                    // handle_ipv6 (:203-213): reserved identities take the
+                    // ipcache's unless it says CLUSTER_ID
+                    if (ident < HEALTH_ID) {
+                        const uint32_t label = lpm6_lookup(T.ipc6, sa);
+                        if (label && label != CLUSTER_ID)
+                            ident = label;
+                    }
+                    if (local && !(drec.z & LXC_HOST)) {
+                        if (!(drec.z & LXC_HAS_POLICY)) {
+                            act = TC_ACT_SHOT;
+                            ver = DROP_MISSED_TAIL_CALL;
+                            met0 = mkey6<MODE>(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
+                        } else if (!known) {
+                            act = TC_ACT_SHOT;
+                            ver = DROP_CT_UNKNOWN_PROTO;
+                            met0 = mkey6<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
+                        } else {
+                            const PolicyResult pr = policy_access(
+                                T, S, drec.x, drec.y, ident, dport, proto, 0, false);
+                            ctr0 = pr.ctr;
+                            if (pr.verdict < 0) {
+                                act = TC_ACT_SHOT;
+                                ver = DROP_POLICY;
+                                met0 = mkey6<MODE>(DROP_POLICY, METRIC_INGRESS);
+                            } else {
+                                const int v = skip_proxy ? 0 : pr.verdict;
+                                act = (v > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                                ver = v;
+                                met0 = v > 0 ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
+                            }
+                        }
+                    }
+                }
+            } else if (punt) {
+                ver = VERDICT_PUNT;
+            } else {
+                act = TC_ACT_SHOT;
+                const uint4 srec = lxc6_find(T, lxc_lds, lxc_off, sa_raw);
+                const bool src_ok = (srec.z & LXC_VALID) && (srec.z & 0xFFFF) == E.lxc_id;
+                if (!src_ok) {   // is_valid_lxc_src_ip (lxc.h:46)
+                    ver = DROP_INVALID_SIP;
+                    met0 = mkey6<MODE>(DROP_INVALID_SIP, METRIC_EGRESS);
+                } else if (xd) {
+                    ver = xd;
+                    met0 = mkey6<MODE>(xd, METRIC_EGRESS);
+                } else if (!known) {
+                    ver = DROP_CT_UNKNOWN_PROTO;
+                    met0 = mkey6<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
+                } else {
+                    // destination identity (bpf_lxc.c:206-221)
+                    const uint32_t label = lpm6_lookup(T.ipc6, da);
+                    ident = label ? label
+                          : (da.x == ROUTER6_W0 && da.y == ROUTER6_W1) ? CLUSTER_ID
+                                                                        : WORLD_ID;
+                    const PolicyResult pr = policy_access(T, S, E.pol_base, E.pol_mask,
+                                                          ident, dport, proto, 1, false);
+                    ctr0 = pr.ctr;
+                    if (pr.verdict < 0) {
+                        ver = DROP_POLICY;
+                        met0 = mkey6<MODE>(DROP_POLICY, METRIC_EGRESS);
+                    } else if (pr.verdict > 0) {   // to the proxy
+                        act = TC_ACT_REDIRECT;
+                        ver = pr.verdict;
+                    } else {
+                        met0 = mkey6<MODE>(0, METRIC_EGRESS);   // host/local/stack
+                        ver = 0;
+                        if (!local) {
+                            act = TC_ACT_OK;
+                        } else if (drec.z & LXC_HOST) {
+                            act = TC_ACT_REDIRECT;
+                        } else if (!(drec.z & LXC_HAS_POLICY)) {
+                            ver = DROP_MISSED_TAIL_CALL;
+                            met1 = mkey6<MODE>(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
+                        } else {
+                            // ipv6_local_delivery into the destination's
+                            // ipv6_policy with src = SECLABEL
+                            const PolicyResult pw = policy_access(
+                                T, S, drec.x, drec.y, E.seclabel, dport, proto, 0, false);
+                            ctr1 = pw.ctr;
+                            if (pw.verdict < 0) {
+                                ver = DROP_POLICY;
+                                met1 = mkey6<MODE>(DROP_POLICY, METRIC_INGRESS);
+                            } else {
+                                act = (pw.verdict > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                                ver = pw.verdict;
+                                met1 = pw.verdict > 0 ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        st_nt(ver, out.verdict + i);
+        st_nt(ident, out.identity + i);
+        if (out.action)
+            out.action[i] = (uint8_t)act;
+        if (MODE != CFC_MODE_XDP) {
+            st_nt(ctr0, ctr_idx + i);
+            if (EGR)
+                st_nt(ctr1, ctr_idx + ctr_stride(in.n) + i);
+        }
+        const uint32_t len = mt >> 16;
+        acc.add(valid ? met0 : NONE, len);
+        if (EGR)
+            acc.add(valid ? met1 : NONE, len);
+        if (++iter == 65536 / 2) {
+            acc.flush(s_met);
+            iter = 0;
+        }
+    }
+    acc.flush(s_met);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < 2u * met6_n<MODE>(); j += BLOCK) {
+        const unsigned long long v = s_met[j];
+        if (v)
+            atomicAdd((unsigned long long *)&g_met[met6_reason_dir<MODE>(j >> 1) * 2 + (j & 1)],
+                      v);
+    }
+}
+
+template <int MODE>
+void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
+                  const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
+                  uint32_t grid, uint64_t per_block, hipStream_t s)
+{
+    const LdsPlan6 L = lds_plan6(T);
+    auto kern = k_classify_v6<MODE>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        (void)hipFuncSetAttribute((const void *)kern,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)LDS_PER_WG);
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
+                       out, E, ctr_idx, g_met, per_block);
+}
+
+}  // namespace
+
+int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
+                       const cfc_out &out, int mode, const EgressArgs &E,
+                       uint64_t *g_ctr, uint64_t *g_met, uint32_t *ws,
+                       int num_cus, hipStream_t s, const LaunchTiming *tm)
+{
+    if (in.n == 0)
+        return 0;
+    if (lds_plan6(T).bytes() > LDS_PER_WG)
+        return -22;
+    if ((reinterpret_cast<uintptr_t>(in.saddr) | reinterpret_cast<uintptr_t>(in.daddr)) & 15)
+        return -22;   // 16-byte address loads
+    const uint64_t nwg = (uint64_t)num_cus * CFC_WG_PER_CU;
+    uint64_t per_block = (in.n + nwg - 1) / nwg;
+    per_block = (per_block + BLOCK - 1) / BLOCK * BLOCK;
+    const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
+    if (tm)
+        (void)hipEventRecord(tm->ev[0], s);
+    switch (mode) {
+    case CFC_MODE_INGRESS:
+        launch_mode6<CFC_MODE_INGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    case CFC_MODE_EGRESS:
+        launch_mode6<CFC_MODE_EGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    case CFC_MODE_XDP:
+        launch_mode6<CFC_MODE_XDP>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    case CFC_MODE_FULL:
+        launch_mode6<CFC_MODE_FULL>(T, in, out, E, ws, g_met, grid, per_block, s);
+        break;
+    default: return -22;
+    }
+    if (tm)
+        (void)hipEventRecord(tm->ev[1], s);
+    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s);
+    if (tm)
+        (void)hipEventRecord(tm->ev[2], s);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+}  // namespace cfc

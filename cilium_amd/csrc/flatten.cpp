@@ -20,7 +20,9 @@ uint64_t HostImage::device_bytes() const
                    pf_tbl24.size() + pf_tbl8.size() + pf_fix.size() +
                    pf_bloom.size() + pol_bloom.size()) +
            4ull * l4c.size() + 8ull * l4l.size() +
-           sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size();
+           sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size() +
+           ipc6.bytes() + pf6_fix.bytes() + pf6_dyn.bytes() +
+           sizeof(Lxc6Slot) * lxc6.size();
 }
 
 // DIR-24-8: every prefix <= /24 fills its tbl24 range in ascending length
@@ -158,6 +160,120 @@ bool build_l4trie(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
     return b.ok;
 }
 
+// ---- IPv6 LPM (layout.h Lpm6)
+namespace {
+
+typedef std::pair<uint64_t, uint64_t> U128;
+
+U128 masked128(const uint32_t w[4], uint32_t len)
+{
+    uint32_t m[4];
+    for (int i = 0; i < 4; i++)
+        m[i] = w[i] & l6_word_mask(len, i);
+    return {(uint64_t)m[0] << 32 | m[1], (uint64_t)m[2] << 32 | m[3]};
+}
+
+// most keys of lengths L[i..k] that share one address masked to L[k]
+size_t max_pile(const std::vector<std::vector<const Pfx6 *>> &by_len,
+                const std::vector<uint32_t> &L, size_t i, size_t k)
+{
+    std::vector<U128> v;
+    for (size_t j = i; j <= k; j++)
+        for (const Pfx6 *p : by_len[L[j]])
+            v.push_back(masked128(p->w, L[k]));
+    std::sort(v.begin(), v.end());
+    size_t best = 0;
+    for (size_t a = 0; a < v.size();) {
+        size_t b = a;
+        while (b < v.size() && v[b] == v[a])
+            b++;
+        best = std::max(best, b - a);
+        a = b;
+    }
+    return best;
+}
+
+}  // namespace
+
+void build_lpm6(const std::vector<Pfx6> &pfx, Lpm6Host *out)
+{
+    *out = Lpm6Host();
+    out->n = (uint32_t)pfx.size();
+    std::vector<std::vector<const Pfx6 *>> by_len(129);
+    size_t nkeys = 0;
+    for (const Pfx6 &p : pfx) {
+        if (p.plen == 0) {
+            out->def_label = p.label;
+        } else {
+            by_len[p.plen].push_back(&p);
+            nkeys++;
+        }
+    }
+    std::vector<uint32_t> L;
+    for (uint32_t l = 128; l >= 1; l--)
+        if (!by_len[l].empty())
+            L.push_back(l);
+    if (L.empty())
+        return;
+    // Bloom groups: extend a group to the next shorter length while the
+    // addresses masked to it keep at most L6_GROUP_MAX keys per word
+    uint32_t sel_of[129] = {0};
+    for (size_t i = 0; i < L.size();) {
+        size_t k = i;
+        while (k + 1 < L.size() && max_pile(by_len, L, i, k + 1) <= L6_GROUP_MAX)
+            k++;
+        for (size_t j = i; j <= k; j++) {
+            out->lens.push_back(L[j] | L[k] << 8 | (j == i ? L6_GROUP_FIRST : 0));
+            sel_of[L[j]] = L[k];
+        }
+        out->groups++;
+        i = k + 1;
+    }
+    out->bloom.assign(pow2_at_least(std::max<size_t>(64, nkeys / 4)), 0);
+    const uint32_t bmask = (uint32_t)out->bloom.size() - 1;
+    const uint32_t ns = pow2_at_least(std::max<size_t>(16, 2 * nkeys));
+    out->slots.assign(ns, L6Slot{});
+    for (uint32_t len : L)
+        for (const Pfx6 *p : by_len[len]) {
+            const uint32_t h = l6_hash(p->w[0], p->w[1], p->w[2], p->w[3], len);
+            out->bloom[l6_group_hash(p->w, sel_of[len]) & bmask] |= l6_bloom_bits(h);
+            uint32_t s = h & (ns - 1);
+            while (out->slots[s].len)
+                s = (s + 1) & (ns - 1);
+            L6Slot &d = out->slots[s];
+            memcpy(d.w, p->w, 16);
+            d.label = p->label;
+            d.len = len;
+        }
+}
+
+uint32_t lpm6_lookup_host(const Lpm6Host &t, const uint32_t w[4])
+{
+    const uint32_t mask = (uint32_t)t.slots.size() - 1;
+    const uint32_t bmask = (uint32_t)t.bloom.size() - 1;
+    uint64_t bw = 0;
+    for (uint32_t e : t.lens) {
+        const uint32_t len = e & 255;
+        if (e & L6_GROUP_FIRST)
+            bw = t.bloom[l6_group_hash(w, (e >> 8) & 255) & bmask];
+        uint32_t m[4];
+        for (int i = 0; i < 4; i++)
+            m[i] = w[i] & l6_word_mask(len, i);
+        const uint32_t h = l6_hash(m[0], m[1], m[2], m[3], len);
+        const uint64_t b = l6_bloom_bits(h);
+        if ((bw & b) != b)
+            continue;
+        for (uint32_t s = h & mask;; s = (s + 1) & mask) {
+            const L6Slot &d = t.slots[s];
+            if (!d.len)
+                break;
+            if (d.len == len && !memcmp(d.w, m, 16))
+                return d.label;
+        }
+    }
+    return t.def_label;
+}
+
 // Blocked Bloom filter with ~`per_word` keys per 32-bit word, capped.
 static void bloom_size(std::vector<uint32_t> *b, size_t keys, uint32_t max_words)
 {
@@ -220,12 +336,104 @@ static void ipcache_v4(const Map *m, std::vector<Pfx4> *out,
                         leaf_for(b.second.second, ovf)});
 }
 
+// Effective IPv6 prefixes of the ipcache: as ipcache_v4 with the v6 lookup
+// key {prefixlen 160, pad 0,0, family 2, addr} (eps.h:56-66).
+static void ipcache_v6(const Map *m, std::vector<Pfx6> *out)
+{
+    static const uint8_t stat6[4] = {0, 0, 0, 2};
+    std::map<std::pair<U128, int>, std::pair<uint32_t, Pfx6>> best;
+    for (const auto &kv : m->kv) {
+        const uint8_t *k = (const uint8_t *)kv.first.data();  // normalised
+        uint32_t P;
+        memcpy(&P, k, 4);
+        if (P > 160)
+            continue;
+        bool ok = true;
+        for (uint32_t bit = 0; bit < std::min<uint32_t>(P, 32); bit++) {
+            uint32_t byte = bit >> 3, sh = 7 - (bit & 7);
+            if (((k[4 + byte] >> sh) & 1) != ((stat6[byte] >> sh) & 1)) {
+                ok = false;
+                break;
+            }
+        }
+        if (!ok)
+            continue;
+        Pfx6 p;
+        p.plen = (uint8_t)(P > 32 ? P - 32 : 0);
+        for (int i = 0; i < 4; i++) {
+            uint32_t a;
+            memcpy(&a, k + 8 + 4 * i, 4);
+            p.w[i] = bswap(a) & l6_word_mask(p.plen, i);
+        }
+        memcpy(&p.label, kv.second.val.data(), 4);
+        auto key = std::make_pair(masked128(p.w, p.plen), (int)p.plen);
+        auto it = best.find(key);
+        if (it == best.end() || it->second.first < P)
+            best[key] = {P, p};
+    }
+    for (const auto &b : best)
+        out->push_back(b.second.second);
+}
+
+// prefilter v6 maps: key {u32 prefixlen, 16-byte address}
+static void prefilter_v6(const Map *m, bool exact, std::vector<Pfx6> *out)
+{
+    for (const auto &kv : m->kv) {
+        const uint8_t *k = (const uint8_t *)kv.first.data();
+        uint32_t P;
+        memcpy(&P, k, 4);
+        if (exact && P != 128)   // check_v6 looks up {128, saddr} exactly
+            continue;
+        if (P > 128)
+            continue;
+        Pfx6 p;
+        p.plen = (uint8_t)P;
+        p.label = 1;
+        for (int i = 0; i < 4; i++) {
+            uint32_t a;
+            memcpy(&a, k + 4 + 4 * i, 4);
+            p.w[i] = bswap(a) & l6_word_mask(P, i);
+        }
+        out->push_back(p);
+    }
+}
+
+// struct endpoint_info {u32 ifindex; u16 unused; u16 lxc_id; u32 flags; ...}
+static uint32_t lxc_info(const HostImage *img, const uint8_t *v, PolLoc *loc)
+{
+    uint32_t ifindex, flags;
+    uint16_t id;
+    memcpy(&ifindex, v, 4);
+    memcpy(&id, v + 6, 2);
+    memcpy(&flags, v + 8, 4);
+    uint32_t info = id | LXC_VALID | ((flags & 1) ? LXC_HOST : 0) |
+                    (ifindex ? LXC_IFINDEX : 0);
+    auto it = img->pol_loc.find(id);
+    *loc = PolLoc();
+    if (it != img->pol_loc.end()) {
+        *loc = it->second;
+        info |= LXC_HAS_POLICY;
+    }
+    return info;
+}
+
+static Lxc6Slot lxc6_slot(const HostImage *img, const uint8_t *k, const uint8_t *v)
+{
+    Lxc6Slot r{};
+    memcpy(r.a, k, 16);
+    PolLoc loc;
+    r.info = lxc_info(img, v, &loc);
+    r.pol_base = loc.base;
+    r.pol_mask = loc.mask;
+    return r;
+}
+
 void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
                  HostImage *img)
 {
     *img = HostImage();
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,
-              *pf4dyn = nullptr;
+              *pf4dyn = nullptr, *pf6fix = nullptr, *pf6dyn = nullptr;
     std::map<int, Map *> pols;
     for (Map *m : maps) {
         switch (m->role) {
@@ -233,6 +441,8 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         case ROLE_LXC: lxc = m; break;
         case ROLE_PF4_FIX: pf4fix = m; break;
         case ROLE_PF4_DYN: pf4dyn = m; break;
+        case ROLE_PF6_FIX: pf6fix = m; break;
+        case ROLE_PF6_DYN: pf6dyn = m; break;
         case ROLE_POLICY: pols[m->policy_lxc] = m; break;
         default: break;
         }
@@ -262,7 +472,24 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         }
     }
 
+    // ---- ipcache v6
+    if (ipc) {
+        std::vector<Pfx6> pfx;
+        ipcache_v6(ipc, &pfx);
+        build_lpm6(pfx, &img->ipc6);
+    }
+
     // ---- prefilter
+    if (pf6fix && pf6fix->ksz == 20) {
+        std::vector<Pfx6> pfx;
+        prefilter_v6(pf6fix, true, &pfx);
+        build_lpm6(pfx, &img->pf6_fix);
+    }
+    if (pf6dyn && pf6dyn->ksz == 20) {
+        std::vector<Pfx6> pfx;
+        prefilter_v6(pf6dyn, false, &pfx);
+        build_lpm6(pfx, &img->pf6_dyn);
+    }
     if (pf4dyn && pf4dyn->ksz == 8) {
         std::vector<Pfx4> pfx;
         for (const auto &kv : pf4dyn->kv) {
@@ -366,29 +593,24 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
     //      the endpoint record inlined in the slot
     if (lxc && lxc->ksz == 20 && lxc->vsz >= 12) {
         std::vector<LxcSlot> v4;
+        std::vector<Lxc6Slot> v6;
         for (const auto &kv : lxc->kv) {
             const uint8_t *k = (const uint8_t *)kv.first.data();
             const uint8_t *v = (const uint8_t *)kv.second.val.data();
             bool is_v4 = k[16] == 1 && k[17] == 0 && k[18] == 0 && k[19] == 0;
             for (int i = 4; i < 16 && is_v4; i++)
                 is_v4 = k[i] == 0;
-            if (!is_v4)
-                continue;  // IPv6 endpoints: next step of the build
+            if (!is_v4) {
+                if (k[16] == 2 && k[17] == 0 && k[18] == 0 && k[19] == 0)
+                    v6.push_back(lxc6_slot(img, k, (const uint8_t *)kv.second.val.data()));
+                continue;
+            }
             LxcSlot r{};
             memcpy(&r.addr, k, 4);
-            uint32_t ifindex, flags;
-            uint16_t id;
-            memcpy(&ifindex, v, 4);
-            memcpy(&id, v + 6, 2);
-            memcpy(&flags, v + 8, 4);
-            r.info = id | LXC_VALID | ((flags & 1) ? LXC_HOST : 0) |
-                     (ifindex ? LXC_IFINDEX : 0);
-            auto it = img->pol_loc.find(id);
-            if (it != img->pol_loc.end()) {
-                r.pol_base = it->second.base;
-                r.pol_mask = it->second.mask;
-                r.info |= LXC_HAS_POLICY;
-            }
+            PolLoc loc;
+            r.info = lxc_info(img, v, &loc);
+            r.pol_base = loc.base;
+            r.pol_mask = loc.mask;
             v4.push_back(r);
         }
         img->n_eps = (uint32_t)v4.size();
@@ -401,6 +623,18 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
                 while (img->lxc4[s].info & LXC_VALID)
                     s = (s + 1) & (ns - 1);
                 img->lxc4[s] = e;
+            }
+        }
+        img->n_eps6 = (uint32_t)v6.size();
+        if (!v6.empty()) {
+            uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 4ull * v6.size()));
+            img->lxc6.assign(ns, Lxc6Slot{});
+            img->lxc6_mask = ns - 1;
+            for (const Lxc6Slot &e : v6) {
+                uint32_t s = l6_hash(e.a[0], e.a[1], e.a[2], e.a[3], L6_LXC_TAG) & (ns - 1);
+                while (img->lxc6[s].info & LXC_VALID)
+                    s = (s + 1) & (ns - 1);
+                img->lxc6[s] = e;
             }
         }
     }

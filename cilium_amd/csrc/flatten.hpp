@@ -22,6 +22,29 @@ struct BuildOpts {
     int lpm4 = LPM4_AUTO;
 };
 
+// IPv6 LPM (layout.h Lpm6), host side
+struct Pfx6 {
+    uint32_t w[4];   // host-order words, masked
+    uint8_t plen;
+    uint32_t label;
+};
+struct Lpm6Host {
+    std::vector<L6Slot> slots;
+    std::vector<uint64_t> bloom;
+    std::vector<uint32_t> lens;
+    uint32_t def_label = 0;
+    uint32_t n = 0;        // prefixes (incl. /0)
+    uint32_t groups = 0;   // Bloom groups
+    uint64_t bytes() const
+    {
+        return sizeof(L6Slot) * slots.size() + 8ull * bloom.size() + 4ull * lens.size();
+    }
+};
+void build_lpm6(const std::vector<Pfx6> &pfx, Lpm6Host *out);
+// host reference of the device lookup (unit tests): the label of the
+// longest prefix containing w, def_label when none
+uint32_t lpm6_lookup_host(const Lpm6Host &t, const uint32_t w[4]);
+
 struct HostImage {
     // IPv4 ipcache: compact multibit (l4c/l4l) or DIR-24-8 (tbl24/tbl8)
     std::vector<uint32_t> tbl24, tbl8, lbl_ovf;
@@ -42,6 +65,10 @@ struct HostImage {
     std::vector<PolSlot> pol;
     std::vector<uint32_t> pol_bloom;
     std::unordered_map<int, PolLoc> pol_loc;       // lxc_id -> table
+    // IPv6
+    Lpm6Host ipc6, pf6_fix, pf6_dyn;
+    std::vector<Lxc6Slot> lxc6;
+    uint32_t lxc6_mask = 0, n_eps6 = 0;
     std::vector<std::pair<Map *, std::string>> ctr_owner;  // ctr -> entry
     uint64_t device_bytes() const;
 };

@@ -1,0 +1,347 @@
+// Device helpers shared by the IPv4 and IPv6 classify kernels
+// (classify.hip, classify6.hip): streaming loads, the LDS image, the Bloom
+// filters, __policy_can_access and the per-thread metrics accumulators.
+#pragma once
+#include "classify.hpp"
+
+namespace cfc {
+
+namespace {
+
+constexpr uint32_t HOST_ID = 1, WORLD_ID = 2, CLUSTER_ID = 3, HEALTH_ID = 4;
+constexpr uint32_t IPV4_CLUSTER_MASK = 0xff0000u, IPV4_CLUSTER_RANGE = 0x100000u;
+constexpr int DROP_INVALID_SIP = -132, DROP_POLICY = -133,
+              DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140;
+constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
+constexpr int XDP_DROP = 1, XDP_PASS = 2;
+constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+// k_count: the packed u32 byte sums stay exact (64512 headers x 65535
+// bytes < 2^32, so they never carry into the packet count)
+constexpr uint64_t COUNT_PER_BLOCK = 63 * BLOCK;
+// workspace: entry indices [n] (egress: a second array at ctr_stride(n)),
+// then the partial slabs; both arrays 16-byte aligned for k_count
+__host__ __device__ constexpr uint64_t ctr_stride(uint64_t n) { return (n + 3) & ~3ull; }
+#ifndef CFC_UNROLL
+#define CFC_UNROLL 1   // headers in flight per thread
+#endif
+#ifndef CFC_WG_PER_CU
+#define CFC_WG_PER_CU 2   // 1024-thread workgroups resident per CU
+#endif
+constexpr int WAVES_PER_SIMD = 4 * CFC_WG_PER_CU;
+constexpr size_t LDS_PER_WG = LDS_BYTES_MAX / CFC_WG_PER_CU;
+
+template <class T>
+__device__ __forceinline__ T ld_nt(const T *p)
+{
+    return __builtin_nontemporal_load(p);
+}
+template <class T>
+__device__ __forceinline__ void st_nt(T v, T *p)
+{
+    __builtin_nontemporal_store(v, p);
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// 16-byte non-temporal load (p 16-byte aligned)
+__device__ __forceinline__ uint4 ld_nt4(const uint32_t *p)
+{
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint4 ld16(const void *p)
+{
+    return *reinterpret_cast<const uint4 *>(p);
+}
+
+// Workgroup-shared state: LDS copies of the small tables.  Accessed through
+// the extern __shared__ symbol with dword offsets (not through pointers kept
+// in a struct, which would lose the LDS address space and turn every read
+// into a flat load).
+extern __shared__ uint4 cfc_smem[];
+
+struct Lds {
+    bool lxc, pfb, polb;          // which tables are in LDS
+    uint32_t lxc_off;             // uint4 index of the endpoint slots
+    uint32_t pfb_off, polb_off;   // dword index of the Bloom filters
+    uint32_t pfb_mask, polb_mask;
+};
+
+__device__ __forceinline__ unsigned long long *lds_met()
+{
+    return reinterpret_cast<unsigned long long *>(cfc_smem);
+}
+__device__ __forceinline__ uint32_t lds_word(uint32_t off)
+{
+    return reinterpret_cast<const uint32_t *>(cfc_smem)[off];
+}
+
+// ---- compact IPv4 LPM (layout.h): walk from the /16 directory word `e`
+// through chunks to a leaf or a prefix list; the first list entry that
+// matches is the longest prefix.  Returns the label (0 = no match).
+__device__ __forceinline__ uint32_t l4_leaf(const DevTables &T, uint32_t e)
+{
+    return (e & LPM_INDIRECT) ? T.lbl_ovf[e & LPM_PAYLOAD] : e;
+}
+__device__ __forceinline__ uint32_t l4_list_leaf(const DevTables &T, uint32_t hi)
+{
+    const uint32_t l = hi & (LL_INDIRECT | LL_PAYLOAD);
+    return (l & LL_INDIRECT) ? T.lbl_ovf[l & LL_PAYLOAD] : l;
+}
+__device__ __forceinline__ uint32_t l4_lookup(const DevTables &T, uint32_t a,
+                                              uint32_t e)
+{
+    uint32_t shift = 16;   // address bits below the current node
+    while (e & L4_PTR) {
+        const uint32_t cnt = (e >> 24) & 127, off = e & L4_OFF;
+        if (cnt == 0) {
+            shift -= 8;
+            e = T.l4c[off + ((a >> shift) & 255)];
+            continue;
+        }
+        for (uint32_t i = 0; i < cnt; i += 2) {
+            const uint4 v = ld16(T.l4l + off + i);
+            if (l4_match(a, v.x, v.y))
+                return l4_list_leaf(T, v.y);
+            if (l4_match(a, v.z, v.w))
+                return l4_list_leaf(T, v.w);
+        }
+        return 0;   // not reached: a list ends with its node's own prefix
+    }
+    return l4_leaf(T, e);
+}
+
+// ---- endpoint lookup: 16-byte slots, linear probing (layout.h).
+// Returns the slot (info VALID) or a zero slot for a miss.
+__device__ __forceinline__ uint4 lxc_slot(const DevTables &T, const Lds &S,
+                                          uint32_t s)
+{
+    return S.lxc ? cfc_smem[S.lxc_off + s] : ld16(T.lxc4 + s);
+}
+__device__ __forceinline__ uint4 lxc_resolve(const DevTables &T, const Lds &S,
+                                             uint32_t addr, uint32_t s, uint4 v)
+{
+    for (;;) {
+        if (!(v.w & LXC_VALID))
+            return make_uint4(0, 0, 0, 0);
+        if (v.x == addr)
+            return v;
+        s = (s + 1) & T.lxc4_mask;
+        v = lxc_slot(T, S, s);
+    }
+}
+
+// ---- prefilter /32 set: 16-byte buckets of 4 addresses, 0 = free
+__device__ __forceinline__ bool pf_resolve(const DevTables &T, uint32_t addr,
+                                           uint32_t b, uint4 v)
+{
+    for (;;) {
+        if (v.x == addr || v.y == addr || v.z == addr || v.w == addr)
+            return true;
+        if (!v.x || !v.y || !v.z || !v.w)
+            return false;
+        b = (b + 1) & T.pf_fix_mask;
+        v = ld16(T.pf_fix + (size_t)b * PF_SLOTS);
+    }
+}
+
+__device__ __forceinline__ bool bloom_maybe(uint32_t off, uint32_t mask,
+                                            uint32_t h)
+{
+    const uint32_t b = bloom_bits(h);
+    return (lds_word(off + ((uint32_t)h & mask)) & b) == b;
+}
+
+__device__ __forceinline__ uint64_t pkey(uint32_t id, uint32_t dport,
+                                         uint32_t proto, uint32_t egress)
+{
+    return (uint64_t)id | ((uint64_t)dport << 32) | ((uint64_t)proto << 48) |
+           ((uint64_t)egress << 56);
+}
+
+// tuple->dport of a CT_NEW lookup (conntrack.h:496-584): TCP/UDP ports are
+// loaded swapped and swapped back by ipv4_ct_tuple_reverse(); ICMP echo puts
+// its type (8) in tuple->sport, which becomes the dport; other ICMP -> 0;
+// any other protocol -> DROP_CT_UNKNOWN_PROTO.
+__device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
+                                             uint32_t *dport)
+{
+    if (proto == 6 || proto == 17) {
+        *dport = ports >> 16;
+        return true;
+    }
+    *dport = (ports & 0xFF) == 8 ? 8u : 0u;
+    return proto == 1;
+}
+
+// __policy_can_access (policy.h:46-110) with cb[CB_POLICY] == 0, split in
+// two halves so the first probe overlaps other headers' lookups:
+// policy_issue() filters the three keys and loads the first slot of the
+// first key that may exist; policy_resolve() walks the keys in the
+// reference's order (L4, L3, wildcard port; fragments: L3 only).
+struct PolicyProbe {
+    uint32_t id, pp;    // identity; dport | proto << 16
+    uint32_t eg;        // egress << 24
+    uint32_t maybe;     // bit j: key j may exist (and applies)
+    uint32_t j, s;      // key and slot of the issued probe (j = 3: none)
+    uint4 v;
+    // key j by masking, not by selecting among stored keys: the compiler
+    // turns a 3-way select on a per-lane index into a scratch-memory table
+    __device__ __forceinline__ uint32_t lo(uint32_t i) const
+    {
+        return id & (0u - (uint32_t)(i != 2));
+    }
+    __device__ __forceinline__ uint32_t hi(uint32_t i) const
+    {
+        return (pp & (0u - (uint32_t)(i != 1))) | eg;
+    }
+    __device__ __forceinline__ uint64_t key(uint32_t i) const
+    {
+        return ((uint64_t)hi(i) << 32) | lo(i);
+    }
+    __device__ __forceinline__ uint32_t pre(uint32_t i) const
+    {
+        return pol_key_pre(lo(i), hi(i));
+    }
+};
+
+__device__ __forceinline__ void policy_probe_key(const DevTables &T,
+                                                 uint32_t base, uint32_t mask,
+                                                 PolicyProbe &P)
+{
+    P.j = P.maybe ? __builtin_ctz(P.maybe) : 3;
+    if (P.j < 3) {
+        P.s = pol_slot(P.pre(P.j), mask);
+        P.v = ld16(T.pol + base + P.s);
+    }
+}
+
+__device__ __forceinline__ void policy_issue(const DevTables &T, const Lds &S,
+                                             uint32_t base, uint32_t mask,
+                                             uint32_t id, uint32_t dport,
+                                             uint32_t proto, uint32_t egress,
+                                             bool frag, PolicyProbe &P)
+{
+    // keys 0: L4 {id, dport, proto}, 1: L3 {id, 0, 0}, 2: wildcard port
+    // {0, dport, proto}, all with the direction bit
+    P.id = id;
+    P.pp = dport | (proto << 16);
+    P.eg = egress << 24;
+    P.maybe = frag ? 2u : 7u;                // policy.h:61,85
+    if (S.polb) {
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(0))))
+            P.maybe &= ~1u;
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(1))))
+            P.maybe &= ~2u;
+        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(2))))
+            P.maybe &= ~4u;
+    }
+    policy_probe_key(T, base, mask, P);
+}
+
+// Returns the verdict (<0 drop) and the matched counter (or NONE).  Works
+// on register copies of the probe state (writing through a pointer into the
+// per-header state array would keep that array out of registers).
+struct PolicyResult {
+    int verdict;
+    uint32_t ctr;
+};
+__device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
+                                                       uint32_t base,
+                                                       uint32_t mask,
+                                                       const PolicyProbe &P0)
+{
+    uint32_t maybe = P0.maybe, j = P0.j, s = P0.s;
+    uint4 v = P0.v;
+    uint32_t ctr = NONE;
+    int verdict = DROP_POLICY;   // (DROP_FRAG_NOSUPPORT also -> DROP_POLICY)
+    while (j < 3) {
+        const uint64_t want = P0.key(j);
+        bool hit = false;
+        for (;;) {
+            const uint64_t key = ((uint64_t)v.y << 32) | v.x;
+            if (key == want) {
+                hit = true;
+                break;
+            }
+            if (key == POL_EMPTY)
+                break;
+            s = (s + 1) & mask;
+            v = ld16(T.pol + base + s);
+        }
+        if (hit) {
+            ctr = v.w;
+            verdict = j == 1 ? TC_ACT_OK : (int)(v.z & 0xFFFF);
+            break;
+        }
+        maybe &= ~(1u << j);   // a false positive of the filter
+        j = maybe ? __builtin_ctz(maybe) : 3;
+        if (j < 3) {
+            s = pol_slot(P0.pre(j), mask);
+            v = ld16(T.pol + base + s);
+        }
+    }
+    return PolicyResult{verdict, ctr};
+}
+
+__device__ __forceinline__ PolicyResult policy_access(
+    const DevTables &T, const Lds &S, uint32_t base, uint32_t mask, uint32_t id,
+    uint32_t dport, uint32_t proto, uint32_t egress, bool frag)
+{
+    PolicyProbe P;
+    policy_issue(T, S, base, mask, id, dport, proto, egress, frag, P);
+    return policy_resolve(T, base, mask, P);
+}
+
+// Per-thread update_metrics counts (bytes in u32: a thread sees at most
+// 65536 headers between flushes, 65536 x 65535 < 2^32).
+template <int N>
+struct MetAcc {
+    uint32_t cnt[N > 0 ? N : 1], byt[N > 0 ? N : 1];
+    __device__ __forceinline__ void clear()
+    {
+#pragma unroll
+        for (int k = 0; k < N; k++)
+            cnt[k] = byt[k] = 0;
+    }
+    __device__ __forceinline__ void add(uint32_t key, uint32_t len)
+    {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            const bool m = key == (uint32_t)k;
+            cnt[k] += m;
+            byt[k] += m ? len : 0u;
+        }
+    }
+    // whole-wave sums into the LDS histogram (uniform control flow)
+    __device__ __forceinline__ void flush(unsigned long long *s_met)
+    {
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            uint32_t c = cnt[k];
+            uint64_t b = byt[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                c += __shfl_xor(c, o);
+                b += __shfl_xor(b, o);
+            }
+            if ((threadIdx.x & 63) == 0 && c) {
+                atomicAdd(&s_met[2 * k], (unsigned long long)c);
+                atomicAdd(&s_met[2 * k + 1], (unsigned long long)b);
+            }
+        }
+        clear();
+    }
+};
+
+template <class W>
+__device__ __forceinline__ void lds_copy(W *dst, const W *src, uint32_t n)
+{
+    for (uint32_t j = threadIdx.x; j < n; j += BLOCK)
+        dst[j] = src[j];
+}
+
+}  // namespace
+
+}  // namespace cfc

@@ -151,6 +151,72 @@ constexpr uint32_t POL_BLOOM_MAX_WORDS = 8192;    // 32 KiB
 constexpr uint32_t PF_BLOOM_MAX_WORDS = 8192;     // 32 KiB
 constexpr uint32_t LXC_LDS_MAX_SLOTS = 512;       // 8 KiB of endpoint slots
 
+// ---- IPv6 LPM: one hash table over every (prefix, length), probed longest
+// length first, screened by a blocked Bloom filter.
+// A 1M-prefix ipcache cannot be cache-resident whatever its layout (>= 16 MB
+// of keys), so the layout minimises Infinity-Cache accesses: the slots are
+// touched about once per lookup and everything before that is L2-resident.
+//   slots   32 bytes: masked address as host-order words (w[0] = bits 0-31),
+//           label, length (0 = free slot); linear probing, load <= 50%
+//   lens    the lengths present (> 0), longest first:
+//           len | sel << 8 | L6_GROUP_FIRST; consecutive lengths form a
+//           group sharing one Bloom word, chosen by the address masked to
+//           the group's shortest length `sel` (so one 8-byte load screens
+//           the whole group), the bits by the key itself
+//   bloom   u64 words; key (m, len) sets bits (h >> 20) & 63 and h >> 26,
+//           h = l6_hash(m, len); the slot index is h & mask
+// A /0 prefix is def_label (no probe).  The builder closes a group when the
+// addresses masked to the next length would pile more than L6_GROUP_MAX keys
+// into one word.
+constexpr uint32_t L6_GROUP_FIRST = 1u << 16;
+constexpr uint32_t L6_GROUP_MAX = 4;
+struct alignas(16) L6Slot {
+    uint32_t w[4];
+    uint32_t label;
+    uint32_t len;
+    uint32_t pad[2];
+};
+struct Lpm6 {
+    const L6Slot *slots;           // null: empty
+    const uint64_t *bloom;
+    const uint32_t *lens;
+    uint32_t mask;                 // slots - 1
+    uint32_t bloom_mask;           // words - 1
+    uint32_t nlen;                 // entries of lens
+    uint32_t def_label;            // label of ::/0 (0: none)
+};
+__host__ __device__ inline uint32_t l6_word_mask(uint32_t len, int i)
+{
+    const int b = (int)len - 32 * i;   // bits of word i inside the prefix
+    return b >= 32 ? 0xFFFFFFFFu : b <= 0 ? 0u : 0xFFFFFFFFu << (32 - b);
+}
+__host__ __device__ inline uint32_t l6_hash(uint32_t w0, uint32_t w1, uint32_t w2,
+                                            uint32_t w3, uint32_t tag)
+{
+    return fmix32(w0 * 0x9E3779B1u + w1 * 0x85EBCA77u + w2 * 0xC2B2AE3Du +
+                  w3 * 0x27D4EB2Fu + tag * 0x165667B1u);
+}
+// Bloom word of a group with shortest length sel / key bits of (m, len)
+__host__ __device__ inline uint32_t l6_group_hash(const uint32_t w[4], uint32_t sel)
+{
+    return l6_hash(w[0] & l6_word_mask(sel, 0), w[1] & l6_word_mask(sel, 1),
+                   w[2] & l6_word_mask(sel, 2), w[3] & l6_word_mask(sel, 3),
+                   sel | 0x100u);
+}
+__host__ __device__ inline uint64_t l6_bloom_bits(uint32_t h)
+{
+    return (1ull << ((h >> 20) & 63)) | (1ull << (h >> 26));
+}
+
+// ---- IPv6 endpoints: 32-byte slots {raw address words, pol_base, pol_mask,
+// info (as LxcSlot.info), 0}, linear probing on l6_hash(raw, L6_LXC_TAG)
+constexpr uint32_t L6_LXC_TAG = 0x200u;
+struct alignas(16) Lxc6Slot {
+    uint32_t a[4];                 // network-order bytes, loaded LE
+    uint32_t pol_base, pol_mask, info, pad;
+};
+constexpr uint32_t LXC6_LDS_MAX_SLOTS = 256;      // 8 KiB
+
 struct DevTables {
     const uint32_t *l4c;           // compact IPv4 LPM nodes, or null
     const uint64_t *l4l;           // its prefix lists
@@ -171,6 +237,13 @@ struct DevTables {
     uint32_t pf_bloom_words;       // power of two, 0 = no filter
     uint32_t pol_bloom_words;      // power of two, 0 = no filter
     uint32_t lxc4_lds;             // 1: the endpoint table is copied to LDS
+    // IPv6
+    Lpm6 ipc6;                     // ipcache
+    Lpm6 pf6_fix;                  // prefilter exact /128 set (one length)
+    Lpm6 pf6_dyn;                  // prefilter LPM deny list
+    const Lxc6Slot *lxc6;          // null when no IPv6 endpoints
+    uint32_t lxc6_mask;
+    uint32_t lxc6_lds;             // 1: copied to LDS
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]

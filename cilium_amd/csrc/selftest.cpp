@@ -1,0 +1,123 @@
+// Host self-test of the IPv6 LPM flattener (flatten.cpp build_lpm6): the
+// lookup the device performs (lpm6_lookup_host restates k_classify_v6's
+// lpm6_lookup over the same image) against a brute-force longest-prefix
+// match, on prefix sets that exercise the Bloom grouping: random C3-like
+// sets, prefixes piled under one /48 or /64 (groups must split), a ::/0,
+// and label-0 prefixes that shadow shorter ones.  No GPU needed.
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "flatten.hpp"
+
+using namespace cfc;
+
+static uint32_t brute(const std::vector<Pfx6> &pfx, const uint32_t w[4])
+{
+    int best = -1;
+    uint32_t label = 0;
+    for (const Pfx6 &p : pfx) {
+        bool ok = true;
+        for (int i = 0; i < 4 && ok; i++)
+            ok = (w[i] & l6_word_mask(p.plen, i)) == p.w[i];
+        if (ok && (int)p.plen > best) {
+            best = p.plen;
+            label = p.label;
+        }
+    }
+    return label;
+}
+
+static void add(std::vector<Pfx6> &v, const uint32_t a[4], int len, uint32_t label)
+{
+    Pfx6 p;
+    p.plen = (uint8_t)len;
+    p.label = label;
+    for (int i = 0; i < 4; i++)
+        p.w[i] = a[i] & l6_word_mask(len, i);
+    for (const Pfx6 &q : v)
+        if (q.plen == p.plen && !memcmp(q.w, p.w, 16))
+            return;   // unique (prefix, length) like the map
+    v.push_back(p);
+}
+
+template <class R>
+static int run(const char *name, const std::vector<Pfx6> &pfx, R &rng,
+               int queries)
+{
+    Lpm6Host t;
+    build_lpm6(pfx, &t);
+    int bad = 0;
+    for (int q = 0; q < queries; q++) {
+        uint32_t w[4];
+        for (int i = 0; i < 4; i++)
+            w[i] = rng();
+        if (!pfx.empty() && (q & 3)) {   // mostly inside some prefix
+            const Pfx6 &p = pfx[rng() % pfx.size()];
+            for (int i = 0; i < 4; i++)
+                w[i] = p.w[i] | (w[i] & ~l6_word_mask(p.plen, i));
+        }
+        const uint32_t a = lpm6_lookup_host(t, w), b = brute(pfx, w);
+        if (a != b && bad++ < 5)
+            printf("%s: %08x:%08x:%08x:%08x -> %u, want %u\n", name, w[0], w[1],
+                   w[2], w[3], a, b);
+    }
+    printf("%-12s prefixes %5zu lengths %3zu groups %3u bloom %6zu slots %6zu: %s\n",
+           name, pfx.size(), t.lens.size(), t.groups, t.bloom.size(), t.slots.size(),
+           bad ? "FAIL" : "ok");
+    return bad != 0;
+}
+
+int main()
+{
+    std::mt19937 gen(12345);
+    auto rng = [&gen]() -> uint32_t { return (uint32_t)gen(); };
+    int fail = 0;
+    {   // C3-like: /32../128, mass at /48 /56 /64 /128
+        const int lens[] = {32, 40, 48, 48, 48, 56, 56, 64, 64, 64, 96, 128, 128};
+        std::vector<Pfx6> v;
+        for (int i = 0; i < 3000; i++) {
+            uint32_t a[4] = {0x20000000u | (rng() & 0x0FFFFFFFu), rng(), rng(), rng()};
+            add(v, a, lens[rng() % 13], 256 + i);
+        }
+        fail |= run("c3-like", v, rng, 20000);
+    }
+    {   // piled: pods (/128) under few /64s, /64s under one /48, a /0
+        std::vector<Pfx6> v;
+        uint32_t base[4] = {0x20010db8u, 0x00050000u, 0, 0};
+        add(v, base, 48, 1000);
+        for (int n = 0; n < 40; n++) {
+            uint32_t a[4] = {base[0], base[1] | (rng() & 0xFFFF), rng(), rng()};
+            add(v, a, 64, 2000 + n);
+            for (int k = 0; k < 30; k++) {
+                uint32_t b[4] = {a[0], a[1], rng(), rng()};
+                add(v, b, 128, 5000 + 100 * n + k);
+            }
+        }
+        uint32_t z[4] = {0, 0, 0, 0};
+        add(v, z, 0, 7);
+        fail |= run("piled", v, rng, 20000);
+    }
+    {   // every length 1..128, label 0 shadows, overlapping chains
+        std::vector<Pfx6> v;
+        uint32_t a[4] = {0x20010db8u, 0x12345678u, 0x9abcdef0u, 0x0fedcba9u};
+        for (int len = 1; len <= 128; len++)
+            add(v, a, len, (len % 7) ? 100 + len : 0);
+        for (int i = 0; i < 500; i++) {
+            uint32_t b[4] = {rng(), rng(), rng(), rng()};
+            add(v, b, 1 + rng() % 128, (i % 5) ? 300 + i : 0);
+        }
+        fail |= run("all-lengths", v, rng, 20000);
+    }
+    {   // exact /128 set (the prefilter's fix map) and an empty table
+        std::vector<Pfx6> v;
+        for (int i = 0; i < 5000; i++) {
+            uint32_t a[4] = {rng(), rng(), rng(), rng()};
+            add(v, a, 128, 1);
+        }
+        fail |= run("exact128", v, rng, 20000);
+        fail |= run("empty", std::vector<Pfx6>(), rng, 1000);
+    }
+    return fail;
+}

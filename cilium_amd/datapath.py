@@ -3,8 +3,8 @@
 Two halves, as in include/cfc.h:
   * the pkg/bpf-shaped map API (`open_or_create_map`, `update_element`, ...)
     that pkg/maps/* mirrors in this package build on;
-  * `classify_v4`, the batched replacement of the reference's per-packet
-    programs, over torch tensors resident on the GPU.
+  * `classify_v4` / `classify_v6`, the batched replacement of the
+    reference's per-packet programs, over torch tensors resident on the GPU.
 """
 from __future__ import annotations
 
@@ -28,6 +28,20 @@ class HeaderBatchV4:
 
 
 @dataclasses.dataclass
+class HeaderBatchV6:
+    """Device SoA batch of IPv6 headers: saddr/daddr int32 tensors of shape
+    (n, 4) (16 network-order bytes per address), the rest as in V4."""
+    saddr: "torch.Tensor"
+    daddr: "torch.Tensor"
+    ports: "torch.Tensor"
+    meta: "torch.Tensor"      # proto | flags << 8 | len << 16 (HF_EXTHDR)
+    mark: "torch.Tensor | None" = None
+
+    def __len__(self):
+        return int(self.ports.numel())
+
+
+@dataclasses.dataclass
 class Verdicts:
     verdict: "torch.Tensor"   # int32
     identity: "torch.Tensor"  # int32 (u32 bits)
@@ -47,6 +61,27 @@ def pack_v4(h, device="cuda"):
                                 .view(np.int32)).to(device)
     return HeaderBatchV4(t(h.saddr), t(h.daddr), t(ports), t(meta),
                          t(h.mark) if h.mark is not None else None)
+
+
+def pack_v6(h, device="cuda"):
+    """synth.Headers (family 6, numpy) -> HeaderBatchV6 on `device`.  The
+    synth flag HF_EXTHDR (4) becomes the ABI's CFC_HF_EXTHDR bit."""
+    import numpy as np
+    import torch
+    ports = (h.sport.astype(np.uint32) | (h.dport.astype(np.uint32) << 16))
+    meta = (h.proto.astype(np.uint32) | (h.flags.astype(np.uint32) << 8)
+            | (h.length.astype(np.uint32) << 16))
+
+    def t(a):
+        return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
+    return HeaderBatchV6(t(np.ascontiguousarray(h.saddr, np.uint8)).view(-1, 4),
+                         t(np.ascontiguousarray(h.daddr, np.uint8)).view(-1, 4),
+                         t(ports), t(meta),
+                         t(h.mark.astype(np.uint32)) if h.mark is not None else None)
+
+
+def pack(h, device="cuda"):
+    return pack_v4(h, device) if h.family == 4 else pack_v6(h, device)
 
 
 def _ptr(t):
@@ -183,6 +218,39 @@ class Datapath:
                                        self._stream(stream)),"classify")
         return out
 
+    def classify_v6(self, batch: HeaderBatchV6, mode=L.MODE_INGRESS, ep_lxc=0,
+                    out: Verdicts | None = None, want_action=True,
+                    stream=None) -> Verdicts:
+        import torch
+        n = len(batch)
+        dev = batch.ports.device
+        if out is None:
+            out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
+                           torch.empty(n, dtype=torch.int32, device=dev),
+                           torch.empty(n, dtype=torch.uint8, device=dev)
+                           if want_action else None)
+        for t in (batch.saddr, batch.daddr):
+            assert t.is_cuda and t.is_contiguous() and t.dtype == torch.int32
+            assert t.shape == (n, 4) and t.data_ptr() % 16 == 0
+        for t in (batch.ports, batch.meta):
+            assert t.is_cuda and t.is_contiguous() and t.numel() == n
+            assert t.dtype == torch.int32
+        if batch.mark is not None:
+            assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
+        hdr = L.HdrV6(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+                      _ptr(batch.meta), _ptr(batch.mark), n)
+        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action))
+        L.check(self.L.cfc_classify_v6(self.h, ctypes.byref(hdr),
+                                       ctypes.byref(o), mode, ep_lxc,
+                                       self._stream(stream)), "classify v6")
+        return out
+
+    def classify(self, batch, mode=L.MODE_INGRESS, ep_lxc=0, **kw) -> Verdicts:
+        """classify_v4 or classify_v6 by the batch's family."""
+        if isinstance(batch, HeaderBatchV6):
+            return self.classify_v6(batch, mode, ep_lxc, **kw)
+        return self.classify_v4(batch, mode, ep_lxc, **kw)
+
     def counters_sync(self, stream=None):
         L.check(self.L.cfc_counters_sync(self.h, self._stream(stream)),
                 "counters sync")
@@ -224,5 +292,5 @@ def errno_name(e: OSError):
     return errno.errorcode.get(e.errno, str(e.errno))
 
 
-__all__ = ["Datapath", "HeaderBatchV4", "Verdicts", "pack_v4", "host_only",
-           "errno_name"]
+__all__ = ["Datapath", "HeaderBatchV4", "HeaderBatchV6", "Verdicts", "pack_v4",
+           "pack_v6", "pack", "host_only", "errno_name"]

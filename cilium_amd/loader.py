@@ -39,11 +39,19 @@ def load_tables(dp: Datapath, t, commit=True):
                                     cidrmap.maxHKeys)
         dyn4 = cidrmap.OpenMapElems(dp, cidrmap.MapName + "v4_dyn", 32, True,
                                     cidrmap.maxLKeys)
+        fam = set(int(f) for f in t.prefilter["family"])
+        if 2 in fam:
+            fix6 = cidrmap.OpenMapElems(dp, cidrmap.MapName + "v6_fix", 128, False,
+                                        cidrmap.maxHKeys)
+            dyn6 = cidrmap.OpenMapElems(dp, cidrmap.MapName + "v6_dyn", 128, True,
+                                        cidrmap.maxLKeys)
         for p in t.prefilter:
-            if int(p["family"]) != 1:
-                continue
-            key = struct.pack("<I", int(p["plen"])) + bytes(p["addr"][:4])
-            dp.update_element((dyn4 if p["dyn"] else fix4).Fd, key, b"\x00")
+            if int(p["family"]) == 1:
+                key = struct.pack("<I", int(p["plen"])) + bytes(p["addr"][:4])
+                dp.update_element((dyn4 if p["dyn"] else fix4).Fd, key, b"\x00")
+            else:
+                key = struct.pack("<I", int(p["plen"])) + bytes(p["addr"])
+                dp.update_element((dyn6 if p["dyn"] else fix6).Fd, key, b"\x00")
     if commit:
         dp.commit()
     return pms

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 2
+#define CFC_ABI_VERSION 3
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -145,6 +145,22 @@ typedef struct {
     uint64_t n;
 } cfc_hdr_v4;
 
+/* Device-resident SoA batch of IPv6 headers.  saddr/daddr: n addresses of
+ * 16 network-order bytes each (16-byte aligned).  ports, meta and mark as in
+ * cfc_hdr_v4, where meta's proto is the next header ipv6_hdrlen() stops at
+ * (ipv6.h:61-98; 44 FRAGMENT and 59 NONE end in drops) and CFC_HF_EXTHDR
+ * says extension headers precede it; CFC_HF_FRAG is ignored (ipv6_policy
+ * passes is_fragment = false). */
+#define CFC_HF_EXTHDR 0x400u
+typedef struct {
+    const uint8_t *saddr;
+    const uint8_t *daddr;
+    const uint32_t *ports;
+    const uint32_t *meta;
+    const uint32_t *mark;
+    uint64_t n;
+} cfc_hdr_v6;
+
 /* Outputs (device pointers, n elements; action may be NULL).
  *  verdict : bpf/lib/policy.h convention — <0 drop reason (DROP_*, or
  *            CFC_DROP_PREFILTER for an XDP prefilter drop), 0 forwarded,
@@ -155,6 +171,10 @@ typedef struct {
  *            (TC_ACT_OK 0 / TC_ACT_SHOT 2 / TC_ACT_REDIRECT 7, or XDP_DROP 1 /
  *            XDP_PASS 2 in XDP mode and for prefilter drops in FULL mode). */
 #define CFC_DROP_PREFILTER (-1)
+/* IPv6 only: an ICMPv6 neighbour solicitation, or an echo request to the
+ * router address, that the reference answers itself (icmp6_handle,
+ * icmp6.h:390-412) instead of classifying; action TC_ACT_OK. */
+#define CFC_VERDICT_PUNT (-2)
 typedef struct {
     int32_t *verdict;
     uint32_t *identity;
@@ -164,6 +184,11 @@ typedef struct {
 /* Classify a batch (asynchronous on `stream`).  Policy-entry and metrics
  * counters accumulate on the device until cfc_counters_sync(). */
 int cfc_classify_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream);
+/* The IPv6 chain: bpf_netdev.c handle_ipv6 (:172-275) -> bpf_lxc.c
+ * ipv6_policy (:753-895); egress ipv6_l3_from_lxc (:112-436); XDP check_v6
+ * (bpf_xdp.c:132-156).  Same outputs and counters as cfc_classify_v4. */
+int cfc_classify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
 
 /* ---------------------------------------------------------------- counters */
@@ -199,6 +224,13 @@ typedef struct {
     uint32_t prefilter_v4_dyn;
     uint32_t lpm4_layout;       /* CFC_LPM4_DIR24_8 / _TRIE, 0 = empty */
     uint32_t lpm4_kib;          /* device KiB of the IPv4 ipcache layout */
+    uint32_t ipcache_v6_prefixes;
+    uint32_t lpm6_lengths;      /* distinct IPv6 prefix lengths (> 0) */
+    uint32_t lpm6_groups;       /* Bloom groups over them */
+    uint32_t lpm6_kib;          /* device KiB of the IPv6 ipcache layout */
+    uint32_t endpoints_v6;
+    uint32_t prefilter_v6_fix;
+    uint32_t prefilter_v6_dyn;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(_lib.EXPORTS) == fns
-    assert L.cfc_abi_version() == 2
+    assert L.cfc_abi_version() == 3
     assert L.cfc_num_possible_cpus() == 1
 
 
@@ -181,3 +181,16 @@ def test_metrics_map_owned_by_datapath():
     # geometry of the datapath-owned map is fixed
     with pytest.raises(OSError):
         dp.open_or_create_map("cilium_metrics", 1, 8, 16, 65536)
+
+
+def test_flattener_selftest():
+    """The IPv6 LPM image (Bloom groups, hash slots) answers like a brute-force
+    longest-prefix match (cilium_amd/csrc/selftest.cpp, host only)."""
+    import subprocess
+    csrc = os.path.join(ROOT, "cilium_amd", "csrc")
+    exe = os.path.join(csrc, "build", "selftest")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", csrc, "-s", "selftest"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": ok") == 5, r.stdout

@@ -11,7 +11,7 @@ import oracle as O
 from cilium_amd import synth as S
 from cilium_amd import _lib as L
 from cilium_amd import metricsmap
-from cilium_amd.datapath import Datapath, pack_v4
+from cilium_amd.datapath import Datapath, pack, pack_v4
 from cilium_amd.loader import load_tables, policy_rows
 
 pytestmark = pytest.mark.gpu
@@ -31,9 +31,9 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     dp = Datapath(0)
     dp.set_option(L.OPT_LPM4, lpm4)
     pms = load_tables(dp, t)
-    if lpm4 != L.LPM4_AUTO and len(t.ipcache):
+    if lpm4 != L.LPM4_AUTO and (t.ipcache["family"] == 1).any():
         assert dp.stats()["lpm4_layout"] == lpm4
-    b = pack_v4(h)
+    b = pack(h)
     n = len(h)
     act = np.empty(n, np.int32)
     ver = np.empty(n, np.int32)
@@ -41,10 +41,9 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     step = (n + chunks - 1) // chunks
     for a in range(0, n, step):
         sl = lambda x: x[a:a + step] if x is not None else None   # noqa: E731
-        from cilium_amd.datapath import HeaderBatchV4
-        sub = HeaderBatchV4(sl(b.saddr), sl(b.daddr), sl(b.ports), sl(b.meta),
-                            sl(b.mark))
-        out = dp.classify_v4(sub, mode, ep_lxc)
+        sub = type(b)(sl(b.saddr), sl(b.daddr), sl(b.ports), sl(b.meta),
+                      sl(b.mark))
+        out = dp.classify(sub, mode, ep_lxc)
         torch.cuda.synchronize()
         act[a:a + step] = out.action.cpu().numpy()
         ver[a:a + step] = out.verdict.cpu().numpy()
@@ -211,3 +210,116 @@ def test_counters_accumulate_across_batches_and_updates(torch):
     exp = rows[(k.Identity, k.DestPort, k.Nexthdr, k.TrafficDirection)]
     assert (after.Packets, after.Bytes) == (exp[5], exp[6])
     dp.close()
+
+
+# ------------------------------------------------------------------ IPv6
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_c3_vs_oracle(torch, mode):
+    """C3-shaped dual-stack tables (200k IPv6 + 20k IPv4 prefixes, 20k-entry
+    prefilter), 1M IPv6 headers, every mode."""
+    t = S.config_c3(3, n_prefixes=200_000, n_v4_prefixes=20_000,
+                    n_endpoints=3, n_prefilter=20_000)
+    rng = np.random.default_rng(30 + mode)
+    if mode == 1:
+        ipc6 = t.ipcache[t.ipcache["family"] == 2]
+        h = S.gen_headers_v6(rng, 1_000_000, ipc6, S.local_v6_addrs(t),
+                             local_frac=0.1, src_fixed=S.LXC_IPV6, ext=0.05,
+                             exthdr_drop=0.01, mark_host=0, mark_proxy=0)
+        h.daddr = S._addr_in_prefix_v6(rng, ipc6, rng.integers(0, len(ipc6), size=len(h)))
+        r = rng.random(len(h))
+        loc = S.local_v6_addrs(t)
+        h.daddr[r < 0.1] = loc[rng.integers(0, len(loc), size=int((r < 0.1).sum()))]
+        cl = r > 0.97
+        h.daddr[cl, :8] = S.ROUTER_IPV6[:8]
+        h.saddr[rng.random(len(h)) < 0.01] = S.ip6("2001:db8::dead")
+    else:
+        h = S.headers_c3(t, 1_000_000, seed=31 + mode, ext=0.05, exthdr_drop=0.01,
+                         local_frac=0.9)
+        if mode in (2, 3):
+            fix = t.prefilter[(t.prefilter["family"] == 2) & (t.prefilter["dyn"] == 0)]
+            sel = rng.random(len(h)) < 0.2
+            h.saddr[sel] = fix["addr"][rng.integers(0, len(fix), size=int(sel.sum()))]
+    # punted ICMPv6 (NS, echo request to the router) in every mode
+    k = np.arange(0, len(h), 997)
+    h.proto[k] = 58
+    h.sport[k] = np.where(k % 2, 135, 128).astype(np.uint16)
+    h.daddr[k[k % 4 == 0]] = S.ROUTER_IPV6
+    act, ver = compare_with_oracle(torch, t, h, mode, ep_lxc=S.EP_LXC_ID, chunks=2)
+    assert len(np.unique(ver)) >= 3
+
+
+def _v6_entries(rng, specs):
+    out = []
+    for n, lens, labels in specs:
+        a = rng.integers(0, 256, size=(n, 16), dtype=np.uint16).astype(np.uint8)
+        a[:, 0] = 0x20 | (a[:, 0] & 0x0F)
+        out.append(S._v6_entries(a, rng.choice(lens, size=n), labels))
+    e = np.concatenate(out)
+    _, u = np.unique(np.concatenate([e["plen"][:, None], e["addr"]], 1), axis=0,
+                     return_index=True)
+    return e[np.sort(u)]
+
+
+def test_v6_edge_tables(torch):
+    """Every length /1-/128, labels >= 2^30, 0 (shadowing shorter prefixes),
+    HOST and CLUSTER, a ::/0 entry; prefixes piled under one /48 and /64
+    (the Bloom groups split); a dynamic v6 prefilter."""
+    rng = np.random.default_rng(17)
+    ipc = _v6_entries(rng, [(20000, np.arange(1, 129), 256 + np.arange(20000) % 5000)])
+    ipc["label"][:200] = 0x40000000 + np.arange(200)
+    ipc["label"][200:400] = 0
+    ipc["label"][400:450] = S.HOST_ID
+    ipc["label"][450:500] = S.CLUSTER_ID
+    base = S.ip6("2001:db8:5::")
+    pods = np.tile(base, (3000, 1))
+    pods[:, 6:8] = rng.integers(0, 4, size=(3000, 2))
+    pods[:, 8:] = rng.integers(0, 256, size=(3000, 8))
+    piled = np.concatenate([
+        S._v6_entries(pods, [128] * 3000, 9000 + np.arange(3000)),
+        S._v6_entries(pods[:40], [64] * 40, 8000 + np.arange(40)),
+        S._v6_entries(base[None, :], [48], [7777]),
+        S._v6_entries(np.zeros((1, 16), np.uint8), [0], [77])])
+    ipc = np.concatenate([ipc, piled])
+    _, u = np.unique(np.concatenate([ipc["plen"][:, None], ipc["addr"]], 1), axis=0,
+                     return_index=True)
+    ipc = ipc[np.sort(u)]
+    t = S.config_c3(5, n_prefixes=10, n_v4_prefixes=10, n_policy=10, n_prefilter=0)
+    t.ipcache = ipc
+    idents = np.unique(ipc["label"])
+    t.policy = {S.EP_LXC_ID: S.gen_policy(rng, 4000, idents, proxy_frac=0.1)}
+    pf = np.zeros(600, S.PREFILTER_DT)
+    pf["family"] = 2
+    pf["dyn"] = 1
+    pa = rng.integers(0, 256, size=(600, 16), dtype=np.uint16).astype(np.uint8)
+    pa[:, 0] = 0x30 | (pa[:, 0] & 0x0F)
+    pl = rng.integers(8, 129, size=600)
+    pf["plen"] = pl
+    pf["addr"] = S.mask_v6(pa, pl)
+    _, u = np.unique(np.concatenate([pf["plen"][:, None], pf["addr"]], 1), axis=0,
+                     return_index=True)
+    t.prefilter = pf[np.sort(u)]
+    h = S.headers_c3(t, 600_000, seed=17, ext=0.05, local_frac=0.9)
+    h.saddr[::5] = S._addr_in_prefix_v6(rng, t.ipcache[-3100:],
+                                        rng.integers(0, 3100, size=len(h.saddr[::5])))
+    h.saddr[1::7] = S._addr_in_prefix_v6(rng, t.prefilter, rng.integers(0, len(t.prefilter), size=len(h.saddr[1::7])))
+    dp = Datapath(0)
+    load_tables(dp, t)
+    st = dp.stats()
+    dp.close()
+    assert st["lpm6_lengths"] == 128 and st["lpm6_groups"] >= 2, st
+    for mode in (0, 3):
+        compare_with_oracle(torch, t, h, mode)
+
+
+def test_v6_only_endpoints_and_empty(torch):
+    """No IPv4 state at all; then no tables at all."""
+    t = S.config_c3(8, n_prefixes=5000, n_v4_prefixes=10, n_policy=500, n_prefilter=0)
+    t.ipcache = t.ipcache[t.ipcache["family"] == 2]
+    t.endpoints = t.endpoints[t.endpoints["family"] == 2]
+    h = S.headers_c3(t, 100_000, seed=8)
+    for mode in (0, 2, 3):
+        compare_with_oracle(torch, t, h, mode)
+    e = S.Tables(np.zeros(0, S.IPCACHE_DT), np.zeros(0, S.ENDPOINT_DT), {},
+                 np.zeros(0, S.PREFILTER_DT), {})
+    for mode in (0, 2, 3):
+        compare_with_oracle(torch, e, h, mode)
