@@ -245,7 +245,8 @@ def test_c3_vs_oracle(torch, mode):
     h.sport[k] = np.where(k % 2, 135, 128).astype(np.uint16)
     h.daddr[k[k % 4 == 0]] = S.ROUTER_IPV6
     act, ver = compare_with_oracle(torch, t, h, mode, ep_lxc=S.EP_LXC_ID, chunks=2)
-    assert len(np.unique(ver)) >= 3
+    # XDP verdicts are pass/drop only; the tc modes also see proxy ports
+    assert len(np.unique(ver)) >= (2 if mode == 2 else 3)
 
 
 def _v6_entries(rng, specs):
