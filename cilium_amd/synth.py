@@ -23,7 +23,8 @@ import numpy as np
 HOST_ID, WORLD_ID, CLUSTER_ID, HEALTH_ID, INIT_ID = 1, 2, 3, 4, 5
 # header flag bits (cfc.h CFC_HF_*)
 HF_FRAG = 1          # ipv4_is_fragment(): frag_off & htons(0xBFFF)
-HF_TCP_CLOSE = 2     # TCP RST or FIN set (conntrack.h:533)
+HF_TCP_CLOSE = 2     # ct_lookup's "rst || fin" (conntrack.h:533): bit 0 of
+                     # TCP byte 12, where union tcp_flags' bitfields all sit
 HF_EXTHDR = 4        # IPv6: extension headers precede `proto`
 IPPROTO_ICMP, IPPROTO_TCP, IPPROTO_UDP, IPPROTO_ICMPV6 = 1, 6, 17, 58
 
@@ -36,6 +37,13 @@ POLICY_DT = np.dtype([("identity", "<u4"), ("dport", "<u2"), ("proto", "u1"),
                       ("egress", "u1"), ("proxy_port", "<u2")])
 PREFILTER_DT = np.dtype([("family", "u1"), ("plen", "u1"),
                          ("addr", "u1", 16), ("dyn", "u1")])
+
+
+# one conntrack entry: which map (global or an endpoint's local maps, TCP or
+# ANY) and the raw struct ipv{4,6}_ct_tuple / struct ct_entry bytes
+# (bpf/lib/common.h:338-406)
+CT_DT = np.dtype([("family", "u1"), ("lxc", "<i4"), ("any", "u1"),
+                  ("tuple", "u1", 38), ("entry", "u1", 56)])
 
 
 def htons(x):
@@ -77,6 +85,7 @@ class Tables:
     policy: dict                             # lxc_id -> POLICY_DT array
     prefilter: np.ndarray                    # PREFILTER_DT
     seclabel: dict                           # lxc_id -> u32 (endpoint SECLABEL)
+    ct: np.ndarray = None                    # CT_DT pre-populated conntrack
 
 
 @dataclasses.dataclass
@@ -609,3 +618,48 @@ def config_c2_bench(seed=2, n_prefilter=25_000):
     pf["addr"][:, :4] = be32_to_bytes(byteswap32(host))
     t.prefilter = pf
     return t
+
+
+# ------------------------------------------------------------ conntrack
+def take(h: Headers, idx) -> Headers:
+    return Headers(h.family, h.saddr[idx], h.daddr[idx], h.sport[idx],
+                   h.dport[idx], h.proto[idx], h.flags[idx], h.length[idx],
+                   h.mark[idx])
+
+
+def concat(hs) -> Headers:
+    f = hs[0].family
+    cat = lambda k: np.concatenate([getattr(h, k) for h in hs])   # noqa: E731
+    return Headers(f, cat("saddr"), cat("daddr"), cat("sport"), cat("dport"),
+                   cat("proto"), cat("flags"), cat("length"), cat("mark"))
+
+
+def reverse(h: Headers) -> Headers:
+    """The packets travelling the other way: addresses and L4 ports swapped,
+    ICMP echo requests answered by echo replies (type 0 / 129)."""
+    icmp = h.proto == (IPPROTO_ICMP if h.family == 4 else IPPROTO_ICMPV6)
+    echo, reply = (8, 0) if h.family == 4 else (128, 129)
+    sport = np.where(icmp, h.sport, h.dport).astype(np.uint16)
+    dport = np.where(icmp, h.dport, h.sport).astype(np.uint16)
+    sport[icmp & ((h.sport & 0xFF) == echo)] = reply
+    return Headers(h.family, h.daddr.copy(), h.saddr.copy(), sport, dport,
+                   h.proto.copy(), (h.flags & np.uint8(0xFF ^ HF_TCP_CLOSE)).astype(np.uint8),
+                   h.length.copy(), np.zeros(len(h), np.uint32))
+
+
+CT_ROW = 104
+
+
+def ct_from_rows(rows: np.ndarray) -> np.ndarray:
+    """CT dump rows (u16 owner = lxc_id + 1 or 0 for the global maps,
+    u8 map (0 TCP / 1 ANY), u8 family, tuple[40], ct_entry[56], pad[4]) ->
+    CT_DT records."""
+    rows = np.asarray(rows, np.uint8).reshape(-1, CT_ROW)
+    ct = np.zeros(len(rows), CT_DT)
+    owner = rows[:, 0].astype(np.int32) | (rows[:, 1].astype(np.int32) << 8)
+    ct["lxc"] = owner - 1
+    ct["any"] = rows[:, 2]
+    ct["family"] = rows[:, 3]
+    ct["tuple"] = rows[:, 4:42]
+    ct["entry"] = rows[:, 44:100]
+    return ct

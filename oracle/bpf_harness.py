@@ -80,6 +80,11 @@ class Map:
             "<IIQQQ", self.fd, 0, ctypes.addressof(kb), ctypes.addressof(vb),
             flags))
 
+    def delete(self, key: bytes):
+        kb = ctypes.create_string_buffer(key, len(key))
+        _bpf(BPF_MAP_DELETE_ELEM, struct.pack("<IIQ", self.fd, 0,
+                                              ctypes.addressof(kb)))
+
     def lookup(self, key: bytes):
         kb = ctypes.create_string_buffer(key, len(key))
         vb = ctypes.create_string_buffer(self._vlen())

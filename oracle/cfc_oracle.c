@@ -38,6 +38,7 @@
 #define CT_EGRESS 0
 #define CT_INGRESS 1
 #define HF_FRAG 1
+#define HF_TCP_CLOSE 2
 #define ENDPOINT_F_HOST 1u
 #define MARK_MAGIC_HOST_MASK 0xF00u
 #define MARK_MAGIC_PROXY_INGRESS 0xA00u
@@ -196,6 +197,110 @@ static int lpm_lookup(const lpm *l, const uint8_t *addr, uint32_t *val)
     return 0;
 }
 
+/* ------------------------------------------------------------ conntrack */
+/* struct ct_entry (bpf/lib/common.h:380-406), 56 bytes */
+struct ctent {
+    uint64_t rx_packets, rx_bytes, tx_packets, tx_bytes;
+    uint32_t lifetime;
+    uint16_t bits;          /* rx_closing:1 tx_closing:1 nat46:1 lb_loopback:1
+                               seen_non_syn:1 */
+    uint16_t rev_nat_index, slave;
+    uint8_t tx_flags_seen, rx_flags_seen;
+    uint32_t src_sec_id, last_tx_report, last_rx_report;
+};
+_Static_assert(sizeof(struct ctent) == 56, "ct_entry is 56 bytes");
+#define CTB_RX_CLOSING 1u
+#define CTB_TX_CLOSING 2u
+#define CTB_SEEN_NON_SYN 16u
+
+/* CT map key as the oracle stores it: u16 owner (0 = the global maps
+ * cilium_ct{4,_any4,6,_any6}_global, else lxc_id + 1 for the endpoint's
+ * local maps, pkg/maps/ctmap/ctmap.go:59-69,403-425), u8 map kind
+ * (0 = TCP map, 1 = ANY map: get_ct_map4/6, bpf_lxc.c:91-107), u8 family,
+ * then struct ipv4_ct_tuple (14 B) / ipv6_ct_tuple (38 B)
+ * (common.h:338-367) zero padded to 40. */
+#define CTK 44
+#define TUPLE_F_OUT 0
+#define TUPLE_F_IN 1
+#define TUPLE_F_RELATED 2
+enum { CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3 };
+enum { ACTION_UNSPEC = 0, ACTION_CREATE = 1, ACTION_CLOSE = 2 };
+/* per-header CT byte (cfc.h CFC_CT_*): two lookup stages, the second being
+ * the destination endpoint's ingress policy after egress local delivery */
+#define CTO_DONE1 0x04u
+#define CTO_CREATE1 0x08u
+#define CTO_DONE2 0x40u
+#define CTO_CREATE2 0x80u
+
+static void ct_key(uint8_t k[CTK], uint16_t owner, uint8_t kind, int alen,
+                   const uint8_t *daddr, const uint8_t *saddr,
+                   uint16_t dport, uint16_t sport, uint8_t nexthdr,
+                   uint8_t flags)
+{
+    memset(k, 0, CTK);
+    memcpy(k, &owner, 2);
+    k[2] = kind;
+    k[3] = (uint8_t)(alen == 4 ? 1 : 2);
+    uint8_t *t = k + 4;
+    memcpy(t, daddr, alen);
+    memcpy(t + alen, saddr, alen);
+    memcpy(t + 2 * alen, &dport, 2);
+    memcpy(t + 2 * alen + 2, &sport, 2);
+    t[2 * alen + 4] = nexthdr;
+    t[2 * alen + 5] = flags;
+}
+
+/* The two keys ct_lookup4 / ct_lookup6 probe (conntrack.h:467-590,
+ * :310-437).  k1: the tuple as loaded — addresses as in the packet, the L4
+ * ports loaded into {dport, sport} (so swapped), flags TUPLE_F_OUT for
+ * ingress / TUPLE_F_IN for egress; a hit is CT_REPLY (CT_RELATED with
+ * TUPLE_F_RELATED).  k2: ipv{4,6}_ct_tuple_reverse(k1), a hit is
+ * CT_ESTABLISHED, a miss CT_NEW and k2 is what ct_create{4,6} stores.
+ * ICMP: ports zeroed; error types set TUPLE_F_RELATED; echo reply sets
+ * tuple->dport = ECHO; echo request sets tuple->sport = its type.
+ * Returns 0, or DROP_CT_UNKNOWN_PROTO for anything but TCP/UDP/ICMP. */
+static int ct_keys(int alen, uint16_t owner, const uint8_t *sa,
+                   const uint8_t *da, uint8_t proto, uint16_t sport,
+                   uint16_t dport, int close, int dir, uint8_t k1[CTK],
+                   uint8_t k2[CTK], int *action, uint16_t *td, uint16_t *ts)
+{
+    uint8_t fl = dir == CT_INGRESS ? TUPLE_F_OUT : TUPLE_F_IN;
+    const uint8_t icmp = alen == 4 ? 1 : 58;
+    *action = ACTION_UNSPEC;
+    *td = *ts = 0;
+    if (proto == icmp) {
+        uint8_t type = (uint8_t)(sport & 0xFF);
+        int related = alen == 4 ? (type == 3 || type == 11 || type == 12)
+                                : (type >= 1 && type <= 4);
+        uint8_t echo_reply = alen == 4 ? 0 : 129, echo = alen == 4 ? 8 : 128;
+        if (related)
+            fl |= TUPLE_F_RELATED;
+        else if (type == echo_reply)
+            *td = echo;
+        else {
+            if (type == echo)
+                *ts = type;
+            *action = ACTION_CREATE;
+        }
+    } else if (proto == 6) {
+        *action = close ? ACTION_CLOSE : ACTION_CREATE;
+        *td = sport;
+        *ts = dport;
+    } else if (proto == 17) {
+        *action = ACTION_CREATE;
+        *td = sport;
+        *ts = dport;
+    } else {
+        return DROP_CT_UNKNOWN_PROTO;
+    }
+    const uint8_t kind = proto == 6 ? 0 : 1;
+    ct_key(k1, owner, kind, alen, da, sa, *td, *ts, proto, fl);
+    ct_key(k2, owner, kind, alen, sa, da, *ts, *td, proto, fl ^ TUPLE_F_IN);
+    return 0;
+}
+
+static int64_t ct_find(const cfo_t *o, const uint8_t k[CTK]);
+
 /* ------------------------------------------------------------ tables */
 typedef struct {
     uint8_t key[8];      /* struct policy_key (common.h:180-186) raw bytes */
@@ -225,7 +330,28 @@ struct cfo {
     htab pf4_fix, pf6_fix; /* lpm_v{4,6}_key bytes (prefixlen + addr) */
     lpm pf4_dyn, pf6_dyn;
     uint64_t metrics[256][4][2];
+    /* conntrack: every CT map in one table, keyed by (owner, map kind,
+     * family, tuple) -> index into ct_ents */
+    htab ct;
+    struct ctent *ct_ents;
+    uint8_t *ct_live;
+    uint32_t ct_n, ct_cap, ct_added;
+    uint8_t ct_local[65536];   /* endpoint has its own (local) CT maps */
 };
+
+static uint16_t ct_owner(const cfo_t *o, uint16_t lxc)
+{
+    return o->ct_local[lxc] ? (uint16_t)(lxc + 1) : 0;
+}
+
+static int64_t ct_find(const cfo_t *o, const uint8_t k[CTK])
+{
+    int64_t s = ht_find(&o->ct, k);
+    if (s < 0)
+        return -1;
+    uint32_t idx = o->ct.vals[s];
+    return o->ct_live[idx] ? (int64_t)idx : -1;
+}
 
 cfo_t *cfo_new(void)
 {
@@ -237,6 +363,7 @@ cfo_t *cfo_new(void)
     ht_init(&o->lxc, 20);
     ht_init(&o->pf4_fix, 8);
     ht_init(&o->pf6_fix, 20);
+    ht_init(&o->ct, CTK);
     return o;
 }
 
@@ -251,6 +378,9 @@ void cfo_free(cfo_t *o)
     ht_free(&o->lxc);
     ht_free(&o->pf4_fix);
     ht_free(&o->pf6_fix);
+    ht_free(&o->ct);
+    free(o->ct_ents);
+    free(o->ct_live);
     for (int i = 0; i < 65536; i++)
         if (o->pol[i]) {
             ht_free(&o->pol[i]->idx);
@@ -427,50 +557,61 @@ static int policy_can_access(pmap *m, uint32_t identity, uint16_t dport,
     return frag ? DROP_FRAG_NOSUPPORT : DROP_POLICY;
 }
 
-/* Policy port of a CT_NEW packet as ct_lookup4 leaves tuple->dport
- * (bpf/lib/conntrack.h:496-584): TCP/UDP ports are loaded swapped, the
- * reverse lookup misses, ipv4_ct_tuple_reverse() swaps them back.
- * Returns 0 and sets *dp, or DROP_CT_UNKNOWN_PROTO. */
-static int ct_new_dport(uint8_t proto, uint16_t sport, uint16_t dport,
-                        uint16_t *dp)
-{
-    switch (proto) {
-    case 1: { /* IPPROTO_ICMP */
-        uint8_t type = (uint8_t)(sport & 0xFF);
-        uint16_t t_sport = 0, t_dport = 0;
-        if (type == 0)          /* ICMP_ECHOREPLY: tuple->dport = ICMP_ECHO */
-            t_dport = 8;
-        else if (type == 8)     /* ICMP_ECHO: tuple->sport = type */
-            t_sport = type;
-        (void)t_dport;
-        *dp = t_sport;          /* after reverse: dport <- sport */
-        return 0;
-    }
-    case 6:
-    case 17:
-        *dp = dport;
-        return 0;
-    default:
-        return DROP_CT_UNKNOWN_PROTO;
-    }
-}
-
 typedef struct {
     int32_t action, verdict;
     uint32_t identity;
 } res_t;
 
-static int ct6_new_dport(uint8_t proto, uint16_t sport, uint16_t dport,
-                         uint16_t *dp);
 
 /* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
  * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src; with
  * v6 set, ipv6_policy (:753-882) + tail_ipv6_policy (:884-895), which differ
  * only in the CT port derivation and pass is_fragment = false. */
-static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src,
-                         uint8_t proto, uint16_t sport, uint16_t dport,
-                         int frag, uint32_t len, int skip_proxy,
-                         int dir_missed, int v6)
+/* CT byte of the current header (CTO_*) */
+static _Thread_local uint8_t tl_ct;
+
+/* ct_lookup{4,6} against the tables as they were when the batch started:
+ * sets *res and the policy port (tuple->dport after the lookup: the
+ * packet's source port for CT_REPLY, its destination port otherwise). */
+static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
+                     const uint8_t *da, uint8_t proto, uint16_t sport,
+                     uint16_t dport, int close, int dir, int stage, int *res,
+                     uint16_t *pdport)
+{
+    uint8_t k1[CTK], k2[CTK];
+    int action;
+    uint16_t td, ts;
+    int ret = ct_keys(alen, owner, sa, da, proto, sport, dport, close, dir,
+                      k1, k2, &action, &td, &ts);
+    if (ret < 0)
+        return ret;
+    /* two map lookups in the reference; counted in L only when CT maps hold
+     * entries (an empty map cannot change a verdict) */
+    if (o->ct_added)
+        tl_lookups++;
+    if (ct_find(o, k1) >= 0) {
+        *res = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+        *pdport = td;
+    } else {
+        if (o->ct_added)
+            tl_lookups++;
+        *res = ct_find(o, k2) >= 0 ? CT_ESTABLISHED : CT_NEW;
+        *pdport = ts;
+    }
+    tl_ct |= (uint8_t)((*res | 4) << (4 * stage));
+    return 0;
+}
+
+/* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
+ * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src; with
+ * alen 16, ipv6_policy (:753-882) + tail_ipv6_policy (:884-895), which
+ * differ only in the CT tuple and pass is_fragment = false.  stage is 0 for
+ * an ingress batch, 1 after egress local delivery. */
+static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
+                         const uint8_t *sa, const uint8_t *da, uint8_t proto,
+                         uint16_t sport, uint16_t dport, int frag, int close,
+                         uint32_t len, int skip_proxy, int dir_missed,
+                         int stage)
 {
     res_t r = {TC_ACT_SHOT, 0, src};
     if (!o->pol[ep->lxc_id]) {
@@ -482,8 +623,9 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src,
         return r;
     }
     uint16_t pdport;
-    int ret = v6 ? ct6_new_dport(proto, sport, dport, &pdport)
-                 : ct_new_dport(proto, sport, dport, &pdport);
+    int res;
+    int ret = ct_lookup(o, alen, ct_owner(o, ep->lxc_id), sa, da, proto, sport,
+                        dport, close, CT_INGRESS, stage, &res, &pdport);
     if (ret < 0) {
         r.verdict = ret;
         metric(o, ret, METRIC_INGRESS, len);
@@ -491,14 +633,19 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src,
     }
     int verdict = policy_can_access(o->pol[ep->lxc_id], src, pdport, proto,
                                     CT_INGRESS, frag, len);
-    if (verdict < 0) { /* policy_can_access_ingress -> DROP_POLICY */
+    /* replies and related packets skip the policy verdict (:963-970); a
+     * denied CT_ESTABLISHED flow loses its entry (ct_delete4) */
+    if (res != CT_REPLY && res != CT_RELATED && verdict < 0) {
         r.verdict = DROP_POLICY;
         metric(o, DROP_POLICY, METRIC_INGRESS, len);
         return r;
     }
     if (skip_proxy)
         verdict = 0;
-    if (verdict > 0) { /* redirect_to_proxy: cb[CB_IFINDEX] = HOST_IFINDEX */
+    if (res == CT_NEW)
+        tl_ct |= (uint8_t)(CTO_CREATE1 << (4 * stage));   /* ct_create4 */
+    if (verdict > 0 && (res == CT_NEW || res == CT_ESTABLISHED)) {
+        /* redirect_to_proxy: cb[CB_IFINDEX] = HOST_IFINDEX */
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
         return r;
@@ -524,7 +671,7 @@ static uint32_t identity_from_mark(uint32_t mark, int *skip_proxy)
 /* from_netdev (FROM_HOST) -> handle_ipv4 (bpf_netdev.c:128-153, 357-453) */
 static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
                                uint8_t proto, uint16_t sport, uint16_t dport,
-                               int frag, uint32_t len, uint32_t mark)
+                               uint8_t hflags, uint32_t len, uint32_t mark)
 {
     int skip_proxy;
     uint32_t identity = identity_from_mark(mark, &skip_proxy);
@@ -540,14 +687,16 @@ static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
     const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
     if (!ep || (ep->flags & ENDPOINT_F_HOST))
         return r; /* to the stack (tunnel endpoints out of scope) */
-    return lxc_ingress(o, ep, identity, proto, sport, dport, frag, len,
+    return lxc_ingress(o, ep, identity, 4, (const uint8_t *)&saddr,
+                       (const uint8_t *)&daddr, proto, sport, dport,
+                       hflags & HF_FRAG, hflags & HF_TCP_CLOSE, len,
                        skip_proxy, METRIC_INGRESS, 0);
 }
 
 /* handle_ipv4_from_lxc (bpf_lxc.c:440-692) for endpoint lxc */
 static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
                            uint32_t daddr, uint8_t proto, uint16_t sport,
-                           uint16_t dport, int frag, uint32_t len)
+                           uint16_t dport, uint8_t hflags, uint32_t len)
 {
     res_t r = {TC_ACT_SHOT, 0, 0};
     const epinfo *self = lxc_lookup(o, 1, (const uint8_t *)&saddr);
@@ -556,8 +705,11 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         metric(o, DROP_INVALID_SIP, METRIC_EGRESS, len);
         return r;
     }
+    const uint8_t *sa = (const uint8_t *)&saddr, *da = (const uint8_t *)&daddr;
     uint16_t pdport;
-    int ret = ct_new_dport(proto, sport, dport, &pdport);
+    int res;
+    int ret = ct_lookup(o, 4, ct_owner(o, lxc), sa, da, proto, sport, dport,
+                        hflags & HF_TCP_CLOSE, CT_EGRESS, 0, &res, &pdport);
     if (ret < 0) {
         r.verdict = ret;
         metric(o, ret, METRIC_EGRESS, len);
@@ -565,7 +717,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     }
     uint32_t label = 0, dst;
     tl_lookups++;
-    if (lpm_lookup(&o->ipc4, (const uint8_t *)&daddr, &label) && label)
+    if (lpm_lookup(&o->ipc4, da, &label) && label)
         dst = label;
     else if ((daddr & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE)
         dst = CLUSTER_ID;
@@ -574,18 +726,20 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     r.identity = dst;
     int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
                                     CT_EGRESS, 0, len);
-    if (verdict < 0) {
+    if (res != CT_REPLY && res != CT_RELATED && verdict < 0) { /* :538-545 */
         r.verdict = DROP_POLICY;
         metric(o, DROP_POLICY, METRIC_EGRESS, len);
         return r;
     }
+    if (res == CT_NEW)
+        tl_ct |= CTO_CREATE1;                       /* ct_create4, :547-559 */
     if (verdict > 0) { /* proxy: redirect(HOST_IFINDEX), TRACE_TO_PROXY */
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
         return r;
     }
     tl_lookups++;
-    const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
+    const epinfo *ep = lxc_lookup(o, 1, da);
     if (ep) {
         if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST */
             metric(o, 0, METRIC_EGRESS, len);
@@ -595,8 +749,9 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         /* ipv4_local_delivery (l3.h:103-131): egress forward metric, then
          * the destination's policy program with src = SECLABEL */
         metric(o, 0, METRIC_EGRESS, len);
-        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], proto, sport, dport,
-                              frag, len, 0, METRIC_EGRESS, 0);
+        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 4, sa, da, proto, sport,
+                              dport, hflags & HF_FRAG, hflags & HF_TCP_CLOSE,
+                              len, 0, METRIC_EGRESS, 1);
         d.identity = dst;
         return d;
     }
@@ -633,7 +788,7 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, int nthreads)
+                     uint8_t *lookups, uint8_t *ct, int nthreads)
 {
     if (nthreads <= 0)
         nthreads = 1;
@@ -641,6 +796,7 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
     for (size_t i = 0; i < n; i++) {
         res_t r;
         tl_lookups = 0;
+        tl_ct = 0;
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v4(o, saddr[i], daddr[i]);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -649,21 +805,25 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                 identity[i] = 0;
                 if (lookups)
                     lookups[i] = (uint8_t)tl_lookups;
+                if (ct)
+                    ct[i] = 0;
                 continue;
             }
         }
         if (mode == CFO_MODE_EGRESS)
             r = lxc_egress_v4(o, ep_lxc, saddr[i], daddr[i], proto[i],
-                              sport[i], dport[i], flags[i] & HF_FRAG, len[i]);
+                              sport[i], dport[i], flags[i], len[i]);
         else
             r = netdev_ingress_v4(o, saddr[i], daddr[i], proto[i], sport[i],
-                                  dport[i], flags[i] & HF_FRAG, len[i],
+                                  dport[i], flags[i], len[i],
                                   mark ? mark[i] : 0);
         action[i] = r.action;
         verdict[i] = r.verdict;
         identity[i] = r.identity;
         if (lookups)
             lookups[i] = (uint8_t)tl_lookups;
+        if (ct)
+            ct[i] = tl_ct;
     }
 }
 
@@ -677,26 +837,6 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
 /* node_config.h:30 ROUTER_IP */
 static const uint8_t ROUTER_IP6[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0,
                                        0, 0, 0, 1, 0, 1, 0, 0};
-
-/* tuple->dport of a CT_NEW ct_lookup6 (conntrack.h:339-400): TCP/UDP ports
- * loaded swapped and swapped back by ipv6_ct_tuple_reverse(); an ICMPv6
- * echo request puts its type (128) in tuple->sport, which becomes the dport;
- * other ICMPv6 -> 0; anything else -> DROP_CT_UNKNOWN_PROTO. */
-static int ct6_new_dport(uint8_t proto, uint16_t sport, uint16_t dport,
-                         uint16_t *dp)
-{
-    switch (proto) {
-    case IPPROTO_ICMPV6:
-        *dp = (sport & 0xFF) == 128 ? 128 : 0;
-        return 0;
-    case 6:
-    case 17:
-        *dp = dport;
-        return 0;
-    default:
-        return DROP_CT_UNKNOWN_PROTO;
-    }
-}
 
 /* ipv6_hdrlen (ipv6.h:61-98): the header's proto is the next header the
  * extension-header walk stops at; NONE and FRAGMENT end in a drop. */
@@ -751,8 +891,9 @@ static res_t netdev_ingress_v6(cfo_t *o, const uint8_t *saddr,
     const epinfo *ep = lxc_lookup(o, 2, daddr);
     if (!ep || (ep->flags & ENDPOINT_F_HOST))
         return r;
-    return lxc_ingress(o, ep, identity, proto, sport, dport, 0, len,
-                       skip_proxy, METRIC_INGRESS, 1);
+    return lxc_ingress(o, ep, identity, 16, saddr, daddr, proto, sport, dport,
+                       0, flags & HF_TCP_CLOSE, len, skip_proxy,
+                       METRIC_INGRESS, 0);
 }
 
 /* from-container -> handle_ipv6 -> ipv6_l3_from_lxc (bpf_lxc.c:112-436) */
@@ -773,50 +914,55 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
         return r;
     }
     int ret = exthdr_drop(proto);
-    if (!ret) {
-        uint16_t pdport;
-        ret = ct6_new_dport(proto, sport, dport, &pdport);
-        if (!ret) {
-            uint32_t label = 0, dst;
-            tl_lookups++;
-            if (lpm_lookup(&o->ipc6, daddr, &label) && label)
-                dst = label;
-            else if (!memcmp(daddr, ROUTER_IP6, 8)) /* ipv6_match_prefix_64 */
-                dst = CLUSTER_ID;
-            else
-                dst = WORLD_ID;
-            r.identity = dst;
-            int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
-                                            CT_EGRESS, 0, len);
-            if (verdict < 0) {
-                r.verdict = DROP_POLICY;
-                metric(o, DROP_POLICY, METRIC_EGRESS, len);
-                return r;
-            }
-            if (verdict > 0) {
-                r.action = TC_ACT_REDIRECT;
-                r.verdict = verdict;
-                return r;
-            }
-            tl_lookups++;
-            const epinfo *ep = lxc_lookup(o, 2, daddr);
-            metric(o, 0, METRIC_EGRESS, len); /* to_host / local / to_stack */
-            if (ep) {
-                if (ep->flags & ENDPOINT_F_HOST) {
-                    r.action = TC_ACT_REDIRECT;
-                    return r;
-                }
-                res_t d = lxc_ingress(o, ep, o->seclabel[lxc], proto, sport,
-                                      dport, 0, len, 0, METRIC_EGRESS, 1);
-                d.identity = dst;
-                return d;
-            }
-            r.action = TC_ACT_OK;
+    uint16_t pdport;
+    int res;
+    if (!ret)
+        ret = ct_lookup(o, 16, ct_owner(o, lxc), saddr, daddr, proto, sport,
+                        dport, flags & HF_TCP_CLOSE, CT_EGRESS, 0, &res,
+                        &pdport);
+    if (ret) {
+        r.verdict = ret;
+        metric(o, ret, METRIC_EGRESS, len);
+        return r;
+    }
+    uint32_t label = 0, dst;
+    tl_lookups++;
+    if (lpm_lookup(&o->ipc6, daddr, &label) && label)
+        dst = label;
+    else if (!memcmp(daddr, ROUTER_IP6, 8)) /* ipv6_match_prefix_64 */
+        dst = CLUSTER_ID;
+    else
+        dst = WORLD_ID;
+    r.identity = dst;
+    int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
+                                    CT_EGRESS, 0, len);
+    if (res != CT_REPLY && res != CT_RELATED && verdict < 0) { /* :228-235 */
+        r.verdict = DROP_POLICY;
+        metric(o, DROP_POLICY, METRIC_EGRESS, len);
+        return r;
+    }
+    if (res == CT_NEW)
+        tl_ct |= CTO_CREATE1;                       /* ct_create6, :237-249 */
+    if (verdict > 0) {
+        r.action = TC_ACT_REDIRECT;
+        r.verdict = verdict;
+        return r;
+    }
+    tl_lookups++;
+    const epinfo *ep = lxc_lookup(o, 2, daddr);
+    metric(o, 0, METRIC_EGRESS, len); /* to_host / local / to_stack */
+    if (ep) {
+        if (ep->flags & ENDPOINT_F_HOST) {
+            r.action = TC_ACT_REDIRECT;
             return r;
         }
+        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 16, saddr, daddr, proto,
+                              sport, dport, 0, flags & HF_TCP_CLOSE, len, 0,
+                              METRIC_EGRESS, 1);
+        d.identity = dst;
+        return d;
     }
-    r.verdict = ret;
-    metric(o, ret, METRIC_EGRESS, len);
+    r.action = TC_ACT_OK;
     return r;
 }
 
@@ -845,7 +991,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, int nthreads)
+                     uint8_t *lookups, uint8_t *ct, int nthreads)
 {
     if (nthreads <= 0)
         nthreads = 1;
@@ -854,6 +1000,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         res_t r;
         const uint8_t *sa = saddr + 16 * i, *da = daddr + 16 * i;
         tl_lookups = 0;
+        tl_ct = 0;
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v6(o, sa, da);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -862,6 +1009,8 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                 identity[i] = 0;
                 if (lookups)
                     lookups[i] = (uint8_t)tl_lookups;
+                if (ct)
+                    ct[i] = 0;
                 continue;
             }
         }
@@ -876,6 +1025,8 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         identity[i] = r.identity;
         if (lookups)
             lookups[i] = (uint8_t)tl_lookups;
+        if (ct)
+            ct[i] = tl_ct;
     }
 }
 
@@ -947,4 +1098,231 @@ void cfo_counters_reset(cfo_t *o)
         if (o->pol[i])
             for (uint32_t j = 0; j < o->pol[i]->n; j++)
                 o->pol[i]->ents[j].packets = o->pol[i]->ents[j].bytes = 0;
+}
+
+/* ------------------------------------------------------------ CT maps */
+static void ct_put(cfo_t *o, const uint8_t k[CTK], const struct ctent *e)
+{
+    int64_t s = ht_find(&o->ct, k);
+    uint32_t idx;
+    if (s >= 0) {
+        idx = o->ct.vals[s];
+    } else {
+        if (o->ct_n == o->ct_cap) {
+            o->ct_cap = o->ct_cap ? 2 * o->ct_cap : 1024;
+            o->ct_ents = realloc(o->ct_ents, o->ct_cap * sizeof(struct ctent));
+            o->ct_live = realloc(o->ct_live, o->ct_cap);
+        }
+        idx = o->ct_n++;
+        ht_put(&o->ct, k, idx);
+    }
+    o->ct_ents[idx] = *e;
+    o->ct_live[idx] = 1;
+}
+
+int cfo_ct_add(cfo_t *o, int family, int lxc, int any_map,
+               const uint8_t *tuple, const uint8_t entry[56])
+{
+    int alen = family == 1 ? 4 : 16;
+    uint8_t k[CTK];
+    uint16_t owner = 0;
+    if (lxc >= 0) {
+        o->ct_local[lxc & 0xFFFF] = 1;
+        owner = (uint16_t)((lxc & 0xFFFF) + 1);
+    }
+    memset(k, 0, CTK);
+    memcpy(k, &owner, 2);
+    k[2] = (uint8_t)(any_map ? 1 : 0);
+    k[3] = (uint8_t)family;
+    memcpy(k + 4, tuple, 2 * (size_t)alen + 6);
+    struct ctent e;
+    memcpy(&e, entry, sizeof(e));
+    ct_put(o, k, &e);
+    o->ct_added++;
+    return 0;
+}
+
+/* The deterministic part of __ct_lookup's entry update (conntrack.h:221-285):
+ * the per-direction packet/byte accounting, ACTION_CREATE re-opens a
+ * closing entry, ACTION_CLOSE marks the direction closing.  Lifetimes, report timestamps, seen TCP flags and seen_non_syn
+ * depend on the clock or on TCP flag bits the header batch does not carry
+ * and are not modelled. */
+static void ct_hit_update(struct ctent *e, int action, int dir, uint32_t len)
+{
+    /* CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257) */
+    if (dir == CT_INGRESS) {
+        e->rx_packets++;
+        e->rx_bytes += len;
+    } else {
+        e->tx_packets++;
+        e->tx_bytes += len;
+    }
+    if (action == ACTION_CREATE)
+        e->bits &= (uint16_t)~(CTB_RX_CLOSING | CTB_TX_CLOSING);
+    else if (action == ACTION_CLOSE)
+        e->bits |= dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING;
+}
+
+/* ct_create4 / ct_create6 (conntrack.h:615-662, :691-772) without a load
+ * balancer (ct_state->addr == 0): the k2 entry plus the ICMP entry that
+ * relates errors to it, written into the same map.  ipv6_policy derives
+ * ct_state_new.rev_nat_index from the low 16 bits of daddr.s6_addr32[3]
+ * (bpf_lxc.c:787-788), so IPv6 ingress entries carry it. */
+static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
+                      uint32_t len, uint32_t src_sec_id, uint16_t rev_nat)
+{
+    struct ctent e;
+    memset(&e, 0, sizeof(e));
+    e.rev_nat_index = rev_nat;
+    const uint8_t *t = k2 + 4;
+    const int tcp = t[2 * alen + 4] == 6;
+    if (tcp) {  /* ct_update_timeout with seen_flags.syn = is_tcp */
+        if (dir == CT_INGRESS)
+            e.rx_flags_seen = 0x02;
+        else
+            e.tx_flags_seen = 0x02;
+    }
+    if (dir == CT_INGRESS) {
+        e.rx_packets = 1;
+        e.rx_bytes = len;
+    } else {
+        e.tx_packets = 1;
+        e.tx_bytes = len;
+    }
+    e.src_sec_id = src_sec_id;
+    ct_put(o, k2, &e);
+    uint8_t ki[CTK];
+    uint16_t owner;
+    memcpy(&owner, k2, 2);
+    ct_key(ki, owner, k2[2], alen, t, t + alen, 0, 0, alen == 4 ? 1 : 58,
+           (uint8_t)(t[2 * alen + 5] | TUPLE_F_RELATED));
+    e.bits |= CTB_SEEN_NON_SYN;
+    ct_put(o, ki, &e);
+}
+
+/* Fold one classified batch into the CT maps, in header order, as the
+ * engine does between batches: the CT result of every lookup stage was
+ * taken against the maps as they were when the batch started (ct[]), and
+ * the creates (ct_create), deletes (ct_delete on a denied CT_ESTABLISHED
+ * flow) and closing-bit updates are applied here.  A flow created twice in
+ * one batch is created once (the reference sees its second packet as
+ * CT_ESTABLISHED).  hazard[i] (optional) = 1 when the reference, running
+ * the batch one packet at a time, would have seen a different CT result for
+ * header i because of an earlier header of the same batch — streams used for
+ * golden vectors drop those headers. */
+static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
+                     const uint8_t *saddr, const uint8_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *identity,
+                     const int32_t *verdict, const uint8_t *ct,
+                     uint8_t *hazard)
+{
+    for (size_t i = 0; i < n; i++) {
+        if (hazard)
+            hazard[i] = 0;
+        const uint8_t c = ct[i];
+        if (!(c & (CTO_DONE1 | CTO_DONE2)))
+            continue;
+        const uint8_t *sa = saddr + (size_t)alen * i;
+        const uint8_t *da = daddr + (size_t)alen * i;
+        const epinfo *dst = lxc_lookup(o, alen == 4 ? 1 : 2, da);
+        const int last = (c & CTO_DONE2) ? 1 : 0;
+        for (int s = 0; s < 2; s++) {
+            const uint8_t cs = (uint8_t)(c >> (4 * s));
+            if (!(cs & CTO_DONE1))
+                continue;
+            const int egress_stage = mode == CFO_MODE_EGRESS && s == 0;
+            const int dir = egress_stage ? CT_EGRESS : CT_INGRESS;
+            const uint16_t owner = egress_stage ? ct_owner(o, ep_lxc)
+                                   : dst ? ct_owner(o, dst->lxc_id) : 0;
+            const uint32_t sec = mode == CFO_MODE_EGRESS ? o->seclabel[ep_lxc]
+                                                         : identity[i];
+            uint8_t k1[CTK], k2[CTK];
+            int action;
+            uint16_t td, ts;
+            if (ct_keys(alen, owner, sa, da, proto[i], sport[i], dport[i],
+                        flags[i] & HF_TCP_CLOSE, dir, k1, k2, &action, &td,
+                        &ts) < 0)
+                continue;
+            const int b = cs & 3;
+            const int created = (cs & CTO_CREATE1) != 0;
+            const int dropped = s == last && verdict[i] == DROP_POLICY;
+            const int64_t e1 = ct_find(o, k1), e2 = ct_find(o, k2);
+            const int rel = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) != 0;
+            const int q = e1 >= 0 ? (rel ? CT_RELATED : CT_REPLY)
+                          : e2 >= 0 ? CT_ESTABLISHED : CT_NEW;
+            if (hazard && q != b && !(b == CT_NEW && q == CT_ESTABLISHED && created))
+                hazard[i] = 1;
+            if (b == CT_REPLY || b == CT_RELATED) {
+                if (e1 >= 0)
+                    ct_hit_update(&o->ct_ents[e1], action, dir, len[i]);
+            } else if (b == CT_ESTABLISHED) {
+                if (e2 >= 0) {
+                    ct_hit_update(&o->ct_ents[e2], action, dir, len[i]);
+                    if (dropped)
+                        o->ct_live[e2] = 0;
+                }
+            } else if (created) {
+                if (e2 >= 0)
+                    ct_hit_update(&o->ct_ents[e2], action, dir, len[i]);
+                else
+                    ct_create(o, k2, alen, dir, len[i], sec,
+                              alen == 16 && dir == CT_INGRESS
+                                  ? (uint16_t)(da[12] | da[13] << 8) : 0);
+            }
+        }
+    }
+}
+
+void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint32_t *saddr, const uint32_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *identity,
+                     const int32_t *verdict, const uint8_t *ct,
+                     uint8_t *hazard)
+{
+    ct_apply(o, 4, mode, ep_lxc, n, (const uint8_t *)saddr,
+             (const uint8_t *)daddr, sport, dport, proto, flags, len, identity,
+             verdict, ct, hazard);
+}
+
+void cfo_ct_apply_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint8_t *saddr, const uint8_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *identity,
+                     const int32_t *verdict, const uint8_t *ct,
+                     uint8_t *hazard)
+{
+    ct_apply(o, 16, mode, ep_lxc, n, saddr, daddr, sport, dport, proto, flags,
+             len, identity, verdict, ct, hazard);
+}
+
+static int cmp_ctrow(const void *a, const void *b)
+{
+    return memcmp(a, b, CTK);
+}
+
+size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap)
+{
+    size_t n = 0;
+    for (uint32_t s = 0; s < o->ct.cap; s++) {
+        if (!o->ct.used[s])
+            continue;
+        uint32_t idx = o->ct.vals[s];
+        if (!o->ct_live[idx])
+            continue;
+        if (rows && n < cap) {
+            uint8_t *r = rows + CFO_CT_ROW * n;
+            memset(r, 0, CFO_CT_ROW);
+            memcpy(r, o->ct.keys + (size_t)s * CTK, CTK);
+            memcpy(r + CTK, &o->ct_ents[idx], sizeof(struct ctent));
+        }
+        n++;
+    }
+    if (rows && n <= cap)
+        qsort(rows, n, CFO_CT_ROW, cmp_ctrow);
+    return n;
 }

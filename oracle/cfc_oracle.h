@@ -59,7 +59,7 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, int nthreads);
+                     uint8_t *lookups, uint8_t *ct, int nthreads);
 
 /* The same for IPv6: saddr/daddr are n x 16 raw address bytes; proto is the
  * next header ipv6_hdrlen() stops at (44 / 59 drop); flags bit 2 (4) marks
@@ -72,7 +72,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
                      int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, int nthreads);
+                     uint8_t *lookups, uint8_t *ct, int nthreads);
 
 /* rows of 7 u64: identity, dport, proto, egress, proxy_port, packets, bytes
  * (sorted); returns the number of rows (writes at most cap). */
@@ -80,6 +80,37 @@ size_t cfo_policy_dump(cfo_t *o, uint16_t lxc_id, uint64_t *rows, size_t cap);
 /* rows of 4 u64: reason, dir, count, bytes (sorted, non-zero only) */
 size_t cfo_metrics_dump(cfo_t *o, uint64_t *rows, size_t cap);
 void cfo_counters_reset(cfo_t *o);
+
+/* ---- conntrack (bpf/lib/conntrack.h) ----
+ * cfo_classify_* look CT up against the maps as they are when the call
+ * starts and report, per header, a CT byte (ct may be NULL):
+ *   bits 0-1 CT result of stage 1 (CT_NEW 0, ESTABLISHED 1, REPLY 2,
+ *   RELATED 3), bit 2 stage 1 looked up, bit 3 stage 1 creates; bits 4-7 the
+ *   same for stage 2 (the destination's ingress policy after egress local
+ *   delivery).  cfo_ct_apply_* then folds the batch into the maps.
+ * Entries: lxc = -1 for the global maps, else the endpoint's local maps;
+ * tuple = struct ipv{4,6}_ct_tuple bytes; entry = struct ct_entry (56 B). */
+int cfo_ct_add(cfo_t *o, int family, int lxc, int any_map,
+               const uint8_t *tuple, const uint8_t entry[56]);
+void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint32_t *saddr, const uint32_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *identity,
+                     const int32_t *verdict, const uint8_t *ct,
+                     uint8_t *hazard);
+void cfo_ct_apply_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
+                     const uint8_t *saddr, const uint8_t *daddr,
+                     const uint16_t *sport, const uint16_t *dport,
+                     const uint8_t *proto, const uint8_t *flags,
+                     const uint16_t *len, const uint32_t *identity,
+                     const int32_t *verdict, const uint8_t *ct,
+                     uint8_t *hazard);
+/* live CT entries as rows of CFO_CT_ROW bytes: u16 owner (0 global, else
+ * lxc_id + 1), u8 map (0 TCP, 1 ANY), u8 family, tuple (40 B, zero padded),
+ * struct ct_entry (56 B), 4 B pad; sorted by the first 44 bytes. */
+#define CFO_CT_ROW 104
+size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -61,9 +61,14 @@ def build_packet_v4(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
     ip += struct.pack("<II", int(h.saddr[i]), int(h.daddr[i]))
     sp, dp = int(h.sport[i]), int(h.dport[i])
     if proto == S.IPPROTO_TCP:
-        fl = 0x11 if (h.flags[i] & S.HF_TCP_CLOSE) else 0x02
-        l4 = struct.pack("<HH", sp, dp) + struct.pack(">IIBBHHH", 1, 0, 0x50,
-                                                       fl, 1024, 0, 0)
+        # HF_TCP_CLOSE: what ct_lookup reads as "rst || fin".  union
+        # tcp_flags (conntrack.h:86-99) declares its bitfields as separate
+        # union members, so each of them is bit 0 of TCP header byte 12;
+        # FIN|ACK in byte 13 is set too, as a real close would carry.
+        close = bool(h.flags[i] & S.HF_TCP_CLOSE)
+        fl = 0x11 if close else 0x02
+        l4 = struct.pack("<HH", sp, dp) + struct.pack(
+            ">IIBBHHH", 1, 0, 0x51 if close else 0x50, fl, 1024, 0, 0)
     elif proto == S.IPPROTO_UDP:
         l4 = struct.pack("<HH", sp, dp) + struct.pack(">HH", L - 34, 0)
     else:   # ICMP (type/code in sport word, csum in dport word) and others
@@ -82,9 +87,14 @@ def build_packet_v6(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
     ext = bool(h.flags[i] & S.HF_EXTHDR)
     sp, dp = int(h.sport[i]), int(h.dport[i])
     if proto == S.IPPROTO_TCP:
-        fl = 0x11 if (h.flags[i] & S.HF_TCP_CLOSE) else 0x02
-        l4 = struct.pack("<HH", sp, dp) + struct.pack(">IIBBHHH", 1, 0, 0x50,
-                                                       fl, 1024, 0, 0)
+        # HF_TCP_CLOSE: what ct_lookup reads as "rst || fin".  union
+        # tcp_flags (conntrack.h:86-99) declares its bitfields as separate
+        # union members, so each of them is bit 0 of TCP header byte 12;
+        # FIN|ACK in byte 13 is set too, as a real close would carry.
+        close = bool(h.flags[i] & S.HF_TCP_CLOSE)
+        fl = 0x11 if close else 0x02
+        l4 = struct.pack("<HH", sp, dp) + struct.pack(
+            ">IIBBHHH", 1, 0, 0x51 if close else 0x50, fl, 1024, 0, 0)
     elif proto == S.IPPROTO_UDP:
         l4 = struct.pack("<HH", sp, dp) + struct.pack(">HH", 8, 0)
     elif proto == 59:
@@ -108,6 +118,10 @@ def l4_offset(h, i):
 
 
 # ------------------------------------------------------------ datapath
+CT_MAPS = ("cilium_ct_tcp4_111", "cilium_ct_any4_111", "cilium_ct_tcp6_111",
+           "cilium_ct_any6_111")
+
+
 def u32(x):
     return struct.pack("<I", x)
 
@@ -137,9 +151,10 @@ class RefDatapath:
     def __init__(self, t: S.Tables):
         n_ipc = max(512000, len(t.ipcache) + 16)
         n_pf = max(1024, len(t.prefilter) + 16)
+        ct_max = {m: 65536 for m in CT_MAPS}      # LRU: never near full
         self.L = L = H.Loader({"cilium_ipcache": n_ipc, "v4_fix": n_pf,
                                "v4_dyn": n_pf, "v6_fix": n_pf, "v6_dyn": n_pf,
-                               "cilium_policy_foo": 16384 * 2})
+                               "cilium_policy_foo": 16384 * 2, **ct_max})
         self.t = t
         SC = H.PROG_SCHED_CLS
         nd = {"cilium_calls_111": "calls_nd"}
@@ -148,6 +163,7 @@ class RefDatapath:
         L.maps["calls_nd"].update(u32(7), u32(nd_v4))
         self.ep_prog = {}
         self.policy_map = {}
+        self.ct_maps = {}     # lxc -> {ct map name in the object: renamed}
         for k, e in enumerate(t.endpoints):
             lxc = int(e["lxc_id"])
             if int(e["flags"]) & 1 or lxc not in t.policy or lxc in self.ep_prog:
@@ -155,9 +171,9 @@ class RefDatapath:
                            # the second address of a dual-stack endpoint
             rn = {"cilium_calls_111": f"calls_lxc{k}",
                   "cilium_policy_foo": f"policy{k}"}
-            for ct in ("cilium_ct_tcp4_111", "cilium_ct_any4_111",
-                       "cilium_ct_tcp6_111", "cilium_ct_any6_111"):
+            for ct in CT_MAPS:
                 rn[ct] = f"{ct}_{k}"
+            self.ct_maps[lxc] = {ct: f"{ct}_{k}" for ct in CT_MAPS}
             pol = L.load("bpf_lxc.o", "1/0x1010", SC, rn)
             calls = {}
             for sec, idx in (("2/11", 11), ("2/7", 7), ("2/12", 12), ("2/10", 10)):
@@ -188,6 +204,42 @@ class RefDatapath:
 
     def close(self):
         self.L.close()
+
+    # ------------------------------------------------------- conntrack
+    def ct_dump(self):
+        """Every live entry of every endpoint's CT maps as oracle-format
+        rows (cfc_oracle.h CFO_CT_ROW), sorted."""
+        rows = []
+        for lxc, names in self.ct_maps.items():
+            for ct, nm in names.items():
+                m = self.L.maps.get(nm)
+                if m is None:
+                    continue
+                fam = 1 if ct.endswith("4_111") else 2
+                kind = 0 if "_tcp" in ct else 1
+                for k in m.keys():
+                    v = m.lookup(k)
+                    if v is None:
+                        continue
+                    r = bytearray(S.CT_ROW)
+                    struct.pack_into("<HBB", r, 0, lxc + 1, kind, fam)
+                    r[4:4 + len(k)] = k
+                    r[44:100] = v[:56]
+                    rows.append(bytes(r))
+        rows.sort(key=lambda r: r[:44])
+        return np.frombuffer(b"".join(rows), np.uint8).reshape(-1, S.CT_ROW).copy()
+
+    def reset_counters(self):
+        """Zero policy-entry counters and cilium_metrics (after a history
+        run that only exists to populate CT)."""
+        for lxc, pm in self.policy_map.items():
+            for k in pm.keys():
+                v = pm.lookup(k)
+                pm.update(k, v[:2] + bytes(22))
+        m = self.L.maps.get("cilium_metrics")
+        if m is not None:
+            for k in m.keys():
+                m.delete(k)
 
     # ------------------------------------------------------- counters
     def policy_counters(self):
@@ -287,6 +339,10 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
 
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
     action, verdict, ident, idmask = res
+    extra = {}
+    if t.ct is not None:
+        # CT before (loaded by the oracle / engine) and after the stream
+        extra = dict(ct=t.ct, x_ct=dp.ct_dump())
     d = dict(mode=np.int32(mode), ep_lxc=np.int32(ep_lxc or 0),
              ipcache=t.ipcache, endpoints=t.endpoints, prefilter=t.prefilter,
              seclabel=np.array(sorted(t.seclabel.items()), np.uint32).reshape(-1, 2),
@@ -294,7 +350,7 @@ def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
              h_sport=h.sport, h_dport=h.dport, h_proto=h.proto,
              h_flags=h.flags, h_length=h.length, h_mark=h.mark,
              x_action=action, x_verdict=verdict, x_identity=ident,
-             x_idmask=idmask, x_metrics=dp.metrics())
+             x_idmask=idmask, x_metrics=dp.metrics(), **extra)
     for lxc, pol in t.policy.items():
         d[f"policy_{lxc}"] = pol
     for lxc, c in dp.policy_counters().items():
@@ -638,6 +694,113 @@ def sc_xdp_v6(n=20000, seed=10, mode=MODE_XDP):
     return t, h, mode, None
 
 
+# ------------------------------------------------------------ conntrack
+def _ct_tables(seed, family):
+    """small_ingress-sized tables, two endpoints with programs (EP_LXC_ID and
+    0x2020), dual-stack when family == 6."""
+    rng = np.random.default_rng(seed)
+    if family == 4:
+        t = S.config_c2(seed, n_prefixes=2000, n_policy=400, n_endpoints=2)
+    else:
+        t = S.config_c3(seed, n_prefixes=2000, n_v4_prefixes=500, n_policy=400,
+                        n_endpoints=2, n_prefilter=0)
+    return t, rng
+
+
+def _ct_scenario(family, mode, seed, n=6000):
+    """Conntrack: CT state made by the reference
+    itself from a history stream, then a test stream of established
+    packets, replies, ICMP errors related to known flows, FIN/RST on known
+    flows, new flows, and established flows that a policy change now denies
+    (ct_delete).  Intra-batch CT hazards are removed with the oracle's
+    sequential check so the batch engine and the per-packet reference see
+    the same CT state for every header."""
+    import oracle as O
+    t, rng = _ct_tables(seed, family)
+    fam_ipc = t.ipcache[t.ipcache["family"] == (1 if family == 4 else 2)]
+    gen = S.gen_headers_v4 if family == 4 else S.gen_headers_v6
+    loc = S.local_v4_addrs(t) if family == 4 else S.local_v6_addrs(t)
+    ep_addr = S.LXC_IPV4 if family == 4 else S.LXC_IPV6
+    kw = dict(frag=0) if family == 4 else dict(ext=0, exthdr_drop=0)
+    # history: flows into both endpoints, flows out of EP_LXC_ID (some to
+    # the other local endpoint), with extra L3 allow rules that are removed
+    # before the test stream (a policy change: those flows become denied)
+    h_in = gen(rng, 1500, fam_ipc, loc[:2], local_frac=1.0, mark_host=0,
+               mark_proxy=0, other_proto=0, **kw)
+    h_in.flags[:] &= np.uint8(0xFF ^ S.HF_TCP_CLOSE)
+    h_out = gen(rng, 1500, fam_ipc, loc[:2], local_frac=0.4, mark_host=0,
+                mark_proxy=0, other_proto=0, src_fixed=ep_addr, **kw)
+    h_out.flags[:] &= np.uint8(0xFF ^ S.HF_TCP_CLOSE)
+    dst = gen(rng, 1500, fam_ipc, loc[:1], local_frac=1.0, **kw).saddr
+    nonloc = rng.random(1500) < 0.6
+    h_out.daddr[nonloc] = dst[nonloc]
+    idents = np.unique(fam_ipc["label"])
+    extra = rng.choice(idents, size=2 * len(idents) // 3, replace=False)
+    hist_pol = {}
+    for lxc, pol in t.policy.items():
+        add = np.zeros(2 * len(extra), S.POLICY_DT)
+        add["identity"] = np.concatenate([extra, extra])
+        add["egress"][len(extra):] = 1
+        have = {(int(r["identity"]), int(r["dport"]), int(r["proto"]),
+                 int(r["egress"])) for r in pol}
+        add = add[[(int(r["identity"]), 0, 0, int(r["egress"])) not in have
+                   for r in add]]
+        hist_pol[lxc] = np.concatenate([pol, add])
+    th = S.Tables(t.ipcache, t.endpoints, hist_pol, t.prefilter, t.seclabel)
+    dp = RefDatapath(th)
+    run(dp, h_in, MODE_INGRESS)
+    run(dp, h_out, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    for lxc, pol in hist_pol.items():       # the policy change
+        pm = dp.policy_map[lxc]
+        for r in pol[len(t.policy[lxc]):]:
+            pm.delete(policy_key(r))
+    dp.reset_counters()
+    # test stream
+    icmp = S.IPPROTO_ICMP if family == 4 else S.IPPROTO_ICMPV6
+    err = 3 if family == 4 else 1
+    if mode == MODE_INGRESS:
+        fwd, rep = h_in, h_out
+    else:   # replies leave from EP_LXC_ID (the program under test)
+        fwd = h_out
+        rep = S.take(h_in, (h_in.daddr == loc[0]).all(-1) if family == 6
+                     else h_in.daddr == loc[0])
+    m = int(n * 1.4)
+    parts = []
+    a = S.take(fwd, rng.integers(0, len(fwd), size=int(m * 0.35)))
+    a.flags[(rng.random(len(a)) < 0.08) & (a.proto == S.IPPROTO_TCP)] |= np.uint8(S.HF_TCP_CLOSE)
+    parts.append(a)
+    b = S.reverse(S.take(rep, rng.integers(0, len(rep), size=int(m * 0.3))))
+    b.flags[(rng.random(len(b)) < 0.08) & (b.proto == S.IPPROTO_TCP)] |= np.uint8(S.HF_TCP_CLOSE)
+    parts.append(b)
+    c = S.reverse(S.take(rep, rng.integers(0, len(rep), size=int(m * 0.05))))
+    c.proto[:] = icmp
+    c.sport[:] = err
+    c.dport[:] = 0
+    parts.append(c)
+    if mode == MODE_INGRESS:
+        d = gen(rng, int(m * 0.3), fam_ipc, loc, local_frac=0.95, **kw)
+    else:
+        d = gen(rng, int(m * 0.3), fam_ipc, loc, local_frac=0.1,
+                src_fixed=ep_addr, **kw)
+        sel = rng.random(len(d)) < 0.8
+        d.daddr[sel] = dst[rng.integers(0, len(dst), size=int(sel.sum()))]
+    parts.append(d)
+    h = S.concat(parts)
+    h = S.take(h, rng.permutation(len(h)))
+    ep = S.EP_LXC_ID if mode == MODE_EGRESS else 0
+    for _ in range(6):
+        o = O.Oracle(t)
+        oa, ov, oi, ct = o.classify(h, mode, ep, want_ct=True)
+        hz = o.ct_apply(h, mode, ep, oi, ov, ct, hazard=True)
+        if not hz.any():
+            break
+        h = _keep(h, hz == 0)
+    assert not hz.any()
+    h = h.slice(0, n)
+    return t, h, mode, ep or None, dp
+
+
 def _keep(h, m):
     return S.Headers(h.family, h.saddr[m], h.daddr[m], h.sport[m], h.dport[m],
                      h.proto[m], h.flags[m], h.length[m], h.mark[m])
@@ -656,14 +819,19 @@ SCENARIOS = {
     "c3_egress_v6": sc_c3_egress,
     "xdp_v6": sc_xdp_v6,
     "full_v6": lambda: sc_xdp_v6(seed=12, mode=MODE_FULL),
+    "ct_ingress_v4": lambda: _ct_scenario(4, MODE_INGRESS, 21),
+    "ct_egress_v4": lambda: _ct_scenario(4, MODE_EGRESS, 22),
+    "ct_ingress_v6": lambda: _ct_scenario(6, MODE_INGRESS, 23),
+    "ct_egress_v6": lambda: _ct_scenario(6, MODE_EGRESS, 24),
 }
 
 
 def main(names):
     for name in names or SCENARIOS:
         t0 = time.time()
-        t, h, mode, ep = SCENARIOS[name]()
-        dp = RefDatapath(t)
+        sc = SCENARIOS[name]()
+        t, h, mode, ep = sc[:4]
+        dp = sc[4] if len(sc) > 4 else RefDatapath(t)
         try:
             res = run(dp, h, mode, ep)
             path = save(name, t, h, mode, ep, res, dp)

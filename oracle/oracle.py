@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "liboracle.so")
 
 MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
+CT_ROW = 104     # cfc_oracle.h CFO_CT_ROW
 
 _lib = None
 
@@ -41,9 +42,16 @@ def lib():
         L.cfo_prefilter_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, u8p,
                                         ctypes.c_int]
         L.cfo_classify_v4.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
-                                      ctypes.c_size_t] + [vp] * 12 + [ctypes.c_int]
+                                      ctypes.c_size_t] + [vp] * 13 + [ctypes.c_int]
         L.cfo_classify_v6.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
-                                      ctypes.c_size_t] + [vp] * 12 + [ctypes.c_int]
+                                      ctypes.c_size_t] + [vp] * 13 + [ctypes.c_int]
+        L.cfo_ct_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 vp, vp]
+        for f in (L.cfo_ct_apply_v4, L.cfo_ct_apply_v6):
+            f.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
+                          ctypes.c_size_t] + [vp] * 11
+        L.cfo_ct_dump.restype = ctypes.c_size_t
+        L.cfo_ct_dump.argtypes = [vp, vp, ctypes.c_size_t]
         L.cfo_policy_create.argtypes = [vp, ctypes.c_uint16]
         L.cfo_policy_dump.restype = ctypes.c_size_t
         L.cfo_policy_dump.argtypes = [vp, ctypes.c_uint16, vp, ctypes.c_size_t]
@@ -99,13 +107,35 @@ class Oracle:
             a, keep = _u8p(p["addr"])
             L.cfo_prefilter_add(h, int(p["family"]), int(p["plen"]), a,
                                 int(p["dyn"]))
+        if getattr(t, "ct", None) is not None:
+            self.ct_add(t.ct)
 
-    def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False):
+    def ct_add(self, ct):
+        for e in ct:
+            tu = np.ascontiguousarray(e["tuple"], np.uint8)
+            en = np.ascontiguousarray(e["entry"], np.uint8)
+            self.L.cfo_ct_add(self.h, int(e["family"]), int(e["lxc"]),
+                              int(e["any"]), _p(tu), _p(en))
+
+    def _arrays(self, hdr):
+        c = np.ascontiguousarray
+        at = np.uint32 if hdr.family == 4 else np.uint8
+        return [c(hdr.saddr, at), c(hdr.daddr, at),
+                c(hdr.sport, np.uint16), c(hdr.dport, np.uint16),
+                c(hdr.proto, np.uint8), c(hdr.flags, np.uint8),
+                c(hdr.length, np.uint16), c(hdr.mark, np.uint32)]
+
+    def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False,
+                 want_ct=False, apply_ct=False):
+        """-> (action, verdict, identity[, lookups][, ct]).  apply_ct folds
+        the batch's CT creates/deletes into the oracle's CT maps afterwards
+        (what the engine's cfc_ct_apply does)."""
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
         ide = np.zeros(n, np.uint32)
         lk = np.zeros(n, np.uint8) if want_lookups else None
+        ct = np.zeros(n, np.uint8) if (want_ct or apply_ct) else None
         c = np.ascontiguousarray
         at = np.uint32 if hdr.family == 4 else np.uint8
         arrs = [c(hdr.saddr, at), c(hdr.daddr, at),
@@ -116,10 +146,33 @@ class Oracle:
             assert arrs[0].shape == (n, 16) and arrs[1].shape == (n, 16)
         fn = self.L.cfo_classify_v4 if hdr.family == 4 else self.L.cfo_classify_v6
         fn(self.h, mode, ep_lxc, n, *[_p(a) for a in arrs], _p(act), _p(ver),
-           _p(ide), _p(lk), nthreads)
+           _p(ide), _p(lk), _p(ct), nthreads)
+        if apply_ct:
+            self.ct_apply(hdr, mode, ep_lxc, ide, ver, ct)
+        out = (act, ver, ide)
         if want_lookups:
-            return act, ver, ide, lk
-        return act, ver, ide
+            out += (lk,)
+        if want_ct:
+            out += (ct,)
+        return out
+
+    def ct_apply(self, hdr, mode, ep_lxc, identity, verdict, ct, hazard=False):
+        arrs = self._arrays(hdr)
+        hz = np.zeros(len(hdr), np.uint8) if hazard else None
+        fn = self.L.cfo_ct_apply_v4 if hdr.family == 4 else self.L.cfo_ct_apply_v6
+        c = np.ascontiguousarray
+        fn(self.h, mode, ep_lxc, len(hdr), *[_p(a) for a in arrs[:7]],
+           _p(c(identity, np.uint32)), _p(c(verdict, np.int32)),
+           _p(c(ct, np.uint8)), _p(hz))
+        return hz
+
+    def ct_dump(self):
+        """(n, CT_ROW) u8 rows: owner u16, map u8, family u8, tuple[40],
+        ct_entry[56], pad[4]; sorted."""
+        n = self.L.cfo_ct_dump(self.h, None, 0)
+        rows = np.zeros((n, CT_ROW), np.uint8)
+        self.L.cfo_ct_dump(self.h, _p(rows), n)
+        return rows
 
     def policy_counters(self, lxc):
         n = self.L.cfo_policy_dump(self.h, lxc, None, 0)

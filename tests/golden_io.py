@@ -24,7 +24,10 @@ class Golden:
                   if k.startswith("policy_")}
         seclabel = {int(a): int(b) for a, b in d["seclabel"]}
         self.tables = S.Tables(d["ipcache"], d["endpoints"], policy,
-                               d["prefilter"], seclabel)
+                               d["prefilter"], seclabel,
+                               d["ct"] if "ct" in d.files else None)
+        # CT maps after the stream, oracle row format (None: no CT state)
+        self.ct_after = d["x_ct"] if "x_ct" in d.files else None
         self.headers = S.Headers(int(d["h_family"]), d["h_saddr"], d["h_daddr"],
                                  d["h_sport"], d["h_dport"], d["h_proto"],
                                  d["h_flags"], d["h_length"], d["h_mark"])
@@ -42,3 +45,17 @@ def mismatches(g: Golden, action, verdict, identity):
     bad = (action != g.action) | (verdict != g.verdict) | \
           ((identity & g.idmask) != (g.identity & g.idmask))
     return np.nonzero(bad)[0]
+
+
+# ct_entry bytes the comparison ignores: lifetime (offset 32, clock),
+# seen_non_syn (bit 4 of offset 36) and the seen-TCP-flag bytes (42, 43:
+# TCP flag bits the header batch does not carry), last_{tx,rx}_report
+# (48-55, clock).  Row offsets: entry starts at 44.
+def ct_masked(rows):
+    r = np.array(rows, np.uint8).reshape(-1, S.CT_ROW).copy()
+    e = 44
+    r[:, e + 32:e + 36] = 0
+    r[:, e + 36] &= 0xEF
+    r[:, e + 42:e + 44] = 0
+    r[:, e + 48:e + 56] = 0
+    return r
