@@ -26,7 +26,12 @@ EXPORTS = (
     "cfc_counters_sync", "cfc_counters_clear", "cfc_counters_export",
     "cfc_counters_import", "cfc_get_stats", "cfc_strerror",
     "cfc_set_option", "cfc_timing_collect", "cfc_classify_v6",
+    "cfc_ct_apply_v4", "cfc_ct_apply_v6", "cfc_map_update_batch",
 )
+# CT byte (cfc_out.ct): per stage (bits 0-3, then 4-7 for the destination's
+# ingress lookup after egress local delivery)
+CT_NEW, CT_ESTABLISHED, CT_REPLY, CT_RELATED = 0, 1, 2, 3
+CT_RES_MASK, CT_DONE, CT_CREATE = 0x3, 0x4, 0x8
 
 
 class CfcError(OSError):
@@ -45,7 +50,7 @@ class HdrV6(ctypes.Structure):
 
 class Out(ctypes.Structure):
     _fields_ = [("verdict", ctypes.c_void_p), ("identity", ctypes.c_void_p),
-                ("action", ctypes.c_void_p)]
+                ("action", ctypes.c_void_p), ("ct", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -64,7 +69,9 @@ class Stats(ctypes.Structure):
                 ("lpm6_kib", ctypes.c_uint32),
                 ("endpoints_v6", ctypes.c_uint32),
                 ("prefilter_v6_fix", ctypes.c_uint32),
-                ("prefilter_v6_dyn", ctypes.c_uint32)]
+                ("prefilter_v6_dyn", ctypes.c_uint32),
+                ("ct4_entries", ctypes.c_uint32),
+                ("ct6_entries", ctypes.c_uint32)]
 
 
 class Timing(ctypes.Structure):
@@ -92,6 +99,7 @@ def lib():
     L.cfc_map_close.argtypes = [vp, i32]
     L.cfc_map_update.argtypes = [vp, i32, vp, vp, u64]
     L.cfc_map_lookup.argtypes = [vp, i32, vp, vp]
+    L.cfc_map_update_batch.argtypes = [vp, i32, vp, vp, u64, u64]
     L.cfc_map_delete.argtypes = [vp, i32, vp]
     L.cfc_map_get_next_key.argtypes = [vp, i32, vp, vp]
     L.cfc_endpoint_config.argtypes = [vp, ctypes.c_uint16, u32]
@@ -99,6 +107,10 @@ def lib():
     L.cfc_classify_v4.argtypes = [vp, ctypes.POINTER(HdrV4), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
     L.cfc_classify_v6.argtypes = [vp, ctypes.POINTER(HdrV6), ctypes.POINTER(Out),
+                                  i32, ctypes.c_uint16, vp]
+    L.cfc_ct_apply_v4.argtypes = [vp, ctypes.POINTER(HdrV4), ctypes.POINTER(Out),
+                                  i32, ctypes.c_uint16, vp]
+    L.cfc_ct_apply_v6.argtypes = [vp, ctypes.POINTER(HdrV6), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
     L.cfc_counters_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
     L.cfc_counters_sync.argtypes = [vp, vp]

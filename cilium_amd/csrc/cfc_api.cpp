@@ -30,6 +30,18 @@ struct DevBuf {
         p = nullptr;
         bytes = 0;
     }
+    int zeros(size_t n, hipStream_t s)
+    {
+        reset();
+        if (!n)
+            return 0;
+        if (hipMalloc(&p, n) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        bytes = n;
+        return hipMemsetAsync(p, 0, n, s) == hipSuccess ? 0 : -EIO;
+    }
     int upload(const void *src, size_t n, hipStream_t s)
     {
         reset();
@@ -57,6 +69,10 @@ struct Epoch {
     DevBuf tbl24, tbl8, ovf, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
         polbloom, lxc6;
     DevBuf l6[3][3];   // ipc6 / pf6_fix / pf6_dyn: slots, bloom, lens
+    DevBuf ct4, ct6, ct_acct;
+    std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
+    std::vector<Ct6Slot> ct6_host;
+    std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
     DevTables T{};
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
@@ -112,10 +128,70 @@ uint64_t tables_sig(cfc_ctx *c)
     return s;
 }
 
+// CT map and key bytes of a device slot (the slot holds the whole tuple)
+Map *ct_slot_key(const Epoch &E, int family, const uint32_t *d, const uint32_t *sa,
+                 uint32_t z, uint32_t w, std::string *key)
+{
+    const uint32_t al = family == 4 ? 4 : 16;
+    char k[38];
+    memcpy(k, d, al);
+    memcpy(k + al, sa, al);
+    memcpy(k + 2 * al, &z, 4);
+    k[2 * al + 4] = (char)(w & 0xFF);
+    k[2 * al + 5] = (char)((w >> 8) & 7);
+    key->assign(k, 2 * al + 6);
+    auto it = E.ct_maps.find(ct_map_key(family, w & ~0x7FFu, (w & 0xFF) != 6));
+    return it == E.ct_maps.end() ? nullptr : it->second;
+}
+
+// CONNTRACK_ACCOUNTING counts of the device into the CT entries' rx/tx
+// packets and bytes (struct ct_entry offsets 0-31)
+int fold_ct(cfc_ctx *c, hipStream_t s)
+{
+    Epoch &E = *c->epoch;
+    const size_t n4 = E.ct4_host.size(), n = n4 + E.ct6_host.size();
+    if (!n)
+        return 0;
+    std::vector<uint64_t> h(4 * n);
+    if (hipMemcpyAsync(h.data(), E.ct_acct.p, 32 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemsetAsync(E.ct_acct.p, 0, 32 * n, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    std::string key;
+    for (size_t i = 0; i < n; i++) {
+        const uint64_t *a = &h[4 * i];
+        if (!(a[0] | a[1] | a[2] | a[3]))
+            continue;
+        Map *m;
+        if (i < n4) {
+            const Ct4Slot &e = E.ct4_host[i];
+            m = ct_slot_key(E, 4, &e.x, &e.y, e.z, e.w, &key);
+        } else {
+            const Ct6Slot &e = E.ct6_host[i - n4];
+            m = ct_slot_key(E, 6, e.d, e.s, e.z, e.w, &key);
+        }
+        if (!m)
+            continue;
+        auto it = m->kv.find(key);
+        if (it == m->kv.end())
+            continue;   // deleted since (ct_delete): its counts go with it
+        uint64_t v[4];   // rx_packets, rx_bytes, tx_packets, tx_bytes
+        memcpy(v, it->second.val.data(), 32);
+        v[2] += a[0];    // [dir CT_EGRESS 0] -> tx
+        v[3] += a[1];
+        v[0] += a[2];    // [dir CT_INGRESS 1] -> rx
+        v[1] += a[3];
+        memcpy(&it->second.val[0], v, 32);
+    }
+    return 0;
+}
+
 int fold_counters(cfc_ctx *c, hipStream_t s)
 {
     if (!c->ctr_pending || !c->epoch)
         return 0;
+    if (int rc = fold_ct(c, s))
+        return rc;
     std::vector<uint64_t> h(c->ctr_u64);
     if (hipMemcpyAsync(h.data(), c->ctr, c->ctr_u64 * 8, hipMemcpyDeviceToHost,
                        s) != hipSuccess)
@@ -211,9 +287,33 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
         (rc = upload_vec(E->lxc6, img.lxc6, s)) ||
         (rc = upload_lpm6(E->l6[0], img.ipc6, &E->T.ipc6, s)) ||
         (rc = upload_lpm6(E->l6[1], img.pf6_fix, &E->T.pf6_fix, s)) ||
-        (rc = upload_lpm6(E->l6[2], img.pf6_dyn, &E->T.pf6_dyn, s)))
+        (rc = upload_lpm6(E->l6[2], img.pf6_dyn, &E->T.pf6_dyn, s)) ||
+        (rc = upload_vec(E->ct4, img.ct4, s)) || (rc = upload_vec(E->ct6, img.ct6, s)))
         return rc;
+    {
+        const size_t nslots = img.ct4.size() + img.ct6.size();
+        if (nslots && (rc = E->ct_acct.zeros(32 * nslots, s)))
+            return rc;
+    }
+    for (Map *m : ms)
+        if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
+            E->ct_maps[ct_map_key(m->role == ROLE_CT4 ? 4 : 6,
+                                  ct_owner_word((uint32_t)std::max(m->policy_lxc, 0),
+                                                m->policy_lxc >= 0),
+                                  m->ct_any)] = m;
     DevTables &T = E->T;
+    T.ct4 = img.n_ct4 ? (const Ct4Slot *)E->ct4.p : nullptr;
+    T.ct6 = img.n_ct6 ? (const Ct6Slot *)E->ct6.p : nullptr;
+    T.ct_acct = (uint64_t *)E->ct_acct.p;
+    T.ct4_mask = img.ct4_mask;
+    T.ct4_probe = img.ct4_probe;
+    T.ct6_mask = img.ct6_mask;
+    T.ct6_probe = img.ct6_probe;
+    T.ct6_acct_base = (uint32_t)img.ct4.size();
+    E->ct4_host = std::move(img.ct4);
+    E->ct6_host = std::move(img.ct6);
+    E->st.ct4_entries = img.n_ct4;
+    E->st.ct6_entries = img.n_ct6;
     T.lxc6 = (const Lxc6Slot *)E->lxc6.p;
     T.lxc6_mask = img.lxc6_mask;
     T.lxc6_lds = img.lxc6.size() <= LXC6_LDS_MAX_SLOTS;
@@ -296,6 +396,8 @@ bool role_geometry_ok(Role r, uint32_t type, uint32_t ks, uint32_t vs)
     case ROLE_PF4_DYN: return type == MT_LPM_TRIE && ks == 8 && vs == 1;
     case ROLE_PF6_FIX: return type == MT_HASH && ks == 20 && vs == 1;
     case ROLE_PF6_DYN: return type == MT_LPM_TRIE && ks == 20 && vs == 1;
+    case ROLE_CT4: return (type == MT_LRU_HASH || type == MT_HASH) && ks == 14 && vs == 56;
+    case ROLE_CT6: return (type == MT_LRU_HASH || type == MT_HASH) && ks == 38 && vs == 56;
     default: return true;
     }
 }
@@ -304,7 +406,8 @@ bool role_geometry_ok(Role r, uint32_t type, uint32_t ks, uint32_t vs)
 // classified before it (the kernel bumps them in place in the reference)
 int before_counter_write(cfc_ctx *c, Map *m)
 {
-    if (m->role == ROLE_POLICY || m->role == ROLE_METRICS)
+    if (m->role == ROLE_POLICY || m->role == ROLE_METRICS || m->role == ROLE_CT4 ||
+        m->role == ROLE_CT6)
         return fold_counters(c, c->last_stream);
     return 0;
 }
@@ -455,8 +558,8 @@ int cfc_map_open(cfc_ctx *c, const char *path, uint32_t type, uint32_t ks,
     std::lock_guard<std::recursive_mutex> g(c->mu);
     std::string p(path);
     std::string base = p.substr(p.find_last_of('/') + 1);
-    int lxc = -1;
-    Role r = role_for(p, &lxc);
+    int lxc = -1, ct_any = 0;
+    Role r = role_for(p, &lxc, &ct_any);
     if (!role_geometry_ok(r, type, ks, vs))
         return -EINVAL;
     std::string key = r == ROLE_NONE ? p : base;
@@ -474,6 +577,7 @@ int cfc_map_open(cfc_ctx *c, const char *path, uint32_t type, uint32_t ks,
         nm->name = key;
         nm->role = r;
         nm->policy_lxc = lxc;
+        nm->ct_any = ct_any;
         nm->type = type;
         nm->ksz = ks;
         nm->vsz = vs;
@@ -509,6 +613,28 @@ int cfc_map_update(cfc_ctx *c, int fd, const void *key, const void *value,
         return -EBADF;
     int rc = before_counter_write(c, m);
     return rc ? rc : m->update(key, value, flags);
+}
+
+int cfc_map_update_batch(cfc_ctx *c, int fd, const void *keys,
+                         const void *values, uint64_t count, uint64_t flags)
+{
+    if (!c || (count && (!keys || !values)))
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Map *m = get_map(c, fd);
+    if (!m)
+        return -EBADF;
+    int rc = before_counter_write(c, m);
+    if (rc)
+        return rc;
+    const size_t vb = m->value_bytes();
+    for (uint64_t i = 0; i < count; i++) {
+        rc = m->update((const uint8_t *)keys + i * m->ksz,
+                       (const uint8_t *)values + i * vb, flags);
+        if (rc)
+            return rc;
+    }
+    return 0;
 }
 
 int cfc_map_lookup(cfc_ctx *c, int fd, const void *key, void *value)
@@ -588,7 +714,13 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     if (rc)
         return rc;
     Epoch &E = *c->epoch;
-    EgressArgs ea{ep_lxc, c->seclabel[ep_lxc], 0, 0};
+    EgressArgs ea{ep_lxc, c->seclabel[ep_lxc], 0, 0, 0};
+    {   // the sending endpoint's CT maps: its own, or the global ones
+        for (auto &kv : c->maps)
+            if ((kv.second->role == ROLE_CT4 || kv.second->role == ROLE_CT6) &&
+                kv.second->policy_lxc == (int)ep_lxc)
+                ea.ct_owner = ct_owner_word(ep_lxc, true);
+    }
     if (mode == CFC_MODE_EGRESS) {
         auto it = E.pol_loc.find(ep_lxc);
         if (it == E.pol_loc.end())
@@ -737,6 +869,288 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
 const char *cfc_strerror(int err)
 {
     return strerror(err < 0 ? -err : err);
+}
+
+}  // extern "C"
+
+namespace {
+
+// ---- cfc_ct_apply: the per-packet CT map writes of one classified batch
+struct CtApply {
+    cfc_ctx *c;
+    int family;
+    Map *lxc = nullptr;
+    std::vector<uint8_t> local = std::vector<uint8_t>(65536, 0);
+
+    explicit CtApply(cfc_ctx *cc, int fam) : c(cc), family(fam)
+    {
+        for (auto &kv : c->maps) {
+            Map *m = kv.second.get();
+            if (m->role == ROLE_LXC)
+                lxc = m;
+            if ((m->role == ROLE_CT4 || m->role == ROLE_CT6) && m->policy_lxc >= 0)
+                local[m->policy_lxc] = 1;
+        }
+    }
+    // lxc_id of the local endpoint owning addr (cilium_lxc), or -1
+    int endpoint(const uint8_t *addr) const
+    {
+        if (!lxc)
+            return -1;
+        char k[20] = {0};
+        memcpy(k, addr, family == 4 ? 4 : 16);
+        k[16] = (char)(family == 4 ? 1 : 2);
+        auto it = lxc->kv.find(std::string(k, 20));
+        if (it == lxc->kv.end() || it->second.val.size() < 8)
+            return -1;
+        uint16_t id;
+        memcpy(&id, it->second.val.data() + 6, 2);
+        return id;
+    }
+    Map *ct_map(int owner_lxc, int any) const
+    {
+        const Role r = family == 4 ? ROLE_CT4 : ROLE_CT6;
+        const int want = (owner_lxc >= 0 && local[owner_lxc]) ? owner_lxc : -1;
+        for (auto &kv : c->maps) {
+            Map *m = kv.second.get();
+            if (m->role == r && m->policy_lxc == want && m->ct_any == any)
+                return m;
+        }
+        return nullptr;
+    }
+};
+
+// struct ct_entry field offsets (bpf/lib/common.h:380-406)
+constexpr int CTE_RX_PACKETS = 0, CTE_TX_PACKETS = 16, CTE_BITS = 36,
+              CTE_REV_NAT = 38, CTE_SRC_SEC_ID = 44;
+
+void ct_hit_update(Map *m, Map::Entry &e, int action, int dir, bool count,
+                   uint32_t len)
+{
+    char *v = &e.val[0];
+    if (count) {   // CONNTRACK_ACCOUNTING for a hit the device did not see
+        uint64_t pk[2];
+        const int off = dir == 1 ? CTE_RX_PACKETS : CTE_TX_PACKETS;
+        memcpy(pk, v + off, 16);
+        pk[0] += 1;
+        pk[1] += len;
+        memcpy(v + off, pk, 16);
+    }
+    uint16_t bits;
+    memcpy(&bits, v + CTE_BITS, 2);
+    if (action == 1)         // ACTION_CREATE re-opens a closing entry
+        bits &= (uint16_t)~3u;
+    else if (action == 2)    // ACTION_CLOSE: rx_closing / tx_closing
+        bits |= dir == 1 ? 1u : 2u;
+    memcpy(v + CTE_BITS, &bits, 2);
+    m->gen++;
+}
+
+// Device slot of a CT key in the current epoch, or -1.  A write that
+// removes or replaces an entry drops the counts the batch's lookups made on
+// it (in the reference they land on the entry before it goes), so its
+// accounting slot is zeroed before the fold.
+int64_t ct_dev_slot(const Epoch &E, const Map *m, const std::string &k)
+{
+    const bool v6 = m->role == ROLE_CT6;
+    const size_t al = v6 ? 16 : 4;
+    const uint32_t owner = ct_owner_word((uint32_t)std::max(m->policy_lxc, 0),
+                                         m->policy_lxc >= 0);
+    uint32_t z;
+    memcpy(&z, k.data() + 2 * al, 4);
+    const uint8_t nh = (uint8_t)k[2 * al + 4];
+    // entries no lookup reaches are not in the device table (build_ct); the
+    // same tuple in the other map kind is a different entry
+    if (m->ct_any ? (nh != 17 && nh != (v6 ? 58 : 1)) : nh != 6)
+        return -1;
+    const uint32_t w = ct_word(nh, (uint8_t)k[2 * al + 5], owner);
+    if (!v6) {
+        if (E.ct4_host.empty())
+            return -1;
+        uint32_t x, y;
+        memcpy(&x, k.data(), 4);
+        memcpy(&y, k.data() + 4, 4);
+        const uint32_t mask = (uint32_t)E.ct4_host.size() - 1;
+        for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
+            const Ct4Slot &e = E.ct4_host[i];
+            if (!e.w)
+                return -1;
+            if (e.x == x && e.y == y && e.z == z && e.w == w)
+                return i;
+        }
+    }
+    if (E.ct6_host.empty())
+        return -1;
+    uint32_t d[4], sa[4];
+    memcpy(d, k.data(), 16);
+    memcpy(sa, k.data() + 16, 16);
+    const uint32_t mask = (uint32_t)E.ct6_host.size() - 1;
+    for (uint32_t i = ct_hash6(d, sa, z, w) & mask;; i = (i + 1) & mask) {
+        const Ct6Slot &e = E.ct6_host[i];
+        if (!e.w)
+            return -1;
+        if (e.z == z && e.w == w && !memcmp(e.d, d, 16) && !memcmp(e.s, sa, 16))
+            return (int64_t)E.ct4_host.size() + i;
+    }
+}
+
+void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t s)
+{
+    if (!c->epoch || !c->epoch->ct_acct.p)
+        return;
+    const int64_t slot = ct_dev_slot(*c->epoch, m, k);
+    if (slot >= 0)
+        (void)hipMemsetAsync((char *)c->epoch->ct_acct.p + 32 * slot, 0, 32, s);
+}
+
+template <class Hdr>
+int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode,
+             uint16_t ep_lxc, void *stream)
+{
+    if (!c || !in || !out || !out->ct || !out->verdict || !out->identity)
+        return -EINVAL;
+    if (mode < CFC_MODE_INGRESS || mode > CFC_MODE_FULL)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    const size_t n = in->n;
+    if (!n || mode == CFC_MODE_XDP)
+        return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t al = family == 4 ? 4 : 16;
+    std::vector<uint8_t> sa(al * n), da(al * n), ct(n);
+    std::vector<uint32_t> pt(n), mt(n), ident(n);
+    std::vector<int32_t> ver(n);
+    if (hipMemcpyAsync(sa.data(), in->saddr, al * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(da.data(), in->daddr, al * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(pt.data(), in->ports, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(mt.data(), in->meta, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(ident.data(), out->identity, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(ver.data(), out->verdict, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(ct.data(), out->ct, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    CtApply A(c, family);
+    const uint8_t icmp = family == 4 ? 1 : 58;
+    const uint32_t echo = family == 4 ? 8 : 128, echo_reply = family == 4 ? 0 : 129;
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t cb = ct[i];
+        if (!(cb & (CFC_CT_DONE | CFC_CT_DONE << 4)))
+            continue;
+        const uint8_t *s_ = &sa[al * i], *d_ = &da[al * i];
+        const int dst = A.endpoint(d_);
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+        const uint32_t proto = mt[i] & 0xFF, len = mt[i] >> 16;
+        for (int st = 0; st < 2; st++) {
+            const uint8_t cs = (uint8_t)(cb >> (4 * st));
+            if (!(cs & CFC_CT_DONE))
+                continue;
+            const bool eg = mode == CFC_MODE_EGRESS && st == 0;
+            const int dir = eg ? 0 : 1;   // CT_EGRESS / CT_INGRESS
+            Map *m = A.ct_map(eg ? (int)ep_lxc : dst, proto != 6);
+            if (!m)
+                continue;
+            // the tuple exactly as ct_lookup4/6 builds it (conntrack.h)
+            uint32_t td, ts, fl = dir == 1 ? 0u : 1u;
+            int action;
+            if (proto == 6 || proto == 17) {
+                td = pt[i] & 0xFFFF;
+                ts = pt[i] >> 16;
+                action = (proto == 6 && (mt[i] & CFC_HF_TCP_CLOSE)) ? 2 : 1;
+            } else if (proto == icmp) {
+                const uint32_t type = pt[i] & 0xFF;
+                const bool rel = family == 4 ? (type == 3 || type == 11 || type == 12)
+                                             : (type >= 1 && type <= 4);
+                td = (!rel && type == echo_reply) ? echo : 0;
+                ts = (!rel && type == echo) ? echo : 0;
+                fl |= rel ? 2u : 0u;
+                action = (rel || type == echo_reply) ? 0 : 1;
+            } else {
+                continue;
+            }
+            auto tuple = [&](const uint8_t *d, const uint8_t *sr, uint32_t dp,
+                             uint32_t sp, uint32_t f) {
+                char k[38];
+                memcpy(k, d, al);
+                memcpy(k + al, sr, al);
+                const uint16_t a = (uint16_t)dp, b = (uint16_t)sp;
+                memcpy(k + 2 * al, &a, 2);
+                memcpy(k + 2 * al + 2, &b, 2);
+                k[2 * al + 4] = (char)proto;
+                k[2 * al + 5] = (char)f;
+                return std::string(k, 2 * al + 6);
+            };
+            const std::string k1 = tuple(d_, s_, td, ts, fl);
+            const std::string k2 = tuple(s_, d_, ts, td, fl ^ 1u);
+            const int b = cs & CFC_CT_RES_MASK;
+            const bool dropped = st == last && ver[i] == -133;   // DROP_POLICY
+            if (b >= 2) {                       // CT_REPLY / CT_RELATED
+                auto it = m->kv.find(k1);
+                if (it != m->kv.end())
+                    ct_hit_update(m, it->second, action, dir, false, len);
+            } else if (b == 1) {                // CT_ESTABLISHED
+                auto it = m->kv.find(k2);
+                if (it != m->kv.end()) {
+                    ct_hit_update(m, it->second, action, dir, false, len);
+                    if (dropped) {              // ct_delete4/6
+                        ct_drop_counts(c, m, k2, s);
+                        (void)m->erase(k2.data());
+                    }
+                }
+            } else if (cs & CFC_CT_CREATE) {
+                auto it = m->kv.find(k2);
+                if (it != m->kv.end()) {        // created earlier in this batch
+                    ct_hit_update(m, it->second, action, dir, true, len);
+                    continue;
+                }
+                // ct_create4/6 (conntrack.h:615-662, :691-772)
+                char e[56] = {0};
+                const uint64_t one = 1, bytes = len;
+                memcpy(e + (dir == 1 ? CTE_RX_PACKETS : CTE_TX_PACKETS), &one, 8);
+                memcpy(e + (dir == 1 ? CTE_RX_PACKETS : CTE_TX_PACKETS) + 8, &bytes, 8);
+                const uint32_t sec = mode == CFC_MODE_EGRESS ? c->seclabel[ep_lxc] : ident[i];
+                memcpy(e + CTE_SRC_SEC_ID, &sec, 4);
+                if (family == 6 && dir == 1) {  // ipv6_policy, bpf_lxc.c:787-788
+                    const uint16_t rn = (uint16_t)(d_[12] | d_[13] << 8);
+                    memcpy(e + CTE_REV_NAT, &rn, 2);
+                }
+                (void)m->update(k2.data(), e, 0);
+                uint16_t bits = 16;             // seen_non_syn for ICMP
+                memcpy(e + CTE_BITS, &bits, 2);
+                const std::string ki = [&] {
+                    std::string t = k2;
+                    memset(&t[2 * al], 0, 4);
+                    t[2 * al + 4] = (char)icmp;
+                    t[2 * al + 5] = (char)((fl ^ 1u) | 2u);
+                    return t;
+                }();
+                if (m->kv.count(ki))            // overwritten
+                    ct_drop_counts(c, m, ki, s);
+                (void)m->update(ki.data(), e, 0);
+            }
+        }
+    }
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfc_ct_apply_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream)
+{
+    return ct_apply(c, 4, in, out, mode, ep_lxc, stream);
+}
+
+int cfc_ct_apply_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream)
+{
+    return ct_apply(c, 6, in, out, mode, ep_lxc, stream);
 }
 
 }  // extern "C"

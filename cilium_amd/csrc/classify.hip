@@ -115,6 +115,8 @@ struct Hdr {
     uint32_t ident, met0, met1, ctr0, ctr1;
     bool xdp_drop, need_pol, skip_proxy;
     uint32_t pbase, pmask, egress_bit, dport;
+    uint32_t ct_byte, ct_slot;   // CT byte (CFC_CT_*), stage-1 hit slot
+    int ct_res;
     PolicyProbe P;
 };
 
@@ -176,7 +178,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
 
 // round 3: second-level LPM, endpoint resolution, prefilter verdict,
 // identity, and the first policy key that may exist
-template <int MODE>
+template <int MODE, bool CT>
 __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
                                             const EgressArgs &E, Hdr &h)
 {
@@ -223,6 +225,9 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
 
     h.need_pol = h.skip_proxy = false;
     h.pbase = h.pmask = h.egress_bit = h.dport = 0;
+    h.ct_byte = 0;
+    h.ct_slot = NONE;
+    h.ct_res = CT_NEW;
     if (MODE == CFC_MODE_XDP || h.xdp_drop)
         return;
     const uint32_t proto = h.mt & 0xFF;
@@ -252,6 +257,15 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
                 h.need_pol = true;
                 h.pbase = h.rec.y;
                 h.pmask = h.rec.z;
+                if (CT) {   // ipv4_policy's ct_lookup4 (bpf_lxc.c:932)
+                    const CtResult c = ct_stage4(
+                        T, h.sa, h.da, proto, h.pt, CT_INGRESS,
+                        ct_owner_word(h.rec.w & 0xFFFF, (h.rec.w & LXC_CT_LOCAL) != 0));
+                    h.dport = c.dport;
+                    h.ct_res = c.res;
+                    h.ct_slot = c.slot;
+                    h.ct_byte = (uint32_t)c.res | CTO_DONE;
+                }
             }
         }
     } else {
@@ -272,6 +286,14 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
             h.pbase = E.pol_base;
             h.pmask = E.pol_mask;
             h.egress_bit = 1;
+            if (CT) {   // handle_ipv4_from_lxc's ct_lookup4 (bpf_lxc.c:509)
+                const CtResult c = ct_stage4(T, h.sa, h.da, proto, h.pt,
+                                             CT_EGRESS, E.ct_owner);
+                h.dport = c.dport;
+                h.ct_res = c.res;
+                h.ct_slot = c.slot;
+                h.ct_byte = (uint32_t)c.res | CTO_DONE;
+            }
         }
     }
     if (h.need_pol) {
@@ -288,13 +310,17 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
 // to different fields of `h` get merged by the compiler into one store
 // through a selected field address, which pushes the whole per-header state
 // array into scratch memory.
-template <int MODE>
+template <int MODE, bool CT>
 __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                                            const EgressArgs &E, Hdr &h)
 {
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     if (!h.need_pol)
         return;
+    // replies and related packets pass whatever the policy says
+    // (bpf_lxc.c:963-970 ingress, :538-545 egress)
+    const bool reply = CT && h.ct_res >= CT_REPLY;
+    uint32_t ctb = h.ct_byte;
     const bool frag = (h.mt & CFC_HF_FRAG) != 0;
     const uint32_t proto = h.mt & 0xFF;
     const PolicyResult pr = policy_resolve(T, h.pbase, h.pmask, h.P);
@@ -303,17 +329,27 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     int v = pr.verdict;
     int act, ver;
     uint32_t met0 = NONE, met1 = NONE, ctr1 = NONE;
-    if (v < 0) {
+    const uint32_t len = h.mt >> 16;
+    if (CT) {
+        // (lanes past the end of the slice redo its last header: not counted)
+        ct_account(T, h.valid ? h.ct_slot : NONE, EGR ? CT_EGRESS : CT_INGRESS, len);
+        // ct_create4 for a new flow that is not dropped here
+        if (h.ct_res == CT_NEW && (v >= 0 || reply))
+            ctb |= CTO_CREATE;
+    }
+    if (v < 0 && !reply) {
         act = TC_ACT_SHOT;
         ver = DROP_POLICY;
         met0 = mkey<MODE>(DROP_POLICY, mdir);
     } else if (!EGR) {
         if (h.skip_proxy)
             v = 0;
-        // redirect_to_proxy, or TRACE_TO_LXC + delivery
-        act = (v > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
-        ver = v;
-        met0 = v > 0 ? NONE : mkey<MODE>(0, METRIC_INGRESS);
+        // redirect_to_proxy for NEW / ESTABLISHED flows, or TRACE_TO_LXC +
+        // delivery
+        const bool prox = v > 0 && !reply;
+        act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+        ver = prox ? v : 0;
+        met0 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
     } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
         act = TC_ACT_REDIRECT;
         ver = v;
@@ -330,20 +366,35 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
             met1 = mkey<MODE>(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
         } else {
             // local delivery: the destination's ipv4_policy with
-            // src = SECLABEL of the sending endpoint
+            // src = SECLABEL of the sending endpoint, after its own
+            // ct_lookup4 in the destination's CT maps
+            uint32_t dp2 = h.dport;
+            CtResult c2{CT_NEW, NONE, 0};
+            if (CT) {
+                c2 = ct_stage4(T, h.sa, h.da, proto, h.pt, CT_INGRESS,
+                               ct_owner_word(h.rec.w & 0xFFFF,
+                                             (h.rec.w & LXC_CT_LOCAL) != 0));
+                dp2 = c2.dport;
+                ct_account(T, h.valid ? c2.slot : NONE, CT_INGRESS, len);
+            }
+            const bool reply2 = CT && c2.res >= CT_REPLY;
             const PolicyResult pw = policy_access(T, S, h.rec.y, h.rec.z,
-                                                  E.seclabel, h.dport, proto,
+                                                  E.seclabel, dp2, proto,
                                                   0, frag);
             const int w = pw.verdict;
             ctr1 = pw.ctr;
-            if (w < 0) {
+            if (CT)
+                ctb |= ((uint32_t)c2.res | CTO_DONE |
+                        ((c2.res == CT_NEW && (w >= 0 || reply2)) ? CTO_CREATE : 0u)) << 4;
+            if (w < 0 && !reply2) {
                 act = TC_ACT_SHOT;
                 ver = DROP_POLICY;
                 met1 = mkey<MODE>(DROP_POLICY, METRIC_INGRESS);
             } else {
-                act = (w > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
-                ver = w;
-                met1 = w > 0 ? NONE : mkey<MODE>(0, METRIC_INGRESS);
+                const bool prox = w > 0 && !reply2;
+                act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                ver = prox ? w : 0;
+                met1 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
             }
         }
     }
@@ -353,6 +404,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     h.met1 = met1;
     h.ctr0 = pr.ctr;
     h.ctr1 = ctr1;
+    h.ct_byte = ctb;
 }
 
 // LDS image of one launch: the metrics block, then the tables copied in.
@@ -374,7 +426,7 @@ __host__ LdsPlan lds_plan(const DevTables &T)
     return p;
 }
 
-template <int MODE, int U>
+template <int MODE, int U, bool CT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
     uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
@@ -419,10 +471,10 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             r2_issue<MODE>(T, S, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r3_identity<MODE>(T, S, E, h[u]);
+            r3_identity<MODE, CT>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r4_verdict<MODE>(T, S, E, h[u]);
+            r4_verdict<MODE, CT>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
@@ -433,6 +485,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                 st_nt(h[u].ident, out.identity + o);
                 if (out.action)
                     out.action[o] = (uint8_t)h[u].act;
+                if (CT && out.ct)
+                    out.ct[o] = (uint8_t)h[u].ct_byte;
                 if (MODE != CFC_MODE_XDP) {
                     st_nt(h[u].ctr0, ctr_idx + o);
                     if (MODE == CFC_MODE_EGRESS)
@@ -554,13 +608,13 @@ __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
         dst[i] += src[i];
 }
 
-template <int MODE>
+template <int MODE, bool CT>
 void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                  const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
                  uint32_t grid, uint64_t per_block, hipStream_t s)
 {
     const LdsPlan L = lds_plan(T);
-    auto kern = k_classify_v4<MODE, CFC_UNROLL>;
+    auto kern = k_classify_v4<MODE, CFC_UNROLL, CT>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
@@ -622,21 +676,20 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
     const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
     if (tm)
         (void)hipEventRecord(tm->ev[0], s);
+    // conntrack lookups when CT maps hold entries or the caller wants the
+    // CT byte (to fold creates into the maps); an empty map misses anyway
+    const bool ct = T.ct4 || out.ct;
+#define CFC_LAUNCH(M)                                                          \
+    (ct ? launch_mode<M, true>(T, in, out, E, ws, g_met, grid, per_block, s)   \
+        : launch_mode<M, false>(T, in, out, E, ws, g_met, grid, per_block, s))
     switch (mode) {
-    case CFC_MODE_INGRESS:
-        launch_mode<CFC_MODE_INGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
-    case CFC_MODE_EGRESS:
-        launch_mode<CFC_MODE_EGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
-    case CFC_MODE_XDP:
-        launch_mode<CFC_MODE_XDP>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
-    case CFC_MODE_FULL:
-        launch_mode<CFC_MODE_FULL>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
+    case CFC_MODE_INGRESS: CFC_LAUNCH(CFC_MODE_INGRESS); break;
+    case CFC_MODE_EGRESS: CFC_LAUNCH(CFC_MODE_EGRESS); break;
+    case CFC_MODE_XDP: launch_mode<CFC_MODE_XDP, false>(T, in, out, E, ws, g_met, grid, per_block, s); break;
+    case CFC_MODE_FULL: CFC_LAUNCH(CFC_MODE_FULL); break;
     default: return -22;
     }
+#undef CFC_LAUNCH
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
     launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s);

@@ -15,6 +15,7 @@ struct EgressArgs {
     uint32_t seclabel;
     uint32_t pol_base;
     uint32_t pol_mask;
+    uint32_t ct_owner;   // ct_owner_word of the sending endpoint's CT maps
 };
 
 // The counter kernel keeps one packed u64 per policy entry in LDS when

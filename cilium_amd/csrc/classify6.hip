@@ -182,7 +182,7 @@ __host__ LdsPlan6 lds_plan6(const DevTables &T)
     return p;
 }
 
-template <int MODE>
+template <int MODE, bool CT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     DevTables T, LdsPlan6 L, cfc_hdr_v6 in, cfc_out out, EgressArgs E,
     uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
@@ -229,6 +229,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
 
         int act = TC_ACT_OK, ver = 0;
         uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
+        uint32_t ctb = 0;   // CT byte (cfc.h CFC_CT_*)
+        const uint32_t len = mt >> 16;
         const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
         const bool local = (drec.z & LXC_VALID) != 0;
         bool done = false;
@@ -286,18 +288,32 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                             ver = DROP_CT_UNKNOWN_PROTO;
                             met0 = mkey6<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
                         } else {
+                            // ipv6_policy's ct_lookup6 (bpf_lxc.c:808)
+                            CtResult c{CT_NEW, NONE, dport};
+                            if (CT) {
+                                c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS,
+                                              ct_owner_word(drec.z & 0xFFFF,
+                                                            (drec.z & LXC_CT_LOCAL) != 0));
+                                ct_account(T, (!valid || c.slot == NONE) ? NONE : c.slot + T.ct6_acct_base,
+                                           CT_INGRESS, len);
+                            }
+                            const bool reply = CT && c.res >= CT_REPLY;
                             const PolicyResult pr = policy_access(
-                                T, S, drec.x, drec.y, ident, dport, proto, 0, false);
+                                T, S, drec.x, drec.y, ident, c.dport, proto, 0, false);
                             ctr0 = pr.ctr;
-                            if (pr.verdict < 0) {
+                            if (CT)
+                                ctb = (uint32_t)c.res | CTO_DONE |
+                                      ((c.res == CT_NEW && pr.verdict >= 0) ? CTO_CREATE : 0u);
+                            if (pr.verdict < 0 && !reply) {
                                 act = TC_ACT_SHOT;
                                 ver = DROP_POLICY;
                                 met0 = mkey6<MODE>(DROP_POLICY, METRIC_INGRESS);
                             } else {
                                 const int v = skip_proxy ? 0 : pr.verdict;
-                                act = (v > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
-                                ver = v;
-                                met0 = v > 0 ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
+                                const bool prox = v > 0 && !reply;
+                                act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                                ver = prox ? v : 0;
+                                met0 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
                             }
                         }
                     }
@@ -323,10 +339,21 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     ident = label ? label
                           : (da.x == ROUTER6_W0 && da.y == ROUTER6_W1) ? CLUSTER_ID
                                                                         : WORLD_ID;
+                    // ipv6_l3_from_lxc's ct_lookup6 (bpf_lxc.c:190)
+                    CtResult c{CT_NEW, NONE, dport};
+                    if (CT) {
+                        c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_EGRESS, E.ct_owner);
+                        ct_account(T, (!valid || c.slot == NONE) ? NONE : c.slot + T.ct6_acct_base,
+                                   CT_EGRESS, len);
+                    }
+                    const bool reply = CT && c.res >= CT_REPLY;
                     const PolicyResult pr = policy_access(T, S, E.pol_base, E.pol_mask,
-                                                          ident, dport, proto, 1, false);
+                                                          ident, c.dport, proto, 1, false);
                     ctr0 = pr.ctr;
-                    if (pr.verdict < 0) {
+                    if (CT)
+                        ctb = (uint32_t)c.res | CTO_DONE |
+                              ((c.res == CT_NEW && pr.verdict >= 0) ? CTO_CREATE : 0u);
+                    if (pr.verdict < 0 && !reply) {
                         ver = DROP_POLICY;
                         met0 = mkey6<MODE>(DROP_POLICY, METRIC_EGRESS);
                     } else if (pr.verdict > 0) {   // to the proxy
@@ -345,16 +372,30 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                         } else {
                             // ipv6_local_delivery into the destination's
                             // ipv6_policy with src = SECLABEL
+                            CtResult c2{CT_NEW, NONE, dport};
+                            if (CT) {
+                                c2 = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS,
+                                               ct_owner_word(drec.z & 0xFFFF,
+                                                             (drec.z & LXC_CT_LOCAL) != 0));
+                                ct_account(T, (!valid || c2.slot == NONE) ? NONE : c2.slot + T.ct6_acct_base,
+                                           CT_INGRESS, len);
+                            }
+                            const bool reply2 = CT && c2.res >= CT_REPLY;
                             const PolicyResult pw = policy_access(
-                                T, S, drec.x, drec.y, E.seclabel, dport, proto, 0, false);
+                                T, S, drec.x, drec.y, E.seclabel, c2.dport, proto, 0, false);
                             ctr1 = pw.ctr;
-                            if (pw.verdict < 0) {
+                            if (CT)
+                                ctb |= ((uint32_t)c2.res | CTO_DONE |
+                                        ((c2.res == CT_NEW && pw.verdict >= 0) ? CTO_CREATE : 0u))
+                                       << 4;
+                            if (pw.verdict < 0 && !reply2) {
                                 ver = DROP_POLICY;
                                 met1 = mkey6<MODE>(DROP_POLICY, METRIC_INGRESS);
                             } else {
-                                act = (pw.verdict > 0 || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
-                                ver = pw.verdict;
-                                met1 = pw.verdict > 0 ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
+                                const bool prox = pw.verdict > 0 && !reply2;
+                                act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                                ver = prox ? pw.verdict : 0;
+                                met1 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
                             }
                         }
                     }
@@ -365,12 +406,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         st_nt(ident, out.identity + i);
         if (out.action)
             out.action[i] = (uint8_t)act;
+        if (CT && out.ct)
+            out.ct[i] = (uint8_t)ctb;
         if (MODE != CFC_MODE_XDP) {
             st_nt(ctr0, ctr_idx + i);
             if (EGR)
                 st_nt(ctr1, ctr_idx + ctr_stride(in.n) + i);
         }
-        const uint32_t len = mt >> 16;
         acc.add(valid ? met0 : NONE, len);
         if (EGR)
             acc.add(valid ? met1 : NONE, len);
@@ -389,13 +431,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     }
 }
 
-template <int MODE>
+template <int MODE, bool CT>
 void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
                   const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
                   uint32_t grid, uint64_t per_block, hipStream_t s)
 {
     const LdsPlan6 L = lds_plan6(T);
-    auto kern = k_classify_v6<MODE>;
+    auto kern = k_classify_v6<MODE, CT>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
@@ -426,21 +468,18 @@ int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
     const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
     if (tm)
         (void)hipEventRecord(tm->ev[0], s);
+    const bool ct = T.ct6 || out.ct;
+#define CFC_LAUNCH6(M)                                                         \
+    (ct ? launch_mode6<M, true>(T, in, out, E, ws, g_met, grid, per_block, s)  \
+        : launch_mode6<M, false>(T, in, out, E, ws, g_met, grid, per_block, s))
     switch (mode) {
-    case CFC_MODE_INGRESS:
-        launch_mode6<CFC_MODE_INGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
-    case CFC_MODE_EGRESS:
-        launch_mode6<CFC_MODE_EGRESS>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
-    case CFC_MODE_XDP:
-        launch_mode6<CFC_MODE_XDP>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
-    case CFC_MODE_FULL:
-        launch_mode6<CFC_MODE_FULL>(T, in, out, E, ws, g_met, grid, per_block, s);
-        break;
+    case CFC_MODE_INGRESS: CFC_LAUNCH6(CFC_MODE_INGRESS); break;
+    case CFC_MODE_EGRESS: CFC_LAUNCH6(CFC_MODE_EGRESS); break;
+    case CFC_MODE_XDP: launch_mode6<CFC_MODE_XDP, false>(T, in, out, E, ws, g_met, grid, per_block, s); break;
+    case CFC_MODE_FULL: CFC_LAUNCH6(CFC_MODE_FULL); break;
     default: return -22;
     }
+#undef CFC_LAUNCH6
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
     launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s);

@@ -22,7 +22,8 @@ uint64_t HostImage::device_bytes() const
            4ull * l4c.size() + 8ull * l4l.size() +
            sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size() +
            ipc6.bytes() + pf6_fix.bytes() + pf6_dyn.bytes() +
-           sizeof(Lxc6Slot) * lxc6.size();
+           sizeof(Lxc6Slot) * lxc6.size() + sizeof(Ct4Slot) * ct4.size() +
+           sizeof(Ct6Slot) * ct6.size() + 32ull * (ct4.size() + ct6.size());
 }
 
 // DIR-24-8: every prefix <= /24 fills its tbl24 range in ascending length
@@ -407,7 +408,8 @@ static uint32_t lxc_info(const HostImage *img, const uint8_t *v, PolLoc *loc)
     memcpy(&id, v + 6, 2);
     memcpy(&flags, v + 8, 4);
     uint32_t info = id | LXC_VALID | ((flags & 1) ? LXC_HOST : 0) |
-                    (ifindex ? LXC_IFINDEX : 0);
+                    (ifindex ? LXC_IFINDEX : 0) |
+                    (img->ct_local.size() > id && img->ct_local[id] ? LXC_CT_LOCAL : 0);
     auto it = img->pol_loc.find(id);
     *loc = PolLoc();
     if (it != img->pol_loc.end()) {
@@ -428,10 +430,94 @@ static Lxc6Slot lxc6_slot(const HostImage *img, const uint8_t *k, const uint8_t 
     return r;
 }
 
+uint64_t ct_map_key(int family, uint32_t owner, int any)
+{
+    return (uint64_t)family << 40 | (uint64_t)owner << 8 | (uint64_t)any;
+}
+
+// CT maps -> one open-addressed table per family (layout.h).  Entries no
+// lookup can reach (nexthdr not served by their map) are left out.
+static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
+{
+    size_t n4 = 0, n6 = 0;
+    for (const Map *m : cts)
+        (m->role == ROLE_CT4 ? n4 : n6) += m->kv.size();
+    auto reachable = [](const Map *m, uint8_t nh) {
+        const uint8_t icmp = m->role == ROLE_CT4 ? 1 : 58;
+        return m->ct_any ? (nh == 17 || nh == icmp) : nh == 6;
+    };
+    if (n4) {
+        uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n4));
+        img->ct4.assign(ns, Ct4Slot{});
+        img->ct4_mask = ns - 1;
+    }
+    if (n6) {
+        uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n6));
+        img->ct6.assign(ns, Ct6Slot{});
+        img->ct6_mask = ns - 1;
+    }
+    for (const Map *m : cts) {
+        const bool v6 = m->role == ROLE_CT6;
+        if (m->ksz != (v6 ? 38u : 14u))
+            continue;
+        const uint32_t owner = ct_owner_word((uint32_t)std::max(m->policy_lxc, 0),
+                                             m->policy_lxc >= 0);
+        for (const auto &kv : m->kv) {
+            const uint8_t *k = (const uint8_t *)kv.first.data();
+            const uint32_t al = v6 ? 16 : 4;
+            const uint8_t nh = k[2 * al + 4], fl = k[2 * al + 5];
+            if (!reachable(m, nh) || (fl & ~7u))
+                continue;
+            uint32_t z;
+            memcpy(&z, k + 2 * al, 4);
+            const uint32_t w = ct_word(nh, fl, owner);
+            if (!v6) {
+                Ct4Slot e;
+                memcpy(&e.x, k, 4);
+                memcpy(&e.y, k + 4, 4);
+                e.z = z;
+                e.w = w;
+                uint32_t i = ct_hash4(e.x, e.y, e.z, e.w) & img->ct4_mask, p = 0;
+                while (img->ct4[i].w) {
+                    i = (i + 1) & img->ct4_mask;
+                    p++;
+                }
+                img->ct4[i] = e;
+                img->ct4_probe = std::max(img->ct4_probe, p);
+                img->n_ct4++;
+            } else {
+                Ct6Slot e{};
+                memcpy(e.d, k, 16);
+                memcpy(e.s, k + 16, 16);
+                e.z = z;
+                e.w = w;
+                uint32_t i = ct_hash6(e.d, e.s, e.z, e.w) & img->ct6_mask, p = 0;
+                while (img->ct6[i].w) {
+                    i = (i + 1) & img->ct6_mask;
+                    p++;
+                }
+                img->ct6[i] = e;
+                img->ct6_probe = std::max(img->ct6_probe, p);
+                img->n_ct6++;
+            }
+            if (m->policy_lxc >= 0)
+                img->ct_local[m->policy_lxc] = 1;
+        }
+        if (m->policy_lxc >= 0)
+            img->ct_local[m->policy_lxc] = 1;
+    }
+}
+
 void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
                  HostImage *img)
 {
     *img = HostImage();
+    img->ct_local.assign(65536, 0);
+    std::vector<const Map *> cts;
+    for (Map *m : maps)
+        if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
+            cts.push_back(m);
+    build_ct(cts, img);
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,
               *pf4dyn = nullptr, *pf6fix = nullptr, *pf6dyn = nullptr;
     std::map<int, Map *> pols;

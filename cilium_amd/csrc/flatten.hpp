@@ -70,8 +70,17 @@ struct HostImage {
     std::vector<Lxc6Slot> lxc6;
     uint32_t lxc6_mask = 0, n_eps6 = 0;
     std::vector<std::pair<Map *, std::string>> ctr_owner;  // ctr -> entry
+    // conntrack (layout.h): every CT map in one table per family
+    std::vector<Ct4Slot> ct4;
+    std::vector<Ct6Slot> ct6;
+    uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
+    uint32_t n_ct4 = 0, n_ct6 = 0;           // entries placed
+    std::vector<uint8_t> ct_local;           // lxc_id -> has local CT maps
     uint64_t device_bytes() const;
 };
+
+// the CT map a slot's entry lives in: (family 4/6, owner word, any) key
+uint64_t ct_map_key(int family, uint32_t owner, int any);
 
 // maps: every map of the context.
 void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,

@@ -175,6 +175,141 @@ __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
     return proto == 1;
 }
 
+// ---- conntrack: ct_lookup4 / ct_lookup6 (conntrack.h:467-590, :310-437)
+constexpr int CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3;
+constexpr int CT_EGRESS = 0, CT_INGRESS = 1;
+constexpr uint32_t CTO_DONE = 4u, CTO_CREATE = 8u;   // per-stage CT byte bits
+
+// The tuple words of the two probes.  k1 is the tuple as loaded (packet
+// addresses, L4 ports loaded into {dport, sport}, TUPLE_F_OUT for ingress /
+// TUPLE_F_IN for egress): a hit is CT_REPLY, or CT_RELATED when the ICMP type
+// set TUPLE_F_RELATED.  k2 = ipv4_ct_tuple_reverse(k1): a hit is
+// CT_ESTABLISHED, a miss CT_NEW.  td/ts: tuple->dport/sport of k1; the
+// policy port is td after a k1 hit and ts otherwise.
+struct CtProbe {
+    uint32_t z1, z2, w1, w2, td, ts;
+};
+template <bool V6>
+__device__ __forceinline__ CtProbe ct_probe(uint32_t proto, uint32_t pt,
+                                            int dir, uint32_t owner)
+{
+    CtProbe k;
+    uint32_t fl = dir == CT_INGRESS ? 0u : 1u;
+    if (proto == 6 || proto == 17) {
+        k.td = pt & 0xFFFF;
+        k.ts = pt >> 16;
+    } else {   // ICMP / ICMPv6 (callers drop other protocols first)
+        const uint32_t type = pt & 0xFF;
+        const bool related = V6 ? (type >= 1 && type <= 4)
+                                : (type == 3 || type == 11 || type == 12);
+        const uint32_t echo = V6 ? 128u : 8u, reply = V6 ? 129u : 0u;
+        k.td = (!related && type == reply) ? echo : 0u;
+        k.ts = (!related && type == echo) ? echo : 0u;
+        fl |= related ? 2u : 0u;
+    }
+    k.z1 = k.td | k.ts << 16;
+    k.z2 = k.ts | k.td << 16;
+    k.w1 = ct_word(proto, fl, owner);
+    k.w2 = ct_word(proto, fl ^ 1u, owner);
+    return k;
+}
+
+__device__ __forceinline__ uint32_t ct4_find(const DevTables &T, uint32_t x,
+                                             uint32_t y, uint32_t z, uint32_t w)
+{
+    if (!T.ct4)
+        return NONE;
+    uint32_t i = ct_hash4(x, y, z, w) & T.ct4_mask;
+    for (uint32_t p = 0; p <= T.ct4_probe; p++) {
+        const uint4 s = ld16(T.ct4 + i);
+        if (s.w == 0)
+            break;
+        if (s.x == x && s.y == y && s.z == z && s.w == w)
+            return i;
+        i = (i + 1) & T.ct4_mask;
+    }
+    return NONE;
+}
+
+__device__ __forceinline__ uint32_t ct6_find(const DevTables &T, const uint4 &d,
+                                             const uint4 &sa, uint32_t z,
+                                             uint32_t w)
+{
+    if (!T.ct6)
+        return NONE;
+    const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {sa.x, sa.y, sa.z, sa.w};
+    uint32_t i = ct_hash6(dw, sw, z, w) & T.ct6_mask;
+    for (uint32_t p = 0; p <= T.ct6_probe; p++) {
+        const Ct6Slot *e = T.ct6 + i;
+        const uint4 t = ld16(&e->z);
+        if (t.y == 0)
+            break;
+        if (t.x == z && t.y == w) {
+            const uint4 a = ld16(e->d), b = ld16(e->s);
+            if (a.x == d.x && a.y == d.y && a.z == d.z && a.w == d.w &&
+                b.x == sa.x && b.y == sa.y && b.z == sa.z && b.w == sa.w)
+                return i;
+        }
+        i = (i + 1) & T.ct6_mask;
+    }
+    return NONE;
+}
+
+// One CT lookup stage: result, hit slot (or NONE), policy port.
+struct CtResult {
+    int res;
+    uint32_t slot, dport;
+};
+__device__ __forceinline__ CtResult ct_stage4(const DevTables &T, uint32_t sa,
+                                              uint32_t da, uint32_t proto,
+                                              uint32_t pt, int dir,
+                                              uint32_t owner)
+{
+    const CtProbe k = ct_probe<false>(proto, pt, dir, owner);
+    CtResult r;
+    r.slot = ct4_find(T, da, sa, k.z1, k.w1);
+    if (r.slot != NONE) {
+        r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
+        r.dport = k.td;
+        return r;
+    }
+    r.slot = ct4_find(T, sa, da, k.z2, k.w2);
+    r.res = r.slot != NONE ? CT_ESTABLISHED : CT_NEW;
+    r.dport = k.ts;
+    return r;
+}
+__device__ __forceinline__ CtResult ct_stage6(const DevTables &T, const uint4 &sa,
+                                              const uint4 &da, uint32_t proto,
+                                              uint32_t pt, int dir,
+                                              uint32_t owner)
+{
+    const CtProbe k = ct_probe<true>(proto, pt, dir, owner);
+    CtResult r;
+    r.slot = ct6_find(T, da, sa, k.z1, k.w1);
+    if (r.slot != NONE) {
+        r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
+        r.dport = k.td;
+        return r;
+    }
+    r.slot = ct6_find(T, sa, da, k.z2, k.w2);
+    r.res = r.slot != NONE ? CT_ESTABLISHED : CT_NEW;
+    r.dport = k.ts;
+    return r;
+}
+
+// CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257): the hit
+// entry's rx (ingress) or tx (egress) packets/bytes
+__device__ __forceinline__ void ct_account(const DevTables &T, uint32_t slot,
+                                           int dir, uint32_t len)
+{
+    if (slot == NONE)
+        return;
+    unsigned long long *a =
+        reinterpret_cast<unsigned long long *>(T.ct_acct) + 4ull * slot + 2 * dir;
+    atomicAdd(a, 1ull);
+    atomicAdd(a + 1, (unsigned long long)len);
+}
+
 // __policy_can_access (policy.h:46-110) with cb[CB_POLICY] == 0, split in
 // two halves so the first probe overlaps other headers' lookups:
 // policy_issue() filters the three keys and loads the first slot of the

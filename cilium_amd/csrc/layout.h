@@ -88,6 +88,7 @@ struct alignas(16) PolSlot {
 constexpr uint32_t LXC_HOST = 1u << 16;       // ENDPOINT_F_HOST
 constexpr uint32_t LXC_HAS_POLICY = 1u << 17; // an endpoint program exists
 constexpr uint32_t LXC_IFINDEX = 1u << 18;    // ifindex != 0 (redirect)
+constexpr uint32_t LXC_CT_LOCAL = 1u << 19;   // has its own CT maps (else global)
 constexpr uint32_t LXC_VALID = 1u << 31;      // 0 = free slot
 struct alignas(16) LxcSlot {
     uint32_t addr;                 // be32 raw
@@ -217,6 +218,54 @@ struct alignas(16) Lxc6Slot {
 };
 constexpr uint32_t LXC6_LDS_MAX_SLOTS = 256;      // 8 KiB
 
+// ---- conntrack (cilium_ct{4,_any4,6,_any6}_{global,<lxc_id>}) ---------------
+// One open-addressed table per family holds every CT map: a slot is the
+// struct ipv{4,6}_ct_tuple plus a word naming the map.  TCP maps are only
+// ever probed with nexthdr 6 and ANY maps with the others
+// (get_ct_map4/6, bpf_lxc.c:91-107), so entries a lookup can never reach
+// (an ICMP "related" entry in a TCP map, conntrack.h:648-660) are left out
+// and the map kind is implied by nexthdr.  Linear probing, load <= 1/2,
+// w == 0 marks a free slot; ct_probe bounds the longest probe sequence.
+//   v4 slot (16 B): x daddr, y saddr, z dport | sport << 16 (tuple bytes
+//                   8-11), w = ct_word(nexthdr, flags, owner)
+//   v6 slot (48 B): daddr[4], saddr[4], {z, w, 0, 0}
+// owner: 0 = the global maps, else 1 << 11 | lxc_id << 16 (local maps).
+// Per-slot accounting (CONNTRACK_ACCOUNTING, conntrack.h:247-257) lives in
+// ct_acct[slot][dir][packets, bytes] (dir: CT_EGRESS 0 / CT_INGRESS 1).
+__host__ __device__ inline uint32_t ct_word(uint32_t nexthdr, uint32_t flags,
+                                            uint32_t owner)
+{
+    return nexthdr | (flags & 7u) << 8 | owner;
+}
+__host__ __device__ inline uint32_t ct_owner_word(uint32_t lxc, bool local)
+{
+    return local ? (1u << 11 | lxc << 16) : 0u;
+}
+__host__ __device__ inline uint32_t ct_hash4(uint32_t x, uint32_t y, uint32_t z,
+                                             uint32_t w)
+{
+    uint32_t h = fmix32(x ^ 0x9e3779b9u);
+    h = fmix32(h ^ y);
+    h = fmix32(h ^ z);
+    return fmix32(h ^ w);
+}
+__host__ __device__ inline uint32_t ct_hash6(const uint32_t d[4], const uint32_t s[4],
+                                             uint32_t z, uint32_t w)
+{
+    uint32_t h = ct_hash4(d[0], d[1], d[2], d[3]);
+    h = fmix32(h ^ s[0]);
+    h = fmix32(h ^ s[1]);
+    h = fmix32(h ^ s[2]);
+    h = fmix32(h ^ s[3]);
+    return ct_hash4(h, z, w, 0x7f4a7c15u);
+}
+struct alignas(16) Ct4Slot {
+    uint32_t x, y, z, w;
+};
+struct alignas(16) Ct6Slot {
+    uint32_t d[4], s[4], z, w, pad[2];
+};
+
 struct DevTables {
     const uint32_t *l4c;           // compact IPv4 LPM nodes, or null
     const uint64_t *l4l;           // its prefix lists
@@ -244,6 +293,13 @@ struct DevTables {
     const Lxc6Slot *lxc6;          // null when no IPv6 endpoints
     uint32_t lxc6_mask;
     uint32_t lxc6_lds;             // 1: copied to LDS
+    // conntrack (null: every map empty -> every lookup is CT_NEW)
+    const Ct4Slot *ct4;
+    const Ct6Slot *ct6;
+    uint64_t *ct_acct;             // [slot][dir][packets, bytes], v4 then v6
+    uint32_t ct4_mask, ct4_probe;
+    uint32_t ct6_mask, ct6_probe;
+    uint32_t ct6_acct_base;        // first v6 slot in ct_acct
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]

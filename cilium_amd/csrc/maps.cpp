@@ -126,10 +126,44 @@ int Map::next_key(const void *key, void *next) const
     return 0;
 }
 
-Role role_for(const std::string &path, int *policy_lxc)
+// "<decimal lxc_id>" -> id, "global" -> -1; false otherwise
+static bool parse_owner(const std::string &id, int *lxc)
+{
+    if (id == "global") {
+        *lxc = -1;
+        return true;
+    }
+    if (id.empty() || id.size() > 5 || id.find_first_not_of("0123456789") != std::string::npos)
+        return false;
+    long v = std::stol(id);
+    if (v > 0xFFFF)
+        return false;
+    *lxc = (int)v;
+    return true;
+}
+
+Role role_for(const std::string &path, int *policy_lxc, int *ct_any)
 {
     std::string b = path.substr(path.find_last_of('/') + 1);
     *policy_lxc = -1;
+    // pkg/maps/ctmap/ctmap.go:59-69: cilium_ct4_, cilium_ct_any4_, ...
+    static const struct {
+        const char *pfx;
+        Role r;
+        int any;
+    } ct[] = {{"cilium_ct4_", ROLE_CT4, 0}, {"cilium_ct_any4_", ROLE_CT4, 1},
+              {"cilium_ct6_", ROLE_CT6, 0}, {"cilium_ct_any6_", ROLE_CT6, 1}};
+    for (const auto &c : ct) {
+        const std::string pfx = c.pfx;
+        int lxc;
+        if (b.size() > pfx.size() && b.compare(0, pfx.size(), pfx) == 0 &&
+            parse_owner(b.substr(pfx.size()), &lxc)) {
+            *policy_lxc = lxc;
+            if (ct_any)
+                *ct_any = c.any;
+            return c.r;
+        }
+    }
     if (b == "cilium_ipcache")
         return ROLE_IPCACHE;
     if (b == "cilium_lxc")

@@ -30,12 +30,15 @@ enum Role {
     ROLE_PF4_DYN,   // cilium_cidr_v4_dyn
     ROLE_PF6_FIX,   // cilium_cidr_v6_fix
     ROLE_PF6_DYN,   // cilium_cidr_v6_dyn
+    ROLE_CT4,       // cilium_ct4_* / cilium_ct_any4_* (global or <lxc_id>)
+    ROLE_CT6,       // cilium_ct6_* / cilium_ct_any6_*
 };
 
 struct Map {
     std::string name;
     Role role = ROLE_NONE;
-    int policy_lxc = -1;
+    int policy_lxc = -1;   // ROLE_POLICY, ROLE_CT*: lxc_id (-1: global CT)
+    int ct_any = 0;        // ROLE_CT*: 1 = the ANY map, 0 = the TCP map
     uint32_t type = 0, ksz = 0, vsz = 0, max_entries = 0, flags = 0;
     uint64_t gen = 0;   // bumped on every mutation
 
@@ -58,6 +61,6 @@ struct Map {
     int next_key(const void *key, void *next) const;
 };
 
-Role role_for(const std::string &path, int *policy_lxc);
+Role role_for(const std::string &path, int *policy_lxc, int *ct_any = nullptr);
 
 }  // namespace cfc

@@ -46,6 +46,7 @@ class Verdicts:
     verdict: "torch.Tensor"   # int32
     identity: "torch.Tensor"  # int32 (u32 bits)
     action: "torch.Tensor | None"  # uint8
+    ct: "torch.Tensor | None" = None  # uint8 CT byte (cfc.h CFC_CT_*)
 
 
 def pack_v4(h, device="cuda"):
@@ -135,6 +136,17 @@ class Datapath:
         L.check(self.L.cfc_map_update(self.h, fd, key, value, flags),
                 "update element")
 
+    def update_batch(self, fd, keys, values, flags=0):
+        """cfc_map_update_batch (BPF_MAP_UPDATE_BATCH): numpy (n, ksz) keys
+        and (n, vsz) values."""
+        import numpy as np
+        keys = np.ascontiguousarray(keys, np.uint8)
+        values = np.ascontiguousarray(values, np.uint8)
+        assert len(keys) == len(values)
+        L.check(self.L.cfc_map_update_batch(self.h, fd, keys.ctypes.data,
+                                            values.ctypes.data, len(keys),
+                                            flags), "update batch")
+
     def lookup_element(self, fd, key: bytes):
         """bpf.LookupElement (pkg/bpf/bpf.go:177) -> value bytes or None."""
         buf = ctypes.create_string_buffer(self._vsz[fd])
@@ -196,7 +208,7 @@ class Datapath:
 
     def classify_v4(self, batch: HeaderBatchV4, mode=L.MODE_INGRESS, ep_lxc=0,
                     out: Verdicts | None = None, want_action=True,
-                    stream=None) -> Verdicts:
+                    want_ct=False, stream=None) -> Verdicts:
         import torch
         n = len(batch)
         dev = batch.saddr.device
@@ -204,7 +216,9 @@ class Datapath:
             out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
                            torch.empty(n, dtype=torch.int32, device=dev),
                            torch.empty(n, dtype=torch.uint8, device=dev)
-                           if want_action else None)
+                           if want_action else None,
+                           torch.empty(n, dtype=torch.uint8, device=dev)
+                           if want_ct else None)
         for t in (batch.saddr, batch.daddr, batch.ports, batch.meta):
             assert t.is_cuda and t.is_contiguous() and t.numel() == n
             assert t.dtype == torch.int32
@@ -212,7 +226,8 @@ class Datapath:
             assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
         hdr = L.HdrV4(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
                       _ptr(batch.meta), _ptr(batch.mark), n)
-        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action))
+        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
+                  _ptr(out.ct))
         L.check(self.L.cfc_classify_v4(self.h, ctypes.byref(hdr),
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)),"classify")
@@ -220,7 +235,7 @@ class Datapath:
 
     def classify_v6(self, batch: HeaderBatchV6, mode=L.MODE_INGRESS, ep_lxc=0,
                     out: Verdicts | None = None, want_action=True,
-                    stream=None) -> Verdicts:
+                    want_ct=False, stream=None) -> Verdicts:
         import torch
         n = len(batch)
         dev = batch.ports.device
@@ -228,7 +243,9 @@ class Datapath:
             out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
                            torch.empty(n, dtype=torch.int32, device=dev),
                            torch.empty(n, dtype=torch.uint8, device=dev)
-                           if want_action else None)
+                           if want_action else None,
+                           torch.empty(n, dtype=torch.uint8, device=dev)
+                           if want_ct else None)
         for t in (batch.saddr, batch.daddr):
             assert t.is_cuda and t.is_contiguous() and t.dtype == torch.int32
             assert t.shape == (n, 4) and t.data_ptr() % 16 == 0
@@ -239,7 +256,8 @@ class Datapath:
             assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
         hdr = L.HdrV6(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
                       _ptr(batch.meta), _ptr(batch.mark), n)
-        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action))
+        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
+                  _ptr(out.ct))
         L.check(self.L.cfc_classify_v6(self.h, ctypes.byref(hdr),
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)), "classify v6")
@@ -250,6 +268,22 @@ class Datapath:
         if isinstance(batch, HeaderBatchV6):
             return self.classify_v6(batch, mode, ep_lxc, **kw)
         return self.classify_v4(batch, mode, ep_lxc, **kw)
+
+    def ct_apply(self, batch, out: Verdicts, mode=L.MODE_INGRESS, ep_lxc=0,
+                 stream=None):
+        """cfc_ct_apply_v4/v6: fold a classified batch (out.ct set) into the
+        CT maps — creates, deletes of denied established flows, closing
+        flags — in header order.  Synchronises the stream."""
+        assert out.ct is not None, "classify with want_ct=True"
+        v6 = isinstance(batch, HeaderBatchV6)
+        hdr = (L.HdrV6 if v6 else L.HdrV4)(
+            _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+            _ptr(batch.meta), _ptr(batch.mark), len(batch))
+        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
+                  _ptr(out.ct))
+        fn = self.L.cfc_ct_apply_v6 if v6 else self.L.cfc_ct_apply_v4
+        L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
+                   self._stream(stream)), "ct apply")
 
     def counters_sync(self, stream=None):
         L.check(self.L.cfc_counters_sync(self.h, self._stream(stream)),

@@ -52,9 +52,75 @@ def load_tables(dp: Datapath, t, commit=True):
             else:
                 key = struct.pack("<I", int(p["plen"])) + bytes(p["addr"])
                 dp.update_element((dyn6 if p["dyn"] else fix6).Fd, key, b"\x00")
+    if getattr(t, "ct", None) is not None:
+        dp.ct_fds = load_ct(dp, t)
     if commit:
         dp.commit()
     return pms
+
+
+# pkg/maps/ctmap (ctmap.go:59-69): TCP and ANY maps per family, global or
+# per endpoint; LRU_HASH, key struct ipv{4,6}_ct_tuple, value struct ct_entry
+CT_TYPE, CT_VSZ = 9, 56
+
+
+def ct_map_name(family, lxc, any_map):
+    f = "4" if family == 1 else "6"
+    owner = "global" if lxc < 0 else str(lxc)
+    return f"cilium_ct{'_any' if any_map else ''}{f}_{owner}"
+
+
+def open_ct_maps(dp: Datapath, lxc_ids, max_entries=1 << 20):
+    """Every endpoint's local CT maps (the reference compiles CT_MAP_* per
+    endpoint, lxc_config.h:40-45); lxc -1 = the global maps."""
+    fds = {}
+    for lxc in lxc_ids:
+        for fam in (1, 2):
+            for any_map in (0, 1):
+                name = ct_map_name(fam, lxc, any_map)
+                fd, _ = dp.open_or_create_map(name, CT_TYPE,
+                                              14 if fam == 1 else 38, CT_VSZ,
+                                              max_entries)
+                fds[(fam, lxc, any_map)] = fd
+    return fds
+
+
+def load_ct(dp: Datapath, t):
+    ct = t.ct
+    # local CT maps (the reference's per-endpoint CT_MAP_*) for every
+    # endpoint program when the table uses them, else the global maps only
+    lxcs = set(int(x) for x in ct["lxc"])
+    if any(x >= 0 for x in lxcs):
+        lxcs |= set(int(x) for x in t.policy)
+    lxcs = sorted(lxcs | {-1})
+    n = max(1 << 16, 2 * len(ct))
+    fds = open_ct_maps(dp, lxcs, max_entries=n)
+    import numpy as np
+    for (fam, lxc, any_map), fd in fds.items():
+        sel = ct[(ct["family"] == fam) & (ct["lxc"] == lxc) & (ct["any"] == any_map)]
+        if len(sel):
+            ksz = 14 if fam == 1 else 38
+            dp.update_batch(fd, np.ascontiguousarray(sel["tuple"][:, :ksz]),
+                            np.ascontiguousarray(sel["entry"]))
+    return fds
+
+
+def ct_rows(dp: Datapath, fds):
+    """Live CT entries in the oracle's dump format (oracle/cfc_oracle.h
+    CFO_CT_ROW: u16 owner (lxc + 1, 0 global), u8 map (0 TCP / 1 ANY),
+    u8 family, tuple[40], ct_entry[56], pad[4]), sorted."""
+    import numpy as np
+    rows = []
+    for (fam, lxc, any_map), fd in fds.items():
+        for k in dp.keys(fd):
+            v = dp.lookup_element(fd, k)
+            r = bytearray(104)
+            struct.pack_into("<HBB", r, 0, lxc + 1, any_map, fam)
+            r[4:4 + len(k)] = k
+            r[44:100] = v[:56]
+            rows.append(bytes(r))
+    rows.sort(key=lambda r: r[:44])
+    return np.frombuffer(b"".join(rows), np.uint8).reshape(-1, 104).copy()
 
 
 def policy_rows(pm: policymap.PolicyMap):

@@ -663,3 +663,110 @@ def ct_from_rows(rows: np.ndarray) -> np.ndarray:
     ct["tuple"] = rows[:, 4:42]
     ct["entry"] = rows[:, 44:100]
     return ct
+
+
+def _zipf_ranks(rng, n_items, n, s=1.1):
+    """n draws of ranks 0..n_items-1 with P(k) ~ 1 / (k + 1)^s."""
+    w = 1.0 / np.power(np.arange(1, n_items + 1, dtype=np.float64), s)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return np.minimum(np.searchsorted(cdf, rng.random(n)), n_items - 1)
+
+
+def ct_entries_v4(daddr, saddr, dport, sport, proto, flags, dir_ingress,
+                  length, src_sec_id, lxc=-1):
+    """CT_DT records of flows as ct_create4 writes them (conntrack.h:
+    691-772): the flow's entry (tuple k2, rx or tx packets = 1, bytes = len,
+    src_sec_id) plus its ICMP 'related' entry ({daddr, saddr, 0, 0, ICMP,
+    flags | TUPLE_F_RELATED}, seen_non_syn) in the same map."""
+    n = len(daddr)
+    tu = np.zeros((n, 38), np.uint8)
+    tu[:, 0:4] = be32_to_bytes(byteswap32(np.asarray(daddr, np.uint32)))
+    tu[:, 4:8] = be32_to_bytes(byteswap32(np.asarray(saddr, np.uint32)))
+    tu[:, 8:10] = np.asarray(dport, np.uint16).view(np.uint8).reshape(n, 2)
+    tu[:, 10:12] = np.asarray(sport, np.uint16).view(np.uint8).reshape(n, 2)
+    tu[:, 12] = proto
+    tu[:, 13] = flags
+    ent = np.zeros((n, 56), np.uint8)
+    ev = ent.view("<u8")[:, :4]
+    one = np.ones(n, np.uint64)
+    ev[:, 0] = np.where(dir_ingress, one, 0)
+    ev[:, 1] = np.where(dir_ingress, length, 0)
+    ev[:, 2] = np.where(dir_ingress, 0, one)
+    ev[:, 3] = np.where(dir_ingress, 0, length)
+    ent[:, 44:48] = np.asarray(src_sec_id, np.uint32).view(np.uint8).reshape(n, 4)
+    ct = np.zeros(2 * n, CT_DT)
+    ct["family"] = 1
+    ct["lxc"] = lxc
+    ct["any"][:n] = np.asarray(proto) != IPPROTO_TCP
+    ct["any"][n:] = ct["any"][:n]
+    ct["tuple"][:n] = tu
+    rel = tu.copy()
+    rel[:, 8:12] = 0
+    rel[:, 12] = IPPROTO_ICMP
+    rel[:, 13] = np.asarray(flags, np.uint8) | 2
+    ct["tuple"][n:] = rel
+    ct["entry"][:n] = ent
+    ent2 = ent.copy()
+    ent2[:, 36] = 16                                   # seen_non_syn
+    ct["entry"][n:] = ent2
+    # one entry per key (a later flow's related entry overwrites, like
+    # map_update_elem)
+    key = np.concatenate([ct["any"][:, None], ct["tuple"][:, :14]], 1)
+    _, last = np.unique(key[::-1], axis=0, return_index=True)
+    return ct[::-1][np.sort(last)]
+
+
+def config_c5(seed=5, n_flows=10_000_000, n_prefixes=100_000, n_policy=16384,
+              n_prefilter=25_000):
+    """C5: the C2 tables and prefilter plus n_flows live
+    conntrack flows into / out of the endpoint (global CT maps), half opened
+    from outside (ingress-created, TUPLE_F_IN) and half by the endpoint
+    (egress-created, TUPLE_F_OUT); TCP 70% / UDP 30%.  Returns (tables,
+    flows) where flows holds each flow's inbound header fields."""
+    t = config_c2_bench(seed, n_prefilter=n_prefilter) if n_prefixes == 100_000 \
+        else config_c2(seed, n_prefixes=n_prefixes, n_policy=n_policy)
+    rng = np.random.default_rng(seed + 501)
+    ipc = t.ipcache[t.ipcache["family"] == 1]
+    r_addr = _addr_in_prefix_v4(rng, ipc, rng.integers(0, len(ipc), size=n_flows))
+    c_addr = np.full(n_flows, LXC_IPV4, np.uint32)
+    proto = np.where(rng.random(n_flows) < 0.7, IPPROTO_TCP, IPPROTO_UDP).astype(np.uint8)
+    inbound = rng.random(n_flows) < 0.5            # opened from outside
+    svc = htons(rng.choice(PORT_SET, size=n_flows).astype(np.uint32))
+    eph = htons(rng.integers(1024, 65536, size=n_flows).astype(np.uint32))
+    # inbound packet of the flow: r -> c.  Ingress-created: (eph -> svc);
+    # egress-created reply: remote service port -> the endpoint's eph port
+    sport = np.where(inbound, eph, svc).astype(np.uint16)
+    dport = np.where(inbound, svc, eph).astype(np.uint16)
+    length = rng.integers(60, 1501, size=n_flows).astype(np.uint64)
+    # ct_create4 keys: ingress-created k2 = {r, c, dport, sport, IN};
+    # egress-created (pkt c -> r, sport=eph, dport=svc):
+    # k2 = {c, r, svc, eph, OUT}
+    d = np.where(inbound, r_addr, c_addr)
+    s = np.where(inbound, c_addr, r_addr)
+    kd = np.where(inbound, dport, sport)
+    ks = np.where(inbound, sport, dport)
+    sec = np.where(inbound, rng.integers(256, 256 + 16384, size=n_flows),
+                   EP_SECLABEL).astype(np.uint32)
+    t.ct = ct_entries_v4(byteswap32(d), byteswap32(s), kd, ks, proto,
+                         np.where(inbound, 1, 0).astype(np.uint8), inbound,
+                         length, sec)
+    flows = Headers(4, r_addr, c_addr, sport, dport, proto,
+                    np.zeros(n_flows, np.uint8), length.astype(np.uint16),
+                    np.zeros(n_flows, np.uint32))
+    return t, flows
+
+
+def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1):
+    """C5 stream into the endpoint: 95% packets of live flows drawn
+    Zipf(s) by flow (ESTABLISHED for flows opened from outside, REPLY for
+    flows the endpoint opened), 5% packets of new flows (C2 generator)."""
+    rng = np.random.default_rng(seed + 777)
+    m = int(n * (1 - new_frac))
+    pick = _zipf_ranks(rng, len(flows), m, s)
+    old = take(flows, pick)
+    old.length = rng.integers(60, 1501, size=m).astype(np.uint16)
+    new = gen_headers_v4(rng, n - m, t.ipcache, local_v4_addrs(t)[:1],
+                         local_frac=1.0, proxy_ident=proxy_identities(t))
+    h = concat([old, new])
+    return take(h, rng.permutation(n))

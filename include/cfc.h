@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 3
+#define CFC_ABI_VERSION 4
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -80,6 +80,11 @@ int cfc_map_close(cfc_ctx *ctx, int fd);
 /* bpf.UpdateElement (pkg/bpf/bpf.go:153) */
 int cfc_map_update(cfc_ctx *ctx, int fd, const void *key, const void *value,
                    uint64_t flags);
+/* BPF_MAP_UPDATE_BATCH: `count` packed keys and values, applied in order;
+ * stops at the first error and returns it (bulk loads, e.g. a restored
+ * conntrack table). */
+int cfc_map_update_batch(cfc_ctx *ctx, int fd, const void *keys,
+                         const void *values, uint64_t count, uint64_t flags);
 /* bpf.LookupElement (pkg/bpf/bpf.go:177).  LPM maps do longest-prefix
  * match like the kernel trie.  Policy-map values carry the packet/byte
  * counters as of the last cfc_counters_sync(). */
@@ -128,7 +133,10 @@ int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
 
 /* header meta word bits (cfc_hdr_v4.meta) */
 #define CFC_HF_FRAG 0x100u      /* ipv4_is_fragment() (ipv4.h:50-61) */
-#define CFC_HF_TCP_CLOSE 0x200u /* TCP RST|FIN (conntrack.h:533) */
+#define CFC_HF_TCP_CLOSE 0x200u /* what ct_lookup reads as RST|FIN
+                                   (conntrack.h:533): union tcp_flags keeps
+                                   each bitfield as its own union member, so
+                                   all of them are bit 0 of TCP byte 12 */
 
 /* Device-resident SoA batch of IPv4 headers; all pointers are device
  * pointers with n elements.  `ports` is the first 32-bit word of the L4
@@ -175,10 +183,22 @@ typedef struct {
  * router address, that the reference answers itself (icmp6_handle,
  * icmp6.h:390-412) instead of classifying; action TC_ACT_OK. */
 #define CFC_VERDICT_PUNT (-2)
+/*  ct      : (may be NULL) the CT byte of each header — what the reference's
+ *            ct_lookup4/6 returned, against the CT maps as committed when
+ *            the batch started: bits 0-1 CT_NEW 0 / ESTABLISHED 1 / REPLY 2 /
+ *            RELATED 3, bit 2 looked up, bit 3 a new flow the reference
+ *            would ct_create; bits 4-7 the same for the destination
+ *            endpoint's ingress lookup after egress local delivery.  Feed it
+ *            to cfc_ct_apply_v4/v6 to fold creates, deletes and closing
+ *            flags into the CT maps. */
+#define CFC_CT_RES_MASK 0x3u
+#define CFC_CT_DONE 0x4u
+#define CFC_CT_CREATE 0x8u
 typedef struct {
     int32_t *verdict;
     uint32_t *identity;
     uint8_t *action;
+    uint8_t *ct;
 } cfc_out;
 
 /* Classify a batch (asynchronous on `stream`).  Policy-entry and metrics
@@ -189,6 +209,31 @@ int cfc_classify_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
  * ipv6_policy (:753-895); egress ipv6_l3_from_lxc (:112-436); XDP check_v6
  * (bpf_xdp.c:132-156).  Same outputs and counters as cfc_classify_v4. */
 int cfc_classify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream);
+
+/* --------------------------------------------------------------- conntrack */
+/* CT maps are opened through cfc_map_open with the pkg/maps/ctmap names
+ * (ctmap.go:59-69): cilium_ct4_global, cilium_ct_any4_global,
+ * cilium_ct6_global, cilium_ct_any6_global, or an endpoint's local maps
+ * cilium_ct4_<lxc_id>, cilium_ct_any4_<lxc_id>, ... (LRU_HASH or HASH, key
+ * struct ipv4_ct_tuple 14 B / ipv6_ct_tuple 38 B, value struct ct_entry
+ * 56 B).  An endpoint with local maps uses them, every other the global
+ * ones.  Every classify looks them up (ct_lookup4/6: reply / related
+ * packets skip the policy verdict, the policy port of a reply is its source
+ * port) and counts hits into the entries' rx/tx packets and bytes
+ * (CONNTRACK_ACCOUNTING), visible after cfc_counters_sync().
+ *
+ * cfc_ct_apply_v4/v6 folds one classified batch (its headers and outputs,
+ * out->ct set) into the CT maps in header order, as the reference does per
+ * packet: ct_create4/6 for new flows (the flow entry and its ICMP "related"
+ * entry), ct_delete for established flows the policy now denies, the
+ * closing flags of RST/FIN (CFC_HF_TCP_CLOSE) and re-opening.  A flow seen
+ * twice in one batch is created once and counted on its second packet.
+ * Lookups inside one batch all see the maps as committed before it.
+ * Synchronises `stream`. */
+int cfc_ct_apply_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
+                    int mode, uint16_t ep_lxc, void *stream);
+int cfc_ct_apply_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
 
 /* ---------------------------------------------------------------- counters */
@@ -231,6 +276,8 @@ typedef struct {
     uint32_t endpoints_v6;
     uint32_t prefilter_v6_fix;
     uint32_t prefilter_v6_dyn;
+    uint32_t ct4_entries;       /* CT entries a lookup can reach */
+    uint32_t ct6_entries;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

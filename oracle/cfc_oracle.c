@@ -1149,11 +1149,13 @@ int cfo_ct_add(cfo_t *o, int family, int lxc, int any_map,
  * and are not modelled. */
 static void ct_hit_update(struct ctent *e, int action, int dir, uint32_t len)
 {
-    /* CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257) */
-    if (dir == CT_INGRESS) {
+    /* CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257) for a hit
+     * the batch lookup did not see (a flow created earlier in the batch);
+     * len 0 = already counted in pass 1 */
+    if (len && dir == CT_INGRESS) {
         e->rx_packets++;
         e->rx_bytes += len;
-    } else {
+    } else if (len) {
         e->tx_packets++;
         e->tx_bytes += len;
     }
@@ -1175,13 +1177,9 @@ static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
     memset(&e, 0, sizeof(e));
     e.rev_nat_index = rev_nat;
     const uint8_t *t = k2 + 4;
-    const int tcp = t[2 * alen + 4] == 6;
-    if (tcp) {  /* ct_update_timeout with seen_flags.syn = is_tcp */
-        if (dir == CT_INGRESS)
-            e.rx_flags_seen = 0x02;
-        else
-            e.tx_flags_seen = 0x02;
-    }
+    /* ct_update_timeout with seen_flags.syn = is_tcp: syn shares bit 0 of
+     * the union with every other flag bitfield (conntrack.h:86-99), so the
+     * seen-flags byte (lower_bits) stays 0 and seen_non_syn stays clear */
     if (dir == CT_INGRESS) {
         e.rx_packets = 1;
         e.rx_bytes = len;
@@ -1218,8 +1216,15 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                      const int32_t *verdict, const uint8_t *ct,
                      uint8_t *hazard)
 {
+    /* pass 1 counts every hit of the batch on the entry it hit (the maps as
+     * committed); pass 2 applies the writes in header order.  The reference
+     * interleaves the two per packet; they differ only when a write in the
+     * batch (delete, or the ICMP entry a create overwrites) lands on an entry
+     * another header of the same batch hits — a hazard (below). */
+    uint32_t *hit_idx = hazard ? calloc(o->ct_n + 1, sizeof(uint32_t)) : NULL;
+    for (int pass = 1; pass <= 2; pass++)
     for (size_t i = 0; i < n; i++) {
-        if (hazard)
+        if (hazard && pass == 1)
             hazard[i] = 0;
         const uint8_t c = ct[i];
         if (!(c & (CTO_DONE1 | CTO_DONE2)))
@@ -1246,9 +1251,25 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                         &ts) < 0)
                 continue;
             const int b = cs & 3;
+            const int64_t e1 = ct_find(o, k1), e2 = ct_find(o, k2);
+            if (pass == 1) {   /* CONNTRACK_ACCOUNTING of the lookup hits */
+                const int64_t e = b >= CT_REPLY ? e1 : b == CT_ESTABLISHED ? e2 : -1;
+                if (e >= 0) {
+                    struct ctent *x = &o->ct_ents[e];
+                    if (dir == CT_INGRESS) {
+                        x->rx_packets++;
+                        x->rx_bytes += len[i];
+                    } else {
+                        x->tx_packets++;
+                        x->tx_bytes += len[i];
+                    }
+                    if (hit_idx)
+                        hit_idx[e] = (uint32_t)i + 1;   /* last hitting header */
+                }
+                continue;
+            }
             const int created = (cs & CTO_CREATE1) != 0;
             const int dropped = s == last && verdict[i] == DROP_POLICY;
-            const int64_t e1 = ct_find(o, k1), e2 = ct_find(o, k2);
             const int rel = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) != 0;
             const int q = e1 >= 0 ? (rel ? CT_RELATED : CT_REPLY)
                           : e2 >= 0 ? CT_ESTABLISHED : CT_NEW;
@@ -1256,23 +1277,39 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 hazard[i] = 1;
             if (b == CT_REPLY || b == CT_RELATED) {
                 if (e1 >= 0)
-                    ct_hit_update(&o->ct_ents[e1], action, dir, len[i]);
+                    ct_hit_update(&o->ct_ents[e1], action, dir, 0);
             } else if (b == CT_ESTABLISHED) {
                 if (e2 >= 0) {
-                    ct_hit_update(&o->ct_ents[e2], action, dir, len[i]);
-                    if (dropped)
+                    ct_hit_update(&o->ct_ents[e2], action, dir, 0);
+                    if (dropped) {
+                        if (hit_idx && hit_idx[e2] > i + 1)
+                            hazard[hit_idx[e2] - 1] = 1;  /* hit after delete */
                         o->ct_live[e2] = 0;
+                    }
                 }
             } else if (created) {
-                if (e2 >= 0)
+                if (e2 >= 0) {
                     ct_hit_update(&o->ct_ents[e2], action, dir, len[i]);
-                else
+                } else {
+                    if (hit_idx) {   /* the ICMP entry it overwrites */
+                        uint8_t ki[CTK];
+                        uint16_t ow;
+                        memcpy(&ow, k2, 2);
+                        ct_key(ki, ow, k2[2], alen, k2 + 4, k2 + 4 + alen, 0, 0,
+                               alen == 4 ? 1 : 58,
+                               (uint8_t)(k2[4 + 2 * alen + 5] | TUPLE_F_RELATED));
+                        int64_t ei = ct_find(o, ki);
+                        if (ei >= 0 && (size_t)ei < o->ct_n && hit_idx[ei])
+                            hazard[i] = 1;
+                    }
                     ct_create(o, k2, alen, dir, len[i], sec,
                               alen == 16 && dir == CT_INGRESS
                                   ? (uint16_t)(da[12] | da[13] << 8) : 0);
+                }
             }
         }
     }
+    free(hit_idx);
 }
 
 void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,

@@ -7,6 +7,7 @@ import os
 import re
 import struct
 
+import numpy as np
 import pytest
 
 import cilium_amd as C
@@ -29,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(_lib.EXPORTS) == fns
-    assert L.cfc_abi_version() == 3
+    assert L.cfc_abi_version() == 4
     assert L.cfc_num_possible_cpus() == 1
 
 
@@ -194,3 +195,29 @@ def test_flattener_selftest():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count(": ok") == 5, r.stdout
+
+
+def test_ct_maps_host_only():
+    """pkg/maps/ctmap names and geometry; bulk load; the oracle-format dump
+    returns what was loaded (golden fixture CT state)."""
+    import golden_io as G
+    from cilium_amd import loader
+    g = G.Golden("ct_ingress_v4")
+    dp = C.host_only()
+    fds = loader.load_ct(dp, g.tables)
+    rows = loader.ct_rows(dp, fds)
+    want = np.zeros((len(g.tables.ct), 104), np.uint8)
+    ct = g.tables.ct
+    want[:, 0:2] = np.stack([(ct["lxc"] + 1) & 0xFF, (ct["lxc"] + 1) >> 8], 1)
+    want[:, 2] = ct["any"]
+    want[:, 3] = ct["family"]
+    want[:, 4:42] = ct["tuple"]
+    want[:, 44:100] = ct["entry"]
+    want = want[np.lexsort(want[:, :44].T[::-1])]
+    np.testing.assert_array_equal(rows, want)
+    # wrong geometry for a CT role
+    with pytest.raises(OSError) as e:
+        dp.open_or_create_map("cilium_ct4_global", 9, 16, 56, 1024)
+    assert e.value.errno == errno.EINVAL
+    fd, new = dp.open_or_create_map("cilium_ct_any6_77", 9, 38, 56, 1024)
+    assert new

@@ -12,7 +12,7 @@ from cilium_amd import synth as S
 from cilium_amd import _lib as L
 from cilium_amd import metricsmap
 from cilium_amd.datapath import Datapath, pack, pack_v4
-from cilium_amd.loader import load_tables, policy_rows
+from cilium_amd.loader import ct_rows, load_tables, policy_rows
 
 pytestmark = pytest.mark.gpu
 
@@ -38,12 +38,17 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     act = np.empty(n, np.int32)
     ver = np.empty(n, np.int32)
     ide = np.empty(n, np.uint32)
+    ctb = np.empty(n, np.uint8)
+    use_ct = getattr(t, "ct", None) is not None
     step = (n + chunks - 1) // chunks
     for a in range(0, n, step):
         sl = lambda x: x[a:a + step] if x is not None else None   # noqa: E731
         sub = type(b)(sl(b.saddr), sl(b.daddr), sl(b.ports), sl(b.meta),
                       sl(b.mark))
-        out = dp.classify(sub, mode, ep_lxc)
+        out = dp.classify(sub, mode, ep_lxc, want_ct=use_ct)
+        if use_ct:   # fold this batch's creates/deletes before the next one
+            dp.ct_apply(sub, out, mode, ep_lxc)
+            ctb[a:a + step] = out.ct.cpu().numpy()
         torch.cuda.synchronize()
         act[a:a + step] = out.action.cpu().numpy()
         ver[a:a + step] = out.verdict.cpu().numpy()
@@ -52,6 +57,7 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     counters = {lxc: np.array(policy_rows(pm), np.uint64).reshape(-1, 7)
                 for lxc, pm in pms.items()}
     metrics = np.array(metricsmap.dump_rows(dp), np.uint64).reshape(-1, 4)
+    run_gpu.ct = (ctb, ct_rows(dp, dp.ct_fds)) if use_ct else None
     dp.close()
     return act, ver, ide, counters, metrics
 
@@ -70,17 +76,51 @@ def test_golden(torch, name, layout):
     np.testing.assert_array_equal(metrics, g.metrics)
     # and every output, identity bits included, against the pinned oracle
     o = O.Oracle(g.tables)
-    oa, ov, oi = o.classify(g.headers, g.mode, g.ep_lxc, nthreads=8)
+    use_ct = g.ct_after is not None
+    oa, ov, oi, oct_ = o.classify(g.headers, g.mode, g.ep_lxc, nthreads=8,
+                                  want_ct=True, apply_ct=use_ct)
     np.testing.assert_array_equal(act, oa)
     np.testing.assert_array_equal(ver, ov)
     np.testing.assert_array_equal(ide, oi)
+    if use_ct:
+        # CT byte per header, and the CT maps afterwards: against the
+        # reference (clock-derived fields masked) and, every byte, the oracle
+        ctb, rows = run_gpu.ct
+        np.testing.assert_array_equal(ctb, oct_)
+        a, b = G.ct_masked(rows), G.ct_masked(g.ct_after)
+        if a.shape == b.shape:
+            for r in np.nonzero((a != b).any(1))[0][:4]:
+                cols = np.nonzero(a[r] != b[r])[0]
+                print("ct row", r, cols, a[r][cols], b[r][cols], a[r].tobytes().hex())
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(rows, o.ct_dump())
 
 
 def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     act, ver, ide, counters, metrics = run_gpu(torch, t, h, mode, ep_lxc, chunks,
                                                lpm4)
     o = O.Oracle(t)
-    oa, ov, oi = o.classify(h, mode, ep_lxc, nthreads=16)
+    use_ct = getattr(t, "ct", None) is not None
+    if use_ct:   # the same batches, each folded into CT before the next
+        step = (len(h) + chunks - 1) // chunks
+        parts = [o.classify(h.slice(a, a + step), mode, ep_lxc, nthreads=16,
+                            want_ct=True, apply_ct=True)
+                 for a in range(0, len(h), step)]
+        oa, ov, oi, oct_ = (np.concatenate([p[k] for p in parts]) for k in range(4))
+        ctb, rows = run_gpu.ct
+        bad = np.nonzero(ctb != oct_)[0]
+        assert len(bad) == 0, f"ct byte: {len(bad)} differ, first {bad[:8]}"
+        want = o.ct_dump()
+        if rows.shape == want.shape:
+            for r in np.nonzero((rows != want).any(1))[0][:6]:
+                cols = np.nonzero(rows[r] != want[r])[0]
+                print("ct row", r, cols, rows[r][cols], want[r][cols],
+                      rows[r].tobytes().hex())
+        else:
+            print("ct rows", rows.shape, want.shape)
+        np.testing.assert_array_equal(rows, want)
+    else:
+        oa, ov, oi = o.classify(h, mode, ep_lxc, nthreads=16)
     for name, a, b in (("action", act, oa), ("verdict", ver, ov),
                        ("identity", ide, oi)):
         bad = np.nonzero(a != b)[0]
@@ -324,3 +364,26 @@ def test_v6_only_endpoints_and_empty(torch):
                  np.zeros(0, S.PREFILTER_DT), {})
     for mode in (0, 2, 3):
         compare_with_oracle(torch, e, h, mode)
+
+
+@pytest.mark.parametrize("mode", [0, 3])
+def test_c5_conntrack_vs_oracle(torch, mode):
+    """C5 shape at reduced size: 300k live flows (Zipf traffic, ESTABLISHED
+    and REPLY packets, 5% new flows), three batches each folded into CT
+    (cfc_ct_apply) before the next: outputs, CT bytes, policy counters,
+    metrics and every CT entry (accounting included) bit-exact."""
+    t, flows = S.config_c5(5, n_flows=300_000, n_prefixes=100_000)
+    h = S.headers_c5(t, flows, 1_200_000, seed=31)
+    act, ver = compare_with_oracle(torch, t, h, mode, chunks=3)
+    assert (ver == 0).sum() > len(h) // 3
+
+
+def test_c5_egress_and_local_ct(torch):
+    """Egress with local delivery: the sender's and the receiver's CT maps
+    (per-endpoint local maps), two batches with apply in between."""
+    g = G.Golden("ct_egress_v4")
+    t = g.tables
+    rng = np.random.default_rng(5)
+    h = S.concat([g.headers] * 3)
+    h = S.take(h, rng.permutation(len(h)))
+    compare_with_oracle(torch, t, h, 1, ep_lxc=S.EP_LXC_ID, chunks=2)
