@@ -44,6 +44,11 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "trie"],
                     help="IPv4 ipcache device layout (cfc_set_option CFC_OPT_LPM4)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
+                    help="c2: BASELINE.json configs[1] (the metric's config); "
+                         "c5: configs[4], + conntrack with --flows live flows "
+                         "and Zipf(1.1) traffic (a side measurement)")
+    ap.add_argument("--flows", type=int, default=10_000_000)
     args = ap.parse_args()
 
     import torch
@@ -64,7 +69,12 @@ def main():
     ep_lxc = S.EP_LXC_ID if mode == 1 else 0
 
     t0 = time.time()
-    tables = S.config_c2_bench(args.seed)
+    if args.workload == "c5":
+        tables, flows = S.config_c5(args.seed, n_flows=args.flows)
+        log(f"[rank {rank}] C5 tables: {len(tables.ct)} CT entries for "
+            f"{args.flows} flows ({time.time() - t0:.1f}s)")
+    else:
+        tables = S.config_c2_bench(args.seed)
     dp = Datapath(local_rank)
     dp.set_option(LL.OPT_LPM4, {"auto": LL.LPM4_AUTO, "dir24_8": LL.LPM4_DIR24_8,
                                 "trie": LL.LPM4_TRIE}[args.lpm4])
@@ -74,7 +84,13 @@ def main():
 
     n = args.headers
     # each rank owns its shard of the stream: seed differs per rank
-    s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
+    if args.workload == "c5":
+        from cilium_amd.datapath import pack_v4
+        hb = pack_v4(S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank), dev)
+        s, d, p, m = hb.saddr, hb.daddr, hb.ports, hb.meta
+        del hb
+    else:
+        s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
     if mode == 1:
         s.fill_(S.LXC_IPV4 - (1 << 32) if S.LXC_IPV4 >= 1 << 31 else S.LXC_IPV4)
     batch = HeaderBatchV4(s, d, p, m, None)
@@ -157,6 +173,7 @@ def main():
             pm = json.load(open(tf))
             layout = {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none")
             if (pm.get("headers") == n and pm.get("mode") == args.mode
+                    and pm.get("workload", "c2") == args.workload
                     and pm.get("lpm4_layout") == layout):
                 traffic = pm.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
@@ -174,11 +191,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (seeded C2 generator, SURVEY.md §8d)",
+        "data": f"synthetic (seeded {args.workload.upper()} generator, SURVEY.md §8d)",
         "config": {
-            "workload": "C2: 100k IPv4 /8-/32 ipcache prefixes + 16384-entry "
-                        "policymap + 25k /32 prefilter deny-list, "
-                        f"{n}-header batch per GPU, mode {args.mode}",
+            "workload": ("C2: 100k IPv4 /8-/32 ipcache prefixes + 16384-entry "
+                         "policymap + 25k /32 prefilter deny-list, "
+                         if args.workload == "c2" else
+                         f"C5: C2 tables + {st['ct4_entries']} reachable CT4 "
+                         f"entries ({args.flows} live flows, global CT maps), "
+                         "95% Zipf(1.1) packets of live flows + 5% new, ")
+                        + f"{n}-header batch per GPU, mode {args.mode}",
             "headers_per_step_per_gpu": n,
             "ipcache_prefixes": st["ipcache_v4_prefixes"],
             "policy_entries": st["policy_entries"],

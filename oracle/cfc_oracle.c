@@ -1142,6 +1142,21 @@ int cfo_ct_add(cfo_t *o, int family, int lxc, int any_map,
     return 0;
 }
 
+/* n packed synth.CT_DT records (family u8, lxc i32, any u8, tuple[38],
+ * entry[56]; 100 bytes each) */
+int cfo_ct_add_n(cfo_t *o, size_t n, const uint8_t *rec)
+{
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t *r = rec + 100 * i;
+        int32_t lxc;
+        memcpy(&lxc, r + 1, 4);
+        int rc = cfo_ct_add(o, r[0], lxc, r[5], r + 6, r + 44);
+        if (rc)
+            return rc;
+    }
+    return 0;
+}
+
 /* The deterministic part of __ct_lookup's entry update (conntrack.h:221-285):
  * the per-direction packet/byte accounting, ACTION_CREATE re-opens a
  * closing entry, ACTION_CLOSE marks the direction closing.  Lifetimes, report timestamps, seen TCP flags and seen_non_syn

@@ -92,6 +92,7 @@ void cfo_counters_reset(cfo_t *o);
  * tuple = struct ipv{4,6}_ct_tuple bytes; entry = struct ct_entry (56 B). */
 int cfo_ct_add(cfo_t *o, int family, int lxc, int any_map,
                const uint8_t *tuple, const uint8_t entry[56]);
+int cfo_ct_add_n(cfo_t *o, size_t n, const uint8_t *records);
 void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint32_t *saddr, const uint32_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,

@@ -50,6 +50,7 @@ def lib():
         for f in (L.cfo_ct_apply_v4, L.cfo_ct_apply_v6):
             f.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
                           ctypes.c_size_t] + [vp] * 11
+        L.cfo_ct_add_n.argtypes = [vp, ctypes.c_size_t, vp]
         L.cfo_ct_dump.restype = ctypes.c_size_t
         L.cfo_ct_dump.argtypes = [vp, vp, ctypes.c_size_t]
         L.cfo_policy_create.argtypes = [vp, ctypes.c_uint16]
@@ -111,11 +112,9 @@ class Oracle:
             self.ct_add(t.ct)
 
     def ct_add(self, ct):
-        for e in ct:
-            tu = np.ascontiguousarray(e["tuple"], np.uint8)
-            en = np.ascontiguousarray(e["entry"], np.uint8)
-            self.L.cfo_ct_add(self.h, int(e["family"]), int(e["lxc"]),
-                              int(e["any"]), _p(tu), _p(en))
+        rec = np.ascontiguousarray(ct)
+        assert rec.dtype.itemsize == 100, rec.dtype
+        self.L.cfo_ct_add_n(self.h, len(rec), _p(rec))
 
     def _arrays(self, hdr):
         c = np.ascontiguousarray
