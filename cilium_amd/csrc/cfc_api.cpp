@@ -728,7 +728,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
     }
-    size_t need = classify_workspace_bytes(in->n, E.T.n_ctr, mode);
+    size_t need = classify_workspace_bytes(in->n, E.T.n_ctr, mode,
+                                           E.T.ct4 || E.T.ct6 || out->ct);
     if (need > c->ws_bytes) {
         if (c->ws) {
             (void)hipDeviceSynchronize();

@@ -116,6 +116,7 @@ struct Hdr {
     bool xdp_drop, need_pol, skip_proxy;
     uint32_t pbase, pmask, egress_bit, dport;
     uint32_t ct_byte, ct_slot;   // CT byte (CFC_CT_*), stage-1 hit slot
+    uint32_t ct_k1, ct_k2;       // accounting keys (slot * 2 + dir) per stage
     int ct_res;
     PolicyProbe P;
 };
@@ -228,6 +229,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     h.ct_byte = 0;
     h.ct_slot = NONE;
     h.ct_res = CT_NEW;
+    h.ct_k1 = h.ct_k2 = NONE;
     if (MODE == CFC_MODE_XDP || h.xdp_drop)
         return;
     const uint32_t proto = h.mt & 0xFF;
@@ -331,8 +333,8 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     uint32_t met0 = NONE, met1 = NONE, ctr1 = NONE;
     const uint32_t len = h.mt >> 16;
     if (CT) {
-        // (lanes past the end of the slice redo its last header: not counted)
-        ct_account(T, h.valid ? h.ct_slot : NONE, EGR ? CT_EGRESS : CT_INGRESS, len);
+        // the hit's CONNTRACK_ACCOUNTING key, aggregated by k_ct_count
+        h.ct_k1 = ct_acct_key(h.ct_slot, EGR ? CT_EGRESS : CT_INGRESS);
         // ct_create4 for a new flow that is not dropped here
         if (h.ct_res == CT_NEW && (v >= 0 || reply))
             ctb |= CTO_CREATE;
@@ -375,7 +377,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                                ct_owner_word(h.rec.w & 0xFFFF,
                                              (h.rec.w & LXC_CT_LOCAL) != 0));
                 dp2 = c2.dport;
-                ct_account(T, h.valid ? c2.slot : NONE, CT_INGRESS, len);
+                h.ct_k2 = ct_acct_key(c2.slot, CT_INGRESS);
             }
             const bool reply2 = CT && c2.res >= CT_REPLY;
             const PolicyResult pw = policy_access(T, S, h.rec.y, h.rec.z,
@@ -405,6 +407,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     h.ctr0 = pr.ctr;
     h.ctr1 = ctr1;
     h.ct_byte = ctb;
+    (void)len;
 }
 
 // LDS image of one launch: the metrics block, then the tables copied in.
@@ -429,7 +432,7 @@ __host__ LdsPlan lds_plan(const DevTables &T)
 template <int MODE, int U, bool CT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
-    uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
+    uint32_t *ctr_idx, uint32_t *ct_idx, uint64_t *g_met, uint64_t per_block)
 {
     // LDS image (uint4 units): metrics | endpoint slots | pf Bloom | pol Bloom
     unsigned long long *s_met = lds_met();
@@ -487,6 +490,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                     out.action[o] = (uint8_t)h[u].act;
                 if (CT && out.ct)
                     out.ct[o] = (uint8_t)h[u].ct_byte;
+                if (CT) {
+                    st_nt(h[u].ct_k1, ct_idx + o);
+                    if (MODE == CFC_MODE_EGRESS)
+                        st_nt(h[u].ct_k2, ct_idx + ctr_stride(in.n) + o);
+                }
                 if (MODE != CFC_MODE_XDP) {
                     st_nt(h[u].ctr0, ctr_idx + o);
                     if (MODE == CFC_MODE_EGRESS)
@@ -599,6 +607,70 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const uint64_t *partial
     }
 }
 
+// CONNTRACK_ACCOUNTING: the per-header keys (slot * 2 + dir) of a
+// <= COUNT_PER_BLOCK slice aggregated in an LDS hash table — Zipf traffic
+// puts thousands of a slice's packets on a few flows, and one global u64
+// atomic per packet on the same entry would serialise — then flushed with
+// one global atomic pair per distinct (entry, dir).  A key that finds no
+// LDS slot within 8 probes goes straight to the global counters (those are
+// the rare flows, so no contention there).
+constexpr uint32_t CT_LDS_SLOTS = 8192;
+constexpr uint32_t CT_LDS_BYTES = CT_LDS_SLOTS * 12;
+__global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
+                                                    uint64_t stride,
+                                                    const uint32_t *meta,
+                                                    uint64_t n,
+                                                    unsigned long long *acct)
+{
+    uint32_t *keys = reinterpret_cast<uint32_t *>(cfc_smem);
+    unsigned long long *vals =
+        reinterpret_cast<unsigned long long *>(keys + CT_LDS_SLOTS);
+    for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {
+        keys[j] = NONE;
+        vals[j] = 0;
+    }
+    __syncthreads();
+    const uint32_t *idx = ct_idx + blockIdx.y * stride;
+    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
+    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    for (uint64_t i = start + threadIdx.x; i < end; i += BLOCK) {
+        const uint32_t k = ld_nt(idx + i);
+        if (k == NONE)
+            continue;
+        const uint32_t len = ld_nt(meta + i) >> 16;
+        uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
+        bool done = false;
+        for (int p = 0; p < 8 && !done; p++) {
+            uint32_t cur = keys[h];
+            if (cur == NONE) {
+                cur = atomicCAS(&keys[h], NONE, k);
+                if (cur == NONE)
+                    cur = k;
+            }
+            if (cur == k) {
+                // <= 64512 packets of <= 65535 bytes: the byte half of
+                // {packets << 32 | bytes} never carries
+                atomicAdd(&vals[h], (1ull << 32) | len);
+                done = true;
+            }
+            h = (h + 1) & (CT_LDS_SLOTS - 1);
+        }
+        if (!done) {
+            atomicAdd(&acct[2ull * k], 1ull);
+            atomicAdd(&acct[2ull * k + 1], (unsigned long long)len);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {
+        const uint32_t k = keys[j];
+        const unsigned long long v = vals[j];
+        if (k != NONE && v) {
+            atomicAdd(&acct[2ull * k], v >> 32);
+            atomicAdd(&acct[2ull * k + 1], v & 0xFFFFFFFFull);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
                                                  const uint64_t *src,
                                                  uint64_t n)
@@ -623,7 +695,8 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
         attr_set = true;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
-                       out, E, ctr_idx, g_met, per_block);
+                       out, E, ctr_idx, ct_idx_ptr(ctr_idx, in.n, T.n_ctr, MODE),
+                       g_met, per_block);
 }
 
 uint64_t partial_off(uint64_t n, int mode)
@@ -645,7 +718,7 @@ int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode)
+size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode, bool ct)
 {
     if (n == 0 || mode == CFC_MODE_XDP)
         return 0;
@@ -655,7 +728,15 @@ size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode)
         const uint64_t nblk = (n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK;
         bytes += 8ull * n_ctr * nblk * halves;       // partial slabs
     }
+    if (ct)   // CT accounting key per header and stage, 256-byte aligned
+        bytes = (bytes + 255) / 256 * 256 + 4ull * partial_off(n, mode);
     return bytes;
+}
+
+uint32_t *ct_idx_ptr(uint32_t *ws, uint64_t n, uint32_t n_ctr, int mode)
+{
+    const size_t off = (classify_workspace_bytes(n, n_ctr, mode) + 255) / 256 * 256;
+    return ws + off / 4;
 }
 
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
@@ -692,7 +773,7 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 #undef CFC_LAUNCH
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
-    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s);
+    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct && mode != CFC_MODE_XDP);
     if (tm)
         (void)hipEventRecord(tm->ev[2], s);
     hipError_t e = hipGetLastError();
@@ -700,8 +781,23 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 }
 
 void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
-                     int mode, uint32_t *ws, uint64_t *g_ctr, hipStream_t s)
+                     int mode, uint32_t *ws, uint64_t *g_ctr, hipStream_t s,
+                     bool ct)
 {
+    if (ct && T.ct_acct && n) {
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void *)k_ct_count,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)CT_LDS_BYTES);
+            attr_set = true;
+        }
+        const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        hipLaunchKernelGGL(k_ct_count, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
+                           dim3(BLOCK), CT_LDS_BYTES, s,
+                           ct_idx_ptr(ws, n, T.n_ctr, mode), ctr_stride(n), meta, n,
+                           reinterpret_cast<unsigned long long *>(T.ct_acct));
+    }
     if (mode != CFC_MODE_XDP && T.n_ctr && n) {
         const uint32_t halves = mode == CFC_MODE_EGRESS ? 2 : 1;
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);

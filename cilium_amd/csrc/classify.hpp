@@ -35,7 +35,11 @@ struct LaunchTiming {
 // Bytes of workspace a launch over n headers needs: the matched policy-entry
 // index per header (two per header in EGRESS mode) + the counter kernel's
 // partial slabs.
-size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode);
+// With ct, followed by the per-header CT accounting keys
+// (slot * 2 + dir, NONE: no hit) the CT counter kernel aggregates.
+size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode,
+                                bool ct = false);
+uint32_t *ct_idx_ptr(uint32_t *ws, uint64_t n, uint32_t n_ctr, int mode);
 // LDS image of the classify kernel for these tables (must be <= 160 KiB).
 size_t classify_lds_bytes(const DevTables &T);
 
@@ -53,7 +57,7 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 // classify kernel left in the workspace (both families).
 void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
                      int mode, uint32_t *workspace, uint64_t *g_ctr,
-                     hipStream_t stream);
+                     hipStream_t stream, bool ct = false);
 
 int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,

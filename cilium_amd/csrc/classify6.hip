@@ -185,7 +185,7 @@ __host__ LdsPlan6 lds_plan6(const DevTables &T)
 template <int MODE, bool CT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     DevTables T, LdsPlan6 L, cfc_hdr_v6 in, cfc_out out, EgressArgs E,
-    uint32_t *ctr_idx, uint64_t *g_met, uint64_t per_block)
+    uint32_t *ctr_idx, uint32_t *ct_idx, uint64_t *g_met, uint64_t per_block)
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
@@ -230,6 +230,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         int act = TC_ACT_OK, ver = 0;
         uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
         uint32_t ctb = 0;   // CT byte (cfc.h CFC_CT_*)
+        uint32_t ck1 = NONE, ck2 = NONE;   // CT accounting keys per stage
         const uint32_t len = mt >> 16;
         const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
         const bool local = (drec.z & LXC_VALID) != 0;
@@ -294,8 +295,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS,
                                               ct_owner_word(drec.z & 0xFFFF,
                                                             (drec.z & LXC_CT_LOCAL) != 0));
-                                ct_account(T, (!valid || c.slot == NONE) ? NONE : c.slot + T.ct6_acct_base,
-                                           CT_INGRESS, len);
+                                ck1 = ct_acct_key(c.slot == NONE ? NONE : c.slot + T.ct6_acct_base,
+                                                  CT_INGRESS);
                             }
                             const bool reply = CT && c.res >= CT_REPLY;
                             const PolicyResult pr = policy_access(
@@ -343,8 +344,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     CtResult c{CT_NEW, NONE, dport};
                     if (CT) {
                         c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_EGRESS, E.ct_owner);
-                        ct_account(T, (!valid || c.slot == NONE) ? NONE : c.slot + T.ct6_acct_base,
-                                   CT_EGRESS, len);
+                        ck1 = ct_acct_key(c.slot == NONE ? NONE : c.slot + T.ct6_acct_base,
+                                          CT_EGRESS);
                     }
                     const bool reply = CT && c.res >= CT_REPLY;
                     const PolicyResult pr = policy_access(T, S, E.pol_base, E.pol_mask,
@@ -377,8 +378,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 c2 = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS,
                                                ct_owner_word(drec.z & 0xFFFF,
                                                              (drec.z & LXC_CT_LOCAL) != 0));
-                                ct_account(T, (!valid || c2.slot == NONE) ? NONE : c2.slot + T.ct6_acct_base,
-                                           CT_INGRESS, len);
+                                ck2 = ct_acct_key(c2.slot == NONE ? NONE : c2.slot + T.ct6_acct_base,
+                                                  CT_INGRESS);
                             }
                             const bool reply2 = CT && c2.res >= CT_REPLY;
                             const PolicyResult pw = policy_access(
@@ -408,6 +409,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             out.action[i] = (uint8_t)act;
         if (CT && out.ct)
             out.ct[i] = (uint8_t)ctb;
+        if (CT) {
+            st_nt(ck1, ct_idx + i);
+            if (EGR)
+                st_nt(ck2, ct_idx + ctr_stride(in.n) + i);
+        }
         if (MODE != CFC_MODE_XDP) {
             st_nt(ctr0, ctr_idx + i);
             if (EGR)
@@ -446,7 +452,8 @@ void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
         attr_set = true;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
-                       out, E, ctr_idx, g_met, per_block);
+                       out, E, ctr_idx, ct_idx_ptr(ctr_idx, in.n, T.n_ctr, MODE),
+                       g_met, per_block);
 }
 
 }  // namespace
@@ -482,7 +489,7 @@ int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
 #undef CFC_LAUNCH6
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
-    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s);
+    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct && mode != CFC_MODE_XDP);
     if (tm)
         (void)hipEventRecord(tm->ev[2], s);
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -297,6 +297,12 @@ __device__ __forceinline__ CtResult ct_stage6(const DevTables &T, const uint4 &s
     return r;
 }
 
+// key of ct_acct[slot][dir] (k_ct_count), NONE for a miss
+__device__ __forceinline__ uint32_t ct_acct_key(uint32_t slot, int dir)
+{
+    return slot == NONE ? NONE : slot * 2 + (uint32_t)dir;
+}
+
 // CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257): the hit
 // entry's rx (ingress) or tx (egress) packets/bytes
 __device__ __forceinline__ void ct_account(const DevTables &T, uint32_t slot,
