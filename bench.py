@@ -44,10 +44,12 @@ def main():
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "trie"],
                     help="IPv4 ipcache device layout (cfc_set_option CFC_OPT_LPM4)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c5"],
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
                     help="c2: BASELINE.json configs[1] (the metric's config); "
+                         "c3: configs[2], dual stack: 1M IPv6 + 100k IPv4 "
+                         "prefixes, 50k prefilter, half the batch each family; "
                          "c5: configs[4], + conntrack with --flows live flows "
-                         "and Zipf(1.1) traffic (a side measurement)")
+                         "and Zipf(1.1) traffic (side measurements)")
     ap.add_argument("--flows", type=int, default=10_000_000)
     args = ap.parse_args()
 
@@ -73,6 +75,8 @@ def main():
         tables, flows = S.config_c5(args.seed, n_flows=args.flows)
         log(f"[rank {rank}] C5 tables: {len(tables.ct)} CT entries for "
             f"{args.flows} flows ({time.time() - t0:.1f}s)")
+    elif args.workload == "c3":
+        tables = S.config_c3(3)
     else:
         tables = S.config_c2_bench(args.seed)
     dp = Datapath(local_rank)
@@ -83,8 +87,15 @@ def main():
     log(f"[rank {rank}] tables loaded+committed in {time.time() - t0:.1f}s: {st}")
 
     n = args.headers
+    batch6, h6 = None, None
     # each rank owns its shard of the stream: seed differs per rank
-    if args.workload == "c5":
+    if args.workload == "c3":
+        from cilium_amd.datapath import pack_v6
+        h6 = S.headers_c3(tables, n // 2, seed=args.seed * 1000 + rank)
+        batch6 = pack_v6(h6, dev)
+        n = n - n // 2
+        s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
+    elif args.workload == "c5":
         from cilium_amd.datapath import pack_v4
         hb = pack_v4(S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank), dev)
         s, d, p, m = hb.saddr, hb.daddr, hb.ports, hb.meta
@@ -96,11 +107,19 @@ def main():
     batch = HeaderBatchV4(s, d, p, m, None)
     out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
                    torch.empty(n, dtype=torch.int32, device=dev), None)
+    n6 = len(batch6) if batch6 is not None else 0
+    out6 = Verdicts(torch.empty(n6, dtype=torch.int32, device=dev),
+                    torch.empty(n6, dtype=torch.int32, device=dev), None)
+
+    def step():
+        dp.classify_v4(batch, mode, ep_lxc, out=out)
+        if n6:
+            dp.classify_v6(batch6, mode, ep_lxc, out=out6)
     torch.cuda.synchronize()
     log(f"[rank {rank}] batch of {n} headers generated ({(n * S_IN) >> 20} MiB)")
 
     for _ in range(args.warmup):
-        dp.classify_v4(batch, mode, ep_lxc, out=out)
+        step()
     torch.cuda.synchronize()
     dp.counters_clear()
     # HIP events recorded by the library on the launch stream around the
@@ -117,7 +136,7 @@ def main():
     w0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        dp.classify_v4(batch, mode, ep_lxc, out=out)
+        step()
         evs[i][1].record(stream)
     if world > 1:
         allreduce_counters(dp)   # the only collective: counter SUM over RCCL
@@ -127,16 +146,16 @@ def main():
     wall = time.perf_counter() - w0
     call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tm = dp.timing_collect()
-    assert tm["launches"] == args.steps, tm
-    kern_ms = tm["classify_ms"] / tm["launches"]    # k_classify_v4 alone
-    count_ms = tm["count_ms"] / tm["launches"]      # k_count + k_reduce_partials
+    assert tm["launches"] == args.steps * (2 if n6 else 1), tm
+    kern_ms = tm["classify_ms"] / args.steps        # classify kernel(s) per step
+    count_ms = tm["count_ms"] / args.steps          # counter kernels per step
     if world > 1:
         tw = torch.tensor([wall], device=dev, dtype=torch.float64)
         dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         wall = float(tw.item())
     if world == 1:
         dp.counters_sync()
-    total = n * world * args.steps
+    total = (n + n6) * world * args.steps
     mpps = total / wall / 1e6
     log(f"[rank {rank}] {args.steps} steps in {wall * 1e3:.2f} ms; per call "
         f"{call_ms:.3f} ms = classify {kern_ms:.3f} + counters {count_ms:.3f}; "
@@ -165,7 +184,23 @@ def main():
                   np.array_equal(out.identity[:samp].cpu().numpy().view(np.uint32), oi))
     mean_l = float(lk.mean())
     b_hdr = S_IN + S_OUT + 64.0 * mean_l
-    achieved = n * b_hdr / (kern_ms * 1e-3) / 1e9
+    algo_bytes = n * b_hdr
+    if n6:   # the IPv6 half: 40 B in per header, its own lookup counts
+        s6 = min(samp, n6)
+        hs6 = S.take(h6, slice(0, s6))
+        c1 = time.perf_counter()
+        o6a, o6v, o6i, lk6 = orc.classify(hs6, mode, ep_lxc, nthreads=cores,
+                                          want_lookups=True)
+        cpu_s += time.perf_counter() - c1
+        parity = parity and bool(
+            np.array_equal(out6.verdict[:s6].cpu().numpy(), o6v) and
+            np.array_equal(out6.identity[:s6].cpu().numpy().view(np.uint32), o6i))
+        b6 = 40 + S_OUT + 64.0 * float(lk6.mean())
+        algo_bytes += n6 * b6
+        mean_l = (n * mean_l + n6 * float(lk6.mean())) / (n + n6)
+        b_hdr = algo_bytes / (n + n6)
+        samp += s6
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(tf):
@@ -196,11 +231,16 @@ def main():
             "workload": ("C2: 100k IPv4 /8-/32 ipcache prefixes + 16384-entry "
                          "policymap + 25k /32 prefilter deny-list, "
                          if args.workload == "c2" else
+                         f"C3: dual stack, {st['ipcache_v6_prefixes']} IPv6 /32-/128 + "
+                         f"{st['ipcache_v4_prefixes']} IPv4 prefixes, "
+                         f"{st['prefilter_v4_fix'] + st['prefilter_v6_fix']}-entry "
+                         f"prefilter, {n6} IPv6 + {n} IPv4 headers per step, "
+                         if args.workload == "c3" else
                          f"C5: C2 tables + {st['ct4_entries']} reachable CT4 "
                          f"entries ({args.flows} live flows, global CT maps), "
                          "95% Zipf(1.1) packets of live flows + 5% new, ")
-                        + f"{n}-header batch per GPU, mode {args.mode}",
-            "headers_per_step_per_gpu": n,
+                        + f"{n + n6}-header batch per GPU, mode {args.mode}",
+            "headers_per_step_per_gpu": n + n6,
             "ipcache_prefixes": st["ipcache_v4_prefixes"],
             "policy_entries": st["policy_entries"],
             "prefilter_v4_fix": st["prefilter_v4_fix"],
@@ -209,7 +249,7 @@ def main():
             "parallelism": f"header-stream shards x{world}, tables replicated",
         },
         "roofline": {
-            "kernel": "k_classify_v4",
+            "kernel": "k_classify_v4" + (" + k_classify_v6" if n6 else ""),
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,
