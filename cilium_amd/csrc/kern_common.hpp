@@ -214,21 +214,29 @@ __device__ __forceinline__ CtProbe ct_probe(uint32_t proto, uint32_t pt,
     return k;
 }
 
-__device__ __forceinline__ uint32_t ct4_find(const DevTables &T, uint32_t x,
-                                             uint32_t y, uint32_t z, uint32_t w)
+// Probe sequence from slot i whose first slot s is already loaded.
+__device__ __forceinline__ uint32_t ct4_walk(const DevTables &T, uint32_t i,
+                                             uint4 s, uint32_t x, uint32_t y,
+                                             uint32_t z, uint32_t w)
 {
-    if (!T.ct4)
-        return NONE;
-    uint32_t i = ct_hash4(x, y, z, w) & T.ct4_mask;
     for (uint32_t p = 0; p <= T.ct4_probe; p++) {
-        const uint4 s = ld16(T.ct4 + i);
         if (s.w == 0)
             break;
         if (s.x == x && s.y == y && s.z == z && s.w == w)
             return i;
         i = (i + 1) & T.ct4_mask;
+        s = ld16(T.ct4 + i);
     }
     return NONE;
+}
+
+__device__ __forceinline__ uint32_t ct4_find(const DevTables &T, uint32_t x,
+                                             uint32_t y, uint32_t z, uint32_t w)
+{
+    if (!T.ct4)
+        return NONE;
+    const uint32_t i = ct_hash4(x, y, z, w) & T.ct4_mask;
+    return ct4_walk(T, i, ld16(T.ct4 + i), x, y, z, w);
 }
 
 __device__ __forceinline__ uint32_t ct6_find(const DevTables &T, const uint4 &d,
@@ -267,13 +275,24 @@ __device__ __forceinline__ CtResult ct_stage4(const DevTables &T, uint32_t sa,
 {
     const CtProbe k = ct_probe<false>(proto, pt, dir, owner);
     CtResult r;
-    r.slot = ct4_find(T, da, sa, k.z1, k.w1);
+    if (!T.ct4) {
+        r.slot = NONE;
+        r.res = CT_NEW;
+        r.dport = k.ts;
+        return r;
+    }
+    // both home slots in flight together: an ESTABLISHED or NEW packet (k1
+    // misses) then costs one HBM round trip instead of two
+    const uint32_t i1 = ct_hash4(da, sa, k.z1, k.w1) & T.ct4_mask;
+    const uint32_t i2 = ct_hash4(sa, da, k.z2, k.w2) & T.ct4_mask;
+    const uint4 s1 = ld16(T.ct4 + i1), s2 = ld16(T.ct4 + i2);
+    r.slot = ct4_walk(T, i1, s1, da, sa, k.z1, k.w1);
     if (r.slot != NONE) {
         r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
         r.dport = k.td;
         return r;
     }
-    r.slot = ct4_find(T, sa, da, k.z2, k.w2);
+    r.slot = ct4_walk(T, i2, s2, sa, da, k.z2, k.w2);
     r.res = r.slot != NONE ? CT_ESTABLISHED : CT_NEW;
     r.dport = k.ts;
     return r;
