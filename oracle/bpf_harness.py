@@ -243,3 +243,28 @@ def test_run_xdp(prog_fd, pkt: bytes):
                        ctypes.addressof(pin), ctypes.addressof(pout), 1, 0)
     _, b = _bpf(BPF_PROG_TEST_RUN, attr)
     return struct.unpack_from("<IIIIQQII", b.raw, 0)[1]
+
+
+def test_run_duration(prog_fd, pkt: bytes, mark=0, xdp=False):
+    """One BPF_PROG_TEST_RUN (repeat 1) -> (retval, in-kernel ns).  The
+    kernel's `duration` covers the program and its tail calls, not the
+    syscall around them."""
+    pin = ctypes.create_string_buffer(pkt, len(pkt))
+    pout = ctypes.create_string_buffer(len(pkt) + 512)
+    if xdp:
+        attr = struct.pack("<IIIIQQII", prog_fd, 0, len(pkt), len(pout),
+                           ctypes.addressof(pin), ctypes.addressof(pout), 1, 0)
+        _, b = _bpf(BPF_PROG_TEST_RUN, attr)
+        f = struct.unpack_from("<IIIIQQII", b.raw, 0)
+        return f[1], f[7]
+    ctx = bytearray(SKB_CTX_SIZE)
+    struct.pack_into("<I", ctx, SKB_OFF_MARK, mark)
+    cin = ctypes.create_string_buffer(bytes(ctx), SKB_CTX_SIZE)
+    cout = ctypes.create_string_buffer(SKB_CTX_SIZE)
+    attr = struct.pack("<IIIIQQIIIIQQ", prog_fd, 0, len(pkt), len(pout),
+                       ctypes.addressof(pin), ctypes.addressof(pout), 1, 0,
+                       SKB_CTX_SIZE, SKB_CTX_SIZE, ctypes.addressof(cin),
+                       ctypes.addressof(cout))
+    _, b = _bpf(BPF_PROG_TEST_RUN, attr)
+    f = struct.unpack_from("<IIIIQQIIIIQQ", b.raw, 0)
+    return f[1], f[7]
