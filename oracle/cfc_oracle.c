@@ -336,6 +336,7 @@ struct cfo {
     struct ctent *ct_ents;
     uint8_t *ct_live;
     uint32_t ct_n, ct_cap, ct_added;
+    uint32_t *notify_out; /* cfo_set_notify_out */
     uint8_t ct_local[65536];   /* endpoint has its own (local) CT maps */
 };
 
@@ -557,10 +558,30 @@ static int policy_can_access(pmap *m, uint32_t identity, uint16_t dport,
     return frag ? DROP_FRAG_NOSUPPORT : DROP_POLICY;
 }
 
+/* nt: which send_drop_notify reported a drop (drop.h:94-109), as
+ * site << 16 | EVENT_SOURCE; 0 = none.  Sites: 1 bpf_netdev's
+ * send_drop_notify_error (bpf_netdev.c:463,502), 2 the sending endpoint's
+ * (SECLABEL, dstID, 0, 0) (bpf_lxc.c:432,700), 3 the destination's
+ * tail_ipv{4,6}_policy (src_label, SECLABEL, LXC_ID, ifindex)
+ * (bpf_lxc.c:891,1024). */
 typedef struct {
     int32_t action, verdict;
     uint32_t identity;
+    uint32_t nt;
 } res_t;
+#define NT_NETDEV 1u
+#define NT_EGRESS 2u
+#define NT_POLICY 3u
+
+/* sites 1-2 follow from the mode; lxc_ingress sets site 3 itself */
+static uint32_t notify_site(int mode, uint16_t ep_lxc, const res_t *r)
+{
+    if (r->verdict >= 0 || r->verdict == -1 || r->verdict == -2)
+        return 0; /* forwarded / XDP prefilter drop / VERDICT_PUNT */
+    if (r->nt)
+        return r->nt;
+    return mode == CFO_MODE_EGRESS ? NT_EGRESS << 16 | ep_lxc : NT_NETDEV << 16;
+}
 
 
 /* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
@@ -613,7 +634,7 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
                          uint32_t len, int skip_proxy, int dir_missed,
                          int stage)
 {
-    res_t r = {TC_ACT_SHOT, 0, src};
+    res_t r = {TC_ACT_SHOT, 0, src, 0};
     if (!o->pol[ep->lxc_id]) {
         /* no endpoint program behind cilium_policy[lxc_id]: the tail call
          * in ipv4_local_delivery (l3.h:130) falls through and the caller
@@ -628,6 +649,7 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
                         dport, close, CT_INGRESS, stage, &res, &pdport);
     if (ret < 0) {
         r.verdict = ret;
+        r.nt = NT_POLICY << 16 | ep->lxc_id;
         metric(o, ret, METRIC_INGRESS, len);
         return r;
     }
@@ -637,6 +659,7 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
      * denied CT_ESTABLISHED flow loses its entry (ct_delete4) */
     if (res != CT_REPLY && res != CT_RELATED && verdict < 0) {
         r.verdict = DROP_POLICY;
+        r.nt = NT_POLICY << 16 | ep->lxc_id;
         metric(o, DROP_POLICY, METRIC_INGRESS, len);
         return r;
     }
@@ -682,7 +705,7 @@ static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
             label != CLUSTER_ID && label != HOST_ID)
             identity = label;
     }
-    res_t r = {TC_ACT_OK, 0, identity};
+    res_t r = {TC_ACT_OK, 0, identity, 0};
     tl_lookups++;
     const epinfo *ep = lxc_lookup(o, 1, (const uint8_t *)&daddr);
     if (!ep || (ep->flags & ENDPOINT_F_HOST))
@@ -698,7 +721,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
                            uint32_t daddr, uint8_t proto, uint16_t sport,
                            uint16_t dport, uint8_t hflags, uint32_t len)
 {
-    res_t r = {TC_ACT_SHOT, 0, 0};
+    res_t r = {TC_ACT_SHOT, 0, 0, 0};
     const epinfo *self = lxc_lookup(o, 1, (const uint8_t *)&saddr);
     if (!self || self->lxc_id != lxc) { /* is_valid_lxc_src_ipv4, lxc.h:55 */
         r.verdict = DROP_INVALID_SIP;
@@ -807,6 +830,8 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                     lookups[i] = (uint8_t)tl_lookups;
                 if (ct)
                     ct[i] = 0;
+                if (o->notify_out)
+                    o->notify_out[i] = 0;
                 continue;
             }
         }
@@ -824,6 +849,8 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             lookups[i] = (uint8_t)tl_lookups;
         if (ct)
             ct[i] = tl_ct;
+        if (o->notify_out)
+            o->notify_out[i] = notify_site(mode, ep_lxc, &r);
     }
 }
 
@@ -867,7 +894,7 @@ static res_t netdev_ingress_v6(cfo_t *o, const uint8_t *saddr,
 {
     int skip_proxy;
     uint32_t identity = identity_from_mark(mark, &skip_proxy);
-    res_t r = {TC_ACT_SHOT, 0, 0};
+    res_t r = {TC_ACT_SHOT, 0, 0, 0};
     int ret = exthdr_drop(proto);
     if (ret) { /* send_drop_notify_error(skb, ret, TC_ACT_SHOT, INGRESS) */
         r.verdict = ret;
@@ -901,7 +928,7 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
                            const uint8_t *daddr, uint8_t proto, uint16_t sport,
                            uint16_t dport, uint8_t flags, uint32_t len)
 {
-    res_t r = {TC_ACT_SHOT, 0, 0};
+    res_t r = {TC_ACT_SHOT, 0, 0, 0};
     if (icmp6_punt(proto, flags, sport, daddr)) { /* :411-419 */
         r.action = TC_ACT_OK;
         r.verdict = VERDICT_PUNT;
@@ -1011,6 +1038,8 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                     lookups[i] = (uint8_t)tl_lookups;
                 if (ct)
                     ct[i] = 0;
+                if (o->notify_out)
+                    o->notify_out[i] = 0;
                 continue;
             }
         }
@@ -1027,8 +1056,12 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             lookups[i] = (uint8_t)tl_lookups;
         if (ct)
             ct[i] = tl_ct;
+        if (o->notify_out)
+            o->notify_out[i] = notify_site(mode, ep_lxc, &r);
     }
 }
+
+void cfo_set_notify_out(cfo_t *o, uint32_t *words) { o->notify_out = words; }
 
 int cfo_policy_create(cfo_t *o, uint16_t lxc_id)
 {

@@ -76,6 +76,10 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
 
 /* rows of 7 u64: identity, dport, proto, egress, proxy_port, packets, bytes
  * (sorted); returns the number of rows (writes at most cap). */
+/* Drop-notify sites (res_t.nt in cfc_oracle.c) of the next classify calls,
+ * one u32 per header, written to `words` (NULL = off). */
+void cfo_set_notify_out(cfo_t *o, uint32_t *words);
+
 size_t cfo_policy_dump(cfo_t *o, uint16_t lxc_id, uint64_t *rows, size_t cap);
 /* rows of 4 u64: reason, dir, count, bytes (sorted, non-zero only) */
 size_t cfo_metrics_dump(cfo_t *o, uint64_t *rows, size_t cap);

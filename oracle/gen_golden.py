@@ -317,6 +317,11 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     verdict = np.zeros(n, np.int32)
     ident = np.zeros(n, np.uint32)
     idmask = np.zeros(n, np.uint32)
+    # skb->cb[0..4] after the run: for TC_ACT_SHOT these are the arguments
+    # send_drop_notify left for the drop-notify tail call (drop.h:98-102:
+    # exitcode, src << 16 | dst & 0xFFFF, reason, dst_id, ifindex); the tail
+    # call itself is not wired, so they stay visible in ctx_out
+    cbs = np.zeros((n, 5), np.int32)
     build = build_packet_v4 if h.family == 4 else build_packet_v6
     for i in range(n):
         if mode in (MODE_XDP, MODE_FULL):
@@ -334,11 +339,12 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
                 dp.ep_prog[ep_lxc], build(h, i, LXC_MAC, NODE_MAC))
             r = _derive_egress(h, i, ret, cb, po)
         action[i], verdict[i], ident[i], idmask[i] = r
-    return action, verdict, ident, idmask
+        cbs[i] = cb
+    return action, verdict, ident, idmask, cbs
 
 
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
-    action, verdict, ident, idmask = res
+    action, verdict, ident, idmask, cbs = res
     extra = {}
     if t.ct is not None:
         # CT before (loaded by the oracle / engine) and after the stream
@@ -350,7 +356,7 @@ def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
              h_sport=h.sport, h_dport=h.dport, h_proto=h.proto,
              h_flags=h.flags, h_length=h.length, h_mark=h.mark,
              x_action=action, x_verdict=verdict, x_identity=ident,
-             x_idmask=idmask, x_metrics=dp.metrics(), **extra)
+             x_idmask=idmask, x_cb=cbs, x_metrics=dp.metrics(), **extra)
     for lxc, pol in t.policy.items():
         d[f"policy_{lxc}"] = pol
     for lxc, c in dp.policy_counters().items():

@@ -17,6 +17,49 @@ CT_ROW = 104     # cfc_oracle.h CFO_CT_ROW
 
 _lib = None
 
+# cfc_drop_notify (include/cfc.h) = struct drop_notify (bpf/lib/drop.h:40-48)
+DROP_NOTIFY_DT = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"),
+                           ("hash", "<u4"), ("len_orig", "<u4"),
+                           ("len_cap", "<u4"), ("src_label", "<u4"),
+                           ("dst_label", "<u4"), ("dst_id", "<u4"),
+                           ("ifindex", "<u4")])
+assert DROP_NOTIFY_DT.itemsize == 32
+
+
+def _fmix32(h):
+    h = h.astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    h *= np.uint32(0x85EBCA6B)
+    h ^= h >> np.uint32(13)
+    h *= np.uint32(0xC2B2AE35)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+def flow_hash(hdr, idx):
+    """The engine's drop_notify.hash (cfc.h CFC_FLOW_HASH): a symmetric
+    5-tuple hash.  The reference's get_hash_recalc() value is the kernel's
+    flow-dissector hash under a boot-random key, which nothing can reproduce."""
+    with np.errstate(over="ignore"):
+        if hdr.family == 4:
+            a = np.asarray(hdr.saddr, np.uint32)[idx]
+            b = np.asarray(hdr.daddr, np.uint32)[idx]
+        else:
+            def fold(x):
+                w = np.ascontiguousarray(np.asarray(x, np.uint8)[idx]).view("<u4")
+                h = _fmix32(w[:, 3])
+                for k in (2, 1, 0):
+                    h = _fmix32(w[:, k] ^ h)
+                return h
+            a, b = fold(hdr.saddr), fold(hdr.daddr)
+        lo, hi = np.minimum(a, b), np.maximum(a, b)
+        sp = np.asarray(hdr.sport, np.uint32)[idx]
+        dp = np.asarray(hdr.dport, np.uint32)[idx]
+        pw = np.minimum(sp, dp) | (np.maximum(sp, dp) << np.uint32(16))
+        pr = np.asarray(hdr.proto, np.uint32)[idx]
+        return _fmix32(lo * np.uint32(0x9E3779B1) + hi * np.uint32(0x85EBCA77)
+                       + pw * np.uint32(0xC2B2AE3D) + pr)
+
 
 def build():
     subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
@@ -59,6 +102,7 @@ def lib():
         L.cfo_metrics_dump.restype = ctypes.c_size_t
         L.cfo_metrics_dump.argtypes = [vp, vp, ctypes.c_size_t]
         L.cfo_counters_reset.argtypes = [vp]
+        L.cfo_set_notify_out.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -77,6 +121,7 @@ class Oracle:
         self.L = lib()
         self.h = self.L.cfo_new()
         self.lxc_ids = []
+        self.tables = tables
         if tables is not None:
             self.load(tables)
 
@@ -125,10 +170,11 @@ class Oracle:
                 c(hdr.length, np.uint16), c(hdr.mark, np.uint32)]
 
     def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False,
-                 want_ct=False, apply_ct=False):
-        """-> (action, verdict, identity[, lookups][, ct]).  apply_ct folds
-        the batch's CT creates/deletes into the oracle's CT maps afterwards
-        (what the engine's cfc_ct_apply does)."""
+                 want_ct=False, apply_ct=False, want_notify=False):
+        """-> (action, verdict, identity[, lookups][, ct][, notify]).
+        apply_ct folds the batch's CT creates/deletes into the oracle's CT
+        maps afterwards (what the engine's cfc_ct_apply does); notify is the
+        drop-notify site word per header (res_t.nt in cfc_oracle.c)."""
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
@@ -144,8 +190,11 @@ class Oracle:
         if hdr.family == 6:
             assert arrs[0].shape == (n, 16) and arrs[1].shape == (n, 16)
         fn = self.L.cfo_classify_v4 if hdr.family == 4 else self.L.cfo_classify_v6
+        nt = np.zeros(n, np.uint32) if want_notify else None
+        self.L.cfo_set_notify_out(self.h, _p(nt))
         fn(self.h, mode, ep_lxc, n, *[_p(a) for a in arrs], _p(act), _p(ver),
            _p(ide), _p(lk), _p(ct), nthreads)
+        self.L.cfo_set_notify_out(self.h, None)
         if apply_ct:
             self.ct_apply(hdr, mode, ep_lxc, ide, ver, ct)
         out = (act, ver, ide)
@@ -153,7 +202,45 @@ class Oracle:
             out += (lk,)
         if want_ct:
             out += (ct,)
+        if want_notify:
+            out += (nt,)
         return out
+
+    def drop_notify(self, hdr, mode, ep_lxc, verdict, identity, sites):
+        """The struct drop_notify records (bpf/lib/drop.h:40-78) the
+        reference's perf ring would carry for this batch, in header order
+        -> (records DROP_NOTIFY_DT, header indices u64).  Uses the tables
+        this oracle was loaded with for SECLABEL and ifindex."""
+        t = self.tables
+        sec = np.zeros(65536, np.uint32)
+        for lxc, lab in t.seclabel.items():
+            sec[int(lxc)] = int(lab)
+        ifx = np.zeros(65536, np.uint32)
+        ifx[t.endpoints["lxc_id"].astype(np.int64)] = t.endpoints["ifindex"]
+        idx = np.flatnonzero(sites).astype(np.uint64)
+        w = sites[idx].astype(np.uint32)
+        site, src_lxc = w >> 16, (w & 0xFFFF).astype(np.int64)
+        ver = verdict[idx].astype(np.int64)
+        ident = identity[idx].astype(np.uint32)
+        ln = np.asarray(hdr.length, np.uint32)[idx]
+        r = np.zeros(len(idx), DROP_NOTIFY_DT)
+        r["type"] = 1                                   # CILIUM_NOTIFY_DROP
+        r["subtype"] = (-ver) & 0xFF                    # error = -reason
+        r["source"] = np.where(site == 1, 0, src_lxc)   # EVENT_SOURCE
+        r["hash"] = flow_hash(hdr, idx)
+        r["len_orig"] = ln
+        r["len_cap"] = np.minimum(ln, 128)              # TRACE_PAYLOAD_LEN
+        # cb[1] = src << 16 | dst & 0xFFFF: both labels keep 16 bits
+        own = sec[ep_lxc] if mode == MODE_EGRESS else 0
+        src = np.where(site == 2, own,
+                       np.where(site == 3, own if mode == MODE_EGRESS else ident, 0))
+        dst = np.where(site == 2, ident,
+                       np.where(site == 3, sec[src_lxc], 0))
+        r["src_label"] = np.asarray(src, np.uint32) & 0xFFFF
+        r["dst_label"] = np.asarray(dst, np.uint32) & 0xFFFF
+        r["dst_id"] = np.where(site == 3, src_lxc, 0)
+        r["ifindex"] = np.where(site == 3, ifx[src_lxc], 0)
+        return r, idx
 
     def ct_apply(self, hdr, mode, ep_lxc, identity, verdict, ct, hazard=False):
         arrs = self._arrays(hdr)

@@ -36,6 +36,8 @@ class Golden:
         self.identity = d["x_identity"]
         self.idmask = d["x_idmask"]
         self.metrics = d["x_metrics"]
+        # skb->cb[0..4] after the reference ran (None in older fixtures)
+        self.cb = d["x_cb"] if "x_cb" in d.files else None
         self.counters = {int(k.split("_")[2]): d[k] for k in d.files
                          if k.startswith("x_counters_")}
 
@@ -59,3 +61,20 @@ def ct_masked(rows):
     r[:, e + 42:e + 44] = 0
     r[:, e + 48:e + 56] = 0
     return r
+
+
+def expected_drop_notify(g: Golden):
+    """(header indices, fields) of the drop notifications the reference's
+    send_drop_notify armed (drop.h:98-102): cb[1] = src << 16 | dst & 0xFFFF,
+    cb[2] = reason, cb[3] = dst_id, cb[4] = ifindex.  XDP drops notify
+    nothing (bpf_xdp.c has no send_drop_notify)."""
+    tc = g.mode != 2
+    idx = np.flatnonzero((g.action == 2) & (g.verdict < 0) & (g.verdict != -1)
+                         if tc else np.zeros(len(g.action), bool))
+    cb = g.cb[idx].astype(np.int64)
+    f = dict(subtype=(-cb[:, 2]) & 0xFF,
+             src_label=(cb[:, 1] >> 16) & 0xFFFF,
+             dst_label=cb[:, 1] & 0xFFFF,
+             dst_id=cb[:, 3] & 0xFFFFFFFF,
+             ifindex=cb[:, 4] & 0xFFFFFFFF)
+    return idx.astype(np.uint64), f

@@ -6,6 +6,7 @@ import pytest
 
 import golden_io as G
 import oracle as O
+from cilium_amd import synth as S
 
 NAMES = G.names()
 
@@ -61,3 +62,40 @@ def test_ct_goldens_cover_every_ct_state():
         est_denied |= ((ct & 0x70) == 0x50) & (ver == -133)
         assert est_denied.any(), name
         assert (g.headers.flags & 2).any(), name
+
+
+NOTIFY_NAMES = [n for n in NAMES if G.Golden(n).cb is not None]
+
+
+def test_drop_notify_goldens_present():
+    assert len(NOTIFY_NAMES) >= 10, NOTIFY_NAMES
+
+
+@pytest.mark.parametrize("name", NOTIFY_NAMES)
+def test_oracle_drop_notify_matches_reference(name):
+    """Every drop-notify record of the restatement carries the arguments the
+    reference's send_drop_notify left in skb->cb[] for the same header."""
+    g = G.Golden(name)
+    o = O.Oracle(g.tables)
+    act, ver, ide, nt = o.classify(g.headers, g.mode, g.ep_lxc,
+                                   want_notify=True)
+    rec, idx = o.drop_notify(g.headers, g.mode, g.ep_lxc, ver, ide, nt)
+    want_idx, want = G.expected_drop_notify(g)
+    np.testing.assert_array_equal(idx, want_idx)
+    # LXC_ID is compiled into each endpoint program (lxc_config.h); the
+    # harness runs one bpf_lxc.o (LXC_ID 0x1010) behind every endpoint, so
+    # its dst_id is 0x1010 where the engine (one program per endpoint, as
+    # the agent compiles them) reports the destination's own id
+    other = (rec["dst_id"] != 0) & (rec["dst_id"] != S.EP_LXC_ID)
+    assert (want["dst_id"][other] == S.EP_LXC_ID).all()
+    want["dst_id"] = np.where(other, rec["dst_id"], want["dst_id"])
+    for k, v in want.items():
+        np.testing.assert_array_equal(rec[k].astype(np.int64), v, err_msg=k)
+    assert (rec["type"] == 1).all()
+    np.testing.assert_array_equal(rec["len_cap"],
+                                  np.minimum(rec["len_orig"], 128))
+    if g.mode == O.MODE_EGRESS:
+        assert ((rec["source"] == g.ep_lxc) | (rec["source"] == rec["dst_id"])).all()
+    if len(rec) and g.mode != O.MODE_XDP:
+        # records from both an endpoint program and (where present) netdev
+        assert (rec["source"] != 0).any(), name
