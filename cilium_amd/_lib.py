@@ -20,6 +20,7 @@ LPM4_AUTO, LPM4_DIR24_8, LPM4_TRIE = 0, 1, 2
 # every symbol include/cfc.h declares
 EXPORTS = (
     "cfc_open", "cfc_close", "cfc_abi_version", "cfc_map_open",
+    "cfc_drop_notify_v4", "cfc_drop_notify_v6",
     "cfc_map_close", "cfc_map_update", "cfc_map_lookup", "cfc_map_delete",
     "cfc_map_get_next_key", "cfc_num_possible_cpus", "cfc_endpoint_config",
     "cfc_commit", "cfc_classify_v4", "cfc_counters_device",
@@ -50,7 +51,8 @@ class HdrV6(ctypes.Structure):
 
 class Out(ctypes.Structure):
     _fields_ = [("verdict", ctypes.c_void_p), ("identity", ctypes.c_void_p),
-                ("action", ctypes.c_void_p), ("ct", ctypes.c_void_p)]
+                ("action", ctypes.c_void_p), ("ct", ctypes.c_void_p),
+                ("notify", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -112,6 +114,9 @@ def lib():
                                   i32, ctypes.c_uint16, vp]
     L.cfc_ct_apply_v6.argtypes = [vp, ctypes.POINTER(HdrV6), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
+    for f in (L.cfc_drop_notify_v4, L.cfc_drop_notify_v6):
+        f.argtypes = [vp, vp, ctypes.POINTER(Out), i32, ctypes.c_uint16, vp, vp,
+                      u64, vp, vp]
     L.cfc_counters_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]
     L.cfc_counters_sync.argtypes = [vp, vp]
     L.cfc_counters_clear.argtypes = [vp, vp]

@@ -77,6 +77,9 @@ struct Epoch {
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
     cfc_stats st{};
+    // drop notifications: {SECLABEL, ifindex} by LXC_ID, built on first use
+    std::vector<uint2> ep_info_host;
+    DevBuf ep_info;
 };
 
 }  // namespace
@@ -105,6 +108,8 @@ struct cfc_ctx {
     uint32_t *ws = nullptr;
     size_t ws_bytes = 0;
     Map *metrics = nullptr;
+
+    DevBuf nt_ws;   // drop-notify block counts / offsets
 
     // CFC_OPT_TIMING: events of the launches since the last collect
     bool timing = false;
@@ -768,6 +773,99 @@ int cfc_classify_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream)
 {
     return classify(c, in, out, mode, ep_lxc, stream, launch_classify_v6);
+}
+
+}  // extern "C"
+
+namespace {
+
+// cfc_drop_notify_v4 / _v6
+template <class Hdr>
+int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
+                uint16_t ep_lxc, cfc_drop_notify *rec, uint64_t *hdr_index,
+                uint64_t cap, uint64_t *count, void *stream, int family)
+{
+    if (!c || !in || !out || !count || (cap && !rec))
+        return -EINVAL;
+    if (in->n && (!out->notify || !out->verdict || !out->identity ||
+                  !in->saddr || !in->daddr || !in->ports || !in->meta))
+        return -EINVAL;
+    if (mode < CFC_MODE_INGRESS || mode > CFC_MODE_FULL)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (!c->epoch)
+        return -ENOENT;   // nothing classified yet
+    Epoch &E = *c->epoch;
+    if (!E.ep_info.p) {
+        E.ep_info_host.assign(65536, make_uint2(0, 0));
+        for (uint32_t id = 0; id < 65536; id++)
+            E.ep_info_host[id].x = c->seclabel[id];
+        for (auto &kv : c->maps) {
+            if (kv.second->role != ROLE_LXC)
+                continue;
+            for (auto &e : kv.second->kv) {   // struct endpoint_info
+                uint32_t ifx;
+                uint16_t id;
+                memcpy(&ifx, e.second.val.data(), 4);
+                memcpy(&id, e.second.val.data() + 6, 2);
+                E.ep_info_host[id].y = ifx;
+            }
+        }
+        int rc = upload_vec(E.ep_info, E.ep_info_host, s);
+        if (rc)
+            return rc;
+    }
+    const size_t need = drop_notify_workspace_bytes(in->n);
+    if (need > c->nt_ws.bytes) {
+        (void)hipDeviceSynchronize();
+        int rc = c->nt_ws.zeros(need, s);
+        if (rc)
+            return rc;
+    }
+    NotifyArgs a{};
+    a.notify = out->notify;
+    a.verdict = out->verdict;
+    a.identity = out->identity;
+    a.meta = in->meta;
+    a.ports = in->ports;
+    a.saddr = reinterpret_cast<const uint32_t *>(in->saddr);
+    a.daddr = reinterpret_cast<const uint32_t *>(in->daddr);
+    a.n = in->n;
+    a.family = family;
+    a.mode = mode;
+    a.own_seclabel = c->seclabel[ep_lxc];
+    a.ep_info = reinterpret_cast<const uint2 *>(E.ep_info.p);
+    a.rec = rec;
+    a.hdr_index = hdr_index;
+    a.cap = cap;
+    a.count = count;
+    return launch_drop_notify(a, reinterpret_cast<uint64_t *>(c->nt_ws.p), s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfc_drop_notify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
+                       int mode, uint16_t ep_lxc, cfc_drop_notify *rec,
+                       uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                       void *stream)
+{
+    return drop_notify(c, in, out, mode, ep_lxc, rec, hdr_index, cap, count,
+                       stream, 4);
+}
+
+int cfc_drop_notify_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
+                       int mode, uint16_t ep_lxc, cfc_drop_notify *rec,
+                       uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                       void *stream)
+{
+    return drop_notify(c, in, out, mode, ep_lxc, rec, hdr_index, cap, count,
+                       stream, 6);
 }
 
 int cfc_counters_device(cfc_ctx *c, uint64_t **dev, uint64_t *n)

@@ -490,6 +490,12 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                     out.action[o] = (uint8_t)h[u].act;
                 if (CT && out.ct)
                     out.ct[o] = (uint8_t)h[u].ct_byte;
+                if (out.notify)
+                    st_nt(notify_word(MODE, h[u].ver,
+                                      MODE == CFC_MODE_EGRESS &&
+                                          h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
+                                      h[u].rec.w & 0xFFFF, E.lxc_id),
+                          out.notify + o);
                 if (CT) {
                     st_nt(h[u].ct_k1, ct_idx + o);
                     if (MODE == CFC_MODE_EGRESS)

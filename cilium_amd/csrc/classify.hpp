@@ -65,4 +65,28 @@ int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
                        int num_cus, hipStream_t stream,
                        const LaunchTiming *timing = nullptr);
 
+// Drop-notify records of one classified batch (notify.hip): the per-header
+// cfc_out.notify words compacted in header order into cfc_drop_notify.
+struct NotifyArgs {
+    const uint32_t *notify;
+    const int32_t *verdict;
+    const uint32_t *identity;
+    const uint32_t *meta;
+    const uint32_t *ports;
+    const uint32_t *saddr;   // v4: n words; v6: n x 4 words
+    const uint32_t *daddr;
+    uint64_t n;
+    int family;              // 4 or 6
+    int mode;
+    uint32_t own_seclabel;   // SECLABEL of ep_lxc (egress batches)
+    const uint2 *ep_info;    // [65536] {SECLABEL, ifindex} by LXC_ID
+    cfc_drop_notify *rec;
+    uint64_t *hdr_index;     // may be NULL
+    uint64_t cap;
+    uint64_t *count;
+};
+// workspace: one u64 per block of headers (counts, then offsets)
+size_t drop_notify_workspace_bytes(uint64_t n);
+int launch_drop_notify(const NotifyArgs &a, uint64_t *ws, hipStream_t stream);
+
 }  // namespace cfc

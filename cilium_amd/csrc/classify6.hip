@@ -409,6 +409,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             out.action[i] = (uint8_t)act;
         if (CT && out.ct)
             out.ct[i] = (uint8_t)ctb;
+        if (out.notify)
+            st_nt(notify_word(MODE, ver,
+                              EGR && met1 == mkey6<MODE>(DROP_POLICY, METRIC_INGRESS),
+                              drec.z & 0xFFFF, E.lxc_id),
+                  out.notify + i);
         if (CT) {
             st_nt(ck1, ct_idx + i);
             if (EGR)

@@ -19,6 +19,25 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 // k_count: the packed u32 byte sums stay exact (64512 headers x 65535
 // bytes < 2^32, so they never carry into the packet count)
 constexpr uint64_t COUNT_PER_BLOCK = 63 * BLOCK;
+
+// cfc_out.notify word of a header (cfc.h CFC_NT_*): which send_drop_notify
+// the reference ran.  dest_stage: an egress batch's drop came from the
+// destination endpoint's policy program after local delivery.
+__device__ __forceinline__ uint32_t notify_word(int mode, int ver,
+                                                bool dest_stage,
+                                                uint32_t dest_lxc,
+                                                uint32_t ep_lxc)
+{
+    if (ver >= 0 || ver == CFC_DROP_PREFILTER || ver == CFC_VERDICT_PUNT)
+        return 0;
+    if (mode == CFC_MODE_EGRESS)
+        return dest_stage ? (CFC_NT_POLICY << 16 | dest_lxc)
+                          : (CFC_NT_EGRESS << 16 | ep_lxc);
+    // bpf_netdev's own errors: the failed tail call of local delivery
+    // (l3.h:130) and ipv6_hdrlen's DROP_INVALID_EXTHDR / DROP_FRAG_NOSUPPORT
+    const bool netdev = ver == DROP_MISSED_TAIL_CALL || ver == -156 || ver == -157;
+    return netdev ? CFC_NT_NETDEV << 16 : (CFC_NT_POLICY << 16 | dest_lxc);
+}
 // workspace: entry indices [n] (egress: a second array at ctr_stride(n)),
 // then the partial slabs; both arrays 16-byte aligned for k_count
 __host__ __device__ constexpr uint64_t ctr_stride(uint64_t n) { return (n + 3) & ~3ull; }

@@ -47,6 +47,7 @@ class Verdicts:
     identity: "torch.Tensor"  # int32 (u32 bits)
     action: "torch.Tensor | None"  # uint8
     ct: "torch.Tensor | None" = None  # uint8 CT byte (cfc.h CFC_CT_*)
+    notify: "torch.Tensor | None" = None  # int32 drop-notify site (CFC_NT_*)
 
 
 def pack_v4(h, device="cuda"):
@@ -208,7 +209,7 @@ class Datapath:
 
     def classify_v4(self, batch: HeaderBatchV4, mode=L.MODE_INGRESS, ep_lxc=0,
                     out: Verdicts | None = None, want_action=True,
-                    want_ct=False, stream=None) -> Verdicts:
+                    want_ct=False, want_notify=False, stream=None) -> Verdicts:
         import torch
         n = len(batch)
         dev = batch.saddr.device
@@ -218,7 +219,9 @@ class Datapath:
                            torch.empty(n, dtype=torch.uint8, device=dev)
                            if want_action else None,
                            torch.empty(n, dtype=torch.uint8, device=dev)
-                           if want_ct else None)
+                           if want_ct else None,
+                           torch.empty(n, dtype=torch.int32, device=dev)
+                           if want_notify else None)
         for t in (batch.saddr, batch.daddr, batch.ports, batch.meta):
             assert t.is_cuda and t.is_contiguous() and t.numel() == n
             assert t.dtype == torch.int32
@@ -227,7 +230,7 @@ class Datapath:
         hdr = L.HdrV4(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
                       _ptr(batch.meta), _ptr(batch.mark), n)
         o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct))
+                  _ptr(out.ct), _ptr(out.notify))
         L.check(self.L.cfc_classify_v4(self.h, ctypes.byref(hdr),
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)),"classify")
@@ -235,7 +238,7 @@ class Datapath:
 
     def classify_v6(self, batch: HeaderBatchV6, mode=L.MODE_INGRESS, ep_lxc=0,
                     out: Verdicts | None = None, want_action=True,
-                    want_ct=False, stream=None) -> Verdicts:
+                    want_ct=False, want_notify=False, stream=None) -> Verdicts:
         import torch
         n = len(batch)
         dev = batch.ports.device
@@ -245,7 +248,9 @@ class Datapath:
                            torch.empty(n, dtype=torch.uint8, device=dev)
                            if want_action else None,
                            torch.empty(n, dtype=torch.uint8, device=dev)
-                           if want_ct else None)
+                           if want_ct else None,
+                           torch.empty(n, dtype=torch.int32, device=dev)
+                           if want_notify else None)
         for t in (batch.saddr, batch.daddr):
             assert t.is_cuda and t.is_contiguous() and t.dtype == torch.int32
             assert t.shape == (n, 4) and t.data_ptr() % 16 == 0
@@ -257,7 +262,7 @@ class Datapath:
         hdr = L.HdrV6(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
                       _ptr(batch.meta), _ptr(batch.mark), n)
         o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct))
+                  _ptr(out.ct), _ptr(out.notify))
         L.check(self.L.cfc_classify_v6(self.h, ctypes.byref(hdr),
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)), "classify v6")
@@ -280,10 +285,39 @@ class Datapath:
             _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
             _ptr(batch.meta), _ptr(batch.mark), len(batch))
         o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct))
+                  _ptr(out.ct), _ptr(out.notify))
         fn = self.L.cfc_ct_apply_v6 if v6 else self.L.cfc_ct_apply_v4
         L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
                    self._stream(stream)), "ct apply")
+
+    def drop_notify(self, batch, out: Verdicts, mode=L.MODE_INGRESS,
+                    ep_lxc=0, cap=None, stream=None):
+        """cfc_drop_notify_v4/v6: the batch's struct drop_notify records in
+        header order -> (records as an (m, 8) int32 tensor in the
+        cfc_drop_notify layout, header indices int64, total drops).
+        Synchronises the stream to read the total."""
+        import torch
+        assert out.notify is not None, "classify with want_notify=True"
+        n = len(batch)
+        cap = n if cap is None else cap
+        dev = out.verdict.device
+        rec = torch.zeros((max(cap, 1), 8), dtype=torch.int32, device=dev)
+        idx = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        v6 = isinstance(batch, HeaderBatchV6)
+        hdr = (L.HdrV6 if v6 else L.HdrV4)(
+            _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+            _ptr(batch.meta), _ptr(batch.mark), n)
+        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
+                  _ptr(out.ct), _ptr(out.notify))
+        fn = self.L.cfc_drop_notify_v6 if v6 else self.L.cfc_drop_notify_v4
+        L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
+                   _ptr(rec), _ptr(idx), cap, _ptr(cnt), self._stream(stream)),
+                "drop notify")
+        torch.cuda.synchronize(dev)
+        total = int(cnt.item())
+        m = min(total, cap)
+        return rec[:m], idx[:m], total
 
     def counters_sync(self, stream=None):
         L.check(self.L.cfc_counters_sync(self.h, self._stream(stream)),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 4
+#define CFC_ABI_VERSION 5
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -194,11 +194,26 @@ typedef struct {
 #define CFC_CT_RES_MASK 0x3u
 #define CFC_CT_DONE 0x4u
 #define CFC_CT_CREATE 0x8u
+/*  notify  : (may be NULL) which send_drop_notify (bpf/lib/drop.h:94-109) the
+ *            reference ran for the header: 0 none (forwarded, redirected,
+ *            XDP prefilter drop — bpf_xdp.c notifies nothing — or punt), else
+ *            site << 16 | EVENT_SOURCE (the LXC_ID of the program that
+ *            dropped).  Sites: CFC_NT_NETDEV bpf_netdev's
+ *            send_drop_notify_error (bpf_netdev.c:463,502; no identities),
+ *            CFC_NT_EGRESS the sending endpoint's (SECLABEL, dstID, 0, 0)
+ *            (bpf_lxc.c:432,700), CFC_NT_POLICY the destination endpoint's
+ *            tail_ipv{4,6}_policy (src_label, SECLABEL, LXC_ID, ifindex)
+ *            (bpf_lxc.c:891,1024).  cfc_drop_notify_v4/v6 turn it into
+ *            records. */
+#define CFC_NT_NETDEV 1u
+#define CFC_NT_EGRESS 2u
+#define CFC_NT_POLICY 3u
 typedef struct {
     int32_t *verdict;
     uint32_t *identity;
     uint8_t *action;
     uint8_t *ct;
+    uint32_t *notify;
 } cfc_out;
 
 /* Classify a batch (asynchronous on `stream`).  Policy-entry and metrics
@@ -235,6 +250,45 @@ int cfc_ct_apply_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
 int cfc_ct_apply_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
+
+/* ------------------------------------------------------ drop notifications */
+/* struct drop_notify (bpf/lib/drop.h:40-48, NOTIFY_COMMON_HDR common.h:217)
+ * as __send_drop_notify (drop.h:50-78) fills it for the perf ring
+ * cilium_events, which pkg/monitor (datapath_drop.go DropNotify) decodes.
+ * The captured payload that follows it on the ring (len_cap bytes of the
+ * packet) is not part of a header batch; hdr_index locates the header. */
+#define CFC_NOTIFY_DROP 1          /* CILIUM_NOTIFY_DROP (common.h:211) */
+#define CFC_TRACE_PAYLOAD_LEN 128  /* TRACE_PAYLOAD_LEN (common.h:224) */
+typedef struct {
+    uint8_t type;        /* CFC_NOTIFY_DROP */
+    uint8_t subtype;     /* -reason (DROP_* magnitude) */
+    uint16_t source;     /* EVENT_SOURCE: LXC_ID of the endpoint program, 0
+                            for bpf_netdev */
+    uint32_t hash;       /* symmetric 5-tuple flow hash: the reference's
+                            get_hash_recalc() is the kernel's skb hash under
+                            a boot-random key */
+    uint32_t len_orig;   /* skb->len */
+    uint32_t len_cap;    /* min(CFC_TRACE_PAYLOAD_LEN, len_orig) */
+    uint32_t src_label;  /* cb[1] >> 16: 16 bits of the source identity */
+    uint32_t dst_label;  /* cb[1] & 0xFFFF */
+    uint32_t dst_id;     /* cb[3] */
+    uint32_t ifindex;    /* cb[4] */
+} cfc_drop_notify;
+
+/* The drop notifications of one classified batch (in: the headers, out: its
+ * outputs with out->notify set), in header order, into device memory:
+ * records[0 .. min(total, cap)) and, if hdr_index != NULL, the header index
+ * of each.  *count (device u64) receives the total; drops past cap are not
+ * recorded (a full perf ring loses samples the same way).  mode and ep_lxc
+ * as given to the classify call.  Asynchronous on `stream`. */
+int cfc_drop_notify_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
+                       int mode, uint16_t ep_lxc, cfc_drop_notify *records,
+                       uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                       void *stream);
+int cfc_drop_notify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
+                       int mode, uint16_t ep_lxc, cfc_drop_notify *records,
+                       uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                       void *stream);
 
 /* ---------------------------------------------------------------- counters */
 /* The device counter block is a flat u64 array: 2 u64 (packets, bytes) per
