@@ -429,7 +429,7 @@ __host__ LdsPlan lds_plan(const DevTables &T)
     return p;
 }
 
-template <int MODE, int U, bool CT>
+template <int MODE, int U, bool CT, bool NT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
     uint32_t *ctr_idx, uint32_t *ct_idx, uint64_t *g_met, uint64_t per_block)
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                     out.action[o] = (uint8_t)h[u].act;
                 if (CT && out.ct)
                     out.ct[o] = (uint8_t)h[u].ct_byte;
-                if (out.notify)
+                if (NT)   // the drop-notify site word (cfc_out.notify)
                     st_nt(notify_word(MODE, h[u].ver,
                                       MODE == CFC_MODE_EGRESS &&
                                           h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
@@ -686,13 +686,13 @@ __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
         dst[i] += src[i];
 }
 
-template <int MODE, bool CT>
-void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
-                 const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
-                 uint32_t grid, uint64_t per_block, hipStream_t s)
+template <int MODE, bool CT, bool NT>
+void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
+                    const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
+                    uint32_t grid, uint64_t per_block, hipStream_t s)
 {
     const LdsPlan L = lds_plan(T);
-    auto kern = k_classify_v4<MODE, CFC_UNROLL, CT>;
+    auto kern = k_classify_v4<MODE, CFC_UNROLL, CT, NT>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
@@ -703,6 +703,18 @@ void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
                        out, E, ctr_idx, ct_idx_ptr(ctr_idx, in.n, T.n_ctr, MODE),
                        g_met, per_block);
+}
+
+// the notify store is compiled in only when the caller asked for it
+template <int MODE, bool CT>
+void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
+                 const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
+                 uint32_t grid, uint64_t per_block, hipStream_t s)
+{
+    if (out.notify)
+        launch_mode_nt<MODE, CT, true>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
+    else
+        launch_mode_nt<MODE, CT, false>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
 }
 
 uint64_t partial_off(uint64_t n, int mode)

@@ -182,7 +182,7 @@ __host__ LdsPlan6 lds_plan6(const DevTables &T)
     return p;
 }
 
-template <int MODE, bool CT>
+template <int MODE, bool CT, bool NT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     DevTables T, LdsPlan6 L, cfc_hdr_v6 in, cfc_out out, EgressArgs E,
     uint32_t *ctr_idx, uint32_t *ct_idx, uint64_t *g_met, uint64_t per_block)
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             out.action[i] = (uint8_t)act;
         if (CT && out.ct)
             out.ct[i] = (uint8_t)ctb;
-        if (out.notify)
+        if (NT)   // the drop-notify site word (cfc_out.notify)
             st_nt(notify_word(MODE, ver,
                               EGR && met1 == mkey6<MODE>(DROP_POLICY, METRIC_INGRESS),
                               drec.z & 0xFFFF, E.lxc_id),
@@ -442,13 +442,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     }
 }
 
-template <int MODE, bool CT>
-void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
-                  const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
-                  uint32_t grid, uint64_t per_block, hipStream_t s)
+template <int MODE, bool CT, bool NT>
+void launch_mode6_nt(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
+                     const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
+                     uint32_t grid, uint64_t per_block, hipStream_t s)
 {
     const LdsPlan6 L = lds_plan6(T);
-    auto kern = k_classify_v6<MODE, CT>;
+    auto kern = k_classify_v6<MODE, CT, NT>;
     static bool attr_set = false;
     if (!attr_set) {
         (void)hipFuncSetAttribute((const void *)kern,
@@ -459,6 +459,17 @@ void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
                        out, E, ctr_idx, ct_idx_ptr(ctr_idx, in.n, T.n_ctr, MODE),
                        g_met, per_block);
+}
+
+template <int MODE, bool CT>
+void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
+                  const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
+                  uint32_t grid, uint64_t per_block, hipStream_t s)
+{
+    if (out.notify)
+        launch_mode6_nt<MODE, CT, true>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
+    else
+        launch_mode6_nt<MODE, CT, false>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
 }
 
 }  // namespace
