@@ -254,7 +254,8 @@ int cfc_ct_apply_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
 /* ------------------------------------------------------ drop notifications */
 /* struct drop_notify (bpf/lib/drop.h:40-48, NOTIFY_COMMON_HDR common.h:217)
  * as __send_drop_notify (drop.h:50-78) fills it for the perf ring
- * cilium_events, which pkg/monitor (datapath_drop.go DropNotify) decodes.
+ * cilium_events, which pkg/monitor decodes (datapath_drop.go:28-40
+ * DropNotify: the same fields, little-endian, 32 bytes).
  * The captured payload that follows it on the ring (len_cap bytes of the
  * packet) is not part of a header batch; hdr_index locates the header. */
 #define CFC_NOTIFY_DROP 1          /* CILIUM_NOTIFY_DROP (common.h:211) */

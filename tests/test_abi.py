@@ -221,3 +221,29 @@ def test_ct_maps_host_only():
     assert e.value.errno == errno.EINVAL
     fd, new = dp.open_or_create_map("cilium_ct_any6_77", 9, 38, 56, 1024)
     assert new
+
+
+def test_drop_notify_abi_on_host_only_context():
+    """cfc_drop_notify_v4/v6 validate their arguments and need a device; the
+    record layout is pkg/monitor's DropNotify (datapath_drop.go:28-40)."""
+    import ctypes
+    import numpy as np
+    import oracle as O
+    dp = C.host_only()
+    L = dp.L
+    hdr = _lib.HdrV4(None, None, None, None, None, 0)
+    cnt = ctypes.c_uint64(0)
+    out = _lib.Out()
+    for fn in (L.cfc_drop_notify_v4, L.cfc_drop_notify_v6):
+        assert fn(dp.h, ctypes.byref(hdr), ctypes.byref(out), 0, 0, None, None,
+                  0, ctypes.byref(cnt), None) == -errno.ENODEV
+        assert fn(dp.h, ctypes.byref(hdr), ctypes.byref(out), 0, 0, None, None,
+                  0, None, None) == -errno.EINVAL
+        assert fn(dp.h, ctypes.byref(hdr), ctypes.byref(out), 9, 0, None, None,
+                  0, ctypes.byref(cnt), None) == -errno.EINVAL
+    # Out carries five device pointers (cfc_out, ABI 5)
+    assert ctypes.sizeof(_lib.Out) == 40
+    dt = O.DROP_NOTIFY_DT
+    assert dt.itemsize == 32
+    assert [dt.fields[k][1] for k in dt.names] == [0, 1, 2, 4, 8, 12, 16, 20, 24, 28]
+    assert np.zeros(1, dt).view(np.uint8).size == 32
