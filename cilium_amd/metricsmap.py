@@ -39,3 +39,27 @@ def dump(dp: Datapath, fd=None):
 def dump_rows(dp: Datapath):
     """sorted rows (reason, dir, count, bytes) like the golden fixtures."""
     return sorted((r, d, c, b) for (r, d), (c, b) in dump(dp).items())
+
+
+_DIRECTION = {0: "UNKNOWN", 1: "INGRESS", 2: "EGRESS"}   # metricsmap.go:60-64
+
+
+def direction(d: int) -> str:
+    """Key.Direction (metricsmap.go:82-90)."""
+    return _DIRECTION[d] if d in (DirIngress, DirEgress) else _DIRECTION[0]
+
+
+def prometheus_counters(dp: Datapath, fd=None):
+    """What SyncMetricsMap feeds Prometheus (metricsmap.go:142-206):
+    {("drop", reason text, direction): count} for Key.IsDrop() entries
+    (metrics.DropCount) and {("forward", direction): count} for forwards
+    (metrics.ForwardCount); entries mapping to the same labels add up."""
+    from .monitor import drop_reason
+    out = {}
+    for (reason, d), (count, _bytes) in dump(dp, fd).items():
+        if reason:
+            lab = ("drop", drop_reason(reason), direction(d))
+        else:
+            lab = ("forward", direction(d))
+        out[lab] = out.get(lab, 0) + count
+    return out
