@@ -110,6 +110,9 @@ struct cfc_ctx {
     Map *metrics = nullptr;
 
     DevBuf nt_ws;   // drop-notify block counts / offsets
+    hipEvent_t nt_done = nullptr;   // after the last drop-notify launch
+    hipStream_t nt_stream = nullptr;
+    bool nt_pending = false;
 
     // CFC_OPT_TIMING: events of the launches since the last collect
     bool timing = false;
@@ -469,6 +472,7 @@ int cfc_open(int device, cfc_ctx **out)
             p.multiProcessorCount > 0)
             c->num_cus = p.multiProcessorCount;
         (void)hipEventCreateWithFlags(&c->last_done, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&c->nt_done, hipEventDisableTiming);
     }
     // the datapath owns cilium_metrics (bpf/lib/maps.h:35-41)
     auto m = std::make_unique<Map>();
@@ -500,6 +504,8 @@ void cfc_close(cfc_ctx *c)
         (void)hipFree(c->ws);
     if (c->last_done)
         (void)hipEventDestroy(c->last_done);
+    if (c->nt_done)
+        (void)hipEventDestroy(c->nt_done);
     delete c;
 }
 
@@ -800,6 +806,10 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     if (!c->epoch)
         return -ENOENT;   // nothing classified yet
     Epoch &E = *c->epoch;
+    // the workspace and the endpoint table are shared: order this call
+    // after the previous one when it ran on another stream
+    if (c->nt_pending && c->nt_stream != s)
+        (void)hipStreamWaitEvent(s, c->nt_done, 0);
     if (!E.ep_info.p) {
         E.ep_info_host.assign(65536, make_uint2(0, 0));
         for (uint32_t id = 0; id < 65536; id++)
@@ -843,7 +853,13 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     a.hdr_index = hdr_index;
     a.cap = cap;
     a.count = count;
-    return launch_drop_notify(a, reinterpret_cast<uint64_t *>(c->nt_ws.p), s);
+    int rc = launch_drop_notify(a, reinterpret_cast<uint64_t *>(c->nt_ws.p), s);
+    if (rc)
+        return rc;
+    (void)hipEventRecord(c->nt_done, s);
+    c->nt_stream = s;
+    c->nt_pending = true;
+    return 0;
 }
 
 }  // namespace

@@ -132,3 +132,32 @@ def test_cap_and_empty(torch):
     h0 = e.headers
     (a, words, grec, gidx, total), = gpu_notify(torch, e.tables, h0, e.mode)
     assert total == int((oracle_notify(e.tables, h0, e.mode)[0] != 0).sum())
+
+
+def test_two_streams(torch):
+    """Back-to-back calls on two streams share the notify workspace: each
+    waits for the other's kernels, so both batches' records are right."""
+    g1, g2 = G.Golden("c2_ingress_v4"), G.Golden("small_ingress_v4")
+    res = []
+    for g in (g1, g2):
+        dp = Datapath(0)
+        load_tables(dp, g.tables)
+        b = pack(g.headers)
+        out = dp.classify(b, g.mode, g.ep_lxc, want_notify=True)
+        torch.cuda.synchronize()
+        res.append((dp, b, out, g))
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    dp, b, out, g = res[0]
+    # same context twice: a large batch on s1, then a small one on s2
+    big = dp.drop_notify(b, out, g.mode, g.ep_lxc, stream=s1)
+    small_b = type(b)(b.saddr[:5000], b.daddr[:5000], b.ports[:5000],
+                      b.meta[:5000], b.mark[:5000] if b.mark is not None else None)
+    small_out = dp.classify(small_b, g.mode, g.ep_lxc, want_notify=True, stream=s2)
+    small = dp.drop_notify(small_b, small_out, g.mode, g.ep_lxc, stream=s2)
+    torch.cuda.synchronize()
+    nt, rec, idx = oracle_notify(g.tables, g.headers, g.mode)
+    assert big[2] == len(rec)
+    np.testing.assert_array_equal(big[1].cpu().numpy().astype(np.uint64), idx)
+    assert small[2] == int((nt[:5000] != 0).sum())
+    for r in res:
+        r[0].close()
