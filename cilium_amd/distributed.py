@@ -1,7 +1,8 @@
 """Multi-GPU: one process per GPU, the header stream sharded contiguously,
 tables replicated (every rank loads the same maps), and one SUM all-reduce
 of the u64 counter block over RCCL (xGMI) per reporting interval — the only
-collective on this path.  Verdicts need no exchange: each
+collective on the verdict path; drop records, when a monitor
+listens, are gathered to one rank per interval (gather_drop_notify).  Verdicts need no exchange: each
 header's verdict is a pure function of the header and the tables."""
 from __future__ import annotations
 
@@ -42,3 +43,36 @@ def allreduce_counters(dp, group=None, stream=None):
     dp.counters_import(t, stream)
     dp.counters_sync(stream)
     return t
+
+
+def gather_drop_notify(rec, idx, start, dst=0, group=None):
+    """Collect every rank's drop-notify records (cfc_drop_notify_v4/v6: an
+    (m, 8) int32 tensor) on rank `dst`, the one feeding pkg/monitor, in
+    stream order: shards are contiguous and each rank's records are in header
+    order, so rank order is stream order; `start` (the shard's first header)
+    turns the per-shard header indices into stream indices.  Two collectives
+    per reporting interval (counts, then the padded records), off the
+    per-batch path like the counter all-reduce.  -> (records, stream
+    indices) on dst, (None, None) elsewhere."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or \
+            dist.get_world_size(group) == 1:
+        return rec, idx + start
+    world = dist.get_world_size(group)
+    m = torch.tensor([rec.shape[0]], dtype=torch.int64, device=rec.device)
+    counts = [torch.zeros_like(m) for _ in range(world)]
+    dist.all_gather(counts, m, group=group)
+    cmax = max(int(c.item()) for c in counts)
+    # records and stream indices in one int64 row each: 4 record words + index
+    row = torch.zeros((max(cmax, 1), 5), dtype=torch.int64, device=rec.device)
+    if rec.shape[0]:
+        row[:rec.shape[0], :4] = rec.contiguous().view(torch.int64).view(-1, 4)
+        row[:rec.shape[0], 4] = idx.to(torch.int64) + start
+    rows = [torch.zeros_like(row) for _ in range(world)]
+    dist.all_gather(rows, row, group=group)
+    if dist.get_rank(group) != dst:
+        return None, None
+    full = torch.cat([r[:int(c.item())] for r, c in zip(rows, counts)])
+    recs = full[:, :4].contiguous().view(torch.int32).view(-1, 8)
+    return recs, full[:, 4].clone()

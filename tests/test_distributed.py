@@ -12,7 +12,7 @@ import pytest
 import torch.multiprocessing as mp
 
 from cilium_amd import synth as S
-from cilium_amd.distributed import allreduce_block, shard_range
+from cilium_amd.distributed import allreduce_block, gather_drop_notify, shard_range
 
 
 def _free_port():
@@ -46,7 +46,13 @@ def _worker(rank, world, port, q):
         h = S.headers_c2(t, 40_000, seed=11)
         a, b = shard_range(len(h), rank, world)
         o = O.Oracle(t)
-        _, ver, ide = o.classify(h.slice(a, b), 0, 0)
+        part = h.slice(a, b)
+        _, ver, ide, nt = o.classify(part, 0, 0, want_notify=True)
+        rec, idx = o.drop_notify(part, 0, 0, ver, ide, nt)
+        grec, gidx = gather_drop_notify(
+            torch.from_numpy(rec.view(np.int32).reshape(-1, 8).copy()),
+            torch.from_numpy(idx.astype(np.int64)), a)
+        gathered = None if grec is None else (grec.numpy().copy(), gidx.numpy().copy())
         lxc = sorted(t.policy)[0]
         pc = o.policy_counters(lxc)             # rows: ..., packets, bytes
         blk = np.concatenate([pc[:, 5], pc[:, 6]]).astype(np.uint64)
@@ -56,7 +62,8 @@ def _worker(rank, world, port, q):
         # wrap-around stays exact: add 2^64-1 on rank 0, +1 on rank 1
         w = torch.tensor([-1 if rank == 0 else 1], dtype=torch.int64)
         allreduce_block(w)
-        q.put((rank, ver, ide, tb.numpy().view(np.uint64), int(w.item())))
+        q.put((rank, ver, ide, tb.numpy().view(np.uint64), int(w.item()),
+               gathered))
     finally:
         dist.destroy_process_group()
 
@@ -89,3 +96,12 @@ def test_two_rank_shards_and_counter_allreduce():
     for r in res:
         np.testing.assert_array_equal(r[3], want)
         assert r[4] == 0
+    # rank 0 holds every shard's drop records, in stream order, equal to the
+    # single-rank records of the whole stream
+    _, ver1, ide1, nt = o.classify(h, 0, 0, want_notify=True)
+    rec, idx = o.drop_notify(h, 0, 0, ver1, ide1, nt)
+    assert res[1][5] is None
+    grec, gidx = res[0][5]
+    np.testing.assert_array_equal(gidx, idx.astype(np.int64))
+    np.testing.assert_array_equal(grec.view(np.uint8).reshape(-1),
+                                  rec.view(np.uint8))
