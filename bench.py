@@ -42,6 +42,9 @@ def main():
                     help="headers timed on the host-core oracle (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--notify", action="store_true",
+                    help="also produce every dropped header's drop_notify record "
+                         "(cfc_drop_notify_v4) inside the timed step")
     ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "trie"],
                     help="IPv4 ipcache device layout (cfc_set_option CFC_OPT_LPM4)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
@@ -52,6 +55,8 @@ def main():
                          "and Zipf(1.1) traffic (side measurements)")
     ap.add_argument("--flows", type=int, default=10_000_000)
     args = ap.parse_args()
+    if args.notify and args.workload == "c3":
+        ap.error("--notify covers IPv4 batches (c2, c5)")
 
     import torch
     import torch.distributed as dist
@@ -111,8 +116,27 @@ def main():
     out6 = Verdicts(torch.empty(n6, dtype=torch.int32, device=dev),
                     torch.empty(n6, dtype=torch.int32, device=dev), None)
 
+    nt_rec = nt_idx = nt_cnt = None
+    if args.notify:
+        import ctypes
+        from cilium_amd.datapath import _ptr
+        out.notify = torch.empty(n, dtype=torch.int32, device=dev)
+        nt_rec = torch.empty((n, 8), dtype=torch.int32, device=dev)
+        nt_idx = torch.empty(n, dtype=torch.int64, device=dev)
+        nt_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        nt_hdr = LL.HdrV4(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+                          _ptr(batch.meta), None, n)
+        nt_out = LL.Out(_ptr(out.verdict), _ptr(out.identity), None, None,
+                        _ptr(out.notify))
+        nt_stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
     def step():
         dp.classify_v4(batch, mode, ep_lxc, out=out)
+        if args.notify:   # records stay on the device (no sync in the step)
+            LL.check(dp.L.cfc_drop_notify_v4(
+                dp.h, ctypes.byref(nt_hdr), ctypes.byref(nt_out), mode, ep_lxc,
+                _ptr(nt_rec), _ptr(nt_idx), n, _ptr(nt_cnt), nt_stream),
+                "drop notify")
         if n6:
             dp.classify_v6(batch6, mode, ep_lxc, out=out6)
     torch.cuda.synchronize()
@@ -247,6 +271,7 @@ def main():
             "mode": args.mode,
             "lpm4_layout": {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none"),
             "parallelism": f"header-stream shards x{world}, tables replicated",
+            "drop_notify": bool(args.notify),
         },
         "roofline": {
             "kernel": "k_classify_v4" + (" + k_classify_v6" if n6 else ""),
@@ -271,6 +296,7 @@ def main():
                       f"restatement (oracle/cfc_oracle.c), {cores} OpenMP threads",
         },
         "parity_sample_ok": parity,
+        "drop_records_per_step_per_gpu": int(nt_cnt.item()) if args.notify else None,
     }
     print(json.dumps(res), flush=True)
     if world > 1:
