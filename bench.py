@@ -57,6 +57,15 @@ def main():
     args = ap.parse_args()
     if args.notify and args.workload == "c3":
         ap.error("--notify covers IPv4 batches (c2, c5)")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks before anything touches the
+        # GPU (torchrun on 127.0.0.1), wait for them, exit with their status
+        import subprocess
+        port = 29500 + os.getpid() % 2000
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
 
     import torch
     import torch.distributed as dist
@@ -67,6 +76,7 @@ def main():
     from cilium_amd.loader import load_tables
 
     rank, local_rank, world = env_rank()
+    assert world == args.gpus, f"WORLD_SIZE {world} != --gpus {args.gpus}"
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")

@@ -28,6 +28,7 @@ EXPORTS = (
     "cfc_counters_import", "cfc_get_stats", "cfc_strerror",
     "cfc_set_option", "cfc_timing_collect", "cfc_classify_v6",
     "cfc_ct_apply_v4", "cfc_ct_apply_v6", "cfc_map_update_batch",
+    "cfc_set_node_config", "cfc_get_node_config", "cfc_identity_counters",
 )
 # CT byte (cfc_out.ct): per stage (bits 0-3, then 4-7 for the destination's
 # ingress lookup after egress local delivery)
@@ -76,6 +77,22 @@ class Stats(ctypes.Structure):
                 ("ct6_entries", ctypes.c_uint32)]
 
 
+class NodeConfig(ctypes.Structure):
+    _fields_ = [("ipv4_cluster_range", ctypes.c_uint32),
+                ("ipv4_cluster_mask", ctypes.c_uint32),
+                ("router_ip6", ctypes.c_uint8 * 16)]
+
+
+class IdentityCount(ctypes.Structure):
+    _fields_ = [("identity", ctypes.c_uint32), ("dir", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8 * 3),
+                ("fwd_packets", ctypes.c_uint64), ("fwd_bytes", ctypes.c_uint64),
+                ("drop_packets", ctypes.c_uint64), ("drop_bytes", ctypes.c_uint64)]
+
+
+IDENTITY_OUT_OF_RANGE = 0xFFFFFFFF
+
+
 class Timing(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("classify_ms", ctypes.c_double),
                 ("count_ms", ctypes.c_double)]
@@ -105,6 +122,8 @@ def lib():
     L.cfc_map_delete.argtypes = [vp, i32, vp]
     L.cfc_map_get_next_key.argtypes = [vp, i32, vp, vp]
     L.cfc_endpoint_config.argtypes = [vp, ctypes.c_uint16, u32]
+    L.cfc_set_node_config.argtypes = [vp, ctypes.POINTER(NodeConfig)]
+    L.cfc_get_node_config.argtypes = [vp, ctypes.POINTER(NodeConfig)]
     L.cfc_commit.argtypes = [vp, vp]
     L.cfc_classify_v4.argtypes = [vp, ctypes.POINTER(HdrV4), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
@@ -123,6 +142,7 @@ def lib():
     L.cfc_counters_export.argtypes = [vp, vp, u64, vp]
     L.cfc_counters_import.argtypes = [vp, vp, u64, vp]
     L.cfc_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.cfc_identity_counters.argtypes = [vp, vp, u64, ctypes.POINTER(u64)]
     L.cfc_set_option.argtypes = [vp, i32, ctypes.c_int64]
     L.cfc_timing_collect.argtypes = [vp, ctypes.POINTER(Timing)]
     L.cfc_strerror.argtypes = [i32]

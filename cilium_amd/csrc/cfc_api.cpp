@@ -2,6 +2,7 @@
 // publication of the flattened tables, classify dispatch and counters.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 #include <map>
@@ -70,6 +71,7 @@ struct Epoch {
         polbloom, lxc6;
     DevBuf l6[3][3];   // ipc6 / pf6_fix / pf6_dyn: slots, bloom, lens
     DevBuf ct4, ct6, ct_acct;
+    std::vector<uint32_t> seclabel;   // SECLABEL by LXC_ID at commit
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
     std::vector<Ct6Slot> ct6_host;
     std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
@@ -77,8 +79,8 @@ struct Epoch {
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
     cfc_stats st{};
-    // drop notifications: {SECLABEL, ifindex} by LXC_ID, built on first use
-    std::vector<uint2> ep_info_host;
+    // drop notifications: {SECLABEL, ifindex} by LXC_ID, from the same
+    // snapshot of the maps as the tables
     DevBuf ep_info;
 };
 
@@ -94,6 +96,9 @@ struct cfc_ctx {
     std::vector<uint32_t> seclabel = std::vector<uint32_t>(65536, 0);
     uint64_t seclabel_gen = 0;
     BuildOpts opts;
+    // node_config.h defaults (IPV4_CLUSTER_RANGE/MASK, ROUTER_IP)
+    cfc_node_config node{0x100000u, 0xff0000u,
+                         {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 0}};
 
     std::unique_ptr<Epoch> epoch;
     uint64_t epoch_seq = 0;
@@ -108,6 +113,9 @@ struct cfc_ctx {
     uint32_t *ws = nullptr;
     size_t ws_bytes = 0;
     Map *metrics = nullptr;
+    // per-identity forward/drop counters folded so far ([dir][slot][fwd,
+    // drop][packets, bytes], the device block's layout)
+    std::vector<uint64_t> idc = std::vector<uint64_t>(ID_U64, 0);
 
     DevBuf nt_ws;   // drop-notify block counts / offsets
     hipEvent_t nt_done = nullptr;   // after the last drop-notify launch
@@ -224,6 +232,9 @@ int fold_counters(cfc_ctx *c, hipStream_t s)
         v[1] += by;
         memcpy(&it->second.val[8], v, 16);
     }
+    const uint64_t *idb = h.data() + 2 * nctr + METRIC_U64;
+    for (uint64_t i = 0; i < ID_U64; i++)
+        c->idc[i] += idb[i];
     const uint64_t *met = h.data() + 2 * nctr;
     for (int r = 0; r < METRIC_REASONS; r++)
         for (int d = 0; d < METRIC_DIRS; d++) {
@@ -303,6 +314,38 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
         if (nslots && (rc = E->ct_acct.zeros(32 * nslots, s)))
             return rc;
     }
+    // per-identity counters: the histogram ranges holding the reserved
+    // identities and every ipcache identity; others count directly
+    E->T.id_cover = 1u;
+    for (Map *m : ms)
+        if (m->role == ROLE_IPCACHE)
+            for (const auto &kv : m->kv) {
+                uint32_t lab;
+                memcpy(&lab, kv.second.val.data(), 4);
+                if (lab < ID_PACK_LIMIT)
+                    E->T.id_cover |= 1u << id_range_of(lab);
+            }
+    // drop notifications: {SECLABEL, ifindex} by LXC_ID (struct
+    // endpoint_info), and the SECLABELs the epoch's verdicts use
+    E->seclabel = c->seclabel;
+    {
+        std::vector<uint2> info(65536, make_uint2(0, 0));
+        for (uint32_t id = 0; id < 65536; id++)
+            info[id].x = c->seclabel[id];
+        for (Map *m : ms) {
+            if (m->role != ROLE_LXC)
+                continue;
+            for (auto &e : m->kv) {
+                uint32_t ifx;
+                uint16_t id;
+                memcpy(&ifx, e.second.val.data(), 4);
+                memcpy(&id, e.second.val.data() + 6, 2);
+                info[id].y = ifx;
+            }
+        }
+        if ((rc = upload_vec(E->ep_info, info, s)))
+            return rc;
+    }
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
             E->ct_maps[ct_map_key(m->role == ROLE_CT4 ? 4 : 6,
@@ -367,7 +410,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->st.prefilter_v6_dyn = img.pf6_dyn.n;
 
     // counters for the new entry layout (old ones were folded above)
-    size_t need = 2ull * T.n_ctr + METRIC_U64;
+    size_t need = 2ull * T.n_ctr + METRIC_U64 + ID_U64;
     if (need != c->ctr_u64) {
         if (c->ctr)
             (void)hipFree(c->ctr);
@@ -690,6 +733,24 @@ int cfc_endpoint_config(cfc_ctx *c, uint16_t lxc_id, uint32_t seclabel)
     return 0;
 }
 
+int cfc_set_node_config(cfc_ctx *c, const cfc_node_config *cfg)
+{
+    if (!c || !cfg)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    c->node = *cfg;
+    return 0;
+}
+
+int cfc_get_node_config(cfc_ctx *c, cfc_node_config *cfg)
+{
+    if (!c || !cfg)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    *cfg = c->node;
+    return 0;
+}
+
 int cfc_commit(cfc_ctx *c, void *stream)
 {
     if (!c)
@@ -725,7 +786,15 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     if (rc)
         return rc;
     Epoch &E = *c->epoch;
-    EgressArgs ea{ep_lxc, c->seclabel[ep_lxc], 0, 0, 0};
+    // the launch's copy of the epoch's tables, with the node constants
+    DevTables T = E.T;
+    T.v4_cluster_range = c->node.ipv4_cluster_range;
+    T.v4_cluster_mask = c->node.ipv4_cluster_mask;
+    for (int w = 0; w < 4; w++) {
+        const uint8_t *b = c->node.router_ip6 + 4 * w;
+        T.router6[w] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+    }
+    EgressArgs ea{ep_lxc, E.seclabel[ep_lxc], 0, 0, 0};
     {   // the sending endpoint's CT maps: its own, or the global ones
         for (auto &kv : c->maps)
             if ((kv.second->role == ROLE_CT4 || kv.second->role == ROLE_CT6) &&
@@ -739,8 +808,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
     }
-    size_t need = classify_workspace_bytes(in->n, E.T.n_ctr, mode,
-                                           E.T.ct4 || E.T.ct6 || out->ct);
+    size_t need = ws_layout(in->n, E.T, mode, E.T.ct4 || E.T.ct6 || out->ct).total;
     if (need > c->ws_bytes) {
         if (c->ws) {
             (void)hipDeviceSynchronize();
@@ -755,8 +823,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     // the workspace is shared: order this launch after the previous one
     if (c->ctr_pending && c->last_stream != s)
         (void)hipStreamWaitEvent(s, c->last_done, 0);
-    rc = launch(E.T, *in, *out, mode, ea, c->ctr, c->ctr + 2ull * E.T.n_ctr,
-                c->ws, c->num_cus, s, in->n ? next_timing(c) : nullptr);
+    rc = launch(T, *in, *out, mode, ea, c->ctr, c->ws, c->num_cus, s,
+                in->n ? next_timing(c) : nullptr);
     if (rc)
         return rc;
     (void)hipEventRecord(c->last_done, s);
@@ -793,6 +861,8 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
 {
     if (!c || !in || !out || !count || (cap && !rec))
         return -EINVAL;
+    if (reinterpret_cast<uintptr_t>(rec) & 15)
+        return -EINVAL;   // records are written as 16-byte stores (cfc.h)
     if (in->n && (!out->notify || !out->verdict || !out->identity ||
                   !in->saddr || !in->daddr || !in->ports || !in->meta))
         return -EINVAL;
@@ -810,25 +880,6 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     // after the previous one when it ran on another stream
     if (c->nt_pending && c->nt_stream != s)
         (void)hipStreamWaitEvent(s, c->nt_done, 0);
-    if (!E.ep_info.p) {
-        E.ep_info_host.assign(65536, make_uint2(0, 0));
-        for (uint32_t id = 0; id < 65536; id++)
-            E.ep_info_host[id].x = c->seclabel[id];
-        for (auto &kv : c->maps) {
-            if (kv.second->role != ROLE_LXC)
-                continue;
-            for (auto &e : kv.second->kv) {   // struct endpoint_info
-                uint32_t ifx;
-                uint16_t id;
-                memcpy(&ifx, e.second.val.data(), 4);
-                memcpy(&id, e.second.val.data() + 6, 2);
-                E.ep_info_host[id].y = ifx;
-            }
-        }
-        int rc = upload_vec(E.ep_info, E.ep_info_host, s);
-        if (rc)
-            return rc;
-    }
     const size_t need = drop_notify_workspace_bytes(in->n);
     if (need > c->nt_ws.bytes) {
         (void)hipDeviceSynchronize();
@@ -847,7 +898,7 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     a.n = in->n;
     a.family = family;
     a.mode = mode;
-    a.own_seclabel = c->seclabel[ep_lxc];
+    a.own_seclabel = E.seclabel[ep_lxc];   // as the batch was classified
     a.ep_info = reinterpret_cast<const uint2 *>(E.ep_info.p);
     a.rec = rec;
     a.hdr_index = hdr_index;
@@ -967,6 +1018,34 @@ int cfc_counters_import(cfc_ctx *c, const uint64_t *src, uint64_t n,
     (void)hipEventRecord(c->last_done, s);
     c->last_stream = s;
     c->ctr_pending = true;
+    return 0;
+}
+
+int cfc_identity_counters(cfc_ctx *c, cfc_identity_count *rows, uint64_t cap,
+                          uint64_t *n)
+{
+    if (!c || !n || (cap && !rows))
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    uint64_t k = 0;
+    for (uint32_t id = 0; id < ID_SLOTS; id++)
+        for (uint32_t dir = 0; dir < 2; dir++) {
+            const uint64_t *v = &c->idc[id_index(dir, id, 0)];   // fwd, then drop
+            if (!(v[0] | v[1] | v[2] | v[3]))
+                continue;
+            if (k < cap) {
+                cfc_identity_count &r = rows[k];
+                memset(&r, 0, sizeof(r));
+                r.identity = id == ID_SLOTS - 1 ? CFC_IDENTITY_OUT_OF_RANGE : id;
+                r.dir = (uint8_t)(dir + 1);
+                r.fwd_packets = v[0];
+                r.fwd_bytes = v[1];
+                r.drop_packets = v[2];
+                r.drop_bytes = v[3];
+            }
+            k++;
+        }
+    *n = k;
     return 0;
 }
 

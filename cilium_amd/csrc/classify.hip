@@ -53,6 +53,12 @@
 //   ct ports  bpf/lib/conntrack.h:467-590 (tuple->dport of a CT_NEW lookup)
 //   xdp       bpf_xdp.c:88-121
 //   metrics   bpf/lib/metrics.h:43-61
+#include <algorithm>
+#include <mutex>
+#include <set>
+#include <tuple>
+#include <vector>
+
 #include "kern_common.hpp"
 
 namespace cfc {
@@ -62,11 +68,19 @@ namespace {
 // update_metrics keys (reason, direction) a mode can produce.  A header
 // carries the index of its key, or NONE; every thread counts its headers per
 // key in registers, and the workgroup sums them in LDS at the end.
-constexpr int LDS_MET_U64 = 16;   // 2 x 7 keys, rounded to uint4 units
+// Egress batches add two keys for the per-identity counters of the
+// destination endpoint's policy verdict after local delivery, whose source
+// identity is the sender's SECLABEL for the whole batch (fwd, drop).
+constexpr int LDS_MET_U64 = 18;   // 2 x 9 keys
 template <int MODE>
 constexpr int met_n()
 {
     return MODE == CFC_MODE_EGRESS ? 7 : MODE == CFC_MODE_XDP ? 0 : 4;
+}
+template <int MODE>
+constexpr int acc_n()
+{
+    return met_n<MODE>() + (MODE == CFC_MODE_EGRESS ? 2 : 0);
 }
 // reason (as the positive DROP_* magnitude) and direction of key k
 template <int MODE>
@@ -118,6 +132,9 @@ struct Hdr {
     uint32_t ct_byte, ct_slot;   // CT byte (CFC_CT_*), stage-1 hit slot
     uint32_t ct_k1, ct_k2;       // accounting keys (slot * 2 + dir) per stage
     int ct_res;
+    uint32_t idw;                // identity counter key (CountArgs.id)
+    bool id_ovf, drop1;          // ident has no histogram range; stage-1 drop
+    uint32_t ev2;                // stage-2 identity event: 0, 1 fwd, 2 drop
     PolicyProbe P;
 };
 
@@ -230,6 +247,9 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     h.ct_slot = NONE;
     h.ct_res = CT_NEW;
     h.ct_k1 = h.ct_k2 = NONE;
+    h.idw = KEY_NONE;
+    h.id_ovf = h.drop1 = false;
+    h.ev2 = 0;
     if (MODE == CFC_MODE_XDP || h.xdp_drop)
         return;
     const uint32_t proto = h.mt & 0xFF;
@@ -281,7 +301,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
         } else {
             // destination identity (bpf_lxc.c:516-532)
             h.ident = h.e24 ? h.e24
-                            : ((h.da & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE
+                            : ((h.da & T.v4_cluster_mask) == T.v4_cluster_range
                                    ? CLUSTER_ID
                                    : WORLD_ID);
             h.need_pol = true;
@@ -339,7 +359,13 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
         if (h.ct_res == CT_NEW && (v >= 0 || reply))
             ctb |= CTO_CREATE;
     }
-    if (v < 0 && !reply) {
+    // the per-identity forward/drop counter of this policy verdict
+    const bool drop1 = v < 0 && !reply;
+    h.drop1 = drop1;
+    h.idw = id_key(T, h.ident, drop1, len);
+    h.id_ovf = h.idw == KEY_NONE;
+    uint32_t ev2 = 0;
+    if (drop1) {
         act = TC_ACT_SHOT;
         ver = DROP_POLICY;
         met0 = mkey<MODE>(DROP_POLICY, mdir);
@@ -392,14 +418,17 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                 act = TC_ACT_SHOT;
                 ver = DROP_POLICY;
                 met1 = mkey<MODE>(DROP_POLICY, METRIC_INGRESS);
+                ev2 = 2;
             } else {
                 const bool prox = w > 0 && !reply2;
                 act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
                 ver = prox ? w : 0;
                 met1 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
+                ev2 = 1;
             }
         }
     }
+    h.ev2 = ev2;
     h.act = act;
     h.ver = ver;
     h.met0 = met0;
@@ -407,7 +436,6 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     h.ctr0 = pr.ctr;
     h.ctr1 = ctr1;
     h.ct_byte = ctb;
-    (void)len;
 }
 
 // LDS image of one launch: the metrics block, then the tables copied in.
@@ -429,10 +457,28 @@ __host__ LdsPlan lds_plan(const DevTables &T)
     return p;
 }
 
+// the workgroup's metrics (and, egress, stage-2 identity) sums into the
+// counter block
+template <int MODE>
+__device__ __forceinline__ void acc_publish(const unsigned long long *s_met,
+                                            const CountArgs &C, uint32_t seclabel)
+{
+    for (uint32_t j = threadIdx.x; j < 2u * acc_n<MODE>(); j += BLOCK) {
+        const unsigned long long v = s_met[j];
+        if (!v)
+            continue;
+        const uint32_t k = j >> 1;
+        uint64_t *dst = k < (uint32_t)met_n<MODE>()
+                            ? C.g_met + met_reason_dir<MODE>(k) * 2
+                            : C.g_id + id_index(ID_DIR_INGRESS, seclabel, k - met_n<MODE>());
+        atomicAdd((unsigned long long *)dst + (j & 1), v);
+    }
+}
+
 template <int MODE, int U, bool CT, bool NT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
-    uint32_t *ctr_idx, uint32_t *ct_idx, uint64_t *g_met, uint64_t per_block)
+    CountArgs C, uint64_t per_block)
 {
     // LDS image (uint4 units): metrics | endpoint slots | pf Bloom | pol Bloom
     unsigned long long *s_met = lds_met();
@@ -457,11 +503,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
              L.pol_words / 4);
     __syncthreads();
 
+    constexpr bool EGR = MODE == CFC_MODE_EGRESS;
+    const uint32_t id_dir = EGR ? ID_DIR_EGRESS : ID_DIR_INGRESS;
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
     const uint64_t end = min(in.n, start + per_block);
     // the trip count is uniform across the workgroup (the metrics flush
     // needs whole waves)
-    MetAcc<met_n<MODE>()> acc;
+    MetAcc<acc_n<MODE>()> acc;
     acc.clear();
     uint32_t iter = 0;
     for (uint64_t base = start; base < end; base += (uint64_t)BLOCK * U) {
@@ -492,24 +540,28 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                     out.ct[o] = (uint8_t)h[u].ct_byte;
                 if (NT)   // the drop-notify site word (cfc_out.notify)
                     st_nt(notify_word(MODE, h[u].ver,
-                                      MODE == CFC_MODE_EGRESS &&
-                                          h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
+                                      EGR && h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
                                       h[u].rec.w & 0xFFFF, E.lxc_id),
                           out.notify + o);
                 if (CT) {
-                    st_nt(h[u].ct_k1, ct_idx + o);
-                    if (MODE == CFC_MODE_EGRESS)
-                        st_nt(h[u].ct_k2, ct_idx + ctr_stride(in.n) + o);
+                    st_nt(h[u].ct_k1, C.ct + o);
+                    if (EGR)
+                        st_nt(h[u].ct_k2, C.ct2 + o);
                 }
                 if (MODE != CFC_MODE_XDP) {
-                    st_nt(h[u].ctr0, ctr_idx + o);
-                    if (MODE == CFC_MODE_EGRESS)
-                        st_nt(h[u].ctr1, ctr_idx + ctr_stride(in.n) + o);
+                    st_nt(ctr_key(C, h[u].ctr0, len), C.ctr + o);
+                    if (EGR)
+                        st_nt(ctr_key(C, h[u].ctr1, len), C.ctr2 + o);
+                    st_nt(h[u].idw, C.id + o);
                 }
             }
+            if (MODE != CFC_MODE_XDP && h[u].valid && h[u].id_ovf && h[u].need_pol)
+                id_count(C, id_dir, h[u].ident, h[u].drop1, len);
             acc.add(h[u].valid ? h[u].met0 : NONE, len);
-            if (MODE == CFC_MODE_EGRESS)
+            if (EGR) {
                 acc.add(h[u].valid ? h[u].met1 : NONE, len);
+                acc.add(h[u].valid && h[u].ev2 ? met_n<MODE>() + h[u].ev2 - 1 : NONE, len);
+            }
         }
         if (++iter == 65536 / (2 * U)) {
             acc.flush(s_met);
@@ -518,99 +570,116 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     }
     acc.flush(s_met);
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < 2u * met_n<MODE>(); j += BLOCK) {
-        const unsigned long long v = s_met[j];
-        if (v)
-            atomicAdd((unsigned long long *)&g_met[met_reason_dir<MODE>(j >> 1) * 2 + (j & 1)],
-                      v);
-    }
+    acc_publish<MODE>(s_met, C, E.seclabel);
 }
 
-// Policy-entry counters from the per-header entry indices: an LDS
-// histogram per <= COUNT_PER_BLOCK headers.  blockIdx.y selects the index
-// array (1: egress local delivery, at ctr_idx + stride), both paired with
-// meta[i].  Four headers per thread and iteration (16-byte loads, four
-// independent LDS atomics); one u64 atomic per header adds {1 << 32 | len}.
-template <bool LDS>
-__global__ __launch_bounds__(BLOCK) void k_count(const uint32_t *ctr_idx,
-                                                 uint64_t stride,
-                                                 const uint32_t *meta,
-                                                 uint64_t n, uint32_t n_ctr,
-                                                 uint64_t *partial,
-                                                 uint64_t *g_ctr)
+}  // namespace
+
+// ---- counters ---------------------------------------------------------------
+// k_hist: the exact sums behind one key range of one key array, per slice of
+// the batch: an LDS histogram of up to HIST_RANGE u64 slots, one packed
+// {packets << 40 | bytes} atomic per header (a slice is at most 2^24
+// headers of <= 65535 bytes, so neither half carries), written as a partial
+// slab; k_hist_reduce sums the slabs per key and adds them into the counter
+// block.  One launch runs every job (policy ranges of each stage, identity
+// ranges) side by side: blockIdx.y is the job, blockIdx.x the slice.
+namespace {
+
+struct HistJob {
+    const uint32_t *keys;
+    uint64_t poff;        // first u64 of the job's partial slabs
+    uint32_t lo, cnt;     // key range [lo, lo + cnt)
+    uint32_t kind;        // 0 policy entry, 1 identity (dense << 1 | drop)
+    uint32_t packed;      // keys carry len in bits 16-31 (else meta does)
+};
+constexpr int HIST_JOBS_MAX = 12;
+struct HistJobs {
+    HistJob j[HIST_JOBS_MAX];
+};
+constexpr uint64_t BYTES_MASK = (1ull << 40) - 1;
+constexpr uint64_t SLICE_MAX = 1ull << 24;
+
+__device__ __forceinline__ void hist_add(unsigned long long *s, const HistJob &jb,
+                                         uint32_t w, uint32_t m)
 {
-    unsigned long long *s_ctr = reinterpret_cast<unsigned long long *>(cfc_smem);
-    if (LDS) {
-        for (uint32_t j = threadIdx.x; j < n_ctr; j += BLOCK)
-            s_ctr[j] = 0;
-        __syncthreads();
+    uint32_t k, len;
+    if (jb.packed) {
+        k = w & 0xFFFF;
+        len = w >> 16;
+    } else {
+        k = w;
+        len = m >> 16;
     }
-    const uint32_t *idx = ctr_idx + blockIdx.y * stride;   // 16-B aligned
-    auto add = [&](uint32_t c, uint32_t m) {
-        if (c == NONE)
-            return;
-        const uint32_t len = m >> 16;
-        if (LDS) {
-            atomicAdd(&s_ctr[c], (1ull << 32) | len);
-        } else {
-            atomicAdd((unsigned long long *)&g_ctr[2 * c], 1ull);
-            atomicAdd((unsigned long long *)&g_ctr[2 * c + 1],
-                      (unsigned long long)len);
-        }
-    };
-    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
-    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    const uint32_t r = k - jb.lo;
+    if (r < jb.cnt)
+        atomicAdd(&s[r], (1ull << 40) | len);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_hist(HistJobs J, const uint32_t *meta,
+                                                uint64_t n, uint64_t per_block,
+                                                uint64_t *partial)
+{
+    const HistJob jb = J.j[blockIdx.y];
+    unsigned long long *s = reinterpret_cast<unsigned long long *>(cfc_smem);
+    for (uint32_t j = threadIdx.x; j < jb.cnt; j += BLOCK)
+        s[j] = 0;
+    __syncthreads();
+    const uint64_t start = (uint64_t)blockIdx.x * per_block;   // multiple of 4
+    const uint64_t end = min(n, start + per_block);
     const uint64_t end4 = start + ((end - start) & ~3ull);
+    const bool meta16 = (reinterpret_cast<uintptr_t>(meta) & 15) == 0;
     for (uint64_t i = start + 4 * threadIdx.x; i < end4; i += 4 * BLOCK) {
-        const uint4 c = ld_nt4(idx + i);
-        uint4 m;
-        if ((reinterpret_cast<uintptr_t>(meta + i) & 15) == 0) {
-            m = ld_nt4(meta + i);
-        } else {
-            m.x = meta[i];
-            m.y = meta[i + 1];
-            m.z = meta[i + 2];
-            m.w = meta[i + 3];
+        const uint4 w = ld_nt4(jb.keys + i);
+        uint4 m = make_uint4(0, 0, 0, 0);
+        if (!jb.packed) {
+            if (meta16) {
+                m = ld_nt4(meta + i);
+            } else {
+                m.x = meta[i];
+                m.y = meta[i + 1];
+                m.z = meta[i + 2];
+                m.w = meta[i + 3];
+            }
         }
-        add(c.x, m.x);
-        add(c.y, m.y);
-        add(c.z, m.z);
-        add(c.w, m.w);
+        hist_add(s, jb, w.x, m.x);
+        hist_add(s, jb, w.y, m.y);
+        hist_add(s, jb, w.z, m.z);
+        hist_add(s, jb, w.w, m.w);
     }
     for (uint64_t i = end4 + threadIdx.x; i < end; i += BLOCK)
-        add(idx[i], meta[i]);
-    if (LDS) {
-        __syncthreads();
-        const size_t row = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-        uint64_t *dst = partial + row * n_ctr;
-        for (uint32_t j = threadIdx.x; j < n_ctr; j += BLOCK)
-            st_nt((uint64_t)s_ctr[j], dst + j);
-    }
+        hist_add(s, jb, jb.keys[i], jb.packed ? 0u : meta[i]);
+    __syncthreads();
+    uint64_t *dst = partial + jb.poff + (uint64_t)blockIdx.x * jb.cnt;
+    for (uint32_t j = threadIdx.x; j < jb.cnt; j += BLOCK)
+        st_nt((uint64_t)s[j], dst + j);
 }
 
-// Sum the per-workgroup partial slabs per counter (column sums, coalesced).
-// blockIdx.x: 256 entries, blockIdx.y: REDUCE_ROWS partial rows.
+// blockIdx.y: job, blockIdx.x: 256 keys of it
+// blockIdx.z: a group of REDUCE_ROWS slices
 constexpr uint32_t REDUCE_ROWS = 32;
-__global__ __launch_bounds__(256) void k_reduce_partials(const uint64_t *partial,
-                                                         uint32_t nblk,
-                                                         uint32_t n_ctr,
-                                                         uint64_t *g_ctr)
+__global__ __launch_bounds__(256) void k_hist_reduce(HistJobs J, const uint64_t *partial,
+                                                     uint32_t nblk, uint64_t *g_ctr,
+                                                     uint64_t *g_id, uint32_t id_dir)
 {
-    uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= n_ctr)
+    const HistJob jb = J.j[blockIdx.y];
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= jb.cnt)
         return;
-    uint32_t b0 = blockIdx.y * REDUCE_ROWS;
-    uint32_t b1 = min(nblk, b0 + REDUCE_ROWS);
     uint64_t pk = 0, by = 0;
+    const uint64_t *p = partial + jb.poff + j;
+    const uint32_t b0 = blockIdx.z * REDUCE_ROWS, b1 = min(nblk, b0 + REDUCE_ROWS);
     for (uint32_t b = b0; b < b1; b++) {
-        const uint64_t v = ld_nt(partial + (size_t)b * n_ctr + j);
-        pk += v >> 32;
-        by += v & 0xFFFFFFFFull;
+        const uint64_t v = ld_nt(p + (uint64_t)b * jb.cnt);
+        pk += v >> 40;
+        by += v & BYTES_MASK;
     }
-    if (pk) {
-        atomicAdd((unsigned long long *)&g_ctr[2 * j], (unsigned long long)pk);
-        atomicAdd((unsigned long long *)&g_ctr[2 * j + 1], (unsigned long long)by);
-    }
+    if (!pk)
+        return;
+    const uint32_t key = jb.lo + j;
+    uint64_t *dst = jb.kind == 0 ? g_ctr + 2ull * key
+                                 : g_id + id_index(id_dir, key >> 1, key & 1);
+    atomicAdd((unsigned long long *)dst, (unsigned long long)pk);
+    atomicAdd((unsigned long long *)dst + 1, (unsigned long long)by);
 }
 
 // CONNTRACK_ACCOUNTING: the per-header keys (slot * 2 + dir) of a
@@ -623,7 +692,7 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const uint64_t *partial
 constexpr uint32_t CT_LDS_SLOTS = 8192;
 constexpr uint32_t CT_LDS_BYTES = CT_LDS_SLOTS * 12;
 __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
-                                                    uint64_t stride,
+                                                    const uint32_t *ct_idx2,
                                                     const uint32_t *meta,
                                                     uint64_t n,
                                                     unsigned long long *acct)
@@ -636,7 +705,7 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
         vals[j] = 0;
     }
     __syncthreads();
-    const uint32_t *idx = ct_idx + blockIdx.y * stride;
+    const uint32_t *idx = blockIdx.y ? ct_idx2 : ct_idx;
     const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
     const uint64_t end = min(n, start + COUNT_PER_BLOCK);
     for (uint64_t i = start + threadIdx.x; i < end; i += BLOCK) {
@@ -688,41 +757,72 @@ __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
 
 template <int MODE, bool CT, bool NT>
 void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
-                    const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
-                    uint32_t grid, uint64_t per_block, hipStream_t s)
+                    const EgressArgs &E, const CountArgs &C, uint32_t grid,
+                    uint64_t per_block, hipStream_t s)
 {
     const LdsPlan L = lds_plan(T);
     auto kern = k_classify_v4<MODE, CFC_UNROLL, CT, NT>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)kern,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)LDS_PER_WG);
-        attr_set = true;
-    }
+    set_lds_limit((const void *)kern, (int)LDS_PER_WG);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
-                       out, E, ctr_idx, ct_idx_ptr(ctr_idx, in.n, T.n_ctr, MODE),
-                       g_met, per_block);
+                       out, E, C, per_block);
 }
 
 // the notify store is compiled in only when the caller asked for it
 template <int MODE, bool CT>
 void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
-                 const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
-                 uint32_t grid, uint64_t per_block, hipStream_t s)
+                 const EgressArgs &E, const CountArgs &C, uint32_t grid,
+                 uint64_t per_block, hipStream_t s)
 {
     if (out.notify)
-        launch_mode_nt<MODE, CT, true>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
+        launch_mode_nt<MODE, CT, true>(T, in, out, E, C, grid, per_block, s);
     else
-        launch_mode_nt<MODE, CT, false>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
+        launch_mode_nt<MODE, CT, false>(T, in, out, E, C, grid, per_block, s);
 }
 
-uint64_t partial_off(uint64_t n, int mode)
+// histogram slices of an n-header batch with `slots` keys in all: one per
+// CU of an MI355X (a slice of at most 2^24 headers, a multiple of 4), fewer
+// when the partial slabs would pass 256 MiB
+uint32_t hist_slices(uint64_t n, uint64_t slots)
 {
-    return (mode == CFC_MODE_EGRESS ? 2 : 1) * ctr_stride(n);
+    if (!n || !slots)
+        return 0;
+    uint64_t nb = std::min<uint64_t>(256, (n + 4095) / 4096);
+    nb = std::min<uint64_t>(nb, std::max<uint64_t>(1, (256ull << 20) / (8 * slots)));
+    nb = std::max<uint64_t>(nb, (n + SLICE_MAX - 1) / SLICE_MAX);
+    return (uint32_t)std::max<uint64_t>(nb, 1);
+}
+
+uint64_t hist_per_block(uint64_t n, uint32_t nblk)
+{
+    const uint64_t pb = (n + nblk - 1) / nblk;
+    return (pb + 3) & ~3ull;
+}
+
+// key slots the histogram covers: policy entries per stage, identities
+uint64_t hist_slots(const DevTables &T, int mode)
+{
+    if (mode == CFC_MODE_XDP)
+        return 0;
+    uint64_t id_slots = 0;
+    for (uint32_t r = 0; r < ID_RANGES; r++)
+        if ((T.id_cover >> r) & 1)
+            id_slots += std::min<uint64_t>(2 * ID_RANGE, 2ull * ID_PACK_LIMIT - 2ull * r * ID_RANGE);
+    return (mode == CFC_MODE_EGRESS ? 2ull : 1ull) * T.n_ctr + id_slots;
 }
 
 }  // namespace
+
+void set_lds_limit(const void *kernel, int bytes)
+{
+    static std::mutex mu;
+    static std::set<std::tuple<int, const void *, int>> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    if (done.insert(std::make_tuple(dev, kernel, bytes)).second)
+        (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  bytes);
+}
 
 size_t classify_lds_bytes(const DevTables &T) { return lds_plan(T).bytes(); }
 
@@ -736,31 +836,61 @@ int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
-size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode, bool ct)
+WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
 {
+    WsLayout w{};
     if (n == 0 || mode == CFC_MODE_XDP)
-        return 0;
-    const uint64_t halves = mode == CFC_MODE_EGRESS ? 2 : 1;
-    size_t bytes = 4ull * partial_off(n, mode);      // entry index per header
-    if (n_ctr && n_ctr <= LDS_CTR_MAX) {
-        const uint64_t nblk = (n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK;
-        bytes += 8ull * n_ctr * nblk * halves;       // partial slabs
+        return w;
+    const bool egr = mode == CFC_MODE_EGRESS;
+    const size_t a = 4 * ctr_stride(n);   // one u32 per header, 16-B aligned
+    size_t off = 0;
+    w.ctr = off;
+    off += a;
+    if (egr) {
+        w.ctr2 = off;
+        off += a;
     }
-    if (ct)   // CT accounting key per header and stage, 256-byte aligned
-        bytes = (bytes + 255) / 256 * 256 + 4ull * partial_off(n, mode);
-    return bytes;
+    w.id = off;
+    off += a;
+    if (ct) {
+        w.ct = off;
+        off += a;
+        if (egr) {
+            w.ct2 = off;
+            off += a;
+        }
+    }
+    off = (off + 255) & ~(size_t)255;
+    w.partial = off;
+    const uint64_t slots = hist_slots(T, mode);
+    w.nblk = hist_slices(n, slots);
+    w.total = off + 8ull * slots * w.nblk;
+    return w;
 }
 
-uint32_t *ct_idx_ptr(uint32_t *ws, uint64_t n, uint32_t n_ctr, int mode)
+CountArgs count_args(uint32_t *ws, const WsLayout &w, const DevTables &T,
+                     uint64_t *g_met, int mode, bool ct)
 {
-    const size_t off = (classify_workspace_bytes(n, n_ctr, mode) + 255) / 256 * 256;
-    return ws + off / 4;
+    CountArgs C{};
+    char *b = reinterpret_cast<char *>(ws);
+    if (w.total) {
+        C.ctr = reinterpret_cast<uint32_t *>(b + w.ctr);
+        C.ctr2 = mode == CFC_MODE_EGRESS ? reinterpret_cast<uint32_t *>(b + w.ctr2) : nullptr;
+        C.id = reinterpret_cast<uint32_t *>(b + w.id);
+        C.ct = ct ? reinterpret_cast<uint32_t *>(b + w.ct) : nullptr;
+        C.ct2 = ct && mode == CFC_MODE_EGRESS ? reinterpret_cast<uint32_t *>(b + w.ct2)
+                                              : nullptr;
+    }
+    C.g_met = g_met;
+    C.g_id = g_met + METRIC_U64;
+    C.ctr_packed = T.n_ctr < PACK_MAX;
+    return C;
 }
 
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,
-                       uint64_t *g_ctr, uint64_t *g_met, uint32_t *ws,
-                       int num_cus, hipStream_t s, const LaunchTiming *tm)
+                       uint64_t *g_ctr, uint32_t *ws, int num_cus, hipStream_t s,
+                       const LaunchTiming *tm)
 {
     if (in.n == 0)
         return 0;
@@ -778,20 +908,22 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
     // conntrack lookups when CT maps hold entries or the caller wants the
     // CT byte (to fold creates into the maps); an empty map misses anyway
     const bool ct = T.ct4 || out.ct;
-#define CFC_LAUNCH(M)                                                          \
-    (ct ? launch_mode<M, true>(T, in, out, E, ws, g_met, grid, per_block, s)   \
-        : launch_mode<M, false>(T, in, out, E, ws, g_met, grid, per_block, s))
+    const WsLayout w = ws_layout(in.n, T, mode, ct);
+    const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
+#define CFC_LAUNCH(M)                                                        \
+    (ct ? launch_mode<M, true>(T, in, out, E, C, grid, per_block, s)         \
+        : launch_mode<M, false>(T, in, out, E, C, grid, per_block, s))
     switch (mode) {
     case CFC_MODE_INGRESS: CFC_LAUNCH(CFC_MODE_INGRESS); break;
     case CFC_MODE_EGRESS: CFC_LAUNCH(CFC_MODE_EGRESS); break;
-    case CFC_MODE_XDP: launch_mode<CFC_MODE_XDP, false>(T, in, out, E, ws, g_met, grid, per_block, s); break;
+    case CFC_MODE_XDP: launch_mode<CFC_MODE_XDP, false>(T, in, out, E, C, grid, per_block, s); break;
     case CFC_MODE_FULL: CFC_LAUNCH(CFC_MODE_FULL); break;
     default: return -22;
     }
 #undef CFC_LAUNCH
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
-    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct && mode != CFC_MODE_XDP);
+    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct);
     if (tm)
         (void)hipEventRecord(tm->ev[2], s);
     hipError_t e = hipGetLastError();
@@ -802,44 +934,58 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
                      int mode, uint32_t *ws, uint64_t *g_ctr, hipStream_t s,
                      bool ct)
 {
-    if (ct && T.ct_acct && n) {
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void *)k_ct_count,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)CT_LDS_BYTES);
-            attr_set = true;
-        }
+    if (!n || mode == CFC_MODE_XDP)
+        return;
+    const WsLayout w = ws_layout(n, T, mode, ct);
+    const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
+    if (ct && T.ct_acct) {
+        set_lds_limit((const void *)k_ct_count, (int)CT_LDS_BYTES);
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
         hipLaunchKernelGGL(k_ct_count, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
-                           dim3(BLOCK), CT_LDS_BYTES, s,
-                           ct_idx_ptr(ws, n, T.n_ctr, mode), ctr_stride(n), meta, n,
+                           dim3(BLOCK), CT_LDS_BYTES, s, C.ct, C.ct2, meta, n,
                            reinterpret_cast<unsigned long long *>(T.ct_acct));
     }
-    if (mode != CFC_MODE_XDP && T.n_ctr && n) {
-        const uint32_t halves = mode == CFC_MODE_EGRESS ? 2 : 1;
-        const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
-        const dim3 grid_c(nblk, halves);
-        const uint64_t stride = ctr_stride(n);
-        if (T.n_ctr <= LDS_CTR_MAX) {
-            static bool attr_set = false;
-            if (!attr_set) {
-                (void)hipFuncSetAttribute((const void *)k_count<true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          LDS_BYTES_MAX);
-                attr_set = true;
-            }
-            uint64_t *partial = reinterpret_cast<uint64_t *>(ws + partial_off(n, mode));
-            const uint32_t rows = nblk * halves;
-            hipLaunchKernelGGL(k_count<true>, grid_c, dim3(BLOCK), 8ull * T.n_ctr,
-                               s, ws, stride, meta, n, T.n_ctr, partial, g_ctr);
-            hipLaunchKernelGGL(k_reduce_partials,
-                               dim3((T.n_ctr + 255) / 256, (rows + REDUCE_ROWS - 1) / REDUCE_ROWS),
-                               dim3(256), 0, s, partial, rows, T.n_ctr, g_ctr);
-        } else {
-            hipLaunchKernelGGL(k_count<false>, grid_c, dim3(BLOCK), 0, s, ws, stride,
-                               meta, n, T.n_ctr, nullptr, g_ctr);
+    // the histogram jobs: policy ranges of each stage, identity ranges
+    std::vector<HistJob> jobs;
+    uint64_t poff = 0;
+    auto add_jobs = [&](const uint32_t *keys, uint32_t nkeys, uint32_t kind,
+                        uint32_t packed) {
+        for (uint32_t lo = 0; lo < nkeys; lo += HIST_RANGE) {
+            HistJob j{keys, poff, lo, std::min(HIST_RANGE, nkeys - lo), kind, packed};
+            poff += (uint64_t)w.nblk * j.cnt;
+            jobs.push_back(j);
         }
+    };
+    add_jobs(C.ctr, T.n_ctr, 0, C.ctr_packed);
+    if (mode == CFC_MODE_EGRESS)
+        add_jobs(C.ctr2, T.n_ctr, 0, C.ctr_packed);
+    for (uint32_t r = 0; r < ID_RANGES; r++) {   // the identity ranges in use
+        if (!((T.id_cover >> r) & 1))
+            continue;
+        const uint32_t lo = 2 * r * ID_RANGE;
+        HistJob j{C.id, poff, lo, std::min(2 * ID_RANGE, 2 * ID_PACK_LIMIT - lo), 1, 1};
+        poff += (uint64_t)w.nblk * j.cnt;
+        jobs.push_back(j);
+    }
+    if (jobs.empty())
+        return;
+    uint64_t *partial = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws) + w.partial);
+    const uint64_t per_block = hist_per_block(n, w.nblk);
+    set_lds_limit((const void *)k_hist, (int)(8 * HIST_RANGE));
+    const uint32_t id_dir = mode == CFC_MODE_EGRESS ? ID_DIR_EGRESS : ID_DIR_INGRESS;
+    for (size_t a = 0; a < jobs.size(); a += HIST_JOBS_MAX) {
+        HistJobs J{};
+        const uint32_t nj = (uint32_t)std::min<size_t>(HIST_JOBS_MAX, jobs.size() - a);
+        uint32_t cmax = 0;
+        for (uint32_t k = 0; k < nj; k++) {
+            J.j[k] = jobs[a + k];
+            cmax = std::max(cmax, J.j[k].cnt);
+        }
+        hipLaunchKernelGGL(k_hist, dim3(w.nblk, nj), dim3(BLOCK), 8ull * cmax, s, J,
+                           meta, n, per_block, partial);
+        hipLaunchKernelGGL(k_hist_reduce,
+                           dim3((cmax + 255) / 256, nj, (w.nblk + REDUCE_ROWS - 1) / REDUCE_ROWS),
+                           dim3(256), 0, s, J, partial, w.nblk, g_ctr, C.g_id, id_dir);
     }
 }
 

@@ -18,12 +18,60 @@ struct EgressArgs {
     uint32_t ct_owner;   // ct_owner_word of the sending endpoint's CT maps
 };
 
-// The counter kernel keeps one packed u64 per policy entry in LDS when
-// n_ctr of them fit in the 160 KiB LDS (one 1024-thread block per CU);
-// beyond, global atomics.
-constexpr uint32_t LDS_CTR_MAX = 18432;
 constexpr int BLOCK = 1024;
 constexpr int LDS_BYTES_MAX = 160 * 1024;
+
+// ---- per-header counter keys (workspace) and the histogram pass
+// The classify kernels leave, per header, the key of every counter the
+// reference would bump; k_hist (classify.hip) turns them into sums with an
+// LDS histogram per slice of the batch and range of keys.
+//   policy   the matched policy entry (its counter index); packed with the
+//            header's skb->len as ctr | len << 16 when the epoch has fewer
+//            than 0xFFFF entries (k_hist then reads 4 bytes per header),
+//            else the bare index (and k_hist reads meta for len)
+//   identity the per-identity forward/drop counter of the header's policy
+//            verdict: identity << 1 | dropped, packed with len << 16, for
+//            identities below ID_PACK_LIMIT whose range of ID_RANGE
+//            identities has a histogram job (DevTables.id_cover: the ranges
+//            holding ipcache identities, and the reserved ones).  Cilium
+//            allocates identities upwards from 256 (pkg/identity), so a
+//            node's identities fill the first ranges; any other identity
+//            is counted by a direct atomic in the classify kernel.
+// NONE (0xFFFFFFFF) = nothing to count.
+constexpr uint32_t KEY_NONE = 0xFFFFFFFFu;
+constexpr uint32_t HIST_RANGE = 18432;   // LDS slots per histogram range (144 KiB)
+constexpr uint32_t PACK_MAX = 0xFFFF;    // packed keys: key < PACK_MAX
+
+// Per-identity forward/drop counters (cfc.h cfc_identity_counters): a block
+// of u64 [dir 2][ID_SLOTS identities][outcome 2][packets, bytes] after the
+// metrics in the counter block.  Identities >= 65536 (outside the
+// pkg/identity allocation range) share the last slot.
+constexpr uint32_t ID_SLOTS = 65537;
+constexpr uint64_t ID_U64 = 2ull * ID_SLOTS * 2 * 2;
+__host__ __device__ inline uint64_t id_index(uint32_t dir, uint32_t ident,
+                                             uint32_t drop)
+{
+    const uint32_t s = ident < ID_SLOTS - 1 ? ident : ID_SLOTS - 1;
+    return (((uint64_t)dir * ID_SLOTS + s) * 2 + drop) * 2;
+}
+// dir index of the identity block: 0 ingress, 1 egress (METRIC_* - 1)
+constexpr uint32_t ID_DIR_INGRESS = 0, ID_DIR_EGRESS = 1;
+constexpr uint32_t ID_RANGE = HIST_RANGE / 2;   // identities per histogram range
+constexpr uint32_t ID_PACK_LIMIT = 32768;        // identity << 1 | drop < 2^16
+constexpr uint32_t ID_RANGES = (ID_PACK_LIMIT + ID_RANGE - 1) / ID_RANGE;
+__host__ __device__ inline uint32_t id_range_of(uint32_t ident) { return ident / ID_RANGE; }
+
+// Per-launch pointers of the counter keys and the counter block.
+struct CountArgs {
+    uint32_t *ctr;       // policy key per header (stage 1)
+    uint32_t *ctr2;      // egress: the destination's policy (stage 2)
+    uint32_t *id;        // identity key per header
+    uint32_t *ct;        // CT accounting key per header (stage 1)
+    uint32_t *ct2;       // egress stage 2
+    uint64_t *g_met;     // metrics block
+    uint64_t *g_id;      // identity block
+    uint32_t ctr_packed; // policy keys packed with len
+};
 
 // Optional per-call timing (CFC_OPT_TIMING): events recorded on the launch
 // stream before the classify kernel, after it, and after the counter
@@ -32,14 +80,15 @@ struct LaunchTiming {
     hipEvent_t ev[3];
 };
 
-// Bytes of workspace a launch over n headers needs: the matched policy-entry
-// index per header (two per header in EGRESS mode) + the counter kernel's
-// partial slabs.
-// With ct, followed by the per-header CT accounting keys
-// (slot * 2 + dir, NONE: no hit) the CT counter kernel aggregates.
-size_t classify_workspace_bytes(uint64_t n, uint32_t n_ctr, int mode,
-                                bool ct = false);
-uint32_t *ct_idx_ptr(uint32_t *ws, uint64_t n, uint32_t n_ctr, int mode);
+// Workspace of one launch over n headers: the key arrays of CountArgs, then
+// the histogram's partial slabs.
+struct WsLayout {
+    size_t ctr, ctr2, id, ct, ct2, partial, total;   // byte offsets / size
+    uint32_t nblk;                                    // histogram slices
+};
+WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct);
+CountArgs count_args(uint32_t *ws, const WsLayout &w, const DevTables &T,
+                     uint64_t *g_met, int mode, bool ct);
 // LDS image of the classify kernel for these tables (must be <= 160 KiB).
 size_t classify_lds_bytes(const DevTables &T);
 
@@ -47,23 +96,26 @@ size_t classify_lds_bytes(const DevTables &T);
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
                    hipStream_t stream);
 
+// g_ctr: the counter block (policy entries, then metrics, then identities)
 int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,
-                       uint64_t *g_ctr, uint64_t *g_met, uint32_t *workspace,
-                       int num_cus, hipStream_t stream,
-                       const LaunchTiming *timing = nullptr);
+                       uint64_t *g_ctr, uint32_t *workspace, int num_cus,
+                       hipStream_t stream, const LaunchTiming *timing = nullptr);
 
-// The policy-entry counter kernels over the per-header entry indices the
-// classify kernel left in the workspace (both families).
+// The counter kernels over the per-header keys the classify kernel left in
+// the workspace (both families): policy entries, identities, CT accounting.
 void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
                      int mode, uint32_t *workspace, uint64_t *g_ctr,
-                     hipStream_t stream, bool ct = false);
+                     hipStream_t stream, bool ct);
 
 int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,
-                       uint64_t *g_ctr, uint64_t *g_met, uint32_t *workspace,
-                       int num_cus, hipStream_t stream,
-                       const LaunchTiming *timing = nullptr);
+                       uint64_t *g_ctr, uint32_t *workspace, int num_cus,
+                       hipStream_t stream, const LaunchTiming *timing = nullptr);
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device,
+// kernel), thread-safe
+void set_lds_limit(const void *kernel, int bytes);
 
 // Drop-notify records of one classified batch (notify.hip): the per-header
 // cfc_out.notify words compacted in header order into cfc_drop_notify.

@@ -32,16 +32,19 @@ namespace {
 
 constexpr int DROP_INVALID_EXTHDR = -156, DROP_FRAG_NOSUPPORT = -157;
 constexpr int VERDICT_PUNT = CFC_VERDICT_PUNT;
-// node_config.h ROUTER_IP beef::1:0:1:0:0 as host-order words
-constexpr uint32_t ROUTER6_W0 = 0xBEEF0000u, ROUTER6_W1 = 0u,
-                   ROUTER6_W2 = 0x00000001u, ROUTER6_W3 = 0x00010000u;
 
 // update_metrics keys (reason, direction) per mode
-constexpr int LDS_MET6_U64 = 18;   // 2 x 9 keys
+// (egress: + 2 keys for the stage-2 per-identity counters, classify.hip)
+constexpr int LDS_MET6_U64 = 22;   // 2 x 11 keys
 template <int MODE>
 constexpr int met6_n()
 {
     return MODE == CFC_MODE_EGRESS ? 9 : MODE == CFC_MODE_XDP ? 0 : 6;
+}
+template <int MODE>
+constexpr int acc6_n()
+{
+    return met6_n<MODE>() + (MODE == CFC_MODE_EGRESS ? 2 : 0);
 }
 template <int MODE>
 __host__ __device__ constexpr uint32_t met6_reason_dir(int k)
@@ -156,14 +159,14 @@ __device__ __forceinline__ bool ct6_new_dport(uint32_t proto, uint32_t ports,
 // icmp6_handle (icmp6.h:390-412): neighbour solicitations and echo requests
 // to the router are answered, not classified.  It reads the type right after
 // the fixed header, so with extension headers it never triggers.
-__device__ __forceinline__ bool icmp6_punt(uint32_t proto, uint32_t meta,
-                                           uint32_t ports, uint4 da)
+__device__ __forceinline__ bool icmp6_punt(const DevTables &T, uint32_t proto,
+                                           uint32_t meta, uint32_t ports, uint4 da)
 {
     if (proto != 58 || (meta & CFC_HF_EXTHDR))
         return false;
     const uint32_t type = ports & 0xFF;
-    return type == 135 || (type == 128 && da.x == ROUTER6_W0 && da.y == ROUTER6_W1 &&
-                           da.z == ROUTER6_W2 && da.w == ROUTER6_W3);
+    return type == 135 || (type == 128 && da.x == T.router6[0] && da.y == T.router6[1] &&
+                           da.z == T.router6[2] && da.w == T.router6[3]);
 }
 
 struct LdsPlan6 {
@@ -182,10 +185,22 @@ __host__ LdsPlan6 lds_plan6(const DevTables &T)
     return p;
 }
 
+// a policy verdict's per-identity counter: its histogram key, or a direct
+// atomic for identities outside every histogram range
+__device__ __forceinline__ uint32_t id_event(const DevTables &T, const CountArgs &C,
+                                             uint32_t dir, uint32_t ident, bool drop,
+                                             uint32_t len, bool valid)
+{
+    const uint32_t k = id_key(T, ident, drop, len);
+    if (k == KEY_NONE && valid)
+        id_count(C, dir, ident, drop, len);
+    return k;
+}
+
 template <int MODE, bool CT, bool NT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     DevTables T, LdsPlan6 L, cfc_hdr_v6 in, cfc_out out, EgressArgs E,
-    uint32_t *ctr_idx, uint32_t *ct_idx, uint64_t *g_met, uint64_t per_block)
+    CountArgs C, uint64_t per_block)
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
@@ -212,7 +227,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     const uint64_t end = min(in.n, start + per_block);
     const uint32_t *sa_in = reinterpret_cast<const uint32_t *>(in.saddr);
     const uint32_t *da_in = reinterpret_cast<const uint32_t *>(in.daddr);
-    MetAcc<met6_n<MODE>()> acc;
+    MetAcc<acc6_n<MODE>()> acc;
     acc.clear();
     uint32_t iter = 0;
     for (uint64_t base = start; base < end; base += BLOCK) {
@@ -231,6 +246,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
         uint32_t ctb = 0;   // CT byte (cfc.h CFC_CT_*)
         uint32_t ck1 = NONE, ck2 = NONE;   // CT accounting keys per stage
+        uint32_t idw = KEY_NONE, ev2 = 0;  // identity counter key; stage-2 event
         const uint32_t len = mt >> 16;
         const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
         const bool local = (drec.z & LXC_VALID) != 0;
@@ -251,7 +267,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             const bool known = ct6_new_dport(proto, pt, &dport);
             const int xd = proto == 59 ? DROP_INVALID_EXTHDR
                          : proto == 44 ? DROP_FRAG_NOSUPPORT : 0;
-            const bool punt = icmp6_punt(proto, mt, pt, da);
+            const bool punt = icmp6_punt(T, proto, mt, pt, da);
             const bool ifx = (drec.z & LXC_IFINDEX) != 0;
             if (!EGR) {
                 // handle_identity_from_host (bpf_netdev.c:128-153)
@@ -305,6 +321,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                             if (CT)
                                 ctb = (uint32_t)c.res | CTO_DONE |
                                       ((c.res == CT_NEW && pr.verdict >= 0) ? CTO_CREATE : 0u);
+                            idw = id_event(T, C, ID_DIR_INGRESS, ident,
+                                           pr.verdict < 0 && !reply, len, valid);
                             if (pr.verdict < 0 && !reply) {
                                 act = TC_ACT_SHOT;
                                 ver = DROP_POLICY;
@@ -338,8 +356,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     // destination identity (bpf_lxc.c:206-221)
                     const uint32_t label = lpm6_lookup(T.ipc6, da);
                     ident = label ? label
-                          : (da.x == ROUTER6_W0 && da.y == ROUTER6_W1) ? CLUSTER_ID
-                                                                        : WORLD_ID;
+                          : (da.x == T.router6[0] && da.y == T.router6[1]) ? CLUSTER_ID
+                                                                            : WORLD_ID;
                     // ipv6_l3_from_lxc's ct_lookup6 (bpf_lxc.c:190)
                     CtResult c{CT_NEW, NONE, dport};
                     if (CT) {
@@ -354,6 +372,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     if (CT)
                         ctb = (uint32_t)c.res | CTO_DONE |
                               ((c.res == CT_NEW && pr.verdict >= 0) ? CTO_CREATE : 0u);
+                    idw = id_event(T, C, ID_DIR_EGRESS, ident, pr.verdict < 0 && !reply,
+                                   len, valid);
                     if (pr.verdict < 0 && !reply) {
                         ver = DROP_POLICY;
                         met0 = mkey6<MODE>(DROP_POLICY, METRIC_EGRESS);
@@ -389,6 +409,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 ctb |= ((uint32_t)c2.res | CTO_DONE |
                                         ((c2.res == CT_NEW && pw.verdict >= 0) ? CTO_CREATE : 0u))
                                        << 4;
+                            ev2 = (pw.verdict < 0 && !reply2) ? 2 : 1;
                             if (pw.verdict < 0 && !reply2) {
                                 ver = DROP_POLICY;
                                 met1 = mkey6<MODE>(DROP_POLICY, METRIC_INGRESS);
@@ -415,18 +436,21 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                               drec.z & 0xFFFF, E.lxc_id),
                   out.notify + i);
         if (CT) {
-            st_nt(ck1, ct_idx + i);
+            st_nt(ck1, C.ct + i);
             if (EGR)
-                st_nt(ck2, ct_idx + ctr_stride(in.n) + i);
+                st_nt(ck2, C.ct2 + i);
         }
         if (MODE != CFC_MODE_XDP) {
-            st_nt(ctr0, ctr_idx + i);
+            st_nt(ctr_key(C, ctr0, len), C.ctr + i);
             if (EGR)
-                st_nt(ctr1, ctr_idx + ctr_stride(in.n) + i);
+                st_nt(ctr_key(C, ctr1, len), C.ctr2 + i);
+            st_nt(idw, C.id + i);
         }
         acc.add(valid ? met0 : NONE, len);
-        if (EGR)
+        if (EGR) {
             acc.add(valid ? met1 : NONE, len);
+            acc.add(valid && ev2 ? met6_n<MODE>() + ev2 - 1 : NONE, len);
+        }
         if (++iter == 65536 / 2) {
             acc.flush(s_met);
             iter = 0;
@@ -434,50 +458,47 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     }
     acc.flush(s_met);
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < 2u * met6_n<MODE>(); j += BLOCK) {
+    for (uint32_t j = threadIdx.x; j < 2u * acc6_n<MODE>(); j += BLOCK) {
         const unsigned long long v = s_met[j];
-        if (v)
-            atomicAdd((unsigned long long *)&g_met[met6_reason_dir<MODE>(j >> 1) * 2 + (j & 1)],
-                      v);
+        if (!v)
+            continue;
+        const uint32_t k = j >> 1;
+        uint64_t *dst = k < (uint32_t)met6_n<MODE>()
+                            ? C.g_met + met6_reason_dir<MODE>(k) * 2
+                            : C.g_id + id_index(ID_DIR_INGRESS, E.seclabel, k - met6_n<MODE>());
+        atomicAdd((unsigned long long *)dst + (j & 1), v);
     }
 }
 
 template <int MODE, bool CT, bool NT>
 void launch_mode6_nt(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
-                     const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
-                     uint32_t grid, uint64_t per_block, hipStream_t s)
+                     const EgressArgs &E, const CountArgs &C, uint32_t grid,
+                     uint64_t per_block, hipStream_t s)
 {
     const LdsPlan6 L = lds_plan6(T);
     auto kern = k_classify_v6<MODE, CT, NT>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        (void)hipFuncSetAttribute((const void *)kern,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)LDS_PER_WG);
-        attr_set = true;
-    }
+    set_lds_limit((const void *)kern, (int)LDS_PER_WG);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
-                       out, E, ctr_idx, ct_idx_ptr(ctr_idx, in.n, T.n_ctr, MODE),
-                       g_met, per_block);
+                       out, E, C, per_block);
 }
 
 template <int MODE, bool CT>
 void launch_mode6(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &out,
-                  const EgressArgs &E, uint32_t *ctr_idx, uint64_t *g_met,
-                  uint32_t grid, uint64_t per_block, hipStream_t s)
+                  const EgressArgs &E, const CountArgs &C, uint32_t grid,
+                  uint64_t per_block, hipStream_t s)
 {
     if (out.notify)
-        launch_mode6_nt<MODE, CT, true>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
+        launch_mode6_nt<MODE, CT, true>(T, in, out, E, C, grid, per_block, s);
     else
-        launch_mode6_nt<MODE, CT, false>(T, in, out, E, ctr_idx, g_met, grid, per_block, s);
+        launch_mode6_nt<MODE, CT, false>(T, in, out, E, C, grid, per_block, s);
 }
 
 }  // namespace
 
 int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
                        const cfc_out &out, int mode, const EgressArgs &E,
-                       uint64_t *g_ctr, uint64_t *g_met, uint32_t *ws,
-                       int num_cus, hipStream_t s, const LaunchTiming *tm)
+                       uint64_t *g_ctr, uint32_t *ws, int num_cus, hipStream_t s,
+                       const LaunchTiming *tm)
 {
     if (in.n == 0)
         return 0;
@@ -492,20 +513,22 @@ int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
     if (tm)
         (void)hipEventRecord(tm->ev[0], s);
     const bool ct = T.ct6 || out.ct;
+    const WsLayout w = ws_layout(in.n, T, mode, ct);
+    const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
 #define CFC_LAUNCH6(M)                                                         \
-    (ct ? launch_mode6<M, true>(T, in, out, E, ws, g_met, grid, per_block, s)  \
-        : launch_mode6<M, false>(T, in, out, E, ws, g_met, grid, per_block, s))
+    (ct ? launch_mode6<M, true>(T, in, out, E, C, grid, per_block, s)          \
+        : launch_mode6<M, false>(T, in, out, E, C, grid, per_block, s))
     switch (mode) {
     case CFC_MODE_INGRESS: CFC_LAUNCH6(CFC_MODE_INGRESS); break;
     case CFC_MODE_EGRESS: CFC_LAUNCH6(CFC_MODE_EGRESS); break;
-    case CFC_MODE_XDP: launch_mode6<CFC_MODE_XDP, false>(T, in, out, E, ws, g_met, grid, per_block, s); break;
+    case CFC_MODE_XDP: launch_mode6<CFC_MODE_XDP, false>(T, in, out, E, C, grid, per_block, s); break;
     case CFC_MODE_FULL: CFC_LAUNCH6(CFC_MODE_FULL); break;
     default: return -22;
     }
 #undef CFC_LAUNCH6
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
-    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct && mode != CFC_MODE_XDP);
+    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct);
     if (tm)
         (void)hipEventRecord(tm->ev[2], s);
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -9,7 +9,6 @@ namespace cfc {
 namespace {
 
 constexpr uint32_t HOST_ID = 1, WORLD_ID = 2, CLUSTER_ID = 3, HEALTH_ID = 4;
-constexpr uint32_t IPV4_CLUSTER_MASK = 0xff0000u, IPV4_CLUSTER_RANGE = 0x100000u;
 constexpr int DROP_INVALID_SIP = -132, DROP_POLICY = -133,
               DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140;
 constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
@@ -513,6 +512,32 @@ struct MetAcc {
         clear();
     }
 };
+
+// the policy counter key of a header (CountArgs.ctr)
+__device__ __forceinline__ uint32_t ctr_key(const CountArgs &C, uint32_t ctr,
+                                            uint32_t len)
+{
+    return ctr == NONE ? KEY_NONE : C.ctr_packed ? (ctr | len << 16) : ctr;
+}
+// the identity counter key of a policy verdict (CountArgs.id), KEY_NONE
+// when the identity has no histogram range (id_count then)
+__device__ __forceinline__ uint32_t id_key(const DevTables &T, uint32_t ident,
+                                           bool drop, uint32_t len)
+{
+    const bool packed = ident < ID_PACK_LIMIT && ((T.id_cover >> id_range_of(ident)) & 1);
+    return packed ? ((ident << 1 | (uint32_t)drop) | len << 16) : KEY_NONE;
+}
+// a per-identity counter bumped directly: identities outside every
+// histogram range (from skb->mark, not in the ipcache) — rare, so plain
+// global atomics
+__device__ __forceinline__ void id_count(const CountArgs &C, uint32_t dir,
+                                         uint32_t ident, bool drop, uint32_t len)
+{
+    unsigned long long *p =
+        reinterpret_cast<unsigned long long *>(C.g_id) + id_index(dir, ident, drop);
+    atomicAdd(p, 1ull);
+    atomicAdd(p + 1, (unsigned long long)len);
+}
 
 template <class W>
 __device__ __forceinline__ void lds_copy(W *dst, const W *src, uint32_t n)

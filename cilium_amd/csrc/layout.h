@@ -300,6 +300,13 @@ struct DevTables {
     uint32_t ct4_mask, ct4_probe;
     uint32_t ct6_mask, ct6_probe;
     uint32_t ct6_acct_base;        // first v6 slot in ct_acct
+    // per-identity counters: bit r set = identities [r * ID_RANGE,
+    // (r + 1) * ID_RANGE) have a histogram range (classify.hpp)
+    uint32_t id_cover;
+    // node_config.h constants (cfc_set_node_config), filled in per launch
+    uint32_t v4_cluster_range;     // IPV4_CLUSTER_RANGE, be32 raw
+    uint32_t v4_cluster_mask;      // IPV4_CLUSTER_MASK, be32 raw
+    uint32_t router6[4];           // ROUTER_IP as host-order words
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]

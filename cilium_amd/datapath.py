@@ -185,6 +185,23 @@ class Datapath:
         L.check(self.L.cfc_endpoint_config(self.h, lxc_id, seclabel),
                 "endpoint config")
 
+    def set_node_config(self, ipv4_cluster_range, ipv4_cluster_mask,
+                        router_ip6):
+        """cfc_set_node_config: what the agent writes into node_config.h
+        (daemon/daemon.go:916-934).  The IPv4 values are raw be32 (the
+        header's %#x), router_ip6 is 16 bytes."""
+        c = L.NodeConfig()
+        c.ipv4_cluster_range = int(ipv4_cluster_range) & 0xFFFFFFFF
+        c.ipv4_cluster_mask = int(ipv4_cluster_mask) & 0xFFFFFFFF
+        c.router_ip6[:] = list(bytes(bytearray(router_ip6)))
+        L.check(self.L.cfc_set_node_config(self.h, ctypes.byref(c)),
+                "node config")
+
+    def node_config(self):
+        c = L.NodeConfig()
+        L.check(self.L.cfc_get_node_config(self.h, ctypes.byref(c)), "node config")
+        return c.ipv4_cluster_range, c.ipv4_cluster_mask, bytes(c.router_ip6)
+
     # ------------------------------------------------ datapath
     def _stream(self, stream):
         if self.device == L.CFC_DEVICE_NONE:
@@ -291,11 +308,13 @@ class Datapath:
                    self._stream(stream)), "ct apply")
 
     def drop_notify(self, batch, out: Verdicts, mode=L.MODE_INGRESS,
-                    ep_lxc=0, cap=None, stream=None):
+                    ep_lxc=0, cap=None, stream=None, sync=True):
         """cfc_drop_notify_v4/v6: the batch's struct drop_notify records in
         header order -> (records as an (m, 8) int32 tensor in the
         cfc_drop_notify layout, header indices int64, total drops).
-        Synchronises the stream to read the total."""
+        sync=True synchronises the device to read the total and trims the
+        tensors to it; sync=False returns (records, indices, total as a
+        1-element int64 device tensor) with nothing waited for."""
         import torch
         assert out.notify is not None, "classify with want_notify=True"
         n = len(batch)
@@ -314,6 +333,8 @@ class Datapath:
         L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
                    _ptr(rec), _ptr(idx), cap, _ptr(cnt), self._stream(stream)),
                 "drop notify")
+        if not sync:
+            return rec, idx, cnt
         torch.cuda.synchronize(dev)
         total = int(cnt.item())
         m = min(total, cap)
@@ -343,6 +364,21 @@ class Datapath:
         L.check(self.L.cfc_counters_device(self.h, ctypes.byref(p),
                                            ctypes.byref(n)), "counters device")
         return p.value, n.value
+
+    def identity_counters(self):
+        """cfc_identity_counters: the per-identity forward/drop totals folded
+        by counters_sync -> numpy (n, 6) u64 rows {identity, dir (1 ingress,
+        2 egress), fwd packets, fwd bytes, drop packets, drop bytes}."""
+        import numpy as np
+        n = ctypes.c_uint64()
+        L.check(self.L.cfc_identity_counters(self.h, None, 0, ctypes.byref(n)),
+                "identity counters")
+        rows = (L.IdentityCount * max(n.value, 1))()
+        L.check(self.L.cfc_identity_counters(self.h, rows, n.value, ctypes.byref(n)),
+                "identity counters")
+        return np.array([(r.identity, r.dir, r.fwd_packets, r.fwd_bytes,
+                          r.drop_packets, r.drop_bytes) for r in rows[:n.value]],
+                        np.uint64).reshape(-1, 6)
 
     def stats(self):
         st = L.Stats()

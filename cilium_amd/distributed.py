@@ -53,7 +53,9 @@ def gather_drop_notify(rec, idx, start, dst=0, group=None):
     turns the per-shard header indices into stream indices.  Two collectives
     per reporting interval (counts, then the padded records), off the
     per-batch path like the counter all-reduce.  -> (records, stream
-    indices) on dst, (None, None) elsewhere."""
+    indices) on dst, (None, None) elsewhere.  Only the counts are
+    all-gathered (every rank needs them to pad); the records themselves are
+    gathered to dst alone."""
     import torch
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or \
@@ -69,9 +71,10 @@ def gather_drop_notify(rec, idx, start, dst=0, group=None):
     if rec.shape[0]:
         row[:rec.shape[0], :4] = rec.contiguous().view(torch.int64).view(-1, 4)
         row[:rec.shape[0], 4] = idx.to(torch.int64) + start
-    rows = [torch.zeros_like(row) for _ in range(world)]
-    dist.all_gather(rows, row, group=group)
-    if dist.get_rank(group) != dst:
+    me = dist.get_rank(group)
+    rows = [torch.zeros_like(row) for _ in range(world)] if me == dst else None
+    dist.gather(row, rows, dst=dst, group=group)
+    if me != dst:
         return None, None
     full = torch.cat([r[:int(c.item())] for r, c in zip(rows, counts)])
     recs = full[:, :4].contiguous().view(torch.int32).view(-1, 8)

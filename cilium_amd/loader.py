@@ -54,6 +54,8 @@ def load_tables(dp: Datapath, t, commit=True):
                 dp.update_element((dyn6 if p["dyn"] else fix6).Fd, key, b"\x00")
     if getattr(t, "ct", None) is not None:
         dp.ct_fds = load_ct(dp, t)
+    if getattr(t, "node", None) is not None:
+        dp.set_node_config(*t.node)
     if commit:
         dp.commit()
     return pms

@@ -86,6 +86,9 @@ class Tables:
     prefilter: np.ndarray                    # PREFILTER_DT
     seclabel: dict                           # lxc_id -> u32 (endpoint SECLABEL)
     ct: np.ndarray = None                    # CT_DT pre-populated conntrack
+    # node_config.h (IPV4_CLUSTER_RANGE, IPV4_CLUSTER_MASK, ROUTER_IP); None =
+    # the reference's compiled-in values
+    node: tuple = None
 
 
 @dataclasses.dataclass

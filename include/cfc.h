@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 5
+#define CFC_ABI_VERSION 6
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -103,6 +103,26 @@ int cfc_num_possible_cpus(void);
  * of its egress traffic. */
 int cfc_endpoint_config(cfc_ctx *ctx, uint16_t lxc_id, uint32_t seclabel);
 
+/* Per-node datapath constants the agent writes into node_config.h
+ * (daemon/daemon.go:916-934 writeNetdevHeader / compileBase):
+ *   ipv4_cluster_range / ipv4_cluster_mask  IPV4_CLUSTER_RANGE / _MASK, as
+ *       the %#x of byteorder.HostSliceToNetwork(...) — i.e. the raw
+ *       network-order address bytes loaded little-endian, the form
+ *       handle_ipv4_from_lxc compares orig_dip against (bpf_lxc.c:523);
+ *   router_ip6  ROUTER_IP, the node's IPv6 router address (the /64 that
+ *       makes an egress destination CLUSTER_ID, bpf_lxc.c:214, and the
+ *       echo-request target icmp6_handle answers, icmp6.h:390-412).
+ * A new context starts with the values of the reference's
+ * bpf/node_config.h (0x100000 / 0xff0000, beef::1:0:1:0:0).  Takes effect
+ * for every classify call made after it returns. */
+typedef struct {
+    uint32_t ipv4_cluster_range;
+    uint32_t ipv4_cluster_mask;
+    uint8_t router_ip6[16];
+} cfc_node_config;
+int cfc_set_node_config(cfc_ctx *ctx, const cfc_node_config *cfg);
+int cfc_get_node_config(cfc_ctx *ctx, cfc_node_config *cfg);
+
 /* Flatten the host tables into device layouts and publish them as the new
  * epoch.  Enqueued on `stream` (hipStream_t, NULL = default stream). */
 int cfc_commit(cfc_ctx *ctx, void *stream);
@@ -142,7 +162,9 @@ int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
  * pointers with n elements.  `ports` is the first 32-bit word of the L4
  * header exactly as ct_lookup4 loads it (sport be16 in bits 0-15, dport be16
  * in bits 16-31; for ICMP: type | code << 8 | csum << 16).  `meta` packs
- * proto (bits 0-7), CFC_HF_* flags (bits 8-15) and skb->len (bits 16-31).
+ * proto (bits 0-7), CFC_HF_* flags (bits 8-15) and skb->len (bits 16-31):
+ * the batch format carries packets of at most 65535 bytes; a larger (GSO)
+ * skb cannot be expressed and must be classified on the slow path.
  * `mark` (skb->mark, FROM_HOST identity) may be NULL = 0. */
 typedef struct {
     const uint32_t *saddr;
@@ -277,7 +299,8 @@ typedef struct {
 } cfc_drop_notify;
 
 /* The drop notifications of one classified batch (in: the headers, out: its
- * outputs with out->notify set), in header order, into device memory:
+ * outputs with out->notify set), in header order, into device memory
+ * (`records` 16-byte aligned, else -EINVAL):
  * records[0 .. min(total, cap)) and, if hdr_index != NULL, the header index
  * of each.  *count (device u64) receives the total; drops past cap are not
  * recorded (a full perf ring loses samples the same way).  mode and ep_lxc
@@ -292,14 +315,18 @@ int cfc_drop_notify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
                        void *stream);
 
 /* ---------------------------------------------------------------- counters */
-/* The device counter block is a flat u64 array: 2 u64 (packets, bytes) per
- * policy entry in the committed epoch's entry order, then 256 reasons x 4
- * directions x 2 u64 for cilium_metrics.  It is identical in layout on
- * every rank holding the same tables, so it can be all-reduced in place
- * (RCCL) before cfc_counters_sync(). */
+/* The device counter block is a flat u64 array:
+ *   [n_entries][packets, bytes]   policy entries, in the committed epoch's
+ *                                 entry order (policy_entry counters);
+ *   [256 reasons][4 dirs][count, bytes]   cilium_metrics (update_metrics);
+ *   [2 dirs][65537 identities][fwd, drop][packets, bytes]   the
+ *                                 per-identity forward/drop counters below.
+ * It is identical in layout on every rank holding the same tables, so it
+ * can be all-reduced in place (RCCL) before cfc_counters_sync(). */
 int cfc_counters_device(cfc_ctx *ctx, uint64_t **dev_ptr, uint64_t *n_u64);
 /* Fold the device counters into the host maps (policy entry packets/bytes,
- * cilium_metrics) and zero them.  Synchronises `stream`. */
+ * cilium_metrics, the per-identity totals) and zero them.  Synchronises
+ * `stream`. */
 int cfc_counters_sync(cfc_ctx *ctx, void *stream);
 /* Zero the device counters without folding (e.g. on non-root ranks after
  * an all-reduce whose result was folded elsewhere). */
@@ -311,6 +338,34 @@ int cfc_counters_export(cfc_ctx *ctx, uint64_t *dst, uint64_t n_u64,
                         void *stream);
 int cfc_counters_import(cfc_ctx *ctx, const uint64_t *src, uint64_t n_u64,
                         void *stream);
+
+/* Per-identity forward/drop counters (BASELINE north_star: the counters the
+ * multi-GPU path all-reduces over RCCL).  One event per policy verdict the
+ * datapath makes — every __policy_can_access the reference runs
+ * (policy.h:46-110) through ipv{4,6}_policy (bpf_lxc.c:753-1028, dir
+ * ingress, identity = the source identity) or handle_ipv4_from_lxc /
+ * ipv6_l3_from_lxc (:112-704, dir egress, identity = the destination
+ * identity); after egress local delivery the destination's ingress verdict
+ * is a second event (identity = the sender's SECLABEL).  The event is a
+ * drop when the verdict path drops it (DROP_POLICY: a denied verdict not
+ * overridden by CT_REPLY/CT_RELATED), a forward otherwise (including proxy
+ * redirects).  Packets and skb->len bytes.  Identities >= 65536 (outside
+ * pkg/identity's allocation range, numericidentity.go) are counted in one
+ * row with identity CFC_IDENTITY_OUT_OF_RANGE.
+ * cfc_identity_counters returns the totals folded by cfc_counters_sync
+ * (since the context was opened), one row per (identity, dir) with a
+ * non-zero count, sorted by identity then dir: rows[0 .. min(*n, cap)),
+ * *n = the number of rows. */
+#define CFC_IDENTITY_OUT_OF_RANGE 0xFFFFFFFFu
+typedef struct {
+    uint32_t identity;
+    uint8_t dir;          /* METRIC_INGRESS 1 / METRIC_EGRESS 2 */
+    uint8_t pad[3];
+    uint64_t fwd_packets, fwd_bytes;
+    uint64_t drop_packets, drop_bytes;
+} cfc_identity_count;
+int cfc_identity_counters(cfc_ctx *ctx, cfc_identity_count *rows, uint64_t cap,
+                          uint64_t *n);
 
 /* ------------------------------------------------------------- diagnostics */
 typedef struct {

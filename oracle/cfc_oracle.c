@@ -19,8 +19,6 @@
 #define WORLD_ID 2u
 #define CLUSTER_ID 3u
 #define HEALTH_ID 4u
-#define IPV4_CLUSTER_MASK 0xff0000u
-#define IPV4_CLUSTER_RANGE 0x100000u
 /* bpf/lib/common.h:237-269 */
 #define DROP_INVALID_SIP -132
 #define DROP_POLICY -133
@@ -338,7 +336,16 @@ struct cfo {
     uint32_t ct_n, ct_cap, ct_added;
     uint32_t *notify_out; /* cfo_set_notify_out */
     uint8_t ct_local[65536];   /* endpoint has its own (local) CT maps */
+    /* node_config.h constants the agent writes per node (daemon.go:916-934):
+     * IPV4_CLUSTER_RANGE / _MASK (raw be32 as loaded), ROUTER_IP */
+    uint32_t v4_cluster_range, v4_cluster_mask;
+    uint8_t router_ip6[16];
+    /* per-identity forward/drop counters (cfc.h cfc_identity_counters):
+     * [dir 0 ingress / 1 egress][identity, >= 65536 in the last slot]
+     * [fwd, drop][packets, bytes] */
+    uint64_t *idc;
 };
+#define ID_SLOTS 65537u
 
 static uint16_t ct_owner(const cfo_t *o, uint16_t lxc)
 {
@@ -365,7 +372,20 @@ cfo_t *cfo_new(void)
     ht_init(&o->pf4_fix, 8);
     ht_init(&o->pf6_fix, 20);
     ht_init(&o->ct, CTK);
+    o->idc = calloc((size_t)2 * ID_SLOTS * 4, sizeof(uint64_t));
+    /* bpf/node_config.h:30,42-43 */
+    static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0,
+                                       0, 0, 0, 1, 0, 1, 0, 0};
+    cfo_node_config(o, 0x100000u, 0xff0000u, router);
     return o;
+}
+
+void cfo_node_config(cfo_t *o, uint32_t v4_cluster_range,
+                     uint32_t v4_cluster_mask, const uint8_t router_ip6[16])
+{
+    o->v4_cluster_range = v4_cluster_range;
+    o->v4_cluster_mask = v4_cluster_mask;
+    memcpy(o->router_ip6, router_ip6, 16);
 }
 
 void cfo_free(cfo_t *o)
@@ -382,6 +402,7 @@ void cfo_free(cfo_t *o)
     ht_free(&o->ct);
     free(o->ct_ents);
     free(o->ct_live);
+    free(o->idc);
     for (int i = 0; i < 65536; i++)
         if (o->pol[i]) {
             ht_free(&o->pol[i]->idx);
@@ -495,6 +516,19 @@ static void metric(cfo_t *o, int reason, int dir, uint32_t len)
     uint8_t r = (uint8_t)(-reason);
     add64(&o->metrics[r][dir][0], 1);
     add64(&o->metrics[r][dir][1], len);
+}
+
+/* one policy verdict (a __policy_can_access call, policy.h:46-110) of
+ * identity `ident` in direction dir (0 ingress: ipv{4,6}_policy's source
+ * identity; 1 egress: handle_ipv4_from_lxc's destination identity): a drop
+ * when the verdict path drops the packet for it (DROP_POLICY), else a
+ * forward */
+static void id_event(cfo_t *o, int dir, uint32_t ident, int drop, uint32_t len)
+{
+    uint32_t s = ident < ID_SLOTS - 1 ? ident : ID_SLOTS - 1;
+    uint64_t *p = o->idc + (((size_t)dir * ID_SLOTS + s) * 2 + (drop ? 1 : 0)) * 2;
+    add64(p, 1);
+    add64(p + 1, len);
 }
 
 static const epinfo *lxc_lookup(const cfo_t *o, int family,
@@ -655,6 +689,7 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     }
     int verdict = policy_can_access(o->pol[ep->lxc_id], src, pdport, proto,
                                     CT_INGRESS, frag, len);
+    id_event(o, 0, src, res != CT_REPLY && res != CT_RELATED && verdict < 0, len);
     /* replies and related packets skip the policy verdict (:963-970); a
      * denied CT_ESTABLISHED flow loses its entry (ct_delete4) */
     if (res != CT_REPLY && res != CT_RELATED && verdict < 0) {
@@ -742,13 +777,14 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     tl_lookups++;
     if (lpm_lookup(&o->ipc4, da, &label) && label)
         dst = label;
-    else if ((daddr & IPV4_CLUSTER_MASK) == IPV4_CLUSTER_RANGE)
+    else if ((daddr & o->v4_cluster_mask) == o->v4_cluster_range)
         dst = CLUSTER_ID;
     else
         dst = WORLD_ID;
     r.identity = dst;
     int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
                                     CT_EGRESS, 0, len);
+    id_event(o, 1, dst, res != CT_REPLY && res != CT_RELATED && verdict < 0, len);
     if (res != CT_REPLY && res != CT_RELATED && verdict < 0) { /* :538-545 */
         r.verdict = DROP_POLICY;
         metric(o, DROP_POLICY, METRIC_EGRESS, len);
@@ -861,9 +897,6 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
 #define NEXTHDR_NONE 59
 #define HF_EXTHDR 4
 #define VERDICT_PUNT -2
-/* node_config.h:30 ROUTER_IP */
-static const uint8_t ROUTER_IP6[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0,
-                                       0, 0, 0, 1, 0, 1, 0, 0};
 
 /* ipv6_hdrlen (ipv6.h:61-98): the header's proto is the next header the
  * extension-header walk stops at; NONE and FRAGMENT end in a drop. */
@@ -877,13 +910,13 @@ static int exthdr_drop(uint8_t proto)
  * requests to the router itself; those headers are reported as punted.  It
  * reads the type right after the fixed header, so behind extension headers
  * it sees the next-header byte and never triggers. */
-static int icmp6_punt(uint8_t proto, uint8_t flags, uint16_t sport,
-                      const uint8_t *daddr)
+static int icmp6_punt(const cfo_t *o, uint8_t proto, uint8_t flags,
+                      uint16_t sport, const uint8_t *daddr)
 {
     if (proto != IPPROTO_ICMPV6 || (flags & HF_EXTHDR))
         return 0;
     uint8_t type = (uint8_t)(sport & 0xFF);
-    return type == 135 || (type == 128 && !memcmp(daddr, ROUTER_IP6, 16));
+    return type == 135 || (type == 128 && !memcmp(daddr, o->router_ip6, 16));
 }
 
 /* from_netdev (FROM_HOST) -> handle_ipv6 (bpf_netdev.c:172-275, 494-503) */
@@ -901,7 +934,7 @@ static res_t netdev_ingress_v6(cfo_t *o, const uint8_t *saddr,
         metric(o, ret, METRIC_INGRESS, len);
         return r;
     }
-    if (icmp6_punt(proto, flags, sport, daddr)) {
+    if (icmp6_punt(o, proto, flags, sport, daddr)) {
         r.action = TC_ACT_OK;
         r.verdict = VERDICT_PUNT;
         return r;
@@ -929,7 +962,7 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
                            uint16_t dport, uint8_t flags, uint32_t len)
 {
     res_t r = {TC_ACT_SHOT, 0, 0, 0};
-    if (icmp6_punt(proto, flags, sport, daddr)) { /* :411-419 */
+    if (icmp6_punt(o, proto, flags, sport, daddr)) { /* :411-419 */
         r.action = TC_ACT_OK;
         r.verdict = VERDICT_PUNT;
         return r;
@@ -956,13 +989,14 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
     tl_lookups++;
     if (lpm_lookup(&o->ipc6, daddr, &label) && label)
         dst = label;
-    else if (!memcmp(daddr, ROUTER_IP6, 8)) /* ipv6_match_prefix_64 */
+    else if (!memcmp(daddr, o->router_ip6, 8)) /* ipv6_match_prefix_64 */
         dst = CLUSTER_ID;
     else
         dst = WORLD_ID;
     r.identity = dst;
     int verdict = policy_can_access(o->pol[lxc], dst, pdport, proto,
                                     CT_EGRESS, 0, len);
+    id_event(o, 1, dst, res != CT_REPLY && res != CT_RELATED && verdict < 0, len);
     if (res != CT_REPLY && res != CT_RELATED && verdict < 0) { /* :228-235 */
         r.verdict = DROP_POLICY;
         metric(o, DROP_POLICY, METRIC_EGRESS, len);
@@ -1124,8 +1158,28 @@ size_t cfo_metrics_dump(cfo_t *o, uint64_t *rows, size_t cap)
     return n;
 }
 
+size_t cfo_identity_dump(cfo_t *o, uint64_t *rows, size_t cap)
+{
+    size_t n = 0;
+    for (uint32_t id = 0; id < ID_SLOTS; id++)
+        for (uint32_t dir = 0; dir < 2; dir++) {
+            const uint64_t *v = o->idc + ((size_t)dir * ID_SLOTS + id) * 4;
+            if (!(v[0] | v[1] | v[2] | v[3]))
+                continue;
+            if (rows && n < cap) {
+                uint64_t *r = rows + 6 * n;
+                r[0] = id == ID_SLOTS - 1 ? 0xFFFFFFFFu : id;
+                r[1] = dir + 1;
+                memcpy(r + 2, v, 32);
+            }
+            n++;
+        }
+    return n;
+}
+
 void cfo_counters_reset(cfo_t *o)
 {
+    memset(o->idc, 0, (size_t)2 * ID_SLOTS * 4 * sizeof(uint64_t));
     memset(o->metrics, 0, sizeof(o->metrics));
     for (int i = 0; i < 65536; i++)
         if (o->pol[i])

@@ -36,6 +36,14 @@ int cfo_ipcache_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
 int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
                      uint32_t ifindex, uint16_t lxc_id, uint32_t flags);
 int cfo_seclabel_set(cfo_t *o, uint16_t lxc_id, uint32_t seclabel);
+/* node_config.h IPV4_CLUSTER_RANGE / IPV4_CLUSTER_MASK (raw be32 as loaded)
+ * and ROUTER_IP; cfo_new() starts with the reference's values */
+/* per-identity forward/drop counters: rows of 6 u64 {identity (0xFFFFFFFF
+ * for >= 65536), dir (1 ingress / 2 egress), fwd packets, fwd bytes, drop
+ * packets, drop bytes}, sorted; returns the row count */
+size_t cfo_identity_dump(cfo_t *o, uint64_t *rows, size_t cap);
+void cfo_node_config(cfo_t *o, uint32_t v4_cluster_range,
+                     uint32_t v4_cluster_mask, const uint8_t router_ip6[16]);
 /* An endpoint program (and its policymap) exists for lxc_id.  Endpoints in
  * cilium_lxc without one drop with DROP_MISSED_TAIL_CALL. */
 int cfo_policy_create(cfo_t *o, uint16_t lxc_id);

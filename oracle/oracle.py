@@ -102,7 +102,11 @@ def lib():
         L.cfo_metrics_dump.restype = ctypes.c_size_t
         L.cfo_metrics_dump.argtypes = [vp, vp, ctypes.c_size_t]
         L.cfo_counters_reset.argtypes = [vp]
+        L.cfo_identity_dump.restype = ctypes.c_size_t
+        L.cfo_identity_dump.argtypes = [vp, vp, ctypes.c_size_t]
         L.cfo_set_notify_out.argtypes = [vp, vp]
+        L.cfo_node_config.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p]
+        L.cfo_node_config.restype = None
         _lib = L
     return _lib
 
@@ -155,6 +159,15 @@ class Oracle:
                                 int(p["dyn"]))
         if getattr(t, "ct", None) is not None:
             self.ct_add(t.ct)
+        if getattr(t, "node", None) is not None:
+            self.node_config(*t.node)
+
+    def node_config(self, v4_cluster_range, v4_cluster_mask, router_ip6):
+        """node_config.h IPV4_CLUSTER_RANGE / _MASK (raw be32 as loaded) and
+        ROUTER_IP (16 bytes)."""
+        p, keep = _u8p(np.asarray(router_ip6, np.uint8).reshape(16))
+        self.L.cfo_node_config(self.h, int(v4_cluster_range) & 0xFFFFFFFF,
+                               int(v4_cluster_mask) & 0xFFFFFFFF, p)
 
     def ct_add(self, ct):
         rec = np.ascontiguousarray(ct)
@@ -270,6 +283,14 @@ class Oracle:
         n = self.L.cfo_metrics_dump(self.h, None, 0)
         rows = np.zeros((n, 4), np.uint64)
         self.L.cfo_metrics_dump(self.h, _p(rows), n)
+        return rows
+
+    def identity_counters(self):
+        """(n, 6) u64 rows {identity, dir, fwd packets, fwd bytes, drop
+        packets, drop bytes} (cfc.h cfc_identity_counters), sorted."""
+        n = self.L.cfo_identity_dump(self.h, None, 0)
+        rows = np.zeros((n, 6), np.uint64)
+        self.L.cfo_identity_dump(self.h, _p(rows), n)
         return rows
 
     def reset_counters(self):

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(_lib.EXPORTS) == fns
-    assert L.cfc_abi_version() == 5
+    assert L.cfc_abi_version() == 6
     assert L.cfc_num_possible_cpus() == 1
 
 
@@ -51,6 +51,17 @@ def test_options_on_host_only_context():
     assert errno_of(lambda: dp.set_option(99, 0)) == errno.EINVAL
     assert errno_of(lambda: dp.set_option(_lib.OPT_TIMING, 1)) == errno.ENODEV
     assert errno_of(dp.timing_collect) == errno.ENODEV
+
+
+def test_node_config_on_host_only_context():
+    """cfc_set/get_node_config: starts at bpf/node_config.h's values
+    (IPV4_CLUSTER_RANGE 0x100000, MASK 0xff0000, ROUTER_IP beef::1:0:1:0:0)."""
+    dp = C.host_only()
+    rng, mask, router = dp.node_config()
+    assert (rng, mask) == (0x100000, 0xFF0000)
+    assert router == bytes([0xbe, 0xef] + [0] * 9 + [1, 0, 1, 0, 0])
+    dp.set_node_config(0x0A, 0xFF, bytes(range(16)))
+    assert dp.node_config() == (0x0A, 0xFF, bytes(range(16)))
 
 
 def errno_of(fn):

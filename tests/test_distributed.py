@@ -1,9 +1,11 @@
 """Multi-rank path on CPU (gloo, world_size 2): the header stream is sharded
 contiguously, every rank classifies its shard against replicated tables, and
-the u64 counter blocks are SUM-all-reduced (cilium_amd/distributed.py,
-SURVEY.md §8e).  The oracle stands in for each rank's engine here; the GPU
-side of the same exchange (cfc_counters_export/import) runs in
-tests/test_gpu_parity.py and bench.py --gpus N."""
+the u64 counter blocks — policy entries and the per-identity forward/drop
+counters — are SUM-all-reduced (cilium_amd/distributed.py).
+No GPU here, so the oracle stands in for each rank's engine; the engine's
+side of the exchange (cfc_counters_export -> sum -> cfc_counters_import ->
+cfc_counters_sync) is tests/test_gpu_distributed.py, and bench.py --gpus N
+runs it over RCCL."""
 import os
 import socket
 
@@ -34,6 +36,16 @@ def test_shard_range_partitions_the_stream():
             assert max(sizes) - min(sizes) <= 1
 
 
+def identity_block(rows):
+    """cfc_identity_counters rows -> the device block's identity part
+    ([dir][65537][fwd, drop][packets, bytes], include/cfc.h)"""
+    blk = np.zeros((2, 65537, 4), np.uint64)
+    for r in rows:
+        ident = 65536 if int(r[0]) == 0xFFFFFFFF else int(r[0])
+        blk[int(r[1]) - 1, ident] = r[2:6]
+    return blk.reshape(-1)
+
+
 def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
@@ -55,7 +67,8 @@ def _worker(rank, world, port, q):
         gathered = None if grec is None else (grec.numpy().copy(), gidx.numpy().copy())
         lxc = sorted(t.policy)[0]
         pc = o.policy_counters(lxc)             # rows: ..., packets, bytes
-        blk = np.concatenate([pc[:, 5], pc[:, 6]]).astype(np.uint64)
+        blk = np.concatenate([pc[:, 5], pc[:, 6],
+                              identity_block(o.identity_counters())]).astype(np.uint64)
         # u64 counters travel as int64 (two's complement == mod 2^64)
         tb = torch.from_numpy(blk.view(np.int64).copy())
         allreduce_block(tb)
@@ -92,7 +105,10 @@ def test_two_rank_shards_and_counter_allreduce():
     np.testing.assert_array_equal(np.concatenate([r[2] for r in res]), ide)
     # the all-reduced counter block equals the single-rank totals
     pc = o.policy_counters(sorted(t.policy)[0])
-    want = np.concatenate([pc[:, 5], pc[:, 6]]).astype(np.uint64)
+    idrows = o.identity_counters()
+    assert idrows[:, 2].sum() > 0 and idrows[:, 4].sum() > 0
+    want = np.concatenate([pc[:, 5], pc[:, 6],
+                           identity_block(idrows)]).astype(np.uint64)
     for r in res:
         np.testing.assert_array_equal(r[3], want)
         assert r[4] == 0

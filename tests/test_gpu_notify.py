@@ -135,29 +135,55 @@ def test_cap_and_empty(torch):
 
 
 def test_two_streams(torch):
-    """Back-to-back calls on two streams share the notify workspace: each
-    waits for the other's kernels, so both batches' records are right."""
-    g1, g2 = G.Golden("c2_ingress_v4"), G.Golden("small_ingress_v4")
-    res = []
-    for g in (g1, g2):
-        dp = Datapath(0)
-        load_tables(dp, g.tables)
-        b = pack(g.headers)
-        out = dp.classify(b, g.mode, g.ep_lxc, want_notify=True)
-        torch.cuda.synchronize()
-        res.append((dp, b, out, g))
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    dp, b, out, g = res[0]
-    # same context twice: a large batch on s1, then a small one on s2
-    big = dp.drop_notify(b, out, g.mode, g.ep_lxc, stream=s1)
+    """Back-to-back calls on two streams share the notify workspace: the
+    second waits for the first's kernels (hipStreamWaitEvent on the
+    library's event), with no host synchronisation between them."""
+    g = G.Golden("c2_ingress_v4")
+    dp = Datapath(0)
+    load_tables(dp, g.tables)
+    b = pack(g.headers)
+    out = dp.classify(b, g.mode, g.ep_lxc, want_notify=True)
     small_b = type(b)(b.saddr[:5000], b.daddr[:5000], b.ports[:5000],
                       b.meta[:5000], b.mark[:5000] if b.mark is not None else None)
-    small_out = dp.classify(small_b, g.mode, g.ep_lxc, want_notify=True, stream=s2)
-    small = dp.drop_notify(small_b, small_out, g.mode, g.ep_lxc, stream=s2)
+    small_out = dp.classify(small_b, g.mode, g.ep_lxc, want_notify=True)
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    # a large batch on s1, then a small one on s2, neither waited for
+    big = dp.drop_notify(b, out, g.mode, g.ep_lxc, stream=s1, sync=False)
+    small = dp.drop_notify(small_b, small_out, g.mode, g.ep_lxc, stream=s2,
+                           sync=False)
     torch.cuda.synchronize()
     nt, rec, idx = oracle_notify(g.tables, g.headers, g.mode)
-    assert big[2] == len(rec)
-    np.testing.assert_array_equal(big[1].cpu().numpy().astype(np.uint64), idx)
-    assert small[2] == int((nt[:5000] != 0).sum())
-    for r in res:
-        r[0].close()
+    nb = int(big[2].item())
+    assert nb == len(rec)
+    np.testing.assert_array_equal(big[1][:nb].cpu().numpy().astype(np.uint64), idx)
+    np.testing.assert_array_equal(
+        np.ascontiguousarray(big[0][:nb].cpu().numpy()).view(np.uint8).reshape(-1),
+        rec.view(np.uint8))
+    ns = int(small[2].item())
+    k = int((idx < 5000).sum())
+    assert ns == k
+    np.testing.assert_array_equal(small[1][:ns].cpu().numpy().astype(np.uint64), idx[:k])
+    np.testing.assert_array_equal(
+        np.ascontiguousarray(small[0][:ns].cpu().numpy()).view(np.uint8).reshape(-1),
+        rec[:k].view(np.uint8))
+    dp.close()
+
+
+def test_records_use_the_classified_epoch(torch):
+    """An endpoint's SECLABEL changed between classify and drop_notify: the
+    records carry the labels the batch was classified with (the epoch's
+    snapshot), not the new ones."""
+    g = G.Golden("c2_egress_v4")
+    dp = Datapath(0)
+    load_tables(dp, g.tables)
+    b = pack(g.headers)
+    out = dp.classify(b, g.mode, g.ep_lxc, want_notify=True)
+    dp.endpoint_config(g.ep_lxc, 0xABCDE)
+    rec, idx, total = dp.drop_notify(b, out, g.mode, g.ep_lxc)
+    nt, orec, oidx = oracle_notify(g.tables, g.headers, g.mode, g.ep_lxc)
+    assert total == len(orec) > 0
+    np.testing.assert_array_equal(
+        np.ascontiguousarray(rec.cpu().numpy()).view(np.uint8).reshape(-1),
+        orec.view(np.uint8))
+    dp.close()

@@ -58,6 +58,7 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
                 for lxc, pm in pms.items()}
     metrics = np.array(metricsmap.dump_rows(dp), np.uint64).reshape(-1, 4)
     run_gpu.ct = (ctb, ct_rows(dp, dp.ct_fds)) if use_ct else None
+    run_gpu.identity = dp.identity_counters()
     dp.close()
     return act, ver, ide, counters, metrics
 
@@ -82,6 +83,7 @@ def test_golden(torch, name, layout):
     np.testing.assert_array_equal(act, oa)
     np.testing.assert_array_equal(ver, ov)
     np.testing.assert_array_equal(ide, oi)
+    np.testing.assert_array_equal(run_gpu.identity, o.identity_counters())
     if use_ct:
         # CT byte per header, and the CT maps afterwards: against the
         # reference (clock-derived fields masked) and, every byte, the oracle
@@ -128,6 +130,7 @@ def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO)
     for lxc in t.policy:
         np.testing.assert_array_equal(counters[lxc], o.policy_counters(lxc))
     np.testing.assert_array_equal(metrics, o.metrics())
+    np.testing.assert_array_equal(run_gpu.identity, o.identity_counters())
     return act, ver
 
 
@@ -387,3 +390,40 @@ def test_c5_egress_and_local_ct(torch):
     h = S.concat([g.headers] * 3)
     h = S.take(h, rng.permutation(len(h)))
     compare_with_oracle(torch, t, h, 1, ep_lxc=S.EP_LXC_ID, chunks=2)
+
+
+def test_node_config_runtime(torch):
+    """cfc_set_node_config: IPV4_CLUSTER_RANGE/MASK and ROUTER_IP other than
+    the compiled-in node_config.h values (daemon/daemon.go:916-934) change
+    the egress CLUSTER_ID fallback and the ICMPv6 router punt exactly as
+    the oracle configured the same way."""
+    rng = np.random.default_rng(41)
+    # IPv4: cluster 10.0.0.0/8 (raw be32 0x0a, mask 0xff)
+    t = S.config_c2(41, n_prefixes=20_000, n_policy=4000, n_endpoints=2)
+    t.node = (0x0000000A, 0x000000FF, S.ip6("fd00:1:2:3::1"))
+    h = S.gen_headers_v4(rng, 300_000, t.ipcache, S.local_v4_addrs(t),
+                         local_frac=0.1, src_fixed=S.LXC_IPV4)
+    cl = rng.random(len(h)) < 0.3
+    h.daddr[cl] = (h.daddr[cl] & np.uint32(0xFFFFFF00)) | np.uint32(0x0A)
+    act, ver = compare_with_oracle(torch, t, h, 1, ep_lxc=S.EP_LXC_ID)
+    # IPv6: destinations inside the configured router /64, echo requests to it
+    t6 = S.config_c3(42, n_prefixes=20_000, n_v4_prefixes=100, n_policy=2000,
+                     n_endpoints=2, n_prefilter=0)
+    router = S.ip6("fd00:1:2:3::1")
+    t6.node = (0x0000000A, 0x000000FF, router)
+    ipc6 = t6.ipcache[t6.ipcache["family"] == 2]
+    h6 = S.gen_headers_v6(rng, 300_000, ipc6, S.local_v6_addrs(t6), local_frac=0.1,
+                          src_fixed=S.LXC_IPV6, mark_host=0, mark_proxy=0)
+    sel = rng.random(len(h6)) < 0.3
+    h6.daddr[sel, :8] = router[:8]
+    k = np.arange(0, len(h6), 101)
+    h6.proto[k] = 58
+    h6.sport[k] = 128
+    h6.daddr[k] = router
+    h6.flags[k] = 0
+    for mode, ep in ((1, S.EP_LXC_ID), (0, 0)):
+        compare_with_oracle(torch, t6, h6, mode, ep_lxc=ep)
+    o = O.Oracle(t6)
+    _, ov, oi = o.classify(h6, 1, S.EP_LXC_ID)
+    assert (ov == L.VERDICT_PUNT).sum() >= len(k) // 2
+    assert (oi == S.CLUSTER_ID).sum() > 1000

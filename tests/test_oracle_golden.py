@@ -99,3 +99,61 @@ def test_oracle_drop_notify_matches_reference(name):
     if len(rec) and g.mode != O.MODE_XDP:
         # records from both an endpoint program and (where present) netdev
         assert (rec["source"] != 0).any(), name
+
+
+def test_oracle_node_config():
+    """cfo_node_config: the reference's own values reproduce the golden
+    (pinned above); another IPV4_CLUSTER_RANGE/MASK moves exactly the egress
+    destinations inside it to CLUSTER_ID (bpf_lxc.c:521-529) and leaves every
+    other output unchanged."""
+    g = G.Golden("c2_egress_v4")
+    o = O.Oracle(g.tables)
+    o.node_config(0x100000, 0xFF0000, S.ROUTER_IPV6)
+    a0, v0, i0 = o.classify(g.headers, g.mode, g.ep_lxc)
+    assert len(G.mismatches(g, a0, v0, i0)) == 0
+    o = O.Oracle(g.tables)
+    o.node_config(0x0000000A, 0x000000FF, S.ROUTER_IPV6)
+    a1, v1, i1 = o.classify(g.headers, g.mode, g.ep_lxc)
+    d = np.asarray(g.headers.daddr, np.uint32)
+    in_old = (d & 0xFF0000) == 0x100000
+    in_new = (d & 0xFF) == 0x0A
+    changed = i0 != i1
+    assert changed.any()
+    assert not (changed & ~(in_old | in_new)).any()
+    assert (i1[changed & in_new] == S.CLUSTER_ID).all()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_identity_counters_consistent(name):
+    """The per-identity forward/drop counters (cfc.h cfc_identity_counters)
+    against what the reference's own outputs in the fixture imply: every
+    DROP_POLICY of the batch's direction is one drop event, and (without
+    conntrack) every forwarded ingress header that reached the endpoint's
+    policy is a forward event — TRACE_TO_LXC's update_metrics(FORWARDED,
+    INGRESS) plus the proxy redirects (bpf_lxc.c:985-1008)."""
+    g = G.Golden(name)
+    o = O.Oracle(g.tables)
+    act, ver, ide = o.classify(g.headers, g.mode, g.ep_lxc,
+                               apply_ct=g.ct_after is not None)
+    rows = o.identity_counters()
+    if g.mode == O.MODE_XDP:
+        assert len(rows) == 0
+        return
+    met = {(int(r[0]), int(r[1])): int(r[2]) for r in g.metrics}
+    drops = {d: int(rows[rows[:, 1] == d][:, 4].sum()) for d in (1, 2)}
+    fwd = {d: int(rows[rows[:, 1] == d][:, 2].sum()) for d in (1, 2)}
+    if g.mode == O.MODE_EGRESS:
+        assert drops[2] == met.get((133, 2), 0)
+        assert drops[1] == met.get((133, 1), 0)
+    else:
+        assert drops[1] == met.get((133, 1), 0)
+        assert drops[2] == fwd[2] == 0
+        if g.ct_after is None:
+            redirects = int(((act == 7) & (ver > 0)).sum())
+            assert fwd[1] == met.get((0, 1), 0) + redirects
+    # identities are the verdict's: every drop row's identity dropped a header
+    v = np.asarray(ver)
+    dropped = set(int(x) for x in np.asarray(ide)[v == -133])
+    for r in rows[rows[:, 4] > 0]:
+        if g.mode != O.MODE_EGRESS or r[1] == 2:
+            assert int(r[0]) in dropped or int(r[0]) == 0xFFFFFFFF
