@@ -43,8 +43,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--seed", type=int, default=2)
     ap.add_argument("--notify", action="store_true",
-                    help="also produce every dropped header's drop_notify record "
-                         "(cfc_drop_notify_v4) inside the timed step")
+                    help="also produce every monitor record — drop_notify and "
+                         "trace_notify (cfc_monitor_events_v4) — inside the timed step")
     ap.add_argument("--lpm4", default="auto", choices=["auto", "dir24_8", "trie"],
                     help="IPv4 ipcache device layout (cfc_set_option CFC_OPT_LPM4)")
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"],
@@ -113,13 +113,15 @@ def main():
     elif args.workload == "c5":
         from cilium_amd.datapath import pack_v4
         hb = pack_v4(S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank), dev)
-        s, d, p, m = hb.saddr, hb.daddr, hb.ports, hb.meta
+        s, d, p, m, tf = hb.saddr, hb.daddr, hb.ports, hb.meta, hb.tcp_flags
         del hb
     else:
         s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
     if mode == 1:
         s.fill_(S.LXC_IPV4 - (1 << 32) if S.LXC_IPV4 >= 1 << 31 else S.LXC_IPV4)
-    batch = HeaderBatchV4(s, d, p, m, None)
+    if args.workload != "c5":
+        tf = None    # no TCP flag bytes in the C2/C3 streams (all CT_NEW)
+    batch = HeaderBatchV4(s, d, p, m, None, tf)
     out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
                    torch.empty(n, dtype=torch.int32, device=dev), None)
     n6 = len(batch6) if batch6 is not None else 0
@@ -134,19 +136,18 @@ def main():
         nt_rec = torch.empty((n, 8), dtype=torch.int32, device=dev)
         nt_idx = torch.empty(n, dtype=torch.int64, device=dev)
         nt_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-        nt_hdr = LL.HdrV4(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
-                          _ptr(batch.meta), None, n)
-        nt_out = LL.Out(_ptr(out.verdict), _ptr(out.identity), None, None,
-                        _ptr(out.notify))
+        from cilium_amd.datapath import hdr_struct, out_struct
+        nt_hdr = hdr_struct(batch)
+        nt_out = out_struct(out)
         nt_stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def step():
         dp.classify_v4(batch, mode, ep_lxc, out=out)
         if args.notify:   # records stay on the device (no sync in the step)
-            LL.check(dp.L.cfc_drop_notify_v4(
+            LL.check(dp.L.cfc_monitor_events_v4(
                 dp.h, ctypes.byref(nt_hdr), ctypes.byref(nt_out), mode, ep_lxc,
                 _ptr(nt_rec), _ptr(nt_idx), n, _ptr(nt_cnt), nt_stream),
-                "drop notify")
+                "monitor events")
         if n6:
             dp.classify_v6(batch6, mode, ep_lxc, out=out6)
     torch.cuda.synchronize()
@@ -207,6 +208,8 @@ def main():
     samp = min(samp, n)
     hs = S.unpack_v4(s[:samp].cpu().numpy(), d[:samp].cpu().numpy(),
                      p[:samp].cpu().numpy(), m[:samp].cpu().numpy())
+    hs.tcpflags = (tf[:samp].cpu().numpy() if tf is not None
+                   else np.zeros(samp, np.uint8))
     orc = O.Oracle(tables)
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
     c0 = time.perf_counter()
@@ -216,6 +219,16 @@ def main():
     # the timed region's last launch wrote `out` for this same batch
     parity = bool(np.array_equal(out.verdict[:samp].cpu().numpy(), ov) and
                   np.array_equal(out.identity[:samp].cpu().numpy().view(np.uint32), oi))
+    if args.notify:   # the sample's monitor records, every field
+        _, ov2, oi2, ow = orc.classify(hs, mode, ep_lxc, nthreads=cores,
+                                       want_notify=True)
+        orec, oidx = orc.events(hs, mode, ep_lxc, ov2, oi2, ow)
+        k = len(oidx)
+        grec = nt_rec[:k].cpu().numpy()
+        gidx = nt_idx[:k].cpu().numpy().astype(np.uint64)
+        parity = parity and bool(np.array_equal(gidx, oidx) and np.array_equal(
+            np.ascontiguousarray(grec).view(np.uint8).reshape(-1),
+            np.ascontiguousarray(orec).view(np.uint8).reshape(-1)))
     mean_l = float(lk.mean())
     b_hdr = S_IN + S_OUT + 64.0 * mean_l
     algo_bytes = n * b_hdr
@@ -306,7 +319,7 @@ def main():
                       f"restatement (oracle/cfc_oracle.c), {cores} OpenMP threads",
         },
         "parity_sample_ok": parity,
-        "drop_records_per_step_per_gpu": int(nt_cnt.item()) if args.notify else None,
+        "monitor_records_per_step_per_gpu": int(nt_cnt.item()) if args.notify else None,
     }
     print(json.dumps(res), flush=True)
     if world > 1:

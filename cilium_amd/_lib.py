@@ -29,6 +29,7 @@ EXPORTS = (
     "cfc_set_option", "cfc_timing_collect", "cfc_classify_v6",
     "cfc_ct_apply_v4", "cfc_ct_apply_v6", "cfc_map_update_batch",
     "cfc_set_node_config", "cfc_get_node_config", "cfc_identity_counters",
+    "cfc_set_clock", "cfc_monitor_events_v4", "cfc_monitor_events_v6",
 )
 # CT byte (cfc_out.ct): per stage (bits 0-3, then 4-7 for the destination's
 # ingress lookup after egress local delivery)
@@ -43,7 +44,8 @@ class CfcError(OSError):
 class HdrV4(ctypes.Structure):
     _fields_ = [("saddr", ctypes.c_void_p), ("daddr", ctypes.c_void_p),
                 ("ports", ctypes.c_void_p), ("meta", ctypes.c_void_p),
-                ("mark", ctypes.c_void_p), ("n", ctypes.c_uint64)]
+                ("mark", ctypes.c_void_p), ("tcp_flags", ctypes.c_void_p),
+                ("n", ctypes.c_uint64)]
 
 
 class HdrV6(ctypes.Structure):
@@ -80,7 +82,8 @@ class Stats(ctypes.Structure):
 class NodeConfig(ctypes.Structure):
     _fields_ = [("ipv4_cluster_range", ctypes.c_uint32),
                 ("ipv4_cluster_mask", ctypes.c_uint32),
-                ("router_ip6", ctypes.c_uint8 * 16)]
+                ("router_ip6", ctypes.c_uint8 * 16),
+                ("host_ifindex", ctypes.c_uint32)]
 
 
 class IdentityCount(ctypes.Structure):
@@ -133,7 +136,9 @@ def lib():
                                   i32, ctypes.c_uint16, vp]
     L.cfc_ct_apply_v6.argtypes = [vp, ctypes.POINTER(HdrV6), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
-    for f in (L.cfc_drop_notify_v4, L.cfc_drop_notify_v6):
+    L.cfc_set_clock.argtypes = [vp, u32]
+    for f in (L.cfc_drop_notify_v4, L.cfc_drop_notify_v6,
+              L.cfc_monitor_events_v4, L.cfc_monitor_events_v6):
         f.argtypes = [vp, vp, ctypes.POINTER(Out), i32, ctypes.c_uint16, vp, vp,
                       u64, vp, vp]
     L.cfc_counters_device.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(u64)]

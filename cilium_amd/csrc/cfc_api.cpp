@@ -70,7 +70,7 @@ struct Epoch {
     DevBuf tbl24, tbl8, ovf, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
         polbloom, lxc6;
     DevBuf l6[3][3];   // ipc6 / pf6_fix / pf6_dyn: slots, bloom, lens
-    DevBuf ct4, ct6, ct_acct;
+    DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
     std::vector<uint32_t> seclabel;   // SECLABEL by LXC_ID at commit
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
     std::vector<Ct6Slot> ct6_host;
@@ -98,7 +98,8 @@ struct cfc_ctx {
     BuildOpts opts;
     // node_config.h defaults (IPV4_CLUSTER_RANGE/MASK, ROUTER_IP)
     cfc_node_config node{0x100000u, 0xff0000u,
-                         {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 0}};
+                         {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 0}, 1u};
+    uint32_t now = 0;   // bpf_ktime_get_sec() (cfc_set_clock)
 
     std::unique_ptr<Epoch> epoch;
     uint64_t epoch_seq = 0;
@@ -307,7 +308,9 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
         (rc = upload_lpm6(E->l6[0], img.ipc6, &E->T.ipc6, s)) ||
         (rc = upload_lpm6(E->l6[1], img.pf6_fix, &E->T.pf6_fix, s)) ||
         (rc = upload_lpm6(E->l6[2], img.pf6_dyn, &E->T.pf6_dyn, s)) ||
-        (rc = upload_vec(E->ct4, img.ct4, s)) || (rc = upload_vec(E->ct6, img.ct6, s)))
+        (rc = upload_vec(E->ct4, img.ct4, s)) || (rc = upload_vec(E->ct6, img.ct6, s)) ||
+        (rc = upload_vec(E->ct4_tm, img.ct4_tm, s)) ||
+        (rc = upload_vec(E->ct6_tm, img.ct6_tm, s)))
         return rc;
     {
         const size_t nslots = img.ct4.size() + img.ct6.size();
@@ -356,6 +359,8 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     T.ct4 = img.n_ct4 ? (const Ct4Slot *)E->ct4.p : nullptr;
     T.ct6 = img.n_ct6 ? (const Ct6Slot *)E->ct6.p : nullptr;
     T.ct_acct = (uint64_t *)E->ct_acct.p;
+    T.ct4_tm = (const CtTimer *)E->ct4_tm.p;
+    T.ct6_tm = (const CtTimer *)E->ct6_tm.p;
     T.ct4_mask = img.ct4_mask;
     T.ct4_probe = img.ct4_probe;
     T.ct6_mask = img.ct6_mask;
@@ -742,6 +747,15 @@ int cfc_set_node_config(cfc_ctx *c, const cfc_node_config *cfg)
     return 0;
 }
 
+int cfc_set_clock(cfc_ctx *c, uint32_t now_sec)
+{
+    if (!c)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    c->now = now_sec;
+    return 0;
+}
+
 int cfc_get_node_config(cfc_ctx *c, cfc_node_config *cfg)
 {
     if (!c || !cfg)
@@ -790,6 +804,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     DevTables T = E.T;
     T.v4_cluster_range = c->node.ipv4_cluster_range;
     T.v4_cluster_mask = c->node.ipv4_cluster_mask;
+    T.host_ifindex = c->node.host_ifindex;
+    T.now = c->now;
     for (int w = 0; w < 4; w++) {
         const uint8_t *b = c->node.router_ip6 + 4 * w;
         T.router6[w] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
@@ -857,7 +873,8 @@ namespace {
 template <class Hdr>
 int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
                 uint16_t ep_lxc, cfc_drop_notify *rec, uint64_t *hdr_index,
-                uint64_t cap, uint64_t *count, void *stream, int family)
+                uint64_t cap, uint64_t *count, void *stream, int family,
+                int traces)
 {
     if (!c || !in || !out || !count || (cap && !rec))
         return -EINVAL;
@@ -900,6 +917,8 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     a.mode = mode;
     a.own_seclabel = E.seclabel[ep_lxc];   // as the batch was classified
     a.ep_info = reinterpret_cast<const uint2 *>(E.ep_info.p);
+    a.host_ifindex = c->node.host_ifindex;
+    a.traces = traces;
     a.rec = rec;
     a.hdr_index = hdr_index;
     a.cap = cap;
@@ -923,7 +942,7 @@ int cfc_drop_notify_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
                        void *stream)
 {
     return drop_notify(c, in, out, mode, ep_lxc, rec, hdr_index, cap, count,
-                       stream, 4);
+                       stream, 4, 0);
 }
 
 int cfc_drop_notify_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
@@ -932,7 +951,25 @@ int cfc_drop_notify_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
                        void *stream)
 {
     return drop_notify(c, in, out, mode, ep_lxc, rec, hdr_index, cap, count,
-                       stream, 6);
+                       stream, 6, 0);
+}
+
+int cfc_monitor_events_v4(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out,
+                          int mode, uint16_t ep_lxc, void *rec,
+                          uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                          void *stream)
+{
+    return drop_notify(c, in, out, mode, ep_lxc, (cfc_drop_notify *)rec, hdr_index,
+                       cap, count, stream, 4, 1);
+}
+
+int cfc_monitor_events_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
+                          int mode, uint16_t ep_lxc, void *rec,
+                          uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                          void *stream)
+{
+    return drop_notify(c, in, out, mode, ep_lxc, (cfc_drop_notify *)rec, hdr_index,
+                       cap, count, stream, 6, 1);
 }
 
 int cfc_counters_device(cfc_ctx *c, uint64_t **dev, uint64_t *n)
@@ -1114,29 +1151,73 @@ struct CtApply {
     }
 };
 
-// struct ct_entry field offsets (bpf/lib/common.h:380-406)
-constexpr int CTE_RX_PACKETS = 0, CTE_TX_PACKETS = 16, CTE_BITS = 36,
-              CTE_REV_NAT = 38, CTE_SRC_SEC_ID = 44;
+// struct ct_entry (bpf/lib/common.h:380-406)
+struct CtEntry {
+    uint64_t rx_packets, rx_bytes, tx_packets, tx_bytes;
+    uint32_t lifetime;
+    uint16_t bits;   // rx_closing:1 tx_closing:1 nat46:1 lb_loopback:1 seen_non_syn:1
+    uint16_t rev_nat_index, slave;
+    uint8_t tx_flags_seen, rx_flags_seen;
+    uint32_t src_sec_id, last_tx_report, last_rx_report;
+};
+static_assert(sizeof(CtEntry) == 56, "struct ct_entry is 56 bytes");
+constexpr uint16_t CTB_RX_CLOSING = 1, CTB_TX_CLOSING = 2, CTB_SEEN_NON_SYN = 16;
+// conntrack.h:31-35
+constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,
+                   CT_CLOSE_TIMEOUT = 10, CT_REPORT_INTERVAL = 5;
 
-void ct_hit_update(Map *m, Map::Entry &e, int action, int dir, bool count,
-                   uint32_t len)
+// __ct_update_timeout (conntrack.h:125-185)
+void ct_upd(CtEntry &e, uint32_t now, uint32_t lifetime, int dir, uint8_t flags)
 {
-    char *v = &e.val[0];
-    if (count) {   // CONNTRACK_ACCOUNTING for a hit the device did not see
-        uint64_t pk[2];
-        const int off = dir == 1 ? CTE_RX_PACKETS : CTE_TX_PACKETS;
-        memcpy(pk, v + off, 16);
-        pk[0] += 1;
-        pk[1] += len;
-        memcpy(v + off, pk, 16);
+    e.lifetime = now + lifetime;
+    uint8_t &acc = dir == 1 ? e.rx_flags_seen : e.tx_flags_seen;
+    uint32_t &last = dir == 1 ? e.last_rx_report : e.last_tx_report;
+    const uint8_t seen = (uint8_t)(flags | acc);
+    if (last + CT_REPORT_INTERVAL < now || acc != seen) {
+        last = now;
+        acc = seen;
     }
-    uint16_t bits;
-    memcpy(&bits, v + CTE_BITS, 2);
-    if (action == 1)         // ACTION_CREATE re-opens a closing entry
-        bits &= (uint16_t)~3u;
-    else if (action == 2)    // ACTION_CLOSE: rx_closing / tx_closing
-        bits |= dir == 1 ? 1u : 2u;
-    memcpy(v + CTE_BITS, &bits, 2);
+}
+// ct_update_timeout (:191-205); syn is bit 0 of TCP byte 12 (union tcp_flags)
+void ct_upd_timeout(CtEntry &e, uint32_t now, bool is_tcp, int dir, bool syn,
+                    uint8_t flags)
+{
+    uint32_t lifetime = CT_LIFETIME_NONTCP;
+    if (is_tcp) {
+        if (!syn)
+            e.bits |= CTB_SEEN_NON_SYN;
+        lifetime = (e.bits & CTB_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+    }
+    ct_upd(e, now, lifetime, dir, flags);
+}
+
+// What __ct_lookup (:221-285) does to a hit entry, applied in header order
+// at the batch's clock: timeouts, report times, seen flags, the closing
+// bits of ACTION_CREATE / ACTION_CLOSE; with count, CONNTRACK_ACCOUNTING
+// for a hit the device did not see (a flow created earlier in the batch)
+void ct_hit_update(Map *m, Map::Entry &me, int action, int dir, bool count,
+                   uint32_t len, uint32_t now, bool is_tcp, bool syn, uint8_t flags)
+{
+    CtEntry e;
+    memcpy(&e, me.val.data(), sizeof(e));
+    if (count) {
+        (dir == 1 ? e.rx_packets : e.tx_packets) += 1;
+        (dir == 1 ? e.rx_bytes : e.tx_bytes) += len;
+    }
+    auto alive = [&] { return !(e.bits & CTB_RX_CLOSING) || !(e.bits & CTB_TX_CLOSING); };
+    if (alive())
+        ct_upd_timeout(e, now, is_tcp, dir, syn, flags);
+    if (action == 1) {            // ACTION_CREATE re-opens a closing entry
+        if (e.bits & (CTB_RX_CLOSING | CTB_TX_CLOSING)) {
+            e.bits &= (uint16_t)~(CTB_RX_CLOSING | CTB_TX_CLOSING);
+            ct_upd_timeout(e, now, is_tcp, dir, syn, flags);
+        }
+    } else if (action == 2) {     // ACTION_CLOSE: rx_closing / tx_closing
+        e.bits |= dir == 1 ? CTB_RX_CLOSING : CTB_TX_CLOSING;
+        if (!alive())
+            ct_upd(e, now, CT_CLOSE_TIMEOUT, dir, flags);
+    }
+    memcpy(&me.val[0], &e, sizeof(e));
     m->gen++;
 }
 
@@ -1214,7 +1295,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         return 0;
     hipStream_t s = (hipStream_t)stream;
     const size_t al = family == 4 ? 4 : 16;
-    std::vector<uint8_t> sa(al * n), da(al * n), ct(n);
+    std::vector<uint8_t> sa(al * n), da(al * n), ct(n), tf(n, 0);
     std::vector<uint32_t> pt(n), mt(n), ident(n);
     std::vector<int32_t> ver(n);
     if (hipMemcpyAsync(sa.data(), in->saddr, al * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1224,9 +1305,12 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         hipMemcpyAsync(ident.data(), out->identity, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(ver.data(), out->verdict, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipMemcpyAsync(ct.data(), out->ct, n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        (in->tcp_flags &&
+         hipMemcpyAsync(tf.data(), in->tcp_flags, n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     CtApply A(c, family);
+    const uint32_t now = c->now;
     const uint8_t icmp = family == 4 ? 1 : 58;
     const uint32_t echo = family == 4 ? 8 : 128, echo_reply = family == 4 ? 0 : 129;
     for (size_t i = 0; i < n; i++) {
@@ -1237,6 +1321,8 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         const int dst = A.endpoint(d_);
         const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
         const uint32_t proto = mt[i] & 0xFF, len = mt[i] >> 16;
+        const bool is_tcp = proto == 6, syn = (mt[i] & CFC_HF_TCP_CLOSE) != 0;
+        const uint8_t tflags = is_tcp ? tf[i] : 0;
         for (int st = 0; st < 2; st++) {
             const uint8_t cs = (uint8_t)(cb >> (4 * st));
             if (!(cs & CFC_CT_DONE))
@@ -1283,11 +1369,13 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             if (b >= 2) {                       // CT_REPLY / CT_RELATED
                 auto it = m->kv.find(k1);
                 if (it != m->kv.end())
-                    ct_hit_update(m, it->second, action, dir, false, len);
+                    ct_hit_update(m, it->second, action, dir, false, len, now, is_tcp,
+                                  syn, tflags);
             } else if (b == 1) {                // CT_ESTABLISHED
                 auto it = m->kv.find(k2);
                 if (it != m->kv.end()) {
-                    ct_hit_update(m, it->second, action, dir, false, len);
+                    ct_hit_update(m, it->second, action, dir, false, len, now, is_tcp,
+                                  syn, tflags);
                     if (dropped) {              // ct_delete4/6
                         ct_drop_counts(c, m, k2, s);
                         (void)m->erase(k2.data());
@@ -1296,23 +1384,21 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             } else if (cs & CFC_CT_CREATE) {
                 auto it = m->kv.find(k2);
                 if (it != m->kv.end()) {        // created earlier in this batch
-                    ct_hit_update(m, it->second, action, dir, true, len);
+                    ct_hit_update(m, it->second, action, dir, true, len, now, is_tcp,
+                                  syn, tflags);
                     continue;
                 }
-                // ct_create4/6 (conntrack.h:615-662, :691-772)
-                char e[56] = {0};
-                const uint64_t one = 1, bytes = len;
-                memcpy(e + (dir == 1 ? CTE_RX_PACKETS : CTE_TX_PACKETS), &one, 8);
-                memcpy(e + (dir == 1 ? CTE_RX_PACKETS : CTE_TX_PACKETS) + 8, &bytes, 8);
-                const uint32_t sec = mode == CFC_MODE_EGRESS ? c->seclabel[ep_lxc] : ident[i];
-                memcpy(e + CTE_SRC_SEC_ID, &sec, 4);
-                if (family == 6 && dir == 1) {  // ipv6_policy, bpf_lxc.c:787-788
-                    const uint16_t rn = (uint16_t)(d_[12] | d_[13] << 8);
-                    memcpy(e + CTE_REV_NAT, &rn, 2);
-                }
-                (void)m->update(k2.data(), e, 0);
-                uint16_t bits = 16;             // seen_non_syn for ICMP
-                memcpy(e + CTE_BITS, &bits, 2);
+                // ct_create4/6 (conntrack.h:615-662, :691-772): timeouts
+                // with seen_flags.syn = is_tcp (lower_bits stay 0)
+                CtEntry e{};
+                ct_upd_timeout(e, now, is_tcp, dir, is_tcp, 0);
+                (dir == 1 ? e.rx_packets : e.tx_packets) = 1;
+                (dir == 1 ? e.rx_bytes : e.tx_bytes) = len;
+                e.src_sec_id = mode == CFC_MODE_EGRESS ? c->seclabel[ep_lxc] : ident[i];
+                if (family == 6 && dir == 1)    // ipv6_policy, bpf_lxc.c:787-788
+                    e.rev_nat_index = (uint16_t)(d_[12] | d_[13] << 8);
+                (void)m->update(k2.data(), &e, 0);
+                e.bits |= CTB_SEEN_NON_SYN;     // "For ICMP, there is no SYN"
                 const std::string ki = [&] {
                     std::string t = k2;
                     memset(&t[2 * al], 0, 4);
@@ -1322,7 +1408,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 }();
                 if (m->kv.count(ki))            // overwritten
                     ct_drop_counts(c, m, ki, s);
-                (void)m->update(ki.data(), e, 0);
+                (void)m->update(ki.data(), &e, 0);
             }
         }
     }

@@ -135,6 +135,8 @@ struct Hdr {
     uint32_t idw;                // identity counter key (CountArgs.id)
     bool id_ovf, drop1;          // ident has no histogram range; stage-1 drop
     uint32_t ev2;                // stage-2 identity event: 0, 1 fwd, 2 drop
+    uint32_t tf;                 // TCP header byte 13 (cfc_hdr_v4.tcp_flags)
+    uint32_t evw;                // trace event word of a forwarded header
     PolicyProbe P;
 };
 
@@ -152,6 +154,7 @@ __device__ __forceinline__ void r1_load(const cfc_hdr_v4 &in, uint64_t i,
     h.pt = ld_nt(in.ports + i);
     h.mt = ld_nt(in.meta + i);
     h.mk = in.mark ? ld_nt(in.mark + i) : 0u;
+    h.tf = in.tcp_flags ? (uint32_t)in.tcp_flags[i] : 0u;
 }
 
 // round 2: every lookup that only needs the header
@@ -250,6 +253,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     h.idw = KEY_NONE;
     h.id_ovf = h.drop1 = false;
     h.ev2 = 0;
+    h.evw = 0;
     if (MODE == CFC_MODE_XDP || h.xdp_drop)
         return;
     const uint32_t proto = h.mt & 0xFF;
@@ -332,13 +336,23 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
 // to different fields of `h` get merged by the compiler into one store
 // through a selected field address, which pushes the whole per-header state
 // array into scratch memory.
-template <int MODE, bool CT>
+template <int MODE, bool CT, bool NT>
 __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                                            const EgressArgs &E, Hdr &h)
 {
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     if (!h.need_pol)
         return;
+    // the monitor length of a trace this header may send (NT: the caller
+    // wants the event words)
+    const uint32_t action = ct_action(false, h.mt & 0xFF, h.pt, h.mt);
+    const uint32_t tfl = (h.mt & 0xFF) == 6 ? h.tf : 0u;
+    const uint32_t mon1 = NT ? ct_monitor(T, CT ? T.ct4_tm : nullptr, h.ct_slot,
+                                          EGR ? CT_EGRESS : CT_INGRESS, action, tfl,
+                                          h.dport)
+                             : 0u;
+    const uint32_t res1 = CT ? (uint32_t)h.ct_res : 0u;
+    uint32_t evw = 0;
     // replies and related packets pass whatever the policy says
     // (bpf_lxc.c:963-970 ingress, :538-545 egress)
     const bool reply = CT && h.ct_res >= CT_REPLY;
@@ -372,22 +386,26 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     } else if (!EGR) {
         if (h.skip_proxy)
             v = 0;
-        // redirect_to_proxy for NEW / ESTABLISHED flows, or TRACE_TO_LXC +
-        // delivery
+        // redirect_to_proxy for NEW / ESTABLISHED flows (TRACE_TO_PROXY,
+        // lxc.h:117), or TRACE_TO_LXC + delivery (bpf_lxc.c:1006)
         const bool prox = v > 0 && !reply;
         act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
         ver = prox ? v : 0;
         met0 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
+        evw = trace_word(prox ? OBS_TO_PROXY : OBS_TO_LXC, h.rec.w & 0xFFFF, res1, mon1);
     } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
         act = TC_ACT_REDIRECT;
         ver = v;
+        evw = trace_word(OBS_TO_PROXY, E.lxc_id, res1, mon1);
     } else {
         met0 = mkey<MODE>(0, METRIC_EGRESS);   // to_host/local/to_stack
         ver = 0;
         if (!(h.rec.w & LXC_VALID)) {
-            act = TC_ACT_OK;
+            act = TC_ACT_OK;   // pass_to_stack: TRACE_TO_STACK (bpf_lxc.c:687)
+            evw = trace_word(OBS_TO_STACK, E.lxc_id, res1, mon1);
         } else if (h.rec.w & LXC_HOST) {
-            act = TC_ACT_REDIRECT;
+            act = TC_ACT_REDIRECT;   // to_host: TRACE_TO_HOST (:668)
+            evw = trace_word(OBS_TO_HOST, E.lxc_id, res1, mon1);
         } else if (!(h.rec.w & LXC_HAS_POLICY)) {
             act = TC_ACT_SHOT;
             ver = DROP_MISSED_TAIL_CALL;
@@ -425,10 +443,18 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                 ver = prox ? w : 0;
                 met1 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
                 ev2 = 1;
+                if (NT) {   // the destination program's trace
+                    const uint32_t mon2 = ct_monitor(T, CT ? T.ct4_tm : nullptr,
+                                                     CT ? c2.slot : NONE, CT_INGRESS,
+                                                     action, tfl, dp2);
+                    evw = trace_word(prox ? OBS_TO_PROXY : OBS_TO_LXC, h.rec.w & 0xFFFF,
+                                     CT ? (uint32_t)c2.res : 0u, mon2);
+                }
             }
         }
     }
     h.ev2 = ev2;
+    h.evw = evw;
     h.act = act;
     h.ver = ver;
     h.met0 = met0;
@@ -525,7 +551,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             r3_identity<MODE, CT>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r4_verdict<MODE, CT>(T, S, E, h[u]);
+            r4_verdict<MODE, CT, NT>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
@@ -538,10 +564,12 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                     out.action[o] = (uint8_t)h[u].act;
                 if (CT && out.ct)
                     out.ct[o] = (uint8_t)h[u].ct_byte;
-                if (NT)   // the drop-notify site word (cfc_out.notify)
-                    st_nt(notify_word(MODE, h[u].ver,
-                                      EGR && h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
-                                      h[u].rec.w & 0xFFFF, E.lxc_id),
+                if (NT)   // the monitor event word (cfc_out.notify)
+                    st_nt(h[u].ver < 0
+                              ? notify_word(MODE, h[u].ver,
+                                            EGR && h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
+                                            h[u].rec.w & 0xFFFF, E.lxc_id)
+                              : h[u].evw,
                           out.notify + o);
                 if (CT) {
                     st_nt(h[u].ct_k1, C.ct + o);

@@ -132,6 +132,8 @@ struct NotifyArgs {
     int mode;
     uint32_t own_seclabel;   // SECLABEL of ep_lxc (egress batches)
     const uint2 *ep_info;    // [65536] {SECLABEL, ifindex} by LXC_ID
+    uint32_t host_ifindex;   // HOST_IFINDEX (trace records)
+    int traces;              // 1: trace records too (cfc_monitor_events)
     cfc_drop_notify *rec;
     uint64_t *hdr_index;     // may be NULL
     uint64_t cap;

@@ -239,6 +239,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         const uint32_t pt = ld_nt(in.ports + i);
         const uint32_t mt = ld_nt(in.meta + i);
         const uint32_t mk = in.mark ? ld_nt(in.mark + i) : 0u;
+        const uint32_t tfl = (in.tcp_flags && (mt & 0xFF) == 6) ? (uint32_t)in.tcp_flags[i] : 0u;
         const uint4 sa = bswap4(sa_raw), da = bswap4(da_raw);
         const uint32_t proto = mt & 0xFF;
 
@@ -247,6 +248,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         uint32_t ctb = 0;   // CT byte (cfc.h CFC_CT_*)
         uint32_t ck1 = NONE, ck2 = NONE;   // CT accounting keys per stage
         uint32_t idw = KEY_NONE, ev2 = 0;  // identity counter key; stage-2 event
+        uint32_t evw = 0;                  // trace event word (forwarded)
         const uint32_t len = mt >> 16;
         const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
         const bool local = (drec.z & LXC_VALID) != 0;
@@ -333,6 +335,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
                                 ver = prox ? v : 0;
                                 met0 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
+                                if (NT)   // TRACE_TO_PROXY / TRACE_TO_LXC (:873)
+                                    evw = trace_word(
+                                        prox ? OBS_TO_PROXY : OBS_TO_LXC, drec.z & 0xFFFF,
+                                        (uint32_t)c.res,
+                                        ct_monitor(T, CT ? T.ct6_tm : nullptr, c.slot,
+                                                   CT_INGRESS, ct_action(true, proto, pt, mt),
+                                                   tfl, c.dport));
                             }
                         }
                     }
@@ -374,19 +383,30 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                               ((c.res == CT_NEW && pr.verdict >= 0) ? CTO_CREATE : 0u);
                     idw = id_event(T, C, ID_DIR_EGRESS, ident, pr.verdict < 0 && !reply,
                                    len, valid);
+                    // the sender's trace: after ct_create6 the v6 egress path
+                    // sets monitor = TRACE_PAYLOAD_LEN (bpf_lxc.c:248)
+                    const uint32_t mon1 =
+                        !NT ? 0u
+                        : c.res == CT_NEW ? TRACE_PAYLOAD_LEN
+                                          : ct_monitor(T, CT ? T.ct6_tm : nullptr, c.slot,
+                                                       CT_EGRESS, ct_action(true, proto, pt, mt),
+                                                       tfl, c.dport);
                     if (pr.verdict < 0 && !reply) {
                         ver = DROP_POLICY;
                         met0 = mkey6<MODE>(DROP_POLICY, METRIC_EGRESS);
                     } else if (pr.verdict > 0) {   // to the proxy
                         act = TC_ACT_REDIRECT;
                         ver = pr.verdict;
+                        evw = trace_word(OBS_TO_PROXY, E.lxc_id, (uint32_t)c.res, mon1);
                     } else {
                         met0 = mkey6<MODE>(0, METRIC_EGRESS);   // host/local/stack
                         ver = 0;
                         if (!local) {
-                            act = TC_ACT_OK;
+                            act = TC_ACT_OK;   // TRACE_TO_STACK (:390)
+                            evw = trace_word(OBS_TO_STACK, E.lxc_id, (uint32_t)c.res, mon1);
                         } else if (drec.z & LXC_HOST) {
-                            act = TC_ACT_REDIRECT;
+                            act = TC_ACT_REDIRECT;   // TRACE_TO_HOST (:373)
+                            evw = trace_word(OBS_TO_HOST, E.lxc_id, (uint32_t)c.res, mon1);
                         } else if (!(drec.z & LXC_HAS_POLICY)) {
                             ver = DROP_MISSED_TAIL_CALL;
                             met1 = mkey6<MODE>(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
@@ -418,6 +438,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
                                 ver = prox ? pw.verdict : 0;
                                 met1 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
+                                if (NT)
+                                    evw = trace_word(
+                                        prox ? OBS_TO_PROXY : OBS_TO_LXC, drec.z & 0xFFFF,
+                                        (uint32_t)c2.res,
+                                        ct_monitor(T, CT ? T.ct6_tm : nullptr, c2.slot,
+                                                   CT_INGRESS, ct_action(true, proto, pt, mt),
+                                                   tfl, c2.dport));
                             }
                         }
                     }
@@ -430,10 +457,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             out.action[i] = (uint8_t)act;
         if (CT && out.ct)
             out.ct[i] = (uint8_t)ctb;
-        if (NT)   // the drop-notify site word (cfc_out.notify)
-            st_nt(notify_word(MODE, ver,
-                              EGR && met1 == mkey6<MODE>(DROP_POLICY, METRIC_INGRESS),
-                              drec.z & 0xFFFF, E.lxc_id),
+        if (NT)   // the monitor event word (cfc_out.notify)
+            st_nt(ver < 0 ? notify_word(MODE, ver,
+                                        EGR && met1 == mkey6<MODE>(DROP_POLICY, METRIC_INGRESS),
+                                        drec.z & 0xFFFF, E.lxc_id)
+                          : evw,
                   out.notify + i);
         if (CT) {
             st_nt(ck1, C.ct + i);

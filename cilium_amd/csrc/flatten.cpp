@@ -23,7 +23,7 @@ uint64_t HostImage::device_bytes() const
            sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size() +
            ipc6.bytes() + pf6_fix.bytes() + pf6_dyn.bytes() +
            sizeof(Lxc6Slot) * lxc6.size() + sizeof(Ct4Slot) * ct4.size() +
-           sizeof(Ct6Slot) * ct6.size() + 32ull * (ct4.size() + ct6.size());
+           sizeof(Ct6Slot) * ct6.size() + 48ull * (ct4.size() + ct6.size());
 }
 
 // DIR-24-8: every prefix <= /24 fills its tbl24 range in ascending length
@@ -449,11 +449,13 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
     if (n4) {
         uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n4));
         img->ct4.assign(ns, Ct4Slot{});
+        img->ct4_tm.assign(ns, CtTimer{});
         img->ct4_mask = ns - 1;
     }
     if (n6) {
         uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n6));
         img->ct6.assign(ns, Ct6Slot{});
+        img->ct6_tm.assign(ns, CtTimer{});
         img->ct6_mask = ns - 1;
     }
     for (const Map *m : cts) {
@@ -471,6 +473,17 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
             uint32_t z;
             memcpy(&z, k + 2 * al, 4);
             const uint32_t w = ct_word(nh, fl, owner);
+            // struct ct_entry: bits @36, tx/rx_flags_seen @42/43,
+            // last_tx/rx_report @48/52
+            const uint8_t *v = (const uint8_t *)kv.second.val.data();
+            CtTimer tm{};
+            if (kv.second.val.size() >= 56) {
+                uint16_t bits;
+                memcpy(&bits, v + 36, 2);
+                memcpy(&tm.last_tx, v + 48, 4);
+                memcpy(&tm.last_rx, v + 52, 4);
+                tm.flags = v[43] | (uint32_t)v[42] << 8 | (uint32_t)(bits & 3) << 16;
+            }
             if (!v6) {
                 Ct4Slot e;
                 memcpy(&e.x, k, 4);
@@ -483,6 +496,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                     p++;
                 }
                 img->ct4[i] = e;
+                img->ct4_tm[i] = tm;
                 img->ct4_probe = std::max(img->ct4_probe, p);
                 img->n_ct4++;
             } else {
@@ -497,6 +511,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                     p++;
                 }
                 img->ct6[i] = e;
+                img->ct6_tm[i] = tm;
                 img->ct6_probe = std::max(img->ct6_probe, p);
                 img->n_ct6++;
             }

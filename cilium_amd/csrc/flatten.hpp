@@ -73,6 +73,7 @@ struct HostImage {
     // conntrack (layout.h): every CT map in one table per family
     std::vector<Ct4Slot> ct4;
     std::vector<Ct6Slot> ct6;
+    std::vector<CtTimer> ct4_tm, ct6_tm;     // parallel to ct4 / ct6
     uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
     uint32_t n_ct4 = 0, n_ct6 = 0;           // entries placed
     std::vector<uint8_t> ct_local;           // lxc_id -> has local CT maps

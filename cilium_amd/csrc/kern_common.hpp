@@ -37,6 +37,20 @@ __device__ __forceinline__ uint32_t notify_word(int mode, int ver,
     const bool netdev = ver == DROP_MISSED_TAIL_CALL || ver == -156 || ver == -157;
     return netdev ? CFC_NT_NETDEV << 16 : (CFC_NT_POLICY << 16 | dest_lxc);
 }
+// ---- monitor events (cfc.h CFC_NT_*): the trace_notify of a forwarded
+// packet.  obs: TRACE_TO_LXC 0, TO_PROXY 1, TO_HOST 2, TO_STACK 3; reason:
+// the CT result; mon: the monitor length (0 = not sent, MONITOR_AGGREGATION
+// 5 drops traces of flows inside their report interval, trace.h:131-132)
+constexpr uint32_t OBS_TO_LXC = 0, OBS_TO_PROXY = 1, OBS_TO_HOST = 2, OBS_TO_STACK = 3;
+constexpr uint32_t TRACE_PAYLOAD_LEN = 128, MTU_LEN = 1500;
+__device__ __forceinline__ uint32_t trace_word(uint32_t obs, uint32_t source,
+                                               uint32_t reason, uint32_t mon)
+{
+    return mon ? ((CFC_NT_TRACE + obs) << 16 | source | reason << 20 |
+                  (mon == MTU_LEN ? 2u : mon == 1u ? 3u : 1u) << 22)
+               : 0u;
+}
+
 // workspace: entry indices [n] (egress: a second array at ctr_stride(n)),
 // then the partial slabs; both arrays 16-byte aligned for k_count
 __host__ __device__ constexpr uint64_t ctr_stride(uint64_t n) { return (n + 3) & ~3ull; }
@@ -332,6 +346,62 @@ __device__ __forceinline__ CtResult ct_stage6(const DevTables &T, const uint4 &s
     r.res = r.slot != NONE ? CT_ESTABLISHED : CT_NEW;
     r.dport = k.ts;
     return r;
+}
+
+// *monitor of a ct_lookup (conntrack.h:221-285, 587-589) against the entry
+// as committed: a miss reports TRACE_PAYLOAD_LEN; a hit runs
+// __ct_update_timeout's report decision (the flow's interval of
+// CT_REPORT_INTERVAL 5 s passed, or the packet carries TCP flags the
+// direction has not seen; :125-185) on a copy of the slot's report state,
+// as __ct_lookup's action would (re-open a closing entry: CREATE; RST/FIN:
+// CLOSE, always reported); a DNS port captures MTU bytes.
+// action: 1 CREATE, 2 CLOSE, 0 UNSPEC (ICMP replies and errors).
+__device__ __forceinline__ uint32_t ct_action(bool v6, uint32_t proto, uint32_t pt,
+                                              uint32_t meta)
+{
+    if (proto == 6)
+        return (meta & CFC_HF_TCP_CLOSE) ? 2u : 1u;
+    if (proto == 17)
+        return 1u;
+    const uint32_t type = pt & 0xFF;
+    const bool unspec = v6 ? ((type >= 1 && type <= 4) || type == 129)
+                           : (type == 3 || type == 11 || type == 12 || type == 0);
+    return unspec ? 0u : 1u;
+}
+// ct_update_timeout is declared bool: a reported hit's monitor length is 1
+__device__ __forceinline__ uint32_t ct_report(uint32_t &last, uint32_t &acc,
+                                              uint32_t fl, uint32_t now)
+{
+    const uint32_t seen = fl | acc;
+    if (last + 5u < now || acc != seen) {
+        last = now;
+        acc = seen;
+        return 1u;
+    }
+    return 0u;
+}
+__device__ __forceinline__ uint32_t ct_monitor(const DevTables &T, const CtTimer *tm,
+                                               uint32_t slot, int dir, uint32_t action,
+                                               uint32_t fl, uint32_t dport)
+{
+    uint32_t m = TRACE_PAYLOAD_LEN;
+    if (slot != NONE && tm) {
+        const uint4 t = ld16(tm + slot);
+        const bool in = dir == CT_INGRESS;
+        uint32_t last = in ? t.x : t.y;
+        uint32_t acc = in ? (t.z & 0xFF) : ((t.z >> 8) & 0xFF);
+        uint32_t clo = (t.z >> 16) & 3;
+        m = 0;
+        if (clo != 3)   // ct_entry_alive
+            m = ct_report(last, acc, fl, T.now);
+        if (action == 1u) {
+            if (clo)
+                m = ct_report(last, acc, fl, T.now);
+        } else if (action == 2u) {
+            m = TRACE_PAYLOAD_LEN;
+        }
+    }
+    return dport == 0x3500u ? MTU_LEN : m;   // conn_is_dns: htons(53)
 }
 
 // key of ct_acct[slot][dir] (k_ct_count), NONE for a miss

@@ -262,6 +262,15 @@ __host__ __device__ inline uint32_t ct_hash6(const uint32_t d[4], const uint32_t
 struct alignas(16) Ct4Slot {
     uint32_t x, y, z, w;
 };
+// The report state of a CT slot's entry (struct ct_entry, common.h:380-406)
+// that decides whether a hit is traced (__ct_update_timeout,
+// conntrack.h:125-185): last_{rx,tx}_report and rx/tx_flags_seen | the
+// rx/tx_closing bits << 16
+struct alignas(16) CtTimer {
+    uint32_t last_rx, last_tx;
+    uint32_t flags;      // rx_flags_seen | tx_flags_seen << 8 | closing << 16
+    uint32_t pad;
+};
 struct alignas(16) Ct6Slot {
     uint32_t d[4], s[4], z, w, pad[2];
 };
@@ -300,6 +309,11 @@ struct DevTables {
     uint32_t ct4_mask, ct4_probe;
     uint32_t ct6_mask, ct6_probe;
     uint32_t ct6_acct_base;        // first v6 slot in ct_acct
+    const CtTimer *ct4_tm;         // report state per slot (parallel to ct4 / ct6)
+    const CtTimer *ct6_tm;
+    // the launch: bpf_ktime_get_sec() (cfc_set_clock), HOST_IFINDEX
+    uint32_t now;
+    uint32_t host_ifindex;
     // per-identity counters: bit r set = identities [r * ID_RANGE,
     // (r + 1) * ID_RANGE) have a histogram range (classify.hpp)
     uint32_t id_cover;

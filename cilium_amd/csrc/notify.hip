@@ -1,5 +1,6 @@
-// Drop notifications of a classified batch: struct drop_notify records
-// (bpf/lib/drop.h:40-78) in header order.
+// Monitor events of a classified batch: struct drop_notify records
+// (bpf/lib/drop.h:40-78) and struct trace_notify records (trace.h:71-81,
+// send_trace_notify :97-155) in header order.
 //
 // The reference emits one perf-ring sample per dropped packet from
 // __send_drop_notify, a tail call armed by send_drop_notify (drop.h:94-109)
@@ -49,8 +50,15 @@ __device__ __forceinline__ uint32_t flow_hash(const NotifyArgs &a, uint64_t i)
     return fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + pw * 0xC2B2AE3Du + proto);
 }
 
+// the events a call records: drops (kinds 1-3), and traces when asked
+__device__ __forceinline__ bool nt_selected(uint32_t w, int traces)
+{
+    const uint32_t kind = (w >> 16) & 0xF;
+    return w != 0 && (kind < CFC_NT_TRACE || traces);
+}
+
 __global__ __launch_bounds__(NT_THREADS) void k_nt_count(const uint32_t *notify,
-                                                         uint64_t n,
+                                                         uint64_t n, int traces,
                                                          uint64_t *blk)
 {
     const uint64_t base = (uint64_t)blockIdx.x * NT_PER_BLOCK;
@@ -58,7 +66,7 @@ __global__ __launch_bounds__(NT_THREADS) void k_nt_count(const uint32_t *notify,
 #pragma unroll
     for (int r = 0; r < NT_ITERS; r++) {
         const uint64_t i = base + (uint64_t)r * NT_THREADS + threadIdx.x;
-        c += (i < n && ld_nt(notify + i) != 0) ? 1u : 0u;
+        c += (i < n && nt_selected(ld_nt(notify + i), traces)) ? 1u : 0u;
     }
     // wave sums, then the block's
     for (int o = 32; o > 0; o >>= 1)
@@ -113,7 +121,8 @@ __global__ __launch_bounds__(NT_THREADS) void k_nt_write(NotifyArgs a,
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int r = 0; r < NT_ITERS; r++) {
         const uint64_t i = base + (uint64_t)r * NT_THREADS + threadIdx.x;
-        const uint32_t w = i < a.n ? ld_nt(a.notify + i) : 0u;
+        uint32_t w = i < a.n ? ld_nt(a.notify + i) : 0u;
+        w = nt_selected(w, a.traces) ? w : 0u;
         const uint64_t m = __ballot(w != 0);
         const uint32_t below = __popcll(m & ((1ull << lane) - 1));
         if (lane == 0)
@@ -125,8 +134,37 @@ __global__ __launch_bounds__(NT_THREADS) void k_nt_write(NotifyArgs a,
             total += s[v];
         }
         const uint64_t pos = off + before + below;
-        if (w && pos < a.cap) {
-            const uint32_t site = w >> 16, lxc = w & 0xFFFF;
+        if (w && pos < a.cap && ((w >> 16) & 0xF) >= CFC_NT_TRACE) {
+            // trace_notify: src/dst labels in full (trace.h:137-151)
+            const uint32_t obs = ((w >> 16) & 0xF) - CFC_NT_TRACE, lxc = w & 0xFFFF;
+            const uint32_t reason = (w >> 20) & 3;
+            const uint32_t mc = (w >> 22) & 3;   // TRACE_PAYLOAD_LEN / MTU / 1
+            const uint32_t mon = mc == 2 ? MTU_LEN : mc == 3 ? 1u : TRACE_PAYLOAD_LEN;
+            const uint32_t ident = a.identity[i];
+            const uint32_t len = a.meta[i] >> 16;
+            const uint2 e = a.ep_info[lxc];
+            uint32_t src = e.x, dst = 0, dst_id = 0, ifx = 0;
+            if (obs == OBS_TO_LXC) {   // the destination's ipv{4,6}_policy
+                src = a.mode == CFC_MODE_EGRESS ? a.own_seclabel : ident;
+                dst = e.x;
+                dst_id = lxc;
+                ifx = e.y;
+            } else if (obs == OBS_TO_PROXY) {
+                ifx = a.host_ifindex;
+            } else if (obs == OBS_TO_HOST) {
+                dst = 1;   // HOST_ID
+                ifx = a.host_ifindex;
+            } else {   // TO_STACK: the destination identity
+                dst = ident;
+            }
+            const uint32_t w0 = CFC_NOTIFY_TRACE | obs << 8 | lxc << 16;
+            uint4 *p = reinterpret_cast<uint4 *>(a.rec) + 2 * pos;
+            p[0] = make_uint4(w0, flow_hash(a, i), len, min(len, mon));
+            p[1] = make_uint4(src, dst, dst_id | reason << 16, ifx);
+            if (a.hdr_index)
+                a.hdr_index[pos] = i;
+        } else if (w && pos < a.cap) {
+            const uint32_t site = (w >> 16) & 0xF, lxc = w & 0xFFFF;
             const int ver = a.verdict[i];
             const uint32_t ident = a.identity[i];
             const uint32_t len = a.meta[i] >> 16;
@@ -145,7 +183,7 @@ __global__ __launch_bounds__(NT_THREADS) void k_nt_write(NotifyArgs a,
             }
             const uint32_t w0 = CFC_NOTIFY_DROP | (((uint32_t)(-ver) & 0xFF) << 8) |
                                 (source << 16);
-            uint4 *p = reinterpret_cast<uint4 *>(a.rec + pos);
+            uint4 *p = reinterpret_cast<uint4 *>(a.rec) + 2 * pos;
             p[0] = make_uint4(w0, flow_hash(a, i), len,
                               min(len, (uint32_t)CFC_TRACE_PAYLOAD_LEN));
 
@@ -173,7 +211,7 @@ int launch_drop_notify(const NotifyArgs &a, uint64_t *ws, hipStream_t s)
     const uint64_t nb = (a.n + NT_PER_BLOCK - 1) / NT_PER_BLOCK;
     if (nb > 0x7FFFFFFFull)
         return -E2BIG;
-    k_nt_count<<<(uint32_t)nb, NT_THREADS, 0, s>>>(a.notify, a.n, ws);
+    k_nt_count<<<(uint32_t)nb, NT_THREADS, 0, s>>>(a.notify, a.n, a.traces, ws);
     k_nt_scan<<<1, 1024, 0, s>>>(ws, nb, a.count);
     k_nt_write<<<(uint32_t)nb, NT_THREADS, 0, s>>>(a, ws);
     return hipGetLastError() == hipSuccess ? 0 : -EINVAL;

@@ -22,9 +22,16 @@ class HeaderBatchV4:
     ports: "torch.Tensor"     # sport | dport << 16 (be16 raw each)
     meta: "torch.Tensor"      # proto | flags << 8 | len << 16
     mark: "torch.Tensor | None" = None
+    tcp_flags: "torch.Tensor | None" = None   # uint8 TCP header byte 13
 
     def __len__(self):
         return int(self.saddr.numel())
+
+    def slice(self, a, b):
+        """headers [a, b) (views of the same device memory)"""
+        sl = lambda x: None if x is None else x[a:b]   # noqa: E731
+        return type(self)(*(sl(getattr(self, f.name))
+                            for f in dataclasses.fields(self)))
 
 
 @dataclasses.dataclass
@@ -36,9 +43,16 @@ class HeaderBatchV6:
     ports: "torch.Tensor"
     meta: "torch.Tensor"      # proto | flags << 8 | len << 16 (HF_EXTHDR)
     mark: "torch.Tensor | None" = None
+    tcp_flags: "torch.Tensor | None" = None   # uint8 TCP header byte 13
 
     def __len__(self):
         return int(self.ports.numel())
+
+    def slice(self, a, b):
+        """headers [a, b) (views of the same device memory)"""
+        sl = lambda x: None if x is None else x[a:b]   # noqa: E731
+        return type(self)(*(sl(getattr(self, f.name))
+                            for f in dataclasses.fields(self)))
 
 
 @dataclasses.dataclass
@@ -61,8 +75,10 @@ def pack_v4(h, device="cuda"):
     def t(a):
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32)
                                 .view(np.int32)).to(device)
+    from .synth import tcp_flags_of
     return HeaderBatchV4(t(h.saddr), t(h.daddr), t(ports), t(meta),
-                         t(h.mark) if h.mark is not None else None)
+                         t(h.mark) if h.mark is not None else None,
+                         torch.from_numpy(tcp_flags_of(h).copy()).to(device))
 
 
 def pack_v6(h, device="cuda"):
@@ -76,10 +92,12 @@ def pack_v6(h, device="cuda"):
 
     def t(a):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
+    from .synth import tcp_flags_of
     return HeaderBatchV6(t(np.ascontiguousarray(h.saddr, np.uint8)).view(-1, 4),
                          t(np.ascontiguousarray(h.daddr, np.uint8)).view(-1, 4),
                          t(ports), t(meta),
-                         t(h.mark.astype(np.uint32)) if h.mark is not None else None)
+                         t(h.mark.astype(np.uint32)) if h.mark is not None else None,
+                         torch.from_numpy(tcp_flags_of(h).copy()).to(device))
 
 
 def pack(h, device="cuda"):
@@ -88,6 +106,20 @@ def pack(h, device="cuda"):
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def hdr_struct(batch, n=None):
+    """cfc_hdr_v4 / cfc_hdr_v6 of a device batch (optionally its first n)."""
+    v6 = isinstance(batch, HeaderBatchV6)
+    return (L.HdrV6 if v6 else L.HdrV4)(
+        _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+        _ptr(batch.meta), _ptr(batch.mark), _ptr(batch.tcp_flags),
+        len(batch) if n is None else n)
+
+
+def out_struct(out):
+    return L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
+                 _ptr(out.ct), _ptr(out.notify))
 
 
 def _stream_handle(stream):
@@ -186,7 +218,7 @@ class Datapath:
                 "endpoint config")
 
     def set_node_config(self, ipv4_cluster_range, ipv4_cluster_mask,
-                        router_ip6):
+                        router_ip6, host_ifindex=1):
         """cfc_set_node_config: what the agent writes into node_config.h
         (daemon/daemon.go:916-934).  The IPv4 values are raw be32 (the
         header's %#x), router_ip6 is 16 bytes."""
@@ -194,13 +226,15 @@ class Datapath:
         c.ipv4_cluster_range = int(ipv4_cluster_range) & 0xFFFFFFFF
         c.ipv4_cluster_mask = int(ipv4_cluster_mask) & 0xFFFFFFFF
         c.router_ip6[:] = list(bytes(bytearray(router_ip6)))
+        c.host_ifindex = int(host_ifindex)
         L.check(self.L.cfc_set_node_config(self.h, ctypes.byref(c)),
                 "node config")
 
     def node_config(self):
         c = L.NodeConfig()
         L.check(self.L.cfc_get_node_config(self.h, ctypes.byref(c)), "node config")
-        return c.ipv4_cluster_range, c.ipv4_cluster_mask, bytes(c.router_ip6)
+        return (c.ipv4_cluster_range, c.ipv4_cluster_mask, bytes(c.router_ip6),
+                c.host_ifindex)
 
     # ------------------------------------------------ datapath
     def _stream(self, stream):
@@ -244,8 +278,9 @@ class Datapath:
             assert t.dtype == torch.int32
         if batch.mark is not None:
             assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
-        hdr = L.HdrV4(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
-                      _ptr(batch.meta), _ptr(batch.mark), n)
+        if batch.tcp_flags is not None:
+            assert batch.tcp_flags.numel() == n and batch.tcp_flags.dtype == torch.uint8
+        hdr = hdr_struct(batch)
         o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
                   _ptr(out.ct), _ptr(out.notify))
         L.check(self.L.cfc_classify_v4(self.h, ctypes.byref(hdr),
@@ -276,8 +311,9 @@ class Datapath:
             assert t.dtype == torch.int32
         if batch.mark is not None:
             assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
-        hdr = L.HdrV6(_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
-                      _ptr(batch.meta), _ptr(batch.mark), n)
+        if batch.tcp_flags is not None:
+            assert batch.tcp_flags.numel() == n and batch.tcp_flags.dtype == torch.uint8
+        hdr = hdr_struct(batch)
         o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
                   _ptr(out.ct), _ptr(out.notify))
         L.check(self.L.cfc_classify_v6(self.h, ctypes.byref(hdr),
@@ -298,11 +334,8 @@ class Datapath:
         flags — in header order.  Synchronises the stream."""
         assert out.ct is not None, "classify with want_ct=True"
         v6 = isinstance(batch, HeaderBatchV6)
-        hdr = (L.HdrV6 if v6 else L.HdrV4)(
-            _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
-            _ptr(batch.meta), _ptr(batch.mark), len(batch))
-        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct), _ptr(out.notify))
+        hdr = hdr_struct(batch)
+        o = out_struct(out)
         fn = self.L.cfc_ct_apply_v6 if v6 else self.L.cfc_ct_apply_v4
         L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
                    self._stream(stream)), "ct apply")
@@ -315,6 +348,16 @@ class Datapath:
         sync=True synchronises the device to read the total and trims the
         tensors to it; sync=False returns (records, indices, total as a
         1-element int64 device tensor) with nothing waited for."""
+        return self._events(batch, out, mode, ep_lxc, cap, stream, sync, False)
+
+    def monitor_events(self, batch, out: Verdicts, mode=L.MODE_INGRESS,
+                       ep_lxc=0, cap=None, stream=None, sync=True):
+        """cfc_monitor_events_v4/v6: every drop_notify and trace_notify
+        record of the batch in header order (32 bytes each, the `type` byte
+        tells them apart); returns as drop_notify does."""
+        return self._events(batch, out, mode, ep_lxc, cap, stream, sync, True)
+
+    def _events(self, batch, out, mode, ep_lxc, cap, stream, sync, traces):
         import torch
         assert out.notify is not None, "classify with want_notify=True"
         n = len(batch)
@@ -324,21 +367,23 @@ class Datapath:
         idx = torch.zeros(max(cap, 1), dtype=torch.int64, device=dev)
         cnt = torch.zeros(1, dtype=torch.int64, device=dev)
         v6 = isinstance(batch, HeaderBatchV6)
-        hdr = (L.HdrV6 if v6 else L.HdrV4)(
-            _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
-            _ptr(batch.meta), _ptr(batch.mark), n)
-        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct), _ptr(out.notify))
-        fn = self.L.cfc_drop_notify_v6 if v6 else self.L.cfc_drop_notify_v4
-        L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
-                   _ptr(rec), _ptr(idx), cap, _ptr(cnt), self._stream(stream)),
-                "drop notify")
+        if traces:
+            fn = self.L.cfc_monitor_events_v6 if v6 else self.L.cfc_monitor_events_v4
+        else:
+            fn = self.L.cfc_drop_notify_v6 if v6 else self.L.cfc_drop_notify_v4
+        L.check(fn(self.h, ctypes.byref(hdr_struct(batch)), ctypes.byref(out_struct(out)),
+                   mode, ep_lxc, _ptr(rec), _ptr(idx), cap, _ptr(cnt),
+                   self._stream(stream)), "monitor events")
         if not sync:
             return rec, idx, cnt
         torch.cuda.synchronize(dev)
         total = int(cnt.item())
         m = min(total, cap)
         return rec[:m], idx[:m], total
+
+    def set_clock(self, now):
+        """cfc_set_clock: bpf_ktime_get_sec() for the next calls."""
+        L.check(self.L.cfc_set_clock(self.h, int(now) & 0xFFFFFFFF), "clock")
 
     def counters_sync(self, stream=None):
         L.check(self.L.cfc_counters_sync(self.h, self._stream(stream)),

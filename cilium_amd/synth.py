@@ -102,6 +102,10 @@ class Headers:
     flags: np.ndarray                        # (n,) u1 HF_*
     length: np.ndarray                       # (n,) <u2 skb->len
     mark: np.ndarray                         # (n,) <u4 skb->mark
+    # (n,) u1 TCP header byte 13 (the flag bits ct_lookup accumulates into
+    # the CT entry's seen flags, conntrack.h:137-185); None = the default
+    # the packet builders use: FIN|ACK with HF_TCP_CLOSE, else SYN
+    tcpflags: np.ndarray = None
 
     def __len__(self):
         return len(self.proto)
@@ -109,7 +113,17 @@ class Headers:
     def slice(self, a, b):
         return Headers(self.family, self.saddr[a:b], self.daddr[a:b],
                        self.sport[a:b], self.dport[a:b], self.proto[a:b],
-                       self.flags[a:b], self.length[a:b], self.mark[a:b])
+                       self.flags[a:b], self.length[a:b], self.mark[a:b],
+                       None if self.tcpflags is None else self.tcpflags[a:b])
+
+
+def tcp_flags_of(h) -> np.ndarray:
+    """TCP header byte 13 of every header (0 for other protocols)."""
+    if h.tcpflags is not None:
+        return np.asarray(h.tcpflags, np.uint8)
+    tcp = np.asarray(h.proto) == IPPROTO_TCP
+    close = (np.asarray(h.flags) & HF_TCP_CLOSE) != 0
+    return np.where(tcp, np.where(close, 0x11, 0x02), 0).astype(np.uint8)
 
 
 def _v4_entries(addr_be32, plen, label):
@@ -627,14 +641,17 @@ def config_c2_bench(seed=2, n_prefilter=25_000):
 def take(h: Headers, idx) -> Headers:
     return Headers(h.family, h.saddr[idx], h.daddr[idx], h.sport[idx],
                    h.dport[idx], h.proto[idx], h.flags[idx], h.length[idx],
-                   h.mark[idx])
+                   h.mark[idx], None if h.tcpflags is None else h.tcpflags[idx])
 
 
 def concat(hs) -> Headers:
     f = hs[0].family
     cat = lambda k: np.concatenate([getattr(h, k) for h in hs])   # noqa: E731
+    tf = None
+    if any(h.tcpflags is not None for h in hs):
+        tf = np.concatenate([tcp_flags_of(h) for h in hs])
     return Headers(f, cat("saddr"), cat("daddr"), cat("sport"), cat("dport"),
-                   cat("proto"), cat("flags"), cat("length"), cat("mark"))
+                   cat("proto"), cat("flags"), cat("length"), cat("mark"), tf)
 
 
 def reverse(h: Headers) -> Headers:
@@ -677,11 +694,13 @@ def _zipf_ranks(rng, n_items, n, s=1.1):
 
 
 def ct_entries_v4(daddr, saddr, dport, sport, proto, flags, dir_ingress,
-                  length, src_sec_id, lxc=-1):
+                  length, src_sec_id, lxc=-1, now=0):
     """CT_DT records of flows as ct_create4 writes them (conntrack.h:
-    691-772): the flow's entry (tuple k2, rx or tx packets = 1, bytes = len,
-    src_sec_id) plus its ICMP 'related' entry ({daddr, saddr, 0, 0, ICMP,
-    flags | TUPLE_F_RELATED}, seen_non_syn) in the same map."""
+    691-772) at clock `now` (bpf_ktime_get_sec): the flow's entry (tuple k2,
+    rx or tx packets = 1, bytes = len, src_sec_id, lifetime now + 60 —
+    CT_SYN_TIMEOUT / CT_LIFETIME_NONTCP — and the direction's report time)
+    plus its ICMP 'related' entry ({daddr, saddr, 0, 0, ICMP, flags |
+    TUPLE_F_RELATED}, seen_non_syn) in the same map."""
     n = len(daddr)
     tu = np.zeros((n, 38), np.uint8)
     tu[:, 0:4] = be32_to_bytes(byteswap32(np.asarray(daddr, np.uint32)))
@@ -698,6 +717,12 @@ def ct_entries_v4(daddr, saddr, dport, sport, proto, flags, dir_ingress,
     ev[:, 2] = np.where(dir_ingress, 0, one)
     ev[:, 3] = np.where(dir_ingress, 0, length)
     ent[:, 44:48] = np.asarray(src_sec_id, np.uint32).view(np.uint8).reshape(n, 4)
+    ent[:, 32:36] = np.full(n, now + 60, np.uint32).view(np.uint8).reshape(n, 4)
+    if now > 5:   # __ct_update_timeout: last_report + 5 < now (from 0)
+        rep = np.full(n, now, np.uint32).view(np.uint8).reshape(n, 4)
+        ing = np.asarray(dir_ingress, bool)
+        ent[ing, 52:56] = rep[ing]       # last_rx_report
+        ent[~ing, 48:52] = rep[~ing]     # last_tx_report
     ct = np.zeros(2 * n, CT_DT)
     ct["family"] = 1
     ct["lxc"] = lxc
@@ -721,7 +746,7 @@ def ct_entries_v4(daddr, saddr, dport, sport, proto, flags, dir_ingress,
 
 
 def config_c5(seed=5, n_flows=10_000_000, n_prefixes=100_000, n_policy=16384,
-              n_prefilter=25_000):
+              n_prefilter=25_000, now=0):
     """C5: the C2 tables and prefilter plus n_flows live
     conntrack flows into / out of the endpoint (global CT maps), half opened
     from outside (ingress-created, TUPLE_F_IN) and half by the endpoint
@@ -753,7 +778,7 @@ def config_c5(seed=5, n_flows=10_000_000, n_prefixes=100_000, n_policy=16384,
                    EP_SECLABEL).astype(np.uint32)
     t.ct = ct_entries_v4(byteswap32(d), byteswap32(s), kd, ks, proto,
                          np.where(inbound, 1, 0).astype(np.uint8), inbound,
-                         length, sec)
+                         length, sec, now=now)
     flows = Headers(4, r_addr, c_addr, sport, dport, proto,
                     np.zeros(n_flows, np.uint8), length.astype(np.uint16),
                     np.zeros(n_flows, np.uint32))

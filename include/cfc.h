@@ -119,9 +119,19 @@ typedef struct {
     uint32_t ipv4_cluster_range;
     uint32_t ipv4_cluster_mask;
     uint8_t router_ip6[16];
+    uint32_t host_ifindex;    /* HOST_IFINDEX (trace records of proxy and
+                                 host deliveries); node_config.h: 1 */
 } cfc_node_config;
 int cfc_set_node_config(cfc_ctx *ctx, const cfc_node_config *cfg);
 int cfc_get_node_config(cfc_ctx *ctx, cfc_node_config *cfg);
+
+/* The datapath clock, bpf_ktime_get_sec(): seconds of CLOCK_MONOTONIC (or
+ * any clock the agent's CT garbage collector reads the same way,
+ * pkg/maps/ctmap/ctmap.go:272).  It stamps the CT entries' lifetimes and
+ * report times and decides which packets of an active flow are traced
+ * (conntrack.h:125-205, CT_REPORT_INTERVAL 5 s) for every classify and
+ * CT-apply call made after it returns.  A new context starts at 0. */
+int cfc_set_clock(cfc_ctx *ctx, uint32_t now_sec);
 
 /* Flatten the host tables into device layouts and publish them as the new
  * epoch.  Enqueued on `stream` (hipStream_t, NULL = default stream). */
@@ -165,13 +175,19 @@ int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
  * proto (bits 0-7), CFC_HF_* flags (bits 8-15) and skb->len (bits 16-31):
  * the batch format carries packets of at most 65535 bytes; a larger (GSO)
  * skb cannot be expressed and must be classified on the slow path.
- * `mark` (skb->mark, FROM_HOST identity) may be NULL = 0. */
+ * `mark` (skb->mark, FROM_HOST identity) may be NULL = 0.  `tcp_flags`
+ * (may be NULL = 0) is TCP header byte 13 of each header (FIN SYN RST PSH
+ * ACK ...): ct_lookup accumulates it into the CT entry's seen flags and
+ * traces a packet whose flags the flow had not seen (conntrack.h:137-185);
+ * the close bit in meta is byte 12's bit 0, which union tcp_flags reads as
+ * rst/fin/syn alike. */
 typedef struct {
     const uint32_t *saddr;
     const uint32_t *daddr;
     const uint32_t *ports;
     const uint32_t *meta;
     const uint32_t *mark;
+    const uint8_t *tcp_flags;   /* may be NULL = 0 */
     uint64_t n;
 } cfc_hdr_v4;
 
@@ -188,6 +204,7 @@ typedef struct {
     const uint32_t *ports;
     const uint32_t *meta;
     const uint32_t *mark;
+    const uint8_t *tcp_flags;
     uint64_t n;
 } cfc_hdr_v6;
 
@@ -216,20 +233,36 @@ typedef struct {
 #define CFC_CT_RES_MASK 0x3u
 #define CFC_CT_DONE 0x4u
 #define CFC_CT_CREATE 0x8u
-/*  notify  : (may be NULL) which send_drop_notify (bpf/lib/drop.h:94-109) the
- *            reference ran for the header: 0 none (forwarded, redirected,
- *            XDP prefilter drop — bpf_xdp.c notifies nothing — or punt), else
- *            site << 16 | EVENT_SOURCE (the LXC_ID of the program that
- *            dropped).  Sites: CFC_NT_NETDEV bpf_netdev's
- *            send_drop_notify_error (bpf_netdev.c:463,502; no identities),
- *            CFC_NT_EGRESS the sending endpoint's (SECLABEL, dstID, 0, 0)
- *            (bpf_lxc.c:432,700), CFC_NT_POLICY the destination endpoint's
- *            tail_ipv{4,6}_policy (src_label, SECLABEL, LXC_ID, ifindex)
- *            (bpf_lxc.c:891,1024).  cfc_drop_notify_v4/v6 turn it into
- *            records. */
+/*  notify  : (may be NULL) the monitor event the reference sent on its perf
+ *            ring cilium_events for the header — at most one per header:
+ *            0 none, else EVENT_SOURCE (the LXC_ID of the program that sent
+ *            it, 0 for bpf_netdev) | kind << 16 with kind
+ *              CFC_NT_NETDEV  drop: bpf_netdev's send_drop_notify_error
+ *                             (bpf_netdev.c:463,502; no identities)
+ *              CFC_NT_EGRESS  drop: the sending endpoint's send_drop_notify
+ *                             (SECLABEL, dstID, 0, 0) (bpf_lxc.c:432,700)
+ *              CFC_NT_POLICY  drop: the destination's tail_ipv{4,6}_policy
+ *                             (src_label, SECLABEL, LXC_ID, ifindex)
+ *                             (bpf_lxc.c:891,1024)
+ *              CFC_NT_TRACE + obs   send_trace_notify at observation point
+ *                             obs (TRACE_TO_LXC 0, TO_PROXY 1, TO_HOST 2,
+ *                             TO_STACK 3; trace.h:37-48, call sites
+ *                             bpf_lxc.c:373,390,668,687,873,1006, lxc.h:117,
+ *                             169), with the CT result as reason in bits
+ *                             20-21 and the monitor length in bits 22-23
+ *                             (1 TRACE_PAYLOAD_LEN, 2 MTU, 3 one byte: an
+ *                             active flow's periodic report, ct_update_timeout
+ *                             returns bool, conntrack.h:191).
+ *            No event: forwarded packets the reference does not trace (to
+ *            the stack from bpf_netdev; FROM_* points and flows inside their
+ *            report interval under MONITOR_AGGREGATION 5), XDP prefilter
+ *            drops (bpf_xdp.c notifies nothing), punts.
+ *            cfc_drop_notify_v4/v6 turn the drops into records,
+ *            cfc_monitor_events_v4/v6 every event. */
 #define CFC_NT_NETDEV 1u
 #define CFC_NT_EGRESS 2u
 #define CFC_NT_POLICY 3u
+#define CFC_NT_TRACE 4u
 typedef struct {
     int32_t *verdict;
     uint32_t *identity;
@@ -313,6 +346,38 @@ int cfc_drop_notify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
                        int mode, uint16_t ep_lxc, cfc_drop_notify *records,
                        uint64_t *hdr_index, uint64_t cap, uint64_t *count,
                        void *stream);
+
+/* struct trace_notify (bpf/lib/trace.h:71-81) as send_trace_notify
+ * (:97-155) fills it; pkg/monitor decodes it (datapath_trace.go:28-40
+ * TraceNotify).  32 bytes, like cfc_drop_notify: the `type` byte tells a
+ * record of cfc_monitor_events apart. */
+#define CFC_NOTIFY_TRACE 4         /* CILIUM_NOTIFY_TRACE (common.h:214) */
+typedef struct {
+    uint8_t type;        /* CFC_NOTIFY_TRACE */
+    uint8_t subtype;     /* observation point TRACE_TO_* */
+    uint16_t source;     /* EVENT_SOURCE */
+    uint32_t hash;       /* symmetric flow hash (see cfc_drop_notify) */
+    uint32_t len_orig;
+    uint32_t len_cap;    /* min(monitor length, len_orig) */
+    uint32_t src_label;  /* full 32-bit identities */
+    uint32_t dst_label;
+    uint16_t dst_id;
+    uint8_t reason;      /* TRACE_REASON_*: the CT result */
+    uint8_t pad;
+    uint32_t ifindex;
+} cfc_trace_notify;
+
+/* Every monitor event of one classified batch (out->notify set) — drop and
+ * trace records, 32 bytes each, in header order — as the perf ring
+ * cilium_events would carry them; otherwise as cfc_drop_notify_v4/v6. */
+int cfc_monitor_events_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
+                          int mode, uint16_t ep_lxc, void *records,
+                          uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                          void *stream);
+int cfc_monitor_events_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
+                          int mode, uint16_t ep_lxc, void *records,
+                          uint64_t *hdr_index, uint64_t cap, uint64_t *count,
+                          void *stream);
 
 /* ---------------------------------------------------------------- counters */
 /* The device counter block is a flat u64 array:

@@ -216,6 +216,81 @@ class Loader:
         self.progs.clear()
 
 
+# ------------------------------------------------------------ perf ring
+# The datapath's notifications go to the perf event array cilium_events
+# (bpf/lib/events.h:23-29) through skb_event_output(..., BPF_F_CURRENT_CPU):
+# send_trace_notify (trace.h:97-155) and __send_drop_notify (drop.h:50-78).
+# PerfRing opens a PERF_COUNT_SW_BPF_OUTPUT event on one CPU, maps its ring
+# and hands out the raw samples; the caller pins itself to that CPU so every
+# BPF_PROG_TEST_RUN lands there.
+_NR_perf_event_open = 298
+PERF_TYPE_SOFTWARE, PERF_COUNT_SW_BPF_OUTPUT = 1, 10
+PERF_SAMPLE_RAW = 1 << 10
+PERF_RECORD_LOST, PERF_RECORD_SAMPLE = 2, 9
+PERF_FLAG_FD_CLOEXEC = 8
+
+
+def pin_cpu():
+    """Pin this process to its first allowed CPU (< __NR_CPUS__ 8, the size
+    of cilium_events) and return it."""
+    cpu = min(c for c in os.sched_getaffinity(0) if c < 8)
+    os.sched_setaffinity(0, {cpu})
+    return cpu
+
+
+class PerfRing:
+    def __init__(self, cpu, pages=256):
+        import mmap
+        self.cpu = cpu
+        attr = bytearray(128)
+        struct.pack_into("<IIQQQ", attr, 0, PERF_TYPE_SOFTWARE, 128,
+                         PERF_COUNT_SW_BPF_OUTPUT, 1, PERF_SAMPLE_RAW)
+        struct.pack_into("<I", attr, 48, 1)        # wakeup_events
+        ab = ctypes.create_string_buffer(bytes(attr), 128)
+        fd = _libc.syscall(_NR_perf_event_open, ab, -1, cpu, -1,
+                           PERF_FLAG_FD_CLOEXEC)
+        if fd < 0:
+            e = ctypes.get_errno()
+            raise BpfError(e, f"perf_event_open: {os.strerror(e)}")
+        self.fd = fd
+        self.psz = mmap.PAGESIZE
+        self.size = pages * self.psz
+        self.mm = mmap.mmap(fd, self.psz + self.size, mmap.MAP_SHARED,
+                            mmap.PROT_READ | mmap.PROT_WRITE)
+        self.lost = 0
+
+    def read(self):
+        """-> list of raw sample payloads (bytes) since the last read."""
+        mm = self.mm
+        head, = struct.unpack_from("<Q", mm, 1024)
+        tail, = struct.unpack_from("<Q", mm, 1032)
+        out = []
+        base = self.psz
+        while tail < head:
+            off = tail % self.size
+            hdr = self._bytes(base, off, 8)
+            typ, misc, sz = struct.unpack("<IHH", hdr)
+            rec = self._bytes(base, off, sz)
+            if typ == PERF_RECORD_SAMPLE:
+                n, = struct.unpack_from("<I", rec, 8)
+                out.append(rec[12:12 + n])
+            elif typ == PERF_RECORD_LOST:
+                self.lost += struct.unpack_from("<Q", rec, 16)[0]
+            tail += sz
+        struct.pack_into("<Q", mm, 1032, tail)
+        return out
+
+    def _bytes(self, base, off, n):
+        a = self.mm[base + off: base + min(off + n, self.size)]
+        if len(a) < n:
+            a += self.mm[base: base + n - len(a)]
+        return bytes(a)
+
+    def close(self):
+        self.mm.close()
+        os.close(self.fd)
+
+
 def test_run_skb(prog_fd, pkt: bytes, mark=0, cb=(0, 0, 0, 0, 0)):
     """One BPF_PROG_TEST_RUN of a tc program. Returns (retval, cb_out, pkt_out)."""
     pin = ctypes.create_string_buffer(pkt, len(pkt))

@@ -210,6 +210,14 @@ _Static_assert(sizeof(struct ctent) == 56, "ct_entry is 56 bytes");
 #define CTB_RX_CLOSING 1u
 #define CTB_TX_CLOSING 2u
 #define CTB_SEEN_NON_SYN 16u
+/* conntrack.h:31-35, common.h:224, node_config.h:69 */
+#define CT_LIFETIME_TCP 21600u
+#define CT_LIFETIME_NONTCP 60u
+#define CT_SYN_TIMEOUT 60u
+#define CT_CLOSE_TIMEOUT 10u
+#define CT_REPORT_INTERVAL 5u
+#define TRACE_PAYLOAD_LEN 128u
+#define MTU 1500u
 
 /* CT map key as the oracle stores it: u16 owner (0 = the global maps
  * cilium_ct{4,_any4,6,_any6}_global, else lxc_id + 1 for the endpoint's
@@ -344,6 +352,9 @@ struct cfo {
      * [dir 0 ingress / 1 egress][identity, >= 65536 in the last slot]
      * [fwd, drop][packets, bytes] */
     uint64_t *idc;
+    uint32_t host_ifindex;     /* node_config.h HOST_IFINDEX */
+    uint32_t now;              /* bpf_ktime_get_sec() of the batch (cfo_set_clock) */
+    uint32_t *notify_mon;      /* cfo_set_notify_out: per-header monitor lengths */
 };
 #define ID_SLOTS 65537u
 
@@ -376,17 +387,21 @@ cfo_t *cfo_new(void)
     /* bpf/node_config.h:30,42-43 */
     static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0,
                                        0, 0, 0, 1, 0, 1, 0, 0};
-    cfo_node_config(o, 0x100000u, 0xff0000u, router);
+    cfo_node_config(o, 0x100000u, 0xff0000u, router, 1);
     return o;
 }
 
 void cfo_node_config(cfo_t *o, uint32_t v4_cluster_range,
-                     uint32_t v4_cluster_mask, const uint8_t router_ip6[16])
+                     uint32_t v4_cluster_mask, const uint8_t router_ip6[16],
+                     uint32_t host_ifindex)
 {
     o->v4_cluster_range = v4_cluster_range;
     o->v4_cluster_mask = v4_cluster_mask;
     memcpy(o->router_ip6, router_ip6, 16);
+    o->host_ifindex = host_ifindex;
 }
+
+void cfo_set_clock(cfo_t *o, uint32_t now) { o->now = now; }
 
 void cfo_free(cfo_t *o)
 {
@@ -606,14 +621,32 @@ typedef struct {
 #define NT_NETDEV 1u
 #define NT_EGRESS 2u
 #define NT_POLICY 3u
+/* The monitor event of a header (cfc.h CFC_NT_*): bits 0-15 EVENT_SOURCE,
+ * bits 16-19 the kind — drop sites 1-3 above, or a trace_notify at
+ * observation point kind - 4 (TRACE_TO_LXC 4, TO_PROXY 5, TO_HOST 6,
+ * TO_STACK 7; trace.h:37-48) — and for traces bits 20-21 the reason (the CT
+ * result, trace.h:51-56) and bits 22-23 the monitor length: 1 =
+ * TRACE_PAYLOAD_LEN, 2 = MTU, 3 = 1 (an active flow's report).  With MONITOR_AGGREGATION 5 (node_config.h:68)
+ * the FROM_* points and every trace whose monitor length is 0 are not sent
+ * (trace.h:119-132); no header has more than one event. */
+#define NT_TRACE 4u
+enum { OBS_TO_LXC = 0, OBS_TO_PROXY = 1, OBS_TO_HOST = 2, OBS_TO_STACK = 3 };
+
+static uint32_t trace_word(uint32_t obs, uint16_t source, int reason, uint32_t mon)
+{
+    if (!mon)
+        return 0;
+    return (NT_TRACE + obs) << 16 | source | (uint32_t)reason << 20 |
+           (mon == MTU ? 2u : mon == 1 ? 3u : 1u) << 22;
+}
 
 /* sites 1-2 follow from the mode; lxc_ingress sets site 3 itself */
 static uint32_t notify_site(int mode, uint16_t ep_lxc, const res_t *r)
 {
-    if (r->verdict >= 0 || r->verdict == -1 || r->verdict == -2)
-        return 0; /* forwarded / XDP prefilter drop / VERDICT_PUNT */
-    if (r->nt)
-        return r->nt;
+    if (r->verdict == -1 || r->verdict == -2)
+        return 0; /* XDP prefilter drop / VERDICT_PUNT */
+    if (r->verdict >= 0 || r->nt)
+        return r->nt; /* a trace (or nothing), or the policy drop site */
     return mode == CFO_MODE_EGRESS ? NT_EGRESS << 16 | ep_lxc : NT_NETDEV << 16;
 }
 
@@ -624,6 +657,72 @@ static uint32_t notify_site(int mode, uint16_t ep_lxc, const res_t *r)
  * only in the CT port derivation and pass is_fragment = false. */
 /* CT byte of the current header (CTO_*) */
 static _Thread_local uint8_t tl_ct;
+/* the current header's TCP flag byte (byte 13) and the monitor length each
+ * CT stage's lookup returned (0 / TRACE_PAYLOAD_LEN / MTU) */
+static _Thread_local uint8_t tl_tcpfl;
+static _Thread_local uint32_t tl_mon[2];
+
+/* __ct_update_timeout (conntrack.h:125-185): the lifetime, and whether this
+ * packet is reported (the flow's report interval passed, or it carries TCP
+ * flags the direction has not seen) */
+static uint32_t ct_upd(struct ctent *e, uint32_t now, uint32_t lifetime, int dir,
+                       uint8_t flags)
+{
+    e->lifetime = now + lifetime;
+    uint8_t *acc = dir == CT_INGRESS ? &e->rx_flags_seen : &e->tx_flags_seen;
+    uint32_t *last = dir == CT_INGRESS ? &e->last_rx_report : &e->last_tx_report;
+    const uint8_t seen = (uint8_t)(flags | *acc);
+    if (*last + CT_REPORT_INTERVAL < now || *acc != seen) {
+        *last = now;
+        *acc = seen;
+        return TRACE_PAYLOAD_LEN;
+    }
+    return 0;
+}
+
+/* ct_update_timeout (:191-205); syn is bit 0 of TCP byte 12, which every
+ * bitfield of union tcp_flags aliases (:92-104).  It is declared bool, so
+ * the monitor length it hands __ct_lookup is 1, not TRACE_PAYLOAD_LEN: a
+ * reported packet of an active flow captures one byte. */
+static uint32_t ct_upd_timeout(struct ctent *e, uint32_t now, int is_tcp, int dir,
+                               int syn, uint8_t flags)
+{
+    uint32_t lifetime = CT_LIFETIME_NONTCP;
+    if (is_tcp) {
+        if (!syn)
+            e->bits |= CTB_SEEN_NON_SYN;
+        lifetime = (e->bits & CTB_SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+    }
+    return ct_upd(e, now, lifetime, dir, flags) != 0;
+}
+
+static int ct_alive(const struct ctent *e)
+{
+    return !(e->bits & CTB_RX_CLOSING) || !(e->bits & CTB_TX_CLOSING);
+}
+
+/* What __ct_lookup (:221-285) does to a hit entry (timeouts, report
+ * timestamps, seen flags, closing bits; the accounting is counted apart),
+ * returning *monitor */
+static uint32_t ct_hit_entry(struct ctent *e, uint32_t now, int action, int dir,
+                             int is_tcp, int syn, uint8_t flags)
+{
+    uint32_t m = 0;
+    if (ct_alive(e))
+        m = ct_upd_timeout(e, now, is_tcp, dir, syn, flags);
+    if (action == ACTION_CREATE) {
+        if (e->bits & (CTB_RX_CLOSING | CTB_TX_CLOSING)) {
+            e->bits &= (uint16_t)~(CTB_RX_CLOSING | CTB_TX_CLOSING);
+            m = ct_upd_timeout(e, now, is_tcp, dir, syn, flags);
+        }
+    } else if (action == ACTION_CLOSE) {
+        e->bits |= dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING;
+        m = TRACE_PAYLOAD_LEN;
+        if (!ct_alive(e))
+            ct_upd(e, now, CT_CLOSE_TIMEOUT, dir, flags);
+    }
+    return m;
+}
 
 /* ct_lookup{4,6} against the tables as they were when the batch started:
  * sets *res and the policy port (tuple->dport after the lookup: the
@@ -644,15 +743,28 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
      * entries (an empty map cannot change a verdict) */
     if (o->ct_added)
         tl_lookups++;
-    if (ct_find(o, k1) >= 0) {
+    /* *monitor (conntrack.h:221-285, 587-589) against the entry as
+     * committed: the batch's own updates are applied afterwards (ct_apply) */
+    int64_t e = ct_find(o, k1);
+    if (e >= 0) {
         *res = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
         *pdport = td;
     } else {
         if (o->ct_added)
             tl_lookups++;
-        *res = ct_find(o, k2) >= 0 ? CT_ESTABLISHED : CT_NEW;
+        e = ct_find(o, k2);
+        *res = e >= 0 ? CT_ESTABLISHED : CT_NEW;
         *pdport = ts;
     }
+    uint32_t mon = TRACE_PAYLOAD_LEN;
+    if (e >= 0) {
+        struct ctent copy = o->ct_ents[e];
+        mon = ct_hit_entry(&copy, o->now, action, dir, proto == 6, close,
+                           proto == 6 ? tl_tcpfl : 0);
+    }
+    if (*pdport == 0x3500)   /* conn_is_dns: tuple->dport == htons(53) */
+        mon = MTU;
+    tl_mon[stage] = mon;
     tl_ct |= (uint8_t)((*res | 4) << (4 * stage));
     return 0;
 }
@@ -703,14 +815,17 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     if (res == CT_NEW)
         tl_ct |= (uint8_t)(CTO_CREATE1 << (4 * stage));   /* ct_create4 */
     if (verdict > 0 && (res == CT_NEW || res == CT_ESTABLISHED)) {
-        /* redirect_to_proxy: cb[CB_IFINDEX] = HOST_IFINDEX */
+        /* redirect_to_proxy: cb[CB_IFINDEX] = HOST_IFINDEX; TRACE_TO_PROXY
+         * from ipv4_redirect_to_host_port (lxc.h:117) */
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
+        r.nt = trace_word(OBS_TO_PROXY, ep->lxc_id, res, tl_mon[stage]);
         return r;
     }
     metric(o, 0, METRIC_INGRESS, len); /* send_trace_notify(TRACE_TO_LXC) */
     r.action = ep->ifindex ? TC_ACT_REDIRECT : TC_ACT_OK;
     r.verdict = 0;
+    r.nt = trace_word(OBS_TO_LXC, ep->lxc_id, res, tl_mon[stage]);   /* :1006 */
     return r;
 }
 
@@ -795,14 +910,16 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     if (verdict > 0) { /* proxy: redirect(HOST_IFINDEX), TRACE_TO_PROXY */
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
+        r.nt = trace_word(OBS_TO_PROXY, lxc, res, tl_mon[0]);
         return r;
     }
     tl_lookups++;
     const epinfo *ep = lxc_lookup(o, 1, da);
     if (ep) {
-        if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST */
+        if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST, :668 */
             metric(o, 0, METRIC_EGRESS, len);
             r.action = TC_ACT_REDIRECT;
+            r.nt = trace_word(OBS_TO_HOST, lxc, res, tl_mon[0]);
             return r;
         }
         /* ipv4_local_delivery (l3.h:103-131): egress forward metric, then
@@ -816,6 +933,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     }
     metric(o, 0, METRIC_EGRESS, len); /* pass_to_stack: TRACE_TO_STACK */
     r.action = TC_ACT_OK;
+    r.nt = trace_word(OBS_TO_STACK, lxc, res, tl_mon[0]);   /* :687 */
     return r;
 }
 
@@ -846,8 +964,9 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
-                     int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, uint8_t *ct, int nthreads)
+                     const uint8_t *tcpflags, int32_t *action, int32_t *verdict,
+                     uint32_t *identity, uint8_t *lookups, uint8_t *ct,
+                     int nthreads)
 {
     if (nthreads <= 0)
         nthreads = 1;
@@ -856,6 +975,8 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         res_t r;
         tl_lookups = 0;
         tl_ct = 0;
+        tl_tcpfl = tcpflags ? tcpflags[i] : 0;
+        tl_mon[0] = tl_mon[1] = 0;
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v4(o, saddr[i], daddr[i]);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -868,6 +989,8 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                     ct[i] = 0;
                 if (o->notify_out)
                     o->notify_out[i] = 0;
+                if (o->notify_mon)
+                    o->notify_mon[i] = 0;
                 continue;
             }
         }
@@ -887,6 +1010,8 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             ct[i] = tl_ct;
         if (o->notify_out)
             o->notify_out[i] = notify_site(mode, ep_lxc, &r);
+        if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
+            o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
     }
 }
 
@@ -1002,19 +1127,24 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
         metric(o, DROP_POLICY, METRIC_EGRESS, len);
         return r;
     }
+    /* after ct_create6 the v6 egress path sets monitor = TRACE_PAYLOAD_LEN
+     * (bpf_lxc.c:248), so a new DNS flow is not captured at MTU */
+    const uint32_t mon = res == CT_NEW ? TRACE_PAYLOAD_LEN : tl_mon[0];
     if (res == CT_NEW)
         tl_ct |= CTO_CREATE1;                       /* ct_create6, :237-249 */
     if (verdict > 0) {
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
+        r.nt = trace_word(OBS_TO_PROXY, lxc, res, mon);
         return r;
     }
     tl_lookups++;
     const epinfo *ep = lxc_lookup(o, 2, daddr);
     metric(o, 0, METRIC_EGRESS, len); /* to_host / local / to_stack */
     if (ep) {
-        if (ep->flags & ENDPOINT_F_HOST) {
+        if (ep->flags & ENDPOINT_F_HOST) {   /* TRACE_TO_HOST, :373 */
             r.action = TC_ACT_REDIRECT;
+            r.nt = trace_word(OBS_TO_HOST, lxc, res, mon);
             return r;
         }
         res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 16, saddr, daddr, proto,
@@ -1024,6 +1154,7 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
         return d;
     }
     r.action = TC_ACT_OK;
+    r.nt = trace_word(OBS_TO_STACK, lxc, res, mon);   /* :390 */
     return r;
 }
 
@@ -1051,8 +1182,9 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
-                     int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, uint8_t *ct, int nthreads)
+                     const uint8_t *tcpflags, int32_t *action, int32_t *verdict,
+                     uint32_t *identity, uint8_t *lookups, uint8_t *ct,
+                     int nthreads)
 {
     if (nthreads <= 0)
         nthreads = 1;
@@ -1062,6 +1194,8 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         const uint8_t *sa = saddr + 16 * i, *da = daddr + 16 * i;
         tl_lookups = 0;
         tl_ct = 0;
+        tl_tcpfl = tcpflags ? tcpflags[i] : 0;
+        tl_mon[0] = tl_mon[1] = 0;
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v6(o, sa, da);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -1074,6 +1208,8 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                     ct[i] = 0;
                 if (o->notify_out)
                     o->notify_out[i] = 0;
+                if (o->notify_mon)
+                    o->notify_mon[i] = 0;
                 continue;
             }
         }
@@ -1092,10 +1228,16 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             ct[i] = tl_ct;
         if (o->notify_out)
             o->notify_out[i] = notify_site(mode, ep_lxc, &r);
+        if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
+            o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
     }
 }
 
-void cfo_set_notify_out(cfo_t *o, uint32_t *words) { o->notify_out = words; }
+void cfo_set_notify_out(cfo_t *o, uint32_t *words, uint32_t *mon)
+{
+    o->notify_out = words;
+    o->notify_mon = mon;
+}
 
 int cfo_policy_create(cfo_t *o, uint16_t lxc_id)
 {
@@ -1244,16 +1386,13 @@ int cfo_ct_add_n(cfo_t *o, size_t n, const uint8_t *rec)
     return 0;
 }
 
-/* The deterministic part of __ct_lookup's entry update (conntrack.h:221-285):
- * the per-direction packet/byte accounting, ACTION_CREATE re-opens a
- * closing entry, ACTION_CLOSE marks the direction closing.  Lifetimes, report timestamps, seen TCP flags and seen_non_syn
- * depend on the clock or on TCP flag bits the header batch does not carry
- * and are not modelled. */
-static void ct_hit_update(struct ctent *e, int action, int dir, uint32_t len)
+/* A hit's entry update (__ct_lookup, conntrack.h:221-285) applied in header
+ * order, plus CONNTRACK_ACCOUNTING (lxc_config.h:50, :247-257) for a hit
+ * the batch's lookup did not see (len 0: counted in pass 1).  Returns the
+ * monitor length the reference's lookup would have produced. */
+static uint32_t ct_hit_update(cfo_t *o, struct ctent *e, int action, int dir,
+                              int is_tcp, int syn, uint8_t flags, uint32_t len)
 {
-    /* CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257) for a hit
-     * the batch lookup did not see (a flow created earlier in the batch);
-     * len 0 = already counted in pass 1 */
     if (len && dir == CT_INGRESS) {
         e->rx_packets++;
         e->rx_bytes += len;
@@ -1261,17 +1400,17 @@ static void ct_hit_update(struct ctent *e, int action, int dir, uint32_t len)
         e->tx_packets++;
         e->tx_bytes += len;
     }
-    if (action == ACTION_CREATE)
-        e->bits &= (uint16_t)~(CTB_RX_CLOSING | CTB_TX_CLOSING);
-    else if (action == ACTION_CLOSE)
-        e->bits |= dir == CT_INGRESS ? CTB_RX_CLOSING : CTB_TX_CLOSING;
+    return ct_hit_entry(e, o->now, action, dir, is_tcp, syn, flags);
 }
 
 /* ct_create4 / ct_create6 (conntrack.h:615-662, :691-772) without a load
  * balancer (ct_state->addr == 0): the k2 entry plus the ICMP entry that
- * relates errors to it, written into the same map.  ipv6_policy derives
- * ct_state_new.rev_nat_index from the low 16 bits of daddr.s6_addr32[3]
- * (bpf_lxc.c:787-788), so IPv6 ingress entries carry it. */
+ * relates errors to it, written into the same map.  ct_update_timeout runs
+ * with seen_flags.syn = is_tcp — bit 0 of the union, so lower_bits stays 0
+ * and a TCP entry keeps seen_non_syn clear (CT_SYN_TIMEOUT).  ipv6_policy
+ * derives ct_state_new.rev_nat_index from the low 16 bits of
+ * daddr.s6_addr32[3] (bpf_lxc.c:787-788), so IPv6 ingress entries carry
+ * it. */
 static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
                       uint32_t len, uint32_t src_sec_id, uint16_t rev_nat)
 {
@@ -1279,9 +1418,8 @@ static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
     memset(&e, 0, sizeof(e));
     e.rev_nat_index = rev_nat;
     const uint8_t *t = k2 + 4;
-    /* ct_update_timeout with seen_flags.syn = is_tcp: syn shares bit 0 of
-     * the union with every other flag bitfield (conntrack.h:86-99), so the
-     * seen-flags byte (lower_bits) stays 0 and seen_non_syn stays clear */
+    const int is_tcp = t[2 * alen + 4] == 6;
+    ct_upd_timeout(&e, o->now, is_tcp, dir, is_tcp, 0);
     if (dir == CT_INGRESS) {
         e.rx_packets = 1;
         e.rx_bytes = len;
@@ -1296,27 +1434,29 @@ static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
     memcpy(&owner, k2, 2);
     ct_key(ki, owner, k2[2], alen, t, t + alen, 0, 0, alen == 4 ? 1 : 58,
            (uint8_t)(t[2 * alen + 5] | TUPLE_F_RELATED));
-    e.bits |= CTB_SEEN_NON_SYN;
+    e.bits |= CTB_SEEN_NON_SYN;   /* "For ICMP, there is no SYN" */
     ct_put(o, ki, &e);
 }
 
 /* Fold one classified batch into the CT maps, in header order, as the
- * engine does between batches: the CT result of every lookup stage was
- * taken against the maps as they were when the batch started (ct[]), and
- * the creates (ct_create), deletes (ct_delete on a denied CT_ESTABLISHED
- * flow) and closing-bit updates are applied here.  A flow created twice in
- * one batch is created once (the reference sees its second packet as
- * CT_ESTABLISHED).  hazard[i] (optional) = 1 when the reference, running
- * the batch one packet at a time, would have seen a different CT result for
- * header i because of an earlier header of the same batch — streams used for
- * golden vectors drop those headers. */
+ * engine does between batches: the CT result (and the monitor length) of
+ * every lookup stage was taken against the maps as they were when the
+ * batch started (ct[], mon[]), and the entry updates of the hits, the
+ * creates (ct_create), deletes (ct_delete on a denied CT_ESTABLISHED flow)
+ * and closing-bit / timeout updates are applied here, at the batch's clock.
+ * A flow created twice in one batch is created once (the reference sees its
+ * second packet as CT_ESTABLISHED).  hazard[i] (optional) = 1 when the
+ * reference, running the batch one packet at a time, would have seen a
+ * different CT result or monitor length for header i because of an earlier
+ * header of the same batch — streams used for golden vectors drop those
+ * headers. */
 static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *saddr, const uint8_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
-                     const uint16_t *len, const uint32_t *identity,
-                     const int32_t *verdict, const uint8_t *ct,
-                     uint8_t *hazard)
+                     const uint16_t *len, const uint8_t *tcpflags,
+                     const uint32_t *identity, const int32_t *verdict,
+                     const uint8_t *ct, const uint32_t *mon, uint8_t *hazard)
 {
     /* pass 1 counts every hit of the batch on the entry it hit (the maps as
      * committed); pass 2 applies the writes in header order.  The reference
@@ -1335,6 +1475,9 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
         const uint8_t *da = daddr + (size_t)alen * i;
         const epinfo *dst = lxc_lookup(o, alen == 4 ? 1 : 2, da);
         const int last = (c & CTO_DONE2) ? 1 : 0;
+        const int is_tcp = proto[i] == 6;
+        const int syn = (flags[i] & HF_TCP_CLOSE) != 0;
+        const uint8_t fl = is_tcp && tcpflags ? tcpflags[i] : 0;
         for (int s = 0; s < 2; s++) {
             const uint8_t cs = (uint8_t)(c >> (4 * s));
             if (!(cs & CTO_DONE1))
@@ -1349,8 +1492,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             int action;
             uint16_t td, ts;
             if (ct_keys(alen, owner, sa, da, proto[i], sport[i], dport[i],
-                        flags[i] & HF_TCP_CLOSE, dir, k1, k2, &action, &td,
-                        &ts) < 0)
+                        syn, dir, k1, k2, &action, &td, &ts) < 0)
                 continue;
             const int b = cs & 3;
             const int64_t e1 = ct_find(o, k1), e2 = ct_find(o, k2);
@@ -1377,12 +1519,14 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                           : e2 >= 0 ? CT_ESTABLISHED : CT_NEW;
             if (hazard && q != b && !(b == CT_NEW && q == CT_ESTABLISHED && created))
                 hazard[i] = 1;
+            /* the monitor length a packet-at-a-time lookup would return */
+            uint32_t m = TRACE_PAYLOAD_LEN;
             if (b == CT_REPLY || b == CT_RELATED) {
                 if (e1 >= 0)
-                    ct_hit_update(&o->ct_ents[e1], action, dir, 0);
+                    m = ct_hit_update(o, &o->ct_ents[e1], action, dir, is_tcp, syn, fl, 0);
             } else if (b == CT_ESTABLISHED) {
                 if (e2 >= 0) {
-                    ct_hit_update(&o->ct_ents[e2], action, dir, 0);
+                    m = ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl, 0);
                     if (dropped) {
                         if (hit_idx && hit_idx[e2] > i + 1)
                             hazard[hit_idx[e2] - 1] = 1;  /* hit after delete */
@@ -1391,7 +1535,8 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 }
             } else if (created) {
                 if (e2 >= 0) {
-                    ct_hit_update(&o->ct_ents[e2], action, dir, len[i]);
+                    m = ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl,
+                                      len[i]);
                 } else {
                     if (hit_idx) {   /* the ICMP entry it overwrites */
                         uint8_t ki[CTK];
@@ -1409,6 +1554,11 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                                   ? (uint16_t)(da[12] | da[13] << 8) : 0);
                 }
             }
+            const uint16_t pdport = q >= CT_REPLY ? td : ts;
+            if (pdport == 0x3500)
+                m = MTU;
+            if (hazard && mon && m != ((mon[i] >> (16 * s)) & 0xFFFF))
+                hazard[i] = 1;
         }
     }
     free(hit_idx);
@@ -1418,25 +1568,25 @@ void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint32_t *saddr, const uint32_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
-                     const uint16_t *len, const uint32_t *identity,
-                     const int32_t *verdict, const uint8_t *ct,
-                     uint8_t *hazard)
+                     const uint16_t *len, const uint8_t *tcpflags,
+                     const uint32_t *identity, const int32_t *verdict,
+                     const uint8_t *ct, const uint32_t *mon, uint8_t *hazard)
 {
     ct_apply(o, 4, mode, ep_lxc, n, (const uint8_t *)saddr,
-             (const uint8_t *)daddr, sport, dport, proto, flags, len, identity,
-             verdict, ct, hazard);
+             (const uint8_t *)daddr, sport, dport, proto, flags, len, tcpflags,
+             identity, verdict, ct, mon, hazard);
 }
 
 void cfo_ct_apply_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *saddr, const uint8_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
-                     const uint16_t *len, const uint32_t *identity,
-                     const int32_t *verdict, const uint8_t *ct,
-                     uint8_t *hazard)
+                     const uint16_t *len, const uint8_t *tcpflags,
+                     const uint32_t *identity, const int32_t *verdict,
+                     const uint8_t *ct, const uint32_t *mon, uint8_t *hazard)
 {
     ct_apply(o, 16, mode, ep_lxc, n, saddr, daddr, sport, dport, proto, flags,
-             len, identity, verdict, ct, hazard);
+             len, tcpflags, identity, verdict, ct, mon, hazard);
 }
 
 static int cmp_ctrow(const void *a, const void *b)

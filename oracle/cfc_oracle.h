@@ -43,7 +43,8 @@ int cfo_seclabel_set(cfo_t *o, uint16_t lxc_id, uint32_t seclabel);
  * packets, drop bytes}, sorted; returns the row count */
 size_t cfo_identity_dump(cfo_t *o, uint64_t *rows, size_t cap);
 void cfo_node_config(cfo_t *o, uint32_t v4_cluster_range,
-                     uint32_t v4_cluster_mask, const uint8_t router_ip6[16]);
+                     uint32_t v4_cluster_mask, const uint8_t router_ip6[16],
+                     uint32_t host_ifindex);
 /* An endpoint program (and its policymap) exists for lxc_id.  Endpoints in
  * cilium_lxc without one drop with DROP_MISSED_TAIL_CALL. */
 int cfo_policy_create(cfo_t *o, uint16_t lxc_id);
@@ -66,8 +67,9 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
-                     int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, uint8_t *ct, int nthreads);
+                     const uint8_t *tcpflags, int32_t *action, int32_t *verdict,
+                     uint32_t *identity, uint8_t *lookups, uint8_t *ct,
+                     int nthreads);
 
 /* The same for IPv6: saddr/daddr are n x 16 raw address bytes; proto is the
  * next header ipv6_hdrlen() stops at (44 / 59 drop); flags bit 2 (4) marks
@@ -79,14 +81,22 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
                      const uint16_t *len, const uint32_t *mark,
-                     int32_t *action, int32_t *verdict, uint32_t *identity,
-                     uint8_t *lookups, uint8_t *ct, int nthreads);
+                     const uint8_t *tcpflags, int32_t *action, int32_t *verdict,
+                     uint32_t *identity, uint8_t *lookups, uint8_t *ct,
+                     int nthreads);
 
 /* rows of 7 u64: identity, dport, proto, egress, proxy_port, packets, bytes
  * (sorted); returns the number of rows (writes at most cap). */
-/* Drop-notify sites (res_t.nt in cfc_oracle.c) of the next classify calls,
- * one u32 per header, written to `words` (NULL = off). */
-void cfo_set_notify_out(cfo_t *o, uint32_t *words);
+/* The monitor event of every header of the next classify calls (a drop
+ * site or a trace_notify observation point, cfc_oracle.c NT_*), one u32 per
+ * header into `words`, and each CT stage's monitor length (stage 1 in bits
+ * 0-15, stage 2 in 16-31) into `mon`; NULL = off.  tcpflags (classify, may
+ * be NULL = 0) is TCP header byte 13 of each header, the flags ct_lookup
+ * accumulates into the CT entry. */
+void cfo_set_notify_out(cfo_t *o, uint32_t *words, uint32_t *mon);
+/* bpf_ktime_get_sec() for the next classify / ct_apply calls: the clock of
+ * the CT lifetimes and report intervals (conntrack.h:125-205) */
+void cfo_set_clock(cfo_t *o, uint32_t now);
 
 size_t cfo_policy_dump(cfo_t *o, uint16_t lxc_id, uint64_t *rows, size_t cap);
 /* rows of 4 u64: reason, dir, count, bytes (sorted, non-zero only) */
@@ -109,16 +119,16 @@ void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint32_t *saddr, const uint32_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
-                     const uint16_t *len, const uint32_t *identity,
-                     const int32_t *verdict, const uint8_t *ct,
-                     uint8_t *hazard);
+                     const uint16_t *len, const uint8_t *tcpflags,
+                     const uint32_t *identity, const int32_t *verdict,
+                     const uint8_t *ct, const uint32_t *mon, uint8_t *hazard);
 void cfo_ct_apply_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint8_t *saddr, const uint8_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
                      const uint8_t *proto, const uint8_t *flags,
-                     const uint16_t *len, const uint32_t *identity,
-                     const int32_t *verdict, const uint8_t *ct,
-                     uint8_t *hazard);
+                     const uint16_t *len, const uint8_t *tcpflags,
+                     const uint32_t *identity, const int32_t *verdict,
+                     const uint8_t *ct, const uint32_t *mon, uint8_t *hazard);
 /* live CT entries as rows of CFO_CT_ROW bytes: u16 owner (0 global, else
  * lxc_id + 1), u8 map (0 TCP, 1 ANY), u8 family, tuple (40 B, zero padded),
  * struct ct_entry (56 B), 4 B pad; sorted by the first 44 bytes. */

@@ -66,7 +66,7 @@ def build_packet_v4(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
         # union members, so each of them is bit 0 of TCP header byte 12;
         # FIN|ACK in byte 13 is set too, as a real close would carry.
         close = bool(h.flags[i] & S.HF_TCP_CLOSE)
-        fl = 0x11 if close else 0x02
+        fl = int(S.tcp_flags_of(h.slice(i, i + 1))[0])
         l4 = struct.pack("<HH", sp, dp) + struct.pack(
             ">IIBBHHH", 1, 0, 0x51 if close else 0x50, fl, 1024, 0, 0)
     elif proto == S.IPPROTO_UDP:
@@ -92,7 +92,7 @@ def build_packet_v6(h, i, eth_src=b"\x02" * 6, eth_dst=b"\x04" * 6):
         # union members, so each of them is bit 0 of TCP header byte 12;
         # FIN|ACK in byte 13 is set too, as a real close would carry.
         close = bool(h.flags[i] & S.HF_TCP_CLOSE)
-        fl = 0x11 if close else 0x02
+        fl = int(S.tcp_flags_of(h.slice(i, i + 1))[0])
         l4 = struct.pack("<HH", sp, dp) + struct.pack(
             ">IIBBHHH", 1, 0, 0x51 if close else 0x50, fl, 1024, 0, 0)
     elif proto == S.IPPROTO_UDP:
@@ -161,6 +161,8 @@ class RefDatapath:
         self.netdev = L.load("bpf_netdev.o", "from-netdev", SC, nd)
         nd_v4 = L.load("bpf_netdev.o", "2/7", SC, nd)
         L.maps["calls_nd"].update(u32(7), u32(nd_v4))
+        # __send_drop_notify (drop.h:50, tail call CILIUM_CALL_DROP_NOTIFY 1)
+        L.maps["calls_nd"].update(u32(1), u32(L.load("bpf_netdev.o", "2/1", SC, nd)))
         self.ep_prog = {}
         self.policy_map = {}
         self.ct_maps = {}     # lxc -> {ct map name in the object: renamed}
@@ -179,6 +181,7 @@ class RefDatapath:
             for sec, idx in (("2/11", 11), ("2/7", 7), ("2/12", 12), ("2/10", 10)):
                 calls[idx] = L.load("bpf_lxc.o", sec, SC, rn)
             egress = L.load("bpf_lxc.o", "from-container", SC, rn)
+            calls[1] = L.load("bpf_lxc.o", "2/1", SC, rn)   # __send_drop_notify
             for idx, fd in calls.items():
                 L.maps[f"calls_lxc{k}"].update(u32(idx), u32(fd))
             L.maps["cilium_policy"].update(u32(lxc), u32(pol))
@@ -189,6 +192,11 @@ class RefDatapath:
                 pm.update(policy_key(r), struct.pack("<H6xQQ",
                                                      int(r["proxy_port"]), 0, 0))
         self.xdp = L.load("bpf_xdp.o", "from-netdev", H.PROG_XDP)
+        # the perf ring cilium_events on the CPU this process is pinned to:
+        # every trace_notify / drop_notify sample of a test run lands there
+        self.cpu = H.pin_cpu()
+        self.ring = H.PerfRing(self.cpu)
+        L.maps["cilium_events"].update(u32(self.cpu), u32(self.ring.fd))
         for e in t.ipcache:
             L.maps["cilium_ipcache"].update(
                 ipcache_key(e), struct.pack("<II", int(e["label"]),
@@ -203,7 +211,25 @@ class RefDatapath:
             L.maps[name].update(key, b"\x01")
 
     def close(self):
+        self.ring.close()
         self.L.close()
+
+    def take_proxy_identity(self, family):
+        """The identity ipv{4,6}_redirect_to_host_port stored in the proxy
+        map (lxc.h:101-131: proxy4_tbl_value.identity) for the last packet;
+        the map is emptied after each read."""
+        m = self.L.maps.get("cilium_proxy4" if family == 4 else "cilium_proxy6")
+        if m is None:
+            return None
+        keys = m.keys()
+        ids = set()
+        for k in keys:
+            v = m.lookup(k)
+            off = 8 if family == 4 else 20   # orig_daddr + orig_dport + pad
+            ids.add(struct.unpack_from("<I", v, off)[0])
+            m.delete(k)
+        assert len(ids) <= 1, ids
+        return ids.pop() if ids else None
 
     # ------------------------------------------------------- conntrack
     def ct_dump(self):
@@ -277,7 +303,24 @@ def _dport_out(pkt_out, off=14 + 20):
     return struct.unpack_from("<H", pkt_out, off + 2)[0]
 
 
-def _derive_ingress(h, i, ret, cb, pkt_out):
+NOTIFY_DROP, NOTIFY_TRACE = 1, 4                 # common.h:210-215
+TRACE_TO_LXC, TRACE_TO_PROXY, TRACE_TO_HOST, TRACE_TO_STACK = 0, 1, 2, 3
+EV_DT = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"),
+                  ("hash", "<u4"), ("len_orig", "<u4"), ("len_cap", "<u4"),
+                  ("src_label", "<u4"), ("dst_label", "<u4"), ("w6", "<u4"),
+                  ("ifindex", "<u4")])
+assert EV_DT.itemsize == 32
+
+
+def _trace(evs, obs):
+    """the trace_notify record (trace.h:71-81) at observation point obs"""
+    for e in evs:
+        if e["type"] == NOTIFY_TRACE and e["subtype"] == obs:
+            return e
+    return None
+
+
+def _derive_ingress(h, i, ret, cb, pkt_out, evs, proxy_id):
     """-> action, verdict, identity, id_mask"""
     if ret == TC_ACT_SHOT:
         # send_drop_notify(skb, src_label, SECLABEL, LXC_ID, ...):
@@ -288,16 +331,23 @@ def _derive_ingress(h, i, ret, cb, pkt_out):
             # no identities recorded)
             return ret, cb[2], 0, 0
         return ret, cb[2], (cb[1] >> 16) & 0xFFFF, 0xFFFF
-    if ret == TC_ACT_REDIRECT:
+    if ret == TC_ACT_REDIRECT and cb[1] == HOST_IFINDEX:
         # proxy redirect rewrote the dport (lxc.h:118) and set
-        # cb[CB_IFINDEX] = HOST_IFINDEX (bpf_lxc.c:1004)
-        v = _dport_out(pkt_out, l4_offset(h, i)) if cb[1] == HOST_IFINDEX else 0
-        return ret, v, cb[0] & 0xFFFFFFFF, 0xFFFFFFFF
-    # TC_ACT_OK: non-local / host endpoint: identity not observable
+        # cb[CB_IFINDEX] = HOST_IFINDEX (bpf_lxc.c:1004); the source
+        # identity is what the proxy map entry records
+        v = _dport_out(pkt_out, l4_offset(h, i))
+        assert proxy_id is not None
+        assert proxy_id == cb[0] & 0xFFFFFFFF   # cb[CB_SRC_LABEL], l3.h:119
+        return ret, v, proxy_id, 0xFFFFFFFF
+    # delivered to a local endpoint: TRACE_TO_LXC carries the full source
+    # identity (bpf_lxc.c:1006, :873); to the stack: not observable
+    e = _trace(evs, TRACE_TO_LXC)
+    if e is not None:
+        return ret, 0, int(e["src_label"]), 0xFFFFFFFF
     return ret, 0, 0, 0
 
 
-def _derive_egress(h, i, ret, cb, pkt_out):
+def _derive_egress(h, i, ret, cb, pkt_out, evs, proxy_id):
     if ret == TC_ACT_SHOT:
         if cb[3] == 0:
             # egress-stage drop: send_drop_notify(SECLABEL, dstID, 0, ...)
@@ -308,7 +358,28 @@ def _derive_egress(h, i, ret, cb, pkt_out):
         dp = _dport_out(pkt_out, l4_offset(h, i))
         v = dp if dp != int(h.dport[i]) else 0
         return ret, v, 0, 0
+    # to the stack: TRACE_TO_STACK carries dstID (bpf_lxc.c:687, :390)
+    e = _trace(evs, TRACE_TO_STACK)
+    if e is not None:
+        return ret, 0, int(e["dst_label"]), 0xFFFFFFFF
     return ret, 0, 0, 0
+
+
+def _events(dp, pkt):
+    """the perf-ring samples of one packet -> EV_DT records (the len_cap
+    payload bytes after each — the packet as the program had rewritten it
+    so far — are not kept).  The
+    reference objects are built with the config headers' DEBUG on, so the
+    ring also carries cilium_dbg messages (CILIUM_NOTIFY_DBG_MSG, dbg.h) —
+    a debugging aid outside the verdict path, skipped here."""
+    out = []
+    for raw in dp.ring.read():
+        if raw[0] not in (NOTIFY_DROP, NOTIFY_TRACE):
+            continue
+        rec = np.frombuffer(raw[:32], EV_DT)[0]
+        assert len(raw) >= 32 + int(rec["len_cap"])
+        out.append(rec)
+    return out
 
 
 def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
@@ -319,32 +390,53 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     idmask = np.zeros(n, np.uint32)
     # skb->cb[0..4] after the run: for TC_ACT_SHOT these are the arguments
     # send_drop_notify left for the drop-notify tail call (drop.h:98-102:
-    # exitcode, src << 16 | dst & 0xFFFF, reason, dst_id, ifindex); the tail
-    # call itself is not wired, so they stay visible in ctx_out
+    # exitcode, src << 16 | dst & 0xFFFF, reason, dst_id, ifindex)
     cbs = np.zeros((n, 5), np.int32)
+    ev_hdr, ev_rec = [], []
+    # bpf_ktime_get_sec() of each header's run (CLOCK_MONOTONIC seconds,
+    # read before and after; 0xFFFFFFFF when a second boundary fell inside)
+    clock = np.zeros(n, np.uint32)
     build = build_packet_v4 if h.family == 4 else build_packet_v6
+    dp.ring.read()
     for i in range(n):
+        # keep each run inside one second of bpf_ktime_get_sec() so its
+        # clock is known exactly
+        t = time.clock_gettime(time.CLOCK_MONOTONIC)
+        if t - int(t) > 0.995:
+            time.sleep(int(t) + 1.0005 - t)
+        t0 = int(time.clock_gettime(time.CLOCK_MONOTONIC))
         if mode in (MODE_XDP, MODE_FULL):
             ret = H.test_run_xdp(dp.xdp, build(h, i))
             if mode == MODE_XDP or ret == XDP_DROP:
                 action[i] = ret
                 verdict[i] = 0 if ret == XDP_PASS else -1
+                assert not dp.ring.read()   # bpf_xdp.c notifies nothing
                 continue
         if mode in (MODE_INGRESS, MODE_FULL):
-            ret, cb, po = H.test_run_skb(dp.netdev, build(h, i),
-                                         mark=int(h.mark[i]))
-            r = _derive_ingress(h, i, ret, cb, po)
+            pkt = build(h, i)
+            ret, cb, po = H.test_run_skb(dp.netdev, pkt, mark=int(h.mark[i]))
+            evs = _events(dp, pkt)
+            r = _derive_ingress(h, i, ret, cb, po, evs, dp.take_proxy_identity(h.family))
         else:
-            ret, cb, po = H.test_run_skb(
-                dp.ep_prog[ep_lxc], build(h, i, LXC_MAC, NODE_MAC))
-            r = _derive_egress(h, i, ret, cb, po)
+            pkt = build(h, i, LXC_MAC, NODE_MAC)
+            ret, cb, po = H.test_run_skb(dp.ep_prog[ep_lxc], pkt)
+            evs = _events(dp, pkt)
+            r = _derive_egress(h, i, ret, cb, po, evs, dp.take_proxy_identity(h.family))
         action[i], verdict[i], ident[i], idmask[i] = r
         cbs[i] = cb
-    return action, verdict, ident, idmask, cbs
+        t1 = int(time.clock_gettime(time.CLOCK_MONOTONIC))
+        clock[i] = t0 if t0 == t1 else 0xFFFFFFFF
+        for e in evs:
+            ev_hdr.append(i)
+            ev_rec.append(e)
+    assert dp.ring.lost == 0, f"perf ring lost {dp.ring.lost} samples"
+    ev = np.array(ev_rec, EV_DT) if ev_rec else np.zeros(0, EV_DT)
+    return (action, verdict, ident, idmask, cbs, np.array(ev_hdr, np.uint32), ev,
+            clock)
 
 
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
-    action, verdict, ident, idmask, cbs = res
+    action, verdict, ident, idmask, cbs, ev_hdr, ev, clock = res
     extra = {}
     if t.ct is not None:
         # CT before (loaded by the oracle / engine) and after the stream
@@ -356,7 +448,13 @@ def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
              h_sport=h.sport, h_dport=h.dport, h_proto=h.proto,
              h_flags=h.flags, h_length=h.length, h_mark=h.mark,
              x_action=action, x_verdict=verdict, x_identity=ident,
-             x_idmask=idmask, x_cb=cbs, x_metrics=dp.metrics(), **extra)
+             x_idmask=idmask, x_cb=cbs, x_metrics=dp.metrics(),
+             # cilium_events perf-ring samples (trace_notify / drop_notify
+             # records, 32 bytes each) and the header each belongs to
+             x_ev_hdr=ev_hdr, x_ev=ev.view(np.uint8).reshape(-1, 32),
+             x_clock=clock, **extra)
+    if h.tcpflags is not None:
+        d["h_tcpflags"] = h.tcpflags
     for lxc, pol in t.policy.items():
         d[f"policy_{lxc}"] = pol
     for lxc, c in dp.policy_counters().items():
@@ -773,12 +871,24 @@ def _ct_scenario(family, mode, seed, n=6000):
                      else h_in.daddr == loc[0])
     m = int(n * 1.4)
     parts = []
+
+    def tcp_flags(x, opening):
+        """TCP byte 13 of established traffic: ACK, PSH|ACK, (SYN|)ACK, and
+        FIN|ACK or RST on the closing packets (HF_TCP_CLOSE, byte 12 bit 0):
+        what ct_update_timeout accumulates into the entry's seen flags and
+        reports on change (conntrack.h:137-185)"""
+        k = len(x)
+        close = (x.flags & S.HF_TCP_CLOSE) != 0
+        f = rng.choice(np.array([0x10, 0x18, opening], np.uint8), size=k)
+        f = np.where(close, rng.choice(np.array([0x11, 0x04], np.uint8), size=k), f)
+        x.tcpflags = np.where(x.proto == S.IPPROTO_TCP, f, 0).astype(np.uint8)
+        return x
     a = S.take(fwd, rng.integers(0, len(fwd), size=int(m * 0.35)))
     a.flags[(rng.random(len(a)) < 0.08) & (a.proto == S.IPPROTO_TCP)] |= np.uint8(S.HF_TCP_CLOSE)
-    parts.append(a)
+    parts.append(tcp_flags(a, 0x02))
     b = S.reverse(S.take(rep, rng.integers(0, len(rep), size=int(m * 0.3))))
     b.flags[(rng.random(len(b)) < 0.08) & (b.proto == S.IPPROTO_TCP)] |= np.uint8(S.HF_TCP_CLOSE)
-    parts.append(b)
+    parts.append(tcp_flags(b, 0x12))
     c = S.reverse(S.take(rep, rng.integers(0, len(rep), size=int(m * 0.05))))
     c.proto[:] = icmp
     c.sport[:] = err
@@ -808,8 +918,7 @@ def _ct_scenario(family, mode, seed, n=6000):
 
 
 def _keep(h, m):
-    return S.Headers(h.family, h.saddr[m], h.daddr[m], h.sport[m], h.dport[m],
-                     h.proto[m], h.flags[m], h.length[m], h.mark[m])
+    return S.take(h, m)
 
 
 SCENARIOS = {

@@ -24,6 +24,13 @@ DROP_NOTIFY_DT = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"),
                            ("dst_label", "<u4"), ("dst_id", "<u4"),
                            ("ifindex", "<u4")])
 assert DROP_NOTIFY_DT.itemsize == 32
+# one perf-ring record of either kind (32 bytes): w6 is drop_notify.dst_id,
+# or trace_notify's {u16 dst_id, u8 reason, u8 pad}
+EVENT_DT = np.dtype([("type", "u1"), ("subtype", "u1"), ("source", "<u2"),
+                     ("hash", "<u4"), ("len_orig", "<u4"), ("len_cap", "<u4"),
+                     ("src_label", "<u4"), ("dst_label", "<u4"), ("w6", "<u4"),
+                     ("ifindex", "<u4")])
+TRACE_TO_LXC, TRACE_TO_PROXY, TRACE_TO_HOST, TRACE_TO_STACK = 0, 1, 2, 3
 
 
 def _fmix32(h):
@@ -61,6 +68,16 @@ def flow_hash(hdr, idx):
                        + pw * np.uint32(0xC2B2AE3D) + pr)
 
 
+def _tcp_flags(hdr):
+    """TCP header byte 13 per header (synth.tcp_flags_of, restated so the
+    oracle does not import the product package)"""
+    if getattr(hdr, "tcpflags", None) is not None:
+        return np.asarray(hdr.tcpflags, np.uint8)
+    tcp = np.asarray(hdr.proto) == 6
+    close = (np.asarray(hdr.flags) & 2) != 0
+    return np.where(tcp, np.where(close, 0x11, 0x02), 0).astype(np.uint8)
+
+
 def build():
     subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
 
@@ -85,14 +102,14 @@ def lib():
         L.cfo_prefilter_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, u8p,
                                         ctypes.c_int]
         L.cfo_classify_v4.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
-                                      ctypes.c_size_t] + [vp] * 13 + [ctypes.c_int]
+                                      ctypes.c_size_t] + [vp] * 14 + [ctypes.c_int]
         L.cfo_classify_v6.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
-                                      ctypes.c_size_t] + [vp] * 13 + [ctypes.c_int]
+                                      ctypes.c_size_t] + [vp] * 14 + [ctypes.c_int]
         L.cfo_ct_add.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  vp, vp]
         for f in (L.cfo_ct_apply_v4, L.cfo_ct_apply_v6):
             f.argtypes = [vp, ctypes.c_int, ctypes.c_uint16,
-                          ctypes.c_size_t] + [vp] * 11
+                          ctypes.c_size_t] + [vp] * 13
         L.cfo_ct_add_n.argtypes = [vp, ctypes.c_size_t, vp]
         L.cfo_ct_dump.restype = ctypes.c_size_t
         L.cfo_ct_dump.argtypes = [vp, vp, ctypes.c_size_t]
@@ -104,9 +121,12 @@ def lib():
         L.cfo_counters_reset.argtypes = [vp]
         L.cfo_identity_dump.restype = ctypes.c_size_t
         L.cfo_identity_dump.argtypes = [vp, vp, ctypes.c_size_t]
-        L.cfo_set_notify_out.argtypes = [vp, vp]
-        L.cfo_node_config.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p]
+        L.cfo_set_notify_out.argtypes = [vp, vp, vp]
+        L.cfo_node_config.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, u8p,
+                                      ctypes.c_uint32]
         L.cfo_node_config.restype = None
+        L.cfo_set_clock.argtypes = [vp, ctypes.c_uint32]
+        L.cfo_set_clock.restype = None
         _lib = L
     return _lib
 
@@ -125,6 +145,8 @@ class Oracle:
         self.L = lib()
         self.h = self.L.cfo_new()
         self.lxc_ids = []
+        self.host_ifindex = 1
+        self.mon = None       # the last classify's per-header monitor lengths
         self.tables = tables
         if tables is not None:
             self.load(tables)
@@ -162,12 +184,19 @@ class Oracle:
         if getattr(t, "node", None) is not None:
             self.node_config(*t.node)
 
-    def node_config(self, v4_cluster_range, v4_cluster_mask, router_ip6):
-        """node_config.h IPV4_CLUSTER_RANGE / _MASK (raw be32 as loaded) and
-        ROUTER_IP (16 bytes)."""
+    def node_config(self, v4_cluster_range, v4_cluster_mask, router_ip6,
+                    host_ifindex=1):
+        """node_config.h IPV4_CLUSTER_RANGE / _MASK (raw be32 as loaded),
+        ROUTER_IP (16 bytes) and HOST_IFINDEX."""
         p, keep = _u8p(np.asarray(router_ip6, np.uint8).reshape(16))
+        self.host_ifindex = int(host_ifindex)
         self.L.cfo_node_config(self.h, int(v4_cluster_range) & 0xFFFFFFFF,
-                               int(v4_cluster_mask) & 0xFFFFFFFF, p)
+                               int(v4_cluster_mask) & 0xFFFFFFFF, p,
+                               self.host_ifindex)
+
+    def set_clock(self, now):
+        """bpf_ktime_get_sec() of the next classify / ct_apply calls."""
+        self.L.cfo_set_clock(self.h, int(now) & 0xFFFFFFFF)
 
     def ct_add(self, ct):
         rec = np.ascontiguousarray(ct)
@@ -180,7 +209,8 @@ class Oracle:
         return [c(hdr.saddr, at), c(hdr.daddr, at),
                 c(hdr.sport, np.uint16), c(hdr.dport, np.uint16),
                 c(hdr.proto, np.uint8), c(hdr.flags, np.uint8),
-                c(hdr.length, np.uint16), c(hdr.mark, np.uint32)]
+                c(hdr.length, np.uint16), c(hdr.mark, np.uint32),
+                c(_tcp_flags(hdr), np.uint8)]
 
     def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False,
                  want_ct=False, apply_ct=False, want_notify=False):
@@ -196,18 +226,16 @@ class Oracle:
         ct = np.zeros(n, np.uint8) if (want_ct or apply_ct) else None
         c = np.ascontiguousarray
         at = np.uint32 if hdr.family == 4 else np.uint8
-        arrs = [c(hdr.saddr, at), c(hdr.daddr, at),
-                c(hdr.sport, np.uint16), c(hdr.dport, np.uint16),
-                c(hdr.proto, np.uint8), c(hdr.flags, np.uint8),
-                c(hdr.length, np.uint16), c(hdr.mark, np.uint32)]
+        arrs = self._arrays(hdr)
         if hdr.family == 6:
             assert arrs[0].shape == (n, 16) and arrs[1].shape == (n, 16)
         fn = self.L.cfo_classify_v4 if hdr.family == 4 else self.L.cfo_classify_v6
         nt = np.zeros(n, np.uint32) if want_notify else None
-        self.L.cfo_set_notify_out(self.h, _p(nt))
+        self.mon = np.zeros(n, np.uint32)
+        self.L.cfo_set_notify_out(self.h, _p(nt), _p(self.mon))
         fn(self.h, mode, ep_lxc, n, *[_p(a) for a in arrs], _p(act), _p(ver),
            _p(ide), _p(lk), _p(ct), nthreads)
-        self.L.cfo_set_notify_out(self.h, None)
+        self.L.cfo_set_notify_out(self.h, None, None)
         if apply_ct:
             self.ct_apply(hdr, mode, ep_lxc, ide, ver, ct)
         out = (act, ver, ide)
@@ -219,50 +247,99 @@ class Oracle:
             out += (nt,)
         return out
 
-    def drop_notify(self, hdr, mode, ep_lxc, verdict, identity, sites):
-        """The struct drop_notify records (bpf/lib/drop.h:40-78) the
-        reference's perf ring would carry for this batch, in header order
-        -> (records DROP_NOTIFY_DT, header indices u64).  Uses the tables
-        this oracle was loaded with for SECLABEL and ifindex."""
+    def events(self, hdr, mode, ep_lxc, verdict, identity, words, drops=True,
+               traces=True):
+        """The monitor events the reference's perf ring cilium_events would
+        carry for this batch, in header order -> (EVENT_DT records, header
+        indices u64): struct drop_notify (bpf/lib/drop.h:40-78) for drops,
+        struct trace_notify (trace.h:71-81, send_trace_notify :97-155) for
+        forwarded packets.  words = the classify's per-header event words
+        (want_notify).  SECLABEL / ifindex come from the loaded tables."""
         t = self.tables
         sec = np.zeros(65536, np.uint32)
         for lxc, lab in t.seclabel.items():
             sec[int(lxc)] = int(lab)
         ifx = np.zeros(65536, np.uint32)
         ifx[t.endpoints["lxc_id"].astype(np.int64)] = t.endpoints["ifindex"]
-        idx = np.flatnonzero(sites).astype(np.uint64)
-        w = sites[idx].astype(np.uint32)
-        site, src_lxc = w >> 16, (w & 0xFFFF).astype(np.int64)
-        ver = verdict[idx].astype(np.int64)
-        ident = identity[idx].astype(np.uint32)
+        words = np.asarray(words, np.uint32)
+        kind = (words >> 16) & 0xF
+        sel = ((kind >= 1) & (kind <= 3) & drops) | ((kind >= 4) & traces)
+        idx = np.flatnonzero(sel).astype(np.uint64)
+        w = words[idx]
+        k, lxc = (w >> 16) & 0xF, (w & 0xFFFF).astype(np.int64)
+        ver = np.asarray(verdict)[idx].astype(np.int64)
+        ident = np.asarray(identity)[idx].astype(np.uint32)
         ln = np.asarray(hdr.length, np.uint32)[idx]
-        r = np.zeros(len(idx), DROP_NOTIFY_DT)
-        r["type"] = 1                                   # CILIUM_NOTIFY_DROP
-        r["subtype"] = (-ver) & 0xFF                    # error = -reason
-        r["source"] = np.where(site == 1, 0, src_lxc)   # EVENT_SOURCE
+        own = sec[ep_lxc] if mode == MODE_EGRESS else 0
+        r = np.zeros(len(idx), EVENT_DT)
         r["hash"] = flow_hash(hdr, idx)
         r["len_orig"] = ln
-        r["len_cap"] = np.minimum(ln, 128)              # TRACE_PAYLOAD_LEN
-        # cb[1] = src << 16 | dst & 0xFFFF: both labels keep 16 bits
-        own = sec[ep_lxc] if mode == MODE_EGRESS else 0
-        src = np.where(site == 2, own,
-                       np.where(site == 3, own if mode == MODE_EGRESS else ident, 0))
-        dst = np.where(site == 2, ident,
-                       np.where(site == 3, sec[src_lxc], 0))
-        r["src_label"] = np.asarray(src, np.uint32) & 0xFFFF
-        r["dst_label"] = np.asarray(dst, np.uint32) & 0xFFFF
-        r["dst_id"] = np.where(site == 3, src_lxc, 0)
-        r["ifindex"] = np.where(site == 3, ifx[src_lxc], 0)
+        # drops: cb[1] = src << 16 | dst & 0xFFFF, both labels 16 bits
+        d = k <= 3
+        r["type"] = np.where(d, 1, 4)                     # CILIUM_NOTIFY_DROP / TRACE
+        r["subtype"] = np.where(d, (-ver) & 0xFF, k - 4)  # -reason / obs point
+        r["source"] = np.where(k == 1, 0, lxc)            # EVENT_SOURCE
+        mc = (w >> 22) & 3                                # TRACE_PAYLOAD_LEN / MTU / 1
+        mon = np.where(mc == 2, 1500, np.where(mc == 3, 1, 128))
+        r["len_cap"] = np.minimum(ln, np.where(d, 128, mon))
+        i64 = lambda x: np.broadcast_to(np.asarray(x, np.int64), k.shape)  # noqa: E731
+        ownv = i64(own)
+        peer = ownv if mode == MODE_EGRESS else i64(ident)
+        src = np.select([k == 2, k == 3, k == 4, k >= 5],
+                        [ownv, peer, peer, i64(sec[lxc])], 0)
+        dst = np.select([k == 2, k == 3, k == 4, k == 6, k == 7],
+                        [i64(ident), i64(sec[lxc]), i64(sec[lxc]), i64(1), i64(ident)], 0)
+        r["src_label"] = np.where(d, np.asarray(src, np.uint32) & 0xFFFF, src)
+        r["dst_label"] = np.where(d, np.asarray(dst, np.uint32) & 0xFFFF, dst)
+        # drop_notify.dst_id (u32) / trace_notify {dst_id u16, reason u8, pad}
+        reason = (w >> 20) & 3
+        reason = reason.astype(np.int64)
+        r["w6"] = np.select([k == 3, k == 4, k >= 5],
+                            [lxc, lxc | reason << 16, reason << 16], 0)
+        r["ifindex"] = np.select([k == 3, k == 4, (k == 5) | (k == 6)],
+                                 [i64(ifx[lxc]), i64(ifx[lxc]), i64(self.host_ifindex)], 0)
         return r, idx
 
-    def ct_apply(self, hdr, mode, ep_lxc, identity, verdict, ct, hazard=False):
+    def run_sequential(self, hdr, mode, ep_lxc, clock):
+        """The reference's own semantics: one header at a time, each folded
+        into the CT maps before the next (the batch engine's lookups all see
+        the batch-start state instead), at the bpf_ktime_get_sec() value
+        clock[i] -> (action, verdict, identity, event words)."""
+        n = len(hdr)
+        act = np.zeros(n, np.int32)
+        ver = np.zeros(n, np.int32)
+        ide = np.zeros(n, np.uint32)
+        words = np.zeros(n, np.uint32)
+        for i in range(n):
+            self.set_clock(int(clock[i]))
+            one = hdr.slice(i, i + 1)
+            a, v, d, ct, w = self.classify(one, mode, ep_lxc, want_ct=True,
+                                           want_notify=True)
+            self.ct_apply(one, mode, ep_lxc, d, v, ct)
+            act[i], ver[i], ide[i], words[i] = a[0], v[0], d[0], w[0]
+        return act, ver, ide, words
+
+    def drop_notify(self, hdr, mode, ep_lxc, verdict, identity, sites):
+        """The struct drop_notify records (bpf/lib/drop.h:40-78) of this
+        batch in header order -> (records DROP_NOTIFY_DT, header indices)."""
+        r, idx = self.events(hdr, mode, ep_lxc, verdict, identity, sites,
+                             traces=False)
+        return r.view(DROP_NOTIFY_DT), idx
+
+    def ct_apply(self, hdr, mode, ep_lxc, identity, verdict, ct, hazard=False,
+                 trace_hazards=False):
+        """Fold a classified batch into the CT maps (cfo_ct_apply_*).  With
+        hazard, returns per header 1 where a packet-at-a-time run would see a
+        different CT result — and, with trace_hazards, a different monitor
+        length (from the last classify) — because of an earlier header."""
         arrs = self._arrays(hdr)
         hz = np.zeros(len(hdr), np.uint8) if hazard else None
         fn = self.L.cfo_ct_apply_v4 if hdr.family == 4 else self.L.cfo_ct_apply_v6
         c = np.ascontiguousarray
+        mon = c(self.mon, np.uint32) if trace_hazards else None
         fn(self.h, mode, ep_lxc, len(hdr), *[_p(a) for a in arrs[:7]],
-           _p(c(identity, np.uint32)), _p(c(verdict, np.int32)),
-           _p(c(ct, np.uint8)), _p(hz))
+           _p(arrs[8]), _p(c(identity, np.uint32)), _p(c(verdict, np.int32)),
+           _p(c(ct, np.uint8)), _p(mon), _p(hz))
         return hz
 
     def ct_dump(self):

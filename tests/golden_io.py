@@ -4,6 +4,7 @@ import os
 
 import numpy as np
 
+import oracle as O
 from cilium_amd import synth as S
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -30,7 +31,17 @@ class Golden:
         self.ct_after = d["x_ct"] if "x_ct" in d.files else None
         self.headers = S.Headers(int(d["h_family"]), d["h_saddr"], d["h_daddr"],
                                  d["h_sport"], d["h_dport"], d["h_proto"],
-                                 d["h_flags"], d["h_length"], d["h_mark"])
+                                 d["h_flags"], d["h_length"], d["h_mark"],
+                                 d["h_tcpflags"] if "h_tcpflags" in d.files else None)
+        # the cilium_events perf-ring samples (trace_notify / drop_notify,
+        # 32 bytes each, EVENT_DT) and the header of each; None in older
+        # fixtures
+        self.ev = (d["x_ev"].reshape(-1).view(O.EVENT_DT)
+                   if "x_ev" in d.files else None)
+        self.ev_hdr = d["x_ev_hdr"] if "x_ev_hdr" in d.files else None
+        # bpf_ktime_get_sec() while each header ran (0xFFFFFFFF: a second
+        # boundary fell inside its run); None in older fixtures
+        self.clock = d["x_clock"] if "x_clock" in d.files else None
         self.action = d["x_action"]
         self.verdict = d["x_verdict"]
         self.identity = d["x_identity"]

@@ -57,11 +57,12 @@ def test_node_config_on_host_only_context():
     """cfc_set/get_node_config: starts at bpf/node_config.h's values
     (IPV4_CLUSTER_RANGE 0x100000, MASK 0xff0000, ROUTER_IP beef::1:0:1:0:0)."""
     dp = C.host_only()
-    rng, mask, router = dp.node_config()
-    assert (rng, mask) == (0x100000, 0xFF0000)
+    rng, mask, router, hif = dp.node_config()
+    assert (rng, mask, hif) == (0x100000, 0xFF0000, 1)
     assert router == bytes([0xbe, 0xef] + [0] * 9 + [1, 0, 1, 0, 0])
-    dp.set_node_config(0x0A, 0xFF, bytes(range(16)))
-    assert dp.node_config() == (0x0A, 0xFF, bytes(range(16)))
+    dp.set_node_config(0x0A, 0xFF, bytes(range(16)), 7)
+    assert dp.node_config() == (0x0A, 0xFF, bytes(range(16)), 7)
+    dp.set_clock(12345)
 
 
 def errno_of(fn):
@@ -242,7 +243,7 @@ def test_drop_notify_abi_on_host_only_context():
     import oracle as O
     dp = C.host_only()
     L = dp.L
-    hdr = _lib.HdrV4(None, None, None, None, None, 0)
+    hdr = _lib.HdrV4(None, None, None, None, None, None, 0)
     cnt = ctypes.c_uint64(0)
     out = _lib.Out()
     for fn in (L.cfc_drop_notify_v4, L.cfc_drop_notify_v6):

@@ -31,9 +31,7 @@ def gpu_notify(torch, t, h, mode, ep_lxc=0, cap=None, chunks=1):
     step = max(1, (n + chunks - 1) // chunks)
     res = []
     for a in range(0, max(n, 1), step):
-        sl = lambda x: x[a:a + step] if x is not None else None   # noqa: E731
-        sub = type(b)(sl(b.saddr), sl(b.daddr), sl(b.ports), sl(b.meta),
-                      sl(b.mark))
+        sub = b.slice(a, a + step)
         out = dp.classify(sub, mode, ep_lxc, want_notify=True)
         rec, idx, total = dp.drop_notify(sub, out, mode, ep_lxc, cap=cap)
         torch.cuda.synchronize()
@@ -143,8 +141,7 @@ def test_two_streams(torch):
     load_tables(dp, g.tables)
     b = pack(g.headers)
     out = dp.classify(b, g.mode, g.ep_lxc, want_notify=True)
-    small_b = type(b)(b.saddr[:5000], b.daddr[:5000], b.ports[:5000],
-                      b.meta[:5000], b.mark[:5000] if b.mark is not None else None)
+    small_b = b.slice(0, 5000)
     small_out = dp.classify(small_b, g.mode, g.ep_lxc, want_notify=True)
     torch.cuda.synchronize()
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
@@ -187,3 +184,106 @@ def test_records_use_the_classified_epoch(torch):
         np.ascontiguousarray(rec.cpu().numpy()).view(np.uint8).reshape(-1),
         orec.view(np.uint8))
     dp.close()
+
+
+def gpu_events(torch, t, h, mode, ep_lxc=0, clock=0, chunks=1):
+    """-> (event words, records, header indices, total) of the engine,
+    chunk by chunk (CT folded between chunks)."""
+    dp = Datapath(0)
+    load_tables(dp, t)
+    dp.set_clock(clock)
+    b = pack(h)
+    n = len(h)
+    step = max(1, (n + chunks - 1) // chunks)
+    use_ct = getattr(t, "ct", None) is not None
+    words, recs, idxs, tot = [], [], [], 0
+    for a in range(0, max(n, 1), step):
+        sub = b.slice(a, a + step)
+        out = dp.classify(sub, mode, ep_lxc, want_notify=True, want_ct=use_ct)
+        rec, idx, total = dp.monitor_events(sub, out, mode, ep_lxc)
+        if use_ct:
+            dp.ct_apply(sub, out, mode, ep_lxc)
+        torch.cuda.synchronize()
+        words.append(out.notify.cpu().numpy().view(np.uint32))
+        recs.append(np.ascontiguousarray(rec.cpu().numpy()).view(O.EVENT_DT).reshape(-1))
+        idxs.append(idx.cpu().numpy().astype(np.uint64) + a)
+        tot += total
+    dp.close()
+    return (np.concatenate(words)[:n], np.concatenate(recs), np.concatenate(idxs), tot)
+
+
+def oracle_events(t, h, mode, ep_lxc=0, clock=0, chunks=1):
+    o = O.Oracle(t)
+    o.set_clock(clock)
+    n = len(h)
+    step = max(1, (n + chunks - 1) // chunks)
+    use_ct = getattr(t, "ct", None) is not None
+    words, recs, idxs = [], [], []
+    for a in range(0, max(n, 1), step):
+        part = h.slice(a, a + step)
+        act, ver, ide, nt = o.classify(part, mode, ep_lxc, nthreads=16,
+                                       want_notify=True, apply_ct=use_ct)
+        rec, idx = o.events(part, mode, ep_lxc, ver, ide, nt)
+        words.append(nt)
+        recs.append(rec)
+        idxs.append(idx + np.uint64(a))
+    return np.concatenate(words)[:n], np.concatenate(recs), np.concatenate(idxs)
+
+
+def check_events(torch, t, h, mode, ep_lxc=0, clock=0, chunks=1):
+    ow, orec, oidx = oracle_events(t, h, mode, ep_lxc, clock, chunks)
+    gw, grec, gidx, total = gpu_events(torch, t, h, mode, ep_lxc, clock, chunks)
+    bad = np.nonzero(gw != ow)[0]
+    assert len(bad) == 0, f"event words: {len(bad)} differ, first {bad[:5]} " \
+                          f"{gw[bad[:5]]} vs {ow[bad[:5]]}"
+    assert total == len(orec)
+    np.testing.assert_array_equal(gidx, oidx)
+    np.testing.assert_array_equal(grec.view(np.uint8), orec.view(np.uint8))
+    return orec
+
+
+@pytest.mark.parametrize("name", G.names())
+def test_golden_monitor_events(torch, name):
+    """Drop and trace records of every fixture, engine vs the oracle (which
+    the CPU suite pins record by record to the reference's perf ring) on the
+    same batch at the fixture's clock."""
+    g = G.Golden(name)
+    clock = int(np.median(g.clock[g.clock != 0xFFFFFFFF])) if g.clock is not None else 0
+    rec = check_events(torch, g.tables, g.headers, g.mode, g.ep_lxc, clock)
+    if g.ev is not None and (g.ev["type"] == 4).any():
+        assert (rec["type"] == 4).any(), name
+
+
+@pytest.mark.parametrize("mode", [0, 1, 3])
+def test_c2_monitor_events(torch, mode):
+    t = S.config_c2(2, n_endpoints=3)
+    if mode == 1:
+        rng = np.random.default_rng(9)
+        h = S.gen_headers_v4(rng, 2_000_000, t.ipcache, S.local_v4_addrs(t),
+                             local_frac=0.2, src_fixed=S.LXC_IPV4)
+    else:
+        h = S.headers_c2(t, 2_000_000, seed=9)
+    rec = check_events(torch, t, h, mode, S.EP_LXC_ID if mode == 1 else 0)
+    assert set(np.unique(rec["type"])) == {1, 4}
+
+
+def test_c5_monitor_events(torch):
+    """Conntrack hits: which packets of an active flow are traced (report
+    interval, new TCP flags, closes), at a clock inside and past the
+    flows' report interval, three batches folded into CT in between."""
+    t, flows = S.config_c5(5, n_flows=200_000, n_prefixes=50_000, now=1000)
+    h = S.headers_c5(t, flows, 900_000, seed=8)
+    rng = np.random.default_rng(3)
+    h.tcpflags = rng.choice(np.array([0x10, 0x18, 0x02, 0x12], np.uint8), size=len(h))
+    for clock in (1003, 2000):
+        rec = check_events(torch, t, h, 3, 0, clock, chunks=3)
+        caps = np.unique(rec["len_cap"][rec["type"] == 4])
+        assert 1 in caps and 128 in caps, caps
+
+
+def test_c3_monitor_events(torch):
+    t = S.config_c3(3, n_prefixes=100_000, n_v4_prefixes=10_000, n_endpoints=3,
+                    n_prefilter=5000)
+    h = S.headers_c3(t, 500_000, seed=12, ext=0.05, exthdr_drop=0.01, local_frac=0.9)
+    for mode in (0, 3):
+        check_events(torch, t, h, mode)

@@ -42,9 +42,7 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
     use_ct = getattr(t, "ct", None) is not None
     step = (n + chunks - 1) // chunks
     for a in range(0, n, step):
-        sl = lambda x: x[a:a + step] if x is not None else None   # noqa: E731
-        sub = type(b)(sl(b.saddr), sl(b.daddr), sl(b.ports), sl(b.meta),
-                      sl(b.mark))
+        sub = b.slice(a, a + step)
         out = dp.classify(sub, mode, ep_lxc, want_ct=use_ct)
         if use_ct:   # fold this batch's creates/deletes before the next one
             dp.ct_apply(sub, out, mode, ep_lxc)
