@@ -30,6 +30,7 @@ EXPORTS = (
     "cfc_ct_apply_v4", "cfc_ct_apply_v6", "cfc_map_update_batch",
     "cfc_set_node_config", "cfc_get_node_config", "cfc_identity_counters",
     "cfc_set_clock", "cfc_monitor_events_v4", "cfc_monitor_events_v6",
+    "cfc_map_dump",
 )
 # CT byte (cfc_out.ct): per stage (bits 0-3, then 4-7 for the destination's
 # ingress lookup after egress local delivery)
@@ -124,6 +125,7 @@ def lib():
     L.cfc_map_update_batch.argtypes = [vp, i32, vp, vp, u64, u64]
     L.cfc_map_delete.argtypes = [vp, i32, vp]
     L.cfc_map_get_next_key.argtypes = [vp, i32, vp, vp]
+    L.cfc_map_dump.argtypes = [vp, i32, vp, vp, u64, ctypes.POINTER(u64)]
     L.cfc_endpoint_config.argtypes = [vp, ctypes.c_uint16, u32]
     L.cfc_set_node_config.argtypes = [vp, ctypes.POINTER(NodeConfig)]
     L.cfc_get_node_config.argtypes = [vp, ctypes.POINTER(NodeConfig)]

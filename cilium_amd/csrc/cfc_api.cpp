@@ -726,6 +726,28 @@ int cfc_map_get_next_key(cfc_ctx *c, int fd, const void *key, void *next)
     return m ? m->next_key(key, next) : -EBADF;
 }
 
+int cfc_map_dump(cfc_ctx *c, int fd, void *keys, void *values, uint64_t cap,
+                 uint64_t *n)
+{
+    if (!c || !n || (cap && (!keys || !values)))
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    Map *m = get_map(c, fd);
+    if (!m)
+        return -EBADF;
+    const size_t vb = m->value_bytes();
+    uint64_t k = 0;
+    for (const auto &kv : m->kv) {
+        if (k < cap) {
+            memcpy((uint8_t *)keys + k * m->ksz, kv.first.data(), m->ksz);
+            memcpy((uint8_t *)values + k * vb, kv.second.val.data(), vb);
+        }
+        k++;
+    }
+    *n = k;
+    return 0;
+}
+
 int cfc_endpoint_config(cfc_ctx *c, uint16_t lxc_id, uint32_t seclabel)
 {
     if (!c)

@@ -202,6 +202,19 @@ class Datapath:
         L.check(rc, "get next key")
         return buf.raw
 
+    def dump(self, fd):
+        """cfc_map_dump -> (keys (n, key_size) u8, values (n, value_size)
+        u8) numpy arrays, in iteration order."""
+        import numpy as np
+        n = ctypes.c_uint64()
+        L.check(self.L.cfc_map_dump(self.h, fd, None, None, 0, ctypes.byref(n)), "dump")
+        k = np.zeros((n.value, self._ksz[fd]), np.uint8)
+        v = np.zeros((n.value, self._vsz[fd]), np.uint8)
+        if n.value:
+            L.check(self.L.cfc_map_dump(self.h, fd, k.ctypes.data, v.ctypes.data,
+                                        n.value, ctypes.byref(n)), "dump")
+        return k, v
+
     def keys(self, fd):
         out, k = [], None
         while True:

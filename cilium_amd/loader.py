@@ -112,17 +112,24 @@ def ct_rows(dp: Datapath, fds):
     CFO_CT_ROW: u16 owner (lxc + 1, 0 global), u8 map (0 TCP / 1 ANY),
     u8 family, tuple[40], ct_entry[56], pad[4]), sorted."""
     import numpy as np
-    rows = []
+    parts = []
     for (fam, lxc, any_map), fd in fds.items():
-        for k in dp.keys(fd):
-            v = dp.lookup_element(fd, k)
-            r = bytearray(104)
-            struct.pack_into("<HBB", r, 0, lxc + 1, any_map, fam)
-            r[4:4 + len(k)] = k
-            r[44:100] = v[:56]
-            rows.append(bytes(r))
-    rows.sort(key=lambda r: r[:44])
-    return np.frombuffer(b"".join(rows), np.uint8).reshape(-1, 104).copy()
+        k, v = dp.dump(fd)                 # cfc_map_dump
+        r = np.zeros((len(k), 104), np.uint8)
+        r[:, 0:2] = np.uint16(lxc + 1).tobytes()[0], np.uint16(lxc + 1).tobytes()[1]
+        r[:, 2] = any_map
+        r[:, 3] = fam
+        r[:, 4:4 + k.shape[1]] = k
+        r[:, 44:100] = v[:, :56]
+        parts.append(r)
+    rows = np.concatenate(parts) if parts else np.zeros((0, 104), np.uint8)
+    # sort by the first 44 bytes in memcmp order, as the oracle's dump:
+    # lexicographic over big-endian 8-byte words
+    w = np.zeros((len(rows), 48), np.uint8)
+    w[:, :44] = rows[:, :44]
+    keys = w.view(">u8").astype(np.uint64)
+    order = np.lexsort(keys.T[::-1])
+    return rows[order]
 
 
 def policy_rows(pm: policymap.PolicyMap):

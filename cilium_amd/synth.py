@@ -740,9 +740,13 @@ def ct_entries_v4(daddr, saddr, dport, sport, proto, flags, dir_ingress,
     ct["entry"][n:] = ent2
     # one entry per key (a later flow's related entry overwrites, like
     # map_update_elem)
-    key = np.concatenate([ct["any"][:, None], ct["tuple"][:, :14]], 1)
-    _, last = np.unique(key[::-1], axis=0, return_index=True)
-    return ct[::-1][np.sort(last)]
+    import pandas as pd
+    tu = np.ascontiguousarray(ct["tuple"][:, :16])
+    k0 = tu[:, :8].copy().view("<u8").ravel()
+    k1 = (tu[:, 8:16].copy().view("<u8").ravel() & np.uint64((1 << 48) - 1)) | \
+        (ct["any"].astype(np.uint64) << np.uint64(48))
+    dup = pd.DataFrame({"a": k0, "b": k1}).duplicated(keep="last").to_numpy()
+    return ct[~dup]
 
 
 def config_c5(seed=5, n_flows=10_000_000, n_prefixes=100_000, n_policy=16384,

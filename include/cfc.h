@@ -94,6 +94,13 @@ int cfc_map_delete(cfc_ctx *ctx, int fd, const void *key);
 /* bpf.GetNextKey (pkg/bpf/bpf.go:225); key == NULL (or absent) -> first. */
 int cfc_map_get_next_key(cfc_ctx *ctx, int fd, const void *key,
                          void *next_key);
+/* BPF_MAP_LOOKUP_BATCH over the whole map (what DumpWithCallback,
+ * pkg/bpf/map.go:479, does one GetNextKey/Lookup pair at a time, and what
+ * ctmap GC walks, ctmap.go:272): keys[0 .. min(*n, cap)) and their values
+ * (value_size bytes, per-CPU maps rounded as cfc_map_lookup), in iteration
+ * order; *n = the number of entries. */
+int cfc_map_dump(cfc_ctx *ctx, int fd, void *keys, void *values, uint64_t cap,
+                 uint64_t *n);
 /* Number of per-CPU value slots of PERCPU maps (always 1). */
 int cfc_num_possible_cpus(void);
 
