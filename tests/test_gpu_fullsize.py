@@ -101,7 +101,9 @@ def test_c5_full_flows(torch):
     dp = Datapath(0)
     pms = load_tables(dp, t)
     st = dp.stats()
-    assert st["ct4_entries"] >= 16_000_000, st
+    # ICMP 'related' entries in the TCP maps are unreachable by a lookup and
+    # stay host-side (layout.h); the rest is the device table (> 8M -> 32M slots)
+    assert st["ct4_entries"] >= 10_000_000, st
     log(f"C5: engine tables {time.time() - t0:.1f}s")
     o = O.Oracle(t)
     log(f"C5: oracle tables {time.time() - t0:.1f}s")
