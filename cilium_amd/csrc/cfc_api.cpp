@@ -67,7 +67,7 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 
 struct Epoch {
     uint64_t id = 0;
-    DevBuf tbl24, tbl8, ovf, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
+    DevBuf tbl24, tbl8, ovf, l4d, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
         polbloom, lxc6;
     DevBuf l6[3][3];   // ipc6 / pf6_fix / pf6_dyn: slots, bloom, lens
     DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
@@ -298,7 +298,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->id = ++c->epoch_seq;
     if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
         (rc = upload_vec(E->ovf, img.lbl_ovf, s)) ||
-        (rc = upload_vec(E->l4c, img.l4c, s)) || (rc = upload_vec(E->l4l, img.l4l, s)) ||
+        (rc = upload_vec(E->l4d, img.l4d, s)) || (rc = upload_vec(E->l4c, img.l4c, s)) || (rc = upload_vec(E->l4l, img.l4l, s)) ||
         (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
         (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
         (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)) ||
@@ -373,6 +373,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     T.lxc6 = (const Lxc6Slot *)E->lxc6.p;
     T.lxc6_mask = img.lxc6_mask;
     T.lxc6_lds = img.lxc6.size() <= LXC6_LDS_MAX_SLOTS;
+    T.l4d = (const uint4 *)E->l4d.p;
     T.l4c = (const uint32_t *)E->l4c.p;
     T.l4l = (const uint64_t *)E->l4l.p;
     T.tbl24 = (const uint32_t *)E->tbl24.p;
@@ -403,7 +404,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     E->st.prefilter_v4_fix = img.n_pf_fix;
     E->st.prefilter_v4_dyn = img.n_pf_dyn;
     E->st.lpm4_layout = (uint32_t)img.lpm4_layout;
-    E->st.lpm4_kib = (uint32_t)((4ull * (img.l4c.size() + img.tbl24.size() +
+    E->st.lpm4_kib = (uint32_t)((4ull * (img.l4d.size() + img.l4c.size() + img.tbl24.size() +
                                         img.tbl8.size()) +
                                  8ull * img.l4l.size() + 1023) / 1024);
     E->st.ipcache_v6_prefixes = img.ipc6.n;

@@ -120,7 +120,7 @@ __device__ __forceinline__ uint32_t mkey(int reason, int dir)
 struct Hdr {
     uint32_t sa, da, pt, mt, mk;
     bool valid;
-    uint32_t l4e;
+    uint4 l4d;                   // the /16 directory entry (compact LPM)
     uint32_t e24, pfd, lh, hsh, lxs, lss, pfb;
     uint4 lx, ls, pf, rec;
     bool pf_maybe;
@@ -165,7 +165,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     constexpr bool LPM = MODE != CFC_MODE_XDP;
-    h.l4e = 0;
+    h.l4d = make_uint4(0, 0, 0, 0);
     h.e24 = h.pfd = 0;
     h.lx = h.ls = h.pf = make_uint4(0, 0, 0, 0);
     h.lh = __builtin_bswap32(EGR ? h.da : h.sa);
@@ -173,8 +173,8 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.lxs = h.lss = h.pfb = 0;
     h.pf_maybe = false;
     if (LPM) {
-        if (T.l4c)
-            h.l4e = T.l4c[h.lh >> 16];
+        if (T.l4d)
+            h.l4d = ld16(T.l4d + (h.lh >> 16));
         else if (T.tbl24)
             h.e24 = T.tbl24[h.lh >> 8];
     }
@@ -206,8 +206,8 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     constexpr bool LPM = MODE != CFC_MODE_XDP;
-    if (LPM && T.l4c) {
-        h.e24 = l4_lookup(T, h.lh, h.l4e);
+    if (LPM && T.l4d) {
+        h.e24 = l4_lookup(T, h.lh, h.l4d);
     } else {
         if (h.e24 & LPM_GROUP)
             h.e24 = T.tbl8[((h.e24 & ~LPM_GROUP) << 8) | (h.lh & 0xFF)];

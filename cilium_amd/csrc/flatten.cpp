@@ -19,7 +19,7 @@ uint64_t HostImage::device_bytes() const
     return 4ull * (tbl24.size() + tbl8.size() + lbl_ovf.size() +
                    pf_tbl24.size() + pf_tbl8.size() + pf_fix.size() +
                    pf_bloom.size() + pol_bloom.size()) +
-           4ull * l4c.size() + 8ull * l4l.size() +
+           4ull * (l4d.size() + l4c.size()) + 8ull * l4l.size() +
            sizeof(LxcSlot) * lxc4.size() + sizeof(PolSlot) * pol.size() +
            ipc6.bytes() + pf6_fix.bytes() + pf6_dyn.bytes() +
            sizeof(Lxc6Slot) * lxc6.size() + sizeof(Ct4Slot) * ct4.size() +
@@ -63,7 +63,7 @@ namespace {
 
 // Builder of the compact multibit layout (layout.h).
 struct L4Trie {
-    std::vector<uint32_t> *c, *ovf;
+    std::vector<uint32_t> *d, *c, *ovf;
     std::vector<uint64_t> *l;
     bool ok = true;
 
@@ -84,17 +84,31 @@ struct L4Trie {
     }
 
     // The node for the range `base`/`lvl` whose own covering leaf is `def`;
-    // `longp` holds the prefixes longer than lvl inside the range.
-    uint32_t node(std::vector<Pfx4> &longp, uint32_t base, int lvl, uint32_t def)
+    // `longp` holds the prefixes longer than lvl inside the range.  At the
+    // /16 level (dir != null) the longest two go into the directory entry.
+    uint32_t node(std::vector<Pfx4> &longp, uint32_t base, int lvl, uint32_t def,
+                  uint32_t *dir = nullptr)
     {
         if (longp.empty())
             return def;
         if (longp.size() + 1 < L4_LIST_MAX) {
             std::stable_sort(longp.begin(), longp.end(),
                              [](const Pfx4 &a, const Pfx4 &b) { return a.plen > b.plen; });
+            size_t first = 0;
+            if (dir) {
+                uint64_t e[L4_INLINE] = {0, 0};
+                for (; first < longp.size() && first < L4_INLINE; first++)
+                    e[first] = l4_inline_entry(longp[first].addr, longp[first].plen,
+                                               list_leaf(longp[first].leaf));
+                dir[1] = (uint32_t)e[0];
+                dir[2] = (uint32_t)(e[0] >> 32) | (uint32_t)(e[1] << 16);
+                dir[3] = (uint32_t)(e[1] >> 16);
+                if (first == longp.size())
+                    return def;
+            }
             const size_t off = l->size();   // always even
-            for (const Pfx4 &p : longp)
-                l->push_back(entry(p.addr, p.plen, p.leaf));
+            for (size_t i = first; i < longp.size(); i++)
+                l->push_back(entry(longp[i].addr, longp[i].plen, longp[i].leaf));
             l->push_back(entry(base, lvl, def));
             if (l->size() & 1)
                 l->push_back(l->back());
@@ -134,29 +148,30 @@ struct L4Trie {
 }  // namespace
 
 bool build_l4trie(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
-                  std::vector<uint32_t> *l4c, std::vector<uint64_t> *l4l)
+                  std::vector<uint32_t> *l4d, std::vector<uint32_t> *l4c,
+                  std::vector<uint64_t> *l4l)
 {
     std::stable_sort(pfx.begin(), pfx.end(),
                      [](const Pfx4 &a, const Pfx4 &b) { return a.plen < b.plen; });
-    l4c->assign(1u << 16, 0);
+    l4d->assign(4u << 16, 0);
+    l4c->clear();
     l4l->clear();
     // /0../16: paint the directory's covering leaves, shortest first
     for (const Pfx4 &p : pfx) {
         if (p.plen > 16)
             break;
         const uint32_t start = p.plen ? (p.addr >> 16) & ~((1u << (16 - p.plen)) - 1) : 0;
-        std::fill(l4c->begin() + start, l4c->begin() + start + (1u << (16 - p.plen)),
-                  p.leaf);
+        for (uint32_t j = start; j < start + (1u << (16 - p.plen)); j++)
+            (*l4d)[4 * j] = p.leaf;
     }
     std::map<uint32_t, std::vector<Pfx4>> by16;
     for (const Pfx4 &p : pfx)
         if (p.plen > 16)
             by16[p.addr >> 16].push_back(p);
-    L4Trie b{l4c, ovf, l4l};
+    L4Trie b{l4d, l4c, ovf, l4l};
     for (auto &g : by16) {
-        const uint32_t def = (*l4c)[g.first];
-        const uint32_t e = b.node(g.second, g.first << 16, 16, def);
-        (*l4c)[g.first] = e;
+        uint32_t *dir = l4d->data() + 4 * g.first;
+        dir[0] = b.node(g.second, g.first << 16, 16, dir[0], dir);
     }
     return b.ok;
 }
@@ -558,7 +573,9 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         if (!pfx.empty()) {
             const size_t n_ovf = img->lbl_ovf.size();
             bool trie = opt.lpm4 != LPM4_DIR24_8;
-            if (trie && !build_l4trie(pfx, &img->lbl_ovf, &img->l4c, &img->l4l)) {
+            if (trie && !build_l4trie(pfx, &img->lbl_ovf, &img->l4d, &img->l4c,
+                                      &img->l4l)) {
+                img->l4d.clear();
                 img->l4c.clear();
                 img->l4l.clear();
                 img->lbl_ovf.resize(n_ovf);

@@ -48,7 +48,7 @@ uint32_t lpm6_lookup_host(const Lpm6Host &t, const uint32_t w[4]);
 struct HostImage {
     // IPv4 ipcache: compact multibit (l4c/l4l) or DIR-24-8 (tbl24/tbl8)
     std::vector<uint32_t> tbl24, tbl8, lbl_ovf;
-    std::vector<uint32_t> l4c;
+    std::vector<uint32_t> l4d, l4c;    // l4d: 4 words per /16
     std::vector<uint64_t> l4l;
     int lpm4_layout = 0;           // LPM4_DIR24_8 / LPM4_TRIE, 0 = empty
     uint32_t n_prefix4 = 0;
@@ -98,6 +98,7 @@ void build_dir24_8(std::vector<Pfx4> pfx, std::vector<uint32_t> *tbl24,
 // compact multibit layout (layout.h); labels too wide for a list entry get
 // lbl_ovf entries.  False when an offset would not fit its 24 bits.
 bool build_l4trie(std::vector<Pfx4> pfx, std::vector<uint32_t> *ovf,
-                  std::vector<uint32_t> *l4c, std::vector<uint64_t> *l4l);
+                  std::vector<uint32_t> *l4d, std::vector<uint32_t> *l4c,
+                  std::vector<uint64_t> *l4l);
 
 }  // namespace cfc

@@ -122,8 +122,15 @@ __device__ __forceinline__ uint32_t l4_list_leaf(const DevTables &T, uint32_t hi
     return (l & LL_INDIRECT) ? T.lbl_ovf[l & LL_PAYLOAD] : l;
 }
 __device__ __forceinline__ uint32_t l4_lookup(const DevTables &T, uint32_t a,
-                                              uint32_t e)
+                                              uint4 d)
 {
+    // the directory's inline prefixes first (longest first, layout.h)
+    const uint32_t e1 = (d.z >> 16) | (d.w << 16);
+    if (l4_inline_match(a, d.y))
+        return l4_list_leaf(T, (d.y >> 21) | (d.z << 11));
+    if (l4_inline_match(a, e1))
+        return l4_list_leaf(T, d.w >> 5);
+    uint32_t e = d.x;
     uint32_t shift = 16;   // address bits below the current node
     while (e & L4_PTR) {
         const uint32_t cnt = (e >> 24) & 127, off = e & L4_OFF;

@@ -10,8 +10,8 @@
 // they are small next to 288 GB of HBM3E and stay L2/Infinity-Cache resident.
 //
 // HBM layout of one epoch (read-only while classifying):
-//   lpm4      IPv4 ipcache: the compact multibit layout (l4c nodes + l4l
-//             prefix lists, L2-resident), or DIR-24-8: tbl24 (2^24 x u32 =
+//   lpm4      IPv4 ipcache: the compact multibit layout (l4d directory +
+//             l4c chunks + l4l prefix lists, L2-resident), or DIR-24-8: tbl24 (2^24 x u32 =
 //             64 MiB, Infinity Cache) + 256-entry tbl8 groups for /25-/32
 //   pf4_dyn   same structure for the prefilter LPM deny-list (when used)
 //   pf4_fix   exact /32 deny set: 16-B buckets of 4 addresses (0 = empty)
@@ -43,10 +43,15 @@ constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 
 // ---- IPv4 LPM, compact multibit layout (default) --------------------------
 // DIR-24-8 costs ~1.3 Infinity-Cache accesses per lookup (tbl24 is 64 MiB).
-// The compact layout keeps the whole ipcache in about 1-2 MiB, resident in
-// every XCD's 4 MiB L2:
-//   l4c (u32 nodes)  l4c[0..65535] is the /16 directory; 256-entry chunks
-//                    for the next 8 bits follow.  A node is
+// The compact layout keeps the whole ipcache in about 2-3 MiB, resident in
+// every XCD's 4 MiB L2, and resolves most lookups with ONE 16-byte load:
+//   l4d (16 B x 65536) the /16 directory.  x = the node word (below); y, z, w
+//                    hold up to two of the node's prefixes longer than /16
+//                    inline (48-bit entries, below), its longest two, which
+//                    a lookup checks before following x: a /16 with at most
+//                    two longer prefixes is a single load (x is then the
+//                    covering leaf), a longer list continues in l4l
+//   l4c (u32 nodes)  256-entry chunks for the next 8 bits.  A node word is
 //      bit31 clear              a leaf (LPM leaf encoding above; 0 = none)
 //      bit31 set, cnt == 0      a chunk at l4c[off] for the next 8 bits
 //      bit31 set, cnt  > 0      a list of cnt prefixes at l4l[off]
@@ -57,11 +62,14 @@ constexpr uint32_t EMPTY = 0xFFFFFFFFu;
 //                    lo = prefix address (host order, masked),
 //                    hi = (len & 31) << 27 | leaf27 (LL_INDIRECT -> lbl_ovf)
 // A node lists its prefixes while it has fewer than L4_LIST_MAX, and is
-// split into a chunk beyond; a lookup is the directory word plus, usually,
-// one 16-byte list load.
+// split into a chunk beyond (a split /16 has no inline entries).
+// Inline entry (48 bits; e0 = y | (z & 0xFFFF) << 32, e1 = z >> 16 | w << 16):
+//   bits 0-15 the prefix's address bits 0-15 (masked), bits 16-20 len - 16
+//   (1..16: never 0, so a zero entry is empty), bits 21-47 leaf27.
 constexpr uint32_t L4_PTR = 0x80000000u;
 constexpr uint32_t L4_OFF = 0xFFFFFFu;
 constexpr uint32_t L4_LIST_MAX = 16;
+constexpr uint32_t L4_INLINE = 2;
 constexpr uint32_t LL_INDIRECT = 1u << 26;
 constexpr uint32_t LL_PAYLOAD = (1u << 26) - 1;
 __host__ __device__ inline bool l4_match(uint32_t a, uint32_t addr, uint32_t hi)
@@ -69,6 +77,20 @@ __host__ __device__ inline bool l4_match(uint32_t a, uint32_t addr, uint32_t hi)
     const uint32_t len = hi >> 27;   // 0 stands for 32
     const uint32_t m = len ? 0xFFFFFFFFu << (32 - len) : 0xFFFFFFFFu;
     return (a & m) == addr;
+}
+__host__ __device__ inline uint64_t l4_inline_entry(uint32_t addr, uint32_t len,
+                                                    uint32_t leaf27)
+{
+    return (uint64_t)(addr & 0xFFFFu) | (uint64_t)(len - 16) << 16 |
+           (uint64_t)leaf27 << 21;
+}
+// does inline entry e (nonzero) hold a prefix containing address a (whose
+// top 16 bits are the directory index)
+__host__ __device__ inline bool l4_inline_match(uint32_t a, uint32_t e_lo32)
+{
+    const uint32_t l = (e_lo32 >> 16) & 31;            // len - 16, 0 = empty
+    const uint32_t m = (0xFFFFu << (16 - l)) & 0xFFFFu;
+    return l != 0 && ((a ^ e_lo32) & m) == 0;
 }
 
 // ---- policy: open addressing, linear probing over 16-byte slots -------------
@@ -276,7 +298,8 @@ struct alignas(16) Ct6Slot {
 };
 
 struct DevTables {
-    const uint32_t *l4c;           // compact IPv4 LPM nodes, or null
+    const uint4 *l4d;              // compact IPv4 LPM /16 directory, or null
+    const uint32_t *l4c;           // its chunks
     const uint64_t *l4l;           // its prefix lists
     const uint32_t *tbl24;         // DIR-24-8 layout (null: none or compact)
     const uint32_t *tbl8;

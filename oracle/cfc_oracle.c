@@ -739,10 +739,10 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
                       k1, k2, &action, &td, &ts);
     if (ret < 0)
         return ret;
-    /* two map lookups in the reference; counted in L only when CT maps hold
-     * entries (an empty map cannot change a verdict) */
-    if (o->ct_added)
-        tl_lookups++;
+    /* one or two map lookups in the reference (k1, then k2 on a miss),
+     * counted in L whether or not the maps hold entries: ct_lookup4/6 runs
+     * them on every tc-path packet (conntrack.h:587-640) */
+    tl_lookups++;
     /* *monitor (conntrack.h:221-285, 587-589) against the entry as
      * committed: the batch's own updates are applied afterwards (ct_apply) */
     int64_t e = ct_find(o, k1);
@@ -750,8 +750,7 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
         *res = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
         *pdport = td;
     } else {
-        if (o->ct_added)
-            tl_lookups++;
+        tl_lookups++;
         e = ct_find(o, k2);
         *res = e >= 0 ? CT_ESTABLISHED : CT_NEW;
         *pdport = ts;

@@ -19,7 +19,7 @@ for grp in \
     "WRITE_SIZE" \
     "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" \
     "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT" \
-    "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum" ; do
+    "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum" ; do
     i=$((i+1))
     timeout -s KILL 240 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o run \
         --output-format csv -- python3 bench.py $ARGS > "$OUT/pmc$i.log" 2>&1
