@@ -24,6 +24,47 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 S_IN, S_OUT = 16, 8        # SoA bytes per header in (saddr,daddr,ports,meta) / out
+# bytes the classify kernel streams per header through HBM: the SoA input,
+# verdict + identity + action, and the two counter-key arrays k_hist reads
+STREAM_V4 = S_IN + 4 + 4 + 1 + 4 + 4
+STREAM_V6 = 40 + 4 + 4 + 1 + 4 + 4
+
+
+def ubench_ceilings():
+    """Measured chip-wide random-load rate (G loads/s, best over load width
+    and loads in flight) per table size in MiB: scripts/ubench_random.hip,
+    committed under profiles/ubench/.  One L2 request per load (TCC_REQ of
+    the same kernel, profiles/ubench/README)."""
+    import glob
+    best = {}
+    for f in glob.glob(os.path.join(ROOT, "profiles", "ubench", "random_access_*.jsonl")):
+        for line in open(f):
+            r = json.loads(line)
+            best[r["table_mib"]] = max(best.get(r["table_mib"], 0.0), r["gloads_per_s"])
+    return sorted(best.items())
+
+
+def ceiling_for(ws_bytes, rows):
+    """(table MiB, G loads/s) of the smallest measured table holding ws_bytes."""
+    for mib, rate in rows:
+        if mib * (1 << 20) >= ws_bytes:
+            return mib, rate
+    return rows[-1]
+
+
+def pmc_entry(workload, mode, layout, kernels):
+    """This configuration's per-kernel PMC record (scripts/pmc_summary.py
+    --record), or None when absent or made for other batch sizes."""
+    try:
+        db = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    except (OSError, ValueError):
+        return None
+    for e in db.get("entries", []):
+        if (e["workload"], e["mode"], e["lpm4_layout"]) != (workload, mode, layout):
+            continue
+        if all(k in e["kernels"] and e["kernels"][k]["headers"] == n for k, n in kernels):
+            return e
+    return None
 
 
 def log(*a):
@@ -184,6 +225,7 @@ def main():
     assert tm["launches"] == args.steps * (2 if n6 else 1), tm
     kern_ms = tm["classify_ms"] / args.steps        # classify kernel(s) per step
     count_ms = tm["count_ms"] / args.steps          # counter kernels per step
+    kern6_ms = tm["classify_v6_ms"] / args.steps    # the IPv6 kernel's share
     if world > 1:
         tw = torch.tensor([wall], device=dev, dtype=torch.float64)
         dist.all_reduce(tw, op=dist.ReduceOp.MAX)
@@ -247,19 +289,45 @@ def main():
         mean_l = (n * mean_l + n6 * float(lk6.mean())) / (n + n6)
         b_hdr = algo_bytes / (n + n6)
         samp += s6
-    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            pm = json.load(open(tf))
-            layout = {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none")
-            if (pm.get("headers") == n and pm.get("mode") == args.mode
-                    and pm.get("workload", "c2") == args.workload
-                    and pm.get("lpm4_layout") == layout):
-                traffic = pm.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    algo_gbs = algo_bytes / (kern_ms * 1e-3) / 1e9
+    layout = {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none")
+    # ---- the bound: the chip's random-request rate for the tables' size.
+    # Per kernel: its working set (device tables; CT slots with their timer
+    # and accounting words), the measured random-load ceiling for that size,
+    # and its L2 requests per launch (TCC_REQ, committed PMC pass of this
+    # configuration) over its live HIP-event duration.
+    ws_ct4 = 64 * (1 << max(0, 2 * st["ct4_entries"] - 1).bit_length()) if st["ct4_entries"] else 0
+    ws_ct6 = 96 * (1 << max(0, 2 * st["ct6_entries"] - 1).bit_length()) if st["ct6_entries"] else 0
+    ws4 = st["device_bytes"] - 1024 * st["lpm6_kib"] + ws_ct4
+    ws6 = st["device_bytes"] - 1024 * st["lpm4_kib"] + ws_ct6
+    kernels = [("k_classify_v4", n, kern_ms - kern6_ms, ws4)]
+    if n6:
+        kernels.append(("k_classify_v6", n6, kern6_ms, ws6))
+    rows = ubench_ceilings()
+    pe = pmc_entry(args.workload, args.mode, layout, [(k, hn) for k, hn, _, _ in kernels])
+    per_kernel = []
+    req_tot = ideal_s = traffic = 0.0
+    for k, hn, ms, ws in kernels:
+        mib, peak_k = ceiling_for(ws, rows)
+        d = {"kernel": k, "headers": hn, "ms_per_launch": round(ms, 4),
+             "working_set_mib": round(ws / (1 << 20), 2),
+             "ceiling_table_mib": mib, "ceiling_greq_s": peak_k}
+        if pe:
+            pk = pe["kernels"][k]
+            req = pk["l2_requests_per_launch"]
+            d.update({"l2_requests_per_launch": req,
+                      "l2_requests_per_header": round(req / hn, 3),
+                      "achieved_greq_s": round(req / (ms * 1e-3) / 1e9, 1),
+                      "frac": round(req / (ms * 1e-3) / 1e9 / peak_k, 4),
+                      "hbm_bytes_per_launch": pk["hbm_bytes_per_launch"]})
+            req_tot += req
+            ideal_s += req / (peak_k * 1e9)
+            traffic += pk["hbm_bytes_per_launch"]
+        per_kernel.append(d)
+    stream_b = n * STREAM_V4 + n6 * STREAM_V6
+    bound = ("l2" if all(d["ceiling_table_mib"] <= 6 for d in per_kernel)
+             else "infinity-cache" if all(d["ceiling_table_mib"] <= 256 for d in per_kernel)
+             else "hbm-random")
     res = {
         "metric": "classified headers/sec (Mpps, whole node) at 100k-prefix "
                   "ipcache + 16k-ID policy",
@@ -298,14 +366,27 @@ def main():
         },
         "roofline": {
             "kernel": "k_classify_v4" + (" + k_classify_v6" if n6 else ""),
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "bytes_per_header": round(b_hdr, 2),
-            "mean_lookups_per_header": round(mean_l, 4),
+            # random L2 (or Infinity-Cache) requests: the measured request-rate
+            # ceiling for the tables' size is the bound
+            "bound": bound,
+            "achieved": round(req_tot / (kern_ms * 1e-3) / 1e9, 1) if pe else None,
+            "peak": round(req_tot / ideal_s / 1e9, 1) if pe else None,
+            "unit": "Greq/s",
+            "frac": round(ideal_s / (kern_ms * 1e-3), 4) if pe else None,
+            "traffic": traffic if pe else None,
+            "pmc_source": pe["source"] if pe else None,
+            "kernels": per_kernel,
+            "hbm_stream": {
+                "bytes_per_header": round(stream_b / (n + n6), 2),
+                "achieved_gbs": round(stream_b / (kern_ms * 1e-3) / 1e9, 1),
+                "peak_gbs": HBM_PEAK_GBS,
+                "frac": round(stream_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "algorithmic": {   # 24 B of header I/O + 64 B per map lookup
+                "bytes_per_header": round(b_hdr, 2),
+                "mean_lookups_per_header": round(mean_l, 4),
+                "gbs": round(algo_gbs, 1),
+            },
             "kernel_ms_per_launch": round(kern_ms, 4),
             "count_kernels_ms_per_launch": round(count_ms, 4),
             "call_ms_per_launch": round(call_ms, 4),

@@ -99,7 +99,8 @@ IDENTITY_OUT_OF_RANGE = 0xFFFFFFFF
 
 class Timing(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("classify_ms", ctypes.c_double),
-                ("count_ms", ctypes.c_double)]
+                ("count_ms", ctypes.c_double), ("launches_v6", ctypes.c_uint64),
+                ("classify_v6_ms", ctypes.c_double), ("count_v6_ms", ctypes.c_double)]
 
 
 _lib = None

@@ -9,6 +9,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/cfc.h"
@@ -470,7 +471,7 @@ int before_counter_write(cfc_ctx *c, Map *m)
 }
 
 // the next set of timing events (grown on demand, reused after a collect)
-const LaunchTiming *next_timing(cfc_ctx *c)
+const LaunchTiming *next_timing(cfc_ctx *c, bool v6)
 {
     if (!c->timing)
         return nullptr;
@@ -481,6 +482,7 @@ const LaunchTiming *next_timing(cfc_ctx *c)
                 return nullptr;
         c->tpool.push_back(t);
     }
+    c->tpool[c->tused].v6 = v6;
     return &c->tpool[c->tused++];
 }
 
@@ -599,6 +601,11 @@ int cfc_timing_collect(cfc_ctx *c, cfc_timing *out)
         out->launches++;
         out->classify_ms += a;
         out->count_ms += b;
+        if (t.v6) {
+            out->launches_v6++;
+            out->classify_v6_ms += a;
+            out->count_v6_ms += b;
+        }
     }
     c->tused = 0;
     return 0;
@@ -863,7 +870,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     if (c->ctr_pending && c->last_stream != s)
         (void)hipStreamWaitEvent(s, c->last_done, 0);
     rc = launch(T, *in, *out, mode, ea, c->ctr, c->ws, c->num_cus, s,
-                in->n ? next_timing(c) : nullptr);
+                in->n ? next_timing(c, std::is_same<Hdr, cfc_hdr_v6>::value) : nullptr);
     if (rc)
         return rc;
     (void)hipEventRecord(c->last_done, s);

@@ -174,7 +174,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.pf_maybe = false;
     if (LPM) {
         if (T.l4d)
-            h.l4d = ld16(T.l4d + (h.lh >> 16));
+            h.l4d = ldt16(T.l4d, (h.lh >> 16) * 16u);
         else if (T.tbl24)
             h.e24 = T.tbl24[h.lh >> 8];
     }
@@ -192,7 +192,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
         h.pf_maybe = !S.pfb || bloom_maybe(S.pfb_off, S.pfb_mask, pf_bloom_hash(h.sa));
         if (h.pf_maybe) {
             h.pfb = hash32(h.sa, T.pf_fix_mask);
-            h.pf = ld16(T.pf_fix + (size_t)h.pfb * PF_SLOTS);
+            h.pf = ldt16(T.pf_fix, h.pfb * 16u);
         }
     }
 }

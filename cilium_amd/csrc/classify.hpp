@@ -78,6 +78,7 @@ struct CountArgs {
 // kernels.
 struct LaunchTiming {
     hipEvent_t ev[3];
+    bool v6;            // an IPv6 launch (cfc_timing's *_v6 sums)
 };
 
 // Workspace of one launch over n headers: the key arrays of CountArgs, then

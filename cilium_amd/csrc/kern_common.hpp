@@ -87,6 +87,18 @@ __device__ __forceinline__ uint4 ld16(const void *p)
     return *reinterpret_cast<const uint4 *>(p);
 }
 
+// 16-byte table load that stays ONE load: a plain uint4 load whose upper
+// half is only used on some paths gets split by the compiler into two
+// dependent 8-byte loads (a second L2 round trip); a buffer load is never
+// split.  base: the table (wave-uniform, < 4 GiB), off: byte offset.
+__device__ __forceinline__ uint4 ldt16(const void *base, uint32_t off)
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // Workgroup-shared state: LDS copies of the small tables.  Accessed through
 // the extern __shared__ symbol with dword offsets (not through pointers kept
 // in a struct, which would lose the LDS address space and turn every read
@@ -140,11 +152,10 @@ __device__ __forceinline__ uint32_t l4_lookup(const DevTables &T, uint32_t a,
             continue;
         }
         for (uint32_t i = 0; i < cnt; i += 2) {
-            const uint4 v = ld16(T.l4l + off + i);
-            if (l4_match(a, v.x, v.y))
-                return l4_list_leaf(T, v.y);
-            if (l4_match(a, v.z, v.w))
-                return l4_list_leaf(T, v.w);
+            const uint4 v = ldt16(T.l4l, (off + i) * 8u);
+            const bool m0 = l4_match(a, v.x, v.y);
+            if (m0 || l4_match(a, v.z, v.w))
+                return l4_list_leaf(T, m0 ? v.y : v.w);
         }
         return 0;   // not reached: a list ends with its node's own prefix
     }
@@ -181,7 +192,7 @@ __device__ __forceinline__ bool pf_resolve(const DevTables &T, uint32_t addr,
         if (!v.x || !v.y || !v.z || !v.w)
             return false;
         b = (b + 1) & T.pf_fix_mask;
-        v = ld16(T.pf_fix + (size_t)b * PF_SLOTS);
+        v = ldt16(T.pf_fix, b * 16u);
     }
 }
 
@@ -468,7 +479,7 @@ __device__ __forceinline__ void policy_probe_key(const DevTables &T,
     P.j = P.maybe ? __builtin_ctz(P.maybe) : 3;
     if (P.j < 3) {
         P.s = pol_slot(P.pre(P.j), mask);
-        P.v = ld16(T.pol + base + P.s);
+        P.v = ldt16(T.pol, (base + P.s) * 16u);
     }
 }
 
@@ -523,7 +534,7 @@ __device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
             if (key == POL_EMPTY)
                 break;
             s = (s + 1) & mask;
-            v = ld16(T.pol + base + s);
+            v = ldt16(T.pol, (base + s) * 16u);
         }
         if (hit) {
             ctr = v.w;
@@ -534,7 +545,7 @@ __device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
         j = maybe ? __builtin_ctz(maybe) : 3;
         if (j < 3) {
             s = pol_slot(P0.pre(j), mask);
-            v = ld16(T.pol + base + s);
+            v = ldt16(T.pol, (base + s) * 16u);
         }
     }
     return PolicyResult{verdict, ctr};

@@ -262,11 +262,11 @@ class Datapath:
 
     def timing_collect(self):
         """Kernel device time of the calls since the last collect (needs
-        OPT_TIMING): {launches, classify_ms, count_ms} (sums)."""
+        OPT_TIMING): {launches, classify_ms, count_ms} (sums over every
+        call) and the same three for the IPv6 calls among them (*_v6)."""
         t = L.Timing()
         L.check(self.L.cfc_timing_collect(self.h, ctypes.byref(t)), "timing")
-        return {"launches": t.launches, "classify_ms": t.classify_ms,
-                "count_ms": t.count_ms}
+        return {f: getattr(t, f) for f, _ in L.Timing._fields_}
 
     def commit(self, stream=None):
         L.check(self.L.cfc_commit(self.h, self._stream(stream)),"commit")

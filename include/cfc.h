@@ -466,11 +466,15 @@ const char *cfc_strerror(int err);
 
 /* Device time of the kernels of the cfc_classify_* calls made since the
  * previous collect with CFC_OPT_TIMING on (waits for them to finish):
- * classify_ms sums the lookup kernel, count_ms the counter kernels. */
+ * classify_ms sums the lookup kernel, count_ms the counter kernels, over
+ * every call; the *_v6 fields the cfc_classify_v6 calls among them. */
 typedef struct {
     uint64_t launches;
     double classify_ms;
     double count_ms;
+    uint64_t launches_v6;
+    double classify_v6_ms;
+    double count_v6_ms;
 } cfc_timing;
 int cfc_timing_collect(cfc_ctx *ctx, cfc_timing *out);
 

@@ -1,74 +1,149 @@
 """Summarise a scripts/profile.sh output directory: per-kernel average
-duration (kernel trace) and per-launch counter values for the classify
-kernel, plus HBM traffic per launch corrected as MI355X_MICROARCH.md's HBM
+duration (kernel trace) and per-launch counter values of every engine
+kernel, with HBM traffic per launch corrected as MI355X_MICROARCH.md's HBM
 section prescribes (FETCH_SIZE reads 1/2 of wide coalesced streaming reads
 on gfx950; the random 4-64 B lookups are reported as measured).
 
-usage: python3 scripts/pmc_summary.py OUTDIR [kernel-substring] [--traffic HEADERS MODE STREAM_BYTES_PER_HDR LPM4_LAYOUT]
+usage: python3 scripts/pmc_summary.py OUTDIR [kernel-substring]
+           [--save PROFILE_DIR]
+           [--record WORKLOAD MODE LPM4_LAYOUT KERNEL:HEADERS:STREAM_BYTES ...]
 
-With --traffic, also writes profiles/pmc_traffic.json, which bench.py reports
-as roofline.traffic when its batch size, mode and ipcache layout match: HBM-side bytes per
-launch = FETCH_SIZE (x1 for the random lookups, +1x the streamed SoA input
-bytes, which FETCH_SIZE counts at half on gfx950) + WRITE_SIZE.
+--save copies the kernel statistics, the engine's rows of every counter pass
+(cfc:: kernels only) and this summary into PROFILE_DIR (the committed
+profiles/ tree).
+
+--record adds (or replaces) this configuration's entry in
+profiles/pmc_traffic.json, which bench.py reads for its roofline when the
+workload, mode, ipcache layout and per-kernel batch sizes match: per kernel
+the L2 requests per launch (TCC_REQ_sum) and the HBM-side bytes per launch =
+FETCH_SIZE + 1/2 x the streamed input bytes (HEADERS x STREAM_BYTES, which
+FETCH_SIZE counts at half on gfx950) + WRITE_SIZE.
 """
 import csv
 import glob
-import re
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-def main(out, kname="k_classify_v4", traffic=None):
+
+def kernel_name(full):
+    m = re.search(r"(k_\w+)", full)
+    return m.group(1) if m else full.split("(")[0]
+
+
+def collect(out):
     res = {"kernels": {}, "counters": {}}
     ks = glob.glob(os.path.join(out, "kt", "*kernel_stats.csv"))
     if ks:
         for r in csv.DictReader(open(ks[0])):
-            if "cfc" in r["Name"] or kname in r["Name"]:
-                m = re.search(r"(k_\w+)", r["Name"])
-                res["kernels"][m.group(1) if m else r["Name"].split("(")[0]] = {
-                    "calls": int(r["Calls"]),
-                    "avg_ms": float(r["AverageNs"]) / 1e6}
-    vals = defaultdict(list)
+            if "cfc::" in r["Name"]:
+                res["kernels"][kernel_name(r["Name"])] = {
+                    "calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
+    vals = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(out, "pmc*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
-            if kname in r["Kernel_Name"]:
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for k, v in vals.items():
-        res["counters"][k] = sum(v) / len(v)
-    c = res["counters"]
-    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        res["hbm_fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
-        res["hbm_write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
-    if "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"]:
+            if "cfc::" in r["Kernel_Name"]:
+                vals[kernel_name(r["Kernel_Name"])][r["Counter_Name"]].append(
+                    float(r["Counter_Value"]))
+    for k, cs in vals.items():
+        res["counters"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
+    return res
+
+
+def derived(c):
+    d = {}
+    if "FETCH_SIZE" in c:
+        d["hbm_fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in c:
+        d["hbm_write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+    if c.get("SQ_WAVE_CYCLES"):
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in c:
-                res[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
+                d[k + "_frac"] = c[k] / c["SQ_WAVE_CYCLES"]
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
-        res["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
-    if traffic and "hbm_fetch_bytes_per_launch" in res:
-        n, mode, sb, layout = int(traffic[0]), traffic[1], float(traffic[2]), traffic[3]
-        fix = 0.5 * n * sb
-        res["hbm_bytes_per_launch"] = (res["hbm_fetch_bytes_per_launch"] + fix
-                                       + res["hbm_write_bytes_per_launch"])
-        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        with open(os.path.join(root, "profiles", "pmc_traffic.json"), "w") as f:
-            json.dump({"headers": n, "mode": mode, "lpm4_layout": layout,
-                       "source": out,
-                       "stream_read_bytes_per_header": sb,
-                       "fetch_size_bytes": res["hbm_fetch_bytes_per_launch"],
-                       "write_size_bytes": res["hbm_write_bytes_per_launch"],
-                       "hbm_bytes_per_launch": res["hbm_bytes_per_launch"]},
-                      f, indent=1)
-    print(json.dumps(res, indent=1))
+        d["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    return d
+
+
+def save(out, dst, res):
+    import shutil
+    os.makedirs(dst, exist_ok=True)
+    ks = glob.glob(os.path.join(out, "kt", "*kernel_stats.csv"))
+    if ks:
+        shutil.copy(ks[0], os.path.join(dst, "kernel_stats.csv"))
+    for f in sorted(glob.glob(os.path.join(out, "pmc*", "*counter_collection.csv"))):
+        name = os.path.basename(os.path.dirname(f)) + ".csv"
+        with open(f) as fi, open(os.path.join(dst, name), "w", newline="") as fo:
+            r = csv.DictReader(fi)
+            w = csv.DictWriter(fo, fieldnames=r.fieldnames)
+            w.writeheader()
+            for row in r:
+                if "cfc::" in row["Kernel_Name"]:
+                    w.writerow(row)
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def record(res, workload, mode, layout, specs, source):
+    """Write this configuration's per-kernel entry into profiles/pmc_traffic.json."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        db = json.load(open(path))
+        entries = db.get("entries", [])
+    except (OSError, ValueError):
+        entries = []
+    kern = {}
+    for spec in specs:
+        k, n, sb = spec.split(":")
+        c = res["counters"][k]
+        kern[k] = {
+            "headers": int(n),
+            "stream_read_bytes_per_header": float(sb),
+            "l2_requests_per_launch": c["TCC_REQ_sum"],
+            "hbm_bytes_per_launch": (c["FETCH_SIZE"] * 1024 + 0.5 * int(n) * float(sb)
+                                     + c["WRITE_SIZE"] * 1024),
+            "avg_ms": res["kernels"][k]["avg_ms"],
+        }
+    e = {"workload": workload, "mode": mode, "lpm4_layout": layout,
+         "source": source, "kernels": kern}
+    entries = [x for x in entries
+               if (x["workload"], x["mode"], x["lpm4_layout"]) != (workload, mode, layout)]
+    entries.append(e)
+    with open(path, "w") as f:
+        json.dump({"entries": entries}, f, indent=1)
+    return e
+
+
+def main(argv):
+    a = list(argv)
+    rec = dst = None
+    if "--record" in a:
+        i = a.index("--record")
+        rec = a[i + 1:]
+        a = a[:i]
+    if "--save" in a:
+        i = a.index("--save")
+        dst = a[i + 1]
+        a = a[:i] + a[i + 2:]
+    out = a[0]
+    kname = a[1] if len(a) > 1 else "k_classify_v4"
+    res = collect(out)
+    for k, c in res["counters"].items():
+        res.setdefault("derived", {})[k] = derived(c)
+    res["focus"] = kname
+    if dst:
+        save(out, dst, res)
+    if rec:
+        res["recorded"] = record(res, rec[0], rec[1], rec[2], rec[3:],
+                                 os.path.relpath(dst or out, ROOT))
+    print(json.dumps({"kernels": res["kernels"],
+                      "counters": res["counters"].get(kname),
+                      "derived": res.get("derived", {}).get(kname)}, indent=1))
 
 
 if __name__ == "__main__":
-    a = sys.argv[1:]
-    tr = None
-    if "--traffic" in a:
-        i = a.index("--traffic")
-        tr = a[i + 1:i + 5]
-        a = a[:i] + a[i + 5:]
-    main(*a, traffic=tr)
+    main(sys.argv[1:])

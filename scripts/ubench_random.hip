@@ -7,7 +7,8 @@
 // and HBM-resident tables, 4-byte and 16-byte loads.
 //
 //   hipcc --offload-arch=gfx950 -O3 -o ubench_random scripts/ubench_random.hip
-//   ./ubench_random            -> one JSON line per (table size, load width)
+//   ./ubench_random [MiB ...]  -> one JSON line per (table size, load width,
+//                                 loads in flight per lane)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -70,13 +71,43 @@ __global__ __launch_bounds__(1024) void k_random(const uint4 *tab, uint32_t mask
         sink[0] = acc;
 }
 
-int main()
+template <int ILP>
+static float run(bool wide, int grid, const uint4 *tab, uint32_t mask, int iters,
+                 uint32_t *sink)
+{
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    for (int rep = 0; rep < 2; rep++) {   // first pass warms caches
+        CHECK(hipEventRecord(a));
+        if (wide)
+            hipLaunchKernelGGL((k_random<ILP, true>), dim3(grid), dim3(1024), 0, 0,
+                               tab, mask, iters, sink);
+        else
+            hipLaunchKernelGGL((k_random<ILP, false>), dim3(grid), dim3(1024), 0, 0,
+                               tab, mask, iters, sink);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+    }
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return ms;
+}
+
+int main(int argc, char **argv)
 {
     int cus = 256;
     hipDeviceProp_t p;
     CHECK(hipGetDeviceProperties(&p, 0));
     cus = p.multiProcessorCount;
-    const size_t sizes_mb[] = {1, 2, 8, 32, 64, 128, 192, 512, 4096};
+    std::vector<size_t> sizes_mb = {1, 2, 8, 32, 64, 128, 192, 512, 4096};
+    if (argc > 1) {
+        sizes_mb.clear();
+        for (int i = 1; i < argc; i++)
+            sizes_mb.push_back((size_t)atoi(argv[i]));
+    }
     uint32_t *sink;
     CHECK(hipMalloc(&sink, 4));
     for (size_t mb : sizes_mb) {
@@ -86,31 +117,18 @@ int main()
         CHECK(hipMalloc(&tab, bytes));
         CHECK(hipMemset(tab, 1, bytes));
         for (int wide = 0; wide < 2; wide++) {
-            const int grid = cus * 2, iters = 64;
-            const int ILP = 8;
-            hipEvent_t a, b;
-            CHECK(hipEventCreate(&a));
-            CHECK(hipEventCreate(&b));
-            for (int rep = 0; rep < 2; rep++) {   // first pass warms caches
-                CHECK(hipEventRecord(a));
-                if (wide)
-                    hipLaunchKernelGGL((k_random<ILP, true>), dim3(grid), dim3(1024), 0, 0,
-                                       tab, (uint32_t)(n16 - 1), iters, sink);
-                else
-                    hipLaunchKernelGGL((k_random<ILP, false>), dim3(grid), dim3(1024), 0, 0,
-                                       tab, (uint32_t)(n16 - 1), iters, sink);
-                CHECK(hipEventRecord(b));
-                CHECK(hipEventSynchronize(b));
+            for (int ilp : {4, 8, 16}) {
+                const int grid = cus * 2, iters = 64;
+                const uint32_t mask = (uint32_t)(n16 - 1);
+                const float ms = ilp == 4 ? run<4>(wide, grid, tab, mask, iters, sink)
+                                 : ilp == 8 ? run<8>(wide, grid, tab, mask, iters, sink)
+                                            : run<16>(wide, grid, tab, mask, iters, sink);
+                const double loads = (double)grid * 1024 * iters * ilp;
+                printf("{\"table_mib\": %zu, \"load_bytes\": %d, \"ilp\": %d, "
+                       "\"gloads_per_s\": %.2f, \"ms\": %.3f}\n",
+                       mb, wide ? 16 : 4, ilp, loads / (ms * 1e-3) / 1e9, ms);
+                fflush(stdout);
             }
-            float ms;
-            CHECK(hipEventElapsedTime(&ms, a, b));
-            double loads = (double)grid * 1024 * iters * ILP;
-            printf("{\"table_mib\": %zu, \"load_bytes\": %d, \"gloads_per_s\": %.2f, "
-                   "\"ms\": %.3f}\n",
-                   mb, wide ? 16 : 4, loads / (ms * 1e-3) / 1e9, ms);
-            fflush(stdout);
-            CHECK(hipEventDestroy(a));
-            CHECK(hipEventDestroy(b));
         }
         CHECK(hipFree(tab));
     }
