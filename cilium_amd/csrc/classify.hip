@@ -140,21 +140,43 @@ struct Hdr {
     PolicyProbe P;
 };
 
-// round 1: the header (non-temporal streaming loads).  Lanes past the end
-// of the slice take the slice's last header: they compute exactly what its
-// own lane computes and store the same values to the same places, so no
-// round needs a validity branch; only the metrics count them out.
-__device__ __forceinline__ void r1_load(const cfc_hdr_v4 &in, uint64_t i,
-                                        uint64_t end, Hdr &h)
+// round 1: the header (non-temporal streaming loads), issued one iteration
+// ahead: the loads of iteration k + 1 go out right after iteration k's last
+// table probe, so their HBM latency overlaps that probe's (loads return in
+// issue order, so waiting for the probe does not wait for them).  Lanes past
+// the end of the slice take the slice's last header: they compute exactly
+// what its own lane computes and store the same values to the same places,
+// so no round needs a validity branch; only the metrics count them out.
+struct Raw {
+    uint32_t sa, da, pt, mt, mk, tf;
+};
+__device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, uint64_t i,
+                                         uint64_t end, Raw &r)
+{
+    // no branches here: a load issued on only one side of a branch makes the
+    // compiler's wait at the join conservative (vmcnt(0)), which would wait
+    // for these HBM loads together with the probe before them.  Absent
+    // optional arrays read saddr instead and the value is dropped.
+    i = i < end ? i : end - 1;
+    r.sa = ld_nt(in.saddr + i);
+    r.da = ld_nt(in.daddr + i);
+    r.pt = ld_nt(in.ports + i);
+    r.mt = ld_nt(in.meta + i);
+    const uint32_t mk = ld_nt((in.mark ? in.mark : in.saddr) + i);
+    const uint32_t tf = (in.tcp_flags ? in.tcp_flags : (const uint8_t *)in.saddr)[i];
+    r.mk = in.mark ? mk : 0u;
+    r.tf = in.tcp_flags ? tf : 0u;
+}
+__device__ __forceinline__ void r1_take(const Raw &r, uint64_t i, uint64_t end,
+                                        Hdr &h)
 {
     h.valid = i < end;
-    i = h.valid ? i : end - 1;
-    h.sa = ld_nt(in.saddr + i);
-    h.da = ld_nt(in.daddr + i);
-    h.pt = ld_nt(in.ports + i);
-    h.mt = ld_nt(in.meta + i);
-    h.mk = in.mark ? ld_nt(in.mark + i) : 0u;
-    h.tf = in.tcp_flags ? (uint32_t)in.tcp_flags[i] : 0u;
+    h.sa = r.sa;
+    h.da = r.da;
+    h.pt = r.pt;
+    h.mt = r.mt;
+    h.mk = r.mk;
+    h.tf = r.tf;
 }
 
 // round 2: every lookup that only needs the header
@@ -538,17 +560,29 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     MetAcc<acc_n<MODE>()> acc;
     acc.clear();
     uint32_t iter = 0;
+    Raw nx[U];
+    if (start >= end)
+        return;   // (uniform: no header for this workgroup; nothing to publish)
+#pragma unroll
+    for (int u = 0; u < U; u++)
+        r1_issue(in, start + (uint64_t)u * BLOCK + threadIdx.x, end, nx[u]);
     for (uint64_t base = start; base < end; base += (uint64_t)BLOCK * U) {
         Hdr h[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r1_load(in, base + (uint64_t)u * BLOCK + threadIdx.x, end, h[u]);
+            r1_take(nx[u], base + (uint64_t)u * BLOCK + threadIdx.x, end, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r2_issue<MODE>(T, S, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r3_identity<MODE, CT>(T, S, E, h[u]);
+        // the next iteration's headers, behind this one's policy probe (the
+        // last iteration re-reads the slice's last header)
+        const uint64_t nb = base + (uint64_t)BLOCK * U;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            r1_issue(in, nb + (uint64_t)u * BLOCK + threadIdx.x, end, nx[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r4_verdict<MODE, CT, NT>(T, S, E, h[u]);

@@ -802,3 +802,101 @@ def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1):
                          local_frac=1.0, proxy_ident=proxy_identities(t))
     h = concat([old, new])
     return take(h, rng.permutation(n))
+
+
+# ------------------------------------------------------------ C1
+C1_POLICIES = "tests/golden/c1_policies.json"
+C1_PORTS = np.array([80, 443, 53, 8080], dtype=np.uint32)
+# label values the example policies select on (examples/policies/{l3,l4})
+C1_LABELS = {"role": ["frontend", "backend", "crawler", "restricted", "public",
+                      "victim", "db"],
+             "app": ["myService", "test-app", "web"],
+             "env": ["dev", "prod"],
+             "app-type": ["dns"],
+             "id": ["app2"]}
+# the local endpoints: one per label set some example rule selects
+C1_LOCAL = [{"role": "backend"}, {"app": "myService"}, {"role": "frontend"},
+            {"role": "crawler"}, {"env": "prod", "role": "backend"},
+            {"role": "public"}, {"role": "victim"}, {"env": "dev"},
+            {"role": "restricted"}, {"id": "app2"}, {"app": "test-app"}]
+
+
+def config_c1(seed=1, n_pods=100, policies=None):
+    """C1 (BASELINE.json configs[0]): the MapState of every
+    local endpoint under the example policies of examples/policies/{l3,l4}
+    (cilium_amd.policy_resolver), ~100 pod identities 256-355 plus the
+    reserved ones and one CIDR identity per prefix the rules name; ipcache:
+    /32s of every pod (1-4 each) and local endpoint, plus the CIDR prefixes.
+    Returns (tables, resolver context {identities, local labels})."""
+    import os
+    from . import policy_resolver as R
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    repo = R.Repository(R.load_fixture(policies or os.path.join(root, C1_POLICIES)))
+    rng = np.random.default_rng(seed)
+    pods = {}
+    for i, lb in enumerate(C1_LOCAL):          # the local endpoints' identities
+        pods[256 + i] = lb
+    while len(pods) < n_pods:
+        d = {}
+        for k, vals in C1_LABELS.items():
+            p = {"role": 0.85, "app": 0.5, "env": 0.6}.get(k, 0.08)
+            if rng.random() < p:
+                d[k] = str(rng.choice(vals))
+        if d:
+            pods[256 + len(pods)] = d
+    pod_ids = {i: R.pod_labels(d) for i, d in pods.items()}
+    cidrs = repo.cidrs()
+    cidr_ids = {R.LOCAL_IDENTITY_FLAG + 1 + j: R.cidr_labels(c) for j, c in enumerate(cidrs)}
+    idents = R.identity_cache(pod_ids, cidr_ids)
+    # local endpoints: EP_LXC_ID first (the reference harness's own LXC)
+    eps, pol, sec = [], {}, {}
+    for i, lb in enumerate(C1_LOCAL):
+        lxc = EP_LXC_ID if i == 0 else 0x2000 + i
+        addr = LXC_IPV4 if i == 0 else ip4(f"10.0.1.{i}")
+        eps.append(endpoint_v4(addr, 100 + i, lxc))
+        ms = repo.map_state(R.pod_labels(lb), idents)
+        rows = np.zeros(len(ms), POLICY_DT)
+        for j, (k, proxy) in enumerate(sorted(ms.items())):
+            rows[j] = (k[0], int(htons(k[1])), k[2], k[3], proxy)
+        pol[lxc] = rows
+        sec[lxc] = 256 + i
+    eps.append(endpoint_v4(ip4("10.0.255.254"), 0, 0xFFF0, flags=1))   # host
+    sec[0xFFF0] = EP_SECLABEL
+    eps = np.concatenate(eps)
+    # ipcache: pods' /32s (in 10.1.0.0/16 and 172.20.0.0/16), the local
+    # endpoints, the CIDR prefixes with their CIDR identities
+    a, l, ident = [], [], []
+    for pid in range(256 + len(C1_LOCAL), 256 + len(pods)):
+        for _ in range(int(rng.integers(1, 5))):
+            base = ip4("10.1.0.0") if rng.random() < 0.7 else ip4("172.20.0.0")
+            a.append(byteswap32(np.uint32(byteswap32(np.uint32(base)) +
+                                          int(rng.integers(1, 65535)))))
+            l.append(32)
+            ident.append(pid)
+    for e, lxc in zip(eps, [int(x) for x in eps["lxc_id"]]):
+        if lxc in sec and lxc != 0xFFF0:
+            a.append(e["addr"][:4].copy().view("<u4")[0])
+            l.append(32)
+            ident.append(sec[lxc])
+    for j, c in enumerate(cidrs):
+        net = c.split("/")
+        a.append(ip4(net[0]))
+        l.append(int(net[1]))
+        ident.append(R.LOCAL_IDENTITY_FLAG + 1 + j)
+    a = np.array(a, np.uint32)
+    _, first = np.unique(np.stack([a, np.array(l)]), axis=1, return_index=True)
+    first = np.sort(first)
+    ipc = _v4_entries(a[first], np.array(l)[first], np.array(ident, np.uint32)[first])
+    t = Tables(ipc, eps, pol, np.zeros(0, PREFILTER_DT), sec)
+    return t, {"identities": idents, "local": C1_LOCAL}
+
+
+def headers_c1(t: Tables, n, seed=1):
+    """C1 stream: sources 90% inside an ipcache prefix,
+    10% uniform; destinations the local endpoints (97%); dport from
+    {80, 443, 53, 8080} (60%) or uniform; TCP 70% / UDP 25% / ICMP 5%;
+    1% fragments; len U[60, 1500]."""
+    rng = np.random.default_rng(seed + 1000)
+    loc = local_v4_addrs(t)[:len(C1_LOCAL)]
+    return gen_headers_v4(rng, n, t.ipcache, loc, ports=C1_PORTS, other_proto=0.0,
+                          mark_host=0.02, mark_proxy=0.0)

@@ -499,6 +499,19 @@ def sc_small_ingress(n=20000, seed=1):
     return t, h, MODE_INGRESS, None
 
 
+def sc_c1_ingress(n=20000, seed=1):
+    """C1 (BASELINE.json configs[0]): the MapState the example policies of
+    examples/policies/{l3,l4} give 11 local endpoints (cilium_amd.
+    policy_resolver), ~100 pod + reserved + CIDR identities; the C1 stream
+    into those endpoints.  The harness runs one bpf_lxc.o, so every
+    endpoint carries the compiled SECLABEL here."""
+    t, _ = S.config_c1(seed)
+    t.seclabel = {k: S.EP_SECLABEL for k in t.seclabel}
+    h = S.headers_c1(t, int(n * 1.02), seed=seed)
+    h = _keep(h, S.ensure_no_reverse(h)).slice(0, n)
+    return t, h, MODE_INGRESS, None
+
+
 def sc_edge_ingress(seed=7):
     """Hand-picked fallback cases: L4 hit, L3 fallback, wildcard port,
     fragments (L3 only), proxy, ICMP echo -> port 2048 quirk, unknown proto,
@@ -924,6 +937,7 @@ def _keep(h, m):
 SCENARIOS = {
     "edge_ingress_v4": sc_edge_ingress,
     "small_ingress_v4": sc_small_ingress,
+    "c1_ingress_v4": sc_c1_ingress,
     "c2_ingress_v4": sc_c2_ingress,
     "c2_egress_v4": sc_c2_egress,
     "xdp_v4": sc_xdp,

@@ -137,3 +137,30 @@ def test_c5_full_flows(torch):
     np.testing.assert_array_equal(got, want)
     log(f"C5: CT maps compared ({len(got)} entries) {time.time() - t0:.1f}s")
     dp.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_c1_million(torch, mode):
+    """C1 (configs[0]): the example policies' MapState over 11 endpoints,
+    1M headers: ingress to every endpoint, or egress from app=myService
+    (L4 + CIDR rules), every output and counter against the oracle."""
+    t, _ = S.config_c1(1)
+    if mode == 0:
+        ep, h = 0, S.headers_c1(t, 1_000_000, seed=11)
+    else:
+        ep = [x for x in t.policy if t.seclabel[x] == 257][0]
+        addr = t.endpoints["addr"][t.endpoints["lxc_id"] == ep][0, :4].copy().view("<u4")[0]
+        rng = np.random.default_rng(12)
+        h = S.gen_headers_v4(rng, 1_000_000, t.ipcache, S.local_v4_addrs(t),
+                             local_frac=0.2, src_fixed=addr, ports=S.C1_PORTS,
+                             other_proto=0.0)
+    dp = Datapath(0)
+    pms = load_tables(dp, t)
+    out = dp.classify(pack(h), mode, ep)
+    torch.cuda.synchronize()
+    o = O.Oracle(t)
+    oa, ov, oi = o.classify(h, mode, ep, nthreads=16)
+    compare_outputs(out, oa, ov, oi)
+    compare_counters(dp, pms, o)
+    assert len(np.unique(ov)) >= 2
+    dp.close()
