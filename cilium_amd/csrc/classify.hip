@@ -60,6 +60,9 @@
 #include <vector>
 
 #include "kern_common.hpp"
+#ifndef CFC_EXP
+#define CFC_EXP 0   // timing experiments only (1: no LPM, 2: no policy, 3: no key stores)
+#endif
 
 namespace cfc {
 
@@ -150,24 +153,31 @@ struct Hdr {
 struct Raw {
     uint32_t sa, da, pt, mt, mk, tf;
 };
-__device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, uint64_t i,
-                                         uint64_t end, Raw &r)
+// in: the workgroup's slice (arrays advanced to its first header), i: the
+// header's index in it, nloc: the slice's length
+template <bool OPT>
+__device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, uint32_t i,
+                                         uint32_t nloc, Raw &r)
 {
     // no branches here: a load issued on only one side of a branch makes the
     // compiler's wait at the join conservative (vmcnt(0)), which would wait
     // for these HBM loads together with the probe before them.  Absent
     // optional arrays read saddr instead and the value is dropped.
-    i = i < end ? i : end - 1;
-    r.sa = ld_nt(in.saddr + i);
-    r.da = ld_nt(in.daddr + i);
-    r.pt = ld_nt(in.ports + i);
-    r.mt = ld_nt(in.meta + i);
-    const uint32_t mk = ld_nt((in.mark ? in.mark : in.saddr) + i);
-    const uint32_t tf = (in.tcp_flags ? in.tcp_flags : (const uint8_t *)in.saddr)[i];
-    r.mk = in.mark ? mk : 0u;
-    r.tf = in.tcp_flags ? tf : 0u;
+    i = i < nloc ? i : nloc - 1;
+    const uint32_t o = i << 2;
+    r.sa = ldo_nt(in.saddr, o);
+    r.da = ldo_nt(in.daddr, o);
+    r.pt = ldo_nt(in.ports, o);
+    r.mt = ldo_nt(in.meta, o);
+    r.mk = r.tf = 0;
+    if (OPT) {   // (the optional arrays: compiled out when the call has none)
+        const uint32_t mk = ldo_nt(in.mark ? in.mark : in.saddr, o);
+        const uint32_t tf = *((in.tcp_flags ? in.tcp_flags : (const uint8_t *)in.saddr) + i);
+        r.mk = in.mark ? mk : 0u;
+        r.tf = in.tcp_flags ? tf : 0u;
+    }
 }
-__device__ __forceinline__ void r1_take(const Raw &r, uint64_t i, uint64_t end,
+__device__ __forceinline__ void r1_take(const Raw &r, uint32_t i, uint32_t end,
                                         Hdr &h)
 {
     h.valid = i < end;
@@ -196,7 +206,11 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.pf_maybe = false;
     if (LPM) {
         if (T.l4d)
+#if CFC_EXP == 1
+            h.l4d = make_uint4(h.lh & 0xFFFF, 0, 0, 0);
+#else
             h.l4d = ldt16(T.l4d, (h.lh >> 16) * 16u);
+#endif
         else if (T.tbl24)
             h.e24 = T.tbl24[h.lh >> 8];
     }
@@ -281,40 +295,37 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     const uint32_t proto = h.mt & 0xFF;
     const bool known = ct_new_dport(proto, h.pt, &h.dport);
     if (!EGR) {
-        // handle_identity_from_host (bpf_netdev.c:128-153)
+        // handle_identity_from_host (bpf_netdev.c:128-153), branch-free
         const uint32_t magic = h.mk & 0xF00u;
-        if (magic == 0xA00u || magic == 0xB00u) {
-            h.ident = ((h.mk & 0xFF) << 16) | (h.mk >> 16);
-            h.skip_proxy = magic == 0xA00u;
-        } else {
-            h.ident = magic == 0xC00u ? HOST_ID : WORLD_ID;
-        }
+        const bool viap = (magic == 0xA00u) | (magic == 0xB00u);
+        const uint32_t id = viap ? (((h.mk & 0xFF) << 16) | (h.mk >> 16))
+                                 : (magic == 0xC00u ? HOST_ID : WORLD_ID);
+        h.skip_proxy = magic == 0xA00u;
         // handle_ipv4 (:375-398): reserved identities take the ipcache's
-        if (h.ident < HEALTH_ID && h.e24 && h.e24 != CLUSTER_ID && h.e24 != HOST_ID)
-            h.ident = h.e24;
-        if (local && !(h.rec.w & LXC_HOST)) {
-            if (!(h.rec.w & LXC_HAS_POLICY)) {
-                h.act = TC_ACT_SHOT;
-                h.ver = DROP_MISSED_TAIL_CALL;
-                h.met0 = mkey<MODE>(DROP_MISSED_TAIL_CALL, METRIC_INGRESS);
-            } else if (!known) {
-                h.act = TC_ACT_SHOT;
-                h.ver = DROP_CT_UNKNOWN_PROTO;
-                h.met0 = mkey<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
-            } else {
-                h.need_pol = true;
-                h.pbase = h.rec.y;
-                h.pmask = h.rec.z;
-                if (CT) {   // ipv4_policy's ct_lookup4 (bpf_lxc.c:932)
-                    const CtResult c = ct_stage4(
-                        T, h.sa, h.da, proto, h.pt, CT_INGRESS,
-                        ct_owner_word(h.rec.w & 0xFFFF, (h.rec.w & LXC_CT_LOCAL) != 0));
-                    h.dport = c.dport;
-                    h.ct_res = c.res;
-                    h.ct_slot = c.slot;
-                    h.ct_byte = (uint32_t)c.res | CTO_DONE;
-                }
-            }
+        const bool ovr = (id < HEALTH_ID) & (h.e24 != 0u) & (h.e24 != CLUSTER_ID) &
+                         (h.e24 != HOST_ID);
+        h.ident = ovr ? h.e24 : id;
+        // the destination endpoint's program: missed tail call, unknown
+        // protocol, or its policy
+        const bool ep = local & !(h.rec.w & LXC_HOST);
+        const bool noprog = ep & !(h.rec.w & LXC_HAS_POLICY);
+        const bool unk = ep & !noprog & !known;
+        h.need_pol = ep & !noprog & known;
+        h.act = (noprog | unk) ? TC_ACT_SHOT : TC_ACT_OK;
+        h.ver = noprog ? DROP_MISSED_TAIL_CALL : unk ? DROP_CT_UNKNOWN_PROTO : 0;
+        h.met0 = noprog ? mkey<MODE>(DROP_MISSED_TAIL_CALL, METRIC_INGRESS)
+                 : unk  ? mkey<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS)
+                        : NONE;
+        h.pbase = h.rec.y;
+        h.pmask = h.rec.z;
+        if (CT && h.need_pol) {   // ipv4_policy's ct_lookup4 (bpf_lxc.c:932)
+            const CtResult c = ct_stage4(
+                T, h.sa, h.da, proto, h.pt, CT_INGRESS,
+                ct_owner_word(h.rec.w & 0xFFFF, (h.rec.w & LXC_CT_LOCAL) != 0));
+            h.dport = c.dport;
+            h.ct_res = c.res;
+            h.ct_slot = c.slot;
+            h.ct_byte = (uint32_t)c.res | CTO_DONE;
         }
     } else {
         h.act = TC_ACT_SHOT;
@@ -348,6 +359,10 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
         // ingress fragments look up the L3 key only (policy.h:61,85); the
         // egress path passes is_fragment = false (policy.h:153-154)
         const bool frag = !EGR && (h.mt & CFC_HF_FRAG);
+#if CFC_EXP == 2
+        h.P.maybe = 0; h.P.j = 3;
+        if (0)
+#endif
         policy_issue(T, S, h.pbase, h.pmask, h.ident, h.dport, proto,
                      h.egress_bit, frag, h.P);
     }
@@ -401,20 +416,24 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     h.idw = id_key(T, h.ident, drop1, len);
     h.id_ovf = h.idw == KEY_NONE;
     uint32_t ev2 = 0;
-    if (drop1) {
+    if (!EGR) {
+        // (branch-free) drop, or redirect_to_proxy for NEW / ESTABLISHED
+        // flows (TRACE_TO_PROXY, lxc.h:117), or TRACE_TO_LXC + delivery
+        // (bpf_lxc.c:1006)
+        const int v2 = h.skip_proxy ? 0 : v;
+        const bool prox = !drop1 & (v2 > 0) & !reply;
+        act = drop1 ? TC_ACT_SHOT : (prox | ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+        ver = drop1 ? DROP_POLICY : prox ? v2 : 0;
+        met0 = drop1 ? mkey<MODE>(DROP_POLICY, mdir)
+               : prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
+        if (NT)
+            evw = drop1 ? 0u
+                        : trace_word(prox ? OBS_TO_PROXY : OBS_TO_LXC, h.rec.w & 0xFFFF,
+                                     res1, mon1);
+    } else if (drop1) {
         act = TC_ACT_SHOT;
         ver = DROP_POLICY;
         met0 = mkey<MODE>(DROP_POLICY, mdir);
-    } else if (!EGR) {
-        if (h.skip_proxy)
-            v = 0;
-        // redirect_to_proxy for NEW / ESTABLISHED flows (TRACE_TO_PROXY,
-        // lxc.h:117), or TRACE_TO_LXC + delivery (bpf_lxc.c:1006)
-        const bool prox = v > 0 && !reply;
-        act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
-        ver = prox ? v : 0;
-        met0 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
-        evw = trace_word(prox ? OBS_TO_PROXY : OBS_TO_LXC, h.rec.w & 0xFFFF, res1, mon1);
     } else if (v > 0) {        // egress proxy (bpf_lxc.c:582-604)
         act = TC_ACT_REDIRECT;
         ver = v;
@@ -523,7 +542,9 @@ __device__ __forceinline__ void acc_publish(const unsigned long long *s_met,
     }
 }
 
-template <int MODE, int U, bool CT, bool NT>
+// OPT: the call passes some optional array (mark, tcp_flags, action, ct);
+// without, their pointers and branches are compiled out (fewer live SGPRs)
+template <int MODE, int U, bool CT, bool NT, bool OPT>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
     CountArgs C, uint64_t per_block)
@@ -554,23 +575,54 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     const uint32_t id_dir = EGR ? ID_DIR_EGRESS : ID_DIR_INGRESS;
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
-    const uint64_t end = min(in.n, start + per_block);
+    if (start >= in.n)
+        return;   // (uniform: no header for this workgroup; nothing to publish)
+    // the workgroup's slice: every array advanced to its first header, so
+    // per-lane addresses are 32-bit offsets from wave-uniform bases
+    // (launch_classify_v4 keeps per_block < 2^30)
+    const uint32_t end = (uint32_t)min(in.n - start, per_block);
+    in.saddr += start;
+    in.daddr += start;
+    in.ports += start;
+    in.meta += start;
+    if (OPT) {
+        if (in.mark)
+            in.mark += start;
+        if (in.tcp_flags)
+            in.tcp_flags += start;
+        if (out.action)
+            out.action += start;
+        if (out.ct)
+            out.ct += start;
+    }
+    out.verdict += start;
+    out.identity += start;
+    if (out.notify)
+        out.notify += start;
+    if (C.ct)
+        C.ct += start;
+    if (C.ct2)
+        C.ct2 += start;
+    if (C.ctr)
+        C.ctr += start;
+    if (C.ctr2)
+        C.ctr2 += start;
+    if (C.id)
+        C.id += start;
     // the trip count is uniform across the workgroup (the metrics flush
     // needs whole waves)
     MetAcc<acc_n<MODE>()> acc;
     acc.clear();
     uint32_t iter = 0;
     Raw nx[U];
-    if (start >= end)
-        return;   // (uniform: no header for this workgroup; nothing to publish)
 #pragma unroll
     for (int u = 0; u < U; u++)
-        r1_issue(in, start + (uint64_t)u * BLOCK + threadIdx.x, end, nx[u]);
-    for (uint64_t base = start; base < end; base += (uint64_t)BLOCK * U) {
+        r1_issue<OPT>(in, u * BLOCK + threadIdx.x, end, nx[u]);
+    for (uint32_t base = 0; base < end; base += BLOCK * U) {
         Hdr h[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r1_take(nx[u], base + (uint64_t)u * BLOCK + threadIdx.x, end, h[u]);
+            r1_take(nx[u], base + u * BLOCK + threadIdx.x, end, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r2_issue<MODE>(T, S, h[u]);
@@ -579,42 +631,46 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             r3_identity<MODE, CT>(T, S, E, h[u]);
         // the next iteration's headers, behind this one's policy probe (the
         // last iteration re-reads the slice's last header)
-        const uint64_t nb = base + (uint64_t)BLOCK * U;
+        const uint32_t nb = base + BLOCK * U;
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r1_issue(in, nb + (uint64_t)u * BLOCK + threadIdx.x, end, nx[u]);
+            r1_issue<OPT>(in, nb + u * BLOCK + threadIdx.x, end, nx[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r4_verdict<MODE, CT, NT>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint64_t i = base + (uint64_t)u * BLOCK + threadIdx.x;
+            const uint32_t i = base + u * BLOCK + threadIdx.x;
             const uint32_t len = h[u].mt >> 16;
             {   // (lanes past the end rewrite the last header's values)
-                const uint64_t o = h[u].valid ? i : end - 1;
-                st_nt(h[u].ver, out.verdict + o);
-                st_nt(h[u].ident, out.identity + o);
-                if (out.action)
-                    out.action[o] = (uint8_t)h[u].act;
-                if (CT && out.ct)
-                    out.ct[o] = (uint8_t)h[u].ct_byte;
+                const uint32_t o = h[u].valid ? i : end - 1, o4 = o << 2;
+                sto_nt(h[u].ver, out.verdict, o4);
+                sto_nt(h[u].ident, out.identity, o4);
+                if (OPT && out.action)
+                    sto((uint8_t)h[u].act, out.action, o);
+                if (CT && OPT && out.ct)
+                    sto((uint8_t)h[u].ct_byte, out.ct, o);
                 if (NT)   // the monitor event word (cfc_out.notify)
-                    st_nt(h[u].ver < 0
+                    sto_nt((uint32_t)(h[u].ver < 0
                               ? notify_word(MODE, h[u].ver,
                                             EGR && h[u].met1 == mkey<MODE>(DROP_POLICY, METRIC_INGRESS),
                                             h[u].rec.w & 0xFFFF, E.lxc_id)
-                              : h[u].evw,
-                          out.notify + o);
+                              : h[u].evw),
+                          out.notify, o4);
                 if (CT) {
-                    st_nt(h[u].ct_k1, C.ct + o);
+                    sto_nt(h[u].ct_k1, C.ct, o4);
                     if (EGR)
-                        st_nt(h[u].ct_k2, C.ct2 + o);
+                        sto_nt(h[u].ct_k2, C.ct2, o4);
                 }
                 if (MODE != CFC_MODE_XDP) {
-                    st_nt(ctr_key(C, h[u].ctr0, len), C.ctr + o);
+#if CFC_EXP != 3
+                    sto_nt(ctr_key(C, h[u].ctr0, len), C.ctr, o4);
+#endif
                     if (EGR)
-                        st_nt(ctr_key(C, h[u].ctr1, len), C.ctr2 + o);
-                    st_nt(h[u].idw, C.id + o);
+                        sto_nt(ctr_key(C, h[u].ctr1, len), C.ctr2, o4);
+#if CFC_EXP != 3
+                    sto_nt(h[u].idw, C.id, o4);
+#endif
                 }
             }
             if (MODE != CFC_MODE_XDP && h[u].valid && h[u].id_ovf && h[u].need_pol)
@@ -823,7 +879,9 @@ void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out
                     uint64_t per_block, hipStream_t s)
 {
     const LdsPlan L = lds_plan(T);
-    auto kern = k_classify_v4<MODE, CFC_UNROLL, CT, NT>;
+    const bool opt = in.mark || in.tcp_flags || out.action || (CT && out.ct);
+    auto kern = opt ? k_classify_v4<MODE, CFC_UNROLL, CT, NT, true>
+                    : k_classify_v4<MODE, CFC_UNROLL, CT, NT, false>;
     set_lds_limit((const void *)kern, (int)LDS_PER_WG);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
                        out, E, C, per_block);
@@ -964,6 +1022,8 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
     const uint64_t nwg = (uint64_t)num_cus * CFC_WG_PER_CU;
     uint64_t per_block = (in.n + nwg - 1) / nwg;
     per_block = (per_block + step - 1) / step * step;
+    // slices stay below 2^30 headers (32-bit byte offsets in the kernel)
+    per_block = std::min<uint64_t>(per_block, (1ull << 30) / step * step);
     const uint32_t grid = (uint32_t)((in.n + per_block - 1) / per_block);
     if (tm)
         (void)hipEventRecord(tm->ev[0], s);

@@ -73,6 +73,24 @@ __device__ __forceinline__ void st_nt(T v, T *p)
 {
     __builtin_nontemporal_store(v, p);
 }
+// the same at a 32-bit byte offset from a wave-uniform base: the address is
+// then the SGPR base plus a VGPR offset (no 64-bit address arithmetic)
+template <class T>
+__device__ __forceinline__ T ldo_nt(const T *base, uint32_t off)
+{
+    return __builtin_nontemporal_load(
+        reinterpret_cast<const T *>(reinterpret_cast<const char *>(base) + off));
+}
+template <class T>
+__device__ __forceinline__ void sto_nt(T v, T *base, uint32_t off)
+{
+    __builtin_nontemporal_store(v, reinterpret_cast<T *>(reinterpret_cast<char *>(base) + off));
+}
+template <class T>
+__device__ __forceinline__ void sto(T v, T *base, uint32_t off)
+{
+    *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + off) = v;
+}
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // 16-byte non-temporal load (p 16-byte aligned)
@@ -214,15 +232,14 @@ __device__ __forceinline__ uint64_t pkey(uint32_t id, uint32_t dport,
 // loaded swapped and swapped back by ipv4_ct_tuple_reverse(); ICMP echo puts
 // its type (8) in tuple->sport, which becomes the dport; other ICMP -> 0;
 // any other protocol -> DROP_CT_UNKNOWN_PROTO.
+// (Branch-free: a divergent if here costs more scalar exec-mask work than
+// the arithmetic itself.)
 __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
                                              uint32_t *dport)
 {
-    if (proto == 6 || proto == 17) {
-        *dport = ports >> 16;
-        return true;
-    }
-    *dport = (ports & 0xFF) == 8 ? 8u : 0u;
-    return proto == 1;
+    const bool tu = (proto == 6) | (proto == 17);
+    *dport = tu ? ports >> 16 : ((ports & 0xFF) == 8 ? 8u : 0u);
+    return tu | (proto == 1);
 }
 
 // ---- conntrack: ct_lookup4 / ct_lookup6 (conntrack.h:467-590, :310-437)
