@@ -699,7 +699,7 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
             while (tab[s].key != POL_EMPTY)
                 s = (s + 1) & loc.mask;
             tab[s].key = key;
-            bloom_add(&img->pol_bloom, pol_bloom_hash(loc.base, pre));
+            bloom_add(&img->pol_bloom, pol_bloom_hash(pol_bloom_salt(loc.base), pre));
             tab[s].proxy_port = proxy;
             tab[s].ctr = (uint32_t)img->ctr_owner.size();
             img->ctr_owner.emplace_back(m, kv.first);

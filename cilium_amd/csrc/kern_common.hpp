@@ -513,12 +513,11 @@ __device__ __forceinline__ void policy_issue(const DevTables &T, const Lds &S,
     P.eg = egress << 24;
     P.maybe = frag ? 2u : 7u;                // policy.h:61,85
     if (S.polb) {
-        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(0))))
-            P.maybe &= ~1u;
-        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(1))))
-            P.maybe &= ~2u;
-        if (!bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(base, P.pre(2))))
-            P.maybe &= ~4u;
+        const uint32_t salt = pol_bloom_salt(base);
+        const bool m0 = bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(salt, P.pre(0)));
+        const bool m1 = bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(salt, P.pre(1)));
+        const bool m2 = bloom_maybe(S.polb_off, S.polb_mask, pol_bloom_hash(salt, P.pre(2)));
+        P.maybe &= (uint32_t)m0 | (uint32_t)m1 << 1 | (uint32_t)m2 << 2;
     }
     policy_probe_key(T, base, mask, P);
 }
