@@ -864,6 +864,271 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
     }
 }
 
+// ---- CT accounting by key range ---------------------------------------------
+// The per-slice LDS table above leaves one global atomic pair per distinct
+// (flow, slice) — on Zipf traffic over millions of flows most of the
+// packets of the tail, ~25M atomics per 64M-header batch.  Partitioned
+// instead, every distinct key of the batch costs one plain read-modify-
+// write of its counters:
+//   A k_ctp_agg      per slice: the LDS table (hot flows collapse), its
+//                    entries and overflow packets staged as records
+//                    {key, packets << 32 | bytes}, counted per key bucket
+//                    (CTP_BUCKET consecutive keys)
+//   B k_scan_*       exclusive scan of the (bucket, slice) counts
+//   C k_ctp_scatter  records into bucket order
+//   D k_ctp_reduce   one workgroup per bucket: LDS sums per key, then its
+//                    counters, which no other workgroup touches
+constexpr uint32_t CTP_BUCKET_BITS = 13, CTP_BUCKET = 1u << CTP_BUCKET_BITS;
+// slot of this lane in an LDS-counted list, one atomic per wave (the lanes
+// of a wave appending together would otherwise serialise on the counter);
+// every lane of the wave must call it
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool want)
+{
+    const uint64_t m = __ballot(want);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+    uint32_t base = 0;
+    if (m && lane == lead)
+        base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)lead, 64);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+}
+constexpr uint32_t CTP_MAX_BUCKETS = 8192;     // keys < 2^26 (32M CT slots)
+constexpr uint32_t CTP_AGG_LDS = CT_LDS_SLOTS * 12 + CTP_MAX_BUCKETS * 4 + 16;
+// probes before a key becomes a record of its own: the hot flows take their
+// slots early; later keys are mostly the Zipf tail, for which a full table's
+// long probe sequences cost more than the record
+constexpr int CTP_PROBES = 3;
+
+__global__ __launch_bounds__(BLOCK) void k_ctp_agg(const uint32_t *ct_idx,
+                                                   const uint32_t *ct_idx2,
+                                                   const uint32_t *meta, uint64_t n,
+                                                   uint32_t nbuck, uint32_t *rkey,
+                                                   uint64_t *rval, uint32_t *rcnt,
+                                                   uint32_t *cnt)
+{
+    uint32_t *keys = reinterpret_cast<uint32_t *>(cfc_smem);
+    unsigned long long *vals = reinterpret_cast<unsigned long long *>(keys + CT_LDS_SLOTS);
+    uint32_t *bcnt = reinterpret_cast<uint32_t *>(vals + CT_LDS_SLOTS);
+    uint32_t *nrec = bcnt + CTP_MAX_BUCKETS;
+    for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {
+        keys[j] = NONE;
+        vals[j] = 0;
+    }
+    for (uint32_t j = threadIdx.x; j < nbuck; j += BLOCK)
+        bcnt[j] = 0;
+    if (threadIdx.x == 0)
+        *nrec = 0;
+    __syncthreads();
+    const uint32_t nv = gridDim.x * gridDim.y;
+    const uint32_t vw = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t *idx = blockIdx.y ? ct_idx2 : ct_idx;
+    uint32_t *rk = rkey + (uint64_t)vw * COUNT_PER_BLOCK;
+    uint64_t *rv = rval + (uint64_t)vw * COUNT_PER_BLOCK;
+    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
+    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    for (uint64_t i0 = start; i0 < end; i0 += BLOCK) {   // (uniform trip count)
+        const uint64_t i = i0 + threadIdx.x;
+        const uint32_t k = i < end ? ld_nt(idx + i) : NONE;
+        const uint32_t len = i < end ? ld_nt(meta + i) >> 16 : 0u;
+        const uint32_t npk = 1;
+        uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
+        bool done = k == NONE;
+        for (int p = 0; p < CTP_PROBES && !done; p++) {
+            uint32_t cur = keys[h];
+            if (cur == NONE) {
+                cur = atomicCAS(&keys[h], NONE, k);
+                if (cur == NONE)
+                    cur = k;
+            }
+            if (cur == k) {
+                // <= 64512 packets of <= 65535 bytes: {packets << 32 | bytes}
+                atomicAdd(&vals[h], ((unsigned long long)npk << 32) | len);
+                done = true;
+            }
+            h = (h + 1) & (CT_LDS_SLOTS - 1);
+        }
+        const uint32_t r = wave_append(nrec, !done);   // a record of its own
+        if (!done) {
+            rk[r] = k;
+            rv[r] = ((uint64_t)npk << 32) | len;
+            atomicAdd(&bcnt[k >> CTP_BUCKET_BITS], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {   // (uniform)
+        const uint32_t k = keys[j];
+        const uint32_t r = wave_append(nrec, k != NONE);
+        if (k == NONE)
+            continue;
+        rk[r] = k;
+        rv[r] = vals[j];
+        atomicAdd(&bcnt[k >> CTP_BUCKET_BITS], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbuck; b += BLOCK)
+        cnt[(uint64_t)b * nv + vw] = bcnt[b];
+    if (threadIdx.x == 0)
+        rcnt[vw] = *nrec;
+}
+
+// exclusive scan of n u32 (n < 2^32 total): per 4096-element block, block
+// sums, then the sums' offsets added back; out[n] = the total
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *tmp)
+{
+    // inclusive scan of one value per thread over the 1024-thread block
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d)
+            x += y;
+    }
+    if (lane == 63)
+        tmp[wv] = x;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        uint32_t t = tmp[threadIdx.x];
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const uint32_t y = __shfl_up(t, d, 16);
+            if (threadIdx.x >= (uint32_t)d)
+                t += y;
+        }
+        tmp[16 + threadIdx.x] = t;
+    }
+    __syncthreads();
+    const uint32_t before = wv ? tmp[16 + wv - 1] : 0u;
+    const uint32_t r = before + x - v;
+    __syncthreads();
+    return r;
+}
+__global__ __launch_bounds__(BLOCK) void k_scan_local(const uint32_t *in, uint32_t *out,
+                                                      uint64_t n, uint32_t *bsum)
+{
+    __shared__ uint32_t tmp[32];
+    const uint64_t b0 = (uint64_t)blockIdx.x * 4 * BLOCK + 4ull * threadIdx.x;
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        v[j] = b0 + j < n ? in[b0 + j] : 0u;
+        s += v[j];
+    }
+    uint32_t e = block_excl_scan(s, tmp);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (b0 + j < n)
+            out[b0 + j] = e;
+        e += v[j];
+    }
+    if (threadIdx.x == BLOCK - 1)
+        bsum[blockIdx.x] = e;
+}
+__global__ __launch_bounds__(BLOCK) void k_scan_top(uint32_t *bsum, uint32_t nb,
+                                                    uint32_t *total)
+{
+    __shared__ uint32_t tmp[32];
+    uint32_t carry = 0;
+    for (uint32_t c = 0; c < nb; c += BLOCK) {   // (uniform trip count)
+        const uint32_t i = c + threadIdx.x;
+        const uint32_t v = i < nb ? bsum[i] : 0u;
+        const uint32_t e = block_excl_scan(v, tmp);
+        if (i < nb)
+            bsum[i] = carry + e;
+        carry += tmp[31];   // (block_excl_scan left the block total there)
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        *total = carry;
+}
+__global__ __launch_bounds__(BLOCK) void k_scan_add(uint32_t *out, uint64_t n,
+                                                    const uint32_t *bsum)
+{
+    const uint64_t b0 = (uint64_t)blockIdx.x * 4 * BLOCK + 4ull * threadIdx.x;
+    const uint32_t add = bsum[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        if (b0 + j < n)
+            out[b0 + j] += add;
+}
+
+// the scanned offsets transposed to slice-major (one contiguous row per
+// slice for k_ctp_scatter): in[b * nv + v] -> out[v * nb + b]
+__global__ __launch_bounds__(256) void k_transpose_u32(const uint32_t *in, uint32_t *out,
+                                                       uint32_t nb, uint32_t nv)
+{
+    __shared__ uint32_t t[32][33];
+    const uint32_t bx = blockIdx.x * 32, vy = blockIdx.y * 32;
+    const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+    for (uint32_t r = ty; r < 32; r += 8) {
+        const uint32_t b = bx + r, v = vy + tx;
+        t[r][tx] = (b < nb && v < nv) ? in[(uint64_t)b * nv + v] : 0u;
+    }
+    __syncthreads();
+    for (uint32_t r = ty; r < 32; r += 8) {
+        const uint32_t v = vy + r, b = bx + tx;
+        if (b < nb && v < nv)
+            out[(uint64_t)v * nb + b] = t[tx][r];
+    }
+}
+
+// C: the staged records of slice vw into bucket order: {key within the
+// bucket << 48 | packets << 32 | bytes}; offt: the slice's row of offsets
+__global__ __launch_bounds__(BLOCK) void k_ctp_scatter(const uint32_t *rkey,
+                                                       const uint64_t *rval,
+                                                       const uint32_t *rcnt,
+                                                       const uint32_t *offt, uint32_t nbuck,
+                                                       uint64_t *outr)
+{
+    uint32_t *cur = reinterpret_cast<uint32_t *>(cfc_smem);
+    const uint32_t vw = blockIdx.x;
+    for (uint32_t j = threadIdx.x; j < nbuck; j += BLOCK)
+        cur[j] = offt[(uint64_t)vw * nbuck + j];
+    __syncthreads();
+    const uint32_t m = rcnt[vw];
+    const uint32_t *rk = rkey + (uint64_t)vw * COUNT_PER_BLOCK;
+    const uint64_t *rv = rval + (uint64_t)vw * COUNT_PER_BLOCK;
+    for (uint32_t r = threadIdx.x; r < m; r += BLOCK) {
+        const uint32_t k = rk[r];
+        const uint32_t pos = atomicAdd(&cur[k >> CTP_BUCKET_BITS], 1u);
+        outr[pos] = (uint64_t)(k & (CTP_BUCKET - 1)) << 48 | rv[r];
+    }
+}
+
+// D: bucket b's sums per key, added to its counters (acct[2k], acct[2k+1])
+__global__ __launch_bounds__(BLOCK) void k_ctp_reduce(const uint64_t *recs,
+                                                      const uint32_t *off, uint32_t nv,
+                                                      uint32_t nbuck, const uint32_t *total,
+                                                      uint64_t *acct)
+{
+    uint32_t *pk = reinterpret_cast<uint32_t *>(cfc_smem);
+    unsigned long long *by = reinterpret_cast<unsigned long long *>(pk + CTP_BUCKET);
+    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
+        pk[j] = 0;
+        by[j] = 0;
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x;
+    const uint32_t r0 = off[(uint64_t)b * nv];
+    const uint32_t r1 = b + 1 < nbuck ? off[(uint64_t)(b + 1) * nv] : *total;
+    for (uint32_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
+        const uint64_t v = ld_nt(recs + r);
+        const uint32_t lo = (uint32_t)(v >> 48);
+        atomicAdd(&pk[lo], (uint32_t)(v >> 32) & 0xFFFFu);
+        atomicAdd(&by[lo], v & 0xFFFFFFFFull);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
+        const uint32_t p = pk[j];
+        if (!p)
+            continue;
+        const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
+        acct[2 * k] += p;
+        acct[2 * k + 1] += by[j];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
                                                  const uint64_t *src,
                                                  uint64_t n)
@@ -956,6 +1221,15 @@ int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
 
+// key buckets of the CT accounting partition (0: too many keys, the
+// per-slice kernel k_ct_count counts instead)
+uint32_t ctp_buckets(const DevTables &T)
+{
+    const uint64_t slots = (T.ct4 ? T.ct4_mask + 1ull : 0) + (T.ct6 ? T.ct6_mask + 1ull : 0);
+    const uint64_t nb = (2 * slots + CTP_BUCKET - 1) / CTP_BUCKET;
+    return nb <= CTP_MAX_BUCKETS ? (uint32_t)nb : 0u;
+}
+
 WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
 {
     WsLayout w{};
@@ -984,7 +1258,30 @@ WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
     w.partial = off;
     const uint64_t slots = hist_slots(T, mode);
     w.nblk = hist_slices(n, slots);
-    w.total = off + 8ull * slots * w.nblk;
+    off += 8ull * slots * w.nblk;
+    const uint32_t nbuck = ctp_buckets(T);
+    if (ct && T.ct_acct && nbuck) {
+        const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        w.ctp_nv = nblk * (egr ? 2u : 1u);
+        w.ctp_nbuck = nbuck;
+        const uint64_t cap = (uint64_t)w.ctp_nv * COUNT_PER_BLOCK;
+        const uint64_t nc = (uint64_t)nbuck * w.ctp_nv;
+        auto take = [&](size_t bytes) {
+            off = (off + 255) & ~(size_t)255;
+            const size_t at = off;
+            off += bytes;
+            return at;
+        };
+        w.ctp_rkey = take(4 * cap);
+        w.ctp_rval = take(8 * cap);
+        w.ctp_rcnt = take(4ull * w.ctp_nv);
+        w.ctp_cnt = take(4 * nc);
+        w.ctp_off = take(4 * nc + 4);
+        w.ctp_offt = take(4 * nc);
+        w.ctp_bsum = take(4 * ((nc + 4 * BLOCK - 1) / (4 * BLOCK)) + 4);
+        w.ctp_out = take(8 * cap);
+    }
+    w.total = off;
     return w;
 }
 
@@ -1060,7 +1357,36 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
         return;
     const WsLayout w = ws_layout(n, T, mode, ct);
     const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
-    if (ct && T.ct_acct) {
+    if (ct && T.ct_acct && w.ctp_nv) {
+        char *b = reinterpret_cast<char *>(ws);
+        uint32_t *rkey = reinterpret_cast<uint32_t *>(b + w.ctp_rkey);
+        uint64_t *rval = reinterpret_cast<uint64_t *>(b + w.ctp_rval);
+        uint32_t *rcnt = reinterpret_cast<uint32_t *>(b + w.ctp_rcnt);
+        uint32_t *cnt = reinterpret_cast<uint32_t *>(b + w.ctp_cnt);
+        uint32_t *off = reinterpret_cast<uint32_t *>(b + w.ctp_off);
+        uint32_t *bsum = reinterpret_cast<uint32_t *>(b + w.ctp_bsum);
+        uint32_t *offt = reinterpret_cast<uint32_t *>(b + w.ctp_offt);
+        uint64_t *outr = reinterpret_cast<uint64_t *>(b + w.ctp_out);
+        const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        const uint64_t nc = (uint64_t)w.ctp_nbuck * w.ctp_nv;
+        const uint32_t nsb = (uint32_t)((nc + 4 * BLOCK - 1) / (4 * BLOCK));
+        set_lds_limit((const void *)k_ctp_agg, (int)CTP_AGG_LDS);
+        hipLaunchKernelGGL(k_ctp_agg, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
+                           dim3(BLOCK), CTP_AGG_LDS, s, C.ct, C.ct2, meta, n,
+                           w.ctp_nbuck, rkey, rval, rcnt, cnt);
+        hipLaunchKernelGGL(k_scan_local, dim3(nsb), dim3(BLOCK), 0, s, cnt, off, nc, bsum);
+        hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(BLOCK), 0, s, bsum, nsb, off + nc);
+        hipLaunchKernelGGL(k_scan_add, dim3(nsb), dim3(BLOCK), 0, s, off, nc, bsum);
+        hipLaunchKernelGGL(k_transpose_u32,
+                           dim3((w.ctp_nbuck + 31) / 32, (w.ctp_nv + 31) / 32), dim3(256), 0,
+                           s, off, offt, w.ctp_nbuck, w.ctp_nv);
+        set_lds_limit((const void *)k_ctp_scatter, (int)(4 * CTP_MAX_BUCKETS));
+        hipLaunchKernelGGL(k_ctp_scatter, dim3(w.ctp_nv), dim3(BLOCK), 4 * w.ctp_nbuck, s,
+                           rkey, rval, rcnt, offt, w.ctp_nbuck, outr);
+        set_lds_limit((const void *)k_ctp_reduce, (int)(12 * CTP_BUCKET));
+        hipLaunchKernelGGL(k_ctp_reduce, dim3(w.ctp_nbuck), dim3(BLOCK), 12 * CTP_BUCKET, s,
+                           outr, off, w.ctp_nv, w.ctp_nbuck, off + nc, T.ct_acct);
+    } else if (ct && T.ct_acct) {
         set_lds_limit((const void *)k_ct_count, (int)CT_LDS_BYTES);
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
         hipLaunchKernelGGL(k_ct_count, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
