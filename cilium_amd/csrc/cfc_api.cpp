@@ -66,23 +66,60 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
     return b.upload(v.data(), v.size() * sizeof(T), s);
 }
 
-struct Epoch {
-    uint64_t id = 0;
-    DevBuf tbl24, tbl8, ovf, l4d, l4c, l4l, pf24, pf8, pffix, lxc4, pol, pfbloom,
-        polbloom, lxc6;
-    DevBuf l6[3][3];   // ipc6 / pf6_fix / pf6_dyn: slots, bloom, lens
-    DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
-    std::vector<uint32_t> seclabel;   // SECLABEL by LXC_ID at commit
-    std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
-    std::vector<Ct6Slot> ct6_host;
-    std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
-    DevTables T{};
+// An epoch is four table groups (flatten.hpp GROUP_*), each an immutable
+// set of device buffers shared by every epoch built while its maps did not
+// change: a commit re-flattens and uploads only the groups whose maps did.
+struct GIpc {          // ipcache
+    DevBuf tbl24, tbl8, ovf, l4d, l4c, l4l, l6[3];
+    Lpm6 ipc6{};
+    int layout = 0;
+    uint32_t n_prefix4 = 0, tbl8_groups = 0, lpm4_kib = 0, lpm6_kib = 0,
+             n_prefix6 = 0, lpm6_lengths = 0, lpm6_groups = 0;
+    uint32_t id_cover = 1;   // identity histogram ranges (reserved + ipcache)
+    uint64_t bytes = 0;
+};
+struct GPf {           // prefilter
+    DevBuf pf24, pf8, pffix, pfbloom, l6fix[3], l6dyn[3];
+    Lpm6 fix{}, dyn{};
+    uint32_t fix_mask = 0, fix_zero = 0, bloom_words = 0;
+    uint32_t n_fix4 = 0, n_dyn4 = 0, n_fix6 = 0, n_dyn6 = 0;
+    uint64_t bytes = 0;
+};
+struct GEp {           // endpoints + policy (+ the counter layout)
+    DevBuf lxc4, lxc6, pol, polbloom;
+    uint32_t lxc4_mask = 0, lxc6_mask = 0, pol_bloom_words = 0, n_eps = 0, n_eps6 = 0;
+    bool lxc4_lds = false, lxc6_lds = false;
     std::unordered_map<int, PolLoc> pol_loc;
     std::vector<std::pair<Map *, std::string>> ctr_owner;
-    cfc_stats st{};
+    std::vector<uint32_t> seclabel;   // SECLABEL by LXC_ID at commit
     // drop notifications: {SECLABEL, ifindex} by LXC_ID, from the same
     // snapshot of the maps as the tables
     DevBuf ep_info;
+    uint64_t bytes = 0;
+};
+struct GCt {           // conntrack
+    DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
+    std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
+    std::vector<Ct6Slot> ct6_host;
+    std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
+    uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
+    uint32_t n_ct4 = 0, n_ct6 = 0;
+    uint64_t bytes = 0;
+};
+struct Epoch {
+    uint64_t id = 0;
+    std::shared_ptr<GIpc> ipc;
+    std::shared_ptr<GPf> pf;
+    std::shared_ptr<GEp> ep;
+    std::shared_ptr<GCt> ct;
+    DevTables T{};
+    cfc_stats st{};
+};
+// an epoch replaced while launches on other streams may still read it: kept
+// until the events recorded on those streams at the swap have passed
+struct Retired {
+    std::shared_ptr<Epoch> e;
+    std::vector<hipEvent_t> ev;
 };
 
 }  // namespace
@@ -102,9 +139,11 @@ struct cfc_ctx {
                          {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 1, 0, 0}, 1u};
     uint32_t now = 0;   // bpf_ktime_get_sec() (cfc_set_clock)
 
-    std::unique_ptr<Epoch> epoch;
+    std::shared_ptr<Epoch> epoch;
     uint64_t epoch_seq = 0;
-    uint64_t built_sig = ~0ull;   // signature of the maps the epoch was built from
+    uint64_t built_sig[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // per group
+    std::vector<Retired> retired;
+    std::vector<hipStream_t> streams;   // streams launched on since the last swap
 
     // counters: [n_ctr][2] u64 then metrics
     uint64_t *ctr = nullptr;
@@ -132,18 +171,38 @@ struct cfc_ctx {
 
 namespace {
 
-uint64_t tables_sig(cfc_ctx *c)
+// signature of the maps behind each table group (GROUP_* bit order)
+int group_of(Role r)
 {
-    uint64_t s = 1469598103934665603ull ^ c->seclabel_gen;
-    s = (s ^ (uint64_t)c->opts.lpm4) * 1099511628211ull;
-    for (auto &kv : c->maps) {
-        if (kv.second->role == ROLE_NONE || kv.second->role == ROLE_METRICS)
-            continue;
-        s = (s ^ (uint64_t)(uintptr_t)kv.second.get()) * 1099511628211ull;
-        s = (s ^ kv.second->gen) * 1099511628211ull;
-        s = (s ^ kv.second->kv.size()) * 1099511628211ull;
+    switch (r) {
+    case ROLE_IPCACHE: return 0;
+    case ROLE_PF4_FIX: case ROLE_PF4_DYN: case ROLE_PF6_FIX: case ROLE_PF6_DYN: return 1;
+    case ROLE_LXC: case ROLE_POLICY: return 2;
+    case ROLE_CT4: case ROLE_CT6: return 3;
+    default: return -1;
     }
-    return s;
+}
+void group_sigs(cfc_ctx *c, uint64_t sig[4])
+{
+    for (int g = 0; g < 4; g++)
+        sig[g] = 1469598103934665603ull + (uint64_t)g;
+    sig[0] = (sig[0] ^ (uint64_t)c->opts.lpm4) * 1099511628211ull;
+    sig[2] = (sig[2] ^ c->seclabel_gen) * 1099511628211ull;
+    for (auto &kv : c->maps) {
+        const Map *m = kv.second.get();
+        const int g = group_of(m->role);
+        if (g < 0)
+            continue;
+        for (int x : {g, g == 3 ? 2 : -1}) {   // endpoints see which CT maps exist
+            if (x < 0)
+                continue;
+            sig[x] = (sig[x] ^ (uint64_t)(uintptr_t)m) * 1099511628211ull;
+            if (x == g) {
+                sig[x] = (sig[x] ^ m->gen) * 1099511628211ull;
+                sig[x] = (sig[x] ^ m->kv.size()) * 1099511628211ull;
+            }
+        }
+    }
 }
 
 // CT map and key bytes of a device slot (the slot holds the whole tuple)
@@ -158,8 +217,8 @@ Map *ct_slot_key(const Epoch &E, int family, const uint32_t *d, const uint32_t *
     k[2 * al + 4] = (char)(w & 0xFF);
     k[2 * al + 5] = (char)((w >> 8) & 7);
     key->assign(k, 2 * al + 6);
-    auto it = E.ct_maps.find(ct_map_key(family, w & ~0x7FFu, (w & 0xFF) != 6));
-    return it == E.ct_maps.end() ? nullptr : it->second;
+    auto it = E.ct->ct_maps.find(ct_map_key(family, w & ~0x7FFu, (w & 0xFF) != 6));
+    return it == E.ct->ct_maps.end() ? nullptr : it->second;
 }
 
 // CONNTRACK_ACCOUNTING counts of the device into the CT entries' rx/tx
@@ -167,12 +226,12 @@ Map *ct_slot_key(const Epoch &E, int family, const uint32_t *d, const uint32_t *
 int fold_ct(cfc_ctx *c, hipStream_t s)
 {
     Epoch &E = *c->epoch;
-    const size_t n4 = E.ct4_host.size(), n = n4 + E.ct6_host.size();
+    const size_t n4 = E.ct->ct4_host.size(), n = n4 + E.ct->ct6_host.size();
     if (!n)
         return 0;
     std::vector<uint64_t> h(4 * n);
-    if (hipMemcpyAsync(h.data(), E.ct_acct.p, 32 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemsetAsync(E.ct_acct.p, 0, 32 * n, s) != hipSuccess ||
+    if (hipMemcpyAsync(h.data(), E.ct->ct_acct.p, 32 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemsetAsync(E.ct->ct_acct.p, 0, 32 * n, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     std::string key;
@@ -182,10 +241,10 @@ int fold_ct(cfc_ctx *c, hipStream_t s)
             continue;
         Map *m;
         if (i < n4) {
-            const Ct4Slot &e = E.ct4_host[i];
+            const Ct4Slot &e = E.ct->ct4_host[i];
             m = ct_slot_key(E, 4, &e.x, &e.y, e.z, e.w, &key);
         } else {
-            const Ct6Slot &e = E.ct6_host[i - n4];
+            const Ct6Slot &e = E.ct->ct6_host[i - n4];
             m = ct_slot_key(E, 6, e.d, e.s, e.z, e.w, &key);
         }
         if (!m)
@@ -219,13 +278,13 @@ int fold_counters(cfc_ctx *c, hipStream_t s)
     if (hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     Epoch &E = *c->epoch;
-    size_t nctr = E.ctr_owner.size();
+    size_t nctr = E.ep->ctr_owner.size();
     for (size_t i = 0; i < nctr; i++) {
         uint64_t pk = h[2 * i], by = h[2 * i + 1];
         if (!pk && !by)
             continue;
-        Map *m = E.ctr_owner[i].first;
-        auto it = m->kv.find(E.ctr_owner[i].second);
+        Map *m = E.ep->ctr_owner[i].first;
+        auto it = m->kv.find(E.ep->ctr_owner[i].second);
         if (it == m->kv.end())
             continue;   // entry deleted since: the kernel's update is lost too
         uint64_t v[2];
@@ -281,159 +340,308 @@ int upload_lpm6(DevBuf *b, const Lpm6Host &h, Lpm6 *d, hipStream_t s)
     return 0;
 }
 
-int commit_locked(cfc_ctx *c, hipStream_t s)
+// a launch on stream s reads the current epoch
+void note_stream(cfc_ctx *c, hipStream_t s)
 {
-    uint64_t sig = tables_sig(c);
-    if (c->epoch && sig == c->built_sig)
-        return 0;
-    int rc = fold_counters(c, s);
-    if (rc)
-        return rc;
-    std::vector<Map *> ms;
-    for (auto &kv : c->maps)
-        ms.push_back(kv.second.get());
-    HostImage img;
-    build_image(ms, c->opts, &img);
+    if (std::find(c->streams.begin(), c->streams.end(), s) == c->streams.end())
+        c->streams.push_back(s);
+}
 
-    auto E = std::make_unique<Epoch>();
-    E->id = ++c->epoch_seq;
-    if ((rc = upload_vec(E->tbl24, img.tbl24, s)) || (rc = upload_vec(E->tbl8, img.tbl8, s)) ||
-        (rc = upload_vec(E->ovf, img.lbl_ovf, s)) ||
-        (rc = upload_vec(E->l4d, img.l4d, s)) || (rc = upload_vec(E->l4c, img.l4c, s)) || (rc = upload_vec(E->l4l, img.l4l, s)) ||
-        (rc = upload_vec(E->pf24, img.pf_tbl24, s)) ||
-        (rc = upload_vec(E->pf8, img.pf_tbl8, s)) || (rc = upload_vec(E->pffix, img.pf_fix, s)) ||
-        (rc = upload_vec(E->lxc4, img.lxc4, s)) || (rc = upload_vec(E->pol, img.pol, s)) ||
-        (rc = upload_vec(E->pfbloom, img.pf_bloom, s)) ||
-        (rc = upload_vec(E->polbloom, img.pol_bloom, s)) ||
-        (rc = upload_vec(E->lxc6, img.lxc6, s)) ||
-        (rc = upload_lpm6(E->l6[0], img.ipc6, &E->T.ipc6, s)) ||
-        (rc = upload_lpm6(E->l6[1], img.pf6_fix, &E->T.pf6_fix, s)) ||
-        (rc = upload_lpm6(E->l6[2], img.pf6_dyn, &E->T.pf6_dyn, s)) ||
-        (rc = upload_vec(E->ct4, img.ct4, s)) || (rc = upload_vec(E->ct6, img.ct6, s)) ||
-        (rc = upload_vec(E->ct4_tm, img.ct4_tm, s)) ||
-        (rc = upload_vec(E->ct6_tm, img.ct6_tm, s)))
-        return rc;
-    {
-        const size_t nslots = img.ct4.size() + img.ct6.size();
-        if (nslots && (rc = E->ct_acct.zeros(32 * nslots, s)))
-            return rc;
+// free the retired epochs whose readers have all passed
+void reap_retired(cfc_ctx *c)
+{
+    auto done = [](const Retired &r) {
+        for (hipEvent_t e : r.ev)
+            if (hipEventQuery(e) != hipSuccess)
+                return false;
+        return true;
+    };
+    for (size_t i = 0; i < c->retired.size();) {
+        if (done(c->retired[i])) {
+            for (hipEvent_t e : c->retired[i].ev)
+                (void)hipEventDestroy(e);
+            c->retired.erase(c->retired.begin() + (long)i);
+        } else {
+            i++;
+        }
     }
+}
+
+std::shared_ptr<GIpc> build_ipc(const HostImage &img, const std::vector<Map *> &ms,
+                                hipStream_t s, int *rc)
+{
+    auto g = std::make_shared<GIpc>();
+    if ((*rc = upload_vec(g->tbl24, img.tbl24, s)) || (*rc = upload_vec(g->tbl8, img.tbl8, s)) ||
+        (*rc = upload_vec(g->ovf, img.lbl_ovf, s)) || (*rc = upload_vec(g->l4d, img.l4d, s)) ||
+        (*rc = upload_vec(g->l4c, img.l4c, s)) || (*rc = upload_vec(g->l4l, img.l4l, s)) ||
+        (*rc = upload_lpm6(g->l6, img.ipc6, &g->ipc6, s)))
+        return nullptr;
+    g->layout = img.lpm4_layout;
+    g->n_prefix4 = img.n_prefix4;
+    g->tbl8_groups = (uint32_t)(img.tbl8.size() / 256);
+    g->lpm4_kib = (uint32_t)((4ull * (img.l4d.size() + img.l4c.size() + img.tbl24.size() +
+                                      img.tbl8.size()) + 8ull * img.l4l.size() + 1023) / 1024);
+    g->n_prefix6 = img.ipc6.n;
+    g->lpm6_lengths = (uint32_t)img.ipc6.lens.size();
+    g->lpm6_groups = img.ipc6.groups;
+    g->lpm6_kib = (uint32_t)((img.ipc6.bytes() + 1023) / 1024);
+    g->bytes = 4ull * (img.tbl24.size() + img.tbl8.size() + img.lbl_ovf.size() +
+                       img.l4d.size() + img.l4c.size()) + 8ull * img.l4l.size() +
+               img.ipc6.bytes();
     // per-identity counters: the histogram ranges holding the reserved
     // identities and every ipcache identity; others count directly
-    E->T.id_cover = 1u;
+    g->id_cover = 1u;
     for (Map *m : ms)
         if (m->role == ROLE_IPCACHE)
             for (const auto &kv : m->kv) {
                 uint32_t lab;
                 memcpy(&lab, kv.second.val.data(), 4);
                 if (lab < ID_PACK_LIMIT)
-                    E->T.id_cover |= 1u << id_range_of(lab);
+                    g->id_cover |= 1u << id_range_of(lab);
             }
+    return g;
+}
+
+std::shared_ptr<GPf> build_pf(const HostImage &img, hipStream_t s, int *rc)
+{
+    auto g = std::make_shared<GPf>();
+    if ((*rc = upload_vec(g->pf24, img.pf_tbl24, s)) || (*rc = upload_vec(g->pf8, img.pf_tbl8, s)) ||
+        (*rc = upload_vec(g->pffix, img.pf_fix, s)) ||
+        (*rc = upload_vec(g->pfbloom, img.pf_bloom, s)) ||
+        (*rc = upload_lpm6(g->l6fix, img.pf6_fix, &g->fix, s)) ||
+        (*rc = upload_lpm6(g->l6dyn, img.pf6_dyn, &g->dyn, s)))
+        return nullptr;
+    g->fix_mask = img.pf_fix_mask;
+    g->fix_zero = img.pf_fix_zero;
+    g->bloom_words = (uint32_t)img.pf_bloom.size();
+    g->n_fix4 = img.n_pf_fix;
+    g->n_dyn4 = img.n_pf_dyn;
+    g->n_fix6 = img.pf6_fix.n;
+    g->n_dyn6 = img.pf6_dyn.n;
+    g->bytes = 4ull * (img.pf_tbl24.size() + img.pf_tbl8.size() + img.pf_fix.size() +
+                       img.pf_bloom.size()) + img.pf6_fix.bytes() + img.pf6_dyn.bytes();
+    return g;
+}
+
+std::shared_ptr<GEp> build_ep(cfc_ctx *c, HostImage &img, const std::vector<Map *> &ms,
+                              hipStream_t s, int *rc)
+{
+    auto g = std::make_shared<GEp>();
+    if ((*rc = upload_vec(g->lxc4, img.lxc4, s)) || (*rc = upload_vec(g->pol, img.pol, s)) ||
+        (*rc = upload_vec(g->polbloom, img.pol_bloom, s)) ||
+        (*rc = upload_vec(g->lxc6, img.lxc6, s)))
+        return nullptr;
+    g->lxc4_mask = img.lxc4_mask;
+    g->lxc6_mask = img.lxc6_mask;
+    g->lxc4_lds = img.lxc4.size() <= LXC_LDS_MAX_SLOTS;
+    g->lxc6_lds = img.lxc6.size() <= LXC6_LDS_MAX_SLOTS;
+    g->pol_bloom_words = (uint32_t)img.pol_bloom.size();
+    g->n_eps = img.n_eps;
+    g->n_eps6 = img.n_eps6;
+    g->pol_loc = std::move(img.pol_loc);
+    g->ctr_owner = std::move(img.ctr_owner);
+    g->bytes = sizeof(LxcSlot) * img.lxc4.size() + sizeof(PolSlot) * img.pol.size() +
+               4ull * img.pol_bloom.size() + sizeof(Lxc6Slot) * img.lxc6.size();
     // drop notifications: {SECLABEL, ifindex} by LXC_ID (struct
     // endpoint_info), and the SECLABELs the epoch's verdicts use
-    E->seclabel = c->seclabel;
-    {
-        std::vector<uint2> info(65536, make_uint2(0, 0));
-        for (uint32_t id = 0; id < 65536; id++)
-            info[id].x = c->seclabel[id];
-        for (Map *m : ms) {
-            if (m->role != ROLE_LXC)
-                continue;
-            for (auto &e : m->kv) {
-                uint32_t ifx;
-                uint16_t id;
-                memcpy(&ifx, e.second.val.data(), 4);
-                memcpy(&id, e.second.val.data() + 6, 2);
-                info[id].y = ifx;
-            }
+    g->seclabel = c->seclabel;
+    std::vector<uint2> info(65536, make_uint2(0, 0));
+    for (uint32_t id = 0; id < 65536; id++)
+        info[id].x = c->seclabel[id];
+    for (Map *m : ms) {
+        if (m->role != ROLE_LXC)
+            continue;
+        for (auto &e : m->kv) {
+            uint32_t ifx;
+            uint16_t id;
+            memcpy(&ifx, e.second.val.data(), 4);
+            memcpy(&id, e.second.val.data() + 6, 2);
+            info[id].y = ifx;
         }
-        if ((rc = upload_vec(E->ep_info, info, s)))
-            return rc;
     }
+    if ((*rc = upload_vec(g->ep_info, info, s)))
+        return nullptr;
+    return g;
+}
+
+std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hipStream_t s,
+                               int *rc)
+{
+    auto g = std::make_shared<GCt>();
+    if ((*rc = upload_vec(g->ct4, img.ct4, s)) || (*rc = upload_vec(g->ct6, img.ct6, s)) ||
+        (*rc = upload_vec(g->ct4_tm, img.ct4_tm, s)) ||
+        (*rc = upload_vec(g->ct6_tm, img.ct6_tm, s)))
+        return nullptr;
+    const size_t nslots = img.ct4.size() + img.ct6.size();
+    if (nslots && (*rc = g->ct_acct.zeros(32 * nslots, s)))
+        return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
-            E->ct_maps[ct_map_key(m->role == ROLE_CT4 ? 4 : 6,
+            g->ct_maps[ct_map_key(m->role == ROLE_CT4 ? 4 : 6,
                                   ct_owner_word((uint32_t)std::max(m->policy_lxc, 0),
                                                 m->policy_lxc >= 0),
                                   m->ct_any)] = m;
-    DevTables &T = E->T;
-    T.ct4 = img.n_ct4 ? (const Ct4Slot *)E->ct4.p : nullptr;
-    T.ct6 = img.n_ct6 ? (const Ct6Slot *)E->ct6.p : nullptr;
-    T.ct_acct = (uint64_t *)E->ct_acct.p;
-    T.ct4_tm = (const CtTimer *)E->ct4_tm.p;
-    T.ct6_tm = (const CtTimer *)E->ct6_tm.p;
-    T.ct4_mask = img.ct4_mask;
-    T.ct4_probe = img.ct4_probe;
-    T.ct6_mask = img.ct6_mask;
-    T.ct6_probe = img.ct6_probe;
-    T.ct6_acct_base = (uint32_t)img.ct4.size();
-    E->ct4_host = std::move(img.ct4);
-    E->ct6_host = std::move(img.ct6);
-    E->st.ct4_entries = img.n_ct4;
-    E->st.ct6_entries = img.n_ct6;
-    T.lxc6 = (const Lxc6Slot *)E->lxc6.p;
-    T.lxc6_mask = img.lxc6_mask;
-    T.lxc6_lds = img.lxc6.size() <= LXC6_LDS_MAX_SLOTS;
-    T.l4d = (const uint4 *)E->l4d.p;
-    T.l4c = (const uint32_t *)E->l4c.p;
-    T.l4l = (const uint64_t *)E->l4l.p;
-    T.tbl24 = (const uint32_t *)E->tbl24.p;
-    T.tbl8 = (const uint32_t *)E->tbl8.p;
-    T.lbl_ovf = (const uint32_t *)E->ovf.p;
-    T.pf_tbl24 = (const uint32_t *)E->pf24.p;
-    T.pf_tbl8 = (const uint32_t *)E->pf8.p;
-    T.pf_fix = (const uint32_t *)E->pffix.p;
-    T.pf_fix_mask = img.pf_fix_mask;
-    T.pf_fix_zero = img.pf_fix_zero;
-    T.lxc4 = (const LxcSlot *)E->lxc4.p;
-    T.lxc4_mask = img.lxc4_mask;
-    T.lxc4_lds = img.lxc4.size() <= LXC_LDS_MAX_SLOTS;
-    T.pol = (const PolSlot *)E->pol.p;
-    T.pf_bloom = (const uint32_t *)E->pfbloom.p;
-    T.pf_bloom_words = (uint32_t)img.pf_bloom.size();
-    T.pol_bloom = (const uint32_t *)E->polbloom.p;
-    T.pol_bloom_words = (uint32_t)img.pol_bloom.size();
-    T.n_ctr = (uint32_t)img.ctr_owner.size();
-    E->pol_loc = img.pol_loc;
-    E->ctr_owner = img.ctr_owner;
-    E->st.epoch = E->id;
-    E->st.device_bytes = img.device_bytes();
-    E->st.ipcache_v4_prefixes = img.n_prefix4;
-    E->st.lpm4_tbl8_groups = (uint32_t)(img.tbl8.size() / 256);
-    E->st.policy_entries = T.n_ctr;
-    E->st.endpoints = img.n_eps;
-    E->st.prefilter_v4_fix = img.n_pf_fix;
-    E->st.prefilter_v4_dyn = img.n_pf_dyn;
-    E->st.lpm4_layout = (uint32_t)img.lpm4_layout;
-    E->st.lpm4_kib = (uint32_t)((4ull * (img.l4d.size() + img.l4c.size() + img.tbl24.size() +
-                                        img.tbl8.size()) +
-                                 8ull * img.l4l.size() + 1023) / 1024);
-    E->st.ipcache_v6_prefixes = img.ipc6.n;
-    E->st.lpm6_lengths = (uint32_t)img.ipc6.lens.size();
-    E->st.lpm6_groups = img.ipc6.groups;
-    E->st.lpm6_kib = (uint32_t)((img.ipc6.bytes() + 1023) / 1024);
-    E->st.endpoints_v6 = img.n_eps6;
-    E->st.prefilter_v6_fix = img.pf6_fix.n;
-    E->st.prefilter_v6_dyn = img.pf6_dyn.n;
+    g->ct4_mask = img.ct4_mask;
+    g->ct4_probe = img.ct4_probe;
+    g->ct6_mask = img.ct6_mask;
+    g->ct6_probe = img.ct6_probe;
+    g->n_ct4 = img.n_ct4;
+    g->n_ct6 = img.n_ct6;
+    g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
+               48ull * nslots;
+    g->ct4_host = std::move(img.ct4);
+    g->ct6_host = std::move(img.ct6);
+    return g;
+}
 
-    // counters for the new entry layout (old ones were folded above)
-    size_t need = 2ull * T.n_ctr + METRIC_U64 + ID_U64;
-    if (need != c->ctr_u64) {
-        if (c->ctr)
-            (void)hipFree(c->ctr);
-        c->ctr = nullptr;
-        if (hipMalloc((void **)&c->ctr, need * 8) != hipSuccess)
-            return -ENOMEM;
-        c->ctr_u64 = need;
+// the kernels' view of an epoch's groups
+void assemble(Epoch &E)
+{
+    DevTables &T = E.T;
+    T = DevTables{};
+    const GIpc &I = *E.ipc;
+    const GPf &P = *E.pf;
+    const GEp &D = *E.ep;
+    const GCt &C = *E.ct;
+    T.l4d = (const uint4 *)I.l4d.p;
+    T.l4c = (const uint32_t *)I.l4c.p;
+    T.l4l = (const uint64_t *)I.l4l.p;
+    T.tbl24 = (const uint32_t *)I.tbl24.p;
+    T.tbl8 = (const uint32_t *)I.tbl8.p;
+    T.lbl_ovf = (const uint32_t *)I.ovf.p;
+    T.ipc6 = I.ipc6;
+    T.id_cover = I.id_cover;
+    T.pf_tbl24 = (const uint32_t *)P.pf24.p;
+    T.pf_tbl8 = (const uint32_t *)P.pf8.p;
+    T.pf_fix = (const uint32_t *)P.pffix.p;
+    T.pf_fix_mask = P.fix_mask;
+    T.pf_fix_zero = P.fix_zero;
+    T.pf_bloom = (const uint32_t *)P.pfbloom.p;
+    T.pf_bloom_words = P.bloom_words;
+    T.pf6_fix = P.fix;
+    T.pf6_dyn = P.dyn;
+    T.lxc4 = (const LxcSlot *)D.lxc4.p;
+    T.lxc4_mask = D.lxc4_mask;
+    T.lxc4_lds = D.lxc4_lds;
+    T.lxc6 = (const Lxc6Slot *)D.lxc6.p;
+    T.lxc6_mask = D.lxc6_mask;
+    T.lxc6_lds = D.lxc6_lds;
+    T.pol = (const PolSlot *)D.pol.p;
+    T.pol_bloom = (const uint32_t *)D.polbloom.p;
+    T.pol_bloom_words = D.pol_bloom_words;
+    T.n_ctr = (uint32_t)D.ctr_owner.size();
+    T.ct4 = C.n_ct4 ? (const Ct4Slot *)C.ct4.p : nullptr;
+    T.ct6 = C.n_ct6 ? (const Ct6Slot *)C.ct6.p : nullptr;
+    T.ct_acct = (uint64_t *)C.ct_acct.p;
+    T.ct4_tm = (const CtTimer *)C.ct4_tm.p;
+    T.ct6_tm = (const CtTimer *)C.ct6_tm.p;
+    T.ct4_mask = C.ct4_mask;
+    T.ct4_probe = C.ct4_probe;
+    T.ct6_mask = C.ct6_mask;
+    T.ct6_probe = C.ct6_probe;
+    T.ct6_acct_base = (uint32_t)C.ct4_host.size();
+    cfc_stats &st = E.st;
+    st = cfc_stats{};
+    st.epoch = E.id;
+    st.device_bytes = I.bytes + P.bytes + D.bytes + C.bytes;
+    st.ipcache_v4_prefixes = I.n_prefix4;
+    st.lpm4_tbl8_groups = I.tbl8_groups;
+    st.policy_entries = T.n_ctr;
+    st.endpoints = D.n_eps;
+    st.prefilter_v4_fix = P.n_fix4;
+    st.prefilter_v4_dyn = P.n_dyn4;
+    st.lpm4_layout = (uint32_t)I.layout;
+    st.lpm4_kib = I.lpm4_kib;
+    st.ipcache_v6_prefixes = I.n_prefix6;
+    st.lpm6_lengths = I.lpm6_lengths;
+    st.lpm6_groups = I.lpm6_groups;
+    st.lpm6_kib = I.lpm6_kib;
+    st.endpoints_v6 = D.n_eps6;
+    st.prefilter_v6_fix = P.n_fix6;
+    st.prefilter_v6_dyn = P.n_dyn6;
+    st.ct4_entries = C.n_ct4;
+    st.ct6_entries = C.n_ct6;
+}
+
+// Build the next epoch: re-flatten and upload the groups whose maps changed,
+// share the others with the current epoch, swap without draining the
+// device (the old epoch is retired until the streams that used it pass the
+// swap point).
+int commit_locked(cfc_ctx *c, hipStream_t s)
+{
+    reap_retired(c);
+    uint64_t sig[4];
+    group_sigs(c, sig);
+    unsigned groups = 0;
+    for (int g = 0; g < 4; g++)
+        if (!c->epoch || sig[g] != c->built_sig[g])
+            groups |= 1u << g;
+    if (!groups)
+        return 0;
+    int rc;
+    // counts made under the old layout go to the maps first: policy-entry
+    // counters when the endpoint tables change, CT accounting when CT does
+    if (groups & (GROUP_ENDPOINTS | GROUP_CT))
+        if ((rc = fold_counters(c, s)))
+            return rc;
+    std::vector<Map *> ms;
+    for (auto &kv : c->maps)
+        ms.push_back(kv.second.get());
+    HostImage img;
+    build_image(ms, c->opts, &img, groups);
+
+    auto E = std::make_shared<Epoch>();
+    E->id = ++c->epoch_seq;
+    rc = 0;
+    E->ipc = (groups & GROUP_IPCACHE) ? build_ipc(img, ms, s, &rc) : c->epoch->ipc;
+    if (!rc)
+        E->pf = (groups & GROUP_PREFILTER) ? build_pf(img, s, &rc) : c->epoch->pf;
+    if (!rc)
+        E->ep = (groups & GROUP_ENDPOINTS) ? build_ep(c, img, ms, s, &rc) : c->epoch->ep;
+    if (!rc)
+        E->ct = (groups & GROUP_CT) ? build_ctg(img, ms, s, &rc) : c->epoch->ct;
+    if (rc)
+        return rc;
+    assemble(*E);
+
+    // counters for a new entry layout (the old ones were folded above)
+    if (groups & GROUP_ENDPOINTS) {
+        const size_t need = 2ull * E->T.n_ctr + METRIC_U64 + ID_U64;
+        if (need != c->ctr_u64) {
+            if (c->ctr) {
+                (void)hipStreamSynchronize(s);
+                (void)hipFree(c->ctr);
+            }
+            c->ctr = nullptr;
+            if (hipMalloc((void **)&c->ctr, need * 8) != hipSuccess)
+                return -ENOMEM;
+            c->ctr_u64 = need;
+        }
+        if (hipMemsetAsync(c->ctr, 0, need * 8, s) != hipSuccess)
+            return -EIO;
     }
-    if (hipMemsetAsync(c->ctr, 0, need * 8, s) != hipSuccess)
+    // the uploads read host vectors freed below; launches on other streams
+    // keep reading the old epoch, which stays until they pass this point
+    if (hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
-    // the host images must outlive the copies, and in-flight launches on
-    // other streams may still read the previous epoch: drain the device
-    if (hipDeviceSynchronize() != hipSuccess)
-        return -EIO;
+    if (c->epoch) {
+        Retired r;
+        r.e = c->epoch;
+        for (hipStream_t st : c->streams) {
+            hipEvent_t ev;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(ev, st) != hipSuccess) {
+                (void)hipDeviceSynchronize();   // cannot track it: drain instead
+                break;
+            }
+            r.ev.push_back(ev);
+        }
+        c->retired.push_back(std::move(r));
+    }
+    c->streams.clear();
     c->epoch = std::move(E);
-    c->built_sig = sig;
+    for (int g = 0; g < 4; g++)
+        c->built_sig[g] = sig[g];
     return 0;
 }
 
@@ -547,6 +755,10 @@ void cfc_close(cfc_ctx *c)
         (void)hipSetDevice(c->device);
         (void)hipDeviceSynchronize();
     }
+    for (Retired &r : c->retired)
+        for (hipEvent_t e : r.ev)
+            (void)hipEventDestroy(e);
+    c->retired.clear();
     c->epoch.reset();
     free_timing(c);
     if (c->ctr)
@@ -840,7 +1052,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         const uint8_t *b = c->node.router_ip6 + 4 * w;
         T.router6[w] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
     }
-    EgressArgs ea{ep_lxc, E.seclabel[ep_lxc], 0, 0, 0};
+    EgressArgs ea{ep_lxc, E.ep->seclabel[ep_lxc], 0, 0, 0};
     {   // the sending endpoint's CT maps: its own, or the global ones
         for (auto &kv : c->maps)
             if ((kv.second->role == ROLE_CT4 || kv.second->role == ROLE_CT6) &&
@@ -848,8 +1060,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
                 ea.ct_owner = ct_owner_word(ep_lxc, true);
     }
     if (mode == CFC_MODE_EGRESS) {
-        auto it = E.pol_loc.find(ep_lxc);
-        if (it == E.pol_loc.end())
+        auto it = E.ep->pol_loc.find(ep_lxc);
+        if (it == E.ep->pol_loc.end())
             return -ENOENT;  // no endpoint program (policy map) for ep_lxc
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
@@ -875,6 +1087,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         return rc;
     (void)hipEventRecord(c->last_done, s);
     c->last_stream = s;
+    note_stream(c, s);
     c->ctr_pending = true;
     return 0;
 }
@@ -945,8 +1158,8 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     a.n = in->n;
     a.family = family;
     a.mode = mode;
-    a.own_seclabel = E.seclabel[ep_lxc];   // as the batch was classified
-    a.ep_info = reinterpret_cast<const uint2 *>(E.ep_info.p);
+    a.own_seclabel = E.ep->seclabel[ep_lxc];   // as the batch was classified
+    a.ep_info = reinterpret_cast<const uint2 *>(E.ep->ep_info.p);
     a.host_ifindex = c->node.host_ifindex;
     a.traces = traces;
     a.rec = rec;
@@ -1063,6 +1276,7 @@ int cfc_counters_export(cfc_ctx *c, uint64_t *dst, uint64_t n, void *stream)
         return -EIO;
     (void)hipEventRecord(c->last_done, s);
     c->last_stream = s;
+    note_stream(c, s);
     return 0;
 }
 
@@ -1084,6 +1298,7 @@ int cfc_counters_import(cfc_ctx *c, const uint64_t *src, uint64_t n,
         return rc;
     (void)hipEventRecord(c->last_done, s);
     c->last_stream = s;
+    note_stream(c, s);
     c->ctr_pending = true;
     return 0;
 }
@@ -1270,42 +1485,42 @@ int64_t ct_dev_slot(const Epoch &E, const Map *m, const std::string &k)
         return -1;
     const uint32_t w = ct_word(nh, (uint8_t)k[2 * al + 5], owner);
     if (!v6) {
-        if (E.ct4_host.empty())
+        if (E.ct->ct4_host.empty())
             return -1;
         uint32_t x, y;
         memcpy(&x, k.data(), 4);
         memcpy(&y, k.data() + 4, 4);
-        const uint32_t mask = (uint32_t)E.ct4_host.size() - 1;
+        const uint32_t mask = (uint32_t)E.ct->ct4_host.size() - 1;
         for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
-            const Ct4Slot &e = E.ct4_host[i];
+            const Ct4Slot &e = E.ct->ct4_host[i];
             if (!e.w)
                 return -1;
             if (e.x == x && e.y == y && e.z == z && e.w == w)
                 return i;
         }
     }
-    if (E.ct6_host.empty())
+    if (E.ct->ct6_host.empty())
         return -1;
     uint32_t d[4], sa[4];
     memcpy(d, k.data(), 16);
     memcpy(sa, k.data() + 16, 16);
-    const uint32_t mask = (uint32_t)E.ct6_host.size() - 1;
+    const uint32_t mask = (uint32_t)E.ct->ct6_host.size() - 1;
     for (uint32_t i = ct_hash6(d, sa, z, w) & mask;; i = (i + 1) & mask) {
-        const Ct6Slot &e = E.ct6_host[i];
+        const Ct6Slot &e = E.ct->ct6_host[i];
         if (!e.w)
             return -1;
         if (e.z == z && e.w == w && !memcmp(e.d, d, 16) && !memcmp(e.s, sa, 16))
-            return (int64_t)E.ct4_host.size() + i;
+            return (int64_t)E.ct->ct4_host.size() + i;
     }
 }
 
 void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t s)
 {
-    if (!c->epoch || !c->epoch->ct_acct.p)
+    if (!c->epoch || !c->epoch->ct->ct_acct.p)
         return;
     const int64_t slot = ct_dev_slot(*c->epoch, m, k);
     if (slot >= 0)
-        (void)hipMemsetAsync((char *)c->epoch->ct_acct.p + 32 * slot, 0, 32, s);
+        (void)hipMemsetAsync((char *)c->epoch->ct->ct_acct.p + 32 * slot, 0, 32, s);
 }
 
 template <class Hdr>

@@ -539,15 +539,19 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
 }
 
 void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
-                 HostImage *img)
+                 HostImage *img, unsigned groups)
 {
     *img = HostImage();
     img->ct_local.assign(65536, 0);
     std::vector<const Map *> cts;
     for (Map *m : maps)
-        if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
+        if (m->role == ROLE_CT4 || m->role == ROLE_CT6) {
             cts.push_back(m);
-    build_ct(cts, img);
+            if (m->policy_lxc >= 0)
+                img->ct_local[m->policy_lxc] = 1;
+        }
+    if (groups & GROUP_CT)
+        build_ct(cts, img);
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,
               *pf4dyn = nullptr, *pf6fix = nullptr, *pf6dyn = nullptr;
     std::map<int, Map *> pols;
@@ -564,6 +568,14 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         }
     }
 
+    if (!(groups & GROUP_IPCACHE))
+        ipc = nullptr;
+    if (!(groups & GROUP_PREFILTER))
+        pf4fix = pf4dyn = pf6fix = pf6dyn = nullptr;
+    if (!(groups & GROUP_ENDPOINTS)) {
+        lxc = nullptr;
+        pols.clear();
+    }
     // ---- ipcache v4: the compact multibit layout unless forced (or its
     //      offsets overflow), DIR-24-8 otherwise
     if (ipc) {

@@ -83,9 +83,19 @@ struct HostImage {
 // the CT map a slot's entry lives in: (family 4/6, owner word, any) key
 uint64_t ct_map_key(int family, uint32_t owner, int any);
 
-// maps: every map of the context.
+// Table groups an epoch is built from; a commit rebuilds only the groups
+// whose maps changed (the others' device buffers carry over).
+enum : unsigned {
+    GROUP_IPCACHE = 1,    // ipcache: IPv4 LPM (+ lbl_ovf), IPv6 LPM
+    GROUP_PREFILTER = 2,  // XDP prefilter, both families
+    GROUP_ENDPOINTS = 4,  // cilium_lxc + every policymap (+ counter layout)
+    GROUP_CT = 8,         // every CT map
+    GROUP_ALL = 15,
+};
+// maps: every map of the context; groups: which parts of img to build
+// (ct_local, which only depends on which CT maps exist, always is).
 void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
-                 HostImage *img);
+                 HostImage *img, unsigned groups = GROUP_ALL);
 
 // exposed for host-side unit tests of the LPM builders
 struct Pfx4 {
