@@ -69,13 +69,17 @@ static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 // An epoch is four table groups (flatten.hpp GROUP_*), each an immutable
 // set of device buffers shared by every epoch built while its maps did not
 // change: a commit re-flattens and uploads only the groups whose maps did.
-struct GIpc {          // ipcache
-    DevBuf tbl24, tbl8, ovf, l4d, l4c, l4l, l6[3];
-    Lpm6 ipc6{};
+struct GIpc {          // ipcache, IPv4
+    DevBuf tbl24, tbl8, ovf, l4d, l4c, l4l;
     int layout = 0;
-    uint32_t n_prefix4 = 0, tbl8_groups = 0, lpm4_kib = 0, lpm6_kib = 0,
-             n_prefix6 = 0, lpm6_lengths = 0, lpm6_groups = 0;
-    uint32_t id_cover = 1;   // identity histogram ranges (reserved + ipcache)
+    uint32_t n_prefix4 = 0, tbl8_groups = 0, lpm4_kib = 0;
+    uint64_t bytes = 0;
+};
+struct GIpc6 {         // ipcache, IPv6 (host copy kept for in-place label patches)
+    DevBuf l6[3];
+    Lpm6 ipc6{};
+    Lpm6Host host;
+    uint32_t lpm6_kib = 0, n_prefix6 = 0, lpm6_lengths = 0, lpm6_groups = 0;
     uint64_t bytes = 0;
 };
 struct GPf {           // prefilter
@@ -87,6 +91,7 @@ struct GPf {           // prefilter
 };
 struct GEp {           // endpoints + policy (+ the counter layout)
     DevBuf lxc4, lxc6, pol, polbloom;
+    std::vector<PolSlot> pol_host;    // for in-place proxy-port patches
     uint32_t lxc4_mask = 0, lxc6_mask = 0, pol_bloom_words = 0, n_eps = 0, n_eps6 = 0;
     bool lxc4_lds = false, lxc6_lds = false;
     std::unordered_map<int, PolLoc> pol_loc;
@@ -109,6 +114,7 @@ struct GCt {           // conntrack
 struct Epoch {
     uint64_t id = 0;
     std::shared_ptr<GIpc> ipc;
+    std::shared_ptr<GIpc6> ipc6;
     std::shared_ptr<GPf> pf;
     std::shared_ptr<GEp> ep;
     std::shared_ptr<GCt> ct;
@@ -141,7 +147,8 @@ struct cfc_ctx {
 
     std::shared_ptr<Epoch> epoch;
     uint64_t epoch_seq = 0;
-    uint64_t built_sig[4] = {~0ull, ~0ull, ~0ull, ~0ull};   // per group
+    uint64_t built_sig[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};   // per group
+    uint32_t id_cover = 1;   // identity histogram ranges (reserved + ipcache)
     std::vector<Retired> retired;
     std::vector<hipStream_t> streams;   // streams launched on since the last swap
 
@@ -171,36 +178,41 @@ struct cfc_ctx {
 
 namespace {
 
-// signature of the maps behind each table group (GROUP_* bit order)
-int group_of(Role r)
+// Signatures of the maps behind each table group, bit g of GROUP_*
+// (0 ipcache v4, 1 prefilter, 2 endpoints + policy, 3 CT, 4 ipcache v6).
+// Structural changes (inserts, deletes) count; a value overwritten in place
+// does not where a commit can patch it (ipcache v6 labels, policy entries).
+constexpr int NGROUPS = 5;
+void group_sigs(cfc_ctx *c, uint64_t sig[NGROUPS])
 {
-    switch (r) {
-    case ROLE_IPCACHE: return 0;
-    case ROLE_PF4_FIX: case ROLE_PF4_DYN: case ROLE_PF6_FIX: case ROLE_PF6_DYN: return 1;
-    case ROLE_LXC: case ROLE_POLICY: return 2;
-    case ROLE_CT4: case ROLE_CT6: return 3;
-    default: return -1;
-    }
-}
-void group_sigs(cfc_ctx *c, uint64_t sig[4])
-{
-    for (int g = 0; g < 4; g++)
+    for (int g = 0; g < NGROUPS; g++)
         sig[g] = 1469598103934665603ull + (uint64_t)g;
-    sig[0] = (sig[0] ^ (uint64_t)c->opts.lpm4) * 1099511628211ull;
-    sig[2] = (sig[2] ^ c->seclabel_gen) * 1099511628211ull;
+    auto mix = [&](int g, uint64_t v) { sig[g] = (sig[g] ^ v) * 1099511628211ull; };
+    mix(0, (uint64_t)c->opts.lpm4);
+    mix(2, c->seclabel_gen);
     for (auto &kv : c->maps) {
         const Map *m = kv.second.get();
-        const int g = group_of(m->role);
-        if (g < 0)
-            continue;
-        for (int x : {g, g == 3 ? 2 : -1}) {   // endpoints see which CT maps exist
-            if (x < 0)
-                continue;
-            sig[x] = (sig[x] ^ (uint64_t)(uintptr_t)m) * 1099511628211ull;
-            if (x == g) {
-                sig[x] = (sig[x] ^ m->gen) * 1099511628211ull;
-                sig[x] = (sig[x] ^ m->kv.size()) * 1099511628211ull;
-            }
+        const uint64_t id = (uint64_t)(uintptr_t)m;
+        switch (m->role) {
+        case ROLE_IPCACHE:
+            mix(0, id); mix(0, m->sgen[0]);
+            mix(4, id); mix(4, m->sgen[1]);
+            break;
+        case ROLE_PF4_FIX: case ROLE_PF4_DYN: case ROLE_PF6_FIX: case ROLE_PF6_DYN:
+            mix(1, id); mix(1, m->sgen[0]);
+            break;
+        case ROLE_LXC:
+            mix(2, id); mix(2, m->gen);
+            break;
+        case ROLE_POLICY:
+            mix(2, id); mix(2, m->sgen[0]);
+            break;
+        case ROLE_CT4: case ROLE_CT6:
+            mix(3, id); mix(3, m->gen); mix(3, m->kv.size());
+            mix(2, id);   // endpoints see which CT maps exist
+            break;
+        default:
+            break;
         }
     }
 }
@@ -347,6 +359,28 @@ void note_stream(cfc_ctx *c, hipStream_t s)
         c->streams.push_back(s);
 }
 
+// the identity ranges of the labels overwritten in place since the last
+// commit (added to the cover; a range is never dropped before a rebuild)
+uint32_t identity_cover_touched(cfc_ctx *c)
+{
+    uint32_t cover = 0;
+    for (auto &kv : c->maps) {
+        Map *m = kv.second.get();
+        if (m->role != ROLE_IPCACHE)
+            continue;
+        for (auto &t : m->touched) {
+            auto it = m->kv.find(t.first);
+            if (it == m->kv.end())
+                continue;
+            uint32_t lab;
+            memcpy(&lab, it->second.val.data(), 4);
+            if (lab < ID_PACK_LIMIT)
+                cover |= 1u << id_range_of(lab);
+        }
+    }
+    return cover;
+}
+
 // free the retired epochs whose readers have all passed
 void reap_retired(cfc_ctx *c)
 {
@@ -367,39 +401,51 @@ void reap_retired(cfc_ctx *c)
     }
 }
 
-std::shared_ptr<GIpc> build_ipc(const HostImage &img, const std::vector<Map *> &ms,
-                                hipStream_t s, int *rc)
+std::shared_ptr<GIpc> build_ipc(const HostImage &img, hipStream_t s, int *rc)
 {
     auto g = std::make_shared<GIpc>();
     if ((*rc = upload_vec(g->tbl24, img.tbl24, s)) || (*rc = upload_vec(g->tbl8, img.tbl8, s)) ||
         (*rc = upload_vec(g->ovf, img.lbl_ovf, s)) || (*rc = upload_vec(g->l4d, img.l4d, s)) ||
-        (*rc = upload_vec(g->l4c, img.l4c, s)) || (*rc = upload_vec(g->l4l, img.l4l, s)) ||
-        (*rc = upload_lpm6(g->l6, img.ipc6, &g->ipc6, s)))
+        (*rc = upload_vec(g->l4c, img.l4c, s)) || (*rc = upload_vec(g->l4l, img.l4l, s)))
         return nullptr;
     g->layout = img.lpm4_layout;
     g->n_prefix4 = img.n_prefix4;
     g->tbl8_groups = (uint32_t)(img.tbl8.size() / 256);
     g->lpm4_kib = (uint32_t)((4ull * (img.l4d.size() + img.l4c.size() + img.tbl24.size() +
                                       img.tbl8.size()) + 8ull * img.l4l.size() + 1023) / 1024);
+    g->bytes = 4ull * (img.tbl24.size() + img.tbl8.size() + img.lbl_ovf.size() +
+                       img.l4d.size() + img.l4c.size()) + 8ull * img.l4l.size();
+    return g;
+}
+
+std::shared_ptr<GIpc6> build_ipc6(HostImage &img, hipStream_t s, int *rc)
+{
+    auto g = std::make_shared<GIpc6>();
+    if ((*rc = upload_lpm6(g->l6, img.ipc6, &g->ipc6, s)))
+        return nullptr;
     g->n_prefix6 = img.ipc6.n;
     g->lpm6_lengths = (uint32_t)img.ipc6.lens.size();
     g->lpm6_groups = img.ipc6.groups;
     g->lpm6_kib = (uint32_t)((img.ipc6.bytes() + 1023) / 1024);
-    g->bytes = 4ull * (img.tbl24.size() + img.tbl8.size() + img.lbl_ovf.size() +
-                       img.l4d.size() + img.l4c.size()) + 8ull * img.l4l.size() +
-               img.ipc6.bytes();
-    // per-identity counters: the histogram ranges holding the reserved
-    // identities and every ipcache identity; others count directly
-    g->id_cover = 1u;
+    g->bytes = img.ipc6.bytes();
+    g->host = std::move(img.ipc6);
+    return g;
+}
+
+// per-identity counters: the histogram ranges holding the reserved
+// identities and every ipcache identity; others count directly
+uint32_t identity_cover(const std::vector<Map *> &ms)
+{
+    uint32_t cover = 1u;
     for (Map *m : ms)
         if (m->role == ROLE_IPCACHE)
             for (const auto &kv : m->kv) {
                 uint32_t lab;
                 memcpy(&lab, kv.second.val.data(), 4);
                 if (lab < ID_PACK_LIMIT)
-                    g->id_cover |= 1u << id_range_of(lab);
+                    cover |= 1u << id_range_of(lab);
             }
-    return g;
+    return cover;
 }
 
 std::shared_ptr<GPf> build_pf(const HostImage &img, hipStream_t s, int *rc)
@@ -436,6 +482,7 @@ std::shared_ptr<GEp> build_ep(cfc_ctx *c, HostImage &img, const std::vector<Map 
     g->lxc4_lds = img.lxc4.size() <= LXC_LDS_MAX_SLOTS;
     g->lxc6_lds = img.lxc6.size() <= LXC6_LDS_MAX_SLOTS;
     g->pol_bloom_words = (uint32_t)img.pol_bloom.size();
+    g->pol_host = img.pol;
     g->n_eps = img.n_eps;
     g->n_eps6 = img.n_eps6;
     g->pol_loc = std::move(img.pol_loc);
@@ -500,6 +547,7 @@ void assemble(Epoch &E)
     DevTables &T = E.T;
     T = DevTables{};
     const GIpc &I = *E.ipc;
+    const GIpc6 &I6 = *E.ipc6;
     const GPf &P = *E.pf;
     const GEp &D = *E.ep;
     const GCt &C = *E.ct;
@@ -509,8 +557,7 @@ void assemble(Epoch &E)
     T.tbl24 = (const uint32_t *)I.tbl24.p;
     T.tbl8 = (const uint32_t *)I.tbl8.p;
     T.lbl_ovf = (const uint32_t *)I.ovf.p;
-    T.ipc6 = I.ipc6;
-    T.id_cover = I.id_cover;
+    T.ipc6 = I6.ipc6;
     T.pf_tbl24 = (const uint32_t *)P.pf24.p;
     T.pf_tbl8 = (const uint32_t *)P.pf8.p;
     T.pf_fix = (const uint32_t *)P.pffix.p;
@@ -543,7 +590,7 @@ void assemble(Epoch &E)
     cfc_stats &st = E.st;
     st = cfc_stats{};
     st.epoch = E.id;
-    st.device_bytes = I.bytes + P.bytes + D.bytes + C.bytes;
+    st.device_bytes = I.bytes + I6.bytes + P.bytes + D.bytes + C.bytes;
     st.ipcache_v4_prefixes = I.n_prefix4;
     st.lpm4_tbl8_groups = I.tbl8_groups;
     st.policy_entries = T.n_ctr;
@@ -552,10 +599,10 @@ void assemble(Epoch &E)
     st.prefilter_v4_dyn = P.n_dyn4;
     st.lpm4_layout = (uint32_t)I.layout;
     st.lpm4_kib = I.lpm4_kib;
-    st.ipcache_v6_prefixes = I.n_prefix6;
-    st.lpm6_lengths = I.lpm6_lengths;
-    st.lpm6_groups = I.lpm6_groups;
-    st.lpm6_kib = I.lpm6_kib;
+    st.ipcache_v6_prefixes = I6.n_prefix6;
+    st.lpm6_lengths = I6.lpm6_lengths;
+    st.lpm6_groups = I6.lpm6_groups;
+    st.lpm6_kib = I6.lpm6_kib;
     st.endpoints_v6 = D.n_eps6;
     st.prefilter_v6_fix = P.n_fix6;
     st.prefilter_v6_dyn = P.n_dyn6;
@@ -567,18 +614,102 @@ void assemble(Epoch &E)
 // share the others with the current epoch, swap without draining the
 // device (the old epoch is retired until the streams that used it pass the
 // swap point).
+// Value-only overwrites since the last commit, patched into the live
+// tables in place (a concurrent launch sees the old or the new value, as a
+// BPF program racing a map update does): IPv6 ipcache labels, policy
+// entries' proxy ports.  IPv4 ipcache labels rebuild that (small) group.
+// Returns the groups that still need a rebuild.
+unsigned patch_touched(cfc_ctx *c, unsigned groups, hipStream_t s)
+{
+    Epoch &E = *c->epoch;
+    for (auto &kv : c->maps) {
+        Map *m = kv.second.get();
+        if (m->touched.empty())
+            continue;
+        if (m->role == ROLE_IPCACHE) {
+            for (auto &t : m->touched) {
+                auto it = m->kv.find(t.first);
+                if (it == m->kv.end())
+                    continue;
+                const bool v6 = t.first.size() > 7 && (uint8_t)t.first[7] == 2;
+                if (!v6) {
+                    groups |= GROUP_IPCACHE4;
+                    continue;
+                }
+                if (groups & GROUP_IPCACHE6)
+                    continue;
+                Pfx6 p;
+                const int64_t slot = ipcache_v6_entry(t.first, it->second.val, &p)
+                                         ? lpm6_find_slot(E.ipc6->host, p) : -1;
+                if (slot < 0) {
+                    groups |= GROUP_IPCACHE6;
+                    continue;
+                }
+                L6Slot &d = E.ipc6->host.slots[slot];
+                d.label = p.label;
+                char *dev = (char *)E.ipc6->l6[0].p + sizeof(L6Slot) * slot +
+                            offsetof(L6Slot, label);
+                if (hipMemcpyAsync(dev, &d.label, 4, hipMemcpyHostToDevice, s) != hipSuccess)
+                    groups |= GROUP_IPCACHE6;
+            }
+        } else if (m->role == ROLE_POLICY && !(groups & GROUP_ENDPOINTS)) {
+            auto loc = E.ep->pol_loc.find(m->policy_lxc);
+            for (auto &t : m->touched) {
+                auto it = m->kv.find(t.first);
+                if (it == m->kv.end() || loc == E.ep->pol_loc.end())
+                    continue;
+                uint64_t key;
+                memcpy(&key, t.first.data(), 8);
+                if (((uint8_t)t.first[7] & 0xFE) != 0)
+                    continue;   // not in the device table (flatten.cpp)
+                const uint32_t mask = loc->second.mask, base = loc->second.base;
+                uint32_t sl = pol_slot(pol_key_pre((uint32_t)key, (uint32_t)(key >> 32)), mask);
+                PolSlot *tab = E.ep->pol_host.data() + base;
+                uint32_t n = 0;
+                while (tab[sl].key != key && tab[sl].key != POL_EMPTY && n++ <= mask)
+                    sl = (sl + 1) & mask;
+                if (tab[sl].key != key) {
+                    groups |= GROUP_ENDPOINTS;
+                    break;
+                }
+                memcpy(&tab[sl].proxy_port, it->second.val.data(), 2);
+                char *dev = (char *)E.ep->pol.p + sizeof(PolSlot) * (base + sl) +
+                            offsetof(PolSlot, proxy_port);
+                if (hipMemcpyAsync(dev, &tab[sl].proxy_port, 2, hipMemcpyHostToDevice,
+                                   s) != hipSuccess)
+                    groups |= GROUP_ENDPOINTS;
+            }
+        }
+    }
+    return groups;
+}
+
 int commit_locked(cfc_ctx *c, hipStream_t s)
 {
     reap_retired(c);
-    uint64_t sig[4];
+    uint64_t sig[NGROUPS];
     group_sigs(c, sig);
     unsigned groups = 0;
-    for (int g = 0; g < 4; g++)
+    bool touched = false;
+    for (int g = 0; g < NGROUPS; g++)
         if (!c->epoch || sig[g] != c->built_sig[g])
             groups |= 1u << g;
-    if (!groups)
+    for (auto &kv : c->maps)
+        touched |= !kv.second->touched.empty() &&
+                   (kv.second->role == ROLE_IPCACHE || kv.second->role == ROLE_POLICY);
+    if (!groups && !touched)
         return 0;
     int rc;
+    if (c->epoch && touched) {
+        groups = patch_touched(c, groups, s);
+        c->id_cover |= identity_cover_touched(c);
+        c->epoch->T.id_cover = c->id_cover;
+        if (!groups) {   // all patched in place: the epoch stays
+            for (auto &kv : c->maps)
+                kv.second->touched.clear();
+            return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
+        }
+    }
     // counts made under the old layout go to the maps first: policy-entry
     // counters when the endpoint tables change, CT accounting when CT does
     if (groups & (GROUP_ENDPOINTS | GROUP_CT))
@@ -593,7 +724,9 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     auto E = std::make_shared<Epoch>();
     E->id = ++c->epoch_seq;
     rc = 0;
-    E->ipc = (groups & GROUP_IPCACHE) ? build_ipc(img, ms, s, &rc) : c->epoch->ipc;
+    E->ipc = (groups & GROUP_IPCACHE4) ? build_ipc(img, s, &rc) : c->epoch->ipc;
+    if (!rc)
+        E->ipc6 = (groups & GROUP_IPCACHE6) ? build_ipc6(img, s, &rc) : c->epoch->ipc6;
     if (!rc)
         E->pf = (groups & GROUP_PREFILTER) ? build_pf(img, s, &rc) : c->epoch->pf;
     if (!rc)
@@ -603,6 +736,9 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     if (rc)
         return rc;
     assemble(*E);
+    if (groups & (GROUP_IPCACHE4 | GROUP_IPCACHE6))
+        c->id_cover = identity_cover(ms);
+    E->T.id_cover = c->id_cover;
 
     // counters for a new entry layout (the old ones were folded above)
     if (groups & GROUP_ENDPOINTS) {
@@ -640,8 +776,10 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     }
     c->streams.clear();
     c->epoch = std::move(E);
-    for (int g = 0; g < 4; g++)
+    for (int g = 0; g < NGROUPS; g++)
         c->built_sig[g] = sig[g];
+    for (auto &kv : c->maps)
+        kv.second->touched.clear();
     return 0;
 }
 

@@ -354,6 +354,45 @@ static void ipcache_v4(const Map *m, std::vector<Pfx4> *out,
 
 // Effective IPv6 prefixes of the ipcache: as ipcache_v4 with the v6 lookup
 // key {prefixlen 160, pad 0,0, family 2, addr} (eps.h:56-66).
+bool ipcache_v6_entry(const std::string &nk, const std::string &val, Pfx6 *p)
+{
+    static const uint8_t stat6[4] = {0, 0, 0, 2};
+    const uint8_t *k = (const uint8_t *)nk.data();
+    uint32_t P;
+    memcpy(&P, k, 4);
+    if (P <= 32 || P > 160 || nk.size() < 24 || val.size() < 4)
+        return false;
+    for (uint32_t bit = 0; bit < 32; bit++) {
+        uint32_t byte = bit >> 3, sh = 7 - (bit & 7);
+        if (((k[4 + byte] >> sh) & 1) != ((stat6[byte] >> sh) & 1))
+            return false;
+    }
+    p->plen = (uint8_t)(P - 32);
+    for (int i = 0; i < 4; i++) {
+        uint32_t a;
+        memcpy(&a, k + 8 + 4 * i, 4);
+        p->w[i] = bswap(a) & l6_word_mask(p->plen, i);
+    }
+    memcpy(&p->label, val.data(), 4);
+    return true;
+}
+
+int64_t lpm6_find_slot(const Lpm6Host &t, const Pfx6 &p)
+{
+    if (t.slots.empty() || !p.plen)
+        return -1;
+    const uint32_t mask = (uint32_t)t.slots.size() - 1;
+    uint32_t s = l6_hash(p.w[0], p.w[1], p.w[2], p.w[3], p.plen) & mask;
+    for (uint32_t n = 0; n <= mask; n++, s = (s + 1) & mask) {
+        const L6Slot &d = t.slots[s];
+        if (!d.len)
+            return -1;
+        if (d.len == p.plen && !memcmp(d.w, p.w, 16))
+            return s;
+    }
+    return -1;
+}
+
 static void ipcache_v6(const Map *m, std::vector<Pfx6> *out)
 {
     static const uint8_t stat6[4] = {0, 0, 0, 2};
@@ -568,7 +607,8 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         }
     }
 
-    if (!(groups & GROUP_IPCACHE))
+    const Map *ipc6m = (groups & GROUP_IPCACHE6) ? ipc : nullptr;
+    if (!(groups & GROUP_IPCACHE4))
         ipc = nullptr;
     if (!(groups & GROUP_PREFILTER))
         pf4fix = pf4dyn = pf6fix = pf6dyn = nullptr;
@@ -603,9 +643,9 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
     }
 
     // ---- ipcache v6
-    if (ipc) {
+    if (ipc6m) {
         std::vector<Pfx6> pfx;
-        ipcache_v6(ipc, &pfx);
+        ipcache_v6(ipc6m, &pfx);
         build_lpm6(pfx, &img->ipc6);
     }
 

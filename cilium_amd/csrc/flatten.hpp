@@ -41,6 +41,11 @@ struct Lpm6Host {
     }
 };
 void build_lpm6(const std::vector<Pfx6> &pfx, Lpm6Host *out);
+// one ipcache entry (normalised key, value) as an IPv6 prefix; false when it
+// is not one the IPv6 table holds on its own (prefix within the static part)
+bool ipcache_v6_entry(const std::string &nk, const std::string &val, Pfx6 *p);
+// the slot of prefix p in a built table, or -1
+int64_t lpm6_find_slot(const Lpm6Host &t, const Pfx6 &p);
 // host reference of the device lookup (unit tests): the label of the
 // longest prefix containing w, def_label when none
 uint32_t lpm6_lookup_host(const Lpm6Host &t, const uint32_t w[4]);
@@ -86,11 +91,12 @@ uint64_t ct_map_key(int family, uint32_t owner, int any);
 // Table groups an epoch is built from; a commit rebuilds only the groups
 // whose maps changed (the others' device buffers carry over).
 enum : unsigned {
-    GROUP_IPCACHE = 1,    // ipcache: IPv4 LPM (+ lbl_ovf), IPv6 LPM
+    GROUP_IPCACHE4 = 1,   // ipcache, IPv4 LPM (+ lbl_ovf)
     GROUP_PREFILTER = 2,  // XDP prefilter, both families
     GROUP_ENDPOINTS = 4,  // cilium_lxc + every policymap (+ counter layout)
     GROUP_CT = 8,         // every CT map
-    GROUP_ALL = 15,
+    GROUP_IPCACHE6 = 16,  // ipcache, IPv6 LPM
+    GROUP_ALL = 31,
 };
 // maps: every map of the context; groups: which parts of img to build
 // (ct_local, which only depends on which CT maps exist, always is).

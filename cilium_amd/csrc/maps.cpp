@@ -46,15 +46,20 @@ int Map::update(const void *key, const void *value, uint64_t flags)
     if (it != kv.end()) {
         if (flags == BPF_NOEXIST)
             return -EEXIST;
+        touched[nk] = 1;
     } else {
         if (flags == BPF_EXIST)
             return -ENOENT;
         if (kv.size() >= max_entries) {
-            if (type == MT_LRU_HASH && !kv.empty())
+            if (type == MT_LRU_HASH && !kv.empty()) {
                 kv.erase(kv.begin());  // stand-in for least recently used
-            else
+                sgen[0]++;
+                sgen[1]++;
+            } else {
                 return lpm() ? -ENOSPC : -E2BIG;
+            }
         }
+        bump_sgen(nk);
     }
     Entry &e = kv[nk];
     e.key.assign((const char *)key, ksz);
@@ -102,6 +107,8 @@ int Map::erase(const void *key)
     if (it == kv.end())
         return -ENOENT;
     kv.erase(it);
+    touched.erase(nk);
+    bump_sgen(nk);
     gen++;
     return 0;
 }

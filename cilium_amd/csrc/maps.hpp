@@ -41,6 +41,12 @@ struct Map {
     int ct_any = 0;        // ROLE_CT*: 1 = the ANY map, 0 = the TCP map
     uint32_t type = 0, ksz = 0, vsz = 0, max_entries = 0, flags = 0;
     uint64_t gen = 0;   // bumped on every mutation
+    // structural mutations (insert, delete, eviction): ipcache keys by
+    // family (sgen[0] IPv4, sgen[1] IPv6), other maps in sgen[0]
+    uint64_t sgen[2] = {0, 0};
+    // keys whose value was overwritten in place since the last commit (a
+    // commit may patch those into the device tables instead of rebuilding)
+    std::map<std::string, int> touched;
 
     struct Entry {
         std::string key;  // key bytes as last written
@@ -50,6 +56,22 @@ struct Map {
     std::map<std::string, Entry> kv;
 
     bool lpm() const { return type == MT_LPM_TRIE; }
+    // a structural change to a normalised key: the ipcache's IPv6 keys
+    // count apart (struct ipcache_key: family at byte 7, after the
+    // prefixlen word); a prefix shorter than the family byte counts for both
+    void bump_sgen(const std::string &nk)
+    {
+        uint32_t plen = 32;
+        if (nk.size() >= 4)
+            plen = (uint8_t)nk[0] | (uint8_t)nk[1] << 8 | (uint8_t)nk[2] << 16 |
+                   (uint32_t)(uint8_t)nk[3] << 24;
+        if (role != ROLE_IPCACHE || nk.size() <= 7 || plen < 32) {
+            sgen[0]++;
+            sgen[1]++;
+        } else {
+            sgen[(uint8_t)nk[7] == 2 ? 1 : 0]++;
+        }
+    }
     uint32_t value_bytes() const;  // per-CPU rounded for PERCPU maps
     // normalised key: raw for hashes; prefixlen + masked data for LPM.
     // Returns false for an invalid LPM key (prefixlen too large).

@@ -142,3 +142,53 @@ def test_commit_while_another_stream_runs(torch):
     merge_ipcache(t, rows)
     check(out2, O.Oracle(t), h2)
     dp.close()
+
+
+def test_in_place_patches(torch):
+    """Value-only overwrites: IPv6 ipcache labels and policy proxy ports are
+    patched into the live tables (the epoch stays); an IPv4 label overwrite
+    rebuilds the IPv4 group only.  Results against the oracle each time."""
+    t = S.config_c3(3, n_prefixes=100_000, n_v4_prefixes=10_000, n_endpoints=2,
+                    n_prefilter=2000)
+    dp = Datapath(0)
+    pms = load_tables(dp, t)
+    h6 = S.headers_c3(t, 400_000, seed=31)
+    h4 = S.headers_c2(t, 200_000, seed=32)
+    b6, b4 = pack(h6), pack(h4)
+    e0 = dp.stats()["epoch"]
+    rng = np.random.default_rng(5)
+    # IPv6 labels of existing prefixes
+    i6 = np.flatnonzero(t.ipcache["family"] == 2)
+    pick = rng.choice(i6, size=2000, replace=False)
+    rows = t.ipcache[pick].copy()
+    rows["label"] = rng.integers(256, 256 + 16384, size=len(rows))
+    apply_ipcache(dp, rows)
+    t.ipcache["label"][pick] = rows["label"]
+    out = dp.classify(b6, 0)
+    assert dp.stats()["epoch"] == e0, "patched in place, no new epoch"
+    check(out, O.Oracle(t), h6, mode=0)
+    # policy proxy ports of existing entries
+    pm = pms[S.EP_LXC_ID]
+    pol = t.policy[S.EP_LXC_ID]
+    sel = rng.choice(len(pol), size=200, replace=False)
+    for j in sel:
+        r = pol[j]
+        key = policymap.PolicyKey(int(r["identity"]), int(r["dport"]), int(r["proto"]),
+                                  int(r["egress"]))
+        port = int(S.htons(10001 + int(j) % 4)) if r["dport"] else 0
+        dp.update_element(pm.Fd, key.pack(), policymap.PolicyEntry(port).pack())
+        pol["proxy_port"][j] = port
+    out = dp.classify(b6, 0)
+    assert dp.stats()["epoch"] == e0
+    check(out, O.Oracle(t), h6, mode=0)
+    # IPv4 labels: the IPv4 group is rebuilt
+    i4 = np.flatnonzero(t.ipcache["family"] == 1)
+    pick = rng.choice(i4, size=500, replace=False)
+    rows = t.ipcache[pick].copy()
+    rows["label"] = rng.integers(256, 256 + 16384, size=len(rows))
+    apply_ipcache(dp, rows)
+    t.ipcache["label"][pick] = rows["label"]
+    out = dp.classify(b4, 0)
+    assert dp.stats()["epoch"] == e0 + 1
+    check(out, O.Oracle(t), h4, mode=0)
+    dp.close()
