@@ -243,7 +243,11 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
     constexpr bool LPM = MODE != CFC_MODE_XDP;
     if (LPM && T.l4d) {
+#if CFC_EXP == 4
+        h.e24 = (h.l4d.x & L4_PTR) ? 300u : h.l4d.x;
+#else
         h.e24 = l4_lookup(T, h.lh, h.l4d);
+#endif
     } else {
         if (h.e24 & LPM_GROUP)
             h.e24 = T.tbl8[((h.e24 & ~LPM_GROUP) << 8) | (h.lh & 0xFF)];
@@ -256,7 +260,11 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     h.rec = make_uint4(0, 0, 0, 0);
     uint4 srec = h.rec;
     if (T.lxc4) {
+#if CFC_EXP == 7
+        h.rec = h.lx;
+#else
         h.rec = lxc_resolve(T, S, h.da, h.lxs, h.lx);
+#endif
         if (EGR)
             srec = lxc_resolve(T, S, h.sa, h.lss, h.ls);
     }
@@ -675,7 +683,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             }
             if (MODE != CFC_MODE_XDP && h[u].valid && h[u].id_ovf && h[u].need_pol)
                 id_count(C, id_dir, h[u].ident, h[u].drop1, len);
+#if CFC_EXP != 5
             acc.add(h[u].valid ? h[u].met0 : NONE, len);
+#endif
             if (EGR) {
                 acc.add(h[u].valid ? h[u].met1 : NONE, len);
                 acc.add(h[u].valid && h[u].ev2 ? met_n<MODE>() + h[u].ev2 - 1 : NONE, len);

@@ -6,6 +6,7 @@
 
 namespace cfc {
 
+static constexpr uint64_t POL_SLOTS_PER_KEY = 4;
 static uint32_t pow2_at_least(uint64_t x)
 {
     uint32_t p = 1;
@@ -716,9 +717,10 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
     }
 
     // ---- policy tables (deterministic: ascending lxc id, key order);
-    //      linear probing over 16-byte slots at load factor <= 50% (the
-    //      Bloom filter screens out most lookups of absent keys, so probe
-    //      sequences mostly end in a hit)
+    //      linear probing over 16-byte slots at load factor <= 25%: a hit is
+    //      one 16-byte load 5 times in 6 (at 50% it was every other hit that
+    //      needed a second, dependent, L2 round trip); the Bloom filter
+    //      screens out most lookups of absent keys
     size_t n_pol_keys = 0;
     for (auto &pm : pols)
         n_pol_keys += pm.second->kv.size();
@@ -731,7 +733,7 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         uint32_t n = 0;
         for (const auto &kv : m->kv)
             n += ((uint8_t)kv.first[7] & 0xFE) == 0;
-        uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 2ull * n));
+        uint32_t ns = pow2_at_least(std::max<uint64_t>(8, POL_SLOTS_PER_KEY * n));
         loc.base = (uint32_t)img->pol.size();
         loc.mask = ns - 1;
         PolSlot empty{};

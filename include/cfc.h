@@ -140,8 +140,17 @@ int cfc_get_node_config(cfc_ctx *ctx, cfc_node_config *cfg);
  * CT-apply call made after it returns.  A new context starts at 0. */
 int cfc_set_clock(cfc_ctx *ctx, uint32_t now_sec);
 
-/* Flatten the host tables into device layouts and publish them as the new
- * epoch.  Enqueued on `stream` (hipStream_t, NULL = default stream). */
+/* Publish the maps' changes to the device (the first classify after a
+ * change commits by itself).  The device tables form five groups —
+ * ipcache IPv4, ipcache IPv6, prefilter, endpoints + policymaps, conntrack —
+ * and a commit re-flattens only the groups whose maps changed.  A value
+ * overwritten in place (an existing IPv6 ipcache prefix's identity, an
+ * existing policy entry's proxy port) is patched into the live tables
+ * instead, as a BPF map update is visible to the next packet.  The new
+ * tables are uploaded on `stream` (hipStream_t, NULL = default stream);
+ * launches already queued on other streams keep the tables they were
+ * launched with, which stay allocated until those streams pass the commit
+ * (no device-wide drain). */
 int cfc_commit(cfc_ctx *ctx, void *stream);
 
 /* ----------------------------------------------------------------- options */
