@@ -14,7 +14,8 @@ CFC_DEVICE_NONE = -1
 MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
 HF_FRAG, HF_TCP_CLOSE, HF_EXTHDR = 0x100, 0x200, 0x400
 DROP_PREFILTER, VERDICT_PUNT = -1, -2
-OPT_LPM4, OPT_TIMING = 1, 2
+OPT_LPM4, OPT_TIMING, OPT_CT_APPLY = 1, 2, 3
+CT_APPLY_DEVICE, CT_APPLY_HOST = 0, 1
 LPM4_AUTO, LPM4_DIR24_8, LPM4_TRIE = 0, 1, 2
 
 # every symbol include/cfc.h declares

@@ -44,6 +44,19 @@ struct DevBuf {
         bytes = n;
         return hipMemsetAsync(p, 0, n, s) == hipSuccess ? 0 : -EIO;
     }
+    // at least n bytes (contents not kept)
+    int ensure(size_t n)
+    {
+        if (bytes >= n && p)
+            return 0;
+        reset();
+        if (hipMalloc(&p, std::max<size_t>(n, 256)) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        bytes = std::max<size_t>(n, 256);
+        return 0;
+    }
     int upload(const void *src, size_t n, hipStream_t s)
     {
         reset();
@@ -104,11 +117,13 @@ struct GEp {           // endpoints + policy (+ the counter layout)
 };
 struct GCt {           // conntrack
     DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
+    DevBuf ct4_info, ct4_mark, ct4_sum;   // device CT apply state (ctapply.hip)
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
     std::vector<Ct6Slot> ct6_host;
     std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
     uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
     uint32_t n_ct4 = 0, n_ct6 = 0;
+    uint32_t tomb4 = 0, tomb6 = 0;       // deleted slots (CT_TOMBSTONE)
     uint64_t bytes = 0;
 };
 struct Epoch {
@@ -151,6 +166,17 @@ struct cfc_ctx {
     uint32_t id_cover = 1;   // identity histogram ranges (reserved + ipcache)
     std::vector<Retired> retired;
     std::vector<hipStream_t> streams;   // streams launched on since the last swap
+    // in-place patch records of the last commit (patch_ct)
+    std::vector<Patch16> patch_host;
+    DevBuf patch_dev;
+    // device CT apply (ctapply.hip): the host mirror of the CT maps lags
+    // the device table until ct_sync
+    int ct_apply_mode = CFC_CT_APPLY_DEVICE;
+    bool ct_dirty = false;
+    uint64_t cta_claims = 0;     // device inserts since the last sync
+    uint32_t cta_seq = 0;
+    uint64_t log_used = 0;       // CtLog entries since the last sync
+    DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
 
     // counters: [n_ctr][2] u64 then metrics
     uint64_t *ctr = nullptr;
@@ -208,7 +234,9 @@ void group_sigs(cfc_ctx *c, uint64_t sig[NGROUPS])
             mix(2, id); mix(2, m->sgen[0]);
             break;
         case ROLE_CT4: case ROLE_CT6:
-            mix(3, id); mix(3, m->gen); mix(3, m->kv.size());
+            // inserts, deletes and value changes are patched in place
+            // (patch_ct); the table is rebuilt when it fills up
+            mix(3, id); mix(3, m->sgen[0]);
             mix(2, id);   // endpoints see which CT maps exist
             break;
         default:
@@ -233,10 +261,150 @@ Map *ct_slot_key(const Epoch &E, int family, const uint32_t *d, const uint32_t *
     return it == E.ct->ct_maps.end() ? nullptr : it->second;
 }
 
+// struct ct_entry fields the device keeps (CtTimer, CtInfo) into a value:
+// lifetime @32, bits @36 (rx/tx_closing, seen_non_syn; others kept),
+// rev_nat_index @38, tx/rx_flags_seen @42/43, src_sec_id @44, last_tx/rx
+// @48/52
+void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
+{
+    uint16_t bits = 0;
+    if (!created)
+        memcpy(&bits, &v[36], 2);
+    bits = (uint16_t)((bits & ~(1u | 2u | 16u)) | ((r.flags >> 16) & 3) |
+                      ((r.flags & CTT_NON_SYN) ? 16u : 0u));
+    memcpy(&v[32], &r.lifetime, 4);
+    memcpy(&v[36], &bits, 2);
+    v[42] = (char)((r.flags >> 8) & 0xFF);
+    v[43] = (char)(r.flags & 0xFF);
+    memcpy(&v[48], &r.last_tx, 4);
+    memcpy(&v[52], &r.last_rx, 4);
+    if (created) {
+        const uint16_t rev = (uint16_t)(r.info.y & 0xFFFF);
+        memcpy(&v[38], &rev, 2);
+        memcpy(&v[44], &r.info.sec, 4);
+    }
+}
+
+// The device CT apply's changes into the host mirror of the CT maps: the
+// slots with CtInfo dirty bits (created, updated, deleted) compacted on the
+// device, then the TCP maps' ICMP entries of its creates (CtLog) in batch and
+// header order.  Runs before anything reads or writes a CT map on the host.
+int ct_sync(cfc_ctx *c, hipStream_t s)
+{
+    if (!c->ct_dirty || !c->epoch)
+        return 0;
+    Epoch &E = *c->epoch;
+    GCt &G = *E.ct;
+    const uint64_t slots = G.ct4_host.size();
+    uint32_t n = 0;
+    if (c->cta_cnt.ensure(4 * CTA_NCNT))
+        return -ENOMEM;
+    uint32_t *cnt = (uint32_t *)c->cta_cnt.p;
+    Ct4Slot *ct4 = (Ct4Slot *)G.ct4.p;
+    CtTimer *tm = (CtTimer *)G.ct4_tm.p;
+    CtInfo *info = (CtInfo *)G.ct4_info.p;
+    if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+        cta_collect(ct4, tm, info, slots, nullptr, 0, cnt, s) ||
+        hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    std::vector<CtSyncRec> rec(n);
+    if (n) {
+        if (c->cta_sync.ensure(sizeof(CtSyncRec) * n))
+            return -ENOMEM;
+        CtSyncRec *dr = (CtSyncRec *)c->cta_sync.p;
+        uint32_t n2 = 0;
+        if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+            cta_collect(ct4, tm, info, slots, dr, n, cnt, s) ||
+            hipMemcpyAsync(rec.data(), dr, sizeof(CtSyncRec) * n, hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipMemcpyAsync(&n2, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            cta_tomb(ct4, dr, n, s) || hipStreamSynchronize(s) != hipSuccess || n2 != n)
+            return -EIO;
+    }
+    std::string key;
+    for (const CtSyncRec &r : rec) {
+        const bool del = (r.w & CT_TOMBSTONE) == CT_TOMBSTONE;
+        const uint32_t w = r.w & ~CT_TOMBSTONE;
+        Ct4Slot &h = G.ct4_host[r.slot];
+        const bool prev_live = h.w != 0 && h.w != CT_TOMBSTONE;
+        Map *m = ct_slot_key(E, 4, &r.x, &r.y, r.z, w, &key);
+        if (del) {
+            if (m)
+                m->erase_raw(key);
+            if (prev_live) {
+                G.n_ct4--;
+                G.tomb4++;
+            } else if (h.w == 0) {
+                G.tomb4++;
+            }
+            h = Ct4Slot{0, 0, 0, CT_TOMBSTONE};
+        } else if (r.info.y & CTI_CREATED) {
+            if (m) {
+                std::string v(m->value_bytes(), '\0');
+                ct_value_from_dev(v, r, true);
+                m->put_raw(key, v);
+            }
+            if (!prev_live) {
+                G.n_ct4++;
+                if (h.w == CT_TOMBSTONE)
+                    G.tomb4--;
+            }
+            h = Ct4Slot{r.x, r.y, r.z, w};
+        } else if (m) {
+            auto it = m->kv.find(key);
+            if (it != m->kv.end() && it->second.val.size() >= 56)
+                ct_value_from_dev(it->second.val, r, false);
+        }
+    }
+    if (c->log_used) {
+        std::vector<CtLog> lg(c->log_used);
+        if (hipMemcpyAsync(lg.data(), c->cta_log.p, sizeof(CtLog) * lg.size(),
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        std::sort(lg.begin(), lg.end(), [](const CtLog &a, const CtLog &b) {
+            return a.seq != b.seq ? a.seq < b.seq : a.order < b.order;
+        });
+        for (const CtLog &g : lg) {
+            // ct_create4's second write into the TCP map (conntrack.h:741-760)
+            auto it = G.ct_maps.find(ct_map_key(4, g.w & ~0x7FFu, 0));
+            if (it == G.ct_maps.end())
+                continue;
+            char k[14];
+            const uint32_t z = 0;
+            memcpy(k, &g.x, 4);
+            memcpy(k + 4, &g.y, 4);
+            memcpy(k + 8, &z, 4);
+            k[12] = (char)(g.w & 0xFF);
+            k[13] = (char)((g.w >> 8) & 7);
+            std::string v(it->second->value_bytes(), '\0');
+            const uint32_t dir = g.dirlen >> 31;
+            const uint64_t one = 1, len = g.dirlen & 0x7FFFFFFFu;
+            memcpy(&v[dir ? 0 : 16], &one, 8);
+            memcpy(&v[dir ? 8 : 24], &len, 8);
+            const uint32_t life = g.now + 60, last = 5u < g.now ? g.now : 0u;
+            const uint16_t bits = 16;   // seen_non_syn: "for ICMP, there is no SYN"
+            memcpy(&v[32], &life, 4);
+            memcpy(&v[36], &bits, 2);
+            memcpy(&v[44], &g.sec, 4);
+            memcpy(&v[dir ? 52 : 48], &last, 4);
+            it->second->put_raw(std::string(k, 14), v);
+        }
+    }
+    c->log_used = 0;
+    c->cta_claims = 0;
+    c->ct_dirty = false;
+    E.st.ct4_entries = G.n_ct4;
+    return 0;
+}
+
 // CONNTRACK_ACCOUNTING counts of the device into the CT entries' rx/tx
 // packets and bytes (struct ct_entry offsets 0-31)
 int fold_ct(cfc_ctx *c, hipStream_t s)
 {
+    if (int rc = ct_sync(c, s))
+        return rc;
     Epoch &E = *c->epoch;
     const size_t n4 = E.ct->ct4_host.size(), n = n4 + E.ct->ct6_host.size();
     if (!n)
@@ -522,6 +690,10 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     const size_t nslots = img.ct4.size() + img.ct6.size();
     if (nslots && (*rc = g->ct_acct.zeros(32 * nslots, s)))
         return nullptr;
+    const size_t n4 = img.ct4.size();
+    if (n4 && ((*rc = g->ct4_info.zeros(sizeof(CtInfo) * n4, s)) ||
+               (*rc = g->ct4_mark.zeros(n4, s)) || (*rc = g->ct4_sum.zeros(4 * n4, s))))
+        return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
             g->ct_maps[ct_map_key(m->role == ROLE_CT4 ? 4 : 6,
@@ -535,7 +707,7 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     g->n_ct4 = img.n_ct4;
     g->n_ct6 = img.n_ct6;
     g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
-               48ull * nslots;
+               48ull * nslots + 13ull * n4;
     g->ct4_host = std::move(img.ct4);
     g->ct6_host = std::move(img.ct6);
     return g;
@@ -583,7 +755,8 @@ void assemble(Epoch &E)
     T.ct4_tm = (const CtTimer *)C.ct4_tm.p;
     T.ct6_tm = (const CtTimer *)C.ct6_tm.p;
     T.ct4_mask = C.ct4_mask;
-    T.ct4_probe = C.ct4_probe;
+    // the device CT apply inserts in place: lookups walk to a free slot
+    T.ct4_probe = C.ct4_mask;
     T.ct6_mask = C.ct6_mask;
     T.ct6_probe = C.ct6_probe;
     T.ct6_acct_base = (uint32_t)C.ct4_host.size();
@@ -619,6 +792,8 @@ void assemble(Epoch &E)
 // BPF program racing a map update does): IPv6 ipcache labels, policy
 // entries' proxy ports.  IPv4 ipcache labels rebuild that (small) group.
 // Returns the groups that still need a rebuild.
+bool patch_ct(cfc_ctx *c, hipStream_t s);
+
 unsigned patch_touched(cfc_ctx *c, unsigned groups, hipStream_t s)
 {
     Epoch &E = *c->epoch;
@@ -681,7 +856,173 @@ unsigned patch_touched(cfc_ctx *c, unsigned groups, hipStream_t s)
             }
         }
     }
+    bool ct = false;
+    for (auto &kv : c->maps)
+        ct |= kv.second->ct() && !kv.second->touched.empty();
+    if (ct && !(groups & GROUP_CT)) {
+        if (!patch_ct(c, s)) {
+            groups |= GROUP_CT;
+        } else {
+            const GCt &G = *E.ct;
+            E.T.ct6_probe = G.ct6_probe;
+            E.st.ct4_entries = G.n_ct4;
+            E.st.ct6_entries = G.n_ct6;
+        }
+    }
     return groups;
+}
+
+// CT inserts, deletes and value changes since the last commit (the CT maps'
+// touched journal) patched into the live CT table: a new entry takes the
+// first free or deleted slot of its probe sequence, a deleted one becomes
+// CT_TOMBSTONE, a changed value rewrites the slot's report state (CtTimer);
+// the accounting of a replaced slot restarts from zero.  The records go up
+// in one upload and one scatter launch (k_patch16).  False, with nothing
+// changed, when the table would pass 3/4 load (or lacks the family): the
+// group is rebuilt instead.
+bool patch_ct(cfc_ctx *c, hipStream_t s)
+{
+    GCt &G = *c->epoch->ct;
+    uint64_t ins[2] = {0, 0}, any[2] = {0, 0};
+    for (auto &kv : c->maps) {
+        const Map *m = kv.second.get();
+        if (!m->ct())
+            continue;
+        const int f = m->role == ROLE_CT6;
+        for (auto &t : m->touched) {
+            any[f]++;
+            ins[f] += (t.second & TOUCH_INSERT) ? 1 : 0;
+        }
+    }
+    const uint64_t size[2] = {G.ct4_host.size(), G.ct6_host.size()};
+    const uint64_t used[2] = {(uint64_t)G.n_ct4 + G.tomb4, (uint64_t)G.n_ct6 + G.tomb6};
+    for (int f = 0; f < 2; f++)
+        if (any[f] && (!size[f] || 4 * (used[f] + ins[f]) > 3 * size[f]))
+            return false;
+    std::unordered_map<uint64_t, size_t> at_addr;
+    std::vector<Patch16> &rec = c->patch_host;
+    rec.clear();
+    auto put = [&](const void *dst, const void *val) {
+        Patch16 p{};
+        memcpy(p.val, val, 16);
+        p.dst = (uint64_t)(uintptr_t)dst;
+        auto r = at_addr.emplace(p.dst, rec.size());
+        if (r.second)
+            rec.push_back(p);
+        else
+            rec[r.first->second] = p;
+    };
+    static const uint32_t zero[4] = {0, 0, 0, 0};
+    auto zero_acct = [&](uint64_t slot) {
+        char *a = (char *)G.ct_acct.p + 32 * slot;
+        put(a, zero);
+        put(a + 16, zero);
+    };
+    for (auto &kv : c->maps) {
+        Map *m = kv.second.get();
+        if (!m->ct() || m->touched.empty())
+            continue;
+        const bool v6 = m->role == ROLE_CT6;
+        for (auto &t : m->touched) {
+            Ct4Slot k4;
+            Ct6Slot k6;
+            if (!ct_slot_of(m, t.first, &k4, &k6))
+                continue;   // no lookup reaches it: not in the device table
+            auto it = m->kv.find(t.first);
+            const bool present = it != m->kv.end();
+            // the key's slot, else the first free or deleted one
+            const uint32_t mask = (uint32_t)size[v6] - 1;
+            int64_t at = -1, slot = -1;
+            uint32_t p = 0, pfree = 0;
+            uint32_t i = v6 ? ct_hash6(k6.d, k6.s, k6.z, k6.w) & mask
+                            : ct_hash4(k4.x, k4.y, k4.z, k4.w) & mask;
+            for (;; i = (i + 1) & mask, p++) {
+                const uint32_t w = v6 ? G.ct6_host[i].w : G.ct4_host[i].w;
+                if (w == 0 || w == CT_TOMBSTONE) {
+                    if (slot < 0) {
+                        slot = i;
+                        pfree = p;
+                    }
+                    if (w == 0)
+                        break;
+                    continue;
+                }
+                const bool eq = v6 ? (G.ct6_host[i].z == k6.z && w == k6.w &&
+                                      !memcmp(G.ct6_host[i].d, k6.d, 16) &&
+                                      !memcmp(G.ct6_host[i].s, k6.s, 16))
+                                   : (G.ct4_host[i].x == k4.x && G.ct4_host[i].y == k4.y &&
+                                      G.ct4_host[i].z == k4.z && w == k4.w);
+                if (eq) {
+                    at = i;
+                    break;
+                }
+            }
+            const uint64_t acct = v6 ? size[0] + (uint64_t)(at >= 0 ? at : slot)
+                                     : (uint64_t)(at >= 0 ? at : slot);
+            CtTimer *tm = (CtTimer *)(v6 ? G.ct6_tm.p : G.ct4_tm.p);
+            if (present) {
+                const CtTimer v = ct_timer_of(it->second.val);
+                if (at < 0) {   // insert
+                    at = slot;
+                    if (v6) {
+                        const bool tomb = G.ct6_host[at].w == CT_TOMBSTONE;
+                        G.tomb6 -= tomb;
+                        G.n_ct6++;
+                        G.ct6_host[at] = k6;
+                        G.ct6_probe = std::max(G.ct6_probe, pfree);
+                        const uint32_t *w = (const uint32_t *)&k6;
+                        char *d = (char *)G.ct6.p + sizeof(Ct6Slot) * at;
+                        put(d, w);
+                        put(d + 16, w + 4);
+                        put(d + 32, w + 8);
+                    } else {
+                        const bool tomb = G.ct4_host[at].w == CT_TOMBSTONE;
+                        G.tomb4 -= tomb;
+                        G.n_ct4++;
+                        G.ct4_host[at] = k4;
+                        G.ct4_probe = std::max(G.ct4_probe, pfree);
+                        put((char *)G.ct4.p + sizeof(Ct4Slot) * at, &k4);
+                    }
+                    zero_acct(acct);
+                } else if (t.second & (TOUCH_INSERT | TOUCH_ERASE)) {
+                    zero_acct(acct);   // deleted and created again
+                }
+                put(tm + at, &v);
+            } else if (at >= 0) {       // delete
+                if (v6) {
+                    Ct6Slot d{};
+                    d.w = CT_TOMBSTONE;
+                    G.ct6_host[at] = d;
+                    G.n_ct6--;
+                    G.tomb6++;
+                    const uint32_t *w = (const uint32_t *)&d;
+                    char *dst = (char *)G.ct6.p + sizeof(Ct6Slot) * at;
+                    put(dst + 32, w + 8);   // z, w: probes compare these first
+                } else {
+                    const Ct4Slot d{0, 0, 0, CT_TOMBSTONE};
+                    G.ct4_host[at] = d;
+                    G.n_ct4--;
+                    G.tomb4++;
+                    put((char *)G.ct4.p + sizeof(Ct4Slot) * at, &d);
+                }
+                zero_acct(acct);
+            }
+        }
+    }
+    if (rec.empty())
+        return true;
+    const size_t bytes = rec.size() * sizeof(Patch16);
+    if (c->patch_dev.bytes < bytes) {
+        if (c->patch_dev.p)
+            (void)hipStreamSynchronize(s);
+        if (c->patch_dev.zeros(std::max(bytes, (size_t)1 << 20), s))
+            return false;
+    }
+    if (hipMemcpyAsync(c->patch_dev.p, rec.data(), bytes, hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        launch_patch16((const Patch16 *)c->patch_dev.p, rec.size(), s))
+        return false;
+    return true;
 }
 
 int commit_locked(cfc_ctx *c, hipStream_t s)
@@ -696,10 +1037,15 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
             groups |= 1u << g;
     for (auto &kv : c->maps)
         touched |= !kv.second->touched.empty() &&
-                   (kv.second->role == ROLE_IPCACHE || kv.second->role == ROLE_POLICY);
+                   (kv.second->role == ROLE_IPCACHE || kv.second->role == ROLE_POLICY ||
+                    kv.second->ct());
     if (!groups && !touched)
         return 0;
     int rc;
+    // host-side CT changes or a CT rebuild: take the device's first
+    if ((groups & GROUP_CT) || touched)
+        if ((rc = ct_sync(c, s)))
+            return rc;
     if (c->epoch && touched) {
         groups = patch_touched(c, groups, s);
         c->id_cover |= identity_cover_touched(c);
@@ -810,6 +1156,9 @@ bool role_geometry_ok(Role r, uint32_t type, uint32_t ks, uint32_t vs)
 // classified before it (the kernel bumps them in place in the reference)
 int before_counter_write(cfc_ctx *c, Map *m)
 {
+    if (m->ct())
+        if (int rc = ct_sync(c, c->last_stream))
+            return rc;
     if (m->role == ROLE_POLICY || m->role == ROLE_METRICS || m->role == ROLE_CT4 ||
         m->role == ROLE_CT6)
         return fold_counters(c, c->last_stream);
@@ -927,6 +1276,11 @@ int cfc_set_option(cfc_ctx *c, int option, int64_t value)
         if (c->device == CFC_DEVICE_NONE)
             return -ENODEV;
         c->timing = value != 0;
+        return 0;
+    case CFC_OPT_CT_APPLY:
+        if (value != CFC_CT_APPLY_DEVICE && value != CFC_CT_APPLY_HOST)
+            return -EINVAL;
+        c->ct_apply_mode = (int)value;
         return 0;
     default:
         return -EINVAL;
@@ -1060,6 +1414,9 @@ int cfc_map_lookup(cfc_ctx *c, int fd, const void *key, void *value)
         return -EINVAL;
     std::lock_guard<std::recursive_mutex> g(c->mu);
     Map *m = get_map(c, fd);
+    if (m && m->ct())
+        if (int rc = ct_sync(c, c->last_stream))
+            return rc;
     return m ? m->lookup(key, value) : -EBADF;
 }
 
@@ -1081,6 +1438,9 @@ int cfc_map_get_next_key(cfc_ctx *c, int fd, const void *key, void *next)
         return -EINVAL;
     std::lock_guard<std::recursive_mutex> g(c->mu);
     Map *m = get_map(c, fd);
+    if (m && m->ct())
+        if (int rc = ct_sync(c, c->last_stream))
+            return rc;
     return m ? m->next_key(key, next) : -EBADF;
 }
 
@@ -1093,6 +1453,9 @@ int cfc_map_dump(cfc_ctx *c, int fd, void *keys, void *values, uint64_t cap,
     Map *m = get_map(c, fd);
     if (!m)
         return -EBADF;
+    if (m->ct())
+        if (int rc = ct_sync(c, c->last_stream))
+            return rc;
     const size_t vb = m->value_bytes();
     uint64_t k = 0;
     for (const auto &kv : m->kv) {
@@ -1601,6 +1964,7 @@ void ct_hit_update(Map *m, Map::Entry &me, int action, int dir, bool count,
             ct_upd(e, now, CT_CLOSE_TIMEOUT, dir, flags);
     }
     memcpy(&me.val[0], &e, sizeof(e));
+    m->touched[me.key] |= TOUCH_VALUE;
     m->gen++;
 }
 
@@ -1661,6 +2025,135 @@ void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t 
         (void)hipMemsetAsync((char *)c->epoch->ct->ct_acct.p + 32 * slot, 0, 32, s);
 }
 
+// cfc_ct_apply_v4 on the device (ctapply.hip).  1: take the host path
+// instead (nothing changed), 0 done, <0 error.
+int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
+                 uint16_t ep_lxc, hipStream_t s)
+{
+    if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
+        return 1;
+    // the device table must be the maps as committed: no host-side CT
+    // change waiting for a commit
+    uint64_t sig[NGROUPS];
+    group_sigs(c, sig);
+    if (sig[3] != c->built_sig[3])
+        return 1;
+    bool local_ep = false;
+    for (auto &kv : c->maps) {
+        const Map *m = kv.second.get();
+        if (m->ct() && !m->touched.empty())
+            return 1;
+        local_ep |= m->ct() && m->policy_lxc == (int)ep_lxc;
+    }
+    Epoch &E = *c->epoch;
+    GCt &G = *E.ct;
+    const uint64_t n = in->n, slots = G.ct4_host.size();
+    if (!slots || !G.ct4_info.p || n >= (1ull << 29))
+        return 1;
+    int ob = 2, sb = 1;
+    while ((1ull << ob) < 4 * n)
+        ob++;
+    while ((1ull << sb) < slots)
+        sb++;
+    if (ob + sb > 64)
+        return 1;
+    if (c->cta_hs.ensure(8 * n) || c->cta_req.ensure(16 * n) ||
+        c->cta_cnt.ensure(4 * CTA_NCNT))
+        return -ENOMEM;
+    CtaArgs A{};
+    A.T = E.T;
+    A.sa = in->saddr;
+    A.da = in->daddr;
+    A.pt = in->ports;
+    A.mt = in->meta;
+    A.tf = in->tcp_flags;
+    A.ctb = out->ct;
+    A.ver = out->verdict;
+    A.ident = (const uint32_t *)out->identity;
+    A.n = n;
+    A.mode = mode;
+    A.ep_owner = mode == CFC_MODE_EGRESS ? ct_owner_word(ep_lxc, local_ep) : 0u;
+    A.ep_sec = c->seclabel[ep_lxc];
+    A.now = c->now;
+    A.seq = c->cta_seq;
+    A.ct4 = (Ct4Slot *)G.ct4.p;
+    A.tm = (CtTimer *)G.ct4_tm.p;
+    A.info = (CtInfo *)G.ct4_info.p;
+    A.mark = (uint8_t *)G.ct4_mark.p;
+    A.sum = (uint32_t *)G.ct4_sum.p;
+    A.hs = (uint32_t *)c->cta_hs.p;
+    A.reqA = (uint64_t *)c->cta_req.p;
+    A.req_cap = (uint32_t)std::min<uint64_t>(2 * n, 0xFFFFFFFFu);
+    A.cnt = (uint32_t *)c->cta_cnt.p;
+    A.ob = ob;
+    A.slot_bits = sb;
+    uint32_t hc[CTA_NCNT];
+    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess || cta_scan(A, s) ||
+        hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    const uint64_t nreqA = hc[CTA_NREQA], nhit = hc[CTA_NHIT];
+    // room for every create and its ICMP entry: the table below 3/4 load,
+    // each CT map below max_entries; else the host path (which rebuilds)
+    bool ok = 4 * (G.n_ct4 + G.tomb4 + c->cta_claims + 2 * nreqA) <= 3 * slots &&
+              nreqA <= A.req_cap;
+    for (auto &kv : c->maps) {
+        const Map *m = kv.second.get();
+        if (m->role == ROLE_CT4 &&
+            m->kv.size() + c->cta_claims + c->log_used + 2 * nreqA > m->max_entries)
+            ok = false;
+    }
+    if (!ok) {   // the scan's marks go
+        if (hipMemsetAsync(A.mark, 0, slots, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        return 1;
+    }
+    const uint64_t nr = std::max<uint64_t>(nreqA, 1);
+    const uint64_t cx_cap = nhit + 2 * nreqA + 64;
+    const uint64_t log_need = c->log_used + nreqA;
+    if (cx_cap > 0xFFFFFFFFu)
+        return 1;
+    if (c->cta_req2.ensure(24 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
+        c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)std::max<uint64_t>(cx_cap, nr))))
+        return -ENOMEM;
+    if (c->cta_log.bytes < sizeof(CtLog) * log_need) {   // grow, keeping the entries
+        DevBuf nl;
+        if (nl.ensure(sizeof(CtLog) * std::max<uint64_t>(2 * log_need, 1 << 16)))
+            return -ENOMEM;
+        if (c->log_used && (hipMemcpyAsync(nl.p, c->cta_log.p, sizeof(CtLog) * c->log_used,
+                                           hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                            hipStreamSynchronize(s) != hipSuccess))
+            return -EIO;
+        std::swap(nl.p, c->cta_log.p);
+        std::swap(nl.bytes, c->cta_log.bytes);
+    }
+    uint64_t *r2 = (uint64_t *)c->cta_req2.p, *cx = (uint64_t *)c->cta_cx.p;
+    A.reqA2 = r2;
+    A.reqB = r2 + nr;
+    A.reqB2 = r2 + 2 * nr;
+    A.req_cap = (uint32_t)nr;
+    A.cx = cx;
+    A.cx2 = cx + cx_cap;
+    A.cx_cap = (uint32_t)cx_cap;
+    A.log = (CtLog *)c->cta_log.p;
+    A.log_base = (uint32_t)c->log_used;
+    A.log_cap = (uint32_t)(c->cta_log.bytes / sizeof(CtLog) - c->log_used);
+    A.sort_tmp = c->cta_tmp.p;
+    A.sort_tmp_bytes = c->cta_tmp.bytes;
+    // from here the device table changes: the host mirror lags until ct_sync
+    c->ct_dirty = true;
+    int rc = cta_rest(A, (uint32_t)nreqA, hc, s);
+    if (rc)
+        return rc;
+    if (hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    c->cta_claims += hc[CTA_CLAIMS];
+    c->log_used += hc[CTA_NLOG];
+    c->cta_seq++;
+    return 0;
+}
+
 template <class Hdr>
 int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode,
              uint16_t ep_lxc, void *stream)
@@ -1677,6 +2170,13 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     if (!n || mode == CFC_MODE_XDP)
         return 0;
     hipStream_t s = (hipStream_t)stream;
+    if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value) {
+        const int rc = ct_apply_dev(c, in, out, mode, ep_lxc, s);
+        if (rc <= 0)
+            return rc;
+    }
+    if (int rc = ct_sync(c, s))
+        return rc;
     const size_t al = family == 4 ? 4 : 16;
     std::vector<uint8_t> sa(al * n), da(al * n), ct(n), tf(n, 0);
     std::vector<uint32_t> pt(n), mt(n), ident(n);

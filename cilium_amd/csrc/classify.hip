@@ -1148,6 +1148,15 @@ __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
         dst[i] += src[i];
 }
 
+__global__ __launch_bounds__(256) void k_patch16(const Patch16 *rec, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const uint4 v = *(const uint4 *)rec[i].val;
+        *(uint4 *)rec[i].dst = v;
+    }
+}
+
 template <int MODE, bool CT, bool NT>
 void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                     const EgressArgs &E, const CountArgs &C, uint32_t grid,
@@ -1220,6 +1229,14 @@ void set_lds_limit(const void *kernel, int bytes)
 }
 
 size_t classify_lds_bytes(const DevTables &T) { return lds_plan(T).bytes(); }
+
+int launch_patch16(const Patch16 *rec, uint64_t n, hipStream_t s)
+{
+    if (!n)
+        return 0;
+    hipLaunchKernelGGL(k_patch16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, n);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
 
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
                    hipStream_t s)

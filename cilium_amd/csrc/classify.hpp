@@ -97,6 +97,66 @@ CountArgs count_args(uint32_t *ws, const WsLayout &w, const DevTables &T,
 // LDS image of the classify kernel for these tables (must be <= 160 KiB).
 size_t classify_lds_bytes(const DevTables &T);
 
+// In-place table patches (cfc_commit): each record's 16 bytes stored at its
+// device address, one record per address
+struct alignas(16) Patch16 {
+    uint32_t val[4];
+    uint64_t dst;
+    uint64_t pad;
+};
+int launch_patch16(const Patch16 *rec, uint64_t n, hipStream_t stream);
+
+// ---- device CT apply (ctapply.hip)
+// ct_create4's ICMP entry for a TCP map: not in the device table, replayed
+// into the host map in (seq, order) order at the next synchronisation
+struct CtLog {
+    uint32_t x, y, w;     // key: saddr, daddr (k2 order), ct_word
+    uint32_t now;         // the batch clock of the create
+    uint32_t dirlen;      // dir << 31 | len
+    uint32_t sec;         // src_sec_id
+    uint32_t seq, order;  // apply sequence, header order
+};
+// one changed slot for the host mirror
+struct CtSyncRec {
+    uint32_t slot;
+    CtInfo info;
+    uint32_t x, y, z, w;
+    uint32_t last_rx, last_tx, flags, lifetime;
+    uint32_t pad;
+};
+enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NCNT = 8 };
+struct CtaArgs {
+    DevTables T;
+    const uint32_t *sa, *da, *pt, *mt;
+    const uint8_t *tf;           // may be null
+    const uint8_t *ctb;
+    const int32_t *ver;
+    const uint32_t *ident;
+    uint64_t n;
+    int mode;
+    uint32_t ep_owner, ep_sec, now, seq;
+    Ct4Slot *ct4;
+    CtTimer *tm;
+    CtInfo *info;
+    uint8_t *mark;
+    uint32_t *sum;
+    uint32_t *hs;                // [2n] hit slot per header and stage
+    uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
+    uint32_t req_cap, cx_cap;
+    CtLog *log;
+    uint32_t log_base, log_cap;  // entries before this apply, capacity left
+    uint32_t *cnt;               // CTA_* counters
+    void *sort_tmp;
+    size_t sort_tmp_bytes;
+    int ob, slot_bits;           // sort keys: slot << ob | order
+};
+size_t cta_sort_tmp_bytes(uint32_t n);
+int cta_scan(const CtaArgs &A, hipStream_t s);
+int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s);
+int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec *out,
+                uint32_t cap, uint32_t *cnt, hipStream_t s);
+int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
+
 // dst[i] += src[i] for n u64 (counter import)
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
                    hipStream_t stream);

@@ -1,0 +1,653 @@
+// Device CT apply (cfc_ct_apply_v4): the conntrack writes of one classified
+// IPv4 batch, applied in header order to the device CT table in place —
+// what __ct_lookup (conntrack.h:221-285), ct_create4 (:691-772) and
+// ct_delete4 do to the CT maps while the reference runs the batch one packet
+// at a time, restated for a whole batch:
+//
+//   scan     per header and CT stage: the op (hit, hit + delete, create),
+//            the hit's slot; slots whose ops depend on their order (closing
+//            bits, RST/FIN, deletes) are marked "ordered"; creates become
+//            requests keyed by their home slot
+//   insert   requests sorted by (home slot, header order); one thread per
+//            home slot dedups the keys, inserts each new one into the table
+//            (CAS on the slot's w word), and the first request of a key
+//            creates it: its ICMP "related" entry (ct_create4's second
+//            write) is a second round of requests
+//   route    hits on unordered slots fold into a per-slot summary with
+//            atomicOr (their result does not depend on order, see
+//            k_cta_finish); every other op goes to the ordered list
+//   fold     the ordered list sorted by (slot, header order), one thread per
+//            slot replays its ops in order (cfc_api.cpp ct_hit_update /
+//            the oracle's ct_apply pass 2)
+//   finish   the summaries become the slots' new state
+//
+// The table stays the truth until the host reads a CT map: every changed
+// slot carries CtInfo dirty bits, and cta_collect() compacts them for the
+// host mirror (cfc_api.cpp ct_sync).  ICMP entries ct_create4 writes into a
+// TCP map are not in the device table (no lookup reaches them, flatten.cpp
+// build_ct): they go to a log the host replays in order.
+#include <hipcub/hipcub.hpp>
+
+#include "kern_common.hpp"
+
+namespace cfc {
+
+namespace {
+
+constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,
+                   CT_CLOSE_TIMEOUT = 10, CT_REPORT_INTERVAL = 5;
+constexpr uint32_t RX_CLOSING = 1, TX_CLOSING = 2, SEEN_NON_SYN = 16;   // ct_entry bits
+constexpr uint32_t OP_NONE = 0, OP_HIT = 1, OP_DELETE = 2, OP_CREATE = 3;
+constexpr uint8_t MARK_ORDERED = 1, MARK_FRESH = 2;
+constexpr uint32_t HS_NONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t wave_count(uint32_t *ctr, bool want)
+{
+    const uint64_t m = __ballot(want);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+    uint32_t base = 0;
+    if (m && lane == lead)
+        base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)lead, 64);
+    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+}
+
+// one CT stage of one header, decoded as cfc_api.cpp ct_apply does
+struct Op {
+    uint32_t kind, action, dir;
+    bool is_tcp, syn, ki_form;
+    uint32_t tfl, len, sec, owner, proto;
+    uint32_t x1, y1, z1, w1;   // k1: the tuple as loaded (REPLY / RELATED)
+    uint32_t x2, y2, z2, w2;   // k2: reversed (ESTABLISHED / create)
+};
+
+// owner word of the destination endpoint's CT maps (cilium_lxc lookup)
+__device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint32_t da)
+{
+    if (!T.lxc4)
+        return 0;
+    uint32_t s = hash32(da, T.lxc4_mask);
+    for (;;) {
+        const uint4 v = ld16(T.lxc4 + s);
+        if (!(v.w & LXC_VALID))
+            return 0;
+        if (v.x == da)
+            return ct_owner_word(v.w & 0xFFFF, (v.w & LXC_CT_LOCAL) != 0);
+        s = (s + 1) & T.lxc4_mask;
+    }
+}
+
+__device__ __forceinline__ Op decode(const CtaArgs &A, uint64_t i, int st)
+{
+    Op o;
+    o.kind = OP_NONE;
+    const uint32_t cb = A.ctb[i];
+    const uint32_t cs = (cb >> (4 * st)) & 0xF;
+    if (!(cs & CFC_CT_DONE))
+        return o;
+    const uint32_t sa = A.sa[i], da = A.da[i], pt = A.pt[i], mt = A.mt[i];
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
+    o.dir = eg ? CT_EGRESS : CT_INGRESS;
+    o.owner = eg ? A.ep_owner : dst_owner(A.T, da);
+    o.proto = mt & 0xFF;
+    if (o.proto != 6 && o.proto != 17 && o.proto != 1)
+        return o;
+    o.len = mt >> 16;
+    o.is_tcp = o.proto == 6;
+    o.syn = (mt & CFC_HF_TCP_CLOSE) != 0;
+    o.tfl = (o.is_tcp && A.tf) ? A.tf[i] : 0u;
+    o.action = ct_action(false, o.proto, pt, mt);
+    o.sec = A.mode == CFC_MODE_EGRESS ? A.ep_sec : A.ident[i];
+    const CtProbe k = ct_probe<false>(o.proto, pt, (int)o.dir, o.owner);
+    o.x1 = da; o.y1 = sa; o.z1 = k.z1; o.w1 = k.w1;
+    o.x2 = sa; o.y2 = da; o.z2 = k.z2; o.w2 = k.w2;
+    // a k2 of ICMP-error form is its own related entry (ct_create4 writes
+    // the same key twice)
+    o.ki_form = o.proto == 1 && (k.w2 & 0x200u) && k.z2 == 0;
+    const uint32_t b = cs & CFC_CT_RES_MASK;
+    const bool dropped = st == last && A.ver[i] == DROP_POLICY;
+    if (b >= 2)
+        o.kind = OP_HIT;
+    else if (b == 1)
+        o.kind = dropped ? OP_DELETE : OP_HIT;
+    else if (cs & CFC_CT_CREATE)
+        o.kind = OP_CREATE;
+    return o;
+}
+
+__device__ __forceinline__ uint32_t find4(const CtaArgs &A, uint32_t x, uint32_t y,
+                                          uint32_t z, uint32_t w)
+{
+    const uint32_t mask = A.T.ct4_mask;
+    for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
+        const uint4 s = ld16(A.ct4 + i);
+        if (s.w == 0)
+            return NONE;
+        if (s.x == x && s.y == y && s.z == z && s.w == w)
+            return i;
+    }
+}
+
+// The slot of a key no other thread of this launch inserts: found, or a
+// free one claimed (CAS on w) and filled.
+__device__ uint32_t find_or_insert4(const CtaArgs &A, uint32_t x, uint32_t y, uint32_t z,
+                                    uint32_t w, bool *fresh)
+{
+    const uint32_t f = find4(A, x, y, z, w);
+    *fresh = f == NONE;
+    if (f != NONE)
+        return f;
+    const uint32_t mask = A.T.ct4_mask;
+    for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
+        uint32_t *pw = &A.ct4[i].w;
+        const uint32_t cur = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur != 0 && cur != CT_TOMBSTONE)
+            continue;
+        if (atomicCAS(pw, cur, CT_CLAIM) != cur)
+            continue;
+        A.ct4[i].x = x;
+        A.ct4[i].y = y;
+        A.ct4[i].z = z;
+        __threadfence();
+        __hip_atomic_store(pw, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&A.cnt[CTA_CLAIMS], 1u);
+        return i;
+    }
+}
+
+__device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32_t order2)
+{
+    return ((uint64_t)slot << A.ob) | order2;
+}
+
+// ---- scan: ops, hit slots, ordered marks, create requests
+__global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool in = i < A.n;
+        for (int st = 0; st < 2; st++) {
+            Op o;
+            o.kind = OP_NONE;
+            if (in)
+                o = decode(A, i, st);
+            uint32_t slot = HS_NONE;
+            if (o.kind == OP_HIT || o.kind == OP_DELETE) {
+                const bool rev = (A.ctb[i] >> (4 * st) & CFC_CT_RES_MASK) >= 2;
+                slot = rev ? find4(A, o.x1, o.y1, o.z1, o.w1) : find4(A, o.x2, o.y2, o.z2, o.w2);
+                if (slot != NONE) {
+                    const uint32_t clo = (ld16(A.tm + slot).z >> 16) & 3;
+                    if (o.kind == OP_DELETE || o.action == 2 || clo)
+                        A.mark[slot] = MARK_ORDERED;
+                } else {
+                    slot = HS_NONE;
+                }
+            }
+            if (in)
+                A.hs[2 * i + st] = slot;
+            (void)wave_count(&A.cnt[CTA_NHIT], slot != HS_NONE);
+            const bool req = o.kind == OP_CREATE;
+            const uint32_t r = wave_count(&A.cnt[CTA_NREQA], req);
+            if (req && r < A.req_cap) {
+                const uint32_t home = ct_hash4(o.x2, o.y2, o.z2, o.w2) & A.T.ct4_mask;
+                A.reqA[r] = pack(A, home, (uint32_t)((2 * i + st) << 1));
+            }
+        }
+    }
+}
+
+// key of a request: k2 of its op (round A) or the ICMP entry k2 relates
+// (round B: ports 0, nexthdr ICMP, flags | TUPLE_F_RELATED)
+__device__ __forceinline__ uint4 req_key(const CtaArgs &A, uint32_t order2, bool related,
+                                         Op *po)
+{
+    const uint64_t i = order2 >> 2;
+    const int st = (order2 >> 1) & 1;
+    *po = decode(A, i, st);
+    if (!related)
+        return make_uint4(po->x2, po->y2, po->z2, po->w2);
+    const uint32_t fl = (po->w2 >> 8) & 7;
+    return make_uint4(po->x2, po->y2, 0u, ct_word(1u, fl | 2u, po->owner));
+}
+
+// ---- insert: one thread per home slot; keys deduped in registers (a fifth
+// distinct key of one home slot is found by rescanning the run)
+__global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, const uint64_t *req,
+                                                    uint32_t nreq, int round)
+{
+    const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
+    if (r0 >= nreq)
+        return;
+    const uint64_t home = req[r0] >> A.ob;
+    if (r0 > 0 && (req[r0 - 1] >> A.ob) == home)
+        return;
+    const uint64_t omask = (1ull << A.ob) - 1;
+    uint4 kk[4];
+    uint32_t ks[4];
+    int nk = 0;
+    for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
+        const uint32_t order2 = (uint32_t)(req[r] & omask);
+        Op o;
+        const uint4 k = req_key(A, order2, round == 1, &o);
+        uint32_t slot = NONE;
+        for (int j = 0; j < nk; j++)
+            if (kk[j].x == k.x && kk[j].y == k.y && kk[j].z == k.z && kk[j].w == k.w)
+                slot = ks[j];
+        bool first = false;
+        if (slot == NONE) {
+            // not among the first four keys: an earlier request of the run
+            // may still have it
+            for (uint32_t q = r0; q < r && nk == 4; q++) {
+                Op oq;
+                const uint4 kq = req_key(A, (uint32_t)(req[q] & omask), round == 1, &oq);
+                if (kq.x == k.x && kq.y == k.y && kq.z == k.z && kq.w == k.w) {
+                    slot = find4(A, k.x, k.y, k.z, k.w);
+                    break;
+                }
+            }
+        }
+        if (slot == NONE) {
+            bool fresh;
+            slot = find_or_insert4(A, k.x, k.y, k.z, k.w, &fresh);
+            A.mark[slot] = MARK_ORDERED | (fresh ? MARK_FRESH : 0);
+            first = fresh;
+            if (nk < 4) {
+                kk[nk] = k;
+                ks[nk++] = slot;
+            }
+        }
+        // every create and related-entry write is an ordered op
+        const uint32_t c = atomicAdd(&A.cnt[CTA_NCX], 1u);
+        if (c < A.cx_cap)
+            A.cx[c] = pack(A, slot, order2 | (uint32_t)round);
+        // the key's first create writes its related ICMP entry next: into
+        // the device table for an ANY map (UDP, ICMP echo), into the host
+        // log for a TCP map (no lookup reaches it there)
+        if (round == 0 && first && !o.ki_form) {
+            if (o.is_tcp) {
+                const uint32_t l = atomicAdd(&A.cnt[CTA_NLOG], 1u);
+                if (l < A.log_cap) {
+                    CtLog &g = A.log[A.log_base + l];
+                    g.x = o.x2;
+                    g.y = o.y2;
+                    g.w = ct_word(1u, ((o.w2 >> 8) & 7) | 2u, o.owner);
+                    g.now = A.now;
+                    g.dirlen = o.dir << 31 | o.len;
+                    g.sec = o.sec;
+                    g.seq = A.seq;
+                    g.order = order2;
+                }
+            } else {
+                const uint32_t b = atomicAdd(&A.cnt[CTA_NREQB], 1u);
+                if (b < A.req_cap) {
+                    const uint32_t h =
+                        ct_hash4(o.x2, o.y2, 0u, ct_word(1u, ((o.w2 >> 8) & 7) | 2u, o.owner)) &
+                        A.T.ct4_mask;
+                    A.reqB[b] = pack(A, h, order2);
+                }
+            }
+        }
+    }
+}
+
+// ---- route: hits on unordered slots -> summary; the rest -> ordered list
+__global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < 2 * A.n; base += stride) {
+        const uint64_t j = base + threadIdx.x;
+        const uint32_t slot = j < 2 * A.n ? A.hs[j] : HS_NONE;
+        bool ordered = false;
+        if (slot != HS_NONE) {
+            if (A.mark[slot] & MARK_ORDERED) {
+                ordered = true;
+            } else {
+                const Op o = decode(A, j >> 1, (int)(j & 1));
+                const uint32_t in = o.dir == CT_INGRESS;
+                const uint32_t bits = (in ? o.tfl : o.tfl << 8) | (in ? 1u << 16 : 1u << 17) |
+                                      ((o.is_tcp && !o.syn) ? 1u << 18 : 0u);
+                const uint32_t old = A.sum[slot];
+                if ((old | bits) != old)
+                    atomicOr(&A.sum[slot], bits);
+            }
+        }
+        const uint32_t c = wave_count(&A.cnt[CTA_NCX], ordered);
+        if (ordered && c < A.cx_cap)
+            A.cx[c] = pack(A, slot, (uint32_t)(j << 1));
+    }
+}
+
+// ---- the entry state machine (cfc_api.cpp ct_upd / ct_upd_timeout /
+// ct_hit_update, conntrack.h:125-207, :221-285)
+struct St {
+    uint32_t last_rx, last_tx, seen_rx, seen_tx, bits, lifetime;
+};
+__device__ __forceinline__ void upd(St &e, uint32_t now, uint32_t life, uint32_t dir,
+                                    uint32_t flags)
+{
+    e.lifetime = now + life;
+    uint32_t &acc = dir == CT_INGRESS ? e.seen_rx : e.seen_tx;
+    uint32_t &last = dir == CT_INGRESS ? e.last_rx : e.last_tx;
+    const uint32_t seen = (flags | acc) & 0xFF;
+    if (last + CT_REPORT_INTERVAL < now || acc != seen) {
+        last = now;
+        acc = seen;
+    }
+}
+__device__ __forceinline__ void upd_timeout(St &e, uint32_t now, bool is_tcp, uint32_t dir,
+                                            bool syn, uint32_t flags)
+{
+    uint32_t life = CT_LIFETIME_NONTCP;
+    if (is_tcp) {
+        if (!syn)
+            e.bits |= SEEN_NON_SYN;
+        life = (e.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+    }
+    upd(e, now, life, dir, flags);
+}
+__device__ __forceinline__ void hit(St &e, uint32_t now, const Op &o)
+{
+    auto alive = [&] { return !(e.bits & RX_CLOSING) || !(e.bits & TX_CLOSING); };
+    if (alive())
+        upd_timeout(e, now, o.is_tcp, o.dir, o.syn, o.tfl);
+    if (o.action == 1) {
+        if (e.bits & (RX_CLOSING | TX_CLOSING)) {
+            e.bits &= ~(RX_CLOSING | TX_CLOSING);
+            upd_timeout(e, now, o.is_tcp, o.dir, o.syn, o.tfl);
+        }
+    } else if (o.action == 2) {
+        e.bits |= o.dir == CT_INGRESS ? RX_CLOSING : TX_CLOSING;
+        if (!alive())
+            upd(e, now, CT_CLOSE_TIMEOUT, o.dir, o.tfl);
+    }
+}
+// ct_create4's entry (seen_flags.syn = is_tcp: seen_non_syn stays clear)
+__device__ __forceinline__ St fresh(uint32_t now, bool is_tcp, uint32_t dir)
+{
+    St e{0, 0, 0, 0, 0, 0};
+    upd_timeout(e, now, is_tcp, dir, is_tcp, 0);
+    return e;
+}
+__device__ __forceinline__ St load_state(const CtTimer *tm, uint32_t slot)
+{
+    const uint4 t = ld16(tm + slot);
+    St e;
+    e.last_rx = t.x;
+    e.last_tx = t.y;
+    e.seen_rx = t.z & 0xFF;
+    e.seen_tx = (t.z >> 8) & 0xFF;
+    e.bits = ((t.z >> 16) & 3) | ((t.z & CTT_NON_SYN) ? SEEN_NON_SYN : 0u);
+    e.lifetime = t.w;
+    return e;
+}
+__device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St &e)
+{
+    uint4 t;
+    t.x = e.last_rx;
+    t.y = e.last_tx;
+    t.z = e.seen_rx | e.seen_tx << 8 | (e.bits & 3) << 16 |
+          ((e.bits & SEEN_NON_SYN) ? CTT_NON_SYN : 0u);
+    t.w = e.lifetime;
+    *reinterpret_cast<uint4 *>(tm + slot) = t;
+}
+
+// ---- fold: one thread per slot of the sorted ordered list
+__global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx, uint32_t ncx)
+{
+    const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
+    if (r0 >= ncx)
+        return;
+    const uint32_t slot = (uint32_t)(cx[r0] >> A.ob);
+    if (r0 > 0 && (uint32_t)(cx[r0 - 1] >> A.ob) == slot)
+        return;
+    const uint64_t omask = (1ull << A.ob) - 1;
+    const bool was_fresh = (A.mark[slot] & MARK_FRESH) != 0;
+    bool live = !was_fresh, created = false, deleted = false;
+    St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.tm, slot);
+    uint64_t acct[4] = {0, 0, 0, 0};   // [tx pk, tx by, rx pk, rx by] added / set
+    uint32_t sec = 0;
+    for (uint32_t r = r0; r < ncx && (uint32_t)(cx[r] >> A.ob) == slot; r++) {
+        const uint32_t order2 = (uint32_t)(cx[r] & omask);
+        const Op o = decode(A, order2 >> 2, (order2 >> 1) & 1);
+        const uint32_t d = o.dir == CT_INGRESS ? 2 : 0;
+        if (order2 & 1) {   // ct_create4's related-entry write: overwrite
+            e = fresh(A.now, o.is_tcp, o.dir);
+            e.bits |= SEEN_NON_SYN;
+            live = created = true;
+            acct[0] = acct[1] = acct[2] = acct[3] = 0;
+            acct[d] = 1;
+            acct[d + 1] = o.len;
+            sec = o.sec;
+        } else if (o.kind == OP_CREATE) {
+            if (live) {   // created earlier in this batch: a counted hit
+                hit(e, A.now, o);
+                acct[d] += 1;
+                acct[d + 1] += o.len;
+            } else {
+                e = fresh(A.now, o.is_tcp, o.dir);
+                if (o.ki_form)
+                    e.bits |= SEEN_NON_SYN;
+                live = created = true;
+                acct[0] = acct[1] = acct[2] = acct[3] = 0;
+                acct[d] = 1;
+                acct[d + 1] = o.len;
+                sec = o.sec;
+            }
+        } else if (live) {   // OP_HIT, OP_DELETE
+            hit(e, A.now, o);
+            if (o.kind == OP_DELETE) {
+                live = false;
+                deleted = true;
+            }
+        }
+    }
+    unsigned long long *ac =
+        reinterpret_cast<unsigned long long *>(A.T.ct_acct) + 4ull * slot;
+    CtInfo inf = A.info[slot];
+    if (!live) {
+        // ct_delete4: the entry and its counts go; the key stays readable
+        // for the host (w | CT_TOMBSTONE) until it has synchronised
+        const uint32_t w = A.ct4[slot].w;
+        A.ct4[slot].w = w | CT_TOMBSTONE;
+        ac[0] = ac[1] = ac[2] = ac[3] = 0;
+        inf.y |= CTI_DELETED;
+    } else if (created) {
+        store_state(A.tm, slot, e);
+        ac[0] = acct[0];
+        ac[1] = acct[1];
+        ac[2] = acct[2];
+        ac[3] = acct[3];
+        inf.sec = sec;
+        inf.y = (inf.y & ~0xFFFFu) | CTI_CREATED | (deleted ? CTI_DELETED : 0u);
+    } else {
+        store_state(A.tm, slot, e);
+        ac[0] += acct[0];
+        ac[1] += acct[1];
+        ac[2] += acct[2];
+        ac[3] += acct[3];
+        inf.y |= CTI_UPDATED;
+    }
+    A.info[slot] = inf;
+    A.mark[slot] = 0;
+}
+
+// ---- finish: the summaries of unordered slots.  With no closing bit set
+// and no RST/FIN, every hit re-arms the timeout, so the final state is:
+// seen_non_syn |= any TCP hit without the close bit; lifetime from the last
+// hit = now + (TCP ? (seen_non_syn ? TCP : SYN) : NONTCP); per direction
+// with hits, flags_seen |= their flags and last_report = now iff the
+// interval had passed or the flags grew (the first report sets it to now,
+// later ones keep it).
+__global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
+{
+    const uint64_t slots = (uint64_t)A.T.ct4_mask + 1;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += stride) {
+        const uint32_t m = A.sum[s];
+        if (!m)
+            continue;
+        A.sum[s] = 0;
+        St e = load_state(A.tm, (uint32_t)s);
+        const bool is_tcp = (A.ct4[s].w & 0xFF) == 6;
+        if (is_tcp && (m & (1u << 18)))
+            e.bits |= SEEN_NON_SYN;
+        e.lifetime = A.now + (is_tcp ? ((e.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT)
+                                     : CT_LIFETIME_NONTCP);
+        if (m & (1u << 16)) {
+            const uint32_t seen = (e.seen_rx | (m & 0xFF)) & 0xFF;
+            if (e.last_rx + CT_REPORT_INTERVAL < A.now || seen != e.seen_rx)
+                e.last_rx = A.now;
+            e.seen_rx = seen;
+        }
+        if (m & (1u << 17)) {
+            const uint32_t seen = (e.seen_tx | ((m >> 8) & 0xFF)) & 0xFF;
+            if (e.last_tx + CT_REPORT_INTERVAL < A.now || seen != e.seen_tx)
+                e.last_tx = A.now;
+            e.seen_tx = seen;
+        }
+        store_state(A.tm, (uint32_t)s, e);
+        A.info[s].y |= CTI_UPDATED;
+    }
+}
+
+// ---- host synchronisation: the changed slots, compacted
+__global__ __launch_bounds__(256) void k_cta_collect(const Ct4Slot *ct4, CtTimer *tm,
+                                                     CtInfo *info, uint64_t slots,
+                                                     CtSyncRec *out, uint32_t cap,
+                                                     uint32_t *cnt)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < slots; base += stride) {
+        const uint64_t s = base + threadIdx.x;
+        const bool dirty = s < slots && (info[s].y >> 16) != 0;
+        const uint32_t r = wave_count(cnt, dirty);
+        if (!dirty || r >= cap)
+            continue;
+        CtSyncRec &o = out[r];
+        const uint4 k = ld16(ct4 + s);
+        const uint4 t = ld16(tm + s);
+        o.slot = (uint32_t)s;
+        o.info = info[s];
+        o.x = k.x;
+        o.y = k.y;
+        o.z = k.z;
+        o.w = k.w;
+        o.last_rx = t.x;
+        o.last_tx = t.y;
+        o.flags = t.z;
+        o.lifetime = t.w;
+        info[s].y &= 0xFFFFu;
+    }
+}
+// after the host has taken them: deleted slots become plain tombstones
+// (free for inserts again)
+__global__ __launch_bounds__(256) void k_cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n)
+{
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n)
+        return;
+    const uint32_t s = rec[r].slot;
+    if ((rec[r].w & CT_TOMBSTONE) == CT_TOMBSTONE) {
+        const uint4 t = make_uint4(0, 0, 0, CT_TOMBSTONE);
+        *reinterpret_cast<uint4 *>(ct4 + s) = t;
+    }
+}
+
+unsigned blocks_for(uint64_t n, unsigned cap)
+{
+    const uint64_t b = (n + 255) / 256;
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, cap));
+}
+
+int sort_keys(const CtaArgs &A, uint64_t *keys, uint64_t *alt, uint32_t n, int bits,
+              hipStream_t s, uint64_t **sorted)
+{
+    *sorted = keys;
+    if (n < 2)
+        return 0;
+    size_t tb = A.sort_tmp_bytes;
+    hipcub::DoubleBuffer<uint64_t> db(keys, alt);
+    if (hipcub::DeviceRadixSort::SortKeys(A.sort_tmp, tb, db, (int)n, 0, bits, s) !=
+        hipSuccess)
+        return -EIO;
+    *sorted = db.Current();
+    return 0;
+}
+
+}  // namespace
+
+size_t cta_sort_tmp_bytes(uint32_t n)
+{
+    size_t tb = 0;
+    hipcub::DoubleBuffer<uint64_t> db(nullptr, nullptr);
+    (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tb, db, (int)std::max<uint32_t>(n, 2u), 0,
+                                            64, (hipStream_t)0);
+    return tb;
+}
+
+int cta_scan(const CtaArgs &A, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cta_scan, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+// The rest of the apply after the host has read the scan's counts (nreqA)
+// and allowed the inserts.  Reads two more counts on the way (the sorts
+// take host item counts).
+int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s)
+{
+    const int bits = A.ob + A.slot_bits;
+    uint64_t *sorted;
+    int rc;
+    if ((rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
+        return rc;
+    if (nreqA)
+        hipLaunchKernelGGL(k_cta_insert, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
+                           (const uint64_t *)sorted, nreqA, 0);
+    if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    const uint32_t nreqB = host_cnt[CTA_NREQB];
+    if (nreqB > A.req_cap || host_cnt[CTA_NLOG] > A.log_cap)
+        return -EOVERFLOW;
+    if ((rc = sort_keys(A, A.reqB, A.reqB2, nreqB, bits, s, &sorted)))
+        return rc;
+    if (nreqB)
+        hipLaunchKernelGGL(k_cta_insert, dim3((nreqB + 255) / 256), dim3(256), 0, s, A,
+                           (const uint64_t *)sorted, nreqB, 1);
+    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for(2 * A.n, 8192)), dim3(256), 0, s, A);
+    if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    const uint32_t ncx = host_cnt[CTA_NCX];
+    if (ncx > A.cx_cap)
+        return -EOVERFLOW;
+    if ((rc = sort_keys(A, A.cx, A.cx2, ncx, bits, s, &sorted)))
+        return rc;
+    if (ncx)
+        hipLaunchKernelGGL(k_cta_fold, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
+                           (const uint64_t *)sorted, ncx);
+    hipLaunchKernelGGL(k_cta_finish, dim3(blocks_for((uint64_t)A.T.ct4_mask + 1, 8192)),
+                       dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec *out,
+                uint32_t cap, uint32_t *cnt, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cta_collect, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4, tm,
+                       info, slots, out, cap, cnt);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s)
+{
+    if (n)
+        hipLaunchKernelGGL(k_cta_tomb, dim3((n + 255) / 256), dim3(256), 0, s, ct4, rec, n);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+}  // namespace cfc

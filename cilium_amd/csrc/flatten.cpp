@@ -490,17 +490,62 @@ uint64_t ct_map_key(int family, uint32_t owner, int any)
     return (uint64_t)family << 40 | (uint64_t)owner << 8 | (uint64_t)any;
 }
 
+bool ct_slot_of(const Map *m, const std::string &key, Ct4Slot *s4, Ct6Slot *s6)
+{
+    const bool v6 = m->role == ROLE_CT6;
+    const uint32_t al = v6 ? 16 : 4;
+    if (key.size() != 2 * al + 6)
+        return false;
+    const uint8_t *k = (const uint8_t *)key.data();
+    const uint8_t nh = k[2 * al + 4], fl = k[2 * al + 5];
+    const uint8_t icmp = v6 ? 58 : 1;
+    if (!(m->ct_any ? (nh == 17 || nh == icmp) : nh == 6) || (fl & ~7u))
+        return false;
+    uint32_t z;
+    memcpy(&z, k + 2 * al, 4);
+    const uint32_t w = ct_word(nh, fl, ct_owner_word((uint32_t)std::max(m->policy_lxc, 0),
+                                                      m->policy_lxc >= 0));
+    if (!v6) {
+        memcpy(&s4->x, k, 4);
+        memcpy(&s4->y, k + 4, 4);
+        s4->z = z;
+        s4->w = w;
+    } else {
+        *s6 = Ct6Slot{};
+        memcpy(s6->d, k, 16);
+        memcpy(s6->s, k + 16, 16);
+        s6->z = z;
+        s6->w = w;
+    }
+    return true;
+}
+
+// struct ct_entry: bits @36, tx/rx_flags_seen @42/43, last_tx/rx_report @48/52
+CtTimer ct_timer_of(const std::string &val)
+{
+    CtTimer tm{};
+    if (val.size() >= 56) {
+        const uint8_t *v = (const uint8_t *)val.data();
+        uint16_t bits;
+        memcpy(&bits, v + 36, 2);
+        memcpy(&tm.last_tx, v + 48, 4);
+        memcpy(&tm.last_rx, v + 52, 4);
+        tm.flags = v[43] | (uint32_t)v[42] << 8 | (uint32_t)(bits & 3) << 16 |
+                   ((bits & 16) ? CTT_NON_SYN : 0u);
+        memcpy(&tm.lifetime, v + 32, 4);
+    }
+    return tm;
+}
+
 // CT maps -> one open-addressed table per family (layout.h).  Entries no
-// lookup can reach (nexthdr not served by their map) are left out.
+// lookup can reach (nexthdr not served by their map) are left out.  A
+// commit patches later inserts and deletes into the same table
+// (cfc_api.cpp patch_ct; deleted slots become CT_TOMBSTONE).
 static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
 {
     size_t n4 = 0, n6 = 0;
     for (const Map *m : cts)
         (m->role == ROLE_CT4 ? n4 : n6) += m->kv.size();
-    auto reachable = [](const Map *m, uint8_t nh) {
-        const uint8_t icmp = m->role == ROLE_CT4 ? 1 : 58;
-        return m->ct_any ? (nh == 17 || nh == icmp) : nh == 6;
-    };
     if (n4) {
         uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n4));
         img->ct4.assign(ns, Ct4Slot{});
@@ -517,34 +562,13 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
         const bool v6 = m->role == ROLE_CT6;
         if (m->ksz != (v6 ? 38u : 14u))
             continue;
-        const uint32_t owner = ct_owner_word((uint32_t)std::max(m->policy_lxc, 0),
-                                             m->policy_lxc >= 0);
         for (const auto &kv : m->kv) {
-            const uint8_t *k = (const uint8_t *)kv.first.data();
-            const uint32_t al = v6 ? 16 : 4;
-            const uint8_t nh = k[2 * al + 4], fl = k[2 * al + 5];
-            if (!reachable(m, nh) || (fl & ~7u))
+            Ct4Slot e;
+            Ct6Slot e6;
+            if (!ct_slot_of(m, kv.first, &e, &e6))
                 continue;
-            uint32_t z;
-            memcpy(&z, k + 2 * al, 4);
-            const uint32_t w = ct_word(nh, fl, owner);
-            // struct ct_entry: bits @36, tx/rx_flags_seen @42/43,
-            // last_tx/rx_report @48/52
-            const uint8_t *v = (const uint8_t *)kv.second.val.data();
-            CtTimer tm{};
-            if (kv.second.val.size() >= 56) {
-                uint16_t bits;
-                memcpy(&bits, v + 36, 2);
-                memcpy(&tm.last_tx, v + 48, 4);
-                memcpy(&tm.last_rx, v + 52, 4);
-                tm.flags = v[43] | (uint32_t)v[42] << 8 | (uint32_t)(bits & 3) << 16;
-            }
+            const CtTimer tm = ct_timer_of(kv.second.val);
             if (!v6) {
-                Ct4Slot e;
-                memcpy(&e.x, k, 4);
-                memcpy(&e.y, k + 4, 4);
-                e.z = z;
-                e.w = w;
                 uint32_t i = ct_hash4(e.x, e.y, e.z, e.w) & img->ct4_mask, p = 0;
                 while (img->ct4[i].w) {
                     i = (i + 1) & img->ct4_mask;
@@ -555,11 +579,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                 img->ct4_probe = std::max(img->ct4_probe, p);
                 img->n_ct4++;
             } else {
-                Ct6Slot e{};
-                memcpy(e.d, k, 16);
-                memcpy(e.s, k + 16, 16);
-                e.z = z;
-                e.w = w;
+                const Ct6Slot &e = e6;
                 uint32_t i = ct_hash6(e.d, e.s, e.z, e.w) & img->ct6_mask, p = 0;
                 while (img->ct6[i].w) {
                     i = (i + 1) & img->ct6_mask;

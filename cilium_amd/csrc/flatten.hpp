@@ -87,6 +87,10 @@ struct HostImage {
 
 // the CT map a slot's entry lives in: (family 4/6, owner word, any) key
 uint64_t ct_map_key(int family, uint32_t owner, int any);
+// the device slot of a CT map entry; false when no lookup reaches it
+bool ct_slot_of(const Map *m, const std::string &key, Ct4Slot *s4, Ct6Slot *s6);
+// the report state the kernels read (CtTimer) of a struct ct_entry value
+CtTimer ct_timer_of(const std::string &val);
 
 // Table groups an epoch is built from; a commit rebuilds only the groups
 // whose maps changed (the others' device buffers carry over).

@@ -266,6 +266,9 @@ __host__ __device__ inline uint32_t ct_word(uint32_t nexthdr, uint32_t flags,
 {
     return nexthdr | (flags & 7u) << 8 | owner;
 }
+// a deleted slot (cfc_commit patches deletes in place): nonzero, so probe
+// sequences run through it, and bits 12-15 are never set in a real w
+constexpr uint32_t CT_TOMBSTONE = 0xF000u;
 __host__ __device__ inline uint32_t ct_owner_word(uint32_t lxc, bool local)
 {
     return local ? (1u << 11 | lxc << 16) : 0u;
@@ -291,15 +294,28 @@ __host__ __device__ inline uint32_t ct_hash6(const uint32_t d[4], const uint32_t
 struct alignas(16) Ct4Slot {
     uint32_t x, y, z, w;
 };
-// The report state of a CT slot's entry (struct ct_entry, common.h:380-406)
-// that decides whether a hit is traced (__ct_update_timeout,
-// conntrack.h:125-185): last_{rx,tx}_report and rx/tx_flags_seen | the
-// rx/tx_closing bits << 16
+// The mutable state of a CT slot's entry (struct ct_entry, common.h:380-406):
+// what decides whether a hit is traced (__ct_update_timeout,
+// conntrack.h:125-185) and what the device CT apply (ctapply.hip) updates:
+// last_{rx,tx}_report, rx/tx_flags_seen, the rx/tx_closing and seen_non_syn
+// bits, lifetime.  The packet/byte counts live in ct_acct.
 struct alignas(16) CtTimer {
     uint32_t last_rx, last_tx;
     uint32_t flags;      // rx_flags_seen | tx_flags_seen << 8 | closing << 16
-    uint32_t pad;
+                         // | seen_non_syn << 18
+    uint32_t lifetime;
 };
+constexpr uint32_t CTT_NON_SYN = 1u << 18;
+// per-slot state of the device CT apply (ctapply.hip): src_sec_id and
+// rev_nat_index of an entry the device created, and what changed since the
+// host last synchronised (CTI_*, bits 16-18 of y)
+struct CtInfo {
+    uint32_t sec;
+    uint32_t y;          // rev_nat_index | dirty << 16
+};
+constexpr uint32_t CTI_UPDATED = 1u << 16, CTI_CREATED = 2u << 16, CTI_DELETED = 4u << 16;
+// a slot being filled by a device insert (never matched, never free)
+constexpr uint32_t CT_CLAIM = 0xE000u;
 struct alignas(16) Ct6Slot {
     uint32_t d[4], s[4], z, w, pad[2];
 };

@@ -46,20 +46,26 @@ int Map::update(const void *key, const void *value, uint64_t flags)
     if (it != kv.end()) {
         if (flags == BPF_NOEXIST)
             return -EEXIST;
-        touched[nk] = 1;
+        touched[nk] |= TOUCH_VALUE;
     } else {
         if (flags == BPF_EXIST)
             return -ENOENT;
         if (kv.size() >= max_entries) {
             if (type == MT_LRU_HASH && !kv.empty()) {
-                kv.erase(kv.begin());  // stand-in for least recently used
-                sgen[0]++;
-                sgen[1]++;
+                // stand-in for least recently used
+                if (ct())
+                    touched[kv.begin()->first] = TOUCH_ERASE;
+                else
+                    bump_sgen(kv.begin()->first);
+                kv.erase(kv.begin());
             } else {
                 return lpm() ? -ENOSPC : -E2BIG;
             }
         }
-        bump_sgen(nk);
+        if (ct())
+            touched[nk] = TOUCH_INSERT;
+        else
+            bump_sgen(nk);
     }
     Entry &e = kv[nk];
     e.key.assign((const char *)key, ksz);
@@ -107,8 +113,12 @@ int Map::erase(const void *key)
     if (it == kv.end())
         return -ENOENT;
     kv.erase(it);
-    touched.erase(nk);
-    bump_sgen(nk);
+    if (ct()) {
+        touched[nk] = TOUCH_ERASE;
+    } else {
+        touched.erase(nk);
+        bump_sgen(nk);
+    }
     gen++;
     return 0;
 }

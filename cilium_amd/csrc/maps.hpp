@@ -34,6 +34,8 @@ enum Role {
     ROLE_CT6,       // cilium_ct6_* / cilium_ct_any6_*
 };
 
+enum : int { TOUCH_VALUE = 1, TOUCH_INSERT = 2, TOUCH_ERASE = 4 };
+
 struct Map {
     std::string name;
     Role role = ROLE_NONE;
@@ -45,8 +47,11 @@ struct Map {
     // family (sgen[0] IPv4, sgen[1] IPv6), other maps in sgen[0]
     uint64_t sgen[2] = {0, 0};
     // keys whose value was overwritten in place since the last commit (a
-    // commit may patch those into the device tables instead of rebuilding)
+    // commit may patch those into the device tables instead of rebuilding);
+    // CT maps also journal inserts and deletes here (TOUCH_* bits), which
+    // a commit patches into the device CT table in place
     std::map<std::string, int> touched;
+    bool ct() const { return role == ROLE_CT4 || role == ROLE_CT6; }
 
     struct Entry {
         std::string key;  // key bytes as last written
@@ -76,6 +81,21 @@ struct Map {
     // normalised key: raw for hashes; prefixlen + masked data for LPM.
     // Returns false for an invalid LPM key (prefixlen too large).
     bool norm(const uint8_t *k, std::string *out) const;
+
+    // the device CT apply's changes, taken into the host mirror: no journal,
+    // no structural generation (the device table already has them)
+    void put_raw(const std::string &k, const std::string &v)
+    {
+        Entry &e = kv[k];
+        e.key = k;
+        e.val = v;
+        gen++;
+    }
+    void erase_raw(const std::string &k)
+    {
+        if (kv.erase(k))
+            gen++;
+    }
 
     int update(const void *key, const void *value, uint64_t flags);
     int lookup(const void *key, void *value) const;

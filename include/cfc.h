@@ -161,12 +161,20 @@ int cfc_commit(cfc_ctx *ctx, void *stream);
  * resident), also used when the compact layout's offsets would overflow.
  * Lookups give the same result in every layout.
  * CFC_OPT_TIMING: 1 = record HIP events around the kernels of every
- * cfc_classify_* call (read back with cfc_timing_collect). */
+ * cfc_classify_* call (read back with cfc_timing_collect).
+ * CFC_OPT_CT_APPLY: where cfc_ct_apply_v4 runs: DEVICE (default) applies the
+ * batch's CT writes to the device CT table in place and keeps the host's
+ * view of the CT maps lazily (synchronised when a CT map is next read or
+ * written through this API, or at cfc_counters_sync); HOST walks the batch
+ * on the host.  Both give the same maps. */
 #define CFC_OPT_LPM4 1
 #define CFC_LPM4_AUTO 0
 #define CFC_LPM4_DIR24_8 1
 #define CFC_LPM4_TRIE 2
 #define CFC_OPT_TIMING 2
+#define CFC_OPT_CT_APPLY 3
+#define CFC_CT_APPLY_DEVICE 0
+#define CFC_CT_APPLY_HOST 1
 int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
 
 /* ---------------------------------------------------------------- datapath */
@@ -316,6 +324,9 @@ int cfc_classify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
  * closing flags of RST/FIN (CFC_HF_TCP_CLOSE) and re-opening.  A flow seen
  * twice in one batch is created once and counted on its second packet.
  * Lookups inside one batch all see the maps as committed before it.
+ * IPv4 runs on the device (CFC_OPT_CT_APPLY) unless the CT table could pass
+ * 3/4 load or a CT map its max_entries, or host-side CT map changes wait
+ * for a commit: then, and for IPv6, on the host.
  * Synchronises `stream`. */
 int cfc_ct_apply_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);

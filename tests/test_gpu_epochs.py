@@ -8,10 +8,11 @@ import numpy as np
 import pytest
 
 import oracle as O
+from cilium_amd import _lib as LL
 from cilium_amd import ipcache, metricsmap, policymap
 from cilium_amd import synth as S
 from cilium_amd.datapath import Datapath, pack
-from cilium_amd.loader import load_tables, policy_rows
+from cilium_amd.loader import ct_rows, load_tables, policy_rows
 
 pytestmark = pytest.mark.gpu
 
@@ -191,4 +192,92 @@ def test_in_place_patches(torch):
     out = dp.classify(b4, 0)
     assert dp.stats()["epoch"] == e0 + 1
     check(out, O.Oracle(t), h4, mode=0)
+    dp.close()
+
+
+def ct_table_from_maps(dp):
+    """The CT maps' contents (host truth) as CT_DT records for an oracle."""
+    rows = ct_rows(dp, dp.ct_fds)
+    ct = np.zeros(len(rows), S.CT_DT)
+    ct["family"] = rows[:, 3]
+    ct["lxc"] = rows[:, 0].astype(np.int32) + rows[:, 1].astype(np.int32) * 256 - 1
+    ct["any"] = rows[:, 2]
+    ct["tuple"] = rows[:, 4:42]
+    ct["entry"] = rows[:, 44:100]
+    return ct
+
+
+def check_ct(out, t, h, mode=3):
+    o = O.Oracle(t)
+    oa, ov, oi, oc = o.classify(h, mode, 0, nthreads=16, want_ct=True)
+    for name, a, b in (("action", out.action.cpu().numpy().astype(np.int32), oa),
+                       ("verdict", out.verdict.cpu().numpy(), ov),
+                       ("identity", out.identity.cpu().numpy().view(np.uint32), oi),
+                       ("ct", out.ct.cpu().numpy(), oc)):
+        bad = np.flatnonzero(a != b)
+        assert len(bad) == 0, f"{name}: {len(bad)} of {len(a)} differ, first {bad[:8]}"
+
+
+@pytest.mark.parametrize("apply", ["device", "host"])
+def test_ct_patched_in_place(torch, apply):
+    """CT creates (cfc_ct_apply), deletes and re-inserts through the map API
+    are patched into the live CT table: the epoch stays, deleted slots
+    become tombstones that later inserts reuse.  Past 3/4 load the CT group
+    is rebuilt instead.  Each step against an oracle built from the CT
+    maps' contents."""
+    t, flows = S.config_c5(5, n_flows=50_000, n_prefixes=20_000, n_policy=2000, now=1000)
+    dp = Datapath(0)
+    dp.set_option(LL.OPT_CT_APPLY, LL.CT_APPLY_DEVICE if apply == "device" else LL.CT_APPLY_HOST)
+    load_tables(dp, t)
+    h = S.headers_c5(t, flows, 300_000, seed=11)
+    b = pack(h)
+    out = dp.classify(b, 3, want_ct=True)
+    e0, n0 = dp.stats()["epoch"], dp.stats()["ct4_entries"]
+    check_ct(out, t, h)
+    dp.ct_apply(b, out, 3)
+    # the writes of batch 1 are in the live table: same epoch
+    h2 = S.headers_c5(t, flows, 300_000, seed=12)
+    b2 = pack(h2)
+    out = dp.classify(b2, 3, want_ct=True)
+    t.ct = ct_table_from_maps(dp)
+    st = dp.stats()
+    # creates and deletes (established flows the policy now denies)
+    assert st["epoch"] == e0 and st["ct4_entries"] != n0
+    check_ct(out, t, h2)
+    # deletes through the map API (global v4 maps)
+    rng = np.random.default_rng(3)
+    fds = {k: fd for k, fd in dp.ct_fds.items() if k[0] == 1 and k[1] == -1}
+    gone = {}
+    for k, fd in fds.items():
+        keys, vals = dp.dump(fd)
+        sel = rng.choice(len(keys), size=min(5000, len(keys) // 4), replace=False)
+        gone[k] = (keys[sel], vals[sel])
+        for kk in keys[sel]:
+            dp.delete_element(fd, kk.tobytes())
+    out = dp.classify(b2, 3, want_ct=True)
+    assert dp.stats()["epoch"] == e0
+    t.ct = ct_table_from_maps(dp)
+    check_ct(out, t, h2)
+    # the same entries back: they land in the deleted slots
+    for k, (keys, vals) in gone.items():
+        dp.update_batch(fds[k], keys, vals)
+    out = dp.classify(b2, 3, want_ct=True)
+    assert dp.stats()["epoch"] == e0
+    t.ct = ct_table_from_maps(dp)
+    check_ct(out, t, h2)
+    # bulk inserts, 20k per commit, until the table passes 3/4 load and the
+    # CT group is rebuilt
+    for it in range(40):
+        for k, fd in fds.items():
+            keys, vals = dp.dump(fd)
+            rep = rng.integers(0, len(keys), size=10_000)
+            nk = keys[rep].copy()
+            nk[:, 8:12] = rng.integers(0, 256, size=(len(rep), 4), dtype=np.uint8)
+            dp.update_batch(fd, nk, vals[rep])
+        out = dp.classify(b2, 3, want_ct=True)
+        if dp.stats()["epoch"] != e0:
+            break
+    assert dp.stats()["epoch"] == e0 + 1 and it > 0
+    t.ct = ct_table_from_maps(dp)
+    check_ct(out, t, h2)
     dp.close()

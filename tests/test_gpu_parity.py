@@ -27,9 +27,11 @@ def torch():
 LAYOUTS = {"dir24_8": L.LPM4_DIR24_8, "trie": L.LPM4_TRIE}
 
 
-def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
+def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO,
+            ct_apply=L.CT_APPLY_DEVICE):
     dp = Datapath(0)
     dp.set_option(L.OPT_LPM4, lpm4)
+    dp.set_option(L.OPT_CT_APPLY, ct_apply)
     pms = load_tables(dp, t)
     if lpm4 != L.LPM4_AUTO and (t.ipcache["family"] == 1).any():
         assert dp.stats()["lpm4_layout"] == lpm4
@@ -96,9 +98,10 @@ def test_golden(torch, name, layout):
         np.testing.assert_array_equal(rows, o.ct_dump())
 
 
-def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO):
+def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO,
+                        ct_apply=L.CT_APPLY_DEVICE):
     act, ver, ide, counters, metrics = run_gpu(torch, t, h, mode, ep_lxc, chunks,
-                                               lpm4)
+                                               lpm4, ct_apply)
     o = O.Oracle(t)
     use_ct = getattr(t, "ct", None) is not None
     if use_ct:   # the same batches, each folded into CT before the next
@@ -367,15 +370,19 @@ def test_v6_only_endpoints_and_empty(torch):
         compare_with_oracle(torch, e, h, mode)
 
 
+@pytest.mark.parametrize("apply", ["device", "host"])
 @pytest.mark.parametrize("mode", [0, 3])
-def test_c5_conntrack_vs_oracle(torch, mode):
+def test_c5_conntrack_vs_oracle(torch, mode, apply):
     """C5 shape at reduced size: 300k live flows (Zipf traffic, ESTABLISHED
     and REPLY packets, 5% new flows), three batches each folded into CT
-    (cfc_ct_apply) before the next: outputs, CT bytes, policy counters,
-    metrics and every CT entry (accounting included) bit-exact."""
+    (cfc_ct_apply, on the device or the host) before the next: outputs, CT
+    bytes, policy counters, metrics and every CT entry (accounting
+    included) bit-exact."""
     t, flows = S.config_c5(5, n_flows=300_000, n_prefixes=100_000)
     h = S.headers_c5(t, flows, 1_200_000, seed=31)
-    act, ver = compare_with_oracle(torch, t, h, mode, chunks=3)
+    act, ver = compare_with_oracle(
+        torch, t, h, mode, chunks=3,
+        ct_apply=L.CT_APPLY_DEVICE if apply == "device" else L.CT_APPLY_HOST)
     assert (ver == 0).sum() > len(h) // 3
 
 
