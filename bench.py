@@ -95,7 +95,14 @@ def main():
                          "c5: configs[4], + conntrack with --flows live flows "
                          "and Zipf(1.1) traffic (side measurements)")
     ap.add_argument("--flows", type=int, default=10_000_000)
+    ap.add_argument("--ct-apply", action="store_true",
+                    help="c5: every step is classify + cfc_ct_apply_v4 (the batch's CT "
+                         "creates, deletes and timeouts written into the device CT "
+                         "table); the new flows' source ports are re-drawn on the "
+                         "device at the start of each step, so every step creates")
     args = ap.parse_args()
+    if args.ct_apply and args.workload != "c5":
+        ap.error("--ct-apply needs --workload c5")
     if args.notify and args.workload == "c3":
         ap.error("--notify covers IPv4 batches (c2, c5)")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -153,9 +160,13 @@ def main():
         s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
     elif args.workload == "c5":
         from cilium_amd.datapath import pack_v4
-        hb = pack_v4(S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank), dev)
+        h5, new5 = S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank,
+                                return_new=True)
+        hb = pack_v4(h5, dev)
         s, d, p, m, tf = hb.saddr, hb.daddr, hb.ports, hb.meta, hb.tcp_flags
-        del hb
+        del hb, h5
+        new_idx = torch.from_numpy(np.flatnonzero(new5)).to(dev)
+        new_ports = p[new_idx].clone()
     else:
         s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
     if mode == 1:
@@ -164,7 +175,9 @@ def main():
         tf = None    # no TCP flag bytes in the C2/C3 streams (all CT_NEW)
     batch = HeaderBatchV4(s, d, p, m, None, tf)
     out = Verdicts(torch.empty(n, dtype=torch.int32, device=dev),
-                   torch.empty(n, dtype=torch.int32, device=dev), None)
+                   torch.empty(n, dtype=torch.int32, device=dev), None,
+                   torch.empty(n, dtype=torch.uint8, device=dev) if args.ct_apply else None)
+    salt = [0]
     n6 = len(batch6) if batch6 is not None else 0
     out6 = Verdicts(torch.empty(n6, dtype=torch.int32, device=dev),
                     torch.empty(n6, dtype=torch.int32, device=dev), None)
@@ -183,7 +196,12 @@ def main():
         nt_stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     def step():
+        if args.ct_apply:   # fresh new flows: their source ports re-drawn
+            salt[0] += 1
+            p[new_idx] = new_ports ^ ((salt[0] * 0x9E37) & 0xFFFF)
         dp.classify_v4(batch, mode, ep_lxc, out=out)
+        if args.ct_apply:
+            dp.ct_apply(batch, out, mode, ep_lxc)
         if args.notify:   # records stay on the device (no sync in the step)
             LL.check(dp.L.cfc_monitor_events_v4(
                 dp.h, ctypes.byref(nt_hdr), ctypes.byref(nt_out), mode, ep_lxc,
@@ -259,7 +277,9 @@ def main():
                                   want_lookups=True)
     cpu_s = time.perf_counter() - c0
     # the timed region's last launch wrote `out` for this same batch
-    parity = bool(np.array_equal(out.verdict[:samp].cpu().numpy(), ov) and
+    # (with --ct-apply the tables moved on during the timed steps: the CT
+    # parity of classify + apply is tests/test_gpu_fullsize.py's)
+    parity = None if args.ct_apply else bool(np.array_equal(out.verdict[:samp].cpu().numpy(), ov) and
                   np.array_equal(out.identity[:samp].cpu().numpy().view(np.uint32), oi))
     if args.notify:   # the sample's monitor records, every field
         _, ov2, oi2, ow = orc.classify(hs, mode, ep_lxc, nthreads=cores,
@@ -363,6 +383,7 @@ def main():
             "lpm4_layout": {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none"),
             "parallelism": f"header-stream shards x{world}, tables replicated",
             "drop_notify": bool(args.notify),
+            "ct_apply": bool(args.ct_apply),
         },
         "roofline": {
             "kernel": "k_classify_v4" + (" + k_classify_v6" if n6 else ""),
@@ -402,6 +423,15 @@ def main():
         "parity_sample_ok": parity,
         "monitor_records_per_step_per_gpu": int(nt_cnt.item()) if args.notify else None,
     }
+    if args.ct_apply:   # the step is classify + cfc_ct_apply_v4
+        st2 = dp.stats()
+        res["ct_apply"] = {
+            "path_device_calls": st2["ct_apply_device"],
+            "path_host_calls": st2["ct_apply_host"],
+            "ct4_entries_after": st2["ct4_entries"],
+            "apply_ms_per_step": round(call_ms - tm["classify_ms"] / args.steps
+                                       - count_ms, 4),
+        }
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

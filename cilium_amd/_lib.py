@@ -78,7 +78,9 @@ class Stats(ctypes.Structure):
                 ("prefilter_v6_fix", ctypes.c_uint32),
                 ("prefilter_v6_dyn", ctypes.c_uint32),
                 ("ct4_entries", ctypes.c_uint32),
-                ("ct6_entries", ctypes.c_uint32)]
+                ("ct6_entries", ctypes.c_uint32),
+                ("ct_apply_device", ctypes.c_uint32),
+                ("ct_apply_host", ctypes.c_uint32)]
 
 
 class NodeConfig(ctypes.Structure):

@@ -175,6 +175,7 @@ struct cfc_ctx {
     bool ct_dirty = false;
     uint64_t cta_claims = 0;     // device inserts since the last sync
     uint32_t cta_seq = 0;
+    uint32_t n_apply_dev = 0, n_apply_host = 0;
     uint64_t log_used = 0;       // CtLog entries since the last sync
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
 
@@ -692,7 +693,7 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
         return nullptr;
     const size_t n4 = img.ct4.size();
     if (n4 && ((*rc = g->ct4_info.zeros(sizeof(CtInfo) * n4, s)) ||
-               (*rc = g->ct4_mark.zeros(n4, s)) || (*rc = g->ct4_sum.zeros(4 * n4, s))))
+               (*rc = g->ct4_mark.zeros(4 * n4, s)) || (*rc = g->ct4_sum.zeros(4 * n4, s))))
         return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
@@ -707,7 +708,7 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     g->n_ct4 = img.n_ct4;
     g->n_ct6 = img.n_ct6;
     g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
-               48ull * nslots + 13ull * n4;
+               48ull * nslots + 16ull * n4;
     g->ct4_host = std::move(img.ct4);
     g->ct6_host = std::move(img.ct6);
     return g;
@@ -1840,6 +1841,8 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     if (!c->epoch)
         return -ENOENT;
     *st = c->epoch->st;
+    st->ct_apply_device = c->n_apply_dev;
+    st->ct_apply_host = c->n_apply_host;
     return 0;
 }
 
@@ -2079,7 +2082,7 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     A.ct4 = (Ct4Slot *)G.ct4.p;
     A.tm = (CtTimer *)G.ct4_tm.p;
     A.info = (CtInfo *)G.ct4_info.p;
-    A.mark = (uint8_t *)G.ct4_mark.p;
+    A.mark = (uint32_t *)G.ct4_mark.p;
     A.sum = (uint32_t *)G.ct4_sum.p;
     A.hs = (uint32_t *)c->cta_hs.p;
     A.reqA = (uint64_t *)c->cta_req.p;
@@ -2103,8 +2106,9 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
             m->kv.size() + c->cta_claims + c->log_used + 2 * nreqA > m->max_entries)
             ok = false;
     }
-    if (!ok) {   // the scan's marks go
-        if (hipMemsetAsync(A.mark, 0, slots, s) != hipSuccess ||
+    if (!ok) {   // the scan's marks (and delete orders) go
+        if (hipMemsetAsync(A.mark, 0, 4 * slots, s) != hipSuccess ||
+            hipMemsetAsync(A.sum, 0, 4 * slots, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return -EIO;
         return 1;
@@ -2172,9 +2176,11 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     hipStream_t s = (hipStream_t)stream;
     if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value) {
         const int rc = ct_apply_dev(c, in, out, mode, ep_lxc, s);
+        c->n_apply_dev += rc == 0;
         if (rc <= 0)
             return rc;
     }
+    c->n_apply_host++;
     if (int rc = ct_sync(c, s))
         return rc;
     const size_t al = family == 4 ? 4 : 16;

@@ -138,7 +138,7 @@ struct CtaArgs {
     Ct4Slot *ct4;
     CtTimer *tm;
     CtInfo *info;
-    uint8_t *mark;
+    uint32_t *mark;
     uint32_t *sum;
     uint32_t *hs;                // [2n] hit slot per header and stage
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;

@@ -38,7 +38,14 @@ constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIME
                    CT_CLOSE_TIMEOUT = 10, CT_REPORT_INTERVAL = 5;
 constexpr uint32_t RX_CLOSING = 1, TX_CLOSING = 2, SEEN_NON_SYN = 16;   // ct_entry bits
 constexpr uint32_t OP_NONE = 0, OP_HIT = 1, OP_DELETE = 2, OP_CREATE = 3;
-constexpr uint8_t MARK_ORDERED = 1, MARK_FRESH = 2;
+// per-slot marks of one apply: ordered ops; inserted by this apply; a
+// delete among its ops; a create or related-entry write among its ops
+constexpr uint32_t MARK_ORDERED = 1, MARK_FRESH = 2, MARK_DEL = 4, MARK_PUTC = 8;
+__device__ __forceinline__ void mark_or(uint32_t *m, uint32_t bits)
+{
+    if ((*m & bits) != bits)
+        atomicOr(m, bits);
+}
 constexpr uint32_t HS_NONE = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t wave_count(uint32_t *ctr, bool want)
@@ -180,8 +187,14 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 slot = rev ? find4(A, o.x1, o.y1, o.z1, o.w1) : find4(A, o.x2, o.y2, o.z2, o.w2);
                 if (slot != NONE) {
                     const uint32_t clo = (ld16(A.tm + slot).z >> 16) & 3;
-                    if (o.kind == OP_DELETE || o.action == 2 || clo)
-                        A.mark[slot] = MARK_ORDERED;
+                    if (o.kind == OP_DELETE) {
+                        // the entry goes: only its first delete matters
+                        // (k_cta_route), unless a create revives the key
+                        mark_or(&A.mark[slot], MARK_ORDERED | MARK_DEL);
+                        atomicMax(&A.sum[slot], 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1));
+                    } else if (o.action == 2 || clo) {
+                        mark_or(&A.mark[slot], MARK_ORDERED);
+                    }
                 } else {
                     slot = HS_NONE;
                 }
@@ -252,7 +265,7 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, const uint64_t *r
         if (slot == NONE) {
             bool fresh;
             slot = find_or_insert4(A, k.x, k.y, k.z, k.w, &fresh);
-            A.mark[slot] = MARK_ORDERED | (fresh ? MARK_FRESH : 0);
+            mark_or(&A.mark[slot], MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
             first = fresh;
             if (nk < 4) {
                 kk[nk] = k;
@@ -302,13 +315,21 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
         const uint32_t slot = j < 2 * A.n ? A.hs[j] : HS_NONE;
         bool ordered = false;
         if (slot != HS_NONE) {
-            if (A.mark[slot] & MARK_ORDERED) {
+            const uint32_t mk = A.mark[slot];
+            if ((mk & (MARK_DEL | MARK_PUTC)) == MARK_DEL) {
+                // a deleted entry: its first delete stands for all its ops
+                ordered = (uint32_t)(j << 1) == 0xFFFFFFFFu - A.sum[slot];
+            } else if (mk & MARK_ORDERED) {
                 ordered = true;
             } else {
-                const Op o = decode(A, j >> 1, (int)(j & 1));
-                const uint32_t in = o.dir == CT_INGRESS;
-                const uint32_t bits = (in ? o.tfl : o.tfl << 8) | (in ? 1u << 16 : 1u << 17) |
-                                      ((o.is_tcp && !o.syn) ? 1u << 18 : 0u);
+                // the summary needs direction, TCP flags and the close bit only
+                const uint64_t i = j >> 1;
+                const uint32_t mt = A.mt[i];
+                const bool in = !(A.mode == CFC_MODE_EGRESS && (j & 1) == 0);
+                const bool tcp = (mt & 0xFF) == 6;
+                const uint32_t tfl = (tcp && A.tf) ? A.tf[i] : 0u;
+                const uint32_t bits = (in ? tfl : tfl << 8) | (in ? 1u << 16 : 1u << 17) |
+                                      ((tcp && !(mt & CFC_HF_TCP_CLOSE)) ? 1u << 18 : 0u);
                 const uint32_t old = A.sum[slot];
                 if ((old | bits) != old)
                     atomicOr(&A.sum[slot], bits);
@@ -472,6 +493,7 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     }
     A.info[slot] = inf;
     A.mark[slot] = 0;
+    A.sum[slot] = 0;
 }
 
 // ---- finish: the summaries of unordered slots.  With no closing bit set

@@ -789,10 +789,12 @@ def config_c5(seed=5, n_flows=10_000_000, n_prefixes=100_000, n_policy=16384,
     return t, flows
 
 
-def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1):
+def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1,
+               return_new=False):
     """C5 stream into the endpoint: 95% packets of live flows drawn
     Zipf(s) by flow (ESTABLISHED for flows opened from outside, REPLY for
-    flows the endpoint opened), 5% packets of new flows (C2 generator)."""
+    flows the endpoint opened), 5% packets of new flows (C2 generator).
+    return_new: also the mask of the new flows' headers."""
     rng = np.random.default_rng(seed + 777)
     m = int(n * (1 - new_frac))
     pick = _zipf_ranks(rng, len(flows), m, s)
@@ -801,7 +803,10 @@ def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1):
     new = gen_headers_v4(rng, n - m, t.ipcache, local_v4_addrs(t)[:1],
                          local_frac=1.0, proxy_ident=proxy_identities(t))
     h = concat([old, new])
-    return take(h, rng.permutation(n))
+    perm = rng.permutation(n)
+    if return_new:
+        return take(h, perm), perm >= m
+    return take(h, perm)
 
 
 # ------------------------------------------------------------ C1

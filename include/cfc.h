@@ -478,8 +478,11 @@ typedef struct {
     uint32_t endpoints_v6;
     uint32_t prefilter_v6_fix;
     uint32_t prefilter_v6_dyn;
-    uint32_t ct4_entries;       /* CT entries a lookup can reach */
+    uint32_t ct4_entries;       /* CT entries a lookup can reach (as of the
+                                   last host synchronisation) */
     uint32_t ct6_entries;
+    uint32_t ct_apply_device;   /* cfc_ct_apply_* calls run on the device */
+    uint32_t ct_apply_host;     /* ... and on the host */
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

@@ -131,6 +131,8 @@ def test_c5_full_flows(torch):
         np.testing.assert_array_equal(
             np.ascontiguousarray(rec.cpu().numpy()).view(O.EVENT_DT).reshape(-1), orec)
         log(f"C5: batch {k} compared {time.time() - t0:.1f}s")
+    st = dp.stats()
+    assert (st["ct_apply_device"], st["ct_apply_host"]) == (2, 0), st
     compare_counters(dp, pms, o)
     got, want = ct_rows(dp, dp.ct_fds), o.ct_dump()
     assert got.shape == want.shape

@@ -59,6 +59,7 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO,
     metrics = np.array(metricsmap.dump_rows(dp), np.uint64).reshape(-1, 4)
     run_gpu.ct = (ctb, ct_rows(dp, dp.ct_fds)) if use_ct else None
     run_gpu.identity = dp.identity_counters()
+    run_gpu.stats = dp.stats()
     dp.close()
     return act, ver, ide, counters, metrics
 
@@ -383,6 +384,9 @@ def test_c5_conntrack_vs_oracle(torch, mode, apply):
     act, ver = compare_with_oracle(
         torch, t, h, mode, chunks=3,
         ct_apply=L.CT_APPLY_DEVICE if apply == "device" else L.CT_APPLY_HOST)
+    st = run_gpu.stats
+    assert (st["ct_apply_device"], st["ct_apply_host"]) == ((3, 0) if apply == "device"
+                                                             else (0, 3))
     assert (ver == 0).sum() > len(h) // 3
 
 
