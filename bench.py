@@ -212,8 +212,13 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] batch of {n} headers generated ({(n * S_IN) >> 20} MiB)")
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         step()
+        if args.ct_apply:   # each step grows the CT table by its new flows
+            torch.cuda.synchronize()
+            sw = dp.stats()
+            log(f"[rank {rank}] warmup {w}: {sw['ct4_entries']} CT4 entries, apply "
+                f"device {sw['ct_apply_device']} host {sw['ct_apply_host']}")
     torch.cuda.synchronize()
     dp.counters_clear()
     # HIP events recorded by the library on the launch stream around the
@@ -425,6 +430,9 @@ def main():
     }
     if args.ct_apply:   # the step is classify + cfc_ct_apply_v4
         st2 = dp.stats()
+        # the host fallback (table past 3/4 load) is not the measured path
+        assert st2["ct_apply_host"] == 0, ("CT apply left the device path: "
+                                           "fewer --steps", st2)
         res["ct_apply"] = {
             "path_device_calls": st2["ct_apply_device"],
             "path_host_calls": st2["ct_apply_host"],

@@ -879,16 +879,48 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
 // (flow, slice) — on Zipf traffic over millions of flows most of the
 // packets of the tail, ~25M atomics per 64M-header batch.  Partitioned
 // instead, every distinct key of the batch costs one plain read-modify-
-// write of its counters:
-//   A k_ctp_agg      per slice: the LDS table (hot flows collapse), its
-//                    entries and overflow packets staged as records
-//                    {key, packets << 32 | bytes}, counted per key bucket
-//                    (CTP_BUCKET consecutive keys)
-//   B k_scan_*       exclusive scan of the (bucket, slice) counts
-//   C k_ctp_scatter  records into bucket order
-//   D k_ctp_reduce   one workgroup per bucket: LDS sums per key, then its
-//                    counters, which no other workgroup touches
-constexpr uint32_t CTP_BUCKET_BITS = 13, CTP_BUCKET = 1u << CTP_BUCKET_BITS;
+// write of its counters, and every pass over the staged records reads and
+// writes whole runs (an MSD radix partition in two digits, each digit
+// sorted inside a 16384-record chunk in LDS):
+//   A k_acc_agg    per slice: the LDS table (hot flows collapse); its entries
+//                  and the overflow packets staged as 8-byte records, counted
+//                  per (coarse bucket, 16384-record chunk)
+//   B k_scan_*     exclusive scan of the [coarse][chunk] counts: where each
+//                  chunk's run of each coarse bucket goes
+//   C k_acc_part1  per chunk: records sorted by coarse bucket in LDS, written
+//                  as runs into coarse order
+//   D k_acc_plan   the coarse regions cut into 16384-record chunks
+//   E k_acc_part2  per chunk of a coarse region: sorted by fine bucket in
+//                  LDS, written back in place; the chunk's fine offsets kept
+//   F k_acc_reduce one workgroup per fine bucket (CTP_BUCKET keys): gathers
+//                  its run of every chunk of its coarse region, LDS sums per
+//                  key, then its counters, which no other workgroup touches
+// Records: key (26 bits) << 38 | kind << 37 | payload; kind 0: packets (16)
+// << 21 | bytes (21); kind 1: bytes >> 21 (the high part of an LDS entry's
+// byte count, which can pass 2^21).
+constexpr uint32_t CTP_BUCKET_BITS = 12, CTP_BUCKET = 1u << CTP_BUCKET_BITS;
+constexpr uint32_t CTP_MAX_BUCKETS = 16384;    // keys < 2^26 (32M CT slots)
+constexpr uint32_t ACC_FINE_BITS = 7, ACC_FINE = 1u << ACC_FINE_BITS;
+constexpr uint32_t ACC_MAX_COARSE = CTP_MAX_BUCKETS / ACC_FINE;      // 128
+constexpr uint32_t ACC_CHUNK_BITS = 14, ACC_CHUNK = 1u << ACC_CHUNK_BITS;
+constexpr uint32_t ACC_PER_THREAD = ACC_CHUNK / BLOCK;                // 16
+// records per slice: <= COUNT_PER_BLOCK overflow packets, <= CT_LDS_SLOTS
+// entries and as many high parts
+constexpr uint32_t ACC_SLICE_CHUNKS = 5;
+constexpr uint32_t ACC_RCAP = ACC_SLICE_CHUNKS * ACC_CHUNK;
+static_assert(COUNT_PER_BLOCK + 2 * CT_LDS_SLOTS <= ACC_RCAP, "slice records");
+constexpr int ACC_COARSE_SHIFT = 38 + CTP_BUCKET_BITS + ACC_FINE_BITS;   // 57
+constexpr int ACC_BUCKET_SHIFT = 38 + CTP_BUCKET_BITS;                   // 50
+constexpr uint32_t ACC_AGG_LDS =
+    CT_LDS_SLOTS * 12 + ACC_SLICE_CHUNKS * ACC_MAX_COARSE * 4 + 16;
+constexpr uint32_t ACC_SORT_LDS = ACC_CHUNK * 8 + 3 * ACC_MAX_COARSE * 4 + 16;
+constexpr uint32_t ACC_RED_LDS = CTP_BUCKET * 12;
+
+__device__ __forceinline__ uint64_t acc_rec(uint32_t k, uint32_t pk, uint32_t by)
+{
+    return (uint64_t)k << 38 | (uint64_t)pk << 21 | by;
+}
+
 // slot of this lane in an LDS-counted list, one atomic per wave (the lanes
 // of a wave appending together would otherwise serialise on the counter);
 // every lane of the wave must call it
@@ -903,45 +935,54 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t *ctr, bool want)
     base = __shfl(base, (int)lead, 64);
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
 }
-constexpr uint32_t CTP_MAX_BUCKETS = 8192;     // keys < 2^26 (32M CT slots)
-constexpr uint32_t CTP_AGG_LDS = CT_LDS_SLOTS * 12 + CTP_MAX_BUCKETS * 4 + 16;
 // probes before a key becomes a record of its own: the hot flows take their
 // slots early; later keys are mostly the Zipf tail, for which a full table's
 // long probe sequences cost more than the record
 constexpr int CTP_PROBES = 3;
 
-__global__ __launch_bounds__(BLOCK) void k_ctp_agg(const uint32_t *ct_idx,
+// A: slice vw's records into rec[vw * ACC_RCAP ...]; cnt[c * nch + vw *
+// ACC_SLICE_CHUNKS + q] = records of coarse bucket c in the slice's chunk q
+__global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
                                                    const uint32_t *ct_idx2,
                                                    const uint32_t *meta, uint64_t n,
-                                                   uint32_t nbuck, uint32_t *rkey,
-                                                   uint64_t *rval, uint32_t *rcnt,
-                                                   uint32_t *cnt)
+                                                   uint32_t nco, uint64_t *rec,
+                                                   uint32_t *rcnt, uint32_t *cnt)
 {
     uint32_t *keys = reinterpret_cast<uint32_t *>(cfc_smem);
     unsigned long long *vals = reinterpret_cast<unsigned long long *>(keys + CT_LDS_SLOTS);
-    uint32_t *bcnt = reinterpret_cast<uint32_t *>(vals + CT_LDS_SLOTS);
-    uint32_t *nrec = bcnt + CTP_MAX_BUCKETS;
+    uint32_t *hist = reinterpret_cast<uint32_t *>(vals + CT_LDS_SLOTS);
+    uint32_t *nrec = hist + ACC_SLICE_CHUNKS * ACC_MAX_COARSE;
     for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {
         keys[j] = NONE;
         vals[j] = 0;
     }
-    for (uint32_t j = threadIdx.x; j < nbuck; j += BLOCK)
-        bcnt[j] = 0;
+    for (uint32_t j = threadIdx.x; j < ACC_SLICE_CHUNKS * ACC_MAX_COARSE; j += BLOCK)
+        hist[j] = 0;
     if (threadIdx.x == 0)
         *nrec = 0;
     __syncthreads();
     const uint32_t nv = gridDim.x * gridDim.y;
     const uint32_t vw = blockIdx.y * gridDim.x + blockIdx.x;
     const uint32_t *idx = blockIdx.y ? ct_idx2 : ct_idx;
-    uint32_t *rk = rkey + (uint64_t)vw * COUNT_PER_BLOCK;
-    uint64_t *rv = rval + (uint64_t)vw * COUNT_PER_BLOCK;
+    uint64_t *rs = rec + (uint64_t)vw * ACC_RCAP;
     const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
     const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    auto put = [&](uint32_t r, uint64_t v) {
+        rs[r] = v;
+        atomicAdd(&hist[(r >> ACC_CHUNK_BITS) * ACC_MAX_COARSE + (uint32_t)(v >> ACC_COARSE_SHIFT)],
+                  1u);
+    };
+    // the next iteration's key and length are loaded before this one's LDS
+    // work, so their HBM latency overlaps it
+    uint64_t i = start + threadIdx.x;
+    uint32_t nk = i < end ? ld_nt(idx + i) : NONE;
+    uint32_t nm = i < end ? ld_nt(meta + i) : 0u;
     for (uint64_t i0 = start; i0 < end; i0 += BLOCK) {   // (uniform trip count)
-        const uint64_t i = i0 + threadIdx.x;
-        const uint32_t k = i < end ? ld_nt(idx + i) : NONE;
-        const uint32_t len = i < end ? ld_nt(meta + i) >> 16 : 0u;
-        const uint32_t npk = 1;
+        const uint32_t k = nk;
+        const uint32_t len = nm >> 16;
+        i += BLOCK;
+        nk = i < end ? ld_nt(idx + i) : NONE;
+        nm = i < end ? ld_nt(meta + i) : 0u;
         uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
         bool done = k == NONE;
         for (int p = 0; p < CTP_PROBES && !done; p++) {
@@ -953,33 +994,245 @@ __global__ __launch_bounds__(BLOCK) void k_ctp_agg(const uint32_t *ct_idx,
             }
             if (cur == k) {
                 // <= 64512 packets of <= 65535 bytes: {packets << 32 | bytes}
-                atomicAdd(&vals[h], ((unsigned long long)npk << 32) | len);
+                atomicAdd(&vals[h], (1ull << 32) | len);
                 done = true;
             }
             h = (h + 1) & (CT_LDS_SLOTS - 1);
         }
         const uint32_t r = wave_append(nrec, !done);   // a record of its own
-        if (!done) {
-            rk[r] = k;
-            rv[r] = ((uint64_t)npk << 32) | len;
-            atomicAdd(&bcnt[k >> CTP_BUCKET_BITS], 1u);
-        }
+        if (!done)
+            put(r, acc_rec(k, 1, len));
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {   // (uniform)
         const uint32_t k = keys[j];
+        const unsigned long long v = vals[j];
+        const uint32_t by = (uint32_t)v;
         const uint32_t r = wave_append(nrec, k != NONE);
-        if (k == NONE)
-            continue;
-        rk[r] = k;
-        rv[r] = vals[j];
-        atomicAdd(&bcnt[k >> CTP_BUCKET_BITS], 1u);
+        if (k != NONE)
+            put(r, acc_rec(k, (uint32_t)(v >> 32), by & 0x1FFFFFu));
+        const bool hi = k != NONE && by >= (1u << 21);
+        const uint32_t r2 = wave_append(nrec, hi);
+        if (hi)
+            put(r2, (uint64_t)k << 38 | 1ull << 37 | (by >> 21));
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbuck; b += BLOCK)
-        cnt[(uint64_t)b * nv + vw] = bcnt[b];
+    const uint32_t nch = nv * ACC_SLICE_CHUNKS;
+    for (uint32_t j = threadIdx.x; j < nco * ACC_SLICE_CHUNKS; j += BLOCK) {
+        const uint32_t c = j / ACC_SLICE_CHUNKS, q = j % ACC_SLICE_CHUNKS;
+        cnt[(uint64_t)c * nch + vw * ACC_SLICE_CHUNKS + q] = hist[q * ACC_MAX_COARSE + c];
+    }
     if (threadIdx.x == 0)
         rcnt[vw] = *nrec;
+}
+
+// Sort m <= ACC_CHUNK records (r[], this thread's share: index threadIdx.x +
+// i * BLOCK) by digit (v >> shift) & (nd - 1) in LDS: on return buf[0, m)
+// holds them in digit order and base[d] is digit d's first index (base[nd]
+// = m).  The order inside a digit is arbitrary (sums do not care).
+__device__ __forceinline__ void acc_local_sort(const uint64_t (&r)[ACC_PER_THREAD], uint32_t m,
+                                               int shift, uint32_t mask, uint32_t nd,
+                                               uint64_t *buf, uint32_t *cnt, uint32_t *base)
+{
+    for (uint32_t j = threadIdx.x; j < nd; j += BLOCK)
+        cnt[j] = 0;
+    __syncthreads();
+    uint32_t rank[ACC_PER_THREAD];
+#pragma unroll
+    for (uint32_t i = 0; i < ACC_PER_THREAD; i++) {
+        const uint32_t x = threadIdx.x + i * BLOCK;
+        if (x < m)
+            rank[i] = atomicAdd(&cnt[(uint32_t)(r[i] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {   // exclusive scan of <= 128 counts by one wave
+        const uint32_t l = threadIdx.x;
+        const uint32_t a = 2 * l < nd ? cnt[2 * l] : 0u, b = 2 * l + 1 < nd ? cnt[2 * l + 1] : 0u;
+        uint32_t x = a + b;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (l >= (uint32_t)d)
+                x += y;
+        }
+        const uint32_t e = x - a - b;
+        if (2 * l < nd)
+            base[2 * l] = e;
+        if (2 * l + 1 < nd)
+            base[2 * l + 1] = e + a;
+        if (l == 63)
+            base[nd] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < ACC_PER_THREAD; i++) {
+        const uint32_t x = threadIdx.x + i * BLOCK;
+        if (x < m)
+            buf[base[(uint32_t)(r[i] >> shift) & mask] + rank[i]] = r[i];
+    }
+    __syncthreads();
+}
+
+// C: chunk ch = vw * ACC_SLICE_CHUNKS + q of the staged records, sorted by
+// coarse bucket, each bucket's run written at off[c * nch + ch]
+__global__ __launch_bounds__(BLOCK) void k_acc_part1(const uint64_t *rec, const uint32_t *rcnt,
+                                                     const uint32_t *off, uint32_t nch,
+                                                     uint32_t nco, uint64_t *outA)
+{
+    uint64_t *buf = reinterpret_cast<uint64_t *>(cfc_smem);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(buf + ACC_CHUNK);
+    uint32_t *base = cnt + ACC_MAX_COARSE;
+    uint32_t *goff = base + ACC_MAX_COARSE + 1;
+    const uint32_t ch = blockIdx.x, vw = ch / ACC_SLICE_CHUNKS, q = ch % ACC_SLICE_CHUNKS;
+    const uint32_t all = rcnt[vw], lo = q * ACC_CHUNK;
+    if (lo >= all)
+        return;
+    const uint32_t m = min(ACC_CHUNK, all - lo);
+    const uint64_t *src = rec + (uint64_t)vw * ACC_RCAP + lo;
+    for (uint32_t c = threadIdx.x; c < nco; c += BLOCK)
+        goff[c] = off[(uint64_t)c * nch + ch];
+    uint64_t r[ACC_PER_THREAD];
+#pragma unroll
+    for (uint32_t i = 0; i < ACC_PER_THREAD; i++) {
+        const uint32_t x = threadIdx.x + i * BLOCK;
+        r[i] = x < m ? ld_nt(src + x) : 0ull;
+    }
+    acc_local_sort(r, m, ACC_COARSE_SHIFT, ACC_MAX_COARSE - 1, nco, buf, cnt, base);
+#pragma unroll
+    for (uint32_t i = 0; i < ACC_PER_THREAD; i++) {
+        const uint32_t x = threadIdx.x + i * BLOCK;
+        if (x < m) {
+            const uint64_t v = buf[x];
+            const uint32_t c = (uint32_t)(v >> ACC_COARSE_SHIFT);
+            outA[goff[c] + (x - base[c])] = v;
+        }
+    }
+}
+
+// D: plan[c] = first record of coarse bucket c (plan[nco] = all records),
+// plan[nco + 1 + c] = its first fine-sort chunk (plan[2 nco + 1] = chunks);
+// one wave, two coarse buckets per lane (nco <= 128)
+__global__ __launch_bounds__(64) void k_acc_plan(const uint32_t *off, uint32_t nch,
+                                                 uint32_t nco, uint32_t *plan)
+{
+    const uint32_t l = threadIdx.x;
+    const uint32_t total = off[(uint64_t)nco * nch];
+    uint32_t nc[2], a[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint32_t c = 2 * l + j;
+        a[j] = c < nco ? off[(uint64_t)c * nch] : total;
+        const uint32_t b = c + 1 < nco ? off[(uint64_t)(c + 1) * nch] : total;
+        nc[j] = c < nco ? (b - a[j] + ACC_CHUNK - 1) >> ACC_CHUNK_BITS : 0u;
+    }
+    uint32_t x = nc[0] + nc[1];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (l >= (uint32_t)d)
+            x += y;
+    }
+    const uint32_t e = x - nc[0] - nc[1];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint32_t c = 2 * l + j;
+        if (c <= nco) {
+            plan[c] = a[j];
+            plan[nco + 1 + c] = j ? e + nc[0] : e;
+        }
+    }
+}
+
+// E: fine-sort chunk w of the coarse regions: records [lo, lo + m) of
+// coarse bucket c sorted by fine bucket into out[lo ...]; fo[w * (ACC_FINE
+// + 1) + f] = fine bucket f's first index in the chunk
+__global__ __launch_bounds__(BLOCK) void k_acc_part2(const uint64_t *inA, const uint32_t *plan,
+                                                     uint32_t nco, uint64_t *out, uint32_t *fo)
+{
+    uint64_t *buf = reinterpret_cast<uint64_t *>(cfc_smem);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(buf + ACC_CHUNK);
+    uint32_t *base = cnt + ACC_MAX_COARSE;
+    uint32_t *sc = base + ACC_MAX_COARSE + 1;
+    const uint32_t w = blockIdx.x;
+    const uint32_t *pc = plan + nco + 1;
+    if (w >= pc[nco])
+        return;
+    if (threadIdx.x == 0) {   // the coarse bucket holding chunk w
+        uint32_t a = 0, b = nco;   // pc[a] <= w < pc[b]
+        while (b - a > 1) {
+            const uint32_t mid = (a + b) / 2;
+            if (pc[mid] <= w)
+                a = mid;
+            else
+                b = mid;
+        }
+        *sc = a;
+    }
+    __syncthreads();
+    const uint32_t c = *sc;
+    const uint32_t lo = plan[c] + ((w - pc[c]) << ACC_CHUNK_BITS);
+    const uint32_t m = min(ACC_CHUNK, plan[c + 1] - lo);
+    uint64_t r[ACC_PER_THREAD];
+#pragma unroll
+    for (uint32_t i = 0; i < ACC_PER_THREAD; i++) {
+        const uint32_t x = threadIdx.x + i * BLOCK;
+        r[i] = x < m ? ld_nt(inA + lo + x) : 0ull;
+    }
+    acc_local_sort(r, m, ACC_BUCKET_SHIFT, ACC_FINE - 1, ACC_FINE, buf, cnt, base);
+#pragma unroll
+    for (uint32_t i = 0; i < ACC_PER_THREAD; i++) {
+        const uint32_t x = threadIdx.x + i * BLOCK;
+        if (x < m)
+            out[lo + x] = buf[x];
+    }
+    for (uint32_t f = threadIdx.x; f <= ACC_FINE; f += BLOCK)
+        fo[(uint64_t)w * (ACC_FINE + 1) + f] = base[f];
+}
+
+// F: fine bucket b = c * ACC_FINE + f: its run in every chunk of coarse
+// bucket c (eight groups of 128 threads, a chunk each), summed per key in
+// LDS, then added to its counters (acct[2k] packets, acct[2k + 1] bytes)
+__global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, const uint32_t *plan,
+                                                      const uint32_t *fo, uint32_t nco,
+                                                      uint64_t *acct)
+{
+    uint32_t *pk = reinterpret_cast<uint32_t *>(cfc_smem);
+    unsigned long long *by = reinterpret_cast<unsigned long long *>(pk + CTP_BUCKET);
+    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
+        pk[j] = 0;
+        by[j] = 0;
+    }
+    __syncthreads();
+    const uint32_t b = blockIdx.x, c = b >> ACC_FINE_BITS, f = b & (ACC_FINE - 1);
+    const uint32_t *pc = plan + nco + 1;
+    const uint32_t w0 = pc[c], w1 = pc[c + 1];
+    const uint32_t g = threadIdx.x >> 7, t = threadIdx.x & 127;
+    for (uint32_t w = w0 + g; w < w1; w += BLOCK / 128) {
+        const uint32_t lo = plan[c] + ((w - w0) << ACC_CHUNK_BITS);
+        const uint32_t *o = fo + (uint64_t)w * (ACC_FINE + 1) + f;
+        const uint32_t r0 = lo + o[0], r1 = lo + o[1];
+        uint64_t nv = r0 + t < r1 ? ld_nt(recs + r0 + t) : 0ull;
+        for (uint32_t r = r0 + t; r < r1; r += 128) {
+            const uint64_t v = nv;
+            nv = r + 128 < r1 ? ld_nt(recs + r + 128) : 0ull;
+            const uint32_t j = (uint32_t)(v >> 38) & (CTP_BUCKET - 1);
+            if ((v >> 37) & 1) {
+                atomicAdd(&by[j], (v & ((1ull << 37) - 1)) << 21);
+            } else {
+                atomicAdd(&pk[j], (uint32_t)(v >> 21) & 0xFFFFu);
+                atomicAdd(&by[j], v & 0x1FFFFFull);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
+        const uint32_t p = pk[j];
+        if (!p)
+            continue;
+        const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
+        acct[2 * k] += p;
+        acct[2 * k + 1] += by[j];
+    }
 }
 
 // exclusive scan of n u32 (n < 2^32 total): per 4096-element block, block
@@ -1061,82 +1314,6 @@ __global__ __launch_bounds__(BLOCK) void k_scan_add(uint32_t *out, uint64_t n,
     for (int j = 0; j < 4; j++)
         if (b0 + j < n)
             out[b0 + j] += add;
-}
-
-// the scanned offsets transposed to slice-major (one contiguous row per
-// slice for k_ctp_scatter): in[b * nv + v] -> out[v * nb + b]
-__global__ __launch_bounds__(256) void k_transpose_u32(const uint32_t *in, uint32_t *out,
-                                                       uint32_t nb, uint32_t nv)
-{
-    __shared__ uint32_t t[32][33];
-    const uint32_t bx = blockIdx.x * 32, vy = blockIdx.y * 32;
-    const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
-    for (uint32_t r = ty; r < 32; r += 8) {
-        const uint32_t b = bx + r, v = vy + tx;
-        t[r][tx] = (b < nb && v < nv) ? in[(uint64_t)b * nv + v] : 0u;
-    }
-    __syncthreads();
-    for (uint32_t r = ty; r < 32; r += 8) {
-        const uint32_t v = vy + r, b = bx + tx;
-        if (b < nb && v < nv)
-            out[(uint64_t)v * nb + b] = t[tx][r];
-    }
-}
-
-// C: the staged records of slice vw into bucket order: {key within the
-// bucket << 48 | packets << 32 | bytes}; offt: the slice's row of offsets
-__global__ __launch_bounds__(BLOCK) void k_ctp_scatter(const uint32_t *rkey,
-                                                       const uint64_t *rval,
-                                                       const uint32_t *rcnt,
-                                                       const uint32_t *offt, uint32_t nbuck,
-                                                       uint64_t *outr)
-{
-    uint32_t *cur = reinterpret_cast<uint32_t *>(cfc_smem);
-    const uint32_t vw = blockIdx.x;
-    for (uint32_t j = threadIdx.x; j < nbuck; j += BLOCK)
-        cur[j] = offt[(uint64_t)vw * nbuck + j];
-    __syncthreads();
-    const uint32_t m = rcnt[vw];
-    const uint32_t *rk = rkey + (uint64_t)vw * COUNT_PER_BLOCK;
-    const uint64_t *rv = rval + (uint64_t)vw * COUNT_PER_BLOCK;
-    for (uint32_t r = threadIdx.x; r < m; r += BLOCK) {
-        const uint32_t k = rk[r];
-        const uint32_t pos = atomicAdd(&cur[k >> CTP_BUCKET_BITS], 1u);
-        outr[pos] = (uint64_t)(k & (CTP_BUCKET - 1)) << 48 | rv[r];
-    }
-}
-
-// D: bucket b's sums per key, added to its counters (acct[2k], acct[2k+1])
-__global__ __launch_bounds__(BLOCK) void k_ctp_reduce(const uint64_t *recs,
-                                                      const uint32_t *off, uint32_t nv,
-                                                      uint32_t nbuck, const uint32_t *total,
-                                                      uint64_t *acct)
-{
-    uint32_t *pk = reinterpret_cast<uint32_t *>(cfc_smem);
-    unsigned long long *by = reinterpret_cast<unsigned long long *>(pk + CTP_BUCKET);
-    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
-        pk[j] = 0;
-        by[j] = 0;
-    }
-    __syncthreads();
-    const uint32_t b = blockIdx.x;
-    const uint32_t r0 = off[(uint64_t)b * nv];
-    const uint32_t r1 = b + 1 < nbuck ? off[(uint64_t)(b + 1) * nv] : *total;
-    for (uint32_t r = r0 + threadIdx.x; r < r1; r += BLOCK) {
-        const uint64_t v = ld_nt(recs + r);
-        const uint32_t lo = (uint32_t)(v >> 48);
-        atomicAdd(&pk[lo], (uint32_t)(v >> 32) & 0xFFFFu);
-        atomicAdd(&by[lo], v & 0xFFFFFFFFull);
-    }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
-        const uint32_t p = pk[j];
-        if (!p)
-            continue;
-        const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
-        acct[2 * k] += p;
-        acct[2 * k + 1] += by[j];
-    }
 }
 
 __global__ __launch_bounds__(256) void k_add_u64(uint64_t *dst,
@@ -1291,22 +1468,24 @@ WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
         w.ctp_nv = nblk * (egr ? 2u : 1u);
         w.ctp_nbuck = nbuck;
-        const uint64_t cap = (uint64_t)w.ctp_nv * COUNT_PER_BLOCK;
-        const uint64_t nc = (uint64_t)nbuck * w.ctp_nv;
+        w.ctp_nco = (nbuck + ACC_FINE - 1) / ACC_FINE;
+        const uint64_t cap = (uint64_t)w.ctp_nv * ACC_RCAP;
+        const uint64_t nc = (uint64_t)w.ctp_nco * w.ctp_nv * ACC_SLICE_CHUNKS;
+        w.ctp_g2 = (uint32_t)((cap + ACC_CHUNK - 1) / ACC_CHUNK + w.ctp_nco);
         auto take = [&](size_t bytes) {
             off = (off + 255) & ~(size_t)255;
             const size_t at = off;
             off += bytes;
             return at;
         };
-        w.ctp_rkey = take(4 * cap);
-        w.ctp_rval = take(8 * cap);
+        w.ctp_rec = take(8 * cap);
+        w.ctp_recA = take(8 * cap);
         w.ctp_rcnt = take(4ull * w.ctp_nv);
         w.ctp_cnt = take(4 * nc);
         w.ctp_off = take(4 * nc + 4);
-        w.ctp_offt = take(4 * nc);
         w.ctp_bsum = take(4 * ((nc + 4 * BLOCK - 1) / (4 * BLOCK)) + 4);
-        w.ctp_out = take(8 * cap);
+        w.ctp_plan = take(4ull * (2 * w.ctp_nco + 2));
+        w.ctp_fo = take(4ull * w.ctp_g2 * (ACC_FINE + 1));
     }
     w.total = off;
     return w;
@@ -1386,33 +1565,36 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
     const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
     if (ct && T.ct_acct && w.ctp_nv) {
         char *b = reinterpret_cast<char *>(ws);
-        uint32_t *rkey = reinterpret_cast<uint32_t *>(b + w.ctp_rkey);
-        uint64_t *rval = reinterpret_cast<uint64_t *>(b + w.ctp_rval);
+        uint64_t *rec = reinterpret_cast<uint64_t *>(b + w.ctp_rec);
+        uint64_t *recA = reinterpret_cast<uint64_t *>(b + w.ctp_recA);
         uint32_t *rcnt = reinterpret_cast<uint32_t *>(b + w.ctp_rcnt);
         uint32_t *cnt = reinterpret_cast<uint32_t *>(b + w.ctp_cnt);
         uint32_t *off = reinterpret_cast<uint32_t *>(b + w.ctp_off);
         uint32_t *bsum = reinterpret_cast<uint32_t *>(b + w.ctp_bsum);
-        uint32_t *offt = reinterpret_cast<uint32_t *>(b + w.ctp_offt);
-        uint64_t *outr = reinterpret_cast<uint64_t *>(b + w.ctp_out);
+        uint32_t *plan = reinterpret_cast<uint32_t *>(b + w.ctp_plan);
+        uint32_t *fo = reinterpret_cast<uint32_t *>(b + w.ctp_fo);
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
-        const uint64_t nc = (uint64_t)w.ctp_nbuck * w.ctp_nv;
+        const uint32_t nch = w.ctp_nv * ACC_SLICE_CHUNKS;
+        const uint64_t nc = (uint64_t)w.ctp_nco * nch;
         const uint32_t nsb = (uint32_t)((nc + 4 * BLOCK - 1) / (4 * BLOCK));
-        set_lds_limit((const void *)k_ctp_agg, (int)CTP_AGG_LDS);
-        hipLaunchKernelGGL(k_ctp_agg, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
-                           dim3(BLOCK), CTP_AGG_LDS, s, C.ct, C.ct2, meta, n,
-                           w.ctp_nbuck, rkey, rval, rcnt, cnt);
+        set_lds_limit((const void *)k_acc_agg, (int)ACC_AGG_LDS);
+        hipLaunchKernelGGL(k_acc_agg, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
+                           dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta, n,
+                           w.ctp_nco, rec, rcnt, cnt);
         hipLaunchKernelGGL(k_scan_local, dim3(nsb), dim3(BLOCK), 0, s, cnt, off, nc, bsum);
         hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(BLOCK), 0, s, bsum, nsb, off + nc);
         hipLaunchKernelGGL(k_scan_add, dim3(nsb), dim3(BLOCK), 0, s, off, nc, bsum);
-        hipLaunchKernelGGL(k_transpose_u32,
-                           dim3((w.ctp_nbuck + 31) / 32, (w.ctp_nv + 31) / 32), dim3(256), 0,
-                           s, off, offt, w.ctp_nbuck, w.ctp_nv);
-        set_lds_limit((const void *)k_ctp_scatter, (int)(4 * CTP_MAX_BUCKETS));
-        hipLaunchKernelGGL(k_ctp_scatter, dim3(w.ctp_nv), dim3(BLOCK), 4 * w.ctp_nbuck, s,
-                           rkey, rval, rcnt, offt, w.ctp_nbuck, outr);
-        set_lds_limit((const void *)k_ctp_reduce, (int)(12 * CTP_BUCKET));
-        hipLaunchKernelGGL(k_ctp_reduce, dim3(w.ctp_nbuck), dim3(BLOCK), 12 * CTP_BUCKET, s,
-                           outr, off, w.ctp_nv, w.ctp_nbuck, off + nc, T.ct_acct);
+        set_lds_limit((const void *)k_acc_part1, (int)ACC_SORT_LDS);
+        hipLaunchKernelGGL(k_acc_part1, dim3(nch), dim3(BLOCK), ACC_SORT_LDS, s, rec, rcnt,
+                           off, nch, w.ctp_nco, recA);
+        hipLaunchKernelGGL(k_acc_plan, dim3(1), dim3(64), 0, s, off, nch, w.ctp_nco, plan);
+        // the fine sort writes over the staged records (read by part1 only)
+        set_lds_limit((const void *)k_acc_part2, (int)ACC_SORT_LDS);
+        hipLaunchKernelGGL(k_acc_part2, dim3(w.ctp_g2), dim3(BLOCK), ACC_SORT_LDS, s, recA,
+                           plan, w.ctp_nco, rec, fo);
+        set_lds_limit((const void *)k_acc_reduce, (int)ACC_RED_LDS);
+        hipLaunchKernelGGL(k_acc_reduce, dim3(w.ctp_nbuck), dim3(BLOCK), ACC_RED_LDS, s, rec,
+                           plan, fo, w.ctp_nco, T.ct_acct);
     } else if (ct && T.ct_acct) {
         set_lds_limit((const void *)k_ct_count, (int)CT_LDS_BYTES);
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);

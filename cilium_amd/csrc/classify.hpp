@@ -86,10 +86,12 @@ struct LaunchTiming {
 struct WsLayout {
     size_t ctr, ctr2, id, ct, ct2, partial, total;   // byte offsets / size
     uint32_t nblk;                                    // histogram slices
-    // CT accounting by key range (launch_counters): staged records, their
-    // per-(bucket, slice) counts and offsets, the bucketed records
-    size_t ctp_rkey, ctp_rval, ctp_rcnt, ctp_cnt, ctp_off, ctp_offt, ctp_bsum, ctp_out;
-    uint32_t ctp_nv, ctp_nbuck;                       // slices x stages, buckets
+    // CT accounting by key range (launch_counters): staged records (and,
+    // after the fine sort, the same space again), the coarse-sorted records,
+    // per-(coarse bucket, chunk) counts and their scan, the fine-sort plan
+    size_t ctp_rec, ctp_recA, ctp_rcnt, ctp_cnt, ctp_off, ctp_bsum, ctp_plan, ctp_fo;
+    uint32_t ctp_nv, ctp_nbuck, ctp_nco, ctp_g2;      // slices x stages, buckets,
+                                                      // coarse buckets, fine chunks
 };
 WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct);
 CountArgs count_args(uint32_t *ws, const WsLayout &w, const DevTables &T,
