@@ -45,6 +45,15 @@ PREFILTER_DT = np.dtype([("family", "u1"), ("plen", "u1"),
 CT_DT = np.dtype([("family", "u1"), ("lxc", "<i4"), ("any", "u1"),
                   ("tuple", "u1", 38), ("entry", "u1", 56)])
 
+# cilium_lb4_services: struct lb4_key {address, dport, slave} and struct
+# lb4_service {target, port, count, rev_nat_index, weight} (bpf/lib/common.h:
+# 427-439; addresses be32 raw, ports be16 raw); cilium_lb4_reverse_nat: key
+# rev_nat_index, struct lb4_reverse_nat {address, port} (:441-444)
+LB4_DT = np.dtype([("addr", "<u4"), ("dport", "<u2"), ("slave", "<u2"),
+                   ("target", "<u4"), ("port", "<u2"), ("count", "<u2"),
+                   ("rev_nat", "<u2"), ("weight", "<u2")])
+REVNAT4_DT = np.dtype([("index", "<u2"), ("addr", "<u4"), ("port", "<u2")])
+
 
 def htons(x):
     x = np.asarray(x, dtype=np.uint32)
@@ -89,6 +98,8 @@ class Tables:
     # node_config.h (IPV4_CLUSTER_RANGE, IPV4_CLUSTER_MASK, ROUTER_IP); None =
     # the reference's compiled-in values
     node: tuple = None
+    lb4: np.ndarray = None                   # LB4_DT service / backend slots
+    revnat4: np.ndarray = None               # REVNAT4_DT
 
 
 @dataclasses.dataclass
@@ -106,6 +117,9 @@ class Headers:
     # the CT entry's seen flags, conntrack.h:137-185); None = the default
     # the packet builders use: FIN|ACK with HF_TCP_CLOSE, else SYN
     tcpflags: np.ndarray = None
+    # (n,) <u4 skb->hash (what lb4_select_slave reduces modulo the backend
+    # count, lb.h:158-190); None = the engine's flow hash (cfc.h)
+    hash: np.ndarray = None
 
     def __len__(self):
         return len(self.proto)
@@ -114,7 +128,8 @@ class Headers:
         return Headers(self.family, self.saddr[a:b], self.daddr[a:b],
                        self.sport[a:b], self.dport[a:b], self.proto[a:b],
                        self.flags[a:b], self.length[a:b], self.mark[a:b],
-                       None if self.tcpflags is None else self.tcpflags[a:b])
+                       None if self.tcpflags is None else self.tcpflags[a:b],
+                       None if self.hash is None else self.hash[a:b])
 
 
 def tcp_flags_of(h) -> np.ndarray:
@@ -641,7 +656,8 @@ def config_c2_bench(seed=2, n_prefilter=25_000):
 def take(h: Headers, idx) -> Headers:
     return Headers(h.family, h.saddr[idx], h.daddr[idx], h.sport[idx],
                    h.dport[idx], h.proto[idx], h.flags[idx], h.length[idx],
-                   h.mark[idx], None if h.tcpflags is None else h.tcpflags[idx])
+                   h.mark[idx], None if h.tcpflags is None else h.tcpflags[idx],
+                   None if h.hash is None else h.hash[idx])
 
 
 def concat(hs) -> Headers:
@@ -650,8 +666,12 @@ def concat(hs) -> Headers:
     tf = None
     if any(h.tcpflags is not None for h in hs):
         tf = np.concatenate([tcp_flags_of(h) for h in hs])
+    hs_ = None
+    if any(h.hash is not None for h in hs):
+        hs_ = np.concatenate([h.hash if h.hash is not None
+                              else np.zeros(len(h), np.uint32) for h in hs])
     return Headers(f, cat("saddr"), cat("daddr"), cat("sport"), cat("dport"),
-                   cat("proto"), cat("flags"), cat("length"), cat("mark"), tf)
+                   cat("proto"), cat("flags"), cat("length"), cat("mark"), tf, hs_)
 
 
 def reverse(h: Headers) -> Headers:
@@ -905,3 +925,70 @@ def headers_c1(t: Tables, n, seed=1):
     loc = local_v4_addrs(t)[:len(C1_LOCAL)]
     return gen_headers_v4(rng, n, t.ipcache, loc, ports=C1_PORTS, other_proto=0.0,
                           mark_host=0.02, mark_proxy=0.0)
+
+
+# ------------------------------------------------------------ load balancing
+SVC_NET = ip4("172.20.0.0")          # service VIPs: 172.20.x.y
+IPV4_LOOPBACK = 0x1FFFF50A           # bpf/node_config.h:45
+
+
+def lb4_services(rng, t: Tables, n_services=24, loopback=True, n_backend_pool=None):
+    """Services for cilium_lb4_services (pkg/maps/lbmap shape): per service a
+    master slot {vip, dport, slave 0} -> {count, rev_nat_index} and backend
+    slots 1..count -> {target, port}.  Backends are remote addresses inside
+    ipcache prefixes and the local endpoints; with loopback one service's
+    backend is the endpoint itself (LXC_IPV4, lb4_local's loopback case).
+    Edge services: an L3 service (dport 0: every port and ICMP), a service
+    whose master has count 0 (not a service), one with a missing backend
+    slot (the fall-back lookup, DROP_NO_SERVICE), and one whose missing slot
+    the L3 fall-back key holds.  -> (LB4_DT, REVNAT4_DT, vips u32 array,
+    ports be16 array per service, proto per service)."""
+    ipc = t.ipcache[t.ipcache["family"] == 1]
+    loc = local_v4_addrs(t)
+    loc = loc[loc != LXC_IPV4]
+    pool_n = n_backend_pool or 4 * n_services
+    remote = _addr_in_prefix_v4(rng, ipc, rng.integers(0, len(ipc), size=pool_n))
+    rows, rn = [], []
+    vips = np.zeros(n_services, np.uint32)
+    ports = np.zeros(n_services, np.uint16)
+    protos = np.zeros(n_services, np.uint8)
+
+    def row(addr, dport, slave, target=0, port=0, count=0, rev=0, weight=0):
+        r = np.zeros(1, LB4_DT)
+        r["addr"], r["dport"], r["slave"] = addr, dport, slave
+        r["target"], r["port"], r["count"] = target, port, count
+        r["rev_nat"], r["weight"] = rev, weight
+        rows.append(r)
+
+    for k in range(n_services):
+        vip = (SVC_NET + ((k + 1) << 24)) & 0xFFFFFFFF   # 172.20.0.(k+1)
+        vips[k] = vip
+        protos[k] = IPPROTO_UDP if k % 4 == 3 else IPPROTO_TCP
+        dp = htons(int(rng.choice(np.array([80, 443, 53, 8080, 9090]))))
+        l3 = k == 1                                   # L3 service: dport 0
+        ports[k] = 0 if l3 else dp
+        key_dp = 0 if l3 else int(dp)
+        rev = k + 1
+        count = int(rng.integers(1, 5))
+        if k == 2:
+            count = 0                                 # not a service
+        row(vip, key_dp, 0, count=count, rev=rev)
+        rnr = np.zeros(1, REVNAT4_DT)
+        rnr["index"], rnr["addr"], rnr["port"] = rev, vip, key_dp
+        rn.append(rnr)
+        for j in range(1, max(count, 1) + 1):
+            if k == 4 and j == 2:
+                continue                              # missing backend slot
+            tgt = int(loc[j % len(loc)]) if (k % 5 == 0 and len(loc)) else \
+                int(remote[(4 * k + j) % pool_n])
+            if loopback and k == 6 and j == 1:
+                tgt = LXC_IPV4
+            port = int(htons(8000 + k)) if k % 3 == 0 else 0
+            row(vip, key_dp, j, target=tgt, port=port, rev=rev)
+        if k == 5 and count >= 2:
+            # slot 2 lives only under the L3 key: lb4_lookup_slave misses,
+            # the fall-back lb4_lookup_service finds {vip, 0, 2}
+            rows = [r for r in rows if not (int(r["addr"][0]) == vip and
+                                            int(r["slave"][0]) == 2)]
+            row(vip, 0, 2, target=int(remote[0]), count=2, rev=rev)
+    return (np.concatenate(rows), np.concatenate(rn), vips, ports, protos)

@@ -25,6 +25,7 @@
 #define DROP_CT_UNKNOWN_PROTO -137
 #define DROP_MISSED_TAIL_CALL -140
 #define DROP_FRAG_NOSUPPORT -157
+#define DROP_NO_SERVICE -158
 /* UAPI */
 #define TC_ACT_OK 0
 #define TC_ACT_SHOT 2
@@ -35,6 +36,7 @@
 #define METRIC_EGRESS 2
 #define CT_EGRESS 0
 #define CT_INGRESS 1
+#define CT_SERVICE 2
 #define HF_FRAG 1
 #define HF_TCP_CLOSE 2
 #define ENDPOINT_F_HOST 1u
@@ -209,6 +211,7 @@ struct ctent {
 _Static_assert(sizeof(struct ctent) == 56, "ct_entry is 56 bytes");
 #define CTB_RX_CLOSING 1u
 #define CTB_TX_CLOSING 2u
+#define CTB_LB_LOOPBACK 8u
 #define CTB_SEEN_NON_SYN 16u
 /* conntrack.h:31-35, common.h:224, node_config.h:69 */
 #define CT_LIFETIME_TCP 21600u
@@ -229,6 +232,7 @@ _Static_assert(sizeof(struct ctent) == 56, "ct_entry is 56 bytes");
 #define TUPLE_F_OUT 0
 #define TUPLE_F_IN 1
 #define TUPLE_F_RELATED 2
+#define TUPLE_F_SERVICE 4
 enum { CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3 };
 enum { ACTION_UNSPEC = 0, ACTION_CREATE = 1, ACTION_CLOSE = 2 };
 /* per-header CT byte (cfc.h CFC_CT_*): two lookup stages, the second being
@@ -270,7 +274,8 @@ static int ct_keys(int alen, uint16_t owner, const uint8_t *sa,
                    uint16_t dport, int close, int dir, uint8_t k1[CTK],
                    uint8_t k2[CTK], int *action, uint16_t *td, uint16_t *ts)
 {
-    uint8_t fl = dir == CT_INGRESS ? TUPLE_F_OUT : TUPLE_F_IN;
+    uint8_t fl = dir == CT_INGRESS ? TUPLE_F_OUT
+                 : dir == CT_SERVICE ? TUPLE_F_SERVICE : TUPLE_F_IN;
     const uint8_t icmp = alen == 4 ? 1 : 58;
     *action = ACTION_UNSPEC;
     *td = *ts = 0;
@@ -325,6 +330,13 @@ typedef struct {
     uint16_t lxc_id;
 } epinfo;
 
+/* struct lb4_service (common.h:433-439); the key struct lb4_key {address,
+ * dport, slave} (:427-431) is the htab key */
+typedef struct {
+    uint32_t target;
+    uint16_t port, count, rev_nat_index, weight;
+} lb4svc;
+
 struct cfo {
     lpm ipc4, ipc6;
     htab lxc;            /* 20-byte endpoint_key -> index into eps */
@@ -355,6 +367,19 @@ struct cfo {
     uint32_t host_ifindex;     /* node_config.h HOST_IFINDEX */
     uint32_t now;              /* bpf_ktime_get_sec() of the batch (cfo_set_clock) */
     uint32_t *notify_mon;      /* cfo_set_notify_out: per-header monitor lengths */
+    /* service load balancing (bpf/lib/lb.h): cilium_lb4_services and
+     * cilium_lb4_reverse_nat (struct lb4_reverse_nat {address, port},
+     * common.h:441-444, by rev_nat_index) */
+    htab lb4;
+    lb4svc *lb4v;
+    uint32_t lb4_n, lb4_cap;
+    uint32_t *rnat4_addr;
+    uint16_t *rnat4_port;
+    uint8_t *rnat4_ok;
+    /* cfo_set_lb_io: skb->hash per header (NULL: cfo_flow_hash), and the
+     * packet's addresses after the program's rewrites, 3 u32 per header */
+    const uint32_t *hash_in;
+    uint32_t *pkt_out;
 };
 #define ID_SLOTS 65537u
 
@@ -383,6 +408,10 @@ cfo_t *cfo_new(void)
     ht_init(&o->pf4_fix, 8);
     ht_init(&o->pf6_fix, 20);
     ht_init(&o->ct, CTK);
+    ht_init(&o->lb4, 8);
+    o->rnat4_addr = calloc(65536, 4);
+    o->rnat4_port = calloc(65536, 2);
+    o->rnat4_ok = calloc(65536, 1);
     o->idc = calloc((size_t)2 * ID_SLOTS * 4, sizeof(uint64_t));
     /* bpf/node_config.h:30,42-43 */
     static const uint8_t router[16] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0,
@@ -415,6 +444,11 @@ void cfo_free(cfo_t *o)
     ht_free(&o->pf4_fix);
     ht_free(&o->pf6_fix);
     ht_free(&o->ct);
+    ht_free(&o->lb4);
+    free(o->lb4v);
+    free(o->rnat4_addr);
+    free(o->rnat4_port);
+    free(o->rnat4_ok);
     free(o->ct_ents);
     free(o->ct_live);
     free(o->idc);
@@ -517,6 +551,66 @@ int cfo_prefilter_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
         ht_put(family == 1 ? &o->pf4_fix : &o->pf6_fix, k, 1);
     }
     return 0;
+}
+
+/* cilium_lb4_services: key struct lb4_key (8 bytes: address, dport be16,
+ * slave), value struct lb4_service (12 bytes) — lb.h:70-76 */
+int cfo_lb4_service_add(cfo_t *o, const uint8_t key[8], const uint8_t val[12])
+{
+    uint32_t v;
+    if (!ht_get(&o->lb4, key, &v)) {
+        if (o->lb4_n == o->lb4_cap) {
+            o->lb4_cap = o->lb4_cap ? 2 * o->lb4_cap : 64;
+            o->lb4v = realloc(o->lb4v, o->lb4_cap * sizeof(lb4svc));
+        }
+        v = o->lb4_n++;
+        ht_put(&o->lb4, key, v);
+    }
+    lb4svc *e = &o->lb4v[v];
+    memcpy(&e->target, val, 4);
+    memcpy(&e->port, val + 4, 2);
+    memcpy(&e->count, val + 6, 2);
+    memcpy(&e->rev_nat_index, val + 8, 2);
+    memcpy(&e->weight, val + 10, 2);
+    return 0;
+}
+
+/* cilium_lb4_reverse_nat: key rev_nat_index, value struct lb4_reverse_nat
+ * (6 bytes: address, port be16) — lb.h:62-68 */
+int cfo_lb4_revnat_add(cfo_t *o, uint16_t index, const uint8_t val[6])
+{
+    memcpy(&o->rnat4_addr[index], val, 4);
+    memcpy(&o->rnat4_port[index], val + 4, 2);
+    o->rnat4_ok[index] = 1;
+    return 0;
+}
+
+void cfo_set_lb_io(cfo_t *o, const uint32_t *hash, uint32_t *pkt)
+{
+    o->hash_in = hash;
+    o->pkt_out = pkt;
+}
+
+static uint32_t fmix32(uint32_t h)
+{
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return h;
+}
+
+/* the engine's stand-in for the kernel's skb hash when the batch carries
+ * none (cfc.h CFC_FLOW_HASH, oracle.py flow_hash): symmetric in the
+ * 5-tuple, over the packet as it entered the program */
+uint32_t cfo_flow_hash4(uint32_t sa, uint32_t da, uint16_t sport, uint16_t dport,
+                        uint8_t proto)
+{
+    const uint32_t lo = sa < da ? sa : da, hi = sa < da ? da : sa;
+    const uint32_t a = sport, b = dport;
+    const uint32_t pw = (a < b ? a : b) | (a < b ? b : a) << 16;
+    return fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + pw * 0xC2B2AE3Du + proto);
 }
 
 /* ------------------------------------------------------------ datapath */
@@ -724,13 +818,46 @@ static uint32_t ct_hit_entry(struct ctent *e, uint32_t now, int action, int dir,
     return m;
 }
 
-/* ct_lookup{4,6} against the tables as they were when the batch started:
- * sets *res and the policy port (tuple->dport after the lookup: the
- * packet's source port for CT_REPLY, its destination port otherwise). */
+/* ct_state as ct_create{4,6} reads it (common.h:452-461) */
+typedef struct {
+    uint16_t rev_nat, slave;
+    int loopback;
+    uint32_t addr, svc_addr;
+} ctstate_t;
+static int ct_create_entries(const cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
+                             uint32_t len, uint32_t src_sec_id, const ctstate_t *st,
+                             uint8_t keys[3][CTK], struct ctent ents[3]);
+
+/* The entries the egress stage of the current header created (ct_create4:
+ * main, reverse-NAT and ICMP entries): the destination endpoint's lookup
+ * after local delivery runs on the same skb, after those writes — a service
+ * looped back into the sender finds its own reverse-NAT entry
+ * (CT_ESTABLISHED) there. */
+typedef struct {
+    int n;
+    uint8_t key[3][CTK];
+    struct ctent ent[3];
+} fresh_t;
+static _Thread_local fresh_t tl_fresh;
+
+static int64_t fresh_find(const uint8_t k[CTK])
+{
+    for (int j = 0; j < tl_fresh.n; j++)
+        if (!memcmp(tl_fresh.key[j], k, CTK))
+            return j;
+    return -1;
+}
+
+/* ct_lookup{4,6} against the tables as they were when the batch started
+ * (and, for the destination's lookup after local delivery, the entries the
+ * egress stage of the same header created, tl_fresh): sets *res, the policy
+ * port (tuple->dport after the lookup: the packet's source port for
+ * CT_REPLY, its destination port otherwise), the entry hit (*hent, or NULL)
+ * and, when k2out is given, the tuple ct_create would store (k2). */
 static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
                      const uint8_t *da, uint8_t proto, uint16_t sport,
                      uint16_t dport, int close, int dir, int stage, int *res,
-                     uint16_t *pdport)
+                     uint16_t *pdport, const struct ctent **hent, uint8_t *k2out)
 {
     uint8_t k1[CTK], k2[CTK];
     int action;
@@ -739,25 +866,33 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
                       k1, k2, &action, &td, &ts);
     if (ret < 0)
         return ret;
+    if (k2out)
+        memcpy(k2out, k2, CTK);
     /* one or two map lookups in the reference (k1, then k2 on a miss),
      * counted in L whether or not the maps hold entries: ct_lookup4/6 runs
      * them on every tc-path packet (conntrack.h:587-640) */
     tl_lookups++;
     /* *monitor (conntrack.h:221-285, 587-589) against the entry as
      * committed: the batch's own updates are applied afterwards (ct_apply) */
-    int64_t e = ct_find(o, k1);
-    if (e >= 0) {
+    const struct ctent *ent = NULL;
+    int64_t f = stage == 1 ? fresh_find(k1) : -1, e;
+    if (f >= 0 || (e = ct_find(o, k1)) >= 0) {
+        ent = f >= 0 ? &tl_fresh.ent[f] : &o->ct_ents[e];
         *res = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
         *pdport = td;
     } else {
         tl_lookups++;
-        e = ct_find(o, k2);
-        *res = e >= 0 ? CT_ESTABLISHED : CT_NEW;
+        f = stage == 1 ? fresh_find(k2) : -1;
+        if (f >= 0 || (e = ct_find(o, k2)) >= 0)
+            ent = f >= 0 ? &tl_fresh.ent[f] : &o->ct_ents[e];
+        *res = ent ? CT_ESTABLISHED : CT_NEW;
         *pdport = ts;
     }
+    if (hent)
+        *hent = ent;
     uint32_t mon = TRACE_PAYLOAD_LEN;
-    if (e >= 0) {
-        struct ctent copy = o->ct_ents[e];
+    if (ent) {
+        struct ctent copy = *ent;
         mon = ct_hit_entry(&copy, o->now, action, dir, proto == 6, close,
                            proto == 6 ? tl_tcpfl : 0);
     }
@@ -766,6 +901,155 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
     tl_mon[stage] = mon;
     tl_ct |= (uint8_t)((*res | 4) << (4 * stage));
     return 0;
+}
+
+/* ------------------------------------------------------------ load balancer */
+/* IPV4_LOOPBACK (node_config.h:45), raw be32 as stored */
+#define IPV4_LOOPBACK 0x1ffff50au
+
+/* the packet's addresses as the program leaves them (cfo_set_lb_io), and
+ * skb->hash, per header */
+typedef struct {
+    uint32_t sa, da;
+    uint16_t sport, dport;   /* raw be16, as the L4 header holds them */
+} pkt4_t;
+static _Thread_local pkt4_t tl_pkt;
+static _Thread_local uint32_t tl_hash;
+
+/* one cilium_lb4_services lookup */
+static const lb4svc *lb4_get(cfo_t *o, uint32_t addr, uint16_t dport, uint16_t slave)
+{
+    uint8_t k[8];
+    uint32_t v;
+    memcpy(k, &addr, 4);
+    memcpy(k + 4, &dport, 2);
+    memcpy(k + 6, &slave, 2);
+    tl_lookups++;
+    return ht_get(&o->lb4, k, &v) ? &o->lb4v[v] : NULL;
+}
+
+/* lb4_lookup_service (lb.h:604-635): with LB_L4 the key as given while its
+ * dport is set, and on a miss the dport is cleared in the caller's key;
+ * then (LB_L3) the key with dport 0.  An entry counts only with count != 0. */
+static const lb4svc *lb4_lookup_service(cfo_t *o, uint32_t addr, uint16_t *dport,
+                                        uint16_t slave)
+{
+    const lb4svc *v;
+    if (*dport) {
+        v = lb4_get(o, addr, *dport, slave);
+        if (v && v->count)
+            return v;
+        *dport = 0;
+    }
+    v = lb4_get(o, addr, 0, slave);
+    return v && v->count ? v : NULL;
+}
+
+/* What handle_ipv4_from_lxc's service step (bpf_lxc.c:476-492) did to one
+ * header: lb4_extract_key, lb4_lookup_service, lb4_local (lb.h:590-776). */
+typedef struct {
+    int svc;                 /* a service matched */
+    int drop;                /* DROP_NO_SERVICE, or 0 */
+    uint32_t t_da;           /* tuple->daddr for everything after the step */
+    int svc_res;             /* the CT_SERVICE lookup's result */
+    int64_t svc_hit;         /* its entry, or -1 */
+    int reslave;             /* ct_update4_slave ran (backend gone) */
+    uint8_t k_svc[CTK];      /* the CT_SERVICE tuple */
+    /* ct_state_new as lb4_local leaves it for ct_create4; slave0: the
+     * selection the CT_SERVICE entry is created with */
+    uint16_t slave, rev_nat, slave0;
+    int loopback;
+    uint32_t addr, svc_addr;
+} lbx_t;
+
+static void lb4_egress(cfo_t *o, uint16_t owner, uint32_t sa, uint32_t da,
+                       uint8_t proto, int close, lbx_t *x)
+{
+    memset(x, 0, sizeof(*x));
+    x->t_da = da;
+    x->svc_hit = -1;
+    /* lb4_extract_key: key.address = daddr; LB_L4: the L4 dport for TCP and
+     * UDP, none for ICMP, and any other protocol skips the service step
+     * (DROP_UNKNOWN_L4 -> skip_service_lookup) */
+    if (proto != 6 && proto != 17 && proto != 1)
+        return;
+    uint16_t kd = proto == 1 ? 0 : tl_pkt.dport;
+    const lb4svc *svc = lb4_lookup_service(o, da, &kd, 0);
+    if (!svc)
+        return;
+    x->svc = 1;
+    /* lb4_local: ct_lookup4(CT_SERVICE) — the tuple as loaded, flags
+     * TUPLE_F_SERVICE, one lookup (no reverse, conntrack.h:580); a hit is
+     * CT_REPLY (CT_RELATED for ICMP errors) and fills ct_state from the
+     * entry (:235-239) */
+    uint8_t k2[CTK];
+    int action;
+    uint16_t td, ts;
+    if (ct_keys(4, owner, (const uint8_t *)&sa, (const uint8_t *)&da, proto,
+                tl_pkt.sport, tl_pkt.dport, close, CT_SERVICE, x->k_svc, k2,
+                &action, &td, &ts) < 0)
+        return;
+    tl_lookups++;
+    x->svc_hit = ct_find(o, x->k_svc);
+    if (x->svc_hit >= 0) {
+        const struct ctent *e = &o->ct_ents[x->svc_hit];
+        x->svc_res = (x->k_svc[4 + 13] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
+        x->rev_nat = e->rev_nat_index;
+        x->loopback = (e->bits & CTB_LB_LOOPBACK) != 0;
+        x->slave = e->slave;
+    } else {
+        /* lb4_select_slave (lb.h:158-190): hash % count + 1 */
+        x->svc_res = CT_NEW;
+        x->slave = (uint16_t)(tl_hash % svc->count + 1);
+    }
+    x->slave0 = x->slave;
+    /* lb4_lookup_slave, then the fall-back to the service itself with the
+     * key as it stands (slave set) and a new selection */
+    const lb4svc *b = lb4_get(o, da, kd, x->slave);
+    if (!b) {
+        b = lb4_lookup_service(o, da, &kd, x->slave);
+        if (!b) {
+            x->drop = DROP_NO_SERVICE;
+            return;
+        }
+        x->slave = (uint16_t)(tl_hash % b->count + 1);
+        x->reslave = 1;
+    }
+    x->rev_nat = b->rev_nat_index;
+    x->addr = b->target;
+    uint32_t new_sa = 0;
+    if (sa == b->target) {   /* !DISABLE_LOOPBACK_LB (lb.h:753-767) */
+        new_sa = IPV4_LOOPBACK;
+        x->loopback = 1;
+        x->addr = new_sa;
+        x->svc_addr = sa;
+    }
+    if (!x->loopback)
+        x->t_da = b->target;
+    /* lb4_xlate: daddr, the loopback saddr, the L4 dport */
+    tl_pkt.da = b->target;
+    if (new_sa)
+        tl_pkt.sa = new_sa;
+    if (b->port && kd != b->port && (proto == 6 || proto == 17))
+        tl_pkt.dport = b->port;
+}
+
+/* lb4_rev_nat (lb.h:485-588) on the packet for a CT hit with
+ * rev_nat_index: source address (and port) from cilium_lb4_reverse_nat; a
+ * loopback entry also moves the old source into the destination */
+static void lb4_rev_nat(cfo_t *o, const struct ctent *e, uint8_t proto)
+{
+    tl_lookups++;
+    const uint16_t i = e->rev_nat_index;
+    if (!o->rnat4_ok[i])
+        return;
+    const uint16_t port = o->rnat4_port[i];
+    if (port && (proto == 6 || proto == 17) && port != tl_pkt.sport)
+        tl_pkt.sport = port;   /* reverse_map_l4_port */
+    const uint32_t old_sip = tl_pkt.sa;
+    if (e->bits & CTB_LB_LOOPBACK)
+        tl_pkt.da = old_sip;
+    tl_pkt.sa = o->rnat4_addr[i];
 }
 
 /* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
@@ -790,14 +1074,20 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     }
     uint16_t pdport;
     int res;
+    const struct ctent *hit;
     int ret = ct_lookup(o, alen, ct_owner(o, ep->lxc_id), sa, da, proto, sport,
-                        dport, close, CT_INGRESS, stage, &res, &pdport);
+                        dport, close, CT_INGRESS, stage, &res, &pdport, &hit, NULL);
     if (ret < 0) {
         r.verdict = ret;
         r.nt = NT_POLICY << 16 | ep->lxc_id;
         metric(o, ret, METRIC_INGRESS, len);
         return r;
     }
+    /* bpf_lxc.c:946-955: a reply of a load-balanced flow gets its source
+     * translated back (packet only: the verdict does not depend on it) */
+    if (alen == 4 && res == CT_REPLY && hit->rev_nat_index &&
+        !(hit->bits & CTB_LB_LOOPBACK))
+        lb4_rev_nat(o, hit, proto);
     int verdict = policy_can_access(o->pol[ep->lxc_id], src, pdport, proto,
                                     CT_INGRESS, frag, len);
     id_event(o, 0, src, res != CT_REPLY && res != CT_RELATED && verdict < 0, len);
@@ -870,6 +1160,8 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
                            uint32_t daddr, uint8_t proto, uint16_t sport,
                            uint16_t dport, uint8_t hflags, uint32_t len)
 {
+    (void)sport;
+    (void)dport;   /* the packet's ports are tl_pkt's */
     res_t r = {TC_ACT_SHOT, 0, 0, 0};
     const epinfo *self = lxc_lookup(o, 1, (const uint8_t *)&saddr);
     if (!self || self->lxc_id != lxc) { /* is_valid_lxc_src_ipv4, lxc.h:55 */
@@ -877,11 +1169,23 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         metric(o, DROP_INVALID_SIP, METRIC_EGRESS, len);
         return r;
     }
-    const uint8_t *sa = (const uint8_t *)&saddr, *da = (const uint8_t *)&daddr;
+    /* the service step (:476-492); the tuple's daddr may change */
+    lbx_t x;
+    lb4_egress(o, ct_owner(o, lxc), saddr, daddr, proto, hflags & HF_TCP_CLOSE, &x);
+    if (x.drop) {
+        r.verdict = x.drop;
+        metric(o, x.drop, METRIC_EGRESS, len);
+        return r;
+    }
+    const uint32_t tda = x.t_da;   /* orig_dip */
+    const uint8_t *sa = (const uint8_t *)&saddr, *da = (const uint8_t *)&tda;
     uint16_t pdport;
     int res;
-    int ret = ct_lookup(o, 4, ct_owner(o, lxc), sa, da, proto, sport, dport,
-                        hflags & HF_TCP_CLOSE, CT_EGRESS, 0, &res, &pdport);
+    const struct ctent *hit;
+    uint8_t k2[CTK];
+    int ret = ct_lookup(o, 4, ct_owner(o, lxc), sa, da, proto, tl_pkt.sport,
+                        tl_pkt.dport, hflags & HF_TCP_CLOSE, CT_EGRESS, 0, &res,
+                        &pdport, &hit, k2);
     if (ret < 0) {
         r.verdict = ret;
         metric(o, ret, METRIC_EGRESS, len);
@@ -891,7 +1195,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     tl_lookups++;
     if (lpm_lookup(&o->ipc4, da, &label) && label)
         dst = label;
-    else if ((daddr & o->v4_cluster_mask) == o->v4_cluster_range)
+    else if ((tda & o->v4_cluster_mask) == o->v4_cluster_range)
         dst = CLUSTER_ID;
     else
         dst = WORLD_ID;
@@ -904,16 +1208,26 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         metric(o, DROP_POLICY, METRIC_EGRESS, len);
         return r;
     }
-    if (res == CT_NEW)
-        tl_ct |= CTO_CREATE1;                       /* ct_create4, :547-559 */
+    if (res == CT_NEW) {                            /* ct_create4, :547-559 */
+        tl_ct |= CTO_CREATE1;
+        ctstate_t cs = {0, 0, 0, 0, 0};
+        if (x.svc)
+            cs = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr, x.svc_addr};
+        tl_fresh.n = ct_create_entries(o, k2, 4, CT_EGRESS, len, o->seclabel[lxc], &cs,
+                                       tl_fresh.key, tl_fresh.ent);
+    } else if (res >= CT_REPLY && hit->rev_nat_index) {
+        lb4_rev_nat(o, hit, proto);                 /* :565-576 */
+    }
     if (verdict > 0) { /* proxy: redirect(HOST_IFINDEX), TRACE_TO_PROXY */
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
         r.nt = trace_word(OBS_TO_PROXY, lxc, res, tl_mon[0]);
         return r;
     }
+    /* delivery by the packet's destination (lookup_ip4_endpoint, :617) */
+    const uint8_t *pda = (const uint8_t *)&tl_pkt.da;
     tl_lookups++;
-    const epinfo *ep = lxc_lookup(o, 1, da);
+    const epinfo *ep = lxc_lookup(o, 1, pda);
     if (ep) {
         if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST, :668 */
             metric(o, 0, METRIC_EGRESS, len);
@@ -922,10 +1236,13 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
             return r;
         }
         /* ipv4_local_delivery (l3.h:103-131): egress forward metric, then
-         * the destination's policy program with src = SECLABEL */
+         * the destination's policy program with src = SECLABEL, on the
+         * packet as it now is */
         metric(o, 0, METRIC_EGRESS, len);
-        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 4, sa, da, proto, sport,
-                              dport, hflags & HF_FRAG, hflags & HF_TCP_CLOSE,
+        const uint32_t psa = tl_pkt.sa, pd = tl_pkt.da;
+        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 4, (const uint8_t *)&psa,
+                              (const uint8_t *)&pd, proto, tl_pkt.sport,
+                              tl_pkt.dport, hflags & HF_FRAG, hflags & HF_TCP_CLOSE,
                               len, 0, METRIC_EGRESS, 1);
         d.identity = dst;
         return d;
@@ -976,6 +1293,19 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         tl_ct = 0;
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
         tl_mon[0] = tl_mon[1] = 0;
+        tl_fresh.n = 0;
+        tl_pkt.sa = saddr[i];
+        tl_pkt.da = daddr[i];
+        tl_pkt.sport = sport[i];
+        tl_pkt.dport = dport[i];
+        tl_hash = o->hash_in ? o->hash_in[i]
+                             : cfo_flow_hash4(saddr[i], daddr[i], sport[i], dport[i],
+                                              proto[i]);
+        if (o->pkt_out) {   /* (XDP verdicts leave the packet as it is) */
+            o->pkt_out[3 * i] = saddr[i];
+            o->pkt_out[3 * i + 1] = daddr[i];
+            o->pkt_out[3 * i + 2] = sport[i] | (uint32_t)dport[i] << 16;
+        }
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v4(o, saddr[i], daddr[i]);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -1011,6 +1341,11 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             o->notify_out[i] = notify_site(mode, ep_lxc, &r);
         if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
             o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
+        if (o->pkt_out) {
+            o->pkt_out[3 * i] = tl_pkt.sa;
+            o->pkt_out[3 * i + 1] = tl_pkt.da;
+            o->pkt_out[3 * i + 2] = tl_pkt.sport | (uint32_t)tl_pkt.dport << 16;
+        }
     }
 }
 
@@ -1103,7 +1438,7 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
     if (!ret)
         ret = ct_lookup(o, 16, ct_owner(o, lxc), saddr, daddr, proto, sport,
                         dport, flags & HF_TCP_CLOSE, CT_EGRESS, 0, &res,
-                        &pdport);
+                        &pdport, NULL, NULL);
     if (ret) {
         r.verdict = ret;
         metric(o, ret, METRIC_EGRESS, len);
@@ -1195,6 +1530,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         tl_ct = 0;
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
         tl_mon[0] = tl_mon[1] = 0;
+        tl_fresh.n = 0;
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v6(o, sa, da);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -1402,20 +1738,27 @@ static uint32_t ct_hit_update(cfo_t *o, struct ctent *e, int action, int dir,
     return ct_hit_entry(e, o->now, action, dir, is_tcp, syn, flags);
 }
 
-/* ct_create4 / ct_create6 (conntrack.h:615-662, :691-772) without a load
- * balancer (ct_state->addr == 0): the k2 entry plus the ICMP entry that
+/* ct_create4 / ct_create6 (conntrack.h:615-662, :691-772): the k2 entry,
+ * then — when the load balancer left ct_state->addr set (lb4_local) — the
+ * entry reverse NAT needs (daddr / saddr replaced by addr; a loopback flow's
+ * reply tuple with TUPLE_F_IN and svc_addr), then the ICMP entry that
  * relates errors to it, written into the same map.  ct_update_timeout runs
  * with seen_flags.syn = is_tcp — bit 0 of the union, so lower_bits stays 0
- * and a TCP entry keeps seen_non_syn clear (CT_SYN_TIMEOUT).  ipv6_policy
- * derives ct_state_new.rev_nat_index from the low 16 bits of
- * daddr.s6_addr32[3] (bpf_lxc.c:787-788), so IPv6 ingress entries carry
- * it. */
-static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
-                      uint32_t len, uint32_t src_sec_id, uint16_t rev_nat)
+ * and a TCP entry keeps seen_non_syn clear (CT_SYN_TIMEOUT); CT_SERVICE
+ * entries take the tx side like egress ones.  ipv6_policy derives
+ * ct_state_new.rev_nat_index from the low 16 bits of daddr.s6_addr32[3]
+ * (bpf_lxc.c:787-788), so IPv6 ingress entries carry it. */
+static int ct_create_entries(const cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
+                             uint32_t len, uint32_t src_sec_id, const ctstate_t *st,
+                             uint8_t keys[3][CTK], struct ctent ents[3])
 {
+    int n = 0;
     struct ctent e;
     memset(&e, 0, sizeof(e));
-    e.rev_nat_index = rev_nat;
+    e.rev_nat_index = st->rev_nat;
+    e.slave = st->slave;
+    if (st->loopback)
+        e.bits |= CTB_LB_LOOPBACK;
     const uint8_t *t = k2 + 4;
     const int is_tcp = t[2 * alen + 4] == 6;
     ct_upd_timeout(&e, o->now, is_tcp, dir, is_tcp, 0);
@@ -1427,14 +1770,35 @@ static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
         e.tx_bytes = len;
     }
     e.src_sec_id = src_sec_id;
-    ct_put(o, k2, &e);
-    uint8_t ki[CTK];
+    memcpy(keys[n], k2, CTK);
+    ents[n++] = e;
+    if (st->addr && alen == 4) {
+        memcpy(keys[n], k2, CTK);
+        uint8_t *x = keys[n] + 4;
+        memcpy(dir == CT_INGRESS ? x + 4 : x, &st->addr, 4);
+        if (st->loopback) {
+            x[13] = TUPLE_F_IN;
+            memcpy(dir == CT_INGRESS ? x : x + 4, &st->svc_addr, 4);
+        }
+        ents[n++] = e;
+    }
     uint16_t owner;
     memcpy(&owner, k2, 2);
-    ct_key(ki, owner, k2[2], alen, t, t + alen, 0, 0, alen == 4 ? 1 : 58,
+    ct_key(keys[n], owner, k2[2], alen, t, t + alen, 0, 0, alen == 4 ? 1 : 58,
            (uint8_t)(t[2 * alen + 5] | TUPLE_F_RELATED));
     e.bits |= CTB_SEEN_NON_SYN;   /* "For ICMP, there is no SYN" */
-    ct_put(o, ki, &e);
+    ents[n++] = e;
+    return n;
+}
+
+static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
+                      uint32_t len, uint32_t src_sec_id, const ctstate_t *st)
+{
+    uint8_t keys[3][CTK];
+    struct ctent ents[3];
+    const int n = ct_create_entries(o, k2, alen, dir, len, src_sec_id, st, keys, ents);
+    for (int j = 0; j < n; j++)
+        ct_put(o, keys[j], &ents[j]);
 }
 
 /* Fold one classified batch into the CT maps, in header order, as the
@@ -1463,21 +1827,78 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
      * batch (delete, or the ICMP entry a create overwrites) lands on an entry
      * another header of the same batch hits — a hazard (below). */
     uint32_t *hit_idx = hazard ? calloc(o->ct_n + 1, sizeof(uint32_t)) : NULL;
+    /* per (header, stage): the lookup hit an entry the maps did not hold when
+     * the batch started (one the header's own egress stage created): pass 2
+     * counts it, the device did not */
+    uint8_t *fresh = calloc(2 * n + 1, 1);
     for (int pass = 1; pass <= 2; pass++)
     for (size_t i = 0; i < n; i++) {
         if (hazard && pass == 1)
             hazard[i] = 0;
         const uint8_t c = ct[i];
-        if (!(c & (CTO_DONE1 | CTO_DONE2)))
+        /* (lb4_local created its CT_SERVICE entry before it found no backend) */
+        const int no_svc = alen == 4 && mode == CFO_MODE_EGRESS &&
+                           verdict[i] == DROP_NO_SERVICE;
+        if (!(c & (CTO_DONE1 | CTO_DONE2)) && !no_svc)
             continue;
         const uint8_t *sa = saddr + (size_t)alen * i;
         const uint8_t *da = daddr + (size_t)alen * i;
-        const epinfo *dst = lxc_lookup(o, alen == 4 ? 1 : 2, da);
         const int last = (c & CTO_DONE2) ? 1 : 0;
         const int is_tcp = proto[i] == 6;
         const int syn = (flags[i] & HF_TCP_CLOSE) != 0;
         const uint8_t fl = is_tcp && tcpflags ? tcpflags[i] : 0;
+        /* IPv4 egress: the service step again, on the maps as they now are
+         * (its CT_SERVICE entry: created, or hit and updated), and the tuple
+         * and packet it leaves for the stages */
+        lbx_t x;
+        int lbv = 0;
+        uint32_t tda4 = 0, psa4 = 0, pda4 = 0;
+        uint16_t psp = sport[i], pdp = dport[i];
+        if (alen == 4) {
+            memcpy(&tl_pkt.sa, sa, 4);
+            memcpy(&tl_pkt.da, da, 4);
+            tl_pkt.sport = sport[i];
+            tl_pkt.dport = dport[i];
+            tl_hash = o->hash_in ? o->hash_in[i]
+                                 : cfo_flow_hash4(tl_pkt.sa, tl_pkt.da, sport[i],
+                                                  dport[i], proto[i]);
+            tda4 = tl_pkt.da;
+            if (mode == CFO_MODE_EGRESS && ((c & CTO_DONE1) || no_svc)) {
+                lb4_egress(o, ct_owner(o, ep_lxc), tl_pkt.sa, tl_pkt.da, proto[i],
+                           syn, &x);
+                lbv = x.svc;
+                tda4 = x.t_da;
+                if (pass == 2 && lbv) {
+                    uint8_t kk2[CTK];
+                    int act;
+                    uint16_t a_, b_;
+                    (void)ct_keys(4, ct_owner(o, ep_lxc), sa, da, proto[i], sport[i],
+                                  dport[i], syn, CT_SERVICE, x.k_svc, kk2, &act, &a_, &b_);
+                    if (x.svc_hit >= 0) {   /* __ct_lookup on the service entry */
+                        ct_hit_update(o, &o->ct_ents[x.svc_hit], act, CT_SERVICE, is_tcp,
+                                      syn, fl, len[i]);
+                        if (x.reslave)    /* ct_update4_slave */
+                            o->ct_ents[x.svc_hit].slave = x.slave;
+                    } else {
+                        ctstate_t cs = {0, x.slave0, 0, 0, 0};
+                        ct_create(o, x.k_svc, 4, CT_SERVICE, len[i], 0, &cs);
+                        if (x.reslave) {
+                            int64_t ne = ct_find(o, x.k_svc);
+                            if (ne >= 0)
+                                o->ct_ents[ne].slave = x.slave;
+                        }
+                    }
+                }
+            }
+            psa4 = tl_pkt.sa;
+            pda4 = tl_pkt.da;
+            psp = tl_pkt.sport;
+            pdp = tl_pkt.dport;
+        }
+        const epinfo *dst = lxc_lookup(o, alen == 4 ? 1 : 2, alen == 4 ? (const uint8_t *)&pda4 : da);
         for (int s = 0; s < 2; s++) {
+            if (alen == 4 && s == 1)   /* (a reverse NAT may have moved it) */
+                dst = lxc_lookup(o, 1, (const uint8_t *)&pda4);
             const uint8_t cs = (uint8_t)(c >> (4 * s));
             if (!(cs & CTO_DONE1))
                 continue;
@@ -1490,13 +1911,35 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             uint8_t k1[CTK], k2[CTK];
             int action;
             uint16_t td, ts;
-            if (ct_keys(alen, owner, sa, da, proto[i], sport[i], dport[i],
+            /* IPv4: stage 0 of an egress batch looks up (saddr, the service
+             * step's daddr); every other stage the packet as it now is */
+            const uint8_t *ksa = sa, *kda = da;
+            uint16_t ksp = sport[i], kdp = dport[i];
+            if (alen == 4) {
+                ksa = egress_stage ? sa : (const uint8_t *)&psa4;
+                kda = egress_stage ? (const uint8_t *)&tda4 : (const uint8_t *)&pda4;
+                ksp = egress_stage ? tl_pkt.sport : psp;
+                kdp = egress_stage ? tl_pkt.dport : pdp;
+            }
+            if (ct_keys(alen, owner, ksa, kda, proto[i], ksp, kdp,
                         syn, dir, k1, k2, &action, &td, &ts) < 0)
                 continue;
             const int b = cs & 3;
             const int64_t e1 = ct_find(o, k1), e2 = ct_find(o, k2);
+            /* an egress reply's reverse NAT (bpf_lxc.c:565-576) moves the
+             * packet the destination's stage sees */
+            if (alen == 4 && egress_stage && b >= CT_REPLY && e1 >= 0 &&
+                o->ct_ents[e1].rev_nat_index) {
+                lb4_rev_nat(o, &o->ct_ents[e1], proto[i]);
+                psa4 = tl_pkt.sa;
+                pda4 = tl_pkt.da;
+                psp = tl_pkt.sport;
+                pdp = tl_pkt.dport;
+            }
             if (pass == 1) {   /* CONNTRACK_ACCOUNTING of the lookup hits */
                 const int64_t e = b >= CT_REPLY ? e1 : b == CT_ESTABLISHED ? e2 : -1;
+                if (e < 0 && b != CT_NEW)
+                    fresh[2 * i + s] = 1;
                 if (e >= 0) {
                     struct ctent *x = &o->ct_ents[e];
                     if (dir == CT_INGRESS) {
@@ -1520,12 +1963,13 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 hazard[i] = 1;
             /* the monitor length a packet-at-a-time lookup would return */
             uint32_t m = TRACE_PAYLOAD_LEN;
+            const uint32_t cnt = fresh[2 * i + s] ? len[i] : 0;
             if (b == CT_REPLY || b == CT_RELATED) {
                 if (e1 >= 0)
-                    m = ct_hit_update(o, &o->ct_ents[e1], action, dir, is_tcp, syn, fl, 0);
+                    m = ct_hit_update(o, &o->ct_ents[e1], action, dir, is_tcp, syn, fl, cnt);
             } else if (b == CT_ESTABLISHED) {
                 if (e2 >= 0) {
-                    m = ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl, 0);
+                    m = ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl, cnt);
                     if (dropped) {
                         if (hit_idx && hit_idx[e2] > i + 1)
                             hazard[hit_idx[e2] - 1] = 1;  /* hit after delete */
@@ -1548,9 +1992,13 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                         if (ei >= 0 && (size_t)ei < o->ct_n && hit_idx[ei])
                             hazard[i] = 1;
                     }
-                    ct_create(o, k2, alen, dir, len[i], sec,
-                              alen == 16 && dir == CT_INGRESS
-                                  ? (uint16_t)(da[12] | da[13] << 8) : 0);
+                    ctstate_t cs = {alen == 16 && dir == CT_INGRESS
+                                        ? (uint16_t)(da[12] | da[13] << 8) : 0,
+                                    0, 0, 0, 0};
+                    if (egress_stage && lbv)   /* ct_state_new from lb4_local */
+                        cs = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr,
+                                         x.svc_addr};
+                    ct_create(o, k2, alen, dir, len[i], sec, &cs);
                 }
             }
             const uint16_t pdport = q >= CT_REPLY ? td : ts;
@@ -1561,6 +2009,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
         }
     }
     free(hit_idx);
+    free(fresh);
 }
 
 void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,

@@ -132,6 +132,17 @@ void cfo_ct_apply_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
 /* live CT entries as rows of CFO_CT_ROW bytes: u16 owner (0 global, else
  * lxc_id + 1), u8 map (0 TCP, 1 ANY), u8 family, tuple (40 B, zero padded),
  * struct ct_entry (56 B), 4 B pad; sorted by the first 44 bytes. */
+/* service load balancing (bpf/lib/lb.h, IPv4): cilium_lb4_services
+ * (key struct lb4_key 8 B, value struct lb4_service 12 B) and
+ * cilium_lb4_reverse_nat (value struct lb4_reverse_nat 6 B) */
+int cfo_lb4_service_add(cfo_t *o, const uint8_t key[8], const uint8_t val[12]);
+int cfo_lb4_revnat_add(cfo_t *o, uint16_t index, const uint8_t val[6]);
+/* per-header inputs / outputs of the next classify / ct_apply calls: hash =
+ * skb->hash (NULL: cfo_flow_hash4), pkt = the packet's saddr, daddr and
+ * first L4 word after the program's rewrites (3 u32 per header, or NULL) */
+void cfo_set_lb_io(cfo_t *o, const uint32_t *hash, uint32_t *pkt);
+uint32_t cfo_flow_hash4(uint32_t sa, uint32_t da, uint16_t sport, uint16_t dport,
+                        uint8_t proto);
 #define CFO_CT_ROW 104
 size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap);
 

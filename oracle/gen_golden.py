@@ -203,6 +203,16 @@ class RefDatapath:
                                             int(e["tunnel"])))
         for e in t.endpoints:
             L.maps["cilium_lxc"].update(endpoint_key(e), endpoint_value(e))
+        # service load balancing (bpf/lib/lb.h:62-76): cilium_lb4_services
+        # {struct lb4_key: struct lb4_service}, cilium_lb4_reverse_nat
+        if getattr(t, "lb4", None) is not None:
+            for r in t.lb4:
+                b = r.tobytes()
+                L.maps["cilium_lb4_services"].update(b[:8], b[8:20])
+        if getattr(t, "revnat4", None) is not None:
+            for r in t.revnat4:
+                L.maps["cilium_lb4_reverse_nat"].update(
+                    struct.pack("<H", int(r["index"])), r.tobytes()[2:8])
         for p in t.prefilter:
             fam = int(p["family"])
             an = 4 if fam == 1 else 16
@@ -355,9 +365,12 @@ def _derive_egress(h, i, ret, cb, pkt_out, evs, proxy_id):
         # dropped by the destination endpoint's ingress policy
         return ret, cb[2], 0, 0
     if ret == TC_ACT_REDIRECT:
-        dp = _dport_out(pkt_out, l4_offset(h, i))
-        v = dp if dp != int(h.dport[i]) else 0
-        return ret, v, 0, 0
+        # a proxy redirect (bpf_lxc.c:582-604) rewrote the dport to the proxy
+        # port and left a proxy map entry; local delivery and to_host did
+        # neither (a service may have rewritten the dport itself)
+        if proxy_id is None:
+            return ret, 0, 0, 0
+        return ret, _dport_out(pkt_out, l4_offset(h, i)), 0, 0
     # to the stack: TRACE_TO_STACK carries dstID (bpf_lxc.c:687, :390)
     e = _trace(evs, TRACE_TO_STACK)
     if e is not None:
@@ -392,6 +405,13 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     # send_drop_notify left for the drop-notify tail call (drop.h:98-102:
     # exitcode, src << 16 | dst & 0xFFFF, reason, dst_id, ifindex)
     cbs = np.zeros((n, 5), np.int32)
+    # IPv4: the packet's (saddr, daddr, first L4 word) as the program left
+    # it (service translation, reverse NAT, a proxy's port); skb->hash as
+    # the first perf-ring record of the header reports it (get_hash_recalc,
+    # what lb4_select_slave reduced), hash_ok = 0 where none was sent
+    pktv = np.zeros((n, 3), np.uint32)
+    hsh = np.zeros(n, np.uint32)
+    hsh_ok = np.zeros(n, np.uint8)
     ev_hdr, ev_rec = [], []
     # bpf_ktime_get_sec() of each header's run (CLOCK_MONOTONIC seconds,
     # read before and after; 0xFFFFFFFF when a second boundary fell inside)
@@ -405,6 +425,8 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
         if t - int(t) > 0.995:
             time.sleep(int(t) + 1.0005 - t)
         t0 = int(time.clock_gettime(time.CLOCK_MONOTONIC))
+        if h.family == 4:
+            pktv[i] = (h.saddr[i], h.daddr[i], int(h.sport[i]) | int(h.dport[i]) << 16)
         if mode in (MODE_XDP, MODE_FULL):
             ret = H.test_run_xdp(dp.xdp, build(h, i))
             if mode == MODE_XDP or ret == XDP_DROP:
@@ -424,6 +446,13 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
             r = _derive_egress(h, i, ret, cb, po, evs, dp.take_proxy_identity(h.family))
         action[i], verdict[i], ident[i], idmask[i] = r
         cbs[i] = cb
+        if h.family == 4 and len(po) >= 14 + 20:
+            l4 = l4_offset(h, i)
+            pktv[i, 0], pktv[i, 1] = struct.unpack_from("<II", po, 14 + 12)
+            if len(po) >= l4 + 4 and h.proto[i] in (6, 17):
+                pktv[i, 2] = struct.unpack_from("<I", po, l4)[0]
+        if evs:
+            hsh[i], hsh_ok[i] = int(evs[0]["hash"]), 1
         t1 = int(time.clock_gettime(time.CLOCK_MONOTONIC))
         clock[i] = t0 if t0 == t1 else 0xFFFFFFFF
         for e in evs:
@@ -432,15 +461,20 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     assert dp.ring.lost == 0, f"perf ring lost {dp.ring.lost} samples"
     ev = np.array(ev_rec, EV_DT) if ev_rec else np.zeros(0, EV_DT)
     return (action, verdict, ident, idmask, cbs, np.array(ev_hdr, np.uint32), ev,
-            clock)
+            clock, pktv, hsh, hsh_ok)
 
 
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
-    action, verdict, ident, idmask, cbs, ev_hdr, ev, clock = res
+    action, verdict, ident, idmask, cbs, ev_hdr, ev, clock, pkt, hsh, hsh_ok = res
     extra = {}
+    if getattr(t, "lb4", None) is not None:
+        extra.update(lb4=t.lb4, revnat4=t.revnat4, x_pkt=pkt, x_hash=hsh,
+                     x_hash_ok=hsh_ok)
+        if h.hash is not None:
+            extra["h_hash"] = h.hash
     if t.ct is not None:
         # CT before (loaded by the oracle / engine) and after the stream
-        extra = dict(ct=t.ct, x_ct=dp.ct_dump())
+        extra.update(ct=t.ct, x_ct=dp.ct_dump())
     d = dict(mode=np.int32(mode), ep_lxc=np.int32(ep_lxc or 0),
              ipcache=t.ipcache, endpoints=t.endpoints, prefilter=t.prefilter,
              seclabel=np.array(sorted(t.seclabel.items()), np.uint32).reshape(-1, 2),
@@ -930,6 +964,155 @@ def _ct_scenario(family, mode, seed, n=6000):
     return t, h, mode, ep or None, dp
 
 
+# ------------------------------------------------------------ load balancing
+def _lb_setup(seed):
+    """C2-shaped small tables (two endpoints with programs) plus services
+    (synth.lb4_services); the sending endpoint's egress policy allows most
+    backend identities, the other endpoint admits the sender."""
+    t = S.config_c2(seed, n_prefixes=2000, n_policy=400, n_endpoints=2)
+    rng = np.random.default_rng(seed + 1)
+    t.lb4, t.revnat4, vips, ports, protos = S.lb4_services(rng, t)
+    ipc = t.ipcache[t.ipcache["family"] == 1]
+    idents = np.unique(ipc["label"])
+    allow = rng.choice(idents, size=int(0.8 * len(idents)), replace=False)
+    for lxc, pol in t.policy.items():
+        one = np.zeros(len(allow) + 4, S.POLICY_DT)
+        one["identity"][:len(allow)] = allow
+        one["identity"][len(allow):] = [S.WORLD_ID, S.CLUSTER_ID, S.HOST_ID,
+                                       S.EP_SECLABEL]
+        add = np.concatenate([one, one])
+        add["egress"][len(one):] = 1
+        # the sender's own ingress: half the identities (a looped-back flow
+        # is checked against it, with src = its own SECLABEL)
+        add = add[(add["egress"] == 1) | (np.arange(len(add)) % 2 == 0)]
+        have = {(int(r["identity"]), int(r["dport"]), int(r["proto"]),
+                 int(r["egress"])) for r in pol}
+        add = add[[(int(r["identity"]), 0, 0, int(r["egress"])) not in have
+                   for r in add]]
+        t.policy[lxc] = np.concatenate([pol, add])
+    return t, rng, vips, ports, protos
+
+
+def _svc_flows(rng, n, vips, ports, protos, sport_base):
+    """n new flows from the endpoint to service VIPs (unique source ports):
+    80% on the service's port and protocol, 10% another port (the L3
+    fall-back key), 10% ICMP echo"""
+    k = rng.integers(0, len(vips), size=n)
+    h = S.Headers(4, np.full(n, S.LXC_IPV4, np.uint32), vips[k].copy(),
+                  S.htons(sport_base + np.arange(n)), ports[k].copy(),
+                  protos[k].copy(), np.zeros(n, np.uint8),
+                  rng.integers(60, 1500, size=n).astype(np.uint16),
+                  np.zeros(n, np.uint32))
+    z = h.dport == 0
+    h.dport[z] = S.htons(rng.choice(np.array([80, 8443, 22]), size=int(z.sum())))
+    r = rng.random(n)
+    other = r < 0.1
+    h.dport[other] = S.htons(rng.integers(1, 65536, size=int(other.sum())))
+    icmp = r > 0.9
+    h.proto[icmp] = S.IPPROTO_ICMP
+    h.sport[icmp] = 8          # echo request: type 8, code 0
+    h.dport[icmp] = 0
+    return h
+
+
+def sc_lb_egress(n=5000, seed=41):
+    """Service load balancing in the sending endpoint's egress program
+    (bpf_lxc.c:476-576, lb.h): a history stream opens service flows (the
+    reference's CT_SERVICE and reverse-NAT entries), then the test stream:
+    established service flows, new ones, replies of a flow the service
+    looped back into the endpoint itself (lb4_rev_nat with lb_loopback),
+    and plain traffic.  skb->hash is the reference's (from its records)."""
+    import oracle as O
+    t, rng, vips, ports, protos = _lb_setup(seed)
+    hist = _svc_flows(rng, 1200, vips, ports, protos, 20000)
+    plain = S.gen_headers_v4(rng, 300, t.ipcache[t.ipcache["family"] == 1],
+                             S.local_v4_addrs(t), local_frac=0.3, mark_host=0,
+                             mark_proxy=0, src_fixed=S.LXC_IPV4, frag=0)
+    hist = S.concat([hist, plain])
+    dp = RefDatapath(t)
+    hres = run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    # test stream
+    parts = []
+    est = S.take(hist, rng.integers(0, 1200, size=int(n * 0.45)))
+    est.flags[(rng.random(len(est)) < 0.05) & (est.proto == S.IPPROTO_TCP)] |= \
+        np.uint8(S.HF_TCP_CLOSE)
+    parts.append(est)
+    parts.append(_svc_flows(rng, int(n * 0.35), vips, ports, protos, 40000))
+    # the looped-back flows: the endpoint, as the backend, answers the
+    # client address it saw (IPV4_LOOPBACK) from its translated port
+    pk = hres[8]
+    lb = (pk[:, 0] == S.IPV4_LOOPBACK) & (hres[0] != 2)
+    if lb.any():
+        src = S.take(hist, np.flatnonzero(lb))
+        pr = pk[lb]
+        m = max(1, int(n * 0.05))
+        pick = rng.integers(0, len(src), size=m)
+        rep = S.Headers(4, np.full(m, S.LXC_IPV4, np.uint32),
+                        np.full(m, S.IPV4_LOOPBACK, np.uint32),
+                        (pr[pick, 2] >> 16).astype(np.uint16),
+                        (pr[pick, 2] & 0xFFFF).astype(np.uint16),
+                        src.proto[pick].copy(), np.zeros(m, np.uint8),
+                        src.length[pick].copy(), np.zeros(m, np.uint32))
+        parts.append(rep)
+    parts.append(S.gen_headers_v4(rng, int(n * 0.15), t.ipcache[t.ipcache["family"] == 1],
+                                  S.local_v4_addrs(t), local_frac=0.3, mark_host=0,
+                                  mark_proxy=0, src_fixed=S.LXC_IPV4, frag=0))
+    h = S.concat(parts)
+    h = S.take(h, rng.permutation(len(h)))
+    h.hash = None
+    for _ in range(6):
+        o = O.Oracle(t)
+        oa, ov, oi, ct = o.classify(h, MODE_EGRESS, S.EP_LXC_ID, want_ct=True)
+        hz = o.ct_apply(h, MODE_EGRESS, S.EP_LXC_ID, oi, ov, ct, hazard=True)
+        if not hz.any():
+            break
+        h = _keep(h, hz == 0)
+    assert not hz.any()
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
+def sc_lb_reply(n=4000, seed=43):
+    """Replies of load-balanced flows arriving from the backends (from-netdev,
+    then the client endpoint's ipv4_policy): CT_REPLY on the entries the
+    egress path created, source translated back to the service address
+    (lb4_rev_nat, bpf_lxc.c:946-955); plus new inbound traffic."""
+    t, rng, vips, ports, protos = _lb_setup(seed)
+    hist = _svc_flows(rng, 1500, vips, ports, protos, 20000)
+    dp = RefDatapath(t)
+    hres = run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    pk = hres[8]
+    fw = (hres[0] != 2) & (pk[:, 0] == S.LXC_IPV4) & (hist.proto != S.IPPROTO_ICMP)
+    idx = np.flatnonzero(fw)
+    m = int(n * 0.7)
+    pick = idx[rng.integers(0, len(idx), size=m)]
+    rep = S.Headers(4, pk[pick, 1].copy(), pk[pick, 0].copy(),
+                    (pk[pick, 2] >> 16).astype(np.uint16),
+                    (pk[pick, 2] & 0xFFFF).astype(np.uint16),
+                    hist.proto[pick].copy(), np.zeros(m, np.uint8),
+                    rng.integers(60, 1500, size=m).astype(np.uint16),
+                    np.zeros(m, np.uint32))
+    rep.flags[(rng.random(m) < 0.05) & (rep.proto == S.IPPROTO_TCP)] |= np.uint8(S.HF_TCP_CLOSE)
+    new = S.gen_headers_v4(rng, n - m, t.ipcache[t.ipcache["family"] == 1],
+                           S.local_v4_addrs(t)[:1], local_frac=1.0, mark_host=0,
+                           mark_proxy=0, frag=0)
+    h = S.concat([rep, new])
+    h = S.take(h, rng.permutation(len(h)))
+    import oracle as O
+    for _ in range(6):
+        o = O.Oracle(t)
+        oa, ov, oi, ct = o.classify(h, MODE_INGRESS, 0, want_ct=True)
+        hz = o.ct_apply(h, MODE_INGRESS, 0, oi, ov, ct, hazard=True)
+        if not hz.any():
+            break
+        h = _keep(h, hz == 0)
+    assert not hz.any()
+    return t, h, MODE_INGRESS, None, dp
+
+
 def _keep(h, m):
     return S.take(h, m)
 
@@ -952,6 +1135,8 @@ SCENARIOS = {
     "ct_egress_v4": lambda: _ct_scenario(4, MODE_EGRESS, 22),
     "ct_ingress_v6": lambda: _ct_scenario(6, MODE_INGRESS, 23),
     "ct_egress_v6": lambda: _ct_scenario(6, MODE_EGRESS, 24),
+    "lb_egress_v4": sc_lb_egress,
+    "lb_reply_v4": sc_lb_reply,
 }
 
 

@@ -127,6 +127,10 @@ def lib():
         L.cfo_node_config.restype = None
         L.cfo_set_clock.argtypes = [vp, ctypes.c_uint32]
         L.cfo_set_clock.restype = None
+        L.cfo_lb4_service_add.argtypes = [vp, vp, vp]
+        L.cfo_lb4_revnat_add.argtypes = [vp, ctypes.c_uint16, vp]
+        L.cfo_set_lb_io.argtypes = [vp, vp, vp]
+        L.cfo_set_lb_io.restype = None
         _lib = L
     return _lib
 
@@ -183,6 +187,16 @@ class Oracle:
             self.ct_add(t.ct)
         if getattr(t, "node", None) is not None:
             self.node_config(*t.node)
+        if getattr(t, "lb4", None) is not None:
+            for r in np.asarray(t.lb4):
+                b = r.tobytes()
+                k, v = _u8p(np.frombuffer(b[:8], np.uint8)), _u8p(np.frombuffer(b[8:20], np.uint8))
+                L.cfo_lb4_service_add(h, ctypes.cast(k[0], ctypes.c_void_p),
+                                      ctypes.cast(v[0], ctypes.c_void_p))
+        if getattr(t, "revnat4", None) is not None:
+            for r in np.asarray(t.revnat4):
+                v, keep = _u8p(np.frombuffer(r.tobytes()[2:8], np.uint8))
+                L.cfo_lb4_revnat_add(h, int(r["index"]), ctypes.cast(v, ctypes.c_void_p))
 
     def node_config(self, v4_cluster_range, v4_cluster_mask, router_ip6,
                     host_ifindex=1):
@@ -212,12 +226,20 @@ class Oracle:
                 c(hdr.length, np.uint16), c(hdr.mark, np.uint32),
                 c(_tcp_flags(hdr), np.uint8)]
 
+    def _lb_io(self, hdr, pkt=None):
+        hs = getattr(hdr, "hash", None)
+        hs = None if hs is None or hdr.family != 4 else np.ascontiguousarray(hs, np.uint32)
+        self._lb_keep = hs
+        self.L.cfo_set_lb_io(self.h, _p(hs), _p(pkt))
+
     def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False,
-                 want_ct=False, apply_ct=False, want_notify=False):
-        """-> (action, verdict, identity[, lookups][, ct][, notify]).
+                 want_ct=False, apply_ct=False, want_notify=False, want_pkt=False):
+        """-> (action, verdict, identity[, lookups][, ct][, notify][, pkt]).
         apply_ct folds the batch's CT creates/deletes into the oracle's CT
         maps afterwards (what the engine's cfc_ct_apply does); notify is the
-        drop-notify site word per header (res_t.nt in cfc_oracle.c)."""
+        drop-notify site word per header (res_t.nt in cfc_oracle.c); pkt
+        (IPv4) the packet's (saddr, daddr, sport | dport << 16) after the
+        service translation and reverse NAT, (n, 3) u32."""
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
@@ -232,10 +254,13 @@ class Oracle:
         fn = self.L.cfo_classify_v4 if hdr.family == 4 else self.L.cfo_classify_v6
         nt = np.zeros(n, np.uint32) if want_notify else None
         self.mon = np.zeros(n, np.uint32)
+        pkt = np.zeros((n, 3), np.uint32) if want_pkt else None
         self.L.cfo_set_notify_out(self.h, _p(nt), _p(self.mon))
+        self._lb_io(hdr, pkt)
         fn(self.h, mode, ep_lxc, n, *[_p(a) for a in arrs], _p(act), _p(ver),
            _p(ide), _p(lk), _p(ct), nthreads)
         self.L.cfo_set_notify_out(self.h, None, None)
+        self.L.cfo_set_lb_io(self.h, None, None)
         if apply_ct:
             self.ct_apply(hdr, mode, ep_lxc, ide, ver, ct)
         out = (act, ver, ide)
@@ -245,6 +270,8 @@ class Oracle:
             out += (ct,)
         if want_notify:
             out += (nt,)
+        if want_pkt:
+            out += (pkt,)
         return out
 
     def events(self, hdr, mode, ep_lxc, verdict, identity, words, drops=True,
@@ -272,7 +299,8 @@ class Oracle:
         ln = np.asarray(hdr.length, np.uint32)[idx]
         own = sec[ep_lxc] if mode == MODE_EGRESS else 0
         r = np.zeros(len(idx), EVENT_DT)
-        r["hash"] = flow_hash(hdr, idx)
+        hs = getattr(hdr, "hash", None)
+        r["hash"] = flow_hash(hdr, idx) if hs is None else np.asarray(hs, np.uint32)[idx]
         r["len_orig"] = ln
         # drops: cb[1] = src << 16 | dst & 0xFFFF, both labels 16 bits
         d = k <= 3
@@ -337,9 +365,11 @@ class Oracle:
         fn = self.L.cfo_ct_apply_v4 if hdr.family == 4 else self.L.cfo_ct_apply_v6
         c = np.ascontiguousarray
         mon = c(self.mon, np.uint32) if trace_hazards else None
+        self._lb_io(hdr)
         fn(self.h, mode, ep_lxc, len(hdr), *[_p(a) for a in arrs[:7]],
            _p(arrs[8]), _p(c(identity, np.uint32)), _p(c(verdict, np.int32)),
            _p(c(ct, np.uint8)), _p(mon), _p(hz))
+        self.L.cfo_set_lb_io(self.h, None, None)
         return hz
 
     def ct_dump(self):

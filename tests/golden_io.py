@@ -27,12 +27,22 @@ class Golden:
         self.tables = S.Tables(d["ipcache"], d["endpoints"], policy,
                                d["prefilter"], seclabel,
                                d["ct"] if "ct" in d.files else None)
+        if "lb4" in d.files:   # service load balancing (LB4_DT, REVNAT4_DT)
+            self.tables.lb4 = d["lb4"]
+            self.tables.revnat4 = d["revnat4"]
         # CT maps after the stream, oracle row format (None: no CT state)
         self.ct_after = d["x_ct"] if "x_ct" in d.files else None
         self.headers = S.Headers(int(d["h_family"]), d["h_saddr"], d["h_daddr"],
                                  d["h_sport"], d["h_dport"], d["h_proto"],
                                  d["h_flags"], d["h_length"], d["h_mark"],
                                  d["h_tcpflags"] if "h_tcpflags" in d.files else None)
+        # skb->hash of each header as the reference's records reported it
+        # (lb4_select_slave's input), and the packet the program left:
+        # (saddr, daddr, first L4 word); None in fixtures without a service
+        self.hash_ok = d["x_hash_ok"] if "x_hash_ok" in d.files else None
+        if self.hash_ok is not None:
+            self.headers.hash = d["x_hash"]
+        self.pkt = d["x_pkt"] if "x_pkt" in d.files else None
         # the cilium_events perf-ring samples (trace_notify / drop_notify,
         # 32 bytes each, EVENT_DT) and the header of each; None in older
         # fixtures

@@ -244,3 +244,51 @@ def test_events_pin_identities():
         if g.mode != O.MODE_EGRESS:   # proxy redirects: the proxy map
             prox = (g.action == 7) & (g.verdict > 0)
             assert (g.idmask[prox] == 0xFFFFFFFF).all(), name
+
+
+LB_NAMES = [n for n in NAMES if G.Golden(n).pkt is not None]
+
+
+def test_lb_goldens_cover_the_service_path():
+    """The load-balancing fixtures exercise the service translation, the
+    loopback case, DROP_NO_SERVICE, and reverse NAT in both directions."""
+    assert {"lb_egress_v4", "lb_reply_v4"} <= set(LB_NAMES)
+    g = G.Golden("lb_egress_v4")
+    vips = set(int(x) for x in g.tables.lb4["addr"])
+    assert (g.pkt[:, 1] != g.headers.daddr).sum() > 1000        # translated
+    assert (g.pkt[:, 0] == S.IPV4_LOOPBACK).any()               # loopback
+    assert (g.verdict == -158).any()                            # no backend
+    assert any(int(x) in vips for x in g.pkt[:, 0])             # egress rev NAT
+    r = G.Golden("lb_reply_v4")
+    assert sum(int(x) in vips for x in r.pkt[:, 0]) > 1000      # ingress rev NAT
+
+
+@pytest.mark.parametrize("name", LB_NAMES)
+def test_oracle_packets_match_reference(name):
+    """The packet each program left (service translation lb4_xlate, reverse
+    NAT lb4_rev_nat: addresses and L4 ports) against the reference's output
+    packet, for every header that was not dropped or handed to a proxy (a
+    proxy redirect's port is the verdict itself).  skb->hash comes from the
+    reference's records, so backend selection is the reference's."""
+    g = G.Golden(name)
+    o = O.Oracle(g.tables)
+    act, ver, ide, pkt = o.classify(g.headers, g.mode, g.ep_lxc, want_pkt=True)
+    keep = (g.action != 2) & ~((g.action == 7) & (g.verdict > 0))
+    np.testing.assert_array_equal(pkt[keep], g.pkt[keep])
+
+
+@pytest.mark.parametrize("name", LB_NAMES)
+def test_record_hash_is_the_batch_hash(name):
+    """With skb->hash in the batch, every record carries it (the one field
+    test_oracle_events_match_reference leaves out otherwise)."""
+    g = G.Golden(name)
+    o = O.Oracle(g.tables)
+    act, ver, ide, words = o.classify(g.headers, g.mode, g.ep_lxc, want_notify=True)
+    rec, idx = o.events(g.headers, g.mode, g.ep_lxc, ver, ide, words)
+    first = {}
+    for j, i in enumerate(g.ev_hdr):
+        first.setdefault(int(i), int(g.ev["hash"][j]))
+    got = {int(i): int(h) for i, h in zip(idx, rec["hash"])}
+    common = set(first) & set(got)
+    assert len(common) > 1000
+    assert all(first[i] == got[i] for i in common)
