@@ -43,21 +43,25 @@ class CfcError(OSError):
     pass
 
 
+_HDR = [("saddr", ctypes.c_void_p), ("daddr", ctypes.c_void_p),
+        ("ports", ctypes.c_void_p), ("meta", ctypes.c_void_p),
+        ("mark", ctypes.c_void_p), ("tcp_flags", ctypes.c_void_p),
+        ("n", ctypes.c_uint64)]
+
+
 class HdrV4(ctypes.Structure):
-    _fields_ = [("saddr", ctypes.c_void_p), ("daddr", ctypes.c_void_p),
-                ("ports", ctypes.c_void_p), ("meta", ctypes.c_void_p),
-                ("mark", ctypes.c_void_p), ("tcp_flags", ctypes.c_void_p),
-                ("n", ctypes.c_uint64)]
+    _fields_ = _HDR + [("hash", ctypes.c_void_p)]
 
 
 class HdrV6(ctypes.Structure):
-    _fields_ = HdrV4._fields_
+    _fields_ = _HDR
 
 
 class Out(ctypes.Structure):
     _fields_ = [("verdict", ctypes.c_void_p), ("identity", ctypes.c_void_p),
                 ("action", ctypes.c_void_p), ("ct", ctypes.c_void_p),
-                ("notify", ctypes.c_void_p)]
+                ("notify", ctypes.c_void_p), ("pkt_saddr", ctypes.c_void_p),
+                ("pkt_daddr", ctypes.c_void_p), ("pkt_ports", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):

@@ -9,6 +9,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <unordered_set>
 #include <type_traits>
 #include <vector>
 
@@ -115,8 +116,14 @@ struct GEp {           // endpoints + policy (+ the counter layout)
     DevBuf ep_info;
     uint64_t bytes = 0;
 };
+struct GLb {           // load balancing: services, reverse NAT
+    DevBuf lb4, rnat4;
+    uint32_t lb4_mask = 0, n_lb4 = 0;
+    uint64_t bytes = 0;
+};
 struct GCt {           // conntrack
     DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
+    DevBuf ct4_lb;                        // per-slot LB state (with a load balancer)
     DevBuf ct4_info, ct4_mark, ct4_sum;   // device CT apply state (ctapply.hip)
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
     std::vector<Ct6Slot> ct6_host;
@@ -133,6 +140,7 @@ struct Epoch {
     std::shared_ptr<GPf> pf;
     std::shared_ptr<GEp> ep;
     std::shared_ptr<GCt> ct;
+    std::shared_ptr<GLb> lb;
     DevTables T{};
     cfc_stats st{};
 };
@@ -162,7 +170,7 @@ struct cfc_ctx {
 
     std::shared_ptr<Epoch> epoch;
     uint64_t epoch_seq = 0;
-    uint64_t built_sig[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};   // per group
+    uint64_t built_sig[6] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull, ~0ull};   // per group
     uint32_t id_cover = 1;   // identity histogram ranges (reserved + ipcache)
     std::vector<Retired> retired;
     std::vector<hipStream_t> streams;   // streams launched on since the last swap
@@ -206,10 +214,11 @@ struct cfc_ctx {
 namespace {
 
 // Signatures of the maps behind each table group, bit g of GROUP_*
-// (0 ipcache v4, 1 prefilter, 2 endpoints + policy, 3 CT, 4 ipcache v6).
+// (0 ipcache v4, 1 prefilter, 2 endpoints + policy, 3 CT, 4 ipcache v6,
+// 5 load balancing).
 // Structural changes (inserts, deletes) count; a value overwritten in place
 // does not where a commit can patch it (ipcache v6 labels, policy entries).
-constexpr int NGROUPS = 5;
+constexpr int NGROUPS = 6;
 void group_sigs(cfc_ctx *c, uint64_t sig[NGROUPS])
 {
     for (int g = 0; g < NGROUPS; g++)
@@ -239,6 +248,12 @@ void group_sigs(cfc_ctx *c, uint64_t sig[NGROUPS])
             // (patch_ct); the table is rebuilt when it fills up
             mix(3, id); mix(3, m->sgen[0]);
             mix(2, id);   // endpoints see which CT maps exist
+            break;
+        case ROLE_LB4_SVC: case ROLE_LB4_RNAT:
+            mix(5, id); mix(5, m->gen);
+            // the CT table carries each entry's LB state while a load
+            // balancer is configured
+            mix(3, m->kv.empty() ? 0 : 1);
             break;
         default:
             break;
@@ -680,13 +695,25 @@ std::shared_ptr<GEp> build_ep(cfc_ctx *c, HostImage &img, const std::vector<Map 
     return g;
 }
 
+std::shared_ptr<GLb> build_lbg(const HostImage &img, hipStream_t s, int *rc)
+{
+    auto g = std::make_shared<GLb>();
+    if ((*rc = upload_vec(g->lb4, img.lb4, s)) || (*rc = upload_vec(g->rnat4, img.rnat4, s)))
+        return nullptr;
+    g->lb4_mask = img.lb4_mask;
+    g->n_lb4 = img.n_lb4;
+    g->bytes = 16ull * img.lb4.size() + 8ull * img.rnat4.size();
+    return g;
+}
+
 std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hipStream_t s,
                                int *rc)
 {
     auto g = std::make_shared<GCt>();
     if ((*rc = upload_vec(g->ct4, img.ct4, s)) || (*rc = upload_vec(g->ct6, img.ct6, s)) ||
         (*rc = upload_vec(g->ct4_tm, img.ct4_tm, s)) ||
-        (*rc = upload_vec(g->ct6_tm, img.ct6_tm, s)))
+        (*rc = upload_vec(g->ct6_tm, img.ct6_tm, s)) ||
+        (*rc = upload_vec(g->ct4_lb, img.ct4_lb, s)))
         return nullptr;
     const size_t nslots = img.ct4.size() + img.ct6.size();
     if (nslots && (*rc = g->ct_acct.zeros(32 * nslots, s)))
@@ -708,7 +735,7 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     g->n_ct4 = img.n_ct4;
     g->n_ct6 = img.n_ct6;
     g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
-               48ull * nslots + 16ull * n4;
+               48ull * nslots + 16ull * n4 + 16ull * img.ct4_lb.size();
     g->ct4_host = std::move(img.ct4);
     g->ct6_host = std::move(img.ct6);
     return g;
@@ -724,6 +751,7 @@ void assemble(Epoch &E)
     const GPf &P = *E.pf;
     const GEp &D = *E.ep;
     const GCt &C = *E.ct;
+    const GLb &B = *E.lb;
     T.l4d = (const uint4 *)I.l4d.p;
     T.l4c = (const uint32_t *)I.l4c.p;
     T.l4l = (const uint64_t *)I.l4l.p;
@@ -761,10 +789,14 @@ void assemble(Epoch &E)
     T.ct6_mask = C.ct6_mask;
     T.ct6_probe = C.ct6_probe;
     T.ct6_acct_base = (uint32_t)C.ct4_host.size();
+    T.lb4 = B.n_lb4 ? (const uint4 *)B.lb4.p : nullptr;
+    T.lb4_mask = B.lb4_mask;
+    T.rnat4 = (const uint2 *)B.rnat4.p;
+    T.ct4_lb = T.ct4 ? (const uint4 *)C.ct4_lb.p : nullptr;
     cfc_stats &st = E.st;
     st = cfc_stats{};
     st.epoch = E.id;
-    st.device_bytes = I.bytes + I6.bytes + P.bytes + D.bytes + C.bytes;
+    st.device_bytes = I.bytes + I6.bytes + P.bytes + D.bytes + C.bytes + B.bytes;
     st.ipcache_v4_prefixes = I.n_prefix4;
     st.lpm4_tbl8_groups = I.tbl8_groups;
     st.policy_entries = T.n_ctr;
@@ -893,6 +925,16 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
         for (auto &t : m->touched) {
             any[f]++;
             ins[f] += (t.second & TOUCH_INSERT) ? 1 : 0;
+            // an entry with LB state into a table without the LB state
+            // array: rebuilt with it
+            if (!f && !G.ct4_lb.p) {
+                auto it = m->kv.find(t.first);
+                if (it != m->kv.end()) {
+                    const uint4 l = ct_lb_of(it->second.val);
+                    if (l.x | l.y)
+                        return false;
+                }
+            }
         }
     }
     const uint64_t size[2] = {G.ct4_host.size(), G.ct6_host.size()};
@@ -989,6 +1031,11 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
                     zero_acct(acct);   // deleted and created again
                 }
                 put(tm + at, &v);
+                if (!v6) {
+                    const uint4 l = ct_lb_of(it->second.val);
+                    if (G.ct4_lb.p)
+                        put((uint4 *)G.ct4_lb.p + at, &l);
+                }
             } else if (at >= 0) {       // delete
                 if (v6) {
                     Ct6Slot d{};
@@ -1080,6 +1127,8 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
         E->ep = (groups & GROUP_ENDPOINTS) ? build_ep(c, img, ms, s, &rc) : c->epoch->ep;
     if (!rc)
         E->ct = (groups & GROUP_CT) ? build_ctg(img, ms, s, &rc) : c->epoch->ct;
+    if (!rc)
+        E->lb = (groups & GROUP_LB) ? build_lbg(img, s, &rc) : c->epoch->lb;
     if (rc)
         return rc;
     assemble(*E);
@@ -1568,7 +1617,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
     }
-    size_t need = ws_layout(in->n, E.T, mode, E.T.ct4 || E.T.ct6 || out->ct).total;
+    size_t need = ws_layout(in->n, E.T, mode,
+                            E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4).total;
     if (need > c->ws_bytes) {
         if (c->ws) {
             (void)hipDeviceSynchronize();
@@ -1657,6 +1707,8 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     a.ports = in->ports;
     a.saddr = reinterpret_cast<const uint32_t *>(in->saddr);
     a.daddr = reinterpret_cast<const uint32_t *>(in->daddr);
+    if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value)
+        a.hash = in->hash;
     a.n = in->n;
     a.family = family;
     a.mode = mode;
@@ -1910,7 +1962,8 @@ struct CtEntry {
     uint32_t src_sec_id, last_tx_report, last_rx_report;
 };
 static_assert(sizeof(CtEntry) == 56, "struct ct_entry is 56 bytes");
-constexpr uint16_t CTB_RX_CLOSING = 1, CTB_TX_CLOSING = 2, CTB_SEEN_NON_SYN = 16;
+constexpr uint16_t CTB_RX_CLOSING = 1, CTB_TX_CLOSING = 2, CTB_LB_LOOPBACK = 8,
+                   CTB_SEEN_NON_SYN = 16;
 // conntrack.h:31-35
 constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,
                    CT_CLOSE_TIMEOUT = 10, CT_REPORT_INTERVAL = 5;
@@ -1969,6 +2022,165 @@ void ct_hit_update(Map *m, Map::Entry &me, int action, int dir, bool count,
     memcpy(&me.val[0], &e, sizeof(e));
     m->touched[me.key] |= TOUCH_VALUE;
     m->gen++;
+}
+
+// ---- load balancing on the host CT maps (cfc_ct_apply_v4 with a load
+// balancer): cilium_lb4_services / cilium_lb4_reverse_nat as the kernels see
+// them (lb.hip), for the apply's replay of the service step
+struct LbHost {
+    const Map *svc = nullptr, *rnat = nullptr;
+    explicit LbHost(cfc_ctx *c)
+    {
+        for (auto &kv : c->maps) {
+            if (kv.second->role == ROLE_LB4_SVC)
+                svc = kv.second.get();
+            else if (kv.second->role == ROLE_LB4_RNAT)
+                rnat = kv.second.get();
+        }
+    }
+    bool on() const { return (svc && !svc->kv.empty()) || (rnat && !rnat->kv.empty()); }
+    // struct lb4_service {target, port, count, rev_nat_index, weight}
+    struct Svc {
+        uint32_t target;
+        uint16_t port, count, rev_nat, weight;
+    };
+    bool get(uint32_t addr, uint16_t dport, uint16_t slave, Svc *v) const
+    {
+        if (!svc)
+            return false;
+        char k[8];
+        memcpy(k, &addr, 4);
+        memcpy(k + 4, &dport, 2);
+        memcpy(k + 6, &slave, 2);
+        auto it = svc->kv.find(std::string(k, 8));
+        if (it == svc->kv.end() || it->second.val.size() < 12)
+            return false;
+        memcpy(v, it->second.val.data(), 12);
+        return true;
+    }
+    // lb4_lookup_service (lb.h:604-635)
+    bool service(uint32_t addr, uint16_t &dport, uint16_t slave, Svc *v) const
+    {
+        if (dport) {
+            if (get(addr, dport, slave, v) && v->count)
+                return true;
+            dport = 0;
+        }
+        return get(addr, 0, slave, v) && v->count;
+    }
+    // lb4_rev_nat (lb.h:485-588) on a packet for an entry with LB state
+    void rev_nat(const CtEntry &e, uint8_t proto, uint32_t &sa, uint32_t &da,
+                 uint32_t &pt) const
+    {
+        if (!e.rev_nat_index || !rnat)
+            return;
+        auto it = rnat->kv.find(std::string((const char *)&e.rev_nat_index, 2));
+        if (it == rnat->kv.end() || it->second.val.size() < 6)
+            return;
+        uint32_t addr;
+        uint16_t port;
+        memcpy(&addr, it->second.val.data(), 4);
+        memcpy(&port, it->second.val.data() + 4, 2);
+        if (port && (proto == 6 || proto == 17))
+            pt = (pt & 0xFFFF0000u) | port;
+        if (e.bits & CTB_LB_LOOPBACK)
+            da = sa;
+        sa = addr;
+    }
+};
+
+// cfc.h CFC_FLOW_HASH (kern_common.hpp flow_hash4)
+uint32_t flow_hash4_host(uint32_t sa, uint32_t da, uint32_t pt, uint32_t proto)
+{
+    const uint32_t lo = std::min(sa, da), hi = std::max(sa, da);
+    const uint32_t sp = pt & 0xFFFF, dp = pt >> 16;
+    const uint32_t pw = std::min(sp, dp) | (std::max(sp, dp) << 16);
+    return fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + pw * 0xC2B2AE3Du + proto);
+}
+
+// the ct_state lb4_local leaves for ct_create4 (common.h:452-461)
+struct LbState {
+    bool svc = false, drop = false, reslave = false;
+    uint32_t tda = 0;             // tuple daddr after the service step
+    uint16_t slave0 = 0, slave = 0, rev_nat = 0;
+    bool loopback = false;
+    uint32_t addr = 0, svc_addr = 0;
+    std::string ksvc;             // the CT_SERVICE tuple
+    Map *svc_map = nullptr;
+};
+
+// What handle_ipv4_from_lxc's service step does (bpf_lxc.c:476-492,
+// lb.h:590-776) for one header, against the maps as they now are (the
+// batch's earlier CT_SERVICE creates included).  pt: the packet's first L4
+// word, rewritten; psa: the packet's saddr.
+LbState lb4_step(const LbHost &L, Map *m, uint32_t sa, uint32_t da, uint32_t &pt,
+                 uint32_t &psa, uint32_t &pda, uint8_t proto, uint32_t hash)
+{
+    LbState x;
+    x.tda = da;
+    const bool l4 = proto == 6 || proto == 17;
+    if (!L.svc || (!l4 && proto != 1))
+        return x;
+    uint16_t kd = l4 ? (uint16_t)(pt >> 16) : 0;
+    LbHost::Svc v, b;
+    if (!L.service(da, kd, 0, &v))
+        return x;
+    x.svc = true;
+    x.svc_map = m;
+    // the CT_SERVICE tuple: as loaded, flags TUPLE_F_SERVICE (| RELATED for
+    // an ICMP error)
+    uint16_t td, ts;
+    uint8_t fl = 4;
+    if (l4) {
+        td = (uint16_t)(pt & 0xFFFF);
+        ts = (uint16_t)(pt >> 16);
+    } else {
+        const uint32_t type = pt & 0xFF;
+        const bool rel = type == 3 || type == 11 || type == 12;
+        td = (!rel && type == 0) ? 8 : 0;
+        ts = (!rel && type == 8) ? 8 : 0;
+        fl |= rel ? 2 : 0;
+    }
+    char k[14];
+    memcpy(k, &da, 4);
+    memcpy(k + 4, &sa, 4);
+    memcpy(k + 8, &td, 2);
+    memcpy(k + 10, &ts, 2);
+    k[12] = (char)proto;
+    k[13] = (char)fl;
+    x.ksvc.assign(k, 14);
+    auto it = m ? m->kv.find(x.ksvc) : decltype(m->kv.end()){};
+    if (m && it != m->kv.end()) {   // CT_REPLY: ct_state from the entry
+        CtEntry e;
+        memcpy(&e, it->second.val.data(), sizeof(e));
+        x.slave = e.slave;
+        x.loopback = (e.bits & CTB_LB_LOOPBACK) != 0;
+    } else {
+        x.slave = (uint16_t)(hash % v.count + 1);   // lb4_select_slave
+    }
+    x.slave0 = x.slave;
+    if (!L.get(da, kd, x.slave, &b)) {
+        if (!L.service(da, kd, x.slave, &b)) {
+            x.drop = true;
+            return x;
+        }
+        x.slave = (uint16_t)(hash % b.count + 1);
+        x.reslave = true;
+    }
+    x.rev_nat = b.rev_nat;
+    x.addr = b.target;
+    if (sa == b.target) {
+        x.loopback = true;
+        x.addr = IPV4_LOOPBACK;
+        x.svc_addr = sa;
+        psa = IPV4_LOOPBACK;
+    }
+    if (!x.loopback)
+        x.tda = b.target;
+    pda = b.target;
+    if (b.port && kd != b.port && l4)
+        pt = (pt & 0xFFFFu) | (uint32_t)b.port << 16;
+    return x;
 }
 
 // Device slot of a CT key in the current epoch, or -1.  A write that
@@ -2034,6 +2246,8 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
                  uint16_t ep_lxc, hipStream_t s)
 {
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
+        return 1;
+    if (LbHost(c).on())   // service entries and reverse NAT: the host walk
         return 1;
     // the device table must be the maps as committed: no host-side CT
     // change waiting for a commit
@@ -2198,26 +2412,104 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
          hipMemcpyAsync(tf.data(), in->tcp_flags, n, hipMemcpyDeviceToHost, s) != hipSuccess) ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
+    std::vector<uint32_t> hs;
+    if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value) {
+        if (in->hash) {
+            hs.resize(n);
+            if (hipMemcpyAsync(hs.data(), in->hash, 4 * n, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -EIO;
+        }
+    }
     CtApply A(c, family);
+    const LbHost L(c);
+    const bool lbon = family == 4 && L.on();
     const uint32_t now = c->now;
     const uint8_t icmp = family == 4 ? 1 : 58;
     const uint32_t echo = family == 4 ? 8 : 128, echo_reply = family == 4 ? 0 : 129;
+    // keys this apply wrote: a later hit on one of them was not counted by
+    // the device (the entry did not exist when the batch was classified)
+    std::unordered_set<std::string> made;
     for (size_t i = 0; i < n; i++) {
         const uint8_t cb = ct[i];
-        if (!(cb & (CFC_CT_DONE | CFC_CT_DONE << 4)))
-            continue;
-        const uint8_t *s_ = &sa[al * i], *d_ = &da[al * i];
-        const int dst = A.endpoint(d_);
-        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
         const uint32_t proto = mt[i] & 0xFF, len = mt[i] >> 16;
         const bool is_tcp = proto == 6, syn = (mt[i] & CFC_HF_TCP_CLOSE) != 0;
         const uint8_t tflags = is_tcp ? tf[i] : 0;
+        // lb4_local created its CT_SERVICE entry before it found no backend
+        const bool no_svc = lbon && mode == CFC_MODE_EGRESS && ver[i] == -158;   // DROP_NO_SERVICE
+        if (!(cb & (CFC_CT_DONE | CFC_CT_DONE << 4)) && !no_svc)
+            continue;
+        const uint8_t *s_ = &sa[al * i], *d_ = &da[al * i];
+        // the tuple of the sender's lookup (stage 0 of an egress batch) and
+        // the packet every later stage sees: a service step and a reply's
+        // reverse NAT move them (IPv4 with a load balancer)
+        uint32_t tsa = 0, tda = 0, tpt = pt[i], psa = 0, pda = 0, ppt = pt[i];
+        if (family == 4) {
+            memcpy(&tsa, s_, 4);
+            memcpy(&tda, d_, 4);
+            psa = tsa;
+            pda = tda;
+        }
+        LbState x;
+        if (lbon && mode == CFC_MODE_EGRESS && ((cb & CFC_CT_DONE) || no_svc)) {
+            Map *m0 = A.ct_map((int)ep_lxc, proto != 6);
+            const uint32_t h = hs.empty() ? flow_hash4_host(tsa, tda, pt[i], proto) : hs[i];
+            uint32_t p2 = pt[i];
+            x = lb4_step(L, m0, tsa, tda, p2, psa, pda, (uint8_t)proto, h);
+            if (x.svc) {
+                tda = x.tda;
+                tpt = ppt = p2;
+            }
+            if (x.svc && m0) {   // the CT_SERVICE entry: hit (updated) or created
+                const uint32_t type = pt[i] & 0xFF;
+                const int act = proto == 6 ? (syn ? 2 : 1) : proto == 17 ? 1
+                                : (type == 3 || type == 11 || type == 12 || type == 0) ? 0 : 1;
+                auto it = m0->kv.find(x.ksvc);
+                if (it != m0->kv.end()) {
+                    ct_hit_update(m0, it->second, act, 0, true, len, now, is_tcp, syn, tflags);
+                    if (x.reslave && !x.drop)   // ct_update4_slave
+                        memcpy(&it->second.val[40], &x.slave, 2);
+                } else {
+                    CtEntry e{};
+                    e.slave = x.slave0;
+                    ct_upd_timeout(e, now, is_tcp, 0, is_tcp, 0);
+                    e.tx_packets = 1;
+                    e.tx_bytes = len;
+                    if (x.reslave && !x.drop)
+                        e.slave = x.slave;
+                    (void)m0->update(x.ksvc.data(), &e, 0);
+                    made.insert(x.ksvc);
+                    std::string ki = x.ksvc;
+                    memset(&ki[8], 0, 4);
+                    ki[12] = (char)icmp;
+                    ki[13] = (char)(4 | 2);
+                    e.bits |= CTB_SEEN_NON_SYN;
+                    if (m0->kv.count(ki))
+                        ct_drop_counts(c, m0, ki, s);
+                    (void)m0->update(ki.data(), &e, 0);
+                    made.insert(ki);
+                }
+            }
+        }
+        if (x.drop)
+            continue;
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
         for (int st = 0; st < 2; st++) {
             const uint8_t cs = (uint8_t)(cb >> (4 * st));
             if (!(cs & CFC_CT_DONE))
                 continue;
             const bool eg = mode == CFC_MODE_EGRESS && st == 0;
             const int dir = eg ? 0 : 1;   // CT_EGRESS / CT_INGRESS
+            // the addresses and L4 word this stage's lookup read
+            const uint8_t *ks = s_, *kd_ = d_;
+            uint32_t kp = pt[i];
+            if (family == 4) {
+                ks = eg ? (const uint8_t *)&tsa : (const uint8_t *)&psa;
+                kd_ = eg ? (const uint8_t *)&tda : (const uint8_t *)&pda;
+                kp = eg ? tpt : ppt;
+            }
+            const int dst = A.endpoint(family == 4 ? (const uint8_t *)&pda : d_);
             Map *m = A.ct_map(eg ? (int)ep_lxc : dst, proto != 6);
             if (!m)
                 continue;
@@ -2225,11 +2517,11 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             uint32_t td, ts, fl = dir == 1 ? 0u : 1u;
             int action;
             if (proto == 6 || proto == 17) {
-                td = pt[i] & 0xFFFF;
-                ts = pt[i] >> 16;
+                td = kp & 0xFFFF;
+                ts = kp >> 16;
                 action = (proto == 6 && (mt[i] & CFC_HF_TCP_CLOSE)) ? 2 : 1;
             } else if (proto == icmp) {
-                const uint32_t type = pt[i] & 0xFF;
+                const uint32_t type = kp & 0xFF;
                 const bool rel = family == 4 ? (type == 3 || type == 11 || type == 12)
                                              : (type >= 1 && type <= 4);
                 td = (!rel && type == echo_reply) ? echo : 0;
@@ -2251,20 +2543,26 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 k[2 * al + 5] = (char)f;
                 return std::string(k, 2 * al + 6);
             };
-            const std::string k1 = tuple(d_, s_, td, ts, fl);
-            const std::string k2 = tuple(s_, d_, ts, td, fl ^ 1u);
+            const std::string k1 = tuple(kd_, ks, td, ts, fl);
+            const std::string k2 = tuple(ks, kd_, ts, td, fl ^ 1u);
             const int b = cs & CFC_CT_RES_MASK;
             const bool dropped = st == last && ver[i] == -133;   // DROP_POLICY
             if (b >= 2) {                       // CT_REPLY / CT_RELATED
                 auto it = m->kv.find(k1);
-                if (it != m->kv.end())
-                    ct_hit_update(m, it->second, action, dir, false, len, now, is_tcp,
-                                  syn, tflags);
+                if (it != m->kv.end()) {
+                    ct_hit_update(m, it->second, action, dir, made.count(k1) > 0, len, now,
+                                  is_tcp, syn, tflags);
+                    if (lbon && eg) {   // the egress reply's reverse NAT
+                        CtEntry e;
+                        memcpy(&e, it->second.val.data(), sizeof(e));
+                        L.rev_nat(e, (uint8_t)proto, psa, pda, ppt);
+                    }
+                }
             } else if (b == 1) {                // CT_ESTABLISHED
                 auto it = m->kv.find(k2);
                 if (it != m->kv.end()) {
-                    ct_hit_update(m, it->second, action, dir, false, len, now, is_tcp,
-                                  syn, tflags);
+                    ct_hit_update(m, it->second, action, dir, made.count(k2) > 0, len, now,
+                                  is_tcp, syn, tflags);
                     if (dropped) {              // ct_delete4/6
                         ct_drop_counts(c, m, k2, s);
                         (void)m->erase(k2.data());
@@ -2286,7 +2584,26 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 e.src_sec_id = mode == CFC_MODE_EGRESS ? c->seclabel[ep_lxc] : ident[i];
                 if (family == 6 && dir == 1)    // ipv6_policy, bpf_lxc.c:787-788
                     e.rev_nat_index = (uint16_t)(d_[12] | d_[13] << 8);
+                if (eg && x.svc) {              // lb4_local's ct_state
+                    e.rev_nat_index = x.rev_nat;
+                    e.slave = x.slave;
+                    if (x.loopback)
+                        e.bits |= CTB_LB_LOOPBACK;
+                }
                 (void)m->update(k2.data(), &e, 0);
+                made.insert(k2);
+                if (eg && x.svc && x.addr) {    // the reverse-NAT entry
+                    std::string kx = k2;
+                    memcpy(&kx[0], &x.addr, 4);
+                    if (x.loopback) {
+                        kx[13] = 1;             // TUPLE_F_IN
+                        memcpy(&kx[4], &x.svc_addr, 4);
+                    }
+                    if (m->kv.count(kx))
+                        ct_drop_counts(c, m, kx, s);
+                    (void)m->update(kx.data(), &e, 0);
+                    made.insert(kx);
+                }
                 e.bits |= CTB_SEEN_NON_SYN;     // "For ICMP, there is no SYN"
                 const std::string ki = [&] {
                     std::string t = k2;
@@ -2298,6 +2615,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 if (m->kv.count(ki))            // overwritten
                     ct_drop_counts(c, m, ki, s);
                 (void)m->update(ki.data(), &e, 0);
+                made.insert(ki);
             }
         }
     }

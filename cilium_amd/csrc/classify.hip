@@ -140,6 +140,10 @@ struct Hdr {
     uint32_t ev2;                // stage-2 identity event: 0, 1 fwd, 2 drop
     uint32_t tf;                 // TCP header byte 13 (cfc_hdr_v4.tcp_flags)
     uint32_t evw;                // trace event word of a forwarded header
+    // load balancing (LB launches; else tda = da, tpt = pt, psa = sa):
+    // the sender's tuple daddr / L4 word after the service step (lb.hip),
+    // the packet's saddr and L4 word as it leaves, the service step's flags
+    uint32_t tda, tpt, psa, ppt, lbfl;
     PolicyProbe P;
 };
 
@@ -152,11 +156,12 @@ struct Hdr {
 // so no round needs a validity branch; only the metrics count them out.
 struct Raw {
     uint32_t sa, da, pt, mt, mk, tf;
+    uint32_t tda, tpt, psa, lbfl;
 };
 // in: the workgroup's slice (arrays advanced to its first header), i: the
 // header's index in it, nloc: the slice's length
-template <bool OPT>
-__device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, uint32_t i,
+template <bool OPT, bool LBE>
+__device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, const LbIn &L, uint32_t i,
                                          uint32_t nloc, Raw &r)
 {
     // no branches here: a load issued on only one side of a branch makes the
@@ -176,6 +181,17 @@ __device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, uint32_t i,
         r.mk = in.mark ? mk : 0u;
         r.tf = in.tcp_flags ? tf : 0u;
     }
+    if (LBE) {   // an egress batch's service step (lb.hip)
+        r.tda = ldo_nt(L.tda, o);
+        r.tpt = ldo_nt(L.tpt, o);
+        r.psa = ldo_nt(L.psa, o);
+        r.lbfl = ldo_nt(L.fl, o);
+    } else {
+        r.tda = r.da;
+        r.tpt = r.pt;
+        r.psa = r.sa;
+        r.lbfl = 0;
+    }
 }
 __device__ __forceinline__ void r1_take(const Raw &r, uint32_t i, uint32_t end,
                                         Hdr &h)
@@ -187,6 +203,11 @@ __device__ __forceinline__ void r1_take(const Raw &r, uint32_t i, uint32_t end,
     h.mt = r.mt;
     h.mk = r.mk;
     h.tf = r.tf;
+    h.tda = r.tda;
+    h.tpt = r.tpt;
+    h.psa = r.psa;
+    h.ppt = r.pt;
+    h.lbfl = r.lbfl;
 }
 
 // round 2: every lookup that only needs the header
@@ -200,7 +221,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.l4d = make_uint4(0, 0, 0, 0);
     h.e24 = h.pfd = 0;
     h.lx = h.ls = h.pf = make_uint4(0, 0, 0, 0);
-    h.lh = __builtin_bswap32(EGR ? h.da : h.sa);
+    h.lh = __builtin_bswap32(EGR ? h.tda : h.sa);
     h.hsh = __builtin_bswap32(h.sa);
     h.lxs = h.lss = h.pfb = 0;
     h.pf_maybe = false;
@@ -235,7 +256,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
 
 // round 3: second-level LPM, endpoint resolution, prefilter verdict,
 // identity, and the first policy key that may exist
-template <int MODE, bool CT>
+template <int MODE, bool CT, bool LB>
 __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
                                             const EgressArgs &E, Hdr &h)
 {
@@ -301,7 +322,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     if (MODE == CFC_MODE_XDP || h.xdp_drop)
         return;
     const uint32_t proto = h.mt & 0xFF;
-    const bool known = ct_new_dport(proto, h.pt, &h.dport);
+    const bool known = ct_new_dport(proto, h.tpt, &h.dport);
     if (!EGR) {
         // handle_identity_from_host (bpf_netdev.c:128-153), branch-free
         const uint32_t magic = h.mk & 0xF00u;
@@ -334,19 +355,30 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
             h.ct_res = c.res;
             h.ct_slot = c.slot;
             h.ct_byte = (uint32_t)c.res | CTO_DONE;
+            // a reply of a load-balanced flow: its source translated back
+            // (bpf_lxc.c:946-955; the packet only)
+            if (LB && T.ct4_lb && c.res == CT_REPLY) {
+                const uint4 lw = ld16(T.ct4_lb + c.slot);
+                if (!((lw.x >> 16) & 1)) {
+                    uint32_t da = h.da;
+                    lb4_rev_nat(T, lw, proto, h.psa, da, h.ppt);
+                }
+            }
         }
     } else {
         h.act = TC_ACT_SHOT;
         if (h.src_lxc != E.lxc_id) {   // is_valid_lxc_src_ipv4 (lxc.h:55)
             h.ver = DROP_INVALID_SIP;
             h.met0 = mkey<MODE>(DROP_INVALID_SIP, METRIC_EGRESS);
+        } else if (LB && (h.lbfl & LBF_DROP)) {   // lb4_local: no backend
+            h.ver = DROP_NO_SERVICE;             // (counted in the store loop)
         } else if (!known) {
             h.ver = DROP_CT_UNKNOWN_PROTO;
             h.met0 = mkey<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
         } else {
             // destination identity (bpf_lxc.c:516-532)
             h.ident = h.e24 ? h.e24
-                            : ((h.da & T.v4_cluster_mask) == T.v4_cluster_range
+                            : ((h.tda & T.v4_cluster_mask) == T.v4_cluster_range
                                    ? CLUSTER_ID
                                    : WORLD_ID);
             h.need_pol = true;
@@ -354,7 +386,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
             h.pmask = E.pol_mask;
             h.egress_bit = 1;
             if (CT) {   // handle_ipv4_from_lxc's ct_lookup4 (bpf_lxc.c:509)
-                const CtResult c = ct_stage4(T, h.sa, h.da, proto, h.pt,
+                const CtResult c = ct_stage4(T, h.sa, h.tda, proto, h.tpt,
                                              CT_EGRESS, E.ct_owner);
                 h.dport = c.dport;
                 h.ct_res = c.res;
@@ -381,7 +413,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
 // to different fields of `h` get merged by the compiler into one store
 // through a selected field address, which pushes the whole per-header state
 // array into scratch memory.
-template <int MODE, bool CT, bool NT>
+template <int MODE, bool CT, bool NT, bool LB>
 __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                                            const EgressArgs &E, Hdr &h)
 {
@@ -390,7 +422,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
         return;
     // the monitor length of a trace this header may send (NT: the caller
     // wants the event words)
-    const uint32_t action = ct_action(false, h.mt & 0xFF, h.pt, h.mt);
+    const uint32_t action = ct_action(false, h.mt & 0xFF, h.tpt, h.mt);
     const uint32_t tfl = (h.mt & 0xFF) == 6 ? h.tf : 0u;
     const uint32_t mon1 = NT ? ct_monitor(T, CT ? T.ct4_tm : nullptr, h.ct_slot,
                                           EGR ? CT_EGRESS : CT_INGRESS, action, tfl,
@@ -465,12 +497,54 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
             // ct_lookup4 in the destination's CT maps
             uint32_t dp2 = h.dport;
             CtResult c2{CT_NEW, NONE, 0};
+            bool fresh = false;
             if (CT) {
-                c2 = ct_stage4(T, h.sa, h.da, proto, h.pt, CT_INGRESS,
-                               ct_owner_word(h.rec.w & 0xFFFF,
-                                             (h.rec.w & LXC_CT_LOCAL) != 0));
+                const uint32_t own2 = ct_owner_word(h.rec.w & 0xFFFF,
+                                                    (h.rec.w & LXC_CT_LOCAL) != 0);
+                c2 = ct_stage4(T, h.psa, h.da, proto, h.pt, CT_INGRESS, own2);
                 dp2 = c2.dport;
+                if (LB && own2 == E.ct_owner && h.ct_res == CT_NEW && (v >= 0 || reply)) {
+                    // the entries this header's egress stage created (ct_create4
+                    // with the service's ct_state: main and reverse-NAT entry)
+                    // are in the map the destination's lookup runs on
+                    const CtProbe k0 = ct_probe<false>(proto, h.tpt, CT_EGRESS, E.ct_owner);
+                    const CtProbe k = ct_probe<false>(proto, h.pt, CT_INGRESS, own2);
+                    const bool svc = (h.lbfl & LBF_SVC) != 0, loop = (h.lbfl & LBF_LOOP) != 0;
+                    // main: k2 of the egress lookup; reverse-NAT entry: its
+                    // daddr the service step's address, a looped-back flow's
+                    // with TUPLE_F_IN and the sender as saddr
+                    const uint32_t ex = loop ? IPV4_LOOPBACK : h.da;
+                    const uint32_t ey = loop ? h.sa : h.tda;
+                    const uint32_t ew = loop ? ct_word(proto, 1u, E.ct_owner) : k0.w2;
+                    auto is_fresh = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
+                        return (x == h.sa && y == h.tda && z == k0.z2 && w == k0.w2) ||
+                               (svc && x == ex && y == ey && z == k0.z2 && w == ew);
+                    };
+                    if (is_fresh(h.da, h.psa, k.z1, k.w1)) {
+                        fresh = true;
+                        c2.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
+                        c2.dport = k.td;
+                    } else if (c2.res < CT_REPLY && is_fresh(h.psa, h.da, k.z2, k.w2)) {
+                        fresh = true;
+                        c2.res = CT_ESTABLISHED;
+                        c2.dport = k.ts;
+                    }
+                    if (fresh) {
+                        c2.slot = NONE;   // (not in the table: the apply counts it)
+                        dp2 = c2.dport;
+                    }
+                }
                 h.ct_k2 = ct_acct_key(c2.slot, CT_INGRESS);
+                if (LB && c2.res == CT_REPLY) {   // bpf_lxc.c:946-955, packet only
+                    const uint4 lw = fresh ? make_uint4((h.lbfl >> 16) | (h.lbfl & LBF_LOOP) << 14,
+                                                        0, 0, 0)
+                                           : (T.ct4_lb ? ld16(T.ct4_lb + c2.slot)
+                                                       : make_uint4(0, 0, 0, 0));
+                    if (!((lw.x >> 16) & 1)) {
+                        uint32_t da = h.da;
+                        lb4_rev_nat(T, lw, proto, h.psa, da, h.ppt);
+                    }
+                }
             }
             const bool reply2 = CT && c2.res >= CT_REPLY;
             const PolicyResult pw = policy_access(T, S, h.rec.y, h.rec.z,
@@ -493,9 +567,13 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                 met1 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
                 ev2 = 1;
                 if (NT) {   // the destination program's trace
-                    const uint32_t mon2 = ct_monitor(T, CT ? T.ct4_tm : nullptr,
-                                                     CT ? c2.slot : NONE, CT_INGRESS,
-                                                     action, tfl, dp2);
+                    uint32_t mon2 = ct_monitor(T, CT ? T.ct4_tm : nullptr,
+                                               CT ? c2.slot : NONE, CT_INGRESS,
+                                               action, tfl, dp2);
+                    if (LB && fresh)   // the entry as ct_create4 just wrote it
+                        mon2 = dp2 == 0x3500u ? MTU_LEN
+                               : ct_monitor_of(T, make_uint4(0, T.now, 0, 0), CT_INGRESS,
+                                               action, tfl);
                     evw = trace_word(prox ? OBS_TO_PROXY : OBS_TO_LXC, h.rec.w & 0xFFFF,
                                      CT ? (uint32_t)c2.res : 0u, mon2);
                 }
@@ -552,10 +630,13 @@ __device__ __forceinline__ void acc_publish(const unsigned long long *s_met,
 
 // OPT: the call passes some optional array (mark, tcp_flags, action, ct);
 // without, their pointers and branches are compiled out (fewer live SGPRs)
-template <int MODE, int U, bool CT, bool NT, bool OPT>
+// LB: the launch has a load balancer — an egress batch reads the service
+// step's results (lb.hip), every batch may reverse-NAT replies, and the
+// packet outputs (cfc_out.pkt_*) are written
+template <int MODE, int U, bool CT, bool NT, bool OPT, bool LB>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
-    CountArgs C, uint64_t per_block)
+    CountArgs C, uint64_t per_block, LbIn LI)
 {
     // LDS image (uint4 units): metrics | endpoint slots | pf Bloom | pol Bloom
     unsigned long long *s_met = lds_met();
@@ -607,6 +688,18 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     out.identity += start;
     if (out.notify)
         out.notify += start;
+    constexpr bool LBE = LB && MODE == CFC_MODE_EGRESS;
+    if (LBE) {
+        LI.tda += start;
+        LI.tpt += start;
+        LI.psa += start;
+        LI.fl += start;
+    }
+    if (LB && out.pkt_saddr) {
+        out.pkt_saddr += start;
+        out.pkt_daddr += start;
+        out.pkt_ports += start;
+    }
     if (C.ct)
         C.ct += start;
     if (C.ct2)
@@ -625,7 +718,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     Raw nx[U];
 #pragma unroll
     for (int u = 0; u < U; u++)
-        r1_issue<OPT>(in, u * BLOCK + threadIdx.x, end, nx[u]);
+        r1_issue<OPT, LBE>(in, LI, u * BLOCK + threadIdx.x, end, nx[u]);
     for (uint32_t base = 0; base < end; base += BLOCK * U) {
         Hdr h[U];
 #pragma unroll
@@ -636,16 +729,16 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             r2_issue<MODE>(T, S, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r3_identity<MODE, CT>(T, S, E, h[u]);
+            r3_identity<MODE, CT, LB>(T, S, E, h[u]);
         // the next iteration's headers, behind this one's policy probe (the
         // last iteration re-reads the slice's last header)
         const uint32_t nb = base + BLOCK * U;
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r1_issue<OPT>(in, nb + u * BLOCK + threadIdx.x, end, nx[u]);
+            r1_issue<OPT, LBE>(in, LI, nb + u * BLOCK + threadIdx.x, end, nx[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
-            r4_verdict<MODE, CT, NT>(T, S, E, h[u]);
+            r4_verdict<MODE, CT, NT, LB>(T, S, E, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t i = base + u * BLOCK + threadIdx.x;
@@ -670,6 +763,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
                     if (EGR)
                         sto_nt(h[u].ct_k2, C.ct2, o4);
                 }
+                if (LB && out.pkt_saddr) {   // the packet as it leaves
+                    sto_nt(h[u].psa, out.pkt_saddr, o4);
+                    sto_nt(h[u].da, out.pkt_daddr, o4);
+                    sto_nt(h[u].ppt, out.pkt_ports, o4);
+                }
                 if (MODE != CFC_MODE_XDP) {
 #if CFC_EXP != 3
                     sto_nt(ctr_key(C, h[u].ctr0, len), C.ctr, o4);
@@ -683,6 +781,12 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             }
             if (MODE != CFC_MODE_XDP && h[u].valid && h[u].id_ovf && h[u].need_pol)
                 id_count(C, id_dir, h[u].ident, h[u].drop1, len);
+            if (LBE && h[u].valid && h[u].ver == DROP_NO_SERVICE) {   // (rare)
+                unsigned long long *m = reinterpret_cast<unsigned long long *>(
+                    C.g_met + (uint64_t)(-DROP_NO_SERVICE * METRIC_DIRS + METRIC_EGRESS) * 2);
+                atomicAdd(m, 1ull);
+                atomicAdd(m + 1, (unsigned long long)len);
+            }
 #if CFC_EXP != 5
             acc.add(h[u].valid ? h[u].met0 : NONE, len);
 #endif
@@ -1136,10 +1240,14 @@ __global__ __launch_bounds__(64) void k_acc_plan(const uint32_t *off, uint32_t n
 #pragma unroll
     for (int j = 0; j < 2; j++) {
         const uint32_t c = 2 * l + j;
-        if (c <= nco) {
+        if (c < nco) {
             plan[c] = a[j];
             plan[nco + 1 + c] = j ? e + nc[0] : e;
         }
+    }
+    if (l == 63) {   // the ends (nco may be 128: no lane's own bucket)
+        plan[nco] = total;
+        plan[2 * nco + 1] = x;
     }
 }
 
@@ -1337,27 +1445,32 @@ __global__ __launch_bounds__(256) void k_patch16(const Patch16 *rec, uint64_t n)
 template <int MODE, bool CT, bool NT>
 void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                     const EgressArgs &E, const CountArgs &C, uint32_t grid,
-                    uint64_t per_block, hipStream_t s)
+                    uint64_t per_block, hipStream_t s, const LbIn *lb)
 {
     const LdsPlan L = lds_plan(T);
     const bool opt = in.mark || in.tcp_flags || out.action || (CT && out.ct);
-    auto kern = opt ? k_classify_v4<MODE, CFC_UNROLL, CT, NT, true>
-                    : k_classify_v4<MODE, CFC_UNROLL, CT, NT, false>;
+    auto kern = opt ? k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, false>
+                    : k_classify_v4<MODE, CFC_UNROLL, CT, NT, false, false>;
+    const LbIn none{};
+    if constexpr (CT && MODE != CFC_MODE_XDP) {
+        if (lb)
+            kern = k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, true>;
+    }
     set_lds_limit((const void *)kern, (int)LDS_PER_WG);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
-                       out, E, C, per_block);
+                       out, E, C, per_block, lb ? *lb : none);
 }
 
 // the notify store is compiled in only when the caller asked for it
 template <int MODE, bool CT>
 void launch_mode(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                  const EgressArgs &E, const CountArgs &C, uint32_t grid,
-                 uint64_t per_block, hipStream_t s)
+                 uint64_t per_block, hipStream_t s, const LbIn *lb)
 {
     if (out.notify)
-        launch_mode_nt<MODE, CT, true>(T, in, out, E, C, grid, per_block, s);
+        launch_mode_nt<MODE, CT, true>(T, in, out, E, C, grid, per_block, s, lb);
     else
-        launch_mode_nt<MODE, CT, false>(T, in, out, E, C, grid, per_block, s);
+        launch_mode_nt<MODE, CT, false>(T, in, out, E, C, grid, per_block, s, lb);
 }
 
 // histogram slices of an n-header batch with `slots` keys in all: one per
@@ -1487,6 +1600,11 @@ WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
         w.ctp_plan = take(4ull * (2 * w.ctp_nco + 2));
         w.ctp_fo = take(4ull * w.ctp_g2 * (ACC_FINE + 1));
     }
+    if (egr && (T.lb4 || T.rnat4)) {   // the service step's six arrays (lb.hip)
+        off = (off + 255) & ~(size_t)255;
+        w.lb = off;
+        off += 6 * a;
+    }
     w.total = off;
     return w;
 }
@@ -1532,16 +1650,42 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
         (void)hipEventRecord(tm->ev[0], s);
     // conntrack lookups when CT maps hold entries or the caller wants the
     // CT byte (to fold creates into the maps); an empty map misses anyway
-    const bool ct = T.ct4 || out.ct;
+    // with a load balancer every tc-path batch looks up CT (service entries,
+    // reverse NAT) and runs the LB variant
+    const bool lb = (T.lb4 || T.rnat4) && mode != CFC_MODE_XDP;
+    const bool ct = T.ct4 || out.ct || lb;
     const WsLayout w = ws_layout(in.n, T, mode, ct);
     const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
+    cfc_hdr_v4 hin = in;
+    LbIn li{};
+    if (lb && mode == CFC_MODE_EGRESS) {
+        // the service step first (lb.hip): the classify kernel reads the
+        // packet's daddr / L4 word from it and the tuple it left
+        uint32_t *a = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ws) + w.lb);
+        const uint64_t st = ctr_stride(in.n);
+        LbArgs A{in.saddr, in.daddr, in.ports, in.meta, in.hash, in.n, E.ct_owner,
+                 a, a + st, a + 2 * st, a + 3 * st, a + 4 * st, a + 5 * st};
+        if (int rc = launch_lb4_egress(T, A, s))
+            return rc;
+        li = LbIn{A.tda, A.tpt, A.psa, A.fl};
+        hin.daddr = A.pda;
+        hin.ports = A.ppt;
+    } else if (out.pkt_saddr && !lb) {   // nothing rewrites the packet
+        if (hipMemcpyAsync(out.pkt_saddr, in.saddr, 4 * in.n, hipMemcpyDeviceToDevice, s) ||
+            hipMemcpyAsync(out.pkt_daddr, in.daddr, 4 * in.n, hipMemcpyDeviceToDevice, s) ||
+            hipMemcpyAsync(out.pkt_ports, in.ports, 4 * in.n, hipMemcpyDeviceToDevice, s))
+            return -5;
+    }
+    const LbIn *lbp = lb ? &li : nullptr;
 #define CFC_LAUNCH(M)                                                        \
-    (ct ? launch_mode<M, true>(T, in, out, E, C, grid, per_block, s)         \
-        : launch_mode<M, false>(T, in, out, E, C, grid, per_block, s))
+    (ct ? launch_mode<M, true>(T, hin, out, E, C, grid, per_block, s, lbp)   \
+        : launch_mode<M, false>(T, hin, out, E, C, grid, per_block, s, lbp))
     switch (mode) {
     case CFC_MODE_INGRESS: CFC_LAUNCH(CFC_MODE_INGRESS); break;
     case CFC_MODE_EGRESS: CFC_LAUNCH(CFC_MODE_EGRESS); break;
-    case CFC_MODE_XDP: launch_mode<CFC_MODE_XDP, false>(T, in, out, E, C, grid, per_block, s); break;
+    case CFC_MODE_XDP:
+        launch_mode<CFC_MODE_XDP, false>(T, hin, out, E, C, grid, per_block, s, nullptr);
+        break;
     case CFC_MODE_FULL: CFC_LAUNCH(CFC_MODE_FULL); break;
     default: return -22;
     }

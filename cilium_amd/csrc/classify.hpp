@@ -92,6 +92,7 @@ struct WsLayout {
     size_t ctp_rec, ctp_recA, ctp_rcnt, ctp_cnt, ctp_off, ctp_bsum, ctp_plan, ctp_fo;
     uint32_t ctp_nv, ctp_nbuck, ctp_nco, ctp_g2;      // slices x stages, buckets,
                                                       // coarse buckets, fine chunks
+    size_t lb;   // EGRESS with a load balancer: tda, tpt, psa, pda, ppt, fl
 };
 WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct);
 CountArgs count_args(uint32_t *ws, const WsLayout &w, const DevTables &T,
@@ -159,6 +160,20 @@ int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, C
                 uint32_t cap, uint32_t *cnt, hipStream_t s);
 int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
 
+// ---- service load balancing of an egress batch (lb.hip)
+struct LbArgs {
+    const uint32_t *sa, *da, *pt, *mt, *hash;   // the batch (hash may be null)
+    uint64_t n;
+    uint32_t ct_owner;                            // the sender's CT maps
+    uint32_t *tda, *tpt, *psa, *pda, *ppt, *fl;   // per header (lb.hip)
+};
+int launch_lb4_egress(const DevTables &T, const LbArgs &A, hipStream_t stream);
+// the service step's results a classify launch reads (EGRESS), and the
+// packet outputs; all null when the launch has no load balancer
+struct LbIn {
+    const uint32_t *tda, *tpt, *psa, *fl;
+};
+
 // dst[i] += src[i] for n u64 (counter import)
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,
                    hipStream_t stream);
@@ -194,6 +209,7 @@ struct NotifyArgs {
     const uint32_t *ports;
     const uint32_t *saddr;   // v4: n words; v6: n x 4 words
     const uint32_t *daddr;
+    const uint32_t *hash;    // skb->hash per header (v4), or NULL: flow_hash
     uint64_t n;
     int family;              // 4 or 6
     int mode;

@@ -537,6 +537,55 @@ CtTimer ct_timer_of(const std::string &val)
     return tm;
 }
 
+// struct ct_entry: rev_nat_index @38, bits @36 (lb_loopback = bit 3),
+// slave @40
+uint4 ct_lb_of(const std::string &val)
+{
+    uint16_t bits = 0, rev = 0, slave = 0;
+    if (val.size() >= 42) {
+        memcpy(&bits, &val[36], 2);
+        memcpy(&rev, &val[38], 2);
+        memcpy(&slave, &val[40], 2);
+    }
+    return make_uint4(rev | ((bits >> 3) & 1u) << 16, slave, 0, 0);
+}
+
+// cilium_lb4_services / cilium_lb4_reverse_nat (layout.h)
+static void build_lb(const Map *svc, const Map *rnat, HostImage *img)
+{
+    if (svc && !svc->kv.empty()) {
+        const uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * svc->kv.size()));
+        img->lb4.assign(2ull * ns, make_uint4(0, 0, 0, 0));
+        img->lb4_mask = ns - 1;
+        for (const auto &kv : svc->kv) {
+            if (kv.first.size() != 8 || kv.second.val.size() < 12)
+                continue;
+            uint32_t k[2], v[3];
+            memcpy(k, kv.first.data(), 8);
+            memcpy(v, kv.second.val.data(), 12);
+            uint32_t i = lb4_hash(k[0], k[1]) & img->lb4_mask;
+            while (img->lb4[2 * i + 1].y)
+                i = (i + 1) & img->lb4_mask;
+            img->lb4[2 * i] = make_uint4(k[0], k[1], v[0], v[1]);
+            img->lb4[2 * i + 1] = make_uint4(v[2], 1, 0, 0);
+            img->n_lb4++;
+        }
+    }
+    if (rnat && !rnat->kv.empty()) {
+        img->rnat4.assign(65536, make_uint2(0, 0));
+        for (const auto &kv : rnat->kv) {
+            if (kv.first.size() != 2 || kv.second.val.size() < 6)
+                continue;
+            uint16_t idx, port;
+            uint32_t addr;
+            memcpy(&idx, kv.first.data(), 2);
+            memcpy(&addr, kv.second.val.data(), 4);
+            memcpy(&port, kv.second.val.data() + 4, 2);
+            img->rnat4[idx] = make_uint2(addr, port | 1u << 16);
+        }
+    }
+}
+
 // CT maps -> one open-addressed table per family (layout.h).  Entries no
 // lookup can reach (nexthdr not served by their map) are left out.  A
 // commit patches later inserts and deletes into the same table
@@ -552,6 +601,21 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
         img->ct4_tm.assign(ns, CtTimer{});
         img->ct4_mask = ns - 1;
     }
+    // with a load balancer the kernels read each CT4 entry's LB state; an
+    // entry that carries one asks for it too
+    bool lb = img->lb_ct;
+    for (const Map *m : cts)
+        if (!lb && m->role == ROLE_CT4)
+            for (const auto &kv : m->kv) {
+                const uint4 l = ct_lb_of(kv.second.val);
+                if (l.x | l.y) {
+                    lb = true;
+                    break;
+                }
+            }
+    img->lb_ct = lb;
+    if (n4 && lb)
+        img->ct4_lb.assign(img->ct4.size(), make_uint4(0, 0, 0, 0));
     if (n6) {
         uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n6));
         img->ct6.assign(ns, Ct6Slot{});
@@ -576,6 +640,8 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                 }
                 img->ct4[i] = e;
                 img->ct4_tm[i] = tm;
+                if (!img->ct4_lb.empty())
+                    img->ct4_lb[i] = ct_lb_of(kv.second.val);
                 img->ct4_probe = std::max(img->ct4_probe, p);
                 img->n_ct4++;
             } else {
@@ -610,6 +676,16 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
             if (m->policy_lxc >= 0)
                 img->ct_local[m->policy_lxc] = 1;
         }
+    const Map *lbsvc = nullptr, *lbrnat = nullptr;
+    for (Map *m : maps) {
+        if (m->role == ROLE_LB4_SVC)
+            lbsvc = m;
+        else if (m->role == ROLE_LB4_RNAT)
+            lbrnat = m;
+    }
+    img->lb_ct = (lbsvc && !lbsvc->kv.empty()) || (lbrnat && !lbrnat->kv.empty());
+    if (groups & GROUP_LB)
+        build_lb(lbsvc, lbrnat, img);
     if (groups & GROUP_CT)
         build_ct(cts, img);
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,

@@ -82,6 +82,13 @@ struct HostImage {
     uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
     uint32_t n_ct4 = 0, n_ct6 = 0;           // entries placed
     std::vector<uint8_t> ct_local;           // lxc_id -> has local CT maps
+    // load balancing (layout.h): service slots, reverse NAT, and per CT4
+    // slot the entry's LB state (built with GROUP_CT when lb_ct is set)
+    std::vector<uint4> lb4;
+    uint32_t lb4_mask = 0, n_lb4 = 0;
+    std::vector<uint2> rnat4;
+    std::vector<uint4> ct4_lb;
+    bool lb_ct = false;                      // ct4_lb wanted
     uint64_t device_bytes() const;
 };
 
@@ -91,6 +98,8 @@ uint64_t ct_map_key(int family, uint32_t owner, int any);
 bool ct_slot_of(const Map *m, const std::string &key, Ct4Slot *s4, Ct6Slot *s6);
 // the report state the kernels read (CtTimer) of a struct ct_entry value
 CtTimer ct_timer_of(const std::string &val);
+// the LB state a CT4 slot carries (ct4_lb) of a struct ct_entry value
+uint4 ct_lb_of(const std::string &val);
 
 // Table groups an epoch is built from; a commit rebuilds only the groups
 // whose maps changed (the others' device buffers carry over).
@@ -100,7 +109,8 @@ enum : unsigned {
     GROUP_ENDPOINTS = 4,  // cilium_lxc + every policymap (+ counter layout)
     GROUP_CT = 8,         // every CT map
     GROUP_IPCACHE6 = 16,  // ipcache, IPv6 LPM
-    GROUP_ALL = 31,
+    GROUP_LB = 32,        // cilium_lb4_services, cilium_lb4_reverse_nat
+    GROUP_ALL = 63,
 };
 // maps: every map of the context; groups: which parts of img to build
 // (ct_local, which only depends on which CT maps exist, always is).

@@ -10,7 +10,8 @@ namespace {
 
 constexpr uint32_t HOST_ID = 1, WORLD_ID = 2, CLUSTER_ID = 3, HEALTH_ID = 4;
 constexpr int DROP_INVALID_SIP = -132, DROP_POLICY = -133,
-              DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140;
+              DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140,
+              DROP_NO_SERVICE = -158;
 constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
 constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
@@ -244,7 +245,7 @@ __device__ __forceinline__ bool ct_new_dport(uint32_t proto, uint32_t ports,
 
 // ---- conntrack: ct_lookup4 / ct_lookup6 (conntrack.h:467-590, :310-437)
 constexpr int CT_NEW = 0, CT_ESTABLISHED = 1, CT_REPLY = 2, CT_RELATED = 3;
-constexpr int CT_EGRESS = 0, CT_INGRESS = 1;
+constexpr int CT_EGRESS = 0, CT_INGRESS = 1, CT_SERVICE = 2;
 constexpr uint32_t CTO_DONE = 4u, CTO_CREATE = 8u;   // per-stage CT byte bits
 
 // The tuple words of the two probes.  k1 is the tuple as loaded (packet
@@ -261,7 +262,8 @@ __device__ __forceinline__ CtProbe ct_probe(uint32_t proto, uint32_t pt,
                                             int dir, uint32_t owner)
 {
     CtProbe k;
-    uint32_t fl = dir == CT_INGRESS ? 0u : 1u;
+    // TUPLE_F_OUT / TUPLE_F_IN / TUPLE_F_SERVICE (conntrack.h:487-494)
+    uint32_t fl = dir == CT_INGRESS ? 0u : dir == CT_SERVICE ? 4u : 1u;
     if (proto == 6 || proto == 17) {
         k.td = pt & 0xFFFF;
         k.ts = pt >> 16;
@@ -415,6 +417,25 @@ __device__ __forceinline__ uint32_t ct_report(uint32_t &last, uint32_t &acc,
     }
     return 0u;
 }
+// the same against a given report state t (CtTimer as uint4)
+__device__ __forceinline__ uint32_t ct_monitor_of(const DevTables &T, uint4 t, int dir,
+                                                  uint32_t action, uint32_t fl)
+{
+    const bool in = dir == CT_INGRESS;
+    uint32_t last = in ? t.x : t.y;
+    uint32_t acc = in ? (t.z & 0xFF) : ((t.z >> 8) & 0xFF);
+    uint32_t clo = (t.z >> 16) & 3;
+    uint32_t m = 0;
+    if (clo != 3)   // ct_entry_alive
+        m = ct_report(last, acc, fl, T.now);
+    if (action == 1u) {
+        if (clo)
+            m = ct_report(last, acc, fl, T.now);
+    } else if (action == 2u) {
+        m = TRACE_PAYLOAD_LEN;
+    }
+    return m;
+}
 __device__ __forceinline__ uint32_t ct_monitor(const DevTables &T, const CtTimer *tm,
                                                uint32_t slot, int dir, uint32_t action,
                                                uint32_t fl, uint32_t dport)
@@ -438,6 +459,70 @@ __device__ __forceinline__ uint32_t ct_monitor(const DevTables &T, const CtTimer
     }
     return dport == 0x3500u ? MTU_LEN : m;   // conn_is_dns: htons(53)
 }
+
+// the engine's stand-in for skb->hash (cfc.h CFC_FLOW_HASH)
+__device__ __forceinline__ uint32_t flow_hash4(uint32_t sa, uint32_t da, uint32_t pt,
+                                               uint32_t proto)
+{
+    const uint32_t lo = min(sa, da), hi = max(sa, da);
+    const uint32_t sp = pt & 0xFFFF, dp = pt >> 16;
+    const uint32_t pw = min(sp, dp) | (max(sp, dp) << 16);
+    return fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + pw * 0xC2B2AE3Du + proto);
+}
+
+// ---- load balancing (lb.h) -------------------------------------------------
+// one cilium_lb4_services lookup (layout.h): the slot's two uint4, false on
+// a miss
+__device__ __forceinline__ bool lb4_get(const DevTables &T, uint32_t addr, uint32_t dport,
+                                        uint32_t slave, uint4 &a, uint4 &b)
+{
+    const uint32_t ps = dport | slave << 16;
+    uint32_t i = lb4_hash(addr, ps) & T.lb4_mask;
+    for (uint32_t p = 0; p <= T.lb4_mask; p++) {
+        a = ld16(T.lb4 + 2 * i);
+        b = ld16(T.lb4 + 2 * i + 1);
+        if (!b.y)
+            return false;
+        if (a.x == addr && a.y == ps)
+            return true;
+        i = (i + 1) & T.lb4_mask;
+    }
+    return false;
+}
+// lb4_lookup_service (lb.h:604-635): the L4 key while its dport is set (a
+// miss clears the caller's dport), then the L3 key; count must be nonzero
+__device__ __forceinline__ bool lb4_service(const DevTables &T, uint32_t addr,
+                                            uint32_t &dport, uint32_t slave, uint4 &a,
+                                            uint4 &b)
+{
+    if (dport) {
+        if (lb4_get(T, addr, dport, slave, a, b) && (a.w >> 16))
+            return true;
+        dport = 0;
+    }
+    return lb4_get(T, addr, 0, slave, a, b) && (a.w >> 16);
+}
+// lb4_rev_nat (lb.h:485-588) on a packet {sa, da, pt} for a CT entry whose
+// LB state is lw (ct4_lb): the source back to the service address and port,
+// and for a looped-back flow the old source into the destination
+__device__ __forceinline__ void lb4_rev_nat(const DevTables &T, uint4 lw, uint32_t proto,
+                                            uint32_t &sa, uint32_t &da, uint32_t &pt)
+{
+    const uint32_t rev = lw.x & 0xFFFF;
+    if (!rev || !T.rnat4)
+        return;
+    const uint2 rn = T.rnat4[rev];
+    if (!(rn.y >> 16))
+        return;
+    const uint32_t port = rn.y & 0xFFFF;
+    if (port && (proto == 6 || proto == 17))
+        pt = (pt & 0xFFFF0000u) | port;   // reverse_map_l4_port: the sport
+    if ((lw.x >> 16) & 1)
+        da = sa;
+    sa = rn.x;
+}
+// the service step's flags per header (lb.hip, cfc_api.cpp)
+constexpr uint32_t LBF_DROP = 1, LBF_SVC = 2, LBF_LOOP = 4;
 
 // key of ct_acct[slot][dir] (k_ct_count), NONE for a miss
 __device__ __forceinline__ uint32_t ct_acct_key(uint32_t slot, int dir)

@@ -320,6 +320,20 @@ struct alignas(16) Ct6Slot {
     uint32_t d[4], s[4], z, w, pad[2];
 };
 
+// ---- service load balancing (cilium_lb4_services, cilium_lb4_reverse_nat)
+// Services: open-addressed 32-byte slots keyed by struct lb4_key {address,
+// dport, slave} (load <= 1/2, linear probing, used == 0 marks a free slot):
+//   {addr, dport | slave << 16, target, port | count << 16,
+//    rev_nat_index | weight << 16, used, 0, 0}
+// Reverse NAT: direct-indexed by rev_nat_index, {address, port | 1 << 16}
+// (bit 16: present).  Per CT4 slot (ct4_lb, with a load balancer): the
+// entry's {rev_nat_index | lb_loopback << 16, slave, 0, 0}.
+__host__ __device__ inline uint32_t lb4_hash(uint32_t addr, uint32_t ps)
+{
+    return fmix32(fmix32(addr ^ 0x85ebca6bu) ^ ps);
+}
+constexpr uint32_t IPV4_LOOPBACK = 0x1FFFF50Au;   // node_config.h:45 (be32 raw)
+
 struct DevTables {
     const uint4 *l4d;              // compact IPv4 LPM /16 directory, or null
     const uint32_t *l4c;           // its chunks
@@ -367,6 +381,11 @@ struct DevTables {
     uint32_t v4_cluster_range;     // IPV4_CLUSTER_RANGE, be32 raw
     uint32_t v4_cluster_mask;      // IPV4_CLUSTER_MASK, be32 raw
     uint32_t router6[4];           // ROUTER_IP as host-order words
+    // load balancing (null: no service, no reverse NAT)
+    const uint4 *lb4;              // 2 uint4 per service slot
+    uint32_t lb4_mask;             // slots - 1
+    const uint2 *rnat4;            // [65536] or null
+    const uint4 *ct4_lb;           // per CT4 slot, or null
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]

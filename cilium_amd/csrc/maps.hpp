@@ -32,6 +32,8 @@ enum Role {
     ROLE_PF6_DYN,   // cilium_cidr_v6_dyn
     ROLE_CT4,       // cilium_ct4_* / cilium_ct_any4_* (global or <lxc_id>)
     ROLE_CT6,       // cilium_ct6_* / cilium_ct_any6_*
+    ROLE_LB4_SVC,   // cilium_lb4_services
+    ROLE_LB4_RNAT,  // cilium_lb4_reverse_nat
 };
 
 enum : int { TOUCH_VALUE = 1, TOUCH_INSERT = 2, TOUCH_ERASE = 4 };

@@ -34,6 +34,8 @@ __device__ __forceinline__ uint32_t fold6(const uint32_t *w)
 // symmetric 5-tuple hash (oracle/oracle.py flow_hash)
 __device__ __forceinline__ uint32_t flow_hash(const NotifyArgs &a, uint64_t i)
 {
+    if (a.hash)   // the batch's skb->hash
+        return a.hash[i];
     uint32_t x, y;
     if (a.family == 4) {
         x = a.saddr[i];

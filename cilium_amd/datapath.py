@@ -23,6 +23,7 @@ class HeaderBatchV4:
     meta: "torch.Tensor"      # proto | flags << 8 | len << 16
     mark: "torch.Tensor | None" = None
     tcp_flags: "torch.Tensor | None" = None   # uint8 TCP header byte 13
+    hash: "torch.Tensor | None" = None        # skb->hash (lb4_select_slave)
 
     def __len__(self):
         return int(self.saddr.numel())
@@ -62,6 +63,9 @@ class Verdicts:
     action: "torch.Tensor | None"  # uint8
     ct: "torch.Tensor | None" = None  # uint8 CT byte (cfc.h CFC_CT_*)
     notify: "torch.Tensor | None" = None  # int32 drop-notify site (CFC_NT_*)
+    # (IPv4) the packet as the programs left it: int32 (n, 3) saddr, daddr,
+    # first L4 word (cfc_out.pkt_*)
+    pkt: "torch.Tensor | None" = None
 
 
 def pack_v4(h, device="cuda"):
@@ -76,9 +80,11 @@ def pack_v4(h, device="cuda"):
         return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32)
                                 .view(np.int32)).to(device)
     from .synth import tcp_flags_of
+    hs = getattr(h, "hash", None)
     return HeaderBatchV4(t(h.saddr), t(h.daddr), t(ports), t(meta),
                          t(h.mark) if h.mark is not None else None,
-                         torch.from_numpy(tcp_flags_of(h).copy()).to(device))
+                         torch.from_numpy(tcp_flags_of(h).copy()).to(device),
+                         t(hs) if hs is not None else None)
 
 
 def pack_v6(h, device="cuda"):
@@ -111,15 +117,23 @@ def _ptr(t):
 def hdr_struct(batch, n=None):
     """cfc_hdr_v4 / cfc_hdr_v6 of a device batch (optionally its first n)."""
     v6 = isinstance(batch, HeaderBatchV6)
-    return (L.HdrV6 if v6 else L.HdrV4)(
-        _ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
-        _ptr(batch.meta), _ptr(batch.mark), _ptr(batch.tcp_flags),
-        len(batch) if n is None else n)
+    args = (_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
+            _ptr(batch.meta), _ptr(batch.mark), _ptr(batch.tcp_flags),
+            len(batch) if n is None else n)
+    return L.HdrV6(*args) if v6 else L.HdrV4(*args, _ptr(batch.hash))
 
 
 def out_struct(out):
+    pk = getattr(out, "pkt", None)
+    cols = (None, None, None) if pk is None else (pk[:, 0], pk[:, 1], pk[:, 2])
     return L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                 _ptr(out.ct), _ptr(out.notify))
+                 _ptr(out.ct), _ptr(out.notify), *[_col_ptr(c) for c in cols])
+
+
+def _col_ptr(c):
+    # a column of the (n, 3) packet output: every third int32 — the ABI wants
+    # three separate arrays, so the tensor is laid out column-major (3, n).T
+    return ctypes.c_void_p(c.data_ptr()) if c is not None else None
 
 
 def _stream_handle(stream):
@@ -273,7 +287,8 @@ class Datapath:
 
     def classify_v4(self, batch: HeaderBatchV4, mode=L.MODE_INGRESS, ep_lxc=0,
                     out: Verdicts | None = None, want_action=True,
-                    want_ct=False, want_notify=False, stream=None) -> Verdicts:
+                    want_ct=False, want_notify=False, want_pkt=False,
+                    stream=None) -> Verdicts:
         import torch
         n = len(batch)
         dev = batch.saddr.device
@@ -285,7 +300,14 @@ class Datapath:
                            torch.empty(n, dtype=torch.uint8, device=dev)
                            if want_ct else None,
                            torch.empty(n, dtype=torch.int32, device=dev)
-                           if want_notify else None)
+                           if want_notify else None,
+                           # column-major: each column one contiguous array
+                           torch.empty((3, n), dtype=torch.int32, device=dev).t()
+                           if want_pkt else None)
+        if out.pkt is not None:
+            assert out.pkt.shape == (n, 3) and out.pkt.stride() == (1, n)
+        if batch.hash is not None:
+            assert batch.hash.numel() == n and batch.hash.dtype == torch.int32
         for t in (batch.saddr, batch.daddr, batch.ports, batch.meta):
             assert t.is_cuda and t.is_contiguous() and t.numel() == n
             assert t.dtype == torch.int32
@@ -294,8 +316,7 @@ class Datapath:
         if batch.tcp_flags is not None:
             assert batch.tcp_flags.numel() == n and batch.tcp_flags.dtype == torch.uint8
         hdr = hdr_struct(batch)
-        o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct), _ptr(out.notify))
+        o = out_struct(out)
         L.check(self.L.cfc_classify_v4(self.h, ctypes.byref(hdr),
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)),"classify")

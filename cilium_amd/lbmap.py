@@ -1,0 +1,102 @@
+"""pkg/maps/lbmap (IPv4) over the engine's map API: cilium_lb4_services and
+cilium_lb4_reverse_nat with the reference's key and value layouts
+(lbmap/ipv4.go: Service4Key {Address, Port, Slave}, Service4Value {Address,
+Port, Count, RevNat, Weight}, RevNat4Key, RevNat4Value) and byte order
+(ToNetwork: ports, rev-NAT ids and weights network order; count host order),
+and UpdateService's slot layout (lbmap.go:351-420): backends in slots
+1..n, the master slot 0 carrying the count."""
+from __future__ import annotations
+
+import socket
+import struct
+
+from .datapath import Datapath
+
+MaxEntries = 65536                        # lbmap.go MaxEntries
+Service4MapName = "cilium_lb4_services"
+RevNat4MapName = "cilium_lb4_reverse_nat"
+MAP_TYPE_HASH = 1
+
+
+def _be16(x):
+    return struct.unpack("<H", struct.pack(">H", x & 0xFFFF))[0]
+
+
+def _ip(ip):
+    return ip if isinstance(ip, bytes) else socket.inet_aton(ip)
+
+
+class Service4Key:
+    """struct lb4_key (bpf/lib/common.h:427-431); port in host order here,
+    pack() is ToNetwork()."""
+
+    def __init__(self, ip, port, slave=0):
+        self.address, self.port, self.slave = _ip(ip), int(port), int(slave)
+
+    def pack(self):
+        return self.address + struct.pack("<HH", _be16(self.port), self.slave)
+
+
+class Service4Value:
+    """struct lb4_service (common.h:433-439)."""
+
+    def __init__(self, count=0, target="0.0.0.0", port=0, rev_nat=0, weight=0):
+        self.count, self.target, self.port = int(count), _ip(target), int(port)
+        self.rev_nat, self.weight = int(rev_nat), int(weight)
+
+    def pack(self):
+        return self.target + struct.pack("<HHHH", _be16(self.port), self.count,
+                                         _be16(self.rev_nat), _be16(self.weight))
+
+
+class RevNat4Value:
+    def __init__(self, ip, port):
+        self.address, self.port = _ip(ip), int(port)
+
+    def pack(self):
+        return self.address + struct.pack("<H", _be16(self.port))
+
+
+class LBMap:
+    def __init__(self, dp: Datapath):
+        self.dp = dp
+        self.svc, _ = dp.open_or_create_map(Service4MapName, MAP_TYPE_HASH, 8, 12,
+                                            MaxEntries)
+        self.rnat, _ = dp.open_or_create_map(RevNat4MapName, MAP_TYPE_HASH, 2, 6,
+                                             MaxEntries)
+
+    def UpdateService(self, fe: Service4Key, backends, add_revnat=True, revnat_id=0):
+        """lbmap.go UpdateService: backends[i] into slot i + 1, the reverse
+        NAT entry revnat_id -> frontend, then the master slot (count,
+        non-zero weights), then stale slots past the new count removed."""
+        old = self.dp.lookup_element(self.svc, Service4Key(fe.address, fe.port, 0).pack())
+        existing = struct.unpack_from("<H", old, 6)[0] if old else 0
+        for i, be in enumerate(backends):
+            self.dp.update_element(self.svc, Service4Key(fe.address, fe.port, i + 1).pack(),
+                                   be.pack())
+        if add_revnat:
+            self.dp.update_element(self.rnat, struct.pack("<H", _be16(revnat_id)),
+                                   RevNat4Value(fe.address, fe.port).pack())
+        nz = sum(1 for be in backends if be.weight)
+        self.dp.update_element(self.svc, Service4Key(fe.address, fe.port, 0).pack(),
+                               Service4Value(len(backends), weight=nz).pack())
+        for i in range(len(backends) + 1, existing + 1):
+            self.dp.delete_element(self.svc, Service4Key(fe.address, fe.port, i).pack())
+
+    def DeleteService(self, fe: Service4Key):
+        old = self.dp.lookup_element(self.svc, Service4Key(fe.address, fe.port, 0).pack())
+        n = struct.unpack_from("<H", old, 6)[0] if old else 0
+        for i in range(n, -1, -1):
+            k = Service4Key(fe.address, fe.port, i).pack()
+            if self.dp.lookup_element(self.svc, k) is not None:
+                self.dp.delete_element(self.svc, k)
+
+    def load_rows(self, lb4, revnat4):
+        """Raw synth.LB4_DT / REVNAT4_DT rows (already in map byte order)."""
+        import numpy as np
+        if lb4 is not None and len(lb4):
+            b = np.ascontiguousarray(lb4).view(np.uint8).reshape(len(lb4), 20)
+            self.dp.update_batch(self.svc, b[:, :8], b[:, 8:20])
+        if revnat4 is not None and len(revnat4):
+            b = np.ascontiguousarray(revnat4).view(np.uint8).reshape(len(revnat4), 8)
+            self.dp.update_batch(self.rnat, b[:, :2], b[:, 2:8])

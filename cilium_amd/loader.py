@@ -5,7 +5,7 @@ from __future__ import annotations
 
 import struct
 
-from . import cidrmap, ipcache, lxcmap, policymap
+from . import cidrmap, ipcache, lbmap, lxcmap, policymap
 from .datapath import Datapath
 
 
@@ -56,6 +56,8 @@ def load_tables(dp: Datapath, t, commit=True):
         dp.ct_fds = load_ct(dp, t)
     if getattr(t, "node", None) is not None:
         dp.set_node_config(*t.node)
+    if getattr(t, "lb4", None) is not None or getattr(t, "revnat4", None) is not None:
+        lbmap.LBMap(dp).load_rows(getattr(t, "lb4", None), getattr(t, "revnat4", None))
     if commit:
         dp.commit()
     return pms

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 6
+#define CFC_ABI_VERSION 7
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -67,6 +67,13 @@ int cfc_abi_version(void);
  *   cilium_metrics          PERCPU_HASH key 8 value 16 (one "CPU": the GPU)
  *   cilium_cidr_v4_fix|v4_dyn|v6_fix|v6_dyn   prefilter (pkg/maps/cidrmap)
  *                           HASH or LPM_TRIE, key 4+addr bytes, value 1
+ *   cilium_lb4_services     HASH key 8 (struct lb4_key {address, dport,
+ *                           slave}) value 12 (struct lb4_service {target,
+ *                           port, count, rev_nat_index, weight}); the
+ *                           master slot (slave 0) carries count, slots
+ *                           1..count the backends (pkg/maps/lbmap)
+ *   cilium_lb4_reverse_nat  HASH key 2 (rev_nat_index) value 6 (struct
+ *                           lb4_reverse_nat {address, port})
  * Any other name is a plain map with no datapath role.  Opening an existing
  * path with the same geometry returns a new handle to it (*created = 0);
  * a geometry mismatch returns -EINVAL (pkg/bpf/bpf.go:306 objCheck).
@@ -213,7 +220,15 @@ typedef struct {
     const uint32_t *mark;
     const uint8_t *tcp_flags;   /* may be NULL = 0 */
     uint64_t n;
+    /* skb->hash of each header (the kernel's flow hash, what
+     * lb4_select_slave reduces modulo a service's backend count, lb.h:158-190,
+     * and what the monitor records carry).  NULL = CFC_FLOW_HASH (below). */
+    const uint32_t *hash;
 } cfc_hdr_v4;
+/* The engine's stand-in for skb->hash when a batch carries none: symmetric
+ * in the 5-tuple, h = fmix32(min(sa,da) * 0x9E3779B1 + max(sa,da) *
+ * 0x85EBCA77 + (min(sp,dp) | max(sp,dp) << 16) * 0xC2B2AE3D + proto) over
+ * the header as it arrived (fmix32: murmur3's finalizer). */
 
 /* Device-resident SoA batch of IPv6 headers.  saddr/daddr: n addresses of
  * 16 network-order bytes each (16-byte aligned).  ports, meta and mark as in
@@ -293,6 +308,17 @@ typedef struct {
     uint8_t *action;
     uint8_t *ct;
     uint32_t *notify;
+    /* (IPv4, may be NULL) the packet's L3/L4 addresses as the programs left
+     * them: saddr, daddr and the first L4 word after service translation
+     * (lb4_local / lb4_xlate: a service address and port replaced by the
+     * backend's, a looped-back flow's source by IPV4_LOOPBACK) and reverse
+     * NAT of load-balanced replies (lb4_rev_nat: the backend's source back
+     * to the service address and port).  Headers the programs did not
+     * rewrite keep their input.  (A proxy redirect's new port is the
+     * verdict.) */
+    uint32_t *pkt_saddr;
+    uint32_t *pkt_daddr;
+    uint32_t *pkt_ports;
 } cfc_out;
 
 /* Classify a batch (asynchronous on `stream`).  Policy-entry and metrics

@@ -1,0 +1,140 @@
+"""GPU parity of service load balancing (bpf/lib/lb.h in the egress program,
+reverse NAT on both sides): the HIP engine through its C ABI against the
+reference's packets (lb_* goldens: skb->hash taken from the reference's own
+records, so backend selection is the reference's) and against the pinned
+oracle on larger seeded streams — verdicts, the packet each program left,
+the monitor records, CT maps with their CT_SERVICE and reverse-NAT entries.
+(Verdicts, counters and CT maps of the lb_* goldens are also checked by
+test_gpu_parity.test_golden.)"""
+import numpy as np
+import pytest
+
+import golden_io as G
+import oracle as O
+from cilium_amd import synth as S
+from cilium_amd import _lib as L
+from cilium_amd.datapath import Datapath, pack_v4
+from cilium_amd.loader import ct_rows, load_tables
+
+pytestmark = pytest.mark.gpu
+
+LB = [n for n in G.names() if n.startswith("lb_")]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "needs a GPU"
+    return torch
+
+
+def _run(torch, t, h, mode, ep, notify=False):
+    dp = Datapath(0)
+    load_tables(dp, t)
+    b = pack_v4(h, "cuda:0")
+    out = dp.classify_v4(b, mode, ep, want_ct=True, want_pkt=True, want_notify=notify)
+    torch.cuda.synchronize()
+    res = dict(act=out.action.cpu().numpy().astype(np.int32),
+               ver=out.verdict.cpu().numpy(),
+               ide=out.identity.cpu().numpy().view(np.uint32),
+               ct=out.ct.cpu().numpy(),
+               pkt=out.pkt.cpu().numpy().view(np.uint32))
+    if notify:
+        rec, idx, total = dp.monitor_events(b, out, mode, ep)
+        res["rec"] = rec.cpu().numpy()
+        res["idx"] = idx.cpu().numpy().astype(np.uint64)
+    dp.ct_apply(b, out, mode, ep)
+    res["ct_rows"] = ct_rows(dp, dp.ct_fds)
+    res["stats"] = dp.stats()
+    dp.close()
+    return res
+
+
+@pytest.mark.parametrize("name", LB)
+def test_lb_golden_packets(torch, name):
+    g = G.Golden(name)
+    r = _run(torch, g.tables, g.headers, g.mode, g.ep_lxc)
+    assert len(G.mismatches(g, r["act"], r["ver"], r["ide"])) == 0
+    keep = (g.action != 2) & ~((g.action == 7) & (g.verdict > 0))
+    np.testing.assert_array_equal(r["pkt"][keep], g.pkt[keep])
+    o = O.Oracle(g.tables)
+    oa, ov, oi, oct_, opk = o.classify(g.headers, g.mode, g.ep_lxc, nthreads=8,
+                                       want_ct=True, want_pkt=True, apply_ct=True)
+    np.testing.assert_array_equal(r["pkt"], opk)
+    np.testing.assert_array_equal(r["ct"], oct_)
+    np.testing.assert_array_equal(r["ct_rows"], o.ct_dump())
+    np.testing.assert_array_equal(G.ct_masked(r["ct_rows"]), G.ct_masked(g.ct_after))
+    # the device CT apply leaves service entries to the host walk
+    assert r["stats"]["ct_apply_host"] == 1
+
+
+@pytest.mark.parametrize("name", LB)
+def test_lb_golden_records(torch, name):
+    """trace / drop records of the batch, the batch's skb->hash in each"""
+    g = G.Golden(name)
+    r = _run(torch, g.tables, g.headers, g.mode, g.ep_lxc, notify=True)
+    o = O.Oracle(g.tables)
+    oa, ov, oi, ow = o.classify(g.headers, g.mode, g.ep_lxc, nthreads=8,
+                                want_notify=True)
+    orec, oidx = o.events(g.headers, g.mode, g.ep_lxc, ov, oi, ow)
+    np.testing.assert_array_equal(r["idx"], oidx)
+    np.testing.assert_array_equal(
+        np.ascontiguousarray(r["rec"]).view(np.uint8).reshape(-1),
+        np.ascontiguousarray(orec).view(np.uint8).reshape(-1))
+
+
+def _lb_stream(seed, n, mode):
+    """C2-sized tables with services; an egress history folded into CT by
+    the oracle, then a stream of established and new service flows, looped
+    back flows' replies, plain traffic (egress) or backends' replies
+    (ingress)."""
+    rng = np.random.default_rng(seed)
+    t = S.config_c2(seed, n_prefixes=20_000, n_policy=2000, n_endpoints=2)
+    t.lb4, t.revnat4, vips, ports, protos = S.lb4_services(rng, t, n_services=200)
+    k = rng.integers(0, len(vips), size=n)
+    h = S.Headers(4, np.full(n, S.LXC_IPV4, np.uint32), vips[k].copy(),
+                  S.htons(rng.integers(1024, 65536, size=n)), ports[k].copy(),
+                  protos[k].copy(), np.zeros(n, np.uint8),
+                  rng.integers(60, 1500, size=n).astype(np.uint16),
+                  np.zeros(n, np.uint32))
+    z = h.dport == 0
+    h.dport[z] = S.htons(rng.integers(1, 65536, size=int(z.sum())))
+    h.hash = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    o = O.Oracle(t)
+    hist = h.slice(0, n // 2)
+    _, _, _, ct, pk = o.classify(hist, 1, S.EP_LXC_ID, want_ct=True, want_pkt=True,
+                                 apply_ct=True)
+    t.ct = S.ct_from_rows(o.ct_dump())
+    if mode == 1:
+        test = h.slice(n // 2, n)
+        plain = S.gen_headers_v4(rng, n // 4, t.ipcache, S.local_v4_addrs(t),
+                                 local_frac=0.3, mark_host=0, mark_proxy=0,
+                                 src_fixed=S.LXC_IPV4, frag=0)
+        plain.hash = rng.integers(0, 1 << 32, size=len(plain), dtype=np.uint64).astype(np.uint32)
+        test = S.concat([test, hist.slice(0, n // 4), plain])
+    else:   # replies from the backends the history reached
+        ok = (pk[:, 0] == S.LXC_IPV4) & (hist.proto != S.IPPROTO_ICMP)
+        p = pk[ok]
+        test = S.Headers(4, p[:, 1].copy(), p[:, 0].copy(),
+                         (p[:, 2] >> 16).astype(np.uint16),
+                         (p[:, 2] & 0xFFFF).astype(np.uint16), hist.proto[ok].copy(),
+                         np.zeros(len(p), np.uint8), hist.length[ok].copy(),
+                         np.zeros(len(p), np.uint32))
+    test = S.take(test, rng.permutation(len(test)))
+    return t, test
+
+
+@pytest.mark.parametrize("mode", [1, 0])
+def test_lb_stream_vs_oracle(torch, mode):
+    t, h = _lb_stream(71 + mode, 200_000, mode)
+    ep = S.EP_LXC_ID if mode == 1 else 0
+    r = _run(torch, t, h, mode, ep)
+    o = O.Oracle(t)
+    oa, ov, oi, oct_, opk = o.classify(h, mode, ep, nthreads=16, want_ct=True,
+                                       want_pkt=True, apply_ct=True)
+    for k, want in (("act", oa), ("ver", ov), ("ide", oi), ("ct", oct_), ("pkt", opk)):
+        bad = np.nonzero((r[k] != want).reshape(len(h), -1).any(1))[0]
+        assert len(bad) == 0, f"{k}: {len(bad)} differ, first {bad[:8]}"
+    assert (r["ver"] == -158).any() or mode == 0
+    assert (r["pkt"][:, 1] != h.daddr).sum() > len(h) // 10 or mode == 0
+    np.testing.assert_array_equal(r["ct_rows"], o.ct_dump())
