@@ -1198,6 +1198,8 @@ bool role_geometry_ok(Role r, uint32_t type, uint32_t ks, uint32_t vs)
     case ROLE_PF6_DYN: return type == MT_LPM_TRIE && ks == 20 && vs == 1;
     case ROLE_CT4: return (type == MT_LRU_HASH || type == MT_HASH) && ks == 14 && vs == 56;
     case ROLE_CT6: return (type == MT_LRU_HASH || type == MT_HASH) && ks == 38 && vs == 56;
+    case ROLE_LB4_SVC: return type == MT_HASH && ks == 8 && vs == 12;     // lbmap/ipv4.go:27
+    case ROLE_LB4_RNAT: return type == MT_HASH && ks == 2 && vs == 6;     // :43
     default: return true;
     }
 }
@@ -2428,9 +2430,22 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     const uint32_t now = c->now;
     const uint8_t icmp = family == 4 ? 1 : 58;
     const uint32_t echo = family == 4 ? 8 : 128, echo_reply = family == 4 ? 0 : 129;
-    // keys this apply wrote: a later hit on one of them was not counted by
-    // the device (the entry did not exist when the batch was classified)
-    std::unordered_set<std::string> made;
+    // whether each key this apply writes was in the maps when the batch was
+    // classified: a hit on an entry that was not (one a header's own egress
+    // stage created, which its destination stage then finds) was not counted
+    // by the device, so the walk counts it
+    std::unordered_map<std::string, bool> initial;
+    auto note = [&](Map *mp, const std::string &key) {
+        initial.emplace(key, mp->kv.count(key) != 0);
+    };
+    auto put_new = [&](Map *mp, const std::string &key, const CtEntry &e) {
+        note(mp, key);
+        (void)mp->update(key.data(), &e, 0);
+    };
+    auto fresh = [&](const std::string &key) {
+        auto it = initial.find(key);
+        return it != initial.end() && !it->second;
+    };
     for (size_t i = 0; i < n; i++) {
         const uint8_t cb = ct[i];
         const uint32_t proto = mt[i] & 0xFF, len = mt[i] >> 16;
@@ -2476,10 +2491,10 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                     ct_upd_timeout(e, now, is_tcp, 0, is_tcp, 0);
                     e.tx_packets = 1;
                     e.tx_bytes = len;
-                    if (x.reslave && !x.drop)
-                        e.slave = x.slave;
-                    (void)m0->update(x.ksvc.data(), &e, 0);
-                    made.insert(x.ksvc);
+                    CtEntry es = e;
+                    if (x.reslave && !x.drop)   // ct_update4_slave: this entry only
+                        es.slave = x.slave;
+                    put_new(m0, x.ksvc, es);
                     std::string ki = x.ksvc;
                     memset(&ki[8], 0, 4);
                     ki[12] = (char)icmp;
@@ -2487,8 +2502,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                     e.bits |= CTB_SEEN_NON_SYN;
                     if (m0->kv.count(ki))
                         ct_drop_counts(c, m0, ki, s);
-                    (void)m0->update(ki.data(), &e, 0);
-                    made.insert(ki);
+                    put_new(m0, ki, e);
                 }
             }
         }
@@ -2550,7 +2564,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             if (b >= 2) {                       // CT_REPLY / CT_RELATED
                 auto it = m->kv.find(k1);
                 if (it != m->kv.end()) {
-                    ct_hit_update(m, it->second, action, dir, made.count(k1) > 0, len, now,
+                    ct_hit_update(m, it->second, action, dir, fresh(k1), len, now,
                                   is_tcp, syn, tflags);
                     if (lbon && eg) {   // the egress reply's reverse NAT
                         CtEntry e;
@@ -2561,10 +2575,11 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             } else if (b == 1) {                // CT_ESTABLISHED
                 auto it = m->kv.find(k2);
                 if (it != m->kv.end()) {
-                    ct_hit_update(m, it->second, action, dir, made.count(k2) > 0, len, now,
+                    ct_hit_update(m, it->second, action, dir, fresh(k2), len, now,
                                   is_tcp, syn, tflags);
                     if (dropped) {              // ct_delete4/6
                         ct_drop_counts(c, m, k2, s);
+                        note(m, k2);
                         (void)m->erase(k2.data());
                     }
                 }
@@ -2590,8 +2605,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                     if (x.loopback)
                         e.bits |= CTB_LB_LOOPBACK;
                 }
-                (void)m->update(k2.data(), &e, 0);
-                made.insert(k2);
+                put_new(m, k2, e);
                 if (eg && x.svc && x.addr) {    // the reverse-NAT entry
                     std::string kx = k2;
                     memcpy(&kx[0], &x.addr, 4);
@@ -2601,8 +2615,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                     }
                     if (m->kv.count(kx))
                         ct_drop_counts(c, m, kx, s);
-                    (void)m->update(kx.data(), &e, 0);
-                    made.insert(kx);
+                    put_new(m, kx, e);
                 }
                 e.bits |= CTB_SEEN_NON_SYN;     // "For ICMP, there is no SYN"
                 const std::string ki = [&] {
@@ -2614,8 +2627,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 }();
                 if (m->kv.count(ki))            // overwritten
                     ct_drop_counts(c, m, ki, s);
-                (void)m->update(ki.data(), &e, 0);
-                made.insert(ki);
+                put_new(m, ki, e);
             }
         }
     }

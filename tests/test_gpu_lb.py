@@ -44,6 +44,7 @@ def _run(torch, t, h, mode, ep, notify=False):
         res["rec"] = rec.cpu().numpy()
         res["idx"] = idx.cpu().numpy().astype(np.uint64)
     dp.ct_apply(b, out, mode, ep)
+    dp.counters_sync()   # the device's CONNTRACK_ACCOUNTING into the maps
     res["ct_rows"] = ct_rows(dp, dp.ct_fds)
     res["stats"] = dp.stats()
     dp.close()
@@ -62,6 +63,16 @@ def test_lb_golden_packets(torch, name):
                                        want_ct=True, want_pkt=True, apply_ct=True)
     np.testing.assert_array_equal(r["pkt"], opk)
     np.testing.assert_array_equal(r["ct"], oct_)
+    keys = _ct_diff(r["ct_rows"], o.ct_dump())
+    h = g.headers
+    for k in keys[:3]:   # the headers whose ports are the differing entry's
+        kb = np.frombuffer(k, np.uint8)
+        a, b = int(kb[12]) | int(kb[13]) << 8, int(kb[14]) | int(kb[15]) << 8
+        sel = np.flatnonzero(((h.sport == a) & (h.dport == b)) | ((h.sport == b) & (h.dport == a)))
+        for i in sel[:6]:
+            print("  hdr", i, hex(h.saddr[i]), hex(h.daddr[i]), hex(h.sport[i]), hex(h.dport[i]),
+                  h.proto[i], "ct", hex(r["ct"][i]), "ver", r["ver"][i], "pkt",
+                  [hex(x) for x in r["pkt"][i]], "hash", h.hash[i])
     np.testing.assert_array_equal(r["ct_rows"], o.ct_dump())
     np.testing.assert_array_equal(G.ct_masked(r["ct_rows"]), G.ct_masked(g.ct_after))
     # the device CT apply leaves service entries to the host walk
@@ -81,6 +92,25 @@ def test_lb_golden_records(torch, name):
     np.testing.assert_array_equal(
         np.ascontiguousarray(r["rec"]).view(np.uint8).reshape(-1),
         np.ascontiguousarray(orec).view(np.uint8).reshape(-1))
+
+
+def _ct_diff(got, want):
+    """print what differs between two CT dumps (keys, then values)"""
+    kg = {bytes(r[:44]): r for r in got}
+    kw = {bytes(r[:44]): r for r in want}
+    for k in list(set(kg) - set(kw))[:6]:
+        print("engine only", k.hex())
+    for k in list(set(kw) - set(kg))[:6]:
+        print("oracle only", k.hex())
+    out = []
+    for k in kg:
+        if k in kw and not np.array_equal(kg[k], kw[k]):
+            cols = np.nonzero(kg[k] != kw[k])[0]
+            if len(out) < 8:
+                print("differs", k.hex(), cols, kg[k][cols], kw[k][cols])
+            out.append(k)
+    print("differing entries", len(out), "of", len(kg))
+    return out
 
 
 def _lb_stream(seed, n, mode):
@@ -137,4 +167,5 @@ def test_lb_stream_vs_oracle(torch, mode):
         assert len(bad) == 0, f"{k}: {len(bad)} differ, first {bad[:8]}"
     assert (r["ver"] == -158).any() or mode == 0
     assert (r["pkt"][:, 1] != h.daddr).sum() > len(h) // 10 or mode == 0
+    _ct_diff(r["ct_rows"], o.ct_dump())
     np.testing.assert_array_equal(r["ct_rows"], o.ct_dump())

@@ -53,3 +53,16 @@ def test_synth_rows_load():
     want = sorted(r.tobytes() for r in lb)
     assert got == want
     dp.close()
+
+
+def test_lb_map_geometry_checked():
+    """objCheck: the load balancer's maps only with the reference's geometry"""
+    import errno
+    import pytest
+    dp = host_only()
+    with pytest.raises(OSError) as e:
+        dp.open_or_create_map("cilium_lb4_services", 1, 8, 16, 65536)
+    assert e.value.errno == errno.EINVAL
+    with pytest.raises(OSError):
+        dp.open_or_create_map("cilium_lb4_reverse_nat", 1, 4, 6, 65536)
+    dp.close()
