@@ -2434,16 +2434,18 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     // classified: a hit on an entry that was not (one a header's own egress
     // stage created, which its destination stage then finds) was not counted
     // by the device, so the walk counts it
-    std::unordered_map<std::string, bool> initial;
+    // (keyed by map and tuple: one tuple can live in several maps, e.g. a
+    // TCP and a UDP create's ICMP entry, or a global and a local map)
+    std::map<std::pair<const Map *, std::string>, bool> initial;
     auto note = [&](Map *mp, const std::string &key) {
-        initial.emplace(key, mp->kv.count(key) != 0);
+        initial.emplace(std::make_pair((const Map *)mp, key), mp->kv.count(key) != 0);
     };
     auto put_new = [&](Map *mp, const std::string &key, const CtEntry &e) {
         note(mp, key);
         (void)mp->update(key.data(), &e, 0);
     };
-    auto fresh = [&](const std::string &key) {
-        auto it = initial.find(key);
+    auto fresh = [&](const Map *mp, const std::string &key) {
+        auto it = initial.find(std::make_pair(mp, key));
         return it != initial.end() && !it->second;
     };
     for (size_t i = 0; i < n; i++) {
@@ -2564,7 +2566,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             if (b >= 2) {                       // CT_REPLY / CT_RELATED
                 auto it = m->kv.find(k1);
                 if (it != m->kv.end()) {
-                    ct_hit_update(m, it->second, action, dir, fresh(k1), len, now,
+                    ct_hit_update(m, it->second, action, dir, fresh(m, k1), len, now,
                                   is_tcp, syn, tflags);
                     if (lbon && eg) {   // the egress reply's reverse NAT
                         CtEntry e;
@@ -2575,7 +2577,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             } else if (b == 1) {                // CT_ESTABLISHED
                 auto it = m->kv.find(k2);
                 if (it != m->kv.end()) {
-                    ct_hit_update(m, it->second, action, dir, fresh(k2), len, now,
+                    ct_hit_update(m, it->second, action, dir, fresh(m, k2), len, now,
                                   is_tcp, syn, tflags);
                     if (dropped) {              // ct_delete4/6
                         ct_drop_counts(c, m, k2, s);

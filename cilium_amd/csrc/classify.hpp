@@ -127,7 +127,7 @@ struct CtSyncRec {
     uint32_t last_rx, last_tx, flags, lifetime;
     uint32_t pad;
 };
-enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NCNT = 8 };
+enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NCNT = 8 };
 struct CtaArgs {
     DevTables T;
     const uint32_t *sa, *da, *pt, *mt;
@@ -146,6 +146,7 @@ struct CtaArgs {
     uint32_t *hs;                // [2n] hit slot per header and stage
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
     uint32_t req_cap, cx_cap;
+    uint32_t cx_base;            // route: its ordered ops start here
     CtLog *log;
     uint32_t log_base, log_cap;  // entries before this apply, capacity left
     uint32_t *cnt;               // CTA_* counters

@@ -60,6 +60,37 @@ __device__ __forceinline__ uint32_t wave_count(uint32_t *ctr, bool want)
     return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
 }
 
+// the same for a whole block of 256 threads: one atomic per block, not per
+// wave (a counter every wave of a 64M-header pass bumps serialises at its
+// L2 channel).  Every thread of the block calls it.
+__device__ __forceinline__ uint32_t block_count(uint32_t *ctr, bool want)
+{
+    __shared__ uint32_t wsum[4], base;
+    const uint64_t m = __ballot(want);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0)
+        wsum[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        base = t ? atomicAdd(ctr, t) : 0u;
+    }
+    __syncthreads();
+    uint32_t r = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    for (uint32_t k = 0; k < wv; k++)
+        r += wsum[k];
+    __syncthreads();   // wsum and base are reused by the next call
+    return r;
+}
+// a per-thread count added once per wave (every lane of the wave calls it)
+__device__ __forceinline__ void wave_add(uint32_t *ctr, uint32_t v)
+{
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v)
+        atomicAdd(ctr, v);
+}
+
 // one CT stage of one header, decoded as cfc_api.cpp ct_apply does
 struct Op {
     uint32_t kind, action, dir;
@@ -173,6 +204,7 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
 __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint32_t nhit = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
         const uint64_t i = base + threadIdx.x;
         const bool in = i < A.n;
@@ -190,8 +222,14 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     if (o.kind == OP_DELETE) {
                         // the entry goes: only its first delete matters
                         // (k_cta_route), unless a create revives the key
+                        // (a dropped hot flow deletes its entry once per
+                        // packet: only a lower order than the one stored
+                        // needs the atomic)
                         mark_or(&A.mark[slot], MARK_ORDERED | MARK_DEL);
-                        atomicMax(&A.sum[slot], 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1));
+                        const uint32_t v = 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1);
+                        if (__hip_atomic_load(&A.sum[slot], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) < v)
+                            atomicMax(&A.sum[slot], v);
                     } else if (o.action == 2 || clo) {
                         mark_or(&A.mark[slot], MARK_ORDERED);
                     }
@@ -201,15 +239,16 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
             }
             if (in)
                 A.hs[2 * i + st] = slot;
-            (void)wave_count(&A.cnt[CTA_NHIT], slot != HS_NONE);
+            nhit += slot != HS_NONE;
             const bool req = o.kind == OP_CREATE;
-            const uint32_t r = wave_count(&A.cnt[CTA_NREQA], req);
+            const uint32_t r = block_count(&A.cnt[CTA_NREQA], req);
             if (req && r < A.req_cap) {
                 const uint32_t home = ct_hash4(o.x2, o.y2, o.z2, o.w2) & A.T.ct4_mask;
                 A.reqA[r] = pack(A, home, (uint32_t)((2 * i + st) << 1));
             }
         }
     }
+    wave_add(&A.cnt[CTA_NHIT], nhit);
 }
 
 // key of a request: k2 of its op (round A) or the ICMP entry k2 relates
@@ -229,7 +268,7 @@ __device__ __forceinline__ uint4 req_key(const CtaArgs &A, uint32_t order2, bool
 // ---- insert: one thread per home slot; keys deduped in registers (a fifth
 // distinct key of one home slot is found by rescanning the run)
 __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, const uint64_t *req,
-                                                    uint32_t nreq, int round)
+                                                    uint32_t nreq, int round, uint32_t cx_off)
 {
     const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
     if (r0 >= nreq)
@@ -272,8 +311,9 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, const uint64_t *r
                 ks[nk++] = slot;
             }
         }
-        // every create and related-entry write is an ordered op
-        const uint32_t c = atomicAdd(&A.cnt[CTA_NCX], 1u);
+        // every create and related-entry write is an ordered op: request r
+        // of the round has its own place in the list
+        const uint32_t c = cx_off + r;
         if (c < A.cx_cap)
             A.cx[c] = pack(A, slot, order2 | (uint32_t)round);
         // the key's first create writes its related ICMP entry next: into
@@ -335,7 +375,7 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
                     atomicOr(&A.sum[slot], bits);
             }
         }
-        const uint32_t c = wave_count(&A.cnt[CTA_NCX], ordered);
+        const uint32_t c = A.cx_base + block_count(&A.cnt[CTA_NCX], ordered);
         if (ordered && c < A.cx_cap)
             A.cx[c] = pack(A, slot, (uint32_t)(j << 1));
     }
@@ -415,9 +455,51 @@ __device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St
     *reinterpret_cast<uint4 *>(tm + slot) = t;
 }
 
-// ---- fold: one thread per slot of the sorted ordered list
-__global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx, uint32_t ncx)
+// ---- dedup: in the sorted ordered list, a plain hit identical to the op
+// before it on the same slot (same direction, action, protocol, close bit
+// and TCP flags) changes nothing — with one clock per batch a hit's state
+// update is idempotent: hit(hit(e)) = hit(e) — so only the first of each
+// such run is replayed.  A hot flow's hits in a Zipf batch become one op.
+// (Creates, deletes and related-entry writes are always kept.)
+__device__ __forceinline__ uint32_t hit_sig(const CtaArgs &A, uint32_t order2)
 {
+    if (order2 & 1)
+        return 0;   // a related-entry write
+    const uint64_t i = order2 >> 2;
+    const int st = (order2 >> 1) & 1;
+    const uint32_t cb = A.ctb[i];
+    const uint32_t cs = (cb >> (4 * st)) & 0xF;
+    const uint32_t b = cs & CFC_CT_RES_MASK;
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    const bool dropped = st == last && A.ver[i] == DROP_POLICY;
+    if (!(cs & CFC_CT_DONE) || (b == 0) || (b == 1 && dropped))
+        return 0;   // not a plain hit
+    const uint32_t mt = A.mt[i], proto = mt & 0xFF;
+    const uint32_t tfl = (proto == 6 && A.tf) ? A.tf[i] : 0u;
+    const uint32_t act = ct_action(false, proto, A.pt[i], mt);
+    return 1u | (uint32_t)st << 1 | act << 2 | (mt & CFC_HF_TCP_CLOSE ? 1u : 0u) << 4 |
+           tfl << 8 | proto << 16;
+}
+__global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx, uint32_t ncx,
+                                                   uint8_t *keep)
+{
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= ncx)
+        return;
+    const uint64_t omask = (1ull << A.ob) - 1;
+    bool k = true;
+    if (r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob)) {
+        const uint32_t s1 = hit_sig(A, (uint32_t)(cx[r] & omask));
+        k = !s1 || s1 != hit_sig(A, (uint32_t)(cx[r - 1] & omask));
+    }
+    keep[r] = k;
+}
+
+// ---- fold: one thread per slot of the sorted ordered list
+__global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
+                                                  const uint32_t *pncx)
+{
+    const uint32_t ncx = *pncx;   // (the deduplicated list's length)
     const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
     if (r0 >= ncx)
         return;
@@ -545,7 +627,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const Ct4Slot *ct4, CtTimer
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < slots; base += stride) {
         const uint64_t s = base + threadIdx.x;
         const bool dirty = s < slots && (info[s].y >> 16) != 0;
-        const uint32_t r = wave_count(cnt, dirty);
+        const uint32_t r = block_count(cnt, dirty);
         if (!dirty || r >= cap)
             continue;
         CtSyncRec &o = out[r];
@@ -603,11 +685,15 @@ int sort_keys(const CtaArgs &A, uint64_t *keys, uint64_t *alt, uint32_t n, int b
 
 size_t cta_sort_tmp_bytes(uint32_t n)
 {
-    size_t tb = 0;
+    size_t tb = 0, ts = 0;
     hipcub::DoubleBuffer<uint64_t> db(nullptr, nullptr);
     (void)hipcub::DeviceRadixSort::SortKeys(nullptr, tb, db, (int)std::max<uint32_t>(n, 2u), 0,
                                             64, (hipStream_t)0);
-    return tb;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, ts, (const uint64_t *)nullptr,
+                                        (const uint8_t *)nullptr, (uint64_t *)nullptr,
+                                        (uint32_t *)nullptr, (int)std::max<uint32_t>(n, 2u),
+                                        (hipStream_t)0);
+    return std::max(tb, ts);
 }
 
 int cta_scan(const CtaArgs &A, hipStream_t s)
@@ -628,7 +714,7 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
         return rc;
     if (nreqA)
         hipLaunchKernelGGL(k_cta_insert, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
-                           (const uint64_t *)sorted, nreqA, 0);
+                           (const uint64_t *)sorted, nreqA, 0, 0u);
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -639,19 +725,38 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
         return rc;
     if (nreqB)
         hipLaunchKernelGGL(k_cta_insert, dim3((nreqB + 255) / 256), dim3(256), 0, s, A,
-                           (const uint64_t *)sorted, nreqB, 1);
-    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for(2 * A.n, 8192)), dim3(256), 0, s, A);
+                           (const uint64_t *)sorted, nreqB, 1, nreqA);
+    // the creates' ops take the list's first nreqA + nreqB places, route's
+    // ordered hits follow
+    CtaArgs R = A;
+    R.cx_base = nreqA + nreqB;
+    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for(2 * A.n, 8192)), dim3(256), 0, s, R);
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
-    const uint32_t ncx = host_cnt[CTA_NCX];
+    const uint64_t ncx64 = (uint64_t)nreqA + nreqB + host_cnt[CTA_NCX];
+    if (ncx64 > A.cx_cap)
+        return -EOVERFLOW;
+    const uint32_t ncx = (uint32_t)ncx64;
     if (ncx > A.cx_cap)
         return -EOVERFLOW;
     if ((rc = sort_keys(A, A.cx, A.cx2, ncx, bits, s, &sorted)))
         return rc;
-    if (ncx)
+    if (ncx) {
+        // drop the repeated plain hits, compact what stays into the other
+        // buffer, fold that
+        uint64_t *dst = sorted == A.cx ? A.cx2 : A.cx;
+        uint8_t *keep = reinterpret_cast<uint8_t *>(A.hs);   // (hit slots: read by route only)
+        uint32_t *nsel = A.cnt + CTA_NDEDUP;
+        hipLaunchKernelGGL(k_cta_dedup, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
+                           (const uint64_t *)sorted, ncx, keep);
+        size_t tb = A.sort_tmp_bytes;
+        if (hipcub::DeviceSelect::Flagged(A.sort_tmp, tb, sorted, keep, dst, nsel, (int)ncx, s) !=
+            hipSuccess)
+            return -EIO;
         hipLaunchKernelGGL(k_cta_fold, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
-                           (const uint64_t *)sorted, ncx);
+                           (const uint64_t *)dst, (const uint32_t *)nsel);
+    }
     hipLaunchKernelGGL(k_cta_finish, dim3(blocks_for((uint64_t)A.T.ct4_mask + 1, 8192)),
                        dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
