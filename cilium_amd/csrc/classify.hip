@@ -860,9 +860,15 @@ __global__ __launch_bounds__(BLOCK) void k_hist(HistJobs J, const uint32_t *meta
     const uint64_t end = min(n, start + per_block);
     const uint64_t end4 = start + ((end - start) & ~3ull);
     const bool meta16 = (reinterpret_cast<uintptr_t>(meta) & 15) == 0;
-    for (uint64_t i = start + 4 * threadIdx.x; i < end4; i += 4 * BLOCK) {
-        const uint4 w = ld_nt4(jb.keys + i);
-        uint4 m = make_uint4(0, 0, 0, 0);
+    // the loads of the next two steps are in flight during this step's LDS
+    // atomics (one workgroup per CU: a step that waits for its own loads
+    // waits a full HBM latency)
+    auto load = [&](uint64_t i, uint4 &w, uint4 &m) {
+        w = make_uint4(KEY_NONE, KEY_NONE, KEY_NONE, KEY_NONE);
+        m = make_uint4(0, 0, 0, 0);
+        if (i >= end4)
+            return;
+        w = ld_nt4(jb.keys + i);
         if (!jb.packed) {
             if (meta16) {
                 m = ld_nt4(meta + i);
@@ -873,10 +879,20 @@ __global__ __launch_bounds__(BLOCK) void k_hist(HistJobs J, const uint32_t *meta
                 m.w = meta[i + 3];
             }
         }
-        hist_add(s, jb, w.x, m.x);
-        hist_add(s, jb, w.y, m.y);
-        hist_add(s, jb, w.z, m.z);
-        hist_add(s, jb, w.w, m.w);
+    };
+    const uint64_t i0 = start + 4 * threadIdx.x;
+    uint4 w0, m0, w1, m1;
+    load(i0, w0, m0);
+    load(i0 + 4 * BLOCK, w1, m1);
+    for (uint64_t i = i0; i < end4; i += 4 * BLOCK) {
+        uint4 w2, m2;
+        load(i + 8 * BLOCK, w2, m2);
+        hist_add(s, jb, w0.x, m0.x);
+        hist_add(s, jb, w0.y, m0.y);
+        hist_add(s, jb, w0.z, m0.z);
+        hist_add(s, jb, w0.w, m0.w);
+        w0 = w1; m0 = m1;
+        w1 = w2; m1 = m2;
     }
     for (uint64_t i = end4 + threadIdx.x; i < end; i += BLOCK)
         hist_add(s, jb, jb.keys[i], jb.packed ? 0u : meta[i]);
@@ -1020,6 +1036,19 @@ constexpr uint32_t ACC_AGG_LDS =
 constexpr uint32_t ACC_SORT_LDS = ACC_CHUNK * 8 + 3 * ACC_MAX_COARSE * 4 + 16;
 constexpr uint32_t ACC_RED_LDS = CTP_BUCKET * 12;
 
+// slice of one k_acc_agg workgroup: <= COUNT_PER_BLOCK headers (a multiple
+// of 4), sized so that a large batch's slices come in whole rounds of 256
+// workgroups (one per CU) rather than four rounds and a few stragglers
+uint64_t acc_slice(uint64_t n)
+{
+    const uint64_t full = 256ull * COUNT_PER_BLOCK;
+    if (n <= full)
+        return COUNT_PER_BLOCK;
+    const uint64_t rounds = (n + full - 1) / full;
+    const uint64_t per = (n + 256 * rounds - 1) / (256 * rounds);
+    return (per + 3) & ~3ull;
+}
+
 __device__ __forceinline__ uint64_t acc_rec(uint32_t k, uint32_t pk, uint32_t by)
 {
     return (uint64_t)k << 38 | (uint64_t)pk << 21 | by;
@@ -1046,11 +1075,12 @@ constexpr int CTP_PROBES = 3;
 
 // A: slice vw's records into rec[vw * ACC_RCAP ...]; cnt[c * nch + vw *
 // ACC_SLICE_CHUNKS + q] = records of coarse bucket c in the slice's chunk q
+template <bool VEC>
 __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
                                                    const uint32_t *ct_idx2,
                                                    const uint32_t *meta, uint64_t n,
                                                    uint32_t nco, uint64_t *rec,
-                                                   uint32_t *rcnt, uint32_t *cnt)
+                                                   uint32_t *rcnt, uint32_t *cnt, uint64_t per)
 {
     uint32_t *keys = reinterpret_cast<uint32_t *>(cfc_smem);
     unsigned long long *vals = reinterpret_cast<unsigned long long *>(keys + CT_LDS_SLOTS);
@@ -1069,24 +1099,16 @@ __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
     const uint32_t vw = blockIdx.y * gridDim.x + blockIdx.x;
     const uint32_t *idx = blockIdx.y ? ct_idx2 : ct_idx;
     uint64_t *rs = rec + (uint64_t)vw * ACC_RCAP;
-    const uint64_t start = (uint64_t)blockIdx.x * COUNT_PER_BLOCK;
-    const uint64_t end = min(n, start + COUNT_PER_BLOCK);
+    const uint64_t start = (uint64_t)blockIdx.x * per;
+    const uint64_t end = min(n, start + per);
     auto put = [&](uint32_t r, uint64_t v) {
         rs[r] = v;
         atomicAdd(&hist[(r >> ACC_CHUNK_BITS) * ACC_MAX_COARSE + (uint32_t)(v >> ACC_COARSE_SHIFT)],
                   1u);
     };
-    // the next iteration's key and length are loaded before this one's LDS
-    // work, so their HBM latency overlaps it
-    uint64_t i = start + threadIdx.x;
-    uint32_t nk = i < end ? ld_nt(idx + i) : NONE;
-    uint32_t nm = i < end ? ld_nt(meta + i) : 0u;
-    for (uint64_t i0 = start; i0 < end; i0 += BLOCK) {   // (uniform trip count)
-        const uint32_t k = nk;
-        const uint32_t len = nm >> 16;
-        i += BLOCK;
-        nk = i < end ? ld_nt(idx + i) : NONE;
-        nm = i < end ? ld_nt(meta + i) : 0u;
+    // one header: its LDS entry, or a record of its own (every lane of the
+    // wave calls it)
+    auto one = [&](uint32_t k, uint32_t len) {
         uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
         bool done = k == NONE;
         for (int p = 0; p < CTP_PROBES && !done; p++) {
@@ -1106,6 +1128,39 @@ __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
         const uint32_t r = wave_append(nrec, !done);   // a record of its own
         if (!done)
             put(r, acc_rec(k, 1, len));
+    };
+    // VEC: four consecutive headers per thread and step (16-byte loads),
+    // the loads of the next two steps in flight during this step's LDS work
+    // (one 1024-thread workgroup per CU: with one step of look-ahead the
+    // pass waits on HBM latency every step)
+    constexpr uint32_t W = VEC ? 4 : 1, STEP = W * BLOCK;
+    auto load = [&](uint64_t e, uint4 &kk, uint4 &mm) {
+        if (VEC && e + 4 <= end) {
+            kk = ld_nt4(idx + e);
+            mm = ld_nt4(meta + e);
+        } else {
+            kk = make_uint4(NONE, NONE, NONE, NONE);
+            mm = make_uint4(0, 0, 0, 0);
+            if (e < end) { kk.x = ld_nt(idx + e); mm.x = ld_nt(meta + e); }
+            if (VEC && e + 1 < end) { kk.y = ld_nt(idx + e + 1); mm.y = ld_nt(meta + e + 1); }
+            if (VEC && e + 2 < end) { kk.z = ld_nt(idx + e + 2); mm.z = ld_nt(meta + e + 2); }
+        }
+    };
+    const uint64_t e0 = start + (uint64_t)threadIdx.x * W;
+    uint4 k0, m0, k1, m1;
+    load(e0, k0, m0);
+    load(e0 + STEP, k1, m1);
+    for (uint64_t i0 = start; i0 < end; i0 += STEP) {   // (uniform trip count)
+        uint4 k2, m2;
+        load(e0 + (i0 - start) + 2 * STEP, k2, m2);
+        one(k0.x, m0.x >> 16);
+        if (VEC) {
+            one(k0.y, m0.y >> 16);
+            one(k0.z, m0.z >> 16);
+            one(k0.w, m0.w >> 16);
+        }
+        k0 = k1; m0 = m1;
+        k1 = k2; m1 = m2;
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {   // (uniform)
@@ -1578,7 +1633,8 @@ WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
     off += 8ull * slots * w.nblk;
     const uint32_t nbuck = ctp_buckets(T);
     if (ct && T.ct_acct && nbuck) {
-        const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        const uint64_t per = acc_slice(n);
+        const uint32_t nblk = (uint32_t)((n + per - 1) / per);
         w.ctp_nv = nblk * (egr ? 2u : 1u);
         w.ctp_nbuck = nbuck;
         w.ctp_nco = (nbuck + ACC_FINE - 1) / ACC_FINE;
@@ -1717,14 +1773,24 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
         uint32_t *bsum = reinterpret_cast<uint32_t *>(b + w.ctp_bsum);
         uint32_t *plan = reinterpret_cast<uint32_t *>(b + w.ctp_plan);
         uint32_t *fo = reinterpret_cast<uint32_t *>(b + w.ctp_fo);
-        const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
+        const uint64_t per = acc_slice(n);
+        const uint32_t nblk = (uint32_t)((n + per - 1) / per);
         const uint32_t nch = w.ctp_nv * ACC_SLICE_CHUNKS;
         const uint64_t nc = (uint64_t)w.ctp_nco * nch;
         const uint32_t nsb = (uint32_t)((nc + 4 * BLOCK - 1) / (4 * BLOCK));
-        set_lds_limit((const void *)k_acc_agg, (int)ACC_AGG_LDS);
-        hipLaunchKernelGGL(k_acc_agg, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
-                           dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta, n,
-                           w.ctp_nco, rec, rcnt, cnt);
+        // 16-byte loads when the header meta allows (the key arrays are
+        // 16-byte aligned workspace)
+        const bool vec = ((uintptr_t)meta & 15) == 0;
+        const void *agg = vec ? (const void *)k_acc_agg<true> : (const void *)k_acc_agg<false>;
+        set_lds_limit(agg, (int)ACC_AGG_LDS);
+        if (vec)
+            hipLaunchKernelGGL(k_acc_agg<true>, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
+                               dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta, n,
+                               w.ctp_nco, rec, rcnt, cnt, per);
+        else
+            hipLaunchKernelGGL(k_acc_agg<false>, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
+                               dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta, n,
+                               w.ctp_nco, rec, rcnt, cnt, per);
         hipLaunchKernelGGL(k_scan_local, dim3(nsb), dim3(BLOCK), 0, s, cnt, off, nc, bsum);
         hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(BLOCK), 0, s, bsum, nsb, off + nc);
         hipLaunchKernelGGL(k_scan_add, dim3(nsb), dim3(BLOCK), 0, s, off, nc, bsum);
