@@ -169,7 +169,15 @@ __device__ __forceinline__ uint32_t find4(const CtaArgs &A, uint32_t x, uint32_t
 }
 
 // The slot of a key no other thread of this launch inserts: found, or a
-// free one claimed (CAS on w) and filled.
+// free one claimed (CAS on w: atomics are coherent across the XCDs) and
+// filled.  No agent-scope fence between the key words and w: that is an L2
+// write-back and invalidate per insert (MI355X_MICROARCH.md), and nothing in
+// this launch needs it — the only thread that looks this key up is this one
+// (one thread per home slot), another thread's probe only needs to see the
+// slot taken (w != 0 once the CAS is done), and a reader on another XCD
+// that saw w ahead of the key words would see them as the zeros of the free
+// slot, which no CT key has (saddr and daddr are never both 0 on the path).
+// The launch's end writes the L2s back for the kernels after it.
 __device__ uint32_t find_or_insert4(const CtaArgs &A, uint32_t x, uint32_t y, uint32_t z,
                                     uint32_t w, bool *fresh)
 {
@@ -188,9 +196,8 @@ __device__ uint32_t find_or_insert4(const CtaArgs &A, uint32_t x, uint32_t y, ui
         A.ct4[i].x = x;
         A.ct4[i].y = y;
         A.ct4[i].z = z;
-        __threadfence();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (store order)
         __hip_atomic_store(pw, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicAdd(&A.cnt[CTA_CLAIMS], 1u);
         return i;
     }
 }
@@ -266,83 +273,98 @@ __device__ __forceinline__ uint4 req_key(const CtaArgs &A, uint32_t order2, bool
 }
 
 // ---- insert: one thread per home slot; keys deduped in registers (a fifth
-// distinct key of one home slot is found by rescanning the run)
-__global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, const uint64_t *req,
-                                                    uint32_t nreq, int round, uint32_t cx_off)
+// distinct key of one home slot is found by rescanning the run).  A key's
+// first create also needs its related ICMP entry (round 0): the request is
+// marked (bit 0 of its word, free in a request) and k_cta_related writes
+// the entries — no per-request atomic on a shared counter here.
+__global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, uint32_t nreq,
+                                                    int round, uint32_t cx_off)
 {
     const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
-    if (r0 >= nreq)
-        return;
-    const uint64_t home = req[r0] >> A.ob;
-    if (r0 > 0 && (req[r0 - 1] >> A.ob) == home)
-        return;
+    const uint64_t home = r0 < nreq ? req[r0] >> A.ob : 0;
+    const bool lead = r0 < nreq && (r0 == 0 || (req[r0 - 1] >> A.ob) != home);
     const uint64_t omask = (1ull << A.ob) - 1;
-    uint4 kk[4];
-    uint32_t ks[4];
-    int nk = 0;
-    for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
-        const uint32_t order2 = (uint32_t)(req[r] & omask);
-        Op o;
-        const uint4 k = req_key(A, order2, round == 1, &o);
-        uint32_t slot = NONE;
-        for (int j = 0; j < nk; j++)
-            if (kk[j].x == k.x && kk[j].y == k.y && kk[j].z == k.z && kk[j].w == k.w)
-                slot = ks[j];
-        bool first = false;
-        if (slot == NONE) {
-            // not among the first four keys: an earlier request of the run
-            // may still have it
-            for (uint32_t q = r0; q < r && nk == 4; q++) {
-                Op oq;
-                const uint4 kq = req_key(A, (uint32_t)(req[q] & omask), round == 1, &oq);
-                if (kq.x == k.x && kq.y == k.y && kq.z == k.z && kq.w == k.w) {
-                    slot = find4(A, k.x, k.y, k.z, k.w);
-                    break;
+    uint32_t claims = 0;
+    if (lead) {
+        uint4 kk[4];
+        uint32_t ks[4];
+        int nk = 0;
+        for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
+            const uint32_t order2 = (uint32_t)(req[r] & omask) & ~1u;
+            Op o;
+            const uint4 k = req_key(A, order2, round == 1, &o);
+            uint32_t slot = NONE;
+            for (int j = 0; j < nk; j++)
+                if (kk[j].x == k.x && kk[j].y == k.y && kk[j].z == k.z && kk[j].w == k.w)
+                    slot = ks[j];
+            bool first = false;
+            if (slot == NONE) {
+                // not among the first four keys: an earlier request of the
+                // run may still have it
+                for (uint32_t q = r0; q < r && nk == 4; q++) {
+                    Op oq;
+                    const uint4 kq = req_key(A, (uint32_t)(req[q] & omask), round == 1, &oq);
+                    if (kq.x == k.x && kq.y == k.y && kq.z == k.z && kq.w == k.w) {
+                        slot = find4(A, k.x, k.y, k.z, k.w);
+                        break;
+                    }
                 }
             }
-        }
-        if (slot == NONE) {
-            bool fresh;
-            slot = find_or_insert4(A, k.x, k.y, k.z, k.w, &fresh);
-            mark_or(&A.mark[slot], MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
-            first = fresh;
-            if (nk < 4) {
-                kk[nk] = k;
-                ks[nk++] = slot;
-            }
-        }
-        // every create and related-entry write is an ordered op: request r
-        // of the round has its own place in the list
-        const uint32_t c = cx_off + r;
-        if (c < A.cx_cap)
-            A.cx[c] = pack(A, slot, order2 | (uint32_t)round);
-        // the key's first create writes its related ICMP entry next: into
-        // the device table for an ANY map (UDP, ICMP echo), into the host
-        // log for a TCP map (no lookup reaches it there)
-        if (round == 0 && first && !o.ki_form) {
-            if (o.is_tcp) {
-                const uint32_t l = atomicAdd(&A.cnt[CTA_NLOG], 1u);
-                if (l < A.log_cap) {
-                    CtLog &g = A.log[A.log_base + l];
-                    g.x = o.x2;
-                    g.y = o.y2;
-                    g.w = ct_word(1u, ((o.w2 >> 8) & 7) | 2u, o.owner);
-                    g.now = A.now;
-                    g.dirlen = o.dir << 31 | o.len;
-                    g.sec = o.sec;
-                    g.seq = A.seq;
-                    g.order = order2;
-                }
-            } else {
-                const uint32_t b = atomicAdd(&A.cnt[CTA_NREQB], 1u);
-                if (b < A.req_cap) {
-                    const uint32_t h =
-                        ct_hash4(o.x2, o.y2, 0u, ct_word(1u, ((o.w2 >> 8) & 7) | 2u, o.owner)) &
-                        A.T.ct4_mask;
-                    A.reqB[b] = pack(A, h, order2);
+            if (slot == NONE) {
+                bool fresh;
+                slot = find_or_insert4(A, k.x, k.y, k.z, k.w, &fresh);
+                mark_or(&A.mark[slot], MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
+                first = fresh;
+                claims += fresh;
+                if (nk < 4) {
+                    kk[nk] = k;
+                    ks[nk++] = slot;
                 }
             }
+            // every create and related-entry write is an ordered op: request
+            // r of the round has its own place in the list
+            const uint32_t c = cx_off + r;
+            if (c < A.cx_cap)
+                A.cx[c] = pack(A, slot, order2 | (uint32_t)round);
+            if (round == 0 && first && !o.ki_form)
+                req[r] |= 1ull;
         }
+    }
+    wave_add(&A.cnt[CTA_CLAIMS], claims);
+}
+
+// ---- related: one thread per (sorted) round-0 request; a marked one is a
+// key's first create, whose related ICMP entry goes into the device table
+// for an ANY map (UDP, ICMP echo: a round-1 request) or into the host log
+// for a TCP map (no lookup reaches it there)
+__global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *req,
+                                                     uint32_t nreq)
+{
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    const uint64_t v = r < nreq ? req[r] : 0ull;
+    const uint32_t order2 = (uint32_t)(v & ((1ull << A.ob) - 1)) & ~1u;
+    Op o;
+    o.is_tcp = false;
+    if (v & 1)
+        o = decode(A, order2 >> 2, (order2 >> 1) & 1);
+    const bool lg = (v & 1) && o.is_tcp, rb = (v & 1) && !o.is_tcp;
+    const uint32_t l = block_count(&A.cnt[CTA_NLOG], lg);
+    const uint32_t b = block_count(&A.cnt[CTA_NREQB], rb);
+    const uint32_t fl = ((o.w2 >> 8) & 7) | 2u;
+    if (lg && l < A.log_cap) {
+        CtLog &g = A.log[A.log_base + l];
+        g.x = o.x2;
+        g.y = o.y2;
+        g.w = ct_word(1u, fl, o.owner);
+        g.now = A.now;
+        g.dirlen = o.dir << 31 | o.len;
+        g.sec = o.sec;
+        g.seq = A.seq;
+        g.order = order2;
+    }
+    if (rb && b < A.req_cap) {
+        const uint32_t h = ct_hash4(o.x2, o.y2, 0u, ct_word(1u, fl, o.owner)) & A.T.ct4_mask;
+        A.reqB[b] = pack(A, h, order2);
     }
 }
 
@@ -712,9 +734,12 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
     int rc;
     if ((rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
         return rc;
-    if (nreqA)
-        hipLaunchKernelGGL(k_cta_insert, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
-                           (const uint64_t *)sorted, nreqA, 0, 0u);
+    if (nreqA) {
+        hipLaunchKernelGGL(k_cta_insert, dim3((nreqA + 255) / 256), dim3(256), 0, s, A, sorted,
+                           nreqA, 0, 0u);
+        hipLaunchKernelGGL(k_cta_related, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
+                           (const uint64_t *)sorted, nreqA);
+    }
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -724,8 +749,8 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
     if ((rc = sort_keys(A, A.reqB, A.reqB2, nreqB, bits, s, &sorted)))
         return rc;
     if (nreqB)
-        hipLaunchKernelGGL(k_cta_insert, dim3((nreqB + 255) / 256), dim3(256), 0, s, A,
-                           (const uint64_t *)sorted, nreqB, 1, nreqA);
+        hipLaunchKernelGGL(k_cta_insert, dim3((nreqB + 255) / 256), dim3(256), 0, s, A, sorted,
+                           nreqB, 1, nreqA);
     // the creates' ops take the list's first nreqA + nreqB places, route's
     // ordered hits follow
     CtaArgs R = A;
