@@ -184,6 +184,21 @@ struct cfc_ctx {
     uint64_t cta_claims = 0;     // device inserts since the last sync
     uint32_t cta_seq = 0;
     uint32_t n_apply_dev = 0, n_apply_host = 0;
+    // the CT table's version: bumped by every commit that changes tables
+    // and every CT apply
+    uint64_t ct_gen = 0;
+    // the last IPv4 classify launch: its CT hit slots (the accounting keys,
+    // slot * 2 + dir per stage) stay in the workspace until the next launch,
+    // and the device apply of that same batch reads them instead of probing
+    // the table again (valid while ct_gen is unchanged)
+    struct {
+        bool valid = false;
+        const void *ct = nullptr, *saddr = nullptr;
+        uint64_t n = 0, gen = 0;
+        int mode = 0;
+        uint16_t ep = 0;
+        size_t k1 = 0, k2 = 0;   // byte offsets in ws; k2 = 0: no stage 2
+    } last_cls;
     uint64_t log_used = 0;       // CtLog entries since the last sync
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
 
@@ -309,6 +324,8 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
 {
     if (!c->ct_dirty || !c->epoch)
         return 0;
+    // (no ct_gen bump: live entries keep their slots; the deleted ones it
+    // turns into tombstones were deleted by an apply, which bumped it)
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
     const uint64_t slots = G.ct4_host.size();
@@ -1089,6 +1106,7 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
                     kv.second->ct());
     if (!groups && !touched)
         return 0;
+    c->ct_gen++;
     int rc;
     // host-side CT changes or a CT rebuild: take the device's first
     if ((groups & GROUP_CT) || touched)
@@ -1619,8 +1637,10 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
     }
-    size_t need = ws_layout(in->n, E.T, mode,
-                            E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4).total;
+    const WsLayout wl = ws_layout(in->n, E.T, mode,
+                                  E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4);
+    const size_t need = wl.total;
+    c->last_cls.valid = false;
     if (need > c->ws_bytes) {
         if (c->ws) {
             (void)hipDeviceSynchronize();
@@ -1643,6 +1663,18 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     c->last_stream = s;
     note_stream(c, s);
     c->ctr_pending = true;
+    if (std::is_same<Hdr, cfc_hdr_v4>::value && out->ct && in->n && wl.ct) {
+        auto &L = c->last_cls;
+        L.valid = true;
+        L.ct = out->ct;
+        L.saddr = in->saddr;
+        L.n = in->n;
+        L.gen = c->ct_gen;
+        L.mode = mode;
+        L.ep = ep_lxc;
+        L.k1 = wl.ct;
+        L.k2 = mode == CFC_MODE_EGRESS ? wl.ct2 : 0;
+    }
     return 0;
 }
 
@@ -2306,6 +2338,14 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     A.cnt = (uint32_t *)c->cta_cnt.p;
     A.ob = ob;
     A.slot_bits = sb;
+    {   // this batch's hit slots from its classify launch, if still there
+        const auto &L = c->last_cls;
+        if (L.valid && L.gen == c->ct_gen && L.ct == out->ct && L.saddr == in->saddr &&
+            L.n == n && L.mode == mode && L.ep == ep_lxc) {
+            A.ck1 = (const uint32_t *)((const char *)c->ws + L.k1);
+            A.ck2 = L.k2 ? (const uint32_t *)((const char *)c->ws + L.k2) : nullptr;
+        }
+    }
     uint32_t hc[CTA_NCNT];
     if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess || cta_scan(A, s) ||
         hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -2392,6 +2432,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     hipStream_t s = (hipStream_t)stream;
     if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value) {
         const int rc = ct_apply_dev(c, in, out, mode, ep_lxc, s);
+        c->ct_gen++;   // (the table, or the host maps, change from here)
         c->n_apply_dev += rc == 0;
         if (rc <= 0)
             return rc;

@@ -135,6 +135,10 @@ struct CtaArgs {
     const uint8_t *ctb;
     const int32_t *ver;
     const uint32_t *ident;
+    // the classify launch's CT accounting keys (slot * 2 + dir) of stage 0
+    // and 1, when they are still in its workspace: the scan's hit slots
+    // without a second probe (null: probe)
+    const uint32_t *ck1, *ck2;
     uint64_t n;
     int mode;
     uint32_t ep_owner, ep_sec, now, seq;

@@ -222,8 +222,15 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 o = decode(A, i, st);
             uint32_t slot = HS_NONE;
             if (o.kind == OP_HIT || o.kind == OP_DELETE) {
-                const bool rev = (A.ctb[i] >> (4 * st) & CFC_CT_RES_MASK) >= 2;
-                slot = rev ? find4(A, o.x1, o.y1, o.z1, o.w1) : find4(A, o.x2, o.y2, o.z2, o.w2);
+                const uint32_t *ck = st ? A.ck2 : A.ck1;
+                const uint32_t key = ck ? ck[i] : NONE;
+                if (key != NONE) {   // the slot the classify launch hit
+                    slot = key >> 1;
+                } else {
+                    const bool rev = (A.ctb[i] >> (4 * st) & CFC_CT_RES_MASK) >= 2;
+                    slot = rev ? find4(A, o.x1, o.y1, o.z1, o.w1)
+                               : find4(A, o.x2, o.y2, o.z2, o.w2);
+                }
                 if (slot != NONE) {
                     const uint32_t clo = (ld16(A.tm + slot).z >> 16) & 3;
                     if (o.kind == OP_DELETE) {
