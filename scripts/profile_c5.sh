@@ -11,7 +11,8 @@ mkdir -p "$OUT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run \
     --output-format csv -- python3 bench.py $ARGS > "$OUT/kt.log" 2>&1
 i=0
-for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum" \
+    "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT"; do
     i=$((i+1))
     timeout -s KILL 400 rocprofv3 --pmc $grp -d "$OUT/pmc$i" -o run \
         --output-format csv -- python3 bench.py $ARGS > "$OUT/pmc$i.log" 2>&1
