@@ -82,6 +82,33 @@ __device__ __forceinline__ uint32_t block_count(uint32_t *ctr, bool want)
     __syncthreads();   // wsum and base are reused by the next call
     return r;
 }
+// n items of this thread in a block-wide list: the first one's index, one
+// atomic per block (every thread of the block calls it)
+__device__ __forceinline__ uint32_t block_count_n(uint32_t *ctr, uint32_t v)
+{
+    __shared__ uint32_t wsum[4], base;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        base = t ? atomicAdd(ctr, t) : 0u;
+    }
+    __syncthreads();
+    uint32_t r = base + x - v;
+    for (uint32_t k = 0; k < wv; k++)
+        r += wsum[k];
+    __syncthreads();
+    return r;
+}
 // a per-thread count added once per wave (every lane of the wave calls it)
 __device__ __forceinline__ void wave_add(uint32_t *ctr, uint32_t v)
 {
@@ -116,36 +143,42 @@ __device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint32_t da)
     }
 }
 
-__device__ __forceinline__ Op decode(const CtaArgs &A, uint64_t i, int st)
+// one header's inputs of the apply
+struct ScanIn {
+    uint32_t cb, sa, da, pt, mt, ver, ident, tf, k1, k2;
+};
+
+// stage st of a header, from its inputs; dsto: the owner word of the
+// destination endpoint's CT maps (the stages that are not the sender's)
+__device__ __forceinline__ Op decode_from(const CtaArgs &A, const ScanIn &r, int st,
+                                          uint32_t dsto)
 {
     Op o;
     o.kind = OP_NONE;
-    const uint32_t cb = A.ctb[i];
-    const uint32_t cs = (cb >> (4 * st)) & 0xF;
+    const uint32_t cs = (r.cb >> (4 * st)) & 0xF;
     if (!(cs & CFC_CT_DONE))
         return o;
-    const uint32_t sa = A.sa[i], da = A.da[i], pt = A.pt[i], mt = A.mt[i];
-    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    const int last = (r.cb & (CFC_CT_DONE << 4)) ? 1 : 0;
     const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
     o.dir = eg ? CT_EGRESS : CT_INGRESS;
-    o.owner = eg ? A.ep_owner : dst_owner(A.T, da);
-    o.proto = mt & 0xFF;
+    o.owner = eg ? A.ep_owner : dsto;
+    o.proto = r.mt & 0xFF;
     if (o.proto != 6 && o.proto != 17 && o.proto != 1)
         return o;
-    o.len = mt >> 16;
+    o.len = r.mt >> 16;
     o.is_tcp = o.proto == 6;
-    o.syn = (mt & CFC_HF_TCP_CLOSE) != 0;
-    o.tfl = (o.is_tcp && A.tf) ? A.tf[i] : 0u;
-    o.action = ct_action(false, o.proto, pt, mt);
-    o.sec = A.mode == CFC_MODE_EGRESS ? A.ep_sec : A.ident[i];
-    const CtProbe k = ct_probe<false>(o.proto, pt, (int)o.dir, o.owner);
-    o.x1 = da; o.y1 = sa; o.z1 = k.z1; o.w1 = k.w1;
-    o.x2 = sa; o.y2 = da; o.z2 = k.z2; o.w2 = k.w2;
+    o.syn = (r.mt & CFC_HF_TCP_CLOSE) != 0;
+    o.tfl = o.is_tcp ? r.tf : 0u;
+    o.action = ct_action(false, o.proto, r.pt, r.mt);
+    o.sec = A.mode == CFC_MODE_EGRESS ? A.ep_sec : r.ident;
+    const CtProbe k = ct_probe<false>(o.proto, r.pt, (int)o.dir, o.owner);
+    o.x1 = r.da; o.y1 = r.sa; o.z1 = k.z1; o.w1 = k.w1;
+    o.x2 = r.sa; o.y2 = r.da; o.z2 = k.z2; o.w2 = k.w2;
     // a k2 of ICMP-error form is its own related entry (ct_create4 writes
     // the same key twice)
     o.ki_form = o.proto == 1 && (k.w2 & 0x200u) && k.z2 == 0;
     const uint32_t b = cs & CFC_CT_RES_MASK;
-    const bool dropped = st == last && A.ver[i] == DROP_POLICY;
+    const bool dropped = st == last && (int32_t)r.ver == DROP_POLICY;
     if (b >= 2)
         o.kind = OP_HIT;
     else if (b == 1)
@@ -153,6 +186,26 @@ __device__ __forceinline__ Op decode(const CtaArgs &A, uint64_t i, int st)
     else if (cs & CFC_CT_CREATE)
         o.kind = OP_CREATE;
     return o;
+}
+
+__device__ __forceinline__ Op decode(const CtaArgs &A, uint64_t i, int st)
+{
+    ScanIn r;
+    r.cb = A.ctb[i];
+    if (!((r.cb >> (4 * st)) & CFC_CT_DONE)) {
+        Op o;
+        o.kind = OP_NONE;
+        return o;
+    }
+    r.sa = A.sa[i];
+    r.da = A.da[i];
+    r.pt = A.pt[i];
+    r.mt = A.mt[i];
+    r.ver = (uint32_t)A.ver[i];
+    r.ident = A.ident[i];
+    r.tf = A.tf ? A.tf[i] : 0u;
+    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
+    return decode_from(A, r, st, eg ? 0u : dst_owner(A.T, r.da));
 }
 
 __device__ __forceinline__ uint32_t find4(const CtaArgs &A, uint32_t x, uint32_t y,
@@ -207,58 +260,135 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
     return ((uint64_t)slot << A.ob) | order2;
 }
 
-// ---- scan: ops, hit slots, ordered marks, create requests
+// ---- scan: ops, hit slots, ordered marks, create requests.  Four headers
+// per thread and step, each phase's loads for all four issued before any is
+// waited for: the inputs, the destination endpoints, the hit slots' report
+// state (the pass is a chain of dependent loads per header; one header per
+// thread and step left it waiting on one chain at a time).
+constexpr int SCAN_U = 4;
 __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
     uint32_t nhit = 0;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
-        const uint64_t i = base + threadIdx.x;
-        const bool in = i < A.n;
-        for (int st = 0; st < 2; st++) {
-            Op o;
-            o.kind = OP_NONE;
-            if (in)
-                o = decode(A, i, st);
-            uint32_t slot = HS_NONE;
-            if (o.kind == OP_HIT || o.kind == OP_DELETE) {
-                const uint32_t *ck = st ? A.ck2 : A.ck1;
-                const uint32_t key = ck ? ck[i] : NONE;
-                if (key != NONE) {   // the slot the classify launch hit
-                    slot = key >> 1;
-                } else {
-                    const bool rev = (A.ctb[i] >> (4 * st) & CFC_CT_RES_MASK) >= 2;
-                    slot = rev ? find4(A, o.x1, o.y1, o.z1, o.w1)
-                               : find4(A, o.x2, o.y2, o.z2, o.w2);
-                }
-                if (slot != NONE) {
-                    const uint32_t clo = (ld16(A.tm + slot).z >> 16) & 3;
-                    if (o.kind == OP_DELETE) {
-                        // the entry goes: only its first delete matters
-                        // (k_cta_route), unless a create revives the key
-                        // (a dropped hot flow deletes its entry once per
-                        // packet: only a lower order than the one stored
-                        // needs the atomic)
-                        mark_or(&A.mark[slot], MARK_ORDERED | MARK_DEL);
-                        const uint32_t v = 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1);
-                        if (__hip_atomic_load(&A.sum[slot], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) < v)
-                            atomicMax(&A.sum[slot], v);
-                    } else if (o.action == 2 || clo) {
-                        mark_or(&A.mark[slot], MARK_ORDERED);
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
+        ScanIn r[SCAN_U];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {   // inputs (no branches)
+            const uint64_t i = base + u * 256 + threadIdx.x;
+            const uint64_t j = i < A.n ? i : A.n - 1;
+            r[u].cb = A.ctb[j];
+            r[u].sa = A.sa[j];
+            r[u].da = A.da[j];
+            r[u].pt = A.pt[j];
+            r[u].mt = A.mt[j];
+            r[u].ver = (uint32_t)A.ver[j];
+            r[u].ident = A.ident[j];
+            r[u].tf = A.tf ? A.tf[j] : 0u;
+            r[u].k1 = A.ck1 ? A.ck1[j] : NONE;
+            r[u].k2 = A.ck2 ? A.ck2[j] : NONE;
+            if (i >= A.n)
+                r[u].cb = 0;
+        }
+        // the destination endpoint's CT owner: first probes together
+        uint32_t dsto[SCAN_U], ls[SCAN_U];
+        uint4 lv[SCAN_U];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {
+            ls[u] = A.T.lxc4 ? hash32(r[u].da, A.T.lxc4_mask) : 0u;
+            lv[u] = A.T.lxc4 ? ld16(A.T.lxc4 + ls[u]) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {
+            dsto[u] = 0;
+            if (A.T.lxc4) {
+                uint32_t sl = ls[u];
+                uint4 v = lv[u];
+                for (;;) {
+                    if (!(v.w & LXC_VALID))
+                        break;
+                    if (v.x == r[u].da) {
+                        dsto[u] = ct_owner_word(v.w & 0xFFFF, (v.w & LXC_CT_LOCAL) != 0);
+                        break;
                     }
-                } else {
-                    slot = HS_NONE;
+                    sl = (sl + 1) & A.T.lxc4_mask;
+                    v = ld16(A.T.lxc4 + sl);
                 }
             }
-            if (in)
-                A.hs[2 * i + st] = slot;
-            nhit += slot != HS_NONE;
-            const bool req = o.kind == OP_CREATE;
-            const uint32_t r = block_count(&A.cnt[CTA_NREQA], req);
-            if (req && r < A.req_cap) {
-                const uint32_t home = ct_hash4(o.x2, o.y2, o.z2, o.w2) & A.T.ct4_mask;
-                A.reqA[r] = pack(A, home, (uint32_t)((2 * i + st) << 1));
+        }
+        // per stage: the op, its slot, a create's request
+        uint32_t slot[SCAN_U][2], kind[SCAN_U][2], act[SCAN_U][2], home[SCAN_U][2];
+        uint32_t ncr = 0;
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                const Op o = decode_from(A, r[u], st, dsto[u]);
+                kind[u][st] = o.kind;
+                act[u][st] = o.kind == OP_NONE ? 0u : o.action;
+                slot[u][st] = HS_NONE;
+                home[u][st] = 0;
+                if (o.kind == OP_HIT || o.kind == OP_DELETE) {
+                    const uint32_t key = st ? r[u].k2 : r[u].k1;
+                    uint32_t sl;
+                    if (key != NONE) {   // the slot the classify launch hit
+                        sl = key >> 1;
+                    } else {
+                        const bool rev = ((r[u].cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
+                        sl = rev ? find4(A, o.x1, o.y1, o.z1, o.w1)
+                                 : find4(A, o.x2, o.y2, o.z2, o.w2);
+                    }
+                    slot[u][st] = sl == NONE ? HS_NONE : sl;
+                } else if (o.kind == OP_CREATE) {
+                    home[u][st] = ct_hash4(o.x2, o.y2, o.z2, o.w2) & A.T.ct4_mask;
+                    ncr++;
+                }
+            }
+        }
+        // the hit slots' closing bits, loads together
+        uint32_t clo[SCAN_U][2];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++)
+#pragma unroll
+            for (int st = 0; st < 2; st++)
+                clo[u][st] = slot[u][st] != HS_NONE ? A.tm[slot[u][st]].flags : 0u;
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {
+            const uint64_t i = base + u * 256 + threadIdx.x;
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                const uint32_t sl = slot[u][st];
+                if (sl == HS_NONE)
+                    continue;
+                nhit++;
+                if (kind[u][st] == OP_DELETE) {
+                    // the entry goes: only its first delete matters
+                    // (k_cta_route), unless a create revives the key (a
+                    // dropped hot flow deletes its entry once per packet:
+                    // only a lower order than the one stored needs the
+                    // atomic)
+                    mark_or(&A.mark[sl], MARK_ORDERED | MARK_DEL);
+                    const uint32_t v = 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1);
+                    if (__hip_atomic_load(&A.sum[sl], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) < v)
+                        atomicMax(&A.sum[sl], v);
+                } else if (act[u][st] == 2 || ((clo[u][st] >> 16) & 3)) {
+                    mark_or(&A.mark[sl], MARK_ORDERED);
+                }
+            }
+            if (i < A.n)
+                *reinterpret_cast<uint2 *>(A.hs + 2 * i) = make_uint2(slot[u][0], slot[u][1]);
+        }
+        uint32_t rq = block_count_n(&A.cnt[CTA_NREQA], ncr);
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {
+            const uint64_t i = base + u * 256 + threadIdx.x;
+#pragma unroll
+            for (int st = 0; st < 2; st++) {
+                if (kind[u][st] != OP_CREATE)
+                    continue;
+                if (rq < A.req_cap)
+                    A.reqA[rq] = pack(A, home[u][st], (uint32_t)((2 * i + st) << 1));
+                rq++;
             }
         }
     }
@@ -375,38 +505,64 @@ __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *
     }
 }
 
-// ---- route: hits on unordered slots -> summary; the rest -> ordered list
+// ---- route: hits on unordered slots -> summary; the rest -> ordered list.
+// Four header stages per thread and step, the loads of each phase together
+// (as the scan).
 __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < 2 * A.n; base += stride) {
-        const uint64_t j = base + threadIdx.x;
-        const uint32_t slot = j < 2 * A.n ? A.hs[j] : HS_NONE;
-        bool ordered = false;
-        if (slot != HS_NONE) {
-            const uint32_t mk = A.mark[slot];
-            if ((mk & (MARK_DEL | MARK_PUTC)) == MARK_DEL) {
+    constexpr int RU = 4;
+    const uint64_t n2 = 2 * A.n;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * RU;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < n2; base += stride) {
+        uint32_t slot[RU], mk[RU], sm[RU], mt[RU], tf[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const uint64_t j = base + u * 256 + threadIdx.x;
+            slot[u] = j < n2 ? A.hs[j] : HS_NONE;
+            const uint64_t i = (j < n2 ? j : n2 - 1) >> 1;
+            mt[u] = A.mt[i];
+            tf[u] = A.tf ? A.tf[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            mk[u] = slot[u] != HS_NONE ? A.mark[slot[u]] : 0u;
+            sm[u] = slot[u] != HS_NONE ? A.sum[slot[u]] : 0u;
+        }
+        bool ordered[RU];
+        uint32_t nord = 0;
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const uint64_t j = base + u * 256 + threadIdx.x;
+            ordered[u] = false;
+            if (slot[u] == HS_NONE)
+                continue;
+            if ((mk[u] & (MARK_DEL | MARK_PUTC)) == MARK_DEL) {
                 // a deleted entry: its first delete stands for all its ops
-                ordered = (uint32_t)(j << 1) == 0xFFFFFFFFu - A.sum[slot];
-            } else if (mk & MARK_ORDERED) {
-                ordered = true;
+                ordered[u] = (uint32_t)(j << 1) == 0xFFFFFFFFu - sm[u];
+            } else if (mk[u] & MARK_ORDERED) {
+                ordered[u] = true;
             } else {
                 // the summary needs direction, TCP flags and the close bit only
-                const uint64_t i = j >> 1;
-                const uint32_t mt = A.mt[i];
                 const bool in = !(A.mode == CFC_MODE_EGRESS && (j & 1) == 0);
-                const bool tcp = (mt & 0xFF) == 6;
-                const uint32_t tfl = (tcp && A.tf) ? A.tf[i] : 0u;
+                const bool tcp = (mt[u] & 0xFF) == 6;
+                const uint32_t tfl = tcp ? tf[u] : 0u;
                 const uint32_t bits = (in ? tfl : tfl << 8) | (in ? 1u << 16 : 1u << 17) |
-                                      ((tcp && !(mt & CFC_HF_TCP_CLOSE)) ? 1u << 18 : 0u);
-                const uint32_t old = A.sum[slot];
-                if ((old | bits) != old)
-                    atomicOr(&A.sum[slot], bits);
+                                      ((tcp && !(mt[u] & CFC_HF_TCP_CLOSE)) ? 1u << 18 : 0u);
+                if ((sm[u] | bits) != sm[u])
+                    atomicOr(&A.sum[slot[u]], bits);
             }
+            nord += ordered[u];
         }
-        const uint32_t c = A.cx_base + block_count(&A.cnt[CTA_NCX], ordered);
-        if (ordered && c < A.cx_cap)
-            A.cx[c] = pack(A, slot, (uint32_t)(j << 1));
+        uint32_t c = A.cx_base + block_count_n(&A.cnt[CTA_NCX], nord);
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const uint64_t j = base + u * 256 + threadIdx.x;
+            if (!ordered[u])
+                continue;
+            if (c < A.cx_cap)
+                A.cx[c] = pack(A, slot[u], (uint32_t)(j << 1));
+            c++;
+        }
     }
 }
 
