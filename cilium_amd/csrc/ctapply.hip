@@ -772,33 +772,55 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
 // later ones keep it).
 __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 {
+    // four slots per thread and step, each phase's loads together
+    constexpr int FU = 4;
     const uint64_t slots = (uint64_t)A.T.ct4_mask + 1;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += stride) {
-        const uint32_t m = A.sum[s];
-        if (!m)
-            continue;
-        A.sum[s] = 0;
-        St e = load_state(A.tm, (uint32_t)s);
-        const bool is_tcp = (A.ct4[s].w & 0xFF) == 6;
-        if (is_tcp && (m & (1u << 18)))
-            e.bits |= SEEN_NON_SYN;
-        e.lifetime = A.now + (is_tcp ? ((e.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT)
-                                     : CT_LIFETIME_NONTCP);
-        if (m & (1u << 16)) {
-            const uint32_t seen = (e.seen_rx | (m & 0xFF)) & 0xFF;
-            if (e.last_rx + CT_REPORT_INTERVAL < A.now || seen != e.seen_rx)
-                e.last_rx = A.now;
-            e.seen_rx = seen;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * FU;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * FU; base < slots; base += stride) {
+        uint32_t m[FU], w[FU];
+        St e[FU];
+#pragma unroll
+        for (int u = 0; u < FU; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            m[u] = s < slots ? A.sum[s] : 0u;
         }
-        if (m & (1u << 17)) {
-            const uint32_t seen = (e.seen_tx | ((m >> 8) & 0xFF)) & 0xFF;
-            if (e.last_tx + CT_REPORT_INTERVAL < A.now || seen != e.seen_tx)
-                e.last_tx = A.now;
-            e.seen_tx = seen;
+#pragma unroll
+        for (int u = 0; u < FU; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            w[u] = 0;
+            if (m[u]) {
+                e[u] = load_state(A.tm, (uint32_t)s);
+                w[u] = A.ct4[s].w;
+            }
         }
-        store_state(A.tm, (uint32_t)s, e);
-        A.info[s].y |= CTI_UPDATED;
+#pragma unroll
+        for (int u = 0; u < FU; u++) {
+            if (!m[u])
+                continue;
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            A.sum[s] = 0;
+            St &x = e[u];
+            const bool is_tcp = (w[u] & 0xFF) == 6;
+            if (is_tcp && (m[u] & (1u << 18)))
+                x.bits |= SEEN_NON_SYN;
+            x.lifetime = A.now + (is_tcp ? ((x.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP
+                                                                    : CT_SYN_TIMEOUT)
+                                         : CT_LIFETIME_NONTCP);
+            if (m[u] & (1u << 16)) {
+                const uint32_t seen = (x.seen_rx | (m[u] & 0xFF)) & 0xFF;
+                if (x.last_rx + CT_REPORT_INTERVAL < A.now || seen != x.seen_rx)
+                    x.last_rx = A.now;
+                x.seen_rx = seen;
+            }
+            if (m[u] & (1u << 17)) {
+                const uint32_t seen = (x.seen_tx | ((m[u] >> 8) & 0xFF)) & 0xFF;
+                if (x.last_tx + CT_REPORT_INTERVAL < A.now || seen != x.seen_tx)
+                    x.last_tx = A.now;
+                x.seen_tx = seen;
+            }
+            store_state(A.tm, (uint32_t)s, x);
+            A.info[s].y |= CTI_UPDATED;
+        }
     }
 }
 
@@ -808,27 +830,49 @@ __global__ __launch_bounds__(256) void k_cta_collect(const Ct4Slot *ct4, CtTimer
                                                      CtSyncRec *out, uint32_t cap,
                                                      uint32_t *cnt)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < slots; base += stride) {
-        const uint64_t s = base + threadIdx.x;
-        const bool dirty = s < slots && (info[s].y >> 16) != 0;
-        const uint32_t r = block_count(cnt, dirty);
-        if (!dirty || r >= cap)
-            continue;
-        CtSyncRec &o = out[r];
-        const uint4 k = ld16(ct4 + s);
-        const uint4 t = ld16(tm + s);
-        o.slot = (uint32_t)s;
-        o.info = info[s];
-        o.x = k.x;
-        o.y = k.y;
-        o.z = k.z;
-        o.w = k.w;
-        o.last_rx = t.x;
-        o.last_tx = t.y;
-        o.flags = t.z;
-        o.lifetime = t.w;
-        info[s].y &= 0xFFFFu;
+    // four slots per thread and step, each phase's loads together
+    constexpr int CU = 4;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * CU;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * CU; base < slots; base += stride) {
+        CtInfo in[CU];
+        uint32_t nd = 0;
+#pragma unroll
+        for (int u = 0; u < CU; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            in[u] = s < slots ? info[s] : CtInfo{0, 0};
+            nd += (in[u].y >> 16) != 0;
+        }
+        uint4 k[CU], t[CU];
+#pragma unroll
+        for (int u = 0; u < CU; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            if ((in[u].y >> 16) != 0) {
+                k[u] = ld16(ct4 + s);
+                t[u] = ld16(tm + s);
+            }
+        }
+        uint32_t r = block_count_n(cnt, nd);
+#pragma unroll
+        for (int u = 0; u < CU; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            if ((in[u].y >> 16) == 0)
+                continue;
+            if (r < cap) {
+                CtSyncRec &o = out[r];
+                o.slot = (uint32_t)s;
+                o.info = in[u];
+                o.x = k[u].x;
+                o.y = k[u].y;
+                o.z = k[u].z;
+                o.w = k[u].w;
+                o.last_rx = t[u].x;
+                o.last_tx = t[u].y;
+                o.flags = t[u].z;
+                o.lifetime = t[u].w;
+                info[s].y = in[u].y & 0xFFFFu;
+            }
+            r++;
+        }
     }
 }
 // after the host has taken them: deleted slots become plain tombstones
