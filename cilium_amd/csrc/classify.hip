@@ -1029,6 +1029,7 @@ constexpr uint32_t ACC_PER_THREAD = ACC_CHUNK / BLOCK;                // 16
 constexpr uint32_t ACC_SLICE_CHUNKS = 5;
 constexpr uint32_t ACC_RCAP = ACC_SLICE_CHUNKS * ACC_CHUNK;
 static_assert(COUNT_PER_BLOCK + 2 * CT_LDS_SLOTS <= ACC_RCAP, "slice records");
+static_assert(CTP_BUCKET % BLOCK == 0, "reduce flush");
 constexpr int ACC_COARSE_SHIFT = 38 + CTP_BUCKET_BITS + ACC_FINE_BITS;   // 57
 constexpr int ACC_BUCKET_SHIFT = 38 + CTP_BUCKET_BITS;                   // 50
 constexpr uint32_t ACC_AGG_LDS =
@@ -1388,13 +1389,28 @@ __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, cons
         }
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
-        const uint32_t p = pk[j];
-        if (!p)
-            continue;
+    // the bucket's counters: every touched key's {packets, bytes} loaded
+    // before any is written back (in a loop of read-modify-writes the loads
+    // of the next key wait behind the store of this one)
+    constexpr uint32_t FJ = CTP_BUCKET / BLOCK;
+    uint32_t p[FJ];
+    ulonglong2 cv[FJ];
+#pragma unroll
+    for (uint32_t q = 0; q < FJ; q++) {
+        const uint32_t j = threadIdx.x + q * BLOCK;
+        p[q] = pk[j];
         const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
-        acct[2 * k] += p;
-        acct[2 * k + 1] += by[j];
+        cv[q] = p[q] ? *reinterpret_cast<const ulonglong2 *>(acct + 2 * k) : ulonglong2{0, 0};
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < FJ; q++) {
+        if (!p[q])
+            continue;
+        const uint32_t j = threadIdx.x + q * BLOCK;
+        const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
+        cv[q].x += p[q];
+        cv[q].y += by[j];
+        *reinterpret_cast<ulonglong2 *>(acct + 2 * k) = cv[q];
     }
 }
 
