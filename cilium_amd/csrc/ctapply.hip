@@ -697,9 +697,28 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.tm, slot);
     uint64_t acct[4] = {0, 0, 0, 0};   // [tx pk, tx by, rx pk, rx by] added / set
     uint32_t sec = 0;
+    // the next op's header is loaded (branch-free) while this one is
+    // replayed; the owner word does not matter here (the slot is the key),
+    // so no endpoint lookup
+    auto load_in = [&](uint32_t r, ScanIn &in) {
+        const uint64_t i = (cx[r] & omask) >> 2;
+        in.cb = A.ctb[i];
+        in.sa = A.sa[i];
+        in.da = A.da[i];
+        in.pt = A.pt[i];
+        in.mt = A.mt[i];
+        in.ver = (uint32_t)A.ver[i];
+        in.ident = A.ident[i];
+        in.tf = A.tf ? A.tf[i] : 0u;
+    };
+    ScanIn cur;
+    load_in(r0, cur);
     for (uint32_t r = r0; r < ncx && (uint32_t)(cx[r] >> A.ob) == slot; r++) {
         const uint32_t order2 = (uint32_t)(cx[r] & omask);
-        const Op o = decode(A, order2 >> 2, (order2 >> 1) & 1);
+        ScanIn nxt;
+        load_in(r + 1 < ncx ? r + 1 : r, nxt);
+        const Op o = decode_from(A, cur, (order2 >> 1) & 1, 0u);
+        cur = nxt;
         const uint32_t d = o.dir == CT_INGRESS ? 2 : 0;
         if (order2 & 1) {   // ct_create4's related-entry write: overwrite
             e = fresh(A.now, o.is_tcp, o.dir);
