@@ -28,7 +28,7 @@ LAYOUTS = {"dir24_8": L.LPM4_DIR24_8, "trie": L.LPM4_TRIE}
 
 
 def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO,
-            ct_apply=L.CT_APPLY_DEVICE):
+            ct_apply=L.CT_APPLY_DEVICE, interpose=False):
     dp = Datapath(0)
     dp.set_option(L.OPT_LPM4, lpm4)
     dp.set_option(L.OPT_CT_APPLY, ct_apply)
@@ -47,6 +47,14 @@ def run_gpu(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO,
         sub = b.slice(a, a + step)
         out = dp.classify(sub, mode, ep_lxc, want_ct=use_ct)
         if use_ct:   # fold this batch's creates/deletes before the next one
+            if interpose:   # another (empty) launch in between: the apply probes
+                import ctypes
+                from cilium_amd.datapath import hdr_struct, out_struct
+                hdr = hdr_struct(sub)
+                hdr.n = 0
+                L.check(dp.L.cfc_classify_v4(dp.h, ctypes.byref(hdr),
+                                             ctypes.byref(out_struct(out)), mode,
+                                             ep_lxc, dp._stream(None)), "classify")
             dp.ct_apply(sub, out, mode, ep_lxc)
             ctb[a:a + step] = out.ct.cpu().numpy()
         torch.cuda.synchronize()
@@ -100,9 +108,9 @@ def test_golden(torch, name, layout):
 
 
 def compare_with_oracle(torch, t, h, mode, ep_lxc=0, chunks=1, lpm4=L.LPM4_AUTO,
-                        ct_apply=L.CT_APPLY_DEVICE):
+                        ct_apply=L.CT_APPLY_DEVICE, interpose=False):
     act, ver, ide, counters, metrics = run_gpu(torch, t, h, mode, ep_lxc, chunks,
-                                               lpm4, ct_apply)
+                                               lpm4, ct_apply, interpose)
     o = O.Oracle(t)
     use_ct = getattr(t, "ct", None) is not None
     if use_ct:   # the same batches, each folded into CT before the next
@@ -388,6 +396,17 @@ def test_c5_conntrack_vs_oracle(torch, mode, apply):
     assert (st["ct_apply_device"], st["ct_apply_host"]) == ((3, 0) if apply == "device"
                                                              else (0, 3))
     assert (ver == 0).sum() > len(h) // 3
+
+
+def test_c5_conntrack_apply_after_other_launch(torch):
+    """The device apply of a batch whose classify launch is no longer the
+    last one (an empty launch in between): it cannot take the launch's hit
+    slots from the workspace and probes the table itself — same CT entries,
+    accounting included, as the oracle."""
+    t, flows = S.config_c5(5, n_flows=300_000, n_prefixes=100_000)
+    h = S.headers_c5(t, flows, 1_200_000, seed=37)
+    compare_with_oracle(torch, t, h, 3, chunks=3, interpose=True)
+    assert run_gpu.stats["ct_apply_device"] == 3
 
 
 def test_c5_egress_and_local_ct(torch):
