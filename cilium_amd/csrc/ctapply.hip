@@ -511,15 +511,19 @@ __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *
 __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
     constexpr int RU = 4;
-    const uint64_t n2 = 2 * A.n;
+    // item k is header stage j = k (egress: two CT stages per header) or
+    // j = 2k (one stage: the odd stages never hold a hit)
+    const bool two = A.mode == CFC_MODE_EGRESS;
+    const uint64_t n2 = 2 * A.n, nk = two ? n2 : A.n;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * RU;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < n2; base += stride) {
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < nk; base += stride) {
         uint32_t slot[RU], mk[RU], sm[RU], mt[RU], tf[RU];
 #pragma unroll
         for (int u = 0; u < RU; u++) {
-            const uint64_t j = base + u * 256 + threadIdx.x;
-            slot[u] = j < n2 ? A.hs[j] : HS_NONE;
-            const uint64_t i = (j < n2 ? j : n2 - 1) >> 1;
+            const uint64_t k = base + u * 256 + threadIdx.x;
+            const uint64_t j = two ? k : 2 * k;
+            slot[u] = k < nk ? A.hs[j] : HS_NONE;
+            const uint64_t i = (k < nk ? j : n2 - 1) >> 1;
             mt[u] = A.mt[i];
             tf[u] = A.tf ? A.tf[i] : 0u;
         }
@@ -532,7 +536,8 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
         uint32_t nord = 0;
 #pragma unroll
         for (int u = 0; u < RU; u++) {
-            const uint64_t j = base + u * 256 + threadIdx.x;
+            const uint64_t k = base + u * 256 + threadIdx.x;
+            const uint64_t j = two ? k : 2 * k;
             ordered[u] = false;
             if (slot[u] == HS_NONE)
                 continue;
@@ -556,7 +561,8 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
         uint32_t c = A.cx_base + block_count_n(&A.cnt[CTA_NCX], nord);
 #pragma unroll
         for (int u = 0; u < RU; u++) {
-            const uint64_t j = base + u * 256 + threadIdx.x;
+            const uint64_t k = base + u * 256 + threadIdx.x;
+            const uint64_t j = two ? k : 2 * k;
             if (!ordered[u])
                 continue;
             if (c < A.cx_cap)
