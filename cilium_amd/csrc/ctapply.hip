@@ -265,9 +265,13 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
 // waited for: the inputs, the destination endpoints, the hit slots' report
 // state (the pass is a chain of dependent loads per header; one header per
 // thread and step left it waiting on one chain at a time).
+// TWO: the mode has two CT stages per header (egress); else only stage 0
+// exists and the odd hit-slot entries are never read (k_cta_route).
 constexpr int SCAN_U = 4;
+template <bool TWO>
 __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 {
+    constexpr int NST = TWO ? 2 : 1;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
     uint32_t nhit = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
 #pragma unroll
-            for (int st = 0; st < 2; st++) {
+            for (int st = 0; st < NST; st++) {
                 const Op o = decode_from(A, r[u], st, dsto[u]);
                 kind[u][st] = o.kind;
                 act[u][st] = o.kind == OP_NONE ? 0u : o.action;
@@ -349,13 +353,13 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++)
 #pragma unroll
-            for (int st = 0; st < 2; st++)
+            for (int st = 0; st < NST; st++)
                 clo[u][st] = slot[u][st] != HS_NONE ? A.tm[slot[u][st]].flags : 0u;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
 #pragma unroll
-            for (int st = 0; st < 2; st++) {
+            for (int st = 0; st < NST; st++) {
                 const uint32_t sl = slot[u][st];
                 if (sl == HS_NONE)
                     continue;
@@ -375,15 +379,19 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     mark_or(&A.mark[sl], MARK_ORDERED);
                 }
             }
-            if (i < A.n)
-                *reinterpret_cast<uint2 *>(A.hs + 2 * i) = make_uint2(slot[u][0], slot[u][1]);
+            if (i < A.n) {
+                if (TWO)
+                    *reinterpret_cast<uint2 *>(A.hs + 2 * i) = make_uint2(slot[u][0], slot[u][1]);
+                else
+                    A.hs[2 * i] = slot[u][0];
+            }
         }
         uint32_t rq = block_count_n(&A.cnt[CTA_NREQA], ncr);
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
 #pragma unroll
-            for (int st = 0; st < 2; st++) {
+            for (int st = 0; st < NST; st++) {
                 if (kind[u][st] != OP_CREATE)
                     continue;
                 if (rq < A.req_cap)
@@ -952,7 +960,10 @@ size_t cta_sort_tmp_bytes(uint32_t n)
 
 int cta_scan(const CtaArgs &A, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cta_scan, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+    if (A.mode == CFC_MODE_EGRESS)
+        hipLaunchKernelGGL(k_cta_scan<true>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+    else
+        hipLaunchKernelGGL(k_cta_scan<false>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
