@@ -67,6 +67,24 @@ def pmc_entry(workload, mode, layout, kernels):
     return None
 
 
+def reference_bpf_baseline():
+    """The reference's own BPF datapath timed under BPF_PROG_TEST_RUN in the
+    build container (oracle/time_reference.py; the GPU box has no reference
+    and no BPF objects), newest committed measurement."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "cpu_reference_bpf_*.json")))
+    if not fs:
+        return None
+    r = json.load(open(fs[-1]))
+    return {"value": r["mpps_per_core"], "unit": "Mpps per core",
+            "cores": 1, "kind": "reference",
+            "where": f"build container ({r['cpu']}, kernel {r['kernel']}), not the GPU box",
+            "sample": f"{r['headers']} distinct C2 headers, FULL mode (bpf_xdp -> "
+                      f"bpf_netdev -> bpf_lxc tail calls), in-program time summed, "
+                      f"one header per BPF_PROG_TEST_RUN",
+            "source": os.path.relpath(fs[-1], ROOT)}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -424,6 +442,8 @@ def main():
             "kind": "port",
             "sample": f"first {samp} headers of the same stream through the C "
                       f"restatement (oracle/cfc_oracle.c), {cores} OpenMP threads",
+            # the reference itself, measured where it can run
+            "reference_bpf": reference_bpf_baseline(),
         },
         "parity_sample_ok": parity,
         "monitor_records_per_step_per_gpu": int(nt_cnt.item()) if args.notify else None,

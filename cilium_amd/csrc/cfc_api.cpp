@@ -228,6 +228,17 @@ struct cfc_ctx {
 
 namespace {
 
+// Order work on stream s after the last classify / counter / notify launch
+// when that ran on another stream: folds, CT syncs and applies read the
+// counter block, the CT table and the workspace those launches write.
+void order_after_launches(cfc_ctx *c, hipStream_t s)
+{
+    if (c->ctr_pending && c->last_done && c->last_stream != s)
+        (void)hipStreamWaitEvent(s, c->last_done, 0);
+    if (c->nt_pending && c->nt_done && c->nt_stream != s)
+        (void)hipStreamWaitEvent(s, c->nt_done, 0);
+}
+
 // Signatures of the maps behind each table group, bit g of GROUP_*
 // (0 ipcache v4, 1 prefilter, 2 endpoints + policy, 3 CT, 4 ipcache v6,
 // 5 load balancing).
@@ -324,6 +335,7 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
 {
     if (!c->ct_dirty || !c->epoch)
         return 0;
+    order_after_launches(c, s);
     // (no ct_gen bump: live entries keep their slots; the deleted ones it
     // turns into tombstones were deleted by an apply, which bumped it)
     Epoch &E = *c->epoch;
@@ -480,6 +492,7 @@ int fold_counters(cfc_ctx *c, hipStream_t s)
 {
     if (!c->ctr_pending || !c->epoch)
         return 0;
+    order_after_launches(c, s);
     if (int rc = fold_ct(c, s))
         return rc;
     std::vector<uint64_t> h(c->ctr_u64);
@@ -1760,6 +1773,7 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     (void)hipEventRecord(c->nt_done, s);
     c->nt_stream = s;
     c->nt_pending = true;
+    note_stream(c, s);   // it reads the epoch's endpoint table
     return 0;
 }
 
@@ -2301,6 +2315,9 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     const uint64_t n = in->n, slots = G.ct4_host.size();
     if (!slots || !G.ct4_info.p || n >= (1ull << 29))
         return 1;
+    // the batch's classify (its CT bytes, verdicts and the workspace's hit
+    // slots) may have run on another stream
+    order_after_launches(c, s);
     int ob = 2, sb = 1;
     while ((1ull << ob) < 4 * n)
         ob++;
@@ -2404,10 +2421,22 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     // from here the device table changes: the host mirror lags until ct_sync
     c->ct_dirty = true;
     int rc = cta_rest(A, (uint32_t)nreqA, hc, s);
-    if (rc)
+    if (!rc && hipStreamSynchronize(s) != hipSuccess)
+        rc = -EIO;
+    if (rc) {
+        // the table may hold some of the batch's inserts: no per-slot mark
+        // or summary may leak into the next apply, the claims made count,
+        // and the next commit rebuilds the CT group from the synced maps
+        (void)hipStreamSynchronize(s);
+        (void)hipMemsetAsync(A.mark, 0, 4 * slots, s);
+        (void)hipMemsetAsync(A.sum, 0, 4 * slots, s);
+        uint32_t claims = 0;
+        (void)hipMemcpyAsync(&claims, A.cnt + CTA_CLAIMS, 4, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        c->cta_claims += claims;
+        c->built_sig[3] = ~0ull;
         return rc;
-    if (hipStreamSynchronize(s) != hipSuccess)
-        return -EIO;
+    }
     c->cta_claims += hc[CTA_CLAIMS];
     c->log_used += hc[CTA_NLOG];
     c->cta_seq++;

@@ -390,7 +390,10 @@ typedef struct {
  * records[0 .. min(total, cap)) and, if hdr_index != NULL, the header index
  * of each.  *count (device u64) receives the total; drops past cap are not
  * recorded (a full perf ring loses samples the same way).  mode and ep_lxc
- * as given to the classify call.  Asynchronous on `stream`. */
+ * as given to the classify call.  The records' endpoint fields (SECLABEL,
+ * ifindex) come from the endpoint table committed at the time of this call:
+ * call it before a commit that changes cilium_lxc or an endpoint's config.
+ * Asynchronous on `stream`. */
 int cfc_drop_notify_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
                        int mode, uint16_t ep_lxc, cfc_drop_notify *records,
                        uint64_t *hdr_index, uint64_t cap, uint64_t *count,

@@ -172,6 +172,16 @@ class Loader:
             self._elf_cache[obj] = _Elf(os.path.join(REF_DIR, obj))
         return self._elf_cache[obj]
 
+    def map_from_elf(self, obj, name):
+        """Create (or return) map `name` exactly as obj's maps section
+        defines it (struct bpf_elf_map), without loading any program."""
+        if name not in self.maps:
+            elf = self._elf(obj)
+            val = next(v for n, sh, v in elf.syms if n == name and sh == elf.maps_sec)
+            t, ks, vs, me, fl = elf.mapdef(val)
+            self.maps[name] = Map(name, t, ks, vs, self.max_elem.get(name, me), fl)
+        return self.maps[name]
+
     def load(self, obj, section, prog_type, rename=None):
         rename = rename or {}
         elf = self._elf(obj)

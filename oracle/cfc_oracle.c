@@ -474,6 +474,19 @@ int cfo_ipcache_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
     return 0;
 }
 
+/* ipcache_lookup4/6 (eps.h:56-80) on n addresses */
+void cfo_ipcache_lookup(cfo_t *o, int family, size_t n, const uint8_t *addrs,
+                        uint32_t *label, uint8_t *hit)
+{
+    const lpm *l = family == 1 ? &o->ipc4 : &o->ipc6;
+    const size_t al = family == 1 ? 4 : 16;
+    for (size_t i = 0; i < n; i++) {
+        uint32_t v = 0;
+        hit[i] = (uint8_t)lpm_lookup(l, addrs + al * i, &v);
+        label[i] = hit[i] ? v : 0;
+    }
+}
+
 static void ep_key(uint8_t k[20], int family, const uint8_t *addr)
 {
     memset(k, 0, 20);

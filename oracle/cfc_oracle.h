@@ -33,6 +33,11 @@ void cfo_free(cfo_t *o);
 /* family: 1 = IPv4, 2 = IPv6 (ENDPOINT_KEY_IPV4/6, common.h:139-140) */
 int cfo_ipcache_add(cfo_t *o, int family, int plen, const uint8_t addr[16],
                     uint32_t label);
+/* ipcache_lookup4/6 (eps.h:56-80): the longest prefix holding each of n
+ * addresses (IPv4: 4 bytes each, IPv6: 16) -> label[i], hit[i] = 1 when a
+ * prefix matched; the lookup the identity derivations make */
+void cfo_ipcache_lookup(cfo_t *o, int family, size_t n, const uint8_t *addrs,
+                        uint32_t *label, uint8_t *hit);
 int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
                      uint32_t ifindex, uint16_t lxc_id, uint32_t flags);
 int cfo_seclabel_set(cfo_t *o, uint16_t lxc_id, uint32_t seclabel);

@@ -131,6 +131,8 @@ def lib():
         L.cfo_lb4_revnat_add.argtypes = [vp, ctypes.c_uint16, vp]
         L.cfo_set_lb_io.argtypes = [vp, vp, vp]
         L.cfo_set_lb_io.restype = None
+        L.cfo_ipcache_lookup.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp]
+        L.cfo_ipcache_lookup.restype = None
         _lib = L
     return _lib
 
@@ -371,6 +373,16 @@ class Oracle:
            _p(c(ct, np.uint8)), _p(mon), _p(hz))
         self.L.cfo_set_lb_io(self.h, None, None)
         return hz
+
+    def ipcache_lookup(self, family, addrs):
+        """ipcache_lookup4/6 (eps.h:56-80) of each address -> (label u32,
+        hit u8); family 4: u32 addresses as loaded, 6: (n, 16) bytes."""
+        a = np.ascontiguousarray(addrs, np.uint32 if family == 4 else np.uint8)
+        n = len(a)
+        lab = np.zeros(n, np.uint32)
+        hit = np.zeros(n, np.uint8)
+        self.L.cfo_ipcache_lookup(self.h, 1 if family == 4 else 2, n, _p(a), _p(lab), _p(hit))
+        return lab, hit
 
     def ct_dump(self):
         """(n, CT_ROW) u8 rows: owner u16, map u8, family u8, tuple[40],

@@ -145,6 +145,48 @@ def test_commit_while_another_stream_runs(torch):
     dp.close()
 
 
+def test_endpoint_rebuild_while_another_stream_counts(torch):
+    """A long conntrack batch on stream 1; meanwhile a new policy entry
+    (a structural change: the endpoint group and its counter layout are
+    rebuilt) is committed on stream 2, which must fold stream 1's counts
+    under the old layout first, and a second batch runs on stream 2.  Policy
+    entry counters and metrics equal the oracle's run of the
+    two batches on their own tables (CT accounting is compared after
+    applies, in test_gpu_parity / test_gpu_fullsize)."""
+    t, flows = S.config_c5(5, n_flows=50_000, n_prefixes=20_000, n_policy=2000, now=1000)
+    dp = Datapath(0)
+    pms = load_tables(dp, t)
+    h1 = S.headers_c5(t, flows, 8_000_000, seed=81)
+    h2 = S.headers_c5(t, flows, 300_000, seed=82)
+    b1, b2 = pack(h1), pack(h2)
+    o = O.Oracle(t)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    dp.classify(b1, 3, stream=s1)
+    # an identity no header carries: the verdicts stay, the layout moves
+    new = (70_000, 0, 0, 0, 0)
+    pm = pms[S.EP_LXC_ID]
+    dp.update_element(pm.Fd, policymap.PolicyKey(*new[:4]).pack(),
+                      policymap.PolicyEntry(0).pack())
+    dp.commit(stream=s2)
+    out2 = dp.classify(b2, 3, stream=s2)
+    dp.counters_sync(stream=s2)
+    torch.cuda.synchronize()
+    o.classify(h1, 3, 0, nthreads=16)
+    o.L.cfo_policy_add(o.h, S.EP_LXC_ID, *new)
+    t.policy[S.EP_LXC_ID] = np.concatenate(
+        [t.policy[S.EP_LXC_ID], np.array([new], S.POLICY_DT)])
+    check(out2, O.Oracle(t), h2)
+    o.classify(h2, 3, 0, nthreads=16)
+    want = {tuple(int(x) for x in r[:4]): tuple(r[5:7]) for r in o.policy_counters(S.EP_LXC_ID)}
+    got = {tuple(int(x) for x in r[:4]): tuple(r[5:7])
+           for r in np.array(policy_rows(pm), np.uint64).reshape(-1, 7)}
+    assert got == want
+    m = np.array(metricsmap.dump_rows(dp), np.uint64).reshape(-1, 4)
+    assert sorted(map(tuple, m.tolist())) == sorted(map(tuple, o.metrics().tolist()))
+    dp.close()
+
+
 def test_in_place_patches(torch):
     """Value-only overwrites: IPv6 ipcache labels and policy proxy ports are
     patched into the live tables (the epoch stays); an IPv4 label overwrite
