@@ -464,9 +464,38 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
             clock, pktv, hsh, hsh_ok)
 
 
+def lpm_pin(ipc_map, h: S.Headers, pkt=None):
+    """The kernel's own longest-prefix match (BPF_MAP_LOOKUP_ELEM on the LPM
+    trie cilium_ipcache, kernel/bpf/lpm_trie.c) of every header's addresses,
+    with the key ipcache_lookup4/6 builds (eps.h:49-80: prefixlen 32 static
+    bits + the full address, family byte) -> (labels (n, 4) u32, hits (n, 4)
+    u8) for the columns saddr, daddr, and the packet's saddr / daddr as the
+    program left them (pkt: IPv4 service translation; else saddr / daddr
+    again).  The identity derivations of headers the reference reports
+    nothing for rest on these lookups (bpf_netdev.c:374-398, bpf_lxc.c:516-532)."""
+    n = len(h)
+    fam = 1 if h.family == 4 else 2
+    cols = [h.saddr, h.daddr,
+            h.saddr if pkt is None else pkt[:, 0], h.daddr if pkt is None else pkt[:, 1]]
+    lab = np.zeros((n, 4), np.uint32)
+    hit = np.zeros((n, 4), np.uint8)
+    for c, a in enumerate(cols):
+        for i in range(n):
+            ab = struct.pack("<I", int(a[i])) + bytes(12) if fam == 1 else bytes(a[i])
+            key = struct.pack("<IHBB", 32 + (32 if fam == 1 else 128), 0, 0, fam) + ab
+            v = ipc_map.lookup(key)
+            if v is not None:
+                lab[i, c] = struct.unpack_from("<I", v, 0)[0]
+                hit[i, c] = 1
+    return lab, hit
+
+
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
     action, verdict, ident, idmask, cbs, ev_hdr, ev, clock, pkt, hsh, hsh_ok = res
     extra = {}
+    lab, hit = lpm_pin(dp.L.maps["cilium_ipcache"], h,
+                       pkt if getattr(t, "lb4", None) is not None else None)
+    extra.update(x_lpm=lab, x_lpm_hit=hit)
     if getattr(t, "lb4", None) is not None:
         extra.update(lb4=t.lb4, revnat4=t.revnat4, x_pkt=pkt, x_hash=hsh,
                      x_hash_ok=hsh_ok)

@@ -61,6 +61,88 @@ class Golden:
         self.cb = d["x_cb"] if "x_cb" in d.files else None
         self.counters = {int(k.split("_")[2]): d[k] for k in d.files
                          if k.startswith("x_counters_")}
+        # the kernel's own LPM of each header's addresses in cilium_ipcache
+        # (oracle/pin_lpm.py, gen_golden.lpm_pin): (n, 4) labels and hits for
+        # saddr, daddr, the packet's saddr, daddr (services: translated)
+        self.lpm = d["x_lpm"] if "x_lpm" in d.files else None
+        self.lpm_hit = d["x_lpm_hit"] if "x_lpm_hit" in d.files else None
+        # what the reference reported itself (perf-ring records, drop cb[],
+        # proxy map); identity / idmask below add the identities derived
+        # from the kernel's LPM for every other tc-path header
+        self.identity_reported = self.identity
+        self.idmask_reported = self.idmask
+        if self.lpm is not None:
+            exp, applies = lpm_identity(self)
+            full = np.uint32(0xFFFFFFFF)
+            self.identity = np.where(applies, exp, self.identity).astype(np.uint32)
+            self.idmask = np.where(applies, full, self.idmask).astype(np.uint32)
+            self.lpm_expected, self.lpm_applies = exp, applies
+
+
+# Drops that end a program before its ipcache lookup, so no identity is
+# derived (common.h:239-265): egress DROP_INVALID_SIP (lxc.h:55),
+# DROP_CT_UNKNOWN_PROTO (ct_lookup4/6 runs before the dstID lookup,
+# bpf_lxc.c:497-532), DROP_INVALID_EXTHDR / DROP_FRAG_NOSUPPORT
+# (ipv6_hdrlen), DROP_NO_SERVICE (lb4_local); ingress only the IPv6 header
+# walk of handle_ipv6 (bpf_netdev.c:172-200) — its CT drops come after the
+# source identity
+NO_IDENTITY_EGRESS = (-132, -137, -156, -157, -158)
+NO_IDENTITY_INGRESS = (-156, -157)
+
+
+def no_identity(g):
+    return np.isin(g.verdict, NO_IDENTITY_EGRESS if g.mode == 1 else NO_IDENTITY_INGRESS)
+
+
+def identity_from_mark(mark):
+    """handle_identity_from_host (bpf_netdev.c:128-153) on skb->mark"""
+    m = np.asarray(mark, np.uint64)
+    magic = m & 0x0F00
+    proxy = (magic == 0x0A00) | (magic == 0x0B00)   # MARK_MAGIC_PROXY_{INGRESS,EGRESS}
+    return np.where(proxy, ((m & 0xFF) << 16) | (m >> 16),
+                    np.where(magic == 0x0C00, 1, 2)).astype(np.uint32)   # HOST / WORLD
+
+
+def lpm_identity(g: Golden):
+    """The identity of every tc-path header from the kernel's own LPM
+    results (g.lpm) by the reference's derivation -> (identity u32, applies):
+    ingress (bpf_netdev.c:374-398, v6 :202-213): the mark's identity; if it
+    is reserved (policy.h:41-44, < HEALTH_ID) the LPM label of saddr when
+    != 0, != CLUSTER_ID (v4 also != HOST_ID); egress (bpf_lxc.c:516-532, v6
+    :206-221): the LPM label of the tuple's daddr (the service's backend,
+    or the VIP for a looped-back flow) when != 0, else CLUSTER_ID inside
+    IPV4_CLUSTER_RANGE/MASK (v6: the /64 of ROUTER_IP), else WORLD_ID.
+    applies: tc-path headers (not XDP, not an XDP drop of FULL mode) whose
+    program reached the lookup (no_identity)."""
+    n = len(g.verdict)
+    v4 = g.headers.family == 4
+    tc = np.full(n, g.mode != 2)
+    if g.mode == 3:
+        tc &= ~((g.action == 1) & (g.verdict == -1))   # XDP_DROP
+    applies = tc & ~no_identity(g)
+    lab, hit = g.lpm.astype(np.uint32), g.lpm_hit.astype(bool)
+    if g.mode == 1:
+        col = np.full(n, 1)
+        da = np.asarray(g.headers.daddr)
+        if g.pkt is not None:   # lb4_local: the tuple's daddr is the backend
+            loop = g.pkt[:, 0] == S.IPV4_LOOPBACK
+            col = np.where(loop, 1, 3)
+            da = np.where(loop, np.asarray(g.headers.daddr, np.uint32), g.pkt[:, 1])
+        l, h = lab[np.arange(n), col], hit[np.arange(n), col]
+        if v4:
+            cluster = (np.asarray(da, np.uint32) & 0xFF0000) == 0x100000
+        else:
+            cluster = (np.asarray(da, np.uint8)[:, :8] ==
+                       np.asarray(S.ROUTER_IPV6, np.uint8)[:8]).all(axis=1)
+        exp = np.where(h & (l != 0), l, np.where(cluster, S.CLUSTER_ID, S.WORLD_ID))
+    else:
+        ident = identity_from_mark(g.headers.mark)
+        l, h = lab[:, 0], hit[:, 0]
+        ok = h & (l != 0) & (l != S.CLUSTER_ID)
+        if v4:
+            ok &= l != 1   # HOST_ID
+        exp = np.where((ident < 4) & ok, l, ident)
+    return exp.astype(np.uint32), applies
 
 
 def mismatches(g: Golden, action, verdict, identity):

@@ -232,7 +232,8 @@ def test_events_pin_identities():
     redirect) and egress headers sent to the stack (TRACE_TO_STACK
     dst_label).  Forwarded headers it never reports — ingress to the stack
     (bpf_netdev has no TRACE_NOTIFY), repeats inside the 5 s report interval
-    of an active flow — keep an unpinned identity."""
+    of an active flow — are pinned by the kernel's LPM instead
+    (test_lpm_identities_pin_every_tc_header)."""
     for name in G.names():
         g = G.Golden(name)
         if g.ev is None or g.mode == O.MODE_XDP:
@@ -240,10 +241,56 @@ def test_events_pin_identities():
         ev = g.ev
         obs = (O.TRACE_TO_STACK if g.mode == O.MODE_EGRESS else O.TRACE_TO_LXC)
         reported = g.ev_hdr[(ev["type"] == 4) & (ev["subtype"] == obs)]
-        assert (g.idmask[reported] == 0xFFFFFFFF).all(), name
+        assert (g.idmask_reported[reported] == 0xFFFFFFFF).all(), name
         if g.mode != O.MODE_EGRESS:   # proxy redirects: the proxy map
             prox = (g.action == 7) & (g.verdict > 0)
-            assert (g.idmask[prox] == 0xFFFFFFFF).all(), name
+            assert (g.idmask_reported[prox] == 0xFFFFFFFF).all(), name
+
+
+LPM_NAMES = [n for n in NAMES if G.Golden(n).lpm is not None]
+
+
+def test_every_fixture_has_kernel_lpm():
+    assert LPM_NAMES == NAMES
+
+
+@pytest.mark.parametrize("name", LPM_NAMES)
+def test_oracle_lpm_matches_kernel(name):
+    """ipcache_lookup4/6 of the restatement against the kernel's own LPM
+    trie (BPF_MAP_LOOKUP_ELEM on cilium_ipcache, oracle/pin_lpm.py) for
+    every address of every header: label and hit, 100%."""
+    g = G.Golden(name)
+    o = O.Oracle(g.tables)
+    h = g.headers
+    cols = [h.saddr, h.daddr,
+            h.saddr if g.pkt is None else g.pkt[:, 0],
+            h.daddr if g.pkt is None else g.pkt[:, 1]]
+    for c, a in enumerate(cols):
+        lab, hit = o.ipcache_lookup(h.family, a)
+        np.testing.assert_array_equal(hit, g.lpm_hit[:, c], err_msg=f"hit, column {c}")
+        np.testing.assert_array_equal(lab, g.lpm[:, c], err_msg=f"label, column {c}")
+
+
+@pytest.mark.parametrize("name", LPM_NAMES)
+def test_lpm_identities_pin_every_tc_header(name):
+    """The identities derived from the kernel's LPM (golden_io.lpm_identity)
+    agree with every identity bit the reference reported itself (trace
+    records, drop cb[1], proxy map), and together they pin the full 32-bit
+    identity of every tc-path header whose program reached the ipcache
+    lookup — forwarded headers the reference never reports included."""
+    g = G.Golden(name)
+    m = g.idmask_reported
+    both = g.lpm_applies & (m != 0)
+    np.testing.assert_array_equal(g.lpm_expected[both] & m[both],
+                                  g.identity_reported[both] & m[both])
+    tc = g.mode != 2
+    if g.mode == 3:
+        tc = ~((g.action == 1) & (g.verdict == -1))
+    reached = tc & ~G.no_identity(g)
+    assert (g.idmask[reached] == 0xFFFFFFFF).all()
+    unreported = reached & (m != 0xFFFFFFFF)
+    if g.mode != 2 and len(g.verdict) > 100:
+        assert unreported.any(), "the LPM pins headers the reference never reports"
 
 
 LB_NAMES = [n for n in NAMES if G.Golden(n).pkt is not None]
