@@ -633,11 +633,23 @@ __device__ __forceinline__ void acc_publish(const unsigned long long *s_met,
 // LB: the launch has a load balancer — an egress batch reads the service
 // step's results (lb.hip), every batch may reverse-NAT replies, and the
 // packet outputs (cfc_out.pkt_*) are written
-template <int MODE, int U, bool CT, bool NT, bool OPT, bool LB>
+// FAST: the epoch has the common shape (fast_shape): the compact IPv4 LPM,
+// no prefilter LPM, the endpoint table and both Bloom filters in LDS, and
+// (modes with XDP) a prefilter /32 set.  The tests of that shape and the
+// pointers of the other layouts are then compile-time facts, which frees the
+// SGPRs and exec-mask pairs they would hold for the whole loop.
+template <int MODE, int U, bool CT, bool NT, bool OPT, bool LB, bool FAST>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     DevTables T, LdsPlan L, cfc_hdr_v4 in, cfc_out out, EgressArgs E,
     CountArgs C, uint64_t per_block, LbIn LI)
 {
+    if (FAST) {
+        T.tbl24 = T.tbl8 = T.pf_tbl24 = T.pf_tbl8 = nullptr;
+        __builtin_assume(T.l4d != nullptr);
+        __builtin_assume(T.lxc4 != nullptr);
+        if (MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL)
+            __builtin_assume(T.pf_fix != nullptr);
+    }
     // LDS image (uint4 units): metrics | endpoint slots | pf Bloom | pol Bloom
     unsigned long long *s_met = lds_met();
     Lds S;
@@ -646,9 +658,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     const uint32_t pol4 = pf4 + L.pf_words / 4;
     S.pfb_off = 4 * pf4;
     S.polb_off = 4 * pol4;
-    S.lxc = L.lxc_slots != 0;
-    S.pfb = L.pf_words != 0;
-    S.polb = L.pol_words != 0;
+    S.lxc = FAST || L.lxc_slots != 0;
+    S.pfb = FAST || L.pf_words != 0;
+    S.polb = FAST || L.pol_words != 0;
     S.pfb_mask = L.pf_words - 1;
     S.polb_mask = L.pol_words - 1;
     for (uint32_t j = threadIdx.x; j < (uint32_t)LDS_MET_U64; j += BLOCK)
@@ -1513,6 +1525,19 @@ __global__ __launch_bounds__(256) void k_patch16(const Patch16 *rec, uint64_t n)
     }
 }
 
+#ifndef CFC_FAST
+#define CFC_FAST 1   // 0: always the generic kernel (A/B builds)
+#endif
+// the epoch shape k_classify_v4<..., FAST = true> is compiled for
+bool fast_shape(const DevTables &T, int mode, const LdsPlan &L)
+{
+    if (!CFC_FAST)
+        return false;
+    const bool xdp = mode == CFC_MODE_XDP || mode == CFC_MODE_FULL;
+    return T.l4d && !T.tbl24 && !T.pf_tbl24 && T.lxc4 && L.lxc_slots && L.pol_words &&
+           (!xdp || (T.pf_fix && L.pf_words));
+}
+
 template <int MODE, bool CT, bool NT>
 void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out,
                     const EgressArgs &E, const CountArgs &C, uint32_t grid,
@@ -1520,12 +1545,15 @@ void launch_mode_nt(const DevTables &T, const cfc_hdr_v4 &in, const cfc_out &out
 {
     const LdsPlan L = lds_plan(T);
     const bool opt = in.mark || in.tcp_flags || out.action || (CT && out.ct);
-    auto kern = opt ? k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, false>
-                    : k_classify_v4<MODE, CFC_UNROLL, CT, NT, false, false>;
+    const bool fast = fast_shape(T, MODE, L);
+    auto kern = opt ? (fast ? k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, false, true>
+                            : k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, false, false>)
+                    : (fast ? k_classify_v4<MODE, CFC_UNROLL, CT, NT, false, false, true>
+                            : k_classify_v4<MODE, CFC_UNROLL, CT, NT, false, false, false>);
     const LbIn none{};
     if constexpr (CT && MODE != CFC_MODE_XDP) {
         if (lb)
-            kern = k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, true>;
+            kern = k_classify_v4<MODE, CFC_UNROLL, CT, NT, true, true, false>;
     }
     set_lds_limit((const void *)kern, (int)LDS_PER_WG);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
