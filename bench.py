@@ -116,8 +116,16 @@ def main():
     ap.add_argument("--ct-apply", action="store_true",
                     help="c5: every step is classify + cfc_ct_apply_v4 (the batch's CT "
                          "creates, deletes and timeouts written into the device CT "
-                         "table); the new flows' source ports are re-drawn on the "
+                         "table) + the CT garbage collector when its interval has "
+                         "passed; the new flows' source ports are re-drawn on the "
                          "device at the start of each step, so every step creates")
+    ap.add_argument("--step-seconds", type=int, default=61,
+                    help="--ct-apply: datapath clock advance per step (cfc_set_clock)")
+    ap.add_argument("--gc-interval", type=int, default=60,
+                    help="--ct-apply: conntrack-garbage-collector-interval "
+                         "(daemon/main.go:367, default 60 s): cfc_ct_gc with "
+                         "RemoveExpired at the step's clock once this much clock "
+                         "has passed since the last one (0: no GC)")
     args = ap.parse_args()
     if args.ct_apply and args.workload != "c5":
         ap.error("--ct-apply needs --workload c5")
@@ -196,6 +204,7 @@ def main():
                    torch.empty(n, dtype=torch.int32, device=dev), None,
                    torch.empty(n, dtype=torch.uint8, device=dev) if args.ct_apply else None)
     salt = [0]
+    clock = {"now": 0, "last_gc": 0, "gcs": 0, "gc_deleted": 0, "alive": None}
     n6 = len(batch6) if batch6 is not None else 0
     out6 = Verdicts(torch.empty(n6, dtype=torch.int32, device=dev),
                     torch.empty(n6, dtype=torch.int32, device=dev), None)
@@ -217,9 +226,18 @@ def main():
         if args.ct_apply:   # fresh new flows: their source ports re-drawn
             salt[0] += 1
             p[new_idx] = new_ports ^ ((salt[0] * 0x9E37) & 0xFFFF)
+            clock["now"] += args.step_seconds
+            dp.set_clock(clock["now"])
         dp.classify_v4(batch, mode, ep_lxc, out=out)
         if args.ct_apply:
             dp.ct_apply(batch, out, mode, ep_lxc)
+            # EnableConntrackGC's loop (pkg/endpointmanager/conntrack.go:96-125)
+            if args.gc_interval and clock["now"] - clock["last_gc"] >= args.gc_interval:
+                g = dp.ct_gc(-1, clock["now"])
+                clock["last_gc"] = clock["now"]
+                clock["gcs"] += 1
+                clock["gc_deleted"] += g["deleted"]
+                clock["alive"] = g["alive"]
         if args.notify:   # records stay on the device (no sync in the step)
             LL.check(dp.L.cfc_monitor_events_v4(
                 dp.h, ctypes.byref(nt_hdr), ctypes.byref(nt_out), mode, ep_lxc,
@@ -232,11 +250,12 @@ def main():
 
     for w in range(args.warmup):
         step()
-        if args.ct_apply:   # each step grows the CT table by its new flows
+        if args.ct_apply:   # each step creates its new flows, the GC drops old ones
             torch.cuda.synchronize()
             sw = dp.stats()
-            log(f"[rank {rank}] warmup {w}: {sw['ct4_entries']} CT4 entries, apply "
-                f"device {sw['ct_apply_device']} host {sw['ct_apply_host']}")
+            log(f"[rank {rank}] warmup {w}: clock {clock['now']} s, apply device "
+                f"{sw['ct_apply_device']} host {sw['ct_apply_host']}, GC runs "
+                f"{clock['gcs']} deleted {clock['gc_deleted']}")
     torch.cuda.synchronize()
     dp.counters_clear()
     # HIP events recorded by the library on the launch stream around the
@@ -448,17 +467,22 @@ def main():
         "parity_sample_ok": parity,
         "monitor_records_per_step_per_gpu": int(nt_cnt.item()) if args.notify else None,
     }
-    if args.ct_apply:   # the step is classify + cfc_ct_apply_v4
+    if args.ct_apply:   # the step is classify + cfc_ct_apply_v4 (+ cfc_ct_gc)
         st2 = dp.stats()
         # the host fallback (table past 3/4 load) is not the measured path
-        assert st2["ct_apply_host"] == 0, ("CT apply left the device path: "
-                                           "fewer --steps", st2)
+        if st2["ct_apply_host"]:
+            log(f"[rank {rank}] CT apply left the device path: {st2}")
+            sys.exit(3)
         res["ct_apply"] = {
             "path_device_calls": st2["ct_apply_device"],
             "path_host_calls": st2["ct_apply_host"],
-            "ct4_entries_after": st2["ct4_entries"],
-            "apply_ms_per_step": round(call_ms - tm["classify_ms"] / args.steps
-                                       - count_ms, 4),
+            "apply_and_gc_ms_per_step": round(call_ms - tm["classify_ms"] / args.steps
+                                              - count_ms, 4),
+            "clock_s_per_step": args.step_seconds,
+            "gc_interval_s": args.gc_interval,
+            "gc_runs": clock["gcs"],
+            "gc_deleted": clock["gc_deleted"],
+            "ct_entries_after_last_gc": clock["alive"],
         }
     print(json.dumps(res), flush=True)
     if world > 1:

@@ -31,7 +31,7 @@ EXPORTS = (
     "cfc_ct_apply_v4", "cfc_ct_apply_v6", "cfc_map_update_batch",
     "cfc_set_node_config", "cfc_get_node_config", "cfc_identity_counters",
     "cfc_set_clock", "cfc_monitor_events_v4", "cfc_monitor_events_v6",
-    "cfc_map_dump",
+    "cfc_map_dump", "cfc_ct_gc",
 )
 # CT byte (cfc_out.ct): per stage (bits 0-3, then 4-7 for the destination's
 # ingress lookup after egress local delivery)
@@ -41,6 +41,29 @@ CT_RES_MASK, CT_DONE, CT_CREATE = 0x3, 0x4, 0x8
 
 class CfcError(OSError):
     pass
+
+
+# cfc_ct_gc (include/cfc.h): struct GCFilter flags and types
+GC_REMOVE_EXPIRED, GC_VALID_IPS, GC_MATCH_IPS = 1, 2, 4
+
+
+class Ip(ctypes.Structure):
+    _fields_ = [("family", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 3),
+                ("addr", ctypes.c_uint8 * 16)]
+
+
+class GcFilter(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint32), ("time", ctypes.c_uint32),
+                ("valid_ips", ctypes.c_void_p), ("n_valid", ctypes.c_uint32),
+                ("pad0", ctypes.c_uint32),
+                ("match_ips", ctypes.c_void_p), ("n_match", ctypes.c_uint32),
+                ("pad1", ctypes.c_uint32)]
+
+
+class GcStats(ctypes.Structure):
+    _fields_ = [("deleted", ctypes.c_uint64), ("alive", ctypes.c_uint64),
+                ("device_deleted", ctypes.c_uint64), ("log_deleted", ctypes.c_uint64),
+                ("host_deleted", ctypes.c_uint64), ("slots_freed", ctypes.c_uint64)]
 
 
 _HDR = [("saddr", ctypes.c_void_p), ("daddr", ctypes.c_void_p),
@@ -147,6 +170,7 @@ def lib():
     L.cfc_ct_apply_v6.argtypes = [vp, ctypes.POINTER(HdrV6), ctypes.POINTER(Out),
                                   i32, ctypes.c_uint16, vp]
     L.cfc_set_clock.argtypes = [vp, u32]
+    L.cfc_ct_gc.argtypes = [vp, i32, ctypes.POINTER(GcFilter), ctypes.POINTER(GcStats), vp]
     for f in (L.cfc_drop_notify_v4, L.cfc_drop_notify_v6,
               L.cfc_monitor_events_v4, L.cfc_monitor_events_v6):
         f.argtypes = [vp, vp, ctypes.POINTER(Out), i32, ctypes.c_uint16, vp, vp,

@@ -181,7 +181,15 @@ struct cfc_ctx {
     // the device table until ct_sync
     int ct_apply_mode = CFC_CT_APPLY_DEVICE;
     bool ct_dirty = false;
-    uint64_t cta_claims = 0;     // device inserts since the last sync
+    uint64_t cta_claims = 0;     // device creates the host mirror lacks (alive)
+    // device-table occupancy for the apply's load check: exact non-free
+    // slots at the last GC (ct_used, while ct_used_valid), plus the inserts
+    // since (cta_ins); otherwise the host's live + tombstone counts
+    uint64_t ct_used = 0, cta_ins = 0;
+    bool ct_used_valid = false;
+    // deletes of the device GC (cfc_ct_gc) the host mirror has not taken
+    DevBuf gc_log, gc_tmp, gc_sets, gc_cnt;
+    uint64_t gc_log_used = 0;
     uint32_t cta_seq = 0;
     uint32_t n_apply_dev = 0, n_apply_host = 0;
     // the CT table's version: bumped by every commit that changes tables
@@ -368,38 +376,68 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
             return -EIO;
     }
     std::string key;
-    for (const CtSyncRec &r : rec) {
-        const bool del = (r.w & CT_TOMBSTONE) == CT_TOMBSTONE;
-        const uint32_t w = r.w & ~CT_TOMBSTONE;
-        Ct4Slot &h = G.ct4_host[r.slot];
-        const bool prev_live = h.w != 0 && h.w != CT_TOMBSTONE;
-        Map *m = ct_slot_key(E, 4, &r.x, &r.y, r.z, w, &key);
-        if (del) {
-            if (m)
+    // the GC's deletes first (they precede every dirty record of their
+    // slots: a GC clears the slot's dirty bits), then the applies' deletes
+    // (an entry deleted and created again lives in another slot, created
+    // after the delete), then creates and updates
+    if (c->gc_log_used) {
+        std::vector<CtGcRec> gl(c->gc_log_used);
+        if (hipMemcpyAsync(gl.data(), c->gc_log.p, sizeof(CtGcRec) * gl.size(),
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        for (const CtGcRec &r : gl) {
+            Ct4Slot &h = G.ct4_host[r.slot];
+            if (Map *m = ct_slot_key(E, 4, &r.x, &r.y, r.z, r.w, &key))
                 m->erase_raw(key);
-            if (prev_live) {
+            if (h.x == r.x && h.y == r.y && h.z == r.z && h.w == r.w) {
                 G.n_ct4--;
                 G.tomb4++;
             } else if (h.w == 0) {
                 G.tomb4++;
             }
             h = Ct4Slot{0, 0, 0, CT_TOMBSTONE};
-        } else if (r.info.y & CTI_CREATED) {
-            if (m) {
-                std::string v(m->value_bytes(), '\0');
-                ct_value_from_dev(v, r, true);
-                m->put_raw(key, v);
+        }
+        c->gc_log_used = 0;
+        for (auto &kv : c->maps)
+            kv.second->gc_pending = 0;
+    }
+    for (int pass = 0; pass < 2; pass++) {
+        for (const CtSyncRec &r : rec) {
+            const bool del = (r.w & CT_TOMBSTONE) == CT_TOMBSTONE;
+            if (del != (pass == 0))
+                continue;
+            const uint32_t w = r.w & ~CT_TOMBSTONE;
+            Ct4Slot &h = G.ct4_host[r.slot];
+            const bool prev_live = h.w != 0 && h.w != CT_TOMBSTONE;
+            Map *m = ct_slot_key(E, 4, &r.x, &r.y, r.z, w, &key);
+            if (del) {
+                if (m)
+                    m->erase_raw(key);
+                if (prev_live) {
+                    G.n_ct4--;
+                    G.tomb4++;
+                } else if (h.w == 0) {
+                    G.tomb4++;
+                }
+                h = Ct4Slot{0, 0, 0, CT_TOMBSTONE};
+            } else if (r.info.y & CTI_CREATED) {
+                if (m) {
+                    std::string v(m->value_bytes(), '\0');
+                    ct_value_from_dev(v, r, true);
+                    m->put_raw(key, v);
+                }
+                if (!prev_live) {
+                    G.n_ct4++;
+                    if (h.w == CT_TOMBSTONE)
+                        G.tomb4--;
+                }
+                h = Ct4Slot{r.x, r.y, r.z, w};
+            } else if (m) {
+                auto it = m->kv.find(key);
+                if (it != m->kv.end() && it->second.val.size() >= 56)
+                    ct_value_from_dev(it->second.val, r, false);
             }
-            if (!prev_live) {
-                G.n_ct4++;
-                if (h.w == CT_TOMBSTONE)
-                    G.tomb4--;
-            }
-            h = Ct4Slot{r.x, r.y, r.z, w};
-        } else if (m) {
-            auto it = m->kv.find(key);
-            if (it != m->kv.end() && it->second.val.size() >= 56)
-                ct_value_from_dev(it->second.val, r, false);
         }
     }
     if (c->log_used) {
@@ -439,6 +477,8 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
     }
     c->log_used = 0;
     c->cta_claims = 0;
+    c->cta_ins = 0;
+    c->ct_used_valid = false;
     c->ct_dirty = false;
     E.st.ct4_entries = G.n_ct4;
     return 0;
@@ -2371,12 +2411,14 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     const uint64_t nreqA = hc[CTA_NREQA], nhit = hc[CTA_NHIT];
     // room for every create and its ICMP entry: the table below 3/4 load,
     // each CT map below max_entries; else the host path (which rebuilds)
-    bool ok = 4 * (G.n_ct4 + G.tomb4 + c->cta_claims + 2 * nreqA) <= 3 * slots &&
+    const uint64_t used = c->ct_used_valid ? c->ct_used : G.n_ct4 + G.tomb4;
+    bool ok = 4 * (used + c->cta_ins + 2 * nreqA) <= 3 * slots &&
               nreqA <= A.req_cap;
     for (auto &kv : c->maps) {
         const Map *m = kv.second.get();
         if (m->role == ROLE_CT4 &&
-            m->kv.size() + c->cta_claims + c->log_used + 2 * nreqA > m->max_entries)
+            m->kv.size() - m->gc_pending + c->cta_claims + c->log_used + 2 * nreqA >
+                m->max_entries)
             ok = false;
     }
     if (!ok) {   // the scan's marks (and delete orders) go
@@ -2434,10 +2476,12 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
         (void)hipMemcpyAsync(&claims, A.cnt + CTA_CLAIMS, 4, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
         c->cta_claims += claims;
+        c->cta_ins += claims;
         c->built_sig[3] = ~0ull;
         return rc;
     }
     c->cta_claims += hc[CTA_CLAIMS];
+    c->cta_ins += hc[CTA_CLAIMS];
     c->log_used += hc[CTA_NLOG];
     c->cta_seq++;
     return 0;
@@ -2708,6 +2752,230 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     return 0;
 }
 
+// ---- cfc_ct_gc: ctmap.GC with doFiltering (pkg/maps/ctmap/ctmap.go:303-350)
+struct GcFilterHost {
+    const cfc_ct_gc_filter &f;
+    // doFiltering on a CT key's two addresses (daddr at 0, saddr at al)
+    bool in(const cfc_ip *set, uint32_t n, int fam, const uint8_t *a) const
+    {
+        const size_t al = fam == 4 ? 4 : 16;
+        for (uint32_t i = 0; i < n; i++)
+            if (set[i].family == fam && !memcmp(set[i].addr, a, al))
+                return true;
+        return false;
+    }
+    bool del(int fam, const uint8_t *key, uint32_t lifetime) const
+    {
+        const size_t al = fam == 4 ? 4 : 16;
+        const uint8_t *da = key, *sa = key + al;
+        if ((f.flags & CFC_GC_REMOVE_EXPIRED) && lifetime < f.time)
+            return true;
+        if ((f.flags & CFC_GC_VALID_IPS) && !in(f.valid_ips, f.n_valid, fam, da) &&
+            !in(f.valid_ips, f.n_valid, fam, sa))
+            return true;
+        return (f.flags & CFC_GC_MATCH_IPS) &&
+               (in(f.match_ips, f.n_match, fam, da) || in(f.match_ips, f.n_match, fam, sa));
+    }
+};
+
+// the IPv4 part on the device: the CT table and the pending CtLog
+int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
+              cfc_ct_gc_stats &st, hipStream_t s)
+{
+    Epoch &E = *c->epoch;
+    GCt &G = *E.ct;
+    const uint64_t slots = G.ct4_host.size();
+    // the selected maps' selector words, and the IPv4 addresses of the sets
+    std::vector<uint32_t> mw;
+    std::vector<Map *> mm;
+    for (Map *m : sel)
+        if (m->role == ROLE_CT4) {
+            mw.push_back(ct_owner_word((uint32_t)std::max(m->policy_lxc, 0), m->policy_lxc >= 0) |
+                         (m->ct_any ? 2u : 0u));
+            mm.push_back(m);
+        }
+    if (mw.empty())
+        return 0;
+    auto v4set = [](const cfc_ip *set, uint32_t n) {
+        std::vector<uint32_t> v;
+        for (uint32_t i = 0; i < n; i++)
+            if (set[i].family == 4) {
+                uint32_t a;
+                memcpy(&a, set[i].addr, 4);
+                v.push_back(a);
+            }
+        std::sort(v.begin(), v.end());
+        return v;
+    };
+    const std::vector<uint32_t> va = (f.flags & CFC_GC_VALID_IPS) ? v4set(f.valid_ips, f.n_valid)
+                                                                   : std::vector<uint32_t>();
+    const std::vector<uint32_t> ma = (f.flags & CFC_GC_MATCH_IPS) ? v4set(f.match_ips, f.n_match)
+                                                                   : std::vector<uint32_t>();
+    // every entry the host mirror holds can be deleted once before its next
+    // sync (one the host never saw needs no log record): the log's room
+    const uint64_t need = c->gc_log_used + G.n_ct4 + 1;
+    if (c->gc_log.bytes < sizeof(CtGcRec) * need) {
+        DevBuf nl;
+        if (nl.ensure(sizeof(CtGcRec) * need))
+            return -ENOMEM;
+        if (c->gc_log_used &&
+            (hipMemcpyAsync(nl.p, c->gc_log.p, sizeof(CtGcRec) * c->gc_log_used,
+                            hipMemcpyDeviceToDevice, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess))
+            return -EIO;
+        std::swap(nl.p, c->gc_log.p);
+        std::swap(nl.bytes, c->gc_log.bytes);
+    }
+    const size_t set_words = CTG_MAX_MAPS * 2 + va.size() + ma.size() + 1;
+    if (c->gc_sets.ensure(4 * set_words) || c->gc_cnt.ensure(4 * CTG_NCNT) ||
+        (c->log_used && c->gc_tmp.ensure(sizeof(CtLog) * c->log_used)))
+        return -ENOMEM;
+    uint32_t *sets = (uint32_t *)c->gc_sets.p, *cnt = (uint32_t *)c->gc_cnt.p;
+    uint64_t deleted = 0, fresh = 0, live = 0, nonfree = 0, freed = 0, last_freed = 0;
+    uint32_t logkept = (uint32_t)c->log_used, logn = (uint32_t)c->log_used;
+    for (size_t a = 0; a < mw.size(); a += CTG_MAX_MAPS) {
+        const uint32_t nm = (uint32_t)std::min<size_t>(CTG_MAX_MAPS, mw.size() - a);
+        std::vector<uint32_t> hs(CTG_MAX_MAPS * 2, 0);
+        std::copy(mw.begin() + (long)a, mw.begin() + (long)a + nm, hs.begin());
+        hs.insert(hs.end(), va.begin(), va.end());
+        hs.insert(hs.end(), ma.begin(), ma.end());
+        CtGcArgs A{};
+        A.ct4 = (Ct4Slot *)G.ct4.p;
+        A.tm = (CtTimer *)G.ct4_tm.p;
+        A.info = (CtInfo *)G.ct4_info.p;
+        A.acct = (uint64_t *)G.ct_acct.p;
+        A.slots = slots;
+        A.mask = (uint32_t)(slots - 1);
+        A.maps = sets;
+        A.n_maps = nm;
+        A.mcnt = sets + CTG_MAX_MAPS;
+        A.flags = ((f.flags & CFC_GC_REMOVE_EXPIRED) ? CTG_REMOVE_EXPIRED : 0u) |
+                  ((f.flags & CFC_GC_VALID_IPS) ? CTG_VALID : 0u) |
+                  ((f.flags & CFC_GC_MATCH_IPS) ? CTG_MATCH : 0u);
+        A.time = f.time;
+        A.valid = sets + 2 * CTG_MAX_MAPS;
+        A.n_valid = (uint32_t)va.size();
+        A.match = A.valid + va.size();
+        A.n_match = (uint32_t)ma.size();
+        A.log = (CtGcRec *)c->gc_log.p + c->gc_log_used + deleted;
+        A.log_cap = (uint32_t)(c->gc_log.bytes / sizeof(CtGcRec) - c->gc_log_used - deleted);
+        A.cnt = cnt;
+        uint32_t hc[CTG_NCNT], hm[CTG_MAX_MAPS];
+        if (hipMemcpyAsync(sets, hs.data(), 4 * hs.size(), hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipMemsetAsync(cnt, 0, 4 * CTG_NCNT, s) != hipSuccess || ct_gc4(A, s))
+            return -EIO;
+        // the pending TCP-map ICMP entries of the applies, compacted
+        if (logn && (ct_gc_log(A, (const CtLog *)c->cta_log.p, logn, (CtLog *)c->gc_tmp.p, s) ||
+                     hipMemcpyAsync(hc, cnt, 4 * CTG_NCNT, hipMemcpyDeviceToHost, s) !=
+                         hipSuccess ||
+                     hipStreamSynchronize(s) != hipSuccess ||
+                     hipMemcpyAsync(c->cta_log.p, c->gc_tmp.p, sizeof(CtLog) * hc[CTG_LOGKEPT],
+                                    hipMemcpyDeviceToDevice, s) != hipSuccess))
+            return -EIO;
+        if (hipMemcpyAsync(hc, cnt, 4 * CTG_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(hm, A.mcnt, 4 * nm, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        if (hc[CTG_DELETED] > A.log_cap)
+            return -EIO;   // (not reached: the log has room for every entry)
+        for (uint32_t j = 0; j < nm; j++)
+            mm[a + j]->gc_pending += hm[j];
+        deleted += hc[CTG_DELETED];
+        fresh += hc[CTG_FRESH];
+        live += hc[CTG_LIVE];
+        nonfree = hc[CTG_NONFREE];
+        freed += hc[CTG_FREED];
+        last_freed = hc[CTG_FREED];
+        if (logn) {
+            logkept = hc[CTG_LOGKEPT];
+            logn = logkept;
+        }
+    }
+    c->gc_log_used += deleted;
+    c->cta_claims -= std::min(c->cta_claims, fresh);
+    // exact occupancy now: the non-free slots the last pass saw, less what
+    // its trim freed (an earlier chunk's deletes are tombstones it counted)
+    c->ct_used = nonfree >= last_freed ? nonfree - last_freed : 0;
+    c->cta_ins = 0;
+    c->ct_used_valid = true;
+    if (deleted || fresh)
+        c->ct_dirty = true;
+    c->ct_gen++;   // the table changed under any classify launch's hit slots
+    st.device_deleted += deleted + fresh;
+    st.log_deleted += c->log_used - logkept;
+    st.alive += live + logkept;
+    st.slots_freed += freed;
+    c->log_used = logkept;
+    return 0;
+}
+
+int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, hipStream_t s)
+{
+    if (f->flags & ~(CFC_GC_REMOVE_EXPIRED | CFC_GC_VALID_IPS | CFC_GC_MATCH_IPS))
+        return -EINVAL;
+    if (((f->flags & CFC_GC_VALID_IPS) && f->n_valid && !f->valid_ips) ||
+        ((f->flags & CFC_GC_MATCH_IPS) && f->n_match && !f->match_ips))
+        return -EINVAL;
+    std::vector<Map *> sel;
+    if (fd >= 0) {
+        Map *m = get_map(c, fd);
+        if (!m)
+            return -EBADF;
+        if (!m->ct())
+            return -EINVAL;
+        sel.push_back(m);
+    } else {
+        for (auto &kv : c->maps)
+            if (kv.second->ct())
+                sel.push_back(kv.second.get());
+    }
+    // host-side CT changes into the device table first
+    if (int rc = commit_locked(c, s))
+        return rc;
+    order_after_launches(c, s);
+    cfc_ct_gc_stats st{};
+    Epoch &E = *c->epoch;
+    const bool dev4 = !E.ct->ct4_host.empty() && E.ct->ct4_info.p;
+    if (dev4)
+        if (int rc = ct_gc_dev(c, sel, *f, st, s))
+            return rc;
+    // what only the host holds: IPv6 maps (their applies run on the host),
+    // IPv4 maps without a device table, IPv4 TCP maps' ICMP entries
+    const GcFilterHost H{*f};
+    for (Map *m : sel) {
+        const bool v6 = m->role == ROLE_CT6, all = v6 || !dev4;
+        if (!all && !m->n_aux)
+            continue;
+        uint64_t kept = 0, gone = 0;
+        for (auto it = m->kv.begin(); it != m->kv.end();) {
+            const std::string &k = it->first;
+            if (!all && !m->aux_key(k)) {
+                ++it;
+                continue;
+            }
+            uint32_t life = 0;
+            if (it->second.val.size() >= 36)
+                memcpy(&life, &it->second.val[32], 4);
+            if (H.del(v6 ? 6 : 4, (const uint8_t *)k.data(), life)) {
+                // journaled where the device table holds it: the next commit
+                // turns its slot into a tombstone
+                it = m->ct_erase_at(it, all);
+                gone++;
+            } else {
+                kept++;
+                ++it;
+            }
+        }
+        st.host_deleted += gone;
+        st.alive += kept;
+    }
+    st.deleted = st.device_deleted + st.log_deleted + st.host_deleted;
+    if (out)
+        *out = st;
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2722,6 +2990,21 @@ int cfc_ct_apply_v6(cfc_ctx *c, const cfc_hdr_v6 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream)
 {
     return ct_apply(c, 6, in, out, mode, ep_lxc, stream);
+}
+
+int cfc_ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *filter, cfc_ct_gc_stats *stats,
+              void *stream)
+{
+    if (!c || !filter)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    const int rc = ct_gc(c, fd, filter, stats, (hipStream_t)stream);
+    if (!rc)
+        (void)hipStreamSynchronize((hipStream_t)stream);
+    return rc;
 }
 
 }  // extern "C"

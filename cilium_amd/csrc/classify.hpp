@@ -165,6 +165,47 @@ int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, C
                 uint32_t cap, uint32_t *cnt, hipStream_t s);
 int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
 
+// ---- CT garbage collection (cfc_ct_gc): ctmap.GC's doFiltering
+// (pkg/maps/ctmap/ctmap.go:303-325) over the device CT4 table.  A deleted
+// entry's slot becomes a plain tombstone at once (free for inserts); its key
+// goes to a log the host mirror replays at its next ct_sync.  Then every
+// cluster's trailing run of tombstones is freed (w = 0): no probe sequence
+// runs through it to a live entry.
+// counters: deletes logged for the host, entries of the selected maps left,
+// non-free slots before
+// the trim, slots the trim freed, log entries kept, deletes of entries the
+// host never saw
+enum { CTG_DELETED, CTG_LIVE, CTG_NONFREE, CTG_FREED, CTG_LOGKEPT, CTG_FRESH, CTG_NCNT = 8 };
+constexpr uint32_t CTG_MAX_MAPS = 64;
+constexpr uint32_t CTG_REMOVE_EXPIRED = 1, CTG_VALID = 2, CTG_MATCH = 4;
+struct CtGcRec {
+    uint32_t slot, x, y, z, w;
+};
+struct CtGcArgs {
+    Ct4Slot *ct4;
+    CtTimer *tm;
+    CtInfo *info;
+    uint64_t *acct;               // [slot][4] (may be null)
+    uint64_t slots;
+    uint32_t mask;
+    // the CT maps selected (owner word | kind << 1: 0 TCP map, 1 ANY map);
+    // an entry of map j counts into mcnt[j]
+    const uint32_t *maps;
+    uint32_t n_maps;
+    uint32_t *mcnt;
+    uint32_t flags, time;
+    const uint32_t *valid, *match; // sorted raw be32 addresses
+    uint32_t n_valid, n_match;
+    CtGcRec *log;
+    uint32_t log_cap;
+    uint32_t *cnt;                // CTG_* counters
+};
+int ct_gc4(const CtGcArgs &A, hipStream_t s);
+// the pending TCP-map ICMP entries of the device applies (CtLog) filtered the
+// same way, kept in order of appearance: in[0, n) -> out; the kept count
+// into A.cnt[CTG_LOGKEPT]
+int ct_gc_log(const CtGcArgs &A, const CtLog *in, uint32_t n, CtLog *out, hipStream_t s);
+
 // ---- service load balancing of an egress batch (lb.hip)
 struct LbArgs {
     const uint32_t *sa, *da, *pt, *mt, *hash;   // the batch (hash may be null)

@@ -922,6 +922,142 @@ __global__ __launch_bounds__(256) void k_cta_tomb(Ct4Slot *ct4, const CtSyncRec 
     }
 }
 
+// ---- garbage collection (cfc_ct_gc, ctmap.go:303-325 doFiltering) ---------
+__device__ __forceinline__ bool gc_in_set(const uint32_t *set, uint32_t n, uint32_t a)
+{
+    uint32_t lo = 0, hi = n;   // sorted ascending
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (set[mid] < a)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo < n && set[lo] == a;
+}
+// doFiltering on the entry's two addresses and lifetime
+__device__ __forceinline__ bool gc_delete(const CtGcArgs &A, uint32_t x, uint32_t y,
+                                          uint32_t lifetime)
+{
+    if ((A.flags & CTG_REMOVE_EXPIRED) && lifetime < A.time)
+        return true;
+    if ((A.flags & CTG_VALID) && !gc_in_set(A.valid, A.n_valid, x) &&
+        !gc_in_set(A.valid, A.n_valid, y))
+        return true;
+    return (A.flags & CTG_MATCH) &&
+           (gc_in_set(A.match, A.n_match, x) || gc_in_set(A.match, A.n_match, y));
+}
+// the selected map an entry belongs to (its CT map: owner word, TCP or ANY
+// kind), or -1
+__device__ __forceinline__ int gc_map(const uint32_t *smaps, uint32_t n, uint32_t mw)
+{
+    for (uint32_t j = 0; j < n; j++)
+        if (smaps[j] == mw)
+            return (int)j;
+    return -1;
+}
+
+// One thread per slot (grid-stride).  A deleted entry the host mirror holds
+// (no CTI_CREATED: created before the host's last sync) is logged for it;
+// one the host never saw is just dropped.  Either way the slot becomes a
+// plain tombstone with no dirty bits and zero accounting.
+__global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
+{
+    __shared__ uint32_t smaps[CTG_MAX_MAPS], scnt[CTG_MAX_MAPS];
+    for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256) {
+        smaps[j] = A.maps[j];
+        scnt[j] = 0;
+    }
+    __syncthreads();
+    uint32_t fresh = 0, live = 0, nonfree = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.slots; base += stride) {
+        const uint64_t s = base + threadIdx.x;
+        uint4 k = make_uint4(0, 0, 0, 0);
+        if (s < A.slots)
+            k = ld16(A.ct4 + s);
+        bool del = false, logit = false;
+        int j = -1;
+        if (k.w != 0) {
+            nonfree++;
+            // a tombstone, a claim, or an apply's delete the host has not taken
+            if (!(k.w & 0xF000u)) {
+                j = gc_map(smaps, A.n_maps, (k.w & 0xFFFF0800u) | ((k.w & 0xFF) != 6 ? 2u : 0u));
+                del = j >= 0 && gc_delete(A, k.x, k.y, A.tm[s].lifetime);
+                live += j >= 0 && !del;
+                if (del) {
+                    logit = !(A.info[s].y & CTI_CREATED);
+                    fresh += !logit;
+                }
+            }
+        }
+        const uint32_t r = wave_count(&A.cnt[CTG_DELETED], logit);
+        if (logit && r < A.log_cap)
+            A.log[r] = CtGcRec{(uint32_t)s, k.x, k.y, k.z, k.w};
+        if (del) {
+            *reinterpret_cast<uint4 *>(A.ct4 + s) = make_uint4(0, 0, 0, CT_TOMBSTONE);
+            A.info[s] = CtInfo{0, 0};
+            if (A.acct)
+                *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s) =
+                    *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s + 2) = make_ulonglong2(0, 0);
+            if (logit)
+                atomicAdd(&scnt[j], 1u);
+        }
+    }
+    wave_add(&A.cnt[CTG_LIVE], live);
+    wave_add(&A.cnt[CTG_NONFREE], nonfree);
+    wave_add(&A.cnt[CTG_FRESH], fresh);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256)
+        if (scnt[j])
+            atomicAdd(&A.mcnt[j], scnt[j]);
+}
+
+// The tail of every cluster: a non-free slot followed by a free one.  Its
+// trailing run of plain tombstones is freed, walking back to the first slot
+// that is not one (a live entry keeps the tombstones before it: a probe
+// for it runs through them).
+__global__ __launch_bounds__(256) void k_ct_trim4(CtGcArgs A)
+{
+    uint32_t freed = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < A.slots; s += stride) {
+        if (A.ct4[s].w != CT_TOMBSTONE || A.ct4[(s + 1) & A.mask].w != 0)
+            continue;
+        // (a thread that started inside another's run meets it: each slot
+        // is freed by exactly one CAS)
+        uint32_t j = (uint32_t)s;
+        while (atomicCAS(&A.ct4[j].w, CT_TOMBSTONE, 0u) == CT_TOMBSTONE) {
+            freed++;
+            j = (j - 1) & A.mask;
+        }
+    }
+    wave_add(&A.cnt[CTG_FREED], freed);
+}
+
+// the pending TCP-map ICMP entries (CtLog): lifetime as ct_create4 wrote it
+// (now + CT_LIFETIME_NONTCP, conntrack.h:741-760; no lookup ever updates
+// one), the TCP map of its owner
+__global__ __launch_bounds__(256) void k_ct_gc_log(CtGcArgs A, const CtLog *in, uint32_t n,
+                                                   CtLog *out)
+{
+    __shared__ uint32_t smaps[CTG_MAX_MAPS];
+    for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256)
+        smaps[j] = A.maps[j];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    CtLog g{};
+    bool keep = false;
+    if (i < n) {
+        g = in[i];
+        keep = gc_map(smaps, A.n_maps, g.w & 0xFFFF0800u) < 0 ||
+               !gc_delete(A, g.x, g.y, g.now + CT_LIFETIME_NONTCP);
+    }
+    const uint32_t r = wave_count(&A.cnt[CTG_LOGKEPT], keep);
+    if (keep)
+        out[r] = g;
+}
+
 unsigned blocks_for(uint64_t n, unsigned cap)
 {
     const uint64_t b = (n + 255) / 256;
@@ -1035,6 +1171,24 @@ int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, C
 {
     hipLaunchKernelGGL(k_cta_collect, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4, tm,
                        info, slots, out, cap, cnt);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_gc4(const CtGcArgs &A, hipStream_t s)
+{
+    if (!A.slots || A.n_maps > CTG_MAX_MAPS)
+        return -EINVAL;
+    hipLaunchKernelGGL(k_ct_gc4, dim3(blocks_for(A.slots, 8192)), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_ct_trim4, dim3(blocks_for(A.slots, 8192)), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_gc_log(const CtGcArgs &A, const CtLog *in, uint32_t n, CtLog *out, hipStream_t s)
+{
+    if (A.n_maps > CTG_MAX_MAPS)
+        return -EINVAL;
+    if (n)
+        hipLaunchKernelGGL(k_ct_gc_log, dim3((n + 255) / 256), dim3(256), 0, s, A, in, n, out);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

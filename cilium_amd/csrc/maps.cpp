@@ -57,6 +57,8 @@ int Map::update(const void *key, const void *value, uint64_t flags)
                     touched[kv.begin()->first] = TOUCH_ERASE;
                 else
                     bump_sgen(kv.begin()->first);
+                if (aux_key(kv.begin()->first))
+                    n_aux--;
                 kv.erase(kv.begin());
             } else {
                 return lpm() ? -ENOSPC : -E2BIG;
@@ -66,6 +68,8 @@ int Map::update(const void *key, const void *value, uint64_t flags)
             touched[nk] = TOUCH_INSERT;
         else
             bump_sgen(nk);
+        if (aux_key(nk))
+            n_aux++;
     }
     Entry &e = kv[nk];
     e.key.assign((const char *)key, ksz);
@@ -113,6 +117,8 @@ int Map::erase(const void *key)
     if (it == kv.end())
         return -ENOENT;
     kv.erase(it);
+    if (aux_key(nk))
+        n_aux--;
     if (ct()) {
         touched[nk] = TOUCH_ERASE;
     } else {

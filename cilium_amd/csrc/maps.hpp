@@ -54,6 +54,18 @@ struct Map {
     // a commit patches into the device CT table in place
     std::map<std::string, int> touched;
     bool ct() const { return role == ROLE_CT4 || role == ROLE_CT6; }
+    // entries of an IPv4 TCP CT map that no lookup reaches (ct_create4's
+    // ICMP "related" entry, nexthdr != TCP at key byte 12): they live only
+    // here, not in the device CT table (flatten.cpp build_ct), so the CT GC
+    // filters them on the host; counted so a GC skips maps without any
+    uint64_t n_aux = 0;
+    bool aux_key(const std::string &k) const
+    {
+        return role == ROLE_CT4 && !ct_any && k.size() >= 13 && (uint8_t)k[12] != 6;
+    }
+    // CT entries the device GC deleted that the host mirror still holds
+    // (erased at the next ct_sync)
+    uint64_t gc_pending = 0;
 
     struct Entry {
         std::string key;  // key bytes as last written
@@ -88,15 +100,34 @@ struct Map {
     // no structural generation (the device table already has them)
     void put_raw(const std::string &k, const std::string &v)
     {
-        Entry &e = kv[k];
+        auto ins = kv.emplace(k, Entry{});
+        if (ins.second && aux_key(k))
+            n_aux++;
+        Entry &e = ins.first->second;
         e.key = k;
         e.val = v;
         gen++;
     }
     void erase_raw(const std::string &k)
     {
-        if (kv.erase(k))
+        if (kv.erase(k)) {
             gen++;
+            if (aux_key(k))
+                n_aux--;
+        }
+    }
+
+    // a CT entry removed while walking the map (the CT GC): journaled for
+    // the next commit unless the device table never held it
+    std::map<std::string, Entry>::iterator ct_erase_at(std::map<std::string, Entry>::iterator it,
+                                                       bool journal)
+    {
+        if (aux_key(it->first))
+            n_aux--;
+        if (journal)
+            touched[it->first] = TOUCH_ERASE;
+        gen++;
+        return kv.erase(it);
     }
 
     int update(const void *key, const void *value, uint64_t flags);

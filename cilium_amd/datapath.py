@@ -419,6 +419,37 @@ class Datapath:
         """cfc_set_clock: bpf_ktime_get_sec() for the next calls."""
         L.check(self.L.cfc_set_clock(self.h, int(now) & 0xFFFFFFFF), "clock")
 
+    def ct_gc(self, fd=-1, time=0, remove_expired=True, valid_ips=None,
+              match_ips=None, stream=None):
+        """cfc_ct_gc: ctmap.GC with doFiltering (pkg/maps/ctmap/ctmap.go:
+        303-350) on CT map `fd` (-1: every CT map).  valid_ips / match_ips:
+        iterables of IP address bytes (4 or 16), None = no such set.
+        -> gcStats as a dict {deleted, alive, ...}."""
+        def ips(lst):
+            if lst is None:
+                return None, 0
+            lst = [bytes(a) for a in lst]
+            arr = (L.Ip * max(len(lst), 1))()
+            for i, a in enumerate(lst):
+                arr[i].family = 4 if len(a) == 4 else 6
+                arr[i].addr[:len(a)] = list(a)
+            return arr, len(lst)
+        va, nv = ips(valid_ips)
+        ma, nm = ips(match_ips)
+        f = L.GcFilter()
+        f.flags = ((L.GC_REMOVE_EXPIRED if remove_expired else 0) |
+                   (L.GC_VALID_IPS if va is not None else 0) |
+                   (L.GC_MATCH_IPS if ma is not None else 0))
+        f.time = int(time) & 0xFFFFFFFF
+        f.valid_ips = ctypes.cast(va, ctypes.c_void_p) if va is not None else None
+        f.n_valid = nv
+        f.match_ips = ctypes.cast(ma, ctypes.c_void_p) if ma is not None else None
+        f.n_match = nm
+        st = L.GcStats()
+        L.check(self.L.cfc_ct_gc(self.h, int(fd), ctypes.byref(f), ctypes.byref(st),
+                                 self._stream(stream)), "ct gc")
+        return {k: getattr(st, k) for k, _ in L.GcStats._fields_}
+
     def counters_sync(self, stream=None):
         L.check(self.L.cfc_counters_sync(self.h, self._stream(stream)),
                 "counters sync")

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 7
+#define CFC_ABI_VERSION 8
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -358,6 +358,54 @@ int cfc_ct_apply_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
 int cfc_ct_apply_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
+
+/* Conntrack garbage collection: ctmap.GC(m, filter) (pkg/maps/ctmap/
+ * ctmap.go:339-350) with doFiltering (:303-325) on one CT map (`fd`), or on
+ * every CT map (fd = -1: what EnableConntrackGC's loop covers,
+ * pkg/endpointmanager/conntrack.go:96-125, every
+ * conntrack-garbage-collector-interval, 60 s by default,
+ * daemon/main.go:367).  struct GCFilter (ctmap.go:163-182): */
+#define CFC_GC_REMOVE_EXPIRED 1u   /* RemoveExpired: delete lifetime < time */
+#define CFC_GC_VALID_IPS 2u        /* ValidIPs set: delete when neither tuple
+                                      address is in valid_ips (empty set: all) */
+#define CFC_GC_MATCH_IPS 4u        /* MatchIPs set: delete when either is in
+                                      match_ips */
+typedef struct {
+    uint8_t family;                /* 4 or 6 */
+    uint8_t pad[3];
+    uint8_t addr[16];              /* network order; IPv4: the first 4 bytes */
+} cfc_ip;
+typedef struct {
+    uint32_t flags;                /* CFC_GC_* */
+    uint32_t time;                 /* Time, bpf_ktime_get_sec() seconds
+                                      (ctmap.GC fills it from bpf.GetMtime) */
+    const cfc_ip *valid_ips;
+    uint32_t n_valid;
+    uint32_t pad0;
+    const cfc_ip *match_ips;
+    uint32_t n_match;
+    uint32_t pad1;
+} cfc_ct_gc_filter;
+/* gcStats (ctmap.go doGC4/doGC6): entries deleted and left in the selected
+ * maps; where the work happened */
+typedef struct {
+    uint64_t deleted;
+    uint64_t alive;
+    uint64_t device_deleted;       /* IPv4 entries in the device table */
+    uint64_t log_deleted;          /* ICMP entries of device creates in TCP
+                                      maps not yet in the host mirror */
+    uint64_t host_deleted;         /* entries only the host holds (IPv6, and
+                                      IPv4 TCP maps' ICMP entries) */
+    uint64_t slots_freed;          /* device slots returned to free (the rest
+                                      of the deletes stay tombstones) */
+} cfc_ct_gc_stats;
+/* The IPv4 part runs on the device (one pass over the CT table: deleted
+ * entries become tombstones at once, a cluster's trailing tombstones become
+ * free slots; the host mirror takes the deletes lazily, like the applies'
+ * changes).  Commits pending host-side map changes first.  Synchronises
+ * `stream`. */
+int cfc_ct_gc(cfc_ctx *ctx, int fd, const cfc_ct_gc_filter *filter,
+              cfc_ct_gc_stats *stats, void *stream);
 
 /* ------------------------------------------------------ drop notifications */
 /* struct drop_notify (bpf/lib/drop.h:40-48, NOTIFY_COMMON_HDR common.h:217)

@@ -2055,6 +2055,55 @@ static int cmp_ctrow(const void *a, const void *b)
     return memcmp(a, b, CTK);
 }
 
+/* an address in a GCFilter IP set: records of 17 bytes {family 1|2,
+ * address[16]} (IPv4: the first 4 bytes) */
+static int gc_ip_in(const uint8_t *set, size_t n, int fam, const uint8_t *a)
+{
+    const size_t al = fam == 1 ? 4 : 16;
+    for (size_t i = 0; i < n; i++)
+        if (set[17 * i] == fam && !memcmp(set + 17 * i + 1, a, al))
+            return 1;
+    return 0;
+}
+
+/* ctmap.GC (pkg/maps/ctmap/ctmap.go:339-350) on the maps selected by
+ * family (0 any, 1, 2), owner (-1 any, 0 global, lxc_id + 1) and kind
+ * (-1 any, 0 TCP, 1 ANY): doFiltering (:303-325) on every live entry —
+ * RemoveExpired: lifetime < time; ValidIPs (n_valid != SIZE_MAX): neither
+ * tuple address in the set; MatchIPs (n_match != SIZE_MAX): either is.
+ * Returns the entries deleted. */
+size_t cfo_ct_gc(cfo_t *o, int family, int owner, int kind, int remove_expired,
+                 uint32_t time, const uint8_t *valid, size_t n_valid,
+                 const uint8_t *match, size_t n_match)
+{
+    size_t del = 0;
+    for (uint32_t s = 0; s < o->ct.cap; s++) {
+        if (!o->ct.used[s])
+            continue;
+        const uint32_t idx = o->ct.vals[s];
+        if (!o->ct_live[idx])
+            continue;
+        const uint8_t *k = o->ct.keys + (size_t)s * CTK;
+        uint16_t ow;
+        memcpy(&ow, k, 2);
+        if ((family && k[3] != family) || (owner >= 0 && ow != owner) ||
+            (kind >= 0 && k[2] != kind))
+            continue;
+        const int fam = k[3], al = fam == 1 ? 4 : 16;
+        const uint8_t *da = k + 4, *sa = k + 4 + al;
+        int d = remove_expired && o->ct_ents[idx].lifetime < time;
+        if (!d && n_valid != (size_t)-1)
+            d = !gc_ip_in(valid, n_valid, fam, da) && !gc_ip_in(valid, n_valid, fam, sa);
+        if (!d && n_match != (size_t)-1)
+            d = gc_ip_in(match, n_match, fam, da) || gc_ip_in(match, n_match, fam, sa);
+        if (d) {
+            o->ct_live[idx] = 0;
+            del++;
+        }
+    }
+    return del;
+}
+
 size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap)
 {
     size_t n = 0;

@@ -150,6 +150,12 @@ uint32_t cfo_flow_hash4(uint32_t sa, uint32_t da, uint16_t sport, uint16_t dport
                         uint8_t proto);
 #define CFO_CT_ROW 104
 size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap);
+/* ctmap.GC with doFiltering (pkg/maps/ctmap/ctmap.go:303-350) on the
+ * selected maps (family 0/1/2, owner -1/0/lxc_id + 1, kind -1/0 TCP/1 ANY);
+ * IP sets are 17-byte {family, address[16]} records, n = SIZE_MAX: no set */
+size_t cfo_ct_gc(cfo_t *o, int family, int owner, int kind, int remove_expired,
+                 uint32_t time, const uint8_t *valid, size_t n_valid,
+                 const uint8_t *match, size_t n_match);
 
 #ifdef __cplusplus
 }

@@ -133,6 +133,9 @@ def lib():
         L.cfo_set_lb_io.restype = None
         L.cfo_ipcache_lookup.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp]
         L.cfo_ipcache_lookup.restype = None
+        L.cfo_ct_gc.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_uint32, vp, ctypes.c_size_t, vp, ctypes.c_size_t]
+        L.cfo_ct_gc.restype = ctypes.c_size_t
         _lib = L
     return _lib
 
@@ -383,6 +386,25 @@ class Oracle:
         hit = np.zeros(n, np.uint8)
         self.L.cfo_ipcache_lookup(self.h, 1 if family == 4 else 2, n, _p(a), _p(lab), _p(hit))
         return lab, hit
+
+    def ct_gc(self, time=None, remove_expired=True, valid=None, match=None,
+              family=0, owner=-1, kind=-1):
+        """ctmap.GC + doFiltering (pkg/maps/ctmap/ctmap.go:303-350) -> entries
+        deleted.  valid / match: lists of (family 4|6, address bytes), None:
+        no such set (an empty list is an empty set)."""
+        def ips(lst):
+            if lst is None:
+                return None, ctypes.c_size_t(-1).value
+            a = np.zeros((max(len(lst), 1), 17), np.uint8)
+            for i, (f, b) in enumerate(lst):
+                a[i, 0] = 1 if f == 4 else 2
+                a[i, 1:1 + len(b)] = np.frombuffer(bytes(b), np.uint8)
+            return a, len(lst)
+        va, nv = ips(valid)
+        ma, nm = ips(match)
+        self._gc_keep = (va, ma)
+        return int(self.L.cfo_ct_gc(self.h, family, owner, kind, int(bool(remove_expired)),
+                                    int(time or 0) & 0xFFFFFFFF, _p(va), nv, _p(ma), nm))
 
     def ct_dump(self):
         """(n, CT_ROW) u8 rows: owner u16, map u8, family u8, tuple[40],

@@ -109,3 +109,44 @@ def test_new_flow_twice_in_one_batch():
     assert len(flow) == 1
     pk = flow["entry"][0].view("<u8")
     assert pk[0] == 2 and pk[1] == 200      # rx: created + counted once more
+
+
+def test_oracle_gc_filtering():
+    """cfo_ct_gc restates doFiltering (pkg/maps/ctmap/ctmap.go:303-325):
+    checked against the rule written out on the dump rows of a reference
+    fixture's CT state — RemoveExpired (lifetime < Time), ValidIPs (neither
+    address in the set), MatchIPs (either address in it), per-map
+    selection."""
+    import golden_io as G
+    for name in ("ct_ingress_v4", "ct_egress_v6"):
+        g = G.Golden(name)
+        rows0 = O.Oracle(g.tables).ct_dump()
+        al = 4 if rows0[0, 3] == 1 else 16
+        life = rows0[:, 44 + 32:44 + 36].copy().view("<u4").ravel()
+        da, sa = rows0[:, 4:4 + al], rows0[:, 4 + al:4 + 2 * al]
+        t = int(np.median(life))
+        o = O.Oracle(g.tables)
+        assert o.ct_gc(time=t) == int((life < t).sum())
+        np.testing.assert_array_equal(o.ct_dump(), rows0[life >= t])
+        # MatchIPs: either address; ValidIPs: neither address
+        pick = [bytes(x) for x in np.unique(da, axis=0)[:3]]
+        inset = lambda a, s: np.array([bytes(x) in s for x in a])   # noqa: E731
+        fam = 4 if al == 4 else 6
+        o = O.Oracle(g.tables)
+        o.ct_gc(remove_expired=False, match=[(fam, b) for b in pick])
+        keep = ~(inset(da, pick) | inset(sa, pick))
+        np.testing.assert_array_equal(o.ct_dump(), rows0[keep])
+        o = O.Oracle(g.tables)
+        o.ct_gc(remove_expired=False, valid=[(fam, b) for b in pick])
+        keep = inset(da, pick) | inset(sa, pick)
+        np.testing.assert_array_equal(o.ct_dump(), rows0[keep])
+        # an empty ValidIPs set (the initial scan with no endpoint) clears all
+        o = O.Oracle(g.tables)
+        assert o.ct_gc(remove_expired=False, valid=[]) == len(rows0)
+        # one map only: the TCP map of the first owner in the dump
+        o = O.Oracle(g.tables)
+        ow = int(rows0[0, 0]) | int(rows0[0, 1]) << 8
+        sel = (rows0[:, 0].astype(int) | rows0[:, 1].astype(int) << 8) == ow
+        sel &= rows0[:, 2] == 0
+        o.ct_gc(time=0xFFFFFFFF, owner=ow, kind=0)
+        np.testing.assert_array_equal(o.ct_dump(), rows0[~sel])
