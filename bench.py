@@ -366,24 +366,41 @@ def main():
     if n6:
         kernels.append(("k_classify_v6", n6, kern6_ms, ws6))
     rows = ubench_ceilings()
+    # L2 hits at the L2 ceiling; misses (TCC_MISS: the header stream, the
+    # output stores, and table lines past L2) at the row of the memory that
+    # serves them: the Infinity-Cache row of a kernel whose tables outgrow
+    # L2, else the HBM row (the largest table measured)
+    l2_peak = ceiling_for(1, rows)[1]
+    hbm_row = rows[-1]
     pe = pmc_entry(args.workload, args.mode, layout, [(k, hn) for k, hn, _, _ in kernels])
     per_kernel = []
-    req_tot = ideal_s = traffic = 0.0
+    req_tot = ideal_s = ideal_u = traffic = 0.0
     for k, hn, ms, ws in kernels:
         mib, peak_k = ceiling_for(ws, rows)
+        miss_mib, miss_peak = (mib, peak_k) if ws > 6 * (1 << 20) else hbm_row
         d = {"kernel": k, "headers": hn, "ms_per_launch": round(ms, 4),
              "working_set_mib": round(ws / (1 << 20), 2),
              "ceiling_table_mib": mib, "ceiling_greq_s": peak_k}
         if pe:
             pk = pe["kernels"][k]
             req = pk["l2_requests_per_launch"]
+            hits, miss = pk.get("l2_hits_per_launch"), pk.get("l2_misses_per_launch")
+            if hits is None or miss is None:
+                hits, miss = req, 0.0
+            t_ideal = hits / (l2_peak * 1e9) + miss / (miss_peak * 1e9)
+            t_unif = req / (peak_k * 1e9)
             d.update({"l2_requests_per_launch": req,
                       "l2_requests_per_header": round(req / hn, 3),
+                      "l2_hits_per_launch": hits, "l2_misses_per_launch": miss,
+                      "hit_ceiling_greq_s": l2_peak,
+                      "miss_ceiling_greq_s": miss_peak, "miss_ceiling_table_mib": miss_mib,
                       "achieved_greq_s": round(req / (ms * 1e-3) / 1e9, 1),
-                      "frac": round(req / (ms * 1e-3) / 1e9 / peak_k, 4),
+                      "frac": round(t_ideal / (ms * 1e-3), 4),
+                      "frac_uniform": round(t_unif / (ms * 1e-3), 4),
                       "hbm_bytes_per_launch": pk["hbm_bytes_per_launch"]})
             req_tot += req
-            ideal_s += req / (peak_k * 1e9)
+            ideal_s += t_ideal
+            ideal_u += t_unif
             traffic += pk["hbm_bytes_per_launch"]
         per_kernel.append(d)
     stream_b = n * STREAM_V4 + n6 * STREAM_V6
@@ -436,6 +453,9 @@ def main():
             "peak": round(req_tot / ideal_s / 1e9, 1) if pe else None,
             "unit": "Greq/s",
             "frac": round(ideal_s / (kern_ms * 1e-3), 4) if pe else None,
+            # every request at the ceiling row of its kernel's working set
+            # (round 2's model: it overprices IC-resident tables' L2 hits)
+            "frac_uniform": round(ideal_u / (kern_ms * 1e-3), 4) if pe else None,
             "traffic": traffic if pe else None,
             "pmc_source": pe["source"] if pe else None,
             "kernels": per_kernel,

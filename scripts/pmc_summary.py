@@ -104,6 +104,8 @@ def record(res, workload, mode, layout, specs, source):
             "headers": int(n),
             "stream_read_bytes_per_header": float(sb),
             "l2_requests_per_launch": c["TCC_REQ_sum"],
+            "l2_hits_per_launch": c.get("TCC_HIT_sum"),
+            "l2_misses_per_launch": c.get("TCC_MISS_sum"),
             "hbm_bytes_per_launch": (c["FETCH_SIZE"] * 1024 + 0.5 * int(n) * float(sb)
                                      + c["WRITE_SIZE"] * 1024),
             "avg_ms": res["kernels"][k]["avg_ms"],
