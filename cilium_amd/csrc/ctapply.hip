@@ -782,7 +782,8 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
         ac[2] = acct[2];
         ac[3] = acct[3];
         inf.sec = sec;
-        inf.y = (inf.y & ~0xFFFFu) | CTI_CREATED | (deleted ? CTI_DELETED : 0u);
+        inf.y = (inf.y & ~0xFFFFu) | CTI_CREATED | (deleted ? CTI_DELETED : 0u) |
+                (was_fresh ? CTI_FRESH : 0u) | (inf.y & CTI_FRESH);
     } else {
         store_state(A.tm, slot, e);
         ac[0] += acct[0];
@@ -957,9 +958,9 @@ __device__ __forceinline__ int gc_map(const uint32_t *smaps, uint32_t n, uint32_
     return -1;
 }
 
-// One thread per slot (grid-stride).  A deleted entry the host mirror holds
-// (no CTI_CREATED: created before the host's last sync) is logged for it;
-// one the host never saw is just dropped.  Either way the slot becomes a
+// One thread per slot (grid-stride).  A deleted entry the host mirror may
+// hold is logged for it; one a device insert brought in since the last sync
+// (CTI_FRESH) is just dropped.  Either way the slot becomes a
 // plain tombstone with no dirty bits and zero accounting.
 __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
 {
@@ -986,7 +987,9 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
                 del = j >= 0 && gc_delete(A, k.x, k.y, A.tm[s].lifetime);
                 live += j >= 0 && !del;
                 if (del) {
-                    logit = !(A.info[s].y & CTI_CREATED);
+                    // only a key a device insert brought in since the last
+                    // sync is unknown to the host
+                    logit = !(A.info[s].y & CTI_FRESH);
                     fresh += !logit;
                 }
             }

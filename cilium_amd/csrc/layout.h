@@ -314,6 +314,10 @@ struct CtInfo {
     uint32_t y;          // rev_nat_index | dirty << 16
 };
 constexpr uint32_t CTI_UPDATED = 1u << 16, CTI_CREATED = 2u << 16, CTI_DELETED = 4u << 16;
+// the slot was claimed by a device insert since the host's last sync: its
+// key is new to the table (CTI_CREATED alone may be an overwrite, e.g. a
+// related ICMP entry written again, of a key the host holds)
+constexpr uint32_t CTI_FRESH = 8u << 16;
 // a slot being filled by a device insert (never matched, never free)
 constexpr uint32_t CT_CLAIM = 0xE000u;
 struct alignas(16) Ct6Slot {

@@ -393,7 +393,9 @@ typedef struct {
     uint64_t alive;
     uint64_t device_deleted;       /* IPv4 entries in the device table */
     uint64_t log_deleted;          /* ICMP entries of device creates in TCP
-                                      maps not yet in the host mirror */
+                                      maps not yet in the host mirror (one
+                                      per pending write: a key written twice
+                                      before the host took it counts twice) */
     uint64_t host_deleted;         /* entries only the host holds (IPv6, and
                                       IPv4 TCP maps' ICMP entries) */
     uint64_t slots_freed;          /* device slots returned to free (the rest
