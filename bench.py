@@ -291,6 +291,9 @@ def main():
         dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         wall = float(tw.item())
     if world == 1:
+        if args.ct_apply:   # (the host mirror takes the device's CT changes)
+            log(f"[rank {rank}] timed steps done in {wall:.2f} s; folding counters "
+                f"and the CT maps into the host mirror")
         dp.counters_sync()
     total = (n + n6) * world * args.steps
     mpps = total / wall / 1e6

@@ -125,6 +125,7 @@ struct GCt {           // conntrack
     DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
     DevBuf ct4_lb;                        // per-slot LB state (with a load balancer)
     DevBuf ct4_info, ct4_mark, ct4_sum;   // device CT apply state (ctapply.hip)
+    DevBuf ct6_info, ct6_mark, ct6_sum;
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
     std::vector<Ct6Slot> ct6_host;
     std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
@@ -203,12 +204,17 @@ struct cfc_ctx {
         bool valid = false;
         const void *ct = nullptr, *saddr = nullptr;
         uint64_t n = 0, gen = 0;
-        int mode = 0;
+        int mode = 0, family = 4;
         uint16_t ep = 0;
         size_t k1 = 0, k2 = 0;   // byte offsets in ws; k2 = 0: no stage 2
     } last_cls;
     uint64_t log_used = 0;       // CtLog entries since the last sync
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
+    // the IPv6 table's device applies: creates the host lacks, inserts
+    // since the last sync, CtLog6 entries
+    uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
+    DevBuf cta_log6;
+    bool ct6_dirty = false;      // an IPv6 device apply since the last sync
 
     // counters: [n_ctr][2] u64 then metrics
     uint64_t *ctr = nullptr;
@@ -333,6 +339,142 @@ void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
         memcpy(&v[38], &rev, 2);
         memcpy(&v[44], &r.info.sec, 4);
     }
+}
+
+// The IPv6 table's part of ct_sync: its dirty slots, then its TCP maps'
+// ICMPv6 entries (CtLog6).
+int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
+{
+    GCt &G = *E.ct;
+    const uint64_t slots = G.ct6_host.size();
+    uint32_t *cnt = (uint32_t *)c->cta_cnt.p;
+    std::vector<CtSyncRec6> rec;
+    if (slots && G.ct6_info.p) {
+        Ct6Slot *ct6 = (Ct6Slot *)G.ct6.p;
+        CtTimer *tm = (CtTimer *)G.ct6_tm.p;
+        CtInfo *info = (CtInfo *)G.ct6_info.p;
+        uint32_t n = 0;
+        if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+            cta_collect6(ct6, tm, info, slots, nullptr, 0, cnt, s) ||
+            hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        rec.resize(n);
+        if (n) {
+            if (c->cta_sync.ensure(sizeof(CtSyncRec6) * n))
+                return -ENOMEM;
+            CtSyncRec6 *dr = (CtSyncRec6 *)c->cta_sync.p;
+            uint32_t n2 = 0;
+            if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+                cta_collect6(ct6, tm, info, slots, dr, n, cnt, s) ||
+                hipMemcpyAsync(rec.data(), dr, sizeof(CtSyncRec6) * n, hipMemcpyDeviceToHost,
+                               s) != hipSuccess ||
+                hipMemcpyAsync(&n2, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                cta_tomb6(ct6, dr, n, s) || hipStreamSynchronize(s) != hipSuccess || n2 != n)
+                return -EIO;
+        }
+    }
+    std::string key;
+    // deletes first (an entry deleted and created again lives in another
+    // slot), then creates and updates
+    for (int pass = 0; pass < 2; pass++) {
+        for (const CtSyncRec6 &r : rec) {
+            const bool del = (r.w & CT_TOMBSTONE) == CT_TOMBSTONE;
+            if (del != (pass == 0))
+                continue;
+            const uint32_t w = r.w & ~CT_TOMBSTONE;
+            Ct6Slot &h = G.ct6_host[r.slot];
+            const bool prev_live = h.w != 0 && h.w != CT_TOMBSTONE;
+            Map *m = ct_slot_key(E, 6, r.d, r.s, r.z, w, &key);
+            if (del) {
+                if (m)
+                    m->erase_raw(key);
+                if (prev_live) {
+                    G.n_ct6--;
+                    G.tomb6++;
+                } else if (h.w == 0) {
+                    G.tomb6++;
+                }
+                h = Ct6Slot{};
+                h.w = CT_TOMBSTONE;
+            } else if (r.info.y & CTI_CREATED) {
+                if (m) {
+                    CtSyncRec r4{};
+                    r4.info = r.info;
+                    r4.last_rx = r.last_rx;
+                    r4.last_tx = r.last_tx;
+                    r4.flags = r.flags;
+                    r4.lifetime = r.lifetime;
+                    std::string v(m->value_bytes(), '\0');
+                    ct_value_from_dev(v, r4, true);
+                    m->put_raw(key, v);
+                }
+                if (!prev_live) {
+                    G.n_ct6++;
+                    if (h.w == CT_TOMBSTONE)
+                        G.tomb6--;
+                }
+                memcpy(h.d, r.d, 16);
+                memcpy(h.s, r.s, 16);
+                h.z = r.z;
+                h.w = w;
+            } else if (m) {
+                auto it = m->kv.find(key);
+                if (it != m->kv.end() && it->second.val.size() >= 56) {
+                    CtSyncRec r4{};
+                    r4.info = r.info;
+                    r4.last_rx = r.last_rx;
+                    r4.last_tx = r.last_tx;
+                    r4.flags = r.flags;
+                    r4.lifetime = r.lifetime;
+                    ct_value_from_dev(it->second.val, r4, false);
+                }
+            }
+        }
+    }
+    if (c->log6_used) {
+        std::vector<CtLog6> lg(c->log6_used);
+        if (hipMemcpyAsync(lg.data(), c->cta_log6.p, sizeof(CtLog6) * lg.size(),
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        std::sort(lg.begin(), lg.end(), [](const CtLog6 &a, const CtLog6 &b) {
+            return a.seq != b.seq ? a.seq < b.seq : a.order < b.order;
+        });
+        for (const CtLog6 &g : lg) {
+            // ct_create6's second write into the TCP map (conntrack.h:648-660)
+            auto it = G.ct_maps.find(ct_map_key(6, g.w & ~0x7FFu, 0));
+            if (it == G.ct_maps.end())
+                continue;
+            char k[38];
+            const uint32_t z = 0;
+            memcpy(k, &g.x, 16);
+            memcpy(k + 16, &g.y, 16);
+            memcpy(k + 32, &z, 4);
+            k[36] = (char)(g.w & 0xFF);
+            k[37] = (char)((g.w >> 8) & 7);
+            std::string v(it->second->value_bytes(), '\0');
+            const uint32_t dir = g.dirlen >> 31;
+            const uint64_t one = 1, len = g.dirlen & 0x7FFFFFFFu;
+            memcpy(&v[dir ? 0 : 16], &one, 8);
+            memcpy(&v[dir ? 8 : 24], &len, 8);
+            const uint32_t life = g.now + 60, last = 5u < g.now ? g.now : 0u;
+            const uint16_t bits = 16;   // seen_non_syn: "for ICMP, there is no SYN"
+            const uint16_t rev = (uint16_t)g.rev;
+            memcpy(&v[32], &life, 4);
+            memcpy(&v[36], &bits, 2);
+            memcpy(&v[38], &rev, 2);
+            memcpy(&v[44], &g.sec, 4);
+            memcpy(&v[dir ? 52 : 48], &last, 4);
+            it->second->put_raw(std::string(k, 38), v);
+        }
+    }
+    c->log6_used = 0;
+    c->cta_claims6 = 0;
+    c->cta_ins6 = 0;
+    c->ct6_dirty = false;
+    E.st.ct6_entries = G.n_ct6;
+    return 0;
 }
 
 // The device CT apply's changes into the host mirror of the CT maps: the
@@ -479,8 +621,10 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
     c->cta_claims = 0;
     c->cta_ins = 0;
     c->ct_used_valid = false;
-    c->ct_dirty = false;
     E.st.ct4_entries = G.n_ct4;
+    if (int rc = ct_sync6(c, E, s))
+        return rc;
+    c->ct_dirty = false;
     return 0;
 }
 
@@ -788,9 +932,12 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     const size_t nslots = img.ct4.size() + img.ct6.size();
     if (nslots && (*rc = g->ct_acct.zeros(32 * nslots, s)))
         return nullptr;
-    const size_t n4 = img.ct4.size();
+    const size_t n4 = img.ct4.size(), n6 = img.ct6.size();
     if (n4 && ((*rc = g->ct4_info.zeros(sizeof(CtInfo) * n4, s)) ||
                (*rc = g->ct4_mark.zeros(4 * n4, s)) || (*rc = g->ct4_sum.zeros(4 * n4, s))))
+        return nullptr;
+    if (n6 && ((*rc = g->ct6_info.zeros(sizeof(CtInfo) * n6, s)) ||
+               (*rc = g->ct6_mark.zeros(4 * n6, s)) || (*rc = g->ct6_sum.zeros(4 * n6, s))))
         return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
@@ -805,7 +952,7 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     g->n_ct4 = img.n_ct4;
     g->n_ct6 = img.n_ct6;
     g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
-               48ull * nslots + 16ull * n4 + 16ull * img.ct4_lb.size();
+               48ull * nslots + 16ull * (n4 + n6) + 16ull * img.ct4_lb.size();
     g->ct4_host = std::move(img.ct4);
     g->ct6_host = std::move(img.ct6);
     return g;
@@ -857,7 +1004,7 @@ void assemble(Epoch &E)
     // the device CT apply inserts in place: lookups walk to a free slot
     T.ct4_probe = C.ct4_mask;
     T.ct6_mask = C.ct6_mask;
-    T.ct6_probe = C.ct6_probe;
+    T.ct6_probe = C.ct6_mask;
     T.ct6_acct_base = (uint32_t)C.ct4_host.size();
     T.lb4 = B.n_lb4 ? (const uint4 *)B.lb4.p : nullptr;
     T.lb4_mask = B.lb4_mask;
@@ -967,7 +1114,6 @@ unsigned patch_touched(cfc_ctx *c, unsigned groups, hipStream_t s)
             groups |= GROUP_CT;
         } else {
             const GCt &G = *E.ct;
-            E.T.ct6_probe = G.ct6_probe;
             E.st.ct4_entries = G.n_ct4;
             E.st.ct6_entries = G.n_ct6;
         }
@@ -1716,9 +1862,10 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     c->last_stream = s;
     note_stream(c, s);
     c->ctr_pending = true;
-    if (std::is_same<Hdr, cfc_hdr_v4>::value && out->ct && in->n && wl.ct) {
+    if (out->ct && in->n && wl.ct) {
         auto &L = c->last_cls;
         L.valid = true;
+        L.family = std::is_same<Hdr, cfc_hdr_v4>::value ? 4 : 6;
         L.ct = out->ct;
         L.saddr = in->saddr;
         L.n = in->n;
@@ -2328,14 +2475,16 @@ void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t 
         (void)hipMemsetAsync((char *)c->epoch->ct->ct_acct.p + 32 * slot, 0, 32, s);
 }
 
-// cfc_ct_apply_v4 on the device (ctapply.hip).  1: take the host path
+// cfc_ct_apply_v4/v6 on the device (ctapply.hip).  1: take the host path
 // instead (nothing changed), 0 done, <0 error.
-int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
-                 uint16_t ep_lxc, hipStream_t s)
+template <class Hdr>
+int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16_t ep_lxc,
+                 hipStream_t s)
 {
+    constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
         return 1;
-    if (LbHost(c).on())   // service entries and reverse NAT: the host walk
+    if (!V6 && LbHost(c).on())   // service entries and reverse NAT: the host walk
         return 1;
     // the device table must be the maps as committed: no host-side CT
     // change waiting for a commit
@@ -2352,8 +2501,8 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     }
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
-    const uint64_t n = in->n, slots = G.ct4_host.size();
-    if (!slots || !G.ct4_info.p || n >= (1ull << 29))
+    const uint64_t n = in->n, slots = V6 ? G.ct6_host.size() : G.ct4_host.size();
+    if (!slots || !(V6 ? G.ct6_info.p : G.ct4_info.p) || n >= (1ull << 29))
         return 1;
     // the batch's classify (its CT bytes, verdicts and the workspace's hit
     // slots) may have run on another stream
@@ -2370,8 +2519,8 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
         return -ENOMEM;
     CtaArgs A{};
     A.T = E.T;
-    A.sa = in->saddr;
-    A.da = in->daddr;
+    A.sa = (const uint32_t *)in->saddr;
+    A.da = (const uint32_t *)in->daddr;
     A.pt = in->ports;
     A.mt = in->meta;
     A.tf = in->tcp_flags;
@@ -2384,11 +2533,23 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     A.ep_sec = c->seclabel[ep_lxc];
     A.now = c->now;
     A.seq = c->cta_seq;
-    A.ct4 = (Ct4Slot *)G.ct4.p;
-    A.tm = (CtTimer *)G.ct4_tm.p;
-    A.info = (CtInfo *)G.ct4_info.p;
-    A.mark = (uint32_t *)G.ct4_mark.p;
-    A.sum = (uint32_t *)G.ct4_sum.p;
+    if (V6) {
+        A.ct6 = (Ct6Slot *)G.ct6.p;
+        A.mask = G.ct6_mask;
+        A.acct_base = E.T.ct6_acct_base;
+        A.tm = (CtTimer *)G.ct6_tm.p;
+        A.info = (CtInfo *)G.ct6_info.p;
+        A.mark = (uint32_t *)G.ct6_mark.p;
+        A.sum = (uint32_t *)G.ct6_sum.p;
+    } else {
+        A.ct4 = (Ct4Slot *)G.ct4.p;
+        A.mask = G.ct4_mask;
+        A.acct_base = 0;
+        A.tm = (CtTimer *)G.ct4_tm.p;
+        A.info = (CtInfo *)G.ct4_info.p;
+        A.mark = (uint32_t *)G.ct4_mark.p;
+        A.sum = (uint32_t *)G.ct4_sum.p;
+    }
     A.hs = (uint32_t *)c->cta_hs.p;
     A.reqA = (uint64_t *)c->cta_req.p;
     A.req_cap = (uint32_t)std::min<uint64_t>(2 * n, 0xFFFFFFFFu);
@@ -2397,28 +2558,32 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     A.slot_bits = sb;
     {   // this batch's hit slots from its classify launch, if still there
         const auto &L = c->last_cls;
-        if (L.valid && L.gen == c->ct_gen && L.ct == out->ct && L.saddr == in->saddr &&
-            L.n == n && L.mode == mode && L.ep == ep_lxc) {
+        if (L.valid && L.family == (V6 ? 6 : 4) && L.gen == c->ct_gen && L.ct == out->ct &&
+            L.saddr == (const void *)in->saddr && L.n == n && L.mode == mode && L.ep == ep_lxc) {
             A.ck1 = (const uint32_t *)((const char *)c->ws + L.k1);
             A.ck2 = L.k2 ? (const uint32_t *)((const char *)c->ws + L.k2) : nullptr;
         }
     }
     uint32_t hc[CTA_NCNT];
-    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess || cta_scan(A, s) ||
+    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess || cta_scan(A, V6, s) ||
         hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     const uint64_t nreqA = hc[CTA_NREQA], nhit = hc[CTA_NHIT];
     // room for every create and its ICMP entry: the table below 3/4 load,
     // each CT map below max_entries; else the host path (which rebuilds)
-    const uint64_t used = c->ct_used_valid ? c->ct_used : G.n_ct4 + G.tomb4;
-    bool ok = 4 * (used + c->cta_ins + 2 * nreqA) <= 3 * slots &&
-              nreqA <= A.req_cap;
+    uint64_t &claims = V6 ? c->cta_claims6 : c->cta_claims;
+    uint64_t &ins = V6 ? c->cta_ins6 : c->cta_ins;
+    uint64_t &log_used = V6 ? c->log6_used : c->log_used;
+    DevBuf &logbuf = V6 ? c->cta_log6 : c->cta_log;
+    const size_t log_rec = V6 ? sizeof(CtLog6) : sizeof(CtLog);
+    const uint64_t used = V6 ? (uint64_t)G.n_ct6 + G.tomb6
+                             : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
+    bool ok = 4 * (used + ins + 2 * nreqA) <= 3 * slots && nreqA <= A.req_cap;
     for (auto &kv : c->maps) {
         const Map *m = kv.second.get();
-        if (m->role == ROLE_CT4 &&
-            m->kv.size() - m->gc_pending + c->cta_claims + c->log_used + 2 * nreqA >
-                m->max_entries)
+        if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
+            m->kv.size() - m->gc_pending + claims + log_used + 2 * nreqA > m->max_entries)
             ok = false;
     }
     if (!ok) {   // the scan's marks (and delete orders) go
@@ -2430,22 +2595,22 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     }
     const uint64_t nr = std::max<uint64_t>(nreqA, 1);
     const uint64_t cx_cap = nhit + 2 * nreqA + 64;
-    const uint64_t log_need = c->log_used + nreqA;
+    const uint64_t log_need = log_used + nreqA;
     if (cx_cap > 0xFFFFFFFFu)
         return 1;
     if (c->cta_req2.ensure(24 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
         c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)std::max<uint64_t>(cx_cap, nr))))
         return -ENOMEM;
-    if (c->cta_log.bytes < sizeof(CtLog) * log_need) {   // grow, keeping the entries
+    if (logbuf.bytes < log_rec * log_need) {   // grow, keeping the entries
         DevBuf nl;
-        if (nl.ensure(sizeof(CtLog) * std::max<uint64_t>(2 * log_need, 1 << 16)))
+        if (nl.ensure(log_rec * std::max<uint64_t>(2 * log_need, 1 << 16)))
             return -ENOMEM;
-        if (c->log_used && (hipMemcpyAsync(nl.p, c->cta_log.p, sizeof(CtLog) * c->log_used,
-                                           hipMemcpyDeviceToDevice, s) != hipSuccess ||
-                            hipStreamSynchronize(s) != hipSuccess))
+        if (log_used && (hipMemcpyAsync(nl.p, logbuf.p, log_rec * log_used,
+                                        hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                         hipStreamSynchronize(s) != hipSuccess))
             return -EIO;
-        std::swap(nl.p, c->cta_log.p);
-        std::swap(nl.bytes, c->cta_log.bytes);
+        std::swap(nl.p, logbuf.p);
+        std::swap(nl.bytes, logbuf.bytes);
     }
     uint64_t *r2 = (uint64_t *)c->cta_req2.p, *cx = (uint64_t *)c->cta_cx.p;
     A.reqA2 = r2;
@@ -2455,14 +2620,16 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
     A.cx = cx;
     A.cx2 = cx + cx_cap;
     A.cx_cap = (uint32_t)cx_cap;
-    A.log = (CtLog *)c->cta_log.p;
-    A.log_base = (uint32_t)c->log_used;
-    A.log_cap = (uint32_t)(c->cta_log.bytes / sizeof(CtLog) - c->log_used);
+    A.log = V6 ? nullptr : (CtLog *)logbuf.p;
+    A.log6 = V6 ? (CtLog6 *)logbuf.p : nullptr;
+    A.log_base = (uint32_t)log_used;
+    A.log_cap = (uint32_t)(logbuf.bytes / log_rec - log_used);
     A.sort_tmp = c->cta_tmp.p;
     A.sort_tmp_bytes = c->cta_tmp.bytes;
     // from here the device table changes: the host mirror lags until ct_sync
     c->ct_dirty = true;
-    int rc = cta_rest(A, (uint32_t)nreqA, hc, s);
+    c->ct6_dirty |= V6;
+    int rc = cta_rest(A, V6, (uint32_t)nreqA, hc, s);
     if (!rc && hipStreamSynchronize(s) != hipSuccess)
         rc = -EIO;
     if (rc) {
@@ -2472,17 +2639,17 @@ int ct_apply_dev(cfc_ctx *c, const cfc_hdr_v4 *in, const cfc_out *out, int mode,
         (void)hipStreamSynchronize(s);
         (void)hipMemsetAsync(A.mark, 0, 4 * slots, s);
         (void)hipMemsetAsync(A.sum, 0, 4 * slots, s);
-        uint32_t claims = 0;
-        (void)hipMemcpyAsync(&claims, A.cnt + CTA_CLAIMS, 4, hipMemcpyDeviceToHost, s);
+        uint32_t cl = 0;
+        (void)hipMemcpyAsync(&cl, A.cnt + CTA_CLAIMS, 4, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);
-        c->cta_claims += claims;
-        c->cta_ins += claims;
+        claims += cl;
+        ins += cl;
         c->built_sig[3] = ~0ull;
         return rc;
     }
-    c->cta_claims += hc[CTA_CLAIMS];
-    c->cta_ins += hc[CTA_CLAIMS];
-    c->log_used += hc[CTA_NLOG];
+    claims += hc[CTA_CLAIMS];
+    ins += hc[CTA_CLAIMS];
+    log_used += hc[CTA_NLOG];
     c->cta_seq++;
     return 0;
 }
@@ -2503,7 +2670,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     if (!n || mode == CFC_MODE_XDP)
         return 0;
     hipStream_t s = (hipStream_t)stream;
-    if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value) {
+    {
         const int rc = ct_apply_dev(c, in, out, mode, ep_lxc, s);
         c->ct_gen++;   // (the table, or the host maps, change from here)
         c->n_apply_dev += rc == 0;
@@ -2940,8 +3107,15 @@ int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, h
     if (dev4)
         if (int rc = ct_gc_dev(c, sel, *f, st, s))
             return rc;
-    // what only the host holds: IPv6 maps (their applies run on the host),
-    // IPv4 maps without a device table, IPv4 TCP maps' ICMP entries
+    // what only the host holds: IPv6 maps (collected on the host, after
+    // their device applies are synchronised), IPv4 maps without a device
+    // table, IPv4 TCP maps' ICMP entries
+    bool v6sel = false;
+    for (Map *m : sel)
+        v6sel |= m->role == ROLE_CT6 && !m->kv.empty();
+    if (v6sel && c->ct6_dirty)
+        if (int rc = ct_sync(c, s))
+            return rc;
     const GcFilterHost H{*f};
     for (Map *m : sel) {
         const bool v6 = m->role == ROLE_CT6, all = v6 || !dev4;

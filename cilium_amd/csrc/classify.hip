@@ -63,6 +63,9 @@
 #ifndef CFC_EXP
 #define CFC_EXP 0   // timing experiments only (1: no LPM, 2: no policy, 3: no key stores)
 #endif
+#ifndef CFC_PIPE
+#define CFC_PIPE 0   // timing experiment: the next header's directory load behind the policy probe
+#endif
 
 namespace cfc {
 
@@ -169,6 +172,9 @@ __device__ __forceinline__ void r1_issue(const cfc_hdr_v4 &in, const LbIn &L, ui
     // for these HBM loads together with the probe before them.  Absent
     // optional arrays read saddr instead and the value is dropped.
     i = i < nloc ? i : nloc - 1;
+#if CFC_EXP == 8   // (timing only: the slice's first 8192 headers again and again, from L2)
+    i &= 8191;
+#endif
     const uint32_t o = i << 2;
     r.sa = ldo_nt(in.saddr, o);
     r.da = ldo_nt(in.daddr, o);
@@ -731,7 +737,21 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #pragma unroll
     for (int u = 0; u < U; u++)
         r1_issue<OPT, LBE>(in, LI, u * BLOCK + threadIdx.x, end, nx[u]);
+#if CFC_PIPE
+    // (timing experiment) the next header's directory load issued behind
+    // this one's policy probe, its headers a full iteration ahead
+    Hdr h[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        r1_take(nx[u], u * BLOCK + threadIdx.x, end, h[u]);
+        r2_issue<MODE>(T, S, h[u]);
+        r1_issue<OPT, LBE>(in, LI, (U + u) * BLOCK + threadIdx.x, end, nx[u]);
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
     for (uint32_t base = 0; base < end; base += BLOCK * U) {
+        const uint32_t nb = base + BLOCK * U;
+#if !CFC_PIPE
         Hdr h[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -739,15 +759,25 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #pragma unroll
         for (int u = 0; u < U; u++)
             r2_issue<MODE>(T, S, h[u]);
+#endif
 #pragma unroll
         for (int u = 0; u < U; u++)
             r3_identity<MODE, CT, LB>(T, S, E, h[u]);
+#if CFC_PIPE
+        Hdr hn[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            r1_take(nx[u], nb + u * BLOCK + threadIdx.x, end, hn[u]);
+            r2_issue<MODE>(T, S, hn[u]);
+            r1_issue<OPT, LBE>(in, LI, nb + (U + u) * BLOCK + threadIdx.x, end, nx[u]);
+        }
+#else
         // the next iteration's headers, behind this one's policy probe (the
         // last iteration re-reads the slice's last header)
-        const uint32_t nb = base + BLOCK * U;
 #pragma unroll
         for (int u = 0; u < U; u++)
             r1_issue<OPT, LBE>(in, LI, nb + u * BLOCK + threadIdx.x, end, nx[u]);
+#endif
 #pragma unroll
         for (int u = 0; u < U; u++)
             r4_verdict<MODE, CT, NT, LB>(T, S, E, h[u]);
@@ -811,6 +841,11 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             acc.flush(s_met);
             iter = 0;
         }
+#if CFC_PIPE
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            h[u] = hn[u];
+#endif
     }
     acc.flush(s_met);
     __syncthreads();

@@ -119,6 +119,12 @@ struct CtLog {
     uint32_t sec;         // src_sec_id
     uint32_t seq, order;  // apply sequence, header order
 };
+// the same for an IPv6 create (ct_create6, conntrack.h:615-662): 16-byte
+// addresses, and the rev_nat_index ipv6_policy sets (bpf_lxc.c:787-788)
+struct CtLog6 {
+    uint4 x, y;           // saddr, daddr (k2 order), raw
+    uint32_t w, now, dirlen, sec, seq, order, rev, pad;
+};
 // one changed slot for the host mirror
 struct CtSyncRec {
     uint32_t slot;
@@ -127,9 +133,17 @@ struct CtSyncRec {
     uint32_t last_rx, last_tx, flags, lifetime;
     uint32_t pad;
 };
+struct CtSyncRec6 {
+    uint32_t slot;
+    CtInfo info;
+    uint32_t d[4], s[4], z, w;
+    uint32_t last_rx, last_tx, flags, lifetime;
+    uint32_t pad;
+};
 enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NCNT = 8 };
 struct CtaArgs {
     DevTables T;
+    // addresses: one word per header (IPv4), four (IPv6, raw network order)
     const uint32_t *sa, *da, *pt, *mt;
     const uint8_t *tf;           // may be null
     const uint8_t *ctb;
@@ -142,7 +156,11 @@ struct CtaArgs {
     uint64_t n;
     int mode;
     uint32_t ep_owner, ep_sec, now, seq;
+    // the family's table (the other is null), its mask, and its first slot
+    // in ct_acct (0 for IPv4, DevTables.ct6_acct_base for IPv6)
     Ct4Slot *ct4;
+    Ct6Slot *ct6;
+    uint32_t mask, acct_base;
     CtTimer *tm;
     CtInfo *info;
     uint32_t *mark;
@@ -151,7 +169,8 @@ struct CtaArgs {
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
     uint32_t req_cap, cx_cap;
     uint32_t cx_base;            // route: its ordered ops start here
-    CtLog *log;
+    CtLog *log;                  // IPv4 applies
+    CtLog6 *log6;                // IPv6 applies
     uint32_t log_base, log_cap;  // entries before this apply, capacity left
     uint32_t *cnt;               // CTA_* counters
     void *sort_tmp;
@@ -159,11 +178,15 @@ struct CtaArgs {
     int ob, slot_bits;           // sort keys: slot << ob | order
 };
 size_t cta_sort_tmp_bytes(uint32_t n);
-int cta_scan(const CtaArgs &A, hipStream_t s);
-int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s);
+// v6: the batch is IPv6 (A.ct6, A.log6)
+int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);
+int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s);
 int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec *out,
                 uint32_t cap, uint32_t *cnt, hipStream_t s);
+int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec6 *out,
+                 uint32_t cap, uint32_t *cnt, hipStream_t s);
 int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
+int cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n, hipStream_t s);
 
 // ---- CT garbage collection (cfc_ct_gc): ctmap.GC's doFiltering
 // (pkg/maps/ctmap/ctmap.go:303-325) over the device CT4 table.  A deleted

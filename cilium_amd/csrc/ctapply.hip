@@ -27,6 +27,7 @@
 // TCP map are not in the device table (no lookup reaches them, flatten.cpp
 // build_ct): they go to a log the host replays in order.
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 
 #include "kern_common.hpp"
 
@@ -118,13 +119,58 @@ __device__ __forceinline__ void wave_add(uint32_t *ctr, uint32_t v)
         atomicAdd(ctr, v);
 }
 
+// ---- the address family.  A CT tuple's addresses are raw (network order,
+// loaded little-endian): one word for IPv4, four for IPv6.  The kernels are
+// templated on V6; the slot layouts are Ct4Slot / Ct6Slot (layout.h).
+template <bool V6>
+using Addr = typename std::conditional<V6, uint4, uint32_t>::type;
+__device__ __forceinline__ bool aeq(uint32_t a, uint32_t b) { return a == b; }
+__device__ __forceinline__ bool aeq(uint4 a, uint4 b)
+{
+    return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+__device__ __forceinline__ uint32_t khash(uint32_t d, uint32_t s, uint32_t z, uint32_t w)
+{
+    return ct_hash4(d, s, z, w);
+}
+__device__ __forceinline__ uint32_t khash(uint4 d, uint4 s, uint32_t z, uint32_t w)
+{
+    const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {s.x, s.y, s.z, s.w};
+    return ct_hash6(dw, sw, z, w);
+}
+template <bool V6>
+__device__ __forceinline__ Addr<V6> ld_addr(const uint32_t *p, uint64_t i)
+{
+    if constexpr (V6)
+        return ld16(reinterpret_cast<const uint4 *>(p) + i);
+    else
+        return p[i];
+}
+// the ICMP protocol of the family (ct_create4/6's related entry)
+template <bool V6>
+constexpr uint32_t icmp_proto()
+{
+    return V6 ? 58u : 1u;
+}
+// the w word of slot i
+template <bool V6>
+__device__ __forceinline__ uint32_t *slot_w(const CtaArgs &A, uint32_t i)
+{
+    if constexpr (V6)
+        return &A.ct6[i].w;
+    else
+        return &A.ct4[i].w;
+}
+
 // one CT stage of one header, decoded as cfc_api.cpp ct_apply does
+template <bool V6>
 struct Op {
     uint32_t kind, action, dir;
     bool is_tcp, syn, ki_form;
-    uint32_t tfl, len, sec, owner, proto;
-    uint32_t x1, y1, z1, w1;   // k1: the tuple as loaded (REPLY / RELATED)
-    uint32_t x2, y2, z2, w2;   // k2: reversed (ESTABLISHED / create)
+    uint32_t tfl, len, sec, owner, proto, rev;
+    Addr<V6> sa, da;           // k1 = (da, sa, z1, w1), k2 = (sa, da, z2, w2)
+    uint32_t z1, w1;           // k1: the tuple as loaded (REPLY / RELATED)
+    uint32_t z2, w2;           // k2: reversed (ESTABLISHED / create)
 };
 
 // owner word of the destination endpoint's CT maps (cilium_lxc lookup)
@@ -142,18 +188,36 @@ __device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint32_t da)
         s = (s + 1) & T.lxc4_mask;
     }
 }
+__device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint4 da)
+{
+    if (!T.lxc6)
+        return 0;
+    uint32_t s = l6_hash(da.x, da.y, da.z, da.w, L6_LXC_TAG) & T.lxc6_mask;
+    for (;;) {
+        const uint4 k = ld16(&T.lxc6[s].a[0]);
+        const uint4 v = ld16(&T.lxc6[s].pol_base);   // {pol_base, pol_mask, info, 0}
+        if (!(v.z & LXC_VALID))
+            return 0;
+        if (aeq(k, da))
+            return ct_owner_word(v.z & 0xFFFF, (v.z & LXC_CT_LOCAL) != 0);
+        s = (s + 1) & T.lxc6_mask;
+    }
+}
 
 // one header's inputs of the apply
+template <bool V6>
 struct ScanIn {
-    uint32_t cb, sa, da, pt, mt, ver, ident, tf, k1, k2;
+    uint32_t cb, pt, mt, ver, ident, tf, k1, k2;
+    Addr<V6> sa, da;
 };
 
 // stage st of a header, from its inputs; dsto: the owner word of the
 // destination endpoint's CT maps (the stages that are not the sender's)
-__device__ __forceinline__ Op decode_from(const CtaArgs &A, const ScanIn &r, int st,
-                                          uint32_t dsto)
+template <bool V6>
+__device__ __forceinline__ Op<V6> decode_from(const CtaArgs &A, const ScanIn<V6> &r, int st,
+                                              uint32_t dsto)
 {
-    Op o;
+    Op<V6> o;
     o.kind = OP_NONE;
     const uint32_t cs = (r.cb >> (4 * st)) & 0xF;
     if (!(cs & CFC_CT_DONE))
@@ -163,20 +227,28 @@ __device__ __forceinline__ Op decode_from(const CtaArgs &A, const ScanIn &r, int
     o.dir = eg ? CT_EGRESS : CT_INGRESS;
     o.owner = eg ? A.ep_owner : dsto;
     o.proto = r.mt & 0xFF;
-    if (o.proto != 6 && o.proto != 17 && o.proto != 1)
+    if (o.proto != 6 && o.proto != 17 && o.proto != icmp_proto<V6>())
         return o;
     o.len = r.mt >> 16;
     o.is_tcp = o.proto == 6;
     o.syn = (r.mt & CFC_HF_TCP_CLOSE) != 0;
     o.tfl = o.is_tcp ? r.tf : 0u;
-    o.action = ct_action(false, o.proto, r.pt, r.mt);
+    o.action = ct_action(V6, o.proto, r.pt, r.mt);
     o.sec = A.mode == CFC_MODE_EGRESS ? A.ep_sec : r.ident;
-    const CtProbe k = ct_probe<false>(o.proto, r.pt, (int)o.dir, o.owner);
-    o.x1 = r.da; o.y1 = r.sa; o.z1 = k.z1; o.w1 = k.w1;
-    o.x2 = r.sa; o.y2 = r.da; o.z2 = k.z2; o.w2 = k.w2;
-    // a k2 of ICMP-error form is its own related entry (ct_create4 writes
+    // ipv6_policy's rev_nat_index: daddr.s6_addr32[3] as a u16
+    // (bpf_lxc.c:787-788); IPv4 creates outside a load balancer carry 0
+    if constexpr (V6)
+        o.rev = o.dir == CT_INGRESS ? (r.da.w & 0xFFFF) : 0u;
+    else
+        o.rev = 0;
+    const CtProbe k = ct_probe<V6>(o.proto, r.pt, (int)o.dir, o.owner);
+    o.sa = r.sa;
+    o.da = r.da;
+    o.z1 = k.z1; o.w1 = k.w1;
+    o.z2 = k.z2; o.w2 = k.w2;
+    // a k2 of ICMP-error form is its own related entry (ct_create4/6 write
     // the same key twice)
-    o.ki_form = o.proto == 1 && (k.w2 & 0x200u) && k.z2 == 0;
+    o.ki_form = o.proto == icmp_proto<V6>() && (k.w2 & 0x200u) && k.z2 == 0;
     const uint32_t b = cs & CFC_CT_RES_MASK;
     const bool dropped = st == last && (int32_t)r.ver == DROP_POLICY;
     if (b >= 2)
@@ -188,30 +260,38 @@ __device__ __forceinline__ Op decode_from(const CtaArgs &A, const ScanIn &r, int
     return o;
 }
 
-__device__ __forceinline__ Op decode(const CtaArgs &A, uint64_t i, int st)
+template <bool V6>
+__device__ __forceinline__ void load_in(const CtaArgs &A, uint64_t i, ScanIn<V6> &r)
 {
-    ScanIn r;
     r.cb = A.ctb[i];
-    if (!((r.cb >> (4 * st)) & CFC_CT_DONE)) {
-        Op o;
-        o.kind = OP_NONE;
-        return o;
-    }
-    r.sa = A.sa[i];
-    r.da = A.da[i];
+    r.sa = ld_addr<V6>(A.sa, i);
+    r.da = ld_addr<V6>(A.da, i);
     r.pt = A.pt[i];
     r.mt = A.mt[i];
     r.ver = (uint32_t)A.ver[i];
     r.ident = A.ident[i];
     r.tf = A.tf ? A.tf[i] : 0u;
-    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
-    return decode_from(A, r, st, eg ? 0u : dst_owner(A.T, r.da));
 }
 
-__device__ __forceinline__ uint32_t find4(const CtaArgs &A, uint32_t x, uint32_t y,
-                                          uint32_t z, uint32_t w)
+template <bool V6>
+__device__ __forceinline__ Op<V6> decode(const CtaArgs &A, uint64_t i, int st)
 {
-    const uint32_t mask = A.T.ct4_mask;
+    ScanIn<V6> r;
+    r.cb = A.ctb[i];
+    if (!((r.cb >> (4 * st)) & CFC_CT_DONE)) {
+        Op<V6> o;
+        o.kind = OP_NONE;
+        return o;
+    }
+    load_in<V6>(A, i, r);
+    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
+    return decode_from<V6>(A, r, st, eg ? 0u : dst_owner(A.T, r.da));
+}
+
+__device__ __forceinline__ uint32_t find(const CtaArgs &A, uint32_t x, uint32_t y, uint32_t z,
+                                         uint32_t w)
+{
+    const uint32_t mask = A.mask;
     for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
         const uint4 s = ld16(A.ct4 + i);
         if (s.w == 0)
@@ -219,6 +299,33 @@ __device__ __forceinline__ uint32_t find4(const CtaArgs &A, uint32_t x, uint32_t
         if (s.x == x && s.y == y && s.z == z && s.w == w)
             return i;
     }
+}
+__device__ __forceinline__ uint32_t find(const CtaArgs &A, uint4 d, uint4 s, uint32_t z,
+                                         uint32_t w)
+{
+    const uint32_t mask = A.mask;
+    for (uint32_t i = khash(d, s, z, w) & mask;; i = (i + 1) & mask) {
+        const uint4 t = ld16(&A.ct6[i].z);   // {z, w, 0, 0}: compared first
+        if (t.y == 0)
+            return NONE;
+        if (t.x == z && t.y == w && aeq(ld16(A.ct6[i].d), d) && aeq(ld16(A.ct6[i].s), s))
+            return i;
+    }
+}
+// a claimed slot's key words (everything but w)
+__device__ __forceinline__ void put_key(const CtaArgs &A, uint32_t i, uint32_t d, uint32_t s,
+                                        uint32_t z)
+{
+    A.ct4[i].x = d;
+    A.ct4[i].y = s;
+    A.ct4[i].z = z;
+}
+__device__ __forceinline__ void put_key(const CtaArgs &A, uint32_t i, uint4 d, uint4 s,
+                                        uint32_t z)
+{
+    *reinterpret_cast<uint4 *>(A.ct6[i].d) = d;
+    *reinterpret_cast<uint4 *>(A.ct6[i].s) = s;
+    A.ct6[i].z = z;
 }
 
 // The slot of a key no other thread of this launch inserts: found, or a
@@ -231,24 +338,23 @@ __device__ __forceinline__ uint32_t find4(const CtaArgs &A, uint32_t x, uint32_t
 // that saw w ahead of the key words would see them as the zeros of the free
 // slot, which no CT key has (saddr and daddr are never both 0 on the path).
 // The launch's end writes the L2s back for the kernels after it.
-__device__ uint32_t find_or_insert4(const CtaArgs &A, uint32_t x, uint32_t y, uint32_t z,
-                                    uint32_t w, bool *fresh)
+template <bool V6>
+__device__ uint32_t find_or_insert(const CtaArgs &A, Addr<V6> d, Addr<V6> s, uint32_t z,
+                                   uint32_t w, bool *fresh)
 {
-    const uint32_t f = find4(A, x, y, z, w);
+    const uint32_t f = find(A, d, s, z, w);
     *fresh = f == NONE;
     if (f != NONE)
         return f;
-    const uint32_t mask = A.T.ct4_mask;
-    for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
-        uint32_t *pw = &A.ct4[i].w;
+    const uint32_t mask = A.mask;
+    for (uint32_t i = khash(d, s, z, w) & mask;; i = (i + 1) & mask) {
+        uint32_t *pw = slot_w<V6>(A, i);
         const uint32_t cur = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur != 0 && cur != CT_TOMBSTONE)
             continue;
         if (atomicCAS(pw, cur, CT_CLAIM) != cur)
             continue;
-        A.ct4[i].x = x;
-        A.ct4[i].y = y;
-        A.ct4[i].z = z;
+        put_key(A, i, d, s, z);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (store order)
         __hip_atomic_store(pw, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return i;
@@ -268,54 +374,54 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
 // TWO: the mode has two CT stages per header (egress); else only stage 0
 // exists and the odd hit-slot entries are never read (k_cta_route).
 constexpr int SCAN_U = 4;
-template <bool TWO>
+template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 {
     constexpr int NST = TWO ? 2 : 1;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
     uint32_t nhit = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
-        ScanIn r[SCAN_U];
+        ScanIn<V6> r[SCAN_U];
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {   // inputs (no branches)
             const uint64_t i = base + u * 256 + threadIdx.x;
             const uint64_t j = i < A.n ? i : A.n - 1;
-            r[u].cb = A.ctb[j];
-            r[u].sa = A.sa[j];
-            r[u].da = A.da[j];
-            r[u].pt = A.pt[j];
-            r[u].mt = A.mt[j];
-            r[u].ver = (uint32_t)A.ver[j];
-            r[u].ident = A.ident[j];
-            r[u].tf = A.tf ? A.tf[j] : 0u;
+            load_in<V6>(A, j, r[u]);
             r[u].k1 = A.ck1 ? A.ck1[j] : NONE;
             r[u].k2 = A.ck2 ? A.ck2[j] : NONE;
             if (i >= A.n)
                 r[u].cb = 0;
         }
         // the destination endpoint's CT owner: first probes together
-        uint32_t dsto[SCAN_U], ls[SCAN_U];
-        uint4 lv[SCAN_U];
+        uint32_t dsto[SCAN_U];
+        if constexpr (V6) {
 #pragma unroll
-        for (int u = 0; u < SCAN_U; u++) {
-            ls[u] = A.T.lxc4 ? hash32(r[u].da, A.T.lxc4_mask) : 0u;
-            lv[u] = A.T.lxc4 ? ld16(A.T.lxc4 + ls[u]) : make_uint4(0, 0, 0, 0);
-        }
+            for (int u = 0; u < SCAN_U; u++)
+                dsto[u] = dst_owner(A.T, r[u].da);
+        } else {
+            uint32_t ls[SCAN_U];
+            uint4 lv[SCAN_U];
 #pragma unroll
-        for (int u = 0; u < SCAN_U; u++) {
-            dsto[u] = 0;
-            if (A.T.lxc4) {
-                uint32_t sl = ls[u];
-                uint4 v = lv[u];
-                for (;;) {
-                    if (!(v.w & LXC_VALID))
-                        break;
-                    if (v.x == r[u].da) {
-                        dsto[u] = ct_owner_word(v.w & 0xFFFF, (v.w & LXC_CT_LOCAL) != 0);
-                        break;
+            for (int u = 0; u < SCAN_U; u++) {
+                ls[u] = A.T.lxc4 ? hash32(r[u].da, A.T.lxc4_mask) : 0u;
+                lv[u] = A.T.lxc4 ? ld16(A.T.lxc4 + ls[u]) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < SCAN_U; u++) {
+                dsto[u] = 0;
+                if (A.T.lxc4) {
+                    uint32_t sl = ls[u];
+                    uint4 v = lv[u];
+                    for (;;) {
+                        if (!(v.w & LXC_VALID))
+                            break;
+                        if (v.x == r[u].da) {
+                            dsto[u] = ct_owner_word(v.w & 0xFFFF, (v.w & LXC_CT_LOCAL) != 0);
+                            break;
+                        }
+                        sl = (sl + 1) & A.T.lxc4_mask;
+                        v = ld16(A.T.lxc4 + sl);
                     }
-                    sl = (sl + 1) & A.T.lxc4_mask;
-                    v = ld16(A.T.lxc4 + sl);
                 }
             }
         }
@@ -326,7 +432,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         for (int u = 0; u < SCAN_U; u++) {
 #pragma unroll
             for (int st = 0; st < NST; st++) {
-                const Op o = decode_from(A, r[u], st, dsto[u]);
+                const Op<V6> o = decode_from<V6>(A, r[u], st, dsto[u]);
                 kind[u][st] = o.kind;
                 act[u][st] = o.kind == OP_NONE ? 0u : o.action;
                 slot[u][st] = HS_NONE;
@@ -335,15 +441,15 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     const uint32_t key = st ? r[u].k2 : r[u].k1;
                     uint32_t sl;
                     if (key != NONE) {   // the slot the classify launch hit
-                        sl = key >> 1;
+                        sl = (key >> 1) - A.acct_base;
                     } else {
                         const bool rev = ((r[u].cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
-                        sl = rev ? find4(A, o.x1, o.y1, o.z1, o.w1)
-                                 : find4(A, o.x2, o.y2, o.z2, o.w2);
+                        sl = rev ? find(A, o.da, o.sa, o.z1, o.w1)
+                                 : find(A, o.sa, o.da, o.z2, o.w2);
                     }
                     slot[u][st] = sl == NONE ? HS_NONE : sl;
                 } else if (o.kind == OP_CREATE) {
-                    home[u][st] = ct_hash4(o.x2, o.y2, o.z2, o.w2) & A.T.ct4_mask;
+                    home[u][st] = khash(o.sa, o.da, o.z2, o.w2) & A.mask;
                     ncr++;
                 }
             }
@@ -404,17 +510,30 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 }
 
 // key of a request: k2 of its op (round A) or the ICMP entry k2 relates
-// (round B: ports 0, nexthdr ICMP, flags | TUPLE_F_RELATED)
-__device__ __forceinline__ uint4 req_key(const CtaArgs &A, uint32_t order2, bool related,
-                                         Op *po)
+// (round B: ports 0, nexthdr ICMP / ICMPv6, flags | TUPLE_F_RELATED)
+template <bool V6>
+struct ReqKey {
+    Addr<V6> d, s;
+    uint32_t z, w;
+    __device__ __forceinline__ bool operator==(const ReqKey &o) const
+    {
+        return z == o.z && w == o.w && aeq(d, o.d) && aeq(s, o.s);
+    }
+};
+template <bool V6>
+__device__ __forceinline__ ReqKey<V6> req_key(const CtaArgs &A, uint32_t order2, bool related,
+                                              Op<V6> *po)
 {
     const uint64_t i = order2 >> 2;
     const int st = (order2 >> 1) & 1;
-    *po = decode(A, i, st);
-    if (!related)
-        return make_uint4(po->x2, po->y2, po->z2, po->w2);
-    const uint32_t fl = (po->w2 >> 8) & 7;
-    return make_uint4(po->x2, po->y2, 0u, ct_word(1u, fl | 2u, po->owner));
+    *po = decode<V6>(A, i, st);
+    ReqKey<V6> k{po->sa, po->da, po->z2, po->w2};
+    if (related) {
+        const uint32_t fl = (po->w2 >> 8) & 7;
+        k.z = 0;
+        k.w = ct_word(icmp_proto<V6>(), fl | 2u, po->owner);
+    }
+    return k;
 }
 
 // ---- insert: one thread per home slot; keys deduped in registers (a fifth
@@ -422,6 +541,7 @@ __device__ __forceinline__ uint4 req_key(const CtaArgs &A, uint32_t order2, bool
 // first create also needs its related ICMP entry (round 0): the request is
 // marked (bit 0 of its word, free in a request) and k_cta_related writes
 // the entries — no per-request atomic on a shared counter here.
+template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, uint32_t nreq,
                                                     int round, uint32_t cx_off)
 {
@@ -431,33 +551,32 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
     const uint64_t omask = (1ull << A.ob) - 1;
     uint32_t claims = 0;
     if (lead) {
-        uint4 kk[4];
+        ReqKey<V6> kk[4];
         uint32_t ks[4];
         int nk = 0;
         for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
             const uint32_t order2 = (uint32_t)(req[r] & omask) & ~1u;
-            Op o;
-            const uint4 k = req_key(A, order2, round == 1, &o);
+            Op<V6> o;
+            const ReqKey<V6> k = req_key<V6>(A, order2, round == 1, &o);
             uint32_t slot = NONE;
             for (int j = 0; j < nk; j++)
-                if (kk[j].x == k.x && kk[j].y == k.y && kk[j].z == k.z && kk[j].w == k.w)
+                if (kk[j] == k)
                     slot = ks[j];
             bool first = false;
             if (slot == NONE) {
                 // not among the first four keys: an earlier request of the
                 // run may still have it
                 for (uint32_t q = r0; q < r && nk == 4; q++) {
-                    Op oq;
-                    const uint4 kq = req_key(A, (uint32_t)(req[q] & omask), round == 1, &oq);
-                    if (kq.x == k.x && kq.y == k.y && kq.z == k.z && kq.w == k.w) {
-                        slot = find4(A, k.x, k.y, k.z, k.w);
+                    Op<V6> oq;
+                    if (req_key<V6>(A, (uint32_t)(req[q] & omask), round == 1, &oq) == k) {
+                        slot = find(A, k.d, k.s, k.z, k.w);
                         break;
                     }
                 }
             }
             if (slot == NONE) {
                 bool fresh;
-                slot = find_or_insert4(A, k.x, k.y, k.z, k.w, &fresh);
+                slot = find_or_insert<V6>(A, k.d, k.s, k.z, k.w, &fresh);
                 mark_or(&A.mark[slot], MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
                 first = fresh;
                 claims += fresh;
@@ -482,40 +601,55 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
 // key's first create, whose related ICMP entry goes into the device table
 // for an ANY map (UDP, ICMP echo: a round-1 request) or into the host log
 // for a TCP map (no lookup reaches it there)
+template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *req,
                                                      uint32_t nreq)
 {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     const uint64_t v = r < nreq ? req[r] : 0ull;
     const uint32_t order2 = (uint32_t)(v & ((1ull << A.ob) - 1)) & ~1u;
-    Op o;
+    Op<V6> o;
     o.is_tcp = false;
     if (v & 1)
-        o = decode(A, order2 >> 2, (order2 >> 1) & 1);
+        o = decode<V6>(A, order2 >> 2, (order2 >> 1) & 1);
     const bool lg = (v & 1) && o.is_tcp, rb = (v & 1) && !o.is_tcp;
     const uint32_t l = block_count(&A.cnt[CTA_NLOG], lg);
     const uint32_t b = block_count(&A.cnt[CTA_NREQB], rb);
     const uint32_t fl = ((o.w2 >> 8) & 7) | 2u;
     if (lg && l < A.log_cap) {
-        CtLog &g = A.log[A.log_base + l];
-        g.x = o.x2;
-        g.y = o.y2;
-        g.w = ct_word(1u, fl, o.owner);
-        g.now = A.now;
-        g.dirlen = o.dir << 31 | o.len;
-        g.sec = o.sec;
-        g.seq = A.seq;
-        g.order = order2;
+        if constexpr (V6) {
+            CtLog6 &g = A.log6[A.log_base + l];
+            g.x = o.sa;
+            g.y = o.da;
+            g.w = ct_word(icmp_proto<V6>(), fl, o.owner);
+            g.now = A.now;
+            g.dirlen = o.dir << 31 | o.len;
+            g.sec = o.sec;
+            g.seq = A.seq;
+            g.order = order2;
+            g.rev = o.rev;
+            g.pad = 0;
+        } else {
+            CtLog &g = A.log[A.log_base + l];
+            g.x = o.sa;
+            g.y = o.da;
+            g.w = ct_word(icmp_proto<V6>(), fl, o.owner);
+            g.now = A.now;
+            g.dirlen = o.dir << 31 | o.len;
+            g.sec = o.sec;
+            g.seq = A.seq;
+            g.order = order2;
+        }
     }
     if (rb && b < A.req_cap) {
-        const uint32_t h = ct_hash4(o.x2, o.y2, 0u, ct_word(1u, fl, o.owner)) & A.T.ct4_mask;
+        const uint32_t h = khash(o.sa, o.da, 0u, ct_word(icmp_proto<V6>(), fl, o.owner)) & A.mask;
         A.reqB[b] = pack(A, h, order2);
     }
 }
 
 // ---- route: hits on unordered slots -> summary; the rest -> ordered list.
 // Four header stages per thread and step, the loads of each phase together
-// (as the scan).
+// (as the scan).  (Family-free: it reads the hit slots, meta and TCP flags.)
 __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
     constexpr int RU = 4;
@@ -608,7 +742,8 @@ __device__ __forceinline__ void upd_timeout(St &e, uint32_t now, bool is_tcp, ui
     }
     upd(e, now, life, dir, flags);
 }
-__device__ __forceinline__ void hit(St &e, uint32_t now, const Op &o)
+template <bool V6>
+__device__ __forceinline__ void hit(St &e, uint32_t now, const Op<V6> &o)
 {
     auto alive = [&] { return !(e.bits & RX_CLOSING) || !(e.bits & TX_CLOSING); };
     if (alive())
@@ -624,7 +759,7 @@ __device__ __forceinline__ void hit(St &e, uint32_t now, const Op &o)
             upd(e, now, CT_CLOSE_TIMEOUT, o.dir, o.tfl);
     }
 }
-// ct_create4's entry (seen_flags.syn = is_tcp: seen_non_syn stays clear)
+// ct_create4/6's entry (seen_flags.syn = is_tcp: seen_non_syn stays clear)
 __device__ __forceinline__ St fresh(uint32_t now, bool is_tcp, uint32_t dir)
 {
     St e{0, 0, 0, 0, 0, 0};
@@ -660,6 +795,7 @@ __device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St
 // update is idempotent: hit(hit(e)) = hit(e) — so only the first of each
 // such run is replayed.  A hot flow's hits in a Zipf batch become one op.
 // (Creates, deletes and related-entry writes are always kept.)
+template <bool V6>
 __device__ __forceinline__ uint32_t hit_sig(const CtaArgs &A, uint32_t order2)
 {
     if (order2 & 1)
@@ -675,10 +811,11 @@ __device__ __forceinline__ uint32_t hit_sig(const CtaArgs &A, uint32_t order2)
         return 0;   // not a plain hit
     const uint32_t mt = A.mt[i], proto = mt & 0xFF;
     const uint32_t tfl = (proto == 6 && A.tf) ? A.tf[i] : 0u;
-    const uint32_t act = ct_action(false, proto, A.pt[i], mt);
+    const uint32_t act = ct_action(V6, proto, A.pt[i], mt);
     return 1u | (uint32_t)st << 1 | act << 2 | (mt & CFC_HF_TCP_CLOSE ? 1u : 0u) << 4 |
            tfl << 8 | proto << 16;
 }
+template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx, uint32_t ncx,
                                                    uint8_t *keep)
 {
@@ -688,13 +825,14 @@ __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx
     const uint64_t omask = (1ull << A.ob) - 1;
     bool k = true;
     if (r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob)) {
-        const uint32_t s1 = hit_sig(A, (uint32_t)(cx[r] & omask));
-        k = !s1 || s1 != hit_sig(A, (uint32_t)(cx[r - 1] & omask));
+        const uint32_t s1 = hit_sig<V6>(A, (uint32_t)(cx[r] & omask));
+        k = !s1 || s1 != hit_sig<V6>(A, (uint32_t)(cx[r - 1] & omask));
     }
     keep[r] = k;
 }
 
 // ---- fold: one thread per slot of the sorted ordered list
+template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
                                                   const uint32_t *pncx)
 {
@@ -710,31 +848,20 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     bool live = !was_fresh, created = false, deleted = false;
     St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.tm, slot);
     uint64_t acct[4] = {0, 0, 0, 0};   // [tx pk, tx by, rx pk, rx by] added / set
-    uint32_t sec = 0;
+    uint32_t sec = 0, rev = 0;
     // the next op's header is loaded (branch-free) while this one is
     // replayed; the owner word does not matter here (the slot is the key),
     // so no endpoint lookup
-    auto load_in = [&](uint32_t r, ScanIn &in) {
-        const uint64_t i = (cx[r] & omask) >> 2;
-        in.cb = A.ctb[i];
-        in.sa = A.sa[i];
-        in.da = A.da[i];
-        in.pt = A.pt[i];
-        in.mt = A.mt[i];
-        in.ver = (uint32_t)A.ver[i];
-        in.ident = A.ident[i];
-        in.tf = A.tf ? A.tf[i] : 0u;
-    };
-    ScanIn cur;
-    load_in(r0, cur);
+    ScanIn<V6> cur;
+    load_in<V6>(A, (cx[r0] & omask) >> 2, cur);
     for (uint32_t r = r0; r < ncx && (uint32_t)(cx[r] >> A.ob) == slot; r++) {
         const uint32_t order2 = (uint32_t)(cx[r] & omask);
-        ScanIn nxt;
-        load_in(r + 1 < ncx ? r + 1 : r, nxt);
-        const Op o = decode_from(A, cur, (order2 >> 1) & 1, 0u);
+        ScanIn<V6> nxt;
+        load_in<V6>(A, (cx[r + 1 < ncx ? r + 1 : r] & omask) >> 2, nxt);
+        const Op<V6> o = decode_from<V6>(A, cur, (order2 >> 1) & 1, 0u);
         cur = nxt;
         const uint32_t d = o.dir == CT_INGRESS ? 2 : 0;
-        if (order2 & 1) {   // ct_create4's related-entry write: overwrite
+        if (order2 & 1) {   // ct_create's related-entry write: overwrite
             e = fresh(A.now, o.is_tcp, o.dir);
             e.bits |= SEEN_NON_SYN;
             live = created = true;
@@ -742,6 +869,7 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
             acct[d] = 1;
             acct[d + 1] = o.len;
             sec = o.sec;
+            rev = o.rev;
         } else if (o.kind == OP_CREATE) {
             if (live) {   // created earlier in this batch: a counted hit
                 hit(e, A.now, o);
@@ -756,6 +884,7 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
                 acct[d] = 1;
                 acct[d + 1] = o.len;
                 sec = o.sec;
+                rev = o.rev;
             }
         } else if (live) {   // OP_HIT, OP_DELETE
             hit(e, A.now, o);
@@ -766,13 +895,13 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
         }
     }
     unsigned long long *ac =
-        reinterpret_cast<unsigned long long *>(A.T.ct_acct) + 4ull * slot;
+        reinterpret_cast<unsigned long long *>(A.T.ct_acct) + 4ull * (A.acct_base + slot);
     CtInfo inf = A.info[slot];
     if (!live) {
-        // ct_delete4: the entry and its counts go; the key stays readable
+        // ct_delete4/6: the entry and its counts go; the key stays readable
         // for the host (w | CT_TOMBSTONE) until it has synchronised
-        const uint32_t w = A.ct4[slot].w;
-        A.ct4[slot].w = w | CT_TOMBSTONE;
+        uint32_t *pw = slot_w<V6>(A, slot);
+        *pw = *pw | CT_TOMBSTONE;
         ac[0] = ac[1] = ac[2] = ac[3] = 0;
         inf.y |= CTI_DELETED;
     } else if (created) {
@@ -782,7 +911,7 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
         ac[2] = acct[2];
         ac[3] = acct[3];
         inf.sec = sec;
-        inf.y = (inf.y & ~0xFFFFu) | CTI_CREATED | (deleted ? CTI_DELETED : 0u) |
+        inf.y = (inf.y & ~0xFFFFu) | rev | CTI_CREATED | (deleted ? CTI_DELETED : 0u) |
                 (was_fresh ? CTI_FRESH : 0u) | (inf.y & CTI_FRESH);
     } else {
         store_state(A.tm, slot, e);
@@ -804,11 +933,12 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
 // with hits, flags_seen |= their flags and last_report = now iff the
 // interval had passed or the flags grew (the first report sets it to now,
 // later ones keep it).
+template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 {
     // four slots per thread and step, each phase's loads together
     constexpr int FU = 4;
-    const uint64_t slots = (uint64_t)A.T.ct4_mask + 1;
+    const uint64_t slots = (uint64_t)A.mask + 1;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * FU;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * FU; base < slots; base += stride) {
         uint32_t m[FU], w[FU];
@@ -824,7 +954,7 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             w[u] = 0;
             if (m[u]) {
                 e[u] = load_state(A.tm, (uint32_t)s);
-                w[u] = A.ct4[s].w;
+                w[u] = *slot_w<V6>(A, (uint32_t)s);
             }
         }
 #pragma unroll
@@ -859,10 +989,23 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 }
 
 // ---- host synchronisation: the changed slots, compacted
-__global__ __launch_bounds__(256) void k_cta_collect(const Ct4Slot *ct4, CtTimer *tm,
-                                                     CtInfo *info, uint64_t slots,
-                                                     CtSyncRec *out, uint32_t cap,
-                                                     uint32_t *cnt)
+template <bool V6>
+struct SyncOf;
+template <>
+struct SyncOf<false> {
+    using Rec = CtSyncRec;
+    using Slot = Ct4Slot;
+};
+template <>
+struct SyncOf<true> {
+    using Rec = CtSyncRec6;
+    using Slot = Ct6Slot;
+};
+template <bool V6>
+__global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::Slot *ct,
+                                                     CtTimer *tm, CtInfo *info, uint64_t slots,
+                                                     typename SyncOf<V6>::Rec *out,
+                                                     uint32_t cap, uint32_t *cnt)
 {
     // four slots per thread and step, each phase's loads together
     constexpr int CU = 4;
@@ -876,12 +1019,18 @@ __global__ __launch_bounds__(256) void k_cta_collect(const Ct4Slot *ct4, CtTimer
             in[u] = s < slots ? info[s] : CtInfo{0, 0};
             nd += (in[u].y >> 16) != 0;
         }
-        uint4 k[CU], t[CU];
+        uint4 k[CU], t[CU], k2[CU], k3[CU];
 #pragma unroll
         for (int u = 0; u < CU; u++) {
             const uint64_t s = base + u * 256 + threadIdx.x;
             if ((in[u].y >> 16) != 0) {
-                k[u] = ld16(ct4 + s);
+                if constexpr (V6) {
+                    k[u] = ld16(ct[s].d);
+                    k2[u] = ld16(ct[s].s);
+                    k3[u] = ld16(&ct[s].z);
+                } else {
+                    k[u] = ld16(ct + s);
+                }
                 t[u] = ld16(tm + s);
             }
         }
@@ -892,13 +1041,20 @@ __global__ __launch_bounds__(256) void k_cta_collect(const Ct4Slot *ct4, CtTimer
             if ((in[u].y >> 16) == 0)
                 continue;
             if (r < cap) {
-                CtSyncRec &o = out[r];
+                typename SyncOf<V6>::Rec &o = out[r];
                 o.slot = (uint32_t)s;
                 o.info = in[u];
-                o.x = k[u].x;
-                o.y = k[u].y;
-                o.z = k[u].z;
-                o.w = k[u].w;
+                if constexpr (V6) {
+                    o.d[0] = k[u].x; o.d[1] = k[u].y; o.d[2] = k[u].z; o.d[3] = k[u].w;
+                    o.s[0] = k2[u].x; o.s[1] = k2[u].y; o.s[2] = k2[u].z; o.s[3] = k2[u].w;
+                    o.z = k3[u].x;
+                    o.w = k3[u].y;
+                } else {
+                    o.x = k[u].x;
+                    o.y = k[u].y;
+                    o.z = k[u].z;
+                    o.w = k[u].w;
+                }
                 o.last_rx = t[u].x;
                 o.last_tx = t[u].y;
                 o.flags = t[u].z;
@@ -922,7 +1078,19 @@ __global__ __launch_bounds__(256) void k_cta_tomb(Ct4Slot *ct4, const CtSyncRec 
         *reinterpret_cast<uint4 *>(ct4 + s) = t;
     }
 }
-
+__global__ __launch_bounds__(256) void k_cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n)
+{
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n)
+        return;
+    const uint32_t s = rec[r].slot;
+    if ((rec[r].w & CT_TOMBSTONE) == CT_TOMBSTONE) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4 *>(ct6[s].d) = z;
+        *reinterpret_cast<uint4 *>(ct6[s].s) = z;
+        *reinterpret_cast<uint4 *>(&ct6[s].z) = make_uint4(0, CT_TOMBSTONE, 0, 0);
+    }
+}
 // ---- garbage collection (cfc_ct_gc, ctmap.go:303-325 doFiltering) ---------
 __device__ __forceinline__ bool gc_in_set(const uint32_t *set, uint32_t n, uint32_t a)
 {
@@ -1097,19 +1265,21 @@ size_t cta_sort_tmp_bytes(uint32_t n)
     return std::max(tb, ts);
 }
 
-int cta_scan(const CtaArgs &A, hipStream_t s)
+template <bool V6>
+int cta_scan_t(const CtaArgs &A, hipStream_t s)
 {
     if (A.mode == CFC_MODE_EGRESS)
-        hipLaunchKernelGGL(k_cta_scan<true>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+        hipLaunchKernelGGL((k_cta_scan<V6, true>), dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
     else
-        hipLaunchKernelGGL(k_cta_scan<false>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+        hipLaunchKernelGGL((k_cta_scan<V6, false>), dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 // The rest of the apply after the host has read the scan's counts (nreqA)
 // and allowed the inserts.  Reads two more counts on the way (the sorts
 // take host item counts).
-int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s)
+template <bool V6>
+int cta_rest_t(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s)
 {
     const int bits = A.ob + A.slot_bits;
     uint64_t *sorted;
@@ -1117,9 +1287,9 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
     if ((rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
         return rc;
     if (nreqA) {
-        hipLaunchKernelGGL(k_cta_insert, dim3((nreqA + 255) / 256), dim3(256), 0, s, A, sorted,
+        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A, sorted,
                            nreqA, 0, 0u);
-        hipLaunchKernelGGL(k_cta_related, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
+        hipLaunchKernelGGL(k_cta_related<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
                            (const uint64_t *)sorted, nreqA);
     }
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1131,7 +1301,7 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
     if ((rc = sort_keys(A, A.reqB, A.reqB2, nreqB, bits, s, &sorted)))
         return rc;
     if (nreqB)
-        hipLaunchKernelGGL(k_cta_insert, dim3((nreqB + 255) / 256), dim3(256), 0, s, A, sorted,
+        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqB + 255) / 256), dim3(256), 0, s, A, sorted,
                            nreqB, 1, nreqA);
     // the creates' ops take the list's first nreqA + nreqB places, route's
     // ordered hits follow
@@ -1145,8 +1315,6 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
     if (ncx64 > A.cx_cap)
         return -EOVERFLOW;
     const uint32_t ncx = (uint32_t)ncx64;
-    if (ncx > A.cx_cap)
-        return -EOVERFLOW;
     if ((rc = sort_keys(A, A.cx, A.cx2, ncx, bits, s, &sorted)))
         return rc;
     if (ncx) {
@@ -1155,25 +1323,43 @@ int cta_rest(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s
         uint64_t *dst = sorted == A.cx ? A.cx2 : A.cx;
         uint8_t *keep = reinterpret_cast<uint8_t *>(A.hs);   // (hit slots: read by route only)
         uint32_t *nsel = A.cnt + CTA_NDEDUP;
-        hipLaunchKernelGGL(k_cta_dedup, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
+        hipLaunchKernelGGL(k_cta_dedup<V6>, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
                            (const uint64_t *)sorted, ncx, keep);
         size_t tb = A.sort_tmp_bytes;
         if (hipcub::DeviceSelect::Flagged(A.sort_tmp, tb, sorted, keep, dst, nsel, (int)ncx, s) !=
             hipSuccess)
             return -EIO;
-        hipLaunchKernelGGL(k_cta_fold, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
+        hipLaunchKernelGGL(k_cta_fold<V6>, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
                            (const uint64_t *)dst, (const uint32_t *)nsel);
     }
-    hipLaunchKernelGGL(k_cta_finish, dim3(blocks_for((uint64_t)A.T.ct4_mask + 1, 8192)),
+    hipLaunchKernelGGL(k_cta_finish<V6>, dim3(blocks_for((uint64_t)A.mask + 1, 8192)),
                        dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_scan(const CtaArgs &A, bool v6, hipStream_t s)
+{
+    return v6 ? cta_scan_t<true>(A, s) : cta_scan_t<false>(A, s);
+}
+
+int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s)
+{
+    return v6 ? cta_rest_t<true>(A, nreqA, host_cnt, s) : cta_rest_t<false>(A, nreqA, host_cnt, s);
 }
 
 int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec *out,
                 uint32_t cap, uint32_t *cnt, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_cta_collect, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4, tm,
-                       info, slots, out, cap, cnt);
+    hipLaunchKernelGGL(k_cta_collect<false>, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4,
+                       tm, info, slots, out, cap, cnt);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec6 *out,
+                 uint32_t cap, uint32_t *cnt, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cta_collect<true>, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct6,
+                       tm, info, slots, out, cap, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -1199,6 +1385,13 @@ int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s)
 {
     if (n)
         hipLaunchKernelGGL(k_cta_tomb, dim3((n + 255) / 256), dim3(256), 0, s, ct4, rec, n);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n, hipStream_t s)
+{
+    if (n)
+        hipLaunchKernelGGL(k_cta_tomb6, dim3((n + 255) / 256), dim3(256), 0, s, ct6, rec, n);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

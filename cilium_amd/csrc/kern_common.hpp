@@ -614,10 +614,10 @@ struct PolicyResult {
     int verdict;
     uint32_t ctr;
 };
-__device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
-                                                       uint32_t base,
-                                                       uint32_t mask,
-                                                       const PolicyProbe &P0)
+__device__ __forceinline__ PolicyResult policy_resolve_walk(const DevTables &T,
+                                                            uint32_t base,
+                                                            uint32_t mask,
+                                                            const PolicyProbe &P0)
 {
     uint32_t maybe = P0.maybe, j = P0.j, s = P0.s;
     uint4 v = P0.v;
@@ -650,6 +650,25 @@ __device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
         }
     }
     return PolicyResult{verdict, ctr};
+}
+// The issued probe decides most headers: its slot holds the key, or is
+// empty with no other key that may exist.  Only the rest walk (a probe
+// sequence, a Bloom false positive, the next key): kept out of the common
+// path, whose wait at the walk's loop would otherwise cover every load
+// issued after the probe (vmcnt counts in issue order).
+__device__ __forceinline__ PolicyResult policy_resolve(const DevTables &T,
+                                                       uint32_t base,
+                                                       uint32_t mask,
+                                                       const PolicyProbe &P0)
+{
+    const uint32_t j = P0.j;
+    const uint64_t key = ((uint64_t)P0.v.y << 32) | P0.v.x;
+    const bool hit = j < 3 && key == P0.key(j);
+    const bool done = j >= 3 || hit || (key == POL_EMPTY && !(P0.maybe & ~(1u << j)));
+    if (done)
+        return hit ? PolicyResult{j == 1 ? TC_ACT_OK : (int)(P0.v.z & 0xFFFF), P0.v.w}
+                   : PolicyResult{DROP_POLICY, NONE};
+    return policy_resolve_walk(T, base, mask, P0);
 }
 
 __device__ __forceinline__ PolicyResult policy_access(

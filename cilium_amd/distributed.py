@@ -79,3 +79,80 @@ def gather_drop_notify(rec, idx, start, dst=0, group=None):
     full = torch.cat([r[:int(c.item())] for r, c in zip(rows, counts)])
     recs = full[:, :4].contiguous().view(torch.int32).view(-1, 8)
     return recs, full[:, 4].clone()
+
+
+# ---- conntrack across GPUs: flow-affinity shards -----------------------------
+# CT writes are per key, and every key a header's lookups and ct_create4/6
+# touch (the flow's entry in either direction, its ICMP "related" entry, which
+# has ports 0 and is shared by every flow of the address pair) carries the
+# header's two addresses.  So the header stream is steered like RSS steers
+# flows to CPUs, by a symmetric hash of the unordered address pair, and each
+# rank owns the CT entries of its address pairs: it loads only those, applies
+# only its own headers' writes, and the union of the ranks' CT maps is the
+# single-GPU result for the same batches (ops on different address pairs
+# touch different keys, so they commute).  No CT collective.  A load
+# balancer moves a flow's address pair (service address -> backend) between
+# its CT_SERVICE entry and its main entry, so batches with services stay on
+# one rank.
+
+def _mix64(x):
+    import numpy as np
+    x = np.asarray(x, np.uint64)
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(33))) * np.uint64(0xFF51AFD7ED558CCD)
+        x = (x ^ (x >> np.uint64(33))) * np.uint64(0xC4CEB9FE1A85EC53)
+        return x ^ (x >> np.uint64(33))
+
+
+def addr_keys(addrs, family):
+    """One u64 per address: IPv4 raw u32 words as they are, IPv6 (n, 16)
+    network-order bytes folded."""
+    import numpy as np
+    if family == 4:
+        return np.asarray(addrs, np.uint32).astype(np.uint64)
+    a = np.ascontiguousarray(np.asarray(addrs, np.uint8).reshape(-1, 16))
+    hi = a[:, :8].copy().view(">u8").ravel().astype(np.uint64)
+    lo = a[:, 8:].copy().view(">u8").ravel().astype(np.uint64)
+    return hi ^ _mix64(lo)
+
+
+def pair_owner(ka, kb, world):
+    """Owner rank of the unordered address pair {a, b} (u64 keys)."""
+    import numpy as np
+    lo, hi = np.minimum(ka, kb), np.maximum(ka, kb)
+    with np.errstate(over="ignore"):
+        h = _mix64(_mix64(lo) ^ hi)
+    return (h % np.uint64(world)).astype(np.int64)
+
+
+def shard_headers(h, rank, world):
+    """This rank's headers of a batch (stream order kept) and their indices
+    in it."""
+    import numpy as np
+    own = pair_owner(addr_keys(h.saddr, h.family), addr_keys(h.daddr, h.family), world)
+    idx = np.nonzero(own == rank)[0]
+    from .synth import take
+    return take(h, idx), idx
+
+
+def shard_ct(ct, rank, world):
+    """The CT entries (synth.CT_DT records) this rank owns."""
+    import numpy as np
+    if ct is None or len(ct) == 0:
+        return ct
+    tu = np.asarray(ct["tuple"], np.uint8)
+    own = np.empty(len(ct), np.int64)
+    for fam, al in ((1, 4), (2, 16)):
+        m = ct["family"] == fam
+        if not m.any():
+            continue
+        d, s = tu[m, :al], tu[m, al:2 * al]
+        if fam == 1:
+            # (header batches hold IPv4 addresses as the raw network-order
+            # word loaded little-endian, as the tuple bytes read)
+            kd = addr_keys(np.ascontiguousarray(d).view("<u4").ravel(), 4)
+            ks = addr_keys(np.ascontiguousarray(s).view("<u4").ravel(), 4)
+        else:
+            kd, ks = addr_keys(d, 6), addr_keys(s, 6)
+        own[m] = pair_owner(kd, ks, world)
+    return ct[own == rank]

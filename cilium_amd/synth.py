@@ -53,6 +53,12 @@ LB4_DT = np.dtype([("addr", "<u4"), ("dport", "<u2"), ("slave", "<u2"),
                    ("target", "<u4"), ("port", "<u2"), ("count", "<u2"),
                    ("rev_nat", "<u2"), ("weight", "<u2")])
 REVNAT4_DT = np.dtype([("index", "<u2"), ("addr", "<u4"), ("port", "<u2")])
+# struct lb6_key + struct lb6_service (common.h:408-420), packed; struct
+# lb6_reverse_nat (:422-425) behind its u16 index
+LB6_DT = np.dtype([("addr", "u1", 16), ("dport", "<u2"), ("slave", "<u2"),
+                   ("target", "u1", 16), ("port", "<u2"), ("count", "<u2"),
+                   ("rev_nat", "<u2"), ("weight", "<u2")])
+REVNAT6_DT = np.dtype([("index", "<u2"), ("addr", "u1", 16), ("port", "<u2")])
 
 
 def htons(x):
@@ -809,6 +815,106 @@ def config_c5(seed=5, n_flows=10_000_000, n_prefixes=100_000, n_policy=16384,
     return t, flows
 
 
+def ct_entries_v6(daddr, saddr, dport, sport, proto, flags, dir_ingress,
+                  length, src_sec_id, rev_nat, lxc=-1, now=0):
+    """CT_DT records of IPv6 flows as ct_create6 writes them (conntrack.h:
+    615-662): as ct_entries_v4, 16-byte addresses, rev_nat_index (ipv6_policy
+    sets it from daddr.s6_addr32[3] for flows it creates, bpf_lxc.c:787-788)
+    and an ICMPv6 related entry."""
+    n = len(daddr)
+    tu = np.zeros((n, 38), np.uint8)
+    tu[:, 0:16] = np.asarray(daddr, np.uint8).reshape(n, 16)
+    tu[:, 16:32] = np.asarray(saddr, np.uint8).reshape(n, 16)
+    tu[:, 32:34] = np.asarray(dport, np.uint16).view(np.uint8).reshape(n, 2)
+    tu[:, 34:36] = np.asarray(sport, np.uint16).view(np.uint8).reshape(n, 2)
+    tu[:, 36] = proto
+    tu[:, 37] = flags
+    ent = np.zeros((n, 56), np.uint8)
+    ev = ent.view("<u8")[:, :4]
+    one = np.ones(n, np.uint64)
+    ev[:, 0] = np.where(dir_ingress, one, 0)
+    ev[:, 1] = np.where(dir_ingress, length, 0)
+    ev[:, 2] = np.where(dir_ingress, 0, one)
+    ev[:, 3] = np.where(dir_ingress, 0, length)
+    ent[:, 38:40] = np.asarray(rev_nat, np.uint16).view(np.uint8).reshape(n, 2)
+    ent[:, 44:48] = np.asarray(src_sec_id, np.uint32).view(np.uint8).reshape(n, 4)
+    ent[:, 32:36] = np.full(n, now + 60, np.uint32).view(np.uint8).reshape(n, 4)
+    if now > 5:
+        rep = np.full(n, now, np.uint32).view(np.uint8).reshape(n, 4)
+        ing = np.asarray(dir_ingress, bool)
+        ent[ing, 52:56] = rep[ing]
+        ent[~ing, 48:52] = rep[~ing]
+    ct = np.zeros(2 * n, CT_DT)
+    ct["family"] = 2
+    ct["lxc"] = lxc
+    ct["any"][:n] = np.asarray(proto) != IPPROTO_TCP
+    ct["any"][n:] = ct["any"][:n]
+    ct["tuple"][:n] = tu
+    rel = tu.copy()
+    rel[:, 32:36] = 0
+    rel[:, 36] = IPPROTO_ICMPV6
+    rel[:, 37] = np.asarray(flags, np.uint8) | 2
+    ct["tuple"][n:] = rel
+    ct["entry"][:n] = ent
+    ent2 = ent.copy()
+    ent2[:, 36] = 16                                   # seen_non_syn
+    ct["entry"][n:] = ent2
+    import pandas as pd
+    key = np.ascontiguousarray(ct["tuple"]).view(np.dtype((np.void, 38))).ravel()
+    df = pd.DataFrame({"k": [bytes(k) for k in key], "a": ct["any"]})
+    return ct[~df.duplicated(keep="last").to_numpy()]
+
+
+def config_c5_v6(seed=6, n_flows=300_000, n_prefixes=100_000, n_policy=16384, now=0):
+    """The C5 shape for IPv6: C3's tables (n_prefixes IPv6 ipcache prefixes,
+    no prefilter) plus n_flows live flows into / out of the endpoint's IPv6
+    address in the global CT6 maps, half opened from outside, TCP 70% /
+    UDP 30%.  Returns (tables, flows) as config_c5."""
+    t = config_c3(seed, n_prefixes=n_prefixes, n_v4_prefixes=1000, n_policy=n_policy,
+                  n_prefilter=0)
+    rng = np.random.default_rng(seed + 601)
+    ipc = t.ipcache[t.ipcache["family"] == 2]
+    r_addr = _addr_in_prefix_v6(rng, ipc, rng.integers(0, len(ipc), size=n_flows))
+    c_addr = np.tile(LXC_IPV6, (n_flows, 1))
+    proto = np.where(rng.random(n_flows) < 0.7, IPPROTO_TCP, IPPROTO_UDP).astype(np.uint8)
+    inbound = rng.random(n_flows) < 0.5
+    svc = htons(rng.choice(PORT_SET, size=n_flows).astype(np.uint32))
+    eph = htons(rng.integers(1024, 65536, size=n_flows).astype(np.uint32))
+    sport = np.where(inbound, eph, svc).astype(np.uint16)
+    dport = np.where(inbound, svc, eph).astype(np.uint16)
+    length = rng.integers(60, 1501, size=n_flows).astype(np.uint64)
+    ib = inbound[:, None]
+    d = np.where(ib, r_addr, c_addr)
+    s = np.where(ib, c_addr, r_addr)
+    kd = np.where(inbound, dport, sport)
+    ks = np.where(inbound, sport, dport)
+    sec = np.where(inbound, rng.integers(256, 256 + 16384, size=n_flows),
+                   EP_SECLABEL).astype(np.uint32)
+    # ingress-created entries: rev_nat_index from the packet's daddr (c)
+    rev = np.where(inbound, c_addr[:, 12].astype(np.uint16) |
+                   (c_addr[:, 13].astype(np.uint16) << 8), 0).astype(np.uint16)
+    t.ct = ct_entries_v6(d, s, kd, ks, proto, np.where(inbound, 1, 0).astype(np.uint8),
+                         inbound, length, sec, rev, now=now)
+    flows = Headers(6, r_addr, c_addr, sport, dport, proto,
+                    np.zeros(n_flows, np.uint8), length.astype(np.uint16),
+                    np.zeros(n_flows, np.uint32))
+    return t, flows
+
+
+def headers_c5_v6(t: Tables, flows: Headers, n, seed=6, new_frac=0.05, s=1.1):
+    """IPv6 C5 stream: Zipf packets of live flows plus new flows (C3
+    generator, every one to the endpoint)."""
+    rng = np.random.default_rng(seed + 777)
+    m = int(n * (1 - new_frac))
+    old = take(flows, _zipf_ranks(rng, len(flows), m, s))
+    old.length = rng.integers(60, 1501, size=m).astype(np.uint16)
+    ipc6 = t.ipcache[t.ipcache["family"] == 2]
+    new = gen_headers_v6(rng, n - m, ipc6, local_v6_addrs(t)[:1], local_frac=1.0,
+                         proxy_ident=proxy_identities(t))
+    h = concat([old, new])
+    return take(h, rng.permutation(n))
+
+
 def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1,
                return_new=False):
     """C5 stream into the endpoint: 95% packets of live flows drawn
@@ -991,4 +1097,76 @@ def lb4_services(rng, t: Tables, n_services=24, loopback=True, n_backend_pool=No
             rows = [r for r in rows if not (int(r["addr"][0]) == vip and
                                             int(r["slave"][0]) == 2)]
             row(vip, 0, 2, target=int(remote[0]), count=2, rev=rev)
+    return (np.concatenate(rows), np.concatenate(rn), vips, ports, protos)
+
+
+SVC6_NET = np.array([0xfd, 0x00, 0x5e, 0xc0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0], np.uint8)
+
+
+def lb6_services(rng, t: Tables, n_services=24, n_backend_pool=None):
+    """IPv6 services for cilium_lb6_services, the lb4_services shapes: per
+    service a master slot {vip, dport, 0} -> {count, rev_nat_index} and
+    backend slots 1..count; backends remote (inside IPv6 ipcache prefixes)
+    or local endpoints; one service's backend is the sending endpoint itself
+    (lb6_local has no loopback translation: the packet comes back to it);
+    an L3 service, a count-0 master, a missing backend slot and one held
+    under the L3 key.  -> (LB6_DT, REVNAT6_DT, vips (n, 16) u8, ports be16,
+    protos)."""
+    ipc = t.ipcache[t.ipcache["family"] == 2]
+    loc = local_v6_addrs(t)
+    loc = loc[~(loc == LXC_IPV6).all(1)]
+    pool_n = n_backend_pool or 4 * n_services
+    remote = _addr_in_prefix_v6(rng, ipc, rng.integers(0, len(ipc), size=pool_n))
+    rows, rn = [], []
+    vips = np.zeros((n_services, 16), np.uint8)
+    ports = np.zeros(n_services, np.uint16)
+    protos = np.zeros(n_services, np.uint8)
+
+    def row(addr, dport, slave, target=None, port=0, count=0, rev=0, weight=0):
+        r = np.zeros(1, LB6_DT)
+        r["addr"][0], r["dport"], r["slave"] = addr, dport, slave
+        if target is not None:
+            r["target"][0] = target
+        r["port"], r["count"], r["rev_nat"], r["weight"] = port, count, rev, weight
+        rows.append(r)
+
+    for k in range(n_services):
+        vip = SVC6_NET.copy()
+        vip[14], vip[15] = (k + 1) >> 8, (k + 1) & 255
+        vips[k] = vip
+        protos[k] = IPPROTO_UDP if k % 4 == 3 else IPPROTO_TCP
+        dp = htons(int(rng.choice(np.array([80, 443, 53, 8080, 9090]))))
+        l3 = k == 1
+        ports[k] = 0 if l3 else dp
+        key_dp = 0 if l3 else int(dp)
+        rev = k + 1
+        count = int(rng.integers(1, 5))
+        if k == 2:
+            count = 0
+        row(vip, key_dp, 0, count=count, rev=rev)
+        rnr = np.zeros(1, REVNAT6_DT)
+        rnr["index"], rnr["addr"][0], rnr["port"] = rev, vip, key_dp
+        rn.append(rnr)
+        for j in range(1, max(count, 1) + 1):
+            if k == 4 and j == 2:
+                continue
+            tgt = loc[j % len(loc)] if (k % 5 == 0 and len(loc)) else \
+                remote[(4 * k + j) % pool_n]
+            if k == 6 and j == 1:
+                tgt = LXC_IPV6
+            port = int(htons(8000 + k)) if k % 3 == 0 else 0
+            row(vip, key_dp, j, target=tgt, port=port, rev=rev)
+        if k == 5 and count >= 2:
+            rows = [r for r in rows if not ((r["addr"][0] == vip).all() and
+                                            int(r["slave"][0]) == 2)]
+            row(vip, 0, 2, target=remote[0], count=2, rev=rev)
+    # ipv6_policy stores daddr.s6_addr32[3] & 0xFFFF as the rev_nat_index of
+    # the flows it creates (bpf_lxc.c:787-788) and reverse-NATs every later
+    # hit whose index cilium_lb6_reverse_nat holds (:808-815): an entry under
+    # the endpoint's own index exercises that
+    rnr = np.zeros(1, REVNAT6_DT)
+    rnr["index"] = int(LXC_IPV6[12]) | int(LXC_IPV6[13]) << 8
+    rnr["addr"][0] = vips[0]
+    rnr["port"] = 0
+    rn.append(rnr)
     return (np.concatenate(rows), np.concatenate(rn), vips, ports, protos)

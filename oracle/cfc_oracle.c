@@ -336,6 +336,12 @@ typedef struct {
     uint32_t target;
     uint16_t port, count, rev_nat_index, weight;
 } lb4svc;
+/* struct lb6_service (common.h:414-420); the key struct lb6_key {address[16],
+ * dport, slave} (:408-412, 20 bytes packed) is the htab key */
+typedef struct {
+    uint8_t target[16];
+    uint16_t port, count, rev_nat_index, weight;
+} lb6svc;
 
 struct cfo {
     lpm ipc4, ipc6;
@@ -376,8 +382,17 @@ struct cfo {
     uint32_t *rnat4_addr;
     uint16_t *rnat4_port;
     uint8_t *rnat4_ok;
-    /* cfo_set_lb_io: skb->hash per header (NULL: cfo_flow_hash), and the
-     * packet's addresses after the program's rewrites, 3 u32 per header */
+    /* IPv6: cilium_lb6_services and cilium_lb6_reverse_nat (struct
+     * lb6_reverse_nat {address[16], port}, common.h:422-425) */
+    htab lb6;
+    lb6svc *lb6v;
+    uint32_t lb6_n, lb6_cap;
+    uint8_t *rnat6_addr;       /* [65536][16] */
+    uint16_t *rnat6_port;
+    uint8_t *rnat6_ok;
+    /* cfo_set_lb_io: skb->hash per header (NULL: cfo_flow_hash4/6), and the
+     * packet's addresses after the program's rewrites: IPv4 3 u32 per header
+     * (saddr, daddr, L4 word), IPv6 9 (saddr[4], daddr[4], L4 word) */
     const uint32_t *hash_in;
     uint32_t *pkt_out;
 };
@@ -409,6 +424,10 @@ cfo_t *cfo_new(void)
     ht_init(&o->pf6_fix, 20);
     ht_init(&o->ct, CTK);
     ht_init(&o->lb4, 8);
+    ht_init(&o->lb6, 20);
+    o->rnat6_addr = calloc(65536, 16);
+    o->rnat6_port = calloc(65536, 2);
+    o->rnat6_ok = calloc(65536, 1);
     o->rnat4_addr = calloc(65536, 4);
     o->rnat4_port = calloc(65536, 2);
     o->rnat4_ok = calloc(65536, 1);
@@ -446,6 +465,11 @@ void cfo_free(cfo_t *o)
     ht_free(&o->ct);
     ht_free(&o->lb4);
     free(o->lb4v);
+    ht_free(&o->lb6);
+    free(o->lb6v);
+    free(o->rnat6_addr);
+    free(o->rnat6_port);
+    free(o->rnat6_ok);
     free(o->rnat4_addr);
     free(o->rnat4_port);
     free(o->rnat4_ok);
@@ -598,6 +622,38 @@ int cfo_lb4_revnat_add(cfo_t *o, uint16_t index, const uint8_t val[6])
     return 0;
 }
 
+/* cilium_lb6_services: key struct lb6_key (20 bytes: address, dport be16,
+ * slave), value struct lb6_service (24 bytes) — lb.h:46-53 */
+int cfo_lb6_service_add(cfo_t *o, const uint8_t key[20], const uint8_t val[24])
+{
+    uint32_t v;
+    if (!ht_get(&o->lb6, key, &v)) {
+        if (o->lb6_n == o->lb6_cap) {
+            o->lb6_cap = o->lb6_cap ? 2 * o->lb6_cap : 64;
+            o->lb6v = realloc(o->lb6v, o->lb6_cap * sizeof(lb6svc));
+        }
+        v = o->lb6_n++;
+        ht_put(&o->lb6, key, v);
+    }
+    lb6svc *e = &o->lb6v[v];
+    memcpy(e->target, val, 16);
+    memcpy(&e->port, val + 16, 2);
+    memcpy(&e->count, val + 18, 2);
+    memcpy(&e->rev_nat_index, val + 20, 2);
+    memcpy(&e->weight, val + 22, 2);
+    return 0;
+}
+
+/* cilium_lb6_reverse_nat: key rev_nat_index, value struct lb6_reverse_nat
+ * (18 bytes: address, port be16) — lb.h:38-45 */
+int cfo_lb6_revnat_add(cfo_t *o, uint16_t index, const uint8_t val[18])
+{
+    memcpy(o->rnat6_addr + 16 * (size_t)index, val, 16);
+    memcpy(&o->rnat6_port[index], val + 16, 2);
+    o->rnat6_ok[index] = 1;
+    return 0;
+}
+
 void cfo_set_lb_io(cfo_t *o, const uint32_t *hash, uint32_t *pkt)
 {
     o->hash_in = hash;
@@ -624,6 +680,23 @@ uint32_t cfo_flow_hash4(uint32_t sa, uint32_t da, uint16_t sport, uint16_t dport
     const uint32_t a = sport, b = dport;
     const uint32_t pw = (a < b ? a : b) | (a < b ? b : a) << 16;
     return fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + pw * 0xC2B2AE3Du + proto);
+}
+
+/* the same over IPv6 addresses, each folded to a word as notify.hip fold6
+ * (raw words loaded little-endian) */
+static uint32_t fold6(const uint8_t *a)
+{
+    uint32_t w[4];
+    memcpy(w, a, 16);
+    uint32_t h = fmix32(w[3]);
+    h = fmix32(w[2] ^ h);
+    h = fmix32(w[1] ^ h);
+    return fmix32(w[0] ^ h);
+}
+uint32_t cfo_flow_hash6(const uint8_t sa[16], const uint8_t da[16], uint16_t sport,
+                        uint16_t dport, uint8_t proto)
+{
+    return cfo_flow_hash4(fold6(sa), fold6(da), sport, dport, proto);
 }
 
 /* ------------------------------------------------------------ datapath */
@@ -1065,6 +1138,125 @@ static void lb4_rev_nat(cfo_t *o, const struct ctent *e, uint8_t proto)
     tl_pkt.sa = o->rnat4_addr[i];
 }
 
+/* IPv6: the packet as the programs leave it (cfo_set_lb_io) */
+typedef struct {
+    uint8_t sa[16], da[16];
+    uint16_t sport, dport;   /* raw be16, as the L4 header holds them */
+} pkt6_t;
+static _Thread_local pkt6_t tl_pkt6;
+
+/* one cilium_lb6_services lookup */
+static const lb6svc *lb6_get(cfo_t *o, const uint8_t addr[16], uint16_t dport,
+                             uint16_t slave)
+{
+    uint8_t k[20];
+    uint32_t v;
+    memcpy(k, addr, 16);
+    memcpy(k + 16, &dport, 2);
+    memcpy(k + 18, &slave, 2);
+    tl_lookups++;
+    return ht_get(&o->lb6, k, &v) ? &o->lb6v[v] : NULL;
+}
+
+/* lb6_lookup_service (lb.h:352-381): as lb4_lookup_service */
+static const lb6svc *lb6_lookup_service(cfo_t *o, const uint8_t addr[16],
+                                        uint16_t *dport, uint16_t slave)
+{
+    const lb6svc *v;
+    if (*dport) {
+        v = lb6_get(o, addr, *dport, slave);
+        if (v && v->count)
+            return v;
+        *dport = 0;
+    }
+    v = lb6_get(o, addr, 0, slave);
+    return v && v->count ? v : NULL;
+}
+
+/* What ipv6_l3_from_lxc's service step (bpf_lxc.c:149-167) did to one
+ * header: lb6_extract_key (lb.h:336-350), lb6_lookup_service, lb6_local
+ * (:427-481).  No loopback translation and no reverse-NAT CT entry for
+ * IPv6 (ct_create6, conntrack.h:615-662, writes the flow's entry and its
+ * ICMPv6 entry only). */
+typedef struct {
+    int svc, drop;
+    uint8_t t_da[16];        /* tuple->daddr (orig_dip) after the step */
+    int64_t svc_hit;         /* the CT_SERVICE entry, or -1 */
+    int reslave;
+    uint8_t k_svc[CTK];
+    uint16_t slave, rev_nat, slave0;
+} lbx6_t;
+
+static void lb6_egress(cfo_t *o, uint16_t owner, const uint8_t *sa, const uint8_t *da,
+                       uint8_t proto, int close, lbx6_t *x)
+{
+    memset(x, 0, sizeof(*x));
+    memcpy(x->t_da, da, 16);
+    x->svc_hit = -1;
+    /* lb6_extract_key: key.address = tuple->daddr; extract_l4_port: TCP
+     * and UDP the dport, ICMPv6 none, anything else DROP_UNKNOWN_L4 ->
+     * skip_service_lookup */
+    if (proto != 6 && proto != 17 && proto != 58)
+        return;
+    if (!o->lb6_n)
+        return;
+    uint16_t kd = proto == 58 ? 0 : tl_pkt6.dport;
+    const lb6svc *svc = lb6_lookup_service(o, da, &kd, 0);
+    if (!svc)
+        return;
+    x->svc = 1;
+    /* lb6_local: ct_lookup6(CT_SERVICE) — one lookup of the tuple as
+     * loaded with TUPLE_F_SERVICE (conntrack.h:414-424); a hit fills
+     * ct_state from the entry */
+    uint8_t k2[CTK];
+    int action;
+    uint16_t td, ts;
+    if (ct_keys(16, owner, sa, da, proto, tl_pkt6.sport, tl_pkt6.dport, close, CT_SERVICE,
+                x->k_svc, k2, &action, &td, &ts) < 0)
+        return;
+    tl_lookups++;
+    x->svc_hit = ct_find(o, x->k_svc);
+    if (x->svc_hit >= 0) {
+        x->slave = o->ct_ents[x->svc_hit].slave;
+    } else {
+        /* lb6_select_slave (lb.h:124-152): hash % count + 1 */
+        x->slave = (uint16_t)(tl_hash % svc->count + 1);
+    }
+    x->slave0 = x->slave;
+    /* lb6_lookup_slave, then the fall-back to the service with the key as
+     * it stands (slave set) and a new selection (ct_update6_slave) */
+    const lb6svc *b = lb6_get(o, da, kd, x->slave);
+    if (!b) {
+        b = lb6_lookup_service(o, da, &kd, x->slave);
+        if (!b) {
+            x->drop = DROP_NO_SERVICE;
+            return;
+        }
+        x->slave = (uint16_t)(tl_hash % b->count + 1);
+        x->reslave = 1;
+    }
+    x->rev_nat = b->rev_nat_index;
+    memcpy(x->t_da, b->target, 16);
+    /* lb6_xlate: daddr, then the L4 dport (the tuple's ports are reloaded
+     * from the packet by the next ct_lookup6) */
+    memcpy(tl_pkt6.da, b->target, 16);
+    if (b->port && kd != b->port && (proto == 6 || proto == 17))
+        tl_pkt6.dport = b->port;
+}
+
+/* lb6_rev_nat (lb.h:306-319) with flags 0: the packet's source address
+ * (and port: reverse_map_l4_port) from cilium_lb6_reverse_nat[index] */
+static void lb6_rev_nat(cfo_t *o, uint16_t index, uint8_t proto)
+{
+    tl_lookups++;
+    if (!o->rnat6_ok[index])
+        return;
+    const uint16_t port = o->rnat6_port[index];
+    if (port && (proto == 6 || proto == 17) && port != tl_pkt6.sport)
+        tl_pkt6.sport = port;
+    memcpy(tl_pkt6.sa, o->rnat6_addr + 16 * (size_t)index, 16);
+}
+
 /* ipv4_policy (bpf_lxc.c:898-1015) + tail_ipv4_policy (:1017-1028) for
  * endpoint ep, called after local delivery with cb[CB_SRC_LABEL]=src; with
  * alen 16, ipv6_policy (:753-882) + tail_ipv6_policy (:884-895), which
@@ -1088,6 +1280,18 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     uint16_t pdport;
     int res;
     const struct ctent *hit;
+    /* ipv6_policy (:785-801): the tuple keeps daddr, the packet's daddr
+     * loses the low 16 bits of its last word (the rev_nat_index a create
+     * stores) */
+    uint8_t da0[16];
+    if (alen == 16) {
+        memcpy(da0, da, 16);
+        da = da0;
+        uint16_t rv;
+        memcpy(&rv, tl_pkt6.da + 12, 2);
+        if (rv)
+            memset(tl_pkt6.da + 12, 0, 2);
+    }
     int ret = ct_lookup(o, alen, ct_owner(o, ep->lxc_id), sa, da, proto, sport,
                         dport, close, CT_INGRESS, stage, &res, &pdport, &hit, NULL);
     if (ret < 0) {
@@ -1096,6 +1300,10 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
         metric(o, ret, METRIC_INGRESS, len);
         return r;
     }
+    /* (:808-815) any hit whose entry carries a rev_nat_index: the packet's
+     * source from cilium_lb6_reverse_nat, when it holds the index */
+    if (alen == 16 && hit && hit->rev_nat_index)
+        lb6_rev_nat(o, hit->rev_nat_index, proto);
     /* bpf_lxc.c:946-955: a reply of a load-balanced flow gets its source
      * translated back (packet only: the verdict does not depend on it) */
     if (alen == 4 && res == CT_REPLY && hit->rev_nat_index &&
@@ -1445,13 +1653,26 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
         metric(o, DROP_INVALID_SIP, METRIC_EGRESS, len);
         return r;
     }
+    (void)sport;
+    (void)dport;   /* the packet's ports are tl_pkt6's */
     int ret = exthdr_drop(proto);
     uint16_t pdport;
     int res;
+    const struct ctent *hit = NULL;
+    /* the service step (:149-167); the tuple's daddr may change */
+    lbx6_t x;
+    memset(&x, 0, sizeof(x));
+    memcpy(x.t_da, daddr, 16);
+    if (!ret) {
+        lb6_egress(o, ct_owner(o, lxc), saddr, daddr, proto, flags & HF_TCP_CLOSE, &x);
+        ret = x.drop;
+    }
+    const uint8_t *tda = x.t_da;   /* orig_dip */
+    uint8_t k2[CTK];
     if (!ret)
-        ret = ct_lookup(o, 16, ct_owner(o, lxc), saddr, daddr, proto, sport,
-                        dport, flags & HF_TCP_CLOSE, CT_EGRESS, 0, &res,
-                        &pdport, NULL, NULL);
+        ret = ct_lookup(o, 16, ct_owner(o, lxc), saddr, tda, proto, tl_pkt6.sport,
+                        tl_pkt6.dport, flags & HF_TCP_CLOSE, CT_EGRESS, 0, &res,
+                        &pdport, &hit, k2);
     if (ret) {
         r.verdict = ret;
         metric(o, ret, METRIC_EGRESS, len);
@@ -1459,9 +1680,9 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
     }
     uint32_t label = 0, dst;
     tl_lookups++;
-    if (lpm_lookup(&o->ipc6, daddr, &label) && label)
+    if (lpm_lookup(&o->ipc6, tda, &label) && label)
         dst = label;
-    else if (!memcmp(daddr, o->router_ip6, 8)) /* ipv6_match_prefix_64 */
+    else if (!memcmp(tl_pkt6.da, o->router_ip6, 8)) /* ipv6_match_prefix_64 */
         dst = CLUSTER_ID;
     else
         dst = WORLD_ID;
@@ -1479,14 +1700,17 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
     const uint32_t mon = res == CT_NEW ? TRACE_PAYLOAD_LEN : tl_mon[0];
     if (res == CT_NEW)
         tl_ct |= CTO_CREATE1;                       /* ct_create6, :237-249 */
+    else if (res >= CT_REPLY && hit->rev_nat_index)
+        lb6_rev_nat(o, hit->rev_nat_index, proto);  /* :255-266 */
     if (verdict > 0) {
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
         r.nt = trace_word(OBS_TO_PROXY, lxc, res, mon);
         return r;
     }
+    /* delivery by the packet's destination (lookup_ip6_endpoint, :305) */
     tl_lookups++;
-    const epinfo *ep = lxc_lookup(o, 2, daddr);
+    const epinfo *ep = lxc_lookup(o, 2, tl_pkt6.da);
     metric(o, 0, METRIC_EGRESS, len); /* to_host / local / to_stack */
     if (ep) {
         if (ep->flags & ENDPOINT_F_HOST) {   /* TRACE_TO_HOST, :373 */
@@ -1494,8 +1718,13 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
             r.nt = trace_word(OBS_TO_HOST, lxc, res, mon);
             return r;
         }
-        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 16, saddr, daddr, proto,
-                              sport, dport, 0, flags & HF_TCP_CLOSE, len, 0,
+        /* ipv6_local_delivery: the destination's ipv6_policy on the packet
+         * as it now is */
+        uint8_t psa[16], pda[16];
+        memcpy(psa, tl_pkt6.sa, 16);
+        memcpy(pda, tl_pkt6.da, 16);
+        res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 16, psa, pda, proto,
+                              tl_pkt6.sport, tl_pkt6.dport, 0, flags & HF_TCP_CLOSE, len, 0,
                               METRIC_EGRESS, 1);
         d.identity = dst;
         return d;
@@ -1544,6 +1773,17 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
         tl_mon[0] = tl_mon[1] = 0;
         tl_fresh.n = 0;
+        memcpy(tl_pkt6.sa, sa, 16);
+        memcpy(tl_pkt6.da, da, 16);
+        tl_pkt6.sport = sport[i];
+        tl_pkt6.dport = dport[i];
+        tl_hash = o->hash_in ? o->hash_in[i]
+                             : cfo_flow_hash6(sa, da, sport[i], dport[i], proto[i]);
+        if (o->pkt_out) {   /* (XDP verdicts leave the packet as it is) */
+            memcpy(o->pkt_out + 9 * i, sa, 16);
+            memcpy(o->pkt_out + 9 * i + 4, da, 16);
+            o->pkt_out[9 * i + 8] = sport[i] | (uint32_t)dport[i] << 16;
+        }
         if (mode == CFO_MODE_XDP || mode == CFO_MODE_FULL) {
             int x = xdp_v6(o, sa, da);
             if (mode == CFO_MODE_XDP || x == XDP_DROP) {
@@ -1578,6 +1818,11 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             o->notify_out[i] = notify_site(mode, ep_lxc, &r);
         if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
             o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
+        if (o->pkt_out) {
+            memcpy(o->pkt_out + 9 * i, tl_pkt6.sa, 16);
+            memcpy(o->pkt_out + 9 * i + 4, tl_pkt6.da, 16);
+            o->pkt_out[9 * i + 8] = tl_pkt6.sport | (uint32_t)tl_pkt6.dport << 16;
+        }
     }
 }
 
@@ -1849,9 +2094,9 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
         if (hazard && pass == 1)
             hazard[i] = 0;
         const uint8_t c = ct[i];
-        /* (lb4_local created its CT_SERVICE entry before it found no backend) */
-        const int no_svc = alen == 4 && mode == CFO_MODE_EGRESS &&
-                           verdict[i] == DROP_NO_SERVICE;
+        /* (lb4_local / lb6_local created its CT_SERVICE entry before it
+         * found no backend) */
+        const int no_svc = mode == CFO_MODE_EGRESS && verdict[i] == DROP_NO_SERVICE;
         if (!(c & (CTO_DONE1 | CTO_DONE2)) && !no_svc)
             continue;
         const uint8_t *sa = saddr + (size_t)alen * i;
@@ -1864,8 +2109,10 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
          * (its CT_SERVICE entry: created, or hit and updated), and the tuple
          * and packet it leaves for the stages */
         lbx_t x;
+        lbx6_t x6;
         int lbv = 0;
         uint32_t tda4 = 0, psa4 = 0, pda4 = 0;
+        uint8_t tda6[16], psa6[16], pda6[16];
         uint16_t psp = sport[i], pdp = dport[i];
         if (alen == 4) {
             memcpy(&tl_pkt.sa, sa, 4);
@@ -1907,11 +2154,53 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             pda4 = tl_pkt.da;
             psp = tl_pkt.sport;
             pdp = tl_pkt.dport;
+        } else {
+            /* IPv6 egress: the same for lb6_local (no loopback, no
+             * reverse-NAT entry) */
+            memcpy(tl_pkt6.sa, sa, 16);
+            memcpy(tl_pkt6.da, da, 16);
+            tl_pkt6.sport = sport[i];
+            tl_pkt6.dport = dport[i];
+            tl_hash = o->hash_in ? o->hash_in[i]
+                                 : cfo_flow_hash6(sa, da, sport[i], dport[i], proto[i]);
+            memcpy(tda6, da, 16);
+            if (mode == CFO_MODE_EGRESS && ((c & CTO_DONE1) || no_svc)) {
+                lb6_egress(o, ct_owner(o, ep_lxc), sa, da, proto[i], syn, &x6);
+                lbv = x6.svc;
+                memcpy(tda6, x6.t_da, 16);
+                if (pass == 2 && lbv) {
+                    uint8_t kk2[CTK];
+                    int act;
+                    uint16_t a_, b_;
+                    (void)ct_keys(16, ct_owner(o, ep_lxc), sa, da, proto[i], sport[i],
+                                  dport[i], syn, CT_SERVICE, x6.k_svc, kk2, &act, &a_, &b_);
+                    if (x6.svc_hit >= 0) {
+                        ct_hit_update(o, &o->ct_ents[x6.svc_hit], act, CT_SERVICE, is_tcp,
+                                      syn, fl, len[i]);
+                        if (x6.reslave)   /* ct_update6_slave */
+                            o->ct_ents[x6.svc_hit].slave = x6.slave;
+                    } else {
+                        ctstate_t cs = {0, x6.slave0, 0, 0, 0};
+                        ct_create(o, x6.k_svc, 16, CT_SERVICE, len[i], 0, &cs);
+                        if (x6.reslave) {
+                            int64_t ne = ct_find(o, x6.k_svc);
+                            if (ne >= 0)
+                                o->ct_ents[ne].slave = x6.slave;
+                        }
+                    }
+                }
+            }
+            memcpy(psa6, tl_pkt6.sa, 16);
+            memcpy(pda6, tl_pkt6.da, 16);
+            psp = tl_pkt6.sport;
+            pdp = tl_pkt6.dport;
         }
-        const epinfo *dst = lxc_lookup(o, alen == 4 ? 1 : 2, alen == 4 ? (const uint8_t *)&pda4 : da);
+        const epinfo *dst = lxc_lookup(o, alen == 4 ? 1 : 2,
+                                       alen == 4 ? (const uint8_t *)&pda4 : pda6);
         for (int s = 0; s < 2; s++) {
-            if (alen == 4 && s == 1)   /* (a reverse NAT may have moved it) */
-                dst = lxc_lookup(o, 1, (const uint8_t *)&pda4);
+            if (s == 1)   /* (a reverse NAT may have moved it) */
+                dst = lxc_lookup(o, alen == 4 ? 1 : 2,
+                                 alen == 4 ? (const uint8_t *)&pda4 : pda6);
             const uint8_t cs = (uint8_t)(c >> (4 * s));
             if (!(cs & CTO_DONE1))
                 continue;
@@ -1933,6 +2222,11 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 kda = egress_stage ? (const uint8_t *)&tda4 : (const uint8_t *)&pda4;
                 ksp = egress_stage ? tl_pkt.sport : psp;
                 kdp = egress_stage ? tl_pkt.dport : pdp;
+            } else {
+                ksa = egress_stage ? sa : psa6;
+                kda = egress_stage ? tda6 : pda6;
+                ksp = egress_stage ? tl_pkt6.sport : psp;
+                kdp = egress_stage ? tl_pkt6.dport : pdp;
             }
             if (ct_keys(alen, owner, ksa, kda, proto[i], ksp, kdp,
                         syn, dir, k1, k2, &action, &td, &ts) < 0)
@@ -1948,6 +2242,12 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 pda4 = tl_pkt.da;
                 psp = tl_pkt.sport;
                 pdp = tl_pkt.dport;
+            }
+            if (alen == 16 && egress_stage && b >= CT_REPLY && e1 >= 0 &&
+                o->ct_ents[e1].rev_nat_index) {
+                lb6_rev_nat(o, o->ct_ents[e1].rev_nat_index, proto[i]);
+                memcpy(psa6, tl_pkt6.sa, 16);
+                psp = tl_pkt6.sport;
             }
             if (pass == 1) {   /* CONNTRACK_ACCOUNTING of the lookup hits */
                 const int64_t e = b >= CT_REPLY ? e1 : b == CT_ESTABLISHED ? e2 : -1;
@@ -1972,7 +2272,14 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             const int rel = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) != 0;
             const int q = e1 >= 0 ? (rel ? CT_RELATED : CT_REPLY)
                           : e2 >= 0 ? CT_ESTABLISHED : CT_NEW;
-            if (hazard && q != b && !(b == CT_NEW && q == CT_ESTABLISHED && created))
+            /* (a flow created earlier in the batch: the reference's second
+             * packet is CT_ESTABLISHED, the batch's CT_NEW — the same
+             * verdict and entry, but ipv6_policy reverse-NATs an IPv6 hit
+             * whose entry's rev_nat_index cilium_lb6_reverse_nat holds,
+             * bpf_lxc.c:808-815, so there the packets differ) */
+            const int rn6 = alen == 16 && dir == CT_INGRESS && e2 >= 0 &&
+                            o->rnat6_ok[o->ct_ents[e2].rev_nat_index];
+            if (hazard && q != b && !(b == CT_NEW && q == CT_ESTABLISHED && created && !rn6))
                 hazard[i] = 1;
             /* the monitor length a packet-at-a-time lookup would return */
             uint32_t m = TRACE_PAYLOAD_LEN;
@@ -2006,11 +2313,13 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                             hazard[i] = 1;
                     }
                     ctstate_t cs = {alen == 16 && dir == CT_INGRESS
-                                        ? (uint16_t)(da[12] | da[13] << 8) : 0,
+                                        ? (uint16_t)(kda[12] | kda[13] << 8) : 0,
                                     0, 0, 0, 0};
-                    if (egress_stage && lbv)   /* ct_state_new from lb4_local */
+                    if (egress_stage && lbv && alen == 4)   /* ct_state_new from lb4_local */
                         cs = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr,
                                          x.svc_addr};
+                    if (egress_stage && lbv && alen == 16)  /* ... from lb6_local */
+                        cs = (ctstate_t){x6.rev_nat, x6.slave, 0, 0, 0};
                     ct_create(o, k2, alen, dir, len[i], sec, &cs);
                 }
             }

@@ -142,12 +142,19 @@ void cfo_ct_apply_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
  * cilium_lb4_reverse_nat (value struct lb4_reverse_nat 6 B) */
 int cfo_lb4_service_add(cfo_t *o, const uint8_t key[8], const uint8_t val[12]);
 int cfo_lb4_revnat_add(cfo_t *o, uint16_t index, const uint8_t val[6]);
+/* IPv6: cilium_lb6_services (key struct lb6_key 20 B, value struct
+ * lb6_service 24 B) and cilium_lb6_reverse_nat (value 18 B) */
+int cfo_lb6_service_add(cfo_t *o, const uint8_t key[20], const uint8_t val[24]);
+int cfo_lb6_revnat_add(cfo_t *o, uint16_t index, const uint8_t val[18]);
 /* per-header inputs / outputs of the next classify / ct_apply calls: hash =
- * skb->hash (NULL: cfo_flow_hash4), pkt = the packet's saddr, daddr and
- * first L4 word after the program's rewrites (3 u32 per header, or NULL) */
+ * skb->hash (NULL: cfo_flow_hash4/6), pkt = the packet's saddr, daddr and
+ * first L4 word after the program's rewrites (IPv4 3 u32 per header, IPv6
+ * 9: saddr[4], daddr[4], L4 word; or NULL) */
 void cfo_set_lb_io(cfo_t *o, const uint32_t *hash, uint32_t *pkt);
 uint32_t cfo_flow_hash4(uint32_t sa, uint32_t da, uint16_t sport, uint16_t dport,
                         uint8_t proto);
+uint32_t cfo_flow_hash6(const uint8_t sa[16], const uint8_t da[16], uint16_t sport,
+                        uint16_t dport, uint8_t proto);
 #define CFO_CT_ROW 104
 size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap);
 /* ctmap.GC with doFiltering (pkg/maps/ctmap/ctmap.go:303-350) on the

@@ -213,6 +213,16 @@ class RefDatapath:
             for r in t.revnat4:
                 L.maps["cilium_lb4_reverse_nat"].update(
                     struct.pack("<H", int(r["index"])), r.tobytes()[2:8])
+        # IPv6 (lb.h:38-53): cilium_lb6_services {struct lb6_key (20 B):
+        # struct lb6_service (24 B)}, cilium_lb6_reverse_nat (18 B)
+        if getattr(t, "lb6", None) is not None:
+            for r in t.lb6:
+                b = r.tobytes()
+                L.maps["cilium_lb6_services"].update(b[:20], b[20:44])
+        if getattr(t, "revnat6", None) is not None:
+            for r in t.revnat6:
+                L.maps["cilium_lb6_reverse_nat"].update(
+                    struct.pack("<H", int(r["index"])), r.tobytes()[2:20])
         for p in t.prefilter:
             fam = int(p["family"])
             an = 4 if fam == 1 else 16
@@ -409,7 +419,7 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     # it (service translation, reverse NAT, a proxy's port); skb->hash as
     # the first perf-ring record of the header reports it (get_hash_recalc,
     # what lb4_select_slave reduced), hash_ok = 0 where none was sent
-    pktv = np.zeros((n, 3), np.uint32)
+    pktv = np.zeros((n, 3 if h.family == 4 else 9), np.uint32)
     hsh = np.zeros(n, np.uint32)
     hsh_ok = np.zeros(n, np.uint8)
     ev_hdr, ev_rec = [], []
@@ -427,6 +437,10 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
         t0 = int(time.clock_gettime(time.CLOCK_MONOTONIC))
         if h.family == 4:
             pktv[i] = (h.saddr[i], h.daddr[i], int(h.sport[i]) | int(h.dport[i]) << 16)
+        else:
+            pktv[i, :4] = np.frombuffer(bytes(h.saddr[i]), "<u4")
+            pktv[i, 4:8] = np.frombuffer(bytes(h.daddr[i]), "<u4")
+            pktv[i, 8] = int(h.sport[i]) | int(h.dport[i]) << 16
         if mode in (MODE_XDP, MODE_FULL):
             ret = H.test_run_xdp(dp.xdp, build(h, i))
             if mode == MODE_XDP or ret == XDP_DROP:
@@ -451,6 +465,11 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
             pktv[i, 0], pktv[i, 1] = struct.unpack_from("<II", po, 14 + 12)
             if len(po) >= l4 + 4 and h.proto[i] in (6, 17):
                 pktv[i, 2] = struct.unpack_from("<I", po, l4)[0]
+        elif h.family == 6 and len(po) >= 14 + 40:
+            l4 = l4_offset(h, i)
+            pktv[i, :8] = struct.unpack_from("<8I", po, 14 + 8)
+            if len(po) >= l4 + 4 and h.proto[i] in (6, 17):
+                pktv[i, 8] = struct.unpack_from("<I", po, l4)[0]
         if evs:
             hsh[i], hsh_ok[i] = int(evs[0]["hash"]), 1
         t1 = int(time.clock_gettime(time.CLOCK_MONOTONIC))
@@ -470,13 +489,13 @@ def lpm_pin(ipc_map, h: S.Headers, pkt=None):
     with the key ipcache_lookup4/6 builds (eps.h:49-80: prefixlen 32 static
     bits + the full address, family byte) -> (labels (n, 4) u32, hits (n, 4)
     u8) for the columns saddr, daddr, and the packet's saddr / daddr as the
-    program left them (pkt: IPv4 service translation; else saddr / daddr
-    again).  The identity derivations of headers the reference reports
+    program left them (pkt = (saddrs, daddrs) after service translation;
+    else saddr / daddr again).  The identity derivations of headers the reference reports
     nothing for rest on these lookups (bpf_netdev.c:374-398, bpf_lxc.c:516-532)."""
     n = len(h)
     fam = 1 if h.family == 4 else 2
     cols = [h.saddr, h.daddr,
-            h.saddr if pkt is None else pkt[:, 0], h.daddr if pkt is None else pkt[:, 1]]
+            h.saddr if pkt is None else pkt[0], h.daddr if pkt is None else pkt[1]]
     lab = np.zeros((n, 4), np.uint32)
     hit = np.zeros((n, 4), np.uint8)
     for c, a in enumerate(cols):
@@ -493,12 +512,20 @@ def lpm_pin(ipc_map, h: S.Headers, pkt=None):
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
     action, verdict, ident, idmask, cbs, ev_hdr, ev, clock, pkt, hsh, hsh_ok = res
     extra = {}
-    lab, hit = lpm_pin(dp.L.maps["cilium_ipcache"], h,
-                       pkt if getattr(t, "lb4", None) is not None else None)
+    lb = getattr(t, "lb4", None) is not None or getattr(t, "lb6", None) is not None
+    pk = None
+    if lb:   # the packet's addresses as the programs left them
+        pk = (pkt[:, 0], pkt[:, 1]) if h.family == 4 else \
+            (np.ascontiguousarray(pkt[:, 0:4]).view(np.uint8).reshape(-1, 16),
+             np.ascontiguousarray(pkt[:, 4:8]).view(np.uint8).reshape(-1, 16))
+    lab, hit = lpm_pin(dp.L.maps["cilium_ipcache"], h, pk)
     extra.update(x_lpm=lab, x_lpm_hit=hit)
-    if getattr(t, "lb4", None) is not None:
-        extra.update(lb4=t.lb4, revnat4=t.revnat4, x_pkt=pkt, x_hash=hsh,
-                     x_hash_ok=hsh_ok)
+    if lb:
+        if getattr(t, "lb4", None) is not None:
+            extra.update(lb4=t.lb4, revnat4=t.revnat4)
+        if getattr(t, "lb6", None) is not None:
+            extra.update(lb6=t.lb6, revnat6=t.revnat6)
+        extra.update(x_pkt=pkt, x_hash=hsh, x_hash_ok=hsh_ok)
         if h.hash is not None:
             extra["h_hash"] = h.hash
     if t.ct is not None:
@@ -1146,6 +1173,147 @@ def _keep(h, m):
     return S.take(h, m)
 
 
+# ------------------------------------------------------------ IPv6 services
+def _lb_setup6(seed):
+    """C3-shaped small tables (two dual-stack endpoints with programs) plus
+    IPv6 services (synth.lb6_services); the sending endpoint's egress policy
+    allows most backend identities, both endpoints' ingress half of them and
+    the sender."""
+    t = S.config_c3(seed, n_prefixes=2000, n_v4_prefixes=100, n_policy=400,
+                    n_endpoints=2, n_prefilter=0)
+    rng = np.random.default_rng(seed + 1)
+    t.lb6, t.revnat6, vips, ports, protos = S.lb6_services(rng, t)
+    ipc = t.ipcache[t.ipcache["family"] == 2]
+    idents = np.unique(ipc["label"])
+    allow = rng.choice(idents, size=int(0.8 * len(idents)), replace=False)
+    for lxc, pol in t.policy.items():
+        one = np.zeros(len(allow) + 4, S.POLICY_DT)
+        one["identity"][:len(allow)] = allow
+        one["identity"][len(allow):] = [S.WORLD_ID, S.CLUSTER_ID, S.HOST_ID,
+                                       S.EP_SECLABEL]
+        add = np.concatenate([one, one])
+        add["egress"][len(one):] = 1
+        add = add[(add["egress"] == 1) | (np.arange(len(add)) % 2 == 0)]
+        have = {(int(r["identity"]), int(r["dport"]), int(r["proto"]),
+                 int(r["egress"])) for r in pol}
+        add = add[[(int(r["identity"]), 0, 0, int(r["egress"])) not in have
+                   for r in add]]
+        t.policy[lxc] = np.concatenate([pol, add])
+    return t, rng, vips, ports, protos
+
+
+def _svc_flows6(rng, n, vips, ports, protos, sport_base):
+    """n new IPv6 flows from the endpoint to service VIPs: 80% on the
+    service's port and protocol, 10% another port (the L3 fall-back key),
+    10% ICMPv6 echo"""
+    k = rng.integers(0, len(vips), size=n)
+    h = S.Headers(6, np.tile(S.LXC_IPV6, (n, 1)), vips[k].copy(),
+                  S.htons(sport_base + np.arange(n)), ports[k].copy(),
+                  protos[k].copy(), np.zeros(n, np.uint8),
+                  rng.integers(100, 1500, size=n).astype(np.uint16),
+                  np.zeros(n, np.uint32))
+    z = h.dport == 0
+    h.dport[z] = S.htons(rng.choice(np.array([80, 8443, 22]), size=int(z.sum())))
+    r = rng.random(n)
+    other = r < 0.1
+    h.dport[other] = S.htons(rng.integers(1, 65536, size=int(other.sum())))
+    icmp = r > 0.9
+    h.proto[icmp] = S.IPPROTO_ICMPV6
+    h.sport[icmp] = 128        # echo request: type 128, code 0
+    h.dport[icmp] = 0
+    return h
+
+
+def _no_hazard(t, h, mode, ep):
+    import oracle as O
+    for _ in range(6):
+        o = O.Oracle(t)
+        oa, ov, oi, ct = o.classify(h, mode, ep or 0, want_ct=True)
+        hz = o.ct_apply(h, mode, ep or 0, oi, ov, ct, hazard=True)
+        if not hz.any():
+            break
+        h = _keep(h, hz == 0)
+    assert not hz.any()
+    return h
+
+
+def sc_lb_egress_v6(n=4000, seed=51):
+    """IPv6 service load balancing in the sending endpoint's egress program
+    (ipv6_l3_from_lxc, bpf_lxc.c:149-167, 255-266; lb.h:336-481): a history
+    stream opens service flows (CT_SERVICE entries, the flows' entries with
+    rev_nat_index and slave), then the test stream: established service
+    flows, new ones, a service whose backend is the sender itself, and plain
+    traffic.  skb->hash is the reference's (from its records)."""
+    t, rng, vips, ports, protos = _lb_setup6(seed)
+    hist = _svc_flows6(rng, 1000, vips, ports, protos, 20000)
+    plain = S.gen_headers_v6(rng, 300, t.ipcache[t.ipcache["family"] == 2],
+                             S.local_v6_addrs(t), local_frac=0.3, mark_host=0,
+                             mark_proxy=0, src_fixed=S.LXC_IPV6, ext=0,
+                             exthdr_drop=0)
+    hist = S.concat([hist, plain])
+    dp = RefDatapath(t)
+    run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    # inbound flows to the endpoint (ipv6_policy's entries carry the
+    # endpoint address's rev_nat_index): the test stream's egress replies
+    # to them are reverse-NATed (bpf_lxc.c:255-266)
+    inb = S.gen_headers_v6(rng, 400, t.ipcache[t.ipcache["family"] == 2],
+                           S.local_v6_addrs(t)[:1], local_frac=1.0, mark_host=0,
+                           mark_proxy=0, ext=0, exthdr_drop=0)
+    inb.proto[:] = np.where(rng.random(len(inb)) < 0.6, S.IPPROTO_TCP, S.IPPROTO_UDP)
+    ires = run(dp, inb, MODE_INGRESS)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    fw_in = np.flatnonzero(ires[0] != 2)
+    replies = S.reverse(S.take(inb, fw_in[rng.integers(0, len(fw_in), size=int(n * 0.1))]))
+    est = S.take(hist, rng.integers(0, 1000, size=int(n * 0.4)))
+    est.flags[(rng.random(len(est)) < 0.05) & (est.proto == S.IPPROTO_TCP)] |= \
+        np.uint8(S.HF_TCP_CLOSE)
+    parts = [est, replies, _svc_flows6(rng, int(n * 0.35), vips, ports, protos, 40000),
+             S.gen_headers_v6(rng, int(n * 0.15), t.ipcache[t.ipcache["family"] == 2],
+                              S.local_v6_addrs(t), local_frac=0.3, mark_host=0,
+                              mark_proxy=0, src_fixed=S.LXC_IPV6, ext=0,
+                              exthdr_drop=0)]
+    h = S.concat(parts)
+    h = S.take(h, rng.permutation(len(h)))
+    h.hash = None
+    h = _no_hazard(t, h, MODE_EGRESS, S.EP_LXC_ID)
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
+def sc_lb_reply_v6(n=3000, seed=53):
+    """Replies of load-balanced IPv6 flows from the backends (from-netdev,
+    then the client endpoint's ipv6_policy): CT_REPLY on the entries the
+    egress path created and lb6_rev_nat of every hit carrying a
+    rev_nat_index (bpf_lxc.c:808-815); plus new inbound traffic."""
+    t, rng, vips, ports, protos = _lb_setup6(seed)
+    hist = _svc_flows6(rng, 1200, vips, ports, protos, 20000)
+    dp = RefDatapath(t)
+    hres = run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    pk = hres[8]
+    src = np.ascontiguousarray(pk[:, 0:4]).view(np.uint8).reshape(-1, 16)
+    dst = np.ascontiguousarray(pk[:, 4:8]).view(np.uint8).reshape(-1, 16)
+    fw = (hres[0] != 2) & (src == S.LXC_IPV6).all(1) & (hist.proto != S.IPPROTO_ICMPV6)
+    idx = np.flatnonzero(fw)
+    m = int(n * 0.7)
+    pick = idx[rng.integers(0, len(idx), size=m)]
+    rep = S.Headers(6, dst[pick].copy(), src[pick].copy(),
+                    (pk[pick, 8] >> 16).astype(np.uint16),
+                    (pk[pick, 8] & 0xFFFF).astype(np.uint16),
+                    hist.proto[pick].copy(), np.zeros(m, np.uint8),
+                    rng.integers(100, 1500, size=m).astype(np.uint16),
+                    np.zeros(m, np.uint32))
+    rep.flags[(rng.random(m) < 0.05) & (rep.proto == S.IPPROTO_TCP)] |= np.uint8(S.HF_TCP_CLOSE)
+    new = S.gen_headers_v6(rng, n - m, t.ipcache[t.ipcache["family"] == 2],
+                           S.local_v6_addrs(t)[:1], local_frac=1.0, mark_host=0,
+                           mark_proxy=0, ext=0, exthdr_drop=0)
+    h = S.concat([rep, new])
+    h = S.take(h, rng.permutation(len(h)))
+    h = _no_hazard(t, h, MODE_INGRESS, None)
+    return t, h, MODE_INGRESS, None, dp
+
+
 SCENARIOS = {
     "edge_ingress_v4": sc_edge_ingress,
     "small_ingress_v4": sc_small_ingress,
@@ -1166,6 +1334,8 @@ SCENARIOS = {
     "ct_egress_v6": lambda: _ct_scenario(6, MODE_EGRESS, 24),
     "lb_egress_v4": sc_lb_egress,
     "lb_reply_v4": sc_lb_reply,
+    "lb_egress_v6": sc_lb_egress_v6,
+    "lb_reply_v6": sc_lb_reply_v6,
 }
 
 

@@ -129,6 +129,8 @@ def lib():
         L.cfo_set_clock.restype = None
         L.cfo_lb4_service_add.argtypes = [vp, vp, vp]
         L.cfo_lb4_revnat_add.argtypes = [vp, ctypes.c_uint16, vp]
+        L.cfo_lb6_service_add.argtypes = [vp, vp, vp]
+        L.cfo_lb6_revnat_add.argtypes = [vp, ctypes.c_uint16, vp]
         L.cfo_set_lb_io.argtypes = [vp, vp, vp]
         L.cfo_set_lb_io.restype = None
         L.cfo_ipcache_lookup.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp, vp, vp]
@@ -202,6 +204,17 @@ class Oracle:
             for r in np.asarray(t.revnat4):
                 v, keep = _u8p(np.frombuffer(r.tobytes()[2:8], np.uint8))
                 L.cfo_lb4_revnat_add(h, int(r["index"]), ctypes.cast(v, ctypes.c_void_p))
+        if getattr(t, "lb6", None) is not None:   # (LB6_DT: key 20 B, value 24 B)
+            for r in np.asarray(t.lb6):
+                b = r.tobytes()
+                k, kk = _u8p(np.frombuffer(b[:20], np.uint8))
+                v, vk = _u8p(np.frombuffer(b[20:44], np.uint8))
+                L.cfo_lb6_service_add(h, ctypes.cast(k, ctypes.c_void_p),
+                                      ctypes.cast(v, ctypes.c_void_p))
+        if getattr(t, "revnat6", None) is not None:   # (REVNAT6_DT: index, 18 B)
+            for r in np.asarray(t.revnat6):
+                v, keep = _u8p(np.frombuffer(r.tobytes()[2:20], np.uint8))
+                L.cfo_lb6_revnat_add(h, int(r["index"]), ctypes.cast(v, ctypes.c_void_p))
 
     def node_config(self, v4_cluster_range, v4_cluster_mask, router_ip6,
                     host_ifindex=1):
@@ -233,7 +246,7 @@ class Oracle:
 
     def _lb_io(self, hdr, pkt=None):
         hs = getattr(hdr, "hash", None)
-        hs = None if hs is None or hdr.family != 4 else np.ascontiguousarray(hs, np.uint32)
+        hs = None if hs is None else np.ascontiguousarray(hs, np.uint32)
         self._lb_keep = hs
         self.L.cfo_set_lb_io(self.h, _p(hs), _p(pkt))
 
@@ -243,8 +256,9 @@ class Oracle:
         apply_ct folds the batch's CT creates/deletes into the oracle's CT
         maps afterwards (what the engine's cfc_ct_apply does); notify is the
         drop-notify site word per header (res_t.nt in cfc_oracle.c); pkt
-        (IPv4) the packet's (saddr, daddr, sport | dport << 16) after the
-        service translation and reverse NAT, (n, 3) u32."""
+        the packet's (saddr, daddr, sport | dport << 16) after the service
+        translation and reverse NAT: (n, 3) u32 for IPv4, (n, 9) u32 for IPv6
+        (saddr and daddr as four raw words each)."""
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
@@ -259,7 +273,7 @@ class Oracle:
         fn = self.L.cfo_classify_v4 if hdr.family == 4 else self.L.cfo_classify_v6
         nt = np.zeros(n, np.uint32) if want_notify else None
         self.mon = np.zeros(n, np.uint32)
-        pkt = np.zeros((n, 3), np.uint32) if want_pkt else None
+        pkt = np.zeros((n, 3 if hdr.family == 4 else 9), np.uint32) if want_pkt else None
         self.L.cfo_set_notify_out(self.h, _p(nt), _p(self.mon))
         self._lb_io(hdr, pkt)
         fn(self.h, mode, ep_lxc, n, *[_p(a) for a in arrs], _p(act), _p(ver),

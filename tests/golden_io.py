@@ -16,6 +16,15 @@ def names():
 
 
 class Golden:
+    def pkt_addrs(self):
+        """The packet's (saddr, daddr) as the programs left them, in the
+        header batch's address format (IPv4 u32, IPv6 (n, 16) bytes)."""
+        if self.headers.family == 4:
+            return self.pkt[:, 0], self.pkt[:, 1]
+        p = np.ascontiguousarray(self.pkt)
+        return (np.ascontiguousarray(p[:, 0:4]).view(np.uint8).reshape(-1, 16),
+                np.ascontiguousarray(p[:, 4:8]).view(np.uint8).reshape(-1, 16))
+
     def __init__(self, name):
         self.name = name
         d = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
@@ -30,6 +39,9 @@ class Golden:
         if "lb4" in d.files:   # service load balancing (LB4_DT, REVNAT4_DT)
             self.tables.lb4 = d["lb4"]
             self.tables.revnat4 = d["revnat4"]
+        if "lb6" in d.files:   # (LB6_DT, REVNAT6_DT)
+            self.tables.lb6 = d["lb6"]
+            self.tables.revnat6 = d["revnat6"]
         # CT maps after the stream, oracle row format (None: no CT state)
         self.ct_after = d["x_ct"] if "x_ct" in d.files else None
         self.headers = S.Headers(int(d["h_family"]), d["h_saddr"], d["h_daddr"],
@@ -42,6 +54,8 @@ class Golden:
         self.hash_ok = d["x_hash_ok"] if "x_hash_ok" in d.files else None
         if self.hash_ok is not None:
             self.headers.hash = d["x_hash"]
+        # ((n, 3) u32 for IPv4; (n, 9) for IPv6: saddr and daddr as four
+        # raw words each, then the L4 word)
         self.pkt = d["x_pkt"] if "x_pkt" in d.files else None
         # the cilium_events perf-ring samples (trace_notify / drop_notify,
         # 32 bytes each, EVENT_DT) and the header of each; None in older
@@ -124,10 +138,13 @@ def lpm_identity(g: Golden):
     if g.mode == 1:
         col = np.full(n, 1)
         da = np.asarray(g.headers.daddr)
-        if g.pkt is not None:   # lb4_local: the tuple's daddr is the backend
+        if g.pkt is not None and v4:   # lb4_local: the tuple's daddr is the backend
             loop = g.pkt[:, 0] == S.IPV4_LOOPBACK
             col = np.where(loop, 1, 3)
             da = np.where(loop, np.asarray(g.headers.daddr, np.uint32), g.pkt[:, 1])
+        elif g.pkt is not None:        # lb6_local (no loopback case)
+            col = np.full(n, 3)
+            da = g.pkt_addrs()[1]
         l, h = lab[np.arange(n), col], hit[np.arange(n), col]
         if v4:
             cluster = (np.asarray(da, np.uint32) & 0xFF0000) == 0x100000

@@ -121,3 +121,99 @@ def test_two_rank_shards_and_counter_allreduce():
     np.testing.assert_array_equal(gidx, idx.astype(np.int64))
     np.testing.assert_array_equal(grec.view(np.uint8).reshape(-1),
                                   rec.view(np.uint8))
+
+
+def _sorted_rows(rows):
+    rows = np.asarray(rows, np.uint8)
+    if not len(rows):
+        return rows
+    order = np.lexsort(rows.T[::-1])
+    return rows[order]
+
+
+def _ct_worker(rank, world, port, family, q):
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from cilium_amd.distributed import shard_ct, shard_headers
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t, h, mode = _ct_case(family)
+        t.ct = shard_ct(t.ct, rank, world)
+        o = O.Oracle(t)
+        vers = []
+        for a, b in _ct_batches(len(h)):
+            part, idx = shard_headers(h.slice(a, b), rank, world)
+            _, ver, _, _ = o.classify(part, mode, 0, want_ct=True, apply_ct=True)
+            vers.append((idx + a, ver))
+        rows = o.ct_dump()
+        # every rank's CT rows to rank 0 (uint8 rows travel as int64 words)
+        n = torch.tensor([len(rows)], dtype=torch.int64)
+        counts = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(counts, n)
+        cmax = max(int(c) for c in counts)
+        buf = np.zeros((max(cmax, 1), 104), np.uint8)
+        buf[:len(rows)] = rows
+        tb = torch.from_numpy(buf.view(np.int64).copy())
+        got = [torch.zeros_like(tb) for _ in range(world)] if rank == 0 else None
+        dist.gather(tb, got, dst=0)
+        union = None
+        if rank == 0:
+            union = np.concatenate([g.numpy().view(np.uint8).reshape(-1, 104)[:int(c)]
+                                    for g, c in zip(got, counts)])
+        q.put((rank, vers, union))
+    finally:
+        dist.destroy_process_group()
+
+
+def _ct_case(family):
+    if family == 4:
+        t, flows = S.config_c5(5, n_flows=20_000, n_prefixes=20_000, n_policy=2000)
+        return t, S.headers_c5(t, flows, 60_000, seed=13), 0
+    t, flows = S.config_c5_v6(6, n_flows=10_000, n_prefixes=10_000, n_policy=2000)
+    return t, S.headers_c5_v6(t, flows, 40_000, seed=14), 3
+
+
+def _ct_batches(n):
+    return [(0, n // 2), (n // 2, n)]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("family", [4, 6])
+def test_two_rank_conntrack_shards(family):
+    """CT across GPUs: each rank takes the
+    headers and CT entries of the address pairs it owns
+    (distributed.shard_headers / shard_ct) and applies its own CT writes,
+    batch by batch.  After two applied batches the ranks' CT maps together
+    are, byte for byte, the single-rank result of the same two batches, and
+    every header's verdict is the single-rank verdict."""
+    import oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ct_worker, args=(r, world, port, family, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    t, h, mode = _ct_case(family)
+    o = O.Oracle(t)
+    want_ver = np.empty(len(h), np.int32)
+    for a, b in _ct_batches(len(h)):
+        _, ver, _, _ = o.classify(h.slice(a, b), mode, 0, want_ct=True, apply_ct=True)
+        want_ver[a:b] = ver
+    got_ver = np.full(len(h), 12345, np.int32)
+    for r in res:
+        for idx, ver in r[1]:
+            got_ver[idx] = ver
+    np.testing.assert_array_equal(got_ver, want_ver)
+    want = _sorted_rows(o.ct_dump())
+    got = _sorted_rows(res[0][2])
+    assert len(want) > 1000
+    np.testing.assert_array_equal(got, want)

@@ -110,3 +110,93 @@ def test_two_ranks_allreduce_counters_on_gpu(mode):
         np.testing.assert_array_equal(r[5], idrows)
     # both ranks hold the same all-reduced block
     np.testing.assert_array_equal(res[0][6], res[1][6])
+
+
+def _ct_case(family):
+    if family == 4:
+        t, flows = S.config_c5(5, n_flows=200_000, n_prefixes=50_000, n_policy=4000)
+        return t, S.headers_c5(t, flows, 800_000, seed=23), 0
+    t, flows = S.config_c5_v6(6, n_flows=100_000, n_prefixes=50_000, n_policy=4000)
+    return t, S.headers_c5_v6(t, flows, 400_000, seed=24), 3
+
+
+def _ct_worker(rank, world, port, family, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cilium_amd.datapath import Datapath, pack
+        from cilium_amd.distributed import shard_ct, shard_headers
+        from cilium_amd.loader import ct_rows, load_tables
+        torch.cuda.set_device(0)
+        t, h, mode = _ct_case(family)
+        t.ct = shard_ct(t.ct, rank, world)
+        dp = Datapath(0)
+        load_tables(dp, t)
+        vers = []
+        n = len(h)
+        for a, b in ((0, n // 2), (n // 2, n)):
+            part, idx = shard_headers(h.slice(a, b), rank, world)
+            bt = pack(part)
+            out = dp.classify(bt, mode, 0, want_ct=True)
+            dp.ct_apply(bt, out, mode, 0)
+            torch.cuda.synchronize()
+            vers.append((idx + a, out.verdict.cpu().numpy()))
+        rows = np.asarray(ct_rows(dp, dp.ct_fds), np.uint8).reshape(-1, 104)
+        st = dp.stats()
+        dp.close()
+        q.put((rank, vers, rows, st["ct_apply_device"], st["ct_apply_host"]))
+    except BaseException as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("family", [4, 6])
+def test_two_ranks_conntrack_shards_on_gpu(family):
+    """CT across GPUs on hardware: two ranks on the one GPU,
+    each owning the address pairs distributed.shard_headers / shard_ct give
+    it, classify and apply their CT writes on the device for two batches.
+    Their CT maps together equal the single-rank oracle's after the same two
+    batches byte for byte, and every verdict is the single-rank one."""
+    import oracle as O
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_ct_worker, args=(r, world, port, family, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = [q.get(timeout=300) for _ in range(world)]
+    finally:
+        for p in ps:
+            p.join(60)
+            if p.exitcode is None:
+                p.kill()
+    for r in res:
+        assert len(r) > 2, f"rank {r[0]} failed: {r[1]}"
+        assert (r[3], r[4]) == (2, 0)   # both batches on the device path
+    t, h, mode = _ct_case(family)
+    o = O.Oracle(t)
+    n = len(h)
+    want = np.empty(n, np.int32)
+    for a, b in ((0, n // 2), (n // 2, n)):
+        _, ver, _, _ = o.classify(h.slice(a, b), mode, 0, nthreads=16, want_ct=True,
+                                  apply_ct=True)
+        want[a:b] = ver
+    got = np.full(n, 12345, np.int32)
+    for r in res:
+        for idx, ver in r[1]:
+            got[idx] = ver
+    np.testing.assert_array_equal(got, want)
+
+    def srt(rows):
+        return rows[np.lexsort(rows.T[::-1])]
+    union = np.concatenate([r[2] for r in res])
+    np.testing.assert_array_equal(srt(union), srt(o.ct_dump()))

@@ -455,3 +455,33 @@ def test_node_config_runtime(torch):
     _, ov, oi = o.classify(h6, 1, S.EP_LXC_ID)
     assert (ov == L.VERDICT_PUNT).sum() >= len(k) // 2
     assert (oi == S.CLUSTER_ID).sum() > 1000
+
+
+@pytest.mark.parametrize("apply", ["device", "host"])
+@pytest.mark.parametrize("mode", [0, 3])
+def test_c5_v6_conntrack_vs_oracle(torch, mode, apply):
+    """IPv6 conntrack writes (ct_create6 / ct_delete6 / timers, conntrack.h:
+    615-662) on the device CT6 table: 100k live IPv6 flows, Zipf traffic,
+    three batches each folded into CT before the next; outputs, CT bytes,
+    counters and every CT6 entry (rev_nat_index, accounting) bit-exact
+    against the oracle, and no batch on the host walk."""
+    t, flows = S.config_c5_v6(6, n_flows=100_000, n_prefixes=50_000)
+    h = S.headers_c5_v6(t, flows, 600_000, seed=41)
+    compare_with_oracle(
+        torch, t, h, mode, chunks=3,
+        ct_apply=L.CT_APPLY_DEVICE if apply == "device" else L.CT_APPLY_HOST)
+    st = run_gpu.stats
+    assert (st["ct_apply_device"], st["ct_apply_host"]) == ((3, 0) if apply == "device"
+                                                             else (0, 3))
+
+
+def test_c5_v6_egress_and_local_ct(torch):
+    """IPv6 egress with local delivery (the sender's and the receiver's CT6
+    maps), the reference's ct_egress_v6 stream three times over in two
+    batches, on the device table."""
+    g = G.Golden("ct_egress_v6")
+    rng = np.random.default_rng(6)
+    h = S.concat([g.headers] * 3)
+    h = S.take(h, rng.permutation(len(h)))
+    compare_with_oracle(torch, g.tables, h, g.mode, ep_lxc=g.ep_lxc, chunks=2)
+    assert run_gpu.stats["ct_apply_host"] == 0

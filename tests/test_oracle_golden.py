@@ -262,9 +262,7 @@ def test_oracle_lpm_matches_kernel(name):
     g = G.Golden(name)
     o = O.Oracle(g.tables)
     h = g.headers
-    cols = [h.saddr, h.daddr,
-            h.saddr if g.pkt is None else g.pkt[:, 0],
-            h.daddr if g.pkt is None else g.pkt[:, 1]]
+    cols = [h.saddr, h.daddr] + ([h.saddr, h.daddr] if g.pkt is None else list(g.pkt_addrs()))
     for c, a in enumerate(cols):
         lab, hit = o.ipcache_lookup(h.family, a)
         np.testing.assert_array_equal(hit, g.lpm_hit[:, c], err_msg=f"hit, column {c}")
@@ -308,6 +306,16 @@ def test_lb_goldens_cover_the_service_path():
     assert any(int(x) in vips for x in g.pkt[:, 0])             # egress rev NAT
     r = G.Golden("lb_reply_v4")
     assert sum(int(x) in vips for x in r.pkt[:, 0]) > 1000      # ingress rev NAT
+    # IPv6 (lb6_local has no loopback case)
+    assert {"lb_egress_v6", "lb_reply_v6"} <= set(LB_NAMES)
+    g = G.Golden("lb_egress_v6")
+    vips6 = {bytes(a) for a in g.tables.lb6["addr"]}
+    psa, pda = g.pkt_addrs()
+    assert (pda != g.headers.daddr).any(1).sum() > 1000           # translated
+    assert (g.verdict == -158).any()                              # no backend
+    assert any(bytes(a) in vips6 for a in psa)                    # egress rev NAT
+    r = G.Golden("lb_reply_v6")
+    assert sum(bytes(a) in vips6 for a in r.pkt_addrs()[0]) > 1000   # ingress rev NAT
 
 
 @pytest.mark.parametrize("name", LB_NAMES)
