@@ -77,7 +77,7 @@ class HdrV4(ctypes.Structure):
 
 
 class HdrV6(ctypes.Structure):
-    _fields_ = _HDR
+    _fields_ = _HDR + [("hash", ctypes.c_void_p)]
 
 
 class Out(ctypes.Structure):

@@ -117,13 +117,13 @@ struct GEp {           // endpoints + policy (+ the counter layout)
     uint64_t bytes = 0;
 };
 struct GLb {           // load balancing: services, reverse NAT
-    DevBuf lb4, rnat4;
-    uint32_t lb4_mask = 0, n_lb4 = 0;
+    DevBuf lb4, rnat4, lb6, rnat6;
+    uint32_t lb4_mask = 0, n_lb4 = 0, lb6_mask = 0, n_lb6 = 0;
     uint64_t bytes = 0;
 };
 struct GCt {           // conntrack
     DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
-    DevBuf ct4_lb;                        // per-slot LB state (with a load balancer)
+    DevBuf ct4_lb, ct6_lb;                // per-slot LB state (with a load balancer)
     DevBuf ct4_info, ct4_mark, ct4_sum;   // device CT apply state (ctapply.hip)
     DevBuf ct6_info, ct6_mark, ct6_sum;
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
@@ -289,7 +289,7 @@ void group_sigs(cfc_ctx *c, uint64_t sig[NGROUPS])
             mix(3, id); mix(3, m->sgen[0]);
             mix(2, id);   // endpoints see which CT maps exist
             break;
-        case ROLE_LB4_SVC: case ROLE_LB4_RNAT:
+        case ROLE_LB4_SVC: case ROLE_LB4_RNAT: case ROLE_LB6_SVC: case ROLE_LB6_RNAT:
             mix(5, id); mix(5, m->gen);
             // the CT table carries each entry's LB state while a load
             // balancer is configured
@@ -912,11 +912,15 @@ std::shared_ptr<GEp> build_ep(cfc_ctx *c, HostImage &img, const std::vector<Map 
 std::shared_ptr<GLb> build_lbg(const HostImage &img, hipStream_t s, int *rc)
 {
     auto g = std::make_shared<GLb>();
-    if ((*rc = upload_vec(g->lb4, img.lb4, s)) || (*rc = upload_vec(g->rnat4, img.rnat4, s)))
+    if ((*rc = upload_vec(g->lb4, img.lb4, s)) || (*rc = upload_vec(g->rnat4, img.rnat4, s)) ||
+        (*rc = upload_vec(g->lb6, img.lb6, s)) || (*rc = upload_vec(g->rnat6, img.rnat6, s)))
         return nullptr;
     g->lb4_mask = img.lb4_mask;
     g->n_lb4 = img.n_lb4;
-    g->bytes = 16ull * img.lb4.size() + 8ull * img.rnat4.size();
+    g->lb6_mask = img.lb6_mask;
+    g->n_lb6 = img.n_lb6;
+    g->bytes = 16ull * img.lb4.size() + 8ull * img.rnat4.size() + 16ull * img.lb6.size() +
+               16ull * img.rnat6.size();
     return g;
 }
 
@@ -927,7 +931,8 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     if ((*rc = upload_vec(g->ct4, img.ct4, s)) || (*rc = upload_vec(g->ct6, img.ct6, s)) ||
         (*rc = upload_vec(g->ct4_tm, img.ct4_tm, s)) ||
         (*rc = upload_vec(g->ct6_tm, img.ct6_tm, s)) ||
-        (*rc = upload_vec(g->ct4_lb, img.ct4_lb, s)))
+        (*rc = upload_vec(g->ct4_lb, img.ct4_lb, s)) ||
+        (*rc = upload_vec(g->ct6_lb, img.ct6_lb, s)))
         return nullptr;
     const size_t nslots = img.ct4.size() + img.ct6.size();
     if (nslots && (*rc = g->ct_acct.zeros(32 * nslots, s)))
@@ -1010,6 +1015,10 @@ void assemble(Epoch &E)
     T.lb4_mask = B.lb4_mask;
     T.rnat4 = (const uint2 *)B.rnat4.p;
     T.ct4_lb = T.ct4 ? (const uint4 *)C.ct4_lb.p : nullptr;
+    T.lb6 = B.n_lb6 ? (const uint4 *)B.lb6.p : nullptr;
+    T.lb6_mask = B.lb6_mask;
+    T.rnat6 = (const uint4 *)B.rnat6.p;
+    T.ct6_lb = T.ct6 ? (const uint4 *)C.ct6_lb.p : nullptr;
     cfc_stats &st = E.st;
     st = cfc_stats{};
     st.epoch = E.id;
@@ -1247,10 +1256,12 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
                     zero_acct(acct);   // deleted and created again
                 }
                 put(tm + at, &v);
-                if (!v6) {
-                    const uint4 l = ct_lb_of(it->second.val);
-                    if (G.ct4_lb.p)
-                        put((uint4 *)G.ct4_lb.p + at, &l);
+                const uint4 l = ct_lb_of(it->second.val);
+                if (!v6 && G.ct4_lb.p)
+                    put((uint4 *)G.ct4_lb.p + at, &l);
+                if (v6 && G.ct6_lb.p) {
+                    const uint4 l6 = make_uint4(l.x & 0xFFFF, l.y, 0, 0);
+                    put((uint4 *)G.ct6_lb.p + at, &l6);
                 }
             } else if (at >= 0) {       // delete
                 if (v6) {
@@ -1837,7 +1848,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.pol_mask = it->second.mask;
     }
     const WsLayout wl = ws_layout(in->n, E.T, mode,
-                                  E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4);
+                                  E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4 ||
+                                      E.T.lb6 || E.T.rnat6);
     const size_t need = wl.total;
     c->last_cls.valid = false;
     if (need > c->ws_bytes) {
@@ -1941,8 +1953,7 @@ int drop_notify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     a.ports = in->ports;
     a.saddr = reinterpret_cast<const uint32_t *>(in->saddr);
     a.daddr = reinterpret_cast<const uint32_t *>(in->daddr);
-    if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value)
-        a.hash = in->hash;
+    a.hash = in->hash;
     a.n = in->n;
     a.family = family;
     a.mode = mode;
@@ -2333,6 +2344,140 @@ uint32_t flow_hash4_host(uint32_t sa, uint32_t da, uint32_t pt, uint32_t proto)
     return fmix32(lo * 0x9E3779B1u + hi * 0x85EBCA77u + pw * 0xC2B2AE3Du + proto);
 }
 
+// IPv6 (cilium_lb6_services / cilium_lb6_reverse_nat) for the apply's
+// replay of ipv6_l3_from_lxc's service step (bpf_lxc.c:149-167)
+struct LbHost6 {
+    const Map *svc = nullptr, *rnat = nullptr;
+    explicit LbHost6(cfc_ctx *c)
+    {
+        for (auto &kv : c->maps) {
+            if (kv.second->role == ROLE_LB6_SVC)
+                svc = kv.second.get();
+            else if (kv.second->role == ROLE_LB6_RNAT)
+                rnat = kv.second.get();
+        }
+    }
+    bool on() const { return (svc && !svc->kv.empty()) || (rnat && !rnat->kv.empty()); }
+    // struct lb6_service {target[16], port, count, rev_nat_index, weight}
+    struct Svc {
+        uint8_t target[16];
+        uint16_t port, count, rev_nat, weight;
+    };
+    bool get(const uint8_t *addr, uint16_t dport, uint16_t slave, Svc *v) const
+    {
+        if (!svc)
+            return false;
+        char k[20];
+        memcpy(k, addr, 16);
+        memcpy(k + 16, &dport, 2);
+        memcpy(k + 18, &slave, 2);
+        auto it = svc->kv.find(std::string(k, 20));
+        if (it == svc->kv.end() || it->second.val.size() < 24)
+            return false;
+        memcpy(v, it->second.val.data(), 24);
+        return true;
+    }
+    // lb6_lookup_service (lb.h:352-381)
+    bool service(const uint8_t *addr, uint16_t &dport, uint16_t slave, Svc *v) const
+    {
+        if (dport) {
+            if (get(addr, dport, slave, v) && v->count)
+                return true;
+            dport = 0;
+        }
+        return get(addr, 0, slave, v) && v->count;
+    }
+    // lb6_rev_nat (lb.h:306-319, flags 0) on a packet
+    void rev_nat(uint16_t index, uint8_t proto, uint8_t *sa, uint32_t &pt) const
+    {
+        if (!index || !rnat)
+            return;
+        auto it = rnat->kv.find(std::string((const char *)&index, 2));
+        if (it == rnat->kv.end() || it->second.val.size() < 18)
+            return;
+        uint16_t port;
+        memcpy(&port, it->second.val.data() + 16, 2);
+        if (port && (proto == 6 || proto == 17))
+            pt = (pt & 0xFFFF0000u) | port;
+        memcpy(sa, it->second.val.data(), 16);
+    }
+};
+
+// cfc.h CFC_FLOW_HASH over IPv6 addresses (kern_common.hpp flow_hash6)
+uint32_t fold6_host(const uint8_t *a)
+{
+    uint32_t w[4];
+    memcpy(w, a, 16);
+    uint32_t h = fmix32(w[3]);
+    h = fmix32(w[2] ^ h);
+    h = fmix32(w[1] ^ h);
+    return fmix32(w[0] ^ h);
+}
+
+// what lb6_local leaves (lb.h:427-481): the CT_SERVICE tuple and ct_state
+struct LbState6 {
+    bool svc = false, drop = false, reslave = false;
+    uint8_t tda[16];
+    uint16_t slave0 = 0, slave = 0, rev_nat = 0;
+    std::string ksvc;
+};
+LbState6 lb6_step(const LbHost6 &L, Map *m, const uint8_t *sa, const uint8_t *da, uint32_t &pt,
+                  uint8_t proto, uint32_t hash)
+{
+    LbState6 x;
+    memcpy(x.tda, da, 16);
+    const bool l4 = proto == 6 || proto == 17;
+    if (!L.svc || (!l4 && proto != 58))
+        return x;
+    uint16_t kd = l4 ? (uint16_t)(pt >> 16) : 0;
+    LbHost6::Svc v, b;
+    if (!L.service(da, kd, 0, &v))
+        return x;
+    x.svc = true;
+    uint16_t td, ts;
+    uint8_t fl = 4;   // TUPLE_F_SERVICE
+    if (l4) {
+        td = (uint16_t)(pt & 0xFFFF);
+        ts = (uint16_t)(pt >> 16);
+    } else {
+        const uint32_t type = pt & 0xFF;
+        const bool rel = type >= 1 && type <= 4;
+        td = (!rel && type == 129) ? 128 : 0;
+        ts = (!rel && type == 128) ? 128 : 0;
+        fl |= rel ? 2 : 0;
+    }
+    char k[38];
+    memcpy(k, da, 16);
+    memcpy(k + 16, sa, 16);
+    memcpy(k + 32, &td, 2);
+    memcpy(k + 34, &ts, 2);
+    k[36] = (char)proto;
+    k[37] = (char)fl;
+    x.ksvc.assign(k, 38);
+    auto it = m ? m->kv.find(x.ksvc) : decltype(m->kv.end()){};
+    if (m && it != m->kv.end()) {   // ct_state from the entry
+        CtEntry e;
+        memcpy(&e, it->second.val.data(), sizeof(e));
+        x.slave = e.slave;
+    } else {
+        x.slave = (uint16_t)(hash % v.count + 1);   // lb6_select_slave
+    }
+    x.slave0 = x.slave;
+    if (!L.get(da, kd, x.slave, &b)) {
+        if (!L.service(da, kd, x.slave, &b)) {
+            x.drop = true;
+            return x;
+        }
+        x.slave = (uint16_t)(hash % b.count + 1);
+        x.reslave = true;
+    }
+    x.rev_nat = b.rev_nat;
+    memcpy(x.tda, b.target, 16);
+    if (b.port && kd != b.port && l4)   // lb6_xlate
+        pt = (pt & 0xFFFFu) | (uint32_t)b.port << 16;
+    return x;
+}
+
 // the ct_state lb4_local leaves for ct_create4 (common.h:452-461)
 struct LbState {
     bool svc = false, drop = false, reslave = false;
@@ -2484,7 +2629,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
         return 1;
-    if (!V6 && LbHost(c).on())   // service entries and reverse NAT: the host walk
+    if (V6 ? LbHost6(c).on() : LbHost(c).on())   // service entries, reverse NAT: the host walk
         return 1;
     // the device table must be the maps as committed: no host-side CT
     // change waiting for a commit
@@ -2696,18 +2841,18 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     std::vector<uint32_t> hs;
-    if constexpr (std::is_same<Hdr, cfc_hdr_v4>::value) {
-        if (in->hash) {
-            hs.resize(n);
-            if (hipMemcpyAsync(hs.data(), in->hash, 4 * n, hipMemcpyDeviceToHost, s) !=
-                    hipSuccess ||
-                hipStreamSynchronize(s) != hipSuccess)
-                return -EIO;
-        }
+    if (in->hash) {
+        hs.resize(n);
+        if (hipMemcpyAsync(hs.data(), in->hash, 4 * n, hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
     }
     CtApply A(c, family);
     const LbHost L(c);
     const bool lbon = family == 4 && L.on();
+    const LbHost6 L6(c);
+    const bool lb6on = family == 6 && L6.on();
     const uint32_t now = c->now;
     const uint8_t icmp = family == 4 ? 1 : 58;
     const uint32_t echo = family == 4 ? 8 : 128, echo_reply = family == 4 ? 0 : 129;
@@ -2734,8 +2879,10 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         const uint32_t proto = mt[i] & 0xFF, len = mt[i] >> 16;
         const bool is_tcp = proto == 6, syn = (mt[i] & CFC_HF_TCP_CLOSE) != 0;
         const uint8_t tflags = is_tcp ? tf[i] : 0;
-        // lb4_local created its CT_SERVICE entry before it found no backend
-        const bool no_svc = lbon && mode == CFC_MODE_EGRESS && ver[i] == -158;   // DROP_NO_SERVICE
+        // lb4_local / lb6_local created its CT_SERVICE entry before it found
+        // no backend
+        const bool no_svc = (lbon || lb6on) && mode == CFC_MODE_EGRESS &&
+                            ver[i] == -158;   // DROP_NO_SERVICE
         if (!(cb & (CFC_CT_DONE | CFC_CT_DONE << 4)) && !no_svc)
             continue;
         const uint8_t *s_ = &sa[al * i], *d_ = &da[al * i];
@@ -2789,6 +2936,54 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 }
             }
         }
+        // IPv6: lb6_local's CT_SERVICE entry, and the tuple / packet it
+        // leaves (no loopback case: the packet's daddr is the tuple's)
+        uint8_t t6da[16], p6sa[16], p6da[16];
+        uint32_t p6pt = pt[i];
+        memcpy(p6sa, s_, al == 16 ? 16 : 0);
+        memcpy(t6da, d_, al == 16 ? 16 : 0);
+        LbState6 x6;
+        if (lb6on && mode == CFC_MODE_EGRESS && ((cb & CFC_CT_DONE) || no_svc)) {
+            Map *m0 = A.ct_map((int)ep_lxc, proto != 6);
+            const uint32_t h = hs.empty() ? flow_hash4_host(fold6_host(s_), fold6_host(d_), pt[i],
+                                                            proto)
+                                          : hs[i];
+            x6 = lb6_step(L6, m0, s_, d_, p6pt, (uint8_t)proto, h);
+            if (x6.svc) {
+                memcpy(t6da, x6.tda, 16);
+                x.drop = x6.drop;
+            }
+            if (x6.svc && m0) {   // the CT_SERVICE entry: hit (updated) or created
+                const uint32_t type = pt[i] & 0xFF;
+                const int act = proto == 6 ? (syn ? 2 : 1) : proto == 17 ? 1
+                                : ((type >= 1 && type <= 4) || type == 129) ? 0 : 1;
+                auto it = m0->kv.find(x6.ksvc);
+                if (it != m0->kv.end()) {
+                    ct_hit_update(m0, it->second, act, 0, true, len, now, is_tcp, syn, tflags);
+                    if (x6.reslave && !x6.drop)   // ct_update6_slave
+                        memcpy(&it->second.val[40], &x6.slave, 2);
+                } else {
+                    CtEntry e{};
+                    e.slave = x6.slave0;
+                    ct_upd_timeout(e, now, is_tcp, 0, is_tcp, 0);
+                    e.tx_packets = 1;
+                    e.tx_bytes = len;
+                    CtEntry es = e;
+                    if (x6.reslave && !x6.drop)
+                        es.slave = x6.slave;
+                    put_new(m0, x6.ksvc, es);
+                    std::string ki = x6.ksvc;
+                    memset(&ki[32], 0, 4);
+                    ki[36] = (char)icmp;
+                    ki[37] = (char)(4 | 2);
+                    e.bits |= CTB_SEEN_NON_SYN;
+                    if (m0->kv.count(ki))
+                        ct_drop_counts(c, m0, ki, s);
+                    put_new(m0, ki, e);
+                }
+            }
+        }
+        memcpy(p6da, t6da, al == 16 ? 16 : 0);
         if (x.drop)
             continue;
         const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
@@ -2805,8 +3000,12 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 ks = eg ? (const uint8_t *)&tsa : (const uint8_t *)&psa;
                 kd_ = eg ? (const uint8_t *)&tda : (const uint8_t *)&pda;
                 kp = eg ? tpt : ppt;
+            } else if (lb6on) {
+                ks = eg ? s_ : p6sa;
+                kd_ = eg ? t6da : p6da;
+                kp = p6pt;
             }
-            const int dst = A.endpoint(family == 4 ? (const uint8_t *)&pda : d_);
+            const int dst = A.endpoint(family == 4 ? (const uint8_t *)&pda : lb6on ? p6da : d_);
             Map *m = A.ct_map(eg ? (int)ep_lxc : dst, proto != 6);
             if (!m)
                 continue;
@@ -2854,6 +3053,11 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                         memcpy(&e, it->second.val.data(), sizeof(e));
                         L.rev_nat(e, (uint8_t)proto, psa, pda, ppt);
                     }
+                    if (lb6on && eg) {
+                        CtEntry e;
+                        memcpy(&e, it->second.val.data(), sizeof(e));
+                        L6.rev_nat(e.rev_nat_index, (uint8_t)proto, p6sa, p6pt);
+                    }
                 }
             } else if (b == 1) {                // CT_ESTABLISHED
                 auto it = m->kv.find(k2);
@@ -2881,7 +3085,11 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                 (dir == 1 ? e.rx_bytes : e.tx_bytes) = len;
                 e.src_sec_id = mode == CFC_MODE_EGRESS ? c->seclabel[ep_lxc] : ident[i];
                 if (family == 6 && dir == 1)    // ipv6_policy, bpf_lxc.c:787-788
-                    e.rev_nat_index = (uint16_t)(d_[12] | d_[13] << 8);
+                    e.rev_nat_index = (uint16_t)(kd_[12] | kd_[13] << 8);
+                if (family == 6 && eg && x6.svc) {   // lb6_local's ct_state
+                    e.rev_nat_index = x6.rev_nat;
+                    e.slave = x6.slave;
+                }
                 if (eg && x.svc) {              // lb4_local's ct_state
                     e.rev_nat_index = x.rev_nat;
                     e.slave = x.slave;

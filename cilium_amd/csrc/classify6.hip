@@ -197,7 +197,53 @@ __device__ __forceinline__ uint32_t id_event(const DevTables &T, const CountArgs
     return k;
 }
 
-template <int MODE, bool CT, bool NT>
+// The egress service step of ipv6_l3_from_lxc (bpf_lxc.c:149-167):
+// lb6_extract_key, lb6_lookup_service and lb6_local (lb.h:336-481) against
+// the tables as committed (the batch's CT_SERVICE creates are folded in by
+// cfc_ct_apply_v6).  A matched service moves the packet's daddr (pda) to the
+// backend and its dport (ppt) to the backend's port; returns true for
+// DROP_NO_SERVICE.
+__device__ __forceinline__ bool lb6_egress(const DevTables &T, const EgressArgs &E,
+                                           const cfc_hdr_v6 &in, uint64_t i, uint4 sa_raw,
+                                           uint4 da_raw, uint32_t proto, uint32_t pt, uint4 &psa,
+                                           uint4 &pda, uint32_t &ppt)
+{
+    (void)psa;
+    const bool l4 = proto == 6 || proto == 17;
+    if (!T.lb6 || (!l4 && proto != 58))   // other protocols skip the step
+        return false;
+    uint32_t kd = l4 ? pt >> 16 : 0u;
+    uint4 b, tg;
+    if (!lb6_service(T, da_raw, kd, 0, b, tg))
+        return false;
+    // lb6_local: ct_lookup6(CT_SERVICE), the tuple as loaded, one probe; a
+    // hit's slave from the entry, else lb6_select_slave: hash % count + 1
+    const CtProbe k = ct_probe<true>(proto, pt, CT_SERVICE, E.ct_owner);
+    const uint32_t slot = ct6_find(T, da_raw, sa_raw, k.z1, k.w1);
+    uint32_t slave;
+    if (slot != NONE) {
+        slave = T.ct6_lb ? ld16(T.ct6_lb + slot).y : 0u;
+    } else {
+        const uint32_t h = in.hash ? in.hash[i] : flow_hash6(sa_raw, da_raw, pt, proto);
+        slave = h % (b.y >> 16) + 1;
+    }
+    uint4 b2, tg2;
+    bool ok = lb6_get(T, da_raw, kd, slave, b2, tg2);   // lb6_lookup_slave
+    if (!ok)   // the fall-back: the key as it stands, slave set
+        ok = lb6_service(T, da_raw, kd, slave, b2, tg2);
+    if (!ok)
+        return true;
+    pda = tg2;   // lb6_xlate
+    const uint32_t port = b2.y & 0xFFFF;
+    if (port && kd != port && l4)
+        ppt = (ppt & 0xFFFFu) | port << 16;
+    return false;
+}
+
+// LB: the launch has an IPv6 load balancer or wants the packet outputs —
+// the egress service step (lb6_local), reverse NAT of hits (lb6_rev_nat) and
+// ipv6_policy's daddr rewrite are followed, and cfc_out.pkt_* written
+template <int MODE, bool CT, bool NT, bool LB>
 __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     DevTables T, LdsPlan6 L, cfc_hdr_v6 in, cfc_out out, EgressArgs E,
     CountArgs C, uint64_t per_block)
@@ -242,6 +288,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         const uint32_t tfl = (in.tcp_flags && (mt & 0xFF) == 6) ? (uint32_t)in.tcp_flags[i] : 0u;
         const uint4 sa = bswap4(sa_raw), da = bswap4(da_raw);
         const uint32_t proto = mt & 0xFF;
+        // the packet as the programs leave it (LB launches)
+        uint4 psa = sa_raw, pda = da_raw;
+        uint32_t ppt = pt;
 
         int act = TC_ACT_OK, ver = 0;
         uint32_t ident = 0, met0 = NONE, met1 = NONE, ctr0 = NONE, ctr1 = NONE;
@@ -252,6 +301,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         const uint32_t len = mt >> 16;
         const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
         const bool local = (drec.z & LXC_VALID) != 0;
+        // the endpoint the packet is delivered to (egress: by the packet's
+        // daddr after the service step)
+        uint4 erec = drec;
         bool done = false;
         if (XDP) {
             bool deny = lpm6_lookup(T.pf6_dyn, sa) != 0;
@@ -316,6 +368,14 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 ck1 = ct_acct_key(c.slot == NONE ? NONE : c.slot + T.ct6_acct_base,
                                                   CT_INGRESS);
                             }
+                            if (LB) {
+                                // ipv6_policy (:785-815): the packet's daddr
+                                // loses its last word's low 16 bits; a hit whose
+                                // entry has a rev_nat_index is reverse-NATed
+                                pda.w &= 0xFFFF0000u;
+                                if (CT && c.slot != NONE && T.ct6_lb)
+                                    lb6_rev_nat(T, ld16(T.ct6_lb + c.slot).x, proto, psa, ppt);
+                            }
                             const bool reply = CT && c.res >= CT_REPLY;
                             const PolicyResult pr = policy_access(
                                 T, S, drec.x, drec.y, ident, c.dport, proto, 0, false);
@@ -361,16 +421,36 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                 } else if (!known) {
                     ver = DROP_CT_UNKNOWN_PROTO;
                     met0 = mkey6<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
+                } else if (LB && lb6_egress(T, E, in, i, sa_raw, da_raw, proto, pt, psa, pda,
+                                            ppt)) {
+                    ver = DROP_NO_SERVICE;   // lb6_local found no backend
+                    if (valid) {
+                        unsigned long long *m = reinterpret_cast<unsigned long long *>(
+                            C.g_met + (uint64_t)(-DROP_NO_SERVICE * METRIC_DIRS + METRIC_EGRESS) * 2);
+                        atomicAdd(m, 1ull);
+                        atomicAdd(m + 1, (unsigned long long)len);
+                    }
                 } else {
+                    // (LB: the service step moved the tuple's daddr and the
+                    // packet's dport to the backend's; lb6_local has no
+                    // loopback case, so tuple and packet agree)
+                    const uint4 tda_raw = LB ? pda : da_raw;
+                    const uint32_t tpt = LB ? ppt : pt;
+                    const uint4 tda = LB ? bswap4(pda) : da;
+                    if (LB)
+                        erec = lxc6_find(T, lxc_lds, lxc_off, pda);
+                    const bool elocal = (erec.z & LXC_VALID) != 0;
+                    if (LB)
+                        ct6_new_dport(proto, tpt, &dport);
                     // destination identity (bpf_lxc.c:206-221)
-                    const uint32_t label = lpm6_lookup(T.ipc6, da);
+                    const uint32_t label = lpm6_lookup(T.ipc6, tda);
                     ident = label ? label
-                          : (da.x == T.router6[0] && da.y == T.router6[1]) ? CLUSTER_ID
-                                                                            : WORLD_ID;
+                          : (tda.x == T.router6[0] && tda.y == T.router6[1]) ? CLUSTER_ID
+                                                                              : WORLD_ID;
                     // ipv6_l3_from_lxc's ct_lookup6 (bpf_lxc.c:190)
                     CtResult c{CT_NEW, NONE, dport};
                     if (CT) {
-                        c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_EGRESS, E.ct_owner);
+                        c = ct_stage6(T, sa_raw, tda_raw, proto, tpt, CT_EGRESS, E.ct_owner);
                         ck1 = ct_acct_key(c.slot == NONE ? NONE : c.slot + T.ct6_acct_base,
                                           CT_EGRESS);
                     }
@@ -389,8 +469,12 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                         !NT ? 0u
                         : c.res == CT_NEW ? TRACE_PAYLOAD_LEN
                                           : ct_monitor(T, CT ? T.ct6_tm : nullptr, c.slot,
-                                                       CT_EGRESS, ct_action(true, proto, pt, mt),
+                                                       CT_EGRESS, ct_action(true, proto, tpt, mt),
                                                        tfl, c.dport);
+                    // a reply of a load-balanced flow: the packet's source
+                    // back to the service (bpf_lxc.c:255-266)
+                    if (LB && CT && reply && c.slot != NONE && T.ct6_lb)
+                        lb6_rev_nat(T, ld16(T.ct6_lb + c.slot).x, proto, psa, ppt);
                     if (pr.verdict < 0 && !reply) {
                         ver = DROP_POLICY;
                         met0 = mkey6<MODE>(DROP_POLICY, METRIC_EGRESS);
@@ -401,29 +485,39 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     } else {
                         met0 = mkey6<MODE>(0, METRIC_EGRESS);   // host/local/stack
                         ver = 0;
-                        if (!local) {
+                        if (!elocal) {
                             act = TC_ACT_OK;   // TRACE_TO_STACK (:390)
                             evw = trace_word(OBS_TO_STACK, E.lxc_id, (uint32_t)c.res, mon1);
-                        } else if (drec.z & LXC_HOST) {
+                        } else if (erec.z & LXC_HOST) {
                             act = TC_ACT_REDIRECT;   // TRACE_TO_HOST (:373)
                             evw = trace_word(OBS_TO_HOST, E.lxc_id, (uint32_t)c.res, mon1);
-                        } else if (!(drec.z & LXC_HAS_POLICY)) {
+                        } else if (!(erec.z & LXC_HAS_POLICY)) {
                             ver = DROP_MISSED_TAIL_CALL;
                             met1 = mkey6<MODE>(DROP_MISSED_TAIL_CALL, METRIC_EGRESS);
                         } else {
                             // ipv6_local_delivery into the destination's
-                            // ipv6_policy with src = SECLABEL
-                            CtResult c2{CT_NEW, NONE, dport};
+                            // ipv6_policy with src = SECLABEL, on the packet
+                            // as it now is
+                            uint32_t dport2 = dport;
+                            if (LB)
+                                ct6_new_dport(proto, ppt, &dport2);
+                            CtResult c2{CT_NEW, NONE, dport2};
+                            const uint4 s2 = LB ? psa : sa_raw;
                             if (CT) {
-                                c2 = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS,
-                                               ct_owner_word(drec.z & 0xFFFF,
-                                                             (drec.z & LXC_CT_LOCAL) != 0));
+                                c2 = ct_stage6(T, s2, tda_raw, proto, LB ? ppt : pt, CT_INGRESS,
+                                               ct_owner_word(erec.z & 0xFFFF,
+                                                             (erec.z & LXC_CT_LOCAL) != 0));
                                 ck2 = ct_acct_key(c2.slot == NONE ? NONE : c2.slot + T.ct6_acct_base,
                                                   CT_INGRESS);
                             }
+                            if (LB) {   // ipv6_policy's rewrites (:785-815)
+                                pda.w &= 0xFFFF0000u;
+                                if (CT && c2.slot != NONE && T.ct6_lb)
+                                    lb6_rev_nat(T, ld16(T.ct6_lb + c2.slot).x, proto, psa, ppt);
+                            }
                             const bool reply2 = CT && c2.res >= CT_REPLY;
                             const PolicyResult pw = policy_access(
-                                T, S, drec.x, drec.y, E.seclabel, c2.dport, proto, 0, false);
+                                T, S, erec.x, erec.y, E.seclabel, c2.dport, proto, 0, false);
                             ctr1 = pw.ctr;
                             if (CT)
                                 ctb |= ((uint32_t)c2.res | CTO_DONE |
@@ -435,15 +529,17 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 met1 = mkey6<MODE>(DROP_POLICY, METRIC_INGRESS);
                             } else {
                                 const bool prox = pw.verdict > 0 && !reply2;
-                                act = (prox || ifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
+                                const bool eifx = (erec.z & LXC_IFINDEX) != 0;
+                                act = (prox || eifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
                                 ver = prox ? pw.verdict : 0;
                                 met1 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
                                 if (NT)
                                     evw = trace_word(
-                                        prox ? OBS_TO_PROXY : OBS_TO_LXC, drec.z & 0xFFFF,
+                                        prox ? OBS_TO_PROXY : OBS_TO_LXC, erec.z & 0xFFFF,
                                         (uint32_t)c2.res,
                                         ct_monitor(T, CT ? T.ct6_tm : nullptr, c2.slot,
-                                                   CT_INGRESS, ct_action(true, proto, pt, mt),
+                                                   CT_INGRESS,
+                                                   ct_action(true, proto, LB ? ppt : pt, mt),
                                                    tfl, c2.dport));
                             }
                         }
@@ -460,9 +556,14 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         if (NT)   // the monitor event word (cfc_out.notify)
             st_nt(ver < 0 ? notify_word(MODE, ver,
                                         EGR && met1 == mkey6<MODE>(DROP_POLICY, METRIC_INGRESS),
-                                        drec.z & 0xFFFF, E.lxc_id)
+                                        erec.z & 0xFFFF, E.lxc_id)
                           : evw,
                   out.notify + i);
+        if (LB && out.pkt_saddr) {   // the packet as it leaves (cfc_out.pkt_*)
+            *reinterpret_cast<uint4 *>(out.pkt_saddr + 4 * i) = psa;
+            *reinterpret_cast<uint4 *>(out.pkt_daddr + 4 * i) = pda;
+            st_nt(ppt, out.pkt_ports + i);
+        }
         if (CT) {
             st_nt(ck1, C.ct + i);
             if (EGR)
@@ -504,7 +605,8 @@ void launch_mode6_nt(const DevTables &T, const cfc_hdr_v6 &in, const cfc_out &ou
                      uint64_t per_block, hipStream_t s)
 {
     const LdsPlan6 L = lds_plan6(T);
-    auto kern = k_classify_v6<MODE, CT, NT>;
+    const bool lb = MODE != CFC_MODE_XDP && (T.lb6 || T.rnat6 || out.pkt_saddr);
+    auto kern = lb ? k_classify_v6<MODE, CT, NT, true> : k_classify_v6<MODE, CT, NT, false>;
     set_lds_limit((const void *)kern, (int)LDS_PER_WG);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(BLOCK), L.bytes(), s, T, L, in,
                        out, E, C, per_block);
@@ -534,6 +636,14 @@ int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
         return -22;
     if ((reinterpret_cast<uintptr_t>(in.saddr) | reinterpret_cast<uintptr_t>(in.daddr)) & 15)
         return -22;   // 16-byte address loads
+    if (out.pkt_saddr && ((reinterpret_cast<uintptr_t>(out.pkt_saddr) |
+                           reinterpret_cast<uintptr_t>(out.pkt_daddr)) & 15))
+        return -22;   // 16-byte address stores
+    if (out.pkt_saddr && mode == CFC_MODE_XDP &&   // the prefilter rewrites nothing
+        (hipMemcpyAsync(out.pkt_saddr, in.saddr, 16 * in.n, hipMemcpyDeviceToDevice, s) ||
+         hipMemcpyAsync(out.pkt_daddr, in.daddr, 16 * in.n, hipMemcpyDeviceToDevice, s) ||
+         hipMemcpyAsync(out.pkt_ports, in.ports, 4 * in.n, hipMemcpyDeviceToDevice, s)))
+        return -5;
     const uint64_t nwg = (uint64_t)num_cus * CFC_WG_PER_CU;
     uint64_t per_block = (in.n + nwg - 1) / nwg;
     per_block = (per_block + BLOCK - 1) / BLOCK * BLOCK;

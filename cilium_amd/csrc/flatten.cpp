@@ -550,6 +550,44 @@ uint4 ct_lb_of(const std::string &val)
     return make_uint4(rev | ((bits >> 3) & 1u) << 16, slave, 0, 0);
 }
 
+// cilium_lb6_services / cilium_lb6_reverse_nat (layout.h)
+static void build_lb6(const Map *svc, const Map *rnat, HostImage *img)
+{
+    if (svc && !svc->kv.empty()) {
+        const uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * svc->kv.size()));
+        img->lb6.assign(3ull * ns, make_uint4(0, 0, 0, 0));
+        img->lb6_mask = ns - 1;
+        for (const auto &kv : svc->kv) {
+            if (kv.first.size() != 20 || kv.second.val.size() < 24)
+                continue;
+            uint32_t k[5], v[6];
+            memcpy(k, kv.first.data(), 20);
+            memcpy(v, kv.second.val.data(), 24);
+            uint32_t i = lb6_hash(k[0], k[1], k[2], k[3], k[4]) & img->lb6_mask;
+            while (img->lb6[3 * i + 1].w)
+                i = (i + 1) & img->lb6_mask;
+            img->lb6[3 * i] = make_uint4(k[0], k[1], k[2], k[3]);
+            img->lb6[3 * i + 1] = make_uint4(k[4], v[4], v[5], 1);
+            img->lb6[3 * i + 2] = make_uint4(v[0], v[1], v[2], v[3]);
+            img->n_lb6++;
+        }
+    }
+    if (rnat && !rnat->kv.empty()) {
+        img->rnat6.assign(2ull * 65536, make_uint4(0, 0, 0, 0));
+        for (const auto &kv : rnat->kv) {
+            if (kv.first.size() != 2 || kv.second.val.size() < 18)
+                continue;
+            uint16_t idx, port;
+            uint32_t a[4];
+            memcpy(&idx, kv.first.data(), 2);
+            memcpy(a, kv.second.val.data(), 16);
+            memcpy(&port, kv.second.val.data() + 16, 2);
+            img->rnat6[2ull * idx] = make_uint4(a[0], a[1], a[2], a[3]);
+            img->rnat6[2ull * idx + 1] = make_uint4(port | 1u << 16, 0, 0, 0);
+        }
+    }
+}
+
 // cilium_lb4_services / cilium_lb4_reverse_nat (layout.h)
 static void build_lb(const Map *svc, const Map *rnat, HostImage *img)
 {
@@ -621,6 +659,8 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
         img->ct6.assign(ns, Ct6Slot{});
         img->ct6_tm.assign(ns, CtTimer{});
         img->ct6_mask = ns - 1;
+        if (img->lb6_ct)   // (IPv6 entries always carry rev_nat_index)
+            img->ct6_lb.assign(ns, make_uint4(0, 0, 0, 0));
     }
     for (const Map *m : cts) {
         const bool v6 = m->role == ROLE_CT6;
@@ -653,6 +693,10 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                 }
                 img->ct6[i] = e;
                 img->ct6_tm[i] = tm;
+                if (!img->ct6_lb.empty()) {
+                    const uint4 l = ct_lb_of(kv.second.val);
+                    img->ct6_lb[i] = make_uint4(l.x & 0xFFFF, l.y, 0, 0);
+                }
                 img->ct6_probe = std::max(img->ct6_probe, p);
                 img->n_ct6++;
             }
@@ -676,16 +720,23 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
             if (m->policy_lxc >= 0)
                 img->ct_local[m->policy_lxc] = 1;
         }
-    const Map *lbsvc = nullptr, *lbrnat = nullptr;
+    const Map *lbsvc = nullptr, *lbrnat = nullptr, *lb6svc = nullptr, *lb6rnat = nullptr;
     for (Map *m : maps) {
         if (m->role == ROLE_LB4_SVC)
             lbsvc = m;
         else if (m->role == ROLE_LB4_RNAT)
             lbrnat = m;
+        else if (m->role == ROLE_LB6_SVC)
+            lb6svc = m;
+        else if (m->role == ROLE_LB6_RNAT)
+            lb6rnat = m;
     }
     img->lb_ct = (lbsvc && !lbsvc->kv.empty()) || (lbrnat && !lbrnat->kv.empty());
-    if (groups & GROUP_LB)
+    img->lb6_ct = (lb6svc && !lb6svc->kv.empty()) || (lb6rnat && !lb6rnat->kv.empty());
+    if (groups & GROUP_LB) {
         build_lb(lbsvc, lbrnat, img);
+        build_lb6(lb6svc, lb6rnat, img);
+    }
     if (groups & GROUP_CT)
         build_ct(cts, img);
     const Map *ipc = nullptr, *lxc = nullptr, *pf4fix = nullptr,

@@ -89,6 +89,11 @@ struct HostImage {
     std::vector<uint2> rnat4;
     std::vector<uint4> ct4_lb;
     bool lb_ct = false;                      // ct4_lb wanted
+    std::vector<uint4> lb6;                  // IPv6: 3 per slot
+    uint32_t lb6_mask = 0, n_lb6 = 0;
+    std::vector<uint4> rnat6;                // 2 per index
+    std::vector<uint4> ct6_lb;
+    bool lb6_ct = false;                     // ct6_lb wanted
     uint64_t device_bytes() const;
 };
 
@@ -109,7 +114,7 @@ enum : unsigned {
     GROUP_ENDPOINTS = 4,  // cilium_lxc + every policymap (+ counter layout)
     GROUP_CT = 8,         // every CT map
     GROUP_IPCACHE6 = 16,  // ipcache, IPv6 LPM
-    GROUP_LB = 32,        // cilium_lb4_services, cilium_lb4_reverse_nat
+    GROUP_LB = 32,        // cilium_lb{4,6}_services, cilium_lb{4,6}_reverse_nat
     GROUP_ALL = 63,
 };
 // maps: every map of the context; groups: which parts of img to build

@@ -524,6 +524,67 @@ __device__ __forceinline__ void lb4_rev_nat(const DevTables &T, uint4 lw, uint32
 // the service step's flags per header (lb.hip, cfc_api.cpp)
 constexpr uint32_t LBF_DROP = 1, LBF_SVC = 2, LBF_LOOP = 4;
 
+// ---- IPv6 services (lb.h:306-481; layout.h lb6 slots) ------------------------
+// one cilium_lb6_services lookup: the slot's {port | count, rev_nat | weight}
+// word pair (b.y, b.z) and target, false on a miss
+__device__ __forceinline__ bool lb6_get(const DevTables &T, uint4 addr, uint32_t dport,
+                                        uint32_t slave, uint4 &b, uint4 &tgt)
+{
+    const uint32_t ps = dport | slave << 16;
+    uint32_t i = lb6_hash(addr.x, addr.y, addr.z, addr.w, ps) & T.lb6_mask;
+    for (uint32_t p = 0; p <= T.lb6_mask; p++) {
+        const uint4 a = ld16(T.lb6 + 3 * i);
+        b = ld16(T.lb6 + 3 * i + 1);
+        if (!b.w)
+            return false;
+        if (b.x == ps && a.x == addr.x && a.y == addr.y && a.z == addr.z && a.w == addr.w) {
+            tgt = ld16(T.lb6 + 3 * i + 2);
+            return true;
+        }
+        i = (i + 1) & T.lb6_mask;
+    }
+    return false;
+}
+// lb6_lookup_service (lb.h:352-381): the L4 key while its dport is set (a
+// miss clears the caller's dport), then the L3 key; count must be nonzero
+__device__ __forceinline__ bool lb6_service(const DevTables &T, uint4 addr, uint32_t &dport,
+                                            uint32_t slave, uint4 &b, uint4 &tgt)
+{
+    if (dport) {
+        if (lb6_get(T, addr, dport, slave, b, tgt) && (b.y >> 16))
+            return true;
+        dport = 0;
+    }
+    return lb6_get(T, addr, 0, slave, b, tgt) && (b.y >> 16);
+}
+// lb6_rev_nat (lb.h:306-319, flags 0) on the packet: its source address and
+// port from cilium_lb6_reverse_nat[index], when that holds the index
+__device__ __forceinline__ void lb6_rev_nat(const DevTables &T, uint32_t index, uint32_t proto,
+                                            uint4 &psa, uint32_t &ppt)
+{
+    if (!index || !T.rnat6)
+        return;
+    const uint4 pw = ld16(T.rnat6 + 2 * index + 1);
+    if (!(pw.x >> 16))
+        return;
+    const uint32_t port = pw.x & 0xFFFF;
+    if (port && (proto == 6 || proto == 17))
+        ppt = (ppt & 0xFFFF0000u) | port;   // reverse_map_l4_port: the sport
+    psa = ld16(T.rnat6 + 2 * index);
+}
+// the engine's skb->hash stand-in for IPv6 (notify.hip flow_hash, fold6)
+__device__ __forceinline__ uint32_t fold6w(uint4 a)
+{
+    uint32_t h = fmix32(a.w);
+    h = fmix32(a.z ^ h);
+    h = fmix32(a.y ^ h);
+    return fmix32(a.x ^ h);
+}
+__device__ __forceinline__ uint32_t flow_hash6(uint4 sa, uint4 da, uint32_t pt, uint32_t proto)
+{
+    return flow_hash4(fold6w(sa), fold6w(da), pt, proto);
+}
+
 // key of ct_acct[slot][dir] (k_ct_count), NONE for a miss
 __device__ __forceinline__ uint32_t ct_acct_key(uint32_t slot, int dir)
 {

@@ -337,6 +337,17 @@ __host__ __device__ inline uint32_t lb4_hash(uint32_t addr, uint32_t ps)
     return fmix32(fmix32(addr ^ 0x85ebca6bu) ^ ps);
 }
 constexpr uint32_t IPV4_LOOPBACK = 0x1FFFF50Au;   // node_config.h:45 (be32 raw)
+// IPv6 (cilium_lb6_services, cilium_lb6_reverse_nat): 48-byte service slots
+// keyed by struct lb6_key {address[16], dport, slave}, load <= 1/2:
+//   {address words}, {dport | slave << 16, port | count << 16,
+//    rev_nat_index | weight << 16, used}, {target words}
+// Reverse NAT direct-indexed: {address words}, {port | 1 << 16, 0, 0, 0}.
+// Per CT6 slot (ct6_lb, with a load balancer): {rev_nat_index, slave, 0, 0}.
+__host__ __device__ inline uint32_t lb6_hash(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3,
+                                             uint32_t ps)
+{
+    return l6_hash(a0, a1, a2, a3, ps ^ 0x6b43a9b5u);
+}
 
 struct DevTables {
     const uint4 *l4d;              // compact IPv4 LPM /16 directory, or null
@@ -390,6 +401,10 @@ struct DevTables {
     uint32_t lb4_mask;             // slots - 1
     const uint2 *rnat4;            // [65536] or null
     const uint4 *ct4_lb;           // per CT4 slot, or null
+    const uint4 *lb6;              // 3 uint4 per IPv6 service slot, or null
+    uint32_t lb6_mask;
+    const uint4 *rnat6;            // [65536][2] or null
+    const uint4 *ct6_lb;           // per CT6 slot, or null
 };
 
 // metrics block: [reason 256][dir 4][count, bytes]

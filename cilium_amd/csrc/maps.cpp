@@ -193,6 +193,10 @@ Role role_for(const std::string &path, int *policy_lxc, int *ct_any)
         return ROLE_LB4_SVC;
     if (b == "cilium_lb4_reverse_nat")
         return ROLE_LB4_RNAT;
+    if (b == "cilium_lb6_services")
+        return ROLE_LB6_SVC;
+    if (b == "cilium_lb6_reverse_nat")
+        return ROLE_LB6_RNAT;
     if (b == "cilium_lxc")
         return ROLE_LXC;
     if (b == "cilium_metrics")

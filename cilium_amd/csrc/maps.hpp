@@ -34,6 +34,8 @@ enum Role {
     ROLE_CT6,       // cilium_ct6_* / cilium_ct_any6_*
     ROLE_LB4_SVC,   // cilium_lb4_services
     ROLE_LB4_RNAT,  // cilium_lb4_reverse_nat
+    ROLE_LB6_SVC,   // cilium_lb6_services
+    ROLE_LB6_RNAT,  // cilium_lb6_reverse_nat
 };
 
 enum : int { TOUCH_VALUE = 1, TOUCH_INSERT = 2, TOUCH_ERASE = 4 };

@@ -45,6 +45,7 @@ class HeaderBatchV6:
     meta: "torch.Tensor"      # proto | flags << 8 | len << 16 (HF_EXTHDR)
     mark: "torch.Tensor | None" = None
     tcp_flags: "torch.Tensor | None" = None   # uint8 TCP header byte 13
+    hash: "torch.Tensor | None" = None        # skb->hash (lb6_select_slave)
 
     def __len__(self):
         return int(self.ports.numel())
@@ -63,8 +64,8 @@ class Verdicts:
     action: "torch.Tensor | None"  # uint8
     ct: "torch.Tensor | None" = None  # uint8 CT byte (cfc.h CFC_CT_*)
     notify: "torch.Tensor | None" = None  # int32 drop-notify site (CFC_NT_*)
-    # (IPv4) the packet as the programs left it: int32 (n, 3) saddr, daddr,
-    # first L4 word (cfc_out.pkt_*)
+    # the packet as the programs left it (cfc_out.pkt_*): int32 (n, 3) saddr,
+    # daddr, first L4 word (IPv4); (n, 9) saddr[4], daddr[4], L4 word (IPv6)
     pkt: "torch.Tensor | None" = None
 
 
@@ -99,11 +100,13 @@ def pack_v6(h, device="cuda"):
     def t(a):
         return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
     from .synth import tcp_flags_of
+    hs = getattr(h, "hash", None)
     return HeaderBatchV6(t(np.ascontiguousarray(h.saddr, np.uint8)).view(-1, 4),
                          t(np.ascontiguousarray(h.daddr, np.uint8)).view(-1, 4),
                          t(ports), t(meta),
                          t(h.mark.astype(np.uint32)) if h.mark is not None else None,
-                         torch.from_numpy(tcp_flags_of(h).copy()).to(device))
+                         torch.from_numpy(tcp_flags_of(h).copy()).to(device),
+                         t(np.asarray(hs, np.uint32)) if hs is not None else None)
 
 
 def pack(h, device="cuda"):
@@ -120,7 +123,7 @@ def hdr_struct(batch, n=None):
     args = (_ptr(batch.saddr), _ptr(batch.daddr), _ptr(batch.ports),
             _ptr(batch.meta), _ptr(batch.mark), _ptr(batch.tcp_flags),
             len(batch) if n is None else n)
-    return L.HdrV6(*args) if v6 else L.HdrV4(*args, _ptr(batch.hash))
+    return L.HdrV6(*args, _ptr(batch.hash)) if v6 else L.HdrV4(*args, _ptr(batch.hash))
 
 
 def out_struct(out):
@@ -324,7 +327,8 @@ class Datapath:
 
     def classify_v6(self, batch: HeaderBatchV6, mode=L.MODE_INGRESS, ep_lxc=0,
                     out: Verdicts | None = None, want_action=True,
-                    want_ct=False, want_notify=False, stream=None) -> Verdicts:
+                    want_ct=False, want_notify=False, want_pkt=False,
+                    stream=None) -> Verdicts:
         import torch
         n = len(batch)
         dev = batch.ports.device
@@ -347,12 +351,22 @@ class Datapath:
             assert batch.mark.numel() == n and batch.mark.dtype == torch.int32
         if batch.tcp_flags is not None:
             assert batch.tcp_flags.numel() == n and batch.tcp_flags.dtype == torch.uint8
+        if batch.hash is not None:
+            assert batch.hash.numel() == n and batch.hash.dtype == torch.int32
         hdr = hdr_struct(batch)
+        pk = None
+        if want_pkt:   # saddr rows, daddr rows, L4 words: three arrays
+            pk = torch.empty(9 * n, dtype=torch.int32, device=dev)
         o = L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
-                  _ptr(out.ct), _ptr(out.notify))
+                  _ptr(out.ct), _ptr(out.notify),
+                  *((_ptr(pk[:4 * n]), _ptr(pk[4 * n:8 * n]), _ptr(pk[8 * n:]))
+                    if pk is not None else (None, None, None)))
         L.check(self.L.cfc_classify_v6(self.h, ctypes.byref(hdr),
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)), "classify v6")
+        if pk is not None:
+            out.pkt = torch.cat([pk[:4 * n].view(n, 4), pk[4 * n:8 * n].view(n, 4),
+                                 pk[8 * n:].view(n, 1)], 1)
         return out
 
     def classify(self, batch, mode=L.MODE_INGRESS, ep_lxc=0, **kw) -> Verdicts:

@@ -1,10 +1,12 @@
-"""pkg/maps/lbmap (IPv4) over the engine's map API: cilium_lb4_services and
+"""pkg/maps/lbmap over the engine's map API: cilium_lb4_services and
 cilium_lb4_reverse_nat with the reference's key and value layouts
 (lbmap/ipv4.go: Service4Key {Address, Port, Slave}, Service4Value {Address,
 Port, Count, RevNat, Weight}, RevNat4Key, RevNat4Value) and byte order
 (ToNetwork: ports, rev-NAT ids and weights network order; count host order),
 and UpdateService's slot layout (lbmap.go:351-420): backends in slots
-1..n, the master slot 0 carrying the count."""
+1..n, the master slot 0 carrying the count.  IPv6 (lbmap/ipv6.go):
+cilium_lb6_services {Service6Key: Service6Value} and cilium_lb6_reverse_nat,
+the same layouts with 16-byte addresses (LBMap6)."""
 from __future__ import annotations
 
 import socket
@@ -15,6 +17,8 @@ from .datapath import Datapath
 MaxEntries = 65536                        # lbmap.go MaxEntries
 Service4MapName = "cilium_lb4_services"
 RevNat4MapName = "cilium_lb4_reverse_nat"
+Service6MapName = "cilium_lb6_services"
+RevNat6MapName = "cilium_lb6_reverse_nat"
 MAP_TYPE_HASH = 1
 
 
@@ -24,6 +28,10 @@ def _be16(x):
 
 def _ip(ip):
     return ip if isinstance(ip, bytes) else socket.inet_aton(ip)
+
+
+def _ip6(ip):
+    return ip if isinstance(ip, bytes) else socket.inet_pton(socket.AF_INET6, ip)
 
 
 class Service4Key:
@@ -100,3 +108,70 @@ class LBMap:
         if revnat4 is not None and len(revnat4):
             b = np.ascontiguousarray(revnat4).view(np.uint8).reshape(len(revnat4), 8)
             self.dp.update_batch(self.rnat, b[:, :2], b[:, 2:8])
+
+
+class Service6Key(Service4Key):
+    """struct lb6_key (common.h:408-412)."""
+
+    def __init__(self, ip, port, slave=0):
+        self.address, self.port, self.slave = _ip6(ip), int(port), int(slave)
+
+
+class Service6Value(Service4Value):
+    """struct lb6_service (common.h:414-420)."""
+
+    def __init__(self, count=0, target="::", port=0, rev_nat=0, weight=0):
+        self.count, self.target, self.port = int(count), _ip6(target), int(port)
+        self.rev_nat, self.weight = int(rev_nat), int(weight)
+
+
+class RevNat6Value(RevNat4Value):
+    """struct lb6_reverse_nat (common.h:422-425)."""
+
+    def __init__(self, ip, port):
+        self.address, self.port = _ip6(ip), int(port)
+
+
+class LBMap6(LBMap):
+    """The IPv6 maps (lbmap/ipv6.go) with LBMap's UpdateService / DeleteService
+    slot discipline."""
+
+    def __init__(self, dp: Datapath):
+        self.dp = dp
+        self.svc, _ = dp.open_or_create_map(Service6MapName, MAP_TYPE_HASH, 20, 24,
+                                            MaxEntries)
+        self.rnat, _ = dp.open_or_create_map(RevNat6MapName, MAP_TYPE_HASH, 2, 18,
+                                             MaxEntries)
+
+    def UpdateService(self, fe: Service6Key, backends, add_revnat=True, revnat_id=0):
+        old = self.dp.lookup_element(self.svc, Service6Key(fe.address, fe.port, 0).pack())
+        existing = struct.unpack_from("<H", old, 18)[0] if old else 0
+        for i, be in enumerate(backends):
+            self.dp.update_element(self.svc, Service6Key(fe.address, fe.port, i + 1).pack(),
+                                   be.pack())
+        if add_revnat:
+            self.dp.update_element(self.rnat, struct.pack("<H", _be16(revnat_id)),
+                                   RevNat6Value(fe.address, fe.port).pack())
+        nz = sum(1 for be in backends if be.weight)
+        self.dp.update_element(self.svc, Service6Key(fe.address, fe.port, 0).pack(),
+                               Service6Value(len(backends), weight=nz).pack())
+        for i in range(len(backends) + 1, existing + 1):
+            self.dp.delete_element(self.svc, Service6Key(fe.address, fe.port, i).pack())
+
+    def DeleteService(self, fe: Service6Key):
+        old = self.dp.lookup_element(self.svc, Service6Key(fe.address, fe.port, 0).pack())
+        n = struct.unpack_from("<H", old, 18)[0] if old else 0
+        for i in range(n, -1, -1):
+            k = Service6Key(fe.address, fe.port, i).pack()
+            if self.dp.lookup_element(self.svc, k) is not None:
+                self.dp.delete_element(self.svc, k)
+
+    def load_rows(self, lb6, revnat6):
+        """Raw synth.LB6_DT / REVNAT6_DT rows (already in map byte order)."""
+        import numpy as np
+        if lb6 is not None and len(lb6):
+            b = np.ascontiguousarray(lb6).view(np.uint8).reshape(len(lb6), 44)
+            self.dp.update_batch(self.svc, b[:, :20], b[:, 20:44])
+        if revnat6 is not None and len(revnat6):
+            b = np.ascontiguousarray(revnat6).view(np.uint8).reshape(len(revnat6), 20)
+            self.dp.update_batch(self.rnat, b[:, :2], b[:, 2:20])

@@ -58,6 +58,8 @@ def load_tables(dp: Datapath, t, commit=True):
         dp.set_node_config(*t.node)
     if getattr(t, "lb4", None) is not None or getattr(t, "revnat4", None) is not None:
         lbmap.LBMap(dp).load_rows(getattr(t, "lb4", None), getattr(t, "revnat4", None))
+    if getattr(t, "lb6", None) is not None or getattr(t, "revnat6", None) is not None:
+        lbmap.LBMap6(dp).load_rows(getattr(t, "lb6", None), getattr(t, "revnat6", None))
     if commit:
         dp.commit()
     return pms

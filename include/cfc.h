@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 8
+#define CFC_ABI_VERSION 9
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -245,6 +245,11 @@ typedef struct {
     const uint32_t *mark;
     const uint8_t *tcp_flags;
     uint64_t n;
+    /* skb->hash of each header (lb6_select_slave, lb.h:124-152, and the
+     * monitor records), or NULL = CFC_FLOW_HASH over the addresses folded to
+     * a word each (fold(a) = fmix32(w0 ^ fmix32(w1 ^ fmix32(w2 ^ fmix32(w3)))),
+     * w = the address's raw words) */
+    const uint32_t *hash;
 } cfc_hdr_v6;
 
 /* Outputs (device pointers, n elements; action may be NULL).
@@ -308,14 +313,18 @@ typedef struct {
     uint8_t *action;
     uint8_t *ct;
     uint32_t *notify;
-    /* (IPv4, may be NULL) the packet's L3/L4 addresses as the programs left
+    /* (may be NULL) the packet's L3/L4 addresses as the programs left
      * them: saddr, daddr and the first L4 word after service translation
      * (lb4_local / lb4_xlate: a service address and port replaced by the
      * backend's, a looped-back flow's source by IPV4_LOOPBACK) and reverse
      * NAT of load-balanced replies (lb4_rev_nat: the backend's source back
      * to the service address and port).  Headers the programs did not
      * rewrite keep their input.  (A proxy redirect's new port is the
-     * verdict.) */
+     * verdict.)  cfc_classify_v6: pkt_saddr / pkt_daddr are n 16-byte rows
+     * (16-byte aligned) — lb6_local / lb6_xlate, lb6_rev_nat of egress
+     * replies, and ipv6_policy's rewrites (bpf_lxc.c:785-815: the last
+     * word's low 16 bits of daddr cleared, the source of every hit whose
+     * entry's rev_nat_index cilium_lb6_reverse_nat holds reverse-NATed). */
     uint32_t *pkt_saddr;
     uint32_t *pkt_daddr;
     uint32_t *pkt_ports;

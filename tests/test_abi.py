@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(_lib.EXPORTS) == fns
-    assert L.cfc_abi_version() == 8
+    assert L.cfc_abi_version() == 9
     assert L.cfc_num_possible_cpus() == 1
 
 
@@ -256,7 +256,7 @@ def test_drop_notify_abi_on_host_only_context():
     # Out carries eight device pointers (cfc_out, ABI 7: + the packet's
     # rewritten addresses); cfc_hdr_v4 gained skb->hash
     assert ctypes.sizeof(_lib.Out) == 64
-    assert ctypes.sizeof(_lib.HdrV4) == 64 and ctypes.sizeof(_lib.HdrV6) == 56
+    assert ctypes.sizeof(_lib.HdrV4) == 64 and ctypes.sizeof(_lib.HdrV6) == 64
     dt = O.DROP_NOTIFY_DT
     assert dt.itemsize == 32
     assert [dt.fields[k][1] for k in dt.names] == [0, 1, 2, 4, 8, 12, 16, 20, 24, 28]

@@ -13,7 +13,7 @@ import golden_io as G
 import oracle as O
 from cilium_amd import synth as S
 from cilium_amd import _lib as L
-from cilium_amd.datapath import Datapath, pack_v4
+from cilium_amd.datapath import Datapath, pack, pack_v4
 from cilium_amd.loader import ct_rows, load_tables
 
 pytestmark = pytest.mark.gpu
@@ -31,8 +31,8 @@ def torch():
 def _run(torch, t, h, mode, ep, notify=False):
     dp = Datapath(0)
     load_tables(dp, t)
-    b = pack_v4(h, "cuda:0")
-    out = dp.classify_v4(b, mode, ep, want_ct=True, want_pkt=True, want_notify=notify)
+    b = pack(h, "cuda:0")
+    out = dp.classify(b, mode, ep, want_ct=True, want_pkt=True, want_notify=notify)
     torch.cuda.synchronize()
     res = dict(act=out.action.cpu().numpy().astype(np.int32),
                ver=out.verdict.cpu().numpy(),
