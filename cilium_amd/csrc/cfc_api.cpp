@@ -124,8 +124,8 @@ struct GLb {           // load balancing: services, reverse NAT
 struct GCt {           // conntrack
     DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
     DevBuf ct4_lb, ct6_lb;                // per-slot LB state (with a load balancer)
-    DevBuf ct4_info, ct4_mark, ct4_sum;   // device CT apply state (ctapply.hip)
-    DevBuf ct6_info, ct6_mark, ct6_sum;
+    DevBuf ct4_info, ct4_ms;   // device CT apply state (ctapply.hip)
+    DevBuf ct6_info, ct6_ms;
     std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
     std::vector<Ct6Slot> ct6_host;
     std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
@@ -939,10 +939,10 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
         return nullptr;
     const size_t n4 = img.ct4.size(), n6 = img.ct6.size();
     if (n4 && ((*rc = g->ct4_info.zeros(sizeof(CtInfo) * n4, s)) ||
-               (*rc = g->ct4_mark.zeros(4 * n4, s)) || (*rc = g->ct4_sum.zeros(4 * n4, s))))
+               (*rc = g->ct4_ms.zeros(8 * n4, s))))
         return nullptr;
     if (n6 && ((*rc = g->ct6_info.zeros(sizeof(CtInfo) * n6, s)) ||
-               (*rc = g->ct6_mark.zeros(4 * n6, s)) || (*rc = g->ct6_sum.zeros(4 * n6, s))))
+               (*rc = g->ct6_ms.zeros(8 * n6, s))))
         return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
@@ -2684,16 +2684,14 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         A.acct_base = E.T.ct6_acct_base;
         A.tm = (CtTimer *)G.ct6_tm.p;
         A.info = (CtInfo *)G.ct6_info.p;
-        A.mark = (uint32_t *)G.ct6_mark.p;
-        A.sum = (uint32_t *)G.ct6_sum.p;
+        A.ms = (uint2 *)G.ct6_ms.p;
     } else {
         A.ct4 = (Ct4Slot *)G.ct4.p;
         A.mask = G.ct4_mask;
         A.acct_base = 0;
         A.tm = (CtTimer *)G.ct4_tm.p;
         A.info = (CtInfo *)G.ct4_info.p;
-        A.mark = (uint32_t *)G.ct4_mark.p;
-        A.sum = (uint32_t *)G.ct4_sum.p;
+        A.ms = (uint2 *)G.ct4_ms.p;
     }
     A.hs = (uint32_t *)c->cta_hs.p;
     A.reqA = (uint64_t *)c->cta_req.p;
@@ -2732,8 +2730,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             ok = false;
     }
     if (!ok) {   // the scan's marks (and delete orders) go
-        if (hipMemsetAsync(A.mark, 0, 4 * slots, s) != hipSuccess ||
-            hipMemsetAsync(A.sum, 0, 4 * slots, s) != hipSuccess ||
+        if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return -EIO;
         return 1;
@@ -2782,8 +2779,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         // or summary may leak into the next apply, the claims made count,
         // and the next commit rebuilds the CT group from the synced maps
         (void)hipStreamSynchronize(s);
-        (void)hipMemsetAsync(A.mark, 0, 4 * slots, s);
-        (void)hipMemsetAsync(A.sum, 0, 4 * slots, s);
+        (void)hipMemsetAsync(A.ms, 0, 8 * slots, s);
         uint32_t cl = 0;
         (void)hipMemcpyAsync(&cl, A.cnt + CTA_CLAIMS, 4, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);

@@ -63,9 +63,6 @@
 #ifndef CFC_EXP
 #define CFC_EXP 0   // timing experiments only (1: no LPM, 2: no policy, 3: no key stores)
 #endif
-#ifndef CFC_PIPE
-#define CFC_PIPE 0   // timing experiment: the next header's directory load behind the policy probe
-#endif
 
 namespace cfc {
 
@@ -737,21 +734,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #pragma unroll
     for (int u = 0; u < U; u++)
         r1_issue<OPT, LBE>(in, LI, u * BLOCK + threadIdx.x, end, nx[u]);
-#if CFC_PIPE
-    // (timing experiment) the next header's directory load issued behind
-    // this one's policy probe, its headers a full iteration ahead
-    Hdr h[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        r1_take(nx[u], u * BLOCK + threadIdx.x, end, h[u]);
-        r2_issue<MODE>(T, S, h[u]);
-        r1_issue<OPT, LBE>(in, LI, (U + u) * BLOCK + threadIdx.x, end, nx[u]);
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
     for (uint32_t base = 0; base < end; base += BLOCK * U) {
-        const uint32_t nb = base + BLOCK * U;
-#if !CFC_PIPE
         Hdr h[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
@@ -759,25 +742,15 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #pragma unroll
         for (int u = 0; u < U; u++)
             r2_issue<MODE>(T, S, h[u]);
-#endif
 #pragma unroll
         for (int u = 0; u < U; u++)
             r3_identity<MODE, CT, LB>(T, S, E, h[u]);
-#if CFC_PIPE
-        Hdr hn[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            r1_take(nx[u], nb + u * BLOCK + threadIdx.x, end, hn[u]);
-            r2_issue<MODE>(T, S, hn[u]);
-            r1_issue<OPT, LBE>(in, LI, nb + (U + u) * BLOCK + threadIdx.x, end, nx[u]);
-        }
-#else
         // the next iteration's headers, behind this one's policy probe (the
         // last iteration re-reads the slice's last header)
+        const uint32_t nb = base + BLOCK * U;
 #pragma unroll
         for (int u = 0; u < U; u++)
             r1_issue<OPT, LBE>(in, LI, nb + u * BLOCK + threadIdx.x, end, nx[u]);
-#endif
 #pragma unroll
         for (int u = 0; u < U; u++)
             r4_verdict<MODE, CT, NT, LB>(T, S, E, h[u]);
@@ -841,11 +814,6 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
             acc.flush(s_met);
             iter = 0;
         }
-#if CFC_PIPE
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            h[u] = hn[u];
-#endif
     }
     acc.flush(s_met);
     __syncthreads();

@@ -163,8 +163,9 @@ struct CtaArgs {
     uint32_t mask, acct_base;
     CtTimer *tm;
     CtInfo *info;
-    uint32_t *mark;
-    uint32_t *sum;
+    // per slot {mark, summary} of this apply (one 8-byte word: route reads
+    // both with one random load)
+    uint2 *ms;
     uint32_t *hs;                // [2n] hit slot per header and stage
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
     uint32_t req_cap, cx_cap;

@@ -358,6 +358,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                             act = TC_ACT_SHOT;
                             ver = DROP_CT_UNKNOWN_PROTO;
                             met0 = mkey6<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_INGRESS);
+                            if (LB)   // (ipv6_policy's rewrite precedes its ct_lookup6)
+                                pda.w &= 0xFFFF0000u;
                         } else {
                             // ipv6_policy's ct_lookup6 (bpf_lxc.c:808)
                             CtResult c{CT_NEW, NONE, dport};

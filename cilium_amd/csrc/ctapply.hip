@@ -368,9 +368,11 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
 
 // ---- scan: ops, hit slots, ordered marks, create requests.  Four headers
 // per thread and step, each phase's loads for all four issued before any is
-// waited for: the inputs, the destination endpoints, the hit slots' report
-// state (the pass is a chain of dependent loads per header; one header per
-// thread and step left it waiting on one chain at a time).
+// waited for: the inputs, then the destination endpoints (the pass is a
+// chain of dependent loads per header; one header per thread and step left
+// it waiting on one chain at a time).  A slot is ordered by a delete or a
+// RST/FIN (ACTION_CLOSE) among its ops, never by the entry's own closing
+// bits: k_cta_finish resolves those without a load here (see there).
 // TWO: the mode has two CT stages per header (egress); else only stage 0
 // exists and the odd hit-slot entries are never read (k_cta_route).
 constexpr int SCAN_U = 4;
@@ -454,13 +456,6 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 }
             }
         }
-        // the hit slots' closing bits, loads together
-        uint32_t clo[SCAN_U][2];
-#pragma unroll
-        for (int u = 0; u < SCAN_U; u++)
-#pragma unroll
-            for (int st = 0; st < NST; st++)
-                clo[u][st] = slot[u][st] != HS_NONE ? A.tm[slot[u][st]].flags : 0u;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
@@ -476,13 +471,13 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     // dropped hot flow deletes its entry once per packet:
                     // only a lower order than the one stored needs the
                     // atomic)
-                    mark_or(&A.mark[sl], MARK_ORDERED | MARK_DEL);
+                    mark_or(&A.ms[sl].x, MARK_ORDERED | MARK_DEL);
                     const uint32_t v = 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1);
-                    if (__hip_atomic_load(&A.sum[sl], __ATOMIC_RELAXED,
+                    if (__hip_atomic_load(&A.ms[sl].y, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) < v)
-                        atomicMax(&A.sum[sl], v);
-                } else if (act[u][st] == 2 || ((clo[u][st] >> 16) & 3)) {
-                    mark_or(&A.mark[sl], MARK_ORDERED);
+                        atomicMax(&A.ms[sl].y, v);
+                } else if (act[u][st] == 2) {   // RST / FIN: ACTION_CLOSE
+                    mark_or(&A.ms[sl].x, MARK_ORDERED);
                 }
             }
             if (i < A.n) {
@@ -577,7 +572,7 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
             if (slot == NONE) {
                 bool fresh;
                 slot = find_or_insert<V6>(A, k.d, k.s, k.z, k.w, &fresh);
-                mark_or(&A.mark[slot], MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
+                mark_or(&A.ms[slot].x, MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
                 first = fresh;
                 claims += fresh;
                 if (nk < 4) {
@@ -671,8 +666,9 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
         }
 #pragma unroll
         for (int u = 0; u < RU; u++) {
-            mk[u] = slot[u] != HS_NONE ? A.mark[slot[u]] : 0u;
-            sm[u] = slot[u] != HS_NONE ? A.sum[slot[u]] : 0u;
+            const uint2 v = slot[u] != HS_NONE ? A.ms[slot[u]] : make_uint2(0, 0);
+            mk[u] = v.x;
+            sm[u] = v.y;
         }
         bool ordered[RU];
         uint32_t nord = 0;
@@ -696,7 +692,7 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
                 const uint32_t bits = (in ? tfl : tfl << 8) | (in ? 1u << 16 : 1u << 17) |
                                       ((tcp && !(mt[u] & CFC_HF_TCP_CLOSE)) ? 1u << 18 : 0u);
                 if ((sm[u] | bits) != sm[u])
-                    atomicOr(&A.sum[slot[u]], bits);
+                    atomicOr(&A.ms[slot[u]].y, bits);
             }
             nord += ordered[u];
         }
@@ -844,7 +840,7 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     if (r0 > 0 && (uint32_t)(cx[r0 - 1] >> A.ob) == slot)
         return;
     const uint64_t omask = (1ull << A.ob) - 1;
-    const bool was_fresh = (A.mark[slot] & MARK_FRESH) != 0;
+    const bool was_fresh = (A.ms[slot].x & MARK_FRESH) != 0;
     bool live = !was_fresh, created = false, deleted = false;
     St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.tm, slot);
     uint64_t acct[4] = {0, 0, 0, 0};   // [tx pk, tx by, rx pk, rx by] added / set
@@ -922,12 +918,18 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
         inf.y |= CTI_UPDATED;
     }
     A.info[slot] = inf;
-    A.mark[slot] = 0;
-    A.sum[slot] = 0;
+    A.ms[slot] = make_uint2(0, 0);
 }
 
-// ---- finish: the summaries of unordered slots.  With no closing bit set
-// and no RST/FIN, every hit re-arms the timeout, so the final state is:
+// ---- finish: the summaries of unordered slots.  Their hits are plain
+// ACTION_CREATE or ACTION_UNSPEC (RST/FIN and deletes are ordered), and a
+// closing bit is only ever set by a TCP RST/FIN, on a TCP entry, whose
+// other packets are ACTION_CREATE: the first such hit clears both closing
+// bits and re-arms the timeout (__ct_lookup, conntrack.h:259-266; a dead
+// entry skips the first update and takes the second — one update either
+// way), so an entry with closing bits ends with them cleared and the
+// summary applied.  With no closing bit set every hit re-arms the timeout,
+// so the final state is:
 // seen_non_syn |= any TCP hit without the close bit; lifetime from the last
 // hit = now + (TCP ? (seen_non_syn ? TCP : SYN) : NONTCP); per direction
 // with hits, flags_seen |= their flags and last_report = now iff the
@@ -946,7 +948,7 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < FU; u++) {
             const uint64_t s = base + u * 256 + threadIdx.x;
-            m[u] = s < slots ? A.sum[s] : 0u;
+            m[u] = s < slots ? A.ms[s].y : 0u;
         }
 #pragma unroll
         for (int u = 0; u < FU; u++) {
@@ -962,8 +964,9 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             if (!m[u])
                 continue;
             const uint64_t s = base + u * 256 + threadIdx.x;
-            A.sum[s] = 0;
+            A.ms[s].y = 0;
             St &x = e[u];
+            x.bits &= ~(RX_CLOSING | TX_CLOSING);
             const bool is_tcp = (w[u] & 0xFF) == 6;
             if (is_tcp && (m[u] & (1u << 18)))
                 x.bits |= SEEN_NON_SYN;

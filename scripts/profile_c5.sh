@@ -2,10 +2,11 @@
 # rocprofv3 passes over the C5 (conntrack) bench on the GPU box:
 # kernel trace + stats, then one PMC pass per counter group (never combined
 # with tracing).  Each pass has its own time limit; stops at the first
-# failure.
+# failure.  usage: profile_c5.sh OUTDIR [extra bench args, e.g. --ct-apply]
 set -e
 OUT=${1:-gpurun_out/prof_c5}
-ARGS="--workload c5 --steps 3 --warmup 1 --no-cpu"
+shift || true
+ARGS="--workload c5 --steps 3 --warmup 1 --no-cpu $*"
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run \

@@ -144,6 +144,7 @@ def _ct_worker(rank, world, port, family, q):
             dp.ct_apply(bt, out, mode, 0)
             torch.cuda.synchronize()
             vers.append((idx + a, out.verdict.cpu().numpy()))
+        dp.counters_sync()   # the device's CONNTRACK_ACCOUNTING into the maps
         rows = np.asarray(ct_rows(dp, dp.ct_fds), np.uint8).reshape(-1, 104)
         st = dp.stats()
         dp.close()
