@@ -222,7 +222,16 @@ def main():
         nt_out = out_struct(out)
         nt_stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
-    def step():
+    # --ct-apply: HIP events around the apply and the GC of each timed step
+    # (both synchronise with the host inside: the events bracket that too)
+    ct_ev = []
+
+    def ev():
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    def step(timed=False):
         if args.ct_apply:   # fresh new flows: their source ports re-drawn
             salt[0] += 1
             p[new_idx] = new_ports ^ ((salt[0] * 0x9E37) & 0xFFFF)
@@ -230,14 +239,20 @@ def main():
             dp.set_clock(clock["now"])
         dp.classify_v4(batch, mode, ep_lxc, out=out)
         if args.ct_apply:
+            e0 = ev() if timed else None
             dp.ct_apply(batch, out, mode, ep_lxc)
+            e1 = ev() if timed else None
+            e2 = None
             # EnableConntrackGC's loop (pkg/endpointmanager/conntrack.go:96-125)
             if args.gc_interval and clock["now"] - clock["last_gc"] >= args.gc_interval:
                 g = dp.ct_gc(-1, clock["now"])
+                e2 = ev() if timed else None
                 clock["last_gc"] = clock["now"]
                 clock["gcs"] += 1
                 clock["gc_deleted"] += g["deleted"]
                 clock["alive"] = g["alive"]
+            if timed:
+                ct_ev.append((e0, e1, e2))
         if args.notify:   # records stay on the device (no sync in the step)
             LL.check(dp.L.cfc_monitor_events_v4(
                 dp.h, ctypes.byref(nt_hdr), ctypes.byref(nt_out), mode, ep_lxc,
@@ -272,7 +287,7 @@ def main():
     w0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        step()
+        step(timed=True)
         evs[i][1].record(stream)
     if world > 1:
         allreduce_counters(dp)   # the only collective: counter SUM over RCCL
@@ -501,6 +516,12 @@ def main():
             "path_host_calls": st2["ct_apply_host"],
             "apply_and_gc_ms_per_step": round(call_ms - tm["classify_ms"] / args.steps
                                               - count_ms, 4),
+            # HIP events around cfc_ct_apply_v4 and cfc_ct_gc of each step
+            "apply_ms_per_step": round(float(np.mean([a.elapsed_time(b)
+                                                      for a, b, _ in ct_ev])), 4),
+            "gc_ms_per_run": round(float(np.mean([b.elapsed_time(c) for _, b, c in ct_ev
+                                                  if c is not None])), 4)
+            if any(c is not None for _, _, c in ct_ev) else None,
             "clock_s_per_step": args.step_seconds,
             "gc_interval_s": args.gc_interval,
             "gc_runs": clock["gcs"],

@@ -210,6 +210,7 @@ struct cfc_ctx {
     } last_cls;
     uint64_t log_used = 0;       // CtLog entries since the last sync
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
+    DevBuf cta_lbr, cta_reqs;     // a load balancer's service step per header (LbRec4/6)
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -318,8 +319,9 @@ Map *ct_slot_key(const Epoch &E, int family, const uint32_t *d, const uint32_t *
 }
 
 // struct ct_entry fields the device keeps (CtTimer, CtInfo) into a value:
-// lifetime @32, bits @36 (rx/tx_closing, seen_non_syn; others kept),
-// rev_nat_index @38, tx/rx_flags_seen @42/43, src_sec_id @44, last_tx/rx
+// lifetime @32, bits @36 (rx/tx_closing, seen_non_syn, lb_loopback with a
+// load balancer; others kept), rev_nat_index @38, slave @40 (with a load
+// balancer), tx/rx_flags_seen @42/43, src_sec_id @44, last_tx/rx
 // @48/52
 void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
 {
@@ -328,6 +330,11 @@ void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
         memcpy(&bits, &v[36], 2);
     bits = (uint16_t)((bits & ~(1u | 2u | 16u)) | ((r.flags >> 16) & 3) |
                       ((r.flags & CTT_NON_SYN) ? 16u : 0u));
+    if (r.pad >> 31) {   // the load balancer's ct_state (ct4_lb / ct6_lb)
+        bits = (uint16_t)((bits & ~8u) | (((r.pad >> 16) & 1) ? 8u : 0u));
+        const uint16_t slave = (uint16_t)(r.pad & 0xFFFF);
+        memcpy(&v[40], &slave, 2);
+    }
     memcpy(&v[32], &r.lifetime, 4);
     memcpy(&v[36], &bits, 2);
     v[42] = (char)((r.flags >> 8) & 0xFF);
@@ -353,9 +360,10 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
         Ct6Slot *ct6 = (Ct6Slot *)G.ct6.p;
         CtTimer *tm = (CtTimer *)G.ct6_tm.p;
         CtInfo *info = (CtInfo *)G.ct6_info.p;
+        const uint4 *lb6 = (const uint4 *)G.ct6_lb.p;
         uint32_t n = 0;
         if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-            cta_collect6(ct6, tm, info, slots, nullptr, 0, cnt, s) ||
+            cta_collect6(ct6, tm, info, lb6, slots, nullptr, 0, cnt, s) ||
             hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return -EIO;
@@ -366,7 +374,7 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
             CtSyncRec6 *dr = (CtSyncRec6 *)c->cta_sync.p;
             uint32_t n2 = 0;
             if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-                cta_collect6(ct6, tm, info, slots, dr, n, cnt, s) ||
+                cta_collect6(ct6, tm, info, lb6, slots, dr, n, cnt, s) ||
                 hipMemcpyAsync(rec.data(), dr, sizeof(CtSyncRec6) * n, hipMemcpyDeviceToHost,
                                s) != hipSuccess ||
                 hipMemcpyAsync(&n2, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -405,6 +413,7 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
                     r4.last_tx = r.last_tx;
                     r4.flags = r.flags;
                     r4.lifetime = r.lifetime;
+                    r4.pad = r.pad;
                     std::string v(m->value_bytes(), '\0');
                     ct_value_from_dev(v, r4, true);
                     m->put_raw(key, v);
@@ -427,6 +436,7 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
                     r4.last_tx = r.last_tx;
                     r4.flags = r.flags;
                     r4.lifetime = r.lifetime;
+                    r4.pad = r.pad;
                     ct_value_from_dev(it->second.val, r4, false);
                 }
             }
@@ -460,10 +470,11 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
             memcpy(&v[dir ? 8 : 24], &len, 8);
             const uint32_t life = g.now + 60, last = 5u < g.now ? g.now : 0u;
             const uint16_t bits = 16;   // seen_non_syn: "for ICMP, there is no SYN"
-            const uint16_t rev = (uint16_t)g.rev;
+            const uint16_t rev = (uint16_t)g.rev, slave = (uint16_t)g.slave;
             memcpy(&v[32], &life, 4);
             memcpy(&v[36], &bits, 2);
             memcpy(&v[38], &rev, 2);
+            memcpy(&v[40], &slave, 2);
             memcpy(&v[44], &g.sec, 4);
             memcpy(&v[dir ? 52 : 48], &last, 4);
             it->second->put_raw(std::string(k, 38), v);
@@ -498,8 +509,9 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
     Ct4Slot *ct4 = (Ct4Slot *)G.ct4.p;
     CtTimer *tm = (CtTimer *)G.ct4_tm.p;
     CtInfo *info = (CtInfo *)G.ct4_info.p;
+    const uint4 *lb4 = (const uint4 *)G.ct4_lb.p;
     if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-        cta_collect(ct4, tm, info, slots, nullptr, 0, cnt, s) ||
+        cta_collect(ct4, tm, info, lb4, slots, nullptr, 0, cnt, s) ||
         hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -510,7 +522,7 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
         CtSyncRec *dr = (CtSyncRec *)c->cta_sync.p;
         uint32_t n2 = 0;
         if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-            cta_collect(ct4, tm, info, slots, dr, n, cnt, s) ||
+            cta_collect(ct4, tm, info, lb4, slots, dr, n, cnt, s) ||
             hipMemcpyAsync(rec.data(), dr, sizeof(CtSyncRec) * n, hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||
             hipMemcpyAsync(&n2, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -609,9 +621,14 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
             memcpy(&v[dir ? 0 : 16], &one, 8);
             memcpy(&v[dir ? 8 : 24], &len, 8);
             const uint32_t life = g.now + 60, last = 5u < g.now ? g.now : 0u;
-            const uint16_t bits = 16;   // seen_non_syn: "for ICMP, there is no SYN"
+            // seen_non_syn ("for ICMP, there is no SYN"), and a load
+            // balancer's ct_state
+            const uint16_t bits = (uint16_t)(16u | (((g.lbw >> 16) & 1) ? 8u : 0u));
+            const uint16_t rev = (uint16_t)(g.lbw & 0xFFFF), slave = (uint16_t)g.slave;
             memcpy(&v[32], &life, 4);
             memcpy(&v[36], &bits, 2);
+            memcpy(&v[38], &rev, 2);
+            memcpy(&v[40], &slave, 2);
             memcpy(&v[44], &g.sec, 4);
             memcpy(&v[dir ? 52 : 48], &last, 4);
             it->second->put_raw(std::string(k, 14), v);
@@ -2629,8 +2646,6 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
         return 1;
-    if (V6 ? LbHost6(c).on() : LbHost(c).on())   // service entries, reverse NAT: the host walk
-        return 1;
     // the device table must be the maps as committed: no host-side CT
     // change waiting for a commit
     uint64_t sig[NGROUPS];
@@ -2646,21 +2661,34 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     }
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
+    // a load balancer: its per-slot ct_state is on the device (the apply
+    // writes it with every create), and an egress batch replays the service
+    // step (lb4_local / lb6_local, the egress reply's reverse NAT: k_cta_lb)
+    const bool lbt = V6 ? (E.T.lb6 || E.T.rnat6) : (E.T.lb4 || E.T.rnat4);
+    DevBuf &lbst = V6 ? G.ct6_lb : G.ct4_lb;
+    if (lbt && !lbst.p)
+        return 1;
+    const bool lbm = lbt && mode == CFC_MODE_EGRESS;
+    const uint64_t k3 = lbm ? 3 : 2;   // requests per header, writes per create
     const uint64_t n = in->n, slots = V6 ? G.ct6_host.size() : G.ct4_host.size();
-    if (!slots || !(V6 ? G.ct6_info.p : G.ct4_info.p) || n >= (1ull << 29))
+    if (!slots || !(V6 ? G.ct6_info.p : G.ct4_info.p) || n >= (lbm ? 1ull << 27 : 1ull << 28))
         return 1;
     // the batch's classify (its CT bytes, verdicts and the workspace's hit
     // slots) may have run on another stream
     order_after_launches(c, s);
-    int ob = 2, sb = 1;
-    while ((1ull << ob) < 4 * n)
+    int ob = 4, sb = 1;   // (op order: ((2 * header + stage) << 3) | write << 1)
+    while ((1ull << ob) < (lbm ? 32 : 16) * n)
         ob++;
     while ((1ull << sb) < slots)
         sb++;
     if (ob + sb > 64)
         return 1;
-    if (c->cta_hs.ensure(8 * n) || c->cta_req.ensure(16 * n) ||
+    if (c->cta_hs.ensure((lbm ? 16 : 8) * n) || c->cta_req.ensure(8 * k3 * n) ||
         c->cta_cnt.ensure(4 * CTA_NCNT))
+        return -ENOMEM;
+    if (lbm && (c->cta_lbr.ensure((V6 ? sizeof(LbRec6) : sizeof(LbRec4)) * n) ||
+                c->cta_reqs.ensure(16 * n) ||
+                c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)n))))
         return -ENOMEM;
     CtaArgs A{};
     A.T = E.T;
@@ -2695,13 +2723,23 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     }
     A.hs = (uint32_t *)c->cta_hs.p;
     A.reqA = (uint64_t *)c->cta_req.p;
-    A.req_cap = (uint32_t)std::min<uint64_t>(2 * n, 0xFFFFFFFFu);
+    A.req_cap = (uint32_t)std::min<uint64_t>(k3 * n, 0xFFFFFFFFu);
     A.cnt = (uint32_t *)c->cta_cnt.p;
     A.ob = ob;
     A.slot_bits = sb;
+    A.lb = lbst.p ? (uint4 *)lbst.p : nullptr;
+    if (lbm) {
+        A.lbr = c->cta_lbr.p;
+        A.hash = in->hash;
+        A.reqS = (uint64_t *)c->cta_reqs.p;
+        A.reqS2 = A.reqS + n;
+        A.sort_tmp = c->cta_tmp.p;
+        A.sort_tmp_bytes = c->cta_tmp.bytes;
+    }
     {   // this batch's hit slots from its classify launch, if still there
+        // (not with a service step: its tuples may differ from the launch's)
         const auto &L = c->last_cls;
-        if (L.valid && L.family == (V6 ? 6 : 4) && L.gen == c->ct_gen && L.ct == out->ct &&
+        if (!lbm && L.valid && L.family == (V6 ? 6 : 4) && L.gen == c->ct_gen && L.ct == out->ct &&
             L.saddr == (const void *)in->saddr && L.n == n && L.mode == mode && L.ep == ep_lxc) {
             A.ck1 = (const uint32_t *)((const char *)c->ws + L.k1);
             A.ck2 = L.k2 ? (const uint32_t *)((const char *)c->ws + L.k2) : nullptr;
@@ -2722,11 +2760,11 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     const size_t log_rec = V6 ? sizeof(CtLog6) : sizeof(CtLog);
     const uint64_t used = V6 ? (uint64_t)G.n_ct6 + G.tomb6
                              : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
-    bool ok = 4 * (used + ins + 2 * nreqA) <= 3 * slots && nreqA <= A.req_cap;
+    bool ok = 4 * (used + ins + k3 * nreqA) <= 3 * slots && nreqA <= A.req_cap;
     for (auto &kv : c->maps) {
         const Map *m = kv.second.get();
         if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
-            m->kv.size() - m->gc_pending + claims + log_used + 2 * nreqA > m->max_entries)
+            m->kv.size() - m->gc_pending + claims + log_used + k3 * nreqA > m->max_entries)
             ok = false;
     }
     if (!ok) {   // the scan's marks (and delete orders) go
@@ -2736,12 +2774,12 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         return 1;
     }
     const uint64_t nr = std::max<uint64_t>(nreqA, 1);
-    const uint64_t cx_cap = nhit + 2 * nreqA + 64;
+    const uint64_t cx_cap = nhit + k3 * nreqA + 64;
     const uint64_t log_need = log_used + nreqA;
     if (cx_cap > 0xFFFFFFFFu)
         return 1;
-    if (c->cta_req2.ensure(24 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
-        c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)std::max<uint64_t>(cx_cap, nr))))
+    if (c->cta_req2.ensure(40 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
+        c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)std::max<uint64_t>(cx_cap, 2 * nr))))
         return -ENOMEM;
     if (logbuf.bytes < log_rec * log_need) {   // grow, keeping the entries
         DevBuf nl;
@@ -2756,9 +2794,9 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     }
     uint64_t *r2 = (uint64_t *)c->cta_req2.p, *cx = (uint64_t *)c->cta_cx.p;
     A.reqA2 = r2;
-    A.reqB = r2 + nr;
-    A.reqB2 = r2 + 2 * nr;
-    A.req_cap = (uint32_t)nr;
+    A.reqB = r2 + nr;        // (a create's related entry and reverse-NAT entry)
+    A.reqB2 = r2 + 3 * nr;
+    A.req_cap = (uint32_t)(2 * nr);
     A.cx = cx;
     A.cx2 = cx + cx_cap;
     A.cx_cap = (uint32_t)cx_cap;

@@ -118,13 +118,31 @@ struct CtLog {
     uint32_t dirlen;      // dir << 31 | len
     uint32_t sec;         // src_sec_id
     uint32_t seq, order;  // apply sequence, header order
+    uint32_t lbw, slave;  // rev_nat_index | lb_loopback << 16, slave (a load balancer's creates)
 };
 // the same for an IPv6 create (ct_create6, conntrack.h:615-662): 16-byte
 // addresses, and the rev_nat_index ipv6_policy sets (bpf_lxc.c:787-788)
 struct CtLog6 {
     uint4 x, y;           // saddr, daddr (k2 order), raw
-    uint32_t w, now, dirlen, sec, seq, order, rev, pad;
+    uint32_t w, now, dirlen, sec, seq, order, rev, slave;
 };
+// What the service step of an egress batch with a load balancer left for one
+// header (k_cta_lb: lb4_local / lb6_local and the egress reply's reverse NAT,
+// replayed in header order per CT_SERVICE entry): the tuple of the sender's
+// CT lookup (saddr, tda, tpt), the packet every later stage sees (psa, pda,
+// ppt), LBF_* | LBR_RESLAVE, the ct_state of the sender's create (lbw:
+// rev_nat_index | loopback << 16), slv: slave | slave0 << 16 (slave0: the
+// selection a new CT_SERVICE entry's ICMP entry keeps), svc: the CT_SERVICE
+// entry's slot when the batch started (NONE), addr / sva: ct_state->addr
+// and svc_addr (ct_create4's reverse-NAT entry)
+struct LbRec4 {
+    uint32_t tda, psa, pda, tpt, ppt, fl, lbw, slv, svc, addr, sva;
+};
+struct LbRec6 {
+    uint4 tda, psa, pda;
+    uint32_t tpt, ppt, fl, lbw, slv, svc, addr, sva;
+};
+constexpr uint32_t LBR_RESLAVE = 8;   // ct_update4/6_slave ran
 // one changed slot for the host mirror
 struct CtSyncRec {
     uint32_t slot;
@@ -140,7 +158,8 @@ struct CtSyncRec6 {
     uint32_t last_rx, last_tx, flags, lifetime;
     uint32_t pad;
 };
-enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NCNT = 8 };
+enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NSVC,
+       CTA_NCNT = 8 };
 struct CtaArgs {
     DevTables T;
     // addresses: one word per header (IPv4), four (IPv6, raw network order)
@@ -166,7 +185,15 @@ struct CtaArgs {
     // per slot {mark, summary} of this apply (one 8-byte word: route reads
     // both with one random load)
     uint2 *ms;
-    uint32_t *hs;                // [2n] hit slot per header and stage
+    uint32_t *hs;                // [2n] hit slot per header and stage ([4n] with lbr)
+    // an egress batch with a load balancer: per header LbRec4 / LbRec6 (its
+    // CT_SERVICE ops are virtual headers n..2n-1), null otherwise
+    void *lbr;
+    const uint32_t *hash;        // skb->hash per header, or null (CFC_FLOW_HASH)
+    uint64_t *reqS, *reqS2;      // the CT_SERVICE ops' requests, by home slot
+    // per slot ct_state of the load balancer (ct4_lb / ct6_lb), or null:
+    // written for every entry the apply creates
+    uint4 *lb;
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
     uint32_t req_cap, cx_cap;
     uint32_t cx_base;            // route: its ordered ops start here
@@ -182,10 +209,12 @@ size_t cta_sort_tmp_bytes(uint32_t n);
 // v6: the batch is IPv6 (A.ct6, A.log6)
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);
 int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s);
-int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec *out,
-                uint32_t cap, uint32_t *cnt, hipStream_t s);
-int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec6 *out,
-                 uint32_t cap, uint32_t *cnt, hipStream_t s);
+// lb (ct4_lb / ct6_lb, or null): the records carry slave | loopback << 16 |
+// 1 << 31 in pad
+int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+                CtSyncRec *out, uint32_t cap, uint32_t *cnt, hipStream_t s);
+int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+                 CtSyncRec6 *out, uint32_t cap, uint32_t *cnt, hipStream_t s);
 int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
 int cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n, hipStream_t s);
 

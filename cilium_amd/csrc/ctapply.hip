@@ -49,6 +49,22 @@ __device__ __forceinline__ void mark_or(uint32_t *m, uint32_t bits)
 }
 constexpr uint32_t HS_NONE = 0xFFFFFFFFu;
 
+// An op's place in the batch, the low bits of every request and list entry:
+// ((2 * i + st) << 3) | sec << 1 — i the header (with a load balancer,
+// i = n + h is the CT_SERVICE op of header h), st its CT stage, sec the
+// write: the op itself, its create's related ICMP entry, its create's
+// reverse-NAT entry (ct_create4 with ct_state->addr), or a hit on an entry
+// this batch created (the destination's lookup finding what the sender's
+// create just wrote).  Bit 0 is free: a request's first-create mark.
+constexpr uint32_t SEC_OP = 0, SEC_REL = 1, SEC_KX = 2, SEC_FHIT = 3;
+__device__ __forceinline__ uint32_t ord_of(uint64_t i, int st, uint32_t sec)
+{
+    return (uint32_t)(((2 * i + (uint64_t)st) << 3) | sec << 1);
+}
+__device__ __forceinline__ uint64_t ord_hdr(uint32_t o) { return o >> 4; }
+__device__ __forceinline__ int ord_st(uint32_t o) { return (int)((o >> 3) & 1); }
+__device__ __forceinline__ uint32_t ord_sec(uint32_t o) { return (o >> 1) & 3; }
+
 __device__ __forceinline__ uint32_t wave_count(uint32_t *ctr, bool want)
 {
     const uint64_t m = __ballot(want);
@@ -171,6 +187,15 @@ struct Op {
     Addr<V6> sa, da;           // k1 = (da, sa, z1, w1), k2 = (sa, da, z2, w2)
     uint32_t z1, w1;           // k1: the tuple as loaded (REPLY / RELATED)
     uint32_t z2, w2;           // k2: reversed (ESTABLISHED / create)
+    // the ct_state a create writes with the entry (ct4_lb / ct6_lb words:
+    // rev_nat_index | lb_loopback << 16, slave; its related entry's slave)
+    uint32_t lbw, slave, slave_rel;
+    bool reslave;              // a CT_SERVICE op's ct_update4/6_slave
+    // ct_create4's reverse-NAT entry (kx: the create writes one): key
+    // (kxa, kxs, z2, kxw)
+    bool kx;
+    Addr<V6> kxa, kxs;
+    uint32_t kxw;
 };
 
 // owner word of the destination endpoint's CT maps (cilium_lxc lookup)
@@ -204,23 +229,68 @@ __device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint4 da)
     }
 }
 
-// one header's inputs of the apply
+template <bool V6>
+using LbRecT = typename std::conditional<V6, LbRec6, LbRec4>::type;
+
+// one header's inputs of the apply; with a load balancer (LB) its service
+// step's record too, and svcop: the header's CT_SERVICE op (virtual header
+// n + i) rather than its CT stages
 template <bool V6>
 struct ScanIn {
     uint32_t cb, pt, mt, ver, ident, tf, k1, k2;
     Addr<V6> sa, da;
+    Addr<V6> tda, psa, pda;
+    uint32_t tpt, ppt, lfl, lbw, slv, svc, addr, sva;
+    bool svcop;
 };
 
 // stage st of a header, from its inputs; dsto: the owner word of the
 // destination endpoint's CT maps (the stages that are not the sender's)
-template <bool V6>
+template <bool V6, bool LB>
 __device__ __forceinline__ Op<V6> decode_from(const CtaArgs &A, const ScanIn<V6> &r, int st,
                                               uint32_t dsto)
 {
     Op<V6> o;
     o.kind = OP_NONE;
+    o.lbw = o.slave = o.slave_rel = 0;
+    o.reslave = o.kx = false;
+    if (LB && r.svcop) {
+        // lb4_local / lb6_local's ct_lookup4/6(CT_SERVICE): the tuple as
+        // loaded with TUPLE_F_SERVICE, one lookup (conntrack.h:580); a miss
+        // creates the entry (ct_create4/6 with ct_state {slave}, lb.h:699-
+        // 712).  The key sits in the k2 fields, which creates insert.
+        if (st != 0 || !(r.lfl & LBF_SVC))
+            return o;
+        o.proto = r.mt & 0xFF;
+        if (o.proto != 6 && o.proto != 17 && o.proto != icmp_proto<V6>())
+            return o;
+        o.dir = CT_SERVICE;   // (the tx side of the entry, as egress)
+        o.owner = A.ep_owner;
+        o.len = r.mt >> 16;
+        o.is_tcp = o.proto == 6;
+        o.syn = (r.mt & CFC_HF_TCP_CLOSE) != 0;
+        o.tfl = o.is_tcp ? r.tf : 0u;
+        o.action = ct_action(V6, o.proto, r.pt, r.mt);
+        o.sec = 0;
+        o.rev = 0;
+        const CtProbe k = ct_probe<V6>(o.proto, r.pt, CT_SERVICE, o.owner);
+        o.sa = r.da;
+        o.da = r.sa;
+        o.z1 = o.z2 = k.z1;
+        o.w1 = o.w2 = k.w1;
+        o.ki_form = o.proto == icmp_proto<V6>() && (k.w1 & 0x200u) && k.z1 == 0;
+        // the entry's slave: the selection, or ct_update4/6_slave's; its
+        // ICMP entry keeps the selection (slave0)
+        o.reslave = (r.lfl & LBR_RESLAVE) != 0;
+        o.slave = r.slv & 0xFFFF;
+        o.slave_rel = r.slv >> 16;
+        o.kind = r.svc != NONE ? OP_HIT : OP_CREATE;
+        return o;
+    }
     const uint32_t cs = (r.cb >> (4 * st)) & 0xF;
     if (!(cs & CFC_CT_DONE))
+        return o;
+    if (LB && (r.lfl & LBF_DROP))   // (no backend after all: no CT stage ran)
         return o;
     const int last = (r.cb & (CFC_CT_DONE << 4)) ? 1 : 0;
     const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
@@ -229,26 +299,54 @@ __device__ __forceinline__ Op<V6> decode_from(const CtaArgs &A, const ScanIn<V6>
     o.proto = r.mt & 0xFF;
     if (o.proto != 6 && o.proto != 17 && o.proto != icmp_proto<V6>())
         return o;
+    // the tuple this stage looked up: with a load balancer, the sender's
+    // (saddr, the service step's daddr and L4 word), then the packet as
+    // translated and reverse-NATed
+    Addr<V6> ka = r.sa, kb = r.da;
+    uint32_t pt = r.pt;
+    if (LB) {
+        ka = eg ? r.sa : r.psa;
+        kb = eg ? r.tda : r.pda;
+        pt = eg ? r.tpt : r.ppt;
+    }
     o.len = r.mt >> 16;
     o.is_tcp = o.proto == 6;
     o.syn = (r.mt & CFC_HF_TCP_CLOSE) != 0;
     o.tfl = o.is_tcp ? r.tf : 0u;
-    o.action = ct_action(V6, o.proto, r.pt, r.mt);
+    o.action = ct_action(V6, o.proto, pt, r.mt);
     o.sec = A.mode == CFC_MODE_EGRESS ? A.ep_sec : r.ident;
     // ipv6_policy's rev_nat_index: daddr.s6_addr32[3] as a u16
     // (bpf_lxc.c:787-788); IPv4 creates outside a load balancer carry 0
     if constexpr (V6)
-        o.rev = o.dir == CT_INGRESS ? (r.da.w & 0xFFFF) : 0u;
+        o.rev = o.dir == CT_INGRESS ? (kb.w & 0xFFFF) : 0u;
     else
         o.rev = 0;
-    const CtProbe k = ct_probe<V6>(o.proto, r.pt, (int)o.dir, o.owner);
-    o.sa = r.sa;
-    o.da = r.da;
+    const bool svc = LB && eg && (r.lfl & LBF_SVC);
+    if (svc) {   // lb4_local / lb6_local's ct_state for the create
+        o.rev = r.lbw & 0xFFFF;
+        o.slave = o.slave_rel = r.slv & 0xFFFF;
+    }
+    o.lbw = V6 ? o.rev : (svc ? r.lbw : 0u);
+    const CtProbe k = ct_probe<V6>(o.proto, pt, (int)o.dir, o.owner);
+    o.sa = ka;
+    o.da = kb;
     o.z1 = k.z1; o.w1 = k.w1;
     o.z2 = k.z2; o.w2 = k.w2;
     // a k2 of ICMP-error form is its own related entry (ct_create4/6 write
     // the same key twice)
     o.ki_form = o.proto == icmp_proto<V6>() && (k.w2 & 0x200u) && k.z2 == 0;
+    if constexpr (!V6) {
+        // ct_create4 with ct_state->addr: the entry again with daddr
+        // ct_state->addr (a looped-back flow's: TUPLE_F_IN, saddr svc_addr;
+        // conntrack.h:731-739)
+        if (svc && r.addr) {
+            const bool loop = (r.lbw >> 16) & 1;
+            o.kx = true;
+            o.kxa = r.addr;
+            o.kxs = loop ? r.sva : kb;
+            o.kxw = loop ? ct_word(o.proto, 1u, o.owner) : k.w2;
+        }
+    }
     const uint32_t b = cs & CFC_CT_RES_MASK;
     const bool dropped = st == last && (int32_t)r.ver == DROP_POLICY;
     if (b >= 2)
@@ -260,9 +358,12 @@ __device__ __forceinline__ Op<V6> decode_from(const CtaArgs &A, const ScanIn<V6>
     return o;
 }
 
-template <bool V6>
+template <bool V6, bool LB>
 __device__ __forceinline__ void load_in(const CtaArgs &A, uint64_t i, ScanIn<V6> &r)
 {
+    r.svcop = LB && i >= A.n;
+    if (r.svcop)
+        i -= A.n;
     r.cb = A.ctb[i];
     r.sa = ld_addr<V6>(A.sa, i);
     r.da = ld_addr<V6>(A.da, i);
@@ -271,21 +372,45 @@ __device__ __forceinline__ void load_in(const CtaArgs &A, uint64_t i, ScanIn<V6>
     r.ver = (uint32_t)A.ver[i];
     r.ident = A.ident[i];
     r.tf = A.tf ? A.tf[i] : 0u;
+    if constexpr (LB) {
+        const LbRecT<V6> &l = reinterpret_cast<const LbRecT<V6> *>(A.lbr)[i];
+        r.tda = l.tda;
+        r.psa = l.psa;
+        r.pda = l.pda;
+        r.tpt = l.tpt;
+        r.ppt = l.ppt;
+        r.lfl = l.fl;
+        r.lbw = l.lbw;
+        r.slv = l.slv;
+        r.svc = l.svc;
+        r.addr = l.addr;
+        r.sva = l.sva;
+    }
 }
 
+template <bool V6, bool LB>
+__device__ __forceinline__ Op<V6> decode_t(const CtaArgs &A, uint64_t i, int st)
+{
+    ScanIn<V6> r;
+    if (!LB || i < A.n) {
+        r.cb = A.ctb[i];
+        if (!((r.cb >> (4 * st)) & CFC_CT_DONE)) {
+            Op<V6> o;
+            o.kind = OP_NONE;
+            o.kx = false;
+            return o;
+        }
+    }
+    load_in<V6, LB>(A, i, r);
+    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
+    return decode_from<V6, LB>(A, r, st,
+                               (eg || r.svcop) ? 0u : dst_owner(A.T, LB ? r.pda : r.da));
+}
+// op (header i, stage st); i >= n: a CT_SERVICE op (A.lbr)
 template <bool V6>
 __device__ __forceinline__ Op<V6> decode(const CtaArgs &A, uint64_t i, int st)
 {
-    ScanIn<V6> r;
-    r.cb = A.ctb[i];
-    if (!((r.cb >> (4 * st)) & CFC_CT_DONE)) {
-        Op<V6> o;
-        o.kind = OP_NONE;
-        return o;
-    }
-    load_in<V6>(A, i, r);
-    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
-    return decode_from<V6>(A, r, st, eg ? 0u : dst_owner(A.T, r.da));
+    return A.lbr ? decode_t<V6, true>(A, i, st) : decode_t<V6, false>(A, i, st);
 }
 
 __device__ __forceinline__ uint32_t find(const CtaArgs &A, uint32_t x, uint32_t y, uint32_t z,
@@ -388,7 +513,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         for (int u = 0; u < SCAN_U; u++) {   // inputs (no branches)
             const uint64_t i = base + u * 256 + threadIdx.x;
             const uint64_t j = i < A.n ? i : A.n - 1;
-            load_in<V6>(A, j, r[u]);
+            load_in<V6, false>(A, j, r[u]);
             r[u].k1 = A.ck1 ? A.ck1[j] : NONE;
             r[u].k2 = A.ck2 ? A.ck2[j] : NONE;
             if (i >= A.n)
@@ -434,7 +559,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         for (int u = 0; u < SCAN_U; u++) {
 #pragma unroll
             for (int st = 0; st < NST; st++) {
-                const Op<V6> o = decode_from<V6>(A, r[u], st, dsto[u]);
+                const Op<V6> o = decode_from<V6, false>(A, r[u], st, dsto[u]);
                 kind[u][st] = o.kind;
                 act[u][st] = o.kind == OP_NONE ? 0u : o.action;
                 slot[u][st] = HS_NONE;
@@ -472,7 +597,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     // only a lower order than the one stored needs the
                     // atomic)
                     mark_or(&A.ms[sl].x, MARK_ORDERED | MARK_DEL);
-                    const uint32_t v = 0xFFFFFFFFu - (uint32_t)((2 * i + st) << 1);
+                    const uint32_t v = 0xFFFFFFFFu - ord_of(i, st, SEC_OP);
                     if (__hip_atomic_load(&A.ms[sl].y, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) < v)
                         atomicMax(&A.ms[sl].y, v);
@@ -496,7 +621,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 if (kind[u][st] != OP_CREATE)
                     continue;
                 if (rq < A.req_cap)
-                    A.reqA[rq] = pack(A, home[u][st], (uint32_t)((2 * i + st) << 1));
+                    A.reqA[rq] = pack(A, home[u][st], ord_of(i, st, SEC_OP));
                 rq++;
             }
         }
@@ -504,8 +629,303 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
     wave_add(&A.cnt[CTA_NHIT], nhit);
 }
 
-// key of a request: k2 of its op (round A) or the ICMP entry k2 relates
-// (round B: ports 0, nexthdr ICMP / ICMPv6, flags | TUPLE_F_RELATED)
+// ---- the service step of an egress batch with a load balancer.  The
+// reference runs lb4_local / lb6_local packet by packet, so a header finds
+// the CT_SERVICE entry as the headers before it left it (created, its slave
+// re-selected).  k_cta_lb runs the step for every header against the
+// batch's starting table; k_cta_svc replays, per CT_SERVICE key, the headers
+// after the first one in order with the entry as it then is; the scan takes
+// the records (LbRec4 / LbRec6).
+
+// the CT_SERVICE entry as a header finds it
+struct SvcState {
+    bool exists;
+    uint32_t slave, loop;
+};
+
+// lb4_local (lb.h:590-776) for header i, given the entry's state (left as
+// the header leaves it), then the egress reply's reverse NAT (bpf_lxc.c:
+// 565-576, lb4_rev_nat) against the batch's starting table; svc: the
+// entry's slot at the batch's start
+__device__ void lb_step(const CtaArgs &A, uint64_t i, uint32_t svc, SvcState &st, LbRec4 &o)
+{
+    const DevTables &T = A.T;
+    const uint32_t sa = A.sa[i], da = A.da[i], pt = A.pt[i], proto = A.mt[i] & 0xFF;
+    const bool l4 = proto == 6 || proto == 17;
+    o = LbRec4{da, sa, da, pt, pt, 0u, 0u, 0u, svc, 0u, 0u};
+    uint32_t kd = l4 ? pt >> 16 : 0u;
+    uint4 a, b;
+    if (T.lb4 && (l4 || proto == 1) && lb4_service(T, da, kd, 0, a, b)) {
+        const uint32_t hash = A.hash ? A.hash[i] : flow_hash4(sa, da, pt, proto);
+        // a hit's slave and loopback from the entry, else lb4_select_slave
+        uint32_t slave = st.exists ? st.slave : hash % (a.w >> 16) + 1;
+        uint32_t loop = st.exists ? st.loop : 0u;
+        const uint32_t slave0 = slave;
+        uint4 c, d;
+        bool ok = lb4_get(T, da, kd, slave, c, d), reslave = false;   // lb4_lookup_slave
+        if (!ok) {   // the fall-back: the key as it stands, slave set
+            ok = lb4_service(T, da, kd, slave, c, d);
+            if (ok) {
+                slave = hash % (c.w >> 16) + 1;
+                reslave = true;
+            }
+        }
+        o.fl = LBF_SVC | (ok ? 0u : LBF_DROP) | (reslave ? LBR_RESLAVE : 0u);
+        if (ok) {
+            const uint32_t target = c.z, port = c.w & 0xFFFF;
+            o.addr = target;
+            if (sa == target) {   // loopback (lb.h:753-767)
+                loop = 1;
+                o.addr = IPV4_LOOPBACK;
+                o.sva = sa;
+                o.psa = IPV4_LOOPBACK;
+            }
+            if (loop)
+                o.fl |= LBF_LOOP;
+            else
+                o.tda = target;
+            o.pda = target;
+            if (port && kd != port && l4)   // lb4_xlate's L4 dport
+                o.ppt = (o.ppt & 0xFFFFu) | port << 16;
+            o.tpt = o.ppt;
+            o.lbw = (d.x & 0xFFFF) | loop << 16;
+        }
+        o.slv = (slave & 0xFFFF) | slave0 << 16;
+        if (!st.exists)
+            st.loop = 0;
+        st.exists = true;
+        st.slave = slave;
+    }
+    if (!(o.fl & LBF_DROP) && T.ct4_lb && (l4 || proto == 1)) {
+        const CtProbe k = ct_probe<false>(proto, o.tpt, CT_EGRESS, A.ep_owner);
+        const uint32_t s1 = ct4_find(T, o.tda, sa, k.z1, k.w1);
+        if (s1 != NONE)
+            lb4_rev_nat(T, ld16(T.ct4_lb + s1), proto, o.psa, o.pda, o.ppt);
+    }
+}
+// lb6_local (lb.h:427-481, no loopback case), then the egress reply's
+// lb6_rev_nat
+__device__ void lb_step(const CtaArgs &A, uint64_t i, uint32_t svc, SvcState &st, LbRec6 &o)
+{
+    const DevTables &T = A.T;
+    const uint4 sa = ld_addr<true>(A.sa, i), da = ld_addr<true>(A.da, i);
+    const uint32_t pt = A.pt[i], proto = A.mt[i] & 0xFF;
+    const bool l4 = proto == 6 || proto == 17;
+    o.tda = o.pda = da;
+    o.psa = sa;
+    o.tpt = o.ppt = pt;
+    o.fl = o.lbw = o.slv = o.addr = o.sva = 0;
+    o.svc = svc;
+    uint32_t kd = l4 ? pt >> 16 : 0u;
+    uint4 b, tg;
+    if (T.lb6 && (l4 || proto == 58) && lb6_service(T, da, kd, 0, b, tg)) {
+        const uint32_t hash = A.hash ? A.hash[i] : flow_hash6(sa, da, pt, proto);
+        uint32_t slave = st.exists ? st.slave : hash % (b.y >> 16) + 1;   // lb6_select_slave
+        const uint32_t slave0 = slave;
+        uint4 b2, tg2;
+        bool ok = lb6_get(T, da, kd, slave, b2, tg2), reslave = false;
+        if (!ok) {
+            ok = lb6_service(T, da, kd, slave, b2, tg2);
+            if (ok) {
+                slave = hash % (b2.y >> 16) + 1;
+                reslave = true;
+            }
+        }
+        o.fl = LBF_SVC | (ok ? 0u : LBF_DROP) | (reslave ? LBR_RESLAVE : 0u);
+        if (ok) {
+            o.tda = o.pda = tg2;   // lb6_xlate
+            const uint32_t port = b2.y & 0xFFFF;
+            if (port && kd != port && l4)
+                o.ppt = (o.ppt & 0xFFFFu) | port << 16;
+            o.tpt = o.ppt;
+            o.lbw = b2.z & 0xFFFF;
+        }
+        o.slv = (slave & 0xFFFF) | slave0 << 16;
+        st.exists = true;
+        st.slave = slave;
+        st.loop = 0;
+    }
+    if (!(o.fl & LBF_DROP) && T.ct6_lb && (l4 || proto == 58)) {
+        const CtProbe k = ct_probe<true>(proto, o.tpt, CT_EGRESS, A.ep_owner);
+        const uint32_t s1 = ct6_find(T, o.tda, sa, k.z1, k.w1);
+        if (s1 != NONE)
+            lb6_rev_nat(T, ld16(T.ct6_lb + s1).x, proto, o.psa, o.ppt);
+    }
+}
+
+// the CT_SERVICE key of header i: the tuple as loaded, TUPLE_F_SERVICE
+template <bool V6>
+__device__ __forceinline__ void svc_key(const CtaArgs &A, uint64_t i, Addr<V6> &d, Addr<V6> &s,
+                                        uint32_t &z, uint32_t &w)
+{
+    const CtProbe k = ct_probe<V6>(A.mt[i] & 0xFF, A.pt[i], CT_SERVICE, A.ep_owner);
+    d = ld_addr<V6>(A.da, i);
+    s = ld_addr<V6>(A.sa, i);
+    z = k.z1;
+    w = k.w1;
+}
+
+// one thread per header: its service step against the starting table, and
+// a request for its CT_SERVICE op when the reference reaches lb4_local /
+// lb6_local with it (the header reached a CT stage, or lb4_local dropped it)
+template <bool V6>
+__global__ __launch_bounds__(256) void k_cta_lb(CtaArgs A)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    bool want = false;
+    uint32_t home = 0;
+    if (i < A.n) {
+        const uint32_t proto = A.mt[i] & 0xFF;
+        uint32_t svc = NONE;
+        SvcState st{false, 0u, 0u};
+        Addr<V6> d, s;
+        uint32_t z, w;
+        svc_key<V6>(A, i, d, s, z, w);
+        if (proto == 6 || proto == 17 || proto == icmp_proto<V6>()) {
+            svc = find(A, d, s, z, w);
+            if (svc != NONE && A.lb) {
+                const uint4 lw = A.lb[svc];
+                st = SvcState{true, lw.y, V6 ? 0u : (lw.x >> 16) & 1};
+            } else if (svc != NONE) {
+                st = SvcState{true, 0u, 0u};
+            }
+        }
+        LbRecT<V6> o;
+        lb_step(A, i, svc, st, o);
+        reinterpret_cast<LbRecT<V6> *>(A.lbr)[i] = o;
+        want = (o.fl & LBF_SVC) && ((A.ctb[i] & CFC_CT_DONE) || A.ver[i] == DROP_NO_SERVICE);
+        home = khash(d, s, z, w) & A.mask;
+    }
+    const uint32_t r = block_count(&A.cnt[CTA_NSVC], want);
+    if (want)
+        A.reqS[r] = pack(A, home, ord_of(A.n + i, 0, SEC_OP));
+}
+
+// one thread per home slot of the sorted CT_SERVICE requests: per key, the
+// headers after its first in header order, each with the entry as the one
+// before it left it
+template <bool V6>
+__global__ __launch_bounds__(256) void k_cta_svc(CtaArgs A, uint64_t *req, uint32_t nreq)
+{
+    const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
+    if (r0 >= nreq)
+        return;
+    const uint64_t home = req[r0] >> A.ob;
+    if (r0 > 0 && (req[r0 - 1] >> A.ob) == home)
+        return;
+    const uint64_t omask = (1ull << A.ob) - 1;
+    LbRecT<V6> *L = reinterpret_cast<LbRecT<V6> *>(A.lbr);
+    for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
+        if (req[r] & 1)   // (a later header of a key done before)
+            continue;
+        const uint64_t i = ord_hdr((uint32_t)(req[r] & omask)) - A.n;
+        Addr<V6> d, s;
+        uint32_t z, w;
+        svc_key<V6>(A, i, d, s, z, w);
+        // the entry as header i leaves it: created or hit, its slave the
+        // selection (or the re-selection)
+        const LbRecT<V6> l = L[i];
+        SvcState st{true, l.slv & 0xFFFF, 0u};
+        if constexpr (!V6)
+            st.loop = (l.svc != NONE && A.lb) ? (A.lb[l.svc].x >> 16) & 1 : 0u;
+        for (uint32_t q = r + 1; q < nreq && (req[q] >> A.ob) == home; q++) {
+            if (req[q] & 1)
+                continue;
+            const uint64_t iq = ord_hdr((uint32_t)(req[q] & omask)) - A.n;
+            Addr<V6> dq, sq;
+            uint32_t zq, wq;
+            svc_key<V6>(A, iq, dq, sq, zq, wq);
+            if (zq != z || wq != w || !aeq(dq, d) || !aeq(sq, s))
+                continue;
+            req[q] |= 1ull;
+            LbRecT<V6> o;
+            lb_step(A, iq, l.svc, st, o);
+            L[iq] = o;
+        }
+    }
+}
+
+// ---- scan with a load balancer: one header per thread, its CT_SERVICE op
+// (hit slot, or a create request of virtual header n + i) and its stages
+// with the service step's tuples.  A stage hit on a key the starting table
+// lacks is on an entry this batch creates before it (the sender's create,
+// found by the destination's lookup): a request, counted in the fold.
+template <bool V6>
+__global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
+{
+    uint32_t nhit = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool in = i < A.n;
+        ScanIn<V6> r;
+        load_in<V6, true>(A, in ? i : A.n - 1, r);
+        if (!in)
+            r.cb = 0;
+        const bool any = (r.cb & (CFC_CT_DONE | CFC_CT_DONE << 4)) != 0;
+        const uint32_t dsto = any ? dst_owner(A.T, r.pda) : 0u;
+        uint32_t hs2[3] = {HS_NONE, HS_NONE, HS_NONE};
+        uint64_t rq[3];
+        uint32_t ncr = 0;
+        for (int st = 0; st < 2; st++) {
+            const Op<V6> o = decode_from<V6, true>(A, r, st, dsto);
+            if (o.kind == OP_HIT || o.kind == OP_DELETE) {
+                const bool rev = ((r.cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
+                const uint32_t sl = rev ? find(A, o.da, o.sa, o.z1, o.w1)
+                                        : find(A, o.sa, o.da, o.z2, o.w2);
+                if (sl == NONE) {
+                    const uint32_t h = rev ? khash(o.da, o.sa, o.z1, o.w1)
+                                           : khash(o.sa, o.da, o.z2, o.w2);
+                    rq[ncr++] = pack(A, h & A.mask, ord_of(i, st, SEC_FHIT));
+                    continue;
+                }
+                hs2[st] = sl;
+                nhit++;
+                if (o.kind == OP_DELETE) {
+                    mark_or(&A.ms[sl].x, MARK_ORDERED | MARK_DEL);
+                    const uint32_t v = 0xFFFFFFFFu - ord_of(i, st, SEC_OP);
+                    if (__hip_atomic_load(&A.ms[sl].y, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) < v)
+                        atomicMax(&A.ms[sl].y, v);
+                } else if (o.action == 2) {
+                    mark_or(&A.ms[sl].x, MARK_ORDERED);
+                }
+            } else if (o.kind == OP_CREATE) {
+                rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP));
+            }
+        }
+        if (in && ((r.cb & CFC_CT_DONE) || (int32_t)r.ver == DROP_NO_SERVICE)) {
+            ScanIn<V6> rs = r;
+            rs.svcop = true;
+            const Op<V6> o = decode_from<V6, true>(A, rs, 0, 0u);
+            if (o.kind == OP_HIT) {
+                hs2[2] = r.svc;
+                nhit++;
+                if (o.action == 2)
+                    mark_or(&A.ms[r.svc].x, MARK_ORDERED);
+                if (o.reslave && A.lb)   // ct_update4/6_slave
+                    A.lb[r.svc].y = o.slave;
+            } else if (o.kind == OP_CREATE) {
+                rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask,
+                                 ord_of(A.n + i, 0, SEC_OP));
+            }
+        }
+        if (in) {
+            *reinterpret_cast<uint2 *>(A.hs + 2 * i) = make_uint2(hs2[0], hs2[1]);
+            *reinterpret_cast<uint2 *>(A.hs + 2 * (A.n + i)) = make_uint2(hs2[2], HS_NONE);
+        }
+        const uint32_t q = block_count_n(&A.cnt[CTA_NREQA], ncr);
+        for (uint32_t k = 0; k < ncr; k++)
+            if (q + k < A.req_cap)
+                A.reqA[q + k] = rq[k];
+    }
+    wave_add(&A.cnt[CTA_NHIT], nhit);
+}
+
+// key of a request, by its write: k2 of its op (a create), the ICMP entry
+// k2 relates (ports 0, nexthdr ICMP / ICMPv6, flags | TUPLE_F_RELATED), the
+// op's reverse-NAT entry, or the key a hit looked up (k1 for REPLY /
+// RELATED, else k2)
 template <bool V6>
 struct ReqKey {
     Addr<V6> d, s;
@@ -516,26 +936,39 @@ struct ReqKey {
     }
 };
 template <bool V6>
-__device__ __forceinline__ ReqKey<V6> req_key(const CtaArgs &A, uint32_t order2, bool related,
-                                              Op<V6> *po)
+__device__ __forceinline__ ReqKey<V6> req_key(const CtaArgs &A, uint32_t ord, Op<V6> *po)
 {
-    const uint64_t i = order2 >> 2;
-    const int st = (order2 >> 1) & 1;
+    const uint64_t i = ord_hdr(ord);
+    const int st = ord_st(ord);
     *po = decode<V6>(A, i, st);
-    ReqKey<V6> k{po->sa, po->da, po->z2, po->w2};
-    if (related) {
-        const uint32_t fl = (po->w2 >> 8) & 7;
+    const Op<V6> &o = *po;
+    ReqKey<V6> k{o.sa, o.da, o.z2, o.w2};
+    switch (ord_sec(ord)) {
+    case SEC_REL:
         k.z = 0;
-        k.w = ct_word(icmp_proto<V6>(), fl | 2u, po->owner);
+        k.w = ct_word(icmp_proto<V6>(), ((o.w2 >> 8) & 7) | 2u, o.owner);
+        break;
+    case SEC_KX:
+        k.d = o.kxa;
+        k.s = o.kxs;
+        k.w = o.kxw;
+        break;
+    case SEC_FHIT:
+        if (((A.ctb[i] >> (4 * st)) & CFC_CT_RES_MASK) >= 2)
+            k = ReqKey<V6>{o.da, o.sa, o.z1, o.w1};
+        break;
+    default:
+        break;
     }
     return k;
 }
 
 // ---- insert: one thread per home slot; keys deduped in registers (a fifth
 // distinct key of one home slot is found by rescanning the run).  A key's
-// first create also needs its related ICMP entry (round 0): the request is
-// marked (bit 0 of its word, free in a request) and k_cta_related writes
-// the entries — no per-request atomic on a shared counter here.
+// first create also writes its related ICMP entry and, with a load
+// balancer's ct_state, its reverse-NAT entry (round 1): the request is
+// marked (bit 0 of its word) and k_cta_related makes those requests — no
+// per-request atomic on a shared counter here.
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, uint32_t nreq,
                                                     int round, uint32_t cx_off)
@@ -550,9 +983,9 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
         uint32_t ks[4];
         int nk = 0;
         for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
-            const uint32_t order2 = (uint32_t)(req[r] & omask) & ~1u;
+            const uint32_t ord = (uint32_t)(req[r] & omask) & ~1u;
             Op<V6> o;
-            const ReqKey<V6> k = req_key<V6>(A, order2, round == 1, &o);
+            const ReqKey<V6> k = req_key<V6>(A, ord, &o);
             uint32_t slot = NONE;
             for (int j = 0; j < nk; j++)
                 if (kk[j] == k)
@@ -563,7 +996,7 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
                 // run may still have it
                 for (uint32_t q = r0; q < r && nk == 4; q++) {
                     Op<V6> oq;
-                    if (req_key<V6>(A, (uint32_t)(req[q] & omask), round == 1, &oq) == k) {
+                    if (req_key<V6>(A, (uint32_t)(req[q] & omask) & ~1u, &oq) == k) {
                         slot = find(A, k.d, k.s, k.z, k.w);
                         break;
                     }
@@ -584,8 +1017,8 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
             // r of the round has its own place in the list
             const uint32_t c = cx_off + r;
             if (c < A.cx_cap)
-                A.cx[c] = pack(A, slot, order2 | (uint32_t)round);
-            if (round == 0 && first && !o.ki_form)
+                A.cx[c] = pack(A, slot, ord);
+            if (round == 0 && first && ord_sec(ord) == SEC_OP)
                 req[r] |= 1ull;
         }
     }
@@ -595,22 +1028,27 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
 // ---- related: one thread per (sorted) round-0 request; a marked one is a
 // key's first create, whose related ICMP entry goes into the device table
 // for an ANY map (UDP, ICMP echo: a round-1 request) or into the host log
-// for a TCP map (no lookup reaches it there)
+// for a TCP map (no lookup reaches it there), and whose reverse-NAT entry
+// (ct_create4 with ct_state->addr) is a round-1 request
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *req,
                                                      uint32_t nreq)
 {
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
     const uint64_t v = r < nreq ? req[r] : 0ull;
-    const uint32_t order2 = (uint32_t)(v & ((1ull << A.ob) - 1)) & ~1u;
+    const uint32_t ord = (uint32_t)(v & ((1ull << A.ob) - 1)) & ~1u;
     Op<V6> o;
     o.is_tcp = false;
+    o.ki_form = true;
+    o.kx = false;
     if (v & 1)
-        o = decode<V6>(A, order2 >> 2, (order2 >> 1) & 1);
-    const bool lg = (v & 1) && o.is_tcp, rb = (v & 1) && !o.is_tcp;
+        o = decode<V6>(A, ord_hdr(ord), ord_st(ord));
+    const bool rel = (v & 1) && !o.ki_form;
+    const bool lg = rel && o.is_tcp, rb = rel && !o.is_tcp, kx = (v & 1) && o.kx;
     const uint32_t l = block_count(&A.cnt[CTA_NLOG], lg);
-    const uint32_t b = block_count(&A.cnt[CTA_NREQB], rb);
+    uint32_t b = block_count_n(&A.cnt[CTA_NREQB], (uint32_t)rb + (uint32_t)kx);
     const uint32_t fl = ((o.w2 >> 8) & 7) | 2u;
+    const uint32_t dirlen = (o.dir == CT_INGRESS ? 1u << 31 : 0u) | o.len;
     if (lg && l < A.log_cap) {
         if constexpr (V6) {
             CtLog6 &g = A.log6[A.log_base + l];
@@ -618,28 +1056,36 @@ __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *
             g.y = o.da;
             g.w = ct_word(icmp_proto<V6>(), fl, o.owner);
             g.now = A.now;
-            g.dirlen = o.dir << 31 | o.len;
+            g.dirlen = dirlen;
             g.sec = o.sec;
             g.seq = A.seq;
-            g.order = order2;
+            g.order = ord;
             g.rev = o.rev;
-            g.pad = 0;
+            g.slave = o.slave_rel;
         } else {
             CtLog &g = A.log[A.log_base + l];
             g.x = o.sa;
             g.y = o.da;
             g.w = ct_word(icmp_proto<V6>(), fl, o.owner);
             g.now = A.now;
-            g.dirlen = o.dir << 31 | o.len;
+            g.dirlen = dirlen;
             g.sec = o.sec;
             g.seq = A.seq;
-            g.order = order2;
+            g.order = ord;
+            g.lbw = o.lbw;
+            g.slave = o.slave_rel;
         }
     }
-    if (rb && b < A.req_cap) {
-        const uint32_t h = khash(o.sa, o.da, 0u, ct_word(icmp_proto<V6>(), fl, o.owner)) & A.mask;
-        A.reqB[b] = pack(A, h, order2);
+    if (rb) {
+        if (b < A.req_cap) {
+            const uint32_t h =
+                khash(o.sa, o.da, 0u, ct_word(icmp_proto<V6>(), fl, o.owner)) & A.mask;
+            A.reqB[b] = pack(A, h, ord | SEC_REL << 1);
+        }
+        b++;
     }
+    if (kx && b < A.req_cap)
+        A.reqB[b] = pack(A, khash(o.kxa, o.kxs, o.z2, o.kxw) & A.mask, ord | SEC_KX << 1);
 }
 
 // ---- route: hits on unordered slots -> summary; the rest -> ordered list.
@@ -649,9 +1095,11 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
     constexpr int RU = 4;
     // item k is header stage j = k (egress: two CT stages per header) or
-    // j = 2k (one stage: the odd stages never hold a hit)
+    // j = 2k (one stage: the odd stages never hold a hit); with a load
+    // balancer (egress) j in [2n, 4n) are the CT_SERVICE ops (virtual
+    // headers n..2n-1, stage 0: the entry's tx side)
     const bool two = A.mode == CFC_MODE_EGRESS;
-    const uint64_t n2 = 2 * A.n, nk = two ? n2 : A.n;
+    const uint64_t n2 = 2 * A.n, nk = A.lbr ? 2 * n2 : two ? n2 : A.n;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * RU;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < nk; base += stride) {
         uint32_t slot[RU], mk[RU], sm[RU], mt[RU], tf[RU];
@@ -660,7 +1108,9 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
             const uint64_t k = base + u * 256 + threadIdx.x;
             const uint64_t j = two ? k : 2 * k;
             slot[u] = k < nk ? A.hs[j] : HS_NONE;
-            const uint64_t i = (k < nk ? j : n2 - 1) >> 1;
+            uint64_t i = (k < nk ? j : 0) >> 1;
+            if (i >= A.n)
+                i -= A.n;
             mt[u] = A.mt[i];
             tf[u] = A.tf ? A.tf[i] : 0u;
         }
@@ -681,7 +1131,7 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
                 continue;
             if ((mk[u] & (MARK_DEL | MARK_PUTC)) == MARK_DEL) {
                 // a deleted entry: its first delete stands for all its ops
-                ordered[u] = (uint32_t)(j << 1) == 0xFFFFFFFFu - sm[u];
+                ordered[u] = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - sm[u];
             } else if (mk[u] & MARK_ORDERED) {
                 ordered[u] = true;
             } else {
@@ -704,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
             if (!ordered[u])
                 continue;
             if (c < A.cx_cap)
-                A.cx[c] = pack(A, slot[u], (uint32_t)(j << 1));
+                A.cx[c] = pack(A, slot[u], ord_of(j >> 1, (int)(j & 1), SEC_OP));
             c++;
         }
     }
@@ -792,12 +1242,12 @@ __device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St
 // such run is replayed.  A hot flow's hits in a Zipf batch become one op.
 // (Creates, deletes and related-entry writes are always kept.)
 template <bool V6>
-__device__ __forceinline__ uint32_t hit_sig(const CtaArgs &A, uint32_t order2)
+__device__ __forceinline__ uint32_t hit_sig(const CtaArgs &A, uint32_t ord)
 {
-    if (order2 & 1)
-        return 0;   // a related-entry write
-    const uint64_t i = order2 >> 2;
-    const int st = (order2 >> 1) & 1;
+    const uint64_t i = ord_hdr(ord);
+    if (ord_sec(ord) != SEC_OP || i >= A.n)
+        return 0;   // a create's second write, a counted hit, a CT_SERVICE op
+    const int st = ord_st(ord);
     const uint32_t cb = A.ctb[i];
     const uint32_t cs = (cb >> (4 * st)) & 0xF;
     const uint32_t b = cs & CFC_CT_RES_MASK;
@@ -828,7 +1278,7 @@ __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx
 }
 
 // ---- fold: one thread per slot of the sorted ordered list
-template <bool V6>
+template <bool V6, bool LB>
 __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
                                                   const uint32_t *pncx)
 {
@@ -841,36 +1291,51 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
         return;
     const uint64_t omask = (1ull << A.ob) - 1;
     const bool was_fresh = (A.ms[slot].x & MARK_FRESH) != 0;
-    bool live = !was_fresh, created = false, deleted = false;
+    bool live = !was_fresh, created = false, deleted = false, reslaved = false;
     St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.tm, slot);
     uint64_t acct[4] = {0, 0, 0, 0};   // [tx pk, tx by, rx pk, rx by] added / set
-    uint32_t sec = 0, rev = 0;
+    uint32_t sec = 0, rev = 0, lbx = 0, lby = 0;
     // the next op's header is loaded (branch-free) while this one is
     // replayed; the owner word does not matter here (the slot is the key),
     // so no endpoint lookup
     ScanIn<V6> cur;
-    load_in<V6>(A, (cx[r0] & omask) >> 2, cur);
+    load_in<V6, LB>(A, ord_hdr((uint32_t)(cx[r0] & omask)), cur);
     for (uint32_t r = r0; r < ncx && (uint32_t)(cx[r] >> A.ob) == slot; r++) {
-        const uint32_t order2 = (uint32_t)(cx[r] & omask);
+        const uint32_t ord = (uint32_t)(cx[r] & omask);
         ScanIn<V6> nxt;
-        load_in<V6>(A, (cx[r + 1 < ncx ? r + 1 : r] & omask) >> 2, nxt);
-        const Op<V6> o = decode_from<V6>(A, cur, (order2 >> 1) & 1, 0u);
+        load_in<V6, LB>(A, ord_hdr((uint32_t)(cx[r + 1 < ncx ? r + 1 : r] & omask)), nxt);
+        const Op<V6> o = decode_from<V6, LB>(A, cur, ord_st(ord), 0u);
         cur = nxt;
         const uint32_t d = o.dir == CT_INGRESS ? 2 : 0;
-        if (order2 & 1) {   // ct_create's related-entry write: overwrite
+        const uint32_t wr = ord_sec(ord);
+        if (wr == SEC_REL || wr == SEC_KX) {
+            // ct_create's related-entry (or reverse-NAT entry) write: overwrite
             e = fresh(A.now, o.is_tcp, o.dir);
-            e.bits |= SEEN_NON_SYN;
+            if (wr == SEC_REL)
+                e.bits |= SEEN_NON_SYN;
             live = created = true;
             acct[0] = acct[1] = acct[2] = acct[3] = 0;
             acct[d] = 1;
             acct[d + 1] = o.len;
             sec = o.sec;
             rev = o.rev;
+            lbx = o.lbw;
+            lby = wr == SEC_REL ? o.slave_rel : o.slave;
+        } else if (wr == SEC_FHIT) {   // a hit the classify launch could not count
+            if (live) {
+                hit(e, A.now, o);
+                acct[d] += 1;
+                acct[d + 1] += o.len;
+            }
         } else if (o.kind == OP_CREATE) {
             if (live) {   // created earlier in this batch: a counted hit
                 hit(e, A.now, o);
                 acct[d] += 1;
                 acct[d + 1] += o.len;
+                if (o.reslave) {   // ct_update4/6_slave
+                    lby = o.slave;
+                    reslaved = true;
+                }
             } else {
                 e = fresh(A.now, o.is_tcp, o.dir);
                 if (o.ki_form)
@@ -881,6 +1346,8 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
                 acct[d + 1] = o.len;
                 sec = o.sec;
                 rev = o.rev;
+                lbx = o.lbw;
+                lby = o.slave;
             }
         } else if (live) {   // OP_HIT, OP_DELETE
             hit(e, A.now, o);
@@ -890,6 +1357,11 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
             }
         }
     }
+    // the load balancer's per-slot ct_state of what this batch wrote
+    if (A.lb && live && created)
+        A.lb[slot] = make_uint4(lbx, lby, 0, 0);
+    else if (A.lb && live && reslaved)
+        A.lb[slot].y = lby;
     unsigned long long *ac =
         reinterpret_cast<unsigned long long *>(A.T.ct_acct) + 4ull * (A.acct_base + slot);
     CtInfo inf = A.info[slot];
@@ -1006,7 +1478,8 @@ struct SyncOf<true> {
 };
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::Slot *ct,
-                                                     CtTimer *tm, CtInfo *info, uint64_t slots,
+                                                     CtTimer *tm, CtInfo *info, const uint4 *lb,
+                                                     uint64_t slots,
                                                      typename SyncOf<V6>::Rec *out,
                                                      uint32_t cap, uint32_t *cnt)
 {
@@ -1022,7 +1495,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::
             in[u] = s < slots ? info[s] : CtInfo{0, 0};
             nd += (in[u].y >> 16) != 0;
         }
-        uint4 k[CU], t[CU], k2[CU], k3[CU];
+        uint4 k[CU], t[CU], k2[CU], k3[CU], l[CU];
 #pragma unroll
         for (int u = 0; u < CU; u++) {
             const uint64_t s = base + u * 256 + threadIdx.x;
@@ -1035,6 +1508,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::
                     k[u] = ld16(ct + s);
                 }
                 t[u] = ld16(tm + s);
+                l[u] = lb ? ld16(lb + s) : make_uint4(0, 0, 0, 0);
             }
         }
         uint32_t r = block_count_n(cnt, nd);
@@ -1062,6 +1536,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::
                 o.last_tx = t[u].y;
                 o.flags = t[u].z;
                 o.lifetime = t[u].w;
+                o.pad = lb ? (l[u].y & 0xFFFF) | ((l[u].x >> 16) & 1) << 16 | 1u << 31 : 0u;
                 info[s].y = in[u].y & 0xFFFFu;
             }
             r++;
@@ -1271,6 +1746,20 @@ size_t cta_sort_tmp_bytes(uint32_t n)
 template <bool V6>
 int cta_scan_t(const CtaArgs &A, hipStream_t s)
 {
+    if (A.lbr) {   // (an egress batch with a load balancer)
+        hipLaunchKernelGGL(k_cta_lb<V6>, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);
+        uint32_t ns = 0;
+        if (hipMemcpyAsync(&ns, A.cnt + CTA_NSVC, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        uint64_t *sorted;
+        if (int rc = sort_keys(A, A.reqS, A.reqS2, ns, A.ob + A.slot_bits, s, &sorted))
+            return rc;
+        if (ns)
+            hipLaunchKernelGGL(k_cta_svc<V6>, dim3((ns + 255) / 256), dim3(256), 0, s, A, sorted, ns);
+        hipLaunchKernelGGL(k_cta_scan_lb<V6>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
     if (A.mode == CFC_MODE_EGRESS)
         hipLaunchKernelGGL((k_cta_scan<V6, true>), dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
     else
@@ -1310,7 +1799,8 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t
     // ordered hits follow
     CtaArgs R = A;
     R.cx_base = nreqA + nreqB;
-    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for(2 * A.n, 8192)), dim3(256), 0, s, R);
+    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for((A.lbr ? 4 : 2) * A.n, 8192)), dim3(256), 0,
+                       s, R);
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -1332,8 +1822,12 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t
         if (hipcub::DeviceSelect::Flagged(A.sort_tmp, tb, sorted, keep, dst, nsel, (int)ncx, s) !=
             hipSuccess)
             return -EIO;
-        hipLaunchKernelGGL(k_cta_fold<V6>, dim3((ncx + 255) / 256), dim3(256), 0, s, A,
-                           (const uint64_t *)dst, (const uint32_t *)nsel);
+        if (A.lbr)
+            hipLaunchKernelGGL((k_cta_fold<V6, true>), dim3((ncx + 255) / 256), dim3(256), 0, s, A,
+                               (const uint64_t *)dst, (const uint32_t *)nsel);
+        else
+            hipLaunchKernelGGL((k_cta_fold<V6, false>), dim3((ncx + 255) / 256), dim3(256), 0, s,
+                               A, (const uint64_t *)dst, (const uint32_t *)nsel);
     }
     hipLaunchKernelGGL(k_cta_finish<V6>, dim3(blocks_for((uint64_t)A.mask + 1, 8192)),
                        dim3(256), 0, s, A);
@@ -1350,19 +1844,19 @@ int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, uint32_t *host_cnt, hipS
     return v6 ? cta_rest_t<true>(A, nreqA, host_cnt, s) : cta_rest_t<false>(A, nreqA, host_cnt, s);
 }
 
-int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec *out,
-                uint32_t cap, uint32_t *cnt, hipStream_t s)
+int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+                CtSyncRec *out, uint32_t cap, uint32_t *cnt, hipStream_t s)
 {
     hipLaunchKernelGGL(k_cta_collect<false>, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4,
-                       tm, info, slots, out, cap, cnt);
+                       tm, info, lb, slots, out, cap, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, uint64_t slots, CtSyncRec6 *out,
-                 uint32_t cap, uint32_t *cnt, hipStream_t s)
+int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+                 CtSyncRec6 *out, uint32_t cap, uint32_t *cnt, hipStream_t s)
 {
     hipLaunchKernelGGL(k_cta_collect<true>, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct6,
-                       tm, info, slots, out, cap, cnt);
+                       tm, info, lb, slots, out, cap, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
