@@ -4,6 +4,8 @@
 
 #include <algorithm>
 #include <cerrno>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -2751,6 +2753,10 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     const uint64_t nreqA = hc[CTA_NREQA], nhit = hc[CTA_NHIT];
+    // keys the batch may add: each create its own and its related entry,
+    // a load balancer's creates their reverse-NAT entry too (counted hits
+    // add none)
+    const uint64_t newk = 2 * (nreqA - hc[CTA_NFHIT]) + hc[CTA_NKX];
     // room for every create and its ICMP entry: the table below 3/4 load,
     // each CT map below max_entries; else the host path (which rebuilds)
     uint64_t &claims = V6 ? c->cta_claims6 : c->cta_claims;
@@ -2760,13 +2766,18 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     const size_t log_rec = V6 ? sizeof(CtLog6) : sizeof(CtLog);
     const uint64_t used = V6 ? (uint64_t)G.n_ct6 + G.tomb6
                              : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
-    bool ok = 4 * (used + ins + k3 * nreqA) <= 3 * slots && nreqA <= A.req_cap;
+    bool ok = 4 * (used + ins + newk) <= 3 * slots && nreqA <= A.req_cap;
     for (auto &kv : c->maps) {
         const Map *m = kv.second.get();
         if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
-            m->kv.size() - m->gc_pending + claims + log_used + k3 * nreqA > m->max_entries)
+            m->kv.size() - m->gc_pending + claims + log_used + newk > m->max_entries)
             ok = false;
     }
+    if (!ok && getenv("CFC_DEBUG_APPLY"))
+        fprintf(stderr, "cfc: CT apply to the host path: %llu requests, %llu new keys, "
+                        "%llu used of %llu slots\n", (unsigned long long)nreqA,
+                (unsigned long long)newk, (unsigned long long)(used + ins),
+                (unsigned long long)slots);
     if (!ok) {   // the scan's marks (and delete orders) go
         if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)

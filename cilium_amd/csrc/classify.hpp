@@ -158,8 +158,9 @@ struct CtSyncRec6 {
     uint32_t last_rx, last_tx, flags, lifetime;
     uint32_t pad;
 };
+// (NFHIT: requests that are counted hits; NKX: creates with a reverse-NAT entry)
 enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NSVC,
-       CTA_NCNT = 8 };
+       CTA_NFHIT, CTA_NKX, CTA_NCNT };
 struct CtaArgs {
     DevTables T;
     // addresses: one word per header (IPv4), four (IPv6, raw network order)

@@ -853,7 +853,7 @@ __global__ __launch_bounds__(256) void k_cta_svc(CtaArgs A, uint64_t *req, uint3
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
 {
-    uint32_t nhit = 0;
+    uint32_t nhit = 0, nfh = 0, nkx = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
         const uint64_t i = base + threadIdx.x;
@@ -877,6 +877,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                     const uint32_t h = rev ? khash(o.da, o.sa, o.z1, o.w1)
                                            : khash(o.sa, o.da, o.z2, o.w2);
                     rq[ncr++] = pack(A, h & A.mask, ord_of(i, st, SEC_FHIT));
+                    nfh++;
                     continue;
                 }
                 hs2[st] = sl;
@@ -892,6 +893,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                 }
             } else if (o.kind == OP_CREATE) {
                 rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP));
+                nkx += o.kx;
             }
         }
         if (in && ((r.cb & CFC_CT_DONE) || (int32_t)r.ver == DROP_NO_SERVICE)) {
@@ -920,6 +922,8 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                 A.reqA[q + k] = rq[k];
     }
     wave_add(&A.cnt[CTA_NHIT], nhit);
+    wave_add(&A.cnt[CTA_NFHIT], nfh);
+    wave_add(&A.cnt[CTA_NKX], nkx);
 }
 
 // key of a request, by its write: k2 of its op (a create), the ICMP entry

@@ -1,6 +1,7 @@
 # round 3: device CT apply for batches with a load balancer (run via gpurun)
 set -o pipefail
 mkdir -p gpurun_out/r3f
+export CFC_DEBUG_APPLY=1
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider"
 timeout -k 10 500 $T tests/test_gpu_lb.py > gpurun_out/r3f/t_lb.log 2>&1
 rc=$?
