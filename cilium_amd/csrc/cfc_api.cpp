@@ -2753,12 +2753,6 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     const uint64_t nreqA = hc[CTA_NREQA], nhit = hc[CTA_NHIT];
-    // keys the batch may add: each create its own and its related entry,
-    // a load balancer's creates their reverse-NAT entry too (counted hits
-    // add none)
-    const uint64_t newk = 2 * (nreqA - hc[CTA_NFHIT]) + hc[CTA_NKX];
-    // room for every create and its ICMP entry: the table below 3/4 load,
-    // each CT map below max_entries; else the host path (which rebuilds)
     uint64_t &claims = V6 ? c->cta_claims6 : c->cta_claims;
     uint64_t &ins = V6 ? c->cta_ins6 : c->cta_ins;
     uint64_t &log_used = V6 ? c->log6_used : c->log_used;
@@ -2766,13 +2760,41 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     const size_t log_rec = V6 ? sizeof(CtLog6) : sizeof(CtLog);
     const uint64_t used = V6 ? (uint64_t)G.n_ct6 + G.tomb6
                              : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
-    bool ok = 4 * (used + ins + newk) <= 3 * slots && nreqA <= A.req_cap;
-    for (auto &kv : c->maps) {
-        const Map *m = kv.second.get();
-        if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
-            m->kv.size() - m->gc_pending + claims + log_used + newk > m->max_entries)
-            ok = false;
+    const uint64_t nr = std::max<uint64_t>(nreqA, 1);
+    const uint64_t cx_cap = nhit + k3 * nreqA + 64;
+    const uint64_t log_need = log_used + nreqA;
+    bool ok = nreqA <= A.req_cap && cx_cap <= 0xFFFFFFFFu;
+    if (ok && (c->cta_req2.ensure(40 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
+               c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)std::max<uint64_t>(cx_cap, 2 * nr)))))
+        return -ENOMEM;
+    uint64_t *r2 = (uint64_t *)c->cta_req2.p, *cx = (uint64_t *)c->cta_cx.p;
+    A.reqA2 = r2;
+    A.sort_tmp = c->cta_tmp.p;
+    A.sort_tmp_bytes = c->cta_tmp.bytes;
+    // room for every key the batch adds: the table below 3/4 load, each CT
+    // map below max_entries; else the host path (which rebuilds).  First the
+    // quick bound — each create its key and its related entry, a load
+    // balancer's creates their reverse-NAT entry (counted hits add none) —
+    // and when that fails the exact count (k_cta_newkeys)
+    auto room = [&](uint64_t newk) {
+        bool r = 4 * (used + ins + newk) <= 3 * slots;
+        for (auto &kv : c->maps) {
+            const Map *m = kv.second.get();
+            if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
+                m->kv.size() - m->gc_pending + claims + log_used + newk > m->max_entries)
+                r = false;
+        }
+        return r;
+    };
+    uint64_t newk = 2 * (nreqA - hc[CTA_NFHIT]) + hc[CTA_NKX];
+    uint64_t *presorted = nullptr;
+    if (ok && !room(newk)) {
+        uint32_t exact = 0;
+        if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, &exact, s))
+            return -EIO;
+        newk = exact;
     }
+    ok = ok && room(newk);
     if (!ok && getenv("CFC_DEBUG_APPLY"))
         fprintf(stderr, "cfc: CT apply to the host path: %llu requests, %llu new keys, "
                         "%llu used of %llu slots\n", (unsigned long long)nreqA,
@@ -2784,14 +2806,6 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             return -EIO;
         return 1;
     }
-    const uint64_t nr = std::max<uint64_t>(nreqA, 1);
-    const uint64_t cx_cap = nhit + k3 * nreqA + 64;
-    const uint64_t log_need = log_used + nreqA;
-    if (cx_cap > 0xFFFFFFFFu)
-        return 1;
-    if (c->cta_req2.ensure(40 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
-        c->cta_tmp.ensure(cta_sort_tmp_bytes((uint32_t)std::max<uint64_t>(cx_cap, 2 * nr))))
-        return -ENOMEM;
     if (logbuf.bytes < log_rec * log_need) {   // grow, keeping the entries
         DevBuf nl;
         if (nl.ensure(log_rec * std::max<uint64_t>(2 * log_need, 1 << 16)))
@@ -2803,8 +2817,6 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         std::swap(nl.p, logbuf.p);
         std::swap(nl.bytes, logbuf.bytes);
     }
-    uint64_t *r2 = (uint64_t *)c->cta_req2.p, *cx = (uint64_t *)c->cta_cx.p;
-    A.reqA2 = r2;
     A.reqB = r2 + nr;        // (a create's related entry and reverse-NAT entry)
     A.reqB2 = r2 + 3 * nr;
     A.req_cap = (uint32_t)(2 * nr);
@@ -2815,12 +2827,10 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     A.log6 = V6 ? (CtLog6 *)logbuf.p : nullptr;
     A.log_base = (uint32_t)log_used;
     A.log_cap = (uint32_t)(logbuf.bytes / log_rec - log_used);
-    A.sort_tmp = c->cta_tmp.p;
-    A.sort_tmp_bytes = c->cta_tmp.bytes;
     // from here the device table changes: the host mirror lags until ct_sync
     c->ct_dirty = true;
     c->ct6_dirty |= V6;
-    int rc = cta_rest(A, V6, (uint32_t)nreqA, hc, s);
+    int rc = cta_rest(A, V6, (uint32_t)nreqA, presorted, hc, s);
     if (!rc && hipStreamSynchronize(s) != hipSuccess)
         rc = -EIO;
     if (rc) {

@@ -160,7 +160,7 @@ struct CtSyncRec6 {
 };
 // (NFHIT: requests that are counted hits; NKX: creates with a reverse-NAT entry)
 enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NSVC,
-       CTA_NFHIT, CTA_NKX, CTA_NCNT };
+       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NCNT };
 struct CtaArgs {
     DevTables T;
     // addresses: one word per header (IPv4), four (IPv6, raw network order)
@@ -209,7 +209,13 @@ struct CtaArgs {
 size_t cta_sort_tmp_bytes(uint32_t n);
 // v6: the batch is IPv6 (A.ct6, A.log6)
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);
-int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s);
+// the keys the creates would add, exactly (requests sorted and deduplicated,
+// the table probed): into *newk; *sorted: the sorted requests for cta_rest
+int cta_newkeys(const CtaArgs &A, bool v6, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,
+                hipStream_t s);
+// presorted: cta_newkeys' sorted requests, or null
+int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, const uint64_t *presorted,
+             uint32_t *host_cnt, hipStream_t s);
 // lb (ct4_lb / ct6_lb, or null): the records carry slave | loopback << 16 |
 // 1 << 31 in pad
 int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,

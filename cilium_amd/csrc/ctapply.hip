@@ -1029,6 +1029,46 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
     wave_add(&A.cnt[CTA_CLAIMS], claims);
 }
 
+// ---- the keys round 0 and its second writes would add, counted before any
+// insert (when the quick bound says the table may fill): per home slot, each
+// distinct key the table lacks, and for a create its related and
+// reverse-NAT entries
+template <bool V6>
+__global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *req, uint32_t nreq)
+{
+    const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
+    const uint64_t home = r0 < nreq ? req[r0] >> A.ob : 0;
+    const bool lead = r0 < nreq && (r0 == 0 || (req[r0 - 1] >> A.ob) != home);
+    const uint64_t omask = (1ull << A.ob) - 1;
+    uint32_t nk_new = 0;
+    if (lead) {
+        ReqKey<V6> kk[4];
+        int nk = 0;
+        for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
+            const uint32_t ord = (uint32_t)(req[r] & omask) & ~1u;
+            Op<V6> o;
+            const ReqKey<V6> k = req_key<V6>(A, ord, &o);
+            bool seen = false;
+            for (int j = 0; j < nk; j++)
+                seen |= kk[j] == k;
+            for (uint32_t q = r0; q < r && nk == 4 && !seen; q++) {
+                Op<V6> oq;
+                seen = req_key<V6>(A, (uint32_t)(req[q] & omask) & ~1u, &oq) == k;
+            }
+            if (seen)
+                continue;
+            if (nk < 4)
+                kk[nk++] = k;
+            if (find(A, k.d, k.s, k.z, k.w) != NONE)
+                continue;
+            nk_new += 1;
+            if (ord_sec(ord) == SEC_OP)
+                nk_new += (o.ki_form ? 0u : 1u) + (o.kx ? 1u : 0u);
+        }
+    }
+    wave_add(&A.cnt[CTA_NEWK], nk_new);
+}
+
 // ---- related: one thread per (sorted) round-0 request; a marked one is a
 // key's first create, whose related ICMP entry goes into the device table
 // for an ANY map (UDP, ICMP echo: a round-1 request) or into the host log
@@ -1775,12 +1815,30 @@ int cta_scan_t(const CtaArgs &A, hipStream_t s)
 // and allowed the inserts.  Reads two more counts on the way (the sorts
 // take host item counts).
 template <bool V6>
-int cta_rest_t(const CtaArgs &A, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s)
+int cta_newkeys_t(const CtaArgs &A, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,
+                  hipStream_t s)
+{
+    if (int rc = sort_keys(A, A.reqA, A.reqA2, nreqA, A.ob + A.slot_bits, s, sorted))
+        return rc;
+    if (hipMemsetAsync(A.cnt + CTA_NEWK, 0, 4, s) != hipSuccess)
+        return -EIO;
+    if (nreqA)
+        hipLaunchKernelGGL(k_cta_newkeys<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
+                           (const uint64_t *)*sorted, nreqA);
+    if (hipMemcpyAsync(newk, A.cnt + CTA_NEWK, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    return 0;
+}
+
+template <bool V6>
+int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint32_t *host_cnt,
+               hipStream_t s)
 {
     const int bits = A.ob + A.slot_bits;
-    uint64_t *sorted;
+    uint64_t *sorted = const_cast<uint64_t *>(presorted);
     int rc;
-    if ((rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
+    if (!sorted && (rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
         return rc;
     if (nreqA) {
         hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A, sorted,
@@ -1843,9 +1901,18 @@ int cta_scan(const CtaArgs &A, bool v6, hipStream_t s)
     return v6 ? cta_scan_t<true>(A, s) : cta_scan_t<false>(A, s);
 }
 
-int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, uint32_t *host_cnt, hipStream_t s)
+int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, const uint64_t *presorted,
+             uint32_t *host_cnt, hipStream_t s)
 {
-    return v6 ? cta_rest_t<true>(A, nreqA, host_cnt, s) : cta_rest_t<false>(A, nreqA, host_cnt, s);
+    return v6 ? cta_rest_t<true>(A, nreqA, presorted, host_cnt, s)
+              : cta_rest_t<false>(A, nreqA, presorted, host_cnt, s);
+}
+
+int cta_newkeys(const CtaArgs &A, bool v6, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,
+                hipStream_t s)
+{
+    return v6 ? cta_newkeys_t<true>(A, nreqA, sorted, newk, s)
+              : cta_newkeys_t<false>(A, nreqA, sorted, newk, s);
 }
 
 int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
