@@ -190,6 +190,8 @@ struct cfc_ctx {
     // since (cta_ins); otherwise the host's live + tombstone counts
     uint64_t ct_used = 0, cta_ins = 0;
     bool ct_used_valid = false;
+    // least CT table slots (a batch outgrew the table: it was rebuilt larger)
+    uint64_t ct_min4 = 0, ct_min6 = 0;
     // deletes of the device GC (cfc_ct_gc) the host mirror has not taken
     DevBuf gc_log, gc_tmp, gc_sets, gc_cnt;
     uint64_t gc_log_used = 0;
@@ -1360,6 +1362,8 @@ int commit_locked(cfc_ctx *c, hipStream_t s)
     for (auto &kv : c->maps)
         ms.push_back(kv.second.get());
     HostImage img;
+    img.ct_min4 = c->ct_min4;
+    img.ct_min6 = c->ct_min6;
     build_image(ms, c->opts, &img, groups);
 
     auto E = std::make_shared<Epoch>();
@@ -2643,7 +2647,7 @@ void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t 
 // instead (nothing changed), 0 done, <0 error.
 template <class Hdr>
 int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16_t ep_lxc,
-                 hipStream_t s)
+                 hipStream_t s, bool may_grow = true)
 {
     constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
@@ -2776,8 +2780,9 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     // quick bound — each create its key and its related entry, a load
     // balancer's creates their reverse-NAT entry (counted hits add none) —
     // and when that fails the exact count (k_cta_newkeys)
+    auto fits = [&](uint64_t newk) { return 4 * (used + ins + newk) <= 3 * slots; };
     auto room = [&](uint64_t newk) {
-        bool r = 4 * (used + ins + newk) <= 3 * slots;
+        bool r = fits(newk);
         for (auto &kv : c->maps) {
             const Map *m = kv.second.get();
             if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
@@ -2793,6 +2798,34 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, &exact, s))
             return -EIO;
         newk = exact;
+    }
+    if (ok && !fits(newk) && may_grow) {
+        // the batch outgrows the table but not its maps: rebuild the CT
+        // group larger (the device's state synced into the maps first) and
+        // apply again — unless other map groups wait for a commit, which
+        // would change the tables the batch was classified with
+        bool others = false;
+        uint64_t sg[NGROUPS];
+        group_sigs(c, sg);
+        for (int g = 0; g < NGROUPS; g++)
+            others |= g != 3 && sg[g] != c->built_sig[g];
+        bool maps_ok = true;
+        for (auto &kv : c->maps) {
+            const Map *m = kv.second.get();
+            if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
+                m->kv.size() - m->gc_pending + claims + log_used + newk > m->max_entries)
+                maps_ok = false;
+        }
+        if (!others && maps_ok) {
+            uint64_t &mn = V6 ? c->ct_min6 : c->ct_min4;
+            mn = std::max<uint64_t>(mn, 2 * (used + ins + newk));
+            if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess)
+                return -EIO;
+            c->built_sig[3] = ~0ull;
+            if (int rc = commit_locked(c, s))
+                return rc;
+            return ct_apply_dev(c, in, out, mode, ep_lxc, s, false);
+        }
     }
     ok = ok && room(newk);
     if (!ok && getenv("CFC_DEBUG_APPLY"))

@@ -519,24 +519,40 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
             if (i >= A.n)
                 r[u].cb = 0;
         }
-        // the destination endpoint's CT owner: first probes together
+        // the destination endpoint's CT owner, for the stages whose key the
+        // scan builds (a create, a hit the classify launch did not leave):
+        // first probes together.  A hit with the launch's slot needs none
+        // (most of a conntrack batch: no endpoint lookup per header).
         uint32_t dsto[SCAN_U];
+        bool need[SCAN_U];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++) {
+            need[u] = false;
+#pragma unroll
+            for (int st = 0; st < NST; st++) {
+                const uint32_t cs = (r[u].cb >> (4 * st)) & 0xF;
+                const bool mine = A.mode == CFC_MODE_EGRESS && st == 0;   // (owner: the sender)
+                const uint32_t key = st ? r[u].k2 : r[u].k1;
+                need[u] |= (cs & CFC_CT_DONE) && !mine &&
+                           ((cs & CFC_CT_RES_MASK) == 0 || key == NONE);
+            }
+        }
         if constexpr (V6) {
 #pragma unroll
             for (int u = 0; u < SCAN_U; u++)
-                dsto[u] = dst_owner(A.T, r[u].da);
+                dsto[u] = need[u] ? dst_owner(A.T, r[u].da) : 0u;
         } else {
             uint32_t ls[SCAN_U];
             uint4 lv[SCAN_U];
 #pragma unroll
             for (int u = 0; u < SCAN_U; u++) {
                 ls[u] = A.T.lxc4 ? hash32(r[u].da, A.T.lxc4_mask) : 0u;
-                lv[u] = A.T.lxc4 ? ld16(A.T.lxc4 + ls[u]) : make_uint4(0, 0, 0, 0);
+                lv[u] = (A.T.lxc4 && need[u]) ? ld16(A.T.lxc4 + ls[u]) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < SCAN_U; u++) {
                 dsto[u] = 0;
-                if (A.T.lxc4) {
+                if (A.T.lxc4 && need[u]) {
                     uint32_t sl = ls[u];
                     uint4 v = lv[u];
                     for (;;) {

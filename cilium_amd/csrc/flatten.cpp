@@ -634,7 +634,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
     for (const Map *m : cts)
         (m->role == ROLE_CT4 ? n4 : n6) += m->kv.size();
     if (n4) {
-        uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n4));
+        uint32_t ns = pow2_at_least(std::max<uint64_t>({16, 2ull * n4, img->ct_min4}));
         img->ct4.assign(ns, Ct4Slot{});
         img->ct4_tm.assign(ns, CtTimer{});
         img->ct4_mask = ns - 1;
@@ -655,7 +655,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
     if (n4 && lb)
         img->ct4_lb.assign(img->ct4.size(), make_uint4(0, 0, 0, 0));
     if (n6) {
-        uint32_t ns = pow2_at_least(std::max<uint64_t>(16, 2ull * n6));
+        uint32_t ns = pow2_at_least(std::max<uint64_t>({16, 2ull * n6, img->ct_min6}));
         img->ct6.assign(ns, Ct6Slot{});
         img->ct6_tm.assign(ns, CtTimer{});
         img->ct6_mask = ns - 1;

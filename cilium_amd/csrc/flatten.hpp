@@ -51,6 +51,9 @@ int64_t lpm6_find_slot(const Lpm6Host &t, const Pfx6 &p);
 uint32_t lpm6_lookup_host(const Lpm6Host &t, const uint32_t w[4]);
 
 struct HostImage {
+    // the CT tables' least slot counts (a device apply that outgrew the
+    // table asked for more: cfc_api.cpp ct_apply_dev)
+    uint64_t ct_min4 = 0, ct_min6 = 0;
     // IPv4 ipcache: compact multibit (l4c/l4l) or DIR-24-8 (tbl24/tbl8)
     std::vector<uint32_t> tbl24, tbl8, lbl_ovf;
     std::vector<uint32_t> l4d, l4c;    // l4d: 4 words per /16
