@@ -215,6 +215,7 @@ struct cfc_ctx {
     uint64_t log_used = 0;       // CtLog entries since the last sync
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
     DevBuf cta_lbr, cta_reqs;     // a load balancer's service step per header (LbRec4/6)
+    DevBuf cta_obm;               // the apply's ordered-slot bitmap
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -2689,8 +2690,9 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         sb++;
     if (ob + sb > 64)
         return 1;
+    const uint64_t obm_bytes = 4 * ((slots + 31) / 32);
     if (c->cta_hs.ensure((lbm ? 16 : 8) * n) || c->cta_req.ensure(8 * k3 * n) ||
-        c->cta_cnt.ensure(4 * CTA_NCNT))
+        c->cta_cnt.ensure(4 * CTA_NCNT) || c->cta_obm.ensure(obm_bytes))
         return -ENOMEM;
     if (lbm && (c->cta_lbr.ensure((V6 ? sizeof(LbRec6) : sizeof(LbRec4)) * n) ||
                 c->cta_reqs.ensure(16 * n) ||
@@ -2731,6 +2733,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     A.reqA = (uint64_t *)c->cta_req.p;
     A.req_cap = (uint32_t)std::min<uint64_t>(k3 * n, 0xFFFFFFFFu);
     A.cnt = (uint32_t *)c->cta_cnt.p;
+    A.obm = (uint32_t *)c->cta_obm.p;
     A.ob = ob;
     A.slot_bits = sb;
     A.lb = lbst.p ? (uint4 *)lbst.p : nullptr;
@@ -2752,7 +2755,8 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         }
     }
     uint32_t hc[CTA_NCNT];
-    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess || cta_scan(A, V6, s) ||
+    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess ||
+        hipMemsetAsync(A.obm, 0, obm_bytes, s) != hipSuccess || cta_scan(A, V6, s) ||
         hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;

@@ -202,6 +202,7 @@ struct CtaArgs {
     CtLog6 *log6;                // IPv6 applies
     uint32_t log_base, log_cap;  // entries before this apply, capacity left
     uint32_t *cnt;               // CTA_* counters
+    uint32_t *obm;               // ordered slots, one bit each (cleared per apply)
     void *sort_tmp;
     size_t sort_tmp_bytes;
     int ob, slot_bits;           // sort keys: slot << ob | order

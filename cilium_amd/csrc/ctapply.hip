@@ -13,9 +13,10 @@
 //            (CAS on the slot's w word), and the first request of a key
 //            creates it: its ICMP "related" entry (ct_create4's second
 //            write) is a second round of requests
-//   route    hits on unordered slots fold into a per-slot summary with
-//            atomicOr (their result does not depend on order, see
-//            k_cta_finish); every other op goes to the ordered list
+//   route    every op on an ordered slot goes to the ordered list (the
+//            scan folded the plain hits into per-slot summaries with
+//            atomicOr: on the other slots their result does not depend on
+//            order, see k_cta_finish)
 //   fold     the ordered list sorted by (slot, header order), one thread per
 //            slot replays its ops in order (cfc_api.cpp ct_hit_update /
 //            the oracle's ct_apply pass 2)
@@ -46,6 +47,26 @@ __device__ __forceinline__ void mark_or(uint32_t *m, uint32_t bits)
 {
     if ((*m & bits) != bits)
         atomicOr(m, bits);
+}
+// A slot's word x holds its marks (bits 0-3) and the summary of its plain
+// hits (bits 8-26, see k_cta_finish): both only ever OR'ed in.  y holds the
+// order of a deleted entry's first delete.  The ordered slots are also bits
+// of A.obm, which k_cta_route tests per hit (a few MiB: cache-resident,
+// where the per-slot words are not).
+constexpr int SUM_SH = 8;
+__device__ __forceinline__ uint32_t sum_bits(bool in, bool tcp, bool close, uint32_t tfl)
+{
+    return ((in ? tfl : tfl << 8) | (in ? 1u << 16 : 1u << 17) |
+            ((tcp && !close) ? 1u << 18 : 0u)) << SUM_SH;
+}
+__device__ __forceinline__ void order_mark(const CtaArgs &A, uint32_t sl, uint32_t bits)
+{
+    if ((A.ms[sl].x & bits) != bits) {
+        atomicOr(&A.ms[sl].x, bits);
+        const uint32_t b = 1u << (sl & 31);
+        if (!(A.obm[sl >> 5] & b))
+            atomicOr(&A.obm[sl >> 5], b);
+    }
 }
 constexpr uint32_t HS_NONE = 0xFFFFFFFFu;
 
@@ -568,8 +589,10 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 }
             }
         }
-        // per stage: the op, its slot, a create's request
+        // per stage: the op, its slot, a create's request, a plain hit's
+        // summary bits
         uint32_t slot[SCAN_U][2], kind[SCAN_U][2], act[SCAN_U][2], home[SCAN_U][2];
+        uint32_t sb[SCAN_U][2];
         uint32_t ncr = 0;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
@@ -580,6 +603,8 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 act[u][st] = o.kind == OP_NONE ? 0u : o.action;
                 slot[u][st] = HS_NONE;
                 home[u][st] = 0;
+                sb[u][st] = (o.kind == OP_HIT && o.action != 2)
+                                ? sum_bits(o.dir == CT_INGRESS, o.is_tcp, o.syn, o.tfl) : 0u;
                 if (o.kind == OP_HIT || o.kind == OP_DELETE) {
                     const uint32_t key = st ? r[u].k2 : r[u].k1;
                     uint32_t sl;
@@ -597,6 +622,13 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 }
             }
         }
+        // the plain hits' slot words, loaded together
+        uint32_t cur[SCAN_U][2];
+#pragma unroll
+        for (int u = 0; u < SCAN_U; u++)
+#pragma unroll
+            for (int st = 0; st < NST; st++)
+                cur[u][st] = (sb[u][st] && slot[u][st] != HS_NONE) ? A.ms[slot[u][st]].x : 0u;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
@@ -606,19 +638,22 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 if (sl == HS_NONE)
                     continue;
                 nhit++;
-                if (kind[u][st] == OP_DELETE) {
+                if (sb[u][st]) {   // a plain hit: into the slot's summary
+                    if ((cur[u][st] | sb[u][st]) != cur[u][st])
+                        atomicOr(&A.ms[sl].x, sb[u][st]);
+                } else if (kind[u][st] == OP_DELETE) {
                     // the entry goes: only its first delete matters
                     // (k_cta_route), unless a create revives the key (a
                     // dropped hot flow deletes its entry once per packet:
                     // only a lower order than the one stored needs the
                     // atomic)
-                    mark_or(&A.ms[sl].x, MARK_ORDERED | MARK_DEL);
+                    order_mark(A, sl, MARK_ORDERED | MARK_DEL);
                     const uint32_t v = 0xFFFFFFFFu - ord_of(i, st, SEC_OP);
                     if (__hip_atomic_load(&A.ms[sl].y, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) < v)
                         atomicMax(&A.ms[sl].y, v);
                 } else if (act[u][st] == 2) {   // RST / FIN: ACTION_CLOSE
-                    mark_or(&A.ms[sl].x, MARK_ORDERED);
+                    order_mark(A, sl, MARK_ORDERED);
                 }
             }
             if (i < A.n) {
@@ -898,14 +933,18 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                 }
                 hs2[st] = sl;
                 nhit++;
-                if (o.kind == OP_DELETE) {
-                    mark_or(&A.ms[sl].x, MARK_ORDERED | MARK_DEL);
+                if (o.kind == OP_HIT && o.action != 2) {   // a plain hit: its summary
+                    const uint32_t b = sum_bits(o.dir == CT_INGRESS, o.is_tcp, o.syn, o.tfl);
+                    if ((A.ms[sl].x & b) != b)
+                        atomicOr(&A.ms[sl].x, b);
+                } else if (o.kind == OP_DELETE) {
+                    order_mark(A, sl, MARK_ORDERED | MARK_DEL);
                     const uint32_t v = 0xFFFFFFFFu - ord_of(i, st, SEC_OP);
                     if (__hip_atomic_load(&A.ms[sl].y, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT) < v)
                         atomicMax(&A.ms[sl].y, v);
                 } else if (o.action == 2) {
-                    mark_or(&A.ms[sl].x, MARK_ORDERED);
+                    order_mark(A, sl, MARK_ORDERED);
                 }
             } else if (o.kind == OP_CREATE) {
                 rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP));
@@ -919,8 +958,13 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
             if (o.kind == OP_HIT) {
                 hs2[2] = r.svc;
                 nhit++;
-                if (o.action == 2)
-                    mark_or(&A.ms[r.svc].x, MARK_ORDERED);
+                if (o.action == 2) {
+                    order_mark(A, r.svc, MARK_ORDERED);
+                } else {
+                    const uint32_t b = sum_bits(false, o.is_tcp, o.syn, o.tfl);
+                    if ((A.ms[r.svc].x & b) != b)
+                        atomicOr(&A.ms[r.svc].x, b);
+                }
                 if (o.reslave && A.lb)   // ct_update4/6_slave
                     A.lb[r.svc].y = o.slave;
             } else if (o.kind == OP_CREATE) {
@@ -1025,7 +1069,7 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
             if (slot == NONE) {
                 bool fresh;
                 slot = find_or_insert<V6>(A, k.d, k.s, k.z, k.w, &fresh);
-                mark_or(&A.ms[slot].x, MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
+                order_mark(A, slot, MARK_ORDERED | MARK_PUTC | (fresh ? MARK_FRESH : 0u));
                 first = fresh;
                 claims += fresh;
                 if (nk < 4) {
@@ -1148,38 +1192,30 @@ __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *
         A.reqB[b] = pack(A, khash(o.kxa, o.kxs, o.z2, o.kxw) & A.mask, ord | SEC_KX << 1);
 }
 
-// ---- route: hits on unordered slots -> summary; the rest -> ordered list.
-// Four header stages per thread and step, the loads of each phase together
-// (as the scan).  (Family-free: it reads the hit slots, meta and TCP flags.)
+// ---- route: every op on an ordered slot -> the ordered list (the plain
+// hits of the other slots are in their summaries: k_cta_scan).  Four header
+// stages per thread and step; per hit one test of the ordered-slot bitmap,
+// the slot's words only for the ordered ones.  (Family-free.)
 __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
     constexpr int RU = 4;
     // item k is header stage j = k (egress: two CT stages per header) or
     // j = 2k (one stage: the odd stages never hold a hit); with a load
     // balancer (egress) j in [2n, 4n) are the CT_SERVICE ops (virtual
-    // headers n..2n-1, stage 0: the entry's tx side)
+    // headers n..2n-1)
     const bool two = A.mode == CFC_MODE_EGRESS;
     const uint64_t n2 = 2 * A.n, nk = A.lbr ? 2 * n2 : two ? n2 : A.n;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * RU;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < nk; base += stride) {
-        uint32_t slot[RU], mk[RU], sm[RU], mt[RU], tf[RU];
+        uint32_t slot[RU], bw[RU];
 #pragma unroll
         for (int u = 0; u < RU; u++) {
             const uint64_t k = base + u * 256 + threadIdx.x;
-            const uint64_t j = two ? k : 2 * k;
-            slot[u] = k < nk ? A.hs[j] : HS_NONE;
-            uint64_t i = (k < nk ? j : 0) >> 1;
-            if (i >= A.n)
-                i -= A.n;
-            mt[u] = A.mt[i];
-            tf[u] = A.tf ? A.tf[i] : 0u;
+            slot[u] = k < nk ? A.hs[two ? k : 2 * k] : HS_NONE;
         }
 #pragma unroll
-        for (int u = 0; u < RU; u++) {
-            const uint2 v = slot[u] != HS_NONE ? A.ms[slot[u]] : make_uint2(0, 0);
-            mk[u] = v.x;
-            sm[u] = v.y;
-        }
+        for (int u = 0; u < RU; u++)
+            bw[u] = slot[u] != HS_NONE ? A.obm[slot[u] >> 5] : 0u;
         bool ordered[RU];
         uint32_t nord = 0;
 #pragma unroll
@@ -1187,23 +1223,14 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
             const uint64_t k = base + u * 256 + threadIdx.x;
             const uint64_t j = two ? k : 2 * k;
             ordered[u] = false;
-            if (slot[u] == HS_NONE)
+            if (slot[u] == HS_NONE || !((bw[u] >> (slot[u] & 31)) & 1))
                 continue;
-            if ((mk[u] & (MARK_DEL | MARK_PUTC)) == MARK_DEL) {
+            const uint2 v = A.ms[slot[u]];
+            if ((v.x & (MARK_DEL | MARK_PUTC)) == MARK_DEL)
                 // a deleted entry: its first delete stands for all its ops
-                ordered[u] = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - sm[u];
-            } else if (mk[u] & MARK_ORDERED) {
-                ordered[u] = true;
-            } else {
-                // the summary needs direction, TCP flags and the close bit only
-                const bool in = !(A.mode == CFC_MODE_EGRESS && (j & 1) == 0);
-                const bool tcp = (mt[u] & 0xFF) == 6;
-                const uint32_t tfl = tcp ? tf[u] : 0u;
-                const uint32_t bits = (in ? tfl : tfl << 8) | (in ? 1u << 16 : 1u << 17) |
-                                      ((tcp && !(mt[u] & CFC_HF_TCP_CLOSE)) ? 1u << 18 : 0u);
-                if ((sm[u] | bits) != sm[u])
-                    atomicOr(&A.ms[slot[u]].y, bits);
-            }
+                ordered[u] = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - v.y;
+            else
+                ordered[u] = (v.x & MARK_ORDERED) != 0;
             nord += ordered[u];
         }
         uint32_t c = A.cx_base + block_count_n(&A.cnt[CTA_NCX], nord);
@@ -1480,7 +1507,7 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < FU; u++) {
             const uint64_t s = base + u * 256 + threadIdx.x;
-            m[u] = s < slots ? A.ms[s].y : 0u;
+            m[u] = s < slots ? A.ms[s].x >> SUM_SH : 0u;
         }
 #pragma unroll
         for (int u = 0; u < FU; u++) {
@@ -1496,7 +1523,7 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             if (!m[u])
                 continue;
             const uint64_t s = base + u * 256 + threadIdx.x;
-            A.ms[s].y = 0;
+            A.ms[s].x = 0;
             St &x = e[u];
             x.bits &= ~(RX_CLOSING | TX_CLOSING);
             const bool is_tcp = (w[u] & 0xFF) == 6;

@@ -10,4 +10,8 @@ tail -40 gpurun_out/r3f/t_lb.log
 timeout -k 10 600 $T tests/test_gpu_parity.py -k "golden or ct or conntrack or c5 or gc" \
     > gpurun_out/r3f/t_ct.log 2>&1 || { tail -40 gpurun_out/r3f/t_ct.log; exit 1; }
 tail -2 gpurun_out/r3f/t_ct.log
+
+timeout -k 10 400 python -u bench.py --workload c5 --ct-apply --no-cpu --steps 20 --warmup 3 \
+    > gpurun_out/r3f/c5a.json 2> gpurun_out/r3f/c5a.err || { tail -5 gpurun_out/r3f/c5a.err; exit 1; }
+grep -o '"ct_apply": {[^}]*}' gpurun_out/r3f/c5a.json
 echo done
