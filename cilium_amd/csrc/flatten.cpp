@@ -711,7 +711,10 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
 void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
                  HostImage *img, unsigned groups)
 {
+    const uint64_t ct_min4 = img->ct_min4, ct_min6 = img->ct_min6;   // (the caller's)
     *img = HostImage();
+    img->ct_min4 = ct_min4;
+    img->ct_min6 = ct_min6;
     img->ct_local.assign(65536, 0);
     std::vector<const Map *> cts;
     for (Map *m : maps)
