@@ -2784,24 +2784,30 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     // quick bound — each create its key and its related entry, a load
     // balancer's creates their reverse-NAT entry (counted hits add none) —
     // and when that fails the exact count (k_cta_newkeys)
-    auto fits = [&](uint64_t newk) { return 4 * (used + ins + newk) <= 3 * slots; };
-    auto room = [&](uint64_t newk) {
-        bool r = fits(newk);
+    // (per map: the keys of its kind — TCP or ANY — once counted exactly,
+    // else all of them)
+    uint64_t newk = 2 * (nreqA - hc[CTA_NFHIT]) + hc[CTA_NKX];
+    uint64_t newk_kind[2] = {newk, newk};   // [TCP map, ANY map]
+    auto fits = [&](uint64_t nk) { return 4 * (used + ins + nk) <= 3 * slots; };
+    auto maps_fit = [&]() {
         for (auto &kv : c->maps) {
             const Map *m = kv.second.get();
             if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
-                m->kv.size() - m->gc_pending + claims + log_used + newk > m->max_entries)
-                r = false;
+                m->kv.size() - m->gc_pending + claims + log_used + newk_kind[m->ct_any ? 1 : 0] >
+                    m->max_entries)
+                return false;
         }
-        return r;
+        return true;
     };
-    uint64_t newk = 2 * (nreqA - hc[CTA_NFHIT]) + hc[CTA_NKX];
+    auto room = [&](uint64_t nk) { return fits(nk) && maps_fit(); };
     uint64_t *presorted = nullptr;
     if (ok && !room(newk)) {
-        uint32_t exact = 0;
-        if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, &exact, s))
+        uint32_t exact[2] = {0, 0};
+        if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, exact, s))
             return -EIO;
-        newk = exact;
+        newk = exact[0];
+        newk_kind[0] = exact[1];
+        newk_kind[1] = exact[0] - exact[1];
     }
     if (ok && !fits(newk) && may_grow) {
         // the batch outgrows the table but not its maps: rebuild the CT
@@ -2813,14 +2819,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         group_sigs(c, sg);
         for (int g = 0; g < NGROUPS; g++)
             others |= g != 3 && sg[g] != c->built_sig[g];
-        bool maps_ok = true;
-        for (auto &kv : c->maps) {
-            const Map *m = kv.second.get();
-            if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
-                m->kv.size() - m->gc_pending + claims + log_used + newk > m->max_entries)
-                maps_ok = false;
-        }
-        if (!others && maps_ok) {
+        if (!others && maps_fit()) {
             uint64_t &mn = V6 ? c->ct_min6 : c->ct_min4;
             mn = std::max<uint64_t>(mn, 2 * (used + ins + newk));
             if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess)
@@ -2911,6 +2910,14 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         const int rc = ct_apply_dev(c, in, out, mode, ep_lxc, s);
         c->ct_gen++;   // (the table, or the host maps, change from here)
         c->n_apply_dev += rc == 0;
+        if (rc == 0) {
+            // the creates' CONNTRACK_ACCOUNTING is in the device counts now:
+            // they wait for a fold like a classify launch's (a CT group the
+            // apply grew was folded before the rebuild, which cleared the flag)
+            (void)hipEventRecord(c->last_done, s);
+            c->last_stream = s;
+            c->ctr_pending = true;
+        }
         if (rc <= 0)
             return rc;
     }

@@ -160,7 +160,7 @@ struct CtSyncRec6 {
 };
 // (NFHIT: requests that are counted hits; NKX: creates with a reverse-NAT entry)
 enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NSVC,
-       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NCNT };
+       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NEWKT, CTA_NCNT };
 struct CtaArgs {
     DevTables T;
     // addresses: one word per header (IPv4), four (IPv6, raw network order)
@@ -211,7 +211,9 @@ size_t cta_sort_tmp_bytes(uint32_t n);
 // v6: the batch is IPv6 (A.ct6, A.log6)
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);
 // the keys the creates would add, exactly (requests sorted and deduplicated,
-// the table probed): into *newk; *sorted: the sorted requests for cta_rest
+// the table probed): newk[0] all of them, newk[1] those of TCP creates (they
+// go to TCP maps, the others to ANY maps); *sorted: the sorted requests for
+// cta_rest
 int cta_newkeys(const CtaArgs &A, bool v6, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,
                 hipStream_t s);
 // presorted: cta_newkeys' sorted requests, or null

@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *
     const uint64_t home = r0 < nreq ? req[r0] >> A.ob : 0;
     const bool lead = r0 < nreq && (r0 == 0 || (req[r0 - 1] >> A.ob) != home);
     const uint64_t omask = (1ull << A.ob) - 1;
-    uint32_t nk_new = 0;
+    uint32_t nk_new = 0, nk_tcp = 0;   // (keys of a TCP create go to a TCP map)
     if (lead) {
         ReqKey<V6> kk[4];
         int nk = 0;
@@ -1121,12 +1121,14 @@ __global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *
                 kk[nk++] = k;
             if (find(A, k.d, k.s, k.z, k.w) != NONE)
                 continue;
-            nk_new += 1;
-            if (ord_sec(ord) == SEC_OP)
-                nk_new += (o.ki_form ? 0u : 1u) + (o.kx ? 1u : 0u);
+            const uint32_t nk = 1u + (ord_sec(ord) == SEC_OP
+                                          ? (o.ki_form ? 0u : 1u) + (o.kx ? 1u : 0u) : 0u);
+            nk_new += nk;
+            nk_tcp += o.is_tcp ? nk : 0u;
         }
     }
     wave_add(&A.cnt[CTA_NEWK], nk_new);
+    wave_add(&A.cnt[CTA_NEWKT], nk_tcp);
 }
 
 // ---- related: one thread per (sorted) round-0 request; a marked one is a
@@ -1863,12 +1865,12 @@ int cta_newkeys_t(const CtaArgs &A, uint32_t nreqA, uint64_t **sorted, uint32_t 
 {
     if (int rc = sort_keys(A, A.reqA, A.reqA2, nreqA, A.ob + A.slot_bits, s, sorted))
         return rc;
-    if (hipMemsetAsync(A.cnt + CTA_NEWK, 0, 4, s) != hipSuccess)
+    if (hipMemsetAsync(A.cnt + CTA_NEWK, 0, 8, s) != hipSuccess)   // (NEWK, NEWKT)
         return -EIO;
     if (nreqA)
         hipLaunchKernelGGL(k_cta_newkeys<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
                            (const uint64_t *)*sorted, nreqA);
-    if (hipMemcpyAsync(newk, A.cnt + CTA_NEWK, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(newk, A.cnt + CTA_NEWK, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     return 0;
