@@ -2803,6 +2803,10 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     uint64_t *presorted = nullptr;
     if (ok && !room(newk)) {
         uint32_t exact[2] = {0, 0};
+        A.cx = cx;   // (its set of related keys; the list reuses it later)
+        A.rel_mask = 1;
+        while (2ull * A.rel_mask + 1 <= 2 * cx_cap && A.rel_mask < (1u << 30))
+            A.rel_mask = 2 * A.rel_mask + 1;
         if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, exact, s))
             return -EIO;
         newk = exact[0];

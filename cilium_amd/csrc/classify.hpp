@@ -197,6 +197,7 @@ struct CtaArgs {
     uint4 *lb;
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
     uint32_t req_cap, cx_cap;
+    uint32_t rel_mask;           // cta_newkeys: A.cx as a set of 2^k words, mask
     uint32_t cx_base;            // route: its ordered ops start here
     CtLog *log;                  // IPv4 applies
     CtLog6 *log6;                // IPv6 applies

@@ -91,14 +91,25 @@ __device__ __forceinline__ uint4 bswap4(uint4 v)
 // ---- IPv6 LPM (layout.h Lpm6): the label of the longest prefix holding the
 // host-order address a (a matched label 0 shadows shorter prefixes, as the
 // reference's trie does), def_label when none
-__device__ __forceinline__ uint32_t lpm6_lookup(const Lpm6 &P, uint4 a)
+// The first group's Bloom word is a separate step (lpm6_bloom0) so that the
+// first loads of independent lookups of one header go out together.
+// loff: the dword offset of the table's length list in LDS (LdsPlan6)
+__device__ __forceinline__ uint64_t lpm6_bloom0(const Lpm6 &P, uint32_t loff, uint4 a)
+{
+    if (!P.nlen)
+        return 0;
+    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+    return P.bloom[l6_group_hash(w, (lds_word(loff) >> 8) & 255) & P.bloom_mask];
+}
+__device__ __forceinline__ uint32_t lpm6_lookup(const Lpm6 &P, uint32_t loff, uint4 a,
+                                                uint64_t bw0)
 {
     const uint32_t w[4] = {a.x, a.y, a.z, a.w};
-    uint64_t bw = 0;
+    uint64_t bw = bw0;
     for (uint32_t j = 0; j < P.nlen; j++) {
-        const uint32_t e = P.lens[j];   // uniform
+        const uint32_t e = lds_word(loff + j);   // uniform
         const uint32_t len = e & 255;
-        if (e & L6_GROUP_FIRST)
+        if ((e & L6_GROUP_FIRST) && j)
             bw = P.bloom[l6_group_hash(w, (e >> 8) & 255) & P.bloom_mask];
         const uint32_t m0 = a.x & l6_word_mask(len, 0), m1 = a.y & l6_word_mask(len, 1),
                        m2 = a.z & l6_word_mask(len, 2), m3 = a.w & l6_word_mask(len, 3);
@@ -116,6 +127,10 @@ __device__ __forceinline__ uint32_t lpm6_lookup(const Lpm6 &P, uint4 a)
         }
     }
     return P.def_label;
+}
+__device__ __forceinline__ uint32_t lpm6_lookup(const Lpm6 &P, uint32_t loff, uint4 a)
+{
+    return lpm6_lookup(P, loff, a, lpm6_bloom0(P, loff, a));
 }
 
 // ---- endpoints: {pol_base, pol_mask, info, 0} of the slot holding the raw
@@ -169,11 +184,14 @@ __device__ __forceinline__ bool icmp6_punt(const DevTables &T, uint32_t proto,
                            da.z == T.router6[2] && da.w == T.router6[3]);
 }
 
+// LDS image of a v6 launch: metrics | endpoint slots | policy Bloom | the
+// length lists of the three Lpm6 tables (ipcache, prefilter fix, dyn): a
+// lookup reads its next length from LDS, not by a dependent global load
 struct LdsPlan6 {
-    uint32_t lxc_slots, pol_words;
+    uint32_t lxc_slots, pol_words, nlens;
     __host__ __device__ size_t bytes() const
     {
-        return 8ull * LDS_MET6_U64 + 32ull * lxc_slots + 4ull * pol_words;
+        return 8ull * LDS_MET6_U64 + 32ull * lxc_slots + 4ull * pol_words + 4ull * nlens;
     }
 };
 
@@ -182,6 +200,7 @@ __host__ LdsPlan6 lds_plan6(const DevTables &T)
     LdsPlan6 p;
     p.lxc_slots = (T.lxc6 && T.lxc6_lds) ? T.lxc6_mask + 1 : 0;
     p.pol_words = T.pol_bloom ? T.pol_bloom_words : 0;
+    p.nlens = T.ipc6.nlen + T.pf6_fix.nlen + T.pf6_dyn.nlen;
     return p;
 }
 
@@ -267,6 +286,16 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
              2 * L.lxc_slots);
     lds_copy(cfc_smem + pol4, reinterpret_cast<const uint4 *>(T.pol_bloom),
              L.pol_words / 4);
+    // the length lists (dword offsets)
+    const uint32_t lo_ipc = 4 * pol4 + L.pol_words;
+    const uint32_t lo_fix = lo_ipc + T.ipc6.nlen, lo_dyn = lo_fix + T.pf6_fix.nlen;
+    {
+        uint32_t *lw = reinterpret_cast<uint32_t *>(cfc_smem);
+        for (uint32_t j = threadIdx.x; j < L.nlens; j += BLOCK)
+            lw[lo_ipc + j] = j < T.ipc6.nlen ? T.ipc6.lens[j]
+                           : j < T.ipc6.nlen + T.pf6_fix.nlen ? T.pf6_fix.lens[j - T.ipc6.nlen]
+                           : T.pf6_dyn.lens[j - T.ipc6.nlen - T.pf6_fix.nlen];
+    }
     __syncthreads();
 
     const uint64_t start = (uint64_t)blockIdx.x * per_block;
@@ -299,6 +328,13 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         uint32_t idw = KEY_NONE, ev2 = 0;  // identity counter key; stage-2 event
         uint32_t evw = 0;                  // trace event word (forwarded)
         const uint32_t len = mt >> 16;
+        // the Bloom words of the prefilter's and the ipcache's lookups of
+        // this header's address, loaded together (egress with a load
+        // balancer looks up the address after its service step instead)
+        const uint64_t bwf = XDP ? lpm6_bloom0(T.pf6_fix, lo_fix, sa) : 0ull;
+        const uint64_t bwi = MODE == CFC_MODE_XDP ? 0ull
+                           : !EGR ? lpm6_bloom0(T.ipc6, lo_ipc, sa)
+                           : !LB  ? lpm6_bloom0(T.ipc6, lo_ipc, da) : 0ull;
         const uint4 drec = lxc6_find(T, lxc_lds, lxc_off, da_raw);
         const bool local = (drec.z & LXC_VALID) != 0;
         // the endpoint the packet is delivered to (egress: by the packet's
@@ -306,9 +342,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         uint4 erec = drec;
         bool done = false;
         if (XDP) {
-            bool deny = lpm6_lookup(T.pf6_dyn, sa) != 0;
+            bool deny = lpm6_lookup(T.pf6_dyn, lo_dyn, sa) != 0;
             if (!deny)
-                deny = lpm6_lookup(T.pf6_fix, sa) != 0;
+                deny = lpm6_lookup(T.pf6_fix, lo_fix, sa, bwf) != 0;
             const bool drop = deny || !local;
             if (MODE == CFC_MODE_XDP || drop) {
                 act = drop ? XDP_DROP : XDP_PASS;
@@ -345,7 +381,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     // handle_ipv6 (:203-213): reserved identities take the
                     // ipcache's unless it says CLUSTER_ID
                     if (ident < HEALTH_ID) {
-                        const uint32_t label = lpm6_lookup(T.ipc6, sa);
+                        const uint32_t label = lpm6_lookup(T.ipc6, lo_ipc, sa, bwi);
                         if (label && label != CLUSTER_ID)
                             ident = label;
                     }
@@ -445,7 +481,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     if (LB)
                         ct6_new_dport(proto, tpt, &dport);
                     // destination identity (bpf_lxc.c:206-221)
-                    const uint32_t label = lpm6_lookup(T.ipc6, tda);
+                    const uint32_t label = LB ? lpm6_lookup(T.ipc6, lo_ipc, tda)
+                                              : lpm6_lookup(T.ipc6, lo_ipc, tda, bwi);
                     ident = label ? label
                           : (tda.x == T.router6[0] && tda.y == T.router6[1]) ? CLUSTER_ID
                                                                               : WORLD_ID;

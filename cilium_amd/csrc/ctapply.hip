@@ -956,7 +956,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
             rs.svcop = true;
             const Op<V6> o = decode_from<V6, true>(A, rs, 0, 0u);
             if (o.kind == OP_HIT) {
-                hs2[2] = r.svc;
+                hs2[2] = r.svc;   // (its accounting: k_cta_route)
                 nhit++;
                 if (o.action == 2) {
                     order_mark(A, r.svc, MARK_ORDERED);
@@ -1089,6 +1089,26 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
     wave_add(&A.cnt[CTA_CLAIMS], claims);
 }
 
+// first sighting in this batch of a related entry's key: a CAS into the
+// fingerprint set (A.cx as 2 * cx_cap words, zeroed by cta_newkeys; mask:
+// its largest power of two - 1).  Fingerprints are two independent 32-bit
+// key hashes, never 0.
+template <class AD>
+__device__ __forceinline__ uint32_t rel_first(const CtaArgs &A, AD sa, AD da, uint32_t w)
+{
+    const uint64_t fp = ((uint64_t)khash(sa, da, 0x5bd1e995u, w) << 32 |
+                         khash(da, sa, 0x27d4eb2fu, ~w)) | 1ull;
+    const uint32_t mask = A.rel_mask;
+    for (uint32_t i = (uint32_t)fp & mask;; i = (i + 1) & mask) {
+        const unsigned long long cur =
+            atomicCAS((unsigned long long *)A.cx + i, 0ull, (unsigned long long)fp);
+        if (cur == 0)
+            return 1;
+        if (cur == fp)
+            return 0;
+    }
+}
+
 // ---- the keys round 0 and its second writes would add, counted before any
 // insert (when the quick bound says the table may fill): per home slot, each
 // distinct key the table lacks, and for a create its related and
@@ -1121,8 +1141,16 @@ __global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *
                 kk[nk++] = k;
             if (find(A, k.d, k.s, k.z, k.w) != NONE)
                 continue;
-            const uint32_t nk = 1u + (ord_sec(ord) == SEC_OP
-                                          ? (o.ki_form ? 0u : 1u) + (o.kx ? 1u : 0u) : 0u);
+            uint32_t nk = 1u + (ord_sec(ord) == SEC_OP && o.kx ? 1u : 0u);
+            if (ord_sec(ord) == SEC_OP && !o.ki_form) {
+                // its related ICMP entry: one per address pair and map, which
+                // many creates share — counted once per batch (a set of the
+                // keys' 64-bit fingerprints in A.cx) and only when the table
+                // lacks it (an ANY map's; a TCP map's is host-side only)
+                const uint32_t rw = ct_word(icmp_proto<V6>(), ((o.w2 >> 8) & 7) | 2u, o.owner);
+                if (o.is_tcp || find(A, o.sa, o.da, 0u, rw) == NONE)
+                    nk += rel_first(A, o.sa, o.da, rw);
+            }
             nk_new += nk;
             nk_tcp += o.is_tcp ? nk : 0u;
         }
@@ -1218,6 +1246,23 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < RU; u++)
             bw[u] = slot[u] != HS_NONE ? A.obm[slot[u] >> 5] : 0u;
+        if (A.lbr) {
+            // a CT_SERVICE hit on the batch's starting table: its
+            // CONNTRACK_ACCOUNTING (__ct_lookup counts every hit; the
+            // CT_SERVICE lookup's on the tx side), which no classify launch
+            // counts — here, after the apply has committed to the device
+            // (a scan may run twice when the table grows)
+#pragma unroll
+            for (int u = 0; u < RU; u++) {
+                const uint64_t k = base + u * 256 + threadIdx.x;
+                if (k < n2 || slot[u] == HS_NONE)
+                    continue;
+                unsigned long long *ac = reinterpret_cast<unsigned long long *>(A.T.ct_acct) +
+                                         4ull * (A.acct_base + slot[u]);
+                atomicAdd(ac, 1ull);
+                atomicAdd(ac + 1, (unsigned long long)(A.mt[(k >> 1) - A.n] >> 16));
+            }
+        }
         bool ordered[RU];
         uint32_t nord = 0;
 #pragma unroll
@@ -1865,7 +1910,8 @@ int cta_newkeys_t(const CtaArgs &A, uint32_t nreqA, uint64_t **sorted, uint32_t 
 {
     if (int rc = sort_keys(A, A.reqA, A.reqA2, nreqA, A.ob + A.slot_bits, s, sorted))
         return rc;
-    if (hipMemsetAsync(A.cnt + CTA_NEWK, 0, 8, s) != hipSuccess)   // (NEWK, NEWKT)
+    if (hipMemsetAsync(A.cnt + CTA_NEWK, 0, 8, s) != hipSuccess ||   // (NEWK, NEWKT)
+        hipMemsetAsync(A.cx, 0, 8ull * (A.rel_mask + 1), s) != hipSuccess)
         return -EIO;
     if (nreqA)
         hipLaunchKernelGGL(k_cta_newkeys<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
