@@ -147,6 +147,72 @@ __device__ __forceinline__ uint32_t block_count_n(uint32_t *ctr, uint32_t v)
     __syncthreads();
     return r;
 }
+// n items of this thread in a block's LDS staging list: their first index
+// there (the list's length in *sn); every thread of the block calls it
+__device__ __forceinline__ uint32_t block_stage_n(uint32_t *sn, uint32_t v)
+{
+    __shared__ uint32_t wsum[4], base;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wv] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        base = *sn;
+        *sn = base + wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    }
+    __syncthreads();
+    uint32_t r = base + x - v;
+    for (uint32_t k = 0; k < wv; k++)
+        r += wsum[k];
+    __syncthreads();
+    return r;
+}
+// the block's staged list into dst at places taken by one atomic on *ctr
+// (cap: dst's capacity); every thread of the block calls it
+__device__ __forceinline__ void block_flush(uint64_t *stage, uint32_t *sn, uint32_t *ctr,
+                                            uint64_t *dst, uint32_t cap)
+{
+    __shared__ uint32_t gbase;
+    const uint32_t n = *sn;
+    if (threadIdx.x == 0)
+        gbase = n ? atomicAdd(ctr, n) : 0u;
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x)
+        if (gbase + j < cap)
+            dst[gbase + j] = stage[j];
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *sn = 0;
+    __syncthreads();
+}
+
+// a per-thread count added once per block (every thread of the block calls
+// it): counters that every wave of a full-table pass bumps serialise at
+// their L2 channel
+__device__ __forceinline__ void block_add(uint32_t *ctr, uint32_t v)
+{
+    __shared__ uint32_t wsum[4];
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0)
+        wsum[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < (blockDim.x >> 6); k++)
+            t += wsum[k];
+        if (t)
+            atomicAdd(ctr, t);
+    }
+    __syncthreads();
+}
 // a per-thread count added once per wave (every lane of the wave calls it)
 __device__ __forceinline__ void wave_add(uint32_t *ctr, uint32_t v)
 {
@@ -522,10 +588,16 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
 // TWO: the mode has two CT stages per header (egress); else only stage 0
 // exists and the odd hit-slot entries are never read (k_cta_route).
 constexpr int SCAN_U = 4;
+constexpr uint32_t SCAN_STAGE = 4096;   // staged create requests per block (32 KiB)
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 {
     constexpr int NST = TWO ? 2 : 1;
+    __shared__ uint64_t s_req[SCAN_STAGE];
+    __shared__ uint32_t s_nreq;
+    if (threadIdx.x == 0)
+        s_nreq = 0;
+    __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
     uint32_t nhit = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
@@ -663,7 +735,10 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     A.hs[2 * i] = slot[u][0];
             }
         }
-        uint32_t rq = block_count_n(&A.cnt[CTA_NREQA], ncr);
+        // the creates' requests: staged in LDS, the block's list taken from
+        // reqA by one atomic when the stage fills and at the end (one
+        // atomic per block step on the shared counter serialised there)
+        uint32_t rq = block_stage_n(&s_nreq, ncr);
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
@@ -671,13 +746,15 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
             for (int st = 0; st < NST; st++) {
                 if (kind[u][st] != OP_CREATE)
                     continue;
-                if (rq < A.req_cap)
-                    A.reqA[rq] = pack(A, home[u][st], ord_of(i, st, SEC_OP));
-                rq++;
+                s_req[rq++] = pack(A, home[u][st], ord_of(i, st, SEC_OP));
             }
         }
+        __syncthreads();
+        if (s_nreq > SCAN_STAGE - 256 * SCAN_U * NST)   // (uniform)
+            block_flush(s_req, &s_nreq, &A.cnt[CTA_NREQA], A.reqA, A.req_cap);
     }
-    wave_add(&A.cnt[CTA_NHIT], nhit);
+    block_flush(s_req, &s_nreq, &A.cnt[CTA_NREQA], A.reqA, A.req_cap);
+    block_add(&A.cnt[CTA_NHIT], nhit);
 }
 
 // ---- the service step of an egress batch with a load balancer.  The
@@ -1086,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, ui
                 req[r] |= 1ull;
         }
     }
-    wave_add(&A.cnt[CTA_CLAIMS], claims);
+    block_add(&A.cnt[CTA_CLAIMS], claims);
 }
 
 // first sighting in this batch of a related entry's key: a CAS into the
@@ -1738,10 +1815,14 @@ __device__ __forceinline__ int gc_map(const uint32_t *smaps, uint32_t n, uint32_
     return -1;
 }
 
-// One thread per slot (grid-stride).  A deleted entry the host mirror may
-// hold is logged for it; one a device insert brought in since the last sync
-// (CTI_FRESH) is just dropped.  Either way the slot becomes a
-// plain tombstone with no dirty bits and zero accounting.
+// Four slots per thread and step (grid-stride), each phase's loads issued
+// together.  A deleted entry the host mirror may hold is logged for it; one
+// a device insert brought in since the last sync (CTI_FRESH) is just
+// dropped.  Either way the slot becomes a plain tombstone with no dirty bits
+// and zero accounting.  The log's places are taken once per block and step
+// (block_count_n): a steady-state GC deletes millions of entries, and one
+// atomic per wave on the shared counter serialised at its L2 channel.
+constexpr int GC_U = 4;
 __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
 {
     __shared__ uint32_t smaps[CTG_MAX_MAPS], scnt[CTG_MAX_MAPS];
@@ -1751,46 +1832,72 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
     }
     __syncthreads();
     uint32_t fresh = 0, live = 0, nonfree = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.slots; base += stride) {
-        const uint64_t s = base + threadIdx.x;
-        uint4 k = make_uint4(0, 0, 0, 0);
-        if (s < A.slots)
-            k = ld16(A.ct4 + s);
-        bool del = false, logit = false;
-        int j = -1;
-        if (k.w != 0) {
-            nonfree++;
-            // a tombstone, a claim, or an apply's delete the host has not taken
-            if (!(k.w & 0xF000u)) {
-                j = gc_map(smaps, A.n_maps, (k.w & 0xFFFF0800u) | ((k.w & 0xFF) != 6 ? 2u : 0u));
-                del = j >= 0 && gc_delete(A, k.x, k.y, A.tm[s].lifetime);
-                live += j >= 0 && !del;
-                if (del) {
-                    // only a key a device insert brought in since the last
-                    // sync is unknown to the host
-                    logit = !(A.info[s].y & CTI_FRESH);
-                    fresh += !logit;
-                }
-            }
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * GC_U;
+    // (every thread runs the same number of steps: block_count_n needs the
+    // whole block)
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * GC_U; base < A.slots; base += stride) {
+        uint4 k[GC_U];
+        int j[GC_U];
+        uint32_t life[GC_U], infy[GC_U];
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            k[u] = s < A.slots ? ld16(A.ct4 + s) : make_uint4(0, 0, 0, 0);
         }
-        const uint32_t r = wave_count(&A.cnt[CTG_DELETED], logit);
-        if (logit && r < A.log_cap)
-            A.log[r] = CtGcRec{(uint32_t)s, k.x, k.y, k.z, k.w};
-        if (del) {
+        // a tombstone, a claim, or an apply's delete the host has not taken
+        // is no entry of a map
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            nonfree += k[u].w != 0;
+            j[u] = (k[u].w != 0 && !(k[u].w & 0xF000u))
+                       ? gc_map(smaps, A.n_maps,
+                                (k[u].w & 0xFFFF0800u) | ((k[u].w & 0xFF) != 6 ? 2u : 0u))
+                       : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            life[u] = j[u] >= 0 ? A.tm[s].lifetime : 0u;
+        }
+        bool del[GC_U], logit[GC_U];
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            del[u] = j[u] >= 0 && gc_delete(A, k[u].x, k[u].y, life[u]);
+            infy[u] = del[u] ? A.info[s].y : 0u;
+        }
+        uint32_t nl = 0;
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            live += j[u] >= 0 && !del[u];
+            // only a key a device insert brought in since the last sync is
+            // unknown to the host
+            logit[u] = del[u] && !(infy[u] & CTI_FRESH);
+            fresh += del[u] && !logit[u];
+            nl += logit[u];
+        }
+        uint32_t r = block_count_n(&A.cnt[CTG_DELETED], nl);
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            if (!del[u])
+                continue;
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            if (logit[u]) {
+                if (r < A.log_cap)
+                    A.log[r] = CtGcRec{(uint32_t)s, k[u].x, k[u].y, k[u].z, k[u].w};
+                r++;
+                atomicAdd(&scnt[j[u]], 1u);
+            }
             *reinterpret_cast<uint4 *>(A.ct4 + s) = make_uint4(0, 0, 0, CT_TOMBSTONE);
             A.info[s] = CtInfo{0, 0};
             if (A.acct)
                 *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s) =
                     *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s + 2) = make_ulonglong2(0, 0);
-            if (logit)
-                atomicAdd(&scnt[j], 1u);
         }
     }
-    wave_add(&A.cnt[CTG_LIVE], live);
-    wave_add(&A.cnt[CTG_NONFREE], nonfree);
-    wave_add(&A.cnt[CTG_FRESH], fresh);
-    __syncthreads();
+    block_add(&A.cnt[CTG_LIVE], live);
+    block_add(&A.cnt[CTG_NONFREE], nonfree);
+    block_add(&A.cnt[CTG_FRESH], fresh);
     for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256)
         if (scnt[j])
             atomicAdd(&A.mcnt[j], scnt[j]);
@@ -1803,19 +1910,31 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
 __global__ __launch_bounds__(256) void k_ct_trim4(CtGcArgs A)
 {
     uint32_t freed = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < A.slots; s += stride) {
-        if (A.ct4[s].w != CT_TOMBSTONE || A.ct4[(s + 1) & A.mask].w != 0)
-            continue;
-        // (a thread that started inside another's run meets it: each slot
-        // is freed by exactly one CAS)
-        uint32_t j = (uint32_t)s;
-        while (atomicCAS(&A.ct4[j].w, CT_TOMBSTONE, 0u) == CT_TOMBSTONE) {
-            freed++;
-            j = (j - 1) & A.mask;
+    // four slots per thread and step, their words (and the next slots')
+    // loaded together
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * GC_U;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * GC_U; base < A.slots; base += stride) {
+        uint32_t w[GC_U], wn[GC_U];
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            w[u] = s < A.slots ? A.ct4[s].w : 0u;
+            wn[u] = s < A.slots ? A.ct4[(s + 1) & A.mask].w : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            if (w[u] != CT_TOMBSTONE || wn[u] != 0)
+                continue;
+            // (a thread that started inside another's run meets it: each
+            // slot is freed by exactly one CAS)
+            uint32_t j = (uint32_t)(base + u * 256 + threadIdx.x);
+            while (atomicCAS(&A.ct4[j].w, CT_TOMBSTONE, 0u) == CT_TOMBSTONE) {
+                freed++;
+                j = (j - 1) & A.mask;
+            }
         }
     }
-    wave_add(&A.cnt[CTG_FREED], freed);
+    block_add(&A.cnt[CTG_FREED], freed);
 }
 
 // the pending TCP-map ICMP entries (CtLog): lifetime as ct_create4 wrote it

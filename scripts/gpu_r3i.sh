@@ -5,7 +5,7 @@ O=gpurun_out/r3i
 mkdir -p $O
 export TMPDIR=/tmp
 T="python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider"
-timeout -k 10 400 $T tests/test_gpu_lb.py tests/test_gpu_parity.py -k "lb" > $O/lb.log 2>&1
+timeout -k 10 400 $T tests/test_gpu_lb.py tests/test_gpu_ctgc.py tests/test_gpu_parity.py -k "lb or gc" > $O/lb.log 2>&1
 rc=$?
 tail -8 $O/lb.log
 [ $rc -le 1 ] || exit 1
