@@ -587,8 +587,12 @@ __device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32
 // bits: k_cta_finish resolves those without a load here (see there).
 // TWO: the mode has two CT stages per header (egress); else only stage 0
 // exists and the odd hit-slot entries are never read (k_cta_route).
-constexpr int SCAN_U = 4;
-constexpr uint32_t SCAN_STAGE = 4096;   // staged create requests per block (32 KiB)
+#ifndef CFC_SCAN_U
+#define CFC_SCAN_U 4   // headers per scan thread and step (A/B builds)
+#endif
+constexpr int SCAN_U = CFC_SCAN_U;
+// staged create requests per block (24 KiB at four headers per thread)
+constexpr uint32_t SCAN_STAGE = 256 * SCAN_U * 2 + 1024;   // (a step's worst case fits)
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
 {
@@ -732,7 +736,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 if (TWO)
                     *reinterpret_cast<uint2 *>(A.hs + 2 * i) = make_uint2(slot[u][0], slot[u][1]);
                 else
-                    A.hs[2 * i] = slot[u][0];
+                    A.hs[i] = slot[u][0];   // (one stage: one word per header)
             }
         }
         // the creates' requests: staged in LDS, the block's list taken from
@@ -1318,7 +1322,7 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < RU; u++) {
             const uint64_t k = base + u * 256 + threadIdx.x;
-            slot[u] = k < nk ? A.hs[two ? k : 2 * k] : HS_NONE;
+            slot[u] = k < nk ? A.hs[k] : HS_NONE;   // (one stage: one word per header)
         }
 #pragma unroll
         for (int u = 0; u < RU; u++)
@@ -1626,16 +1630,19 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
     const uint64_t slots = (uint64_t)A.mask + 1;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * FU;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * FU; base < slots; base += stride) {
-        uint32_t m[FU], w[FU];
+        uint32_t m[FU], w[FU], sl[FU];
         St e[FU];
 #pragma unroll
         for (int u = 0; u < FU; u++) {
-            const uint64_t s = base + u * 256 + threadIdx.x;
-            m[u] = s < slots ? A.ms[s].x >> SUM_SH : 0u;
+            const uint64_t k = base + u * 256 + threadIdx.x;
+            sl[u] = k < slots ? (uint32_t)k : NONE;
         }
 #pragma unroll
+        for (int u = 0; u < FU; u++)
+            m[u] = sl[u] != NONE ? A.ms[sl[u]].x >> SUM_SH : 0u;
+#pragma unroll
         for (int u = 0; u < FU; u++) {
-            const uint64_t s = base + u * 256 + threadIdx.x;
+            const uint64_t s = sl[u];
             w[u] = 0;
             if (m[u]) {
                 e[u] = load_state(A.tm, (uint32_t)s);
@@ -1646,7 +1653,7 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
         for (int u = 0; u < FU; u++) {
             if (!m[u])
                 continue;
-            const uint64_t s = base + u * 256 + threadIdx.x;
+            const uint64_t s = sl[u];
             A.ms[s].x = 0;
             St &x = e[u];
             x.bits &= ~(RX_CLOSING | TX_CLOSING);
@@ -2101,6 +2108,9 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
             hipLaunchKernelGGL((k_cta_fold<V6, false>), dim3((ncx + 255) / 256), dim3(256), 0, s,
                                A, (const uint64_t *)dst, (const uint32_t *)nsel);
     }
+    // (a sweep of the whole table: a list of the touched slots, A/B'd,
+    // took 0.43 ms against the sweep's 0.30 — its random loads cost more
+    // than the sequential ones they save)
     hipLaunchKernelGGL(k_cta_finish<V6>, dim3(blocks_for((uint64_t)A.mask + 1, 8192)),
                        dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

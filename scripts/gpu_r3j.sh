@@ -2,7 +2,7 @@
 # counters, four slots per GC thread): CT tests, C5 --ct-apply bench and its
 # kernel trace (run via gpurun)
 set -o pipefail
-O=gpurun_out/r3j
+O=gpurun_out/r3k
 mkdir -p $O
 export TMPDIR=/tmp
 T="python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider"
