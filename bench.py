@@ -67,6 +67,40 @@ def pmc_entry(workload, mode, layout, kernels):
     return None
 
 
+def kernel_roofline(k, hn, ms, ws, pk, rows):
+    """One kernel's roofline entry: the launch's L2 hits priced at the L2
+    ceiling, its misses (TCC_MISS: the header stream, the output stores, and
+    table lines past L2) at the row of the memory that serves them — the
+    Infinity-Cache row of a kernel whose tables outgrow L2, else the HBM row
+    (the largest table measured) — over its live duration ms; pk: its PMC
+    record (profiles/pmc_traffic.json) or None.  Returns (entry, ideal
+    seconds, uniform-model seconds)."""
+    l2_peak = ceiling_for(1, rows)[1]
+    mib, peak_k = ceiling_for(ws, rows)
+    miss_mib, miss_peak = (mib, peak_k) if ws > 6 * (1 << 20) else rows[-1]
+    d = {"kernel": k, "headers": hn, "ms_per_launch": round(ms, 4),
+         "working_set_mib": round(ws / (1 << 20), 2),
+         "ceiling_table_mib": mib, "ceiling_greq_s": peak_k}
+    if not pk:
+        return d, 0.0, 0.0
+    req = pk["l2_requests_per_launch"]
+    hits, miss = pk.get("l2_hits_per_launch"), pk.get("l2_misses_per_launch")
+    if hits is None or miss is None:
+        hits, miss = req, 0.0
+    t_ideal = hits / (l2_peak * 1e9) + miss / (miss_peak * 1e9)
+    t_unif = req / (peak_k * 1e9)
+    d.update({"l2_requests_per_launch": req,
+              "l2_requests_per_header": round(req / hn, 3),
+              "l2_hits_per_launch": hits, "l2_misses_per_launch": miss,
+              "hit_ceiling_greq_s": l2_peak,
+              "miss_ceiling_greq_s": miss_peak, "miss_ceiling_table_mib": miss_mib,
+              "achieved_greq_s": round(req / (ms * 1e-3) / 1e9, 1),
+              "frac": round(t_ideal / (ms * 1e-3), 4),
+              "frac_uniform": round(t_unif / (ms * 1e-3), 4),
+              "hbm_bytes_per_launch": pk["hbm_bytes_per_launch"]})
+    return d, t_ideal, t_unif
+
+
 def reference_bpf_baseline():
     """The reference's own BPF datapath timed under BPF_PROG_TEST_RUN in the
     build container (oracle/time_reference.py; the GPU box has no reference
@@ -388,38 +422,17 @@ def main():
     # output stores, and table lines past L2) at the row of the memory that
     # serves them: the Infinity-Cache row of a kernel whose tables outgrow
     # L2, else the HBM row (the largest table measured)
-    l2_peak = ceiling_for(1, rows)[1]
-    hbm_row = rows[-1]
     pe = pmc_entry(args.workload, args.mode, layout, [(k, hn) for k, hn, _, _ in kernels])
     per_kernel = []
     req_tot = ideal_s = ideal_u = traffic = 0.0
     for k, hn, ms, ws in kernels:
-        mib, peak_k = ceiling_for(ws, rows)
-        miss_mib, miss_peak = (mib, peak_k) if ws > 6 * (1 << 20) else hbm_row
-        d = {"kernel": k, "headers": hn, "ms_per_launch": round(ms, 4),
-             "working_set_mib": round(ws / (1 << 20), 2),
-             "ceiling_table_mib": mib, "ceiling_greq_s": peak_k}
+        d, t_ideal, t_unif = kernel_roofline(k, hn, ms, ws, pe["kernels"][k] if pe else None,
+                                             rows)
         if pe:
-            pk = pe["kernels"][k]
-            req = pk["l2_requests_per_launch"]
-            hits, miss = pk.get("l2_hits_per_launch"), pk.get("l2_misses_per_launch")
-            if hits is None or miss is None:
-                hits, miss = req, 0.0
-            t_ideal = hits / (l2_peak * 1e9) + miss / (miss_peak * 1e9)
-            t_unif = req / (peak_k * 1e9)
-            d.update({"l2_requests_per_launch": req,
-                      "l2_requests_per_header": round(req / hn, 3),
-                      "l2_hits_per_launch": hits, "l2_misses_per_launch": miss,
-                      "hit_ceiling_greq_s": l2_peak,
-                      "miss_ceiling_greq_s": miss_peak, "miss_ceiling_table_mib": miss_mib,
-                      "achieved_greq_s": round(req / (ms * 1e-3) / 1e9, 1),
-                      "frac": round(t_ideal / (ms * 1e-3), 4),
-                      "frac_uniform": round(t_unif / (ms * 1e-3), 4),
-                      "hbm_bytes_per_launch": pk["hbm_bytes_per_launch"]})
-            req_tot += req
+            req_tot += d["l2_requests_per_launch"]
             ideal_s += t_ideal
             ideal_u += t_unif
-            traffic += pk["hbm_bytes_per_launch"]
+            traffic += d["hbm_bytes_per_launch"]
         per_kernel.append(d)
     stream_b = n * STREAM_V4 + n6 * STREAM_V6
     bound = ("l2" if all(d["ceiling_table_mib"] <= 6 for d in per_kernel)

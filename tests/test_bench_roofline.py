@@ -1,0 +1,50 @@
+"""The bench line's roofline from the committed PMC records
+(profiles/pmc_traffic.json, written by scripts/pmc_summary.py --record) and
+the random-access ceilings (profiles/ubench/): every recorded kernel prices
+below its ceiling (frac <= 1) under the slowest row its misses can be
+priced at, and the headline C2 kernel sits at >= 0.5 of it.  CPU only: the
+records carry each kernel's average launch time from the same profile."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+DB = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))["entries"]
+
+
+def test_ceilings_measured():
+    rows = bench.ubench_ceilings()
+    assert rows, "profiles/ubench has no random-access rows"
+    mibs = [m for m, _ in rows]
+    assert mibs == sorted(mibs)
+    # the L2-resident rows are the fastest, the largest tables the slowest
+    assert rows[0][1] > rows[-1][1]
+
+
+@pytest.mark.parametrize("e", DB, ids=[x["workload"] for x in DB])
+def test_recorded_kernels_below_ceiling(e):
+    rows = bench.ubench_ceilings()
+    assert os.path.isdir(os.path.join(ROOT, e["source"])), e["source"]
+    for k, pk in e["kernels"].items():
+        for field in ("headers", "l2_requests_per_launch", "hbm_bytes_per_launch", "avg_ms"):
+            assert field in pk, (k, field)
+        assert pk["l2_hits_per_launch"] + pk["l2_misses_per_launch"] == pytest.approx(
+            pk["l2_requests_per_launch"], rel=1e-6)
+        # a small working set prices misses at the HBM row, the slowest
+        d, t_ideal, _ = bench.kernel_roofline(k, pk["headers"], pk["avg_ms"], 1 << 20, pk, rows)
+        assert 0 < d["frac"] <= 1.0, (e["workload"], k, d["frac"])
+        assert t_ideal > 0
+
+
+def test_headline_c2_at_half_of_its_ceiling():
+    e = next(x for x in DB if x["workload"] == "c2")
+    pk = e["kernels"]["k_classify_v4"]
+    d, _, _ = bench.kernel_roofline("k_classify_v4", pk["headers"], pk["avg_ms"],
+                                    3 << 20, pk, bench.ubench_ceilings())
+    assert d["frac"] >= 0.5, d
+    assert pk["headers"] == 64 << 20
