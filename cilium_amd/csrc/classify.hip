@@ -60,9 +60,6 @@
 #include <vector>
 
 #include "kern_common.hpp"
-#ifndef CFC_DIR_AHEAD
-#define CFC_DIR_AHEAD 0   // 1: directory probes an iteration ahead (A/B builds)
-#endif
 #ifndef CFC_EXP
 #define CFC_EXP 0   // timing experiments only (1: no LPM, 2: no policy, 3: no key stores)
 #endif
@@ -216,11 +213,10 @@ __device__ __forceinline__ void r1_take(const Raw &r, uint32_t i, uint32_t end,
     h.lbfl = r.lbfl;
 }
 
-// round 2: every lookup that only needs the header (PRE: the directory
-// entry was loaded an iteration ahead, into pre)
-template <int MODE, bool PRE = false>
+// round 2: every lookup that only needs the header
+template <int MODE>
 __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
-                                         Hdr &h, uint4 pre = uint4{})
+                                         Hdr &h)
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
@@ -233,9 +229,7 @@ __device__ __forceinline__ void r2_issue(const DevTables &T, const Lds &S,
     h.lxs = h.lss = h.pfb = 0;
     h.pf_maybe = false;
     if (LPM) {
-        if (PRE)
-            h.l4d = pre;
-        else if (T.l4d)
+        if (T.l4d)
 #if CFC_EXP == 1
             h.l4d = make_uint4(h.lh & 0xFFFF, 0, 0, 0);
 #else
@@ -740,55 +734,23 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #pragma unroll
     for (int u = 0; u < U; u++)
         r1_issue<OPT, LBE>(in, LI, u * BLOCK + threadIdx.x, end, nx[u]);
-    // AHEAD: headers two iterations ahead, and the next iteration's /16
-    // directory entry issued behind this one's policy probe (one L2 round
-    // trip off each iteration's chain, for four more registers)
-    constexpr bool AHEAD = CFC_DIR_AHEAD && FAST && MODE != CFC_MODE_XDP;
-    Raw nx2[U];
-    uint4 nd[U];
-    auto dir_of = [&](const Raw &r) {
-        return ldt16(T.l4d, (__builtin_bswap32(EGR ? r.tda : r.sa) >> 16) * 16u);
-    };
-    if (AHEAD) {
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            r1_issue<OPT, LBE>(in, LI, BLOCK * U + u * BLOCK + threadIdx.x, end, nx2[u]);
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            nd[u] = dir_of(nx[u]);
-    }
     for (uint32_t base = 0; base < end; base += BLOCK * U) {
         Hdr h[U];
 #pragma unroll
         for (int u = 0; u < U; u++)
             r1_take(nx[u], base + u * BLOCK + threadIdx.x, end, h[u]);
 #pragma unroll
-        for (int u = 0; u < U; u++) {
-            if (AHEAD)
-                r2_issue<MODE, true>(T, S, h[u], nd[u]);
-            else
-                r2_issue<MODE>(T, S, h[u]);
-        }
+        for (int u = 0; u < U; u++)
+            r2_issue<MODE>(T, S, h[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r3_identity<MODE, CT, LB>(T, S, E, h[u]);
         // the next iteration's headers, behind this one's policy probe (the
         // last iteration re-reads the slice's last header)
         const uint32_t nb = base + BLOCK * U;
-        if (AHEAD) {
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                nx[u] = nx2[u];
-                r1_issue<OPT, LBE>(in, LI, nb + BLOCK * U + u * BLOCK + threadIdx.x, end, nx2[u]);
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                nd[u] = dir_of(nx[u]);
-        } else {
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                r1_issue<OPT, LBE>(in, LI, nb + u * BLOCK + threadIdx.x, end, nx[u]);
-        }
+        for (int u = 0; u < U; u++)
+            r1_issue<OPT, LBE>(in, LI, nb + u * BLOCK + threadIdx.x, end, nx[u]);
 #pragma unroll
         for (int u = 0; u < U; u++)
             r4_verdict<MODE, CT, NT, LB>(T, S, E, h[u]);

@@ -106,9 +106,6 @@ __device__ __forceinline__ uint4 ld16(const void *p)
     return *reinterpret_cast<const uint4 *>(p);
 }
 
-#ifndef CFC_LDT_AUX
-#define CFC_LDT_AUX 0   // cache-policy bits of the table probes (A/B builds: 16 sc1, 2 nt)
-#endif
 // 16-byte table load that stays ONE load: a plain uint4 load whose upper
 // half is only used on some paths gets split by the compiler into two
 // dependent 8-byte loads (a second L2 round trip); a buffer load is never
@@ -117,7 +114,7 @@ __device__ __forceinline__ uint4 ldt16(const void *base, uint32_t off)
 {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, CFC_LDT_AUX);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
