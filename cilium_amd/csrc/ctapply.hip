@@ -704,11 +704,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         for (int u = 0; u < SCAN_U; u++)
 #pragma unroll
             for (int st = 0; st < NST; st++)
-#if CFC_EXP == 9   // (timing only: no plain-hit summaries — the floor a sort-based one would face)
-                cur[u][st] = sb[u][st];
-#else
                 cur[u][st] = (sb[u][st] && slot[u][st] != HS_NONE) ? A.ms[slot[u][st]].x : 0u;
-#endif
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
