@@ -2,7 +2,7 @@
 # bench, C5 --ct-apply (20 steps, GC at the reference's cadence), C3, and a
 # kernel trace of the default bench (run via gpurun)
 set -o pipefail
-O=gpurun_out/r3final
+O=gpurun_out/r3final2
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -p no:cacheprovider --durations=15 > $O/gpu_tests.log 2>&1
