@@ -2434,3 +2434,56 @@ size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap)
         qsort(rows, n, CFO_CT_ROW, cmp_ctrow);
     return n;
 }
+
+/* The reference's own semantics, in C (TEST INFRASTRUCTURE): the headers one
+ * at a time, each classified against the CT maps as the headers before it
+ * left them and folded into them before the next — what the kernel does
+ * packet by packet (conntrack.h:221-285 lookups, :615-772 creates, the
+ * ct_delete of a denied established flow), at bpf_ktime_get_sec() = clock[i]
+ * (clock NULL: the clock as set).  Outputs as cfo_classify_* (+ the CT byte
+ * and the monitor event site word of every header). */
+void cfo_run_seq(cfo_t *o, int family, int mode, uint16_t ep_lxc, size_t n,
+                 const uint8_t *saddr, const uint8_t *daddr, const uint16_t *sport,
+                 const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+                 const uint16_t *len, const uint32_t *mark, const uint8_t *tcpflags,
+                 const uint32_t *clock, int32_t *action, int32_t *verdict,
+                 uint32_t *identity, uint8_t *ct, uint32_t *words)
+{
+    const size_t al = family == 4 ? 4 : 16, pw = family == 4 ? 3 : 9;
+    const uint32_t *hash0 = o->hash_in;
+    uint32_t *pkt0 = o->pkt_out;
+    uint32_t *nt0 = o->notify_out, *mon0 = o->notify_mon;
+    uint32_t mon1 = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (clock)
+            o->now = clock[i];
+        o->hash_in = hash0 ? hash0 + i : NULL;
+        o->pkt_out = pkt0 ? pkt0 + pw * i : NULL;
+        o->notify_out = words ? words + i : NULL;
+        o->notify_mon = &mon1;
+        uint8_t c = 0;
+        const uint8_t *sa = saddr + al * i, *da = daddr + al * i;
+        if (family == 4)
+            cfo_classify_v4(o, mode, ep_lxc, 1, (const uint32_t *)sa, (const uint32_t *)da,
+                            sport + i, dport + i, proto + i, flags + i, len + i,
+                            mark ? mark + i : NULL, tcpflags ? tcpflags + i : NULL,
+                            action + i, verdict + i, identity + i, NULL, &c, 1);
+        else
+            cfo_classify_v6(o, mode, ep_lxc, 1, sa, da, sport + i, dport + i, proto + i,
+                            flags + i, len + i, mark ? mark + i : NULL,
+                            tcpflags ? tcpflags + i : NULL, action + i, verdict + i,
+                            identity + i, NULL, &c, 1);
+        o->pkt_out = NULL;
+        o->notify_out = NULL;
+        o->notify_mon = NULL;
+        ct_apply(o, (int)al, mode, ep_lxc, 1, sa, da, sport + i, dport + i, proto + i,
+                 flags + i, len + i, tcpflags ? tcpflags + i : NULL,
+                 (const uint32_t *)identity + i, verdict + i, &c, NULL, NULL);
+        if (ct)
+            ct[i] = c;
+    }
+    o->hash_in = hash0;
+    o->pkt_out = pkt0;
+    o->notify_out = nt0;
+    o->notify_mon = mon0;
+}

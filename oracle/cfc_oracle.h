@@ -157,6 +157,14 @@ uint32_t cfo_flow_hash6(const uint8_t sa[16], const uint8_t da[16], uint16_t spo
                         uint16_t dport, uint8_t proto);
 #define CFO_CT_ROW 104
 size_t cfo_ct_dump(cfo_t *o, uint8_t *rows, size_t cap);
+/* the reference's semantics: headers one at a time, each folded into the CT
+ * maps before the next, at clock[i] (NULL: the clock as set) */
+void cfo_run_seq(cfo_t *o, int family, int mode, uint16_t ep_lxc, size_t n,
+                 const uint8_t *saddr, const uint8_t *daddr, const uint16_t *sport,
+                 const uint16_t *dport, const uint8_t *proto, const uint8_t *flags,
+                 const uint16_t *len, const uint32_t *mark, const uint8_t *tcpflags,
+                 const uint32_t *clock, int32_t *action, int32_t *verdict,
+                 uint32_t *identity, uint8_t *ct, uint32_t *words);
 /* ctmap.GC with doFiltering (pkg/maps/ctmap/ctmap.go:303-350) on the
  * selected maps (family 0/1/2, owner -1/0/lxc_id + 1, kind -1/0 TCP/1 ANY);
  * IP sets are 17-byte {family, address[16]} records, n = SIZE_MAX: no set */

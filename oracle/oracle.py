@@ -138,6 +138,9 @@ def lib():
         L.cfo_ct_gc.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_uint32, vp, ctypes.c_size_t, vp, ctypes.c_size_t]
         L.cfo_ct_gc.restype = ctypes.c_size_t
+        L.cfo_run_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_uint16,
+                                  ctypes.c_size_t] + [vp] * 15
+        L.cfo_run_seq.restype = None
         _lib = L
     return _lib
 
@@ -347,24 +350,35 @@ class Oracle:
                                  [i64(ifx[lxc]), i64(ifx[lxc]), i64(self.host_ifindex)], 0)
         return r, idx
 
-    def run_sequential(self, hdr, mode, ep_lxc, clock):
+    def run_sequential(self, hdr, mode, ep_lxc, clock=None, want_ct=False, want_pkt=False):
         """The reference's own semantics: one header at a time, each folded
-        into the CT maps before the next (the batch engine's lookups all see
-        the batch-start state instead), at the bpf_ktime_get_sec() value
-        clock[i] -> (action, verdict, identity, event words)."""
+        into the CT maps before the next (cfo_run_seq), at the
+        bpf_ktime_get_sec() value clock[i] (None: the clock as set; a scalar:
+        that clock for every header) -> (action, verdict, identity, event
+        words[, ct][, pkt])."""
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
         ide = np.zeros(n, np.uint32)
         words = np.zeros(n, np.uint32)
-        for i in range(n):
-            self.set_clock(int(clock[i]))
-            one = hdr.slice(i, i + 1)
-            a, v, d, ct, w = self.classify(one, mode, ep_lxc, want_ct=True,
-                                           want_notify=True)
-            self.ct_apply(one, mode, ep_lxc, d, v, ct)
-            act[i], ver[i], ide[i], words[i] = a[0], v[0], d[0], w[0]
-        return act, ver, ide, words
+        ct = np.zeros(n, np.uint8)
+        pkt = np.zeros((n, 3 if hdr.family == 4 else 9), np.uint32) if want_pkt else None
+        clk = None
+        if clock is not None:
+            clk = np.ascontiguousarray(np.broadcast_to(np.asarray(clock, np.int64), (n,))
+                                       .astype(np.uint32))
+        arrs = self._arrays(hdr)
+        self._lb_io(hdr, pkt)
+        self.L.cfo_run_seq(self.h, hdr.family, mode, ep_lxc, n,
+                           *[_p(a) for a in arrs], _p(clk), _p(act), _p(ver), _p(ide),
+                           _p(ct), _p(words))
+        self.L.cfo_set_lb_io(self.h, None, None)
+        out = (act, ver, ide, words)
+        if want_ct:
+            out += (ct,)
+        if want_pkt:
+            out += (pkt,)
+        return out
 
     def drop_notify(self, hdr, mode, ep_lxc, verdict, identity, sites):
         """The struct drop_notify records (bpf/lib/drop.h:40-78) of this
