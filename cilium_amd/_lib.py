@@ -107,7 +107,9 @@ class Stats(ctypes.Structure):
                 ("ct4_entries", ctypes.c_uint32),
                 ("ct6_entries", ctypes.c_uint32),
                 ("ct_apply_device", ctypes.c_uint32),
-                ("ct_apply_host", ctypes.c_uint32)]
+                ("ct_apply_host", ctypes.c_uint32),
+                ("ct_order_changed", ctypes.c_uint32),
+                ("ct_slots", ctypes.c_uint32)]
 
 
 class NodeConfig(ctypes.Structure):

@@ -24,58 +24,6 @@ using namespace cfc;
 
 namespace {
 
-struct DevBuf {
-    void *p = nullptr;
-    size_t bytes = 0;
-    ~DevBuf() { reset(); }
-    void reset()
-    {
-        if (p)
-            (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    int zeros(size_t n, hipStream_t s)
-    {
-        reset();
-        if (!n)
-            return 0;
-        if (hipMalloc(&p, n) != hipSuccess) {
-            p = nullptr;
-            return -ENOMEM;
-        }
-        bytes = n;
-        return hipMemsetAsync(p, 0, n, s) == hipSuccess ? 0 : -EIO;
-    }
-    // at least n bytes (contents not kept)
-    int ensure(size_t n)
-    {
-        if (bytes >= n && p)
-            return 0;
-        reset();
-        if (hipMalloc(&p, std::max<size_t>(n, 256)) != hipSuccess) {
-            p = nullptr;
-            return -ENOMEM;
-        }
-        bytes = std::max<size_t>(n, 256);
-        return 0;
-    }
-    int upload(const void *src, size_t n, hipStream_t s)
-    {
-        reset();
-        if (!n)
-            return 0;
-        if (hipMalloc(&p, n) != hipSuccess) {
-            p = nullptr;
-            return -ENOMEM;
-        }
-        bytes = n;
-        if (hipMemcpyAsync(p, src, n, hipMemcpyHostToDevice, s) != hipSuccess)
-            return -EIO;
-        return 0;
-    }
-};
-
 template <class T>
 static int upload_vec(DevBuf &b, const std::vector<T> &v, hipStream_t s)
 {
@@ -216,6 +164,12 @@ struct cfc_ctx {
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
     DevBuf cta_lbr, cta_reqs;     // a load balancer's service step per header (LbRec4/6)
     DevBuf cta_obm;               // the apply's ordered-slot bitmap
+    // packet-order CT results (ctorder.hip): buffers, the deleted-slot
+    // bitmap (zero between applies), counters; the stages it changed
+    OrdBufs ordb;
+    DevBuf ord_delbm, ord_cnt;
+    DevBuf cta_mon;               // per header stage: the fold's monitor length
+    uint64_t n_ord_changed = 0;
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -2165,6 +2119,9 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     *st = c->epoch->st;
     st->ct_apply_device = c->n_apply_dev;
     st->ct_apply_host = c->n_apply_host;
+    st->ct_order_changed = (uint32_t)c->n_ord_changed;
+    st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->ct4_host.size() + c->epoch->ct->ct6_host.size())
+                            : 0u;
     return 0;
 }
 
@@ -2754,6 +2711,35 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             A.ck2 = L.k2 ? (const uint32_t *)((const char *)c->ws + L.k2) : nullptr;
         }
     }
+    // the reference's packet-order CT results (ctorder.hip): the stages a
+    // CT write earlier in the batch changes get their CT byte rewritten
+    // before the apply folds it (once per call: not again after a rebuild)
+    // (a batch with a load balancer's service step: TODO, its records come
+    // from the scan)
+    if (may_grow && !lbm) {
+        if (c->ord_delbm.bytes < obm_bytes && c->ord_delbm.zeros(obm_bytes, s))
+            return -ENOMEM;
+        if (c->ord_cnt.ensure(4 * ORD_NCNT))
+            return -ENOMEM;
+        OrdArgs O{};
+        O.ctb = out->ct;
+        O.ck1 = const_cast<uint32_t *>(A.ck1);
+        O.ck2 = const_cast<uint32_t *>(A.ck2);
+        O.delbm = (uint32_t *)c->ord_delbm.p;
+        O.cnt = (uint32_t *)c->ord_cnt.p;
+        uint32_t changed = 0;
+        if (int rc = ord_resolve(A, O, c->ordb, V6, &changed, s))
+            return rc;
+        c->n_ord_changed += changed;
+    }
+    // the caller wants the event words: the trace words' monitor lengths in
+    // packet order (every hit replayed by the fold, k_cta_mon)
+    if (out->notify && !lbm) {
+        if (c->cta_mon.ensure(2 * n) || hipMemsetAsync(c->cta_mon.p, 0xFF, 2 * n, s) != hipSuccess)
+            return -ENOMEM;
+        A.nt = out->notify;
+        A.mon = (uint8_t *)c->cta_mon.p;
+    }
     uint32_t hc[CTA_NCNT];
     if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess ||
         hipMemsetAsync(A.obm, 0, obm_bytes, s) != hipSuccess || cta_scan(A, V6, s) ||
@@ -2977,6 +2963,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
         auto it = initial.find(std::make_pair(mp, key));
         return it != initial.end() && !it->second;
     };
+    bool ct_changed = false;   // (CT bytes the packet order changed)
     for (size_t i = 0; i < n; i++) {
         const uint8_t cb = ct[i];
         const uint32_t proto = mt[i] & 0xFF, len = mt[i] >> 16;
@@ -3144,8 +3131,22 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             };
             const std::string k1 = tuple(kd_, ks, td, ts, fl);
             const std::string k2 = tuple(ks, kd_, ts, td, fl ^ 1u);
-            const int b = cs & CFC_CT_RES_MASK;
+            int b = cs & CFC_CT_RES_MASK;
             const bool dropped = st == last && ver[i] == -133;   // DROP_POLICY
+            if (b < 2) {
+                // CT_NEW / CT_ESTABLISHED as the headers before left k2 (the
+                // reference's packet order, ctorder.hip); the launch's k1
+                // result stands (no write of the batch has k1's flag)
+                const bool allowed = (cs & CFC_CT_CREATE) || (b == 1 && !dropped);
+                b = m->kv.count(k2) ? 1 : 0;
+                const uint8_t ncs = (uint8_t)(b | CFC_CT_DONE | ((b == 0 && allowed) ? CFC_CT_CREATE : 0));
+                if (ncs != cs) {
+                    ct[i] = (uint8_t)((ct[i] & ~(0xF << (4 * st))) | ncs << (4 * st));
+                    ct_changed = true;
+                    c->n_ord_changed++;
+                }
+            }
+            const uint8_t csn = (uint8_t)(ct[i] >> (4 * st));
             if (b >= 2) {                       // CT_REPLY / CT_RELATED
                 auto it = m->kv.find(k1);
                 if (it != m->kv.end()) {
@@ -3173,7 +3174,7 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                         (void)m->erase(k2.data());
                     }
                 }
-            } else if (cs & CFC_CT_CREATE) {
+            } else if (csn & CFC_CT_CREATE) {
                 auto it = m->kv.find(k2);
                 if (it != m->kv.end()) {        // created earlier in this batch
                     ct_hit_update(m, it->second, action, dir, true, len, now, is_tcp,
@@ -3225,6 +3226,9 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
             }
         }
     }
+    if (ct_changed &&
+        hipMemcpyAsync(out->ct, ct.data(), n, hipMemcpyHostToDevice, s) != hipSuccess)
+        return -EIO;
     if (hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     return 0;

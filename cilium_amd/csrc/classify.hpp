@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cerrno>
+
 #include "../../include/cfc.h"
 #include "layout.h"
 
@@ -207,7 +210,92 @@ struct CtaArgs {
     void *sort_tmp;
     size_t sort_tmp_bytes;
     int ob, slot_bits;           // sort keys: slot << ob | order
+    // the batch's monitor event words (cfc_out.notify), or null: then every
+    // hit is replayed in order and the trace words get the packet-order
+    // monitor length (k_cta_mon); mon: per header stage the length the
+    // fold found (MON_* codes), 0xFF not replayed
+    uint32_t *nt;
+    uint8_t *mon;
 };
+// a device buffer owned by the host library (grown on demand)
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { reset(); }
+    void reset()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    int zeros(size_t n, hipStream_t s)
+    {
+        reset();
+        if (!n)
+            return 0;
+        if (hipMalloc(&p, n) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        bytes = n;
+        return hipMemsetAsync(p, 0, n, s) == hipSuccess ? 0 : -EIO;
+    }
+    // at least n bytes (contents not kept)
+    int ensure(size_t n)
+    {
+        if (bytes >= n && p)
+            return 0;
+        reset();
+        if (hipMalloc(&p, std::max<size_t>(n, 256)) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        bytes = std::max<size_t>(n, 256);
+        return 0;
+    }
+    int upload(const void *src, size_t n, hipStream_t s)
+    {
+        reset();
+        if (!n)
+            return 0;
+        if (hipMalloc(&p, n) != hipSuccess) {
+            p = nullptr;
+            return -ENOMEM;
+        }
+        bytes = n;
+        if (hipMemcpyAsync(p, src, n, hipMemcpyHostToDevice, s) != hipSuccess)
+            return -EIO;
+        return 0;
+    }
+};
+
+// ---- packet-order CT results (ctorder.hip), run by cfc_ct_apply before
+// the apply proper
+enum { ORD_NPART, ORD_NPART2, ORD_NDEL, ORD_NRELKEY, ORD_NREL, ORD_COLL, ORD_CHANGED,
+       ORD_NCNT };
+struct OrdArgs {
+    uint8_t *ctb;                 // the batch's CT bytes (rewritten in place)
+    uint32_t *ck1, *ck2;          // the classify launch's hit keys (or null)
+    uint32_t *delbm;              // deleted-slot bitmap (zero between applies)
+    uint32_t *cnt;                // ORD_* counters
+    uint32_t *part;               // participants: header << 1 | stage
+    uint32_t part_cap, part_base;
+    uint32_t *rel_src;
+    void *rk;                     // per record its key (16 B; IPv6 48 B)
+    uint64_t *rh, *rh2, *rh3;     // fingerprints
+    uint32_t *rord, *rord2, *ridx, *ridx2;
+    uint8_t *pinfo, *nres;
+    void *tmp;
+    size_t tmp_bytes;
+};
+struct OrdBufs {
+    DevBuf part, rel_src, rk, rh, rh2, rh3, rord, rord2, ridx, ridx2, pinfo, nres, tmp;
+};
+// rewrites the CT bytes (and hit keys) of the stages whose packet-order
+// result differs from the launch's; *changed: how many
+int ord_resolve(const CtaArgs &A, OrdArgs &O, OrdBufs &B, bool v6, uint32_t *changed,
+                hipStream_t s);
 size_t cta_sort_tmp_bytes(uint32_t n);
 // v6: the batch is IPv6 (A.ct6, A.log6)
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);

@@ -28,555 +28,12 @@
 // TCP map are not in the device table (no lookup reaches them, flatten.cpp
 // build_ct): they go to a log the host replays in order.
 #include <hipcub/hipcub.hpp>
-#include <type_traits>
 
-#include "kern_common.hpp"
+#include "ctops.hpp"
 
 namespace cfc {
 
 namespace {
-
-constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,
-                   CT_CLOSE_TIMEOUT = 10, CT_REPORT_INTERVAL = 5;
-constexpr uint32_t RX_CLOSING = 1, TX_CLOSING = 2, SEEN_NON_SYN = 16;   // ct_entry bits
-constexpr uint32_t OP_NONE = 0, OP_HIT = 1, OP_DELETE = 2, OP_CREATE = 3;
-// per-slot marks of one apply: ordered ops; inserted by this apply; a
-// delete among its ops; a create or related-entry write among its ops
-constexpr uint32_t MARK_ORDERED = 1, MARK_FRESH = 2, MARK_DEL = 4, MARK_PUTC = 8;
-__device__ __forceinline__ void mark_or(uint32_t *m, uint32_t bits)
-{
-    if ((*m & bits) != bits)
-        atomicOr(m, bits);
-}
-// A slot's word x holds its marks (bits 0-3) and the summary of its plain
-// hits (bits 8-26, see k_cta_finish): both only ever OR'ed in.  y holds the
-// order of a deleted entry's first delete.  The ordered slots are also bits
-// of A.obm, which k_cta_route tests per hit (a few MiB: cache-resident,
-// where the per-slot words are not).
-constexpr int SUM_SH = 8;
-__device__ __forceinline__ uint32_t sum_bits(bool in, bool tcp, bool close, uint32_t tfl)
-{
-    return ((in ? tfl : tfl << 8) | (in ? 1u << 16 : 1u << 17) |
-            ((tcp && !close) ? 1u << 18 : 0u)) << SUM_SH;
-}
-__device__ __forceinline__ void order_mark(const CtaArgs &A, uint32_t sl, uint32_t bits)
-{
-    if ((A.ms[sl].x & bits) != bits) {
-        atomicOr(&A.ms[sl].x, bits);
-        const uint32_t b = 1u << (sl & 31);
-        if (!(A.obm[sl >> 5] & b))
-            atomicOr(&A.obm[sl >> 5], b);
-    }
-}
-constexpr uint32_t HS_NONE = 0xFFFFFFFFu;
-
-// An op's place in the batch, the low bits of every request and list entry:
-// ((2 * i + st) << 3) | sec << 1 — i the header (with a load balancer,
-// i = n + h is the CT_SERVICE op of header h), st its CT stage, sec the
-// write: the op itself, its create's related ICMP entry, its create's
-// reverse-NAT entry (ct_create4 with ct_state->addr), or a hit on an entry
-// this batch created (the destination's lookup finding what the sender's
-// create just wrote).  Bit 0 is free: a request's first-create mark.
-constexpr uint32_t SEC_OP = 0, SEC_REL = 1, SEC_KX = 2, SEC_FHIT = 3;
-__device__ __forceinline__ uint32_t ord_of(uint64_t i, int st, uint32_t sec)
-{
-    return (uint32_t)(((2 * i + (uint64_t)st) << 3) | sec << 1);
-}
-__device__ __forceinline__ uint64_t ord_hdr(uint32_t o) { return o >> 4; }
-__device__ __forceinline__ int ord_st(uint32_t o) { return (int)((o >> 3) & 1); }
-__device__ __forceinline__ uint32_t ord_sec(uint32_t o) { return (o >> 1) & 3; }
-
-__device__ __forceinline__ uint32_t wave_count(uint32_t *ctr, bool want)
-{
-    const uint64_t m = __ballot(want);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t lead = m ? (uint32_t)__builtin_ctzll(m) : 0u;
-    uint32_t base = 0;
-    if (m && lane == lead)
-        base = atomicAdd(ctr, (uint32_t)__popcll(m));
-    base = __shfl(base, (int)lead, 64);
-    return base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-}
-
-// the same for a whole block of 256 threads: one atomic per block, not per
-// wave (a counter every wave of a 64M-header pass bumps serialises at its
-// L2 channel).  Every thread of the block calls it.
-__device__ __forceinline__ uint32_t block_count(uint32_t *ctr, bool want)
-{
-    __shared__ uint32_t wsum[4], base;
-    const uint64_t m = __ballot(want);
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane == 0)
-        wsum[wv] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        base = t ? atomicAdd(ctr, t) : 0u;
-    }
-    __syncthreads();
-    uint32_t r = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-    for (uint32_t k = 0; k < wv; k++)
-        r += wsum[k];
-    __syncthreads();   // wsum and base are reused by the next call
-    return r;
-}
-// n items of this thread in a block-wide list: the first one's index, one
-// atomic per block (every thread of the block calls it)
-__device__ __forceinline__ uint32_t block_count_n(uint32_t *ctr, uint32_t v)
-{
-    __shared__ uint32_t wsum[4], base;
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d)
-            x += y;
-    }
-    if (lane == 63)
-        wsum[wv] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        base = t ? atomicAdd(ctr, t) : 0u;
-    }
-    __syncthreads();
-    uint32_t r = base + x - v;
-    for (uint32_t k = 0; k < wv; k++)
-        r += wsum[k];
-    __syncthreads();
-    return r;
-}
-// n items of this thread in a block's LDS staging list: their first index
-// there (the list's length in *sn); every thread of the block calls it
-__device__ __forceinline__ uint32_t block_stage_n(uint32_t *sn, uint32_t v)
-{
-    __shared__ uint32_t wsum[4], base;
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d)
-            x += y;
-    }
-    if (lane == 63)
-        wsum[wv] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        base = *sn;
-        *sn = base + wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    }
-    __syncthreads();
-    uint32_t r = base + x - v;
-    for (uint32_t k = 0; k < wv; k++)
-        r += wsum[k];
-    __syncthreads();
-    return r;
-}
-// the block's staged list into dst at places taken by one atomic on *ctr
-// (cap: dst's capacity); every thread of the block calls it
-__device__ __forceinline__ void block_flush(uint64_t *stage, uint32_t *sn, uint32_t *ctr,
-                                            uint64_t *dst, uint32_t cap)
-{
-    __shared__ uint32_t gbase;
-    const uint32_t n = *sn;
-    if (threadIdx.x == 0)
-        gbase = n ? atomicAdd(ctr, n) : 0u;
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x)
-        if (gbase + j < cap)
-            dst[gbase + j] = stage[j];
-    __syncthreads();
-    if (threadIdx.x == 0)
-        *sn = 0;
-    __syncthreads();
-}
-
-// a per-thread count added once per block (every thread of the block calls
-// it): counters that every wave of a full-table pass bumps serialise at
-// their L2 channel
-__device__ __forceinline__ void block_add(uint32_t *ctr, uint32_t v)
-{
-    __shared__ uint32_t wsum[4];
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0)
-        wsum[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t k = 0; k < (blockDim.x >> 6); k++)
-            t += wsum[k];
-        if (t)
-            atomicAdd(ctr, t);
-    }
-    __syncthreads();
-}
-// a per-thread count added once per wave (every lane of the wave calls it)
-__device__ __forceinline__ void wave_add(uint32_t *ctr, uint32_t v)
-{
-    for (int o = 32; o > 0; o >>= 1)
-        v += __shfl_xor(v, o, 64);
-    if ((threadIdx.x & 63) == 0 && v)
-        atomicAdd(ctr, v);
-}
-
-// ---- the address family.  A CT tuple's addresses are raw (network order,
-// loaded little-endian): one word for IPv4, four for IPv6.  The kernels are
-// templated on V6; the slot layouts are Ct4Slot / Ct6Slot (layout.h).
-template <bool V6>
-using Addr = typename std::conditional<V6, uint4, uint32_t>::type;
-__device__ __forceinline__ bool aeq(uint32_t a, uint32_t b) { return a == b; }
-__device__ __forceinline__ bool aeq(uint4 a, uint4 b)
-{
-    return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
-}
-__device__ __forceinline__ uint32_t khash(uint32_t d, uint32_t s, uint32_t z, uint32_t w)
-{
-    return ct_hash4(d, s, z, w);
-}
-__device__ __forceinline__ uint32_t khash(uint4 d, uint4 s, uint32_t z, uint32_t w)
-{
-    const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {s.x, s.y, s.z, s.w};
-    return ct_hash6(dw, sw, z, w);
-}
-template <bool V6>
-__device__ __forceinline__ Addr<V6> ld_addr(const uint32_t *p, uint64_t i)
-{
-    if constexpr (V6)
-        return ld16(reinterpret_cast<const uint4 *>(p) + i);
-    else
-        return p[i];
-}
-// the ICMP protocol of the family (ct_create4/6's related entry)
-template <bool V6>
-constexpr uint32_t icmp_proto()
-{
-    return V6 ? 58u : 1u;
-}
-// the w word of slot i
-template <bool V6>
-__device__ __forceinline__ uint32_t *slot_w(const CtaArgs &A, uint32_t i)
-{
-    if constexpr (V6)
-        return &A.ct6[i].w;
-    else
-        return &A.ct4[i].w;
-}
-
-// one CT stage of one header, decoded as cfc_api.cpp ct_apply does
-template <bool V6>
-struct Op {
-    uint32_t kind, action, dir;
-    bool is_tcp, syn, ki_form;
-    uint32_t tfl, len, sec, owner, proto, rev;
-    Addr<V6> sa, da;           // k1 = (da, sa, z1, w1), k2 = (sa, da, z2, w2)
-    uint32_t z1, w1;           // k1: the tuple as loaded (REPLY / RELATED)
-    uint32_t z2, w2;           // k2: reversed (ESTABLISHED / create)
-    // the ct_state a create writes with the entry (ct4_lb / ct6_lb words:
-    // rev_nat_index | lb_loopback << 16, slave; its related entry's slave)
-    uint32_t lbw, slave, slave_rel;
-    bool reslave;              // a CT_SERVICE op's ct_update4/6_slave
-    // ct_create4's reverse-NAT entry (kx: the create writes one): key
-    // (kxa, kxs, z2, kxw)
-    bool kx;
-    Addr<V6> kxa, kxs;
-    uint32_t kxw;
-};
-
-// owner word of the destination endpoint's CT maps (cilium_lxc lookup)
-__device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint32_t da)
-{
-    if (!T.lxc4)
-        return 0;
-    uint32_t s = hash32(da, T.lxc4_mask);
-    for (;;) {
-        const uint4 v = ld16(T.lxc4 + s);
-        if (!(v.w & LXC_VALID))
-            return 0;
-        if (v.x == da)
-            return ct_owner_word(v.w & 0xFFFF, (v.w & LXC_CT_LOCAL) != 0);
-        s = (s + 1) & T.lxc4_mask;
-    }
-}
-__device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint4 da)
-{
-    if (!T.lxc6)
-        return 0;
-    uint32_t s = l6_hash(da.x, da.y, da.z, da.w, L6_LXC_TAG) & T.lxc6_mask;
-    for (;;) {
-        const uint4 k = ld16(&T.lxc6[s].a[0]);
-        const uint4 v = ld16(&T.lxc6[s].pol_base);   // {pol_base, pol_mask, info, 0}
-        if (!(v.z & LXC_VALID))
-            return 0;
-        if (aeq(k, da))
-            return ct_owner_word(v.z & 0xFFFF, (v.z & LXC_CT_LOCAL) != 0);
-        s = (s + 1) & T.lxc6_mask;
-    }
-}
-
-template <bool V6>
-using LbRecT = typename std::conditional<V6, LbRec6, LbRec4>::type;
-
-// one header's inputs of the apply; with a load balancer (LB) its service
-// step's record too, and svcop: the header's CT_SERVICE op (virtual header
-// n + i) rather than its CT stages
-template <bool V6>
-struct ScanIn {
-    uint32_t cb, pt, mt, ver, ident, tf, k1, k2;
-    Addr<V6> sa, da;
-    Addr<V6> tda, psa, pda;
-    uint32_t tpt, ppt, lfl, lbw, slv, svc, addr, sva;
-    bool svcop;
-};
-
-// stage st of a header, from its inputs; dsto: the owner word of the
-// destination endpoint's CT maps (the stages that are not the sender's)
-template <bool V6, bool LB>
-__device__ __forceinline__ Op<V6> decode_from(const CtaArgs &A, const ScanIn<V6> &r, int st,
-                                              uint32_t dsto)
-{
-    Op<V6> o;
-    o.kind = OP_NONE;
-    o.lbw = o.slave = o.slave_rel = 0;
-    o.reslave = o.kx = false;
-    if (LB && r.svcop) {
-        // lb4_local / lb6_local's ct_lookup4/6(CT_SERVICE): the tuple as
-        // loaded with TUPLE_F_SERVICE, one lookup (conntrack.h:580); a miss
-        // creates the entry (ct_create4/6 with ct_state {slave}, lb.h:699-
-        // 712).  The key sits in the k2 fields, which creates insert.
-        if (st != 0 || !(r.lfl & LBF_SVC))
-            return o;
-        o.proto = r.mt & 0xFF;
-        if (o.proto != 6 && o.proto != 17 && o.proto != icmp_proto<V6>())
-            return o;
-        o.dir = CT_SERVICE;   // (the tx side of the entry, as egress)
-        o.owner = A.ep_owner;
-        o.len = r.mt >> 16;
-        o.is_tcp = o.proto == 6;
-        o.syn = (r.mt & CFC_HF_TCP_CLOSE) != 0;
-        o.tfl = o.is_tcp ? r.tf : 0u;
-        o.action = ct_action(V6, o.proto, r.pt, r.mt);
-        o.sec = 0;
-        o.rev = 0;
-        const CtProbe k = ct_probe<V6>(o.proto, r.pt, CT_SERVICE, o.owner);
-        o.sa = r.da;
-        o.da = r.sa;
-        o.z1 = o.z2 = k.z1;
-        o.w1 = o.w2 = k.w1;
-        o.ki_form = o.proto == icmp_proto<V6>() && (k.w1 & 0x200u) && k.z1 == 0;
-        // the entry's slave: the selection, or ct_update4/6_slave's; its
-        // ICMP entry keeps the selection (slave0)
-        o.reslave = (r.lfl & LBR_RESLAVE) != 0;
-        o.slave = r.slv & 0xFFFF;
-        o.slave_rel = r.slv >> 16;
-        o.kind = r.svc != NONE ? OP_HIT : OP_CREATE;
-        return o;
-    }
-    const uint32_t cs = (r.cb >> (4 * st)) & 0xF;
-    if (!(cs & CFC_CT_DONE))
-        return o;
-    if (LB && (r.lfl & LBF_DROP))   // (no backend after all: no CT stage ran)
-        return o;
-    const int last = (r.cb & (CFC_CT_DONE << 4)) ? 1 : 0;
-    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
-    o.dir = eg ? CT_EGRESS : CT_INGRESS;
-    o.owner = eg ? A.ep_owner : dsto;
-    o.proto = r.mt & 0xFF;
-    if (o.proto != 6 && o.proto != 17 && o.proto != icmp_proto<V6>())
-        return o;
-    // the tuple this stage looked up: with a load balancer, the sender's
-    // (saddr, the service step's daddr and L4 word), then the packet as
-    // translated and reverse-NATed
-    Addr<V6> ka = r.sa, kb = r.da;
-    uint32_t pt = r.pt;
-    if (LB) {
-        ka = eg ? r.sa : r.psa;
-        kb = eg ? r.tda : r.pda;
-        pt = eg ? r.tpt : r.ppt;
-    }
-    o.len = r.mt >> 16;
-    o.is_tcp = o.proto == 6;
-    o.syn = (r.mt & CFC_HF_TCP_CLOSE) != 0;
-    o.tfl = o.is_tcp ? r.tf : 0u;
-    o.action = ct_action(V6, o.proto, pt, r.mt);
-    o.sec = A.mode == CFC_MODE_EGRESS ? A.ep_sec : r.ident;
-    // ipv6_policy's rev_nat_index: daddr.s6_addr32[3] as a u16
-    // (bpf_lxc.c:787-788); IPv4 creates outside a load balancer carry 0
-    if constexpr (V6)
-        o.rev = o.dir == CT_INGRESS ? (kb.w & 0xFFFF) : 0u;
-    else
-        o.rev = 0;
-    const bool svc = LB && eg && (r.lfl & LBF_SVC);
-    if (svc) {   // lb4_local / lb6_local's ct_state for the create
-        o.rev = r.lbw & 0xFFFF;
-        o.slave = o.slave_rel = r.slv & 0xFFFF;
-    }
-    o.lbw = V6 ? o.rev : (svc ? r.lbw : 0u);
-    const CtProbe k = ct_probe<V6>(o.proto, pt, (int)o.dir, o.owner);
-    o.sa = ka;
-    o.da = kb;
-    o.z1 = k.z1; o.w1 = k.w1;
-    o.z2 = k.z2; o.w2 = k.w2;
-    // a k2 of ICMP-error form is its own related entry (ct_create4/6 write
-    // the same key twice)
-    o.ki_form = o.proto == icmp_proto<V6>() && (k.w2 & 0x200u) && k.z2 == 0;
-    if constexpr (!V6) {
-        // ct_create4 with ct_state->addr: the entry again with daddr
-        // ct_state->addr (a looped-back flow's: TUPLE_F_IN, saddr svc_addr;
-        // conntrack.h:731-739)
-        if (svc && r.addr) {
-            const bool loop = (r.lbw >> 16) & 1;
-            o.kx = true;
-            o.kxa = r.addr;
-            o.kxs = loop ? r.sva : kb;
-            o.kxw = loop ? ct_word(o.proto, 1u, o.owner) : k.w2;
-        }
-    }
-    const uint32_t b = cs & CFC_CT_RES_MASK;
-    const bool dropped = st == last && (int32_t)r.ver == DROP_POLICY;
-    if (b >= 2)
-        o.kind = OP_HIT;
-    else if (b == 1)
-        o.kind = dropped ? OP_DELETE : OP_HIT;
-    else if (cs & CFC_CT_CREATE)
-        o.kind = OP_CREATE;
-    return o;
-}
-
-template <bool V6, bool LB>
-__device__ __forceinline__ void load_in(const CtaArgs &A, uint64_t i, ScanIn<V6> &r)
-{
-    r.svcop = LB && i >= A.n;
-    if (r.svcop)
-        i -= A.n;
-    r.cb = A.ctb[i];
-    r.sa = ld_addr<V6>(A.sa, i);
-    r.da = ld_addr<V6>(A.da, i);
-    r.pt = A.pt[i];
-    r.mt = A.mt[i];
-    r.ver = (uint32_t)A.ver[i];
-    r.ident = A.ident[i];
-    r.tf = A.tf ? A.tf[i] : 0u;
-    if constexpr (LB) {
-        const LbRecT<V6> &l = reinterpret_cast<const LbRecT<V6> *>(A.lbr)[i];
-        r.tda = l.tda;
-        r.psa = l.psa;
-        r.pda = l.pda;
-        r.tpt = l.tpt;
-        r.ppt = l.ppt;
-        r.lfl = l.fl;
-        r.lbw = l.lbw;
-        r.slv = l.slv;
-        r.svc = l.svc;
-        r.addr = l.addr;
-        r.sva = l.sva;
-    }
-}
-
-template <bool V6, bool LB>
-__device__ __forceinline__ Op<V6> decode_t(const CtaArgs &A, uint64_t i, int st)
-{
-    ScanIn<V6> r;
-    if (!LB || i < A.n) {
-        r.cb = A.ctb[i];
-        if (!((r.cb >> (4 * st)) & CFC_CT_DONE)) {
-            Op<V6> o;
-            o.kind = OP_NONE;
-            o.kx = false;
-            return o;
-        }
-    }
-    load_in<V6, LB>(A, i, r);
-    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
-    return decode_from<V6, LB>(A, r, st,
-                               (eg || r.svcop) ? 0u : dst_owner(A.T, LB ? r.pda : r.da));
-}
-// op (header i, stage st); i >= n: a CT_SERVICE op (A.lbr)
-template <bool V6>
-__device__ __forceinline__ Op<V6> decode(const CtaArgs &A, uint64_t i, int st)
-{
-    return A.lbr ? decode_t<V6, true>(A, i, st) : decode_t<V6, false>(A, i, st);
-}
-
-__device__ __forceinline__ uint32_t find(const CtaArgs &A, uint32_t x, uint32_t y, uint32_t z,
-                                         uint32_t w)
-{
-    const uint32_t mask = A.mask;
-    for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
-        const uint4 s = ld16(A.ct4 + i);
-        if (s.w == 0)
-            return NONE;
-        if (s.x == x && s.y == y && s.z == z && s.w == w)
-            return i;
-    }
-}
-__device__ __forceinline__ uint32_t find(const CtaArgs &A, uint4 d, uint4 s, uint32_t z,
-                                         uint32_t w)
-{
-    const uint32_t mask = A.mask;
-    for (uint32_t i = khash(d, s, z, w) & mask;; i = (i + 1) & mask) {
-        const uint4 t = ld16(&A.ct6[i].z);   // {z, w, 0, 0}: compared first
-        if (t.y == 0)
-            return NONE;
-        if (t.x == z && t.y == w && aeq(ld16(A.ct6[i].d), d) && aeq(ld16(A.ct6[i].s), s))
-            return i;
-    }
-}
-// a claimed slot's key words (everything but w)
-__device__ __forceinline__ void put_key(const CtaArgs &A, uint32_t i, uint32_t d, uint32_t s,
-                                        uint32_t z)
-{
-    A.ct4[i].x = d;
-    A.ct4[i].y = s;
-    A.ct4[i].z = z;
-}
-__device__ __forceinline__ void put_key(const CtaArgs &A, uint32_t i, uint4 d, uint4 s,
-                                        uint32_t z)
-{
-    *reinterpret_cast<uint4 *>(A.ct6[i].d) = d;
-    *reinterpret_cast<uint4 *>(A.ct6[i].s) = s;
-    A.ct6[i].z = z;
-}
-
-// The slot of a key no other thread of this launch inserts: found, or a
-// free one claimed (CAS on w: atomics are coherent across the XCDs) and
-// filled.  No agent-scope fence between the key words and w: that is an L2
-// write-back and invalidate per insert (MI355X_MICROARCH.md), and nothing in
-// this launch needs it — the only thread that looks this key up is this one
-// (one thread per home slot), another thread's probe only needs to see the
-// slot taken (w != 0 once the CAS is done), and a reader on another XCD
-// that saw w ahead of the key words would see them as the zeros of the free
-// slot, which no CT key has (saddr and daddr are never both 0 on the path).
-// The launch's end writes the L2s back for the kernels after it.
-template <bool V6>
-__device__ uint32_t find_or_insert(const CtaArgs &A, Addr<V6> d, Addr<V6> s, uint32_t z,
-                                   uint32_t w, bool *fresh)
-{
-    const uint32_t f = find(A, d, s, z, w);
-    *fresh = f == NONE;
-    if (f != NONE)
-        return f;
-    const uint32_t mask = A.mask;
-    for (uint32_t i = khash(d, s, z, w) & mask;; i = (i + 1) & mask) {
-        uint32_t *pw = slot_w<V6>(A, i);
-        const uint32_t cur = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur != 0 && cur != CT_TOMBSTONE)
-            continue;
-        if (atomicCAS(pw, cur, CT_CLAIM) != cur)
-            continue;
-        put_key(A, i, d, s, z);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (store order)
-        __hip_atomic_store(pw, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return i;
-    }
-}
-
-__device__ __forceinline__ uint64_t pack(const CtaArgs &A, uint32_t slot, uint32_t order2)
-{
-    return ((uint64_t)slot << A.ob) | order2;
-}
 
 // ---- scan: ops, hit slots, ordered marks, create requests.  Four headers
 // per thread and step, each phase's loads for all four issued before any is
@@ -603,7 +60,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         s_nreq = 0;
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
-    uint32_t nhit = 0;
+    uint32_t nhit = 0, nfh = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
         ScanIn<V6> r[SCAN_U];
 #pragma unroll
@@ -669,6 +126,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         // summary bits
         uint32_t slot[SCAN_U][2], kind[SCAN_U][2], act[SCAN_U][2], home[SCAN_U][2];
         uint32_t sb[SCAN_U][2];
+        bool fh[SCAN_U][2];
         uint32_t ncr = 0;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
@@ -679,19 +137,29 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 act[u][st] = o.kind == OP_NONE ? 0u : o.action;
                 slot[u][st] = HS_NONE;
                 home[u][st] = 0;
+                fh[u][st] = false;
                 sb[u][st] = (o.kind == OP_HIT && o.action != 2)
                                 ? sum_bits(o.dir == CT_INGRESS, o.is_tcp, o.syn, o.tfl) : 0u;
                 if (o.kind == OP_HIT || o.kind == OP_DELETE) {
                     const uint32_t key = st ? r[u].k2 : r[u].k1;
+                    const bool rev = ((r[u].cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
                     uint32_t sl;
                     if (key != NONE) {   // the slot the classify launch hit
                         sl = (key >> 1) - A.acct_base;
                     } else {
-                        const bool rev = ((r[u].cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
                         sl = rev ? find(A, o.da, o.sa, o.z1, o.w1)
                                  : find(A, o.sa, o.da, o.z2, o.w2);
                     }
                     slot[u][st] = sl == NONE ? HS_NONE : sl;
+                    if (sl == NONE) {
+                        // a hit on an entry an earlier header of this batch
+                        // creates (ctorder.hip): a request, resolved after
+                        // the inserts and replayed in the fold
+                        fh[u][st] = true;
+                        home[u][st] = (rev ? khash(o.da, o.sa, o.z1, o.w1)
+                                           : khash(o.sa, o.da, o.z2, o.w2)) & A.mask;
+                        ncr++;
+                    }
                 } else if (o.kind == OP_CREATE) {
                     home[u][st] = khash(o.sa, o.da, o.z2, o.w2) & A.mask;
                     ncr++;
@@ -704,7 +172,8 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         for (int u = 0; u < SCAN_U; u++)
 #pragma unroll
             for (int st = 0; st < NST; st++)
-                cur[u][st] = (sb[u][st] && slot[u][st] != HS_NONE) ? A.ms[slot[u][st]].x : 0u;
+                cur[u][st] = (sb[u][st] && slot[u][st] != HS_NONE && !A.nt)
+                                 ? A.ms[slot[u][st]].x : 0u;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
             const uint64_t i = base + u * 256 + threadIdx.x;
@@ -714,7 +183,10 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 if (sl == HS_NONE)
                     continue;
                 nhit++;
-                if (sb[u][st]) {   // a plain hit: into the slot's summary
+                if (A.nt && kind[u][st] == OP_HIT) {
+                    // monitor lengths wanted: every hit replayed in order
+                    order_mark(A, sl, MARK_ORDERED);
+                } else if (sb[u][st]) {   // a plain hit: into the slot's summary
                     if ((cur[u][st] | sb[u][st]) != cur[u][st])
                         atomicOr(&A.ms[sl].x, sb[u][st]);
                 } else if (kind[u][st] == OP_DELETE) {
@@ -748,6 +220,11 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
             const uint64_t i = base + u * 256 + threadIdx.x;
 #pragma unroll
             for (int st = 0; st < NST; st++) {
+                if (fh[u][st]) {
+                    s_req[rq++] = pack(A, home[u][st], ord_of(i, st, SEC_FHIT));
+                    nfh++;
+                    continue;
+                }
                 if (kind[u][st] != OP_CREATE)
                     continue;
                 s_req[rq++] = pack(A, home[u][st], ord_of(i, st, SEC_OP));
@@ -759,6 +236,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
     }
     block_flush(s_req, &s_nreq, &A.cnt[CTA_NREQA], A.reqA, A.req_cap);
     block_add(&A.cnt[CTA_NHIT], nhit);
+    block_add(&A.cnt[CTA_NFHIT], nfh);
 }
 
 // ---- the service step of an egress batch with a load balancer.  The
@@ -1354,7 +832,7 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
             if (slot[u] == HS_NONE || !((bw[u] >> (slot[u] & 31)) & 1))
                 continue;
             const uint2 v = A.ms[slot[u]];
-            if ((v.x & (MARK_DEL | MARK_PUTC)) == MARK_DEL)
+            if ((v.x & (MARK_DEL | MARK_PUTC)) == MARK_DEL && !A.nt)
                 // a deleted entry: its first delete stands for all its ops
                 ordered[u] = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - v.y;
             else
@@ -1380,8 +858,8 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 struct St {
     uint32_t last_rx, last_tx, seen_rx, seen_tx, bits, lifetime;
 };
-__device__ __forceinline__ void upd(St &e, uint32_t now, uint32_t life, uint32_t dir,
-                                    uint32_t flags)
+__device__ __forceinline__ uint32_t upd(St &e, uint32_t now, uint32_t life, uint32_t dir,
+                                        uint32_t flags)
 {
     e.lifetime = now + life;
     uint32_t &acc = dir == CT_INGRESS ? e.seen_rx : e.seen_tx;
@@ -1390,10 +868,12 @@ __device__ __forceinline__ void upd(St &e, uint32_t now, uint32_t life, uint32_t
     if (last + CT_REPORT_INTERVAL < now || acc != seen) {
         last = now;
         acc = seen;
+        return 1;   // (ct_update_timeout is bool: TRACE_PAYLOAD_LEN becomes 1)
     }
+    return 0;
 }
-__device__ __forceinline__ void upd_timeout(St &e, uint32_t now, bool is_tcp, uint32_t dir,
-                                            bool syn, uint32_t flags)
+__device__ __forceinline__ uint32_t upd_timeout(St &e, uint32_t now, bool is_tcp, uint32_t dir,
+                                                bool syn, uint32_t flags)
 {
     uint32_t life = CT_LIFETIME_NONTCP;
     if (is_tcp) {
@@ -1401,24 +881,29 @@ __device__ __forceinline__ void upd_timeout(St &e, uint32_t now, bool is_tcp, ui
             e.bits |= SEEN_NON_SYN;
         life = (e.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
     }
-    upd(e, now, life, dir, flags);
+    return upd(e, now, life, dir, flags);
 }
+// returns *monitor as __ct_lookup leaves it (0; 1: ct_update_timeout's bool;
+// TRACE_PAYLOAD_LEN for ACTION_CLOSE)
 template <bool V6>
-__device__ __forceinline__ void hit(St &e, uint32_t now, const Op<V6> &o)
+__device__ __forceinline__ uint32_t hit(St &e, uint32_t now, const Op<V6> &o)
 {
     auto alive = [&] { return !(e.bits & RX_CLOSING) || !(e.bits & TX_CLOSING); };
+    uint32_t m = 0;
     if (alive())
-        upd_timeout(e, now, o.is_tcp, o.dir, o.syn, o.tfl);
+        m = upd_timeout(e, now, o.is_tcp, o.dir, o.syn, o.tfl);
     if (o.action == 1) {
         if (e.bits & (RX_CLOSING | TX_CLOSING)) {
             e.bits &= ~(RX_CLOSING | TX_CLOSING);
-            upd_timeout(e, now, o.is_tcp, o.dir, o.syn, o.tfl);
+            m = upd_timeout(e, now, o.is_tcp, o.dir, o.syn, o.tfl);
         }
     } else if (o.action == 2) {
         e.bits |= o.dir == CT_INGRESS ? RX_CLOSING : TX_CLOSING;
+        m = TRACE_PAYLOAD_LEN;
         if (!alive())
             upd(e, now, CT_CLOSE_TIMEOUT, o.dir, o.tfl);
     }
+    return m;
 }
 // ct_create4/6's entry (seen_flags.syn = is_tcp: seen_non_syn stays clear)
 __device__ __forceinline__ St fresh(uint32_t now, bool is_tcp, uint32_t dir)
@@ -1492,6 +977,14 @@ __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx
     keep[r] = k;
 }
 
+// the monitor length of op `ord` (a header's own stage, not a CT_SERVICE op)
+__device__ __forceinline__ void put_mon(const CtaArgs &A, uint32_t ord, uint32_t m)
+{
+    const uint64_t i = ord_hdr(ord);
+    if (A.mon && i < A.n)
+        A.mon[2 * i + ord_st(ord)] = m == 0 ? 0 : m == 1 ? 1 : 2;
+}
+
 // ---- fold: one thread per slot of the sorted ordered list
 template <bool V6, bool LB>
 __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
@@ -1538,13 +1031,17 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
             lby = wr == SEC_REL ? o.slave_rel : o.slave;
         } else if (wr == SEC_FHIT) {   // a hit the classify launch could not count
             if (live) {
-                hit(e, A.now, o);
+                put_mon(A, ord, hit(e, A.now, o));
                 acct[d] += 1;
                 acct[d + 1] += o.len;
+                if (o.kind == OP_DELETE) {   // (an entry this batch created)
+                    live = false;
+                    deleted = true;
+                }
             }
         } else if (o.kind == OP_CREATE) {
             if (live) {   // created earlier in this batch: a counted hit
-                hit(e, A.now, o);
+                put_mon(A, ord, hit(e, A.now, o));
                 acct[d] += 1;
                 acct[d + 1] += o.len;
                 if (o.reslave) {   // ct_update4/6_slave
@@ -1565,7 +1062,7 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
                 lby = o.slave;
             }
         } else if (live) {   // OP_HIT, OP_DELETE
-            hit(e, A.now, o);
+            put_mon(A, ord, hit(e, A.now, o));
             if (o.kind == OP_DELETE) {
                 live = false;
                 deleted = true;
@@ -1679,6 +1176,39 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             A.info[s].y |= CTI_UPDATED;
         }
     }
+}
+
+// ---- the trace words' CT result and monitor length in packet order (a
+// batch whose caller wants the event words): the stage the trace reports
+// (local delivery's when it ran) with the result the packet order gave it
+// (ctorder.hip) and the length __ct_lookup then left (the fold's; a repeat
+// of the same hit that the fold skipped reports nothing: its state update
+// already happened), conn_is_dns's MTU (conntrack.h:585-586)
+template <bool V6>
+__global__ __launch_bounds__(256) void k_cta_mon(CtaArgs A)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n)
+        return;
+    const uint32_t w = A.nt[i];
+    if (((w >> 16) & 0xF) < CFC_NT_TRACE)
+        return;
+    const uint32_t cb = A.ctb[i];
+    const int st = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    const uint32_t cs = (cb >> (4 * st)) & 0xF;
+    if (!(cs & CFC_CT_DONE))
+        return;
+    const uint32_t res = cs & CFC_CT_RES_MASK;
+    uint32_t m = TRACE_PAYLOAD_LEN;
+    if (res != CT_NEW) {
+        const uint8_t c = A.mon[2 * i + st];
+        m = c == 1 ? 1u : c == 2 ? TRACE_PAYLOAD_LEN : 0u;
+    }
+    const uint32_t proto = A.mt[i] & 0xFF;
+    const CtProbe k = ct_probe<V6>(proto, A.pt[i], CT_INGRESS, 0);
+    if ((res >= CT_REPLY ? k.td : k.ts) == 0x3500u)   // conn_is_dns: htons(53)
+        m = MTU_LEN;
+    A.nt[i] = (w & 0x000FFFFFu) | res << 20 | mon_class(m) << 22;
 }
 
 // ---- host synchronisation: the changed slots, compacted
@@ -2113,6 +1643,8 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     // than the sequential ones they save)
     hipLaunchKernelGGL(k_cta_finish<V6>, dim3(blocks_for((uint64_t)A.mask + 1, 8192)),
                        dim3(256), 0, s, A);
+    if (A.nt && A.mon && A.n)
+        hipLaunchKernelGGL(k_cta_mon<V6>, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

@@ -44,12 +44,16 @@ __device__ __forceinline__ uint32_t notify_word(int mode, int ver,
 // 5 drops traces of flows inside their report interval, trace.h:131-132)
 constexpr uint32_t OBS_TO_LXC = 0, OBS_TO_PROXY = 1, OBS_TO_HOST = 2, OBS_TO_STACK = 3;
 constexpr uint32_t TRACE_PAYLOAD_LEN = 128, MTU_LEN = 1500;
+// mon 0 (not sent) keeps the site with length class 0: cfc_ct_apply
+// re-decides the length in packet order (ctapply.hip k_cta_mon)
+__device__ __forceinline__ uint32_t mon_class(uint32_t mon)
+{
+    return mon == 0 ? 0u : mon == MTU_LEN ? 2u : mon == 1u ? 3u : 1u;
+}
 __device__ __forceinline__ uint32_t trace_word(uint32_t obs, uint32_t source,
                                                uint32_t reason, uint32_t mon)
 {
-    return mon ? ((CFC_NT_TRACE + obs) << 16 | source | reason << 20 |
-                  (mon == MTU_LEN ? 2u : mon == 1u ? 3u : 1u) << 22)
-               : 0u;
+    return (CFC_NT_TRACE + obs) << 16 | source | reason << 20 | mon_class(mon) << 22;
 }
 
 // workspace: entry indices [n] (egress: a second array at ctr_stride(n)),

@@ -55,8 +55,9 @@ __device__ __forceinline__ uint32_t flow_hash(const NotifyArgs &a, uint64_t i)
 // the events a call records: drops (kinds 1-3), and traces when asked
 __device__ __forceinline__ bool nt_selected(uint32_t w, int traces)
 {
+    // (a trace whose monitor length is 0 is not sent: trace.h:119-132)
     const uint32_t kind = (w >> 16) & 0xF;
-    return w != 0 && (kind < CFC_NT_TRACE || traces);
+    return w != 0 && (kind < CFC_NT_TRACE || (traces && ((w >> 22) & 3) != 0));
 }
 
 __global__ __launch_bounds__(NT_THREADS) void k_nt_count(const uint32_t *notify,

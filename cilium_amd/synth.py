@@ -935,6 +935,69 @@ def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1,
     return take(h, perm)
 
 
+def headers_c5_seq(t: Tables, flows: Headers, n, seed=5, new_frac=0.08, s=1.1):
+    """C5 stream with the intra-batch conntrack dependencies a real batch
+    holds (the reference applies each packet's CT writes before the next
+    packet's lookup, conntrack.h:221-285, 615-772): 92% Zipf(s) packets of
+    live flows (ACK / PSH-ACK, 2% FIN or RST; flows the policy now denies
+    lose their entry to their first packet, bpf_lxc.c:963-970, and find
+    none after), and new flows with several packets in order — SYN, then
+    ACK and data, an ICMP error about a UDP flow, a FIN or RST, a packet
+    after the close."""
+    rng = np.random.default_rng(seed + 919)
+    m = int(n * (1 - new_frac))
+    old = take(flows, _zipf_ranks(rng, len(flows), m, s))
+    old.length = rng.integers(60, 1501, size=m).astype(np.uint16)
+    tf = rng.choice(np.array([0x10, 0x18], np.uint8), size=m)
+    close = rng.random(m) < 0.02
+    tf[close] = rng.choice(np.array([0x11, 0x04], np.uint8), size=int(close.sum()))
+    old.flags[close] |= np.uint8(HF_TCP_CLOSE)
+    old.tcpflags = np.where(old.proto == IPPROTO_TCP, tf, 0).astype(np.uint8)
+    parts, pos = [old], [rng.random(m)]
+    k = max(1, (n - m) // 3)
+    base = gen_headers_v4(rng, k, t.ipcache, local_v4_addrs(t)[:1], local_frac=1.0,
+                          mark_host=0, mark_proxy=0, other_proto=0, frag=0)
+    # most new flows from identities the endpoint's policy admits on L3
+    pol = t.policy[EP_LXC_ID]
+    l3 = pol["identity"][(pol["dport"] == 0) & (pol["proto"] == 0) & (pol["egress"] == 0)]
+    okp = np.flatnonzero(np.isin(t.ipcache["label"], l3) & (t.ipcache["family"] == 1))
+    if len(okp):
+        sel = np.flatnonzero(rng.random(k) < 0.8)
+        base.saddr[sel] = _addr_in_prefix_v4(rng, t.ipcache, okp[rng.integers(0, len(okp),
+                                                                              size=len(sel))])
+    ic = base.proto == IPPROTO_ICMP
+    base.sport[ic] = 8            # echo request
+    base.dport[ic] = 0
+    base.flags[:] = 0
+    at = rng.random(k) * 0.9
+    script = [(1.0, 0x02, False, False), (0.8, 0x10, False, False), (0.5, 0x18, False, False),
+              (0.3, 0, False, True), (0.2, 0x11, True, False), (0.1, 0x10, False, False)]
+    left = n - m
+    for p_, f, cl, err in script:
+        sel = np.flatnonzero(rng.random(k) < p_)
+        if err:   # an ICMP error about a UDP flow (destination unreachable)
+            sel = sel[base.proto[sel] == IPPROTO_UDP]
+        sel = sel[:left]
+        left -= len(sel)
+        h = take(base, sel)
+        h.length = rng.integers(60, 1501, size=len(h)).astype(np.uint16)
+        if err:
+            h.proto[:] = IPPROTO_ICMP
+            h.sport[:] = 3
+            h.dport[:] = 0
+            h.tcpflags = np.zeros(len(h), np.uint8)
+        else:
+            h.tcpflags = np.where(h.proto == IPPROTO_TCP, f, 0).astype(np.uint8)
+            if cl:
+                h.flags[h.proto == IPPROTO_TCP] |= np.uint8(HF_TCP_CLOSE)
+        parts.append(h)
+        pos.append(at[sel])
+        at = at + rng.random(k) * 0.01
+    h = concat(parts)
+    h = take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    return h.slice(0, n)
+
+
 # ------------------------------------------------------------ C1
 C1_POLICIES = "tests/golden/c1_policies.json"
 C1_PORTS = np.array([80, 443, 53, 8080], dtype=np.uint32)

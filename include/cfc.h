@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 9
+#define CFC_ABI_VERSION 10
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -296,11 +296,15 @@ typedef struct {
  *                             20-21 and the monitor length in bits 22-23
  *                             (1 TRACE_PAYLOAD_LEN, 2 MTU, 3 one byte: an
  *                             active flow's periodic report, ct_update_timeout
- *                             returns bool, conntrack.h:191).
- *            No event: forwarded packets the reference does not trace (to
- *            the stack from bpf_netdev; FROM_* points and flows inside their
- *            report interval under MONITOR_AGGREGATION 5), XDP prefilter
- *            drops (bpf_xdp.c notifies nothing), punts.
+ *                             returns bool, conntrack.h:191; 0: not sent — a
+ *                             flow inside its report interval under
+ *                             MONITOR_AGGREGATION 5, trace.h:119-132; the
+ *                             site stays in the word so cfc_ct_apply can
+ *                             re-decide the length in packet order).
+ *            No event: a 0 word — forwarded packets the reference does not
+ *            trace (to the stack from bpf_netdev; FROM_* points), XDP
+ *            prefilter drops (bpf_xdp.c notifies nothing), punts — or a trace
+ *            word of length class 0.
  *            cfc_drop_notify_v4/v6 turn the drops into records,
  *            cfc_monitor_events_v4/v6 every event. */
 #define CFC_NT_NETDEV 1u
@@ -571,6 +575,12 @@ typedef struct {
     uint32_t ct6_entries;
     uint32_t ct_apply_device;   /* cfc_ct_apply_* calls run on the device */
     uint32_t ct_apply_host;     /* ... and on the host */
+    /* CT stages whose result the packet order changed from the batch-start
+     * lookup (cfc_ct_apply: a later packet of a flow the batch created,
+     * a packet after a delete), since the context opened */
+    uint32_t ct_order_changed;
+    /* CT slots of the device tables (both families) */
+    uint32_t ct_slots;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

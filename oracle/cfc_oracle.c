@@ -814,10 +814,9 @@ enum { OBS_TO_LXC = 0, OBS_TO_PROXY = 1, OBS_TO_HOST = 2, OBS_TO_STACK = 3 };
 
 static uint32_t trace_word(uint32_t obs, uint16_t source, int reason, uint32_t mon)
 {
-    if (!mon)
-        return 0;
+    /* (monitor length 0, not sent: class 0 — the site stays in the word) */
     return (NT_TRACE + obs) << 16 | source | (uint32_t)reason << 20 |
-           (mon == MTU ? 2u : mon == 1 ? 3u : 1u) << 22;
+           (mon == 0 ? 0u : mon == MTU ? 2u : mon == 1 ? 3u : 1u) << 22;
 }
 
 /* sites 1-2 follow from the mode; lxc_ingress sets site 3 itself */

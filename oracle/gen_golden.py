@@ -914,24 +914,17 @@ def _ct_tables(seed, family):
     return t, rng
 
 
-def _ct_scenario(family, mode, seed, n=6000):
-    """Conntrack (SURVEY.md §8a a8-a10, a15): CT state made by the reference
-    itself from a history stream, then a test stream of established
-    packets, replies, ICMP errors related to known flows, FIN/RST on known
-    flows, new flows, and established flows that a policy change now denies
-    (ct_delete).  Intra-batch CT hazards are removed with the oracle's
-    sequential check so the batch engine and the per-packet reference see
-    the same CT state for every header."""
-    import oracle as O
+def _ct_history(family, seed):
+    """Tables, and the CT state the reference itself made from a history
+    stream: flows into both endpoints, flows out of EP_LXC_ID (some to the
+    other local endpoint), with extra L3 allow rules that are removed before
+    the test stream (a policy change: those flows become denied)."""
     t, rng = _ct_tables(seed, family)
     fam_ipc = t.ipcache[t.ipcache["family"] == (1 if family == 4 else 2)]
     gen = S.gen_headers_v4 if family == 4 else S.gen_headers_v6
     loc = S.local_v4_addrs(t) if family == 4 else S.local_v6_addrs(t)
     ep_addr = S.LXC_IPV4 if family == 4 else S.LXC_IPV6
     kw = dict(frag=0) if family == 4 else dict(ext=0, exthdr_drop=0)
-    # history: flows into both endpoints, flows out of EP_LXC_ID (some to
-    # the other local endpoint), with extra L3 allow rules that are removed
-    # before the test stream (a policy change: those flows become denied)
     h_in = gen(rng, 1500, fam_ipc, loc[:2], local_frac=1.0, mark_host=0,
                mark_proxy=0, other_proto=0, **kw)
     h_in.flags[:] &= np.uint8(0xFF ^ S.HF_TCP_CLOSE)
@@ -963,6 +956,22 @@ def _ct_scenario(family, mode, seed, n=6000):
         for r in pol[len(t.policy[lxc]):]:
             pm.delete(policy_key(r))
     dp.reset_counters()
+    return t, rng, dp, dict(fam_ipc=fam_ipc, gen=gen, loc=loc, ep_addr=ep_addr,
+                            kw=kw, h_in=h_in, h_out=h_out, dst=dst, extra=extra)
+
+
+def _ct_scenario(family, mode, seed, n=6000):
+    """Conntrack (SURVEY.md §8a a8-a10, a15): CT state made by the reference
+    itself from a history stream, then a test stream of established
+    packets, replies, ICMP errors related to known flows, FIN/RST on known
+    flows, new flows, and established flows that a policy change now denies
+    (ct_delete).  Intra-batch CT hazards are removed with the oracle's
+    sequential check so the batch engine and the per-packet reference see
+    the same CT state for every header (the ct_seq_* fixtures keep them)."""
+    import oracle as O
+    t, rng, dp, X = _ct_history(family, seed)
+    fam_ipc, gen, loc, ep_addr, kw = X["fam_ipc"], X["gen"], X["loc"], X["ep_addr"], X["kw"]
+    h_in, h_out, dst = X["h_in"], X["h_out"], X["dst"]
     # test stream
     icmp = S.IPPROTO_ICMP if family == 4 else S.IPPROTO_ICMPV6
     err = 3 if family == 4 else 1
@@ -1018,6 +1027,171 @@ def _ct_scenario(family, mode, seed, n=6000):
     assert not hz.any()
     h = h.slice(0, n)
     return t, h, mode, ep or None, dp
+
+
+def _ct_seq_scenario(family, mode, seed, n=7000):
+    """The tables and CT history of _ct_scenario, and a test stream that
+    keeps every intra-batch conntrack dependency (the reference applies each
+    packet's CT writes before the next packet's lookup, conntrack.h:221-285,
+    615-772; the reply override bpf_lxc.c:963-970, :538-545): new flows with
+    several packets (SYN, then ACK / data, FIN or RST, a packet after the
+    close), the replies of new flows between the two local endpoints and
+    ICMP errors related to them, runs of packets of established flows
+    (report aggregation, __ct_update_timeout), and several packets of
+    established flows the policy change now denies (ct_delete, then the
+    flow's later packets).  Nothing is removed: the reference runs the
+    stream packet by packet and the fixture is its result."""
+    t, rng, dp, X = _ct_history(family, seed)
+    fam_ipc, gen, loc, ep_addr, kw = X["fam_ipc"], X["gen"], X["loc"], X["ep_addr"], X["kw"]
+    h_in, h_out, dst = X["h_in"], X["h_out"], X["dst"]
+    icmp = S.IPPROTO_ICMP if family == 4 else S.IPPROTO_ICMPV6
+    err, echo = (3, 8) if family == 4 else (1, 128)
+    TCP = S.IPPROTO_TCP
+    parts, pos = [], []
+
+    def tcpf(h, f, close=False):
+        h.tcpflags = np.where(h.proto == TCP, np.asarray(f, np.uint8), 0).astype(np.uint8)
+        if close:
+            h.flags[h.proto == TCP] |= np.uint8(S.HF_TCP_CLOSE)
+        else:
+            h.flags[:] &= np.uint8(0xFF ^ S.HF_TCP_CLOSE)
+        return h
+
+    def steps(base, script):
+        """one flow per row of base; script: (probability, make(Headers) ->
+        Headers) per step, in order; every step after the one before"""
+        k = len(base)
+        at = rng.random(k) * 0.85
+        for p, make in script:
+            keep = rng.random(k) < p
+            h = make(S.take(base, np.flatnonzero(keep)))
+            h.length = rng.integers(60 if family == 4 else 100, 1500,
+                                    size=len(h)).astype(np.uint16)
+            parts.append(h)
+            pos.append(at[keep])
+            at = at + rng.random(k) * 0.03
+
+    def fix_icmp(h):   # a new ICMP flow opens with an echo request
+        ic = h.proto == icmp
+        h.sport[ic] = echo
+        h.dport[ic] = 0
+        return h
+
+    def icmp_err(h):   # an ICMP error travelling the other way, related to the flow
+        r = S.reverse(h)
+        r.proto[:] = icmp
+        r.sport[:] = err
+        r.dport[:] = 0
+        r.tcpflags = np.zeros(len(r), np.uint8)
+        return r
+    def icmp_same(h):  # an ICMP error the same way (e.g. a router's, about the flow)
+        r = S.take(h, np.arange(len(h)))
+        r.proto[:] = icmp
+        r.sport[:] = err
+        r.dport[:] = 0
+        r.tcpflags = np.zeros(len(r), np.uint8)
+        return r
+    copy = lambda x: S.take(x, np.arange(len(x)))   # noqa: E731
+    m = n // 7
+    if mode == MODE_INGRESS:   # replies: of the endpoint's own flows (history)
+        fwd, rep = h_in, h_out
+    else:
+        fwd = h_out
+        rep = S.take(h_in, (h_in.daddr == loc[0]).all(-1) if family == 6
+                     else h_in.daddr == loc[0])
+    # the identity each flow is checked with (ingress: its source's;
+    # egress: its destination's), and what the policy (after the change)
+    # admits on L3: most new flows are opened from / to those
+    o = __import__("oracle").Oracle(t)
+    ep0 = S.EP_LXC_ID if mode == MODE_EGRESS else 0
+    _, fv, _, fct = o.classify(fwd, mode, ep0, want_ct=True)
+    est_ok = ((fct & 7) == 5) & (fv >= 0)            # established, still allowed
+    denied = ((fct & 7) == 5) & (fv == -133)         # established, now denied
+    egr = 1 if mode == MODE_EGRESS else 0
+    allow = np.unique(np.concatenate([
+        pol["identity"][(pol["dport"] == 0) & (pol["proto"] == 0) & (pol["egress"] == egr)]
+        for lxc, pol in t.policy.items() if mode == MODE_INGRESS or lxc == S.EP_LXC_ID]))
+    okp = np.flatnonzero(np.isin(fam_ipc["label"], allow))
+    addr_in = S._addr_in_prefix_v4 if family == 4 else S._addr_in_prefix_v6
+
+    def allowed_peers(k):
+        return addr_in(rng, fam_ipc, okp[rng.integers(0, len(okp), size=k)])
+    # established flows: runs of packets, some closing, a packet after the close
+    live = np.flatnonzero(est_ok)
+    est = S.take(fwd, live[rng.integers(0, len(live), size=m)])
+    steps(est, [(1.0, lambda h: tcpf(h, rng.choice([0x10, 0x18], size=len(h)))),
+                (0.7, lambda h: tcpf(h, 0x18)),
+                (0.5, lambda h: tcpf(h, 0x10)),
+                (0.2, lambda h: tcpf(h, rng.choice([0x11, 0x04], size=len(h)), close=True)),
+                (0.15, lambda h: tcpf(h, 0x10))])
+    if len(rep):
+        r = S.reverse(S.take(rep, rng.integers(0, len(rep), size=m // 2)))
+        steps(r, [(1.0, lambda h: tcpf(h, 0x10)), (0.6, lambda h: tcpf(h, 0x18)),
+                  (0.3, lambda h: tcpf(h, 0x10))])
+        steps(S.take(rep, rng.integers(0, len(rep), size=m // 6)),
+              [(1.0, icmp_err)])
+    # new flows into the endpoints (ingress) / out of EP_LXC_ID (egress)
+    if mode == MODE_INGRESS:
+        d = gen(rng, m, fam_ipc, loc, local_frac=0.95, mark_host=0, mark_proxy=0,
+                other_proto=0, **kw)
+    else:
+        d = gen(rng, m, fam_ipc, loc, local_frac=0.3, mark_host=0, mark_proxy=0,
+                other_proto=0, src_fixed=ep_addr, **kw)
+        sel = rng.random(len(d)) < 0.7
+        d.daddr[sel] = dst[rng.integers(0, len(dst), size=int(sel.sum()))]
+    ok = rng.random(len(d)) < 0.8
+    if mode == MODE_INGRESS:
+        d.saddr[ok] = allowed_peers(int(ok.sum()))
+    else:
+        d.daddr[ok] = allowed_peers(int(ok.sum()))
+    d = fix_icmp(d)
+    steps(d, [(1.0, lambda h: tcpf(h, 0x02)), (0.8, lambda h: tcpf(h, 0x10)),
+              (0.3, icmp_same),
+              (0.5, lambda h: tcpf(h, 0x18)),
+              (0.25, lambda h: tcpf(h, rng.choice([0x11, 0x04], size=len(h)), close=True)),
+              (0.15, lambda h: tcpf(h, 0x10))])
+    # new flows between the two local endpoints: both directions pass a CT
+    # lookup (ingress: each end's policy program; egress: the sender's and,
+    # on local delivery, the destination's), so replies and related ICMP
+    # errors of a flow the stream itself opens are in the batch
+    k2 = m // 2
+    a = gen(rng, k2, fam_ipc, loc[:2], local_frac=1.0, mark_host=0, mark_proxy=0,
+            other_proto=0, **kw)
+    if mode == MODE_INGRESS:
+        if family == 4:
+            a.saddr[:] = np.where(a.daddr == loc[0], loc[1], loc[0])
+        else:
+            isl0 = (a.daddr == loc[0]).all(1)
+            a.saddr[:] = np.where(isl0[:, None], loc[1], loc[0])
+        script = [(1.0, lambda h: tcpf(h, 0x02)),
+                  (0.7, lambda h: tcpf(S.reverse(h), 0x12)),
+                  (0.3, icmp_err),
+                  (0.7, lambda h: tcpf(copy(h), 0x10)),
+                  (0.5, lambda h: tcpf(S.reverse(h), 0x18)),
+                  (0.2, lambda h: tcpf(copy(h), rng.choice([0x11, 0x04], size=len(h)),
+                                       close=True)),
+                  (0.2, lambda h: tcpf(S.reverse(h), 0x10))]
+    else:   # (the replies leave the other endpoint: not this program's)
+        a.saddr[:] = ep_addr
+        a.daddr[:] = loc[1] if len(loc) > 1 else loc[0]
+        script = [(1.0, lambda h: tcpf(h, 0x02)), (0.7, lambda h: tcpf(copy(h), 0x10)),
+                  (0.5, lambda h: tcpf(copy(h), 0x18)),
+                  (0.2, lambda h: tcpf(copy(h), rng.choice([0x11, 0x04], size=len(h)),
+                                       close=True)),
+                  (0.2, lambda h: tcpf(copy(h), 0x10))]
+    a = fix_icmp(a)
+    steps(a, script)
+    # established flows the policy change denies: their first packet deletes
+    # the entry (ct_delete), the later ones find none
+    den = np.flatnonzero(denied)
+    if len(den):
+        dn = S.take(fwd, den[rng.integers(0, len(den), size=m // 2)])
+        steps(dn, [(1.0, lambda h: tcpf(h, 0x10)), (0.8, lambda h: tcpf(h, 0x18)),
+                   (0.5, lambda h: tcpf(h, 0x10)), (0.3, lambda h: tcpf(h, 0x02))])
+    h = S.concat(parts)
+    h = S.take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    ep = S.EP_LXC_ID if mode == MODE_EGRESS else 0
+    return t, h.slice(0, n), mode, ep or None, dp
 
 
 # ------------------------------------------------------------ load balancing
@@ -1332,6 +1506,10 @@ SCENARIOS = {
     "ct_egress_v4": lambda: _ct_scenario(4, MODE_EGRESS, 22),
     "ct_ingress_v6": lambda: _ct_scenario(6, MODE_INGRESS, 23),
     "ct_egress_v6": lambda: _ct_scenario(6, MODE_EGRESS, 24),
+    "ct_seq_ingress_v4": lambda: _ct_seq_scenario(4, MODE_INGRESS, 25),
+    "ct_seq_egress_v4": lambda: _ct_seq_scenario(4, MODE_EGRESS, 26),
+    "ct_seq_ingress_v6": lambda: _ct_seq_scenario(6, MODE_INGRESS, 27),
+    "ct_seq_egress_v6": lambda: _ct_seq_scenario(6, MODE_EGRESS, 28),
     "lb_egress_v4": sc_lb_egress,
     "lb_reply_v4": sc_lb_reply,
     "lb_egress_v6": sc_lb_egress_v6,

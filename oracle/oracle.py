@@ -254,14 +254,31 @@ class Oracle:
         self.L.cfo_set_lb_io(self.h, _p(hs), _p(pkt))
 
     def classify(self, hdr, mode, ep_lxc=0, nthreads=1, want_lookups=False,
-                 want_ct=False, apply_ct=False, want_notify=False, want_pkt=False):
+                 want_ct=False, apply_ct=False, want_notify=False, want_pkt=False,
+                 seq=True):
         """-> (action, verdict, identity[, lookups][, ct][, notify][, pkt]).
         apply_ct folds the batch's CT creates/deletes into the oracle's CT
-        maps afterwards (what the engine's cfc_ct_apply does); notify is the
-        drop-notify site word per header (res_t.nt in cfc_oracle.c); pkt
-        the packet's (saddr, daddr, sport | dport << 16) after the service
-        translation and reverse NAT: (n, 3) u32 for IPv4, (n, 9) u32 for IPv6
-        (saddr and daddr as four raw words each)."""
+        maps — by default (seq) the reference's way, one header at a time
+        (run_sequential: what the engine's classify + cfc_ct_apply give);
+        seq=False: every header looked up against the maps as the batch found
+        them, the writes folded afterwards (the batch model whose differences
+        ct_apply(hazard=True) reports).  notify is the drop-notify site word
+        per header (res_t.nt in cfc_oracle.c); pkt the packet's (saddr,
+        daddr, sport | dport << 16) after the service translation and
+        reverse NAT: (n, 3) u32 for IPv4, (n, 9) u32 for IPv6 (saddr and
+        daddr as four raw words each)."""
+        if apply_ct and seq:
+            assert not want_lookups
+            r = self.run_sequential(hdr, mode, ep_lxc, want_ct=True, want_pkt=want_pkt)
+            act, ver, ide, words, ct = r[:5]
+            out = (act, ver, ide)
+            if want_ct:
+                out += (ct,)
+            if want_notify:
+                out += (words,)
+            if want_pkt:
+                out += (r[5],)
+            return out
         n = len(hdr)
         act = np.zeros(n, np.int32)
         ver = np.zeros(n, np.int32)
@@ -312,7 +329,9 @@ class Oracle:
         ifx[t.endpoints["lxc_id"].astype(np.int64)] = t.endpoints["ifindex"]
         words = np.asarray(words, np.uint32)
         kind = (words >> 16) & 0xF
-        sel = ((kind >= 1) & (kind <= 3) & drops) | ((kind >= 4) & traces)
+        # (a trace of monitor length 0 — class 0 — is not sent)
+        sel = ((kind >= 1) & (kind <= 3) & drops) | \
+            ((kind >= 4) & (((words >> 22) & 3) != 0) & traces)
         idx = np.flatnonzero(sel).astype(np.uint64)
         w = words[idx]
         k, lxc = (w >> 16) & 0xF, (w & 0xFFFF).astype(np.int64)

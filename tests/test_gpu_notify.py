@@ -200,9 +200,9 @@ def gpu_events(torch, t, h, mode, ep_lxc=0, clock=0, chunks=1):
     for a in range(0, max(n, 1), step):
         sub = b.slice(a, a + step)
         out = dp.classify(sub, mode, ep_lxc, want_notify=True, want_ct=use_ct)
-        rec, idx, total = dp.monitor_events(sub, out, mode, ep_lxc)
-        if use_ct:
+        if use_ct:   # (the apply settles the trace words in packet order)
             dp.ct_apply(sub, out, mode, ep_lxc)
+        rec, idx, total = dp.monitor_events(sub, out, mode, ep_lxc)
         torch.cuda.synchronize()
         words.append(out.notify.cpu().numpy().view(np.uint32))
         recs.append(np.ascontiguousarray(rec.cpu().numpy()).view(O.EVENT_DT).reshape(-1))
