@@ -597,6 +597,17 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
     c->cta_claims = 0;
     c->cta_ins = 0;
     c->ct_used_valid = false;
+    {   // the device's exact load: a GC's trim freed tombstones the mirror
+        // still holds as deleted (harmless for probes: a trimmed run ends
+        // its cluster), so the count is taken from the table itself
+        uint32_t nonfree = 0;
+        if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+            ct_count_nonfree4(ct4, slots, cnt, s) ||
+            hipMemcpyAsync(&nonfree, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        G.tomb4 = nonfree >= G.n_ct4 ? (uint32_t)(nonfree - G.n_ct4) : 0u;
+    }
     E.st.ct4_entries = G.n_ct4;
     if (int rc = ct_sync6(c, E, s))
         return rc;
@@ -3419,18 +3430,21 @@ int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, h
     cfc_ct_gc_stats st{};
     Epoch &E = *c->epoch;
     const bool dev4 = !E.ct->ct4_host.empty() && E.ct->ct4_info.p;
-    if (dev4)
-        if (int rc = ct_gc_dev(c, sel, *f, st, s))
-            return rc;
-    // what only the host holds: IPv6 maps (collected on the host, after
-    // their device applies are synchronised), IPv4 maps without a device
-    // table, IPv4 TCP maps' ICMP entries
+    // IPv6 maps are collected on the host, after their device applies are
+    // synchronised — before the device pass, whose pending-log entries the
+    // sync would otherwise replay into the host maps after the pass counted
+    // them (and the host loop below count them again)
     bool v6sel = false;
     for (Map *m : sel)
         v6sel |= m->role == ROLE_CT6 && !m->kv.empty();
     if (v6sel && c->ct6_dirty)
         if (int rc = ct_sync(c, s))
             return rc;
+    if (dev4)
+        if (int rc = ct_gc_dev(c, sel, *f, st, s))
+            return rc;
+    // what only the host holds: IPv6 maps, IPv4 maps without a device
+    // table, IPv4 TCP maps' ICMP entries
     const GcFilterHost H{*f};
     for (Map *m : sel) {
         const bool v6 = m->role == ROLE_CT6, all = v6 || !dev4;

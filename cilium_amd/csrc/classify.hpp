@@ -315,6 +315,10 @@ int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, 
 int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
                  CtSyncRec6 *out, uint32_t cap, uint32_t *cnt, hipStream_t s);
 int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
+// the IPv4 table's slots that are not free (live, tombstone or claimed),
+// added into *cnt (the exact load: the GC's trim frees tombstones the host
+// mirror still counts)
+int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStream_t s);
 int cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n, hipStream_t s);
 
 // ---- CT garbage collection (cfc_ct_gc): ctmap.GC's doFiltering

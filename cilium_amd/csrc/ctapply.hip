@@ -1317,6 +1317,26 @@ __global__ __launch_bounds__(256) void k_cta_tomb6(Ct6Slot *ct6, const CtSyncRec
         *reinterpret_cast<uint4 *>(&ct6[s].z) = make_uint4(0, CT_TOMBSTONE, 0, 0);
     }
 }
+// slots whose word is not 0, four per thread and step
+__global__ __launch_bounds__(256) void k_ct_nonfree4(const Ct4Slot *ct4, uint64_t slots,
+                                                     uint32_t *cnt)
+{
+    uint32_t c = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * 4; base < slots; base += stride) {
+        uint32_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t s = base + u * 256 + threadIdx.x;
+            w[u] = s < slots ? ct4[s].w : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            c += w[u] != 0;
+    }
+    block_add(cnt, c);
+}
+
 // ---- garbage collection (cfc_ct_gc, ctmap.go:303-325 doFiltering) ---------
 __device__ __forceinline__ bool gc_in_set(const uint32_t *set, uint32_t n, uint32_t a)
 {
@@ -1698,6 +1718,14 @@ int ct_gc_log(const CtGcArgs &A, const CtLog *in, uint32_t n, CtLog *out, hipStr
         return -EINVAL;
     if (n)
         hipLaunchKernelGGL(k_ct_gc_log, dim3((n + 255) / 256), dim3(256), 0, s, A, in, n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStream_t s)
+{
+    if (slots)
+        hipLaunchKernelGGL(k_ct_nonfree4, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4,
+                           slots, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

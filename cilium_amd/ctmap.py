@@ -37,10 +37,16 @@ class GCFilter:
 
 
 def GC(dp, fd: int, flt: GCFilter, now: int | None = None) -> int:
-    """ctmap.GC(m, filter): Time is taken from the datapath clock `now`
-    when RemoveExpired is set -> entries deleted (gcStats.deleted)."""
-    if flt.remove_expired and now is not None:
-        flt.time = int(now) & 0xFFFFFFFF
+    """ctmap.GC(m, filter): with RemoveExpired, Time is the datapath clock
+    (`now`, else the clock the datapath runs at: bpf.GetMtime) -> entries
+    deleted (gcStats.deleted)."""
+    if flt.remove_expired:
+        flt.time = int(dp.clock if now is None else now) & 0xFFFFFFFF
+    return _do_gc(dp, fd, flt)
+
+
+def _do_gc(dp, fd: int, flt: GCFilter) -> int:
+    """doGC with the filter as given (Flush: Time = MAX_TIME)"""
     st = dp.ct_gc(fd, flt.time, flt.remove_expired,
                   None if flt.valid_ips is None else [_ip_bytes(i) for i in flt.valid_ips],
                   None if flt.match_ips is None else [_ip_bytes(i) for i in flt.match_ips])
@@ -56,4 +62,4 @@ def gc_all(dp, now: int, valid_ips=None) -> int:
 
 def flush(dp, fd: int) -> int:
     """(*Map).Flush (ctmap.go:352-360): every entry goes."""
-    return GC(dp, fd, GCFilter(remove_expired=True, time=MAX_TIME))
+    return _do_gc(dp, fd, GCFilter(remove_expired=True, time=MAX_TIME))

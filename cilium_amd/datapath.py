@@ -432,6 +432,9 @@ class Datapath:
     def set_clock(self, now):
         """cfc_set_clock: bpf_ktime_get_sec() for the next calls."""
         L.check(self.L.cfc_set_clock(self.h, int(now) & 0xFFFFFFFF), "clock")
+        self.clock = int(now) & 0xFFFFFFFF
+
+    clock = 0   # the datapath clock as last set (cfc_set_clock; the library starts at 0)
 
     def ct_gc(self, fd=-1, time=0, remove_expired=True, valid_ips=None,
               match_ips=None, stream=None):

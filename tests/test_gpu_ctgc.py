@@ -101,24 +101,31 @@ def test_gc_expiry_and_ip_filters_vs_oracle(torch):
 
 def test_gc_steady_state_cycles(torch):
     """apply + GC cycles at the reference's cadence (a GC interval per
-    batch, the new flows of every batch different): the device path holds
-    (no host walk), the table does not grow, and the maps stay the
-    oracle's."""
+    batch, the new flows of every batch different), with a host sync
+    (counters, CT maps read) after every GC: the device path holds (no host
+    walk), the device table keeps its size (the sync takes the load from
+    the table itself, not from a mirror that still counts the tombstones
+    the GC's trim freed), and the maps stay the oracle's."""
     t, flows = S.config_c5(5, n_flows=60_000, n_prefixes=20_000, n_policy=2000, now=1000)
     dp = Datapath(0)
     load_tables(dp, t)
     o = O.Oracle(t)
-    now, sizes = 1000, []
+    now, sizes, slots = 1000, [], []
     for k in range(8):
         h = S.headers_c5(t, flows, 150_000, seed=20 + k)
         step(torch, dp, o, h, now)
         now += ctmap.GC_INTERVAL_DEFAULT + 1
+        dp.set_clock(now)
         f = ctmap.GCFilter(remove_expired=True)
-        ctmap.GC(dp, -1, f, now)
+        ctmap.GC(dp, -1, f)   # (Time: the datapath's clock)
+        assert f.time == now
         same_count(f.stats, o.ct_gc(time=now))
+        dp.counters_sync()
         sizes.append(len(o.ct_dump()))
+        slots.append(dp.stats()["ct_slots"])
     assert dp.stats()["ct_apply_host"] == 0
     assert max(sizes[2:]) < 1.3 * min(sizes[2:]), sizes
+    assert len(set(slots[1:])) == 1, slots
     same_ct(dp, o)
     dp.close()
 
