@@ -211,6 +211,7 @@ struct ctent {
 _Static_assert(sizeof(struct ctent) == 56, "ct_entry is 56 bytes");
 #define CTB_RX_CLOSING 1u
 #define CTB_TX_CLOSING 2u
+#define CTB_NAT46 4u
 #define CTB_LB_LOOPBACK 8u
 #define CTB_SEEN_NON_SYN 16u
 /* conntrack.h:31-35, common.h:224, node_config.h:69 */
@@ -395,8 +396,31 @@ struct cfo {
      * (saddr, daddr, L4 word), IPv6 9 (saddr[4], daddr[4], L4 word) */
     const uint32_t *hash_in;
     uint32_t *pkt_out;
+    /* each endpoint's own addresses (LXC_IPV4 / LXC_IP of its program,
+     * lxc_config.h:24-25): NAT64's saddr, NAT46's daddr */
+    uint32_t ep_v4[65536];
+    uint8_t ep_v6[65536][16];
+    uint8_t ep_has4[65536], ep_has6[65536];
+    /* per header of the last classify: the NAT46 / NAT64 hop it took (the
+     * CT stage of the other family, applied by ct_apply as stage 1) */
+    struct hop *hop;
+    size_t hop_cap;
 };
 #define ID_SLOTS 65537u
+
+/* A header's NAT hop (LXC_NAT46, nat46.h): NAT64 — an IPv6 egress packet
+ * to ::ffff:0:0/96 re-entering the IPv4 egress program translated
+ * (tail_ipv6_to_ipv4, bpf_lxc.c:1070-1083); NAT46 — an IPv4 packet whose CT
+ * entry says nat46 re-entering ipv6_policy translated (tail_ipv4_to_ipv6,
+ * :1098-1110).  The hop's CT stage is stage 1 of the CT byte. */
+#define HOP_NAT64 1
+#define HOP_NAT46 2
+struct hop {
+    uint8_t kind, alen, proto, dir;
+    uint16_t owner, sport, dport;
+    uint8_t sa[16], da[16];
+    int32_t dlen;   /* skb->len change: the IPv4 header is 20 bytes shorter */
+};
 
 static uint16_t ct_owner(const cfo_t *o, uint16_t lxc)
 {
@@ -483,6 +507,7 @@ void cfo_free(cfo_t *o)
             free(o->pol[i]);
         }
     free(o->eps);
+    free(o->hop);
     free(o);
 }
 
@@ -529,6 +554,15 @@ int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
     }
     o->eps[o->neps] = (epinfo){ifindex, flags, lxc_id};
     ht_put(&o->lxc, k, o->neps++);
+    if (!(flags & ENDPOINT_F_HOST)) {
+        if (family == 1 && !o->ep_has4[lxc_id]) {
+            memcpy(&o->ep_v4[lxc_id], addr, 4);
+            o->ep_has4[lxc_id] = 1;
+        } else if (family == 2 && !o->ep_has6[lxc_id]) {
+            memcpy(o->ep_v6[lxc_id], addr, 16);
+            o->ep_has6[lxc_id] = 1;
+        }
+    }
     return 0;
 }
 
@@ -801,6 +835,9 @@ typedef struct {
 #define NT_NETDEV 1u
 #define NT_EGRESS 2u
 #define NT_POLICY 3u
+/* bit 24: the event followed a NAT46 / NAT64 hop, its length is the
+ * translated packet's (IPv4 header 20 bytes shorter than IPv6) */
+#define NT_NATLEN 0x01000000u
 /* The monitor event of a header (cfc.h CFC_NT_*): bits 0-15 EVENT_SOURCE,
  * bits 16-19 the kind — drop sites 1-3 above, or a trace_notify at
  * observation point kind - 4 (TRACE_TO_LXC 4, TO_PROXY 5, TO_HOST 6,
@@ -839,7 +876,14 @@ static _Thread_local uint8_t tl_ct;
 /* the current header's TCP flag byte (byte 13) and the monitor length each
  * CT stage's lookup returned (0 / TRACE_PAYLOAD_LEN / MTU) */
 static _Thread_local uint8_t tl_tcpfl;
-static _Thread_local uint32_t tl_mon[2];
+static _Thread_local uint32_t tl_mon[3];
+/* skb->cb[CB_NAT46_STATE] (common.h:316-325): NAT46_CLEAR, NAT64 (set by
+ * tail_ipv6_to_ipv4), NAT46 (set by __ct_lookup on an entry with nat46);
+ * and the NAT hop the current header took */
+#define NAT64 1
+#define NAT46 2
+static _Thread_local int tl_nat;
+static _Thread_local struct hop tl_hop;
 
 /* __ct_update_timeout (conntrack.h:125-185): the lifetime, and whether this
  * packet is reported (the flow's report interval passed, or it carries TCP
@@ -908,6 +952,7 @@ typedef struct {
     uint16_t rev_nat, slave;
     int loopback;
     uint32_t addr, svc_addr;
+    int nat46;     /* ct_create4 under NAT64: entry.nat46 (conntrack.h:714-716) */
 } ctstate_t;
 static int ct_create_entries(const cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
                              uint32_t len, uint32_t src_sec_id, const ctstate_t *st,
@@ -975,6 +1020,13 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
     }
     if (hent)
         *hent = ent;
+    /* __ct_lookup (conntrack.h:241-244): an entry with nat46 asks for the
+     * NAT46 translation; ct_lookup6 clears the state after its forward
+     * lookup (:429-431) */
+    if (ent && (ent->bits & CTB_NAT46) && !tl_nat)
+        tl_nat = NAT46;
+    if (alen == 16 && *res < CT_REPLY)
+        tl_nat = 0;
     uint32_t mon = TRACE_PAYLOAD_LEN;
     if (ent) {
         struct ctent copy = *ent;
@@ -1261,6 +1313,114 @@ static void lb6_rev_nat(cfo_t *o, uint16_t index, uint8_t proto)
  * alen 16, ipv6_policy (:753-882) + tail_ipv6_policy (:884-895), which
  * differ only in the CT tuple and pass is_fragment = false.  stage is 0 for
  * an ingress batch, 1 after egress local delivery. */
+/* ---- NAT46 / NAT64 (LXC_NAT46: lxc_config.h:28 ENABLE_NAT46 with IPv4 and
+ * CONNTRACK, nat46.h:30-32).  Header ports of ICMP hold {type, code} in the
+ * sport word; the translations rewrite them. */
+#define DROP_INVALID -134
+#define DROP_INVALID_EXTHDR -156
+#define IPPROTO_ICMP 1
+#define IPPROTO_ICMPV6 58
+#define HF_EXTHDR 4
+#define DROP_UNKNOWN_ICMP_CODE -143
+#define DROP_UNKNOWN_ICMP_TYPE -144
+#define DROP_UNKNOWN_ICMP6_CODE -145
+#define DROP_UNKNOWN_ICMP6_TYPE -146
+/* NAT46_PREFIX (node_config.h:40): the translated source's first 96 bits */
+static const uint8_t nat46_prefix[12] = {0xbe, 0xef, 0, 0, 0, 0, 0, 0, 0, 0, 0x0a, 0};
+
+/* icmp4_to_icmp6 (nat46.h:60-141) on {type, code}.  Its callers use the
+ * return value as a checksum difference and never test it (nat46.h:303,
+ * :384): an "error" only leaves the ICMP header untranslated — no drop. */
+static int icmp4_to_icmp6(uint16_t *w)
+{
+    const uint8_t type = (uint8_t)(*w & 0xFF), code = (uint8_t)(*w >> 8);
+    uint8_t t6 = 0, c6 = 0;
+    switch (type) {
+    case 8: t6 = 128; break;                        /* ECHO -> ECHO_REQUEST */
+    case 0: t6 = 129; break;                        /* ECHOREPLY */
+    case 3:                                         /* DEST_UNREACH */
+        t6 = 1;
+        switch (code) {
+        case 0: case 1: c6 = 0; break;              /* NOROUTE */
+        case 2: t6 = 4; c6 = 1; break;              /* PARAMPROB / UNK_NEXTHDR */
+        case 3: c6 = 4; break;                      /* PORT_UNREACH */
+        case 4: t6 = 2; c6 = 0; break;              /* PKT_TOOBIG */
+        case 5: c6 = 0; break;
+        case 6: case 7: case 8: case 11: case 12: c6 = 0; break;
+        case 9: case 10: case 13: c6 = 1; break;    /* ADM_PROHIBITED */
+        default: return DROP_UNKNOWN_ICMP_CODE;
+        }
+        break;
+    case 11: t6 = 3; break;                         /* TIME_EXCEEDED (code 0) */
+    case 12: t6 = 4; break;                         /* PARAMETERPROB */
+    default: return DROP_UNKNOWN_ICMP_TYPE;
+    }
+    *w = (uint16_t)(t6 | c6 << 8);
+    return 0;
+}
+
+/* icmp6_to_icmp4 (nat46.h:143-220), fall-throughs included: a destination
+ * unreachable with a known code ends as ICMP_FRAG_NEEDED (no break after
+ * its inner switch), a parameter problem always as an unknown type */
+static int icmp6_to_icmp4(uint16_t *w)
+{
+    const uint8_t type = (uint8_t)(*w & 0xFF), code = (uint8_t)(*w >> 8);
+    uint8_t t4 = 0, c4 = 0;
+    switch (type) {
+    case 128: t4 = 8; break;
+    case 129: t4 = 0; break;
+    case 1:
+        if (code != 0 && code != 2 && code != 3 && code != 1 && code != 4)
+            return DROP_UNKNOWN_ICMP6_CODE;
+        /* fall through */
+    case 2: t4 = 3; c4 = 4; break;                  /* DEST_UNREACH / FRAG_NEEDED */
+    case 3: t4 = 11; c4 = code; break;              /* TIME_EXCEED */
+    case 4:
+        if (code != 0 && code != 1)
+            return DROP_UNKNOWN_ICMP6_CODE;
+        return DROP_UNKNOWN_ICMP6_TYPE;
+    default:
+        return DROP_UNKNOWN_ICMP6_TYPE;
+    }
+    *w = (uint16_t)(t4 | c4 << 8);
+    return 0;
+}
+
+static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
+                         const uint8_t *sa, const uint8_t *da, uint8_t proto,
+                         uint16_t sport, uint16_t dport, int frag, int close,
+                         uint32_t len, int skip_proxy, int dir_missed,
+                         int stage);
+
+/* ipv4_policy's NAT46 tail call (bpf_lxc.c:939-944): tail_ipv4_to_ipv6
+ * (:1098-1110) — ipv4_to_ipv6 (nat46.h:236-328): saddr NAT46_PREFIX/96 +
+ * the IPv4 source, daddr the endpoint's LXC_IP, ICMP as ICMPv6 — then
+ * tail_ipv6_policy on the translated packet with the source identity of
+ * the IPv4 path (cb[CB_SRC_LABEL]); its CT lookup is stage 1 */
+static res_t nat46_ingress(cfo_t *o, const epinfo *ep, uint32_t src, uint32_t sa4,
+                           uint8_t proto, uint16_t sport, uint16_t dport, int close,
+                           uint32_t len, int skip_proxy)
+{
+    uint16_t sp = sport;
+    const uint8_t p6 = proto == IPPROTO_ICMP ? IPPROTO_ICMPV6 : proto;
+    if (proto == IPPROTO_ICMP)   /* (unchecked: see icmp4_to_icmp6) */
+        (void)icmp4_to_icmp6(&sp);
+    uint8_t sa6[16], da6[16];
+    memcpy(sa6, nat46_prefix, 12);
+    memcpy(sa6 + 12, &sa4, 4);
+    memcpy(da6, o->ep_v6[ep->lxc_id], 16);
+    tl_hop = (struct hop){HOP_NAT46, 16, p6, CT_INGRESS, ct_owner(o, ep->lxc_id), sp, dport,
+                          {0}, {0}, 20};
+    memcpy(tl_hop.sa, sa6, 16);
+    memcpy(tl_hop.da, da6, 16);
+    memcpy(tl_pkt6.sa, sa6, 16);
+    memcpy(tl_pkt6.da, da6, 16);
+    tl_pkt6.sport = sp;
+    tl_pkt6.dport = dport;
+    return lxc_ingress(o, ep, src, 16, sa6, da6, p6, sp, dport, 0, close, len + 20,
+                       skip_proxy, METRIC_INGRESS, 1);
+}
+
 static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
                          const uint8_t *sa, const uint8_t *da, uint8_t proto,
                          uint16_t sport, uint16_t dport, int frag, int close,
@@ -1298,6 +1458,11 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
         r.nt = NT_POLICY << 16 | ep->lxc_id;
         metric(o, ret, METRIC_INGRESS, len);
         return r;
+    }
+    if (alen == 4 && tl_nat == NAT46 && o->ep_has6[ep->lxc_id]) {
+        uint32_t sa4;
+        memcpy(&sa4, sa, 4);
+        return nat46_ingress(o, ep, src, sa4, proto, sport, dport, close, len, skip_proxy);
     }
     /* (:808-815) any hit whose entry carries a rev_nat_index: the packet's
      * source from cilium_lb6_reverse_nat, when it holds the index */
@@ -1378,7 +1543,7 @@ static res_t netdev_ingress_v4(cfo_t *o, uint32_t saddr, uint32_t daddr,
 /* handle_ipv4_from_lxc (bpf_lxc.c:440-692) for endpoint lxc */
 static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
                            uint32_t daddr, uint8_t proto, uint16_t sport,
-                           uint16_t dport, uint8_t hflags, uint32_t len)
+                           uint16_t dport, uint8_t hflags, uint32_t len, int st0)
 {
     (void)sport;
     (void)dport;   /* the packet's ports are tl_pkt's */
@@ -1404,7 +1569,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     const struct ctent *hit;
     uint8_t k2[CTK];
     int ret = ct_lookup(o, 4, ct_owner(o, lxc), sa, da, proto, tl_pkt.sport,
-                        tl_pkt.dport, hflags & HF_TCP_CLOSE, CT_EGRESS, 0, &res,
+                        tl_pkt.dport, hflags & HF_TCP_CLOSE, CT_EGRESS, st0, &res,
                         &pdport, &hit, k2);
     if (ret < 0) {
         r.verdict = ret;
@@ -1429,10 +1594,11 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         return r;
     }
     if (res == CT_NEW) {                            /* ct_create4, :547-559 */
-        tl_ct |= CTO_CREATE1;
-        ctstate_t cs = {0, 0, 0, 0, 0};
+        tl_ct |= (uint8_t)(CTO_CREATE1 << (4 * st0));
+        ctstate_t cs = {0, 0, 0, 0, 0, 0};
         if (x.svc)
-            cs = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr, x.svc_addr};
+            cs = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr, x.svc_addr, 0};
+        cs.nat46 = tl_nat == NAT64;
         tl_fresh.n = ct_create_entries(o, k2, 4, CT_EGRESS, len, o->seclabel[lxc], &cs,
                                        tl_fresh.key, tl_fresh.ent);
     } else if (res >= CT_REPLY && hit->rev_nat_index) {
@@ -1441,7 +1607,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
     if (verdict > 0) { /* proxy: redirect(HOST_IFINDEX), TRACE_TO_PROXY */
         r.action = TC_ACT_REDIRECT;
         r.verdict = verdict;
-        r.nt = trace_word(OBS_TO_PROXY, lxc, res, tl_mon[0]);
+        r.nt = trace_word(OBS_TO_PROXY, lxc, res, tl_mon[st0]);
         return r;
     }
     /* delivery by the packet's destination (lookup_ip4_endpoint, :617) */
@@ -1452,7 +1618,7 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
         if (ep->flags & ENDPOINT_F_HOST) { /* to_host: TRACE_TO_HOST, :668 */
             metric(o, 0, METRIC_EGRESS, len);
             r.action = TC_ACT_REDIRECT;
-            r.nt = trace_word(OBS_TO_HOST, lxc, res, tl_mon[0]);
+            r.nt = trace_word(OBS_TO_HOST, lxc, res, tl_mon[st0]);
             return r;
         }
         /* ipv4_local_delivery (l3.h:103-131): egress forward metric, then
@@ -1460,17 +1626,51 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
          * packet as it now is */
         metric(o, 0, METRIC_EGRESS, len);
         const uint32_t psa = tl_pkt.sa, pd = tl_pkt.da;
+        /* (after a NAT64 hop the destination's lookup would be a third CT
+         * stage: its writes are not carried) */
         res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 4, (const uint8_t *)&psa,
                               (const uint8_t *)&pd, proto, tl_pkt.sport,
                               tl_pkt.dport, hflags & HF_FRAG, hflags & HF_TCP_CLOSE,
-                              len, 0, METRIC_EGRESS, 1);
+                              len, 0, METRIC_EGRESS, st0 + 1);
         d.identity = dst;
         return d;
     }
     metric(o, 0, METRIC_EGRESS, len); /* pass_to_stack: TRACE_TO_STACK */
     r.action = TC_ACT_OK;
-    r.nt = trace_word(OBS_TO_STACK, lxc, res, tl_mon[0]);   /* :687 */
+    r.nt = trace_word(OBS_TO_STACK, lxc, res, tl_mon[st0]);   /* :687 */
     return r;
+}
+
+/* ipv6_l3_from_lxc's NAT64 tail call (bpf_lxc.c:353-360, a destination
+ * outside the cluster in ::ffff:0:0/96, ipv6.h:279-282): tail_ipv6_to_ipv4
+ * (:1070-1083) — ipv6_to_ipv4 (nat46.h:336-420): saddr the endpoint's
+ * LXC_IPV4, daddr the last 32 bits, ICMPv6 as ICMP, extension headers
+ * dropped — then handle_ipv4_from_lxc with cb[CB_NAT46_STATE] = NAT64 (its
+ * creates carry nat46); its CT lookup is stage 1 */
+static res_t nat64_egress(cfo_t *o, uint16_t lxc, const uint8_t *da6, uint8_t proto,
+                          uint8_t flags, uint32_t len)
+{
+    res_t r = {TC_ACT_SHOT, 0, 0, 0};
+    uint16_t sp = tl_pkt6.sport;
+    const uint16_t dp = tl_pkt6.dport;
+    const uint8_t p4 = proto == IPPROTO_ICMPV6 ? IPPROTO_ICMP : proto;
+    const int ret = (flags & HF_EXTHDR) ? DROP_INVALID_EXTHDR : 0;
+    if (ret || !o->ep_has4[lxc]) {   /* send_drop_notify(skb, SECLABEL, 0, ..) */
+        r.verdict = ret ? ret : DROP_INVALID;
+        metric(o, r.verdict, METRIC_EGRESS, len);
+        return r;
+    }
+    if (proto == IPPROTO_ICMPV6)   /* (unchecked: see icmp4_to_icmp6) */
+        (void)icmp6_to_icmp4(&sp);
+    const uint32_t sa4 = o->ep_v4[lxc];
+    uint32_t da4;
+    memcpy(&da4, da6 + 12, 4);
+    tl_nat = NAT64;
+    tl_hop = (struct hop){HOP_NAT64, 4, p4, CT_EGRESS, ct_owner(o, lxc), sp, dp, {0}, {0}, -20};
+    memcpy(tl_hop.sa, &sa4, 4);
+    memcpy(tl_hop.da, &da4, 4);
+    tl_pkt = (pkt4_t){sa4, da4, sp, dp};
+    return lxc_egress_v4(o, lxc, sa4, da4, p4, sp, dp, flags, len - 20, 1);
 }
 
 /* check_v4 (bpf_xdp.c:97-121) */
@@ -1495,6 +1695,16 @@ static int xdp_v4(cfo_t *o, uint32_t saddr, uint32_t daddr)
     return lxc_lookup(o, 1, (const uint8_t *)&daddr) ? XDP_PASS : XDP_DROP;
 }
 
+/* the per-header NAT hop records of a classify of n headers */
+static void hop_reserve(cfo_t *o, size_t n)
+{
+    if (n > o->hop_cap) {
+        free(o->hop);
+        o->hop_cap = n;
+        o->hop = calloc(n, sizeof(struct hop));
+    }
+}
+
 void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      const uint32_t *saddr, const uint32_t *daddr,
                      const uint16_t *sport, const uint16_t *dport,
@@ -1504,6 +1714,7 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      uint32_t *identity, uint8_t *lookups, uint8_t *ct,
                      int nthreads)
 {
+    hop_reserve(o, n);
     if (nthreads <= 0)
         nthreads = 1;
 #pragma omp parallel for schedule(static, 4096) num_threads(nthreads)
@@ -1512,8 +1723,10 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         tl_lookups = 0;
         tl_ct = 0;
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
-        tl_mon[0] = tl_mon[1] = 0;
+        tl_mon[0] = tl_mon[1] = tl_mon[2] = 0;
         tl_fresh.n = 0;
+        tl_nat = 0;
+        tl_hop.kind = 0;
         tl_pkt.sa = saddr[i];
         tl_pkt.da = daddr[i];
         tl_pkt.sport = sport[i];
@@ -1540,12 +1753,13 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                     o->notify_out[i] = 0;
                 if (o->notify_mon)
                     o->notify_mon[i] = 0;
+                o->hop[i].kind = 0;
                 continue;
             }
         }
         if (mode == CFO_MODE_EGRESS)
             r = lxc_egress_v4(o, ep_lxc, saddr[i], daddr[i], proto[i],
-                              sport[i], dport[i], flags[i], len[i]);
+                              sport[i], dport[i], flags[i], len[i], 0);
         else
             r = netdev_ingress_v4(o, saddr[i], daddr[i], proto[i], sport[i],
                                   dport[i], flags[i], len[i],
@@ -1557,10 +1771,14 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             lookups[i] = (uint8_t)tl_lookups;
         if (ct)
             ct[i] = tl_ct;
-        if (o->notify_out)
-            o->notify_out[i] = notify_site(mode, ep_lxc, &r);
+        if (o->notify_out) {
+            const uint32_t w = notify_site(mode, ep_lxc, &r);
+            /* (an event after a NAT hop: skb->len of the translated packet) */
+            o->notify_out[i] = w && tl_hop.kind ? w | NT_NATLEN : w;
+        }
         if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
             o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
+        o->hop[i] = tl_hop;
         if (o->pkt_out) {
             o->pkt_out[3 * i] = tl_pkt.sa;
             o->pkt_out[3 * i + 1] = tl_pkt.da;
@@ -1570,11 +1788,8 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
 }
 
 /* ------------------------------------------------------------ IPv6 */
-#define DROP_INVALID_EXTHDR -156
-#define IPPROTO_ICMPV6 58
 #define NEXTHDR_FRAGMENT 44
 #define NEXTHDR_NONE 59
-#define HF_EXTHDR 4
 #define VERDICT_PUNT -2
 
 /* ipv6_hdrlen (ipv6.h:61-98): the header's proto is the next header the
@@ -1710,6 +1925,10 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
     /* delivery by the packet's destination (lookup_ip6_endpoint, :305) */
     tl_lookups++;
     const epinfo *ep = lxc_lookup(o, 2, tl_pkt6.da);
+    /* LXC_NAT46: a peer outside the cluster in ::ffff:0:0/96 (:353-360) */
+    static const uint8_t mapped[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff};
+    if (!ep && dst != CLUSTER_ID && !memcmp(tl_pkt6.da, mapped, 12))
+        return nat64_egress(o, lxc, tl_pkt6.da, proto, flags, len);
     metric(o, 0, METRIC_EGRESS, len); /* to_host / local / to_stack */
     if (ep) {
         if (ep->flags & ENDPOINT_F_HOST) {   /* TRACE_TO_HOST, :373 */
@@ -1761,6 +1980,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                      uint32_t *identity, uint8_t *lookups, uint8_t *ct,
                      int nthreads)
 {
+    hop_reserve(o, n);
     if (nthreads <= 0)
         nthreads = 1;
 #pragma omp parallel for schedule(static, 4096) num_threads(nthreads)
@@ -1770,8 +1990,10 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         tl_lookups = 0;
         tl_ct = 0;
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
-        tl_mon[0] = tl_mon[1] = 0;
+        tl_mon[0] = tl_mon[1] = tl_mon[2] = 0;
         tl_fresh.n = 0;
+        tl_nat = 0;
+        tl_hop.kind = 0;
         memcpy(tl_pkt6.sa, sa, 16);
         memcpy(tl_pkt6.da, da, 16);
         tl_pkt6.sport = sport[i];
@@ -1797,6 +2019,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
                     o->notify_out[i] = 0;
                 if (o->notify_mon)
                     o->notify_mon[i] = 0;
+                o->hop[i].kind = 0;
                 continue;
             }
         }
@@ -1813,10 +2036,14 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
             lookups[i] = (uint8_t)tl_lookups;
         if (ct)
             ct[i] = tl_ct;
-        if (o->notify_out)
-            o->notify_out[i] = notify_site(mode, ep_lxc, &r);
+        if (o->notify_out) {
+            const uint32_t w = notify_site(mode, ep_lxc, &r);
+            /* (an event after a NAT hop: skb->len of the translated packet) */
+            o->notify_out[i] = w && tl_hop.kind ? w | NT_NATLEN : w;
+        }
         if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
             o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
+        o->hop[i] = tl_hop;
         if (o->pkt_out) {
             memcpy(o->pkt_out + 9 * i, tl_pkt6.sa, 16);
             memcpy(o->pkt_out + 9 * i + 4, tl_pkt6.da, 16);
@@ -2016,6 +2243,8 @@ static int ct_create_entries(const cfo_t *o, const uint8_t k2[CTK], int alen, in
     e.slave = st->slave;
     if (st->loopback)
         e.bits |= CTB_LB_LOOPBACK;
+    if (st->nat46)
+        e.bits |= CTB_NAT46;
     const uint8_t *t = k2 + 4;
     const int is_tcp = t[2 * alen + 4] == 6;
     ct_upd_timeout(&e, o->now, is_tcp, dir, is_tcp, 0);
@@ -2056,6 +2285,63 @@ static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
     const int n = ct_create_entries(o, k2, alen, dir, len, src_sec_id, st, keys, ents);
     for (int j = 0; j < n; j++)
         ct_put(o, keys[j], &ents[j]);
+}
+
+/* The CT stage of a header's NAT hop (stage 1, the other family's maps:
+ * the IPv4 egress lookup after NAT64, ipv6_policy's after NAT46), as
+ * ct_apply does for a header's own stages; a NAT64 create carries nat46
+ * (conntrack.h:714-716), an IPv6 ingress create its rev_nat_index
+ * (bpf_lxc.c:787-788).  No load balancer on the hop. */
+static void apply_hop(cfo_t *o, int pass, size_t i, const struct hop *hp, uint8_t cs,
+                      int32_t verdict, uint32_t len, int syn, uint8_t tfl, uint32_t sec,
+                      uint8_t *fresh)
+{
+    const int alen = hp->alen, dir = hp->dir, is_tcp = hp->proto == 6;
+    uint8_t k1[CTK], k2[CTK];
+    int action;
+    uint16_t td, ts;
+    if (ct_keys(alen, hp->owner, hp->sa, hp->da, hp->proto, hp->sport, hp->dport, syn, dir,
+                k1, k2, &action, &td, &ts) < 0)
+        return;
+    const int b = cs & 3;
+    const int64_t e1 = ct_find(o, k1), e2 = ct_find(o, k2);
+    const uint8_t fl = is_tcp ? tfl : 0;
+    if (pass == 1) {   /* CONNTRACK_ACCOUNTING of the lookup's hit */
+        const int64_t e = b >= CT_REPLY ? e1 : b == CT_ESTABLISHED ? e2 : -1;
+        if (e < 0 && b != CT_NEW)
+            fresh[2 * i + 1] = 1;
+        if (e >= 0) {
+            struct ctent *x = &o->ct_ents[e];
+            if (dir == CT_INGRESS) {
+                x->rx_packets++;
+                x->rx_bytes += len;
+            } else {
+                x->tx_packets++;
+                x->tx_bytes += len;
+            }
+        }
+        return;
+    }
+    const uint32_t cnt = fresh[2 * i + 1] ? len : 0;
+    if (b == CT_REPLY || b == CT_RELATED) {
+        if (e1 >= 0)
+            ct_hit_update(o, &o->ct_ents[e1], action, dir, is_tcp, syn, fl, cnt);
+    } else if (b == CT_ESTABLISHED) {
+        if (e2 >= 0) {
+            ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl, cnt);
+            if (verdict == DROP_POLICY)
+                o->ct_live[e2] = 0;   /* ct_delete (the hop is the last stage) */
+        }
+    } else if (cs & CTO_CREATE1) {
+        if (e2 >= 0) {
+            ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl, len);
+        } else {
+            ctstate_t st = {alen == 16 && dir == CT_INGRESS
+                                ? (uint16_t)(hp->da[12] | hp->da[13] << 8) : 0,
+                            0, 0, 0, 0, hp->kind == HOP_NAT64 && dir == CT_EGRESS};
+            ct_create(o, k2, alen, dir, len, sec, &st);
+        }
+    }
 }
 
 /* Fold one classified batch into the CT maps, in header order, as the
@@ -2139,7 +2425,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                         if (x.reslave)    /* ct_update4_slave */
                             o->ct_ents[x.svc_hit].slave = x.slave;
                     } else {
-                        ctstate_t cs = {0, x.slave0, 0, 0, 0};
+                        ctstate_t cs = {0, x.slave0, 0, 0, 0, 0};
                         ct_create(o, x.k_svc, 4, CT_SERVICE, len[i], 0, &cs);
                         if (x.reslave) {
                             int64_t ne = ct_find(o, x.k_svc);
@@ -2179,7 +2465,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                         if (x6.reslave)   /* ct_update6_slave */
                             o->ct_ents[x6.svc_hit].slave = x6.slave;
                     } else {
-                        ctstate_t cs = {0, x6.slave0, 0, 0, 0};
+                        ctstate_t cs = {0, x6.slave0, 0, 0, 0, 0};
                         ct_create(o, x6.k_svc, 16, CT_SERVICE, len[i], 0, &cs);
                         if (x6.reslave) {
                             int64_t ne = ct_find(o, x6.k_svc);
@@ -2203,6 +2489,13 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             const uint8_t cs = (uint8_t)(c >> (4 * s));
             if (!(cs & CTO_DONE1))
                 continue;
+            if (s == 1 && o->hop && i < o->hop_cap && o->hop[i].kind) {
+                apply_hop(o, pass, i, &o->hop[i], cs, verdict[i],
+                          (uint32_t)((int32_t)len[i] + o->hop[i].dlen),
+                          (flags[i] & HF_TCP_CLOSE) != 0, fl,
+                          mode == CFO_MODE_EGRESS ? o->seclabel[ep_lxc] : identity[i], fresh);
+                continue;
+            }
             const int egress_stage = mode == CFO_MODE_EGRESS && s == 0;
             const int dir = egress_stage ? CT_EGRESS : CT_INGRESS;
             const uint16_t owner = egress_stage ? ct_owner(o, ep_lxc)
@@ -2313,12 +2606,12 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                     }
                     ctstate_t cs = {alen == 16 && dir == CT_INGRESS
                                         ? (uint16_t)(kda[12] | kda[13] << 8) : 0,
-                                    0, 0, 0, 0};
+                                    0, 0, 0, 0, 0};
                     if (egress_stage && lbv && alen == 4)   /* ct_state_new from lb4_local */
                         cs = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr,
-                                         x.svc_addr};
+                                         x.svc_addr, 0};
                     if (egress_stage && lbv && alen == 16)  /* ... from lb6_local */
-                        cs = (ctstate_t){x6.rev_nat, x6.slave, 0, 0, 0};
+                        cs = (ctstate_t){x6.rev_nat, x6.slave, 0, 0, 0, 0};
                     ct_create(o, k2, alen, dir, len[i], sec, &cs);
                 }
             }

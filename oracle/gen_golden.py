@@ -178,7 +178,10 @@ class RefDatapath:
             self.ct_maps[lxc] = {ct: f"{ct}_{k}" for ct in CT_MAPS}
             pol = L.load("bpf_lxc.o", "1/0x1010", SC, rn)
             calls = {}
-            for sec, idx in (("2/11", 11), ("2/7", 7), ("2/12", 12), ("2/10", 10)):
+            # (2/8 tail_ipv6_to_ipv4 and 2/9 tail_ipv4_to_ipv6: LXC_NAT46 is on
+            # in the reference's config, lxc_config.h:28 + nat46.h:30-32)
+            for sec, idx in (("2/11", 11), ("2/7", 7), ("2/12", 12), ("2/10", 10),
+                             ("2/8", 8), ("2/9", 9)):
                 calls[idx] = L.load("bpf_lxc.o", sec, SC, rn)
             egress = L.load("bpf_lxc.o", "from-container", SC, rn)
             calls[1] = L.load("bpf_lxc.o", "2/1", SC, rn)   # __send_drop_notify
@@ -520,6 +523,13 @@ def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
              np.ascontiguousarray(pkt[:, 4:8]).view(np.uint8).reshape(-1, 16))
     lab, hit = lpm_pin(dp.L.maps["cilium_ipcache"], h, pk)
     extra.update(x_lpm=lab, x_lpm_hit=hit)
+    if h.family == 6:
+        # NAT64's IPv4 egress looks the v4-mapped destination's low 32 bits
+        # up in the IPv4 ipcache (bpf_lxc.c:516-532 after :1070-1083)
+        d4 = np.ascontiguousarray(np.asarray(h.daddr, np.uint8)[:, 12:16]).view("<u4").ravel()
+        h4 = S.Headers(4, d4, d4, h.sport, h.dport, h.proto, h.flags, h.length, h.mark)
+        l4, k4 = lpm_pin(dp.L.maps["cilium_ipcache"], h4)
+        extra.update(x_lpm_nat=l4[:, 1], x_lpm_nat_hit=k4[:, 1])
     if lb:
         if getattr(t, "lb4", None) is not None:
             extra.update(lb4=t.lb4, revnat4=t.revnat4)
@@ -1488,6 +1498,181 @@ def sc_lb_reply_v6(n=3000, seed=53):
     return t, h, MODE_INGRESS, None, dp
 
 
+# ------------------------------------------------------------ NAT46 / NAT64
+def _nat_setup(seed):
+    """Dual-stack small tables for LXC_NAT46 (lxc_config.h:28): IPv4 peers
+    reached from the endpoint's IPv6 side through ::ffff:0:0/96.  EP_LXC_ID's
+    egress policy admits WORLD (the IPv6 stage: a v4-mapped peer has no
+    IPv6 ipcache entry) and most IPv4 identities (the IPv4 stage after the
+    translation); its ingress policy admits some IPv4 identities (the
+    replies, translated back, are checked by ipv6_policy with the IPv4
+    source's identity).  ::ffff:10.0.0.0/104 is in the ipcache as
+    CLUSTER_ID: those destinations are not translated (bpf_lxc.c:353-354)."""
+    t = S.config_c3(seed, n_prefixes=2000, n_v4_prefixes=500, n_policy=300,
+                    n_endpoints=2, n_prefilter=0)
+    rng = np.random.default_rng(seed + 1)
+    cl = np.zeros(1, S.IPCACHE_DT)
+    cl["family"] = 2
+    cl["plen"] = 104
+    cl["addr"][0, 10:13] = [0xff, 0xff, 10]
+    cl["label"] = S.CLUSTER_ID
+    t.ipcache = np.concatenate([t.ipcache, cl])
+    ipc4 = t.ipcache[t.ipcache["family"] == 1]
+    ids4 = np.unique(ipc4["label"])
+    out_ok = rng.choice(ids4, size=int(0.7 * len(ids4)), replace=False)
+    in_ok = rng.choice(ids4, size=int(0.5 * len(ids4)), replace=False)
+    pol = t.policy[S.EP_LXC_ID]
+    add = np.zeros(1 + len(out_ok) + len(in_ok), S.POLICY_DT)
+    add["identity"][0] = S.WORLD_ID
+    add["egress"][0] = 1
+    add["identity"][1:1 + len(out_ok)] = out_ok
+    add["egress"][1:1 + len(out_ok)] = 1
+    add["identity"][1 + len(out_ok):] = in_ok
+    have = {(int(r["identity"]), int(r["dport"]), int(r["proto"]), int(r["egress"]))
+            for r in pol}
+    add = add[[(int(r["identity"]), 0, 0, int(r["egress"])) not in have for r in add]]
+    t.policy[S.EP_LXC_ID] = np.concatenate([pol, add])
+    return t, rng, ipc4
+
+
+def _mapped(v4):
+    """::ffff:a.b.c.d of raw be32 IPv4 addresses"""
+    a = np.zeros((len(v4), 16), np.uint8)
+    a[:, 10:12] = 0xff
+    a[:, 12:16] = np.asarray(v4, np.uint32).view(np.uint8).reshape(-1, 4)
+    return a
+
+
+def _nat64_flows(rng, ipc4, n, sport_base):
+    """n new IPv6 flows from the endpoint to v4-mapped peers inside IPv4
+    ipcache prefixes: TCP 60%, UDP 25%, ICMPv6 echo 15%"""
+    peers = S._addr_in_prefix_v4(rng, ipc4, rng.integers(0, len(ipc4), size=n))
+    r = rng.random(n)
+    proto = np.where(r < 0.6, S.IPPROTO_TCP,
+                     np.where(r < 0.85, S.IPPROTO_UDP, S.IPPROTO_ICMPV6)).astype(np.uint8)
+    h = S.Headers(6, np.tile(S.LXC_IPV6, (n, 1)), _mapped(peers),
+                  S.htons(sport_base + np.arange(n)),
+                  S.htons(rng.choice(np.array([80, 443, 53, 8080]), size=n)),
+                  proto, np.zeros(n, np.uint8),
+                  rng.integers(100, 1500, size=n).astype(np.uint16), np.zeros(n, np.uint32))
+    ic = proto == S.IPPROTO_ICMPV6
+    h.sport[ic] = 128      # echo request
+    h.dport[ic] = S.htons(np.arange(int(ic.sum())) + 1).astype(np.uint16)
+    h.tcpflags = np.where(proto == S.IPPROTO_TCP, 0x02, 0).astype(np.uint8)
+    return h
+
+
+def sc_nat46_egress_v6(n=3000, seed=61):
+    """NAT64 in the endpoint's IPv6 egress (bpf_lxc.c:353-360,
+    tail_ipv6_to_ipv4 :1070-1083, nat46.h:336-420): packets to v4-mapped
+    peers outside the cluster leave through the IPv4 egress program,
+    translated (saddr LXC_IPV4, daddr the low 32 bits, ICMPv6 as ICMP) — its
+    CT entries carry nat46 (conntrack.h:714-716).  A history stream opens
+    flows; the test stream: their later packets (ESTABLISHED in both maps),
+    new flows with several packets, ICMPv6 errors of every translation
+    outcome (FRAG_NEEDED fall-through, unknown codes and types),
+    extension-header packets (DROP_INVALID_EXTHDR), CLUSTER-mapped peers
+    (not translated) and plain IPv6 traffic."""
+    t, rng, ipc4 = _nat_setup(seed)
+    hist = _nat64_flows(rng, ipc4, 800, 20000)
+    dp = RefDatapath(t)
+    run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    parts, pos = [], []
+
+    def add(h, p):
+        parts.append(h)
+        pos.append(p)
+    est = S.take(hist, rng.integers(0, len(hist), size=int(n * 0.35)))
+    est.tcpflags = np.where(est.proto == S.IPPROTO_TCP,
+                            rng.choice(np.array([0x10, 0x18], np.uint8), size=len(est)), 0
+                            ).astype(np.uint8)
+    est.length = rng.integers(100, 1500, size=len(est)).astype(np.uint16)
+    add(est, rng.random(len(est)))
+    new = _nat64_flows(rng, ipc4, int(n * 0.12), 40000)
+    at = rng.random(len(new)) * 0.9
+    add(new, at)
+    for f, p_ in ((0x10, 0.8), (0x18, 0.5)):
+        sel = np.flatnonzero(rng.random(len(new)) < p_)
+        h = S.take(new, sel)
+        h.tcpflags = np.where(h.proto == S.IPPROTO_TCP, f, 0).astype(np.uint8)
+        at = at + rng.random(len(new)) * 0.03
+        add(h, at[sel])
+    # ICMPv6 errors to mapped peers: each type/code outcome of icmp6_to_icmp4
+    k = int(n * 0.08)
+    e = _nat64_flows(rng, ipc4, k, 50000)
+    tc = np.array([[1, 0], [1, 3], [1, 4], [1, 1], [1, 7], [2, 0], [3, 0], [3, 1],
+                   [4, 0], [4, 1], [4, 2], [137, 0]], np.uint16)
+    pick = tc[rng.integers(0, len(tc), size=k)]
+    e.proto[:] = S.IPPROTO_ICMPV6
+    e.sport[:] = (pick[:, 0] | pick[:, 1] << 8).astype(np.uint16)
+    e.dport[:] = 0
+    e.tcpflags = np.zeros(k, np.uint8)
+    add(e, rng.random(k))
+    # extension headers before the L4 header: ipv6_to_ipv4 drops them
+    x = _nat64_flows(rng, ipc4, int(n * 0.03), 60000)
+    x.flags[:] |= np.uint8(S.HF_EXTHDR)
+    add(x, rng.random(len(x)))
+    # CLUSTER-mapped peers (::ffff:10.x.y.z): to the stack untranslated
+    c = _nat64_flows(rng, ipc4, int(n * 0.04), 61000)
+    c.daddr[:, 12] = 10
+    add(c, rng.random(len(c)))
+    plain = S.gen_headers_v6(rng, int(n * 0.1), t.ipcache[t.ipcache["family"] == 2],
+                             S.local_v6_addrs(t), local_frac=0.3, mark_host=0,
+                             mark_proxy=0, src_fixed=S.LXC_IPV6, ext=0, exthdr_drop=0)
+    add(plain, rng.random(len(plain)))
+    h = S.concat(parts)
+    h = S.take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
+def sc_nat46_reply_v4(n=3000, seed=63):
+    """NAT46 in ipv4_policy (bpf_lxc.c:939-944, tail_ipv4_to_ipv6
+    :1098-1110, nat46.h:236-328): IPv4 replies from the peers of NAT64'd
+    flows find their nat46 CT entry (conntrack.h:241-244) and are checked
+    by ipv6_policy translated (saddr NAT46_PREFIX + the IPv4 source, daddr
+    LXC_IP, ICMP as ICMPv6), with the IPv4 source's identity; ICMP errors
+    related to those flows, new IPv4 traffic, and replies of ordinary
+    flows."""
+    t, rng, ipc4 = _nat_setup(seed)
+    hist = _nat64_flows(rng, ipc4, 1000, 20000)
+    dp = RefDatapath(t)
+    hres = run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    ok = np.flatnonzero(hres[0] != 2)
+    m = int(n * 0.6)
+    pick = ok[rng.integers(0, len(ok), size=m)]
+    src = S.take(hist, pick)
+    peer = np.ascontiguousarray(src.daddr[:, 12:16]).view("<u4").ravel()
+    icmp = src.proto == S.IPPROTO_ICMPV6
+    rep = S.Headers(4, peer.copy(), np.full(m, S.LXC_IPV4, np.uint32),
+                    np.where(icmp, 0, src.dport).astype(np.uint16),
+                    np.where(icmp, src.dport, src.sport).astype(np.uint16),
+                    np.where(icmp, S.IPPROTO_ICMP, src.proto).astype(np.uint8),
+                    np.zeros(m, np.uint8), rng.integers(60, 1500, size=m).astype(np.uint16),
+                    np.zeros(m, np.uint32))
+    rep.tcpflags = np.where(rep.proto == S.IPPROTO_TCP,
+                            rng.choice(np.array([0x12, 0x10, 0x18], np.uint8), size=m), 0
+                            ).astype(np.uint8)
+    # ICMP errors about those flows from their peers: every translation case
+    k = int(n * 0.12)
+    ep_ = S.take(rep, rng.integers(0, m, size=k))
+    tc = np.array([[3, 0], [3, 1], [3, 2], [3, 3], [3, 4], [3, 5], [3, 9], [3, 13],
+                   [3, 14], [11, 0], [12, 0], [5, 0]], np.uint16)
+    pick2 = tc[rng.integers(0, len(tc), size=k)]
+    ep_.proto[:] = S.IPPROTO_ICMP
+    ep_.sport[:] = (pick2[:, 0] | pick2[:, 1] << 8).astype(np.uint16)
+    ep_.dport[:] = 0
+    ep_.tcpflags = np.zeros(k, np.uint8)
+    new = S.gen_headers_v4(rng, n - m - k, ipc4, S.local_v4_addrs(t)[:1], local_frac=1.0,
+                           mark_host=0, mark_proxy=0, frag=0)
+    h = S.concat([rep, ep_, new])
+    h = S.take(h, rng.permutation(len(h)))
+    return t, h, MODE_INGRESS, None, dp
+
+
 SCENARIOS = {
     "edge_ingress_v4": sc_edge_ingress,
     "small_ingress_v4": sc_small_ingress,
@@ -1510,6 +1695,8 @@ SCENARIOS = {
     "ct_seq_egress_v4": lambda: _ct_seq_scenario(4, MODE_EGRESS, 26),
     "ct_seq_ingress_v6": lambda: _ct_seq_scenario(6, MODE_INGRESS, 27),
     "ct_seq_egress_v6": lambda: _ct_seq_scenario(6, MODE_EGRESS, 28),
+    "nat46_egress_v6": sc_nat46_egress_v6,
+    "nat46_reply_v4": sc_nat46_reply_v4,
     "lb_egress_v4": sc_lb_egress,
     "lb_reply_v4": sc_lb_reply,
     "lb_egress_v6": sc_lb_egress_v6,

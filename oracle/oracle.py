@@ -338,6 +338,11 @@ class Oracle:
         ver = np.asarray(verdict)[idx].astype(np.int64)
         ident = np.asarray(identity)[idx].astype(np.uint32)
         ln = np.asarray(hdr.length, np.uint32)[idx]
+        # an event after a NAT hop (cfc.h CFC_NT_NATLEN): the translated
+        # packet's skb->len, the IPv4 header being 20 bytes shorter
+        nat = (w >> 24) & 1 != 0
+        ln = np.where(nat, ln.astype(np.int64) + (20 if hdr.family == 4 else -20),
+                      ln).astype(np.uint32)
         own = sec[ep_lxc] if mode == MODE_EGRESS else 0
         r = np.zeros(len(idx), EVENT_DT)
         hs = getattr(hdr, "hash", None)

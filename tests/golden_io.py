@@ -80,6 +80,10 @@ class Golden:
         # saddr, daddr, the packet's saddr, daddr (services: translated)
         self.lpm = d["x_lpm"] if "x_lpm" in d.files else None
         self.lpm_hit = d["x_lpm_hit"] if "x_lpm_hit" in d.files else None
+        # (IPv6 fixtures) the IPv4 LPM of each daddr's low 32 bits: NAT64's
+        # IPv4 egress lookup of a v4-mapped destination
+        self.lpm_nat = d["x_lpm_nat"] if "x_lpm_nat" in d.files else None
+        self.lpm_nat_hit = d["x_lpm_nat_hit"] if "x_lpm_nat_hit" in d.files else None
         # what the reference reported itself (perf-ring records, drop cb[],
         # proxy map); identity / idmask below add the identities derived
         # from the kernel's LPM for every other tc-path header
@@ -135,6 +139,17 @@ def lpm_identity(g: Golden):
         tc &= ~((g.action == 1) & (g.verdict == -1))   # XDP_DROP
     applies = tc & ~no_identity(g)
     lab, hit = g.lpm.astype(np.uint32), g.lpm_hit.astype(bool)
+    nat = np.zeros(n, bool)
+    if g.mode == 1 and not v4:
+        # NAT64 (bpf_lxc.c:353-360): a peer outside the cluster in
+        # ::ffff:0:0/96 leaves through the IPv4 egress program, whose dstID
+        # is the IPv4 derivation of the low 32 bits (:516-532)
+        da = np.asarray(g.headers.daddr, np.uint8)
+        mapped = (da[:, :10] == 0).all(1) & (da[:, 10] == 0xff) & (da[:, 11] == 0xff)
+        cl = hit[:, 1] & (lab[:, 1] == S.CLUSTER_ID)
+        nat = mapped & ~cl
+        if g.lpm_nat is None:
+            applies &= ~nat
     if g.mode == 1:
         col = np.full(n, 1)
         da = np.asarray(g.headers.daddr)
@@ -152,6 +167,13 @@ def lpm_identity(g: Golden):
             cluster = (np.asarray(da, np.uint8)[:, :8] ==
                        np.asarray(S.ROUTER_IPV6, np.uint8)[:8]).all(axis=1)
         exp = np.where(h & (l != 0), l, np.where(cluster, S.CLUSTER_ID, S.WORLD_ID))
+        if nat.any() and g.lpm_nat is not None:
+            d4 = np.ascontiguousarray(np.asarray(g.headers.daddr, np.uint8)[:, 12:16]
+                                      ).view("<u4").ravel()
+            l4, h4 = g.lpm_nat.astype(np.uint32), g.lpm_nat_hit.astype(bool)
+            e4 = np.where(h4 & (l4 != 0), l4,
+                          np.where((d4 & 0xFF0000) == 0x100000, S.CLUSTER_ID, S.WORLD_ID))
+            exp = np.where(nat, e4, exp)
     else:
         ident = identity_from_mark(g.headers.mark)
         l, h = lab[:, 0], hit[:, 0]
