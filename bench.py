@@ -180,7 +180,7 @@ def main():
     from cilium_amd import synth as S
     from cilium_amd import _lib as LL
     from cilium_amd.datapath import Datapath, HeaderBatchV4, Verdicts
-    from cilium_amd.distributed import allreduce_counters, env_rank
+    from cilium_amd.distributed import allreduce_counters, c5_rank_setup, env_rank
     from cilium_amd.loader import load_tables
 
     rank, local_rank, world = env_rank()
@@ -196,8 +196,12 @@ def main():
     t0 = time.time()
     if args.workload == "c5":
         tables, flows = S.config_c5(args.seed, n_flows=args.flows)
+        # several GPUs: flow affinity — each rank holds the CT
+        # entries and draws the traffic of the address pairs it owns; no CT
+        # collective
+        tables.ct, flows = c5_rank_setup(tables, flows, rank, world)
         log(f"[rank {rank}] C5 tables: {len(tables.ct)} CT entries for "
-            f"{args.flows} flows ({time.time() - t0:.1f}s)")
+            f"{len(flows)} of {args.flows} flows ({time.time() - t0:.1f}s)")
     elif args.workload == "c3":
         tables = S.config_c3(3)
     else:
@@ -221,7 +225,7 @@ def main():
     elif args.workload == "c5":
         from cilium_amd.datapath import pack_v4
         h5, new5 = S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank,
-                                return_new=True)
+                                return_new=True, owner=(rank, world))
         hb = pack_v4(h5, dev)
         s, d, p, m, tf = hb.saddr, hb.daddr, hb.ports, hb.meta, hb.tcp_flags
         del hb, h5
@@ -471,7 +475,10 @@ def main():
             "prefilter_v4_fix": st["prefilter_v4_fix"],
             "mode": args.mode,
             "lpm4_layout": {1: "dir24_8", 2: "trie"}.get(st["lpm4_layout"], "none"),
-            "parallelism": f"header-stream shards x{world}, tables replicated",
+            "parallelism": (f"flow-affinity shards x{world} (address-pair owner: CT "
+                            f"entries and traffic per rank, no CT collective)"
+                            if args.workload == "c5" and world > 1 else
+                            f"header-stream shards x{world}, tables replicated"),
             "drop_notify": bool(args.notify),
             "ct_apply": bool(args.ct_apply),
         },

@@ -109,7 +109,8 @@ class Stats(ctypes.Structure):
                 ("ct_apply_device", ctypes.c_uint32),
                 ("ct_apply_host", ctypes.c_uint32),
                 ("ct_order_changed", ctypes.c_uint32),
-                ("ct_slots", ctypes.c_uint32)]
+                ("ct_slots", ctypes.c_uint32),
+                ("nat_hops", ctypes.c_uint32)]
 
 
 class NodeConfig(ctypes.Structure):

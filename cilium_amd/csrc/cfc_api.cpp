@@ -64,6 +64,11 @@ struct GEp {           // endpoints + policy (+ the counter layout)
     // drop notifications: {SECLABEL, ifindex} by LXC_ID, from the same
     // snapshot of the maps as the tables
     DevBuf ep_info;
+    // LXC_IPV4 / LXC_IP by LXC_ID (nat.hip): the NAT64 source, and on the
+    // device the NAT46 destinations ([65536] raw; null when no endpoint has
+    // an IPv6 address)
+    std::map<uint16_t, uint32_t> nat4;
+    DevBuf nat6;
     uint64_t bytes = 0;
 };
 struct GLb {           // load balancing: services, reverse NAT
@@ -82,6 +87,7 @@ struct GCt {           // conntrack
     uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
     uint32_t n_ct4 = 0, n_ct6 = 0;
     uint32_t tomb4 = 0, tomb6 = 0;       // deleted slots (CT_TOMBSTONE)
+    uint32_t n_nat46 = 0;                // IPv4 entries with nat46 at the build
     uint64_t bytes = 0;
 };
 struct Epoch {
@@ -170,6 +176,27 @@ struct cfc_ctx {
     DevBuf ord_delbm, ord_cnt;
     DevBuf cta_mon;               // per header stage: the fold's monitor length
     uint64_t n_ord_changed = 0;
+    // LXC_NAT46 (nat.hip): the hop batch of each classified batch that had
+    // one, kept for its cfc_ct_apply (by the batch's cfc_out.ct); the
+    // classify kernels' list of hop headers; an IPv4 entry may carry nat46
+    // (one was built, patched in or created since); the hop apply running
+    // is NAT64's (its creates carry nat46)
+    struct NatRec {
+        int family = 0;            // the listing batch's: 6 NAT64, 4 NAT46
+        const void *saddr = nullptr;
+        uint64_t n = 0;
+        int mode = 0;
+        uint16_t ep = 0;
+        uint32_t m = 0;            // hop rows
+        DevBuf idx, rows, outs, ws;
+        cfc_hdr_v4 h4{};
+        cfc_hdr_v6 h6{};
+        cfc_out o{};
+    };
+    std::map<const void *, NatRec> nat;
+    DevBuf nat_list, nat_cnt, nat_tmp;
+    bool nat46_seen = false, hop_nat46 = false;
+    uint64_t n_nat_hops = 0;
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -278,8 +305,8 @@ Map *ct_slot_key(const Epoch &E, int family, const uint32_t *d, const uint32_t *
 }
 
 // struct ct_entry fields the device keeps (CtTimer, CtInfo) into a value:
-// lifetime @32, bits @36 (rx/tx_closing, seen_non_syn, lb_loopback with a
-// load balancer; others kept), rev_nat_index @38, slave @40 (with a load
+// lifetime @32, bits @36 (rx/tx_closing, nat46, seen_non_syn, lb_loopback
+// with a load balancer; others kept), rev_nat_index @38, slave @40 (with a load
 // balancer), tx/rx_flags_seen @42/43, src_sec_id @44, last_tx/rx
 // @48/52
 void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
@@ -287,8 +314,8 @@ void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
     uint16_t bits = 0;
     if (!created)
         memcpy(&bits, &v[36], 2);
-    bits = (uint16_t)((bits & ~(1u | 2u | 16u)) | ((r.flags >> 16) & 3) |
-                      ((r.flags & CTT_NON_SYN) ? 16u : 0u));
+    bits = (uint16_t)((bits & ~(1u | 2u | 4u | 16u)) | ((r.flags >> 16) & 3) |
+                      ((r.flags & CTT_NON_SYN) ? 16u : 0u) | ((r.flags & CTT_NAT46) ? 4u : 0u));
     if (r.pad >> 31) {   // the load balancer's ct_state (ct4_lb / ct6_lb)
         bits = (uint16_t)((bits & ~8u) | (((r.pad >> 16) & 1) ? 8u : 0u));
         const uint16_t slave = (uint16_t)(r.pad & 0xFFFF);
@@ -424,11 +451,12 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
             k[37] = (char)((g.w >> 8) & 7);
             std::string v(it->second->value_bytes(), '\0');
             const uint32_t dir = g.dirlen >> 31;
-            const uint64_t one = 1, len = g.dirlen & 0x7FFFFFFFu;
+            const uint64_t one = 1, len = g.dirlen & (CTLOG_NAT46 - 1);
             memcpy(&v[dir ? 0 : 16], &one, 8);
             memcpy(&v[dir ? 8 : 24], &len, 8);
             const uint32_t life = g.now + 60, last = 5u < g.now ? g.now : 0u;
-            const uint16_t bits = 16;   // seen_non_syn: "for ICMP, there is no SYN"
+            // seen_non_syn ("for ICMP, there is no SYN"), nat46
+            const uint16_t bits = (uint16_t)(16u | ((g.dirlen & CTLOG_NAT46) ? 4u : 0u));
             const uint16_t rev = (uint16_t)g.rev, slave = (uint16_t)g.slave;
             memcpy(&v[32], &life, 4);
             memcpy(&v[36], &bits, 2);
@@ -576,13 +604,14 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
             k[13] = (char)((g.w >> 8) & 7);
             std::string v(it->second->value_bytes(), '\0');
             const uint32_t dir = g.dirlen >> 31;
-            const uint64_t one = 1, len = g.dirlen & 0x7FFFFFFFu;
+            const uint64_t one = 1, len = g.dirlen & (CTLOG_NAT46 - 1);
             memcpy(&v[dir ? 0 : 16], &one, 8);
             memcpy(&v[dir ? 8 : 24], &len, 8);
             const uint32_t life = g.now + 60, last = 5u < g.now ? g.now : 0u;
             // seen_non_syn ("for ICMP, there is no SYN"), and a load
             // balancer's ct_state
-            const uint16_t bits = (uint16_t)(16u | (((g.lbw >> 16) & 1) ? 8u : 0u));
+            const uint16_t bits = (uint16_t)(16u | (((g.lbw >> 16) & 1) ? 8u : 0u) |
+                                             ((g.dirlen & CTLOG_NAT46) ? 4u : 0u));
             const uint16_t rev = (uint16_t)(g.lbw & 0xFFFF), slave = (uint16_t)g.slave;
             memcpy(&v[32], &life, 4);
             memcpy(&v[36], &bits, 2);
@@ -893,6 +922,14 @@ std::shared_ptr<GEp> build_ep(cfc_ctx *c, HostImage &img, const std::vector<Map 
     }
     if ((*rc = upload_vec(g->ep_info, info, s)))
         return nullptr;
+    g->nat4 = img.nat4;
+    if (!img.nat6.empty()) {
+        std::vector<uint4> n6(65536, make_uint4(0, 0, 0, 0));
+        for (const auto &kv : img.nat6)
+            n6[kv.first] = kv.second;
+        if ((*rc = upload_vec(g->nat6, n6, s)))
+            return nullptr;
+    }
     return g;
 }
 
@@ -943,6 +980,7 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     g->ct6_probe = img.ct6_probe;
     g->n_ct4 = img.n_ct4;
     g->n_ct6 = img.n_ct6;
+    g->n_nat46 = img.n_nat46;
     g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
                48ull * nslots + 16ull * (n4 + n6) + 16ull * img.ct4_lb.size();
     g->ct4_host = std::move(img.ct4);
@@ -1217,6 +1255,7 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
             CtTimer *tm = (CtTimer *)(v6 ? G.ct6_tm.p : G.ct4_tm.p);
             if (present) {
                 const CtTimer v = ct_timer_of(it->second.val);
+                c->nat46_seen |= !v6 && (v.flags & CTT_NAT46);
                 if (at < 0) {   // insert
                     at = slot;
                     if (v6) {
@@ -1792,6 +1831,104 @@ int cfc_commit(cfc_ctx *c, void *stream)
 
 namespace {
 
+// LXC_NAT46 (nat.hip): the hop batch of a classified batch whose kernel
+// listed m > 0 headers for a hop — sorted into header order, gathered
+// translated, classified as the other family (NAT64: the sending
+// endpoint's IPv4 egress path; NAT46: ipv6_policy of the destination with
+// the IPv4 path's source identity), its results scattered back.  Kept for
+// the batch's cfc_ct_apply (by its cfc_out.ct).
+template <class Hdr>
+int nat_hop(cfc_ctx *c, const DevTables &T, const EgressArgs &ea, const Hdr &in,
+            const cfc_out &out, int mode, uint16_t ep_lxc, hipStream_t s)
+{
+    constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
+    const void *key = out.ct ? (const void *)out.ct : (const void *)out.verdict;
+    uint32_t m = 0;
+    if (hipMemcpyAsync(&m, c->nat_cnt.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    if (!m) {
+        auto it = c->nat.find(key);
+        if (it != c->nat.end())
+            it->second.family = 0;
+        return 0;
+    }
+    if (m > in.n)
+        return -EIO;
+    if (c->nat.size() > 16) {   // records applied (or never) of other batches
+        (void)hipStreamSynchronize(s);
+        for (auto it = c->nat.begin(); it != c->nat.end();)
+            it = it->second.family == 0 && it->first != key ? c->nat.erase(it) : std::next(it);
+    }
+    cfc_ctx::NatRec &r = c->nat[key];
+    r.family = V6 ? 6 : 4;
+    r.saddr = in.saddr;
+    r.n = in.n;
+    r.mode = mode;
+    r.ep = ep_lxc;
+    r.m = m;
+    const size_t tb = nat_sort_tmp_bytes(m);
+    const size_t m4 = 4ull * ((m + 3) & ~3u);   // (16-byte aligned arrays)
+    const size_t rows = V6 ? 5 * m4 + m4 : 8 * m4 + 4 * m4 + m4;
+    if (r.idx.ensure(4ull * m) || c->nat_tmp.ensure(tb) || r.rows.ensure(rows) ||
+        r.outs.ensure(3 * m4 + 2 * m4))
+        return -ENOMEM;
+    uint32_t *idx = (uint32_t *)r.idx.p;
+    if (int rc = nat_sort((const uint32_t *)c->nat_list.p, idx, m, in.n, c->nat_tmp.p, tb, s))
+        return rc;
+    char *rp = (char *)r.rows.p, *op = (char *)r.outs.p;
+    r.o = cfc_out{};
+    r.o.verdict = (int32_t *)op;
+    r.o.identity = (uint32_t *)(op + m4);
+    r.o.notify = out.notify ? (uint32_t *)(op + 2 * m4) : nullptr;
+    r.o.action = (uint8_t *)(op + 3 * m4);
+    r.o.ct = (uint8_t *)(op + 4 * m4);
+    EgressArgs e2 = ea;
+    e2.nat_idx = e2.nat_cnt = nullptr;
+    const int smode = V6 ? CFC_MODE_EGRESS : CFC_MODE_INGRESS;
+    const WsLayout wl = ws_layout(m, T, smode, true);
+    if (r.ws.ensure(wl.total))
+        return -ENOMEM;
+    int rc;
+    if constexpr (V6) {   // NAT64: IPv4 egress rows
+        NatHop4 h{};
+        h.sa = (uint32_t *)rp;
+        h.da = (uint32_t *)(rp + m4);
+        h.pt = (uint32_t *)(rp + 2 * m4);
+        h.mt = (uint32_t *)(rp + 3 * m4);
+        h.hash = T.lb4 ? (uint32_t *)(rp + 4 * m4) : nullptr;
+        h.tf = (uint8_t *)(rp + 5 * m4);
+        r.h4 = cfc_hdr_v4{h.sa, h.da, h.pt, h.mt, nullptr, h.tf, m, h.hash};
+        rc = nat64_gather(in, idx, m, ea.nat_v4, h, s);
+        if (!rc)
+            rc = launch_classify_v4(T, r.h4, r.o, smode, e2, c->ctr, (uint32_t *)r.ws.p,
+                                    c->num_cus, s, nullptr);
+    } else {              // NAT46: IPv6 ingress rows
+        NatHop6 h{};
+        h.sa = (uint4 *)rp;
+        h.da = (uint4 *)(rp + 4 * m4);
+        h.pt = (uint32_t *)(rp + 8 * m4);
+        h.mt = (uint32_t *)(rp + 9 * m4);
+        h.mk = (uint32_t *)(rp + 10 * m4);
+        h.id = (uint32_t *)(rp + 11 * m4);
+        h.tf = (uint8_t *)(rp + 12 * m4);
+        r.h6 = cfc_hdr_v6{(const uint8_t *)h.sa, (const uint8_t *)h.da, h.pt, h.mt, h.mk, h.tf,
+                          m, nullptr};
+        e2.nat_id = h.id;
+        rc = nat46_gather(T, in, out.identity, idx, m, (const uint4 *)c->epoch->ep->nat6.p, h,
+                          s);
+        if (!rc)
+            rc = launch_classify_v6(T, r.h6, r.o, smode, e2, c->ctr, (uint32_t *)r.ws.p,
+                                    c->num_cus, s, nullptr);
+    }
+    if (!rc)
+        rc = nat_scatter(idx, m, r.o, out, s);
+    c->n_nat_hops += m;
+    if (rc || !out.ct)
+        r.family = 0;   // (no apply follows)
+    return rc;
+}
+
 // cfc_classify_v4 / _v6: validation, auto-commit, workspace, launch
 template <class Hdr, class Launch>
 int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
@@ -1836,6 +1973,33 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.pol_base = it->second.base;
         ea.pol_mask = it->second.mask;
     }
+    // LXC_NAT46: the kernel lists the headers that take a hop — NAT64 from
+    // an IPv6 egress batch of an endpoint with LXC_IPV4, NAT46 from an IPv4
+    // ingress batch while an entry may carry nat46 and an endpoint has an
+    // IPv6 address
+    bool nat_list = false;
+    if constexpr (std::is_same<Hdr, cfc_hdr_v6>::value) {
+        if (mode == CFC_MODE_EGRESS) {
+            auto it = E.ep->nat4.find(ep_lxc);
+            ea.nat_v4 = it == E.ep->nat4.end() ? 0u : it->second;
+            nat_list = ea.nat_v4 != 0 && in->n;
+        }
+    } else {
+        T.nat46 = (mode == CFC_MODE_INGRESS || mode == CFC_MODE_FULL) && E.T.ct4 &&
+                  E.ep->nat6.p && (E.ct->n_nat46 || c->nat46_seen);
+        nat_list = T.nat46 && in->n;
+    }
+    if (nat_list) {
+        if (c->nat_list.bytes < 4 * in->n) {
+            (void)hipStreamSynchronize(s);
+            if (c->nat_list.ensure(4 * in->n))
+                return -ENOMEM;
+        }
+        if (c->nat_cnt.ensure(16) || hipMemsetAsync(c->nat_cnt.p, 0, 4, s) != hipSuccess)
+            return -ENOMEM;
+        ea.nat_idx = (uint32_t *)c->nat_list.p;
+        ea.nat_cnt = (uint32_t *)c->nat_cnt.p;
+    }
     const WsLayout wl = ws_layout(in->n, E.T, mode,
                                   E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4 ||
                                       E.T.lb6 || E.T.rnat6);
@@ -1859,6 +2023,14 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
                 in->n ? next_timing(c, std::is_same<Hdr, cfc_hdr_v6>::value) : nullptr);
     if (rc)
         return rc;
+    if (nat_list) {
+        if ((rc = nat_hop(c, T, ea, *in, *out, mode, ep_lxc, s)))
+            return rc;
+    } else if (!c->nat.empty()) {
+        auto it = c->nat.find(out->ct ? (const void *)out->ct : (const void *)out->verdict);
+        if (it != c->nat.end())
+            it->second.family = 0;
+    }
     (void)hipEventRecord(c->last_done, s);
     c->last_stream = s;
     note_stream(c, s);
@@ -2131,6 +2303,7 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     st->ct_apply_device = c->n_apply_dev;
     st->ct_apply_host = c->n_apply_host;
     st->ct_order_changed = (uint32_t)c->n_ord_changed;
+    st->nat_hops = (uint32_t)c->n_nat_hops;
     st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->ct4_host.size() + c->epoch->ct->ct6_host.size())
                             : 0u;
     return 0;
@@ -2200,7 +2373,7 @@ struct CtEntry {
     uint32_t src_sec_id, last_tx_report, last_rx_report;
 };
 static_assert(sizeof(CtEntry) == 56, "struct ct_entry is 56 bytes");
-constexpr uint16_t CTB_RX_CLOSING = 1, CTB_TX_CLOSING = 2, CTB_LB_LOOPBACK = 8,
+constexpr uint16_t CTB_RX_CLOSING = 1, CTB_TX_CLOSING = 2, CTB_NAT46 = 4, CTB_LB_LOOPBACK = 8,
                    CTB_SEEN_NON_SYN = 16;
 // conntrack.h:31-35
 constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,
@@ -2682,6 +2855,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     A.ep_sec = c->seclabel[ep_lxc];
     A.now = c->now;
     A.seq = c->cta_seq;
+    A.nat46 = c->hop_nat46 ? 1u : 0u;
     if (V6) {
         A.ct6 = (Ct6Slot *)G.ct6.p;
         A.mask = G.ct6_mask;
@@ -2892,8 +3066,8 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
 }
 
 template <class Hdr>
-int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode,
-             uint16_t ep_lxc, void *stream)
+int ct_apply_one(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode,
+                 uint16_t ep_lxc, void *stream)
 {
     if (!c || !in || !out || !out->ct || !out->verdict || !out->identity)
         return -EINVAL;
@@ -3211,6 +3385,8 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
                     if (x.loopback)
                         e.bits |= CTB_LB_LOOPBACK;
                 }
+                if (c->hop_nat46)               // a NAT64 hop (conntrack.h:714-716)
+                    e.bits |= CTB_NAT46;
                 put_new(m, k2, e);
                 if (eg && x.svc && x.addr) {    // the reverse-NAT entry
                     std::string kx = k2;
@@ -3243,6 +3419,43 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     if (hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     return 0;
+}
+
+// cfc_ct_apply_v4 / _v6: the batch's own stages, then — a batch with a NAT
+// hop batch (nat_hop) — the hops' stages into the other family's maps
+// (apply_hop of the oracle): NAT64 as the endpoint's IPv4 egress batch
+// (its creates carry nat46), NAT46 as an IPv6 ingress batch.  While its own
+// family folds, a hop header's stage counts as allowed (it led to the hop)
+// and alone (bits 4-7, the event word aside); nat_scatter puts the hop's
+// results back afterwards, with its packet-order CT result.
+template <class Hdr>
+int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode,
+             uint16_t ep_lxc, void *stream)
+{
+    if (!c || !in || !out || !out->ct || !out->verdict || !out->identity)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    auto it = c->nat.find((const void *)out->ct);
+    if (it == c->nat.end() || it->second.family != family || it->second.saddr != in->saddr ||
+        it->second.n != in->n || it->second.mode != mode || it->second.ep != ep_lxc)
+        return ct_apply_one(c, family, in, out, mode, ep_lxc, stream);
+    cfc_ctx::NatRec &r = it->second;
+    r.family = 0;   // (consumed; its buffers stay for the next hop batch)
+    hipStream_t s = (hipStream_t)stream;
+    (void)hipSetDevice(c->device);
+    const uint32_t *idx = (const uint32_t *)r.idx.p;
+    if (nat_pre(idx, r.m, *out, s))
+        return -EIO;
+    int rc = ct_apply_one(c, family, in, out, mode, ep_lxc, stream);
+    if (!rc) {
+        c->hop_nat46 = family == 6;
+        rc = family == 6 ? ct_apply_one(c, 4, &r.h4, &r.o, CFC_MODE_EGRESS, ep_lxc, stream)
+                         : ct_apply_one(c, 6, &r.h6, &r.o, CFC_MODE_INGRESS, (uint16_t)0, stream);
+        c->hop_nat46 = false;
+        c->nat46_seen |= family == 6;
+    }
+    const int rc2 = nat_scatter(idx, r.m, r.o, *out, s);
+    return rc ? rc : rc2;
 }
 
 // ---- cfc_ct_gc: ctmap.GC with doFiltering (pkg/maps/ctmap/ctmap.go:303-350)

@@ -137,6 +137,7 @@ struct Hdr {
     int ct_res;
     uint32_t idw;                // identity counter key (CountArgs.id)
     bool id_ovf, drop1;          // ident has no histogram range; stage-1 drop
+    bool nat;                    // takes the NAT46 hop (nat.hip)
     uint32_t ev2;                // stage-2 identity event: 0, 1 fwd, 2 drop
     uint32_t tf;                 // TCP header byte 13 (cfc_hdr_v4.tcp_flags)
     uint32_t evw;                // trace event word of a forwarded header
@@ -320,6 +321,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
     h.ct_k1 = h.ct_k2 = NONE;
     h.idw = KEY_NONE;
     h.id_ovf = h.drop1 = false;
+    h.nat = false;
     h.ev2 = 0;
     h.evw = 0;
     if (MODE == CFC_MODE_XDP || h.xdp_drop)
@@ -358,9 +360,20 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
             h.ct_res = c.res;
             h.ct_slot = c.slot;
             h.ct_byte = (uint32_t)c.res | CTO_DONE;
+            // LXC_NAT46: a hit on an entry with nat46 (__ct_lookup,
+            // conntrack.h:241-244) leaves ipv4_policy for NAT46 and
+            // ipv6_policy (bpf_lxc.c:939-944, 1098-1110) when the endpoint
+            // has an IPv6 address: that hop decides (nat.hip); nothing here
+            // counts but the hit
+            if (T.nat46 && c.slot != NONE && (h.rec.w & LXC_HAS6) &&
+                (T.ct4_tm[c.slot].flags & CTT_NAT46)) {
+                h.nat = true;
+                h.need_pol = false;
+                h.ct_k1 = ct_acct_key(c.slot, CT_INGRESS);
+            }
             // a reply of a load-balanced flow: its source translated back
             // (bpf_lxc.c:946-955; the packet only)
-            if (LB && T.ct4_lb && c.res == CT_REPLY) {
+            if (LB && T.ct4_lb && c.res == CT_REPLY && !h.nat) {
                 const uint4 lw = ld16(T.ct4_lb + c.slot);
                 if (!((lw.x >> 16) & 1)) {
                     uint32_t da = h.da;
@@ -794,6 +807,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #endif
                 }
             }
+            if (!EGR && MODE != CFC_MODE_XDP && E.nat_idx)   // (uniform)
+                list_append(E.nat_idx, E.nat_cnt, h[u].nat && h[u].valid, (uint32_t)start + i);
             if (MODE != CFC_MODE_XDP && h[u].valid && h[u].id_ovf && h[u].need_pol)
                 id_count(C, id_dir, h[u].ident, h[u].drop1, len);
             if (LBE && h[u].valid && h[u].ver == DROP_NO_SERVICE) {   // (rare)

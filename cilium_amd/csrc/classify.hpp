@@ -19,6 +19,15 @@ struct EgressArgs {
     uint32_t pol_base;
     uint32_t pol_mask;
     uint32_t ct_owner;   // ct_owner_word of the sending endpoint's CT maps
+    // LXC_NAT46 (nat.hip).  IPv6 egress: LXC_IPV4 of the sending endpoint
+    // (raw; 0 = none: a NAT64 header drops with DROP_INVALID).  nat_idx /
+    // nat_cnt (or null): the headers that take a NAT hop, appended in any
+    // order (IPv6 egress: NAT64; IPv4 ingress: NAT46).  nat_id (an IPv6
+    // ingress batch of NAT46 hops, or null): each header's source identity,
+    // cb[CB_SRC_LABEL] of the IPv4 path (bpf_lxc.c:1098-1110)
+    uint32_t nat_v4;
+    uint32_t *nat_idx, *nat_cnt;
+    const uint32_t *nat_id;
 };
 
 constexpr int BLOCK = 1024;
@@ -118,13 +127,14 @@ int launch_patch16(const Patch16 *rec, uint64_t n, hipStream_t stream);
 struct CtLog {
     uint32_t x, y, w;     // key: saddr, daddr (k2 order), ct_word
     uint32_t now;         // the batch clock of the create
-    uint32_t dirlen;      // dir << 31 | len
+    uint32_t dirlen;      // dir << 31 | nat46 << 30 | len
     uint32_t sec;         // src_sec_id
     uint32_t seq, order;  // apply sequence, header order
     uint32_t lbw, slave;  // rev_nat_index | lb_loopback << 16, slave (a load balancer's creates)
 };
 // the same for an IPv6 create (ct_create6, conntrack.h:615-662): 16-byte
 // addresses, and the rev_nat_index ipv6_policy sets (bpf_lxc.c:787-788)
+constexpr uint32_t CTLOG_NAT46 = 1u << 30;   // (dirlen) the create carries nat46
 struct CtLog6 {
     uint4 x, y;           // saddr, daddr (k2 order), raw
     uint32_t w, now, dirlen, sec, seq, order, rev, slave;
@@ -216,6 +226,9 @@ struct CtaArgs {
     // fold found (MON_* codes), 0xFF not replayed
     uint32_t *nt;
     uint8_t *mon;
+    // a NAT64 hop's batch (the IPv4 egress path after tail_ipv6_to_ipv4): its
+    // creates carry nat46 (conntrack.h:714-716)
+    uint32_t nat46;
 };
 // a device buffer owned by the host library (grown on demand)
 struct DevBuf {
@@ -375,6 +388,34 @@ int launch_lb4_egress(const DevTables &T, const LbArgs &A, hipStream_t stream);
 struct LbIn {
     const uint32_t *tda, *tpt, *psa, *fl;
 };
+
+// ---- NAT46 / NAT64 hops (nat.hip): the hop batch's rows (row k is header
+// idx[k] of the batch that listed it, translated)
+struct NatHop4 {          // NAT64: IPv4 egress rows
+    uint32_t *sa, *da, *pt, *mt, *hash;   // hash may be null (no load balancer)
+    uint8_t *tf;
+};
+struct NatHop6 {          // NAT46: IPv6 ingress rows
+    uint4 *sa, *da;
+    uint32_t *pt, *mt, *mk, *id;          // mk: the skip-proxy magic; id: source identity
+    uint8_t *tf;
+};
+size_t nat_sort_tmp_bytes(uint32_t m);
+// the listed headers in header order: in[0, m) -> out (n: the batch's size)
+int nat_sort(const uint32_t *in, uint32_t *out, uint32_t m, uint64_t n, void *tmp,
+             size_t tmp_bytes, hipStream_t s);
+int nat64_gather(const cfc_hdr_v6 &in, const uint32_t *idx, uint32_t m, uint32_t sa4,
+                 const NatHop4 &h, hipStream_t s);
+int nat46_gather(const DevTables &T, const cfc_hdr_v4 &in, const uint32_t *ident,
+                 const uint32_t *idx, uint32_t m, const uint4 *ep6, const NatHop6 &h,
+                 hipStream_t s);
+// the hop batch's outputs (sub) into the header's (out); sub.ct loses the
+// hop's second stage
+int nat_scatter(const uint32_t *idx, uint32_t m, const cfc_out &sub, const cfc_out &out,
+                hipStream_t s);
+// before the apply of the headers' own family: verdict 0, CT bits 4-7 and
+// the event word cleared (nat_scatter restores them after the hop's apply)
+int nat_pre(const uint32_t *idx, uint32_t m, const cfc_out &out, hipStream_t s);
 
 // dst[i] += src[i] for n u64 (counter import)
 int launch_add_u64(uint64_t *dst, const uint64_t *src, uint64_t n,

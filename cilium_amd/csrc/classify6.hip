@@ -327,6 +327,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         uint32_t ck1 = NONE, ck2 = NONE;   // CT accounting keys per stage
         uint32_t idw = KEY_NONE, ev2 = 0;  // identity counter key; stage-2 event
         uint32_t evw = 0;                  // trace event word (forwarded)
+        bool nat = false, natdrop = false; // NAT64: the hop decides; can't translate
         const uint32_t len = mt >> 16;
         // the Bloom words of the prefilter's and the ipcache's lookups of
         // this header's address, loaded together (egress with a load
@@ -369,18 +370,24 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                 } else {
                     ident = magic == 0xC00u ? HOST_ID : WORLD_ID;
                 }
+                // a NAT46 hop (tail_ipv4_to_ipv6 -> tail_ipv6_policy,
+                // bpf_lxc.c:1098-1110): the IPv4 path's source identity, and
+                // the skip-proxy mark it carried in tc_index
+                const bool hop = E.nat_id != nullptr;
+                if (hop)
+                    ident = E.nat_id[i];
                 if (xd) {   // send_drop_notify_error: no identity recorded
                     act = TC_ACT_SHOT;
                     ver = xd;
                     ident = 0;
                     met0 = mkey6<MODE>(xd, METRIC_INGRESS);
-                } else if (punt) {
+                } else if (punt && !hop) {
                     ver = VERDICT_PUNT;
                     ident = 0;
                 } else {
                     // handle_ipv6 (:203-213): reserved identities take the
                     // ipcache's unless it says CLUSTER_ID
-                    if (ident < HEALTH_ID) {
+                    if (ident < HEALTH_ID && !hop) {
                         const uint32_t label = lpm6_lookup(T.ipc6, lo_ipc, sa, bwi);
                         if (label && label != CLUSTER_ID)
                             ident = label;
@@ -524,7 +531,27 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     } else {
                         met0 = mkey6<MODE>(0, METRIC_EGRESS);   // host/local/stack
                         ver = 0;
-                        if (!elocal) {
+                        if (!elocal && ident != CLUSTER_ID && pda.x == 0 && pda.y == 0 &&
+                            pda.z == 0xFFFF0000u) {
+                            // LXC_NAT46: a v4-mapped peer outside the cluster
+                            // (::ffff:0:0/96, bpf_lxc.c:353-360, ipv6.h:279-282)
+                            // leaves through tail_ipv6_to_ipv4 (:1070-1083):
+                            // ipv6_to_ipv4 drops extension headers, and a
+                            // sender without LXC_IPV4 cannot be translated;
+                            // else the IPv4 egress path decides (nat.hip)
+                            met0 = NONE;
+                            ident = 0;
+                            if ((mt & CFC_HF_EXTHDR) || !E.nat_v4) {
+                                ver = (mt & CFC_HF_EXTHDR) ? DROP_INVALID_EXTHDR : DROP_INVALID;
+                                if (ver == DROP_INVALID_EXTHDR)
+                                    met0 = mkey6<MODE>(DROP_INVALID_EXTHDR, METRIC_EGRESS);
+                                else
+                                    natdrop = true;
+                            } else {
+                                act = TC_ACT_OK;
+                                nat = true;
+                            }
+                        } else if (!elocal) {
                             act = TC_ACT_OK;   // TRACE_TO_STACK (:390)
                             evw = trace_word(OBS_TO_STACK, E.lxc_id, (uint32_t)c.res, mon1);
                         } else if (erec.z & LXC_HOST) {
@@ -607,6 +634,14 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             st_nt(ck1, C.ct + i);
             if (EGR)
                 st_nt(ck2, C.ct2 + i);
+        }
+        if (EGR && E.nat_idx)   // (uniform)
+            list_append(E.nat_idx, E.nat_cnt, nat && valid, (uint32_t)i);
+        if (EGR && natdrop && valid) {   // DROP_INVALID (rare: a direct count)
+            unsigned long long *m = reinterpret_cast<unsigned long long *>(
+                C.g_met + (uint64_t)(-DROP_INVALID * METRIC_DIRS + METRIC_EGRESS) * 2);
+            atomicAdd(m, 1ull);
+            atomicAdd(m + 1, (unsigned long long)len);
         }
         if (MODE != CFC_MODE_XDP) {
             st_nt(ctr_key(C, ctr0, len), C.ctr + i);

@@ -741,7 +741,8 @@ __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *
     const uint32_t l = block_count(&A.cnt[CTA_NLOG], lg);
     uint32_t b = block_count_n(&A.cnt[CTA_NREQB], (uint32_t)rb + (uint32_t)kx);
     const uint32_t fl = ((o.w2 >> 8) & 7) | 2u;
-    const uint32_t dirlen = (o.dir == CT_INGRESS ? 1u << 31 : 0u) | o.len;
+    const uint32_t dirlen = (o.dir == CT_INGRESS ? 1u << 31 : 0u) | (A.nat46 ? CTLOG_NAT46 : 0u) |
+                            o.len;
     if (lg && l < A.log_cap) {
         if constexpr (V6) {
             CtLog6 &g = A.log6[A.log_base + l];
@@ -920,7 +921,8 @@ __device__ __forceinline__ St load_state(const CtTimer *tm, uint32_t slot)
     e.last_tx = t.y;
     e.seen_rx = t.z & 0xFF;
     e.seen_tx = (t.z >> 8) & 0xFF;
-    e.bits = ((t.z >> 16) & 3) | ((t.z & CTT_NON_SYN) ? SEEN_NON_SYN : 0u);
+    e.bits = ((t.z >> 16) & 3) | ((t.z & CTT_NON_SYN) ? SEEN_NON_SYN : 0u) |
+             ((t.z & CTT_NAT46) ? NAT46 : 0u);
     e.lifetime = t.w;
     return e;
 }
@@ -930,7 +932,7 @@ __device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St
     t.x = e.last_rx;
     t.y = e.last_tx;
     t.z = e.seen_rx | e.seen_tx << 8 | (e.bits & 3) << 16 |
-          ((e.bits & SEEN_NON_SYN) ? CTT_NON_SYN : 0u);
+          ((e.bits & SEEN_NON_SYN) ? CTT_NON_SYN : 0u) | ((e.bits & NAT46) ? CTT_NAT46 : 0u);
     t.w = e.lifetime;
     *reinterpret_cast<uint4 *>(tm + slot) = t;
 }
@@ -1021,6 +1023,8 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
             e = fresh(A.now, o.is_tcp, o.dir);
             if (wr == SEC_REL)
                 e.bits |= SEEN_NON_SYN;
+            if (A.nat46)   // a NAT64 hop's create (conntrack.h:714-716)
+                e.bits |= NAT46;
             live = created = true;
             acct[0] = acct[1] = acct[2] = acct[3] = 0;
             acct[d] = 1;
@@ -1052,6 +1056,8 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
                 e = fresh(A.now, o.is_tcp, o.dir);
                 if (o.ki_form)
                     e.bits |= SEEN_NON_SYN;
+                if (A.nat46)
+                    e.bits |= NAT46;
                 live = created = true;
                 acct[0] = acct[1] = acct[2] = acct[3] = 0;
                 acct[d] = 1;
@@ -1200,11 +1206,13 @@ __global__ __launch_bounds__(256) void k_cta_mon(CtaArgs A)
         return;
     const uint32_t res = cs & CFC_CT_RES_MASK;
     uint32_t m = TRACE_PAYLOAD_LEN;
+    const uint32_t proto = A.mt[i] & 0xFF;
     if (res != CT_NEW) {
         const uint8_t c = A.mon[2 * i + st];
         m = c == 1 ? 1u : c == 2 ? TRACE_PAYLOAD_LEN : 0u;
+        if (c == 0xFF && ct_action(V6, proto, A.pt[i], A.mt[i]) == 2)
+            m = TRACE_PAYLOAD_LEN;
     }
-    const uint32_t proto = A.mt[i] & 0xFF;
     const CtProbe k = ct_probe<V6>(proto, A.pt[i], CT_INGRESS, 0);
     if ((res >= CT_REPLY ? k.td : k.ts) == 0x3500u)   // conn_is_dns: htons(53)
         m = MTU_LEN;

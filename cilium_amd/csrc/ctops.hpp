@@ -13,7 +13,7 @@ namespace {
 
 constexpr uint32_t CT_LIFETIME_TCP = 21600, CT_LIFETIME_NONTCP = 60, CT_SYN_TIMEOUT = 60,
                    CT_CLOSE_TIMEOUT = 10, CT_REPORT_INTERVAL = 5;
-constexpr uint32_t RX_CLOSING = 1, TX_CLOSING = 2, SEEN_NON_SYN = 16;   // ct_entry bits
+constexpr uint32_t RX_CLOSING = 1, TX_CLOSING = 2, NAT46 = 4, SEEN_NON_SYN = 16;   // ct_entry bits
 constexpr uint32_t OP_NONE = 0, OP_HIT = 1, OP_DELETE = 2, OP_CREATE = 3;
 // per-slot marks of one apply: ordered ops; inserted by this apply; a
 // delete among its ops; a create or related-entry write among its ops

@@ -531,7 +531,7 @@ CtTimer ct_timer_of(const std::string &val)
         memcpy(&tm.last_tx, v + 48, 4);
         memcpy(&tm.last_rx, v + 52, 4);
         tm.flags = v[43] | (uint32_t)v[42] << 8 | (uint32_t)(bits & 3) << 16 |
-                   ((bits & 16) ? CTT_NON_SYN : 0u);
+                   ((bits & 16) ? CTT_NON_SYN : 0u) | ((bits & 4) ? CTT_NAT46 : 0u);
         memcpy(&tm.lifetime, v + 32, 4);
     }
     return tm;
@@ -684,6 +684,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                     img->ct4_lb[i] = ct_lb_of(kv.second.val);
                 img->ct4_probe = std::max(img->ct4_probe, p);
                 img->n_ct4++;
+                img->n_nat46 += (tm.flags & CTT_NAT46) != 0;
             } else {
                 const Ct6Slot &e = e6;
                 uint32_t i = ct_hash6(e.d, e.s, e.z, e.w) & img->ct6_mask, p = 0;
@@ -935,6 +936,29 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
             r.pol_mask = loc.mask;
             v4.push_back(r);
         }
+        // LXC_IPV4 / LXC_IP of each endpoint (the NAT46 / NAT64 addresses,
+        // nat46.h:236-420): the lowest address of its family in cilium_lxc
+        img->nat4.clear();
+        img->nat6.clear();
+        for (const LxcSlot &e : v4) {
+            if (e.info & LXC_HOST)
+                continue;
+            const uint16_t id = (uint16_t)(e.info & 0xFFFF);
+            auto it = img->nat4.find(id);
+            if (it == img->nat4.end() || memcmp(&e.addr, &it->second, 4) < 0)
+                img->nat4[id] = e.addr;
+        }
+        for (const Lxc6Slot &e : v6) {
+            if (e.info & LXC_HOST)
+                continue;
+            const uint16_t id = (uint16_t)(e.info & 0xFFFF);
+            auto it = img->nat6.find(id);
+            if (it == img->nat6.end() || memcmp(e.a, &it->second, 16) < 0)
+                img->nat6[id] = make_uint4(e.a[0], e.a[1], e.a[2], e.a[3]);
+        }
+        for (LxcSlot &e : v4)
+            if (img->nat6.count((uint16_t)(e.info & 0xFFFF)))
+                e.info |= LXC_HAS6;
         img->n_eps = (uint32_t)v4.size();
         if (!v4.empty()) {
             uint32_t ns = pow2_at_least(std::max<uint64_t>(8, 4ull * v4.size()));

@@ -1,6 +1,7 @@
 // Flattening of the host maps into the device layouts of layout.h.
 #pragma once
 #include <cstdint>
+#include <map>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -77,6 +78,9 @@ struct HostImage {
     Lpm6Host ipc6, pf6_fix, pf6_dyn;
     std::vector<Lxc6Slot> lxc6;
     uint32_t lxc6_mask = 0, n_eps6 = 0;
+    // per LXC_ID its IPv4 / IPv6 address (raw), endpoints with one
+    std::map<uint16_t, uint32_t> nat4;
+    std::map<uint16_t, uint4> nat6;
     std::vector<std::pair<Map *, std::string>> ctr_owner;  // ctr -> entry
     // conntrack (layout.h): every CT map in one table per family
     std::vector<Ct4Slot> ct4;
@@ -84,6 +88,7 @@ struct HostImage {
     std::vector<CtTimer> ct4_tm, ct6_tm;     // parallel to ct4 / ct6
     uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
     uint32_t n_ct4 = 0, n_ct6 = 0;           // entries placed
+    uint32_t n_nat46 = 0;                    // IPv4 entries with nat46
     std::vector<uint8_t> ct_local;           // lxc_id -> has local CT maps
     // load balancing (layout.h): service slots, reverse NAT, and per CT4
     // slot the entry's LB state (built with GROUP_CT when lb_ct is set)

@@ -11,7 +11,7 @@ namespace {
 constexpr uint32_t HOST_ID = 1, WORLD_ID = 2, CLUSTER_ID = 3, HEALTH_ID = 4;
 constexpr int DROP_INVALID_SIP = -132, DROP_POLICY = -133,
               DROP_CT_UNKNOWN_PROTO = -137, DROP_MISSED_TAIL_CALL = -140,
-              DROP_NO_SERVICE = -158;
+              DROP_NO_SERVICE = -158, DROP_INVALID = -134;
 constexpr int TC_ACT_OK = 0, TC_ACT_SHOT = 2, TC_ACT_REDIRECT = 7;
 constexpr int XDP_DROP = 1, XDP_PASS = 2;
 constexpr int METRIC_INGRESS = 1, METRIC_EGRESS = 2;
@@ -46,6 +46,22 @@ constexpr uint32_t OBS_TO_LXC = 0, OBS_TO_PROXY = 1, OBS_TO_HOST = 2, OBS_TO_STA
 constexpr uint32_t TRACE_PAYLOAD_LEN = 128, MTU_LEN = 1500;
 // mon 0 (not sent) keeps the site with length class 0: cfc_ct_apply
 // re-decides the length in packet order (ctapply.hip k_cta_mon)
+// one wave appends header i to a list where want (every lane active):
+// one atomic per wave
+__device__ __forceinline__ void list_append(uint32_t *list, uint32_t *cnt, bool want, uint32_t i)
+{
+    const uint64_t m = __ballot(want);
+    if (!m)
+        return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == lead)
+        base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, (int)lead, 64);
+    if (want)
+        list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = i;
+}
 __device__ __forceinline__ uint32_t mon_class(uint32_t mon)
 {
     return mon == 0 ? 0u : mon == MTU_LEN ? 2u : mon == 1u ? 3u : 1u;

@@ -111,6 +111,8 @@ constexpr uint32_t LXC_HOST = 1u << 16;       // ENDPOINT_F_HOST
 constexpr uint32_t LXC_HAS_POLICY = 1u << 17; // an endpoint program exists
 constexpr uint32_t LXC_IFINDEX = 1u << 18;    // ifindex != 0 (redirect)
 constexpr uint32_t LXC_CT_LOCAL = 1u << 19;   // has its own CT maps (else global)
+constexpr uint32_t LXC_HAS6 = 1u << 20;       // (IPv4 slots) the endpoint has an IPv6
+                                              // address: NAT46 can deliver to it
 constexpr uint32_t LXC_VALID = 1u << 31;      // 0 = free slot
 struct alignas(16) LxcSlot {
     uint32_t addr;                 // be32 raw
@@ -302,10 +304,11 @@ struct alignas(16) Ct4Slot {
 struct alignas(16) CtTimer {
     uint32_t last_rx, last_tx;
     uint32_t flags;      // rx_flags_seen | tx_flags_seen << 8 | closing << 16
-                         // | seen_non_syn << 18
+                         // | seen_non_syn << 18 | nat46 << 19
     uint32_t lifetime;
 };
 constexpr uint32_t CTT_NON_SYN = 1u << 18;
+constexpr uint32_t CTT_NAT46 = 1u << 19;   // ct_entry.nat46 (conntrack.h:241-244, 714-716)
 // per-slot state of the device CT apply (ctapply.hip): src_sec_id and
 // rev_nat_index of an entry the device created, and what changed since the
 // host last synchronised (CTI_*, bits 16-18 of y)
@@ -389,6 +392,10 @@ struct DevTables {
     // the launch: bpf_ktime_get_sec() (cfc_set_clock), HOST_IFINDEX
     uint32_t now;
     uint32_t host_ifindex;
+    // LXC_NAT46 (lxc_config.h:28, nat46.h:30-32): 1 when an IPv4 entry may
+    // carry nat46 and an endpoint has an IPv6 address — the IPv4 ingress
+    // path then checks its CT hits for it (bpf_lxc.c:939-944)
+    uint32_t nat46;
     // per-identity counters: bit r set = identities [r * ID_RANGE,
     // (r + 1) * ID_RANGE) have a histogram range (classify.hpp)
     uint32_t id_cover;

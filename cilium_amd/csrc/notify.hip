@@ -32,6 +32,13 @@ __device__ __forceinline__ uint32_t fold6(const uint32_t *w)
 }
 
 // symmetric 5-tuple hash (oracle/oracle.py flow_hash)
+// skb->len of the event's packet: after a NAT hop (CFC_NT_NATLEN) the
+// translated one — IPv4's header 20 bytes shorter (nat46.h:236-420)
+__device__ __forceinline__ uint32_t rec_len(const NotifyArgs &a, uint64_t i, uint32_t w)
+{
+    const uint32_t len = a.meta[i] >> 16;
+    return (w & CFC_NT_NATLEN) ? (a.family == 4 ? len + 20u : len - 20u) : len;
+}
 __device__ __forceinline__ uint32_t flow_hash(const NotifyArgs &a, uint64_t i)
 {
     if (a.hash)   // the batch's skb->hash
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(NT_THREADS) void k_nt_write(NotifyArgs a,
             const uint32_t mc = (w >> 22) & 3;   // TRACE_PAYLOAD_LEN / MTU / 1
             const uint32_t mon = mc == 2 ? MTU_LEN : mc == 3 ? 1u : TRACE_PAYLOAD_LEN;
             const uint32_t ident = a.identity[i];
-            const uint32_t len = a.meta[i] >> 16;
+            const uint32_t len = rec_len(a, i, w);
             const uint2 e = a.ep_info[lxc];
             uint32_t src = e.x, dst = 0, dst_id = 0, ifx = 0;
             if (obs == OBS_TO_LXC) {   // the destination's ipv{4,6}_policy
@@ -170,7 +177,7 @@ __global__ __launch_bounds__(NT_THREADS) void k_nt_write(NotifyArgs a,
             const uint32_t site = (w >> 16) & 0xF, lxc = w & 0xFFFF;
             const int ver = a.verdict[i];
             const uint32_t ident = a.identity[i];
-            const uint32_t len = a.meta[i] >> 16;
+            const uint32_t len = rec_len(a, i, w);
             uint32_t src = 0, dst = 0, dst_id = 0, ifx = 0, source = 0;
             if (site == CFC_NT_EGRESS) {
                 source = lxc;

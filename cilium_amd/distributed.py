@@ -156,3 +156,16 @@ def shard_ct(ct, rank, world):
             kd, ks = addr_keys(d, 6), addr_keys(s, 6)
         own[m] = pair_owner(kd, ks, world)
     return ct[own == rank]
+
+
+def c5_rank_setup(tables, flows, rank, world):
+    """The C5 conntrack workload of one rank under flow affinity: the CT
+    entries it owns (shard_ct) and its live flows (those whose address pair
+    it owns; the stream is then drawn from them and from new flows it owns,
+    synth.headers_c5(owner=...)).  World 1: everything.  -> (ct, flows)"""
+    if world == 1:
+        return tables.ct, flows
+    import numpy as np
+    from .synth import take
+    own = pair_owner(addr_keys(flows.saddr, 4), addr_keys(flows.daddr, 4), world) == rank
+    return shard_ct(tables.ct, rank, world), take(flows, np.flatnonzero(own))

@@ -916,18 +916,34 @@ def headers_c5_v6(t: Tables, flows: Headers, n, seed=6, new_frac=0.05, s=1.1):
 
 
 def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1,
-               return_new=False):
+               return_new=False, owner=None):
     """C5 stream into the endpoint: 95% packets of live flows drawn
     Zipf(s) by flow (ESTABLISHED for flows opened from outside, REPLY for
     flows the endpoint opened), 5% packets of new flows (C2 generator).
-    return_new: also the mask of the new flows' headers."""
+    return_new: also the mask of the new flows' headers.  owner = (rank,
+    world): only new flows whose address pair that rank owns
+    (distributed.pair_owner; flows should be the rank's own already)."""
     rng = np.random.default_rng(seed + 777)
     m = int(n * (1 - new_frac))
     pick = _zipf_ranks(rng, len(flows), m, s)
     old = take(flows, pick)
     old.length = rng.integers(60, 1501, size=m).astype(np.uint16)
-    new = gen_headers_v4(rng, n - m, t.ipcache, local_v4_addrs(t)[:1],
-                         local_frac=1.0, proxy_ident=proxy_identities(t))
+    if owner is None or owner[1] == 1:
+        new = gen_headers_v4(rng, n - m, t.ipcache, local_v4_addrs(t)[:1],
+                             local_frac=1.0, proxy_ident=proxy_identities(t))
+    else:
+        from .distributed import addr_keys, pair_owner
+        parts, got = [], 0
+        while got < n - m:
+            c = gen_headers_v4(rng, (n - m - got) * owner[1] * 5 // 4 + 1024, t.ipcache,
+                               local_v4_addrs(t)[:1], local_frac=1.0,
+                               proxy_ident=proxy_identities(t))
+            keep = pair_owner(addr_keys(c.saddr, 4), addr_keys(c.daddr, 4),
+                              owner[1]) == owner[0]
+            c = take(c, np.flatnonzero(keep)[:n - m - got])
+            parts.append(c)
+            got += len(c)
+        new = concat(parts)
     h = concat([old, new])
     perm = rng.permutation(n)
     if return_new:
@@ -1233,3 +1249,162 @@ def lb6_services(rng, t: Tables, n_services=24, n_backend_pool=None):
     rnr["port"] = 0
     rn.append(rnr)
     return (np.concatenate(rows), np.concatenate(rn), vips, ports, protos)
+
+
+# ---- LXC_NAT46 (lxc_config.h:28, nat46.h:30-32) -----------------------------
+
+
+def config_nat(seed=61, n_prefixes=2000, n_v4_prefixes=500, n_policy=300,
+               n_endpoints=2):
+    """Dual-stack tables for the NAT hops (oracle/gen_golden.py _nat_setup,
+    same recipe): IPv4 peers reached from the endpoint's IPv6 side through
+    ::ffff:0:0/96; EP_LXC_ID's egress policy admits WORLD (the IPv6 stage)
+    and 70% of the IPv4 identities (the IPv4 stage after NAT64), its ingress
+    policy half of them (the replies after NAT46); ::ffff:10.0.0.0/104 is
+    CLUSTER_ID (not translated, bpf_lxc.c:353-354).  -> (tables, IPv4
+    ipcache rows)"""
+    t = config_c3(seed, n_prefixes=n_prefixes, n_v4_prefixes=n_v4_prefixes,
+                  n_policy=n_policy, n_endpoints=n_endpoints, n_prefilter=0)
+    rng = np.random.default_rng(seed + 1)
+    cl = np.zeros(1, IPCACHE_DT)
+    cl["family"] = 2
+    cl["plen"] = 104
+    cl["addr"][0, 10:13] = [0xff, 0xff, 10]
+    cl["label"] = CLUSTER_ID
+    t.ipcache = np.concatenate([t.ipcache, cl])
+    ipc4 = t.ipcache[t.ipcache["family"] == 1]
+    ids4 = np.unique(ipc4["label"])
+    out_ok = rng.choice(ids4, size=int(0.7 * len(ids4)), replace=False)
+    in_ok = rng.choice(ids4, size=int(0.5 * len(ids4)), replace=False)
+    pol = t.policy[EP_LXC_ID]
+    add = np.zeros(1 + len(out_ok) + len(in_ok), POLICY_DT)
+    add["identity"][0] = WORLD_ID
+    add["egress"][0] = 1
+    add["identity"][1:1 + len(out_ok)] = out_ok
+    add["egress"][1:1 + len(out_ok)] = 1
+    add["identity"][1 + len(out_ok):] = in_ok
+    have = {(int(r["identity"]), int(r["dport"]), int(r["proto"]), int(r["egress"]))
+            for r in pol}
+    add = add[[(int(r["identity"]), 0, 0, int(r["egress"])) not in have for r in add]]
+    t.policy[EP_LXC_ID] = np.concatenate([pol, add])
+    return t, ipc4
+
+
+def v4_mapped(v4):
+    """::ffff:a.b.c.d of raw be32 IPv4 addresses -> (n, 16) u8"""
+    a = np.zeros((len(v4), 16), np.uint8)
+    a[:, 10:12] = 0xff
+    a[:, 12:16] = np.asarray(v4, np.uint32).view(np.uint8).reshape(-1, 4)
+    return a
+
+
+def nat64_flows(rng, ipc4, n, sport_base):
+    """n new IPv6 flows from EP_LXC_ID to v4-mapped peers inside IPv4 ipcache
+    prefixes: TCP 60% (SYN), UDP 25%, ICMPv6 echo 15%"""
+    peers = _addr_in_prefix_v4(rng, ipc4, rng.integers(0, len(ipc4), size=n))
+    r = rng.random(n)
+    proto = np.where(r < 0.6, IPPROTO_TCP,
+                     np.where(r < 0.85, IPPROTO_UDP, IPPROTO_ICMPV6)).astype(np.uint8)
+    h = Headers(6, np.tile(LXC_IPV6, (n, 1)), v4_mapped(peers),
+                htons((sport_base + np.arange(n)) & 0xFFFF),
+                htons(rng.choice(np.array([80, 443, 53, 8080]), size=n)),
+                proto, np.zeros(n, np.uint8),
+                rng.integers(100, 1500, size=n).astype(np.uint16), np.zeros(n, np.uint32))
+    ic = proto == IPPROTO_ICMPV6
+    h.sport[ic] = 128      # echo request
+    h.dport[ic] = htons((np.arange(int(ic.sum())) + 1) & 0xFFFF).astype(np.uint16)
+    h.tcpflags = np.where(proto == IPPROTO_TCP, 0x02, 0).astype(np.uint8)
+    return h
+
+
+def headers_nat64(t, ipc4, hist, n, seed=61):
+    """An IPv6 egress stream of EP_LXC_ID full of NAT64 (bpf_lxc.c:353-360):
+    later packets of the history's flows, new flows with several packets
+    (SYN, ACK, data, FIN), ICMPv6 errors of every icmp6_to_icmp4 outcome,
+    extension headers (DROP_INVALID_EXTHDR), CLUSTER-mapped peers and plain
+    IPv6 traffic, interleaved"""
+    rng = np.random.default_rng(seed + 500)
+    parts, pos = [], []
+
+    def add(h, p):
+        parts.append(h)
+        pos.append(p)
+    est = take(hist, rng.integers(0, len(hist), size=int(n * 0.35)))
+    est.tcpflags = np.where(est.proto == IPPROTO_TCP,
+                            rng.choice(np.array([0x10, 0x18], np.uint8), size=len(est)), 0
+                            ).astype(np.uint8)
+    est.length = rng.integers(100, 1500, size=len(est)).astype(np.uint16)
+    add(est, rng.random(len(est)))
+    new = nat64_flows(rng, ipc4, int(n * 0.1), 40000)
+    at = rng.random(len(new)) * 0.9
+    add(new, at)
+    for f, p_ in ((0x10, 0.8), (0x18, 0.5), (0x11, 0.3)):
+        sel = np.flatnonzero(rng.random(len(new)) < p_)
+        h = take(new, sel)
+        h.tcpflags = np.where(h.proto == IPPROTO_TCP, f, 0).astype(np.uint8)
+        if f == 0x11:
+            h.flags = np.where(h.proto == IPPROTO_TCP, HF_TCP_CLOSE, 0).astype(np.uint8)
+        at = at + rng.random(len(new)) * 0.03
+        add(h, at[sel])
+    k = int(n * 0.08)
+    e = nat64_flows(rng, ipc4, k, 50000)
+    tc = np.array([[1, 0], [1, 3], [1, 4], [1, 1], [1, 7], [2, 0], [3, 0], [3, 1],
+                   [4, 0], [4, 1], [4, 2], [137, 0]], np.uint16)
+    pick = tc[rng.integers(0, len(tc), size=k)]
+    e.proto[:] = IPPROTO_ICMPV6
+    e.sport[:] = (pick[:, 0] | pick[:, 1] << 8).astype(np.uint16)
+    e.dport[:] = 0
+    e.tcpflags = np.zeros(k, np.uint8)
+    add(e, rng.random(k))
+    x = nat64_flows(rng, ipc4, int(n * 0.03), 60000)
+    x.flags[:] |= np.uint8(HF_EXTHDR)
+    add(x, rng.random(len(x)))
+    c = nat64_flows(rng, ipc4, int(n * 0.04), 61000)
+    c.daddr[:, 12] = 10
+    add(c, rng.random(len(c)))
+    plain = gen_headers_v6(rng, int(n * 0.1), t.ipcache[t.ipcache["family"] == 2],
+                           local_v6_addrs(t), local_frac=0.3, mark_host=0,
+                           mark_proxy=0, src_fixed=LXC_IPV6, ext=0, exthdr_drop=0)
+    add(plain, rng.random(len(plain)))
+    h = concat(parts)
+    h = take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    return h.slice(0, n)
+
+
+def headers_nat46(t, ipc4, hist, hist_ok, n, seed=63):
+    """An IPv4 ingress stream toward EP_LXC_ID's IPv4 address: replies from
+    the peers of the history's NAT64 flows (hist_ok: the flows that were
+    forwarded), ICMP errors about them (every icmp4_to_icmp6 case), and new
+    IPv4 traffic; the replies of a flow several times, in order"""
+    rng = np.random.default_rng(seed + 500)
+    m = int(n * 0.6)
+    pick = hist_ok[rng.integers(0, len(hist_ok), size=m)]
+    src = take(hist, pick)
+    peer = np.ascontiguousarray(src.daddr[:, 12:16]).view("<u4").ravel()
+    icmp = src.proto == IPPROTO_ICMPV6
+    rep = Headers(4, peer.copy(), np.full(m, LXC_IPV4, np.uint32),
+                  np.where(icmp, 0, src.dport).astype(np.uint16),
+                  np.where(icmp, src.dport, src.sport).astype(np.uint16),
+                  np.where(icmp, IPPROTO_ICMP, src.proto).astype(np.uint8),
+                  np.zeros(m, np.uint8), rng.integers(60, 1500, size=m).astype(np.uint16),
+                  np.zeros(m, np.uint32))
+    rep.tcpflags = np.where(rep.proto == IPPROTO_TCP,
+                            rng.choice(np.array([0x12, 0x10, 0x18], np.uint8), size=m), 0
+                            ).astype(np.uint8)
+    fin = (rep.proto == IPPROTO_TCP) & (rng.random(m) < 0.05)
+    rep.flags[fin] = HF_TCP_CLOSE
+    rep.tcpflags[fin] = 0x11
+    k = int(n * 0.12)
+    ep_ = take(rep, rng.integers(0, m, size=k))
+    tc = np.array([[3, 0], [3, 1], [3, 2], [3, 3], [3, 4], [3, 5], [3, 9], [3, 13],
+                   [3, 14], [11, 0], [12, 0], [5, 0]], np.uint16)
+    pick2 = tc[rng.integers(0, len(tc), size=k)]
+    ep_.proto[:] = IPPROTO_ICMP
+    ep_.sport[:] = (pick2[:, 0] | pick2[:, 1] << 8).astype(np.uint16)
+    ep_.dport[:] = 0
+    ep_.flags[:] = 0
+    ep_.tcpflags = np.zeros(k, np.uint8)
+    new = gen_headers_v4(rng, n - m - k, ipc4, local_v4_addrs(t)[:1], local_frac=1.0,
+                         mark_host=0, mark_proxy=0, frag=0)
+    h = concat([rep, ep_, new])
+    return take(h, rng.permutation(len(h)))

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 10
+#define CFC_ABI_VERSION 11
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -271,9 +271,17 @@ typedef struct {
  *            the batch started: bits 0-1 CT_NEW 0 / ESTABLISHED 1 / REPLY 2 /
  *            RELATED 3, bit 2 looked up, bit 3 a new flow the reference
  *            would ct_create; bits 4-7 the same for the destination
- *            endpoint's ingress lookup after egress local delivery.  Feed it
- *            to cfc_ct_apply_v4/v6 to fold creates, deletes and closing
- *            flags into the CT maps. */
+ *            endpoint's ingress lookup after egress local delivery, or for
+ *            the other family's lookup after a NAT hop (LXC_NAT46,
+ *            lxc_config.h:28 / nat46.h:30-32: an IPv6 egress header to a
+ *            v4-mapped peer outside the cluster re-runs as IPv4 through the
+ *            endpoint's IPv4 egress path, bpf_lxc.c:353-360, 1070-1083; an
+ *            IPv4 ingress header whose CT entry carries nat46 re-runs as IPv6
+ *            through ipv6_policy, bpf_lxc.c:939-944, 1098-1110 — its verdict,
+ *            identity, action and event are the hop's).  Feed it to
+ *            cfc_ct_apply_v4/v6 of the same batch (cfc_classify's outputs
+ *            untouched in between) to fold creates, deletes and closing flags
+ *            into the CT maps, the hop's into the other family's. */
 #define CFC_CT_RES_MASK 0x3u
 #define CFC_CT_DONE 0x4u
 #define CFC_CT_CREATE 0x8u
@@ -311,6 +319,11 @@ typedef struct {
 #define CFC_NT_EGRESS 2u
 #define CFC_NT_POLICY 3u
 #define CFC_NT_TRACE 4u
+/* bit 24 of a nonzero word: the event was sent after a NAT hop (LXC_NAT46,
+ * below) — the record's skb->len is the translated packet's (an IPv6
+ * header's batch: 20 bytes less; an IPv4 one's: 20 more), its tuple the
+ * header's own */
+#define CFC_NT_NATLEN 0x01000000u
 typedef struct {
     int32_t *verdict;
     uint32_t *identity;
@@ -581,6 +594,9 @@ typedef struct {
     uint32_t ct_order_changed;
     /* CT slots of the device tables (both families) */
     uint32_t ct_slots;
+    /* headers that took a NAT46 / NAT64 hop (cfc_classify_*), since the
+     * context opened */
+    uint32_t nat_hops;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

@@ -554,11 +554,15 @@ int cfo_endpoint_add(cfo_t *o, int family, const uint8_t addr[16],
     }
     o->eps[o->neps] = (epinfo){ifindex, flags, lxc_id};
     ht_put(&o->lxc, k, o->neps++);
+    /* LXC_IPV4 / LXC_IP of the endpoint (the NAT46 / NAT64 addresses): the
+     * lowest address of the family among its cilium_lxc entries (an
+     * endpoint normally has one per family; the engine picks the same) */
     if (!(flags & ENDPOINT_F_HOST)) {
-        if (family == 1 && !o->ep_has4[lxc_id]) {
+        if (family == 1 && (!o->ep_has4[lxc_id] || memcmp(addr, &o->ep_v4[lxc_id], 4) < 0)) {
             memcpy(&o->ep_v4[lxc_id], addr, 4);
             o->ep_has4[lxc_id] = 1;
-        } else if (family == 2 && !o->ep_has6[lxc_id]) {
+        } else if (family == 2 &&
+                   (!o->ep_has6[lxc_id] || memcmp(addr, o->ep_v6[lxc_id], 16) < 0)) {
             memcpy(o->ep_v6[lxc_id], addr, 16);
             o->ep_has6[lxc_id] = 1;
         }

@@ -217,3 +217,32 @@ def test_two_rank_conntrack_shards(family):
     got = _sorted_rows(res[0][2])
     assert len(want) > 1000
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_c5_rank_setup_partitions_ct_and_stream(world):
+    """bench.py --workload c5 --gpus N: each rank loads the CT entries of the
+    address pairs it owns and draws its stream from its own live flows and
+    new flows it owns (distributed.c5_rank_setup, synth.headers_c5(owner)).
+    The ranks' CT shards partition the node's entries; every header of a
+    rank's stream is that rank's under shard_headers; the live flows'
+    headers find their entries in the rank's own shard."""
+    from cilium_amd.distributed import addr_keys, c5_rank_setup, pair_owner, shard_headers
+    t, flows = S.config_c5(5, n_flows=20_000, n_prefixes=5_000, n_policy=500)
+    full = np.sort(t.ct.view(np.dtype((np.void, t.ct.dtype.itemsize))).ravel())
+    shards, nflows = [], 0
+    for r in range(world):
+        ct_r, fl_r = c5_rank_setup(t, flows, r, world)
+        shards.append(ct_r)
+        nflows += len(fl_r)
+        own = pair_owner(addr_keys(fl_r.saddr, 4), addr_keys(fl_r.daddr, 4), world)
+        assert (own == r).all()
+        h, new = S.headers_c5(t, fl_r, 5000, seed=100 + r, return_new=True,
+                              owner=(r, world))
+        assert len(h) == 5000 and new.sum() == 5000 - int(5000 * 0.95)
+        mine, idx = shard_headers(h, r, world)
+        assert len(idx) == len(h)   # every header is the rank's own
+    assert nflows == len(flows)
+    got = np.sort(np.concatenate(shards).view(
+        np.dtype((np.void, t.ct.dtype.itemsize))).ravel())
+    np.testing.assert_array_equal(got, full)   # a partition: nothing lost or doubled
