@@ -14,7 +14,7 @@ CFC_DEVICE_NONE = -1
 MODE_INGRESS, MODE_EGRESS, MODE_XDP, MODE_FULL = 0, 1, 2, 3
 HF_FRAG, HF_TCP_CLOSE, HF_EXTHDR = 0x100, 0x200, 0x400
 DROP_PREFILTER, VERDICT_PUNT = -1, -2
-OPT_LPM4, OPT_TIMING, OPT_CT_APPLY = 1, 2, 3
+OPT_LPM4, OPT_TIMING, OPT_CT_APPLY, OPT_CT_EVICT = 1, 2, 3, 4
 CT_APPLY_DEVICE, CT_APPLY_HOST = 0, 1
 LPM4_AUTO, LPM4_DIR24_8, LPM4_TRIE = 0, 1, 2
 
@@ -110,7 +110,8 @@ class Stats(ctypes.Structure):
                 ("ct_apply_host", ctypes.c_uint32),
                 ("ct_order_changed", ctypes.c_uint32),
                 ("ct_slots", ctypes.c_uint32),
-                ("nat_hops", ctypes.c_uint32)]
+                ("nat_hops", ctypes.c_uint32),
+                ("ct_evicted", ctypes.c_uint32)]
 
 
 class NodeConfig(ctypes.Structure):

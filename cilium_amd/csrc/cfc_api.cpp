@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -197,6 +198,10 @@ struct cfc_ctx {
     DevBuf nat_list, nat_cnt, nat_tmp;
     bool nat46_seen = false, hop_nat46 = false;
     uint64_t n_nat_hops = 0;
+    // eviction at a CT map's capacity (ct_evict; CFC_OPT_CT_EVICT)
+    bool ct_evict = true;
+    DevBuf evict_bm, evict_hist;
+    uint64_t n_evicted = 0;
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -1590,6 +1595,11 @@ int cfc_set_option(cfc_ctx *c, int option, int64_t value)
             return -EINVAL;
         c->ct_apply_mode = (int)value;
         return 0;
+    case CFC_OPT_CT_EVICT:
+        if (value != 0 && value != 1)
+            return -EINVAL;
+        c->ct_evict = value != 0;
+        return 0;
     default:
         return -EINVAL;
     }
@@ -2302,8 +2312,13 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     *st = c->epoch->st;
     st->ct_apply_device = c->n_apply_dev;
     st->ct_apply_host = c->n_apply_host;
-    st->ct_order_changed = (uint32_t)c->n_ord_changed;
+    uint32_t dev_changed = 0;   // (the device applies' count, kept on the device)
+    if (c->ord_cnt.p)
+        (void)hipMemcpy(&dev_changed, (uint32_t *)c->ord_cnt.p + ORD_CHANGED, 4,
+                        hipMemcpyDeviceToHost);
+    st->ct_order_changed = (uint32_t)c->n_ord_changed + dev_changed;
     st->nat_hops = (uint32_t)c->n_nat_hops;
+    st->ct_evicted = (uint32_t)c->n_evicted;
     st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->ct4_host.size() + c->epoch->ct->ct6_host.size())
                             : 0u;
     return 0;
@@ -2785,6 +2800,78 @@ void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t 
         (void)hipMemsetAsync((char *)c->epoch->ct->ct_acct.p + 32 * slot, 0, 32, s);
 }
 
+int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
+              cfc_ct_gc_stats &st, hipStream_t s, const uint32_t *protect);
+
+// A batch whose creates would take an IPv4 CT map past max_entries: the
+// reference's LRU hash evicts its least recently used entries as the
+// inserts come (kernel order, per-CPU lists — not reproducible).  The device
+// frees room the same way a GC does, before the inserts: the map's entries
+// closest to their expiry (a histogram of lifetimes, then the GC pass up to
+// the second that covers `excess`; entries expiring in the same second go
+// together), never one this batch's lookups hit (they are the most recently
+// used).  0: done, -ENOSPC: not enough evictable entries (host walk).
+int ct_evict(cfc_ctx *c, Map *m, uint64_t excess, const uint32_t *hs, uint64_t nk, hipStream_t s)
+{
+    Epoch &E = *c->epoch;
+    GCt &G = *E.ct;
+    const uint64_t slots = G.ct4_host.size();
+    constexpr uint32_t NB = 1u << 16;
+    if (c->evict_bm.ensure(4 * ((slots + 31) / 32)) || c->evict_hist.ensure(4ull * NB))
+        return -ENOMEM;
+    uint32_t *bm = (uint32_t *)c->evict_bm.p, *hist = (uint32_t *)c->evict_hist.p;
+    const uint32_t mw = ct_owner_word((uint32_t)std::max(m->policy_lxc, 0), m->policy_lxc >= 0) |
+                        (m->ct_any ? 2u : 0u);
+    // lifetimes run from the past to now + CT_LIFETIME_TCP (21600 s)
+    const uint32_t base = c->now > NB - 21601 ? c->now - (NB - 21601) : 0u;
+    std::vector<uint32_t> h(NB);
+    if (hipMemsetAsync(bm, 0, c->evict_bm.bytes, s) != hipSuccess ||
+        hipMemsetAsync(hist, 0, 4ull * NB, s) != hipSuccess || ct_protect_hits(hs, nk, bm, s) ||
+        ct_evict_hist((const Ct4Slot *)G.ct4.p, (const CtTimer *)G.ct4_tm.p, slots, mw, bm, base,
+                      hist, NB, s) ||
+        hipMemcpyAsync(h.data(), hist, 4ull * NB, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    // the TCP map's ICMP entries live on the host only (no lookup reaches
+    // them): theirs too
+    auto life_of = [](const std::string &v) {
+        uint32_t l = 0;
+        if (v.size() >= 36)
+            memcpy(&l, &v[32], 4);
+        return l;
+    };
+    if (m->n_aux)
+        for (auto &kv : m->kv)
+            if (m->aux_key(kv.first)) {
+                const uint32_t l = life_of(kv.second.val);
+                h[l < base ? 0u : std::min(l - base, NB - 1)]++;
+            }
+    uint64_t cum = 0;
+    uint32_t b = 0;
+    while (b < NB && cum < excess)
+        cum += h[b++];
+    if (cum < excess)
+        return -ENOSPC;
+    cfc_ct_gc_filter f{};
+    f.flags = CFC_GC_REMOVE_EXPIRED;
+    f.time = base + b;   // lifetime < base + b: buckets [0, b)
+    cfc_ct_gc_stats st{};
+    if (int rc = ct_gc_dev(c, std::vector<Map *>{m}, f, st, s, bm))
+        return rc;
+    uint64_t aux = 0;
+    if (m->n_aux)
+        for (auto it = m->kv.begin(); it != m->kv.end();) {
+            if (m->aux_key(it->first) && life_of(it->second.val) < f.time) {
+                it = m->ct_erase_at(it, false);
+                aux++;
+            } else {
+                ++it;
+            }
+        }
+    c->n_evicted += st.device_deleted + st.log_deleted + aux;
+    return 0;
+}
+
 // cfc_ct_apply_v4/v6 on the device (ctapply.hip).  1: take the host path
 // instead (nothing changed), 0 done, <0 error.
 template <class Hdr>
@@ -2904,7 +2991,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     if (may_grow && !lbm) {
         if (c->ord_delbm.bytes < obm_bytes && c->ord_delbm.zeros(obm_bytes, s))
             return -ENOMEM;
-        if (c->ord_cnt.ensure(4 * ORD_NCNT))
+        if (!c->ord_cnt.p && c->ord_cnt.zeros(4 * ORD_NCNT, s))   // (ORD_CHANGED accumulates)
             return -ENOMEM;
         OrdArgs O{};
         O.ctb = out->ct;
@@ -2937,8 +3024,11 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     uint64_t &log_used = V6 ? c->log6_used : c->log_used;
     DevBuf &logbuf = V6 ? c->cta_log6 : c->cta_log;
     const size_t log_rec = V6 ? sizeof(CtLog6) : sizeof(CtLog);
-    const uint64_t used = V6 ? (uint64_t)G.n_ct6 + G.tomb6
-                             : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
+    auto used_now = [&]() -> uint64_t {
+        return V6 ? (uint64_t)G.n_ct6 + G.tomb6
+                  : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
+    };
+    uint64_t used = used_now();
     const uint64_t nr = std::max<uint64_t>(nreqA, 1);
     const uint64_t cx_cap = nhit + k3 * nreqA + 64;
     const uint64_t log_need = log_used + nreqA;
@@ -3005,6 +3095,24 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             return ct_apply_dev(c, in, out, mode, ep_lxc, s, false);
         }
     }
+    if (!V6 && ok && fits(newk) && !maps_fit() && c->ct_evict) {
+        // an IPv4 map at capacity: evict on the device (ct_evict), then
+        // decide again
+        const uint64_t nk = lbm ? 4 * n : mode == CFC_MODE_EGRESS ? 2 * n : n;
+        for (auto &kv : c->maps) {
+            Map *m = kv.second.get();
+            if (m->role != ROLE_CT4)
+                continue;
+            const uint64_t want = m->kv.size() - m->gc_pending + claims + log_used +
+                                  newk_kind[m->ct_any ? 1 : 0];
+            if (want <= m->max_entries)
+                continue;
+            const int rc = ct_evict(c, m, want - m->max_entries, A.hs, nk, s);
+            if (rc && rc != -ENOSPC)
+                return rc;
+        }
+        used = used_now();
+    }
     ok = ok && room(newk);
     if (!ok && getenv("CFC_DEBUG_APPLY"))
         fprintf(stderr, "cfc: CT apply to the host path: %llu requests, %llu new keys, "
@@ -3041,9 +3149,9 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     // from here the device table changes: the host mirror lags until ct_sync
     c->ct_dirty = true;
     c->ct6_dirty |= V6;
+    // (no wait for the fold: the host's bookkeeping below was read after
+    // route, the rest is stream-ordered before anything that reads the table)
     int rc = cta_rest(A, V6, (uint32_t)nreqA, presorted, hc, s);
-    if (!rc && hipStreamSynchronize(s) != hipSuccess)
-        rc = -EIO;
     if (rc) {
         // the table may hold some of the batch's inserts: no per-slot mark
         // or summary may leak into the next apply, the claims made count,
@@ -3136,17 +3244,22 @@ int ct_apply_one(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int 
     // by the device, so the walk counts it
     // (keyed by map and tuple: one tuple can live in several maps, e.g. a
     // TCP and a UDP create's ICMP entry, or a global and a local map)
+    // (and a hit after this walk wrote the key anew — a related entry a later
+    // create overwrote — counts too: the device's count of it went with the
+    // entry the write replaced, ct_drop_counts)
     std::map<std::pair<const Map *, std::string>, bool> initial;
+    std::set<std::pair<const Map *, std::string>> written;
     auto note = [&](Map *mp, const std::string &key) {
         initial.emplace(std::make_pair((const Map *)mp, key), mp->kv.count(key) != 0);
     };
     auto put_new = [&](Map *mp, const std::string &key, const CtEntry &e) {
         note(mp, key);
+        written.emplace((const Map *)mp, key);
         (void)mp->update(key.data(), &e, 0);
     };
     auto fresh = [&](const Map *mp, const std::string &key) {
         auto it = initial.find(std::make_pair(mp, key));
-        return it != initial.end() && !it->second;
+        return (it != initial.end() && !it->second) || written.count(std::make_pair(mp, key));
     };
     bool ct_changed = false;   // (CT bytes the packet order changed)
     for (size_t i = 0; i < n; i++) {
@@ -3486,7 +3599,7 @@ struct GcFilterHost {
 
 // the IPv4 part on the device: the CT table and the pending CtLog
 int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
-              cfc_ct_gc_stats &st, hipStream_t s)
+              cfc_ct_gc_stats &st, hipStream_t s, const uint32_t *protect)
 {
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
@@ -3566,6 +3679,7 @@ int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter 
         A.log = (CtGcRec *)c->gc_log.p + c->gc_log_used + deleted;
         A.log_cap = (uint32_t)(c->gc_log.bytes / sizeof(CtGcRec) - c->gc_log_used - deleted);
         A.cnt = cnt;
+        A.protect = protect;
         uint32_t hc[CTG_NCNT], hm[CTG_MAX_MAPS];
         if (hipMemcpyAsync(sets, hs.data(), 4 * hs.size(), hipMemcpyHostToDevice, s) !=
                 hipSuccess ||
@@ -3654,7 +3768,7 @@ int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, h
         if (int rc = ct_sync(c, s))
             return rc;
     if (dev4)
-        if (int rc = ct_gc_dev(c, sel, *f, st, s))
+        if (int rc = ct_gc_dev(c, sel, *f, st, s, nullptr))
             return rc;
     // what only the host holds: IPv6 maps, IPv4 maps without a device
     // table, IPv4 TCP maps' ICMP entries

@@ -368,8 +368,17 @@ struct CtGcArgs {
     CtGcRec *log;
     uint32_t log_cap;
     uint32_t *cnt;                // CTG_* counters
+    const uint32_t *protect;      // slots never deleted (one bit each), or null
 };
 int ct_gc4(const CtGcArgs &A, hipStream_t s);
+// Eviction at a CT map's capacity (cfc_ct_apply, cfc_api.cpp ct_evict):
+// the slots a batch's lookups hit (hs: nk hit-slot words, HS_NONE none) as
+// bits in bm, then a histogram of the lifetimes of map `mw`'s other
+// entries (the selector word of CtGcArgs.maps): hist[b] counts lifetime
+// base + b (clamped to [0, nb))
+int ct_protect_hits(const uint32_t *hs, uint64_t nk, uint32_t *bm, hipStream_t s);
+int ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm, uint64_t slots, uint32_t mw,
+                  const uint32_t *bm, uint32_t base, uint32_t *hist, uint32_t nb, hipStream_t s);
 // the pending TCP-map ICMP entries of the device applies (CtLog) filtered the
 // same way, kept in order of appearance: in[0, n) -> out; the kept count
 // into A.cnt[CTG_LOGKEPT]

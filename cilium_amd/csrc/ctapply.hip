@@ -972,7 +972,10 @@ __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx
         return;
     const uint64_t omask = (1ull << A.ob) - 1;
     bool k = true;
-    if (r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob)) {
+    // (a slot this batch writes keeps every hit: after the write each one
+    // counts in the fold)
+    if (r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob) &&
+        !(A.ms[(uint32_t)(cx[r] >> A.ob)].x & MARK_PUTC)) {
         const uint32_t s1 = hit_sig<V6>(A, (uint32_t)(cx[r] & omask));
         k = !s1 || s1 != hit_sig<V6>(A, (uint32_t)(cx[r - 1] & omask));
     }
@@ -1069,6 +1072,13 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
             }
         } else if (live) {   // OP_HIT, OP_DELETE
             put_mon(A, ord, hit(e, A.now, o));
+            if (created) {
+                // a hit after this batch wrote the entry anew (a related
+                // entry overwritten by a later create): the launch counted it
+                // on the entry as it was, which the write replaced
+                acct[d] += 1;
+                acct[d + 1] += o.len;
+            }
             if (o.kind == OP_DELETE) {
                 live = false;
                 deleted = true;
@@ -1188,8 +1198,10 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 // batch whose caller wants the event words): the stage the trace reports
 // (local delivery's when it ran) with the result the packet order gave it
 // (ctorder.hip) and the length __ct_lookup then left (the fold's; a repeat
-// of the same hit that the fold skipped reports nothing: its state update
-// already happened), conn_is_dns's MTU (conntrack.h:585-586)
+// of the same hit that the fold skipped reports nothing — its state update
+// already happened — except a close: ACTION_CLOSE reports TRACE_PAYLOAD_LEN
+// whatever the entry's state, conntrack.h:268-281), conn_is_dns's MTU
+// (conntrack.h:585-586)
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_mon(CtaArgs A)
 {
@@ -1214,7 +1226,10 @@ __global__ __launch_bounds__(256) void k_cta_mon(CtaArgs A)
             m = TRACE_PAYLOAD_LEN;
     }
     const CtProbe k = ct_probe<V6>(proto, A.pt[i], CT_INGRESS, 0);
-    if ((res >= CT_REPLY ? k.td : k.ts) == 0x3500u)   // conn_is_dns: htons(53)
+    // (ipv6_l3_from_lxc sets TRACE_PAYLOAD_LEN after its ct_create6,
+    // bpf_lxc.c:248: a new flow's egress trace is not captured at MTU)
+    const bool v6_new_egress = V6 && A.mode == CFC_MODE_EGRESS && st == 0 && res == CT_NEW;
+    if ((res >= CT_REPLY ? k.td : k.ts) == 0x3500u && !v6_new_egress)   // conn_is_dns
         m = MTU_LEN;
     A.nt[i] = (w & 0x000FFFFFu) | res << 20 | mon_class(m) << 22;
 }
@@ -1428,7 +1443,8 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {
             const uint64_t s = base + u * 256 + threadIdx.x;
-            del[u] = j[u] >= 0 && gc_delete(A, k[u].x, k[u].y, life[u]);
+            del[u] = j[u] >= 0 && gc_delete(A, k[u].x, k[u].y, life[u]) &&
+                     !(A.protect && ((A.protect[s >> 5] >> (s & 31)) & 1u));
             infy[u] = del[u] ? A.info[s].y : 0u;
         }
         uint32_t nl = 0;
@@ -1523,6 +1539,31 @@ __global__ __launch_bounds__(256) void k_ct_gc_log(CtGcArgs A, const CtLog *in, 
     const uint32_t r = wave_count(&A.cnt[CTG_LOGKEPT], keep);
     if (keep)
         out[r] = g;
+}
+
+__global__ __launch_bounds__(256) void k_ct_protect(const uint32_t *hs, uint64_t nk, uint32_t *bm)
+{
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t sl = k < nk ? hs[k] : HS_NONE;
+    if (sl != HS_NONE)
+        atomicOr(&bm[sl >> 5], 1u << (sl & 31));
+}
+__global__ __launch_bounds__(256) void k_ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm,
+                                                       uint64_t slots, uint32_t mw,
+                                                       const uint32_t *bm, uint32_t base,
+                                                       uint32_t *hist, uint32_t nb)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += stride) {
+        const uint32_t w = ct4[s].w;
+        if (!w || (w & 0xF000u) ||
+            ((w & 0xFFFF0800u) | ((w & 0xFF) != 6 ? 2u : 0u)) != mw ||
+            ((bm[s >> 5] >> (s & 31)) & 1u))
+            continue;
+        const uint32_t life = tm[s].lifetime;
+        const uint32_t b = life < base ? 0u : min(life - base, nb - 1);
+        atomicAdd(&hist[b], 1u);
+    }
 }
 
 unsigned blocks_for(uint64_t n, unsigned cap)
@@ -1673,6 +1714,22 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
                        dim3(256), 0, s, A);
     if (A.nt && A.mon && A.n)
         hipLaunchKernelGGL(k_cta_mon<V6>, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_protect_hits(const uint32_t *hs, uint64_t nk, uint32_t *bm, hipStream_t s)
+{
+    if (nk)
+        hipLaunchKernelGGL(k_ct_protect, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, hs,
+                           nk, bm);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm, uint64_t slots, uint32_t mw,
+                  const uint32_t *bm, uint32_t base, uint32_t *hist, uint32_t nb, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_ct_evict_hist, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4, tm,
+                       slots, mw, bm, base, hist, nb);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

@@ -357,8 +357,8 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         return hipMemcpyAsync(hc, O.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) == hipSuccess &&
                hipStreamSynchronize(s) == hipSuccess;
     };
-    *changed = 0;
-    if (hipMemsetAsync(O.cnt, 0, sizeof(hc), s) != hipSuccess)
+    *changed = 0;   // (ORD_CHANGED accumulates on the device: no wait for it)
+    if (hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
         return -EIO;
     O.part = nullptr;
     if (two)
@@ -460,9 +460,6 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
                                0, s, A, O);
     }
     hipLaunchKernelGGL(k_ord_write, dim3(gp), dim3(256), 0, s, A, O, npi);
-    if (!rd())
-        return -EIO;
-    *changed = hc[ORD_CHANGED];
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

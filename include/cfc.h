@@ -173,7 +173,13 @@ int cfc_commit(cfc_ctx *ctx, void *stream);
  * batch's CT writes to the device CT table in place and keeps the host's
  * view of the CT maps lazily (synchronised when a CT map is next read or
  * written through this API, or at cfc_counters_sync); HOST walks the batch
- * on the host.  Both give the same maps. */
+ * on the host.  Both give the same maps.
+ * CFC_OPT_CT_EVICT: 1 (default) = a batch whose creates would take an IPv4
+ * CT map past its max_entries stays on the device: the map's entries
+ * closest to expiry that the batch's lookups did not hit are deleted first
+ * (as a GC would; the reference's LRU hash evicts its least recently used
+ * entries instead, in an order the kernel's per-CPU lists decide); 0 = such
+ * a batch takes the host walk, whose maps evict in LRU order. */
 #define CFC_OPT_LPM4 1
 #define CFC_LPM4_AUTO 0
 #define CFC_LPM4_DIR24_8 1
@@ -182,6 +188,7 @@ int cfc_commit(cfc_ctx *ctx, void *stream);
 #define CFC_OPT_CT_APPLY 3
 #define CFC_CT_APPLY_DEVICE 0
 #define CFC_CT_APPLY_HOST 1
+#define CFC_OPT_CT_EVICT 4
 int cfc_set_option(cfc_ctx *ctx, int option, int64_t value);
 
 /* ---------------------------------------------------------------- datapath */
@@ -375,10 +382,17 @@ int cfc_classify_v6(cfc_ctx *ctx, const cfc_hdr_v6 *in, const cfc_out *out,
  * entry), ct_delete for established flows the policy now denies, the
  * closing flags of RST/FIN (CFC_HF_TCP_CLOSE) and re-opening.  A flow seen
  * twice in one batch is created once and counted on its second packet.
- * Lookups inside one batch all see the maps as committed before it.
- * IPv4 runs on the device (CFC_OPT_CT_APPLY) unless the CT table could pass
- * 3/4 load or a CT map its max_entries, or host-side CT map changes wait
- * for a commit: then, and for IPv6, on the host.
+ * The classify launch looked every header up against the maps as committed
+ * before the batch; the apply first rewrites the CT bytes (and, with
+ * out->notify, the trace words' reason and monitor length) into what the
+ * reference's packet-at-a-time run gives — a later packet of a flow the
+ * batch created is ESTABLISHED, a packet after a delete is NEW — and then
+ * applies the writes.  A batch with a NAT hop (cfc_classify kept its hop
+ * batch) folds the hop's stage into the other family's maps too.
+ * Runs on the device (CFC_OPT_CT_APPLY) unless host-side CT map changes
+ * wait for a commit, or an IPv6 (or, with CFC_OPT_CT_EVICT 0, an IPv4) CT
+ * map could pass its max_entries: then on the host.  A table that would
+ * pass 3/4 load is rebuilt larger.
  * Synchronises `stream`. */
 int cfc_ct_apply_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
@@ -597,6 +611,9 @@ typedef struct {
     /* headers that took a NAT46 / NAT64 hop (cfc_classify_*), since the
      * context opened */
     uint32_t nat_hops;
+    /* CT entries deleted to make room at a map's max_entries on the device
+     * (CFC_OPT_CT_EVICT), since the context opened */
+    uint32_t ct_evicted;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

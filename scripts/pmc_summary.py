@@ -6,7 +6,7 @@ on gfx950; the random 4-64 B lookups are reported as measured).
 
 usage: python3 scripts/pmc_summary.py OUTDIR [kernel-substring]
            [--save PROFILE_DIR]
-           [--record WORKLOAD MODE LPM4_LAYOUT KERNEL:HEADERS:STREAM_BYTES ...]
+           [--record WORKLOAD MODE LPM4_LAYOUT [variant=V] KERNEL:HEADERS:STREAM_BYTES ...]
 
 --save copies the kernel statistics, the engine's rows of every counter pass
 (cfc:: kernels only) and this summary into PROFILE_DIR (the committed
@@ -14,7 +14,11 @@ profiles/ tree).
 
 --record adds (or replaces) this configuration's entry in
 profiles/pmc_traffic.json, which bench.py reads for its roofline when the
-workload, mode, ipcache layout and per-kernel batch sizes match: per kernel
+workload, mode, ipcache layout, variant (lookup: classify only — the
+default; ct_apply: classify + cfc_ct_apply + GC, whose classify kernel also
+stores the CT bytes; notify) and per-kernel batch sizes match.  A spec
+KERNEL:0:0 records a kernel without a batch size (the apply's and GC's, per
+launch).  Per kernel
 the L2 requests per launch (TCC_REQ_sum) and the HBM-side bytes per launch =
 FETCH_SIZE + 1/2 x the streamed input bytes (HEADERS x STREAM_BYTES, which
 FETCH_SIZE counts at half on gfx950) + WRITE_SIZE.
@@ -90,6 +94,10 @@ def save(out, dst, res):
 
 def record(res, workload, mode, layout, specs, source):
     """Write this configuration's per-kernel entry into profiles/pmc_traffic.json."""
+    variant = "lookup"
+    if specs and specs[0].startswith("variant="):
+        variant = specs[0].split("=", 1)[1]
+        specs = specs[1:]
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         db = json.load(open(path))
@@ -99,7 +107,9 @@ def record(res, workload, mode, layout, specs, source):
     kern = {}
     for spec in specs:
         k, n, sb = spec.split(":")
-        c = res["counters"][k]
+        c = res["counters"].get(k)
+        if c is None or "TCC_REQ_sum" not in c or k not in res["kernels"]:
+            continue
         kern[k] = {
             "headers": int(n),
             "stream_read_bytes_per_header": float(sb),
@@ -108,12 +118,15 @@ def record(res, workload, mode, layout, specs, source):
             "l2_misses_per_launch": c.get("TCC_MISS_sum"),
             "hbm_bytes_per_launch": (c["FETCH_SIZE"] * 1024 + 0.5 * int(n) * float(sb)
                                      + c["WRITE_SIZE"] * 1024),
+            "write_bytes_per_launch": c["WRITE_SIZE"] * 1024,
             "avg_ms": res["kernels"][k]["avg_ms"],
+            "calls": res["kernels"][k]["calls"],
         }
-    e = {"workload": workload, "mode": mode, "lpm4_layout": layout,
+    e = {"workload": workload, "mode": mode, "lpm4_layout": layout, "variant": variant,
          "source": source, "kernels": kern}
     entries = [x for x in entries
-               if (x["workload"], x["mode"], x["lpm4_layout"]) != (workload, mode, layout)]
+               if (x["workload"], x["mode"], x["lpm4_layout"], x.get("variant", "lookup")) !=
+               (workload, mode, layout, variant)]
     entries.append(e)
     with open(path, "w") as f:
         json.dump({"entries": entries}, f, indent=1)
