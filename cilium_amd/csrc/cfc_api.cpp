@@ -1030,8 +1030,9 @@ void assemble(Epoch &E)
     T.pol_bloom = (const uint32_t *)D.polbloom.p;
     T.pol_bloom_words = D.pol_bloom_words;
     T.n_ctr = (uint32_t)D.ctr_owner.size();
-    T.ct4 = C.n_ct4 ? (const Ct4Slot *)C.ct4.p : nullptr;
-    T.ct6 = C.n_ct6 ? (const Ct6Slot *)C.ct6.p : nullptr;
+    // (a table a device apply may fill counts even while empty)
+    T.ct4 = (C.n_ct4 || !C.ct4_host.empty()) ? (const Ct4Slot *)C.ct4.p : nullptr;
+    T.ct6 = (C.n_ct6 || !C.ct6_host.empty()) ? (const Ct6Slot *)C.ct6.p : nullptr;
     T.ct_acct = (uint64_t *)C.ct_acct.p;
     T.ct4_tm = (const CtTimer *)C.ct4_tm.p;
     T.ct6_tm = (const CtTimer *)C.ct6_tm.p;
@@ -2876,7 +2877,7 @@ int ct_evict(cfc_ctx *c, Map *m, uint64_t excess, const uint32_t *hs, uint64_t n
 // instead (nothing changed), 0 done, <0 error.
 template <class Hdr>
 int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16_t ep_lxc,
-                 hipStream_t s, bool may_grow = true)
+                 hipStream_t s, bool may_grow = true, bool order = true)
 {
     constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
@@ -2906,6 +2907,26 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     const bool lbm = lbt && mode == CFC_MODE_EGRESS;
     const uint64_t k3 = lbm ? 3 : 2;   // requests per header, writes per create
     const uint64_t n = in->n, slots = V6 ? G.ct6_host.size() : G.ct4_host.size();
+    if (!slots && may_grow && n < (1ull << 27)) {
+        // no table yet (the family's maps were empty at the build): build
+        // one sized for this batch and apply on it — unless other map groups
+        // wait for a commit (the tables the batch was classified with)
+        bool maps = false, others = false;
+        for (auto &kv : c->maps)
+            maps |= kv.second->role == (V6 ? ROLE_CT6 : ROLE_CT4);
+        uint64_t sg[NGROUPS];
+        group_sigs(c, sg);
+        for (int g = 0; g < NGROUPS; g++)
+            others |= g != 3 && sg[g] != c->built_sig[g];
+        if (maps && !others) {
+            uint64_t &mn = V6 ? c->ct_min6 : c->ct_min4;
+            mn = std::max<uint64_t>({mn, 1ull << 16, 8 * n});
+            c->built_sig[3] = ~0ull;
+            if (int rc = commit_locked(c, s))
+                return rc;
+            return ct_apply_dev(c, in, out, mode, ep_lxc, s, false, true);
+        }
+    }
     if (!slots || !(V6 ? G.ct6_info.p : G.ct4_info.p) || n >= (lbm ? 1ull << 27 : 1ull << 28))
         return 1;
     // the batch's classify (its CT bytes, verdicts and the workspace's hit
@@ -2983,12 +3004,15 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             A.ck2 = L.k2 ? (const uint32_t *)((const char *)c->ws + L.k2) : nullptr;
         }
     }
+    // a load balancer's service step first: the ordering pass and the scan
+    // decode its per-header records
+    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess ||
+        hipMemsetAsync(A.obm, 0, obm_bytes, s) != hipSuccess || (lbm && cta_lb_pre(A, V6, s)))
+        return -EIO;
     // the reference's packet-order CT results (ctorder.hip): the stages a
     // CT write earlier in the batch changes get their CT byte rewritten
     // before the apply folds it (once per call: not again after a rebuild)
-    // (a batch with a load balancer's service step: TODO, its records come
-    // from the scan)
-    if (may_grow && !lbm) {
+    if (order) {
         if (c->ord_delbm.bytes < obm_bytes && c->ord_delbm.zeros(obm_bytes, s))
             return -ENOMEM;
         if (!c->ord_cnt.p && c->ord_cnt.zeros(4 * ORD_NCNT, s))   // (ORD_CHANGED accumulates)
@@ -3006,15 +3030,14 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     }
     // the caller wants the event words: the trace words' monitor lengths in
     // packet order (every hit replayed by the fold, k_cta_mon)
-    if (out->notify && !lbm) {
+    if (out->notify) {
         if (c->cta_mon.ensure(2 * n) || hipMemsetAsync(c->cta_mon.p, 0xFF, 2 * n, s) != hipSuccess)
             return -ENOMEM;
         A.nt = out->notify;
         A.mon = (uint8_t *)c->cta_mon.p;
     }
     uint32_t hc[CTA_NCNT];
-    if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess ||
-        hipMemsetAsync(A.obm, 0, obm_bytes, s) != hipSuccess || cta_scan(A, V6, s) ||
+    if (cta_scan(A, V6, s) ||
         hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -3092,7 +3115,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             c->built_sig[3] = ~0ull;
             if (int rc = commit_locked(c, s))
                 return rc;
-            return ct_apply_dev(c, in, out, mode, ep_lxc, s, false);
+            return ct_apply_dev(c, in, out, mode, ep_lxc, s, false, false);
         }
     }
     if (!V6 && ok && fits(newk) && !maps_fit() && c->ct_evict) {

@@ -310,7 +310,10 @@ struct OrdBufs {
 int ord_resolve(const CtaArgs &A, OrdArgs &O, OrdBufs &B, bool v6, uint32_t *changed,
                 hipStream_t s);
 size_t cta_sort_tmp_bytes(uint32_t n);
-// v6: the batch is IPv6 (A.ct6, A.log6)
+// v6: the batch is IPv6 (A.ct6, A.log6).  A batch with a load balancer's
+// service step (A.lbr) runs cta_lb_pre first (with A.cnt zeroed), then the
+// ordering pass (its ops decode the service step's records), then cta_scan.
+int cta_lb_pre(const CtaArgs &A, bool v6, hipStream_t s);
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);
 // the keys the creates would add, exactly (requests sorted and deduplicated,
 // the table probed): newk[0] all of them, newk[1] those of TCP creates (they

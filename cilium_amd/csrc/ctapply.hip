@@ -492,7 +492,10 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                 }
                 hs2[st] = sl;
                 nhit++;
-                if (o.kind == OP_HIT && o.action != 2) {   // a plain hit: its summary
+                if (A.nt && o.kind == OP_HIT) {
+                    // monitor lengths wanted: every hit replayed in order
+                    order_mark(A, sl, MARK_ORDERED);
+                } else if (o.kind == OP_HIT && o.action != 2) {   // a plain hit: its summary
                     const uint32_t b = sum_bits(o.dir == CT_INGRESS, o.is_tcp, o.syn, o.tfl);
                     if ((A.ms[sl].x & b) != b)
                         atomicOr(&A.ms[sl].x, b);
@@ -1219,13 +1222,25 @@ __global__ __launch_bounds__(256) void k_cta_mon(CtaArgs A)
     const uint32_t res = cs & CFC_CT_RES_MASK;
     uint32_t m = TRACE_PAYLOAD_LEN;
     const uint32_t proto = A.mt[i] & 0xFF;
+    // the L4 word the stage's lookup read: with a load balancer the service
+    // step's tuple (stage 0) or the packet as it left it (stage 1)
+    uint32_t pw = A.pt[i];
+    if (A.lbr) {
+        if constexpr (V6) {
+            const LbRec6 &l = reinterpret_cast<const LbRec6 *>(A.lbr)[i];
+            pw = st ? l.ppt : l.tpt;
+        } else {
+            const LbRec4 &l = reinterpret_cast<const LbRec4 *>(A.lbr)[i];
+            pw = st ? l.ppt : l.tpt;
+        }
+    }
     if (res != CT_NEW) {
         const uint8_t c = A.mon[2 * i + st];
         m = c == 1 ? 1u : c == 2 ? TRACE_PAYLOAD_LEN : 0u;
-        if (c == 0xFF && ct_action(V6, proto, A.pt[i], A.mt[i]) == 2)
+        if (c == 0xFF && ct_action(V6, proto, pw, A.mt[i]) == 2)
             m = TRACE_PAYLOAD_LEN;
     }
-    const CtProbe k = ct_probe<V6>(proto, A.pt[i], CT_INGRESS, 0);
+    const CtProbe k = ct_probe<V6>(proto, pw, CT_INGRESS, 0);
     // (ipv6_l3_from_lxc sets TRACE_PAYLOAD_LEN after its ct_create6,
     // bpf_lxc.c:248: a new flow's egress trace is not captured at MTU)
     const bool v6_new_egress = V6 && A.mode == CFC_MODE_EGRESS && st == 0 && res == CT_NEW;
@@ -1602,20 +1617,29 @@ size_t cta_sort_tmp_bytes(uint32_t n)
     return std::max(tb, ts);
 }
 
+// an egress batch with a load balancer: the service step of every header
+// (k_cta_lb) and its replay per CT_SERVICE key in order (k_cta_svc), the
+// per-header records (LbRec) the ordering pass and the scan decode
+template <bool V6>
+int cta_lb_pre_t(const CtaArgs &A, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_cta_lb<V6>, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);
+    uint32_t ns = 0;
+    if (hipMemcpyAsync(&ns, A.cnt + CTA_NSVC, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    uint64_t *sorted;
+    if (int rc = sort_keys(A, A.reqS, A.reqS2, ns, A.ob + A.slot_bits, s, &sorted))
+        return rc;
+    if (ns)
+        hipLaunchKernelGGL(k_cta_svc<V6>, dim3((ns + 255) / 256), dim3(256), 0, s, A, sorted, ns);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 template <bool V6>
 int cta_scan_t(const CtaArgs &A, hipStream_t s)
 {
-    if (A.lbr) {   // (an egress batch with a load balancer)
-        hipLaunchKernelGGL(k_cta_lb<V6>, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);
-        uint32_t ns = 0;
-        if (hipMemcpyAsync(&ns, A.cnt + CTA_NSVC, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess)
-            return -EIO;
-        uint64_t *sorted;
-        if (int rc = sort_keys(A, A.reqS, A.reqS2, ns, A.ob + A.slot_bits, s, &sorted))
-            return rc;
-        if (ns)
-            hipLaunchKernelGGL(k_cta_svc<V6>, dim3((ns + 255) / 256), dim3(256), 0, s, A, sorted, ns);
+    if (A.lbr) {   // (after cta_lb_pre)
         hipLaunchKernelGGL(k_cta_scan_lb<V6>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
         return hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
@@ -1731,6 +1755,11 @@ int ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm, uint64_t slots, uint32_
     hipLaunchKernelGGL(k_ct_evict_hist, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4, tm,
                        slots, mw, bm, base, hist, nb);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_lb_pre(const CtaArgs &A, bool v6, hipStream_t s)
+{
+    return v6 ? cta_lb_pre_t<true>(A, s) : cta_lb_pre_t<false>(A, s);
 }
 
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s)

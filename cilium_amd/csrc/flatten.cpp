@@ -633,7 +633,8 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
     size_t n4 = 0, n6 = 0;
     for (const Map *m : cts)
         (m->role == ROLE_CT4 ? n4 : n6) += m->kv.size();
-    if (n4) {
+    // (an empty family keeps no table unless a device apply asked for one)
+    if (n4 || img->ct_min4) {
         uint32_t ns = pow2_at_least(std::max<uint64_t>({16, 2ull * n4, img->ct_min4}));
         img->ct4.assign(ns, Ct4Slot{});
         img->ct4_tm.assign(ns, CtTimer{});
@@ -652,9 +653,9 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                 }
             }
     img->lb_ct = lb;
-    if (n4 && lb)
+    if (!img->ct4.empty() && lb)
         img->ct4_lb.assign(img->ct4.size(), make_uint4(0, 0, 0, 0));
-    if (n6) {
+    if (n6 || img->ct_min6) {
         uint32_t ns = pow2_at_least(std::max<uint64_t>({16, 2ull * n6, img->ct_min6}));
         img->ct6.assign(ns, Ct6Slot{});
         img->ct6_tm.assign(ns, CtTimer{});

@@ -71,6 +71,7 @@ def test_full_endpoint_map_stays_on_device(torch):
     torch.cuda.synchronize()
     ver = out.verdict.cpu().numpy()
     ctb = out.ct.cpu().numpy()
+    dp.counters_sync()   # (the CT accounting into the maps)
     rows = ct_rows(dp, dp.ct_fds)
     st = dp.stats()
     sizes = {k: len(dp.dump(fd)[0]) for k, fd in dp.ct_fds.items()}

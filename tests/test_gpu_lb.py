@@ -44,6 +44,8 @@ def _run(torch, t, h, mode, ep, notify=False):
         res["rec"] = rec.cpu().numpy()
         res["idx"] = idx.cpu().numpy().astype(np.uint64)
     dp.ct_apply(b, out, mode, ep)
+    # (the CT bytes in the reference's packet order: cfc_ct_apply rewrites them)
+    res["ct"] = out.ct.cpu().numpy()
     dp.counters_sync()   # the device's CONNTRACK_ACCOUNTING into the maps
     res["ct_rows"] = ct_rows(dp, dp.ct_fds)
     res["stats"] = dp.stats()
@@ -160,14 +162,41 @@ def test_lb_stream_vs_oracle(torch, mode):
     t, h = _lb_stream(71 + mode, 200_000, mode)
     ep = S.EP_LXC_ID if mode == 1 else 0
     r = _run(torch, t, h, mode, ep)
+    # the launch's outputs against the batch view (a flow's later packets
+    # select their backend by their own hash: DESIGN.md §7 "Service replay
+    # with per-packet hashes"); the CT bytes after cfc_ct_apply and the CT
+    # maps against the reference's packet order
+    ob = O.Oracle(t)
+    oa, ov, oi, opk = ob.classify(h, mode, ep, nthreads=16, want_pkt=True)
     o = O.Oracle(t)
-    oa, ov, oi, oct_, opk = o.classify(h, mode, ep, nthreads=16, want_ct=True,
-                                       want_pkt=True, apply_ct=True)
+    sa, _, _, oct_, spk = o.classify(h, mode, ep, nthreads=16, want_ct=True, want_pkt=True,
+                                     apply_ct=True)
+    # (the headers that deviation touches: another backend, so other CT keys)
+    dev = (sa != oa) | (spk != opk).any(1)
+    assert dev.sum() <= len(h) // 500, dev.sum()
     for k, want in (("act", oa), ("ver", ov), ("ide", oi), ("ct", oct_), ("pkt", opk)):
-        bad = np.nonzero((r[k] != want).reshape(len(h), -1).any(1))[0]
+        diff = (r[k] != want).reshape(len(h), -1).any(1)
+        bad = np.nonzero(diff & ~dev if k == "ct" else diff)[0]
         assert len(bad) == 0, f"{k}: {len(bad)} differ, first {bad[:8]}"
     assert (r["ver"] == -158).any() or mode == 0
     assert (r["pkt"][:, 1] != h.daddr).sum() > len(h) // 10 or mode == 0
-    _ct_diff(r["ct_rows"], o.ct_dump())
-    np.testing.assert_array_equal(r["ct_rows"], o.ct_dump())
+    # every CT entry but those of the flows the per-packet-hash deviation
+    # touches (their client ports: another backend, other keys)
+    ports = set((h.sport if mode == 1 else h.dport)[dev].tolist())
+
+    # (and the related ICMP entries of their backends' address pairs)
+    backs = set(r["pkt"][dev, 1].tolist()) | set(spk[dev, 1].tolist())
+
+    def keep(rows):
+        tp = rows[:, 12:16].copy().view("<u2").reshape(-1, 2)
+        ad = rows[:, 4:12].copy().view("<u4").reshape(-1, 2)
+        rel = (rows[:, 16] == 1) & ((rows[:, 17] & 2) != 0)
+        k = ~(np.isin(tp[:, 0], list(ports)) | np.isin(tp[:, 1], list(ports)) |
+              (rel & (np.isin(ad[:, 0], list(backs)) | np.isin(ad[:, 1], list(backs)))))
+        return rows[k], int((~k).sum())
+    got, ng = keep(r["ct_rows"])
+    want, nw = keep(o.ct_dump())
+    assert max(ng, nw) <= 8 * dev.sum() + 64, (ng, nw)
+    _ct_diff(got, want)
+    np.testing.assert_array_equal(got, want)
     assert r["stats"]["ct_apply_host"] == 0 and r["stats"]["ct_apply_device"] == 1
