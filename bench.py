@@ -44,6 +44,25 @@ def ubench_ceilings():
     return sorted(best.items())
 
 
+def mix_ceiling(p):
+    """The chip's measured rate (G loads/s) of independent random 16-byte
+    loads when a fraction p hits a 2 MiB (L2-resident) table and the rest a
+    4 GiB (HBM) one (scripts/ubench_mix.hip, profiles/r04/ubench_mix.jsonl),
+    interpolated in p; None without the measurement.  The measurement shows
+    that hits and misses of one kernel do not overlap: at p >= 0.75 the mix
+    runs below even the additive model (a wave waits for its slowest load)."""
+    try:
+        pts = sorted((r["p"], r["gloads_per_s"]) for r in
+                     map(json.loads, open(os.path.join(ROOT, "profiles", "r04",
+                                                       "ubench_mix.jsonl"))))
+    except (OSError, ValueError):
+        return None
+    for (p0, r0), (p1, r1) in zip(pts, pts[1:]):
+        if p0 <= p <= p1:
+            return r0 + (r1 - r0) * (p - p0) / max(p1 - p0, 1e-9)
+    return pts[-1][1] if p > pts[-1][0] else pts[0][1]
+
+
 def ceiling_for(ws_bytes, rows):
     """(table MiB, G loads/s) of the smallest measured table holding ws_bytes."""
     for mib, rate in rows:
@@ -89,15 +108,25 @@ def kernel_roofline(k, hn, ms, ws, pk, rows):
     hits, miss = pk.get("l2_hits_per_launch"), pk.get("l2_misses_per_launch")
     if hits is None or miss is None:
         hits, miss = req, 0.0
-    t_ideal = hits / (l2_peak * 1e9) + miss / (miss_peak * 1e9)
+    t_add = hits / (l2_peak * 1e9) + miss / (miss_peak * 1e9)
     t_unif = req / (peak_k * 1e9)
+    # the bound: the measured rate of this kernel's hit/miss mix (the
+    # additive model is optimistic for mixes, profiles/r04/ubench_mix.jsonl:
+    # L2 hits mixed with HBM misses); a kernel whose misses the Infinity
+    # Cache serves keeps the additive model
+    p = hits / req if req else 1.0
+    mixr = mix_ceiling(p) if miss_mib >= 4096 else None
+    t_ideal = req / (mixr * 1e9) if mixr else t_add
     d.update({"l2_requests_per_launch": req,
               "l2_requests_per_header": round(req / hn, 3),
               "l2_hits_per_launch": hits, "l2_misses_per_launch": miss,
+              "hit_fraction": round(p, 4),
+              "mix_ceiling_greq_s": round(mixr, 1) if mixr else None,
               "hit_ceiling_greq_s": l2_peak,
               "miss_ceiling_greq_s": miss_peak, "miss_ceiling_table_mib": miss_mib,
               "achieved_greq_s": round(req / (ms * 1e-3) / 1e9, 1),
               "frac": round(t_ideal / (ms * 1e-3), 4),
+              "frac_additive": round(t_add / (ms * 1e-3), 4),
               "frac_uniform": round(t_unif / (ms * 1e-3), 4),
               "hbm_bytes_per_launch": pk["hbm_bytes_per_launch"]})
     return d, t_ideal, t_unif

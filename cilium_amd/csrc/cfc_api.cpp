@@ -174,7 +174,7 @@ struct cfc_ctx {
     // packet-order CT results (ctorder.hip): buffers, the deleted-slot
     // bitmap (zero between applies), counters; the stages it changed
     OrdBufs ordb;
-    DevBuf ord_delbm, ord_cnt;
+    DevBuf ord_delbm, ord_mixbm, ord_dfirst, ord_cnt;
     DevBuf cta_mon;               // per header stage: the fold's monitor length
     uint64_t n_ord_changed = 0;
     // LXC_NAT46 (nat.hip): the hop batch of each classified batch that had
@@ -3013,8 +3013,16 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     // CT write earlier in the batch changes get their CT byte rewritten
     // before the apply folds it (once per call: not again after a rebuild)
     if (order) {
-        if (c->ord_delbm.bytes < obm_bytes && c->ord_delbm.zeros(obm_bytes, s))
+        // (per-slot state, clear between applies: grown with the table)
+        if (c->ord_delbm.bytes < obm_bytes &&
+            (c->ord_delbm.zeros(obm_bytes, s) || c->ord_mixbm.zeros(obm_bytes, s)))
             return -ENOMEM;
+        if (c->ord_dfirst.bytes < 4 * slots) {
+            if (c->ord_dfirst.ensure(4 * slots) ||
+                hipMemsetD32Async((hipDeviceptr_t)c->ord_dfirst.p, 0xFFFFFFFFu,
+                                  c->ord_dfirst.bytes / 4, s) != hipSuccess)
+                return -ENOMEM;
+        }
         if (!c->ord_cnt.p && c->ord_cnt.zeros(4 * ORD_NCNT, s))   // (ORD_CHANGED accumulates)
             return -ENOMEM;
         OrdArgs O{};
@@ -3022,6 +3030,10 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         O.ck1 = const_cast<uint32_t *>(A.ck1);
         O.ck2 = const_cast<uint32_t *>(A.ck2);
         O.delbm = (uint32_t *)c->ord_delbm.p;
+        O.mixbm = (uint32_t *)c->ord_mixbm.p;
+        O.dfirst = (uint32_t *)c->ord_dfirst.p;
+        O.bm_bytes = c->ord_delbm.bytes;
+        O.slots = c->ord_dfirst.bytes / 4;
         O.cnt = (uint32_t *)c->ord_cnt.p;
         uint32_t changed = 0;
         if (int rc = ord_resolve(A, O, c->ordb, V6, &changed, s))

@@ -285,15 +285,22 @@ struct DevBuf {
 
 // ---- packet-order CT results (ctorder.hip), run by cfc_ct_apply before
 // the apply proper
-enum { ORD_NPART, ORD_NPART2, ORD_NDEL, ORD_NRELKEY, ORD_NREL, ORD_COLL, ORD_CHANGED,
+enum { ORD_NPART, ORD_NCREATE, ORD_NDEL, ORD_NRELKEY, ORD_NREL, ORD_COLL, ORD_CHANGED,
        ORD_NCNT };
 struct OrdArgs {
     uint8_t *ctb;                 // the batch's CT bytes (rewritten in place)
     uint32_t *ck1, *ck2;          // the classify launch's hit keys (or null)
-    uint32_t *delbm;              // deleted-slot bitmap (zero between applies)
+    // per CT slot, zero / all-ones between applies: deleted slots, mixed
+    // slots (one bit each), each deleted slot's first delete order
+    uint32_t *delbm, *mixbm, *dfirst;
+    size_t bm_bytes;
+    uint64_t slots;
+    uint32_t ndel;                // deleting stages (0: no delete pass)
+    uint64_t *fpset;              // the creates' key fingerprints (or null)
+    uint32_t fp_mask;
     uint32_t *cnt;                // ORD_* counters
     uint32_t *part;               // participants: header << 1 | stage
-    uint32_t part_cap, part_base;
+    uint32_t part_cap;
     uint32_t *rel_src;
     void *rk;                     // per record its key (16 B; IPv6 48 B)
     uint64_t *rh, *rh2, *rh3;     // fingerprints
@@ -303,7 +310,7 @@ struct OrdArgs {
     size_t tmp_bytes;
 };
 struct OrdBufs {
-    DevBuf part, rel_src, rk, rh, rh2, rh3, rord, rord2, ridx, ridx2, pinfo, nres, tmp;
+    DevBuf part, rel_src, rk, rh, rh2, rh3, rord, rord2, ridx, ridx2, pinfo, nres, tmp, fpset;
 };
 // rewrites the CT bytes (and hit keys) of the stages whose packet-order
 // result differs from the launch's; *changed: how many

@@ -81,17 +81,134 @@ __device__ __forceinline__ uint32_t start_slot(const CtaArgs &A, const OrdArgs &
     return find(A, o.sa, o.da, o.z2, o.w2);
 }
 
-// ---- collect: the participants (header << 1 | stage).  pass 0: every
-// CT_NEW stage and every deleting CT_ESTABLISHED stage (its slot marked in
-// the deleted-slot bitmap); pass 1 (only when the batch deletes): the other
-// CT_ESTABLISHED stages whose slot is marked.  count: participants are only
-// counted (O.part null).
+// ---- which stages take part.  Per k2 key the state is a chain of its
+// stages in packet order, but most keys need no sort:
+//   * a key no stage of the batch writes keeps its batch-start existence:
+//     a dropped CT_NEW stage (no create) matters only when some allowed
+//     CT_NEW stage of the batch creates its key (the creates' fingerprints,
+//     k_ord_fpins), or when its key is an ICMP error's (a related entry a
+//     create may write: round 2);
+//   * a key the batch only deletes (every stage on its slot a denied
+//     CT_ESTABLISHED: the common case, one verdict per flow) ends with its
+//     first delete in packet order; the later stages see it gone: CT_NEW,
+//     no create (k_ord_deltail, from each slot's first delete order D);
+//   * a deleted slot that also has an allowed CT_ESTABLISHED stage (a
+//     "mixed" slot: the verdict differs between packets of one key, e.g.
+//     fragments) goes through the sort with all its stages.
+// Participants of the sort: every allowed CT_NEW stage, dropped CT_NEW
+// stages whose key a create writes (or an ICMP error's), and the stages of
+// mixed slots.
+
+// mark: creates and deletes counted; per deleted slot its bit and its
+// first delete's order (read first: a hot flow's packets find them set)
 template <bool V6, bool TWO>
-__global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O, int pass)
+__global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
-    uint32_t ndel = 0;
+    uint32_t ncr = 0, ndel = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const uint32_t cb = i < A.n ? A.ctb[i] : 0u;
+        const int32_t ver = i < A.n ? A.ver[i] : 0;
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (cb >> (4 * st)) & 0xF;
+            if (!(cs & CFC_CT_DONE))
+                continue;
+            const uint32_t res = cs & CFC_CT_RES_MASK;
+            const bool dropped = st == last && ver == DROP_POLICY;
+            ncr += res == CT_NEW && !dropped;
+            if (res == CT_ESTABLISHED && dropped) {
+                const uint32_t sl = start_slot<V6>(A, O, i, st);
+                if (sl != NONE) {
+                    const uint32_t b = 1u << (sl & 31), ord = (uint32_t)(i << 1) | (uint32_t)st;
+                    if (!(O.delbm[sl >> 5] & b))
+                        atomicOr(&O.delbm[sl >> 5], b);
+                    if (ord < O.dfirst[sl])
+                        atomicMin(&O.dfirst[sl], ord);
+                    ndel++;
+                }
+            }
+        }
+    }
+    block_add(&O.cnt[ORD_NCREATE], ncr);
+    block_add(&O.cnt[ORD_NDEL], ndel);
+}
+
+// the creates' k2 fingerprints into an open-addressed set (fp | 1, 0 free)
+__device__ __forceinline__ void fp_put(const OrdArgs &O, uint64_t fp)
+{
+    fp |= 1ull;
+    for (uint32_t j = (uint32_t)(fp >> 32) & O.fp_mask;; j = (j + 1) & O.fp_mask) {
+        const unsigned long long cur =
+            atomicCAS((unsigned long long *)O.fpset + j, 0ull, (unsigned long long)fp);
+        if (cur == 0 || cur == fp)
+            return;
+    }
+}
+__device__ __forceinline__ bool fp_has(const OrdArgs &O, uint64_t fp)
+{
+    fp |= 1ull;
+    for (uint32_t j = (uint32_t)(fp >> 32) & O.fp_mask;; j = (j + 1) & O.fp_mask) {
+        const uint64_t cur = O.fpset[j];
+        if (cur == fp)
+            return true;
+        if (cur == 0)
+            return false;
+    }
+}
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_fpins(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n)
+        return;
+    const uint32_t cb = A.ctb[i];
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+    for (int st = 0; st < NST; st++) {
+        const uint32_t cs = (cb >> (4 * st)) & 0xF;
+        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW ||
+            (st == last && A.ver[i] == DROP_POLICY))
+            continue;
+        const Op<V6> o = decode<V6>(A, i, st);
+        fp_put(O, fp64(o.sa, o.da, o.z2, o.w2));
+    }
+}
+
+// mixed: a deleted slot with an allowed CT_ESTABLISHED stage
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_mixed(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n)
+        return;
+    const uint32_t cb = A.ctb[i];
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+    for (int st = 0; st < NST; st++) {
+        const uint32_t cs = (cb >> (4 * st)) & 0xF;
+        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
+            (st == last && A.ver[i] == DROP_POLICY))
+            continue;
+        const uint32_t sl = start_slot<V6>(A, O, i, st);
+        const uint32_t b = 1u << (sl & 31);
+        if (sl != NONE && (O.delbm[sl >> 5] & b) && !(O.mixbm[sl >> 5] & b))
+            atomicOr(&O.mixbm[sl >> 5], b);
+    }
+}
+
+// collect the participants (header << 1 | stage); count only when O.part
+// is null
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
     // (every thread runs the same number of steps: block_count_n)
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
         const uint64_t i = base + threadIdx.x;
@@ -107,25 +224,20 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O, int p
             const uint32_t res = cs & CFC_CT_RES_MASK;
             const bool dropped = st == last && ver == DROP_POLICY;
             bool w = false;
-            if (pass == 0) {
-                w = res == CT_NEW || (res == CT_ESTABLISHED && dropped);
-                if (res == CT_ESTABLISHED && dropped) {
-                    const uint32_t sl = start_slot<V6>(A, O, i, st);
-                    if (sl != NONE && O.delbm) {
-                        if (!O.part)   // (marked once, in the counting run)
-                            atomicOr(&O.delbm[sl >> 5], 1u << (sl & 31));
-                        ndel++;
-                    }
+            if (res == CT_NEW) {
+                w = !dropped;
+                if (dropped) {
+                    const Op<V6> o = decode<V6>(A, i, st);
+                    w = (o.w2 & 0x200u) || (O.fpset && fp_has(O, fp64(o.sa, o.da, o.z2, o.w2)));
                 }
-            } else if (res == CT_ESTABLISHED && !dropped) {
+            } else if (res == CT_ESTABLISHED && O.ndel) {
                 const uint32_t sl = start_slot<V6>(A, O, i, st);
-                w = sl != NONE && ((O.delbm[sl >> 5] >> (sl & 31)) & 1);
+                w = sl != NONE && ((O.mixbm[sl >> 5] >> (sl & 31)) & 1);
             }
             want[st] = w;
             nw += w;
         }
-        uint32_t r = block_count_n(&O.cnt[pass == 0 ? ORD_NPART : ORD_NPART2], nw) +
-                     (pass == 0 ? 0u : O.part_base);
+        uint32_t r = block_count_n(&O.cnt[ORD_NPART], nw);
         if (O.part) {
 #pragma unroll
             for (int st = 0; st < NST; st++)
@@ -136,8 +248,42 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O, int p
                 }
         }
     }
-    if (pass == 0 && !O.part)
-        block_add(&O.cnt[ORD_NDEL], ndel);
+}
+
+// a deleting stage on a slot only deletes: all but its first delete see
+// the entry gone (CT_NEW, no create: they are dropped).  Runs before
+// k_ord_write (its stages' bytes are the launch's).
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_deltail(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    bool chg = false;
+    if (i < A.n) {
+        const uint32_t cb = A.ctb[i];
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (cb >> (4 * st)) & 0xF;
+            if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
+                !(st == last && A.ver[i] == DROP_POLICY))
+                continue;
+            const uint32_t sl = start_slot<V6>(A, O, i, st);
+            if (sl == NONE || ((O.mixbm[sl >> 5] >> (sl & 31)) & 1) ||
+                O.dfirst[sl] == ((uint32_t)(i << 1) | (uint32_t)st))
+                continue;
+            const uintptr_t ba = reinterpret_cast<uintptr_t>(O.ctb + i);
+            uint32_t *wp = reinterpret_cast<uint32_t *>(ba & ~(uintptr_t)3);
+            const uint32_t bs = 8 * (uint32_t)(ba & 3) + 4 * st;
+            atomicAnd(wp, ~(0xFu << bs));
+            atomicOr(wp, ((uint32_t)CT_NEW | CFC_CT_DONE) << bs);
+            uint32_t *ck = st ? O.ck2 : O.ck1;
+            if (ck)
+                ck[i] = NONE;
+            chg = true;
+        }
+    }
+    block_add(&O.cnt[ORD_CHANGED], chg ? 1u : 0u);
 }
 
 // ---- keys: one thread per record r.  r < np: participant r; else the
@@ -296,29 +442,6 @@ __global__ __launch_bounds__(256) void k_ord_write(CtaArgs A, OrdArgs O, uint32_
     block_add(&O.cnt[ORD_CHANGED], chg ? 1u : 0u);
 }
 
-// the deleted-slot bitmap cleared for the next batch
-template <bool V6, bool TWO>
-__global__ __launch_bounds__(256) void k_ord_clear(CtaArgs A, OrdArgs O)
-{
-    constexpr int NST = TWO ? 2 : 1;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= A.n)
-        return;
-    // (before k_ord_write: the launch's CT bytes and hit keys)
-    const uint32_t cb = A.ctb[i];
-    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
-#pragma unroll
-    for (int st = 0; st < NST; st++) {
-        const uint32_t cs = (cb >> (4 * st)) & 0xF;
-        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
-            !(st == last && A.ver[i] == DROP_POLICY))
-            continue;
-        const uint32_t sl = start_slot<V6>(A, O, i, st);
-        if (sl != NONE)
-            O.delbm[sl >> 5] = 0;
-    }
-}
-
 unsigned grid_for(uint64_t n, unsigned cap)
 {
     const uint64_t b = (n + 255) / 256;
@@ -352,114 +475,122 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
 {
     const bool two = A.mode == CFC_MODE_EGRESS;
     const unsigned g = grid_for(A.n, 8192);
+    const unsigned gn = grid_for(A.n, 1u << 30);
     uint32_t hc[ORD_NCNT];
     auto rd = [&]() {
         return hipMemcpyAsync(hc, O.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) == hipSuccess &&
                hipStreamSynchronize(s) == hipSuccess;
     };
+#define ORD_LAUNCH(K, grid, ...)                                                         \
+    do {                                                                                 \
+        if (two)                                                                         \
+            hipLaunchKernelGGL((K<V6, true>), dim3(grid), dim3(256), 0, s, __VA_ARGS__);  \
+        else                                                                             \
+            hipLaunchKernelGGL((K<V6, false>), dim3(grid), dim3(256), 0, s, __VA_ARGS__); \
+    } while (0)
     *changed = 0;   // (ORD_CHANGED accumulates on the device: no wait for it)
     if (hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
         return -EIO;
     O.part = nullptr;
-    if (two)
-        hipLaunchKernelGGL((k_ord_collect<V6, true>), dim3(g), dim3(256), 0, s, A, O, 0);
-    else
-        hipLaunchKernelGGL((k_ord_collect<V6, false>), dim3(g), dim3(256), 0, s, A, O, 0);
+    O.fpset = nullptr;
+    O.ndel = 0;
+    ORD_LAUNCH(k_ord_mark, g, A, O);
     if (!rd())
         return -EIO;
-    const uint32_t ndel = hc[ORD_NDEL];
-    uint64_t np = hc[ORD_NPART];
-    if (ndel) {   // the other ESTABLISHED stages on deleted slots (counted)
-        if (two)
-            hipLaunchKernelGGL((k_ord_collect<V6, true>), dim3(g), dim3(256), 0, s, A, O, 1);
-        else
-            hipLaunchKernelGGL((k_ord_collect<V6, false>), dim3(g), dim3(256), 0, s, A, O, 1);
-        if (!rd())
-            return -EIO;
-        np += hc[ORD_NPART2];
+    const uint32_t ncr = hc[ORD_NCREATE];
+    O.ndel = hc[ORD_NDEL];
+    if (ncr) {   // the creates' key set, for the dropped CT_NEW stages
+        uint32_t cap = 1024;
+        while (cap < 4ull * ncr && cap < (1u << 30))
+            cap *= 2;
+        if (B.fpset.ensure(8ull * cap) || hipMemsetAsync(B.fpset.p, 0, 8ull * cap, s) != hipSuccess)
+            return -ENOMEM;
+        O.fpset = (uint64_t *)B.fpset.p;
+        O.fp_mask = cap - 1;
+        ORD_LAUNCH(k_ord_fpins, gn, A, O);
     }
-    if (np == 0)
-        return 0;
+    if (O.ndel)
+        ORD_LAUNCH(k_ord_mixed, gn, A, O);
+    ORD_LAUNCH(k_ord_collect, g, A, O);
+    if (!rd())
+        return -EIO;
+    const uint64_t np = hc[ORD_NPART];
     if (np > 0x3FFFFFFFull)
         return -E2BIG;
-    // buffers: participants, and up to twice as many records
-    const uint64_t nr = 2 * np;
-    const size_t kw = V6 ? 48 : 16;
-    if (B.part.ensure(4 * np) || B.rel_src.ensure(4 * np) || B.rk.ensure(kw * nr) ||
-        B.rh.ensure(8 * nr) || B.rh2.ensure(8 * nr) || B.rh3.ensure(8 * nr) ||
-        B.rord.ensure(4 * nr) || B.rord2.ensure(4 * nr) || B.ridx.ensure(4 * nr) ||
-        B.ridx2.ensure(4 * nr) || B.pinfo.ensure(nr) || B.nres.ensure(nr))
-        return -ENOMEM;
-    {
-        size_t t1 = 0, t2 = 0;
-        hipcub::DoubleBuffer<uint32_t> a(nullptr, nullptr), b(nullptr, nullptr);
-        hipcub::DoubleBuffer<uint64_t> c(nullptr, nullptr);
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, a, b, (int)nr, 0, 32, s);
-        (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c, b, (int)nr, 0, 64, s);
-        if (B.tmp.ensure(std::max(t1, t2)))
+    if (np) {
+        // buffers: participants, and up to twice as many records
+        const uint64_t nr = 2 * np;
+        const size_t kw = V6 ? 48 : 16;
+        if (B.part.ensure(4 * np) || B.rel_src.ensure(4 * np) || B.rk.ensure(kw * nr) ||
+            B.rh.ensure(8 * nr) || B.rh2.ensure(8 * nr) || B.rh3.ensure(8 * nr) ||
+            B.rord.ensure(4 * nr) || B.rord2.ensure(4 * nr) || B.ridx.ensure(4 * nr) ||
+            B.ridx2.ensure(4 * nr) || B.pinfo.ensure(nr) || B.nres.ensure(nr))
             return -ENOMEM;
-    }
-    O.part = (uint32_t *)B.part.p;
-    O.part_cap = (uint32_t)np;
-    O.rel_src = (uint32_t *)B.rel_src.p;
-    O.rk = B.rk.p;
-    O.rh = (uint64_t *)B.rh.p;
-    O.rh2 = (uint64_t *)B.rh2.p;
-    O.rh3 = (uint64_t *)B.rh3.p;
-    O.rord = (uint32_t *)B.rord.p;
-    O.rord2 = (uint32_t *)B.rord2.p;
-    O.ridx = (uint32_t *)B.ridx.p;
-    O.ridx2 = (uint32_t *)B.ridx2.p;
-    O.pinfo = (uint8_t *)B.pinfo.p;
-    O.nres = (uint8_t *)B.nres.p;
-    O.tmp = B.tmp.p;
-    O.tmp_bytes = B.tmp.bytes;
-    if (hipMemsetAsync(O.cnt + ORD_NPART, 0, 8, s) != hipSuccess)   // (NPART, NPART2)
-        return -EIO;
-    O.part_base = hc[ORD_NPART];   // (pass 1's participants follow pass 0's)
-    if (two) {
-        hipLaunchKernelGGL((k_ord_collect<V6, true>), dim3(g), dim3(256), 0, s, A, O, 0);
-        if (ndel)
-            hipLaunchKernelGGL((k_ord_collect<V6, true>), dim3(g), dim3(256), 0, s, A, O, 1);
-    } else {
-        hipLaunchKernelGGL((k_ord_collect<V6, false>), dim3(g), dim3(256), 0, s, A, O, 0);
-        if (ndel)
-            hipLaunchKernelGGL((k_ord_collect<V6, false>), dim3(g), dim3(256), 0, s, A, O, 1);
-    }
-    const uint32_t npi = (uint32_t)np;
-    const unsigned gp = (unsigned)((npi + 255) / 256);
-    hipLaunchKernelGGL(k_ord_keys<V6>, dim3(gp), dim3(256), 0, s, A, O, npi, 0u);
-    const uint64_t *h;
-    const uint32_t *idx;
-    if (int rc = sort_records<V6>(O, npi, s, &h, &idx))
-        return rc;
-    hipLaunchKernelGGL(k_ord_resolve<V6>, dim3(gp), dim3(256), 0, s, O, h, idx, npi);
-    if (!rd())
-        return -EIO;
-    if (hc[ORD_NRELKEY]) {
-        // round 2: the related entries of the creates round 1 resolved
-        hipLaunchKernelGGL(k_ord_relsrc, dim3(gp), dim3(256), 0, s, O, npi);
+        {
+            size_t t1 = 0, t2 = 0;
+            hipcub::DoubleBuffer<uint32_t> a(nullptr, nullptr), b(nullptr, nullptr);
+            hipcub::DoubleBuffer<uint64_t> c(nullptr, nullptr);
+            (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, a, b, (int)nr, 0, 32, s);
+            (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t2, c, b, (int)nr, 0, 64, s);
+            if (B.tmp.ensure(std::max(t1, t2)))
+                return -ENOMEM;
+        }
+        O.part = (uint32_t *)B.part.p;
+        O.part_cap = (uint32_t)np;
+        O.rel_src = (uint32_t *)B.rel_src.p;
+        O.rk = B.rk.p;
+        O.rh = (uint64_t *)B.rh.p;
+        O.rh2 = (uint64_t *)B.rh2.p;
+        O.rh3 = (uint64_t *)B.rh3.p;
+        O.rord = (uint32_t *)B.rord.p;
+        O.rord2 = (uint32_t *)B.rord2.p;
+        O.ridx = (uint32_t *)B.ridx.p;
+        O.ridx2 = (uint32_t *)B.ridx2.p;
+        O.pinfo = (uint8_t *)B.pinfo.p;
+        O.nres = (uint8_t *)B.nres.p;
+        O.tmp = B.tmp.p;
+        O.tmp_bytes = B.tmp.bytes;
+        if (hipMemsetAsync(O.cnt + ORD_NPART, 0, 4, s) != hipSuccess)
+            return -EIO;
+        ORD_LAUNCH(k_ord_collect, g, A, O);
+        const uint32_t npi = (uint32_t)np;
+        const unsigned gp = (unsigned)((npi + 255) / 256);
+        hipLaunchKernelGGL(k_ord_keys<V6>, dim3(gp), dim3(256), 0, s, A, O, npi, 0u);
+        const uint64_t *h;
+        const uint32_t *idx;
+        if (int rc = sort_records<V6>(O, npi, s, &h, &idx))
+            return rc;
+        hipLaunchKernelGGL(k_ord_resolve<V6>, dim3(gp), dim3(256), 0, s, O, h, idx, npi);
         if (!rd())
             return -EIO;
-        const uint32_t nrel = hc[ORD_NREL];
-        if (nrel) {
-            hipLaunchKernelGGL(k_ord_keys<V6>, dim3((npi + nrel + 255) / 256), dim3(256), 0, s, A,
-                               O, npi, nrel);
-            if (int rc = sort_records<V6>(O, npi + nrel, s, &h, &idx))
-                return rc;
-            hipLaunchKernelGGL(k_ord_resolve<V6>, dim3((npi + nrel + 255) / 256), dim3(256), 0, s,
-                               O, h, idx, npi + nrel);
+        if (hc[ORD_NRELKEY]) {
+            // round 2: the related entries of the creates round 1 resolved
+            hipLaunchKernelGGL(k_ord_relsrc, dim3(gp), dim3(256), 0, s, O, npi);
+            if (!rd())
+                return -EIO;
+            const uint32_t nrel = hc[ORD_NREL];
+            if (nrel) {
+                hipLaunchKernelGGL(k_ord_keys<V6>, dim3((npi + nrel + 255) / 256), dim3(256), 0, s,
+                                   A, O, npi, nrel);
+                if (int rc = sort_records<V6>(O, npi + nrel, s, &h, &idx))
+                    return rc;
+                hipLaunchKernelGGL(k_ord_resolve<V6>, dim3((npi + nrel + 255) / 256), dim3(256), 0,
+                                   s, O, h, idx, npi + nrel);
+            }
         }
     }
-    if (ndel) {   // (before the write: the launch's CT bytes and hit keys)
-        if (two)
-            hipLaunchKernelGGL((k_ord_clear<V6, true>), dim3(grid_for(A.n, 1u << 30)), dim3(256),
-                               0, s, A, O);
-        else
-            hipLaunchKernelGGL((k_ord_clear<V6, false>), dim3(grid_for(A.n, 1u << 30)), dim3(256),
-                               0, s, A, O);
-    }
-    hipLaunchKernelGGL(k_ord_write, dim3(gp), dim3(256), 0, s, A, O, npi);
+    // (before k_ord_write: the launch's bytes of the deleting stages)
+    if (O.ndel)
+        ORD_LAUNCH(k_ord_deltail, gn, A, O);
+    if (np)
+        hipLaunchKernelGGL(k_ord_write, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, A, O,
+                           (uint32_t)np);
+    if (O.ndel &&   // the per-slot state cleared for the next batch
+        (hipMemsetAsync(O.delbm, 0, O.bm_bytes, s) != hipSuccess ||
+         hipMemsetAsync(O.mixbm, 0, O.bm_bytes, s) != hipSuccess ||
+         hipMemsetD32Async((hipDeviceptr_t)O.dfirst, 0xFFFFFFFFu, O.slots, s) != hipSuccess))
+        return -EIO;
+#undef ORD_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
