@@ -460,8 +460,14 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     uint32_t met0 = NONE, met1 = NONE, ctr1 = NONE;
     const uint32_t len = h.mt >> 16;
     if (CT) {
-        // the hit's CONNTRACK_ACCOUNTING key, aggregated by k_ct_count
-        h.ct_k1 = ct_acct_key(h.ct_slot, EGR ? CT_EGRESS : CT_INGRESS);
+        // the hit's CONNTRACK_ACCOUNTING key, aggregated by k_ct_count; a
+        // CT_NEW stage's miss tag
+        h.ct_k1 = h.ct_slot != NONE
+                      ? ct_acct_key(h.ct_slot, EGR ? CT_EGRESS : CT_INGRESS)
+                  : h.ct_res != CT_NEW ? NONE
+                  : EGR ? ck_miss4(h.sa, h.tda, proto, h.tpt, CT_EGRESS, E.ct_owner)
+                        : ck_miss4(h.sa, h.da, proto, h.pt, CT_INGRESS,
+                                   ct_owner_word(h.rec.w & 0xFFFF, (h.rec.w & LXC_CT_LOCAL) != 0));
         // ct_create4 for a new flow that is not dropped here
         if (h.ct_res == CT_NEW && (v >= 0 || reply))
             ctb |= CTO_CREATE;
@@ -550,7 +556,9 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                         dp2 = c2.dport;
                     }
                 }
-                h.ct_k2 = ct_acct_key(c2.slot, CT_INGRESS);
+                h.ct_k2 = c2.slot != NONE ? ct_acct_key(c2.slot, CT_INGRESS)
+                          : c2.res == CT_NEW ? ck_miss4(h.psa, h.da, proto, h.pt, CT_INGRESS, own2)
+                                             : NONE;
                 if (LB && c2.res == CT_REPLY) {   // bpf_lxc.c:946-955, packet only
                     const uint4 lw = fresh ? make_uint4((h.lbfl >> 16) | (h.lbfl & LBF_LOOP) << 14,
                                                         0, 0, 0)
@@ -988,7 +996,7 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
     const uint64_t end = min(n, start + COUNT_PER_BLOCK);
     for (uint64_t i = start + threadIdx.x; i < end; i += BLOCK) {
         const uint32_t k = ld_nt(idx + i);
-        if (k == NONE)
+        if (k >= CK_MISS)   // (NONE, or a CT_NEW stage's tag)
             continue;
         const uint32_t len = ld_nt(meta + i) >> 16;
         uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
@@ -1141,7 +1149,7 @@ __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
     // wave calls it)
     auto one = [&](uint32_t k, uint32_t len) {
         uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
-        bool done = k == NONE;
+        bool done = k >= CK_MISS;   // (NONE, or a CT_NEW stage's tag)
         for (int p = 0; p < CTP_PROBES && !done; p++) {
             uint32_t cur = keys[h];
             if (cur == NONE) {

@@ -285,8 +285,9 @@ struct DevBuf {
 
 // ---- packet-order CT results (ctorder.hip), run by cfc_ct_apply before
 // the apply proper
-enum { ORD_NPART, ORD_NCREATE, ORD_NDEL, ORD_NRELKEY, ORD_NREL, ORD_COLL, ORD_CHANGED,
-       ORD_NCNT };
+enum { ORD_NPART, ORD_NCREATE, ORD_NDEL, ORD_NNEWDROP, ORD_NEST, ORD_NESTDROP, ORD_UNTAGGED,
+       ORD_NRELKEY, ORD_NREL,
+       ORD_COLL, ORD_CHANGED, ORD_NCNT };
 struct OrdArgs {
     uint8_t *ctb;                 // the batch's CT bytes (rewritten in place)
     uint32_t *ck1, *ck2;          // the classify launch's hit keys (or null)
@@ -296,8 +297,10 @@ struct OrdArgs {
     size_t bm_bytes;
     uint64_t slots;
     uint32_t ndel;                // deleting stages (0: no delete pass)
-    uint64_t *fpset;              // the creates' key fingerprints (or null)
-    uint32_t fp_mask;
+    uint32_t *cbloom;             // the creates' keys (Bloom words, or null)
+    uint32_t cb_mask;
+    bool tagged;                  // the keys from ck1 / ck2's miss tags (CK_MISS), else
+                                  // pre-keys from the headers
     uint32_t *cnt;                // ORD_* counters
     uint32_t *part;               // participants: header << 1 | stage
     uint32_t part_cap;
@@ -311,6 +314,7 @@ struct OrdArgs {
 };
 struct OrdBufs {
     DevBuf part, rel_src, rk, rh, rh2, rh3, rord, rord2, ridx, ridx2, pinfo, nres, tmp, fpset;
+    uint32_t creates_hint = 0;   // the last batch's creates: the filter's size
 };
 // rewrites the CT bytes (and hit keys) of the stages whose packet-order
 // result differs from the launch's; *changed: how many

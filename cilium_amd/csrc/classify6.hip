@@ -407,11 +407,14 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                             // ipv6_policy's ct_lookup6 (bpf_lxc.c:808)
                             CtResult c{CT_NEW, NONE, dport};
                             if (CT) {
-                                c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS,
-                                              ct_owner_word(drec.z & 0xFFFF,
-                                                            (drec.z & LXC_CT_LOCAL) != 0));
-                                ck1 = ct_acct_key(c.slot == NONE ? NONE : c.slot + T.ct6_acct_base,
-                                                  CT_INGRESS);
+                                const uint32_t own = ct_owner_word(drec.z & 0xFFFF,
+                                                                   (drec.z & LXC_CT_LOCAL) != 0);
+                                c = ct_stage6(T, sa_raw, da_raw, proto, pt, CT_INGRESS, own);
+                                ck1 = c.slot != NONE
+                                          ? ct_acct_key(c.slot + T.ct6_acct_base, CT_INGRESS)
+                                      : c.res == CT_NEW
+                                          ? ck_miss6(sa_raw, da_raw, proto, pt, CT_INGRESS, own)
+                                          : NONE;
                             }
                             if (LB) {
                                 // ipv6_policy (:785-815): the packet's daddr
@@ -497,8 +500,10 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     CtResult c{CT_NEW, NONE, dport};
                     if (CT) {
                         c = ct_stage6(T, sa_raw, tda_raw, proto, tpt, CT_EGRESS, E.ct_owner);
-                        ck1 = ct_acct_key(c.slot == NONE ? NONE : c.slot + T.ct6_acct_base,
-                                          CT_EGRESS);
+                        ck1 = c.slot != NONE ? ct_acct_key(c.slot + T.ct6_acct_base, CT_EGRESS)
+                              : c.res == CT_NEW
+                                  ? ck_miss6(sa_raw, tda_raw, proto, tpt, CT_EGRESS, E.ct_owner)
+                                  : NONE;
                     }
                     const bool reply = CT && c.res >= CT_REPLY;
                     const PolicyResult pr = policy_access(T, S, E.pol_base, E.pol_mask,
@@ -570,11 +575,16 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                             CtResult c2{CT_NEW, NONE, dport2};
                             const uint4 s2 = LB ? psa : sa_raw;
                             if (CT) {
+                                const uint32_t own2 = ct_owner_word(erec.z & 0xFFFF,
+                                                                    (erec.z & LXC_CT_LOCAL) != 0);
                                 c2 = ct_stage6(T, s2, tda_raw, proto, LB ? ppt : pt, CT_INGRESS,
-                                               ct_owner_word(erec.z & 0xFFFF,
-                                                             (erec.z & LXC_CT_LOCAL) != 0));
-                                ck2 = ct_acct_key(c2.slot == NONE ? NONE : c2.slot + T.ct6_acct_base,
-                                                  CT_INGRESS);
+                                               own2);
+                                ck2 = c2.slot != NONE
+                                          ? ct_acct_key(c2.slot + T.ct6_acct_base, CT_INGRESS)
+                                      : c2.res == CT_NEW
+                                          ? ck_miss6(s2, tda_raw, proto, LB ? ppt : pt,
+                                                     CT_INGRESS, own2)
+                                          : NONE;
                             }
                             if (LB) {   // ipv6_policy's rewrites (:785-815)
                                 pda.w &= 0xFFFF0000u;

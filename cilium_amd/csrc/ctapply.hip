@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 const bool mine = A.mode == CFC_MODE_EGRESS && st == 0;   // (owner: the sender)
                 const uint32_t key = st ? r[u].k2 : r[u].k1;
                 need[u] |= (cs & CFC_CT_DONE) && !mine &&
-                           ((cs & CFC_CT_RES_MASK) == 0 || key == NONE);
+                           ((cs & CFC_CT_RES_MASK) == 0 || key >= CK_MISS);
             }
         }
         if constexpr (V6) {
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     const uint32_t key = st ? r[u].k2 : r[u].k1;
                     const bool rev = ((r[u].cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
                     uint32_t sl;
-                    if (key != NONE) {   // the slot the classify launch hit
+                    if (key < CK_MISS) {   // the slot the classify launch hit (else NONE or a miss tag)
                         sl = (key >> 1) - A.acct_base;
                     } else {
                         sl = rev ? find(A, o.da, o.sa, o.z1, o.w1)
@@ -1154,8 +1154,12 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             sl[u] = k < slots ? (uint32_t)k : NONE;
         }
 #pragma unroll
+        for (int u = 0; u < FU; u++)   // (no branches: the loads issue together)
+            m[u] = A.ms[sl[u] != NONE ? sl[u] : (uint32_t)(slots - 1)].x >> SUM_SH;
+#pragma unroll
         for (int u = 0; u < FU; u++)
-            m[u] = sl[u] != NONE ? A.ms[sl[u]].x >> SUM_SH : 0u;
+            if (sl[u] == NONE)
+                m[u] = 0;
 #pragma unroll
         for (int u = 0; u < FU; u++) {
             const uint64_t s = sl[u];
@@ -1417,7 +1421,7 @@ __device__ __forceinline__ int gc_map(const uint32_t *smaps, uint32_t n, uint32_
 // and zero accounting.  The log's places are taken once per block and step
 // (block_count_n): a steady-state GC deletes millions of entries, and one
 // atomic per wave on the shared counter serialised at its L2 channel.
-constexpr int GC_U = 4;
+constexpr int GC_U = 8;
 __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
 {
     __shared__ uint32_t smaps[CTG_MAX_MAPS], scnt[CTG_MAX_MAPS];
@@ -1435,10 +1439,14 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
         int j[GC_U];
         uint32_t life[GC_U], infy[GC_U];
 #pragma unroll
-        for (int u = 0; u < GC_U; u++) {
+        for (int u = 0; u < GC_U; u++) {   // (no branches: the loads issue together)
             const uint64_t s = base + u * 256 + threadIdx.x;
-            k[u] = s < A.slots ? ld16(A.ct4 + s) : make_uint4(0, 0, 0, 0);
+            k[u] = ld16(A.ct4 + (s < A.slots ? s : A.slots - 1));
         }
+#pragma unroll
+        for (int u = 0; u < GC_U; u++)
+            if (base + u * 256 + threadIdx.x >= A.slots)
+                k[u] = make_uint4(0, 0, 0, 0);
         // a tombstone, a claim, or an apply's delete the host has not taken
         // is no entry of a map
 #pragma unroll
@@ -1512,11 +1520,15 @@ __global__ __launch_bounds__(256) void k_ct_trim4(CtGcArgs A)
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * GC_U; base < A.slots; base += stride) {
         uint32_t w[GC_U], wn[GC_U];
 #pragma unroll
-        for (int u = 0; u < GC_U; u++) {
-            const uint64_t s = base + u * 256 + threadIdx.x;
-            w[u] = s < A.slots ? A.ct4[s].w : 0u;
-            wn[u] = s < A.slots ? A.ct4[(s + 1) & A.mask].w : 0u;
+        for (int u = 0; u < GC_U; u++) {   // (no branches: the loads issue together)
+            const uint64_t s = base + u * 256 + threadIdx.x, c = s < A.slots ? s : A.slots - 1;
+            w[u] = A.ct4[c].w;
+            wn[u] = A.ct4[(c + 1) & A.mask].w;
         }
+#pragma unroll
+        for (int u = 0; u < GC_U; u++)
+            if (base + u * 256 + threadIdx.x >= A.slots)
+                w[u] = 0;
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {
             if (w[u] != CT_TOMBSTONE || wn[u] != 0)
@@ -1640,13 +1652,13 @@ template <bool V6>
 int cta_scan_t(const CtaArgs &A, hipStream_t s)
 {
     if (A.lbr) {   // (after cta_lb_pre)
-        hipLaunchKernelGGL(k_cta_scan_lb<V6>, dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+        hipLaunchKernelGGL(k_cta_scan_lb<V6>, dim3(blocks_for(A.n, 2048)), dim3(256), 0, s, A);
         return hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
     if (A.mode == CFC_MODE_EGRESS)
-        hipLaunchKernelGGL((k_cta_scan<V6, true>), dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+        hipLaunchKernelGGL((k_cta_scan<V6, true>), dim3(blocks_for(A.n, 2048)), dim3(256), 0, s, A);
     else
-        hipLaunchKernelGGL((k_cta_scan<V6, false>), dim3(blocks_for(A.n, 8192)), dim3(256), 0, s, A);
+        hipLaunchKernelGGL((k_cta_scan<V6, false>), dim3(blocks_for(A.n, 2048)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -1801,8 +1813,8 @@ int ct_gc4(const CtGcArgs &A, hipStream_t s)
 {
     if (!A.slots || A.n_maps > CTG_MAX_MAPS)
         return -EINVAL;
-    hipLaunchKernelGGL(k_ct_gc4, dim3(blocks_for(A.slots, 8192)), dim3(256), 0, s, A);
-    hipLaunchKernelGGL(k_ct_trim4, dim3(blocks_for(A.slots, 8192)), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_ct_gc4, dim3(blocks_for(A.slots, 2048)), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_ct_trim4, dim3(blocks_for(A.slots, 2048)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -1818,7 +1830,7 @@ int ct_gc_log(const CtGcArgs &A, const CtLog *in, uint32_t n, CtLog *out, hipStr
 int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStream_t s)
 {
     if (slots)
-        hipLaunchKernelGGL(k_ct_nonfree4, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4,
+        hipLaunchKernelGGL(k_ct_nonfree4, dim3(blocks_for(slots, 2048)), dim3(256), 0, s, ct4,
                            slots, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

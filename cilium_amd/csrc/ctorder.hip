@@ -42,6 +42,9 @@
 // one, which an ICMP error's k2 lookup may find.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "ctops.hpp"
 
 namespace cfc {
@@ -75,7 +78,7 @@ __device__ __forceinline__ uint32_t start_slot(const CtaArgs &A, const OrdArgs &
     const uint32_t *ck = st ? O.ck2 : O.ck1;
     if (ck) {
         const uint32_t k = ck[i];
-        return k == NONE ? NONE : (k >> 1) - A.acct_base;
+        return k >= CK_MISS ? NONE : (k >> 1) - A.acct_base;
     }
     const Op<V6> o = decode<V6>(A, i, st);
     return find(A, o.sa, o.da, o.z2, o.w2);
@@ -85,9 +88,10 @@ __device__ __forceinline__ uint32_t start_slot(const CtaArgs &A, const OrdArgs &
 // stages in packet order, but most keys need no sort:
 //   * a key no stage of the batch writes keeps its batch-start existence:
 //     a dropped CT_NEW stage (no create) matters only when some allowed
-//     CT_NEW stage of the batch creates its key (the creates' fingerprints,
-//     k_ord_fpins), or when its key is an ICMP error's (a related entry a
-//     create may write: round 2);
+//     CT_NEW stage of the batch creates its key (the creates' pre-keys in
+//     a Bloom filter, k_ord_mark: a false positive only adds a
+//     participant), or when its key is an ICMP error's (a related entry a
+//     create may write: round 2), or with a load balancer (every one);
 //   * a key the batch only deletes (every stage on its slot a denied
 //     CT_ESTABLISHED: the common case, one verdict per flow) ends with its
 //     first delete in packet order; the later stages see it gone: CT_NEW,
@@ -99,84 +103,201 @@ __device__ __forceinline__ uint32_t start_slot(const CtaArgs &A, const OrdArgs &
 // stages whose key a create writes (or an ICMP error's), and the stages of
 // mixed slots.
 
-// mark: creates and deletes counted; per deleted slot its bit and its
-// first delete's order (read first: a hot flow's packets find them set)
+// A stage's pre-key: a hash of its k2 without the owner word (the CT map),
+// so without the destination-endpoint lookup a full decode needs: the raw
+// addresses and ct_probe's L4 word and flags for the stage's direction.
+// Equal k2 keys give equal pre-keys (outside a load balancer's service
+// step, which this is not used with); equal pre-keys of different keys only
+// add participants.
+template <bool V6>
+struct PreIn {   // the fields a pre-key derives from
+    Addr<V6> sa, da;
+    uint32_t pt, mt;
+};
+template <bool V6>
+__device__ __forceinline__ PreIn<V6> pre_in(const CtaArgs &A, uint64_t i)
+{
+    return PreIn<V6>{ld_addr<V6>(A.sa, i), ld_addr<V6>(A.da, i), A.pt[i], A.mt[i]};
+}
+template <bool V6>
+__device__ __forceinline__ uint64_t prekey_of(const CtaArgs &A, const PreIn<V6> &f, int st)
+{
+    const int dir = (A.mode == CFC_MODE_EGRESS && st == 0) ? CT_EGRESS : CT_INGRESS;
+    const CtProbe k = ct_probe<V6>(f.mt & 0xFF, f.pt, dir, 0);
+    uint32_t a, b;
+    if constexpr (V6) {
+        a = ct_hash4(f.sa.x, f.sa.y, f.sa.z, f.sa.w);
+        b = ct_hash4(f.da.x, f.da.y, f.da.z, f.da.w);
+    } else {
+        a = f.sa;
+        b = f.da;
+    }
+    return (uint64_t)ct_hash4(a, b, k.z2, k.w2) << 32 | ct_hash4(k.w2 ^ 0x27d4eb2fu, k.z2, b, a);
+}
+template <bool V6>
+__device__ __forceinline__ uint64_t prekey(const CtaArgs &A, uint64_t i, int st)
+{
+    return prekey_of<V6>(A, pre_in<V6>(A, i), st);
+}
+// an ICMP error's lookup (its k2 carries TUPLE_F_RELATED): types 3, 11, 12
+// (IPv4) / 1-4 (IPv6), ct_lookup4/6
+template <bool V6>
+__device__ __forceinline__ bool icmp_error(uint32_t mt, uint32_t pt)
+{
+    const uint32_t proto = mt & 0xFF, type = pt & 0xFF;
+    if (V6)
+        return proto == 58 && type >= 1 && type <= 4;
+    return proto == 1 && (type == 3 || type == 11 || type == 12);
+}
+// the creates' pre-keys: a blocked Bloom filter (one word, three bits)
+__device__ __forceinline__ void cb_put(const OrdArgs &O, uint64_t h)
+{
+    uint32_t *wp = O.cbloom + ((uint32_t)(h >> 32) & O.cb_mask);
+    const uint32_t b = bloom_bits((uint32_t)h);
+    if ((*wp & b) != b)
+        atomicOr(wp, b);
+}
+__device__ __forceinline__ bool cb_maybe(const OrdArgs &O, uint64_t h)
+{
+    const uint32_t b = bloom_bits((uint32_t)h);
+    return (O.cbloom[(uint32_t)(h >> 32) & O.cb_mask] & b) == b;
+}
+// a miss tag (kern_common.hpp ck_miss_tag) as a filter key
+__device__ __forceinline__ uint64_t tag_key(uint32_t t)
+{
+    return (uint64_t)fmix32(t) << 32 | (t * 0x9E3779B1u);
+}
+__device__ __forceinline__ bool tag_ok(uint32_t t) { return t >= CK_MISS && t != NONE; }
+constexpr int ORD_IT = 16;   // headers per thread and step (mark, collect)
+// The two passes over the whole batch (mark, collect) take ORD_IT headers
+// per thread and step (256 apart: coalesced): their CT bytes and verdicts
+// loaded together without branches (one wait), a cheap unrolled pass that
+// sorts the stages into bit masks (bit NST * k + st), then the rare stages
+// that need more (a key, a probe) in a loop that is not unrolled — with the
+// key derivation inlined once the kernel stays small enough for the
+// instruction cache.
+template <bool TWO>
+struct OrdStep {
+    static constexpr int NST = TWO ? 2 : 1;
+    uint32_t cb[ORD_IT];
+    int32_t ver[ORD_IT];
+    __device__ __forceinline__ void load(const CtaArgs &A, uint64_t base)
+    {
+#pragma unroll
+        for (int k = 0; k < ORD_IT; k++) {
+            const uint64_t i = base + 256ull * k + threadIdx.x;
+            const uint64_t j = i < A.n ? i : A.n - 1;
+            cb[k] = A.ctb[j];
+            ver[k] = A.ver[j];
+        }
+#pragma unroll
+        for (int k = 0; k < ORD_IT; k++)
+            if (base + 256ull * k + threadIdx.x >= A.n)
+                cb[k] = 0;
+    }
+    // res: the stage's CT result, or -1 (no CT stage)
+    __device__ __forceinline__ int res(int k, int st, bool &dropped) const
+    {
+        const uint32_t cs = (cb[k] >> (4 * st)) & 0xF;
+        const int last = (cb[k] & (CFC_CT_DONE << 4)) ? 1 : 0;
+        dropped = st == last && ver[k] == DROP_POLICY;
+        return (cs & CFC_CT_DONE) ? (int)(cs & CFC_CT_RES_MASK) : -1;
+    }
+    __device__ __forceinline__ static uint64_t hdr(uint64_t base, int b)
+    {
+        return base + 256ull * (b / NST) + threadIdx.x;
+    }
+};
+
+// mark: creates and deletes counted; the creates' pre-keys into the Bloom
+// filter; per deleted slot its bit and its first delete's order (read
+// first: a hot flow's packets find them set)
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
 {
-    constexpr int NST = TWO ? 2 : 1;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    uint32_t ncr = 0, ndel = 0;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
-        const uint64_t i = base + threadIdx.x;
-        const uint32_t cb = i < A.n ? A.ctb[i] : 0u;
-        const int32_t ver = i < A.n ? A.ver[i] : 0;
-        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    using S = OrdStep<TWO>;
+    constexpr int NST = S::NST;
+    const uint64_t span = 256ull * ORD_IT, stride = (uint64_t)gridDim.x * span;
+    uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < A.n; base += stride) {
+        S x;
+        x.load(A, base);
+        uint32_t crm = 0, delm = 0;
 #pragma unroll
-        for (int st = 0; st < NST; st++) {
-            const uint32_t cs = (cb >> (4 * st)) & 0xF;
-            if (!(cs & CFC_CT_DONE))
-                continue;
-            const uint32_t res = cs & CFC_CT_RES_MASK;
-            const bool dropped = st == last && ver == DROP_POLICY;
-            ncr += res == CT_NEW && !dropped;
-            if (res == CT_ESTABLISHED && dropped) {
-                const uint32_t sl = start_slot<V6>(A, O, i, st);
-                if (sl != NONE) {
-                    const uint32_t b = 1u << (sl & 31), ord = (uint32_t)(i << 1) | (uint32_t)st;
-                    if (!(O.delbm[sl >> 5] & b))
-                        atomicOr(&O.delbm[sl >> 5], b);
-                    if (ord < O.dfirst[sl])
-                        atomicMin(&O.dfirst[sl], ord);
-                    ndel++;
+        for (int k = 0; k < ORD_IT; k++)
+#pragma unroll
+            for (int st = 0; st < NST; st++) {
+                bool dropped;
+                const int r = x.res(k, st, dropped);
+                const uint32_t bit = 1u << (NST * k + st);
+                if (r == CT_NEW) {
+                    nnd += dropped;
+                    crm |= dropped ? 0u : bit;
+                } else if (r == CT_ESTABLISHED) {
+                    nest++;
+                    delm |= dropped ? bit : 0u;
                 }
             }
+        ncr += __popc(crm);
+        ndt += __popc(delm);
+        if (O.cbloom && O.tagged) {
+            // the creates' miss tags, loaded together (predicated: creates
+            // are sparse), then into the filter
+            uint32_t tg[ORD_IT * NST];
+#pragma unroll
+            for (int q = 0; q < ORD_IT * NST; q++) {
+                tg[q] = NONE;
+                if ((crm >> q) & 1)
+                    tg[q] = ((q % NST) ? O.ck2 : O.ck1)[S::hdr(base, q)];
+            }
+#pragma unroll
+            for (int q = 0; q < ORD_IT * NST; q++)
+                if ((crm >> q) & 1) {
+                    if (tag_ok(tg[q]))
+                        cb_put(O, tag_key(tg[q]));
+                    else
+                        nun++;
+                }
+        }
+        // else the creates' pre-keys, per chunk of PK headers with their
+        // fields loaded together (as k_ord_collect's probes)
+        constexpr int PK = V6 ? 8 : 16;
+#pragma unroll
+        for (int c = 0; c < ORD_IT && !O.tagged; c += PK) {
+            const uint32_t cm = (uint32_t)(((1ull << (NST * PK)) - 1u) << (NST * c));
+            if (!O.cbloom || !__any(crm & cm))   // (wave-uniform)
+                continue;
+            PreIn<V6> f[PK];
+#pragma unroll
+            for (int k = 0; k < PK; k++) {
+                const uint64_t i = base + 256ull * (c + k) + threadIdx.x;
+                f[k] = pre_in<V6>(A, i < A.n ? i : A.n - 1);
+            }
+#pragma unroll
+            for (int q = 0; q < PK * NST; q++)
+                if ((crm >> (NST * c + q)) & 1)
+                    cb_put(O, prekey_of<V6>(A, f[q / NST], q % NST));
+        }
+        for (uint32_t m = delm; m; m &= m - 1) {
+            const int b = __ffs(m) - 1, st = b % NST;
+            const uint64_t i = S::hdr(base, b);
+            const uint32_t sl = start_slot<V6>(A, O, i, st);
+            if (sl == NONE)
+                continue;
+            const uint32_t bb = 1u << (sl & 31), ord = (uint32_t)(i << 1) | (uint32_t)st;
+            if (!(O.delbm[sl >> 5] & bb))
+                atomicOr(&O.delbm[sl >> 5], bb);
+            if (ord < O.dfirst[sl])
+                atomicMin(&O.dfirst[sl], ord);
+            ndel++;
         }
     }
     block_add(&O.cnt[ORD_NCREATE], ncr);
     block_add(&O.cnt[ORD_NDEL], ndel);
-}
-
-// the creates' k2 fingerprints into an open-addressed set (fp | 1, 0 free)
-__device__ __forceinline__ void fp_put(const OrdArgs &O, uint64_t fp)
-{
-    fp |= 1ull;
-    for (uint32_t j = (uint32_t)(fp >> 32) & O.fp_mask;; j = (j + 1) & O.fp_mask) {
-        const unsigned long long cur =
-            atomicCAS((unsigned long long *)O.fpset + j, 0ull, (unsigned long long)fp);
-        if (cur == 0 || cur == fp)
-            return;
-    }
-}
-__device__ __forceinline__ bool fp_has(const OrdArgs &O, uint64_t fp)
-{
-    fp |= 1ull;
-    for (uint32_t j = (uint32_t)(fp >> 32) & O.fp_mask;; j = (j + 1) & O.fp_mask) {
-        const uint64_t cur = O.fpset[j];
-        if (cur == fp)
-            return true;
-        if (cur == 0)
-            return false;
-    }
-}
-template <bool V6, bool TWO>
-__global__ __launch_bounds__(256) void k_ord_fpins(CtaArgs A, OrdArgs O)
-{
-    constexpr int NST = TWO ? 2 : 1;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= A.n)
-        return;
-    const uint32_t cb = A.ctb[i];
-    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
-#pragma unroll
-    for (int st = 0; st < NST; st++) {
-        const uint32_t cs = (cb >> (4 * st)) & 0xF;
-        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW ||
-            (st == last && A.ver[i] == DROP_POLICY))
-            continue;
-        const Op<V6> o = decode<V6>(A, i, st);
-        fp_put(O, fp64(o.sa, o.da, o.z2, o.w2));
-    }
+    block_add(&O.cnt[ORD_NNEWDROP], nnd);
+    block_add(&O.cnt[ORD_NEST], nest);
+    block_add(&O.cnt[ORD_NESTDROP], ndt);
+    block_add(&O.cnt[ORD_UNTAGGED], nun);
 }
 
 // mixed: a deleted slot with an allowed CT_ESTABLISHED stage
@@ -202,50 +323,112 @@ __global__ __launch_bounds__(256) void k_ord_mixed(CtaArgs A, OrdArgs O)
     }
 }
 
-// collect the participants (header << 1 | stage); count only when O.part
-// is null
+// collect the participants (header << 1 | stage) into O.part: a block's one
+// atomic on the list's length covers 256 * ORD_IT headers (a counter every
+// block of a 64M-header pass bumps serialises at its L2 channel)
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
 {
-    constexpr int NST = TWO ? 2 : 1;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    using S = OrdStep<TWO>;
+    constexpr int NST = S::NST;
+    const uint64_t span = 256ull * ORD_IT, stride = (uint64_t)gridDim.x * span;
     // (every thread runs the same number of steps: block_count_n)
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
-        const uint64_t i = base + threadIdx.x;
-        const uint32_t cb = i < A.n ? A.ctb[i] : 0u;
-        const int32_t ver = i < A.n ? A.ver[i] : 0;
-        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
-        uint32_t want[2] = {0, 0}, nw = 0;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < A.n; base += stride) {
+        S x;
+        x.load(A, base);
+        uint32_t bits = 0, probe = 0, estm = 0;
 #pragma unroll
-        for (int st = 0; st < NST; st++) {
-            const uint32_t cs = (cb >> (4 * st)) & 0xF;
-            if (!(cs & CFC_CT_DONE))
-                continue;
-            const uint32_t res = cs & CFC_CT_RES_MASK;
-            const bool dropped = st == last && ver == DROP_POLICY;
-            bool w = false;
-            if (res == CT_NEW) {
-                w = !dropped;
-                if (dropped) {
-                    const Op<V6> o = decode<V6>(A, i, st);
-                    w = (o.w2 & 0x200u) || (O.fpset && fp_has(O, fp64(o.sa, o.da, o.z2, o.w2)));
+        for (int k = 0; k < ORD_IT; k++)
+#pragma unroll
+            for (int st = 0; st < NST; st++) {
+                bool dropped;
+                const int r = x.res(k, st, dropped);
+                const uint32_t bit = 1u << (NST * k + st);
+                if (r == CT_NEW) {
+                    // (with a service step every dropped CT_NEW stage takes part)
+                    if (!dropped || A.lbr)
+                        bits |= bit;
+                    else
+                        probe |= bit;
+                } else if (r == CT_ESTABLISHED) {
+                    estm |= bit;
                 }
-            } else if (res == CT_ESTABLISHED && O.ndel) {
-                const uint32_t sl = start_slot<V6>(A, O, i, st);
-                w = sl != NONE && ((O.mixbm[sl >> 5] >> (sl & 31)) & 1);
             }
-            want[st] = w;
-            nw += w;
-        }
-        uint32_t r = block_count_n(&O.cnt[ORD_NPART], nw);
-        if (O.part) {
+        // the probes (a quarter to a half of a policy-heavy batch's headers
+        // are dropped CT_NEW stages): with miss tags, the tags and then their
+        // filter words loaded together — two waits per step
+        if (O.tagged) {
+            uint32_t tg[ORD_IT * NST], fw[ORD_IT * NST];
 #pragma unroll
-            for (int st = 0; st < NST; st++)
-                if (want[st]) {
-                    if (r < O.part_cap)
-                        O.part[r] = (uint32_t)(i << 1) | (uint32_t)st;
-                    r++;
-                }
+            for (int q = 0; q < ORD_IT * NST; q++) {
+                tg[q] = NONE;
+                if ((probe >> q) & 1)
+                    tg[q] = ((q % NST) ? O.ck2 : O.ck1)[S::hdr(base, q)];
+            }
+#pragma unroll
+            for (int q = 0; q < ORD_IT * NST; q++) {
+                fw[q] = 0;
+                if (((probe >> q) & 1) && O.cbloom && tag_ok(tg[q]))
+                    fw[q] = O.cbloom[(uint32_t)(tag_key(tg[q]) >> 32) & O.cb_mask];
+            }
+#pragma unroll
+            for (int q = 0; q < ORD_IT * NST; q++) {
+                // (an untagged stage, an ICMP error's, or a possible create's key)
+                const uint32_t fb = bloom_bits((uint32_t)tag_key(tg[q]));
+                if (((probe >> q) & 1) &&
+                    (!tag_ok(tg[q]) || (tg[q] & 1) || (O.cbloom && (fw[q] & fb) == fb)))
+                    bits |= 1u << q;
+            }
+        }
+        // else per chunk of PK headers their fields loaded together (clamped,
+        // no branches), then their filter words together — two waits per
+        // chunk rather than two per probe
+        constexpr int PK = V6 ? 8 : 16;
+#pragma unroll
+        for (int c = 0; c < ORD_IT && !O.tagged; c += PK) {
+            const uint32_t cm = (uint32_t)(((1ull << (NST * PK)) - 1u) << (NST * c));
+            if (!__any(probe & cm))   // (wave-uniform)
+                continue;
+            PreIn<V6> f[PK];
+#pragma unroll
+            for (int k = 0; k < PK; k++) {
+                const uint64_t i = base + 256ull * (c + k) + threadIdx.x;
+                f[k] = pre_in<V6>(A, i < A.n ? i : A.n - 1);
+            }
+            uint64_t hk[PK * NST];
+            bool ie[PK];
+#pragma unroll
+            for (int k = 0; k < PK; k++) {
+                ie[k] = icmp_error<V6>(f[k].mt, f[k].pt);
+#pragma unroll
+                for (int st = 0; st < NST; st++)
+                    hk[NST * k + st] = prekey_of<V6>(A, f[k], st);
+            }
+            uint32_t fw[PK * NST];
+#pragma unroll
+            for (int q = 0; q < PK * NST; q++)
+                fw[q] = O.cbloom ? O.cbloom[(uint32_t)(hk[q] >> 32) & O.cb_mask] : 0u;
+#pragma unroll
+            for (int q = 0; q < PK * NST; q++) {
+                const int b = NST * c + q;
+                const uint32_t fb = bloom_bits((uint32_t)hk[q]);
+                if (((probe >> b) & 1) && (ie[q / NST] || (O.cbloom && (fw[q] & fb) == fb)))
+                    bits |= 1u << b;
+            }
+        }
+        if (O.ndel)
+            for (uint32_t m = estm; m; m &= m - 1) {
+                const int b = __ffs(m) - 1;
+                const uint32_t sl = start_slot<V6>(A, O, S::hdr(base, b), b % NST);
+                if (sl != NONE && ((O.mixbm[sl >> 5] >> (sl & 31)) & 1))
+                    bits |= 1u << b;
+            }
+        uint32_t r = block_count_n(&O.cnt[ORD_NPART], (uint32_t)__popc(bits));
+        for (uint32_t m = bits; m; m &= m - 1) {
+            const int b = __ffs(m) - 1;
+            if (r < O.part_cap)
+                O.part[r] = (uint32_t)(S::hdr(base, b) << 1) | (uint32_t)(b % NST);
+            r++;
         }
     }
 }
@@ -474,7 +657,7 @@ template <bool V6>
 int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, hipStream_t s)
 {
     const bool two = A.mode == CFC_MODE_EGRESS;
-    const unsigned g = grid_for(A.n, 8192);
+    const unsigned g = grid_for(A.n, 2048);
     const unsigned gn = grid_for(A.n, 1u << 30);
     uint32_t hc[ORD_NCNT];
     auto rd = [&]() {
@@ -492,36 +675,75 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     if (hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
         return -EIO;
     O.part = nullptr;
-    O.fpset = nullptr;
+    O.cbloom = nullptr;
     O.ndel = 0;
+    // the creates' pre-keys: a filter of about one word per create, sized by
+    // the last batch's count (mark inserts them as it counts); a batch with
+    // many more creates than that runs mark again on a filter of its size
+    auto filter = [&](uint32_t nc) {
+        uint32_t words = 1024;
+        while (words < nc && words < (1u << 26))
+            words *= 2;
+        if (B.fpset.ensure(4ull * words) || hipMemsetAsync(B.fpset.p, 0, 4ull * words, s) != hipSuccess)
+            return false;
+        O.cbloom = (uint32_t *)B.fpset.p;
+        O.cb_mask = words - 1;
+        return true;
+    };
+    // keys from the classify launch's miss tags when this apply follows it
+    // (outside a service step); mark counts the creates without one, and a
+    // batch with any runs mark again on pre-keys
+    O.tagged = A.ck1 && (!two || A.ck2) && !A.lbr;
+    if (!filter(B.creates_hint))
+        return -ENOMEM;
     ORD_LAUNCH(k_ord_mark, g, A, O);
     if (!rd())
         return -EIO;
-    const uint32_t ncr = hc[ORD_NCREATE];
-    O.ndel = hc[ORD_NDEL];
-    if (ncr) {   // the creates' key set, for the dropped CT_NEW stages
-        uint32_t cap = 1024;
-        while (cap < 4ull * ncr && cap < (1u << 30))
-            cap *= 2;
-        if (B.fpset.ensure(8ull * cap) || hipMemsetAsync(B.fpset.p, 0, 8ull * cap, s) != hipSuccess)
+    const bool untagged = O.tagged && hc[ORD_UNTAGGED];
+    if (untagged || (hc[ORD_NCREATE] > 4ull * (O.cb_mask + 1) && O.cb_mask + 1 < (1u << 26))) {
+        // (the delete marks are idempotent; the counts start again)
+        O.tagged = O.tagged && !untagged;
+        if (!filter(hc[ORD_NCREATE]) || hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
             return -ENOMEM;
-        O.fpset = (uint64_t *)B.fpset.p;
-        O.fp_mask = cap - 1;
-        ORD_LAUNCH(k_ord_fpins, gn, A, O);
+        ORD_LAUNCH(k_ord_mark, g, A, O);
+        if (!rd())
+            return -EIO;
     }
+    const uint32_t ncr = hc[ORD_NCREATE];
+    B.creates_hint = ncr;
+    O.ndel = hc[ORD_NDEL];
+    if (!ncr)
+        O.cbloom = nullptr;
     if (O.ndel)
         ORD_LAUNCH(k_ord_mixed, gn, A, O);
+    // one collect, into room for every stage that may take part
+    const uint64_t cap = (uint64_t)ncr + hc[ORD_NNEWDROP] + (O.ndel ? hc[ORD_NEST] : 0u);
+    if (cap > 0x3FFFFFFFull)
+        return -E2BIG;
+    if (!cap)
+        return 0;
+    if (B.part.ensure(4 * cap))
+        return -ENOMEM;
+    O.part = (uint32_t *)B.part.p;
+    O.part_cap = (uint32_t)cap;
     ORD_LAUNCH(k_ord_collect, g, A, O);
     if (!rd())
         return -EIO;
     const uint64_t np = hc[ORD_NPART];
-    if (np > 0x3FFFFFFFull)
-        return -E2BIG;
+    if (np > cap)
+        return -EIO;
+    static const bool dbg = getenv("CFC_DEBUG_ORDER") != nullptr;
+    if (dbg)
+        fprintf(stderr,
+                "ord: n %llu creates %u dropped-new %u est %u dropped-est %u deletes %u "
+                "participants %llu tagged %d\n",
+                (unsigned long long)A.n, ncr, hc[ORD_NNEWDROP], hc[ORD_NEST], hc[ORD_NESTDROP],
+                O.ndel, (unsigned long long)np, (int)O.tagged);
     if (np) {
-        // buffers: participants, and up to twice as many records
+        // records: up to twice as many as participants
         const uint64_t nr = 2 * np;
         const size_t kw = V6 ? 48 : 16;
-        if (B.part.ensure(4 * np) || B.rel_src.ensure(4 * np) || B.rk.ensure(kw * nr) ||
+        if (B.rel_src.ensure(4 * np) || B.rk.ensure(kw * nr) ||
             B.rh.ensure(8 * nr) || B.rh2.ensure(8 * nr) || B.rh3.ensure(8 * nr) ||
             B.rord.ensure(4 * nr) || B.rord2.ensure(4 * nr) || B.ridx.ensure(4 * nr) ||
             B.ridx2.ensure(4 * nr) || B.pinfo.ensure(nr) || B.nres.ensure(nr))
@@ -535,7 +757,6 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
             if (B.tmp.ensure(std::max(t1, t2)))
                 return -ENOMEM;
         }
-        O.part = (uint32_t *)B.part.p;
         O.part_cap = (uint32_t)np;
         O.rel_src = (uint32_t *)B.rel_src.p;
         O.rk = B.rk.p;
@@ -550,9 +771,6 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         O.nres = (uint8_t *)B.nres.p;
         O.tmp = B.tmp.p;
         O.tmp_bytes = B.tmp.bytes;
-        if (hipMemsetAsync(O.cnt + ORD_NPART, 0, 4, s) != hipSuccess)
-            return -EIO;
-        ORD_LAUNCH(k_ord_collect, g, A, O);
         const uint32_t npi = (uint32_t)np;
         const unsigned gp = (unsigned)((npi + 255) / 256);
         hipLaunchKernelGGL(k_ord_keys<V6>, dim3(gp), dim3(256), 0, s, A, O, npi, 0u);

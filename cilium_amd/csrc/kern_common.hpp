@@ -610,6 +610,30 @@ __device__ __forceinline__ uint32_t ct_acct_key(uint32_t slot, int dir)
 {
     return slot == NONE ? NONE : slot * 2 + (uint32_t)dir;
 }
+// A CT_NEW stage leaves in the same key array a tag instead: CK_MISS | a
+// hash of its k2 (owner word included) | 1 when k2 carries TUPLE_F_RELATED
+// (an ICMP error's); never NONE.  The packet-order pass compares the
+// creates' keys with the dropped CT_NEW stages' through them (ctorder.hip)
+// without reading the headers again.  Counting skips every key >= CK_MISS
+// (hit keys are slot * 2 + dir < 2^27).
+constexpr uint32_t CK_MISS = 0x80000000u;
+__device__ __forceinline__ uint32_t ck_miss_tag(uint32_t h, uint32_t w2)
+{
+    return CK_MISS | (h & 0x7FFFFFFCu) | ((w2 & 0x200u) ? 1u : 0u);
+}
+__device__ __forceinline__ uint32_t ck_miss4(uint32_t sa, uint32_t da, uint32_t proto,
+                                             uint32_t pt, int dir, uint32_t owner)
+{
+    const CtProbe k = ct_probe<false>(proto, pt, dir, owner);
+    return ck_miss_tag(ct_hash4(sa, da, k.z2, k.w2), k.w2);
+}
+__device__ __forceinline__ uint32_t ck_miss6(const uint4 &sa, const uint4 &da, uint32_t proto,
+                                             uint32_t pt, int dir, uint32_t owner)
+{
+    const CtProbe k = ct_probe<true>(proto, pt, dir, owner);
+    return ck_miss_tag(ct_hash4(ct_hash4(sa.x, sa.y, sa.z, sa.w),
+                                ct_hash4(da.x, da.y, da.z, da.w), k.z2, k.w2), k.w2);
+}
 
 // CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257): the hit
 // entry's rx (ingress) or tx (egress) packets/bytes

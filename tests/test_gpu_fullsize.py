@@ -118,8 +118,10 @@ def test_c5_full_flows(torch):
         a, e = k * len(h) // 2, (k + 1) * len(h) // 2
         sub = b.slice(a, e)
         out = dp.classify(sub, 3, want_ct=True, want_notify=True)
-        rec, idx, total = dp.monitor_events(sub, out, 3)
+        # (the events after the apply: it rewrites the CT results and monitor
+        # lengths into packet order, DESIGN.md §4 "Packet order")
         dp.ct_apply(sub, out, 3)
+        rec, idx, total = dp.monitor_events(sub, out, 3)
         part = h.slice(a, e)
         oa, ov, oi, oct_, ow = o.classify(part, 3, 0, nthreads=16, want_ct=True,
                                           want_notify=True, apply_ct=True)
