@@ -78,7 +78,7 @@ struct GLb {           // load balancing: services, reverse NAT
     uint64_t bytes = 0;
 };
 struct GCt {           // conntrack
-    DevBuf ct4, ct6, ct_acct, ct4_tm, ct6_tm;
+    DevBuf ct4, ct6, ct_acct, ct_sum, ct4_tm, ct6_tm;
     DevBuf ct4_lb, ct6_lb;                // per-slot LB state (with a load balancer)
     DevBuf ct4_info, ct4_ms;   // device CT apply state (ctapply.hip)
     DevBuf ct6_info, ct6_ms;
@@ -166,7 +166,14 @@ struct cfc_ctx {
         int mode = 0, family = 4;
         uint16_t ep = 0;
         size_t k1 = 0, k2 = 0;   // byte offsets in ws; k2 = 0: no stage 2
+        bool sum = false;        // its accounting wrote the plain-hit summaries
     } last_cls;
+    // DevTables.ct_sum holds summaries no apply has taken (cleared before
+    // the next launch that keeps them); sum_pending: the last launch kept
+    // summaries and no apply has followed it yet; sum_want: launches keep
+    // them — off once a launch's went unused (a lookup-only stream pays
+    // nothing), on again when an apply follows its launch
+    bool sum_dirty = false, sum_pending = false, sum_want = true;
     uint64_t log_used = 0;       // CtLog entries since the last sync
     DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
     DevBuf cta_lbr, cta_reqs;     // a load balancer's service step per header (LbRec4/6)
@@ -964,7 +971,8 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
         (*rc = upload_vec(g->ct6_lb, img.ct6_lb, s)))
         return nullptr;
     const size_t nslots = img.ct4.size() + img.ct6.size();
-    if (nslots && (*rc = g->ct_acct.zeros(32 * nslots, s)))
+    if (nslots && ((*rc = g->ct_acct.zeros(32 * nslots, s)) ||
+                   (*rc = g->ct_sum.zeros(4 * nslots, s))))
         return nullptr;
     const size_t n4 = img.ct4.size(), n6 = img.ct6.size();
     if (n4 && ((*rc = g->ct4_info.zeros(sizeof(CtInfo) * n4, s)) ||
@@ -1034,6 +1042,7 @@ void assemble(Epoch &E)
     T.ct4 = (C.n_ct4 || !C.ct4_host.empty()) ? (const Ct4Slot *)C.ct4.p : nullptr;
     T.ct6 = (C.n_ct6 || !C.ct6_host.empty()) ? (const Ct6Slot *)C.ct6.p : nullptr;
     T.ct_acct = (uint64_t *)C.ct_acct.p;
+    T.ct_sum = (uint32_t *)C.ct_sum.p;
     T.ct4_tm = (const CtTimer *)C.ct4_tm.p;
     T.ct6_tm = (const CtTimer *)C.ct6_tm.p;
     T.ct4_mask = C.ct4_mask;
@@ -1896,10 +1905,13 @@ int nat_hop(cfc_ctx *c, const DevTables &T, const EgressArgs &ea, const Hdr &in,
     r.o.ct = (uint8_t *)(op + 4 * m4);
     EgressArgs e2 = ea;
     e2.nat_idx = e2.nat_cnt = nullptr;
+    e2.sums = nullptr;
     const int smode = V6 ? CFC_MODE_EGRESS : CFC_MODE_INGRESS;
     const WsLayout wl = ws_layout(m, T, smode, true);
     if (r.ws.ensure(wl.total))
         return -ENOMEM;
+    DevTables Th = T;   // (a hop launch keeps no plain-hit summaries)
+    Th.ct_sum = nullptr;
     int rc;
     if constexpr (V6) {   // NAT64: IPv4 egress rows
         NatHop4 h{};
@@ -1912,7 +1924,7 @@ int nat_hop(cfc_ctx *c, const DevTables &T, const EgressArgs &ea, const Hdr &in,
         r.h4 = cfc_hdr_v4{h.sa, h.da, h.pt, h.mt, nullptr, h.tf, m, h.hash};
         rc = nat64_gather(in, idx, m, ea.nat_v4, h, s);
         if (!rc)
-            rc = launch_classify_v4(T, r.h4, r.o, smode, e2, c->ctr, (uint32_t *)r.ws.p,
+            rc = launch_classify_v4(Th, r.h4, r.o, smode, e2, c->ctr, (uint32_t *)r.ws.p,
                                     c->num_cus, s, nullptr);
     } else {              // NAT46: IPv6 ingress rows
         NatHop6 h{};
@@ -1929,7 +1941,7 @@ int nat_hop(cfc_ctx *c, const DevTables &T, const EgressArgs &ea, const Hdr &in,
         rc = nat46_gather(T, in, out.identity, idx, m, (const uint4 *)c->epoch->ep->nat6.p, h,
                           s);
         if (!rc)
-            rc = launch_classify_v6(T, r.h6, r.o, smode, e2, c->ctr, (uint32_t *)r.ws.p,
+            rc = launch_classify_v6(Th, r.h6, r.o, smode, e2, c->ctr, (uint32_t *)r.ws.p,
                                     c->num_cus, s, nullptr);
     }
     if (!rc)
@@ -2030,8 +2042,24 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     // the workspace is shared: order this launch after the previous one
     if (c->ctr_pending && c->last_stream != s)
         (void)hipStreamWaitEvent(s, c->last_done, 0);
+    // plain-hit summaries: only of this launch (a batch with NAT hops keeps
+    // none: its apply takes the scan's)
+    if (c->sum_pending)   // (the last launch's went unused)
+        c->sum_want = false;
+    c->sum_pending = false;
+    if (nat_list || !out->ct || !c->sum_want)   // (no CT bytes: no apply can follow)
+        T.ct_sum = nullptr;
+    if (T.ct_sum && c->sum_dirty) {
+        if (hipMemsetAsync(T.ct_sum, 0, E.ct->ct_sum.bytes, s) != hipSuccess)
+            return -EIO;
+        c->sum_dirty = false;
+    }
+    bool sums = false;
+    ea.sums = &sums;
     rc = launch(T, *in, *out, mode, ea, c->ctr, c->ws, c->num_cus, s,
                 in->n ? next_timing(c, std::is_same<Hdr, cfc_hdr_v6>::value) : nullptr);
+    c->sum_dirty |= sums;
+    c->sum_pending = sums;
     if (rc)
         return rc;
     if (nat_list) {
@@ -2058,6 +2086,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         L.ep = ep_lxc;
         L.k1 = wl.ct;
         L.k2 = mode == CFC_MODE_EGRESS ? wl.ct2 : 0;
+        L.sum = sums;
     }
     return 0;
 }
@@ -3002,6 +3031,12 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             L.saddr == (const void *)in->saddr && L.n == n && L.mode == mode && L.ep == ep_lxc) {
             A.ck1 = (const uint32_t *)((const char *)c->ws + L.k1);
             A.ck2 = L.k2 ? (const uint32_t *)((const char *)c->ws + L.k2) : nullptr;
+            // and its plain-hit summaries (taken once: this apply clears them)
+            if (L.sum && c->sum_dirty && G.ct_sum.p)
+                A.sum = (uint32_t *)G.ct_sum.p + A.acct_base;
+            c->last_cls.sum = false;
+            c->sum_want = true;   // (applies follow their launches: keep them)
+            c->sum_pending = false;
         }
     }
     // a load balancer's service step first: the ordering pass and the scan
@@ -3205,6 +3240,8 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     ins += hc[CTA_CLAIMS];
     log_used += hc[CTA_NLOG];
     c->cta_seq++;
+    if (A.sum)   // (the finish cleared every summary the launch wrote)
+        c->sum_dirty = false;
     return 0;
 }
 

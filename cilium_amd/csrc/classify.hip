@@ -1054,8 +1054,12 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
 //                  its run of every chunk of its coarse region, LDS sums per
 //                  key, then its counters, which no other workgroup touches
 // Records: key (26 bits) << 38 | kind << 37 | payload; kind 0: packets (16)
-// << 21 | bytes (21); kind 1: bytes >> 21 (the high part of an LDS entry's
-// byte count, which can pass 2^21).
+// << 21 | bytes (21) of an LDS entry; kind 1: one << 25 | hit flags (9) << 16
+// | low (16): one = 1, a single packet of length low (the overflow), else an
+// LDS entry's high part (bytes >> 21, which can pass 0) and its flags.
+// Hit flags (acc_flags): the TCP flags, and 1 << 8 for a TCP packet without
+// the close bit — per key (slot, direction) the plain-hit summary the device
+// CT apply needs (k_acc_reduce writes it into DevTables.ct_sum).
 constexpr uint32_t CTP_BUCKET_BITS = 12, CTP_BUCKET = 1u << CTP_BUCKET_BITS;
 constexpr uint32_t CTP_MAX_BUCKETS = 16384;    // keys < 2^26 (32M CT slots)
 constexpr uint32_t ACC_FINE_BITS = 7, ACC_FINE = 1u << ACC_FINE_BITS;
@@ -1071,9 +1075,9 @@ static_assert(CTP_BUCKET % BLOCK == 0, "reduce flush");
 constexpr int ACC_COARSE_SHIFT = 38 + CTP_BUCKET_BITS + ACC_FINE_BITS;   // 57
 constexpr int ACC_BUCKET_SHIFT = 38 + CTP_BUCKET_BITS;                   // 50
 constexpr uint32_t ACC_AGG_LDS =
-    CT_LDS_SLOTS * 12 + ACC_SLICE_CHUNKS * ACC_MAX_COARSE * 4 + 16;
+    CT_LDS_SLOTS * 16 + ACC_SLICE_CHUNKS * ACC_MAX_COARSE * 4 + 16;
 constexpr uint32_t ACC_SORT_LDS = ACC_CHUNK * 8 + 3 * ACC_MAX_COARSE * 4 + 16;
-constexpr uint32_t ACC_RED_LDS = CTP_BUCKET * 12;
+constexpr uint32_t ACC_RED_LDS = CTP_BUCKET * 16;
 
 // slice of one k_acc_agg workgroup: <= COUNT_PER_BLOCK headers (a multiple
 // of 4), sized so that a large batch's slices come in whole rounds of 256
@@ -1091,6 +1095,17 @@ uint64_t acc_slice(uint64_t n)
 __device__ __forceinline__ uint64_t acc_rec(uint32_t k, uint32_t pk, uint32_t by)
 {
     return (uint64_t)k << 38 | (uint64_t)pk << 21 | by;
+}
+// kind 1: a single packet (one) or an LDS entry's high bytes, with flags
+__device__ __forceinline__ uint64_t acc_rec1(uint32_t k, bool one, uint32_t fl, uint32_t low)
+{
+    return (uint64_t)k << 38 | 1ull << 37 | (one ? 1ull << 25 : 0ull) | (uint64_t)fl << 16 | low;
+}
+// a header's hit flags (sum_bits in ctops.hpp, per direction)
+__device__ __forceinline__ uint32_t acc_flags(uint32_t meta, uint32_t tf)
+{
+    const bool tcp = (meta & 0xFF) == 6;
+    return tcp ? ((tf & 0xFF) | ((meta & CFC_HF_TCP_CLOSE) ? 0u : 0x100u)) : 0u;
 }
 
 // slot of this lane in an LDS-counted list, one atomic per wave (the lanes
@@ -1117,17 +1132,20 @@ constexpr int CTP_PROBES = 3;
 template <bool VEC>
 __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
                                                    const uint32_t *ct_idx2,
-                                                   const uint32_t *meta, uint64_t n,
+                                                   const uint32_t *meta, const uint8_t *tf,
+                                                   bool sums, uint64_t n,
                                                    uint32_t nco, uint64_t *rec,
                                                    uint32_t *rcnt, uint32_t *cnt, uint64_t per)
 {
     uint32_t *keys = reinterpret_cast<uint32_t *>(cfc_smem);
     unsigned long long *vals = reinterpret_cast<unsigned long long *>(keys + CT_LDS_SLOTS);
-    uint32_t *hist = reinterpret_cast<uint32_t *>(vals + CT_LDS_SLOTS);
+    uint32_t *fls = reinterpret_cast<uint32_t *>(vals + CT_LDS_SLOTS);
+    uint32_t *hist = fls + CT_LDS_SLOTS;
     uint32_t *nrec = hist + ACC_SLICE_CHUNKS * ACC_MAX_COARSE;
     for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {
         keys[j] = NONE;
         vals[j] = 0;
+        fls[j] = 0;
     }
     for (uint32_t j = threadIdx.x; j < ACC_SLICE_CHUNKS * ACC_MAX_COARSE; j += BLOCK)
         hist[j] = 0;
@@ -1147,7 +1165,7 @@ __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
     };
     // one header: its LDS entry, or a record of its own (every lane of the
     // wave calls it)
-    auto one = [&](uint32_t k, uint32_t len) {
+    auto one = [&](uint32_t k, uint32_t len, uint32_t fl) {
         uint32_t h = fmix32(k) & (CT_LDS_SLOTS - 1);
         bool done = k >= CK_MISS;   // (NONE, or a CT_NEW stage's tag)
         for (int p = 0; p < CTP_PROBES && !done; p++) {
@@ -1160,59 +1178,73 @@ __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
             if (cur == k) {
                 // <= 64512 packets of <= 65535 bytes: {packets << 32 | bytes}
                 atomicAdd(&vals[h], (1ull << 32) | len);
+                if (fl && (fls[h] & fl) != fl)
+                    atomicOr(&fls[h], fl);
                 done = true;
             }
             h = (h + 1) & (CT_LDS_SLOTS - 1);
         }
         const uint32_t r = wave_append(nrec, !done);   // a record of its own
         if (!done)
-            put(r, acc_rec(k, 1, len));
+            put(r, acc_rec1(k, true, fl, len));
     };
     // VEC: four consecutive headers per thread and step (16-byte loads),
     // the loads of the next two steps in flight during this step's LDS work
     // (one 1024-thread workgroup per CU: with one step of look-ahead the
     // pass waits on HBM latency every step)
     constexpr uint32_t W = VEC ? 4 : 1, STEP = W * BLOCK;
-    auto load = [&](uint64_t e, uint4 &kk, uint4 &mm) {
+    // (tf: four headers' TCP flags in one word; none without the array)
+    auto load = [&](uint64_t e, uint4 &kk, uint4 &mm, uint32_t &ff) {
         if (VEC && e + 4 <= end) {
             kk = ld_nt4(idx + e);
             mm = ld_nt4(meta + e);
+            ff = tf ? ld_nt(reinterpret_cast<const uint32_t *>(tf + e)) : 0u;
         } else {
             kk = make_uint4(NONE, NONE, NONE, NONE);
             mm = make_uint4(0, 0, 0, 0);
-            if (e < end) { kk.x = ld_nt(idx + e); mm.x = ld_nt(meta + e); }
-            if (VEC && e + 1 < end) { kk.y = ld_nt(idx + e + 1); mm.y = ld_nt(meta + e + 1); }
-            if (VEC && e + 2 < end) { kk.z = ld_nt(idx + e + 2); mm.z = ld_nt(meta + e + 2); }
+            ff = 0;
+            if (e < end) { kk.x = ld_nt(idx + e); mm.x = ld_nt(meta + e); ff = tf ? tf[e] : 0u; }
+            if (VEC && e + 1 < end) {
+                kk.y = ld_nt(idx + e + 1); mm.y = ld_nt(meta + e + 1);
+                ff |= tf ? (uint32_t)tf[e + 1] << 8 : 0u;
+            }
+            if (VEC && e + 2 < end) {
+                kk.z = ld_nt(idx + e + 2); mm.z = ld_nt(meta + e + 2);
+                ff |= tf ? (uint32_t)tf[e + 2] << 16 : 0u;
+            }
         }
     };
     const uint64_t e0 = start + (uint64_t)threadIdx.x * W;
     uint4 k0, m0, k1, m1;
-    load(e0, k0, m0);
-    load(e0 + STEP, k1, m1);
+    uint32_t f0, f1;
+    load(e0, k0, m0, f0);
+    load(e0 + STEP, k1, m1, f1);
     for (uint64_t i0 = start; i0 < end; i0 += STEP) {   // (uniform trip count)
         uint4 k2, m2;
-        load(e0 + (i0 - start) + 2 * STEP, k2, m2);
-        one(k0.x, m0.x >> 16);
+        uint32_t f2;
+        load(e0 + (i0 - start) + 2 * STEP, k2, m2, f2);
+        // (no summaries kept: no flags, no records for them)
+        one(k0.x, m0.x >> 16, sums ? acc_flags(m0.x, f0) : 0u);
         if (VEC) {
-            one(k0.y, m0.y >> 16);
-            one(k0.z, m0.z >> 16);
-            one(k0.w, m0.w >> 16);
+            one(k0.y, m0.y >> 16, sums ? acc_flags(m0.y, f0 >> 8) : 0u);
+            one(k0.z, m0.z >> 16, sums ? acc_flags(m0.z, f0 >> 16) : 0u);
+            one(k0.w, m0.w >> 16, sums ? acc_flags(m0.w, f0 >> 24) : 0u);
         }
-        k0 = k1; m0 = m1;
-        k1 = k2; m1 = m2;
+        k0 = k1; m0 = m1; f0 = f1;
+        k1 = k2; m1 = m2; f1 = f2;
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < CT_LDS_SLOTS; j += BLOCK) {   // (uniform)
         const uint32_t k = keys[j];
         const unsigned long long v = vals[j];
-        const uint32_t by = (uint32_t)v;
+        const uint32_t by = (uint32_t)v, fl = fls[j];
         const uint32_t r = wave_append(nrec, k != NONE);
         if (k != NONE)
             put(r, acc_rec(k, (uint32_t)(v >> 32), by & 0x1FFFFFu));
-        const bool hi = k != NONE && by >= (1u << 21);
+        const bool hi = k != NONE && (by >= (1u << 21) || fl);
         const uint32_t r2 = wave_append(nrec, hi);
         if (hi)
-            put(r2, (uint64_t)k << 38 | 1ull << 37 | (by >> 21));
+            put(r2, acc_rec1(k, false, fl, by >> 21));
     }
     __syncthreads();
     const uint32_t nch = nv * ACC_SLICE_CHUNKS;
@@ -1396,13 +1428,15 @@ __global__ __launch_bounds__(BLOCK) void k_acc_part2(const uint64_t *inA, const 
 // LDS, then added to its counters (acct[2k] packets, acct[2k + 1] bytes)
 __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, const uint32_t *plan,
                                                       const uint32_t *fo, uint32_t nco,
-                                                      uint64_t *acct)
+                                                      uint64_t *acct, uint32_t *sum)
 {
     uint32_t *pk = reinterpret_cast<uint32_t *>(cfc_smem);
     unsigned long long *by = reinterpret_cast<unsigned long long *>(pk + CTP_BUCKET);
+    uint32_t *fl = reinterpret_cast<uint32_t *>(by + CTP_BUCKET);
     for (uint32_t j = threadIdx.x; j < CTP_BUCKET; j += BLOCK) {
         pk[j] = 0;
         by[j] = 0;
+        fl[j] = 0;
     }
     __syncthreads();
     const uint32_t b = blockIdx.x, c = b >> ACC_FINE_BITS, f = b & (ACC_FINE - 1);
@@ -1419,7 +1453,15 @@ __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, cons
             nv = r + 128 < r1 ? ld_nt(recs + r + 128) : 0ull;
             const uint32_t j = (uint32_t)(v >> 38) & (CTP_BUCKET - 1);
             if ((v >> 37) & 1) {
-                atomicAdd(&by[j], (v & ((1ull << 37) - 1)) << 21);
+                const uint32_t low = (uint32_t)v & 0xFFFFu, f = (uint32_t)(v >> 16) & 0x1FFu;
+                if ((v >> 25) & 1) {   // a single packet
+                    atomicAdd(&pk[j], 1u);
+                    atomicAdd(&by[j], (unsigned long long)low);
+                } else {
+                    atomicAdd(&by[j], (unsigned long long)low << 21);
+                }
+                if (f && (fl[j] & f) != f)
+                    atomicOr(&fl[j], f);
             } else {
                 atomicAdd(&pk[j], (uint32_t)(v >> 21) & 0xFFFFu);
                 atomicAdd(&by[j], v & 0x1FFFFFull);
@@ -1449,6 +1491,21 @@ __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, cons
         cv[q].x += p[q];
         cv[q].y += by[j];
         *reinterpret_cast<ulonglong2 *>(acct + 2 * k) = cv[q];
+    }
+    if (!sum)
+        return;
+    // the plain-hit summary per slot (keys 2s: tx, 2s + 1: rx), as
+    // ctops.hpp sum_bits lays it out: rx flags, tx flags << 8, rx hit << 16,
+    // tx hit << 17, a TCP hit without the close bit << 18
+    for (uint32_t q = threadIdx.x; q < CTP_BUCKET / 2; q += BLOCK) {
+        const uint32_t jt = 2 * q, jr = 2 * q + 1;
+        uint32_t w = 0;
+        if (pk[jt])
+            w |= (fl[jt] & 0xFFu) << 8 | 1u << 17 | ((fl[jt] >> 8) & 1u) << 18;
+        if (pk[jr])
+            w |= (fl[jr] & 0xFFu) | 1u << 16 | ((fl[jr] >> 8) & 1u) << 18;
+        if (w)
+            sum[((uint64_t)b * CTP_BUCKET >> 1) + q] = w;
     }
 }
 
@@ -1818,19 +1875,22 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 #undef CFC_LAUNCH
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
-    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct);
+    const bool sums = launch_counters(T, in.meta, in.tcp_flags, in.n, mode, ws, g_ctr, s, ct);
+    if (E.sums)
+        *E.sums = sums;
     if (tm)
         (void)hipEventRecord(tm->ev[2], s);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : -5;
 }
 
-void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
+bool launch_counters(const DevTables &T, const uint32_t *meta, const uint8_t *tf, uint64_t n,
                      int mode, uint32_t *ws, uint64_t *g_ctr, hipStream_t s,
                      bool ct)
 {
+    bool sums = false;
     if (!n || mode == CFC_MODE_XDP)
-        return;
+        return sums;
     const WsLayout w = ws_layout(n, T, mode, ct);
     const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
     if (ct && T.ct_acct && w.ctp_nv) {
@@ -1850,16 +1910,18 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
         const uint32_t nsb = (uint32_t)((nc + 4 * BLOCK - 1) / (4 * BLOCK));
         // 16-byte loads when the header meta allows (the key arrays are
         // 16-byte aligned workspace)
-        const bool vec = ((uintptr_t)meta & 15) == 0;
+        const bool vec = ((uintptr_t)meta & 15) == 0 && (!T.ct_sum || ((uintptr_t)tf & 3) == 0);
         const void *agg = vec ? (const void *)k_acc_agg<true> : (const void *)k_acc_agg<false>;
         set_lds_limit(agg, (int)ACC_AGG_LDS);
         if (vec)
             hipLaunchKernelGGL(k_acc_agg<true>, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
-                               dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta, n,
+                               dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta,
+                               T.ct_sum ? tf : nullptr, T.ct_sum != nullptr, n,
                                w.ctp_nco, rec, rcnt, cnt, per);
         else
             hipLaunchKernelGGL(k_acc_agg<false>, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
-                               dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta, n,
+                               dim3(BLOCK), ACC_AGG_LDS, s, C.ct, C.ct2, meta,
+                               T.ct_sum ? tf : nullptr, T.ct_sum != nullptr, n,
                                w.ctp_nco, rec, rcnt, cnt, per);
         hipLaunchKernelGGL(k_scan_local, dim3(nsb), dim3(BLOCK), 0, s, cnt, off, nc, bsum);
         hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(BLOCK), 0, s, bsum, nsb, off + nc);
@@ -1874,7 +1936,8 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
                            plan, w.ctp_nco, rec, fo);
         set_lds_limit((const void *)k_acc_reduce, (int)ACC_RED_LDS);
         hipLaunchKernelGGL(k_acc_reduce, dim3(w.ctp_nbuck), dim3(BLOCK), ACC_RED_LDS, s, rec,
-                           plan, fo, w.ctp_nco, T.ct_acct);
+                           plan, fo, w.ctp_nco, T.ct_acct, T.ct_sum);
+        sums = T.ct_sum != nullptr;
     } else if (ct && T.ct_acct) {
         set_lds_limit((const void *)k_ct_count, (int)CT_LDS_BYTES);
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
@@ -1905,7 +1968,7 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
         jobs.push_back(j);
     }
     if (jobs.empty())
-        return;
+        return sums;
     uint64_t *partial = reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(ws) + w.partial);
     const uint64_t per_block = hist_per_block(n, w.nblk);
     set_lds_limit((const void *)k_hist, (int)(8 * HIST_RANGE));
@@ -1924,6 +1987,7 @@ void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
                            dim3((cmax + 255) / 256, nj, (w.nblk + REDUCE_ROWS - 1) / REDUCE_ROWS),
                            dim3(256), 0, s, J, partial, w.nblk, g_ctr, C.g_id, id_dir);
     }
+    return sums;
 }
 
 }  // namespace cfc

@@ -28,6 +28,7 @@ struct EgressArgs {
     uint32_t nat_v4;
     uint32_t *nat_idx, *nat_cnt;
     const uint32_t *nat_id;
+    bool *sums;   // (host) set when the launch wrote DevTables.ct_sum
 };
 
 constexpr int BLOCK = 1024;
@@ -199,6 +200,11 @@ struct CtaArgs {
     // per slot {mark, summary} of this apply (one 8-byte word: route reads
     // both with one random load)
     uint2 *ms;
+    // the classify launch's plain-hit summaries of this family's slots
+    // (DevTables.ct_sum + acct_base) when the apply follows that launch:
+    // the scan then leaves the summaries alone, the fold clears an ordered
+    // slot's, and the finish takes (and clears) them; null: the scan's
+    uint32_t *sum;
     uint32_t *hs;                // [2n] hit slot per header and stage ([4n] with lbr)
     // an egress batch with a load balancer: per header LbRec4 / LbRec6 (its
     // CT_SERVICE ops are virtual headers n..2n-1), null otherwise
@@ -452,7 +458,9 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
 
 // The counter kernels over the per-header keys the classify kernel left in
 // the workspace (both families): policy entries, identities, CT accounting.
-void launch_counters(const DevTables &T, const uint32_t *meta, uint64_t n,
+// returns true when the accounting reduce wrote T.ct_sum (the launch's
+// plain-hit summaries; tf: the batch's TCP flags, or null)
+bool launch_counters(const DevTables &T, const uint32_t *meta, const uint8_t *tf, uint64_t n,
                      int mode, uint32_t *workspace, uint64_t *g_ctr,
                      hipStream_t stream, bool ct);
 

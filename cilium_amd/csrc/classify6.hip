@@ -750,7 +750,9 @@ int launch_classify_v6(const DevTables &T, const cfc_hdr_v6 &in,
 #undef CFC_LAUNCH6
     if (tm)
         (void)hipEventRecord(tm->ev[1], s);
-    launch_counters(T, in.meta, in.n, mode, ws, g_ctr, s, ct);
+    const bool sums = launch_counters(T, in.meta, in.tcp_flags, in.n, mode, ws, g_ctr, s, ct);
+    if (E.sums)
+        *E.sums = sums;
     if (tm)
         (void)hipEventRecord(tm->ev[2], s);
     return hipGetLastError() == hipSuccess ? 0 : -5;

@@ -87,8 +87,10 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 const uint32_t cs = (r[u].cb >> (4 * st)) & 0xF;
                 const bool mine = A.mode == CFC_MODE_EGRESS && st == 0;   // (owner: the sender)
                 const uint32_t key = st ? r[u].k2 : r[u].k1;
+                // (a CT_NEW stage without a create — dropped — has no op)
+                const bool cr = (cs & CFC_CT_RES_MASK) == 0;
                 need[u] |= (cs & CFC_CT_DONE) && !mine &&
-                           ((cs & CFC_CT_RES_MASK) == 0 || key >= CK_MISS);
+                           (cr ? (cs & CFC_CT_CREATE) != 0 : key >= CK_MISS);
             }
         }
         if constexpr (V6) {
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         for (int u = 0; u < SCAN_U; u++)
 #pragma unroll
             for (int st = 0; st < NST; st++)
-                cur[u][st] = (sb[u][st] && slot[u][st] != HS_NONE && !A.nt)
+                cur[u][st] = (sb[u][st] && slot[u][st] != HS_NONE && !A.nt && !A.sum)
                                  ? A.ms[slot[u][st]].x : 0u;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
@@ -187,7 +189,8 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                     // monitor lengths wanted: every hit replayed in order
                     order_mark(A, sl, MARK_ORDERED);
                 } else if (sb[u][st]) {   // a plain hit: into the slot's summary
-                    if ((cur[u][st] | sb[u][st]) != cur[u][st])
+                    // (unless the launch's accounting summarised it: A.sum)
+                    if (!A.sum && (cur[u][st] | sb[u][st]) != cur[u][st])
                         atomicOr(&A.ms[sl].x, sb[u][st]);
                 } else if (kind[u][st] == OP_DELETE) {
                     // the entry goes: only its first delete matters
@@ -1122,6 +1125,8 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     }
     A.info[slot] = inf;
     A.ms[slot] = make_uint2(0, 0);
+    if (A.sum)   // (replayed here: the finish leaves the slot alone)
+        A.sum[slot] = 0;
 }
 
 // ---- finish: the summaries of unordered slots.  Their hits are plain
@@ -1154,8 +1159,10 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             sl[u] = k < slots ? (uint32_t)k : NONE;
         }
 #pragma unroll
-        for (int u = 0; u < FU; u++)   // (no branches: the loads issue together)
-            m[u] = A.ms[sl[u] != NONE ? sl[u] : (uint32_t)(slots - 1)].x >> SUM_SH;
+        for (int u = 0; u < FU; u++) {   // (no branches: the loads issue together)
+            const uint32_t c = sl[u] != NONE ? sl[u] : (uint32_t)(slots - 1);
+            m[u] = A.sum ? A.sum[c] : A.ms[c].x >> SUM_SH;
+        }
 #pragma unroll
         for (int u = 0; u < FU; u++)
             if (sl[u] == NONE)
@@ -1174,7 +1181,10 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
             if (!m[u])
                 continue;
             const uint64_t s = sl[u];
-            A.ms[s].x = 0;
+            if (A.sum)
+                A.sum[s] = 0;
+            else
+                A.ms[s].x = 0;
             St &x = e[u];
             x.bits &= ~(RX_CLOSING | TX_CLOSING);
             const bool is_tcp = (w[u] & 0xFF) == 6;

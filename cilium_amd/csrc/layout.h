@@ -384,6 +384,12 @@ struct DevTables {
     const Ct4Slot *ct4;
     const Ct6Slot *ct6;
     uint64_t *ct_acct;             // [slot][dir][packets, bytes], v4 then v6
+    // per slot (as ct_acct) the plain-hit summary of the launch's hits
+    // (ctapply.hip k_cta_finish's bits: flags per direction, hit per
+    // direction, a TCP hit without the close bit), written by the
+    // accounting reduce (classify.hip k_acc_reduce) for the device CT apply
+    // that follows the launch; cleared by that apply.  Null: not kept.
+    uint32_t *ct_sum;
     uint32_t ct4_mask, ct4_probe;
     uint32_t ct6_mask, ct6_probe;
     uint32_t ct6_acct_base;        // first v6 slot in ct_acct
