@@ -3039,6 +3039,11 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             c->sum_pending = false;
         }
     }
+    {   // 16-byte loads of four headers' words in the scan
+        auto al = [](const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+        A.vec = al(A.sa, 16) && al(A.da, 16) && al(A.pt, 16) && al(A.mt, 16) && al(A.ver, 16) &&
+                al(A.ident, 16) && al(A.ck1, 16) && al(A.ck2, 16) && al(A.ctb, 4) && al(A.tf, 4);
+    }
     // a load balancer's service step first: the ordering pass and the scan
     // decode its per-header records
     if (hipMemsetAsync(A.cnt, 0, 4 * CTA_NCNT, s) != hipSuccess ||
@@ -3757,12 +3762,11 @@ int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter 
                 hipSuccess ||
             hipMemsetAsync(cnt, 0, 4 * CTG_NCNT, s) != hipSuccess || ct_gc4(A, s))
             return -EIO;
-        // the pending TCP-map ICMP entries of the applies, compacted
+        // the pending TCP-map ICMP entries of the applies, compacted (all
+        // logn places copied back: the kept ones lead, the rest is past the
+        // new count — no wait for that count first)
         if (logn && (ct_gc_log(A, (const CtLog *)c->cta_log.p, logn, (CtLog *)c->gc_tmp.p, s) ||
-                     hipMemcpyAsync(hc, cnt, 4 * CTG_NCNT, hipMemcpyDeviceToHost, s) !=
-                         hipSuccess ||
-                     hipStreamSynchronize(s) != hipSuccess ||
-                     hipMemcpyAsync(c->cta_log.p, c->gc_tmp.p, sizeof(CtLog) * hc[CTG_LOGKEPT],
+                     hipMemcpyAsync(c->cta_log.p, c->gc_tmp.p, sizeof(CtLog) * logn,
                                     hipMemcpyDeviceToDevice, s) != hipSuccess))
             return -EIO;
         if (hipMemcpyAsync(hc, cnt, 4 * CTG_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||

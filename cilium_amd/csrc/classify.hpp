@@ -205,6 +205,7 @@ struct CtaArgs {
     // the scan then leaves the summaries alone, the fold clears an ordered
     // slot's, and the finish takes (and clears) them; null: the scan's
     uint32_t *sum;
+    bool vec;                    // the batch's arrays 16-byte aligned (the scan's loads)
     uint32_t *hs;                // [2n] hit slot per header and stage ([4n] with lbr)
     // an egress batch with a load balancer: per header LbRec4 / LbRec6 (its
     // CT_SERVICE ops are virtual headers n..2n-1), null otherwise
@@ -305,6 +306,7 @@ struct OrdArgs {
     uint32_t ndel;                // deleting stages (0: no delete pass)
     uint32_t *cbloom;             // the creates' keys (Bloom words, or null)
     uint32_t cb_mask;
+    bool vec;                     // ctb, ver (and ck1 / ck2) 16-byte aligned
     bool tagged;                  // the keys from ck1 / ck2's miss tags (CK_MISS), else
                                   // pre-keys from the headers
     uint32_t *cnt;                // ORD_* counters
@@ -312,14 +314,14 @@ struct OrdArgs {
     uint32_t part_cap;
     uint32_t *rel_src;
     void *rk;                     // per record its key (16 B; IPv6 48 B)
-    uint64_t *rh, *rh2, *rh3;     // fingerprints
-    uint32_t *rord, *rord2, *ridx, *ridx2;
+    uint64_t *rh, *rh2;           // fingerprint << 32 | header order (sort keys)
+    uint32_t *ridx, *ridx2;
     uint8_t *pinfo, *nres;
     void *tmp;
     size_t tmp_bytes;
 };
 struct OrdBufs {
-    DevBuf part, rel_src, rk, rh, rh2, rh3, rord, rord2, ridx, ridx2, pinfo, nres, tmp, fpset;
+    DevBuf part, rel_src, rk, rh, rh2, ridx, ridx2, pinfo, nres, tmp, fpset;
     uint32_t creates_hint = 0;   // the last batch's creates: the filter's size
 };
 // rewrites the CT bytes (and hit keys) of the stages whose packet-order

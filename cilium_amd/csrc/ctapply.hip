@@ -62,16 +62,69 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
     const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
     uint32_t nhit = 0, nfh = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
+        // SCAN_U consecutive headers per thread: with the batch's arrays
+        // 16-byte aligned (A.vec) their words in one 16-byte load per array
+        // (four bytes for the byte arrays) — a scalar load moves 4 bytes per
+        // lane, and the pass was bound by the load instructions
+        const uint64_t i0 = base + (uint64_t)SCAN_U * threadIdx.x;
         ScanIn<V6> r[SCAN_U];
+        if (SCAN_U == 4 && A.vec && i0 + SCAN_U <= A.n) {
+            const uint4 pt4 = *reinterpret_cast<const uint4 *>(A.pt + i0);
+            const uint4 mt4 = *reinterpret_cast<const uint4 *>(A.mt + i0);
+            const uint4 ve4 = *reinterpret_cast<const uint4 *>(A.ver + i0);
+            const uint4 id4 = *reinterpret_cast<const uint4 *>(A.ident + i0);
+            const uint4 k14 = A.ck1 ? *reinterpret_cast<const uint4 *>(A.ck1 + i0)
+                                    : make_uint4(NONE, NONE, NONE, NONE);
+            const uint4 k24 = A.ck2 ? *reinterpret_cast<const uint4 *>(A.ck2 + i0)
+                                    : make_uint4(NONE, NONE, NONE, NONE);
+            const uint32_t cb4 = *reinterpret_cast<const uint32_t *>(A.ctb + i0);
+            const uint32_t tf4 = A.tf ? *reinterpret_cast<const uint32_t *>(A.tf + i0) : 0u;
+            const uint32_t ptv[4] = {pt4.x, pt4.y, pt4.z, pt4.w};
+            const uint32_t mtv[4] = {mt4.x, mt4.y, mt4.z, mt4.w};
+            const uint32_t vev[4] = {ve4.x, ve4.y, ve4.z, ve4.w};
+            const uint32_t idv[4] = {id4.x, id4.y, id4.z, id4.w};
+            const uint32_t k1v[4] = {k14.x, k14.y, k14.z, k14.w};
+            const uint32_t k2v[4] = {k24.x, k24.y, k24.z, k24.w};
+            if constexpr (V6) {
 #pragma unroll
-        for (int u = 0; u < SCAN_U; u++) {   // inputs (no branches)
-            const uint64_t i = base + u * 256 + threadIdx.x;
-            const uint64_t j = i < A.n ? i : A.n - 1;
-            load_in<V6, false>(A, j, r[u]);
-            r[u].k1 = A.ck1 ? A.ck1[j] : NONE;
-            r[u].k2 = A.ck2 ? A.ck2[j] : NONE;
-            if (i >= A.n)
-                r[u].cb = 0;
+                for (int u = 0; u < SCAN_U; u++) {
+                    r[u].sa = ld_addr<V6>(A.sa, i0 + u);
+                    r[u].da = ld_addr<V6>(A.da, i0 + u);
+                }
+            } else {
+                const uint4 sa4 = *reinterpret_cast<const uint4 *>(A.sa + i0);
+                const uint4 da4 = *reinterpret_cast<const uint4 *>(A.da + i0);
+                const uint32_t sav[4] = {sa4.x, sa4.y, sa4.z, sa4.w};
+                const uint32_t dav[4] = {da4.x, da4.y, da4.z, da4.w};
+#pragma unroll
+                for (int u = 0; u < SCAN_U; u++) {
+                    r[u].sa = sav[u];
+                    r[u].da = dav[u];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < SCAN_U; u++) {
+                r[u].svcop = false;
+                r[u].cb = (cb4 >> (8 * u)) & 0xFFu;
+                r[u].pt = ptv[u];
+                r[u].mt = mtv[u];
+                r[u].ver = vev[u];
+                r[u].ident = idv[u];
+                r[u].tf = (tf4 >> (8 * u)) & 0xFFu;
+                r[u].k1 = k1v[u];
+                r[u].k2 = k2v[u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < SCAN_U; u++) {   // inputs (no branches)
+                const uint64_t i = i0 + u;
+                const uint64_t j = i < A.n ? i : A.n - 1;
+                load_in<V6, false>(A, j, r[u]);
+                r[u].k1 = A.ck1 ? A.ck1[j] : NONE;
+                r[u].k2 = A.ck2 ? A.ck2[j] : NONE;
+                if (i >= A.n)
+                    r[u].cb = 0;
+            }
         }
         // the destination endpoint's CT owner, for the stages whose key the
         // scan builds (a create, a hit the classify launch did not leave):
@@ -178,7 +231,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                                  ? A.ms[slot[u][st]].x : 0u;
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
-            const uint64_t i = base + u * 256 + threadIdx.x;
+            const uint64_t i = i0 + u;
 #pragma unroll
             for (int st = 0; st < NST; st++) {
                 const uint32_t sl = slot[u][st];
@@ -220,7 +273,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         uint32_t rq = block_stage_n(&s_nreq, ncr);
 #pragma unroll
         for (int u = 0; u < SCAN_U; u++) {
-            const uint64_t i = base + u * 256 + threadIdx.x;
+            const uint64_t i = i0 + u;
 #pragma unroll
             for (int st = 0; st < NST; st++) {
                 if (fh[u][st]) {
@@ -789,25 +842,37 @@ __global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *
 }
 
 // ---- route: every op on an ordered slot -> the ordered list (the plain
-// hits of the other slots are in their summaries: k_cta_scan).  Four header
-// stages per thread and step; per hit one test of the ordered-slot bitmap,
-// the slot's words only for the ordered ones.  (Family-free.)
+// hits of the other slots are in their summaries: k_cta_scan / the launch's
+// accounting).  RU consecutive header stages per thread and step: their
+// hit slots in four 16-byte loads, then the ordered-slot bitmap words, the
+// slot's words only for the ordered ones.  (Family-free.)
+constexpr int RU = 16;
 __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
-    constexpr int RU = 4;
     // item k is header stage j = k (egress: two CT stages per header) or
     // j = 2k (one stage: the odd stages never hold a hit); with a load
     // balancer (egress) j in [2n, 4n) are the CT_SERVICE ops (virtual
     // headers n..2n-1)
     const bool two = A.mode == CFC_MODE_EGRESS;
     const uint64_t n2 = 2 * A.n, nk = A.lbr ? 2 * n2 : two ? n2 : A.n;
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * RU;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < nk; base += stride) {
+    const uint64_t span = 256ull * RU, stride = (uint64_t)gridDim.x * span;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < nk; base += stride) {
+        const uint64_t k0 = base + (uint64_t)RU * threadIdx.x;
         uint32_t slot[RU], bw[RU];
+        if (k0 + RU <= nk) {   // (A.hs: 16-byte aligned)
+            const uint4 *hp = reinterpret_cast<const uint4 *>(A.hs + k0);
 #pragma unroll
-        for (int u = 0; u < RU; u++) {
-            const uint64_t k = base + u * 256 + threadIdx.x;
-            slot[u] = k < nk ? A.hs[k] : HS_NONE;   // (one stage: one word per header)
+            for (int q = 0; q < RU / 4; q++) {
+                const uint4 v = hp[q];
+                slot[4 * q] = v.x;
+                slot[4 * q + 1] = v.y;
+                slot[4 * q + 2] = v.z;
+                slot[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < RU; u++)
+                slot[u] = k0 + u < nk ? A.hs[k0 + u] : HS_NONE;
         }
 #pragma unroll
         for (int u = 0; u < RU; u++)
@@ -818,9 +883,8 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
             // CT_SERVICE lookup's on the tx side), which no classify launch
             // counts — here, after the apply has committed to the device
             // (a scan may run twice when the table grows)
-#pragma unroll
             for (int u = 0; u < RU; u++) {
-                const uint64_t k = base + u * 256 + threadIdx.x;
+                const uint64_t k = k0 + u;
                 if (k < n2 || slot[u] == HS_NONE)
                     continue;
                 unsigned long long *ac = reinterpret_cast<unsigned long long *>(A.T.ct_acct) +
@@ -829,30 +893,28 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
                 atomicAdd(ac + 1, (unsigned long long)(A.mt[(k >> 1) - A.n] >> 16));
             }
         }
-        bool ordered[RU];
-        uint32_t nord = 0;
+        uint32_t om = 0;   // bit u: item k0 + u goes to the ordered list
 #pragma unroll
-        for (int u = 0; u < RU; u++) {
-            const uint64_t k = base + u * 256 + threadIdx.x;
-            const uint64_t j = two ? k : 2 * k;
-            ordered[u] = false;
-            if (slot[u] == HS_NONE || !((bw[u] >> (slot[u] & 31)) & 1))
-                continue;
+        for (int u = 0; u < RU; u++)
+            if (slot[u] != HS_NONE && ((bw[u] >> (slot[u] & 31)) & 1))
+                om |= 1u << u;
+        for (uint32_t m = om; m; m &= m - 1) {   // (rare: the ordered slots' ops)
+            const int u = __ffs(m) - 1;
+            const uint64_t j = two ? k0 + u : 2 * (k0 + u);
             const uint2 v = A.ms[slot[u]];
+            bool o;
             if ((v.x & (MARK_DEL | MARK_PUTC)) == MARK_DEL && !A.nt)
                 // a deleted entry: its first delete stands for all its ops
-                ordered[u] = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - v.y;
+                o = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - v.y;
             else
-                ordered[u] = (v.x & MARK_ORDERED) != 0;
-            nord += ordered[u];
+                o = (v.x & MARK_ORDERED) != 0;
+            if (!o)
+                om &= ~(1u << u);
         }
-        uint32_t c = A.cx_base + block_count_n(&A.cnt[CTA_NCX], nord);
-#pragma unroll
-        for (int u = 0; u < RU; u++) {
-            const uint64_t k = base + u * 256 + threadIdx.x;
-            const uint64_t j = two ? k : 2 * k;
-            if (!ordered[u])
-                continue;
+        uint32_t c = A.cx_base + block_count_n(&A.cnt[CTA_NCX], (uint32_t)__popc(om));
+        for (uint32_t m = om; m; m &= m - 1) {
+            const int u = __ffs(m) - 1;
+            const uint64_t j = two ? k0 + u : 2 * (k0 + u);
             if (c < A.cx_cap)
                 A.cx[c] = pack(A, slot[u], ord_of(j >> 1, (int)(j & 1), SEC_OP));
             c++;
@@ -1018,11 +1080,11 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     // replayed; the owner word does not matter here (the slot is the key),
     // so no endpoint lookup
     ScanIn<V6> cur;
-    load_in<V6, LB>(A, ord_hdr((uint32_t)(cx[r0] & omask)), cur);
+    load_in<V6, LB, false>(A, ord_hdr((uint32_t)(cx[r0] & omask)), cur);
     for (uint32_t r = r0; r < ncx && (uint32_t)(cx[r] >> A.ob) == slot; r++) {
         const uint32_t ord = (uint32_t)(cx[r] & omask);
         ScanIn<V6> nxt;
-        load_in<V6, LB>(A, ord_hdr((uint32_t)(cx[r + 1 < ncx ? r + 1 : r] & omask)), nxt);
+        load_in<V6, LB, false>(A, ord_hdr((uint32_t)(cx[r + 1 < ncx ? r + 1 : r] & omask)), nxt);
         const Op<V6> o = decode_from<V6, LB>(A, cur, ord_st(ord), 0u);
         cur = nxt;
         const uint32_t d = o.dir == CT_INGRESS ? 2 : 0;
@@ -1146,48 +1208,54 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 {
-    // four slots per thread and step, each phase's loads together
-    constexpr int FU = 4;
+    // FU consecutive slots per thread and step: their summary words in
+    // 16-byte loads, then the touched slots' state (a few per step)
+    constexpr int FU = 16;
     const uint64_t slots = (uint64_t)A.mask + 1;
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * FU;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 * FU; base < slots; base += stride) {
-        uint32_t m[FU], w[FU], sl[FU];
-        St e[FU];
+    const uint64_t span = 256ull * FU, stride = (uint64_t)gridDim.x * span;
+    for (uint64_t base = (uint64_t)blockIdx.x * span; base < slots; base += stride) {
+        const uint64_t s0 = base + (uint64_t)FU * threadIdx.x;
+        uint32_t m[FU];
+        if (s0 + FU <= slots) {   // (slots: a power of two >= FU; arrays aligned)
+            if (A.sum) {
+                const uint4 *p = reinterpret_cast<const uint4 *>(A.sum + s0);
 #pragma unroll
-        for (int u = 0; u < FU; u++) {
-            const uint64_t k = base + u * 256 + threadIdx.x;
-            sl[u] = k < slots ? (uint32_t)k : NONE;
-        }
+                for (int q = 0; q < FU / 4; q++) {
+                    const uint4 v = p[q];
+                    m[4 * q] = v.x;
+                    m[4 * q + 1] = v.y;
+                    m[4 * q + 2] = v.z;
+                    m[4 * q + 3] = v.w;
+                }
+            } else {
+                const uint4 *p = reinterpret_cast<const uint4 *>(A.ms + s0);
 #pragma unroll
-        for (int u = 0; u < FU; u++) {   // (no branches: the loads issue together)
-            const uint32_t c = sl[u] != NONE ? sl[u] : (uint32_t)(slots - 1);
-            m[u] = A.sum ? A.sum[c] : A.ms[c].x >> SUM_SH;
+                for (int q = 0; q < FU / 2; q++) {
+                    const uint4 v = p[q];   // {ms[2q].x, .y, ms[2q + 1].x, .y}
+                    m[2 * q] = v.x >> SUM_SH;
+                    m[2 * q + 1] = v.z >> SUM_SH;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < FU; u++)
+                m[u] = s0 + u < slots ? (A.sum ? A.sum[s0 + u] : A.ms[s0 + u].x >> SUM_SH) : 0u;
         }
+        uint32_t any = 0;
 #pragma unroll
         for (int u = 0; u < FU; u++)
-            if (sl[u] == NONE)
-                m[u] = 0;
-#pragma unroll
-        for (int u = 0; u < FU; u++) {
-            const uint64_t s = sl[u];
-            w[u] = 0;
-            if (m[u]) {
-                e[u] = load_state(A.tm, (uint32_t)s);
-                w[u] = *slot_w<V6>(A, (uint32_t)s);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < FU; u++) {
-            if (!m[u])
-                continue;
-            const uint64_t s = sl[u];
+            any |= (m[u] != 0u) << u;
+        for (uint32_t mm = any; mm; mm &= mm - 1) {
+            const int u = __ffs(mm) - 1;
+            const uint32_t sl = (uint32_t)(s0 + u);
+            St x = load_state(A.tm, sl);
+            const uint32_t w = *slot_w<V6>(A, sl);
             if (A.sum)
-                A.sum[s] = 0;
+                A.sum[sl] = 0;
             else
-                A.ms[s].x = 0;
-            St &x = e[u];
+                A.ms[sl].x = 0;
             x.bits &= ~(RX_CLOSING | TX_CLOSING);
-            const bool is_tcp = (w[u] & 0xFF) == 6;
+            const bool is_tcp = (w & 0xFF) == 6;
             if (is_tcp && (m[u] & (1u << 18)))
                 x.bits |= SEEN_NON_SYN;
             x.lifetime = A.now + (is_tcp ? ((x.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP
@@ -1205,8 +1273,8 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
                     x.last_tx = A.now;
                 x.seen_tx = seen;
             }
-            store_state(A.tm, (uint32_t)s, x);
-            A.info[s].y |= CTI_UPDATED;
+            store_state(A.tm, sl, x);
+            A.info[sl].y |= CTI_UPDATED;
         }
     }
 }
@@ -1468,9 +1536,9 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
                        : -1;
         }
 #pragma unroll
-        for (int u = 0; u < GC_U; u++) {
+        for (int u = 0; u < GC_U; u++) {   // (every slot's: no branch between the loads)
             const uint64_t s = base + u * 256 + threadIdx.x;
-            life[u] = j[u] >= 0 ? A.tm[s].lifetime : 0u;
+            life[u] = A.tm[s < A.slots ? s : A.slots - 1].lifetime;
         }
         bool del[GC_U], logit[GC_U];
 #pragma unroll
@@ -1723,8 +1791,11 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     // ordered hits follow
     CtaArgs R = A;
     R.cx_base = nreqA + nreqB;
-    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for((A.lbr ? 4 : 2) * A.n, 8192)), dim3(256), 0,
-                       s, R);
+    {
+        const uint64_t nk = A.lbr ? 4 * A.n : A.mode == CFC_MODE_EGRESS ? 2 * A.n : A.n;
+        hipLaunchKernelGGL(k_cta_route, dim3(blocks_for((nk + RU - 1) / RU, 2048)), dim3(256), 0,
+                           s, R);
+    }
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -1756,7 +1827,7 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     // (a sweep of the whole table: a list of the touched slots, A/B'd,
     // took 0.43 ms against the sweep's 0.30 — its random loads cost more
     // than the sequential ones they save)
-    hipLaunchKernelGGL(k_cta_finish<V6>, dim3(blocks_for((uint64_t)A.mask + 1, 8192)),
+    hipLaunchKernelGGL(k_cta_finish<V6>, dim3(blocks_for(((uint64_t)A.mask + 1) / 16 + 1, 2048)),
                        dim3(256), 0, s, A);
     if (A.nt && A.mon && A.n)
         hipLaunchKernelGGL(k_cta_mon<V6>, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A);

@@ -420,15 +420,21 @@ __device__ __forceinline__ Op<V6> decode_from(const CtaArgs &A, const ScanIn<V6>
     return o;
 }
 
-template <bool V6, bool LB>
+// KEY: the op's key words are needed (not by the fold of an IPv4 batch
+// without a load balancer: its slot is the key, and rev is 0)
+template <bool V6, bool LB, bool KEY = true>
 __device__ __forceinline__ void load_in(const CtaArgs &A, uint64_t i, ScanIn<V6> &r)
 {
     r.svcop = LB && i >= A.n;
     if (r.svcop)
         i -= A.n;
     r.cb = A.ctb[i];
-    r.sa = ld_addr<V6>(A.sa, i);
-    r.da = ld_addr<V6>(A.da, i);
+    if (KEY || V6 || LB) {
+        r.sa = ld_addr<V6>(A.sa, i);
+        r.da = ld_addr<V6>(A.da, i);
+    } else {
+        r.sa = r.da = Addr<V6>{};
+    }
     r.pt = A.pt[i];
     r.mt = A.mt[i];
     r.ver = (uint32_t)A.ver[i];

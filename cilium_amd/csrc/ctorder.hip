@@ -169,9 +169,11 @@ __device__ __forceinline__ uint64_t tag_key(uint32_t t)
 }
 __device__ __forceinline__ bool tag_ok(uint32_t t) { return t >= CK_MISS && t != NONE; }
 constexpr int ORD_IT = 16;   // headers per thread and step (mark, collect)
-// The two passes over the whole batch (mark, collect) take ORD_IT headers
-// per thread and step (256 apart: coalesced): their CT bytes and verdicts
-// loaded together without branches (one wait), a cheap unrolled pass that
+// The two passes over the whole batch (mark, collect) take ORD_IT
+// consecutive headers per thread and step: their CT bytes (one 16-byte
+// load) and verdicts (four) loaded together without branches (one wait;
+// byte loads were the pass's limit: one instruction per 64 bytes), a cheap
+// unrolled pass that
 // sorts the stages into bit masks (bit NST * k + st), then the rare stages
 // that need more (a key, a probe) in a loop that is not unrolled — with the
 // key derivation inlined once the kernel stays small enough for the
@@ -181,18 +183,43 @@ struct OrdStep {
     static constexpr int NST = TWO ? 2 : 1;
     uint32_t cb[ORD_IT];
     int32_t ver[ORD_IT];
-    __device__ __forceinline__ void load(const CtaArgs &A, uint64_t base)
+    // header k of this thread's run at base (base: a multiple of 256 * ORD_IT)
+    __device__ __forceinline__ static uint64_t at(uint64_t base, int k)
     {
+        return base + (uint64_t)ORD_IT * threadIdx.x + (uint64_t)k;
+    }
+    // vec: ctb and ver 16-byte aligned (OrdArgs.vec)
+    __device__ __forceinline__ void load(const CtaArgs &A, uint64_t base, bool vec)
+    {
+        const uint64_t i0 = at(base, 0);
+        if (vec && i0 + ORD_IT <= A.n) {
+            const uint4 c = *reinterpret_cast<const uint4 *>(A.ctb + i0);
+            const uint4 *vp = reinterpret_cast<const uint4 *>(A.ver + i0);
+            const uint4 v0 = vp[0], v1 = vp[1], v2 = vp[2], v3 = vp[3];
+            const uint32_t cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int k = 0; k < ORD_IT; k++)
+                cb[k] = (cw[k / 4] >> (8 * (k % 4))) & 0xFFu;
+            const uint4 vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ver[4 * q] = (int32_t)vv[q].x;
+                ver[4 * q + 1] = (int32_t)vv[q].y;
+                ver[4 * q + 2] = (int32_t)vv[q].z;
+                ver[4 * q + 3] = (int32_t)vv[q].w;
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < ORD_IT; k++) {
-            const uint64_t i = base + 256ull * k + threadIdx.x;
+            const uint64_t i = i0 + k;
             const uint64_t j = i < A.n ? i : A.n - 1;
             cb[k] = A.ctb[j];
             ver[k] = A.ver[j];
         }
 #pragma unroll
         for (int k = 0; k < ORD_IT; k++)
-            if (base + 256ull * k + threadIdx.x >= A.n)
+            if (i0 + k >= A.n)
                 cb[k] = 0;
     }
     // res: the stage's CT result, or -1 (no CT stage)
@@ -205,7 +232,7 @@ struct OrdStep {
     }
     __device__ __forceinline__ static uint64_t hdr(uint64_t base, int b)
     {
-        return base + 256ull * (b / NST) + threadIdx.x;
+        return at(base, b / NST);
     }
 };
 
@@ -221,7 +248,7 @@ __global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
     uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < A.n; base += stride) {
         S x;
-        x.load(A, base);
+        x.load(A, base, O.vec);
         uint32_t crm = 0, delm = 0;
 #pragma unroll
         for (int k = 0; k < ORD_IT; k++)
@@ -270,7 +297,7 @@ __global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
             PreIn<V6> f[PK];
 #pragma unroll
             for (int k = 0; k < PK; k++) {
-                const uint64_t i = base + 256ull * (c + k) + threadIdx.x;
+                const uint64_t i = S::at(base, c + k);
                 f[k] = pre_in<V6>(A, i < A.n ? i : A.n - 1);
             }
 #pragma unroll
@@ -335,7 +362,7 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
     // (every thread runs the same number of steps: block_count_n)
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < A.n; base += stride) {
         S x;
-        x.load(A, base);
+        x.load(A, base, O.vec);
         uint32_t bits = 0, probe = 0, estm = 0;
 #pragma unroll
         for (int k = 0; k < ORD_IT; k++)
@@ -359,11 +386,28 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
         // filter words loaded together — two waits per step
         if (O.tagged) {
             uint32_t tg[ORD_IT * NST], fw[ORD_IT * NST];
+            const uint64_t i0 = S::at(base, 0);
+            if (O.vec && i0 + ORD_IT <= A.n) {
+                // (dense: every tag of the run, 16-byte loads)
 #pragma unroll
-            for (int q = 0; q < ORD_IT * NST; q++) {
-                tg[q] = NONE;
-                if ((probe >> q) & 1)
-                    tg[q] = ((q % NST) ? O.ck2 : O.ck1)[S::hdr(base, q)];
+                for (int st = 0; st < NST; st++) {
+                    const uint4 *kp = reinterpret_cast<const uint4 *>((st ? O.ck2 : O.ck1) + i0);
+#pragma unroll
+                    for (int q = 0; q < ORD_IT / 4; q++) {
+                        const uint4 t4 = probe ? kp[q] : make_uint4(NONE, NONE, NONE, NONE);
+                        tg[NST * (4 * q) + st] = t4.x;
+                        tg[NST * (4 * q + 1) + st] = t4.y;
+                        tg[NST * (4 * q + 2) + st] = t4.z;
+                        tg[NST * (4 * q + 3) + st] = t4.w;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < ORD_IT * NST; q++) {
+                    tg[q] = NONE;
+                    if ((probe >> q) & 1)
+                        tg[q] = ((q % NST) ? O.ck2 : O.ck1)[S::hdr(base, q)];
+                }
             }
 #pragma unroll
             for (int q = 0; q < ORD_IT * NST; q++) {
@@ -392,7 +436,7 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
             PreIn<V6> f[PK];
 #pragma unroll
             for (int k = 0; k < PK; k++) {
-                const uint64_t i = base + 256ull * (c + k) + threadIdx.x;
+                const uint64_t i = S::at(base, c + k);
                 f[k] = pre_in<V6>(A, i < A.n ? i : A.n - 1);
             }
             uint64_t hk[PK * NST];
@@ -515,9 +559,10 @@ __global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t
         w = ct_word(icmp_proto<V6>(), ((o.w2 >> 8) & 7) | 2u, o.owner);
     }
     put_rk<V6>(O, r, o.sa, o.da, z, w);
-    O.rh[r] = fp64(o.sa, o.da, z, w);
-    // header order; a create's related write right after its own lookup
-    O.rord[r] = (uint32_t)(((2 * i + (uint64_t)st) << 1) | (rel ? 1u : 0u));
+    // the sort key: a 32-bit key fingerprint, then the header order (a
+    // create's related write right after its own lookup)
+    const uint32_t ord = (uint32_t)(((2 * i + (uint64_t)st) << 1) | (rel ? 1u : 0u));
+    O.rh[r] = (fp64(o.sa, o.da, z, w) & 0xFFFFFFFF00000000ull) | ord;
     O.ridx[r] = r;
     if (rel) {
         O.pinfo[r] = PI_REL | PI_POST;
@@ -543,15 +588,6 @@ __global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t
         atomicAdd(&O.cnt[ORD_NRELKEY], 1u);
 }
 
-// the sorted fingerprints, gathered
-__global__ __launch_bounds__(256) void k_ord_gather(const uint64_t *rh, const uint32_t *idx,
-                                                    uint64_t *out, uint32_t n)
-{
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k < n)
-        out[k] = rh[idx[k]];
-}
-
 // ---- resolve: per record in (key, order) order, a lookup's result is the
 // outcome of the nearest record before it on the same key (the sorted
 // fingerprints group keys; equal fingerprints of different keys — a
@@ -569,7 +605,8 @@ __global__ __launch_bounds__(256) void k_ord_resolve(OrdArgs O, const uint64_t *
     if (f & PI_REL)
         return;
     uint8_t state = (f & PI_START) ? 1 : 0;
-    for (uint32_t j = k; j > 0 && h[j - 1] == h[k]; j--) {
+    const uint32_t fk = (uint32_t)(h[k] >> 32);
+    for (uint32_t j = k; j > 0 && (uint32_t)(h[j - 1] >> 32) == fk; j--) {
         const uint32_t q = idx[j - 1];
         if (rk_eq<V6>(O, q, r)) {
             state = (O.pinfo[q] & PI_POST) ? 1 : 0;
@@ -636,16 +673,10 @@ int sort_records(const OrdArgs &O, uint32_t n, hipStream_t s, const uint64_t **h
                  const uint32_t **idx)
 {
     size_t tb = O.tmp_bytes;
-    // by header order, then (stable) by fingerprint: (key, order)
-    hipcub::DoubleBuffer<uint32_t> ko(O.rord, O.rord2), vi(O.ridx, O.ridx2);
-    if (hipcub::DeviceRadixSort::SortPairs(O.tmp, tb, ko, vi, (int)n, 0, 32, s) != hipSuccess)
-        return -EIO;
-    hipLaunchKernelGGL(k_ord_gather, dim3((n + 255) / 256), dim3(256), 0, s, (const uint64_t *)O.rh,
-                       (const uint32_t *)vi.Current(), O.rh2, n);
-    uint32_t *vin = vi.Current(), *vout = vin == O.ridx ? O.ridx2 : O.ridx;
-    hipcub::DoubleBuffer<uint64_t> kh(O.rh2, O.rh3);
-    hipcub::DoubleBuffer<uint32_t> vv(vin, vout);
-    tb = O.tmp_bytes;
+    // one sort by (fingerprint, header order): the records' keys hold both
+    // (k_ord_keys writes them again for round 2)
+    hipcub::DoubleBuffer<uint64_t> kh(O.rh, O.rh2);
+    hipcub::DoubleBuffer<uint32_t> vv(O.ridx, O.ridx2);
     if (hipcub::DeviceRadixSort::SortPairs(O.tmp, tb, kh, vv, (int)n, 0, 64, s) != hipSuccess)
         return -EIO;
     *h = kh.Current();
@@ -694,6 +725,8 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     // (outside a service step); mark counts the creates without one, and a
     // batch with any runs mark again on pre-keys
     O.tagged = A.ck1 && (!two || A.ck2) && !A.lbr;
+    O.vec = ((uintptr_t)A.ctb & 15) == 0 && ((uintptr_t)A.ver & 15) == 0 &&
+            ((uintptr_t)A.ck1 & 15) == 0 && ((uintptr_t)A.ck2 & 15) == 0;
     if (!filter(B.creates_hint))
         return -ENOMEM;
     ORD_LAUNCH(k_ord_mark, g, A, O);
@@ -744,8 +777,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         const uint64_t nr = 2 * np;
         const size_t kw = V6 ? 48 : 16;
         if (B.rel_src.ensure(4 * np) || B.rk.ensure(kw * nr) ||
-            B.rh.ensure(8 * nr) || B.rh2.ensure(8 * nr) || B.rh3.ensure(8 * nr) ||
-            B.rord.ensure(4 * nr) || B.rord2.ensure(4 * nr) || B.ridx.ensure(4 * nr) ||
+            B.rh.ensure(8 * nr) || B.rh2.ensure(8 * nr) || B.ridx.ensure(4 * nr) ||
             B.ridx2.ensure(4 * nr) || B.pinfo.ensure(nr) || B.nres.ensure(nr))
             return -ENOMEM;
         {
@@ -762,9 +794,6 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         O.rk = B.rk.p;
         O.rh = (uint64_t *)B.rh.p;
         O.rh2 = (uint64_t *)B.rh2.p;
-        O.rh3 = (uint64_t *)B.rh3.p;
-        O.rord = (uint32_t *)B.rord.p;
-        O.rord2 = (uint32_t *)B.rord2.p;
         O.ridx = (uint32_t *)B.ridx.p;
         O.ridx2 = (uint32_t *)B.ridx2.p;
         O.pinfo = (uint8_t *)B.pinfo.p;
