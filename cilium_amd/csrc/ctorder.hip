@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
     using S = OrdStep<TWO>;
     constexpr int NST = S::NST;
     const uint64_t span = 256ull * ORD_IT, stride = (uint64_t)gridDim.x * span;
-    uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0;
+    uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0, nrk = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < A.n; base += stride) {
         S x;
         x.load(A, base, O.vec);
@@ -277,13 +277,18 @@ __global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
                 if ((crm >> q) & 1)
                     tg[q] = ((q % NST) ? O.ck2 : O.ck1)[S::hdr(base, q)];
             }
+            // (the inserts need no answer: no wait on them)
 #pragma unroll
             for (int q = 0; q < ORD_IT * NST; q++)
                 if ((crm >> q) & 1) {
-                    if (tag_ok(tg[q]))
-                        cb_put(O, tag_key(tg[q]));
-                    else
+                    if (tag_ok(tg[q])) {
+                        const uint64_t hk = tag_key(tg[q]);
+                        atomicOr(O.cbloom + ((uint32_t)(hk >> 32) & O.cb_mask),
+                                 bloom_bits((uint32_t)hk));
+                        nrk += tg[q] & 1u;
+                    } else {
                         nun++;
+                    }
                 }
         }
         // else the creates' pre-keys, per chunk of PK headers with their
@@ -325,6 +330,7 @@ __global__ __launch_bounds__(256) void k_ord_mark(CtaArgs A, OrdArgs O)
     block_add(&O.cnt[ORD_NEST], nest);
     block_add(&O.cnt[ORD_NESTDROP], ndt);
     block_add(&O.cnt[ORD_UNTAGGED], nun);
+    block_add(&O.cnt[ORD_RELBOUND], nrk);
 }
 
 // mixed: a deleted slot with an allowed CT_ESTABLISHED stage
@@ -359,6 +365,7 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
     using S = OrdStep<TWO>;
     constexpr int NST = S::NST;
     const uint64_t span = 256ull * ORD_IT, stride = (uint64_t)gridDim.x * span;
+    uint32_t nrk = 0;   // ICMP errors' stages taking part (round 2's bound)
     // (every thread runs the same number of steps: block_count_n)
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < A.n; base += stride) {
         S x;
@@ -422,6 +429,7 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
                 if (((probe >> q) & 1) &&
                     (!tag_ok(tg[q]) || (tg[q] & 1) || (O.cbloom && (fw[q] & fb) == fb)))
                     bits |= 1u << q;
+                nrk += ((probe >> q) & 1) && tag_ok(tg[q]) && (tg[q] & 1);
             }
         }
         // else per chunk of PK headers their fields loaded together (clamped,
@@ -475,6 +483,7 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
             r++;
         }
     }
+    block_add(&O.cnt[ORD_RELBOUND], nrk);
 }
 
 // a deleting stage on a slot only deletes: all but its first delete see
@@ -808,9 +817,12 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         if (int rc = sort_records<V6>(O, npi, s, &h, &idx))
             return rc;
         hipLaunchKernelGGL(k_ord_resolve<V6>, dim3(gp), dim3(256), 0, s, O, h, idx, npi);
-        if (!rd())
+        // round 2 only with an ICMP error among the participants: with the
+        // launch's tags and no deleted slot, mark and collect counted them
+        const bool relkeys = !O.tagged || O.ndel || hc[ORD_RELBOUND];
+        if (relkeys && !rd())
             return -EIO;
-        if (hc[ORD_NRELKEY]) {
+        if (relkeys && hc[ORD_NRELKEY]) {
             // round 2: the related entries of the creates round 1 resolved
             hipLaunchKernelGGL(k_ord_relsrc, dim3(gp), dim3(256), 0, s, O, npi);
             if (!rd())
