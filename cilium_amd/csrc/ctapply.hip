@@ -1500,30 +1500,32 @@ __device__ __forceinline__ int gc_map(const uint32_t *smaps, uint32_t n, uint32_
 // (block_count_n): a steady-state GC deletes millions of entries, and one
 // atomic per wave on the shared counter serialised at its L2 channel.
 constexpr int GC_U = 8;
-__global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
+// (1024-thread blocks, one per CU: one list atomic per 8192 slots)
+constexpr int GC_B = 1024;
+__global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
 {
     __shared__ uint32_t smaps[CTG_MAX_MAPS], scnt[CTG_MAX_MAPS];
-    for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256) {
+    for (uint32_t j = threadIdx.x; j < A.n_maps; j += GC_B) {
         smaps[j] = A.maps[j];
         scnt[j] = 0;
     }
     __syncthreads();
     uint32_t fresh = 0, live = 0, nonfree = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * GC_U;
+    const uint64_t stride = (uint64_t)gridDim.x * GC_B * GC_U;
     // (every thread runs the same number of steps: block_count_n needs the
     // whole block)
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 * GC_U; base < A.slots; base += stride) {
+    for (uint64_t base = (uint64_t)blockIdx.x * GC_B * GC_U; base < A.slots; base += stride) {
         uint4 k[GC_U];
         int j[GC_U];
         uint32_t life[GC_U], infy[GC_U];
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {   // (no branches: the loads issue together)
-            const uint64_t s = base + u * 256 + threadIdx.x;
+            const uint64_t s = base + u * GC_B + threadIdx.x;
             k[u] = ld16(A.ct4 + (s < A.slots ? s : A.slots - 1));
         }
 #pragma unroll
         for (int u = 0; u < GC_U; u++)
-            if (base + u * 256 + threadIdx.x >= A.slots)
+            if (base + u * GC_B + threadIdx.x >= A.slots)
                 k[u] = make_uint4(0, 0, 0, 0);
         // a tombstone, a claim, or an apply's delete the host has not taken
         // is no entry of a map
@@ -1537,13 +1539,13 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
         }
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {   // (every slot's: no branch between the loads)
-            const uint64_t s = base + u * 256 + threadIdx.x;
+            const uint64_t s = base + u * GC_B + threadIdx.x;
             life[u] = A.tm[s < A.slots ? s : A.slots - 1].lifetime;
         }
         bool del[GC_U], logit[GC_U];
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {
-            const uint64_t s = base + u * 256 + threadIdx.x;
+            const uint64_t s = base + u * GC_B + threadIdx.x;
             del[u] = j[u] >= 0 && gc_delete(A, k[u].x, k[u].y, life[u]) &&
                      !(A.protect && ((A.protect[s >> 5] >> (s & 31)) & 1u));
             infy[u] = del[u] ? A.info[s].y : 0u;
@@ -1563,7 +1565,7 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
         for (int u = 0; u < GC_U; u++) {
             if (!del[u])
                 continue;
-            const uint64_t s = base + u * 256 + threadIdx.x;
+            const uint64_t s = base + u * GC_B + threadIdx.x;
             if (logit[u]) {
                 if (r < A.log_cap)
                     A.log[r] = CtGcRec{(uint32_t)s, k[u].x, k[u].y, k[u].z, k[u].w};
@@ -1580,7 +1582,7 @@ __global__ __launch_bounds__(256) void k_ct_gc4(CtGcArgs A)
     block_add(&A.cnt[CTG_LIVE], live);
     block_add(&A.cnt[CTG_NONFREE], nonfree);
     block_add(&A.cnt[CTG_FRESH], fresh);
-    for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256)
+    for (uint32_t j = threadIdx.x; j < A.n_maps; j += GC_B)
         if (scnt[j])
             atomicAdd(&A.mcnt[j], scnt[j]);
 }
@@ -1641,7 +1643,9 @@ __global__ __launch_bounds__(256) void k_ct_gc_log(CtGcArgs A, const CtLog *in, 
         keep = gc_map(smaps, A.n_maps, g.w & 0xFFFF0800u) < 0 ||
                !gc_delete(A, g.x, g.y, g.now + CT_LIFETIME_NONTCP);
     }
-    const uint32_t r = wave_count(&A.cnt[CTG_LOGKEPT], keep);
+    // (one list atomic per block: per wave, a million entries' worth
+    // serialised at the counter's L2 channel)
+    const uint32_t r = block_count(&A.cnt[CTG_LOGKEPT], keep);
     if (keep)
         out[r] = g;
 }
@@ -1894,7 +1898,11 @@ int ct_gc4(const CtGcArgs &A, hipStream_t s)
 {
     if (!A.slots || A.n_maps > CTG_MAX_MAPS)
         return -EINVAL;
-    hipLaunchKernelGGL(k_ct_gc4, dim3(blocks_for(A.slots, 2048)), dim3(256), 0, s, A);
+    hipLaunchKernelGGL(k_ct_gc4, dim3((unsigned)std::max<uint64_t>(
+                                     1, std::min<uint64_t>((A.slots + GC_B * GC_U - 1) /
+                                                               (GC_B * GC_U),
+                                                           256))),
+                       dim3(GC_B), 0, s, A);
     hipLaunchKernelGGL(k_ct_trim4, dim3(blocks_for(A.slots, 2048)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -96,10 +96,10 @@ __device__ __forceinline__ uint32_t block_count(uint32_t *ctr, bool want)
     return r;
 }
 // n items of this thread in a block-wide list: the first one's index, one
-// atomic per block (every thread of the block calls it)
+// atomic per block (every thread of the block calls it; up to 1024 threads)
 __device__ __forceinline__ uint32_t block_count_n(uint32_t *ctr, uint32_t v)
 {
-    __shared__ uint32_t wsum[4], base;
+    __shared__ uint32_t wsum[16], base;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     uint32_t x = v;
 #pragma unroll
@@ -112,7 +112,9 @@ __device__ __forceinline__ uint32_t block_count_n(uint32_t *ctr, uint32_t v)
         wsum[wv] = x;
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < (blockDim.x >> 6); k++)
+            t += wsum[k];
         base = t ? atomicAdd(ctr, t) : 0u;
     }
     __syncthreads();
@@ -173,7 +175,7 @@ __device__ __forceinline__ void block_flush(uint64_t *stage, uint32_t *sn, uint3
 // their L2 channel
 __device__ __forceinline__ void block_add(uint32_t *ctr, uint32_t v)
 {
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[16];   // (up to 1024 threads)
     for (int o = 32; o > 0; o >>= 1)
         v += __shfl_xor(v, o, 64);
     if ((threadIdx.x & 63) == 0)
