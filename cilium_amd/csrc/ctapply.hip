@@ -651,11 +651,14 @@ __device__ __forceinline__ ReqKey<V6> req_key(const CtaArgs &A, uint32_t ord, Op
 // balancer's ct_state, its reverse-NAT entry (round 1): the request is
 // marked (bit 0 of its word) and k_cta_related makes those requests — no
 // per-request atomic on a shared counter here.
+// (1024-thread blocks for the per-request passes: one counter atomic per
+// 1024 requests)
+constexpr int RQ_B = 1024;
 template <bool V6>
-__global__ __launch_bounds__(256) void k_cta_insert(CtaArgs A, uint64_t *req, uint32_t nreq,
+__global__ __launch_bounds__(RQ_B) void k_cta_insert(CtaArgs A, uint64_t *req, uint32_t nreq,
                                                     int round, uint32_t cx_off)
 {
-    const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t r0 = blockIdx.x * RQ_B + threadIdx.x;
     const uint64_t home = r0 < nreq ? req[r0] >> A.ob : 0;
     const bool lead = r0 < nreq && (r0 == 0 || (req[r0 - 1] >> A.ob) != home);
     const uint64_t omask = (1ull << A.ob) - 1;
@@ -783,10 +786,10 @@ __global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *
 // for a TCP map (no lookup reaches it there), and whose reverse-NAT entry
 // (ct_create4 with ct_state->addr) is a round-1 request
 template <bool V6>
-__global__ __launch_bounds__(256) void k_cta_related(CtaArgs A, const uint64_t *req,
+__global__ __launch_bounds__(RQ_B) void k_cta_related(CtaArgs A, const uint64_t *req,
                                                      uint32_t nreq)
 {
-    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t r = blockIdx.x * RQ_B + threadIdx.x;
     const uint64_t v = r < nreq ? req[r] : 0ull;
     const uint32_t ord = (uint32_t)(v & ((1ull << A.ob) - 1)) & ~1u;
     Op<V6> o;
@@ -1775,9 +1778,9 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     if (!sorted && (rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
         return rc;
     if (nreqA) {
-        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A, sorted,
+        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqA + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A, sorted,
                            nreqA, 0, 0u);
-        hipLaunchKernelGGL(k_cta_related<V6>, dim3((nreqA + 255) / 256), dim3(256), 0, s, A,
+        hipLaunchKernelGGL(k_cta_related<V6>, dim3((nreqA + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A,
                            (const uint64_t *)sorted, nreqA);
     }
     if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1789,7 +1792,7 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     if ((rc = sort_keys(A, A.reqB, A.reqB2, nreqB, bits, s, &sorted)))
         return rc;
     if (nreqB)
-        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqB + 255) / 256), dim3(256), 0, s, A, sorted,
+        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqB + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A, sorted,
                            nreqB, 1, nreqA);
     // the creates' ops take the list's first nreqA + nreqB places, route's
     // ordered hits follow

@@ -78,14 +78,16 @@ __device__ __forceinline__ uint32_t wave_count(uint32_t *ctr, bool want)
 // L2 channel).  Every thread of the block calls it.
 __device__ __forceinline__ uint32_t block_count(uint32_t *ctr, bool want)
 {
-    __shared__ uint32_t wsum[4], base;
+    __shared__ uint32_t wsum[16], base;   // (up to 1024 threads)
     const uint64_t m = __ballot(want);
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0)
         wsum[wv] = (uint32_t)__popcll(m);
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < (blockDim.x >> 6); k++)
+            t += wsum[k];
         base = t ? atomicAdd(ctr, t) : 0u;
     }
     __syncthreads();
