@@ -184,6 +184,11 @@ def main():
                          "table) + the CT garbage collector when its interval has "
                          "passed; the new flows' source ports are re-drawn on the "
                          "device at the start of each step, so every step creates")
+    ap.add_argument("--stream", default="spec", choices=["spec", "seq"],
+                    help="c5: spec = SURVEY.md §8d's C5 stream (new flows whose "
+                         "reverse is not in the batch); seq = synth.headers_c5_seq, "
+                         "the dependency-heavy stream of the packet-order tests "
+                         "(new flows of several packets, closes, deletes, ICMP errors)")
     ap.add_argument("--step-seconds", type=int, default=61,
                     help="--ct-apply: datapath clock advance per step (cfc_set_clock)")
     ap.add_argument("--gc-interval", type=int, default=60,
@@ -255,8 +260,16 @@ def main():
         s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
     elif args.workload == "c5":
         from cilium_amd.datapath import pack_v4
-        h5, new5 = S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank,
-                                return_new=True, owner=(rank, world))
+        if args.stream == "seq":
+            assert world == 1, "--stream seq: one GPU"
+            h5, new5 = S.headers_c5_seq(tables, flows, n, seed=args.seed * 1000 + rank,
+                                        return_new=True)
+            # (the ports of TCP / UDP new flows are re-drawn per step; ICMP
+            # keeps its type: an error stays related to its flow's pair)
+            new5 &= (h5.proto == S.IPPROTO_TCP) | (h5.proto == S.IPPROTO_UDP)
+        else:
+            h5, new5 = S.headers_c5(tables, flows, n, seed=args.seed * 1000 + rank,
+                                    return_new=True, owner=(rank, world))
         hb = pack_v4(h5, dev)
         s, d, p, m, tf = hb.saddr, hb.daddr, hb.ports, hb.meta, hb.tcp_flags
         del hb, h5
@@ -332,6 +345,7 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] batch of {n} headers generated ({(n * S_IN) >> 20} MiB)")
 
+    ord0 = None
     for w in range(args.warmup):
         step()
         if args.ct_apply:   # each step creates its new flows, the GC drops old ones
@@ -346,6 +360,8 @@ def main():
     # classify kernel and the counter kernels of every timed call
     dp.set_option(LL.OPT_TIMING, 1)
     dp.timing_collect()
+    if args.ct_apply:
+        ord0 = dp.stats()["ct_order_changed"]
 
     stream = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -505,7 +521,11 @@ def main():
                          if args.workload == "c3" else
                          f"C5: C2 tables + {st['ct4_entries']} reachable CT4 "
                          f"entries ({args.flows} live flows, global CT maps), "
-                         "95% Zipf(1.1) packets of live flows + 5% new, ")
+                         + ("95% Zipf(1.1) packets of live flows + 5% new, "
+                            if args.stream == "spec" else
+                            "92% Zipf(1.1) packets of live flows (2% closing, denied "
+                            "flows deleted) + 8% new flows of several packets "
+                            "(synth.headers_c5_seq), "))
                         + f"{n + n6}-header batch per GPU, mode {args.mode}",
             "headers_per_step_per_gpu": n + n6,
             "ipcache_prefixes": st["ipcache_v4_prefixes"],
@@ -585,6 +605,10 @@ def main():
             "gc_ms_per_run": round(float(np.mean([b.elapsed_time(c) for _, b, c in ct_ev
                                                   if c is not None])), 4)
             if any(c is not None for _, _, c in ct_ev) else None,
+            "stream": args.stream,
+            # CT stages per step whose packet-order result differs from the
+            # batch-start lookup (ctorder.hip), and their share of the stages
+            "ct_order_changed_per_step": (st2["ct_order_changed"] - ord0) / args.steps,
             "clock_s_per_step": args.step_seconds,
             "gc_interval_s": args.gc_interval,
             "gc_runs": clock["gcs"],

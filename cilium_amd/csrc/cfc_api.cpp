@@ -182,6 +182,7 @@ struct cfc_ctx {
     // bitmap (zero between applies), counters; the stages it changed
     OrdBufs ordb;
     DevBuf ord_delbm, ord_mixbm, ord_dfirst, ord_cnt;
+    DevBuf ord_ct0;               // IPv6: the CT bytes before the pass (ord_pkt6)
     DevBuf cta_mon;               // per header stage: the fold's monitor length
     uint64_t n_ord_changed = 0;
     // LXC_NAT46 (nat.hip): the hop batch of each classified batch that had
@@ -203,6 +204,10 @@ struct cfc_ctx {
     };
     std::map<const void *, NatRec> nat;
     DevBuf nat_list, nat_cnt, nat_tmp;
+    // the service step in packet order (svcorder.hip): sort keys, the
+    // per-header CT_SERVICE entry words (zero between launches), count
+    DevBuf svo_keys, svo_keys2, svo, svo_cnt, svo_tmp;
+    uint64_t n_svo = 0;   // headers handed an entry an earlier header left
     bool nat46_seen = false, hop_nat46 = false;
     uint64_t n_nat_hops = 0;
     // eviction at a CT map's capacity (ct_evict; CFC_OPT_CT_EVICT)
@@ -1906,6 +1911,7 @@ int nat_hop(cfc_ctx *c, const DevTables &T, const EgressArgs &ea, const Hdr &in,
     EgressArgs e2 = ea;
     e2.nat_idx = e2.nat_cnt = nullptr;
     e2.sums = nullptr;
+    e2.svo = nullptr;   // (the hop rows are another batch)
     const int smode = V6 ? CFC_MODE_EGRESS : CFC_MODE_INGRESS;
     const WsLayout wl = ws_layout(m, T, smode, true);
     if (r.ws.ensure(wl.total))
@@ -2023,6 +2029,32 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.nat_idx = (uint32_t *)c->nat_list.p;
         ea.nat_cnt = (uint32_t *)c->nat_cnt.p;
     }
+    // an egress batch with services: the CT_SERVICE entry each header finds
+    // in packet order (the creates and re-selections of the headers before
+    // it), handed to the launch's service step
+    uint32_t nsvo = 0;
+    if (mode == CFC_MODE_EGRESS && in->n &&
+        (std::is_same<Hdr, cfc_hdr_v6>::value ? E.T.lb6 != nullptr : E.T.lb4 != nullptr)) {
+        const uint64_t n = in->n;
+        const size_t tb = svc_order_tmp_bytes(n);
+        if (c->svo_keys.bytes < 8 * n || c->svo.bytes < 4 * n || c->svo_tmp.bytes < tb) {
+            (void)hipStreamSynchronize(s);
+            if (c->svo_keys.ensure(8 * n) || c->svo_keys2.ensure(8 * n) || c->svo_tmp.ensure(tb) ||
+                c->svo.zeros(4 * n, s))
+                return -ENOMEM;
+        }
+        if (c->svo_cnt.ensure(16))
+            return -ENOMEM;
+        SvoArgs sa{(const uint32_t *)in->saddr, (const uint32_t *)in->daddr, in->ports, in->meta,
+                   in->hash, n, ep_lxc, ea.ct_owner,
+                   (uint64_t *)c->svo_keys.p, (uint64_t *)c->svo_keys2.p, (uint32_t *)c->svo.p,
+                   (uint32_t *)c->svo_cnt.p, c->svo_tmp.p, c->svo_tmp.bytes};
+        if ((rc = svc_order(T, sa, std::is_same<Hdr, cfc_hdr_v6>::value, &nsvo, s)))
+            return rc;
+        if (nsvo)
+            ea.svo = (const uint32_t *)c->svo.p;
+        c->n_svo += nsvo;
+    }
     const WsLayout wl = ws_layout(in->n, E.T, mode,
                                   E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4 ||
                                       E.T.lb6 || E.T.rnat6);
@@ -2060,6 +2092,9 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
                 in->n ? next_timing(c, std::is_same<Hdr, cfc_hdr_v6>::value) : nullptr);
     c->sum_dirty |= sums;
     c->sum_pending = sums;
+    if (!rc && nsvo &&   // (the entry words zero again for the next launch)
+        hipMemsetAsync(c->svo.p, 0, 4 * in->n, s) != hipSuccess)
+        rc = -EIO;
     if (rc)
         return rc;
     if (nat_list) {
@@ -3076,8 +3111,17 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         O.slots = c->ord_dfirst.bytes / 4;
         O.cnt = (uint32_t *)c->ord_cnt.p;
         uint32_t changed = 0;
+        // (IPv6 with reverse NAT: the packet outputs follow the new results)
+        const bool pkt6 = V6 && out->pkt_saddr && out->pkt_ports && E.T.rnat6;
+        if (pkt6 && (c->ord_ct0.ensure(n) ||
+                     hipMemcpyAsync(c->ord_ct0.p, out->ct, n, hipMemcpyDeviceToDevice, s) !=
+                         hipSuccess))
+            return -ENOMEM;
         if (int rc = ord_resolve(A, O, c->ordb, V6, &changed, s))
             return rc;
+        if (pkt6)
+            if (int rc = ord_pkt6(A, (const uint8_t *)c->ord_ct0.p, *out, s))
+                return rc;
         c->n_ord_changed += changed;
     }
     // the caller wants the event words: the trace words' monitor lengths in

@@ -525,21 +525,27 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                                                     (h.rec.w & LXC_CT_LOCAL) != 0);
                 c2 = ct_stage4(T, h.psa, h.da, proto, h.pt, CT_INGRESS, own2);
                 dp2 = c2.dport;
-                if (LB && own2 == E.ct_owner && h.ct_res == CT_NEW && (v >= 0 || reply)) {
-                    // the entries this header's egress stage created (ct_create4
-                    // with the service's ct_state: main and reverse-NAT entry)
-                    // are in the map the destination's lookup runs on
+                if (own2 == E.ct_owner && h.ct_res == CT_NEW && (v >= 0 || reply)) {
+                    // the entries this header's egress stage created (ct_create4:
+                    // main, ICMP and, with the service's ct_state, reverse-NAT
+                    // entry) are in the map the destination's lookup runs on
+                    // (an endpoint's traffic to itself, or a looped-back service)
                     const CtProbe k0 = ct_probe<false>(proto, h.tpt, CT_EGRESS, E.ct_owner);
                     const CtProbe k = ct_probe<false>(proto, h.pt, CT_INGRESS, own2);
-                    const bool svc = (h.lbfl & LBF_SVC) != 0, loop = (h.lbfl & LBF_LOOP) != 0;
-                    // main: k2 of the egress lookup; reverse-NAT entry: its
+                    const bool svc = LB && (h.lbfl & LBF_SVC) != 0;
+                    const bool loop = LB && (h.lbfl & LBF_LOOP) != 0;
+                    // main: k2 of the egress lookup; ICMP entry (ANY maps
+                    // only: a TCP map's is one no lookup reaches): ports 0,
+                    // k2's flags | TUPLE_F_RELATED; reverse-NAT entry: its
                     // daddr the service step's address, a looped-back flow's
                     // with TUPLE_F_IN and the sender as saddr
                     const uint32_t ex = loop ? IPV4_LOOPBACK : h.da;
                     const uint32_t ey = loop ? h.sa : h.tda;
                     const uint32_t ew = loop ? ct_word(proto, 1u, E.ct_owner) : k0.w2;
+                    const uint32_t rw = ct_word(1u, ((k0.w2 >> 8) & 7) | 2u, E.ct_owner);
                     auto is_fresh = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t w) {
-                        return (x == h.sa && y == h.tda && z == k0.z2 && w == k0.w2) ||
+                        return (x == h.sa && y == h.tda &&
+                                ((z == k0.z2 && w == k0.w2) || (proto != 6 && z == 0 && w == rw))) ||
                                (svc && x == ex && y == ey && z == k0.z2 && w == ew);
                     };
                     if (is_fresh(h.da, h.psa, k.z1, k.w1)) {
@@ -594,7 +600,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                     uint32_t mon2 = ct_monitor(T, CT ? T.ct4_tm : nullptr,
                                                CT ? c2.slot : NONE, CT_INGRESS,
                                                action, tfl, dp2);
-                    if (LB && fresh)   // the entry as ct_create4 just wrote it
+                    if (fresh)   // the entry as ct_create4 just wrote it
                         mon2 = dp2 == 0x3500u ? MTU_LEN
                                : ct_monitor_of(T, make_uint4(0, T.now, 0, 0), CT_INGRESS,
                                                action, tfl);
@@ -1847,7 +1853,7 @@ int launch_classify_v4(const DevTables &T, const cfc_hdr_v4 &in,
         uint32_t *a = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(ws) + w.lb);
         const uint64_t st = ctr_stride(in.n);
         LbArgs A{in.saddr, in.daddr, in.ports, in.meta, in.hash, in.n, E.ct_owner,
-                 a, a + st, a + 2 * st, a + 3 * st, a + 4 * st, a + 5 * st};
+                 a, a + st, a + 2 * st, a + 3 * st, a + 4 * st, a + 5 * st, E.svo};
         if (int rc = launch_lb4_egress(T, A, s))
             return rc;
         li = LbIn{A.tda, A.tpt, A.psa, A.fl};

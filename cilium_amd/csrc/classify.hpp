@@ -29,6 +29,9 @@ struct EgressArgs {
     uint32_t *nat_idx, *nat_cnt;
     const uint32_t *nat_id;
     bool *sums;   // (host) set when the launch wrote DevTables.ct_sum
+    // an egress batch with services: per header the CT_SERVICE entry as the
+    // headers before it left it (kern_common.hpp SVO_*; svcorder.hip), or null
+    const uint32_t *svo;
 };
 
 constexpr int BLOCK = 1024;
@@ -328,6 +331,10 @@ struct OrdBufs {
 // result differs from the launch's; *changed: how many
 int ord_resolve(const CtaArgs &A, OrdArgs &O, OrdBufs &B, bool v6, uint32_t *changed,
                 hipStream_t s);
+// IPv6: the packet outputs of the ipv6_policy stages ord_resolve turned
+// CT_ESTABLISHED (reverse-NATed by the index their create stored) or CT_NEW
+// (not); ct0: the CT bytes before ord_resolve
+int ord_pkt6(const CtaArgs &A, const uint8_t *ct0, const cfc_out &out, hipStream_t s);
 size_t cta_sort_tmp_bytes(uint32_t n);
 // v6: the batch is IPv6 (A.ct6, A.log6).  A batch with a load balancer's
 // service step (A.lbr) runs cta_lb_pre first (with A.cnt zeroed), then the
@@ -412,8 +419,26 @@ struct LbArgs {
     uint64_t n;
     uint32_t ct_owner;                            // the sender's CT maps
     uint32_t *tda, *tpt, *psa, *pda, *ppt, *fl;   // per header (lb.hip)
+    const uint32_t *svo;   // per header the CT_SERVICE entry in packet order, or null
 };
 int launch_lb4_egress(const DevTables &T, const LbArgs &A, hipStream_t stream);
+// the service step in packet order (svcorder.hip): the headers whose
+// CT_SERVICE entry the batch creates or re-slaves, sorted by entry and
+// header order; per such header after the first of its entry the entry as
+// the ones before it leave it (svo).  n < 2^31.  *count: such headers (0:
+// svo untouched); the caller owns keys (2 x 8n bytes), svo (4n, zero),
+// cnt (4), tmp (svc_order_tmp_bytes(n))
+struct SvoArgs {
+    const uint32_t *sa, *da, *pt, *mt, *hash;   // the batch (IPv6: 4 words per address)
+    uint64_t n;
+    uint32_t lxc_id, ct_owner;                  // the sending endpoint
+    uint64_t *keys, *keys2;
+    uint32_t *svo, *cnt;
+    void *tmp;
+    size_t tmp_bytes;
+};
+size_t svc_order_tmp_bytes(uint64_t n);
+int svc_order(const DevTables &T, const SvoArgs &A, bool v6, uint32_t *count, hipStream_t s);
 // the service step's results a classify launch reads (EGRESS), and the
 // packet outputs; all null when the launch has no load balancer
 struct LbIn {

@@ -82,12 +82,6 @@ __device__ __forceinline__ uint32_t mkey6(int reason, int dir)
     }
 }
 
-__device__ __forceinline__ uint4 bswap4(uint4 v)
-{
-    return make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y),
-                      __builtin_bswap32(v.z), __builtin_bswap32(v.w));
-}
-
 // ---- IPv6 LPM (layout.h Lpm6): the label of the longest prefix holding the
 // host-order address a (a matched label 0 shadows shorter prefixes, as the
 // reference's trie does), def_label when none
@@ -171,19 +165,6 @@ __device__ __forceinline__ bool ct6_new_dport(uint32_t proto, uint32_t ports,
     return proto == 58;
 }
 
-// icmp6_handle (icmp6.h:390-412): neighbour solicitations and echo requests
-// to the router are answered, not classified.  It reads the type right after
-// the fixed header, so with extension headers it never triggers.
-__device__ __forceinline__ bool icmp6_punt(const DevTables &T, uint32_t proto,
-                                           uint32_t meta, uint32_t ports, uint4 da)
-{
-    if (proto != 58 || (meta & CFC_HF_EXTHDR))
-        return false;
-    const uint32_t type = ports & 0xFF;
-    return type == 135 || (type == 128 && da.x == T.router6[0] && da.y == T.router6[1] &&
-                           da.z == T.router6[2] && da.w == T.router6[3]);
-}
-
 // LDS image of a v6 launch: metrics | endpoint slots | policy Bloom | the
 // length lists of the three Lpm6 tables (ipcache, prefilter fix, dyn): a
 // lookup reads its next length from LDS, not by a dependent global load
@@ -225,7 +206,7 @@ __device__ __forceinline__ uint32_t id_event(const DevTables &T, const CountArgs
 __device__ __forceinline__ bool lb6_egress(const DevTables &T, const EgressArgs &E,
                                            const cfc_hdr_v6 &in, uint64_t i, uint4 sa_raw,
                                            uint4 da_raw, uint32_t proto, uint32_t pt, uint4 &psa,
-                                           uint4 &pda, uint32_t &ppt)
+                                           uint4 &pda, uint32_t &ppt, uint32_t &rev)
 {
     (void)psa;
     const bool l4 = proto == 6 || proto == 17;
@@ -238,9 +219,13 @@ __device__ __forceinline__ bool lb6_egress(const DevTables &T, const EgressArgs 
     // lb6_local: ct_lookup6(CT_SERVICE), the tuple as loaded, one probe; a
     // hit's slave from the entry, else lb6_select_slave: hash % count + 1
     const CtProbe k = ct_probe<true>(proto, pt, CT_SERVICE, E.ct_owner);
-    const uint32_t slot = ct6_find(T, da_raw, sa_raw, k.z1, k.w1);
+    // (an entry an earlier header of the batch created or re-slaved: E.svo)
+    const uint32_t ov = E.svo ? E.svo[i] : 0u;
+    const uint32_t slot = (ov & SVO_SET) ? NONE : ct6_find(T, da_raw, sa_raw, k.z1, k.w1);
     uint32_t slave;
-    if (slot != NONE) {
+    if (ov & SVO_SET) {
+        slave = ov & 0xFFFF;
+    } else if (slot != NONE) {
         slave = T.ct6_lb ? ld16(T.ct6_lb + slot).y : 0u;
     } else {
         const uint32_t h = in.hash ? in.hash[i] : flow_hash6(sa_raw, da_raw, pt, proto);
@@ -253,6 +238,7 @@ __device__ __forceinline__ bool lb6_egress(const DevTables &T, const EgressArgs 
     if (!ok)
         return true;
     pda = tg2;   // lb6_xlate
+    rev = b2.z & 0xFFFF;   // (state->rev_nat_index, ct_create6's)
     const uint32_t port = b2.y & 0xFFFF;
     if (port && kd != port && l4)
         ppt = (ppt & 0xFFFFu) | port << 16;
@@ -328,6 +314,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         uint32_t idw = KEY_NONE, ev2 = 0;  // identity counter key; stage-2 event
         uint32_t evw = 0;                  // trace event word (forwarded)
         bool nat = false, natdrop = false; // NAT64: the hop decides; can't translate
+        uint32_t svc_rev = 0;              // the service's rev_nat_index (LB)
         const uint32_t len = mt >> 16;
         // the Bloom words of the prefilter's and the ipcache's lookups of
         // this header's address, loaded together (egress with a load
@@ -470,7 +457,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     ver = DROP_CT_UNKNOWN_PROTO;
                     met0 = mkey6<MODE>(DROP_CT_UNKNOWN_PROTO, METRIC_EGRESS);
                 } else if (LB && lb6_egress(T, E, in, i, sa_raw, da_raw, proto, pt, psa, pda,
-                                            ppt)) {
+                                            ppt, svc_rev)) {
                     ver = DROP_NO_SERVICE;   // lb6_local found no backend
                     if (valid) {
                         unsigned long long *m = reinterpret_cast<unsigned long long *>(
@@ -574,11 +561,44 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 ct6_new_dport(proto, ppt, &dport2);
                             CtResult c2{CT_NEW, NONE, dport2};
                             const uint4 s2 = LB ? psa : sa_raw;
+                            bool fresh = false;
                             if (CT) {
                                 const uint32_t own2 = ct_owner_word(erec.z & 0xFFFF,
                                                                     (erec.z & LXC_CT_LOCAL) != 0);
                                 c2 = ct_stage6(T, s2, tda_raw, proto, LB ? ppt : pt, CT_INGRESS,
                                                own2);
+                                if (own2 == E.ct_owner && c.res == CT_NEW) {
+                                    // the entries this header's ct_create6 wrote (main,
+                                    // and in an ANY map its ICMPv6 entry) are in the map
+                                    // the destination's lookup runs on: an endpoint's
+                                    // traffic to itself finds its own entry
+                                    const CtProbe k0 =
+                                        ct_probe<true>(proto, tpt, CT_EGRESS, E.ct_owner);
+                                    const CtProbe k =
+                                        ct_probe<true>(proto, LB ? ppt : pt, CT_INGRESS, own2);
+                                    const uint32_t rw =
+                                        ct_word(58u, ((k0.w2 >> 8) & 7) | 2u, E.ct_owner);
+                                    auto is_fresh = [&](uint4 d, uint4 sx, uint32_t z, uint32_t w) {
+                                        return d.x == sa_raw.x && d.y == sa_raw.y &&
+                                               d.z == sa_raw.z && d.w == sa_raw.w &&
+                                               sx.x == tda_raw.x && sx.y == tda_raw.y &&
+                                               sx.z == tda_raw.z && sx.w == tda_raw.w &&
+                                               ((z == k0.z2 && w == k0.w2) ||
+                                                (proto != 6 && z == 0 && w == rw));
+                                    };
+                                    if (is_fresh(tda_raw, s2, k.z1, k.w1)) {
+                                        fresh = true;
+                                        c2.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
+                                        c2.dport = k.td;
+                                    } else if (c2.res < CT_REPLY &&
+                                               is_fresh(s2, tda_raw, k.z2, k.w2)) {
+                                        fresh = true;
+                                        c2.res = CT_ESTABLISHED;
+                                        c2.dport = k.ts;
+                                    }
+                                    if (fresh)
+                                        c2.slot = NONE;   // (not in the table: the apply counts it)
+                                }
                                 ck2 = c2.slot != NONE
                                           ? ct_acct_key(c2.slot + T.ct6_acct_base, CT_INGRESS)
                                       : c2.res == CT_NEW
@@ -590,6 +610,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 pda.w &= 0xFFFF0000u;
                                 if (CT && c2.slot != NONE && T.ct6_lb)
                                     lb6_rev_nat(T, ld16(T.ct6_lb + c2.slot).x, proto, psa, ppt);
+                                else if (fresh)   // the entry as ct_create6 just wrote it
+                                    lb6_rev_nat(T, svc_rev, proto, psa, ppt);
                             }
                             const bool reply2 = CT && c2.res >= CT_REPLY;
                             const PolicyResult pw = policy_access(
@@ -609,14 +631,19 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 act = (prox || eifx) ? TC_ACT_REDIRECT : TC_ACT_OK;
                                 ver = prox ? pw.verdict : 0;
                                 met1 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
-                                if (NT)
-                                    evw = trace_word(
-                                        prox ? OBS_TO_PROXY : OBS_TO_LXC, erec.z & 0xFFFF,
-                                        (uint32_t)c2.res,
-                                        ct_monitor(T, CT ? T.ct6_tm : nullptr, c2.slot,
-                                                   CT_INGRESS,
-                                                   ct_action(true, proto, LB ? ppt : pt, mt),
-                                                   tfl, c2.dport));
+                                if (NT) {
+                                    const uint32_t a2 = ct_action(true, proto, LB ? ppt : pt, mt);
+                                    uint32_t mon2 = ct_monitor(T, CT ? T.ct6_tm : nullptr,
+                                                               c2.slot, CT_INGRESS, a2, tfl,
+                                                               c2.dport);
+                                    if (fresh)   // the entry as ct_create6 just wrote it
+                                        mon2 = c2.dport == 0x3500u
+                                                   ? MTU_LEN
+                                                   : ct_monitor_of(T, make_uint4(0, T.now, 0, 0),
+                                                                   CT_INGRESS, a2, tfl);
+                                    evw = trace_word(prox ? OBS_TO_PROXY : OBS_TO_LXC,
+                                                     erec.z & 0xFFFF, (uint32_t)c2.res, mon2);
+                                }
                             }
                         }
                     }

@@ -583,8 +583,11 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                     if ((A.ms[r.svc].x & b) != b)
                         atomicOr(&A.ms[r.svc].x, b);
                 }
-                if (o.reslave && A.lb)   // ct_update4/6_slave
-                    A.lb[r.svc].y = o.slave;
+                // ct_update4/6_slave: the entry's last re-selection in
+                // header order wins (several headers may re-select): the
+                // fold replays the slot's ops in order
+                if (o.reslave && A.lb)
+                    order_mark(A, r.svc, MARK_ORDERED);
             } else if (o.kind == OP_CREATE) {
                 rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask,
                                  ord_of(A.n + i, 0, SEC_OP));
@@ -1143,6 +1146,10 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
             }
         } else if (live) {   // OP_HIT, OP_DELETE
             put_mon(A, ord, hit(e, A.now, o));
+            if (o.reslave) {   // ct_update4/6_slave on an entry the batch found
+                lby = o.slave;
+                reslaved = true;
+            }
             if (created) {
                 // a hit after this batch wrote the entry anew (a related
                 // entry overwritten by a later create): the launch counted it

@@ -295,6 +295,35 @@ __device__ __forceinline__ uint32_t dst_owner(const DevTables &T, uint4 da)
     }
 }
 
+// is_valid_lxc_src_ip (lxc.h:46-57): the source address is the sending
+// endpoint's (cilium_lxc)
+__device__ __forceinline__ bool lb4_src_ok(const DevTables &T, uint32_t sa, uint32_t lxc_id)
+{
+    if (!T.lxc4)
+        return false;
+    for (uint32_t s = hash32(sa, T.lxc4_mask);; s = (s + 1) & T.lxc4_mask) {
+        const uint4 v = ld16(T.lxc4 + s);
+        if (!(v.w & LXC_VALID))
+            return false;
+        if (v.x == sa)
+            return (v.w & 0xFFFF) == lxc_id;
+    }
+}
+__device__ __forceinline__ bool lb6_src_ok(const DevTables &T, uint4 sa, uint32_t lxc_id)
+{
+    if (!T.lxc6)
+        return false;
+    for (uint32_t s = l6_hash(sa.x, sa.y, sa.z, sa.w, L6_LXC_TAG) & T.lxc6_mask;;
+         s = (s + 1) & T.lxc6_mask) {
+        const uint4 k = ld16(&T.lxc6[s].a[0]);
+        const uint4 v = ld16(&T.lxc6[s].pol_base);
+        if (!(v.z & LXC_VALID))
+            return false;
+        if (aeq(k, sa))
+            return (v.z & 0xFFFF) == lxc_id;
+    }
+}
+
 template <bool V6>
 using LbRecT = typename std::conditional<V6, LbRec6, LbRec4>::type;
 

@@ -853,7 +853,59 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
+// ---- IPv6: ipv6_policy reverse-NATs the packet of every CT hit whose
+// entry's rev_nat_index cilium_lb6_reverse_nat holds (bpf_lxc.c:808-815),
+// and a create there stores daddr.s6_addr32[3] & 0xFFFF as that index
+// (:787-788).  A stage the ordering pass turned CT_ESTABLISHED hits the entry
+// an earlier header's create of the same key (so the same daddr) wrote: its
+// packet is reverse-NATed by that index.  One it turned CT_NEW (its entry
+// deleted earlier in the batch) is not: its packet is the one before the
+// stage.  ct0: the CT bytes before the pass.  One thread per header.
+__global__ __launch_bounds__(256) void k_ord_pkt6(CtaArgs A, const uint8_t *ct0, cfc_out out)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.n)
+        return;
+    const uint32_t c0 = ct0[i], c1 = A.ctb[i];
+    if (c0 == c1)
+        return;
+    const int st = A.mode == CFC_MODE_EGRESS ? 1 : 0;   // the ipv6_policy stage
+    const uint32_t n0 = (c0 >> (4 * st)) & 0xF, n1 = (c1 >> (4 * st)) & 0xF;
+    if (!(n0 & CFC_CT_DONE) || !(n1 & CFC_CT_DONE))
+        return;
+    const uint32_t r0 = n0 & CFC_CT_RES_MASK, r1 = n1 & CFC_CT_RES_MASK;
+    const bool est = r0 == CT_NEW && r1 == CT_ESTABLISHED;
+    const bool gone = r0 == CT_ESTABLISHED && r1 == CT_NEW;
+    if (!est && !gone)
+        return;
+    const uint32_t proto = A.mt[i] & 0xFF;
+    uint4 *ps = reinterpret_cast<uint4 *>(out.pkt_saddr) + i;
+    const LbRec6 *l = A.lbr ? reinterpret_cast<const LbRec6 *>(A.lbr) + i : nullptr;
+    if (est) {
+        // the stage's lookup daddr: the packet's (ingress), the service
+        // step's (egress: local delivery of the translated packet)
+        const uint4 da = l ? l->tda : ld16(reinterpret_cast<const uint4 *>(A.da) + i);
+        uint4 psa = *ps;
+        uint32_t ppt = out.pkt_ports[i];
+        lb6_rev_nat(A.T, da.w & 0xFFFF, proto, psa, ppt);
+        *ps = psa;
+        out.pkt_ports[i] = ppt;
+    } else {
+        *ps = l ? l->psa : ld16(reinterpret_cast<const uint4 *>(A.sa) + i);
+        out.pkt_ports[i] = l ? l->ppt : A.pt[i];
+    }
+}
+
 }  // namespace
+
+int ord_pkt6(const CtaArgs &A, const uint8_t *ct0, const cfc_out &out, hipStream_t s)
+{
+    if (!A.n || !out.pkt_saddr || !out.pkt_ports || !A.T.rnat6)
+        return 0;
+    hipLaunchKernelGGL(k_ord_pkt6, dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, s, A, ct0,
+                       out);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
 
 int ord_resolve(const CtaArgs &A, OrdArgs &O, OrdBufs &B, bool v6, uint32_t *changed,
                 hipStream_t s)

@@ -592,6 +592,58 @@ __device__ __forceinline__ void lb6_rev_nat(const DevTables &T, uint32_t index, 
         ppt = (ppt & 0xFFFF0000u) | port;   // reverse_map_l4_port: the sport
     psa = ld16(T.rnat6 + 2 * index);
 }
+// ---- the CT_SERVICE entry a header's lb4_local / lb6_local finds, in packet
+// order (svcorder.hip).  The classify launch looks the entry up as the batch
+// found it; the reference's first packet of a flow creates it with its own
+// selection (lb.h:711-716, 436-441) and ct_update4/6_slave re-selects it
+// when the backend is gone (:737-744, 462-468), so a later packet of the
+// same flow takes that slave whatever its own skb->hash.  An override word
+// per header carries the entry as the header finds it: SVO_SET | slave
+// (| SVO_LOOP: its lb_loopback); 0 = the table's entry.
+constexpr uint32_t SVO_SET = 1u << 31, SVO_LOOP = 1u << 29;
+struct SvcEntry {
+    bool exists;
+    uint32_t slave, loop;
+};
+__device__ __forceinline__ uint32_t svo_word(const SvcEntry &e)
+{
+    return SVO_SET | (e.loop ? SVO_LOOP : 0u) | (e.slave & 0xFFFF);
+}
+// lb4_local's effect on the entry for one header (gated as the egress path
+// gates it: a valid source, TCP / UDP / ICMP, a service): e as the header
+// finds it -> as it leaves it
+__device__ __forceinline__ void svc_next4(const DevTables &T, uint32_t da, uint32_t pt,
+                                          uint32_t proto, uint32_t hash, SvcEntry &e)
+{
+    const bool l4 = proto == 6 || proto == 17;
+    uint32_t kd = l4 ? pt >> 16 : 0u;
+    uint4 a, b, c, d;
+    if (!lb4_service(T, da, kd, 0, a, b))
+        return;
+    uint32_t slave = e.exists ? e.slave : hash % (a.w >> 16) + 1;   // lb4_select_slave
+    if (!lb4_get(T, da, kd, slave, c, d) && lb4_service(T, da, kd, slave, c, d))
+        slave = hash % (c.w >> 16) + 1;                                // ct_update4_slave
+    if (!e.exists)
+        e.loop = 0;   // (ct_create4 from lb4_local: the lookup's ct_state, loopback 0)
+    e.exists = true;
+    e.slave = slave;
+}
+__device__ __forceinline__ void svc_next6(const DevTables &T, uint4 da_raw, uint32_t pt,
+                                          uint32_t proto, uint32_t hash, SvcEntry &e)
+{
+    const bool l4 = proto == 6 || proto == 17;
+    uint32_t kd = l4 ? pt >> 16 : 0u;
+    uint4 b, tg, b2, tg2;
+    if (!lb6_service(T, da_raw, kd, 0, b, tg))
+        return;
+    uint32_t slave = e.exists ? e.slave : hash % (b.y >> 16) + 1;   // lb6_select_slave
+    if (!lb6_get(T, da_raw, kd, slave, b2, tg2) && lb6_service(T, da_raw, kd, slave, b2, tg2))
+        slave = hash % (b2.y >> 16) + 1;                               // ct_update6_slave
+    e.exists = true;
+    e.slave = slave;
+    e.loop = 0;
+}
+
 // the engine's skb->hash stand-in for IPv6 (notify.hip flow_hash, fold6)
 __device__ __forceinline__ uint32_t fold6w(uint4 a)
 {
@@ -603,6 +655,25 @@ __device__ __forceinline__ uint32_t fold6w(uint4 a)
 __device__ __forceinline__ uint32_t flow_hash6(uint4 sa, uint4 da, uint32_t pt, uint32_t proto)
 {
     return flow_hash4(fold6w(sa), fold6w(da), pt, proto);
+}
+
+__device__ __forceinline__ uint4 bswap4(uint4 v)
+{
+    return make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y),
+                      __builtin_bswap32(v.z), __builtin_bswap32(v.w));
+}
+
+// icmp6_handle (icmp6.h:390-412): neighbour solicitations and echo requests
+// to the router are answered, not classified.  It reads the type right after
+// the fixed header, so with extension headers it never triggers.
+__device__ __forceinline__ bool icmp6_punt(const DevTables &T, uint32_t proto,
+                                           uint32_t meta, uint32_t ports, uint4 da)
+{
+    if (proto != 58 || (meta & CFC_HF_EXTHDR))
+        return false;
+    const uint32_t type = ports & 0xFF;
+    return type == 135 || (type == 128 && da.x == T.router6[0] && da.y == T.router6[1] &&
+                           da.z == T.router6[2] && da.w == T.router6[3]);
 }
 
 // key of ct_acct[slot][dir] (k_ct_count), NONE for a miss

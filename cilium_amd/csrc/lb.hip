@@ -2,8 +2,10 @@
 // kernel: what handle_ipv4_from_lxc does to the tuple and the packet before
 // its conntrack lookup (bpf_lxc.c:476-492, lb.h:590-776) and, for a reply
 // of a load-balanced flow, right after it (bpf_lxc.c:565-576, lb4_rev_nat).
-// One thread per header; all lookups are against the tables as committed
-// (the batch's CT_SERVICE creates are folded in by cfc_ct_apply_v4).
+// One thread per header; all lookups are against the tables as committed,
+// but for the CT_SERVICE entry an earlier header of the batch created or
+// re-slaved (LbArgs.svo, svcorder.hip); the batch's CT_SERVICE writes are
+// folded in by cfc_ct_apply_v4.
 //
 // Per header it leaves, for the classify kernel:
 //   tda, tpt  the tuple's daddr and L4 word for the sending endpoint's CT
@@ -35,15 +37,21 @@ __global__ __launch_bounds__(256) void k_lb4_egress(DevTables T, LbArgs A)
     if (T.lb4 && (l4 || proto == 1) && lb4_service(T, da, kd, 0, a, b)) {
         const uint32_t hash = A.hash ? A.hash[i] : flow_hash4(sa, da, pt, proto);
         // lb4_local: ct_lookup4(CT_SERVICE) — the tuple as loaded, one probe
-        const CtProbe k = ct_probe<false>(proto, pt, CT_SERVICE, A.ct_owner);
-        const uint32_t slot = ct4_find(T, da, sa, k.z1, k.w1);
         uint32_t slave, loop = 0;
-        if (slot != NONE && T.ct4_lb) {   // the entry's ct_state (conntrack.h:235-239)
-            const uint4 lw = ld16(T.ct4_lb + slot);
-            slave = lw.y;
-            loop = (lw.x >> 16) & 1;
+        const uint32_t ov = A.svo ? A.svo[i] : 0u;
+        if (ov & SVO_SET) {   // the entry as an earlier header of the batch left it
+            slave = ov & 0xFFFF;
+            loop = (ov & SVO_LOOP) ? 1u : 0u;
         } else {
-            slave = slot != NONE ? 0u : hash % (a.w >> 16) + 1;   // lb4_select_slave
+            const CtProbe k = ct_probe<false>(proto, pt, CT_SERVICE, A.ct_owner);
+            const uint32_t slot = ct4_find(T, da, sa, k.z1, k.w1);
+            if (slot != NONE && T.ct4_lb) {   // the entry's ct_state (conntrack.h:235-239)
+                const uint4 lw = ld16(T.ct4_lb + slot);
+                slave = lw.y;
+                loop = (lw.x >> 16) & 1;
+            } else {
+                slave = slot != NONE ? 0u : hash % (a.w >> 16) + 1;   // lb4_select_slave
+            }
         }
         uint4 c, d;
         bool ok = lb4_get(T, da, kd, slave, c, d);   // lb4_lookup_slave

@@ -67,6 +67,10 @@ class Verdicts:
     # the packet as the programs left it (cfc_out.pkt_*): int32 (n, 3) saddr,
     # daddr, first L4 word (IPv4); (n, 9) saddr[4], daddr[4], L4 word (IPv6)
     pkt: "torch.Tensor | None" = None
+    # IPv6: the three arrays the library writes (saddr rows, daddr rows, L4
+    # words, 9n int32); pkt is assembled from them (cfc_ct_apply_v6 may
+    # rewrite them: ct_apply assembles pkt again)
+    pkt_raw: "torch.Tensor | None" = None
 
 
 def pack_v4(h, device="cuda"):
@@ -126,8 +130,25 @@ def hdr_struct(batch, n=None):
     return L.HdrV6(*args, _ptr(batch.hash)) if v6 else L.HdrV4(*args, _ptr(batch.hash))
 
 
+def _pkt6(raw):
+    n = raw.numel() // 9
+    return torch_cat([raw[:4 * n].view(n, 4), raw[4 * n:8 * n].view(n, 4),
+                      raw[8 * n:].view(n, 1)])
+
+
+def torch_cat(parts):
+    import torch
+    return torch.cat(parts, 1)
+
+
 def out_struct(out):
     pk = getattr(out, "pkt", None)
+    raw = getattr(out, "pkt_raw", None)
+    if raw is not None:   # IPv6: the library's own three arrays
+        n = raw.numel() // 9
+        return L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
+                     _ptr(out.ct), _ptr(out.notify), _ptr(raw[:4 * n]),
+                     _ptr(raw[4 * n:8 * n]), _ptr(raw[8 * n:]))
     cols = (None, None, None) if pk is None else (pk[:, 0], pk[:, 1], pk[:, 2])
     return L.Out(_ptr(out.verdict), _ptr(out.identity), _ptr(out.action),
                  _ptr(out.ct), _ptr(out.notify), *[_col_ptr(c) for c in cols])
@@ -365,8 +386,8 @@ class Datapath:
                                        ctypes.byref(o), mode, ep_lxc,
                                        self._stream(stream)), "classify v6")
         if pk is not None:
-            out.pkt = torch.cat([pk[:4 * n].view(n, 4), pk[4 * n:8 * n].view(n, 4),
-                                 pk[8 * n:].view(n, 1)], 1)
+            out.pkt_raw = pk
+            out.pkt = _pkt6(pk)
         return out
 
     def classify(self, batch, mode=L.MODE_INGRESS, ep_lxc=0, **kw) -> Verdicts:
@@ -387,6 +408,8 @@ class Datapath:
         fn = self.L.cfc_ct_apply_v6 if v6 else self.L.cfc_ct_apply_v4
         L.check(fn(self.h, ctypes.byref(hdr), ctypes.byref(o), mode, ep_lxc,
                    self._stream(stream)), "ct apply")
+        if v6 and out.pkt_raw is not None:   # (the packet outputs in packet order)
+            out.pkt = _pkt6(out.pkt_raw)
 
     def drop_notify(self, batch, out: Verdicts, mode=L.MODE_INGRESS,
                     ep_lxc=0, cap=None, stream=None, sync=True):

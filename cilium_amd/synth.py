@@ -951,7 +951,8 @@ def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1,
     return take(h, perm)
 
 
-def headers_c5_seq(t: Tables, flows: Headers, n, seed=5, new_frac=0.08, s=1.1):
+def headers_c5_seq(t: Tables, flows: Headers, n, seed=5, new_frac=0.08, s=1.1,
+                   return_new=False):
     """C5 stream with the intra-batch conntrack dependencies a real batch
     holds (the reference applies each packet's CT writes before the next
     packet's lookup, conntrack.h:221-285, 615-772): 92% Zipf(s) packets of
@@ -959,7 +960,7 @@ def headers_c5_seq(t: Tables, flows: Headers, n, seed=5, new_frac=0.08, s=1.1):
     lose their entry to their first packet, bpf_lxc.c:963-970, and find
     none after), and new flows with several packets in order — SYN, then
     ACK and data, an ICMP error about a UDP flow, a FIN or RST, a packet
-    after the close."""
+    after the close.  return_new: also the mask of the new flows' headers."""
     rng = np.random.default_rng(seed + 919)
     m = int(n * (1 - new_frac))
     old = take(flows, _zipf_ranks(rng, len(flows), m, s))
@@ -1010,7 +1011,11 @@ def headers_c5_seq(t: Tables, flows: Headers, n, seed=5, new_frac=0.08, s=1.1):
         pos.append(at[sel])
         at = at + rng.random(k) * 0.01
     h = concat(parts)
-    h = take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    order = np.argsort(np.concatenate(pos), kind="stable")
+    h = take(h, order)
+    if return_new:
+        isnew = np.concatenate([np.zeros(m, bool), np.ones(len(h) - m, bool)])[order]
+        return h.slice(0, n), isnew[:n]
     return h.slice(0, n)
 
 

@@ -1916,9 +1916,17 @@ static res_t lxc_egress_v6(cfo_t *o, uint16_t lxc, const uint8_t *saddr,
     /* after ct_create6 the v6 egress path sets monitor = TRACE_PAYLOAD_LEN
      * (bpf_lxc.c:248), so a new DNS flow is not captured at MTU */
     const uint32_t mon = res == CT_NEW ? TRACE_PAYLOAD_LEN : tl_mon[0];
-    if (res == CT_NEW)
+    if (res == CT_NEW) {
         tl_ct |= CTO_CREATE1;                       /* ct_create6, :237-249 */
-    else if (res >= CT_REPLY && hit->rev_nat_index)
+        /* (the destination's lookup after local delivery sees them: an
+         * endpoint's traffic to itself, whose tuple and its reverse
+         * coincide, finds its own entry, CT_REPLY) */
+        ctstate_t cs = {0, 0, 0, 0, 0, 0};
+        if (x.svc)
+            cs = (ctstate_t){x.rev_nat, x.slave, 0, 0, 0, 0};
+        tl_fresh.n = ct_create_entries(o, k2, 16, CT_EGRESS, len, o->seclabel[lxc], &cs,
+                                       tl_fresh.key, tl_fresh.ent);
+    } else if (res >= CT_REPLY && hit->rev_nat_index)
         lb6_rev_nat(o, hit->rev_nat_index, proto);  /* :255-266 */
     if (verdict > 0) {
         r.action = TC_ACT_REDIRECT;

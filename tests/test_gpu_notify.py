@@ -22,8 +22,10 @@ def torch():
     return torch
 
 
-def gpu_notify(torch, t, h, mode, ep_lxc=0, cap=None, chunks=1):
-    """-> per chunk: (notify words, records, header indices, total)."""
+def gpu_notify(torch, t, h, mode, ep_lxc=0, cap=None, chunks=1, seq=False):
+    """-> per chunk: (notify words, records, header indices, total).  seq:
+    each chunk classified and folded into the CT maps (cfc_ct_apply, which
+    rewrites the event words into the reference's packet order)."""
     dp = Datapath(0)
     load_tables(dp, t)
     b = pack(h)
@@ -32,7 +34,9 @@ def gpu_notify(torch, t, h, mode, ep_lxc=0, cap=None, chunks=1):
     res = []
     for a in range(0, max(n, 1), step):
         sub = b.slice(a, a + step)
-        out = dp.classify(sub, mode, ep_lxc, want_notify=True)
+        out = dp.classify(sub, mode, ep_lxc, want_notify=True, want_ct=seq)
+        if seq:
+            dp.ct_apply(sub, out, mode, ep_lxc)
         rec, idx, total = dp.drop_notify(sub, out, mode, ep_lxc, cap=cap)
         torch.cuda.synchronize()
         words = out.notify.cpu().numpy().view(np.uint32)
@@ -42,17 +46,17 @@ def gpu_notify(torch, t, h, mode, ep_lxc=0, cap=None, chunks=1):
     return res
 
 
-def oracle_notify(t, h, mode, ep_lxc=0):
+def oracle_notify(t, h, mode, ep_lxc=0, seq=False):
     o = O.Oracle(t)
     act, ver, ide, nt = o.classify(h, mode, ep_lxc, nthreads=8,
-                                   want_notify=True)
+                                   want_notify=True, apply_ct=seq)
     rec, idx = o.drop_notify(h, mode, ep_lxc, ver, ide, nt)
     return nt, rec, idx
 
 
-def check(torch, t, h, mode, ep_lxc=0, chunks=1):
-    nt, rec, idx = oracle_notify(t, h, mode, ep_lxc)
-    got = gpu_notify(torch, t, h, mode, ep_lxc, chunks=chunks)
+def check(torch, t, h, mode, ep_lxc=0, chunks=1, seq=False):
+    nt, rec, idx = oracle_notify(t, h, mode, ep_lxc, seq)
+    got = gpu_notify(torch, t, h, mode, ep_lxc, chunks=chunks, seq=seq)
     words = np.concatenate([g[1] for g in got])[:len(h)]
     np.testing.assert_array_equal(words, nt)
     grec = np.concatenate([g[2] for g in got])
@@ -70,7 +74,9 @@ NAMES = [n for n in G.names() if G.Golden(n).cb is not None]
 @pytest.mark.parametrize("name", NAMES)
 def test_golden_notify(torch, name):
     g = G.Golden(name)
-    rec = check(torch, g.tables, g.headers, g.mode, g.ep_lxc)
+    # (a fixture with CT state: classify + cfc_ct_apply, the reference's
+    # packet order, against the oracle's sequential run)
+    rec = check(torch, g.tables, g.headers, g.mode, g.ep_lxc, seq=g.ct_after is not None)
     want_idx, want = G.expected_drop_notify(g)
     assert len(rec) == len(want_idx)
     np.testing.assert_array_equal(rec["subtype"].astype(np.int64),

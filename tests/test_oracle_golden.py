@@ -77,8 +77,10 @@ def test_oracle_drop_notify_matches_reference(name):
     reference's send_drop_notify left in skb->cb[] for the same header."""
     g = G.Golden(name)
     o = O.Oracle(g.tables)
+    # (in the reference's packet order when the fixture has CT state: a
+    # stream may hold intra-batch CT dependencies)
     act, ver, ide, nt = o.classify(g.headers, g.mode, g.ep_lxc,
-                                   want_notify=True)
+                                   want_notify=True, apply_ct=g.ct_after is not None)
     rec, idx = o.drop_notify(g.headers, g.mode, g.ep_lxc, ver, ide, nt)
     want_idx, want = G.expected_drop_notify(g)
     np.testing.assert_array_equal(idx, want_idx)
@@ -327,7 +329,8 @@ def test_oracle_packets_match_reference(name):
     reference's records, so backend selection is the reference's."""
     g = G.Golden(name)
     o = O.Oracle(g.tables)
-    act, ver, ide, pkt = o.classify(g.headers, g.mode, g.ep_lxc, want_pkt=True)
+    act, ver, ide, pkt = o.classify(g.headers, g.mode, g.ep_lxc, want_pkt=True,
+                                    apply_ct=g.ct_after is not None)
     keep = (g.action != 2) & ~((g.action == 7) & (g.verdict > 0))
     np.testing.assert_array_equal(pkt[keep], g.pkt[keep])
 
@@ -338,7 +341,8 @@ def test_record_hash_is_the_batch_hash(name):
     test_oracle_events_match_reference leaves out otherwise)."""
     g = G.Golden(name)
     o = O.Oracle(g.tables)
-    act, ver, ide, words = o.classify(g.headers, g.mode, g.ep_lxc, want_notify=True)
+    act, ver, ide, words = o.classify(g.headers, g.mode, g.ep_lxc, want_notify=True,
+                                      apply_ct=g.ct_after is not None)
     rec, idx = o.events(g.headers, g.mode, g.ep_lxc, ver, ide, words)
     first = {}
     for j, i in enumerate(g.ev_hdr):
