@@ -212,7 +212,7 @@ struct cfc_ctx {
     uint64_t n_nat_hops = 0;
     // eviction at a CT map's capacity (ct_evict; CFC_OPT_CT_EVICT)
     bool ct_evict = true;
-    DevBuf evict_bm, evict_hist;
+    DevBuf evict_bm, evict_maps;
     uint64_t n_evicted = 0;
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
@@ -2377,13 +2377,23 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     *st = c->epoch->st;
     st->ct_apply_device = c->n_apply_dev;
     st->ct_apply_host = c->n_apply_host;
-    uint32_t dev_changed = 0;   // (the device applies' count, kept on the device)
-    if (c->ord_cnt.p)
-        (void)hipMemcpy(&dev_changed, (uint32_t *)c->ord_cnt.p + ORD_CHANGED, 4,
-                        hipMemcpyDeviceToHost);
-    st->ct_order_changed = (uint32_t)c->n_ord_changed + dev_changed;
-    st->nat_hops = (uint32_t)c->n_nat_hops;
-    st->ct_evicted = (uint32_t)c->n_evicted;
+    // (the device applies' count accumulates on the device: read after the
+    // last launch, on this context's device; folded into the 64-bit total
+    // and zeroed so the 32-bit device word never wraps)
+    if (c->ord_cnt.p && c->device != CFC_DEVICE_NONE) {
+        (void)hipSetDevice(c->device);
+        uint32_t dev_changed = 0;
+        if (c->last_done)
+            (void)hipEventSynchronize(c->last_done);
+        if (hipMemcpy(&dev_changed, (uint32_t *)c->ord_cnt.p + ORD_CHANGED, 4,
+                      hipMemcpyDeviceToHost) == hipSuccess && dev_changed &&
+            hipMemset((uint32_t *)c->ord_cnt.p + ORD_CHANGED, 0, 4) == hipSuccess)
+            c->n_ord_changed += dev_changed;
+    }
+    st->ct_order_changed = c->n_ord_changed;
+    st->nat_hops = c->n_nat_hops;
+    st->ct_evicted = c->n_evicted;
+    st->svc_ordered = c->n_svo;
     st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->ct4_host.size() + c->epoch->ct->ct6_host.size())
                             : 0u;
     return 0;
@@ -2868,73 +2878,90 @@ void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t 
 int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
               cfc_ct_gc_stats &st, hipStream_t s, const uint32_t *protect);
 
-// A batch whose creates would take an IPv4 CT map past max_entries: the
-// reference's LRU hash evicts its least recently used entries as the
-// inserts come (kernel order, per-CPU lists — not reproducible).  The device
-// frees room the same way a GC does, before the inserts: the map's entries
-// closest to their expiry (a histogram of lifetimes, then the GC pass up to
-// the second that covers `excess`; entries expiring in the same second go
-// together), never one this batch's lookups hit (they are the most recently
-// used).  0: done, -ENOSPC: not enough evictable entries (host walk).
-int ct_evict(cfc_ctx *c, Map *m, uint64_t excess, const uint32_t *hs, uint64_t nk, hipStream_t s)
+// A batch whose creates would take CT maps past max_entries (want[j]: the
+// entries map j would hold): the reference's LRU hash evicts its least
+// recently used entries as the inserts come (kernel order, per-CPU lists —
+// not reproducible).  Here, before the inserts, each overflowing map loses
+// exactly its excess: the entries no lookup of this batch hit (they are the
+// most recently used) with the earliest last refresh — lifetime minus the
+// timeout its state sets (conntrack.h:125-205: CT_CLOSE_TIMEOUT once both
+// closing bits are set, else CT_LIFETIME_TCP for a TCP entry past its SYN,
+// CT_SYN_TIMEOUT before, CT_LIFETIME_NONTCP otherwise) — ties broken by key
+// bytes.  Chosen on the host mirror (synced before), deleted there and
+// patched into the device table (patch_ct).  Every overflowing map is
+// checked before any is touched: 0 done, 1 a map has too few candidates
+// (nothing deleted: the host path), < 0 error.
+int ct_evict_maps(cfc_ctx *c, bool v6, const std::vector<Map *> &fmaps,
+                  const std::vector<uint64_t> &want, const uint32_t *hs, uint64_t nk,
+                  hipStream_t s)
 {
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
-    const uint64_t slots = G.ct4_host.size();
-    constexpr uint32_t NB = 1u << 16;
-    if (c->evict_bm.ensure(4 * ((slots + 31) / 32)) || c->evict_hist.ensure(4ull * NB))
-        return -ENOMEM;
-    uint32_t *bm = (uint32_t *)c->evict_bm.p, *hist = (uint32_t *)c->evict_hist.p;
-    const uint32_t mw = ct_owner_word((uint32_t)std::max(m->policy_lxc, 0), m->policy_lxc >= 0) |
-                        (m->ct_any ? 2u : 0u);
-    // lifetimes run from the past to now + CT_LIFETIME_TCP (21600 s)
-    const uint32_t base = c->now > NB - 21601 ? c->now - (NB - 21601) : 0u;
-    std::vector<uint32_t> h(NB);
-    if (hipMemsetAsync(bm, 0, c->evict_bm.bytes, s) != hipSuccess ||
-        hipMemsetAsync(hist, 0, 4ull * NB, s) != hipSuccess || ct_protect_hits(hs, nk, bm, s) ||
-        ct_evict_hist((const Ct4Slot *)G.ct4.p, (const CtTimer *)G.ct4_tm.p, slots, mw, bm, base,
-                      hist, NB, s) ||
-        hipMemcpyAsync(h.data(), hist, 4ull * NB, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    const uint64_t slots = v6 ? G.ct6_host.size() : G.ct4_host.size();
+    const uint64_t base6 = v6 ? G.ct4_host.size() : 0;   // (ct_dev_slot's IPv6 offset)
+    const size_t words = (slots + 31) / 32;
+    std::vector<uint32_t> bm(words);
+    if (c->evict_bm.ensure(4 * words) ||
+        hipMemsetAsync(c->evict_bm.p, 0, 4 * words, s) != hipSuccess ||
+        ct_protect_hits(hs, nk, (uint32_t *)c->evict_bm.p, s) ||
+        hipMemcpyAsync(bm.data(), c->evict_bm.p, 4 * words, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
-    // the TCP map's ICMP entries live on the host only (no lookup reaches
-    // them): theirs too
-    auto life_of = [](const std::string &v) {
-        uint32_t l = 0;
-        if (v.size() >= 36)
-            memcpy(&l, &v[32], 4);
-        return l;
+    using It = std::map<std::string, Map::Entry>::iterator;
+    struct Cand {
+        int64_t refresh;
+        It it;
     };
-    if (m->n_aux)
-        for (auto &kv : m->kv)
-            if (m->aux_key(kv.first)) {
-                const uint32_t l = life_of(kv.second.val);
-                h[l < base ? 0u : std::min(l - base, NB - 1)]++;
+    std::vector<std::vector<It>> del(fmaps.size());
+    for (size_t j = 0; j < fmaps.size(); j++) {
+        Map *m = fmaps[j];
+        if (want[j] <= m->max_entries)
+            continue;
+        const uint64_t excess = want[j] - m->max_entries;
+        const size_t al = v6 ? 16 : 4;
+        std::vector<Cand> cand;
+        cand.reserve(m->kv.size());
+        for (It it = m->kv.begin(); it != m->kv.end(); ++it) {
+            const int64_t ds = ct_dev_slot(E, m, it->first);
+            if (ds >= 0) {
+                const uint64_t sl = (uint64_t)ds - base6;
+                if (sl < slots && ((bm[sl >> 5] >> (sl & 31)) & 1u))
+                    continue;   // hit by this batch
             }
-    uint64_t cum = 0;
-    uint32_t b = 0;
-    while (b < NB && cum < excess)
-        cum += h[b++];
-    if (cum < excess)
-        return -ENOSPC;
-    cfc_ct_gc_filter f{};
-    f.flags = CFC_GC_REMOVE_EXPIRED;
-    f.time = base + b;   // lifetime < base + b: buckets [0, b)
-    cfc_ct_gc_stats st{};
-    if (int rc = ct_gc_dev(c, std::vector<Map *>{m}, f, st, s, bm))
-        return rc;
-    uint64_t aux = 0;
-    if (m->n_aux)
-        for (auto it = m->kv.begin(); it != m->kv.end();) {
-            if (m->aux_key(it->first) && life_of(it->second.val) < f.time) {
-                it = m->ct_erase_at(it, false);
-                aux++;
-            } else {
-                ++it;
-            }
+            const std::string &v = it->second.val;
+            if (v.size() < 38)
+                continue;
+            uint32_t life;
+            uint16_t bits;
+            memcpy(&life, &v[32], 4);
+            memcpy(&bits, &v[36], 2);
+            const bool tcp = (uint8_t)it->first[2 * al + 4] == 6;
+            const uint32_t to = (bits & 3) == 3 ? 10u      // CT_CLOSE_TIMEOUT
+                                : !tcp ? 60u                // CT_LIFETIME_NONTCP
+                                : (bits & 16) ? 21600u      // CT_LIFETIME_TCP
+                                              : 60u;        // CT_SYN_TIMEOUT
+            cand.push_back(Cand{(int64_t)life - to, it});
         }
-    c->n_evicted += st.device_deleted + st.log_deleted + aux;
-    return 0;
+        if (cand.size() < excess)
+            return 1;
+        auto lt = [](const Cand &a, const Cand &b) {
+            return a.refresh != b.refresh ? a.refresh < b.refresh : a.it->first < b.it->first;
+        };
+        std::nth_element(cand.begin(), cand.begin() + (excess - 1), cand.end(), lt);
+        for (uint64_t k = 0; k < excess; k++)
+            del[j].push_back(cand[k].it);
+    }
+    uint64_t n = 0;
+    for (size_t j = 0; j < fmaps.size(); j++)
+        for (It it : del[j]) {
+            // (an entry the device table does not hold needs no patch)
+            const bool dev = ct_dev_slot(E, fmaps[j], it->first) >= 0;
+            fmaps[j]->ct_erase_at(it, dev);
+            n++;
+        }
+    c->n_evicted += n;
+    return n ? commit_locked(c, s) : 0;
 }
 
 // cfc_ct_apply_v4/v6 on the device (ctapply.hip).  1: take the host path
@@ -3163,20 +3190,26 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     // map below max_entries; else the host path (which rebuilds).  First the
     // quick bound — each create its key and its related entry, a load
     // balancer's creates their reverse-NAT entry (counted hits add none) —
-    // and when that fails the exact count (k_cta_newkeys)
-    // (per map: the keys of its kind — TCP or ANY — once counted exactly,
-    // else all of them)
+    // and when that fails the exact count (k_cta_newkeys), per map when the
+    // family has no more than CTG_MAX_MAPS of them (else per map kind: TCP
+    // or ANY — an over-estimate for a map the batch does not write)
     uint64_t newk = 2 * (nreqA - hc[CTA_NFHIT]) + hc[CTA_NKX];
     uint64_t newk_kind[2] = {newk, newk};   // [TCP map, ANY map]
+    std::vector<Map *> fmaps;               // the family's CT maps
+    for (auto &kv : c->maps)
+        if (kv.second->role == (V6 ? ROLE_CT6 : ROLE_CT4))
+            fmaps.push_back(kv.second.get());
+    std::vector<uint64_t> newk_map;   // per fmaps[j], once counted exactly
+    auto map_want = [&](size_t j) -> uint64_t {
+        const Map *m = fmaps[j];
+        return m->kv.size() - m->gc_pending + claims + log_used +
+               (newk_map.empty() ? newk_kind[m->ct_any ? 1 : 0] : newk_map[j]);
+    };
     auto fits = [&](uint64_t nk) { return 4 * (used + ins + nk) <= 3 * slots; };
     auto maps_fit = [&]() {
-        for (auto &kv : c->maps) {
-            const Map *m = kv.second.get();
-            if (m->role == (V6 ? ROLE_CT6 : ROLE_CT4) &&
-                m->kv.size() - m->gc_pending + claims + log_used + newk_kind[m->ct_any ? 1 : 0] >
-                    m->max_entries)
+        for (size_t j = 0; j < fmaps.size(); j++)
+            if (map_want(j) > fmaps[j]->max_entries)
                 return false;
-        }
         return true;
     };
     auto room = [&](uint64_t nk) { return fits(nk) && maps_fit(); };
@@ -3187,11 +3220,35 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         A.rel_mask = 1;
         while (2ull * A.rel_mask + 1 <= 2 * cx_cap && A.rel_mask < (1u << 30))
             A.rel_mask = 2 * A.rel_mask + 1;
+        const size_t nm = fmaps.size();
+        if (nm && nm <= CTG_MAX_MAPS) {
+            std::vector<uint32_t> sel(2 * nm, 0);
+            for (size_t j = 0; j < nm; j++)
+                sel[j] = ct_owner_word((uint32_t)std::max(fmaps[j]->policy_lxc, 0),
+                                       fmaps[j]->policy_lxc >= 0) | (fmaps[j]->ct_any ? 2u : 0u);
+            if (c->evict_maps.ensure(8 * nm) ||
+                hipMemcpyAsync(c->evict_maps.p, sel.data(), 8 * nm, hipMemcpyHostToDevice, s) !=
+                    hipSuccess)
+                return -EIO;
+            A.emaps = (const uint32_t *)c->evict_maps.p;
+            A.n_emaps = (uint32_t)nm;
+            A.emcnt = (uint32_t *)c->evict_maps.p + nm;
+        }
         if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, exact, s))
             return -EIO;
         newk = exact[0];
         newk_kind[0] = exact[1];
         newk_kind[1] = exact[0] - exact[1];
+        if (A.emcnt) {
+            std::vector<uint32_t> cnt(nm);
+            if (hipMemcpyAsync(cnt.data(), A.emcnt, 4 * nm, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -EIO;
+            newk_map.assign(cnt.begin(), cnt.end());
+            A.emaps = A.emcnt = nullptr;
+            A.n_emaps = 0;
+        }
     }
     if (ok && !fits(newk) && may_grow) {
         // the batch outgrows the table but not its maps: rebuild the CT
@@ -3214,20 +3271,31 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             return ct_apply_dev(c, in, out, mode, ep_lxc, s, false, false);
         }
     }
-    if (!V6 && ok && fits(newk) && !maps_fit() && c->ct_evict) {
-        // an IPv4 map at capacity: evict on the device (ct_evict), then
-        // decide again
-        const uint64_t nk = lbm ? 4 * n : mode == CFC_MODE_EGRESS ? 2 * n : n;
-        for (auto &kv : c->maps) {
-            Map *m = kv.second.get();
-            if (m->role != ROLE_CT4)
-                continue;
-            const uint64_t want = m->kv.size() - m->gc_pending + claims + log_used +
-                                  newk_kind[m->ct_any ? 1 : 0];
-            if (want <= m->max_entries)
-                continue;
-            const int rc = ct_evict(c, m, want - m->max_entries, A.hs, nk, s);
-            if (rc && rc != -ENOSPC)
+    if (ok && fits(newk) && !maps_fit() && c->ct_evict && !newk_map.empty()) {
+        // a map at capacity (its exact new keys known): the device's own
+        // pending inserts and log entries into the host mirror first (then
+        // every map's size is its own), and if a map still overflows, evict
+        // (ct_evict_maps: every overflowing map or none)
+        if (claims || log_used || ins) {
+            std::vector<uint32_t> keep(CTA_NCNT);   // (ct_sync reuses the counters)
+            if (hipMemcpyAsync(keep.data(), A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -EIO;
+            if (int rc = ct_sync(c, s))
+                return rc;
+            if (hipMemcpyAsync(A.cnt, keep.data(), 4 * CTA_NCNT, hipMemcpyHostToDevice, s) !=
+                    hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -EIO;
+        }
+        if (!maps_fit()) {
+            std::vector<uint64_t> want(fmaps.size());
+            for (size_t j = 0; j < fmaps.size(); j++)
+                want[j] = map_want(j);
+            const uint64_t nk = lbm ? 4 * n : mode == CFC_MODE_EGRESS ? 2 * n : n;
+            const int rc = ct_evict_maps(c, V6, fmaps, want, A.hs, nk, s);
+            if (rc < 0)
                 return rc;
         }
         used = used_now();

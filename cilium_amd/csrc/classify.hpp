@@ -177,7 +177,7 @@ struct CtSyncRec6 {
 };
 // (NFHIT: requests that are counted hits; NKX: creates with a reverse-NAT entry)
 enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NSVC,
-       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NEWKT, CTA_NCNT };
+       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NEWKT, CTA_NLONG, CTA_NLCH, CTA_NCNT };
 struct CtaArgs {
     DevTables T;
     // addresses: one word per header (IPv4), four (IPv6, raw network order)
@@ -221,6 +221,11 @@ struct CtaArgs {
     uint64_t *reqA, *reqA2, *reqB, *reqB2, *cx, *cx2;
     uint32_t req_cap, cx_cap;
     uint32_t rel_mask;           // cta_newkeys: A.cx as a set of 2^k words, mask
+    // cta_newkeys per CT map (or null): the family's maps' selector words
+    // (owner word | 2 for an ANY map), the new keys each would take
+    const uint32_t *emaps;
+    uint32_t n_emaps;
+    uint32_t *emcnt;
     uint32_t cx_base;            // route: its ordered ops start here
     CtLog *log;                  // IPv4 applies
     CtLog6 *log6;                // IPv6 applies
@@ -400,14 +405,10 @@ struct CtGcArgs {
     const uint32_t *protect;      // slots never deleted (one bit each), or null
 };
 int ct_gc4(const CtGcArgs &A, hipStream_t s);
-// Eviction at a CT map's capacity (cfc_ct_apply, cfc_api.cpp ct_evict):
+// Eviction at a CT map's capacity (cfc_ct_apply, cfc_api.cpp ct_evict_maps):
 // the slots a batch's lookups hit (hs: nk hit-slot words, HS_NONE none) as
-// bits in bm, then a histogram of the lifetimes of map `mw`'s other
-// entries (the selector word of CtGcArgs.maps): hist[b] counts lifetime
-// base + b (clamped to [0, nb))
+// bits in bm (never evicted)
 int ct_protect_hits(const uint32_t *hs, uint64_t nk, uint32_t *bm, hipStream_t s);
-int ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm, uint64_t slots, uint32_t mw,
-                  const uint32_t *bm, uint32_t base, uint32_t *hist, uint32_t nb, hipStream_t s);
 // the pending TCP-map ICMP entries of the device applies (CtLog) filtered the
 // same way, kept in order of appearance: in[0, n) -> out; the kept count
 // into A.cnt[CTG_LOGKEPT]

@@ -777,6 +777,14 @@ __global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *
             }
             nk_new += nk;
             nk_tcp += o.is_tcp ? nk : 0u;
+            if (A.emcnt) {   // the map its keys go to: its owner's, by kind
+                const uint32_t sel = o.owner | (o.is_tcp ? 0u : 2u);
+                for (uint32_t j = 0; j < A.n_emaps; j++)
+                    if (A.emaps[j] == sel) {
+                        atomicAdd(&A.emcnt[j], nk);
+                        break;
+                    }
+            }
         }
     }
     wave_add(&A.cnt[CTA_NEWK], nk_new);
@@ -1064,10 +1072,16 @@ __device__ __forceinline__ void put_mon(const CtaArgs &A, uint32_t ord, uint32_t
         A.mon[2 * i + ord_st(ord)] = m == 0 ? 0 : m == 1 ? 1 : 2;
 }
 
-// ---- fold: one thread per slot of the sorted ordered list
+// ---- fold: one thread per slot of the sorted ordered list.  A slot with
+// more than FOLD_LONG ops (a hot flow of a Zipf batch whose closes or
+// deletes ordered it: millions of ops at C5) is left to k_cta_fold_long,
+// one workgroup per such slot: its run is listed (long, A.cnt[CTA_NLONG]).
+constexpr uint32_t FOLD_LONG = 512;
+template <bool V6, bool LB>
+__device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uint32_t r0);
 template <bool V6, bool LB>
 __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
-                                                  const uint32_t *pncx)
+                                                  const uint32_t *pncx, uint32_t *lng)
 {
     const uint32_t ncx = *pncx;   // (the deduplicated list's length)
     const uint32_t r0 = blockIdx.x * 256 + threadIdx.x;
@@ -1076,6 +1090,18 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     const uint32_t slot = (uint32_t)(cx[r0] >> A.ob);
     if (r0 > 0 && (uint32_t)(cx[r0 - 1] >> A.ob) == slot)
         return;
+    if (r0 + FOLD_LONG < ncx && (uint32_t)(cx[r0 + FOLD_LONG] >> A.ob) == slot) {
+        lng[atomicAdd(&A.cnt[CTA_NLONG], 1u)] = r0;   // (LongScratch.start)
+        return;
+    }
+    fold_run<V6, LB>(A, cx, ncx, r0);
+}
+
+// the slot's ops in order, one thread (the run starts at r0)
+template <bool V6, bool LB>
+__device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uint32_t r0)
+{
+    const uint32_t slot = (uint32_t)(cx[r0] >> A.ob);
     const uint64_t omask = (1ull << A.ob) - 1;
     const bool was_fresh = (A.ms[slot].x & MARK_FRESH) != 0;
     bool live = !was_fresh, created = false, deleted = false, reslaved = false;
@@ -1199,6 +1225,243 @@ __global__ __launch_bounds__(256) void k_cta_fold(CtaArgs A, const uint64_t *cx,
     A.ms[slot] = make_uint2(0, 0);
     if (A.sum)   // (replayed here: the finish leaves the slot alone)
         A.sum[slot] = 0;
+}
+
+// ---- the long runs (k_cta_fold's list).  When every op of a run is a
+// plain hit of a TCP or UDP entry the batch found (no create, delete,
+// related write or counted hit; no monitor lengths wanted) the final state
+// does not need the ops one by one: every such hit runs ct_update_timeout
+// (ACTION_CREATE directly or after clearing the closing bits; ACTION_CLOSE
+// before setting its bit, or as the close timeout once both are set), so
+// with one clock per batch
+//   flags_seen[dir] = the entry's | the OR of the direction's hits' flags,
+//   last_report[dir] = now iff the direction has hits and its interval had
+//     passed or its flags grew (the first report sets it, later ones keep it),
+//   seen_non_syn |= any TCP hit without the close bit,
+//   closing bits = the closes after the last ACTION_CREATE hit (which leaves
+//     none), or the entry's | every close when there is no such hit,
+//   lifetime = now + CT_CLOSE_TIMEOUT when both closing bits end set (the
+//     last hit was a close on a dead entry), else now + the lifetime of the
+//     entry's protocol and seen_non_syn (conntrack.h:125-205, 221-285).
+// A run is cut into chunks of FOLD_CH ops reduced by whole workgroups
+// (a C5 batch's hottest flow holds millions of ops); any other run is
+// replayed in order by one thread (fold_run).
+//
+// Scratch (the pre-dedup list's buffer, u32 words; R = runs' room, C =
+// chunks' room): [0, R) run starts (k_cta_fold), then per run RUN_W words,
+// then per chunk its run, the OR of its closes, the OR of its closes after
+// its last ACTION_CREATE.
+constexpr uint32_t FOLD_CH = 4096;
+enum { RW_R0, RW_END, RW_CBASE, RW_NCH, RW_BAD, RW_F0, RW_F1, RW_ANY, RW_NONSYN, RW_LASTC,
+       RW_LAST, RUN_W };
+struct LongScratch {
+    uint32_t *start, *run, *crun, *call, *cafter;
+    __device__ LongScratch(uint32_t *lng, uint32_t ncx)
+    {
+        const uint32_t R = ncx / FOLD_LONG + 1, C = ncx / FOLD_CH + R;
+        start = lng;
+        run = lng + R;
+        crun = run + RUN_W * R;
+        call = crun + C;
+        cafter = call + C;
+    }
+};
+// a plain hit, from the header's words alone (no tuple): false for any
+// other op; dir 0 rx (ingress), 1 tx
+template <bool V6, bool LB>
+__device__ __forceinline__ bool plain_hit(const CtaArgs &A, uint32_t ord, uint32_t &dir,
+                                          uint32_t &tfl, uint32_t &close, bool &create,
+                                          bool &nonsyn)
+{
+    const uint64_t i = ord_hdr(ord);
+    if (ord_sec(ord) != SEC_OP || i >= A.n)
+        return false;
+    const int st = ord_st(ord);
+    if (LB && (reinterpret_cast<const LbRecT<V6> *>(A.lbr)[i].fl & LBF_DROP))
+        return false;
+    const uint32_t cb = A.ctb[i], cs = (cb >> (4 * st)) & 0xF;
+    if (!(cs & CFC_CT_DONE))
+        return false;
+    const uint32_t b = cs & CFC_CT_RES_MASK;
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    if (b == 0 || (b == 1 && st == last && A.ver[i] == DROP_POLICY))
+        return false;   // (a create or nothing; a delete)
+    const uint32_t mt = A.mt[i], proto = mt & 0xFF;
+    if (proto != 6 && proto != 17)
+        return false;
+    const bool eg = A.mode == CFC_MODE_EGRESS && st == 0;
+    dir = eg ? 1u : 0u;
+    const bool cl = proto == 6 && (mt & CFC_HF_TCP_CLOSE);   // ACTION_CLOSE
+    tfl = (proto == 6 && A.tf) ? A.tf[i] : 0u;
+    close = cl ? (eg ? TX_CLOSING : RX_CLOSING) : 0u;
+    create = !cl;   // (TCP without RST/FIN, UDP: ACTION_CREATE)
+    nonsyn = proto == 6 && !cl;
+    return true;
+}
+// the long runs' ends and chunks
+template <bool V6, bool LB>
+__global__ __launch_bounds__(256) void k_cta_fold_plan(CtaArgs A, const uint64_t *cx,
+                                                       const uint32_t *pncx, uint32_t *lng)
+{
+    const uint32_t ncx = *pncx, nl = A.cnt[CTA_NLONG];
+    LongScratch L(lng, ncx);
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < nl; k += gridDim.x * 256) {
+        const uint32_t r0 = L.start[k];
+        const uint32_t slot = (uint32_t)(cx[r0] >> A.ob);
+        uint32_t lo = r0 + FOLD_LONG, hi = ncx;   // the first index past the slot
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if ((uint32_t)(cx[mid] >> A.ob) == slot)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        const uint32_t nch = (lo - r0 + FOLD_CH - 1) / FOLD_CH;
+        const uint32_t cb = atomicAdd(&A.cnt[CTA_NLCH], nch);
+        uint32_t *w = L.run + RUN_W * k;
+        w[RW_R0] = r0;
+        w[RW_END] = lo;
+        w[RW_CBASE] = cb;
+        w[RW_NCH] = nch;
+        for (int j = RW_BAD; j < RUN_W; j++)
+            w[j] = 0;
+        for (uint32_t j = 0; j < nch; j++)
+            L.crun[cb + j] = k;
+    }
+}
+// one workgroup per chunk: its ops' aggregates into its run's words
+template <bool V6, bool LB>
+__global__ __launch_bounds__(256) void k_cta_fold_agg(CtaArgs A, const uint64_t *cx,
+                                                      const uint32_t *pncx, uint32_t *lng)
+{
+    const uint32_t ncx = *pncx, nc = A.cnt[CTA_NLCH];
+    const uint64_t omask = (1ull << A.ob) - 1;
+    LongScratch L(lng, ncx);
+    __shared__ uint32_t s_bad, s_f[2], s_any, s_nonsyn, s_lastc, s_last, s_call, s_cafter;
+    for (uint32_t c = blockIdx.x; c < nc; c += gridDim.x) {
+        const uint32_t k = L.crun[c];
+        uint32_t *w = L.run + RUN_W * k;
+        const uint32_t a = w[RW_R0] + (c - w[RW_CBASE]) * FOLD_CH;
+        const uint32_t b = min(w[RW_END], a + FOLD_CH);
+        if (threadIdx.x == 0)
+            s_bad = s_f[0] = s_f[1] = s_any = s_nonsyn = s_lastc = s_last = s_call = s_cafter = 0;
+        __syncthreads();
+        uint32_t bad = 0, f[2] = {0, 0}, any = 0, ns = 0, lastc = 0, last = 0, call = 0;
+        for (uint32_t r = a + threadIdx.x; r < b; r += 256) {
+            uint32_t d, tfl, cl;
+            bool cr, nsy;
+            if (!plain_hit<V6, LB>(A, (uint32_t)(cx[r] & omask), d, tfl, cl, cr, nsy)) {
+                bad = 1;
+                continue;
+            }
+            f[d] |= tfl;
+            any |= 1u << d;
+            ns |= nsy ? 1u : 0u;
+            call |= cl;
+            if (cr)
+                lastc = max(lastc, r + 1);   // (+1: 0 = none)
+            last = max(last, r + 1);
+        }
+        if (bad)
+            atomicOr(&s_bad, 1u);
+        if (f[0])
+            atomicOr(&s_f[0], f[0]);
+        if (f[1])
+            atomicOr(&s_f[1], f[1]);
+        if (any)
+            atomicOr(&s_any, any);
+        if (ns)
+            atomicOr(&s_nonsyn, 1u);
+        if (call)
+            atomicOr(&s_call, call);
+        if (lastc)
+            atomicMax(&s_lastc, lastc);
+        if (last)
+            atomicMax(&s_last, last);
+        __syncthreads();
+        // the chunk's closes after its last ACTION_CREATE hit
+        const uint32_t from = s_lastc;
+        uint32_t after = 0;
+        if (!s_bad)
+            for (uint32_t r = max(a, from) + threadIdx.x; r < b; r += 256) {
+                uint32_t d, tfl, cl;
+                bool cr, nsy;
+                if (plain_hit<V6, LB>(A, (uint32_t)(cx[r] & omask), d, tfl, cl, cr, nsy))
+                    after |= cl;
+            }
+        if (after)
+            atomicOr(&s_cafter, after);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (s_bad)
+                atomicOr(&w[RW_BAD], 1u);
+            atomicOr(&w[RW_F0], s_f[0]);
+            atomicOr(&w[RW_F1], s_f[1]);
+            atomicOr(&w[RW_ANY], s_any);
+            atomicOr(&w[RW_NONSYN], s_nonsyn);
+            atomicMax(&w[RW_LASTC], s_lastc);
+            atomicMax(&w[RW_LAST], s_last);
+            L.call[c] = s_call;
+            L.cafter[c] = s_cafter;
+        }
+        __syncthreads();
+    }
+}
+// one thread per long run: its final state (or its replay)
+template <bool V6, bool LB>
+__global__ __launch_bounds__(256) void k_cta_fold_fin(CtaArgs A, const uint64_t *cx,
+                                                      const uint32_t *pncx, uint32_t *lng)
+{
+    const uint32_t ncx = *pncx, nl = A.cnt[CTA_NLONG];
+    const uint64_t omask = (1ull << A.ob) - 1;
+    LongScratch L(lng, ncx);
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < nl; k += gridDim.x * 256) {
+        const uint32_t *w = L.run + RUN_W * k;
+        const uint32_t r0 = w[RW_R0];
+        const uint32_t slot = (uint32_t)(cx[r0] >> A.ob);
+        if (w[RW_BAD] || A.mon || (A.ms[slot].x & MARK_FRESH)) {
+            fold_run<V6, LB>(A, cx, ncx, r0);
+            continue;
+        }
+        St e = load_state(A.tm, slot);
+        const uint32_t now = A.now;
+        for (int d = 0; d < 2; d++) {   // 0: rx (ingress), 1: tx
+            if (!((w[RW_ANY] >> d) & 1))
+                continue;
+            const uint32_t fl = d == 0 ? w[RW_F0] : w[RW_F1];
+            uint32_t &acc = d == 0 ? e.seen_rx : e.seen_tx;
+            uint32_t &lr = d == 0 ? e.last_rx : e.last_tx;
+            if (lr + CT_REPORT_INTERVAL < now || (fl & ~acc & 0xFFu))
+                lr = now;
+            acc = (acc | fl) & 0xFF;
+        }
+        if (w[RW_NONSYN])
+            e.bits |= SEEN_NON_SYN;
+        const uint32_t cbase = w[RW_CBASE], nch = w[RW_NCH], lastc = w[RW_LASTC];
+        uint32_t cb = 0, j0 = 0;
+        if (lastc) {   // the closes after the last ACTION_CREATE hit
+            j0 = (lastc - 1 - r0) / FOLD_CH;
+            cb = L.cafter[cbase + j0];
+            j0++;
+        } else {
+            cb = e.bits & 3u;
+        }
+        for (uint32_t j = j0; j < nch; j++)
+            cb |= L.call[cbase + j];
+        e.bits = (e.bits & ~3u) | cb;
+        const uint32_t ord = (uint32_t)(cx[w[RW_LAST] - 1] & omask);
+        const bool tcp = (A.mt[ord_hdr(ord)] & 0xFF) == 6;
+        const uint32_t life = !tcp ? CT_LIFETIME_NONTCP
+                              : (e.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
+        e.lifetime = now + ((cb & 3u) == 3u ? CT_CLOSE_TIMEOUT : life);
+        store_state(A.tm, slot, e);
+        CtInfo inf = A.info[slot];
+        inf.y |= CTI_UPDATED;
+        A.info[slot] = inf;
+        A.ms[slot] = make_uint2(0, 0);
+        if (A.sum)
+            A.sum[slot] = 0;
+    }
 }
 
 // ---- finish: the summaries of unordered slots.  Their hits are plain
@@ -1667,23 +1930,6 @@ __global__ __launch_bounds__(256) void k_ct_protect(const uint32_t *hs, uint64_t
     if (sl != HS_NONE)
         atomicOr(&bm[sl >> 5], 1u << (sl & 31));
 }
-__global__ __launch_bounds__(256) void k_ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm,
-                                                       uint64_t slots, uint32_t mw,
-                                                       const uint32_t *bm, uint32_t base,
-                                                       uint32_t *hist, uint32_t nb)
-{
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x; s < slots; s += stride) {
-        const uint32_t w = ct4[s].w;
-        if (!w || (w & 0xF000u) ||
-            ((w & 0xFFFF0800u) | ((w & 0xFF) != 6 ? 2u : 0u)) != mw ||
-            ((bm[s >> 5] >> (s & 31)) & 1u))
-            continue;
-        const uint32_t life = tm[s].lifetime;
-        const uint32_t b = life < base ? 0u : min(life - base, nb - 1);
-        atomicAdd(&hist[b], 1u);
-    }
-}
 
 unsigned blocks_for(uint64_t n, unsigned cap)
 {
@@ -1831,12 +2077,25 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
         if (hipcub::DeviceSelect::Flagged(A.sort_tmp, tb, sorted, keep, dst, nsel, (int)ncx, s) !=
             hipSuccess)
             return -EIO;
-        if (A.lbr)
-            hipLaunchKernelGGL((k_cta_fold<V6, true>), dim3((ncx + 255) / 256), dim3(256), 0, s, A,
-                               (const uint64_t *)dst, (const uint32_t *)nsel);
-        else
-            hipLaunchKernelGGL((k_cta_fold<V6, false>), dim3((ncx + 255) / 256), dim3(256), 0, s,
-                               A, (const uint64_t *)dst, (const uint32_t *)nsel);
+        // (the pre-dedup list is free now: the long runs' list)
+        uint32_t *lng = reinterpret_cast<uint32_t *>(sorted);
+        // (the long runs: plan, chunk reductions, final states; fixed
+        // grids over device counts)
+#define CFC_FOLD(LBV)                                                                          \
+        hipLaunchKernelGGL((k_cta_fold<V6, LBV>), dim3((ncx + 255) / 256), dim3(256), 0, s, A, \
+                           (const uint64_t *)dst, (const uint32_t *)nsel, lng);                 \
+        hipLaunchKernelGGL((k_cta_fold_plan<V6, LBV>), dim3(16), dim3(256), 0, s, A,            \
+                           (const uint64_t *)dst, (const uint32_t *)nsel, lng);                 \
+        hipLaunchKernelGGL((k_cta_fold_agg<V6, LBV>), dim3(1024), dim3(256), 0, s, A,          \
+                           (const uint64_t *)dst, (const uint32_t *)nsel, lng);                 \
+        hipLaunchKernelGGL((k_cta_fold_fin<V6, LBV>), dim3(16), dim3(256), 0, s, A,             \
+                           (const uint64_t *)dst, (const uint32_t *)nsel, lng)
+        if (A.lbr) {
+            CFC_FOLD(true);
+        } else {
+            CFC_FOLD(false);
+        }
+#undef CFC_FOLD
     }
     // (a sweep of the whole table: a list of the touched slots, A/B'd,
     // took 0.43 ms against the sweep's 0.30 — its random loads cost more
@@ -1853,14 +2112,6 @@ int ct_protect_hits(const uint32_t *hs, uint64_t nk, uint32_t *bm, hipStream_t s
     if (nk)
         hipLaunchKernelGGL(k_ct_protect, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, hs,
                            nk, bm);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
-}
-
-int ct_evict_hist(const Ct4Slot *ct4, const CtTimer *tm, uint64_t slots, uint32_t mw,
-                  const uint32_t *bm, uint32_t base, uint32_t *hist, uint32_t nb, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_ct_evict_hist, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4, tm,
-                       slots, mw, bm, base, hist, nb);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

@@ -738,6 +738,22 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
             ((uintptr_t)A.ck1 & 15) == 0 && ((uintptr_t)A.ck2 & 15) == 0;
     if (!filter(B.creates_hint))
         return -ENOMEM;
+    // from the first mark on, the per-slot state (delete bits, mixed bits,
+    // first-delete orders) must be zero again when this returns, on every
+    // path: the next apply reads it
+    struct Clear {
+        const OrdArgs &O;
+        hipStream_t s;
+        bool ok = true, need = true;
+        ~Clear()
+        {
+            if (need)
+                ok = hipMemsetAsync(O.delbm, 0, O.bm_bytes, s) == hipSuccess &&
+                     hipMemsetAsync(O.mixbm, 0, O.bm_bytes, s) == hipSuccess &&
+                     hipMemsetD32Async((hipDeviceptr_t)O.dfirst, 0xFFFFFFFFu, O.slots, s) ==
+                         hipSuccess;
+        }
+    } clear{O, s};
     ORD_LAUNCH(k_ord_mark, g, A, O);
     if (!rd())
         return -EIO;
@@ -754,6 +770,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     const uint32_t ncr = hc[ORD_NCREATE];
     B.creates_hint = ncr;
     O.ndel = hc[ORD_NDEL];
+    clear.need = O.ndel != 0;   // (mark sets per-slot state only for deletes)
     if (!ncr)
         O.cbloom = nullptr;
     if (O.ndel)
@@ -844,12 +861,8 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     if (np)
         hipLaunchKernelGGL(k_ord_write, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, A, O,
                            (uint32_t)np);
-    if (O.ndel &&   // the per-slot state cleared for the next batch
-        (hipMemsetAsync(O.delbm, 0, O.bm_bytes, s) != hipSuccess ||
-         hipMemsetAsync(O.mixbm, 0, O.bm_bytes, s) != hipSuccess ||
-         hipMemsetD32Async((hipDeviceptr_t)O.dfirst, 0xFFFFFFFFu, O.slots, s) != hipSuccess))
-        return -EIO;
 #undef ORD_LAUNCH
+    // (the per-slot state is cleared for the next batch as `clear` goes)
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

@@ -533,7 +533,7 @@ class Datapath:
     def stats(self):
         st = L.Stats()
         L.check(self.L.cfc_get_stats(self.h, ctypes.byref(st)), "stats")
-        return {f: getattr(st, f) for f, _ in L.Stats._fields_}
+        return {f: getattr(st, f) for f, _ in L.Stats._fields_ if f != "pad0"}
 
 
 def host_only():

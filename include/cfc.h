@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 11
+#define CFC_ABI_VERSION 12
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -602,18 +602,23 @@ typedef struct {
     uint32_t ct6_entries;
     uint32_t ct_apply_device;   /* cfc_ct_apply_* calls run on the device */
     uint32_t ct_apply_host;     /* ... and on the host */
-    /* CT stages whose result the packet order changed from the batch-start
-     * lookup (cfc_ct_apply: a later packet of a flow the batch created,
-     * a packet after a delete), since the context opened */
-    uint32_t ct_order_changed;
     /* CT slots of the device tables (both families) */
     uint32_t ct_slots;
+    uint32_t pad0;
+    /* CT stages whose result the packet order changed from the batch-start
+     * lookup (cfc_ct_apply: a later packet of a flow the batch created,
+     * a packet after a delete), since the context opened (ABI 12: 64-bit,
+     * read after the last call on any stream has finished) */
+    uint64_t ct_order_changed;
     /* headers that took a NAT46 / NAT64 hop (cfc_classify_*), since the
      * context opened */
-    uint32_t nat_hops;
-    /* CT entries deleted to make room at a map's max_entries on the device
-     * (CFC_OPT_CT_EVICT), since the context opened */
-    uint32_t ct_evicted;
+    uint64_t nat_hops;
+    /* CT entries deleted to make room at a map's max_entries before a device
+     * apply (CFC_OPT_CT_EVICT), since the context opened */
+    uint64_t ct_evicted;
+    /* headers whose service step found the CT_SERVICE entry an earlier
+     * header of the same batch created or re-selected (cfc_classify_*) */
+    uint64_t svc_ordered;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

@@ -1,14 +1,17 @@
-"""A CT map at capacity stays on the device (CFC_OPT_CT_EVICT, cfc_api.cpp
-ct_evict): per-endpoint CT maps of 4096 entries (CT_MAP_SIZE_TCP/ANY,
-lxc_config.h:44-45) nearly full, then a batch with thousands of new flows.
-The reference's LRU hash evicts least-recently-used entries as the inserts
-come; the engine deletes, before the inserts, the map's entries closest to
-expiry that the batch did not hit.  Checked: the apply stays
-on the device, no map passes max_entries, every verdict and CT byte is the
-oracle's (the batch's results do not depend on the evicted entries), every
-surviving entry is byte-equal to the oracle's (which has no capacity), and
-the evicted ones are exactly those with the earliest lifetimes that no
-header of the batch hit.  Run on an MI355X: pytest -m gpu."""
+"""CT maps at capacity stay on the device (CFC_OPT_CT_EVICT, cfc_api.cpp
+ct_evict_maps), IPv4 and IPv6: per-endpoint CT maps of 4096 entries
+(CT_MAP_SIZE_TCP/ANY, lxc_config.h:44-45) nearly full, the global maps
+nearly full too but written by no header of the batch, then a batch with
+hundreds of new flows.  The reference's LRU hash evicts least-recently-used
+entries as the inserts come; the engine deletes, before the inserts, each
+overflowing map's excess — the entries the batch did not hit with the
+earliest last refresh (lifetime minus the timeout of the entry's state),
+ties by key bytes.  Checked: the apply stays on the device,
+no map passes max_entries, a map the batch does not write loses nothing,
+every verdict and CT byte is the oracle's (the batch's results do not
+depend on the evicted entries), every surviving entry is byte-equal to the
+oracle's (which has no capacity), and the evicted ones are exactly that
+rule's.  Run on an MI355X: pytest -m gpu."""
 import numpy as np
 import pytest
 
@@ -27,14 +30,26 @@ def torch():
     return torch
 
 
-def full_tables(n_flows=2900, seed=5):
-    t, flows = S.config_c5(seed, n_flows=n_flows, n_prefixes=5000, n_policy=500, now=1000)
+def full_tables(fam, n_flows=2900, seed=5):
+    """the endpoint's flows in its own maps, with spread lifetimes and
+    states (SYN-only, established, closing); the same entries again in the
+    global maps (no lookup of the batch reaches them: the endpoint has its
+    own maps)"""
+    cfg = S.config_c5 if fam == 4 else S.config_c5_v6
+    t, flows = cfg(seed, n_flows=n_flows, n_prefixes=5000, n_policy=500, now=1000)
     rng = np.random.default_rng(seed + 3)
     ct = t.ct
-    ct["lxc"] = S.EP_LXC_ID                       # the endpoint's own CT maps
+    ct["lxc"] = S.EP_LXC_ID
     life = (1000 + rng.integers(30, 3000, size=len(ct))).astype(np.uint32)
     ct["entry"][:, 32:36] = life.view(np.uint8).reshape(-1, 4)
-    t.ct = ct
+    st = rng.random(len(ct))
+    bits = ct["entry"][:, 36].copy()
+    bits = np.where(st < 0.4, bits | 16, bits)           # seen_non_syn
+    bits = np.where(st > 0.95, bits | 3, bits)           # both closing bits
+    ct["entry"][:, 36] = bits
+    glob = ct.copy()
+    glob["lxc"] = -1
+    t.ct = np.concatenate([ct, glob])
     return t, flows
 
 
@@ -47,21 +62,37 @@ def load_capped(dp, t):
     fds = open_ct_maps(dp, [-1, S.EP_LXC_ID], max_entries=CAP)
     for (fam, lxc, any_map), fd in fds.items():
         sel = ct[(ct["family"] == fam) & (ct["lxc"] == lxc) & (ct["any"] == any_map)]
+        ks = 14 if fam == 1 else 38
         if len(sel):
-            dp.update_batch(fd, np.ascontiguousarray(sel["tuple"][:, :14]),
+            dp.update_batch(fd, np.ascontiguousarray(sel["tuple"][:, :ks]),
                             np.ascontiguousarray(sel["entry"]))
     dp.ct_fds = fds
     dp.commit()
     return pms
 
 
-def test_full_endpoint_map_stays_on_device(torch):
+def refresh(r, ks):
+    """lifetime minus the timeout of the entry's state (conntrack.h:125-205)"""
+    e = r[44:100]
+    life = int(e[32:36].view("<u4")[0])
+    bits = int(e[36]) | int(e[37]) << 8
+    tcp = r[4 + ks - 2] == 6
+    to = 10 if (bits & 3) == 3 else (21600 if (bits & 16) else 60) if tcp else 60
+    return life - to
+
+
+@pytest.mark.parametrize("fam", [4, 6])
+def test_full_endpoint_maps_stay_on_device(torch, fam):
     from cilium_amd.datapath import Datapath, pack
     from cilium_amd.loader import ct_rows
-    t, flows = full_tables()
-    n_tcp = int(((t.ct["any"] == 0)).sum())
+    t, flows = full_tables(fam)
+    ks = 14 if fam == 4 else 38
+    famb = 1 if fam == 4 else 2
+    mine = (t.ct["lxc"] == S.EP_LXC_ID) & (t.ct["family"] == famb)
+    n_tcp = int((mine & (t.ct["any"] == 0)).sum())
     assert CAP - 200 < n_tcp <= CAP, n_tcp          # the TCP map nearly full
-    h = S.headers_c5(t, flows, 8000, seed=9, new_frac=0.1)
+    h = (S.headers_c5(t, flows, 8000, seed=9, new_frac=0.1) if fam == 4 else
+         S.headers_c5_v6(t, flows, 8000, seed=9, new_frac=0.1))
     dp = Datapath(0)
     load_capped(dp, t)
     dp.set_clock(1003)
@@ -92,16 +123,24 @@ def test_full_endpoint_map_stays_on_device(torch):
         assert key(r) in wmap
         np.testing.assert_array_equal(r, wmap[key(r)])
     kept = {key(r) for r in rows}
-    gone = [r for r in want if key(r) not in kept]
-    assert 0 < len(gone) <= st["ct_evicted"], (len(gone), st)
-    # the evicted: entries the batch did not touch (unchanged since before
-    # it), with the map's earliest lifetimes
-    life = lambda r: int(r[76:80].view("<u4")[0])  # noqa: E731  (ct_entry @32)
-    untouched = {key(r) for r in before if key(r) in wmap and
-                 np.array_equal(r, wmap[key(r)])}
-    assert all(key(r) in untouched for r in gone)
-    for m in (0, 1):   # per map (TCP, ANY): every evicted lifetime < every kept untouched one
-        g = [life(r) for r in gone if r[2] == m]
-        k = [life(r) for r in want if r[2] == m and key(r) in untouched and key(r) in kept]
-        if g and k:
-            assert max(g) < min(k), (m, max(g), min(k))
+    bmap = {key(r): r for r in before}
+    total = 0
+    for owner in (0, S.EP_LXC_ID + 1):          # global maps, the endpoint's
+        for m in (0, 1):                         # TCP, ANY
+            sel = lambda rs: [r for r in rs if r[3] == famb and r[2] == m and  # noqa: E731
+                              int(r[0]) | int(r[1]) << 8 == owner]
+            b_m, w_m = sel(before), sel(want)
+            created = len({key(r) for r in w_m} - {key(r) for r in b_m})
+            excess = max(0, len(b_m) + created - CAP)
+            gone = sorted(key(r) for r in w_m if key(r) not in kept)
+            # the rule: untouched entries (not hit: unchanged), earliest
+            # refresh first, ties by key bytes
+            cand = [r for r in w_m if key(r) in bmap and np.array_equal(r, bmap[key(r)])]
+            cand.sort(key=lambda r: (refresh(r, ks), r[4:4 + ks].tobytes()))
+            expect = sorted(key(r) for r in cand[:excess])
+            assert len(gone) == excess, (owner, m, len(gone), excess)
+            assert gone == expect, (owner, m)
+            if owner == 0:
+                assert excess == 0       # the batch writes no global map
+            total += excess
+    assert total == st["ct_evicted"], (total, st)
