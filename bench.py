@@ -63,6 +63,28 @@ def mix_ceiling(p):
     return pts[-1][1] if p > pts[-1][0] else pts[0][1]
 
 
+def stream_ceiling(probes_per_item):
+    """The chip's measured rate (G items/s) of a kernel whose misses are a
+    coalesced stream: per item (a lane-iteration) P random 16-byte probes of
+    a 2 MiB (L2-resident) table, 16 bytes read one iteration ahead from a
+    4 GiB input stream and 16 bytes written (scripts/ubench_mix.hip stream
+    mode, profiles/r05/ubench_stream.jsonl), interpolated in P; None without
+    the measurement."""
+    try:
+        pts = sorted((r["probes_per_item"], r["gitems_per_s"]) for r in
+                     map(json.loads, open(os.path.join(ROOT, "profiles", "r05",
+                                                       "ubench_stream.jsonl"))))
+    except (OSError, ValueError):
+        return None
+    for (p0, r0), (p1, r1) in zip(pts, pts[1:]):
+        if p0 <= probes_per_item <= p1:
+            # (time per item is what adds up linearly in P)
+            t = 1 / r0 + (1 / r1 - 1 / r0) * (probes_per_item - p0) / max(p1 - p0, 1e-9)
+            return 1 / t
+    p_last, r_last = pts[-1]
+    return r_last * p_last / probes_per_item if probes_per_item > p_last else pts[0][1]
+
+
 def ceiling_for(ws_bytes, rows):
     """(table MiB, G loads/s) of the smallest measured table holding ws_bytes."""
     for mib, rate in rows:
@@ -88,7 +110,7 @@ def pmc_entry(workload, mode, layout, kernels, variant="lookup"):
     return None
 
 
-def kernel_roofline(k, hn, ms, ws, pk, rows):
+def kernel_roofline(k, hn, ms, ws, pk, rows, stream_bph=None):
     """One kernel's roofline entry: the launch's L2 hits priced at the L2
     ceiling, its misses (TCC_MISS: the header stream, the output stores, and
     table lines past L2) at the row of the memory that serves them — the
@@ -116,12 +138,30 @@ def kernel_roofline(k, hn, ms, ws, pk, rows):
     # Cache serves keeps the additive model
     p = hits / req if req else 1.0
     mixr = mix_ceiling(p) if miss_mib >= 4096 else None
-    t_ideal = req / (mixr * 1e9) if mixr else t_add
+    t_mix = req / (mixr * 1e9) if mixr else t_add
+    t_ideal = t_mix
+    # the kernel's own miss type: its header stream and output stores are
+    # coalesced and read an iteration ahead (the stream model: items of 32
+    # stream bytes, the L2 hits spread over them); the misses beyond the
+    # stream's lines (a table past L2, C5's CT slots) at the random row
+    st = None
+    if stream_bph:
+        items = hn * stream_bph / 32.0
+        rate = stream_ceiling(hits / items) if items else None
+        if rate:
+            lines = hn * stream_bph / 128.0
+            rand = max(0.0, miss - lines)
+            t_ideal = items / (rate * 1e9) + rand / (miss_peak * 1e9)
+            st = {"items_per_launch": items, "probes_per_item": round(hits / items, 3),
+                  "stream_ceiling_gitems_s": round(rate, 3),
+                  "stream_lines_per_launch": lines, "random_misses_per_launch": rand}
     d.update({"l2_requests_per_launch": req,
               "l2_requests_per_header": round(req / hn, 3),
               "l2_hits_per_launch": hits, "l2_misses_per_launch": miss,
               "hit_fraction": round(p, 4),
               "mix_ceiling_greq_s": round(mixr, 1) if mixr else None,
+              "stream_model": st,
+              "frac_random_mix": round(t_mix / (ms * 1e-3), 4),
               "hit_ceiling_greq_s": l2_peak,
               "miss_ceiling_greq_s": miss_peak, "miss_ceiling_table_mib": miss_mib,
               "achieved_greq_s": round(req / (ms * 1e-3) / 1e9, 1),
@@ -485,7 +525,7 @@ def main():
     req_tot = ideal_s = ideal_u = traffic = 0.0
     for k, hn, ms, ws in kernels:
         d, t_ideal, t_unif = kernel_roofline(k, hn, ms, ws, pe["kernels"][k] if pe else None,
-                                             rows)
+                                             rows, STREAM_V6 if k.endswith("v6") else STREAM_V4)
         if pe:
             req_tot += d["l2_requests_per_launch"]
             ideal_s += t_ideal

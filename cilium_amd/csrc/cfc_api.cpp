@@ -212,7 +212,7 @@ struct cfc_ctx {
     uint64_t n_nat_hops = 0;
     // eviction at a CT map's capacity (ct_evict; CFC_OPT_CT_EVICT)
     bool ct_evict = true;
-    DevBuf evict_bm, evict_maps;
+    DevBuf evict_bm, evict_maps, evict_rel;
     uint64_t n_evicted = 0;
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
@@ -3200,6 +3200,9 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         if (kv.second->role == (V6 ? ROLE_CT6 : ROLE_CT4))
             fmaps.push_back(kv.second.get());
     std::vector<uint64_t> newk_map;   // per fmaps[j], once counted exactly
+    // the TCP maps' related entries among those keys (saddr, daddr, ct word:
+    // three uint4 each), which only the host maps can tell present or not
+    std::vector<uint4> tcp_rel;
     auto map_want = [&](size_t j) -> uint64_t {
         const Map *m = fmaps[j];
         return m->kv.size() - m->gc_pending + claims + log_used +
@@ -3222,17 +3225,20 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             A.rel_mask = 2 * A.rel_mask + 1;
         const size_t nm = fmaps.size();
         if (nm && nm <= CTG_MAX_MAPS) {
-            std::vector<uint32_t> sel(2 * nm, 0);
+            std::vector<uint32_t> sel(2 * nm + 1, 0);
             for (size_t j = 0; j < nm; j++)
                 sel[j] = ct_owner_word((uint32_t)std::max(fmaps[j]->policy_lxc, 0),
                                        fmaps[j]->policy_lxc >= 0) | (fmaps[j]->ct_any ? 2u : 0u);
-            if (c->evict_maps.ensure(8 * nm) ||
-                hipMemcpyAsync(c->evict_maps.p, sel.data(), 8 * nm, hipMemcpyHostToDevice, s) !=
-                    hipSuccess)
+            const uint32_t rcap = (uint32_t)std::min<uint64_t>(nreqA, 1u << 22);
+            if (c->evict_maps.ensure(4 * (2 * nm + 1)) || c->evict_rel.ensure(48ull * rcap + 48) ||
+                hipMemcpyAsync(c->evict_maps.p, sel.data(), 4 * sel.size(), hipMemcpyHostToDevice,
+                               s) != hipSuccess)
                 return -EIO;
             A.emaps = (const uint32_t *)c->evict_maps.p;
             A.n_emaps = (uint32_t)nm;
             A.emcnt = (uint32_t *)c->evict_maps.p + nm;
+            A.emrel = (uint4 *)c->evict_rel.p;
+            A.emrel_cap = rcap;
         }
         if (cta_newkeys(A, V6, (uint32_t)nreqA, &presorted, exact, s))
             return -EIO;
@@ -3240,13 +3246,22 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         newk_kind[0] = exact[1];
         newk_kind[1] = exact[0] - exact[1];
         if (A.emcnt) {
-            std::vector<uint32_t> cnt(nm);
-            if (hipMemcpyAsync(cnt.data(), A.emcnt, 4 * nm, hipMemcpyDeviceToHost, s) !=
+            std::vector<uint32_t> cnt(nm + 1);
+            if (hipMemcpyAsync(cnt.data(), A.emcnt, 4 * (nm + 1), hipMemcpyDeviceToHost, s) !=
                     hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
                 return -EIO;
-            newk_map.assign(cnt.begin(), cnt.end());
+            newk_map.assign(cnt.begin(), cnt.begin() + nm);
+            if (cnt[nm] <= A.emrel_cap) {   // (else the count stays an upper bound)
+                tcp_rel.resize(3ull * cnt[nm]);
+                if (cnt[nm] &&
+                    (hipMemcpyAsync(tcp_rel.data(), A.emrel, 16 * tcp_rel.size(),
+                                    hipMemcpyDeviceToHost, s) != hipSuccess ||
+                     hipStreamSynchronize(s) != hipSuccess))
+                    return -EIO;
+            }
             A.emaps = A.emcnt = nullptr;
+            A.emrel = nullptr;
             A.n_emaps = 0;
         }
     }
@@ -3289,6 +3304,27 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
                 hipStreamSynchronize(s) != hipSuccess)
                 return -EIO;
         }
+        // a TCP map's related entry the batch's first create of its address
+        // pair writes is a new key only when the map lacks it
+        for (size_t q = 0; q + 2 < tcp_rel.size(); q += 3) {
+            const uint32_t w = tcp_rel[q + 2].x;
+            const size_t al = V6 ? 16 : 4;
+            char k[38];
+            const uint32_t z = 0;
+            memcpy(k, &tcp_rel[q], al);
+            memcpy(k + al, &tcp_rel[q + 1], al);
+            memcpy(k + 2 * al, &z, 4);
+            k[2 * al + 4] = (char)(w & 0xFF);
+            k[2 * al + 5] = (char)((w >> 8) & 7);
+            auto mit = G.ct_maps.find(ct_map_key(V6 ? 6 : 4, w & ~0x7FFu, 0));
+            if (mit == G.ct_maps.end())
+                continue;
+            for (size_t j = 0; j < fmaps.size(); j++)
+                if (fmaps[j] == mit->second && newk_map[j] &&
+                    fmaps[j]->kv.count(std::string(k, 2 * al + 6)))
+                    newk_map[j]--;
+        }
+        tcp_rel.clear();
         if (!maps_fit()) {
             std::vector<uint64_t> want(fmaps.size());
             for (size_t j = 0; j < fmaps.size(); j++)

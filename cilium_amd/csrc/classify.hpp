@@ -225,7 +225,12 @@ struct CtaArgs {
     // (owner word | 2 for an ANY map), the new keys each would take
     const uint32_t *emaps;
     uint32_t n_emaps;
-    uint32_t *emcnt;
+    uint32_t *emcnt;   // per map; emcnt[n_emaps]: the records in emrel
+    // (eviction) the TCP maps' related-entry keys the batch may add, three
+    // words each (saddr, daddr, {ct word}): those maps' related entries are
+    // host-side only, so the host checks which its map already holds
+    uint4 *emrel;
+    uint32_t emrel_cap;
     uint32_t cx_base;            // route: its ordered ops start here
     CtLog *log;                  // IPv4 applies
     CtLog6 *log6;                // IPv6 applies

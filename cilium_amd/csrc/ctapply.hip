@@ -772,8 +772,23 @@ __global__ __launch_bounds__(256) void k_cta_newkeys(CtaArgs A, const uint64_t *
                 // keys' 64-bit fingerprints in A.cx) and only when the table
                 // lacks it (an ANY map's; a TCP map's is host-side only)
                 const uint32_t rw = ct_word(icmp_proto<V6>(), ((o.w2 >> 8) & 7) | 2u, o.owner);
-                if (o.is_tcp || find(A, o.sa, o.da, 0u, rw) == NONE)
-                    nk += rel_first(A, o.sa, o.da, rw);
+                if (o.is_tcp || find(A, o.sa, o.da, 0u, rw) == NONE) {
+                    const uint32_t f = rel_first(A, o.sa, o.da, rw);
+                    nk += f;
+                    if (f && o.is_tcp && A.emrel) {   // (a TCP map's: the host checks it)
+                        const uint32_t q = atomicAdd(&A.emcnt[A.n_emaps], 1u);
+                        if (q < A.emrel_cap) {
+                            if constexpr (V6) {
+                                A.emrel[3 * q] = o.sa;
+                                A.emrel[3 * q + 1] = o.da;
+                            } else {
+                                A.emrel[3 * q] = make_uint4(o.sa, 0, 0, 0);
+                                A.emrel[3 * q + 1] = make_uint4(o.da, 0, 0, 0);
+                            }
+                            A.emrel[3 * q + 2] = make_uint4(rw, 0, 0, 0);
+                        }
+                    }
+                }
             }
             nk_new += nk;
             nk_tcp += o.is_tcp ? nk : 0u;
