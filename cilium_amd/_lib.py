@@ -113,7 +113,8 @@ class Stats(ctypes.Structure):
                 ("ct_order_changed", ctypes.c_uint64),
                 ("nat_hops", ctypes.c_uint64),
                 ("ct_evicted", ctypes.c_uint64),
-                ("svc_ordered", ctypes.c_uint64)]
+                ("svc_ordered", ctypes.c_uint64),
+                ("ct_apply_sparse", ctypes.c_uint64)]
 
 
 class NodeConfig(ctypes.Structure):

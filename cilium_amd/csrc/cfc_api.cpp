@@ -167,7 +167,10 @@ struct cfc_ctx {
         uint16_t ep = 0;
         size_t k1 = 0, k2 = 0;   // byte offsets in ws; k2 = 0: no stage 2
         bool sum = false;        // its accounting wrote the plain-hit summaries
+        // its work bits for the apply's sparse passes (cta_wbits)
+        bool wl = false;
     } last_cls;
+    DevBuf cta_wbits;   // per 64 headers: work word, then (second half) probe word
     // DevTables.ct_sum holds summaries no apply has taken (cleared before
     // the next launch that keeps them); sum_pending: the last launch kept
     // summaries and no apply has followed it yet; sum_want: launches keep
@@ -207,6 +210,7 @@ struct cfc_ctx {
     // the service step in packet order (svcorder.hip): sort keys, the
     // per-header CT_SERVICE entry words (zero between launches), count
     DevBuf svo_keys, svo_keys2, svo, svo_cnt, svo_tmp;
+    uint64_t n_apply_sparse = 0;   // device applies that took the work list
     uint64_t n_svo = 0;   // headers handed an entry an earlier header left
     bool nat46_seen = false, hop_nat46 = false;
     uint64_t n_nat_hops = 0;
@@ -2088,6 +2092,25 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     }
     bool sums = false;
     ea.sums = &sums;
+    // the apply's work list (kern_common.hpp wl_want): a launch whose apply
+    // can take the sparse passes — plain hits summarised (ct_sum), no load
+    // balancer or packet outputs (the service-step variants), no NAT hop,
+    // no monitor words (those replay every hit)
+    {
+        const bool v6 = std::is_same<Hdr, cfc_hdr_v6>::value;
+        const bool lbk = v6 ? (E.T.lb6 || E.T.rnat6 || out->pkt_saddr) : (E.T.lb4 || E.T.rnat4);
+        if (out->ct && in->n && T.ct_sum && !nat_list && !lbk && !out->notify &&
+            mode != CFC_MODE_XDP && !getenv("CFC_DENSE_APPLY")) {
+            const uint64_t words = (in->n + 63) / 64;
+            if (c->cta_wbits.bytes < 16 * words) {
+                (void)hipStreamSynchronize(s);
+                if (c->cta_wbits.ensure(16 * words))
+                    return -ENOMEM;
+            }
+            ea.wbits = (uint64_t *)c->cta_wbits.p;
+            ea.wprobe = ea.wbits + words;
+        }
+    }
     rc = launch(T, *in, *out, mode, ea, c->ctr, c->ws, c->num_cus, s,
                 in->n ? next_timing(c, std::is_same<Hdr, cfc_hdr_v6>::value) : nullptr);
     c->sum_dirty |= sums;
@@ -2122,6 +2145,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         L.k1 = wl.ct;
         L.k2 = mode == CFC_MODE_EGRESS ? wl.ct2 : 0;
         L.sum = sums;
+        L.wl = ea.wbits && sums;
     }
     return 0;
 }
@@ -2394,6 +2418,7 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     st->nat_hops = c->n_nat_hops;
     st->ct_evicted = c->n_evicted;
     st->svc_ordered = c->n_svo;
+    st->ct_apply_sparse = c->n_apply_sparse;
     st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->ct4_host.size() + c->epoch->ct->ct6_host.size())
                             : 0u;
     return 0;
@@ -3096,6 +3121,14 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             // and its plain-hit summaries (taken once: this apply clears them)
             if (L.sum && c->sum_dirty && G.ct_sum.p)
                 A.sum = (uint32_t *)G.ct_sum.p + A.acct_base;
+            // and its work list: the sparse scan and ordering passes
+            if (L.wl && A.sum && !out->notify && (mode != CFC_MODE_EGRESS || A.ck2)) {
+                const uint64_t words = (n + 63) / 64;
+                A.W = WList{(const uint64_t *)c->cta_wbits.p,
+                            (const uint64_t *)c->cta_wbits.p + words, words};
+                A.sparse = true;
+            }
+            c->last_cls.wl = false;
             c->last_cls.sum = false;
             c->sum_want = true;   // (applies follow their launches: keep them)
             c->sum_pending = false;
@@ -3137,6 +3170,8 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         O.bm_bytes = c->ord_delbm.bytes;
         O.slots = c->ord_dfirst.bytes / 4;
         O.cnt = (uint32_t *)c->ord_cnt.p;
+        O.W = A.W;
+        O.sparse = A.sparse;
         uint32_t changed = 0;
         // (IPv6 with reverse NAT: the packet outputs follow the new results)
         const bool pkt6 = V6 && out->pkt_saddr && out->pkt_ports && E.T.rnat6;
@@ -3146,6 +3181,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             return -ENOMEM;
         if (int rc = ord_resolve(A, O, c->ordb, V6, &changed, s))
             return rc;
+        A.sparse = A.sparse && O.sparse;   // (a batch that deletes: the dense scan)
         if (pkt6)
             if (int rc = ord_pkt6(A, (const uint8_t *)c->ord_ct0.p, *out, s))
                 return rc;
@@ -3164,7 +3200,9 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
-    const uint64_t nreqA = hc[CTA_NREQA], nhit = hc[CTA_NHIT];
+    // (a sparse scan does not count the plain hits: route's bound is every stage)
+    const uint64_t nreqA = hc[CTA_NREQA],
+                   nhit = A.sparse ? (mode == CFC_MODE_EGRESS ? 2 * n : n) : hc[CTA_NHIT];
     uint64_t &claims = V6 ? c->cta_claims6 : c->cta_claims;
     uint64_t &ins = V6 ? c->cta_ins6 : c->cta_ins;
     uint64_t &log_used = V6 ? c->log6_used : c->log_used;
@@ -3330,6 +3368,8 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             for (size_t j = 0; j < fmaps.size(); j++)
                 want[j] = map_want(j);
             const uint64_t nk = lbm ? 4 * n : mode == CFC_MODE_EGRESS ? 2 * n : n;
+            if (A.sparse && cta_hs_fill(A, s))   // (the protect pass reads hs)
+                return -EIO;
             const int rc = ct_evict_maps(c, V6, fmaps, want, A.hs, nk, s);
             if (rc < 0)
                 return rc;
@@ -3393,6 +3433,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     ins += hc[CTA_CLAIMS];
     log_used += hc[CTA_NLOG];
     c->cta_seq++;
+    c->n_apply_sparse += A.sparse;
     if (A.sum)   // (the finish cleared every summary the launch wrote)
         c->sum_dirty = false;
     return 0;

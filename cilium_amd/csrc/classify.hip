@@ -695,6 +695,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
     S.polb_mask = L.pol_words - 1;
     for (uint32_t j = threadIdx.x; j < (uint32_t)LDS_MET_U64; j += BLOCK)
         s_met[j] = 0;
+    // the apply's work bits (E.wbits / E.wprobe)
+    constexpr bool WL = CT && MODE != CFC_MODE_XDP && !LB;
     lds_copy(cfc_smem + S.lxc_off, reinterpret_cast<const uint4 *>(T.lxc4),
              L.lxc_slots);
     lds_copy(cfc_smem + pf4, reinterpret_cast<const uint4 *>(T.pf_bloom),
@@ -819,6 +821,17 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v4(
 #if CFC_EXP != 3
                     sto_nt(h[u].idw, C.id, o4);
 #endif
+                }
+            }
+            if (WL && E.wbits) {   // (uniform) the wave's 64 headers' work bits
+                bool pr;
+                const bool w = wl_want<EGR>(h[u].ct_byte, h[u].ver, h[u].mt, h[u].ct_k1,
+                                            EGR ? h[u].ct_k2 : NONE, pr);
+                const uint64_t wb = __ballot(w && h[u].valid), pb = __ballot(pr && h[u].valid);
+                const uint32_t w0 = base + u * BLOCK + (threadIdx.x & ~63u);
+                if ((threadIdx.x & 63) == 0 && w0 < end) {
+                    E.wbits[(start + w0) >> 6] = wb;
+                    E.wprobe[(start + w0) >> 6] = pb;
                 }
             }
             if (!EGR && MODE != CFC_MODE_XDP && E.nat_idx)   // (uniform)

@@ -32,6 +32,15 @@ struct EgressArgs {
     // an egress batch with services: per header the CT_SERVICE entry as the
     // headers before it left it (kern_common.hpp SVO_*; svcorder.hip), or null
     const uint32_t *svo;
+    // (or null) the apply's work bits (kern_common.hpp wl_want): per 64
+    // headers of the batch one word each, written by the launch
+    uint64_t *wbits, *wprobe;
+};
+
+// an apply's view of a launch's work bits (EgressArgs.wbits / wprobe)
+struct WList {
+    const uint64_t *bits, *probe;
+    uint64_t words;
 };
 
 constexpr int BLOCK = 1024;
@@ -210,6 +219,10 @@ struct CtaArgs {
     uint32_t *sum;
     bool vec;                    // the batch's arrays 16-byte aligned (the scan's loads)
     uint32_t *hs;                // [2n] hit slot per header and stage ([4n] with lbr)
+    // (sparse) the launch's work list: the scan reads it rather than the
+    // batch, and route takes the hit slots from ck1 / ck2 (hs is not written)
+    WList W;
+    bool sparse;
     // an egress batch with a load balancer: per header LbRec4 / LbRec6 (its
     // CT_SERVICE ops are virtual headers n..2n-1), null otherwise
     void *lbr;
@@ -332,6 +345,11 @@ struct OrdArgs {
     uint8_t *pinfo, *nres;
     void *tmp;
     size_t tmp_bytes;
+    // the launch's work list (EgressArgs.wl): with `sparse` the mark and
+    // collect passes read it rather than the whole batch; ord_resolve clears
+    // `sparse` when the batch deletes (the dense passes then run)
+    WList W;
+    bool sparse;
 };
 struct OrdBufs {
     DevBuf part, rel_src, rk, rh, rh2, ridx, ridx2, pinfo, nres, tmp, fpset;
@@ -351,6 +369,9 @@ size_t cta_sort_tmp_bytes(uint32_t n);
 // ordering pass (its ops decode the service step's records), then cta_scan.
 int cta_lb_pre(const CtaArgs &A, bool v6, hipStream_t s);
 int cta_scan(const CtaArgs &A, bool v6, hipStream_t s);
+// a sparse scan's batch (A.sparse): hs from the launch's keys, for the
+// eviction's protect pass
+int cta_hs_fill(const CtaArgs &A, hipStream_t s);
 // the keys the creates would add, exactly (requests sorted and deduplicated,
 // the table probed): newk[0] all of them, newk[1] those of TCP creates (they
 // go to TCP maps, the others to ANY maps); *sorted: the sorted requests for

@@ -268,6 +268,8 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
     S.polb_mask = L.pol_words - 1;
     for (uint32_t j = threadIdx.x; j < (uint32_t)LDS_MET6_U64; j += BLOCK)
         s_met[j] = 0;
+    // the apply's work bits (E.wbits / E.wprobe)
+    constexpr bool WL = CT && MODE != CFC_MODE_XDP && !LB;
     lds_copy(cfc_smem + lxc_off, reinterpret_cast<const uint4 *>(T.lxc6),
              2 * L.lxc_slots);
     lds_copy(cfc_smem + pol4, reinterpret_cast<const uint4 *>(T.pol_bloom),
@@ -671,6 +673,16 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
             st_nt(ck1, C.ct + i);
             if (EGR)
                 st_nt(ck2, C.ct2 + i);
+        }
+        if (WL && E.wbits) {   // (uniform) the wave's 64 headers' work bits
+            bool pr;
+            const bool w = wl_want<EGR>(ctb, ver, mt, ck1, ck2, pr);
+            const uint64_t wb = __ballot(w && valid), pb = __ballot(pr && valid);
+            const uint64_t w0 = base + (threadIdx.x & ~63u);
+            if ((threadIdx.x & 63) == 0 && w0 < end) {
+                E.wbits[w0 >> 6] = wb;
+                E.wprobe[w0 >> 6] = pb;
+            }
         }
         if (EGR && E.nat_idx)   // (uniform)
             list_append(E.nat_idx, E.nat_cnt, nat && valid, (uint32_t)i);

@@ -295,6 +295,113 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
     block_add(&A.cnt[CTA_NFHIT], nfh);
 }
 
+// ---- the scan over the classify launch's work bits (A.sparse: A.W, the
+// headers with a stage that is not a plain hit on a launch slot,
+// kern_common.hpp wl_want).  Every other stage is a plain hit whose summary
+// the launch's accounting took (A.sum) and whose slot route reads from the
+// launch's keys (A.ck1 / A.ck2), so nothing of it is left to do here.  Per
+// work header the dense scan's per-stage work; a hit this scan finds a slot
+// for (a key the launch left as a tag) has its slot written into the key
+// array for route.  One thread per word of 64 headers; the requests staged
+// in LDS, the block's list taken from reqA by one atomic.
+constexpr uint32_t SCANW_STAGE = 4096;
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    __shared__ uint64_t s_req[SCANW_STAGE];
+    __shared__ uint32_t s_n, s_base;
+    if (threadIdx.x == 0)
+        s_n = 0;
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t nfh = 0;
+    auto put = [&](uint64_t v) {
+        const uint32_t q = atomicAdd(&s_n, 1u);
+        if (q < SCANW_STAGE) {
+            s_req[q] = v;
+        } else {   // (a full stage: straight into the list)
+            const uint32_t r = atomicAdd(&A.cnt[CTA_NREQA], 1u);
+            if (r < A.req_cap)
+                A.reqA[r] = v;
+        }
+    };
+    for (uint64_t m = t < A.W.words ? A.W.bits[t] : 0; m; m &= m - 1) {
+        const uint64_t i = 64 * t + (uint64_t)(__ffsll((long long)m) - 1);
+        ScanIn<V6> r;
+        load_in<V6, false>(A, i, r);
+        r.k1 = A.ck1[i];
+        r.k2 = TWO ? A.ck2[i] : NONE;
+        bool need = false;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (r.cb >> (4 * st)) & 0xF;
+            const bool mine = A.mode == CFC_MODE_EGRESS && st == 0;
+            const uint32_t key = st ? r.k2 : r.k1;
+            const bool cr = (cs & CFC_CT_RES_MASK) == 0;
+            need |= (cs & CFC_CT_DONE) && !mine &&
+                    (cr ? (cs & CFC_CT_CREATE) != 0 : key >= CK_MISS);
+        }
+        const uint32_t dsto = need ? dst_owner(A.T, r.da) : 0u;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const Op<V6> o = decode_from<V6, false>(A, r, st, dsto);
+            if (o.kind == OP_HIT || o.kind == OP_DELETE) {
+                const uint32_t key = st ? r.k2 : r.k1;
+                const bool rev = ((r.cb >> (4 * st)) & CFC_CT_RES_MASK) >= 2;
+                uint32_t sl;
+                if (key < CK_MISS) {
+                    sl = (key >> 1) - A.acct_base;
+                } else {
+                    sl = rev ? find(A, o.da, o.sa, o.z1, o.w1) : find(A, o.sa, o.da, o.z2, o.w2);
+                    if (sl != NONE)   // (route reads the slot from the key array)
+                        const_cast<uint32_t *>(st ? A.ck2 : A.ck1)[i] =
+                            ct_acct_key(sl + A.acct_base, (int)o.dir);
+                }
+                if (sl == NONE) {   // a hit on an entry an earlier header creates
+                    const uint32_t home = (rev ? khash(o.da, o.sa, o.z1, o.w1)
+                                               : khash(o.sa, o.da, o.z2, o.w2)) & A.mask;
+                    put(pack(A, home, ord_of(i, st, SEC_FHIT)));
+                    nfh++;
+                } else if (o.kind == OP_DELETE) {
+                    order_mark(A, sl, MARK_ORDERED | MARK_DEL);
+                    const uint32_t v = 0xFFFFFFFFu - ord_of(i, st, SEC_OP);
+                    if (__hip_atomic_load(&A.ms[sl].y, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) < v)
+                        atomicMax(&A.ms[sl].y, v);
+                } else if (o.action == 2) {   // RST / FIN: ACTION_CLOSE
+                    order_mark(A, sl, MARK_ORDERED);
+                }
+            } else if (o.kind == OP_CREATE) {
+                put(pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP)));
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t ns = min(s_n, SCANW_STAGE);
+    if (threadIdx.x == 0)
+        s_base = ns ? atomicAdd(&A.cnt[CTA_NREQA], ns) : 0u;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < ns; q += 256)
+        if (s_base + q < A.req_cap)
+            A.reqA[s_base + q] = s_req[q];
+    block_add(&A.cnt[CTA_NFHIT], nfh);
+}
+
+// the hit slots of a sparse scan's batch for the eviction's protect pass
+// (hs, as the dense scan leaves them): from the launch's keys
+__global__ __launch_bounds__(256) void k_cta_hs_fill(CtaArgs A)
+{
+    const bool two = A.mode == CFC_MODE_EGRESS;
+    const uint64_t nk = two ? 2 * A.n : A.n;
+    const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= nk)
+        return;
+    const uint64_t i = two ? k >> 1 : k;
+    const uint32_t key = (two && (k & 1)) ? A.ck2[i] : A.ck1[i];
+    A.hs[k] = key < CK_MISS ? (key >> 1) - A.acct_base : HS_NONE;
+}
+
 // ---- the service step of an egress batch with a load balancer.  The
 // reference runs lb4_local / lb6_local packet by packet, so a header finds
 // the CT_SERVICE entry as the headers before it left it (created, its slave
@@ -888,7 +995,42 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
     for (uint64_t base = (uint64_t)blockIdx.x * span; base < nk; base += stride) {
         const uint64_t k0 = base + (uint64_t)RU * threadIdx.x;
         uint32_t slot[RU], bw[RU];
-        if (k0 + RU <= nk) {   // (A.hs: 16-byte aligned)
+        if (A.sparse) {
+            // the hit slots from the launch's keys (a miss tag or NONE: no
+            // slot); items k0.. are headers k0 / 2.. with two stages
+            uint32_t kv[RU];
+            if (k0 + RU <= nk) {   // (16-byte aligned key arrays)
+                if (two) {
+                    const uint4 *p1 = reinterpret_cast<const uint4 *>(A.ck1 + (k0 >> 1));
+                    const uint4 *p2 = reinterpret_cast<const uint4 *>(A.ck2 + (k0 >> 1));
+#pragma unroll
+                    for (int q = 0; q < RU / 8; q++) {
+                        const uint4 a = p1[q], b = p2[q];
+                        kv[8 * q] = a.x, kv[8 * q + 1] = b.x;
+                        kv[8 * q + 2] = a.y, kv[8 * q + 3] = b.y;
+                        kv[8 * q + 4] = a.z, kv[8 * q + 5] = b.z;
+                        kv[8 * q + 6] = a.w, kv[8 * q + 7] = b.w;
+                    }
+                } else {
+                    const uint4 *p1 = reinterpret_cast<const uint4 *>(A.ck1 + k0);
+#pragma unroll
+                    for (int q = 0; q < RU / 4; q++) {
+                        const uint4 a = p1[q];
+                        kv[4 * q] = a.x, kv[4 * q + 1] = a.y, kv[4 * q + 2] = a.z,
+                                 kv[4 * q + 3] = a.w;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < RU; u++) {
+                    const uint64_t k = k0 + u;
+                    kv[u] = k >= nk ? NONE : two ? ((k & 1) ? A.ck2 : A.ck1)[k >> 1] : A.ck1[k];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < RU; u++)
+                slot[u] = kv[u] < CK_MISS ? (kv[u] >> 1) - A.acct_base : HS_NONE;
+        } else if (k0 + RU <= nk) {   // (A.hs: 16-byte aligned)
             const uint4 *hp = reinterpret_cast<const uint4 *>(A.hs + k0);
 #pragma unroll
             for (int q = 0; q < RU / 4; q++) {
@@ -2008,6 +2150,14 @@ int cta_scan_t(const CtaArgs &A, hipStream_t s)
         hipLaunchKernelGGL(k_cta_scan_lb<V6>, dim3(blocks_for(A.n, 2048)), dim3(256), 0, s, A);
         return hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
+    if (A.sparse) {   // (the launch's work bits; A.ck1 / A.ck2 and A.sum set)
+        const unsigned g = (unsigned)((A.W.words + 255) / 256);
+        if (A.mode == CFC_MODE_EGRESS)
+            hipLaunchKernelGGL((k_cta_scan_w<V6, true>), dim3(g), dim3(256), 0, s, A);
+        else
+            hipLaunchKernelGGL((k_cta_scan_w<V6, false>), dim3(g), dim3(256), 0, s, A);
+        return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    }
     if (A.mode == CFC_MODE_EGRESS)
         hipLaunchKernelGGL((k_cta_scan<V6, true>), dim3(blocks_for(A.n, 2048)), dim3(256), 0, s, A);
     else
@@ -2127,6 +2277,14 @@ int ct_protect_hits(const uint32_t *hs, uint64_t nk, uint32_t *bm, hipStream_t s
     if (nk)
         hipLaunchKernelGGL(k_ct_protect, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, hs,
                            nk, bm);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int cta_hs_fill(const CtaArgs &A, hipStream_t s)
+{
+    const uint64_t nk = A.mode == CFC_MODE_EGRESS ? 2 * A.n : A.n;
+    if (nk)
+        hipLaunchKernelGGL(k_cta_hs_fill, dim3((unsigned)((nk + 255) / 256)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

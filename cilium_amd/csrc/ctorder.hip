@@ -486,6 +486,155 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
     block_add(&O.cnt[ORD_RELBOUND], nrk);
 }
 
+// ---- the same two passes over the classify launch's work bits (O.W,
+// kern_common.hpp wl_want) instead of the whole batch: one thread per word
+// of 64 headers.  Every create, every deleting stage and every ICMP error's
+// stage is a work bit; a dropped CT_NEW stage of another kind is a probe
+// bit.  An ESTABLISHED stage outside them is a plain hit, which takes part
+// only on a mixed slot — a batch with deletes goes back to the dense passes
+// (ord_resolve_t), so ORD_NEST counts the work bits' stages alone.
+
+// a dropped CT_NEW stage that is a probe (its header's probe bit): a key
+// tag that is not an ICMP error's
+__device__ __forceinline__ bool probe_tag(uint32_t tg) { return tag_ok(tg) && !(tg & 1); }
+
+// one wave per word (lane l: header 64 w + l), four words per block and
+// step, grid-stride (every thread runs the same number of steps)
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0, nrk = 0;
+    for (uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < O.W.words;
+         w += (uint64_t)gridDim.x * 4) {
+        if (lane == 0)
+            nnd += (uint32_t)__popcll(O.W.probe[w]);
+        if (!((O.W.bits[w] >> lane) & 1))
+            continue;
+        const uint64_t i = 64 * w + lane;
+        const uint32_t cb = A.ctb[i];
+        const bool drop = A.ver[i] == DROP_POLICY;
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (cb >> (4 * st)) & 0xF;
+            if (!(cs & CFC_CT_DONE))
+                continue;
+            const uint32_t r = cs & CFC_CT_RES_MASK;
+            const bool dropped = st == last && drop;
+            if (r == CT_NEW) {
+                if (dropped) {   // (a probe's is counted from its bit)
+                    nnd += !probe_tag((st ? O.ck2 : O.ck1)[i]);
+                    continue;
+                }
+                ncr++;
+                if (!O.cbloom)
+                    continue;
+                if (O.tagged) {
+                    const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+                    if (tag_ok(tg)) {
+                        cb_put(O, tag_key(tg));
+                        nrk += tg & 1u;
+                    } else {
+                        nun++;
+                    }
+                } else {
+                    cb_put(O, prekey<V6>(A, i, st));
+                }
+            } else if (r == CT_ESTABLISHED) {
+                nest++;
+                if (!dropped)
+                    continue;
+                ndt++;
+                const uint32_t sl = start_slot<V6>(A, O, i, st);
+                if (sl == NONE)
+                    continue;
+                const uint32_t bb = 1u << (sl & 31), ord = (uint32_t)(i << 1) | (uint32_t)st;
+                if (!(O.delbm[sl >> 5] & bb))
+                    atomicOr(&O.delbm[sl >> 5], bb);
+                if (ord < O.dfirst[sl])
+                    atomicMin(&O.dfirst[sl], ord);
+                ndel++;
+            }
+        }
+    }
+    block_add(&O.cnt[ORD_NCREATE], ncr);
+    block_add(&O.cnt[ORD_NDEL], ndel);
+    block_add(&O.cnt[ORD_NNEWDROP], nnd);
+    block_add(&O.cnt[ORD_NEST], nest);
+    block_add(&O.cnt[ORD_NESTDROP], ndt);
+    block_add(&O.cnt[ORD_UNTAGGED], nun);
+    block_add(&O.cnt[ORD_RELBOUND], nrk);
+}
+
+// header i's participating stages (bit st): from its work bit, every allowed
+// CT_NEW stage and every dropped one that is not a probe (an ICMP error's,
+// an untagged one: always); from its probe bit, each probe whose key a
+// create of the batch may write (the creates' filter).  *nrk: its ICMP
+// errors' stages
+template <bool V6, bool TWO>
+__device__ __forceinline__ uint32_t part_bits(const CtaArgs &A, const OrdArgs &O, uint64_t i,
+                                              bool work, uint32_t &nrk)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint32_t cb = A.ctb[i];
+    const bool drop = A.ver[i] == DROP_POLICY;
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int st = 0; st < NST; st++) {
+        const uint32_t cs = (cb >> (4 * st)) & 0xF;
+        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+            continue;
+        const bool dropped = st == last && drop;
+        if (!dropped) {
+            bits |= work ? 1u << st : 0u;
+            continue;
+        }
+        const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+        if (probe_tag(tg) == work)   // (the other bit's stage)
+            continue;
+        bool take;
+        if (O.tagged) {
+            take = !tag_ok(tg) || (tg & 1) || (O.cbloom && cb_maybe(O, tag_key(tg)));
+            nrk += tag_ok(tg) && (tg & 1);
+        } else {   // (the pre-key filter)
+            const PreIn<V6> f = pre_in<V6>(A, i);
+            take = icmp_error<V6>(f.mt, f.pt) || (O.cbloom && cb_maybe(O, prekey_of<V6>(A, f, st)));
+        }
+        bits |= take ? 1u << st : 0u;
+    }
+    return bits;
+}
+
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t nrk = 0;
+    // (one wave per word, as k_ord_mark_w; uniform steps: block_count_n)
+    for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < O.W.words; w0 += (uint64_t)gridDim.x * 4) {
+        const uint64_t w = w0 + (threadIdx.x >> 6), i = 64 * w + lane;
+        uint32_t bits = 0;
+        if (w < O.W.words) {
+            if ((O.W.bits[w] >> lane) & 1)
+                bits |= part_bits<V6, TWO>(A, O, i, true, nrk);
+            if ((O.W.probe[w] >> lane) & 1) {
+                uint32_t k = 0;
+                bits |= part_bits<V6, TWO>(A, O, i, false, k);
+            }
+        }
+        uint32_t r = block_count_n(&O.cnt[ORD_NPART], (uint32_t)__popc(bits));
+        for (uint32_t q = bits; q; q &= q - 1) {
+            if (r < O.part_cap)
+                O.part[r] = (uint32_t)(i << 1) | (uint32_t)(__ffs(q) - 1);
+            r++;
+        }
+    }
+    block_add(&O.cnt[ORD_RELBOUND], nrk);
+}
+
 // a deleting stage on a slot only deletes: all but its first delete see
 // the entry gone (CT_NEW, no create: they are dropped).  Runs before
 // k_ord_write (its stages' bytes are the launch's).
@@ -711,6 +860,13 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         else                                                                             \
             hipLaunchKernelGGL((K<V6, false>), dim3(grid), dim3(256), 0, s, __VA_ARGS__); \
     } while (0)
+    // the mark / collect pass: over the launch's work list, or the batch
+    auto mark = [&]() {
+        if (O.sparse)
+            ORD_LAUNCH(k_ord_mark_w, (unsigned)std::min<uint64_t>((O.W.words + 3) / 4, 8192), A, O);
+        else
+            ORD_LAUNCH(k_ord_mark, g, A, O);
+    };
     *changed = 0;   // (ORD_CHANGED accumulates on the device: no wait for it)
     if (hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
         return -EIO;
@@ -754,16 +910,28 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
                          hipSuccess;
         }
     } clear{O, s};
-    ORD_LAUNCH(k_ord_mark, g, A, O);
+    O.sparse = O.sparse && O.W.bits && O.W.words;
+    mark();
     if (!rd())
         return -EIO;
+    if (O.sparse && hc[ORD_NDEL]) {
+        // a batch that deletes: the dense passes (an allowed ESTABLISHED
+        // stage of a deleted slot, a plain hit outside the list, takes part;
+        // the marks and filter inserts made are idempotent)
+        O.sparse = false;
+        if (hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
+            return -EIO;
+        mark();
+        if (!rd())
+            return -EIO;
+    }
     const bool untagged = O.tagged && hc[ORD_UNTAGGED];
     if (untagged || (hc[ORD_NCREATE] > 4ull * (O.cb_mask + 1) && O.cb_mask + 1 < (1u << 26))) {
         // (the delete marks are idempotent; the counts start again)
         O.tagged = O.tagged && !untagged;
         if (!filter(hc[ORD_NCREATE]) || hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
             return -ENOMEM;
-        ORD_LAUNCH(k_ord_mark, g, A, O);
+        mark();
         if (!rd())
             return -EIO;
     }
@@ -785,7 +953,10 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         return -ENOMEM;
     O.part = (uint32_t *)B.part.p;
     O.part_cap = (uint32_t)cap;
-    ORD_LAUNCH(k_ord_collect, g, A, O);
+    if (O.sparse)
+        ORD_LAUNCH(k_ord_collect_w, (unsigned)std::min<uint64_t>((O.W.words + 3) / 4, 8192), A, O);
+    else
+        ORD_LAUNCH(k_ord_collect, g, A, O);
     if (!rd())
         return -EIO;
     const uint64_t np = hc[ORD_NPART];

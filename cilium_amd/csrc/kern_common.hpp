@@ -706,6 +706,38 @@ __device__ __forceinline__ uint32_t ck_miss6(const uint4 &sa, const uint4 &da, u
                                 ct_hash4(da.x, da.y, da.z, da.w), k.z2, k.w2), k.w2);
 }
 
+// The apply's work bits (ctapply.hip k_cta_scan_w, ctorder.hip): per 64
+// headers of a classify launch two words, one bit per header.  work: a CT
+// stage that is not a plain hit on a slot of the launch's table — an allowed
+// CT_NEW stage (a create), an ICMP error's CT_NEW stage, a hit the launch
+// left no slot for (its key a miss tag or NONE), a delete (CT_ESTABLISHED,
+// dropped at the header's last stage), a TCP close (ACTION_CLOSE).  probe:
+// a dropped CT_NEW stage (no create; its result changes only when a create
+// of the batch writes its key).  Every other stage is a plain hit, which the
+// launch's accounting summarised (DevTables.ct_sum).
+template <bool TWO>
+__device__ __forceinline__ bool wl_want(uint32_t ctb, int32_t ver, uint32_t mt, uint32_t k1,
+                                        uint32_t k2, bool &probe)
+{
+    const int last = (ctb & (CTO_DONE << 4)) ? 1 : 0;
+    const bool close = (mt & 0xFF) == 6 && (mt & CFC_HF_TCP_CLOSE);
+    bool w = false;
+    probe = false;
+#pragma unroll
+    for (int st = 0; st < (TWO ? 2 : 1); st++) {
+        const uint32_t cs = (ctb >> (4 * st)) & 0xF;
+        if (!(cs & CTO_DONE))
+            continue;
+        const uint32_t res = cs & 3u, key = st ? k2 : k1;
+        const bool dropped = st == last && ver == DROP_POLICY;
+        const bool pr = res == 0 && dropped && key != NONE && key >= CK_MISS && !(key & 1);
+        probe |= pr;
+        w |= (res == 0 && !pr) || close || (res != 0 && key >= CK_MISS) ||
+             (res == 1 && dropped);
+    }
+    return w;
+}
+
 // CONNTRACK_ACCOUNTING (lxc_config.h:50, conntrack.h:247-257): the hit
 // entry's rx (ingress) or tx (egress) packets/bytes
 __device__ __forceinline__ void ct_account(const DevTables &T, uint32_t slot,

@@ -619,6 +619,10 @@ typedef struct {
     /* headers whose service step found the CT_SERVICE entry an earlier
      * header of the same batch created or re-selected (cfc_classify_*) */
     uint64_t svc_ordered;
+    /* device applies whose scan and ordering passes read the classify
+     * launch's work list (the headers with a CT stage that is not a plain
+     * hit) rather than the whole batch */
+    uint64_t ct_apply_sparse;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

@@ -140,3 +140,33 @@ def test_c5_packet_order_hot_flows(torch, clock):
     key = h.saddr.astype(np.uint64) << 32 | h.daddr.astype(np.uint64)
     _, cnt = np.unique(key, return_counts=True)
     assert cnt.max() > 4 * 512, cnt.max()
+
+
+@pytest.mark.parametrize("mode", [0, 3])
+def test_sparse_apply_packet_order(torch, mode, monkeypatch):
+    """The apply's sparse passes — ordering and scan over the classify
+    launch's work list (kern_common.hpp wl_want) instead of the whole batch —
+    on a stream without deletes (the headers of denied live flows taken out:
+    a batch that deletes takes the dense passes): multi-packet new flows,
+    closes, ICMP errors, hot flows.  Every output, CT entry and counter
+    against the sequential oracle, and the dense passes (CFC_DENSE_APPLY)
+    give the same."""
+    t, flows = S.config_c5(5, n_flows=100_000, n_prefixes=50_000, n_policy=8000, now=1000)
+    h = S.headers_c5_seq(t, flows, 600_000, seed=17)
+    o = O.Oracle(t)
+    o.set_clock(1003)
+    _, ov, _, oct_ = o.classify(h, mode, 0, nthreads=16, want_ct=True)
+    est_drop = ((oct_ & 0xF) == (1 | 4)) & (ov == -133)   # ESTABLISHED, DROP_POLICY
+    h = S.take(h, np.flatnonzero(~est_drop))
+    g, want = run_both(torch, t, h, mode, chunks=3, notify=False)
+    check(g, want)
+    # (a batch whose sequential run still deletes — a new flow's later packet
+    # the policy drops — takes the dense passes)
+    assert g["stats"]["ct_apply_sparse"] >= 2, g["stats"]
+    assert g["stats"]["ct_order_changed"] > 1000, g["stats"]
+    monkeypatch.setenv("CFC_DENSE_APPLY", "1")
+    gd, _ = run_both(torch, t, h, mode, chunks=3, notify=False)
+    assert gd["stats"]["ct_apply_sparse"] == 0, gd["stats"]
+    for k in ("act", "ver", "ide", "ct"):
+        np.testing.assert_array_equal(g[k], gd[k])
+    np.testing.assert_array_equal(g["rows"], gd["rows"])
