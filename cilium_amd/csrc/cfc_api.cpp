@@ -221,6 +221,13 @@ struct cfc_ctx {
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
+    // a device apply that took no host wait for its own counts (a sparse
+    // scan's, route run early): they follow it into pinned host memory and
+    // settle() adds them before the next reader of claims / log_used
+    bool pend = false, pend_v6 = false;
+    uint32_t *pend_cnt = nullptr;   // CTA_NCNT words, pinned
+    hipEvent_t pend_ev = nullptr;
+    DevBuf cta_cxr;                 // the early route's list
     DevBuf cta_log6;
     bool ct6_dirty = false;      // an IPv6 device apply since the last sync
 
@@ -353,6 +360,22 @@ void ct_value_from_dev(std::string &v, const CtSyncRec &r, bool created)
         memcpy(&v[38], &rev, 2);
         memcpy(&v[44], &r.info.sec, 4);
     }
+}
+
+// a pending apply's counts into the host's bookkeeping (its event waited)
+void settle(cfc_ctx *c)
+{
+    if (!c->pend)
+        return;
+    c->pend = false;
+    (void)hipEventSynchronize(c->pend_ev);
+    const uint32_t *h = c->pend_cnt;
+    uint64_t &claims = c->pend_v6 ? c->cta_claims6 : c->cta_claims;
+    uint64_t &ins = c->pend_v6 ? c->cta_ins6 : c->cta_ins;
+    uint64_t &log_used = c->pend_v6 ? c->log6_used : c->log_used;
+    claims += h[CTA_CLAIMS];
+    ins += h[CTA_CLAIMS];
+    log_used += h[CTA_NLOG];
 }
 
 // The IPv6 table's part of ct_sync: its dirty slots, then its TCP maps'
@@ -502,6 +525,7 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
 // header order.  Runs before anything reads or writes a CT map on the host.
 int ct_sync(cfc_ctx *c, hipStream_t s)
 {
+    settle(c);
     if (!c->ct_dirty || !c->epoch)
         return 0;
     order_after_launches(c, s);
@@ -1586,6 +1610,10 @@ void cfc_close(cfc_ctx *c)
         (void)hipFree(c->ws);
     if (c->last_done)
         (void)hipEventDestroy(c->last_done);
+    if (c->pend_ev)
+        (void)hipEventDestroy(c->pend_ev);
+    if (c->pend_cnt)
+        (void)hipHostFree(c->pend_cnt);
     if (c->nt_done)
         (void)hipEventDestroy(c->nt_done);
     delete c;
@@ -2996,6 +3024,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
                  hipStream_t s, bool may_grow = true, bool order = true)
 {
     constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
+    settle(c);
     if (c->ct_apply_mode != CFC_CT_APPLY_DEVICE || !c->epoch)
         return 1;
     // the device table must be the maps as committed: no host-side CT
@@ -3172,6 +3201,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         O.cnt = (uint32_t *)c->ord_cnt.p;
         O.W = A.W;
         O.sparse = A.sparse;
+        O.rtag = A.sparse ? A.hs : nullptr;   // (hs: the dense scan's, unused)
         uint32_t changed = 0;
         // (IPv6 with reverse NAT: the packet outputs follow the new results)
         const bool pkt6 = V6 && out->pkt_saddr && out->pkt_ports && E.T.rnat6;
@@ -3196,8 +3226,28 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         A.mon = (uint8_t *)c->cta_mon.p;
     }
     uint32_t hc[CTA_NCNT];
-    if (cta_scan(A, V6, s) ||
-        hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    // a sparse scan's batch routes its ordered hits right after the scan
+    // (the creates' slots hold no hit of the launch), into a list of its
+    // own: one wait for both passes' counts, none after the inserts
+    const bool early = A.sparse && !lbm && !out->notify;
+    const uint64_t nroute_cap = mode == CFC_MODE_EGRESS ? 2 * n : n;
+    if (early && (c->cta_cxr.ensure(8 * nroute_cap) ||
+                  (!c->pend_cnt && (hipHostMalloc((void **)&c->pend_cnt, 4 * CTA_NCNT,
+                                                  hipHostMallocDefault) != hipSuccess ||
+                                    hipEventCreateWithFlags(&c->pend_ev, hipEventDisableTiming) !=
+                                        hipSuccess))))
+        return -ENOMEM;
+    if (cta_scan(A, V6, s))
+        return -EIO;
+    if (early) {
+        CtaArgs R = A;
+        R.cx = (uint64_t *)c->cta_cxr.p;
+        R.cx_base = 0;
+        R.cx_cap = (uint32_t)nroute_cap;
+        if (cta_route(R, s))
+            return -EIO;
+    }
+    if (hipMemcpyAsync(hc, A.cnt, sizeof(hc), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     // (a sparse scan does not count the plain hits: route's bound is every stage)
@@ -3214,7 +3264,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     };
     uint64_t used = used_now();
     const uint64_t nr = std::max<uint64_t>(nreqA, 1);
-    const uint64_t cx_cap = nhit + k3 * nreqA + 64;
+    const uint64_t cx_cap = nhit + (k3 + 1) * nreqA + 64;   // (round 1 laid out for 2 per create)
     const uint64_t log_need = log_used + nreqA;
     bool ok = nreqA <= A.req_cap && cx_cap <= 0xFFFFFFFFu;
     if (ok && (c->cta_req2.ensure(40 * nr) || c->cta_cx.ensure(16 * cx_cap) ||
@@ -3414,7 +3464,11 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     c->ct6_dirty |= V6;
     // (no wait for the fold: the host's bookkeeping below was read after
     // route, the rest is stream-ordered before anything that reads the table)
-    int rc = cta_rest(A, V6, (uint32_t)nreqA, presorted, hc, s);
+    if (early && hc[CTA_NCX] > nroute_cap)
+        return -EOVERFLOW;
+    int rc = early ? cta_rest(A, V6, (uint32_t)nreqA, presorted, hc, s,
+                              (const uint64_t *)c->cta_cxr.p, hc[CTA_NCX])
+                   : cta_rest(A, V6, (uint32_t)nreqA, presorted, hc, s);
     if (rc) {
         // the table may hold some of the batch's inserts: no per-slot mark
         // or summary may leak into the next apply, the claims made count,
@@ -3429,9 +3483,19 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         c->built_sig[3] = ~0ull;
         return rc;
     }
-    claims += hc[CTA_CLAIMS];
-    ins += hc[CTA_CLAIMS];
-    log_used += hc[CTA_NLOG];
+    if (early) {
+        // its counts follow it (settle() adds them before their next reader)
+        if (hipMemcpyAsync(c->pend_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipEventRecord(c->pend_ev, s) != hipSuccess)
+            return -EIO;
+        c->pend = true;
+        c->pend_v6 = V6;
+    } else {
+        claims += hc[CTA_CLAIMS];
+        ins += hc[CTA_CLAIMS];
+        log_used += hc[CTA_NLOG];
+    }
     c->cta_seq++;
     c->n_apply_sparse += A.sparse;
     if (A.sum)   // (the finish cleared every summary the launch wrote)
@@ -3867,6 +3931,7 @@ struct GcFilterHost {
 int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
               cfc_ct_gc_stats &st, hipStream_t s, const uint32_t *protect)
 {
+    settle(c);
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
     const uint64_t slots = G.ct4_host.size();

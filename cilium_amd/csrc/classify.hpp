@@ -320,7 +320,7 @@ struct DevBuf {
 // the apply proper
 enum { ORD_NPART, ORD_NCREATE, ORD_NDEL, ORD_NNEWDROP, ORD_NEST, ORD_NESTDROP, ORD_UNTAGGED,
        ORD_RELBOUND, ORD_NRELKEY, ORD_NREL,
-       ORD_COLL, ORD_CHANGED, ORD_NCNT };
+       ORD_COLL, ORD_SETFULL, ORD_CHANGED, ORD_NCNT };
 struct OrdArgs {
     uint8_t *ctb;                 // the batch's CT bytes (rewritten in place)
     uint32_t *ck1, *ck2;          // the classify launch's hit keys (or null)
@@ -350,10 +350,15 @@ struct OrdArgs {
     // `sparse` when the batch deletes (the dense passes then run)
     WList W;
     bool sparse;
+    // (sparse) the batch's key set (cbloom as an open-addressing table of
+    // key tags, cb_mask + 1 words; bit 1 of an entry: shared) and per header
+    // stage a create's related-entry tag (the apply's hs, unused then)
+    uint32_t *rtag;
 };
 struct OrdBufs {
     DevBuf part, rel_src, rk, rh, rh2, ridx, ridx2, pinfo, nres, tmp, fpset;
     uint32_t creates_hint = 0;   // the last batch's creates: the filter's size
+    uint32_t part_hint = 0;      // the last batch's participants: the list's room
 };
 // rewrites the CT bytes (and hit keys) of the stages whose packet-order
 // result differs from the launch's; *changed: how many
@@ -379,8 +384,15 @@ int cta_hs_fill(const CtaArgs &A, hipStream_t s);
 int cta_newkeys(const CtaArgs &A, bool v6, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,
                 hipStream_t s);
 // presorted: cta_newkeys' sorted requests, or null
+// routed: with route run early (a sparse scan's batch: cta_route into
+// `routed`, nroute ops) the rest takes no host wait; host_cnt is then not
+// filled (the caller copies the counters behind it)
 int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, const uint64_t *presorted,
-             uint32_t *host_cnt, hipStream_t s);
+             uint32_t *host_cnt, hipStream_t s, const uint64_t *routed = nullptr,
+             uint32_t nroute = 0);
+// route alone, into A.cx from A.cx_base (a sparse scan's batch: right
+// after the scan, its creates' slots hold no hit of the launch)
+int cta_route(const CtaArgs &A, hipStream_t s);
 // lb (ct4_lb / ct6_lb, or null): the records carry slave | loopback << 16 |
 // 1 << 31 in pad
 int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,

@@ -770,7 +770,8 @@ __global__ __launch_bounds__(RQ_B) void k_cta_insert(CtaArgs A, uint64_t *req, u
 {
     const uint32_t r0 = blockIdx.x * RQ_B + threadIdx.x;
     const uint64_t home = r0 < nreq ? req[r0] >> A.ob : 0;
-    const bool lead = r0 < nreq && (r0 == 0 || (req[r0 - 1] >> A.ob) != home);
+    // (an all-ones request is an unused place of round 1: skipped)
+    const bool lead = r0 < nreq && home <= A.mask && (r0 == 0 || (req[r0 - 1] >> A.ob) != home);
     const uint64_t omask = (1ull << A.ob) - 1;
     uint32_t claims = 0;
     if (lead) {
@@ -1210,10 +1211,10 @@ __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx
     if (r >= ncx)
         return;
     const uint64_t omask = (1ull << A.ob) - 1;
-    bool k = true;
+    bool k = (cx[r] >> A.ob) <= A.mask;   // (an unused place of round 1: dropped)
     // (a slot this batch writes keeps every hit: after the write each one
     // counts in the fold)
-    if (r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob) &&
+    if (k && r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob) &&
         !(A.ms[(uint32_t)(cx[r] >> A.ob)].x & MARK_PUTC)) {
         const uint32_t s1 = hit_sig<V6>(A, (uint32_t)(cx[r] & omask));
         k = !s1 || s1 != hit_sig<V6>(A, (uint32_t)(cx[r - 1] & omask));
@@ -2188,43 +2189,56 @@ int cta_newkeys_t(const CtaArgs &A, uint32_t nreqA, uint64_t **sorted, uint32_t 
 
 template <bool V6>
 int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint32_t *host_cnt,
-               hipStream_t s)
+               hipStream_t s, const uint64_t *routed, uint32_t nroute)
 {
     const int bits = A.ob + A.slot_bits;
     uint64_t *sorted = const_cast<uint64_t *>(presorted);
     int rc;
     if (!sorted && (rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
         return rc;
+    // the second round's requests (a create's related and reverse-NAT
+    // entries, at most two per create) and their ops' places in the list
+    // are laid out for that bound, the unused ones all-ones (sorted last,
+    // skipped by the insert, dropped by dedup): no wait for their count
+    const uint32_t nbB = (uint32_t)std::min<uint64_t>(2ull * nreqA, A.req_cap);
+    if (nbB && (hipMemsetAsync(A.reqB, 0xFF, 8ull * nbB, s) != hipSuccess ||
+                (uint64_t)nreqA + nbB > A.cx_cap ||
+                hipMemsetAsync(A.cx + nreqA, 0xFF, 8ull * nbB, s) != hipSuccess))
+        return -EIO;
     if (nreqA) {
         hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqA + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A, sorted,
                            nreqA, 0, 0u);
         hipLaunchKernelGGL(k_cta_related<V6>, dim3((nreqA + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A,
                            (const uint64_t *)sorted, nreqA);
     }
-    if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return -EIO;
-    const uint32_t nreqB = host_cnt[CTA_NREQB];
-    if (nreqB > A.req_cap || host_cnt[CTA_NLOG] > A.log_cap)
-        return -EOVERFLOW;
-    if ((rc = sort_keys(A, A.reqB, A.reqB2, nreqB, bits, s, &sorted)))
+    if ((rc = sort_keys(A, A.reqB, A.reqB2, nbB, bits, s, &sorted)))
         return rc;
-    if (nreqB)
-        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nreqB + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A, sorted,
-                           nreqB, 1, nreqA);
-    // the creates' ops take the list's first nreqA + nreqB places, route's
+    if (nbB)
+        hipLaunchKernelGGL(k_cta_insert<V6>, dim3((nbB + RQ_B - 1) / RQ_B), dim3(RQ_B), 0, s, A, sorted,
+                           nbB, 1, nreqA);
+    // the creates' ops take the list's first nreqA + nbB places, route's
     // ordered hits follow
-    CtaArgs R = A;
-    R.cx_base = nreqA + nreqB;
-    {
+    uint64_t ncx64;
+    if (routed) {   // (routed already: its list appended, no wait)
+        ncx64 = (uint64_t)nreqA + nbB + nroute;
+        if (ncx64 > A.cx_cap)
+            return -EOVERFLOW;
+        if (nroute && hipMemcpyAsync(A.cx + nreqA + nbB, routed, 8ull * nroute,
+                                     hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return -EIO;
+    } else {
+        CtaArgs R = A;
+        R.cx_base = nreqA + nbB;
         const uint64_t nk = A.lbr ? 4 * A.n : A.mode == CFC_MODE_EGRESS ? 2 * A.n : A.n;
         hipLaunchKernelGGL(k_cta_route, dim3(blocks_for((nk + RU - 1) / RU, 2048)), dim3(256), 0,
                            s, R);
+        if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        if (host_cnt[CTA_NREQB] > nbB || host_cnt[CTA_NLOG] > A.log_cap)
+            return -EOVERFLOW;
+        ncx64 = (uint64_t)nreqA + nbB + host_cnt[CTA_NCX];
     }
-    if (hipMemcpyAsync(host_cnt, A.cnt, 4 * CTA_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return -EIO;
-    const uint64_t ncx64 = (uint64_t)nreqA + nreqB + host_cnt[CTA_NCX];
     if (ncx64 > A.cx_cap)
         return -EOVERFLOW;
     const uint32_t ncx = (uint32_t)ncx64;
@@ -2299,10 +2313,17 @@ int cta_scan(const CtaArgs &A, bool v6, hipStream_t s)
 }
 
 int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, const uint64_t *presorted,
-             uint32_t *host_cnt, hipStream_t s)
+             uint32_t *host_cnt, hipStream_t s, const uint64_t *routed, uint32_t nroute)
 {
-    return v6 ? cta_rest_t<true>(A, nreqA, presorted, host_cnt, s)
-              : cta_rest_t<false>(A, nreqA, presorted, host_cnt, s);
+    return v6 ? cta_rest_t<true>(A, nreqA, presorted, host_cnt, s, routed, nroute)
+              : cta_rest_t<false>(A, nreqA, presorted, host_cnt, s, routed, nroute);
+}
+
+int cta_route(const CtaArgs &A, hipStream_t s)
+{
+    const uint64_t nk = A.lbr ? 4 * A.n : A.mode == CFC_MODE_EGRESS ? 2 * A.n : A.n;
+    hipLaunchKernelGGL(k_cta_route, dim3(blocks_for((nk + RU - 1) / RU, 2048)), dim3(256), 0, s, A);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 int cta_newkeys(const CtaArgs &A, bool v6, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,

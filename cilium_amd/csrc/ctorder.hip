@@ -498,6 +498,108 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
 // tag that is not an ICMP error's
 __device__ __forceinline__ bool probe_tag(uint32_t tg) { return tag_ok(tg) && !(tg & 1); }
 
+// The sparse pass takes part only the stages whose key another stage of the
+// batch may share — the chains; a key with one stage keeps its batch-start
+// existence, so its result stands.  Key tags (CK_MISS | a 29-bit hash, bit
+// 0 TUPLE_F_RELATED, bit 1 clear) go into two open-addressing sets of
+// cb_mask + 1 words each (O.cbloom).  The main set holds the creates' k2
+// tags: a second put of a tag marks it shared (bit 1), and a dropped CT_NEW
+// stage (a probe) that finds its tag there shares it and takes part.  The
+// related set holds the related-form keys: every ICMP error's k2 (bit 0 of
+// the entry: an error's) and every UDP / ICMP create's related entry (the
+// key an ICMP error's k2 lookup finds, ct_create4/6's second write); an
+// entry an error and another stage put is shared.  Collect then takes the
+// creates and ICMP errors whose entries are shared.  Equal tags of
+// different keys only add participants (the sort compares the keys).
+constexpr uint32_t SET_SHARED = 2u, SET_ERR = 1u, SET_PROBES = 64;
+// main set: returns false on a full run (ORD_SETFULL)
+__device__ __forceinline__ bool set_put(uint32_t *set, uint32_t mask, uint32_t tg)
+{
+    uint32_t sl = fmix32(tg) & mask;
+    for (uint32_t p = 0; p < SET_PROBES; p++, sl = (sl + 1) & mask) {
+        uint32_t cur = set[sl];
+        if (cur == 0) {
+            cur = atomicCAS(&set[sl], 0u, tg);
+            if (cur == 0)
+                return true;
+        }
+        if ((cur & ~SET_SHARED) == tg) {
+            if (!(cur & SET_SHARED))
+                atomicOr(&set[sl], SET_SHARED);
+            return true;
+        }
+    }
+    return false;
+}
+// related set: err — an ICMP error's k2 (else a create's related entry)
+__device__ __forceinline__ bool rel_put(uint32_t *set, uint32_t mask, uint32_t tg, bool err)
+{
+    const uint32_t k = tg & ~3u, mine = err ? SET_ERR : 0u;
+    uint32_t sl = fmix32(k) & mask;
+    for (uint32_t p = 0; p < SET_PROBES; p++, sl = (sl + 1) & mask) {
+        uint32_t cur = set[sl];
+        if (cur == 0) {
+            cur = atomicCAS(&set[sl], 0u, k | mine);
+            if (cur == 0)
+                return true;
+        }
+        if ((cur & ~3u) == k) {
+            // another stage put it first: shared when an error is one of them
+            if (err || (cur & SET_ERR)) {
+                if ((cur & (SET_SHARED | mine)) != (SET_SHARED | mine))
+                    atomicOr(&set[sl], SET_SHARED | mine);
+            } else if (!(cur & SET_ERR)) {
+                // (a second create: shared should an error come later —
+                // the error sees the entry there and shares it)
+            }
+            return true;
+        }
+    }
+    return false;
+}
+// the entry of a tag (its slot), or NONE; cmp: the bits compared
+__device__ __forceinline__ uint32_t set_find(const uint32_t *set, uint32_t mask, uint32_t k,
+                                             uint32_t cmp, uint32_t &cur)
+{
+    uint32_t sl = fmix32(k) & mask;
+    for (uint32_t p = 0; p < SET_PROBES; p++, sl = (sl + 1) & mask) {
+        cur = set[sl];
+        if (cur == 0)
+            return NONE;
+        if ((cur & cmp) == k)
+            return sl;
+    }
+    return NONE;
+}
+__device__ __forceinline__ bool main_shared(const OrdArgs &O, uint32_t tg)
+{
+    uint32_t cur;
+    return set_find(O.cbloom, O.cb_mask, tg, ~SET_SHARED, cur) != NONE && (cur & SET_SHARED);
+}
+__device__ __forceinline__ bool rel_shared(const OrdArgs &O, uint32_t tg)
+{
+    uint32_t cur;
+    return set_find(O.cbloom + O.cb_mask + 1, O.cb_mask, tg & ~3u, ~3u, cur) != NONE &&
+           (cur & SET_SHARED);
+}
+// a UDP / ICMP create's related-entry tag (its k2's addresses, ports 0, the
+// ICMP protocol, k2's flags | TUPLE_F_RELATED: ck_miss4 / ck_miss6 of that
+// key), or 0 when it writes none (TCP: the TCP map's, which no lookup
+// reaches; a k2 of ICMP-error form is its own)
+template <bool V6>
+__device__ __forceinline__ uint32_t rel_tag(const CtaArgs &A, uint64_t i, int st)
+{
+    const Op<V6> o = decode<V6>(A, i, st);
+    if (o.kind != OP_CREATE || o.is_tcp || o.ki_form)
+        return 0;
+    const uint32_t rw = ct_word(icmp_proto<V6>(), ((o.w2 >> 8) & 7) | 2u, o.owner);
+    if constexpr (V6)
+        return ck_miss_tag(ct_hash4(ct_hash4(o.sa.x, o.sa.y, o.sa.z, o.sa.w),
+                                    ct_hash4(o.da.x, o.da.y, o.da.z, o.da.w), 0u, rw), rw);
+    else
+        return ck_miss_tag(ct_hash4(o.sa, o.da, 0u, rw), rw);
+}
+
 // one wave per word (lane l: header 64 w + l), four words per block and
 // step, grid-stride (every thread runs the same number of steps)
 template <bool V6, bool TWO>
@@ -505,7 +607,7 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0, nrk = 0;
+    uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0, nrk = 0, full = 0;
     for (uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < O.W.words;
          w += (uint64_t)gridDim.x * 4) {
         if (lane == 0)
@@ -524,24 +626,31 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
             const uint32_t r = cs & CFC_CT_RES_MASK;
             const bool dropped = st == last && drop;
             if (r == CT_NEW) {
+                const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+                uint32_t *const rset = O.cbloom + O.cb_mask + 1;
                 if (dropped) {   // (a probe's is counted from its bit)
-                    nnd += !probe_tag((st ? O.ck2 : O.ck1)[i]);
+                    nnd += !probe_tag(tg);
+                    if (tag_ok(tg) && (tg & 1)) {   // an ICMP error's key
+                        full += !rel_put(rset, O.cb_mask, tg, true);
+                        nrk++;
+                    }
                     continue;
                 }
                 ncr++;
-                if (!O.cbloom)
+                if (!tag_ok(tg)) {
+                    nun++;
                     continue;
-                if (O.tagged) {
-                    const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
-                    if (tag_ok(tg)) {
-                        cb_put(O, tag_key(tg));
-                        nrk += tg & 1u;
-                    } else {
-                        nun++;
-                    }
-                } else {
-                    cb_put(O, prekey<V6>(A, i, st));
                 }
+                if (tg & 1) {   // an ICMP error's k2, created (its own related entry)
+                    full += !rel_put(rset, O.cb_mask, tg, true);
+                    nrk++;
+                    continue;
+                }
+                full += !set_put(O.cbloom, O.cb_mask, tg);
+                const uint32_t rt = rel_tag<V6>(A, i, st);
+                O.rtag[TWO ? 2 * i + st : i] = rt;
+                if (rt)
+                    full += !rel_put(rset, O.cb_mask, rt, false);
             } else if (r == CT_ESTABLISHED) {
                 nest++;
                 if (!dropped)
@@ -566,63 +675,36 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
     block_add(&O.cnt[ORD_NESTDROP], ndt);
     block_add(&O.cnt[ORD_UNTAGGED], nun);
     block_add(&O.cnt[ORD_RELBOUND], nrk);
+    block_add(&O.cnt[ORD_SETFULL], full);
 }
 
-// header i's participating stages (bit st): from its work bit, every allowed
-// CT_NEW stage and every dropped one that is not a probe (an ICMP error's,
-// an untagged one: always); from its probe bit, each probe whose key a
-// create of the batch may write (the creates' filter).  *nrk: its ICMP
-// errors' stages
+// the probes: a dropped CT_NEW stage whose tag the set holds shares the
+// entry and takes part (a create of the batch may write its key)
 template <bool V6, bool TWO>
-__device__ __forceinline__ uint32_t part_bits(const CtaArgs &A, const OrdArgs &O, uint64_t i,
-                                              bool work, uint32_t &nrk)
+__global__ __launch_bounds__(256) void k_ord_probe_w(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
-    const uint32_t cb = A.ctb[i];
-    const bool drop = A.ver[i] == DROP_POLICY;
-    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
-    uint32_t bits = 0;
-#pragma unroll
-    for (int st = 0; st < NST; st++) {
-        const uint32_t cs = (cb >> (4 * st)) & 0xF;
-        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
-            continue;
-        const bool dropped = st == last && drop;
-        if (!dropped) {
-            bits |= work ? 1u << st : 0u;
-            continue;
-        }
-        const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
-        if (probe_tag(tg) == work)   // (the other bit's stage)
-            continue;
-        bool take;
-        if (O.tagged) {
-            take = !tag_ok(tg) || (tg & 1) || (O.cbloom && cb_maybe(O, tag_key(tg)));
-            nrk += tag_ok(tg) && (tg & 1);
-        } else {   // (the pre-key filter)
-            const PreIn<V6> f = pre_in<V6>(A, i);
-            take = icmp_error<V6>(f.mt, f.pt) || (O.cbloom && cb_maybe(O, prekey_of<V6>(A, f, st)));
-        }
-        bits |= take ? 1u << st : 0u;
-    }
-    return bits;
-}
-
-template <bool V6, bool TWO>
-__global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
-{
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t nrk = 0;
-    // (one wave per word, as k_ord_mark_w; uniform steps: block_count_n)
     for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < O.W.words; w0 += (uint64_t)gridDim.x * 4) {
         const uint64_t w = w0 + (threadIdx.x >> 6), i = 64 * w + lane;
         uint32_t bits = 0;
-        if (w < O.W.words) {
-            if ((O.W.bits[w] >> lane) & 1)
-                bits |= part_bits<V6, TWO>(A, O, i, true, nrk);
-            if ((O.W.probe[w] >> lane) & 1) {
-                uint32_t k = 0;
-                bits |= part_bits<V6, TWO>(A, O, i, false, k);
+        if (w < O.W.words && ((O.W.probe[w] >> lane) & 1)) {
+#pragma unroll
+            for (int st = 0; st < NST; st++) {
+                const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+                if (!probe_tag(tg))
+                    continue;
+                // (a probe bit's stages: dropped CT_NEW, the header's last)
+                const uint32_t cs = (A.ctb[i] >> (4 * st)) & 0xF;
+                if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+                    continue;
+                uint32_t cur;
+                const uint32_t sl = set_find(O.cbloom, O.cb_mask, tg, ~SET_SHARED, cur);
+                if (sl == NONE)
+                    continue;
+                if (!(cur & SET_SHARED))
+                    atomicOr(&O.cbloom[sl], SET_SHARED);
+                bits |= 1u << st;
             }
         }
         uint32_t r = block_count_n(&O.cnt[ORD_NPART], (uint32_t)__popc(bits));
@@ -632,7 +714,48 @@ __global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
             r++;
         }
     }
-    block_add(&O.cnt[ORD_RELBOUND], nrk);
+}
+
+// the work bits' participants: a create or an ICMP error whose entry is
+// shared (its k2's, or a create's related entry's), and every untagged
+// CT_NEW stage
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    const uint32_t lane = threadIdx.x & 63;
+    // (one wave per word, as k_ord_mark_w; uniform steps: block_count_n)
+    for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < O.W.words; w0 += (uint64_t)gridDim.x * 4) {
+        const uint64_t w = w0 + (threadIdx.x >> 6), i = 64 * w + lane;
+        uint32_t bits = 0;
+        if (w < O.W.words && ((O.W.bits[w] >> lane) & 1)) {
+            const uint32_t cb = A.ctb[i];
+            const bool drop = A.ver[i] == DROP_POLICY;
+            const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+            for (int st = 0; st < NST; st++) {
+                const uint32_t cs = (cb >> (4 * st)) & 0xF;
+                if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+                    continue;
+                const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+                const bool dropped = st == last && drop;
+                if (dropped && probe_tag(tg))
+                    continue;   // (the probe pass's)
+                bool take = !tag_ok(tg) || ((tg & 1) ? rel_shared(O, tg) : main_shared(O, tg));
+                if (!take && !dropped && !(tg & 1)) {
+                    const uint32_t rt = O.rtag[TWO ? 2 * i + st : i];
+                    take = rt && rel_shared(O, rt);
+                }
+                bits |= take ? 1u << st : 0u;
+            }
+        }
+        uint32_t r = block_count_n(&O.cnt[ORD_NPART], (uint32_t)__popc(bits));
+        for (uint32_t q = bits; q; q &= q - 1) {
+            if (r < O.part_cap)
+                O.part[r] = (uint32_t)(i << 1) | (uint32_t)(__ffs(q) - 1);
+            r++;
+        }
+    }
 }
 
 // a deleting stage on a slot only deletes: all but its first delete see
@@ -860,10 +983,11 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         else                                                                             \
             hipLaunchKernelGGL((K<V6, false>), dim3(grid), dim3(256), 0, s, __VA_ARGS__); \
     } while (0)
-    // the mark / collect pass: over the launch's work list, or the batch
+    // the mark / collect pass: over the launch's work bits, or the batch
+    const unsigned gw = (unsigned)std::min<uint64_t>((O.W.words + 3) / 4, 8192);
     auto mark = [&]() {
         if (O.sparse)
-            ORD_LAUNCH(k_ord_mark_w, (unsigned)std::min<uint64_t>((O.W.words + 3) / 4, 8192), A, O);
+            ORD_LAUNCH(k_ord_mark_w, gw, A, O);
         else
             ORD_LAUNCH(k_ord_mark, g, A, O);
     };
@@ -892,7 +1016,8 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     O.tagged = A.ck1 && (!two || A.ck2) && !A.lbr;
     O.vec = ((uintptr_t)A.ctb & 15) == 0 && ((uintptr_t)A.ver & 15) == 0 &&
             ((uintptr_t)A.ck1 & 15) == 0 && ((uintptr_t)A.ck2 & 15) == 0;
-    if (!filter(B.creates_hint))
+    O.sparse = O.sparse && O.W.bits && O.W.words && O.tagged && O.rtag;
+    if (!O.sparse && !filter(B.creates_hint))
         return -ENOMEM;
     // from the first mark on, the per-slot state (delete bits, mixed bits,
     // first-delete orders) must be zero again when this returns, on every
@@ -910,23 +1035,64 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
                          hipSuccess;
         }
     } clear{O, s};
-    O.sparse = O.sparse && O.W.bits && O.W.words;
-    mark();
-    if (!rd())
-        return -EIO;
-    if (O.sparse && hc[ORD_NDEL]) {
-        // a batch that deletes: the dense passes (an allowed ESTABLISHED
-        // stage of a deleted slot, a plain hit outside the list, takes part;
-        // the marks and filter inserts made are idempotent)
-        O.sparse = false;
-        if (hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
+    bool done = false;   // (the sparse passes ran to the participants)
+    if (O.sparse) {
+        // the key sets instead of the filter: two tables of 4 words per tag
+        // they may take (a create's, its related entry's, an ICMP error's),
+        // and the participants' list sized by the last batch; mark, probe and
+        // collect back to back, one wait for all their counts
+        uint32_t words = 1u << 16;
+        while (words < 8ull * B.creates_hint + 4096 && words < (1u << 28))
+            words *= 2;
+        const uint64_t cap0 = std::max<uint64_t>(B.part.bytes / 4, 2ull * B.part_hint + 65536);
+        if (B.fpset.ensure(8ull * words) ||
+            hipMemsetAsync(B.fpset.p, 0, 8ull * words, s) != hipSuccess ||
+            B.part.ensure(4 * std::min<uint64_t>(cap0, 0x3FFFFFFFull)))
+            return -ENOMEM;
+        O.cbloom = (uint32_t *)B.fpset.p;
+        O.cb_mask = words - 1;
+        O.part = (uint32_t *)B.part.p;
+        O.part_cap = (uint32_t)std::min<uint64_t>(B.part.bytes / 4, 0x3FFFFFFFull);
+        mark();
+        ORD_LAUNCH(k_ord_probe_w, gw, A, O);
+        ORD_LAUNCH(k_ord_collect_w, gw, A, O);
+        if (!rd())
             return -EIO;
+        if (hc[ORD_NDEL] || hc[ORD_UNTAGGED] || hc[ORD_SETFULL]) {
+            // a batch that deletes (an allowed ESTABLISHED stage of a
+            // deleted slot, a plain hit outside the bits, takes part), with
+            // an untagged create, or whose keys the sets cannot hold: the
+            // dense passes on the filter (the delete marks made are
+            // idempotent)
+            O.sparse = false;
+            if (!filter(std::max(B.creates_hint, hc[ORD_NCREATE])) ||
+                hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
+                return -EIO;
+            mark();
+            if (!rd())
+                return -EIO;
+        } else {
+            if (hc[ORD_NPART] > O.part_cap) {   // (a longer list than the room: again)
+                if (B.part.ensure(4ull * hc[ORD_NPART]) ||
+                    hipMemsetAsync(O.cnt + ORD_NPART, 0, 4, s) != hipSuccess)
+                    return -ENOMEM;
+                O.part = (uint32_t *)B.part.p;
+                O.part_cap = hc[ORD_NPART];
+                ORD_LAUNCH(k_ord_probe_w, gw, A, O);
+                ORD_LAUNCH(k_ord_collect_w, gw, A, O);
+                if (!rd())
+                    return -EIO;
+            }
+            done = true;
+        }
+    } else {
         mark();
         if (!rd())
             return -EIO;
     }
     const bool untagged = O.tagged && hc[ORD_UNTAGGED];
-    if (untagged || (hc[ORD_NCREATE] > 4ull * (O.cb_mask + 1) && O.cb_mask + 1 < (1u << 26))) {
+    if (!done &&
+        (untagged || (hc[ORD_NCREATE] > 4ull * (O.cb_mask + 1) && O.cb_mask + 1 < (1u << 26)))) {
         // (the delete marks are idempotent; the counts start again)
         O.tagged = O.tagged && !untagged;
         if (!filter(hc[ORD_NCREATE]) || hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
@@ -939,29 +1105,29 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     B.creates_hint = ncr;
     O.ndel = hc[ORD_NDEL];
     clear.need = O.ndel != 0;   // (mark sets per-slot state only for deletes)
-    if (!ncr)
-        O.cbloom = nullptr;
-    if (O.ndel)
-        ORD_LAUNCH(k_ord_mixed, gn, A, O);
-    // one collect, into room for every stage that may take part
-    const uint64_t cap = (uint64_t)ncr + hc[ORD_NNEWDROP] + (O.ndel ? hc[ORD_NEST] : 0u);
-    if (cap > 0x3FFFFFFFull)
-        return -E2BIG;
-    if (!cap)
-        return 0;
-    if (B.part.ensure(4 * cap))
-        return -ENOMEM;
-    O.part = (uint32_t *)B.part.p;
-    O.part_cap = (uint32_t)cap;
-    if (O.sparse)
-        ORD_LAUNCH(k_ord_collect_w, (unsigned)std::min<uint64_t>((O.W.words + 3) / 4, 8192), A, O);
-    else
+    if (!done) {
+        if (!ncr)
+            O.cbloom = nullptr;
+        if (O.ndel)
+            ORD_LAUNCH(k_ord_mixed, gn, A, O);
+        // one collect, into room for every stage that may take part
+        const uint64_t cap = (uint64_t)ncr + hc[ORD_NNEWDROP] + (O.ndel ? hc[ORD_NEST] : 0u);
+        if (cap > 0x3FFFFFFFull)
+            return -E2BIG;
+        if (!cap)
+            return 0;
+        if (B.part.ensure(4 * cap))
+            return -ENOMEM;
+        O.part = (uint32_t *)B.part.p;
+        O.part_cap = (uint32_t)cap;
         ORD_LAUNCH(k_ord_collect, g, A, O);
-    if (!rd())
-        return -EIO;
+        if (!rd())
+            return -EIO;
+    }
     const uint64_t np = hc[ORD_NPART];
-    if (np > cap)
+    if (np > O.part_cap)
         return -EIO;
+    B.part_hint = (uint32_t)np;
     static const bool dbg = getenv("CFC_DEBUG_ORDER") != nullptr;
     if (dbg)
         fprintf(stderr,
