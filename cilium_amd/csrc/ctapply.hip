@@ -1203,23 +1203,29 @@ __device__ __forceinline__ uint32_t hit_sig(const CtaArgs &A, uint32_t ord)
     return 1u | (uint32_t)st << 1 | act << 2 | (mt & CFC_HF_TCP_CLOSE ? 1u : 0u) << 4 |
            tfl << 8 | proto << 16;
 }
+// (each op's signature computed once: the block's in LDS, the one before
+// the block's first by its first thread)
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx, uint32_t ncx,
                                                    uint8_t *keep)
 {
+    __shared__ uint32_t ssig[257];
     const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    const uint64_t omask = (1ull << A.ob) - 1;
+    const uint64_t v = r < ncx ? cx[r] : ~0ull, vp = (r > 0 && r <= ncx) ? cx[r - 1] : ~0ull;
+    const uint64_t sl = v >> A.ob;
+    // a plain hit on a slot this batch does not write: its signature (a
+    // written slot keeps every hit: after the write each one counts)
+    const bool cand = sl <= A.mask && (vp >> A.ob) == sl && !(A.ms[(uint32_t)sl].x & MARK_PUTC);
+    const uint32_t mine = sl <= A.mask ? hit_sig<V6>(A, (uint32_t)(v & omask)) : 0u;
+    ssig[threadIdx.x + 1] = mine;
+    if (threadIdx.x == 0)
+        ssig[0] = (cand && (vp >> A.ob) <= A.mask) ? hit_sig<V6>(A, (uint32_t)(vp & omask)) : 0u;
+    __syncthreads();
     if (r >= ncx)
         return;
-    const uint64_t omask = (1ull << A.ob) - 1;
-    bool k = (cx[r] >> A.ob) <= A.mask;   // (an unused place of round 1: dropped)
-    // (a slot this batch writes keeps every hit: after the write each one
-    // counts in the fold)
-    if (k && r > 0 && (cx[r] >> A.ob) == (cx[r - 1] >> A.ob) &&
-        !(A.ms[(uint32_t)(cx[r] >> A.ob)].x & MARK_PUTC)) {
-        const uint32_t s1 = hit_sig<V6>(A, (uint32_t)(cx[r] & omask));
-        k = !s1 || s1 != hit_sig<V6>(A, (uint32_t)(cx[r - 1] & omask));
-    }
-    keep[r] = k;
+    // (an unused place of round 1 is dropped)
+    keep[r] = sl <= A.mask && (!cand || !mine || mine != ssig[threadIdx.x]);
 }
 
 // the monitor length of op `ord` (a header's own stage, not a CT_SERVICE op)
