@@ -3828,7 +3828,7 @@ int ct_apply_one(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int 
                     if (x.loopback)
                         e.bits |= CTB_LB_LOOPBACK;
                 }
-                if (c->hop_nat46)               // a NAT64 hop (conntrack.h:714-716)
+                if (c->hop_nat46 && dir != 1)   // a NAT64 hop's egress create (conntrack.h:714-716)
                     e.bits |= CTB_NAT46;
                 put_new(m, k2, e);
                 if (eg && x.svc && x.addr) {    // the reverse-NAT entry

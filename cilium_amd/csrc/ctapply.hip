@@ -937,7 +937,8 @@ __global__ __launch_bounds__(RQ_B) void k_cta_related(CtaArgs A, const uint64_t 
     const uint32_t l = block_count(&A.cnt[CTA_NLOG], lg);
     uint32_t b = block_count_n(&A.cnt[CTA_NREQB], (uint32_t)rb + (uint32_t)kx);
     const uint32_t fl = ((o.w2 >> 8) & 7) | 2u;
-    const uint32_t dirlen = (o.dir == CT_INGRESS ? 1u << 31 : 0u) | (A.nat46 ? CTLOG_NAT46 : 0u) |
+    const uint32_t dirlen = (o.dir == CT_INGRESS ? 1u << 31 : 0u) |
+                            ((A.nat46 && o.dir == CT_EGRESS) ? CTLOG_NAT46 : 0u) |
                             o.len;
     if (lg && l < A.log_cap) {
         if constexpr (V6) {
@@ -1290,7 +1291,7 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
             e = fresh(A.now, o.is_tcp, o.dir);
             if (wr == SEC_REL)
                 e.bits |= SEEN_NON_SYN;
-            if (A.nat46)   // a NAT64 hop's create (conntrack.h:714-716)
+            if (A.nat46 && o.dir == CT_EGRESS)   // a NAT64 hop's create (conntrack.h:714-716)
                 e.bits |= NAT46;
             live = created = true;
             acct[0] = acct[1] = acct[2] = acct[3] = 0;
@@ -1323,7 +1324,7 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
                 e = fresh(A.now, o.is_tcp, o.dir);
                 if (o.ki_form)
                     e.bits |= SEEN_NON_SYN;
-                if (A.nat46)
+                if (A.nat46 && o.dir == CT_EGRESS)   // (not its local delivery's)
                     e.bits |= NAT46;
                 live = created = true;
                 acct[0] = acct[1] = acct[2] = acct[3] = 0;

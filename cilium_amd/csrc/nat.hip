@@ -154,8 +154,10 @@ __global__ __launch_bounds__(256) void k_nat_scatter(const uint32_t *idx, uint32
     if (out.action)
         out.action[i] = sub.action[k];
     if (out.ct) {
+        // (the hop batch keeps its own second stage — a NAT64 hop's local
+        // delivery, the destination's ipv4_policy lookup: a third CT stage
+        // its apply folds — the header's byte has room for the hop's first)
         const uint32_t c = sub.ct[k] & 0x0F;
-        sub.ct[k] = (uint8_t)c;
         out.ct[i] = (uint8_t)((out.ct[i] & 0x0F) | c << 4);
     }
     if (out.notify) {

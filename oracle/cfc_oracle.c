@@ -420,6 +420,12 @@ struct hop {
     uint16_t owner, sport, dport;
     uint8_t sa[16], da[16];
     int32_t dlen;   /* skb->len change: the IPv4 header is 20 bytes shorter */
+    /* a NAT64 hop delivered locally (ipv4_local_delivery, l3.h:103-131):
+     * the destination's ipv4_policy lookup is a third CT stage, in its CT
+     * maps — its tuple and CT nibble (result | done | create) */
+    uint8_t has2, ct2;
+    uint16_t owner2, sport2, dport2;
+    uint8_t sa2[4], da2[4];
 };
 
 static uint16_t ct_owner(const cfo_t *o, uint16_t lxc)
@@ -877,6 +883,7 @@ static uint32_t notify_site(int mode, uint16_t ep_lxc, const res_t *r)
  * only in the CT port derivation and pass is_fragment = false. */
 /* CT byte of the current header (CTO_*) */
 static _Thread_local uint8_t tl_ct;
+static _Thread_local uint8_t tl_ct3;   /* a NAT64 hop's third stage (struct hop ct2) */
 /* the current header's TCP flag byte (byte 13) and the monitor length each
  * CT stage's lookup returned (0 / TRACE_PAYLOAD_LEN / MTU) */
 static _Thread_local uint8_t tl_tcpfl;
@@ -1009,14 +1016,15 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
     /* *monitor (conntrack.h:221-285, 587-589) against the entry as
      * committed: the batch's own updates are applied afterwards (ct_apply) */
     const struct ctent *ent = NULL;
-    int64_t f = stage == 1 ? fresh_find(k1) : -1, e;
+    /* (stage 2: a NAT64 hop's local delivery, after its IPv4 egress stage) */
+    int64_t f = stage >= 1 ? fresh_find(k1) : -1, e;
     if (f >= 0 || (e = ct_find(o, k1)) >= 0) {
         ent = f >= 0 ? &tl_fresh.ent[f] : &o->ct_ents[e];
         *res = (k1[4 + 2 * alen + 5] & TUPLE_F_RELATED) ? CT_RELATED : CT_REPLY;
         *pdport = td;
     } else {
         tl_lookups++;
-        f = stage == 1 ? fresh_find(k2) : -1;
+        f = stage >= 1 ? fresh_find(k2) : -1;
         if (f >= 0 || (e = ct_find(o, k2)) >= 0)
             ent = f >= 0 ? &tl_fresh.ent[f] : &o->ct_ents[e];
         *res = ent ? CT_ESTABLISHED : CT_NEW;
@@ -1040,7 +1048,10 @@ static int ct_lookup(cfo_t *o, int alen, uint16_t owner, const uint8_t *sa,
     if (*pdport == 0x3500)   /* conn_is_dns: tuple->dport == htons(53) */
         mon = MTU;
     tl_mon[stage] = mon;
-    tl_ct |= (uint8_t)((*res | 4) << (4 * stage));
+    if (stage == 2)
+        tl_ct3 = (uint8_t)(*res | 4);
+    else
+        tl_ct |= (uint8_t)((*res | 4) << (4 * stage));
     return 0;
 }
 
@@ -1414,7 +1425,7 @@ static res_t nat46_ingress(cfo_t *o, const epinfo *ep, uint32_t src, uint32_t sa
     memcpy(sa6 + 12, &sa4, 4);
     memcpy(da6, o->ep_v6[ep->lxc_id], 16);
     tl_hop = (struct hop){HOP_NAT46, 16, p6, CT_INGRESS, ct_owner(o, ep->lxc_id), sp, dport,
-                          {0}, {0}, 20};
+                          {0}, {0}, 20, 0, 0, 0, 0, 0, {0}, {0}};
     memcpy(tl_hop.sa, sa6, 16);
     memcpy(tl_hop.da, da6, 16);
     memcpy(tl_pkt6.sa, sa6, 16);
@@ -1490,8 +1501,12 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     }
     if (skip_proxy)
         verdict = 0;
-    if (res == CT_NEW)
-        tl_ct |= (uint8_t)(CTO_CREATE1 << (4 * stage));   /* ct_create4 */
+    if (res == CT_NEW) {   /* ct_create4 */
+        if (stage == 2)
+            tl_ct3 |= CTO_CREATE1;
+        else
+            tl_ct |= (uint8_t)(CTO_CREATE1 << (4 * stage));
+    }
     if (verdict > 0 && (res == CT_NEW || res == CT_ESTABLISHED)) {
         /* redirect_to_proxy: cb[CB_IFINDEX] = HOST_IFINDEX; TRACE_TO_PROXY
          * from ipv4_redirect_to_host_port (lxc.h:117) */
@@ -1630,12 +1645,21 @@ static res_t lxc_egress_v4(cfo_t *o, uint16_t lxc, uint32_t saddr,
          * packet as it now is */
         metric(o, 0, METRIC_EGRESS, len);
         const uint32_t psa = tl_pkt.sa, pd = tl_pkt.da;
-        /* (after a NAT64 hop the destination's lookup would be a third CT
-         * stage: its writes are not carried) */
+        const uint16_t psp = tl_pkt.sport, pdp = tl_pkt.dport;
+        /* (after a NAT64 hop the destination's lookup is a third CT stage:
+         * recorded with the hop, applied after its IPv4 egress stage) */
         res_t d = lxc_ingress(o, ep, o->seclabel[lxc], 4, (const uint8_t *)&psa,
-                              (const uint8_t *)&pd, proto, tl_pkt.sport,
-                              tl_pkt.dport, hflags & HF_FRAG, hflags & HF_TCP_CLOSE,
+                              (const uint8_t *)&pd, proto, psp, pdp,
+                              hflags & HF_FRAG, hflags & HF_TCP_CLOSE,
                               len, 0, METRIC_EGRESS, st0 + 1);
+        if (st0 == 1 && tl_hop.kind == HOP_NAT64 && (tl_ct3 & 4)) {
+            tl_hop.has2 = 1;
+            tl_hop.owner2 = ct_owner(o, ep->lxc_id);
+            tl_hop.sport2 = psp;
+            tl_hop.dport2 = pdp;
+            memcpy(tl_hop.sa2, &psa, 4);
+            memcpy(tl_hop.da2, &pd, 4);
+        }
         d.identity = dst;
         return d;
     }
@@ -1670,7 +1694,8 @@ static res_t nat64_egress(cfo_t *o, uint16_t lxc, const uint8_t *da6, uint8_t pr
     uint32_t da4;
     memcpy(&da4, da6 + 12, 4);
     tl_nat = NAT64;
-    tl_hop = (struct hop){HOP_NAT64, 4, p4, CT_EGRESS, ct_owner(o, lxc), sp, dp, {0}, {0}, -20};
+    tl_hop = (struct hop){HOP_NAT64, 4, p4, CT_EGRESS, ct_owner(o, lxc), sp, dp, {0}, {0}, -20,
+                          0, 0, 0, 0, 0, {0}, {0}};
     memcpy(tl_hop.sa, &sa4, 4);
     memcpy(tl_hop.da, &da4, 4);
     tl_pkt = (pkt4_t){sa4, da4, sp, dp};
@@ -1726,11 +1751,13 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         res_t r;
         tl_lookups = 0;
         tl_ct = 0;
+        tl_ct3 = 0;
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
         tl_mon[0] = tl_mon[1] = tl_mon[2] = 0;
         tl_fresh.n = 0;
         tl_nat = 0;
         tl_hop.kind = 0;
+        tl_hop.has2 = 0;
         tl_pkt.sa = saddr[i];
         tl_pkt.da = daddr[i];
         tl_pkt.sport = sport[i];
@@ -2001,11 +2028,13 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         const uint8_t *sa = saddr + 16 * i, *da = daddr + 16 * i;
         tl_lookups = 0;
         tl_ct = 0;
+        tl_ct3 = 0;
         tl_tcpfl = tcpflags ? tcpflags[i] : 0;
         tl_mon[0] = tl_mon[1] = tl_mon[2] = 0;
         tl_fresh.n = 0;
         tl_nat = 0;
         tl_hop.kind = 0;
+        tl_hop.has2 = 0;
         memcpy(tl_pkt6.sa, sa, 16);
         memcpy(tl_pkt6.da, da, 16);
         tl_pkt6.sport = sport[i];
@@ -2055,6 +2084,7 @@ void cfo_classify_v6(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         }
         if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
             o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
+        tl_hop.ct2 = tl_hop.has2 ? tl_ct3 : 0;
         o->hop[i] = tl_hop;
         if (o->pkt_out) {
             memcpy(o->pkt_out + 9 * i, tl_pkt6.sa, 16);
@@ -2308,6 +2338,7 @@ static void apply_hop(cfo_t *o, int pass, size_t i, const struct hop *hp, uint8_
                       int32_t verdict, uint32_t len, int syn, uint8_t tfl, uint32_t sec,
                       uint8_t *fresh)
 {
+    (void)i;   /* fresh: this stage's "hit an entry the batch created" flag */
     const int alen = hp->alen, dir = hp->dir, is_tcp = hp->proto == 6;
     uint8_t k1[CTK], k2[CTK];
     int action;
@@ -2321,7 +2352,7 @@ static void apply_hop(cfo_t *o, int pass, size_t i, const struct hop *hp, uint8_
     if (pass == 1) {   /* CONNTRACK_ACCOUNTING of the lookup's hit */
         const int64_t e = b >= CT_REPLY ? e1 : b == CT_ESTABLISHED ? e2 : -1;
         if (e < 0 && b != CT_NEW)
-            fresh[2 * i + 1] = 1;
+            *fresh = 1;
         if (e >= 0) {
             struct ctent *x = &o->ct_ents[e];
             if (dir == CT_INGRESS) {
@@ -2334,15 +2365,17 @@ static void apply_hop(cfo_t *o, int pass, size_t i, const struct hop *hp, uint8_
         }
         return;
     }
-    const uint32_t cnt = fresh[2 * i + 1] ? len : 0;
+    const uint32_t cnt = *fresh ? len : 0;
     if (b == CT_REPLY || b == CT_RELATED) {
         if (e1 >= 0)
             ct_hit_update(o, &o->ct_ents[e1], action, dir, is_tcp, syn, fl, cnt);
     } else if (b == CT_ESTABLISHED) {
         if (e2 >= 0) {
             ct_hit_update(o, &o->ct_ents[e2], action, dir, is_tcp, syn, fl, cnt);
-            if (verdict == DROP_POLICY)
-                o->ct_live[e2] = 0;   /* ct_delete (the hop is the last stage) */
+            /* ct_delete at the stage that drops: the hop's, unless a NAT64
+             * hop's local delivery follows it (the destination's) */
+            if (verdict == DROP_POLICY && (!hp->has2 || hp->dir == CT_INGRESS))
+                o->ct_live[e2] = 0;
         }
     } else if (cs & CTO_CREATE1) {
         if (e2 >= 0) {
@@ -2386,6 +2419,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
      * the batch started (one the header's own egress stage created): pass 2
      * counts it, the device did not */
     uint8_t *fresh = calloc(2 * n + 1, 1);
+    uint8_t *fresh3 = calloc(n + 1, 1);   /* (a NAT64 hop's third stage) */
     for (int pass = 1; pass <= 2; pass++)
     for (size_t i = 0; i < n; i++) {
         if (hazard && pass == 1)
@@ -2502,10 +2536,24 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             if (!(cs & CTO_DONE1))
                 continue;
             if (s == 1 && o->hop && i < o->hop_cap && o->hop[i].kind) {
-                apply_hop(o, pass, i, &o->hop[i], cs, verdict[i],
-                          (uint32_t)((int32_t)len[i] + o->hop[i].dlen),
-                          (flags[i] & HF_TCP_CLOSE) != 0, fl,
-                          mode == CFO_MODE_EGRESS ? o->seclabel[ep_lxc] : identity[i], fresh);
+                const struct hop *hp = &o->hop[i];
+                const uint32_t hl = (uint32_t)((int32_t)len[i] + hp->dlen);
+                const uint32_t sec = mode == CFO_MODE_EGRESS ? o->seclabel[ep_lxc] : identity[i];
+                apply_hop(o, pass, i, hp, cs, verdict[i], hl, (flags[i] & HF_TCP_CLOSE) != 0,
+                          fl, sec, fresh + 2 * i + 1);
+                if (hp->has2 && (hp->ct2 & CTO_DONE1)) {
+                    /* a NAT64 hop's local delivery: the destination's
+                     * ipv4_policy lookup, after the hop's egress stage */
+                    struct hop h2 = *hp;
+                    h2.dir = CT_INGRESS;
+                    h2.owner = hp->owner2;
+                    h2.sport = hp->sport2;
+                    h2.dport = hp->dport2;
+                    memcpy(h2.sa, hp->sa2, 4);
+                    memcpy(h2.da, hp->da2, 4);
+                    apply_hop(o, pass, i, &h2, hp->ct2, verdict[i], hl,
+                              (flags[i] & HF_TCP_CLOSE) != 0, fl, sec, fresh3 + i);
+                }
                 continue;
             }
             const int egress_stage = mode == CFO_MODE_EGRESS && s == 0;
@@ -2636,6 +2684,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
     }
     free(hit_idx);
     free(fresh);
+    free(fresh3);
 }
 
 void cfo_ct_apply_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,

@@ -1666,6 +1666,74 @@ def sc_nat46_reply_v4(n=3000, seed=63):
     return t, h, MODE_INGRESS, None, dp
 
 
+def sc_nat64_local_v6(n=2400, seed=65):
+    """NAT64 to a local endpoint: the translated packet's IPv4 destination
+    is an endpoint of this node, so handle_ipv4_from_lxc delivers it
+    locally (ipv4_local_delivery, l3.h:103-131) and the destination's
+    ipv4_policy runs its own ct_lookup4 / ct_create4 — a third CT stage
+    after the IPv6 and the IPv4 egress lookups (its entries without nat46:
+    conntrack.h:714-716 sets it for CT_EGRESS only).  A history stream
+    opens flows; the test stream: their later packets, new flows of several
+    packets (SYN, ACK, data), and NAT64 flows to remote peers beside them."""
+    t, rng, ipc4 = _nat_setup(seed)
+    loc = S.local_v4_addrs(t)
+    # the sender may reach any identity on the flows' ports (identity 0:
+    # the wildcard entry, policy.h:93-101); each endpoint admits the
+    # sender's SECLABEL on some of them only
+    pol = t.policy[S.EP_LXC_ID]
+    add = np.zeros(3, S.POLICY_DT)
+    add["dport"] = S.htons(np.array([80, 53, 443]))
+    add["proto"] = [S.IPPROTO_TCP, S.IPPROTO_UDP, S.IPPROTO_TCP]
+    add["egress"] = 1
+    t.policy[S.EP_LXC_ID] = np.concatenate([pol, add])
+    sec = int(t.seclabel[S.EP_LXC_ID])
+    for lxc in np.unique(t.endpoints["lxc_id"]):
+        p_ = t.policy.get(int(lxc))
+        if p_ is None:
+            continue
+        ing = np.zeros(3, S.POLICY_DT)
+        ing["identity"] = sec
+        ing["dport"] = S.htons(np.array([80, 53, 8080]))
+        ing["proto"] = [S.IPPROTO_TCP, S.IPPROTO_UDP, S.IPPROTO_TCP]
+        t.policy[int(lxc)] = np.concatenate([p_, ing])
+
+    def flows(k, base, local=True):
+        h = _nat64_flows(rng, ipc4, k, base)
+        if local:
+            h.daddr = _mapped(rng.choice(loc, size=k))
+        return h
+    hist = flows(300, 20000)
+    dp = RefDatapath(t)
+    run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    parts, pos = [], []
+
+    def add_(h, p):
+        parts.append(h)
+        pos.append(p)
+    est = S.take(hist, rng.integers(0, len(hist), size=int(n * 0.3)))
+    est.tcpflags = np.where(est.proto == S.IPPROTO_TCP,
+                            rng.choice(np.array([0x10, 0x18], np.uint8), size=len(est)), 0
+                            ).astype(np.uint8)
+    est.length = rng.integers(100, 1500, size=len(est)).astype(np.uint16)
+    add_(est, rng.random(len(est)))
+    new = flows(int(n * 0.2), 40000)
+    at = rng.random(len(new)) * 0.9
+    add_(new, at)
+    for f, p_ in ((0x10, 0.8), (0x18, 0.6)):
+        sel = np.flatnonzero(rng.random(len(new)) < p_)
+        h = S.take(new, sel)
+        h.tcpflags = np.where(h.proto == S.IPPROTO_TCP, f, 0).astype(np.uint8)
+        at = at + rng.random(len(new)) * 0.03
+        add_(h, at[sel])
+    far = flows(int(n * 0.15), 50000, local=False)
+    add_(far, rng.random(len(far)))
+    h = S.concat(parts)
+    h = S.take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
 SCENARIOS = {
     "edge_ingress_v4": sc_edge_ingress,
     "small_ingress_v4": sc_small_ingress,
@@ -1690,6 +1758,7 @@ SCENARIOS = {
     "ct_seq_egress_v6": lambda: _ct_seq_scenario(6, MODE_EGRESS, 28),
     "nat46_egress_v6": sc_nat46_egress_v6,
     "nat46_reply_v4": sc_nat46_reply_v4,
+    "nat64_local_v6": sc_nat64_local_v6,
     "lb_egress_v4": sc_lb_egress,
     "lb_reply_v4": sc_lb_reply,
     "lb_egress_v6": sc_lb_egress_v6,

@@ -51,6 +51,27 @@ def test_nat64_egress_vs_oracle(torch, chunks):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("chunks", [1, 2])
+def test_nat64_local_delivery_vs_oracle(torch, chunks):
+    """NAT64 to an endpoint of this node: the hop's IPv4 egress delivers
+    locally (l3.h:103-131) and the destination's ipv4_policy runs a third CT
+    stage in its CT maps — its creates without nat46 (conntrack.h:714-716),
+    its deletes at that stage.  The nat64_local_v6 fixture's tables (the
+    reference's run pins the oracle there, test_oracle_golden) and its
+    stream three times over, shuffled, against the sequential oracle."""
+    import golden_io as G
+    from test_gpu_ctorder import check, run_both
+    g = G.Golden("nat64_local_v6")
+    rng = np.random.default_rng(7)
+    h = S.concat([g.headers] * 3)
+    h = S.take(h, rng.permutation(len(h)))
+    gg, want = run_both(torch, g.tables, h, MODE_EGRESS, S.EP_LXC_ID, clock=1003,
+                        chunks=chunks)
+    check(gg, want)
+    assert gg["stats"]["nat_hops"] > 3000, gg["stats"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", [MODE_INGRESS, MODE_FULL])
 def test_nat46_reply_vs_oracle(torch, mode):
     from test_gpu_ctorder import check, run_both
