@@ -374,6 +374,18 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                 }
             } else if (o.kind == OP_CREATE) {
                 put(pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP)));
+                if (!o.is_tcp && !o.ki_form) {
+                    // its related entry (ct_create4/6's second write) may
+                    // overwrite a live one: route runs before the inserts
+                    // here, so that slot is marked now, and its hits go to
+                    // the fold in order with the overwrite (every other slot
+                    // an insert writes is new: the launch saw no hit on it)
+                    const uint32_t rw =
+                        ct_word(icmp_proto<V6>(), ((o.w2 >> 8) & 7) | 2u, o.owner);
+                    const uint32_t rs = find(A, o.sa, o.da, 0u, rw);
+                    if (rs != NONE)
+                        order_mark(A, rs, MARK_ORDERED | MARK_PUTC);
+                }
             }
         }
     }
