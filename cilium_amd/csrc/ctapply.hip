@@ -1695,36 +1695,64 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
 #pragma unroll
         for (int u = 0; u < FU; u++)
             any |= (m[u] != 0u) << u;
-        for (uint32_t mm = any; mm; mm &= mm - 1) {
-            const int u = __ffs(mm) - 1;
-            const uint32_t sl = (uint32_t)(s0 + u);
-            St x = load_state(A.tm, sl);
-            const uint32_t w = *slot_w<V6>(A, sl);
+        // the touched slots four at a time, their state loads issued together
+        // (one dependent chain per slot left the pass waiting on each)
+        for (uint32_t mm = any; mm;) {
+            uint32_t sl4[4], m4[4];
+            bool on[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                on[j] = mm != 0;
+                const int u = on[j] ? __ffs(mm) - 1 : 0;
+                mm &= on[j] ? mm - 1 : mm;
+                sl4[j] = (uint32_t)(s0 + u);
+                m4[j] = m[0];
+#pragma unroll
+                for (int q = 1; q < FU; q++)   // (m[u], without dynamic indexing)
+                    m4[j] = u == q ? m[q] : m4[j];
+            }
+            St x4[4];
+            uint32_t w4[4], iy[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                x4[j] = load_state(A.tm, sl4[j]);
+                w4[j] = *slot_w<V6>(A, sl4[j]);
+                iy[j] = A.info[sl4[j]].y;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+            if (!on[j])
+                continue;
+            const uint32_t sl = sl4[j];
+            St x = x4[j];
+            const uint32_t w = w4[j];
+            const uint32_t mu = m4[j];
             if (A.sum)
                 A.sum[sl] = 0;
             else
                 A.ms[sl].x = 0;
             x.bits &= ~(RX_CLOSING | TX_CLOSING);
             const bool is_tcp = (w & 0xFF) == 6;
-            if (is_tcp && (m[u] & (1u << 18)))
+            if (is_tcp && (mu & (1u << 18)))
                 x.bits |= SEEN_NON_SYN;
             x.lifetime = A.now + (is_tcp ? ((x.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP
                                                                     : CT_SYN_TIMEOUT)
                                          : CT_LIFETIME_NONTCP);
-            if (m[u] & (1u << 16)) {
-                const uint32_t seen = (x.seen_rx | (m[u] & 0xFF)) & 0xFF;
+            if (mu & (1u << 16)) {
+                const uint32_t seen = (x.seen_rx | (mu & 0xFF)) & 0xFF;
                 if (x.last_rx + CT_REPORT_INTERVAL < A.now || seen != x.seen_rx)
                     x.last_rx = A.now;
                 x.seen_rx = seen;
             }
-            if (m[u] & (1u << 17)) {
-                const uint32_t seen = (x.seen_tx | ((m[u] >> 8) & 0xFF)) & 0xFF;
+            if (mu & (1u << 17)) {
+                const uint32_t seen = (x.seen_tx | ((mu >> 8) & 0xFF)) & 0xFF;
                 if (x.last_tx + CT_REPORT_INTERVAL < A.now || seen != x.seen_tx)
                     x.last_tx = A.now;
                 x.seen_tx = seen;
             }
             store_state(A.tm, sl, x);
-            A.info[sl].y |= CTI_UPDATED;
+            A.info[sl].y = iy[j] | CTI_UPDATED;
+            }
         }
     }
 }

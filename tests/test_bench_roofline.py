@@ -53,3 +53,28 @@ def test_headline_c2_at_half_of_its_ceiling():
                                     3 << 20, pk, bench.ubench_ceilings())
     assert d["frac"] >= 0.5, d
     assert pk["headers"] == 64 << 20
+
+
+def test_stream_ceiling_measured_and_monotone():
+    """The stream-miss ceiling (scripts/ubench_mix.hip stream mode): more
+    L2 probes per 32-byte stream item, fewer items per second, and a
+    probe-free item runs at a streaming rate."""
+    rates = [bench.stream_ceiling(p) for p in (0.0, 0.5, 1.0, 1.63, 2.0, 4.0, 16.0)]
+    assert all(r for r in rates), rates
+    assert all(a >= b for a, b in zip(rates, rates[1:])), rates
+    assert rates[0] * 32 > 3000   # GB/s of stream with no probes
+
+
+def test_headline_c2_priced_with_its_own_misses():
+    """k_classify_v4 at C2 is priced with its misses as the coalesced header
+    stream they are (33 B per header), its L2 hits spread over it: the
+    stream model is what the line's frac uses, and the kernel sits below
+    that ceiling."""
+    e = next(x for x in DB if x["workload"] == "c2")
+    pk = e["kernels"]["k_classify_v4"]
+    d, t_ideal, _ = bench.kernel_roofline("k_classify_v4", pk["headers"], pk["avg_ms"],
+                                          3 << 20, pk, bench.ubench_ceilings(),
+                                          bench.STREAM_V4)
+    st = d["stream_model"]
+    assert st and st["random_misses_per_launch"] < 0.2 * st["stream_lines_per_launch"], d
+    assert 0.5 <= d["frac"] <= 1.0, d
