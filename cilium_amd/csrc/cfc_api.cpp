@@ -3212,6 +3212,10 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         if (int rc = ord_resolve(A, O, c->ordb, V6, &changed, s))
             return rc;
         A.sparse = A.sparse && O.sparse;   // (a batch that deletes: the dense scan)
+        if (A.sparse) {   // (the ordering's list of the work bits)
+            A.wl = O.wl;
+            A.nwl = O.cnt + ORD_NWL;
+        }
         if (pkt6)
             if (int rc = ord_pkt6(A, (const uint8_t *)c->ord_ct0.p, *out, s))
                 return rc;

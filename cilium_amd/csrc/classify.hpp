@@ -223,6 +223,9 @@ struct CtaArgs {
     // batch, and route takes the hit slots from ck1 / ck2 (hs is not written)
     WList W;
     bool sparse;
+    // (sparse, after the ordering's sparse passes) the work bits as a list of
+    // header indices, *nwl long (OrdArgs.wl): the scan runs a lane per entry
+    const uint32_t *wl, *nwl;
     // an egress batch with a load balancer: per header LbRec4 / LbRec6 (its
     // CT_SERVICE ops are virtual headers n..2n-1), null otherwise
     void *lbr;
@@ -320,7 +323,7 @@ struct DevBuf {
 // the apply proper
 enum { ORD_NPART, ORD_NCREATE, ORD_NDEL, ORD_NNEWDROP, ORD_NEST, ORD_NESTDROP, ORD_UNTAGGED,
        ORD_RELBOUND, ORD_NRELKEY, ORD_NREL,
-       ORD_COLL, ORD_SETFULL, ORD_CHANGED, ORD_NCNT };
+       ORD_COLL, ORD_SETFULL, ORD_NWL, ORD_NUL, ORD_CHANGED, ORD_NCNT };
 struct OrdArgs {
     uint8_t *ctb;                 // the batch's CT bytes (rewritten in place)
     uint32_t *ck1, *ck2;          // the classify launch's hit keys (or null)
@@ -354,9 +357,17 @@ struct OrdArgs {
     // key tags, cb_mask + 1 words; bit 1 of an entry: shared) and per header
     // stage a create's related-entry tag (the apply's hs, unused then)
     uint32_t *rtag;
+    // (sparse) the work bits as a list of header indices (ORD_NWL long,
+    // k_ord_list_w): the passes run a lane per listed header, not a wave per
+    // word of a few percent set bits (ORD_NUL: the UDP / ICMP creates)
+    uint32_t *wl;
+    // (sparse) a Bloom filter of the main set's tags (pf_mask + 1 words,
+    // about 16 bits per create: cache-resident) the probes test first
+    uint32_t *pfilt;
+    uint32_t pf_mask;
 };
 struct OrdBufs {
-    DevBuf part, rel_src, rk, rh, rh2, ridx, ridx2, pinfo, nres, tmp, fpset;
+    DevBuf part, rel_src, rk, rh, rh2, ridx, ridx2, pinfo, nres, tmp, fpset, wl;
     uint32_t creates_hint = 0;   // the last batch's creates: the filter's size
     uint32_t part_hint = 0;      // the last batch's participants: the list's room
 };

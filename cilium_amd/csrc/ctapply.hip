@@ -326,8 +326,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                 A.reqA[r] = v;
         }
     };
-    for (uint64_t m = t < A.W.words ? A.W.bits[t] : 0; m; m &= m - 1) {
-        const uint64_t i = 64 * t + (uint64_t)(__ffsll((long long)m) - 1);
+    auto one = [&](uint64_t i) {
         ScanIn<V6> r;
         load_in<V6, false>(A, i, r);
         r.k1 = A.ck1[i];
@@ -388,6 +387,14 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                 }
             }
         }
+    };
+    if (A.wl) {   // (the list: a lane per work header, grid-stride)
+        const uint32_t nl = *A.nwl;
+        for (uint64_t x = t; x < nl; x += (uint64_t)gridDim.x * 256)
+            one(A.wl[x]);
+    } else {
+        for (uint64_t m = t < A.W.words ? A.W.bits[t] : 0; m; m &= m - 1)
+            one(64 * t + (uint64_t)(__ffsll((long long)m) - 1));
     }
     __syncthreads();
     const uint32_t ns = min(s_n, SCANW_STAGE);
@@ -2199,7 +2206,7 @@ int cta_scan_t(const CtaArgs &A, hipStream_t s)
         return hipGetLastError() == hipSuccess ? 0 : -EIO;
     }
     if (A.sparse) {   // (the launch's work bits; A.ck1 / A.ck2 and A.sum set)
-        const unsigned g = (unsigned)((A.W.words + 255) / 256);
+        const unsigned g = A.wl ? 1024u : (unsigned)((A.W.words + 255) / 256);
         if (A.mode == CFC_MODE_EGRESS)
             hipLaunchKernelGGL((k_cta_scan_w<V6, true>), dim3(g), dim3(256), 0, s, A);
         else

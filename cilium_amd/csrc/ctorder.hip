@@ -600,23 +600,64 @@ __device__ __forceinline__ uint32_t rel_tag(const CtaArgs &A, uint64_t i, int st
         return ck_miss_tag(ct_hash4(o.sa, o.da, 0u, rw), rw);
 }
 
-// one wave per word (lane l: header 64 w + l), four words per block and
-// step, grid-stride (every thread runs the same number of steps)
+// the work bits as a list of header indices (in any order — the sets, the
+// delete marks and the participants' list are order-free), and the probe
+// bits' count.  A block per 1024 words (one atomic per block and counter:
+// same-address atomics serialise): a thread per four words counts, then
+// each wave writes 256 words' indices, a lane per bit, at consecutive
+// positions.
+constexpr uint32_t LISTW = 1024;
+__global__ __launch_bounds__(256) void k_ord_list_w(OrdArgs O)
+{
+    __shared__ uint64_t s_b[LISTW];
+    __shared__ uint32_t s_r[LISTW];
+    const uint64_t w0 = (uint64_t)blockIdx.x * LISTW;
+    uint32_t c = 0, np = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint64_t w = w0 + 4 * threadIdx.x + j;
+        const uint64_t wb = w < O.W.words ? O.W.bits[w] : 0ull;
+        np += w < O.W.words ? (uint32_t)__popcll(O.W.probe[w]) : 0u;
+        s_b[4 * threadIdx.x + j] = wb;
+        s_r[4 * threadIdx.x + j] = c;
+        c += (uint32_t)__popcll(wb);
+    }
+    const uint32_t base = block_count_n(&O.cnt[ORD_NWL], c);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        s_r[4 * threadIdx.x + j] += base;
+    block_add(&O.cnt[ORD_NNEWDROP], np);   // (syncs: s_b / s_r written)
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1;
+    for (uint32_t k = (LISTW / 4) * wv; k < (LISTW / 4) * (wv + 1); k++) {
+        const uint64_t b = s_b[k];
+        if ((b >> lane) & 1)
+            O.wl[s_r[k] + (uint32_t)__popcll(b & below)] = (uint32_t)(64 * (w0 + k)) + lane;
+    }
+}
+
+// the probe filter (OrdArgs.pfilt): a main-set tag's Bloom bits
+__device__ __forceinline__ uint32_t *pf_word(const OrdArgs &O, uint32_t tg)
+{
+    return O.pfilt + ((tg * 0x9E3779B1u) >> 6 & O.pf_mask);
+}
+
+// a lane per work-list entry, grid-stride over its device count: the
+// creates' tags into the sets (and the probe filter), the ICMP errors' into
+// the related set, the deletes' marks (the UDP / ICMP creates' related-entry
+// tags, which need the header decoded, are k_ord_rel_w's)
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
-    const uint32_t lane = threadIdx.x & 63;
     uint32_t ncr = 0, ndel = 0, nnd = 0, nest = 0, ndt = 0, nun = 0, nrk = 0, full = 0;
-    for (uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w < O.W.words;
-         w += (uint64_t)gridDim.x * 4) {
-        if (lane == 0)
-            nnd += (uint32_t)__popcll(O.W.probe[w]);
-        if (!((O.W.bits[w] >> lane) & 1))
-            continue;
-        const uint64_t i = 64 * w + lane;
+    const uint32_t nl = O.cnt[ORD_NWL];
+    uint32_t *const rset = O.cbloom + O.cb_mask + 1;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nl; x += gridDim.x * blockDim.x) {
+        const uint64_t i = O.wl[x];
         const uint32_t cb = A.ctb[i];
         const bool drop = A.ver[i] == DROP_POLICY;
+        const bool tcp = (A.mt[i] & 0xFF) == 6;
         const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
 #pragma unroll
         for (int st = 0; st < NST; st++) {
@@ -627,8 +668,7 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
             const bool dropped = st == last && drop;
             if (r == CT_NEW) {
                 const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
-                uint32_t *const rset = O.cbloom + O.cb_mask + 1;
-                if (dropped) {   // (a probe's is counted from its bit)
+                if (dropped) {   // (a probe bit's stage is the probe pass's)
                     nnd += !probe_tag(tg);
                     if (tag_ok(tg) && (tg & 1)) {   // an ICMP error's key
                         full += !rel_put(rset, O.cb_mask, tg, true);
@@ -647,10 +687,12 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
                     continue;
                 }
                 full += !set_put(O.cbloom, O.cb_mask, tg);
-                const uint32_t rt = rel_tag<V6>(A, i, st);
-                O.rtag[TWO ? 2 * i + st : i] = rt;
-                if (rt)
-                    full += !rel_put(rset, O.cb_mask, rt, false);
+                uint32_t *const fw = pf_word(O, tg);
+                const uint32_t fb = bloom_bits(fmix32(tg));
+                if ((*fw & fb) != fb)
+                    atomicOr(fw, fb);
+                if (tcp)   // (a TCP create writes no related entry)
+                    O.rtag[TWO ? 2 * i + st : i] = 0u;
             } else if (r == CT_ESTABLISHED) {
                 nest++;
                 if (!dropped)
@@ -678,25 +720,125 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
     block_add(&O.cnt[ORD_SETFULL], full);
 }
 
-// the probes: a dropped CT_NEW stage whose tag the set holds shares the
-// entry and takes part (a create of the batch may write its key)
+// the UDP / ICMP creates' related-entry tags into the related set: a lane
+// per work-list entry again (its bytes warm from mark), the decode only for
+// those creates (mark's own registers stay few)
 template <bool V6, bool TWO>
-__global__ __launch_bounds__(256) void k_ord_probe_w(CtaArgs A, OrdArgs O)
+__global__ __launch_bounds__(256) void k_ord_rel_w(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < O.W.words; w0 += (uint64_t)gridDim.x * 4) {
-        const uint64_t w = w0 + (threadIdx.x >> 6), i = 64 * w + lane;
-        uint32_t bits = 0;
-        if (w < O.W.words && ((O.W.probe[w] >> lane) & 1)) {
+    uint32_t full = 0, nu = 0;
+    const uint32_t nl = O.cnt[ORD_NWL];
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nl; x += gridDim.x * blockDim.x) {
+        const uint64_t i = O.wl[x];
+        if ((A.mt[i] & 0xFF) == 6)
+            continue;
+        const uint32_t cb = A.ctb[i];
+        const bool drop = A.ver[i] == DROP_POLICY;
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+#pragma unroll
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (cb >> (4 * st)) & 0xF;
+            if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW || (st == last && drop))
+                continue;
+            const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+            if (!tag_ok(tg) || (tg & 1))   // (mark's: untagged, an ICMP error's k2)
+                continue;
+            const uint32_t rt = rel_tag<V6>(A, i, st);
+            O.rtag[TWO ? 2 * i + st : i] = rt;
+            nu++;
+            if (rt)
+                full += !rel_put(O.cbloom + O.cb_mask + 1, O.cb_mask, rt, false);
+        }
+    }
+    block_add(&O.cnt[ORD_SETFULL], full);
+    block_add(&O.cnt[ORD_NUL], nu);
+}
+
+// the participants a block finds, staged in LDS and taken from the list by
+// one atomic per block (a list atomic per wave or step serialises on the
+// counter); a full stage goes straight to the list
+constexpr uint32_t PSTAGE = 2048;
+struct PartStage {
+    uint32_t n, base;
+    uint32_t v[PSTAGE];
+};
+__device__ __forceinline__ void part_put(PartStage &S, const OrdArgs &O, uint32_t v)
+{
+    const uint32_t q = atomicAdd(&S.n, 1u);
+    if (q < PSTAGE) {
+        S.v[q] = v;
+    } else {
+        const uint32_t r = atomicAdd(&O.cnt[ORD_NPART], 1u);
+        if (r < O.part_cap)
+            O.part[r] = v;
+    }
+}
+// (every thread of the block, after its last part_put)
+__device__ __forceinline__ void part_flush(PartStage &S, const OrdArgs &O)
+{
+    __syncthreads();
+    const uint32_t ns = min(S.n, PSTAGE);
+    if (threadIdx.x == 0)
+        S.base = ns ? atomicAdd(&O.cnt[ORD_NPART], ns) : 0u;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < ns; q += blockDim.x)
+        if (S.base + q < O.part_cap)
+            O.part[S.base + q] = S.v[q];
+}
+
+// the probes: a dropped CT_NEW stage whose tag the set holds shares the
+// entry and takes part (a create of the batch may write its key).  A thread
+// per four headers of the probe bits at a step (16-byte loads of their
+// keys), grid-stride: the filter first, the set on a maybe.
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_probe_v(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    __shared__ PartStage S;
+    if (threadIdx.x == 0)
+        S.n = 0;
+    __syncthreads();
+    const uint64_t ng = 16 * O.W.words;   // (groups of four headers)
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < ng;
+         t += (uint64_t)gridDim.x * 256) {
+        const uint32_t nib = (uint32_t)(O.W.probe[t >> 4] >> (4 * (t & 15))) & 0xFu;
+        if (!nib)
+            continue;
+        const uint64_t i0 = 4 * t;
+        uint32_t cb[4], k1[4], k2[4];
+        if (O.vec && i0 + 4 <= A.n) {
+            // (streamed once, non-temporal: the filter stays in L2)
+            const uint32_t c4 = ld_nt(reinterpret_cast<const uint32_t *>(A.ctb + i0));
+            const uint4 a = ld_nt4(O.ck1 + i0);
+            uint4 b = make_uint4(NONE, NONE, NONE, NONE);
+            if (TWO)
+                b = ld_nt4(O.ck2 + i0);
+            cb[0] = c4 & 0xFF, cb[1] = c4 >> 8 & 0xFF, cb[2] = c4 >> 16 & 0xFF, cb[3] = c4 >> 24;
+            k1[0] = a.x, k1[1] = a.y, k1[2] = a.z, k1[3] = a.w;
+            k2[0] = b.x, k2[1] = b.y, k2[2] = b.z, k2[3] = b.w;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool in = ((nib >> k) & 1) && i0 + k < A.n;
+                cb[k] = in ? A.ctb[i0 + k] : 0u;
+                k1[k] = in ? O.ck1[i0 + k] : NONE;
+                k2[k] = in && TWO ? O.ck2[i0 + k] : NONE;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!((nib >> k) & 1))
+                continue;
 #pragma unroll
             for (int st = 0; st < NST; st++) {
-                const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
-                if (!probe_tag(tg))
-                    continue;
+                const uint32_t tg = st ? k2[k] : k1[k];
                 // (a probe bit's stages: dropped CT_NEW, the header's last)
-                const uint32_t cs = (A.ctb[i] >> (4 * st)) & 0xF;
-                if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+                const uint32_t cs = (cb[k] >> (4 * st)) & 0xF;
+                if (!probe_tag(tg) || !(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+                    continue;
+                const uint32_t fb = bloom_bits(fmix32(tg));
+                if ((*pf_word(O, tg) & fb) != fb)
                     continue;
                 uint32_t cur;
                 const uint32_t sl = set_find(O.cbloom, O.cb_mask, tg, ~SET_SHARED, cur);
@@ -704,58 +846,49 @@ __global__ __launch_bounds__(256) void k_ord_probe_w(CtaArgs A, OrdArgs O)
                     continue;
                 if (!(cur & SET_SHARED))
                     atomicOr(&O.cbloom[sl], SET_SHARED);
-                bits |= 1u << st;
+                part_put(S, O, (uint32_t)((i0 + k) << 1) | (uint32_t)st);
             }
         }
-        uint32_t r = block_count_n(&O.cnt[ORD_NPART], (uint32_t)__popc(bits));
-        for (uint32_t q = bits; q; q &= q - 1) {
-            if (r < O.part_cap)
-                O.part[r] = (uint32_t)(i << 1) | (uint32_t)(__ffs(q) - 1);
-            r++;
-        }
     }
+    part_flush(S, O);
 }
 
 // the work bits' participants: a create or an ICMP error whose entry is
 // shared (its k2's, or a create's related entry's), and every untagged
-// CT_NEW stage
+// CT_NEW stage.  A lane per work-list entry, grid-stride.
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
-    const uint32_t lane = threadIdx.x & 63;
-    // (one wave per word, as k_ord_mark_w; uniform steps: block_count_n)
-    for (uint64_t w0 = (uint64_t)blockIdx.x * 4; w0 < O.W.words; w0 += (uint64_t)gridDim.x * 4) {
-        const uint64_t w = w0 + (threadIdx.x >> 6), i = 64 * w + lane;
-        uint32_t bits = 0;
-        if (w < O.W.words && ((O.W.bits[w] >> lane) & 1)) {
-            const uint32_t cb = A.ctb[i];
-            const bool drop = A.ver[i] == DROP_POLICY;
-            const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    __shared__ PartStage S;
+    if (threadIdx.x == 0)
+        S.n = 0;
+    __syncthreads();
+    const uint32_t nl = O.cnt[ORD_NWL];
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nl; x += gridDim.x * blockDim.x) {
+        const uint64_t i = O.wl[x];
+        const uint32_t cb = A.ctb[i];
+        const bool drop = A.ver[i] == DROP_POLICY;
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
 #pragma unroll
-            for (int st = 0; st < NST; st++) {
-                const uint32_t cs = (cb >> (4 * st)) & 0xF;
-                if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
-                    continue;
-                const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
-                const bool dropped = st == last && drop;
-                if (dropped && probe_tag(tg))
-                    continue;   // (the probe pass's)
-                bool take = !tag_ok(tg) || ((tg & 1) ? rel_shared(O, tg) : main_shared(O, tg));
-                if (!take && !dropped && !(tg & 1)) {
-                    const uint32_t rt = O.rtag[TWO ? 2 * i + st : i];
-                    take = rt && rel_shared(O, rt);
-                }
-                bits |= take ? 1u << st : 0u;
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (cb >> (4 * st)) & 0xF;
+            if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+                continue;
+            const uint32_t tg = (st ? O.ck2 : O.ck1)[i];
+            const bool dropped = st == last && drop;
+            if (dropped && probe_tag(tg))
+                continue;   // (the probe pass's)
+            bool take = !tag_ok(tg) || ((tg & 1) ? rel_shared(O, tg) : main_shared(O, tg));
+            if (!take && !dropped && !(tg & 1)) {
+                const uint32_t rt = O.rtag[TWO ? 2 * i + st : i];
+                take = rt && rel_shared(O, rt);
             }
-        }
-        uint32_t r = block_count_n(&O.cnt[ORD_NPART], (uint32_t)__popc(bits));
-        for (uint32_t q = bits; q; q &= q - 1) {
-            if (r < O.part_cap)
-                O.part[r] = (uint32_t)(i << 1) | (uint32_t)(__ffs(q) - 1);
-            r++;
+            if (take)
+                part_put(S, O, (uint32_t)(i << 1) | (uint32_t)st);
         }
     }
+    part_flush(S, O);
 }
 
 // a deleting stage on a slot only deletes: all but its first delete see
@@ -984,7 +1117,10 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
             hipLaunchKernelGGL((K<V6, false>), dim3(grid), dim3(256), 0, s, __VA_ARGS__); \
     } while (0)
     // the mark / collect pass: over the launch's work bits, or the batch
-    const unsigned gw = (unsigned)std::min<uint64_t>((O.W.words + 3) / 4, 8192);
+    // (the list passes: grid-stride over a device count; a grid of 1024
+    // blocks: their counters' atomics, one per block, serialise)
+    const unsigned gw = 1024;
+    const unsigned gp = 2048;   // (probe_v, grid-stride)
     auto mark = [&]() {
         if (O.sparse)
             ORD_LAUNCH(k_ord_mark_w, gw, A, O);
@@ -1016,7 +1152,8 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     O.tagged = A.ck1 && (!two || A.ck2) && !A.lbr;
     O.vec = ((uintptr_t)A.ctb & 15) == 0 && ((uintptr_t)A.ver & 15) == 0 &&
             ((uintptr_t)A.ck1 & 15) == 0 && ((uintptr_t)A.ck2 & 15) == 0;
-    O.sparse = O.sparse && O.W.bits && O.W.words && O.tagged && O.rtag;
+    O.sparse = O.sparse && O.W.bits && O.W.words && O.tagged && O.rtag &&
+               64 * O.W.words <= 0xFFFFFFFFull;   // (u32 header indices)
     if (!O.sparse && !filter(B.creates_hint))
         return -ENOMEM;
     // from the first mark on, the per-slot state (delete bits, mixed bits,
@@ -1037,24 +1174,36 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     } clear{O, s};
     bool done = false;   // (the sparse passes ran to the participants)
     if (O.sparse) {
-        // the key sets instead of the filter: two tables of 4 words per tag
-        // they may take (a create's, its related entry's, an ICMP error's),
+        // the key sets instead of the filter: two tables of at least 4 words
+        // per create of the last batch (a quarter full: short runs) for the
+        // tags they take (a create's, its related entry's, an ICMP error's),
         // and the participants' list sized by the last batch; mark, probe and
         // collect back to back, one wait for all their counts
-        uint32_t words = 1u << 16;
-        while (words < 8ull * B.creates_hint + 4096 && words < (1u << 28))
+        uint32_t words = 1u << 16, fwords = 1u << 12;
+        while (words < 4ull * B.creates_hint + 4096 && words < (1u << 28))
             words *= 2;
+        while (fwords < B.creates_hint / 2 && fwords < (1u << 26))
+            fwords *= 2;
         const uint64_t cap0 = std::max<uint64_t>(B.part.bytes / 4, 2ull * B.part_hint + 65536);
-        if (B.fpset.ensure(8ull * words) ||
-            hipMemsetAsync(B.fpset.p, 0, 8ull * words, s) != hipSuccess ||
+        if (B.fpset.ensure(8ull * words + 4ull * fwords) ||
+            hipMemsetAsync(B.fpset.p, 0, 8ull * words + 4ull * fwords, s) != hipSuccess ||
             B.part.ensure(4 * std::min<uint64_t>(cap0, 0x3FFFFFFFull)))
             return -ENOMEM;
         O.cbloom = (uint32_t *)B.fpset.p;
         O.cb_mask = words - 1;
+        O.pfilt = O.cbloom + 2ull * words;
+        O.pf_mask = fwords - 1;
         O.part = (uint32_t *)B.part.p;
         O.part_cap = (uint32_t)std::min<uint64_t>(B.part.bytes / 4, 0x3FFFFFFFull);
+        // the work list: room for every header
+        if (B.wl.ensure(4 * 64 * O.W.words))
+            return -ENOMEM;
+        O.wl = (uint32_t *)B.wl.p;
+        hipLaunchKernelGGL(k_ord_list_w, dim3((unsigned)((O.W.words + LISTW - 1) / LISTW)),
+                           dim3(256), 0, s, O);
         mark();
-        ORD_LAUNCH(k_ord_probe_w, gw, A, O);
+        ORD_LAUNCH(k_ord_rel_w, 1024, A, O);
+        ORD_LAUNCH(k_ord_probe_v, gp, A, O);
         ORD_LAUNCH(k_ord_collect_w, gw, A, O);
         if (!rd())
             return -EIO;
@@ -1078,7 +1227,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
                     return -ENOMEM;
                 O.part = (uint32_t *)B.part.p;
                 O.part_cap = hc[ORD_NPART];
-                ORD_LAUNCH(k_ord_probe_w, gw, A, O);
+                ORD_LAUNCH(k_ord_probe_v, gp, A, O);
                 ORD_LAUNCH(k_ord_collect_w, gw, A, O);
                 if (!rd())
                     return -EIO;
@@ -1132,9 +1281,10 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     if (dbg)
         fprintf(stderr,
                 "ord: n %llu creates %u dropped-new %u est %u dropped-est %u deletes %u "
-                "participants %llu tagged %d\n",
+                "participants %llu tagged %d sparse %d work %u udp-creates %u set-words %u\n",
                 (unsigned long long)A.n, ncr, hc[ORD_NNEWDROP], hc[ORD_NEST], hc[ORD_NESTDROP],
-                O.ndel, (unsigned long long)np, (int)O.tagged);
+                O.ndel, (unsigned long long)np, (int)O.tagged, (int)done, hc[ORD_NWL],
+                hc[ORD_NUL], O.cbloom ? O.cb_mask + 1 : 0u);
     if (np) {
         // records: up to twice as many as participants
         const uint64_t nr = 2 * np;
