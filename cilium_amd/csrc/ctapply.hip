@@ -2149,12 +2149,143 @@ unsigned blocks_for(uint64_t n, unsigned cap)
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, cap));
 }
 
+// ---- the request and op lists' sort: keys `home slot << ob | order`, the
+// slots hashed (uniform), many lists a few hundred thousand to a few million
+// long, some laid out for a bound with all-ones keys in the unused places.
+// A device-wide radix sort of 56-bit keys runs seven passes, each two fills
+// and a launch (≈ 35 µs per pass at these sizes, launch- and
+// lookback-bound).  Instead: the keys go into 2048 buckets by their top 11
+// bits (a count, a scan, a scatter — per block an LDS histogram and one
+// global atomic per bucket it holds, so a hot slot's many ops cost no
+// same-address storm), and a segmented radix sort orders each bucket on the
+// bits below (one block per bucket; fewer than rocprim's partitioning
+// threshold of 3000 segments, whose size split reads counts back to the
+// host); all-ones keys are left out and come back all-ones at the end.
+constexpr uint32_t BKT_BITS = 11, BKT_N = 1u << BKT_BITS, BKT_CH = 4096, BKT_MIN = 1u << 15;
+struct BktArgs {
+    const uint64_t *in;
+    uint64_t *out;
+    uint32_t n, shift;
+    uint32_t *cnt, *begin, *end, *cur;   // [BKT_N + 1] each (the last: padding)
+};
+__device__ __forceinline__ uint32_t bkt_of(const BktArgs &B, uint64_t k)
+{
+    return k == ~0ull ? BKT_N : (uint32_t)min<uint64_t>(k >> B.shift, BKT_N - 1);
+}
+// a block per BKT_CH keys: its LDS histogram, then one atomic per bucket
+__global__ __launch_bounds__(256) void k_bkt_count(BktArgs B)
+{
+    __shared__ uint32_t h[BKT_N + 1];
+    for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
+        h[j] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * BKT_CH;
+    for (uint32_t j = threadIdx.x; j < BKT_CH; j += 256)
+        if (base + j < B.n)
+            atomicAdd(&h[bkt_of(B, B.in[base + j])], 1u);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
+        if (h[j])
+            atomicAdd(&B.cnt[j], h[j]);
+}
+// one block: the buckets' places (the padding's after the last) and the
+// scatter's cursors
+__global__ __launch_bounds__(1024) void k_bkt_scan(BktArgs B)
+{
+    __shared__ uint32_t ws[16];
+    constexpr uint32_t PER = (BKT_N + 1024) / 1024;   // (BKT_N + 1 bins)
+    uint32_t v[PER], t = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint32_t j = threadIdx.x * PER + q;
+        v[q] = j <= BKT_N ? B.cnt[j] : 0u;
+        t += v[q];
+    }
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = t;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d)
+            x += y;
+    }
+    if (lane == 63)
+        ws[wv] = x;
+    __syncthreads();
+    uint32_t off = x - t;
+    for (uint32_t k = 0; k < wv; k++)
+        off += ws[k];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint32_t j = threadIdx.x * PER + q;
+        if (j <= BKT_N) {
+            B.begin[j] = off;
+            B.end[j] = off + v[q];
+            B.cur[j] = off;
+        }
+        off += v[q];
+    }
+}
+// a block per BKT_CH keys again: its places taken per bucket by one atomic
+__global__ __launch_bounds__(256) void k_bkt_scatter(BktArgs B)
+{
+    __shared__ uint32_t h[BKT_N + 1];
+    for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
+        h[j] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * BKT_CH;
+    constexpr uint32_t PER = BKT_CH / 256;
+    uint64_t k[PER];
+    uint32_t b[PER], r[PER];
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++) {
+        const uint64_t i = base + q * 256 + threadIdx.x;
+        k[q] = i < B.n ? B.in[i] : 0ull;
+        b[q] = bkt_of(B, k[q]);
+        r[q] = i < B.n ? atomicAdd(&h[b[q]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
+        if (h[j])
+            h[j] = atomicAdd(&B.cur[j], h[j]);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < PER; q++)
+        if (base + q * 256 + threadIdx.x < B.n)
+            B.out[h[b[q]] + r[q]] = k[q];
+}
+
+size_t bkt_scratch_bytes() { return 4ull * 4 * (BKT_N + 1) + 256; }
+
+// pad: the list may hold all-ones keys (a list laid out for a bound)
 int sort_keys(const CtaArgs &A, uint64_t *keys, uint64_t *alt, uint32_t n, int bits,
-              hipStream_t s, uint64_t **sorted)
+              hipStream_t s, uint64_t **sorted, bool pad = true)
 {
     *sorted = keys;
     if (n < 2)
         return 0;
+    if (n >= BKT_MIN && bits > (int)BKT_BITS + 8) {
+        // (scratch after the sorts' temporary storage)
+        const size_t tb0 = A.sort_tmp_bytes - bkt_scratch_bytes();
+        uint32_t *w = reinterpret_cast<uint32_t *>((reinterpret_cast<uintptr_t>(A.sort_tmp) + tb0 + 255) & ~uintptr_t(255));
+        BktArgs B{keys, alt, n, (uint32_t)(bits - (int)BKT_BITS), w, w + (BKT_N + 1),
+                  w + 2 * (BKT_N + 1), w + 3 * (BKT_N + 1)};
+        const unsigned g = (unsigned)((n + BKT_CH - 1) / BKT_CH);
+        if (hipMemsetAsync(B.cnt, 0, 4 * (BKT_N + 1), s) != hipSuccess)
+            return -EIO;
+        hipLaunchKernelGGL(k_bkt_count, dim3(g), dim3(256), 0, s, B);
+        hipLaunchKernelGGL(k_bkt_scan, dim3(1), dim3(1024), 0, s, B);
+        hipLaunchKernelGGL(k_bkt_scatter, dim3(g), dim3(256), 0, s, B);
+        // the padding (all-ones, after the buckets in alt) is no segment:
+        // the output holds all-ones where the segments do not write
+        size_t tb = tb0;
+        if ((pad && hipMemsetAsync(keys, 0xFF, 8ull * n, s) != hipSuccess) ||
+            hipcub::DeviceSegmentedRadixSort::SortKeys(A.sort_tmp, tb, (const uint64_t *)alt, keys,
+                                                       (int)n, (int)BKT_N, (const uint32_t *)B.begin,
+                                                       (const uint32_t *)B.end, 0, (int)B.shift,
+                                                       s) != hipSuccess)
+            return -EIO;
+        return 0;
+    }
     size_t tb = A.sort_tmp_bytes;
     hipcub::DoubleBuffer<uint64_t> db(keys, alt);
     if (hipcub::DeviceRadixSort::SortKeys(A.sort_tmp, tb, db, (int)n, 0, bits, s) !=
@@ -2176,7 +2307,11 @@ size_t cta_sort_tmp_bytes(uint32_t n)
                                         (const uint8_t *)nullptr, (uint64_t *)nullptr,
                                         (uint32_t *)nullptr, (int)std::max<uint32_t>(n, 2u),
                                         (hipStream_t)0);
-    return std::max(tb, ts);
+    size_t tg = 0;   // (the bucketed sort's segments; its scratch after all three)
+    (void)hipcub::DeviceSegmentedRadixSort::SortKeys(
+        nullptr, tg, (const uint64_t *)nullptr, (uint64_t *)nullptr, (int)std::max<uint32_t>(n, 2u),
+        (int)BKT_N, (const uint32_t *)nullptr, (const uint32_t *)nullptr, 0, 64, (hipStream_t)0);
+    return std::max({tb, ts, tg}) + bkt_scratch_bytes();
 }
 
 // an egress batch with a load balancer: the service step of every header
@@ -2191,7 +2326,7 @@ int cta_lb_pre_t(const CtaArgs &A, hipStream_t s)
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     uint64_t *sorted;
-    if (int rc = sort_keys(A, A.reqS, A.reqS2, ns, A.ob + A.slot_bits, s, &sorted))
+    if (int rc = sort_keys(A, A.reqS, A.reqS2, ns, A.ob + A.slot_bits, s, &sorted, false))
         return rc;
     if (ns)
         hipLaunchKernelGGL(k_cta_svc<V6>, dim3((ns + 255) / 256), dim3(256), 0, s, A, sorted, ns);
@@ -2227,7 +2362,7 @@ template <bool V6>
 int cta_newkeys_t(const CtaArgs &A, uint32_t nreqA, uint64_t **sorted, uint32_t *newk,
                   hipStream_t s)
 {
-    if (int rc = sort_keys(A, A.reqA, A.reqA2, nreqA, A.ob + A.slot_bits, s, sorted))
+    if (int rc = sort_keys(A, A.reqA, A.reqA2, nreqA, A.ob + A.slot_bits, s, sorted, false))
         return rc;
     if (hipMemsetAsync(A.cnt + CTA_NEWK, 0, 8, s) != hipSuccess ||   // (NEWK, NEWKT)
         hipMemsetAsync(A.cx, 0, 8ull * (A.rel_mask + 1), s) != hipSuccess)
@@ -2248,7 +2383,7 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     const int bits = A.ob + A.slot_bits;
     uint64_t *sorted = const_cast<uint64_t *>(presorted);
     int rc;
-    if (!sorted && (rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted)))
+    if (!sorted && (rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted, false)))
         return rc;
     // the second round's requests (a create's related and reverse-NAT
     // entries, at most two per create) and their ops' places in the list
