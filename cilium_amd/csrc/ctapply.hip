@@ -1990,12 +1990,13 @@ constexpr int GC_B = 1024;
 __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
 {
     __shared__ uint32_t smaps[CTG_MAX_MAPS], scnt[CTG_MAX_MAPS];
+    __shared__ uint32_t sw[GC_B * GC_U];   // (a step's w words after its deletes)
     for (uint32_t j = threadIdx.x; j < A.n_maps; j += GC_B) {
         smaps[j] = A.maps[j];
         scnt[j] = 0;
     }
     __syncthreads();
-    uint32_t fresh = 0, live = 0, nonfree = 0;
+    uint32_t fresh = 0, live = 0, nonfree = 0, freed = 0;
     const uint64_t stride = (uint64_t)gridDim.x * GC_B * GC_U;
     // (every thread runs the same number of steps: block_count_n needs the
     // whole block)
@@ -2063,51 +2064,56 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
                 *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s) =
                     *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s + 2) = make_ulonglong2(0, 0);
         }
+        // the tails of this step's clusters: a plain tombstone whose run of
+        // tombstones ends at a free slot is freed (a live entry keeps the
+        // tombstones before it: a probe for it runs through them).  The
+        // step's words after its deletes go to LDS and each tombstone walks
+        // forward there; the slot after the step's range is read once at L2.
+        // A slot only goes live -> tombstone -> free here, so a stale read of
+        // it can only keep a tail (one next to another block's slots, which
+        // the next GC frees), never free a slot a probe still runs through.
+        const uint32_t lim = (uint32_t)min<uint64_t>(GC_B * GC_U, A.slots - base);
+        const bool whole = lim == A.slots;   // (the whole table in one step: the walk wraps)
+#pragma unroll
+        for (int u = 0; u < GC_U; u++)
+            sw[u * GC_B + threadIdx.x] = del[u] ? CT_TOMBSTONE : k[u].w;
+        const uint32_t wnext = whole ? 1u
+                                     : __hip_atomic_load(&A.ct4[(base + lim) & A.mask].w,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < GC_U; u++) {
+            const uint32_t c = u * GC_B + threadIdx.x;
+            if (c >= lim || sw[c] != CT_TOMBSTONE)
+                continue;
+            uint32_t e = c, after = 1;
+            for (uint32_t m = 1; m < lim; m++) {
+                if (++e == lim) {
+                    if (!whole) {
+                        after = wnext;
+                        break;
+                    }
+                    e = 0;
+                }
+                if (sw[e] != CT_TOMBSTONE) {
+                    after = sw[e];
+                    break;
+                }
+            }
+            if (after == 0) {
+                A.ct4[base + c].w = 0u;
+                freed++;
+            }
+        }
+        __syncthreads();   // (sw again next step)
     }
+    block_add(&A.cnt[CTG_FREED], freed);
     block_add(&A.cnt[CTG_LIVE], live);
     block_add(&A.cnt[CTG_NONFREE], nonfree);
     block_add(&A.cnt[CTG_FRESH], fresh);
     for (uint32_t j = threadIdx.x; j < A.n_maps; j += GC_B)
         if (scnt[j])
             atomicAdd(&A.mcnt[j], scnt[j]);
-}
-
-// The tail of every cluster: a non-free slot followed by a free one.  Its
-// trailing run of plain tombstones is freed, walking back to the first slot
-// that is not one (a live entry keeps the tombstones before it: a probe
-// for it runs through them).
-__global__ __launch_bounds__(256) void k_ct_trim4(CtGcArgs A)
-{
-    uint32_t freed = 0;
-    // four slots per thread and step, their words (and the next slots')
-    // loaded together
-    const uint64_t stride = (uint64_t)gridDim.x * 256 * GC_U;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256 * GC_U; base < A.slots; base += stride) {
-        uint32_t w[GC_U], wn[GC_U];
-#pragma unroll
-        for (int u = 0; u < GC_U; u++) {   // (no branches: the loads issue together)
-            const uint64_t s = base + u * 256 + threadIdx.x, c = s < A.slots ? s : A.slots - 1;
-            w[u] = A.ct4[c].w;
-            wn[u] = A.ct4[(c + 1) & A.mask].w;
-        }
-#pragma unroll
-        for (int u = 0; u < GC_U; u++)
-            if (base + u * 256 + threadIdx.x >= A.slots)
-                w[u] = 0;
-#pragma unroll
-        for (int u = 0; u < GC_U; u++) {
-            if (w[u] != CT_TOMBSTONE || wn[u] != 0)
-                continue;
-            // (a thread that started inside another's run meets it: each
-            // slot is freed by exactly one CAS)
-            uint32_t j = (uint32_t)(base + u * 256 + threadIdx.x);
-            while (atomicCAS(&A.ct4[j].w, CT_TOMBSTONE, 0u) == CT_TOMBSTONE) {
-                freed++;
-                j = (j - 1) & A.mask;
-            }
-        }
-    }
-    block_add(&A.cnt[CTG_FREED], freed);
 }
 
 // the pending TCP-map ICMP entries (CtLog): lifetime as ct_create4 wrote it
@@ -2547,7 +2553,6 @@ int ct_gc4(const CtGcArgs &A, hipStream_t s)
                                                                (GC_B * GC_U),
                                                            256))),
                        dim3(GC_B), 0, s, A);
-    hipLaunchKernelGGL(k_ct_trim4, dim3(blocks_for(A.slots, 2048)), dim3(256), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
