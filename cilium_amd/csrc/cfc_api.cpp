@@ -178,7 +178,7 @@ struct cfc_ctx {
     // nothing), on again when an apply follows its launch
     bool sum_dirty = false, sum_pending = false, sum_want = true;
     uint64_t log_used = 0;       // CtLog entries since the last sync
-    DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync;
+    DevBuf cta_hs, cta_req, cta_req2, cta_cx, cta_cnt, cta_tmp, cta_log, cta_sync, cta_rk;
     DevBuf cta_lbr, cta_reqs;     // a load balancer's service step per header (LbRec4/6)
     DevBuf cta_obm;               // the apply's ordered-slot bitmap
     // packet-order CT results (ctorder.hip): buffers, the deleted-slot
@@ -3241,6 +3241,13 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
                                     hipEventCreateWithFlags(&c->pend_ev, hipEventDisableTiming) !=
                                         hipSuccess))))
         return -ENOMEM;
+    // (IPv4 sparse scan: the requests' keys for the insert, per header stage)
+    A.rk4 = nullptr;
+    if (!V6 && A.sparse && !A.lbr) {
+        if (c->cta_rk.ensure(16ull * nroute_cap))
+            return -ENOMEM;
+        A.rk4 = (uint4 *)c->cta_rk.p;
+    }
     if (cta_scan(A, V6, s))
         return -EIO;
     if (early) {

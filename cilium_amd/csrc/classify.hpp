@@ -219,6 +219,10 @@ struct CtaArgs {
     uint32_t *sum;
     bool vec;                    // the batch's arrays 16-byte aligned (the scan's loads)
     uint32_t *hs;                // [2n] hit slot per header and stage ([4n] with lbr)
+    // (IPv4, sparse scan) per header stage ([2n] egress, [n] else) the key of
+    // the request the scan made for it — a create's k2, a hit's looked-up
+    // key — so the insert needs no decode; null: decoded there
+    uint4 *rk4;
     // (sparse) the launch's work list: the scan reads it rather than the
     // batch, and route takes the hit slots from ck1 / ck2 (hs is not written)
     WList W;

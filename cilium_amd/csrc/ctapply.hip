@@ -361,6 +361,11 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                     const uint32_t home = (rev ? khash(o.da, o.sa, o.z1, o.w1)
                                                : khash(o.sa, o.da, o.z2, o.w2)) & A.mask;
                     put(pack(A, home, ord_of(i, st, SEC_FHIT)));
+                    if constexpr (!V6)
+                        if (A.rk4)
+                            A.rk4[TWO ? 2 * i + st : i] =
+                                rev ? make_uint4(o.da, o.sa, o.z1, o.w1)
+                                    : make_uint4(o.sa, o.da, o.z2, o.w2);
                     nfh++;
                 } else if (o.kind == OP_DELETE) {
                     order_mark(A, sl, MARK_ORDERED | MARK_DEL);
@@ -373,6 +378,9 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                 }
             } else if (o.kind == OP_CREATE) {
                 put(pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP)));
+                if constexpr (!V6)
+                    if (A.rk4)
+                        A.rk4[TWO ? 2 * i + st : i] = make_uint4(o.sa, o.da, o.z2, o.w2);
                 if (!o.is_tcp && !o.ki_form) {
                     // its related entry (ct_create4/6's second write) may
                     // overwrite a live one: route runs before the inserts
@@ -774,6 +782,23 @@ __device__ __forceinline__ ReqKey<V6> req_key(const CtaArgs &A, uint32_t ord, Op
     return k;
 }
 
+// a request's key from the scan's record of it (IPv4 sparse scan: creates
+// and hits), else decoded
+template <bool V6>
+__device__ __forceinline__ ReqKey<V6> req_key_of(const CtaArgs &A, uint32_t ord)
+{
+    if constexpr (!V6) {
+        const uint32_t sec = ord_sec(ord);
+        if (A.rk4 && (sec == SEC_OP || sec == SEC_FHIT)) {
+            const uint64_t i = ord_hdr(ord);
+            const uint4 v = ld16(A.rk4 + (A.mode == CFC_MODE_EGRESS ? 2 * i + ord_st(ord) : i));
+            return ReqKey<false>{v.x, v.y, v.z, v.w};
+        }
+    }
+    Op<V6> o;
+    return req_key<V6>(A, ord, &o);
+}
+
 // ---- insert: one thread per home slot; keys deduped in registers (a fifth
 // distinct key of one home slot is found by rescanning the run).  A key's
 // first create also writes its related ICMP entry and, with a load
@@ -799,8 +824,7 @@ __global__ __launch_bounds__(RQ_B) void k_cta_insert(CtaArgs A, uint64_t *req, u
         int nk = 0;
         for (uint32_t r = r0; r < nreq && (req[r] >> A.ob) == home; r++) {
             const uint32_t ord = (uint32_t)(req[r] & omask) & ~1u;
-            Op<V6> o;
-            const ReqKey<V6> k = req_key<V6>(A, ord, &o);
+            const ReqKey<V6> k = req_key_of<V6>(A, ord);
             uint32_t slot = NONE;
             for (int j = 0; j < nk; j++)
                 if (kk[j] == k)
@@ -810,8 +834,7 @@ __global__ __launch_bounds__(RQ_B) void k_cta_insert(CtaArgs A, uint64_t *req, u
                 // not among the first four keys: an earlier request of the
                 // run may still have it
                 for (uint32_t q = r0; q < r && nk == 4; q++) {
-                    Op<V6> oq;
-                    if (req_key<V6>(A, (uint32_t)(req[q] & omask) & ~1u, &oq) == k) {
+                    if (req_key_of<V6>(A, (uint32_t)(req[q] & omask) & ~1u) == k) {
                         slot = find(A, k.d, k.s, k.z, k.w);
                         break;
                     }
@@ -2155,40 +2178,88 @@ unsigned blocks_for(uint64_t n, unsigned cap)
     return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(b, cap));
 }
 
-// ---- the request and op lists' sort: keys `home slot << ob | order`, the
-// slots hashed (uniform), many lists a few hundred thousand to a few million
-// long, some laid out for a bound with all-ones keys in the unused places.
-// A device-wide radix sort of 56-bit keys runs seven passes, each two fills
-// and a launch (≈ 35 µs per pass at these sizes, launch- and
-// lookback-bound).  Instead: the keys go into 2048 buckets by their top 11
-// bits (a count, a scan, a scatter — per block an LDS histogram and one
-// global atomic per bucket it holds, so a hot slot's many ops cost no
-// same-address storm), and a segmented radix sort orders each bucket on the
-// bits below (one block per bucket; fewer than rocprim's partitioning
-// threshold of 3000 segments, whose size split reads counts back to the
-// host); all-ones keys are left out and come back all-ones at the end.
+// ---- the request and op lists' sort: keys `home slot << ob | order`,
+// unique, a few hundred thousand to a few million long, some laid out for a
+// bound with all-ones keys in the unused places.  A device-wide radix sort
+// of 56-bit keys runs seven passes, each two fills and a launch (≈ 35 µs per
+// pass at these sizes, launch- and lookback-bound).  Instead the keys go
+// into 2048 buckets (a count, a scan, a scatter — per block an LDS
+// histogram and one global atomic per bucket it holds) and a segmented
+// radix sort orders each bucket (one block per bucket; fewer than rocprim's
+// partitioning threshold of 3000 segments, whose size split reads counts
+// back to the host).  The requests' buckets are their home slots' top 11
+// bits (the slots are hashed: even buckets).  The op list's are bounded by
+// splitters — 4096 keys sampled at even strides, sorted in one workgroup,
+// every second one — found by a binary search in LDS: its ops crowd on hot
+// slots (a hot flow's hits, all ordered by one close), and a bucket per top
+// bits left one block sorting a million keys (89 ms per step on the
+// dependency stream).  All-ones keys are left out and come back all-ones.
 constexpr uint32_t BKT_BITS = 11, BKT_N = 1u << BKT_BITS, BKT_CH = 4096, BKT_MIN = 1u << 15;
+constexpr uint32_t BKT_SAMPLES = 4096;
 struct BktArgs {
     const uint64_t *in;
     uint64_t *out;
-    uint32_t n, shift;
+    uint32_t n, bits;
     uint32_t *cnt, *begin, *end, *cur;   // [BKT_N + 1] each (the last: padding)
+    uint64_t *split;                     // [BKT_N - 1]
 };
-__device__ __forceinline__ uint32_t bkt_of(const BktArgs &B, uint64_t k)
+// the bucket of key k: SPLIT, how many splitters are below it (sp in LDS);
+// else its top BKT_BITS of `bits`
+template <bool SPLIT>
+__device__ __forceinline__ uint32_t bkt_of(const BktArgs &B, const uint64_t *sp, uint64_t k)
 {
-    return k == ~0ull ? BKT_N : (uint32_t)min<uint64_t>(k >> B.shift, BKT_N - 1);
+    if (k == ~0ull)
+        return BKT_N;
+    if (!SPLIT)
+        return (uint32_t)min<uint64_t>(k >> (B.bits - BKT_BITS), BKT_N - 1);
+    uint32_t lo = 0, hi = BKT_N - 1;   // (the answer in [lo, hi])
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sp[mid] < k)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+// one workgroup: the samples sorted (a block radix sort), every second one
+// a splitter
+__global__ __launch_bounds__(512) void k_bkt_sample(BktArgs B)
+{
+    using Sort = hipcub::BlockRadixSort<uint64_t, 512, BKT_SAMPLES / 512>;
+    __shared__ typename Sort::TempStorage ts;
+    uint64_t v[BKT_SAMPLES / 512];
+#pragma unroll
+    for (uint32_t q = 0; q < BKT_SAMPLES / 512; q++)
+        v[q] = B.in[(uint64_t)(threadIdx.x * (BKT_SAMPLES / 512) + q) * B.n / BKT_SAMPLES];
+    Sort(ts).Sort(v, 0, (int)B.bits);   // (all-ones keys: their low bits are all ones, last)
+#pragma unroll
+    for (uint32_t q = 0; q < BKT_SAMPLES / 512; q++) {
+        const uint32_t m = threadIdx.x * (BKT_SAMPLES / 512) + q;   // (blocked: sample m)
+        if (!(m & 1) && m >= 2 && m / 2 - 1 < BKT_N - 1)
+            B.split[m / 2 - 1] = v[q];
+    }
+}
+__device__ __forceinline__ void bkt_load_split(const BktArgs &B, uint64_t *sp)
+{
+    for (uint32_t j = threadIdx.x; j < BKT_N - 1; j += 256)
+        sp[j] = B.split[j];
 }
 // a block per BKT_CH keys: its LDS histogram, then one atomic per bucket
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_bkt_count(BktArgs B)
 {
     __shared__ uint32_t h[BKT_N + 1];
+    __shared__ uint64_t sp[SPLIT ? BKT_N - 1 : 1];
     for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
         h[j] = 0;
+    if (SPLIT)
+        bkt_load_split(B, sp);
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * BKT_CH;
     for (uint32_t j = threadIdx.x; j < BKT_CH; j += 256)
         if (base + j < B.n)
-            atomicAdd(&h[bkt_of(B, B.in[base + j])], 1u);
+            atomicAdd(&h[bkt_of<SPLIT>(B, sp, B.in[base + j])], 1u);
     __syncthreads();
     for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
         if (h[j])
@@ -2232,11 +2303,15 @@ __global__ __launch_bounds__(1024) void k_bkt_scan(BktArgs B)
     }
 }
 // a block per BKT_CH keys again: its places taken per bucket by one atomic
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void k_bkt_scatter(BktArgs B)
 {
     __shared__ uint32_t h[BKT_N + 1];
+    __shared__ uint64_t sp[SPLIT ? BKT_N - 1 : 1];
     for (uint32_t j = threadIdx.x; j <= BKT_N; j += 256)
         h[j] = 0;
+    if (SPLIT)
+        bkt_load_split(B, sp);
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * BKT_CH;
     constexpr uint32_t PER = BKT_CH / 256;
@@ -2246,7 +2321,7 @@ __global__ __launch_bounds__(256) void k_bkt_scatter(BktArgs B)
     for (uint32_t q = 0; q < PER; q++) {
         const uint64_t i = base + q * 256 + threadIdx.x;
         k[q] = i < B.n ? B.in[i] : 0ull;
-        b[q] = bkt_of(B, k[q]);
+        b[q] = bkt_of<SPLIT>(B, sp, k[q]);
         r[q] = i < B.n ? atomicAdd(&h[b[q]], 1u) : 0u;
     }
     __syncthreads();
@@ -2260,11 +2335,12 @@ __global__ __launch_bounds__(256) void k_bkt_scatter(BktArgs B)
             B.out[h[b[q]] + r[q]] = k[q];
 }
 
-size_t bkt_scratch_bytes() { return 4ull * 4 * (BKT_N + 1) + 256; }
+size_t bkt_scratch_bytes() { return 4ull * 4 * (BKT_N + 1) + 8ull * BKT_N + 512; }
 
-// pad: the list may hold all-ones keys (a list laid out for a bound)
+// pad: the list may hold all-ones keys (a list laid out for a bound);
+// crowd: its keys may crowd on a few slots (the op list: splitters)
 int sort_keys(const CtaArgs &A, uint64_t *keys, uint64_t *alt, uint32_t n, int bits,
-              hipStream_t s, uint64_t **sorted, bool pad = true)
+              hipStream_t s, uint64_t **sorted, bool pad = true, bool crowd = false)
 {
     *sorted = keys;
     if (n < 2)
@@ -2273,21 +2349,32 @@ int sort_keys(const CtaArgs &A, uint64_t *keys, uint64_t *alt, uint32_t n, int b
         // (scratch after the sorts' temporary storage)
         const size_t tb0 = A.sort_tmp_bytes - bkt_scratch_bytes();
         uint32_t *w = reinterpret_cast<uint32_t *>((reinterpret_cast<uintptr_t>(A.sort_tmp) + tb0 + 255) & ~uintptr_t(255));
-        BktArgs B{keys, alt, n, (uint32_t)(bits - (int)BKT_BITS), w, w + (BKT_N + 1),
-                  w + 2 * (BKT_N + 1), w + 3 * (BKT_N + 1)};
+        uint64_t *sp = reinterpret_cast<uint64_t *>(
+            (reinterpret_cast<uintptr_t>(w + 4 * (BKT_N + 1)) + 255) & ~uintptr_t(255));
+        BktArgs B{keys, alt, n, (uint32_t)bits, w, w + (BKT_N + 1), w + 2 * (BKT_N + 1),
+                  w + 3 * (BKT_N + 1), sp};
         const unsigned g = (unsigned)((n + BKT_CH - 1) / BKT_CH);
         if (hipMemsetAsync(B.cnt, 0, 4 * (BKT_N + 1), s) != hipSuccess)
             return -EIO;
-        hipLaunchKernelGGL(k_bkt_count, dim3(g), dim3(256), 0, s, B);
+        if (crowd) {
+            hipLaunchKernelGGL(k_bkt_sample, dim3(1), dim3(512), 0, s, B);
+            hipLaunchKernelGGL(k_bkt_count<true>, dim3(g), dim3(256), 0, s, B);
+        } else {
+            hipLaunchKernelGGL(k_bkt_count<false>, dim3(g), dim3(256), 0, s, B);
+        }
         hipLaunchKernelGGL(k_bkt_scan, dim3(1), dim3(1024), 0, s, B);
-        hipLaunchKernelGGL(k_bkt_scatter, dim3(g), dim3(256), 0, s, B);
+        if (crowd)
+            hipLaunchKernelGGL(k_bkt_scatter<true>, dim3(g), dim3(256), 0, s, B);
+        else
+            hipLaunchKernelGGL(k_bkt_scatter<false>, dim3(g), dim3(256), 0, s, B);
         // the padding (all-ones, after the buckets in alt) is no segment:
         // the output holds all-ones where the segments do not write
         size_t tb = tb0;
         if ((pad && hipMemsetAsync(keys, 0xFF, 8ull * n, s) != hipSuccess) ||
             hipcub::DeviceSegmentedRadixSort::SortKeys(A.sort_tmp, tb, (const uint64_t *)alt, keys,
                                                        (int)n, (int)BKT_N, (const uint32_t *)B.begin,
-                                                       (const uint32_t *)B.end, 0, (int)B.shift,
+                                                       (const uint32_t *)B.end, 0,
+                                                       crowd ? bits : bits - (int)BKT_BITS,
                                                        s) != hipSuccess)
             return -EIO;
         return 0;
@@ -2437,7 +2524,7 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     if (ncx64 > A.cx_cap)
         return -EOVERFLOW;
     const uint32_t ncx = (uint32_t)ncx64;
-    if ((rc = sort_keys(A, A.cx, A.cx2, ncx, bits, s, &sorted)))
+    if ((rc = sort_keys(A, A.cx, A.cx2, ncx, bits, s, &sorted, true, true)))
         return rc;
     if (ncx) {
         // drop the repeated plain hits, compact what stays into the other
