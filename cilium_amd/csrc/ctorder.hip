@@ -517,12 +517,11 @@ __device__ __forceinline__ bool set_put(uint32_t *set, uint32_t mask, uint32_t t
 {
     uint32_t sl = fmix32(tg) & mask;
     for (uint32_t p = 0; p < SET_PROBES; p++, sl = (sl + 1) & mask) {
-        uint32_t cur = set[sl];
-        if (cur == 0) {
-            cur = atomicCAS(&set[sl], 0u, tg);
-            if (cur == 0)
-                return true;
-        }
+        // (the CAS straight away: a first load would add a round trip to
+        // the usual empty slot)
+        const uint32_t cur = atomicCAS(&set[sl], 0u, tg);
+        if (cur == 0)
+            return true;
         if ((cur & ~SET_SHARED) == tg) {
             if (!(cur & SET_SHARED))
                 atomicOr(&set[sl], SET_SHARED);
@@ -537,12 +536,9 @@ __device__ __forceinline__ bool rel_put(uint32_t *set, uint32_t mask, uint32_t t
     const uint32_t k = tg & ~3u, mine = err ? SET_ERR : 0u;
     uint32_t sl = fmix32(k) & mask;
     for (uint32_t p = 0; p < SET_PROBES; p++, sl = (sl + 1) & mask) {
-        uint32_t cur = set[sl];
-        if (cur == 0) {
-            cur = atomicCAS(&set[sl], 0u, k | mine);
-            if (cur == 0)
-                return true;
-        }
+        const uint32_t cur = atomicCAS(&set[sl], 0u, k | mine);
+        if (cur == 0)
+            return true;
         if ((cur & ~3u) == k) {
             // another stage put it first: shared when an error is one of them
             if (err || (cur & SET_ERR)) {
@@ -687,10 +683,8 @@ __global__ __launch_bounds__(256) void k_ord_mark_w(CtaArgs A, OrdArgs O)
                     continue;
                 }
                 full += !set_put(O.cbloom, O.cb_mask, tg);
-                uint32_t *const fw = pf_word(O, tg);
-                const uint32_t fb = bloom_bits(fmix32(tg));
-                if ((*fw & fb) != fb)
-                    atomicOr(fw, fb);
+                // (no return value waited for: no load first either)
+                atomicOr(pf_word(O, tg), bloom_bits(fmix32(tg)));
                 if (tcp)   // (a TCP create writes no related entry)
                     O.rtag[TWO ? 2 * i + st : i] = 0u;
             } else if (r == CT_ESTABLISHED) {
