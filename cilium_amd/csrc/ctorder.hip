@@ -796,18 +796,24 @@ __global__ __launch_bounds__(256) void k_ord_probe_v(CtaArgs A, OrdArgs O)
     const uint64_t ng = 16 * O.W.words;   // (groups of four headers)
     for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < ng;
          t += (uint64_t)gridDim.x * 256) {
+        const uint64_t i0 = 4 * t;
+        const bool vec = O.vec && i0 + 4 <= A.n;
+        // (the group's keys loaded with its probe bits, not after them: most
+        // groups hold a probe, and a dependent load costs a full round trip;
+        // streamed once, non-temporal: the filter stays in L2)
+        uint32_t c4 = 0;
+        uint4 a = make_uint4(NONE, NONE, NONE, NONE), b = a;
+        if (vec) {
+            c4 = ld_nt(reinterpret_cast<const uint32_t *>(A.ctb + i0));
+            a = ld_nt4(O.ck1 + i0);
+            if (TWO)
+                b = ld_nt4(O.ck2 + i0);
+        }
         const uint32_t nib = (uint32_t)(O.W.probe[t >> 4] >> (4 * (t & 15))) & 0xFu;
         if (!nib)
             continue;
-        const uint64_t i0 = 4 * t;
         uint32_t cb[4], k1[4], k2[4];
-        if (O.vec && i0 + 4 <= A.n) {
-            // (streamed once, non-temporal: the filter stays in L2)
-            const uint32_t c4 = ld_nt(reinterpret_cast<const uint32_t *>(A.ctb + i0));
-            const uint4 a = ld_nt4(O.ck1 + i0);
-            uint4 b = make_uint4(NONE, NONE, NONE, NONE);
-            if (TWO)
-                b = ld_nt4(O.ck2 + i0);
+        if (vec) {
             cb[0] = c4 & 0xFF, cb[1] = c4 >> 8 & 0xFF, cb[2] = c4 >> 16 & 0xFF, cb[3] = c4 >> 24;
             k1[0] = a.x, k1[1] = a.y, k1[2] = a.z, k1[3] = a.w;
             k2[0] = b.x, k2[1] = b.y, k2[2] = b.z, k2[3] = b.w;
