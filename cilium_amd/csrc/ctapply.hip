@@ -2189,13 +2189,13 @@ unsigned blocks_for(uint64_t n, unsigned cap)
 // partitioning threshold of 3000 segments, whose size split reads counts
 // back to the host).  The requests' buckets are their home slots' top 11
 // bits (the slots are hashed: even buckets).  The op list's are bounded by
-// splitters — 4096 keys sampled at even strides, sorted in one workgroup,
-// every second one — found by a binary search in LDS: its ops crowd on hot
+// splitters — 2048 keys sampled at even strides, sorted in one workgroup —
+// found by a binary search in LDS: its ops crowd on hot
 // slots (a hot flow's hits, all ordered by one close), and a bucket per top
 // bits left one block sorting a million keys (89 ms per step on the
 // dependency stream).  All-ones keys are left out and come back all-ones.
 constexpr uint32_t BKT_BITS = 11, BKT_N = 1u << BKT_BITS, BKT_CH = 4096, BKT_MIN = 1u << 15;
-constexpr uint32_t BKT_SAMPLES = 4096;
+constexpr uint32_t BKT_SAMPLES = 2048, BKT_PER_SPLIT = BKT_SAMPLES / BKT_N;
 struct BktArgs {
     const uint64_t *in;
     uint64_t *out;
@@ -2222,8 +2222,8 @@ __device__ __forceinline__ uint32_t bkt_of(const BktArgs &B, const uint64_t *sp,
     }
     return lo;
 }
-// one workgroup: the samples sorted (a block radix sort), every second one
-// a splitter
+// one workgroup: the samples sorted (a block radix sort), each after the
+// first a splitter
 __global__ __launch_bounds__(512) void k_bkt_sample(BktArgs B)
 {
     using Sort = hipcub::BlockRadixSort<uint64_t, 512, BKT_SAMPLES / 512>;
@@ -2236,8 +2236,8 @@ __global__ __launch_bounds__(512) void k_bkt_sample(BktArgs B)
 #pragma unroll
     for (uint32_t q = 0; q < BKT_SAMPLES / 512; q++) {
         const uint32_t m = threadIdx.x * (BKT_SAMPLES / 512) + q;   // (blocked: sample m)
-        if (!(m & 1) && m >= 2 && m / 2 - 1 < BKT_N - 1)
-            B.split[m / 2 - 1] = v[q];
+        if (m % BKT_PER_SPLIT == 0 && m >= BKT_PER_SPLIT && m / BKT_PER_SPLIT - 1 < BKT_N - 1)
+            B.split[m / BKT_PER_SPLIT - 1] = v[q];
     }
 }
 __device__ __forceinline__ void bkt_load_split(const BktArgs &B, uint64_t *sp)
