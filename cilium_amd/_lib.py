@@ -109,7 +109,7 @@ class Stats(ctypes.Structure):
                 ("ct_apply_device", ctypes.c_uint32),
                 ("ct_apply_host", ctypes.c_uint32),
                 ("ct_slots", ctypes.c_uint32),
-                ("pad0", ctypes.c_uint32),
+                ("ct_grown", ctypes.c_uint32),
                 ("ct_order_changed", ctypes.c_uint64),
                 ("nat_hops", ctypes.c_uint64),
                 ("ct_evicted", ctypes.c_uint64),

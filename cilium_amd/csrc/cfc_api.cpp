@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <type_traits>
 #include <vector>
@@ -78,12 +79,22 @@ struct GLb {           // load balancing: services, reverse NAT
     uint64_t bytes = 0;
 };
 struct GCt {           // conntrack
-    DevBuf ct4, ct6, ct_acct, ct_sum, ct4_tm, ct6_tm;
+    DevBuf ct4, ct6, ct_sum;
+    // per slot one CtState line (report state, accounting, the device
+    // apply's record): IPv4 slots, then IPv6
+    DevBuf ct_st;
     DevBuf ct4_lb, ct6_lb;                // per-slot LB state (with a load balancer)
-    DevBuf ct4_info, ct4_ms;   // device CT apply state (ctapply.hip)
-    DevBuf ct6_info, ct6_ms;
-    std::vector<Ct4Slot> ct4_host;    // slot -> key, to fold the accounting
+    DevBuf ct4_ms, ct6_ms;     // device CT apply state (ctapply.hip)
+    // the host mirror: slot -> key as the host maps hold it (to fold the
+    // accounting, patch host-side changes, take the device's records)
+    std::vector<Ct4Slot> ct4_host;
     std::vector<Ct6Slot> ct6_host;
+    // the device tables' slots (the mirrors' sizes, once any growth's remap
+    // has been applied to them)
+    uint64_t slots4 = 0, slots6 = 0;
+    // a device growth's remap still to apply to a mirror (mirror_sync): per
+    // mirror slot its slot in the current table (NONE: dropped)
+    DevBuf pend4, pend6;
     std::map<uint64_t, Map *> ct_maps;   // ct_map_key -> map
     uint32_t ct4_mask = 0, ct4_probe = 0, ct6_mask = 0, ct6_probe = 0;
     uint32_t n_ct4 = 0, n_ct6 = 0;
@@ -218,6 +229,7 @@ struct cfc_ctx {
     bool ct_evict = true;
     DevBuf evict_bm, evict_maps, evict_rel;
     uint64_t n_evicted = 0;
+    uint64_t n_ct_grow = 0;   // device-side CT table growths (ct_grow)
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -378,22 +390,65 @@ void settle(cfc_ctx *c)
     log_used += h[CTA_NLOG];
 }
 
+// A device growth's remap into the host mirror of one family (ct_grow):
+// the mirror's entries moved to their slots in the current table, plain
+// tombstones dropped with theirs.  *tomb: the mirror's tombstones after.
+template <class Slot>
+int remap_mirror(std::vector<Slot> &h, DevBuf &pend, uint64_t slots, uint32_t *tomb,
+                 hipStream_t s)
+{
+    if (!pend.p)
+        return 0;
+    const uint64_t n = h.size();
+    std::vector<uint32_t> map(n);
+    if (n && (hipMemcpyAsync(map.data(), pend.p, 4 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+              hipStreamSynchronize(s) != hipSuccess))
+        return -EIO;
+    std::vector<Slot> nh(slots);
+    // (tens of millions of scattered copies: spread over the host's cores)
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<uint64_t> tb(nt, 0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; t++)
+        th.emplace_back([&, t]() {
+            for (uint64_t i = n * t / nt, e = n * (t + 1) / nt; i < e; i++)
+                if (map[i] != 0xFFFFFFFFu) {   // (NONE: dropped)
+                    nh[map[i]] = h[i];
+                    tb[t] += h[i].w == CT_TOMBSTONE;
+                }
+        });
+    for (std::thread &x : th)
+        x.join();
+    uint64_t tt = 0;
+    for (uint64_t v : tb)
+        tt += v;
+    *tomb = (uint32_t)tt;
+    h.swap(nh);
+    pend.reset();
+    return 0;
+}
+int mirror_sync(GCt &G, hipStream_t s)
+{
+    if (int rc = remap_mirror(G.ct4_host, G.pend4, G.slots4, &G.tomb4, s))
+        return rc;
+    return remap_mirror(G.ct6_host, G.pend6, G.slots6, &G.tomb6, s);
+}
+
 // The IPv6 table's part of ct_sync: its dirty slots, then its TCP maps'
 // ICMPv6 entries (CtLog6).
 int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
 {
     GCt &G = *E.ct;
-    const uint64_t slots = G.ct6_host.size();
+    const uint64_t slots = G.slots6;
     uint32_t *cnt = (uint32_t *)c->cta_cnt.p;
     std::vector<CtSyncRec6> rec;
-    if (slots && G.ct6_info.p) {
+    if (slots && G.ct_st.p) {
         Ct6Slot *ct6 = (Ct6Slot *)G.ct6.p;
-        CtTimer *tm = (CtTimer *)G.ct6_tm.p;
-        CtInfo *info = (CtInfo *)G.ct6_info.p;
+        CtState *st = (CtState *)G.ct_st.p + G.slots4;
         const uint4 *lb6 = (const uint4 *)G.ct6_lb.p;
         uint32_t n = 0;
         if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-            cta_collect6(ct6, tm, info, lb6, slots, nullptr, 0, cnt, s) ||
+            cta_collect6(ct6, st, lb6, slots, nullptr, 0, cnt, s) ||
             hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return -EIO;
@@ -404,7 +459,7 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
             CtSyncRec6 *dr = (CtSyncRec6 *)c->cta_sync.p;
             uint32_t n2 = 0;
             if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-                cta_collect6(ct6, tm, info, lb6, slots, dr, n, cnt, s) ||
+                cta_collect6(ct6, st, lb6, slots, dr, n, cnt, s) ||
                 hipMemcpyAsync(rec.data(), dr, sizeof(CtSyncRec6) * n, hipMemcpyDeviceToHost,
                                s) != hipSuccess ||
                 hipMemcpyAsync(&n2, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -526,6 +581,9 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
 int ct_sync(cfc_ctx *c, hipStream_t s)
 {
     settle(c);
+    if (c->epoch)
+        if (int rc = mirror_sync(*c->epoch->ct, s))
+            return rc;
     if (!c->ct_dirty || !c->epoch)
         return 0;
     order_after_launches(c, s);
@@ -533,17 +591,16 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
     // turns into tombstones were deleted by an apply, which bumped it)
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
-    const uint64_t slots = G.ct4_host.size();
+    const uint64_t slots = G.slots4;
     uint32_t n = 0;
     if (c->cta_cnt.ensure(4 * CTA_NCNT))
         return -ENOMEM;
     uint32_t *cnt = (uint32_t *)c->cta_cnt.p;
     Ct4Slot *ct4 = (Ct4Slot *)G.ct4.p;
-    CtTimer *tm = (CtTimer *)G.ct4_tm.p;
-    CtInfo *info = (CtInfo *)G.ct4_info.p;
+    CtState *st = (CtState *)G.ct_st.p;
     const uint4 *lb4 = (const uint4 *)G.ct4_lb.p;
     if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-        cta_collect(ct4, tm, info, lb4, slots, nullptr, 0, cnt, s) ||
+        cta_collect(ct4, st, lb4, slots, nullptr, 0, cnt, s) ||
         hipMemcpyAsync(&n, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
@@ -554,7 +611,7 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
         CtSyncRec *dr = (CtSyncRec *)c->cta_sync.p;
         uint32_t n2 = 0;
         if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
-            cta_collect(ct4, tm, info, lb4, slots, dr, n, cnt, s) ||
+            cta_collect(ct4, st, lb4, slots, dr, n, cnt, s) ||
             hipMemcpyAsync(rec.data(), dr, sizeof(CtSyncRec) * n, hipMemcpyDeviceToHost, s) !=
                 hipSuccess ||
             hipMemcpyAsync(&n2, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -573,9 +630,13 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
             hipStreamSynchronize(s) != hipSuccess)
             return -EIO;
         for (const CtGcRec &r : gl) {
-            Ct4Slot &h = G.ct4_host[r.slot];
             if (Map *m = ct_slot_key(E, 4, &r.x, &r.y, r.z, r.w, &key))
                 m->erase_raw(key);
+            if (r.slot == 0xFFFFFFFFu) {   // (a growth since dropped its tombstone: ct_grow)
+                G.n_ct4--;
+                continue;
+            }
+            Ct4Slot &h = G.ct4_host[r.slot];
             if (h.x == r.x && h.y == r.y && h.z == r.z && h.w == r.w) {
                 G.n_ct4--;
                 G.tomb4++;
@@ -696,12 +757,13 @@ int fold_ct(cfc_ctx *c, hipStream_t s)
     if (int rc = ct_sync(c, s))
         return rc;
     Epoch &E = *c->epoch;
-    const size_t n4 = E.ct->ct4_host.size(), n = n4 + E.ct->ct6_host.size();
+    const size_t n4 = E.ct->slots4, n = n4 + E.ct->slots6;
     if (!n)
         return 0;
     std::vector<uint64_t> h(4 * n);
-    if (hipMemcpyAsync(h.data(), E.ct->ct_acct.p, 32 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemsetAsync(E.ct->ct_acct.p, 0, 32 * n, s) != hipSuccess ||
+    DevBuf tmp;   // (the lines' counts, dense)
+    if (tmp.ensure(32 * n) || ct_acct_take((CtState *)E.ct->ct_st.p, (uint64_t *)tmp.p, n, s) ||
+        hipMemcpyAsync(h.data(), tmp.p, 32 * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     std::string key;
@@ -998,21 +1060,38 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
 {
     auto g = std::make_shared<GCt>();
     if ((*rc = upload_vec(g->ct4, img.ct4, s)) || (*rc = upload_vec(g->ct6, img.ct6, s)) ||
-        (*rc = upload_vec(g->ct4_tm, img.ct4_tm, s)) ||
-        (*rc = upload_vec(g->ct6_tm, img.ct6_tm, s)) ||
         (*rc = upload_vec(g->ct4_lb, img.ct4_lb, s)) ||
         (*rc = upload_vec(g->ct6_lb, img.ct6_lb, s)))
         return nullptr;
     const size_t nslots = img.ct4.size() + img.ct6.size();
-    if (nslots && ((*rc = g->ct_acct.zeros(32 * nslots, s)) ||
-                   (*rc = g->ct_sum.zeros(4 * nslots, s))))
+    if (nslots && (*rc = g->ct_sum.zeros(4 * nslots, s)))
         return nullptr;
     const size_t n4 = img.ct4.size(), n6 = img.ct6.size();
-    if (n4 && ((*rc = g->ct4_info.zeros(sizeof(CtInfo) * n4, s)) ||
-               (*rc = g->ct4_ms.zeros(8 * n4, s))))
+    if (nslots) {   // the report states into their lines (through a staging copy)
+        DevBuf tm;
+        if (g->ct_st.ensure(sizeof(CtState) * nslots) ||
+            tm.ensure(sizeof(CtTimer) * std::max(n4, n6))) {
+            *rc = -ENOMEM;
+            return nullptr;
+        }
+        g->ct_st.bytes = sizeof(CtState) * nslots;
+        CtState *st = (CtState *)g->ct_st.p;
+        for (int f = 0; f < 2; f++) {
+            const std::vector<CtTimer> &v = f ? img.ct6_tm : img.ct4_tm;
+            if (v.empty())
+                continue;
+            if (hipMemcpyAsync(tm.p, v.data(), sizeof(CtTimer) * v.size(),
+                               hipMemcpyHostToDevice, s) != hipSuccess ||
+                ct_state_init(st + (f ? n4 : 0), (const CtTimer *)tm.p, v.size(), s) ||
+                hipStreamSynchronize(s) != hipSuccess) {   // (tm is freed on return)
+                *rc = -EIO;
+                return nullptr;
+            }
+        }
+    }
+    if (n4 && (*rc = g->ct4_ms.zeros(8 * n4, s)))
         return nullptr;
-    if (n6 && ((*rc = g->ct6_info.zeros(sizeof(CtInfo) * n6, s)) ||
-               (*rc = g->ct6_ms.zeros(8 * n6, s))))
+    if (n6 && (*rc = g->ct6_ms.zeros(8 * n6, s)))
         return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
@@ -1028,7 +1107,9 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
     g->n_ct6 = img.n_ct6;
     g->n_nat46 = img.n_nat46;
     g->bytes = sizeof(Ct4Slot) * img.ct4.size() + sizeof(Ct6Slot) * img.ct6.size() +
-               48ull * nslots + 16ull * (n4 + n6) + 16ull * img.ct4_lb.size();
+               (sizeof(CtState) + 4) * nslots + 8ull * (n4 + n6) + 16ull * img.ct4_lb.size();
+    g->slots4 = img.ct4.size();
+    g->slots6 = img.ct6.size();
     g->ct4_host = std::move(img.ct4);
     g->ct6_host = std::move(img.ct6);
     return g;
@@ -1072,18 +1153,16 @@ void assemble(Epoch &E)
     T.pol_bloom_words = D.pol_bloom_words;
     T.n_ctr = (uint32_t)D.ctr_owner.size();
     // (a table a device apply may fill counts even while empty)
-    T.ct4 = (C.n_ct4 || !C.ct4_host.empty()) ? (const Ct4Slot *)C.ct4.p : nullptr;
-    T.ct6 = (C.n_ct6 || !C.ct6_host.empty()) ? (const Ct6Slot *)C.ct6.p : nullptr;
-    T.ct_acct = (uint64_t *)C.ct_acct.p;
+    T.ct4 = (C.n_ct4 || C.slots4) ? (const Ct4Slot *)C.ct4.p : nullptr;
+    T.ct6 = (C.n_ct6 || C.slots6) ? (const Ct6Slot *)C.ct6.p : nullptr;
+    T.ct_st = (CtState *)C.ct_st.p;
     T.ct_sum = (uint32_t *)C.ct_sum.p;
-    T.ct4_tm = (const CtTimer *)C.ct4_tm.p;
-    T.ct6_tm = (const CtTimer *)C.ct6_tm.p;
     T.ct4_mask = C.ct4_mask;
     // the device CT apply inserts in place: lookups walk to a free slot
     T.ct4_probe = C.ct4_mask;
     T.ct6_mask = C.ct6_mask;
     T.ct6_probe = C.ct6_mask;
-    T.ct6_acct_base = (uint32_t)C.ct4_host.size();
+    T.ct6_acct_base = (uint32_t)C.slots4;
     T.lb4 = B.n_lb4 ? (const uint4 *)B.lb4.p : nullptr;
     T.lb4_mask = B.lb4_mask;
     T.rnat4 = (const uint2 *)B.rnat4.p;
@@ -1214,6 +1293,8 @@ unsigned patch_touched(cfc_ctx *c, unsigned groups, hipStream_t s)
 bool patch_ct(cfc_ctx *c, hipStream_t s)
 {
     GCt &G = *c->epoch->ct;
+    if (mirror_sync(G, s))
+        return false;
     uint64_t ins[2] = {0, 0}, any[2] = {0, 0};
     for (auto &kv : c->maps) {
         const Map *m = kv.second.get();
@@ -1235,7 +1316,7 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
             }
         }
     }
-    const uint64_t size[2] = {G.ct4_host.size(), G.ct6_host.size()};
+    const uint64_t size[2] = {G.slots4, G.slots6};
     const uint64_t used[2] = {(uint64_t)G.n_ct4 + G.tomb4, (uint64_t)G.n_ct6 + G.tomb6};
     for (int f = 0; f < 2; f++)
         if (any[f] && (!size[f] || 4 * (used[f] + ins[f]) > 3 * size[f]))
@@ -1255,7 +1336,7 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
     };
     static const uint32_t zero[4] = {0, 0, 0, 0};
     auto zero_acct = [&](uint64_t slot) {
-        char *a = (char *)G.ct_acct.p + 32 * slot;
+        char *a = (char *)((CtState *)G.ct_st.p + slot)->acct;
         put(a, zero);
         put(a + 16, zero);
     };
@@ -1275,8 +1356,8 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
             const uint32_t mask = (uint32_t)size[v6] - 1;
             int64_t at = -1, slot = -1;
             uint32_t p = 0, pfree = 0;
-            uint32_t i = v6 ? ct_hash6(k6.d, k6.s, k6.z, k6.w) & mask
-                            : ct_hash4(k4.x, k4.y, k4.z, k4.w) & mask;
+            uint32_t i = v6 ? ct_home6(k6.d, k6.s, k6.z, k6.w) & mask
+                            : ct_home4(k4.x, k4.y, k4.z, k4.w) & mask;
             for (;; i = (i + 1) & mask, p++) {
                 const uint32_t w = v6 ? G.ct6_host[i].w : G.ct4_host[i].w;
                 if (w == 0 || w == CT_TOMBSTONE) {
@@ -1300,7 +1381,7 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
             }
             const uint64_t acct = v6 ? size[0] + (uint64_t)(at >= 0 ? at : slot)
                                      : (uint64_t)(at >= 0 ? at : slot);
-            CtTimer *tm = (CtTimer *)(v6 ? G.ct6_tm.p : G.ct4_tm.p);
+            CtState *tm = (CtState *)G.ct_st.p + (v6 ? size[0] : 0);
             if (present) {
                 const CtTimer v = ct_timer_of(it->second.val);
                 c->nat46_seen |= !v6 && (v.flags & CTT_NAT46);
@@ -1329,7 +1410,7 @@ bool patch_ct(cfc_ctx *c, hipStream_t s)
                 } else if (t.second & (TOUCH_INSERT | TOUCH_ERASE)) {
                     zero_acct(acct);   // deleted and created again
                 }
-                put(tm + at, &v);
+                put(&tm[at].tm, &v);
                 const uint4 l = ct_lb_of(it->second.val);
                 if (!v6 && G.ct4_lb.p)
                     put((uint4 *)G.ct4_lb.p + at, &l);
@@ -2447,7 +2528,8 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     st->ct_evicted = c->n_evicted;
     st->svc_ordered = c->n_svo;
     st->ct_apply_sparse = c->n_apply_sparse;
-    st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->ct4_host.size() + c->epoch->ct->ct6_host.size())
+    st->ct_grown = (uint32_t)c->n_ct_grow;
+    st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->slots4 + c->epoch->ct->slots6)
                             : 0u;
     return 0;
 }
@@ -2890,13 +2972,13 @@ int64_t ct_dev_slot(const Epoch &E, const Map *m, const std::string &k)
         return -1;
     const uint32_t w = ct_word(nh, (uint8_t)k[2 * al + 5], owner);
     if (!v6) {
-        if (E.ct->ct4_host.empty())
+        if (!E.ct->slots4)
             return -1;
         uint32_t x, y;
         memcpy(&x, k.data(), 4);
         memcpy(&y, k.data() + 4, 4);
-        const uint32_t mask = (uint32_t)E.ct->ct4_host.size() - 1;
-        for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
+        const uint32_t mask = (uint32_t)E.ct->slots4 - 1;
+        for (uint32_t i = ct_home4(x, y, z, w) & mask;; i = (i + 1) & mask) {
             const Ct4Slot &e = E.ct->ct4_host[i];
             if (!e.w)
                 return -1;
@@ -2904,28 +2986,28 @@ int64_t ct_dev_slot(const Epoch &E, const Map *m, const std::string &k)
                 return i;
         }
     }
-    if (E.ct->ct6_host.empty())
+    if (!E.ct->slots6)
         return -1;
     uint32_t d[4], sa[4];
     memcpy(d, k.data(), 16);
     memcpy(sa, k.data() + 16, 16);
-    const uint32_t mask = (uint32_t)E.ct->ct6_host.size() - 1;
-    for (uint32_t i = ct_hash6(d, sa, z, w) & mask;; i = (i + 1) & mask) {
+    const uint32_t mask = (uint32_t)E.ct->slots6 - 1;
+    for (uint32_t i = ct_home6(d, sa, z, w) & mask;; i = (i + 1) & mask) {
         const Ct6Slot &e = E.ct->ct6_host[i];
         if (!e.w)
             return -1;
         if (e.z == z && e.w == w && !memcmp(e.d, d, 16) && !memcmp(e.s, sa, 16))
-            return (int64_t)E.ct->ct4_host.size() + i;
+            return (int64_t)E.ct->slots4 + i;
     }
 }
 
 void ct_drop_counts(cfc_ctx *c, const Map *m, const std::string &k, hipStream_t s)
 {
-    if (!c->epoch || !c->epoch->ct->ct_acct.p)
+    if (!c->epoch || !c->epoch->ct->ct_st.p || mirror_sync(*c->epoch->ct, s))
         return;
     const int64_t slot = ct_dev_slot(*c->epoch, m, k);
     if (slot >= 0)
-        (void)hipMemsetAsync((char *)c->epoch->ct->ct_acct.p + 32 * slot, 0, 32, s);
+        (void)hipMemsetAsync(((CtState *)c->epoch->ct->ct_st.p + slot)->acct, 0, 32, s);
 }
 
 int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
@@ -2950,8 +3032,10 @@ int ct_evict_maps(cfc_ctx *c, bool v6, const std::vector<Map *> &fmaps,
 {
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
-    const uint64_t slots = v6 ? G.ct6_host.size() : G.ct4_host.size();
-    const uint64_t base6 = v6 ? G.ct4_host.size() : 0;   // (ct_dev_slot's IPv6 offset)
+    if (int rc = mirror_sync(G, s))
+        return rc;
+    const uint64_t slots = v6 ? G.slots6 : G.slots4;
+    const uint64_t base6 = v6 ? G.slots4 : 0;   // (ct_dev_slot's IPv6 offset)
     const size_t words = (slots + 31) / 32;
     std::vector<uint32_t> bm(words);
     if (c->evict_bm.ensure(4 * words) ||
@@ -3017,6 +3101,127 @@ int ct_evict_maps(cfc_ctx *c, bool v6, const std::vector<Map *> &fmaps,
     return n ? commit_locked(c, s) : 0;
 }
 
+// Device-side growth of family v6's CT table to `want` slots (a power of
+// two): the rehash kernel (ctapply.hip k_ct_rehash) moves every key-holding
+// slot, its CtState line and LB word into new buffers; the other family's
+// lines are copied as they are (the IPv6 lines start after the IPv4 ones);
+// the plain-hit summaries start empty.  The apply never stops for a host
+// rebuild: the host mirror follows lazily (mirror_sync, before its next
+// reader), and the pending GC log's slots are remapped on the device.  The
+// replaced buffers are retired like an epoch (launches on other streams may
+// still read them).  0 grown, 1 not possible (the host path), < 0 error.
+int ct_grow(cfc_ctx *c, bool v6, uint64_t want, hipStream_t s)
+{
+    Epoch &E = *c->epoch;
+    GCt &G = *E.ct;
+    const uint64_t n4 = G.slots4, n6 = G.slots6, o = v6 ? n6 : n4;
+    if (!o || want <= o || want > (1ull << 30) || (want & (want - 1)))
+        return 1;
+    const uint64_t m4 = v6 ? n4 : want, m6 = v6 ? want : n6;
+    const size_t ksz = v6 ? sizeof(Ct6Slot) : sizeof(Ct4Slot);
+    DevBuf &key = v6 ? G.ct6 : G.ct4, &lb = v6 ? G.ct6_lb : G.ct4_lb, &ms = v6 ? G.ct6_ms : G.ct4_ms;
+    auto nk = std::make_unique<DevBuf>(), nst = std::make_unique<DevBuf>(),
+         nsum = std::make_unique<DevBuf>(), nms = std::make_unique<DevBuf>(),
+         nlb = std::make_unique<DevBuf>();
+    DevBuf map;
+    if (nk->zeros(ksz * want, s) || nst->ensure(sizeof(CtState) * (m4 + m6)) ||
+        nsum->zeros(4 * (m4 + m6), s) || nms->zeros(8 * want, s) ||
+        (lb.p && nlb->zeros(16 * want, s)) || map.ensure(4 * o) ||
+        c->cta_cnt.ensure(4 * CTA_NCNT))
+        return -ENOMEM;
+    nst->bytes = sizeof(CtState) * (m4 + m6);
+    CtState *ost = (CtState *)G.ct_st.p, *ns = (CtState *)nst->p;
+    uint32_t *cnt = (uint32_t *)c->cta_cnt.p, moved = 0;
+    const uint64_t other = v6 ? n4 : n6;
+    if ((other && hipMemcpyAsync(v6 ? ns : ns + m4, v6 ? ost : ost + n4, sizeof(CtState) * other,
+                                 hipMemcpyDeviceToDevice, s) != hipSuccess) ||
+        hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+        ct_rehash(v6, key.p, ost + (v6 ? n4 : 0), (const uint4 *)lb.p, o, nk->p,
+                  ns + (v6 ? m4 : 0), (uint4 *)nlb->p, (uint32_t)(want - 1), (uint32_t *)map.p,
+                  cnt, s))
+        return -EIO;
+    // the GC log's slots (IPv4: its deletes the host has not taken)
+    if (!v6 && c->gc_log_used &&
+        ct_remap(&((CtGcRec *)c->gc_log.p)->slot, c->gc_log_used, sizeof(CtGcRec) / 4,
+                 (const uint32_t *)map.p, s))
+        return -EIO;
+    // the host mirror's remap: this one, or composed with one still pending
+    DevBuf &pend = v6 ? G.pend6 : G.pend4;
+    if (pend.p) {
+        if (ct_remap((uint32_t *)pend.p, v6 ? G.ct6_host.size() : G.ct4_host.size(), 1,
+                     (const uint32_t *)map.p, s))
+            return -EIO;
+    } else {
+        std::swap(pend.p, map.p);
+        std::swap(pend.bytes, map.bytes);
+    }
+    if (hipMemcpyAsync(&moved, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    // the replaced buffers stay until the launches on other streams that
+    // may read them have passed this point
+    {
+        auto old = std::make_shared<Epoch>();
+        old->ct = std::make_shared<GCt>();
+        GCt &R = *old->ct;
+        auto give = [](DevBuf &from, DevBuf &to, std::unique_ptr<DevBuf> &nb) {
+            std::swap(to.p, from.p);
+            std::swap(to.bytes, from.bytes);
+            if (nb) {
+                std::swap(from.p, nb->p);
+                std::swap(from.bytes, nb->bytes);
+            }
+        };
+        give(key, v6 ? R.ct6 : R.ct4, nk);
+        give(G.ct_st, R.ct_st, nst);
+        give(G.ct_sum, R.ct_sum, nsum);
+        give(ms, v6 ? R.ct6_ms : R.ct4_ms, nms);
+        if (lb.p)
+            give(lb, v6 ? R.ct6_lb : R.ct4_lb, nlb);
+        Retired r;
+        r.e = old;
+        for (hipStream_t st : c->streams) {
+            if (st == s)
+                continue;   // (stream-ordered behind this call already)
+            hipEvent_t ev;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(ev, st) != hipSuccess) {
+                (void)hipDeviceSynchronize();
+                break;
+            }
+            r.ev.push_back(ev);
+        }
+        c->retired.push_back(std::move(r));
+    }
+    if (v6) {
+        G.slots6 = want;
+        G.ct6_mask = (uint32_t)(want - 1);
+        G.ct6_probe = G.ct6_mask;
+        // (the load check's count: live, plus the inserts since the sync)
+        G.tomb6 = moved > (uint64_t)G.n_ct6 + c->cta_ins6
+                      ? (uint32_t)(moved - G.n_ct6 - c->cta_ins6) : 0u;
+        c->ct_min6 = std::max<uint64_t>(c->ct_min6, want);
+    } else {
+        G.slots4 = want;
+        G.ct4_mask = (uint32_t)(want - 1);
+        G.ct4_probe = G.ct4_mask;
+        G.tomb4 = moved > G.n_ct4 ? (uint32_t)(moved - G.n_ct4) : 0u;
+        c->ct_used = moved;
+        c->ct_used_valid = true;
+        c->cta_ins = 0;
+        c->ct_min4 = std::max<uint64_t>(c->ct_min4, want);
+    }
+    assemble(E);
+    E.T.id_cover = c->id_cover;
+    // the table moved under every hit slot and summary a launch left
+    c->ct_gen++;
+    c->last_cls.valid = false;
+    c->sum_dirty = c->sum_pending = false;
+    c->ct_dirty = true;   // (the mirror lags the table until mirror_sync)
+    c->n_ct_grow++;
+    return 0;
+}
+
 // cfc_ct_apply_v4/v6 on the device (ctapply.hip).  1: take the host path
 // instead (nothing changed), 0 done, <0 error.
 template <class Hdr>
@@ -3051,7 +3256,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         return 1;
     const bool lbm = lbt && mode == CFC_MODE_EGRESS;
     const uint64_t k3 = lbm ? 3 : 2;   // requests per header, writes per create
-    const uint64_t n = in->n, slots = V6 ? G.ct6_host.size() : G.ct4_host.size();
+    const uint64_t n = in->n, slots = V6 ? G.slots6 : G.slots4;
     if (!slots && may_grow && n < (1ull << 27)) {
         // no table yet (the family's maps were empty at the build): build
         // one sized for this batch and apply on it — unless other map groups
@@ -3072,7 +3277,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             return ct_apply_dev(c, in, out, mode, ep_lxc, s, false, true);
         }
     }
-    if (!slots || !(V6 ? G.ct6_info.p : G.ct4_info.p) || n >= (lbm ? 1ull << 27 : 1ull << 28))
+    if (!slots || !G.ct_st.p || n >= (lbm ? 1ull << 27 : 1ull << 28))
         return 1;
     // the batch's classify (its CT bytes, verdicts and the workspace's hit
     // slots) may have run on another stream
@@ -3113,15 +3318,13 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         A.ct6 = (Ct6Slot *)G.ct6.p;
         A.mask = G.ct6_mask;
         A.acct_base = E.T.ct6_acct_base;
-        A.tm = (CtTimer *)G.ct6_tm.p;
-        A.info = (CtInfo *)G.ct6_info.p;
+        A.st = (CtState *)G.ct_st.p + A.acct_base;
         A.ms = (uint2 *)G.ct6_ms.p;
     } else {
         A.ct4 = (Ct4Slot *)G.ct4.p;
         A.mask = G.ct4_mask;
         A.acct_base = 0;
-        A.tm = (CtTimer *)G.ct4_tm.p;
-        A.info = (CtInfo *)G.ct4_info.p;
+        A.st = (CtState *)G.ct_st.p;
         A.ms = (uint2 *)G.ct4_ms.p;
     }
     A.hs = (uint32_t *)c->cta_hs.p;
@@ -3364,26 +3567,19 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             A.n_emaps = 0;
         }
     }
-    if (ok && !fits(newk) && may_grow) {
-        // the batch outgrows the table but not its maps: rebuild the CT
-        // group larger (the device's state synced into the maps first) and
-        // apply again — unless other map groups wait for a commit, which
-        // would change the tables the batch was classified with
-        bool others = false;
-        uint64_t sg[NGROUPS];
-        group_sigs(c, sg);
-        for (int g = 0; g < NGROUPS; g++)
-            others |= g != 3 && sg[g] != c->built_sig[g];
-        if (!others && maps_fit()) {
-            uint64_t &mn = V6 ? c->ct_min6 : c->ct_min4;
-            mn = std::max<uint64_t>(mn, 2 * (used + ins + newk));
-            if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess)
-                return -EIO;
-            c->built_sig[3] = ~0ull;
-            if (int rc = commit_locked(c, s))
-                return rc;
+    if (ok && !fits(newk) && may_grow && maps_fit()) {
+        // the batch outgrows the table but not its maps: the table grows on
+        // the device (ct_grow: at least twice the slots, room for this
+        // batch at under half load) and the batch is applied again on it —
+        // its CT bytes keep the packet order already resolved
+        uint64_t want = 2 * slots;
+        while (want < 2 * (used + ins + newk))
+            want *= 2;
+        const int g = ct_grow(c, V6, want, s);
+        if (g < 0)
+            return g;
+        if (g == 0)
             return ct_apply_dev(c, in, out, mode, ep_lxc, s, false, false);
-        }
     }
     if (ok && fits(newk) && !maps_fit() && c->ct_evict && !newk_map.empty()) {
         // a map at capacity (its exact new keys known): the device's own
@@ -3945,7 +4141,7 @@ int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter 
     settle(c);
     Epoch &E = *c->epoch;
     GCt &G = *E.ct;
-    const uint64_t slots = G.ct4_host.size();
+    const uint64_t slots = G.slots4;
     // the selected maps' selector words, and the IPv4 addresses of the sets
     std::vector<uint32_t> mw;
     std::vector<Map *> mm;
@@ -4002,9 +4198,7 @@ int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter 
         hs.insert(hs.end(), ma.begin(), ma.end());
         CtGcArgs A{};
         A.ct4 = (Ct4Slot *)G.ct4.p;
-        A.tm = (CtTimer *)G.ct4_tm.p;
-        A.info = (CtInfo *)G.ct4_info.p;
-        A.acct = (uint64_t *)G.ct_acct.p;
+        A.st = (CtState *)G.ct_st.p;
         A.slots = slots;
         A.mask = (uint32_t)(slots - 1);
         A.maps = sets;
@@ -4097,7 +4291,7 @@ int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, h
     order_after_launches(c, s);
     cfc_ct_gc_stats st{};
     Epoch &E = *c->epoch;
-    const bool dev4 = !E.ct->ct4_host.empty() && E.ct->ct4_info.p;
+    const bool dev4 = E.ct->slots4 && E.ct->ct_st.p;
     // IPv6 maps are collected on the host, after their device applies are
     // synchronised — before the device pass, whose pending-log entries the
     // sync would otherwise replay into the host maps after the pass counted

@@ -366,7 +366,7 @@ __device__ __forceinline__ void r3_identity(const DevTables &T, const Lds &S,
             // has an IPv6 address: that hop decides (nat.hip); nothing here
             // counts but the hit
             if (T.nat46 && c.slot != NONE && (h.rec.w & LXC_HAS6) &&
-                (T.ct4_tm[c.slot].flags & CTT_NAT46)) {
+                (T.ct_st[c.slot].tm.flags & CTT_NAT46)) {
                 h.nat = true;
                 h.need_pol = false;
                 h.ct_k1 = ct_acct_key(c.slot, CT_INGRESS);
@@ -440,7 +440,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
     // wants the event words)
     const uint32_t action = ct_action(false, h.mt & 0xFF, h.tpt, h.mt);
     const uint32_t tfl = (h.mt & 0xFF) == 6 ? h.tf : 0u;
-    const uint32_t mon1 = NT ? ct_monitor(T, CT ? T.ct4_tm : nullptr, h.ct_slot,
+    const uint32_t mon1 = NT ? ct_monitor(T, CT ? T.ct_st : nullptr, h.ct_slot,
                                           EGR ? CT_EGRESS : CT_INGRESS, action, tfl,
                                           h.dport)
                              : 0u;
@@ -597,7 +597,7 @@ __device__ __forceinline__ void r4_verdict(const DevTables &T, const Lds &S,
                 met1 = prox ? NONE : mkey<MODE>(0, METRIC_INGRESS);
                 ev2 = 1;
                 if (NT) {   // the destination program's trace
-                    uint32_t mon2 = ct_monitor(T, CT ? T.ct4_tm : nullptr,
+                    uint32_t mon2 = ct_monitor(T, CT ? T.ct_st : nullptr,
                                                CT ? c2.slot : NONE, CT_INGRESS,
                                                action, tfl, dp2);
                     if (fresh)   // the entry as ct_create4 just wrote it
@@ -1000,7 +1000,7 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
                                                     const uint32_t *ct_idx2,
                                                     const uint32_t *meta,
                                                     uint64_t n,
-                                                    unsigned long long *acct)
+                                                    CtState *st)
 {
     uint32_t *keys = reinterpret_cast<uint32_t *>(cfc_smem);
     unsigned long long *vals =
@@ -1036,8 +1036,9 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
             h = (h + 1) & (CT_LDS_SLOTS - 1);
         }
         if (!done) {
-            atomicAdd(&acct[2ull * k], 1ull);
-            atomicAdd(&acct[2ull * k + 1], (unsigned long long)len);
+            unsigned long long *a = ct_acct_at(st, k);
+            atomicAdd(a, 1ull);
+            atomicAdd(a + 1, (unsigned long long)len);
         }
     }
     __syncthreads();
@@ -1045,8 +1046,9 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
         const uint32_t k = keys[j];
         const unsigned long long v = vals[j];
         if (k != NONE && v) {
-            atomicAdd(&acct[2ull * k], v >> 32);
-            atomicAdd(&acct[2ull * k + 1], v & 0xFFFFFFFFull);
+            unsigned long long *a = ct_acct_at(st, k);
+            atomicAdd(a, v >> 32);
+            atomicAdd(a + 1, v & 0xFFFFFFFFull);
         }
     }
 }
@@ -1447,7 +1449,7 @@ __global__ __launch_bounds__(BLOCK) void k_acc_part2(const uint64_t *inA, const 
 // LDS, then added to its counters (acct[2k] packets, acct[2k + 1] bytes)
 __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, const uint32_t *plan,
                                                       const uint32_t *fo, uint32_t nco,
-                                                      uint64_t *acct, uint32_t *sum)
+                                                      CtState *st, uint32_t *sum)
 {
     uint32_t *pk = reinterpret_cast<uint32_t *>(cfc_smem);
     unsigned long long *by = reinterpret_cast<unsigned long long *>(pk + CTP_BUCKET);
@@ -1499,7 +1501,7 @@ __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, cons
         const uint32_t j = threadIdx.x + q * BLOCK;
         p[q] = pk[j];
         const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
-        cv[q] = p[q] ? *reinterpret_cast<const ulonglong2 *>(acct + 2 * k) : ulonglong2{0, 0};
+        cv[q] = p[q] ? *reinterpret_cast<const ulonglong2 *>(ct_acct_at(st, k)) : ulonglong2{0, 0};
     }
 #pragma unroll
     for (uint32_t q = 0; q < FJ; q++) {
@@ -1509,7 +1511,7 @@ __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, cons
         const uint64_t k = (uint64_t)b * CTP_BUCKET + j;
         cv[q].x += p[q];
         cv[q].y += by[j];
-        *reinterpret_cast<ulonglong2 *>(acct + 2 * k) = cv[q];
+        *reinterpret_cast<ulonglong2 *>(ct_acct_at(st, k)) = cv[q];
     }
     if (!sum)
         return;
@@ -1778,7 +1780,7 @@ WsLayout ws_layout(uint64_t n, const DevTables &T, int mode, bool ct)
     w.nblk = hist_slices(n, slots);
     off += 8ull * slots * w.nblk;
     const uint32_t nbuck = ctp_buckets(T);
-    if (ct && T.ct_acct && nbuck) {
+    if (ct && T.ct_st && nbuck) {
         const uint64_t per = acc_slice(n);
         const uint32_t nblk = (uint32_t)((n + per - 1) / per);
         w.ctp_nv = nblk * (egr ? 2u : 1u);
@@ -1912,7 +1914,7 @@ bool launch_counters(const DevTables &T, const uint32_t *meta, const uint8_t *tf
         return sums;
     const WsLayout w = ws_layout(n, T, mode, ct);
     const CountArgs C = count_args(ws, w, T, g_ctr + 2ull * T.n_ctr, mode, ct);
-    if (ct && T.ct_acct && w.ctp_nv) {
+    if (ct && T.ct_st && w.ctp_nv) {
         char *b = reinterpret_cast<char *>(ws);
         uint64_t *rec = reinterpret_cast<uint64_t *>(b + w.ctp_rec);
         uint64_t *recA = reinterpret_cast<uint64_t *>(b + w.ctp_recA);
@@ -1955,14 +1957,13 @@ bool launch_counters(const DevTables &T, const uint32_t *meta, const uint8_t *tf
                            plan, w.ctp_nco, rec, fo);
         set_lds_limit((const void *)k_acc_reduce, (int)ACC_RED_LDS);
         hipLaunchKernelGGL(k_acc_reduce, dim3(w.ctp_nbuck), dim3(BLOCK), ACC_RED_LDS, s, rec,
-                           plan, fo, w.ctp_nco, T.ct_acct, T.ct_sum);
+                           plan, fo, w.ctp_nco, T.ct_st, T.ct_sum);
         sums = T.ct_sum != nullptr;
-    } else if (ct && T.ct_acct) {
+    } else if (ct && T.ct_st) {
         set_lds_limit((const void *)k_ct_count, (int)CT_LDS_BYTES);
         const uint32_t nblk = (uint32_t)((n + COUNT_PER_BLOCK - 1) / COUNT_PER_BLOCK);
         hipLaunchKernelGGL(k_ct_count, dim3(nblk, mode == CFC_MODE_EGRESS ? 2 : 1),
-                           dim3(BLOCK), CT_LDS_BYTES, s, C.ct, C.ct2, meta, n,
-                           reinterpret_cast<unsigned long long *>(T.ct_acct));
+                           dim3(BLOCK), CT_LDS_BYTES, s, C.ct, C.ct2, meta, n, T.ct_st);
     }
     // the histogram jobs: policy ranges of each stage, identity ranges
     std::vector<HistJob> jobs;

@@ -203,12 +203,12 @@ struct CtaArgs {
     int mode;
     uint32_t ep_owner, ep_sec, now, seq;
     // the family's table (the other is null), its mask, and its first slot
-    // in ct_acct (0 for IPv4, DevTables.ct6_acct_base for IPv6)
+    // in DevTables.ct_st (0 for IPv4, ct6_acct_base for IPv6); st: the
+    // family's CtState lines (DevTables.ct_st + acct_base)
     Ct4Slot *ct4;
     Ct6Slot *ct6;
     uint32_t mask, acct_base;
-    CtTimer *tm;
-    CtInfo *info;
+    CtState *st;
     // per slot {mark, summary} of this apply (one 8-byte word: route reads
     // both with one random load)
     uint2 *ms;
@@ -410,9 +410,9 @@ int cta_rest(const CtaArgs &A, bool v6, uint32_t nreqA, const uint64_t *presorte
 int cta_route(const CtaArgs &A, hipStream_t s);
 // lb (ct4_lb / ct6_lb, or null): the records carry slave | loopback << 16 |
 // 1 << 31 in pad
-int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+int cta_collect(const Ct4Slot *ct4, CtState *st, const uint4 *lb, uint64_t slots,
                 CtSyncRec *out, uint32_t cap, uint32_t *cnt, hipStream_t s);
-int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+int cta_collect6(const Ct6Slot *ct6, CtState *st, const uint4 *lb, uint64_t slots,
                  CtSyncRec6 *out, uint32_t cap, uint32_t *cnt, hipStream_t s);
 int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
 // the IPv4 table's slots that are not free (live, tombstone or claimed),
@@ -420,6 +420,19 @@ int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
 // mirror still counts)
 int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStream_t s);
 int cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n, hipStream_t s);
+// device-side growth (ct_grow): every key-holding slot of the old table
+// (ok: Ct4Slot / Ct6Slot, oslots) into the new one (nk, nmask + 1 slots,
+// zeroed), with its CtState line (ost -> nst) and LB word (olb -> nlb, when
+// olb); map[old slot] = new slot or NONE; *cnt += the slots moved
+int ct_rehash(bool v6, const void *ok, const CtState *ost, const uint4 *olb, uint64_t oslots,
+              void *nk, CtState *nst, uint4 *nlb, uint32_t nmask, uint32_t *map, uint32_t *cnt,
+              hipStream_t s);
+// slot[i * stride] = map[slot[i * stride]] for i < n (NONE stays NONE)
+int ct_remap(uint32_t *slot, uint64_t n, uint32_t stride, const uint32_t *map, hipStream_t s);
+// a built table's CtTimer array (device) into its n CtState lines
+int ct_state_init(CtState *st, const CtTimer *tm, uint64_t n, hipStream_t s);
+// the n lines' accounting into out ([slot][4] u64, device), cleared in the lines
+int ct_acct_take(CtState *st, uint64_t *out, uint64_t n, hipStream_t s);
 
 // ---- CT garbage collection (cfc_ct_gc): ctmap.GC's doFiltering
 // (pkg/maps/ctmap/ctmap.go:303-325) over the device CT4 table.  A deleted
@@ -439,9 +452,7 @@ struct CtGcRec {
 };
 struct CtGcArgs {
     Ct4Slot *ct4;
-    CtTimer *tm;
-    CtInfo *info;
-    uint64_t *acct;               // [slot][4] (may be null)
+    CtState *st;                  // the IPv4 slots' lines
     uint64_t slots;
     uint32_t mask;
     // the CT maps selected (owner word | kind << 1: 0 TCP map, 1 ANY map);

@@ -436,7 +436,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                     evw = trace_word(
                                         prox ? OBS_TO_PROXY : OBS_TO_LXC, drec.z & 0xFFFF,
                                         (uint32_t)c.res,
-                                        ct_monitor(T, CT ? T.ct6_tm : nullptr, c.slot,
+                                        ct_monitor(T, CT ? T.ct_st + T.ct6_acct_base : nullptr, c.slot,
                                                    CT_INGRESS, ct_action(true, proto, pt, mt),
                                                    tfl, c.dport));
                             }
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                     const uint32_t mon1 =
                         !NT ? 0u
                         : c.res == CT_NEW ? TRACE_PAYLOAD_LEN
-                                          : ct_monitor(T, CT ? T.ct6_tm : nullptr, c.slot,
+                                          : ct_monitor(T, CT ? T.ct_st + T.ct6_acct_base : nullptr, c.slot,
                                                        CT_EGRESS, ct_action(true, proto, tpt, mt),
                                                        tfl, c.dport);
                     // a reply of a load-balanced flow: the packet's source
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
                                 met1 = prox ? NONE : mkey6<MODE>(0, METRIC_INGRESS);
                                 if (NT) {
                                     const uint32_t a2 = ct_action(true, proto, LB ? ppt : pt, mt);
-                                    uint32_t mon2 = ct_monitor(T, CT ? T.ct6_tm : nullptr,
+                                    uint32_t mon2 = ct_monitor(T, CT ? T.ct_st + T.ct6_acct_base : nullptr,
                                                                c2.slot, CT_INGRESS, a2, tfl,
                                                                c2.dport);
                                     if (fresh)   // the entry as ct_create6 just wrote it

@@ -211,12 +211,12 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                         // creates (ctorder.hip): a request, resolved after
                         // the inserts and replayed in the fold
                         fh[u][st] = true;
-                        home[u][st] = (rev ? khash(o.da, o.sa, o.z1, o.w1)
-                                           : khash(o.sa, o.da, o.z2, o.w2)) & A.mask;
+                        home[u][st] = (rev ? khome(o.da, o.sa, o.z1, o.w1)
+                                           : khome(o.sa, o.da, o.z2, o.w2)) & A.mask;
                         ncr++;
                     }
                 } else if (o.kind == OP_CREATE) {
-                    home[u][st] = khash(o.sa, o.da, o.z2, o.w2) & A.mask;
+                    home[u][st] = khome(o.sa, o.da, o.z2, o.w2) & A.mask;
                     ncr++;
                 }
             }
@@ -358,8 +358,8 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                             ct_acct_key(sl + A.acct_base, (int)o.dir);
                 }
                 if (sl == NONE) {   // a hit on an entry an earlier header creates
-                    const uint32_t home = (rev ? khash(o.da, o.sa, o.z1, o.w1)
-                                               : khash(o.sa, o.da, o.z2, o.w2)) & A.mask;
+                    const uint32_t home = (rev ? khome(o.da, o.sa, o.z1, o.w1)
+                                               : khome(o.sa, o.da, o.z2, o.w2)) & A.mask;
                     put(pack(A, home, ord_of(i, st, SEC_FHIT)));
                     if constexpr (!V6)
                         if (A.rk4)
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                     order_mark(A, sl, MARK_ORDERED);
                 }
             } else if (o.kind == OP_CREATE) {
-                put(pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP)));
+                put(pack(A, khome(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP)));
                 if constexpr (!V6)
                     if (A.rk4)
                         A.rk4[TWO ? 2 * i + st : i] = make_uint4(o.sa, o.da, o.z2, o.w2);
@@ -594,7 +594,7 @@ __global__ __launch_bounds__(256) void k_cta_lb(CtaArgs A)
         lb_step(A, i, svc, st, o);
         reinterpret_cast<LbRecT<V6> *>(A.lbr)[i] = o;
         want = (o.fl & LBF_SVC) && ((A.ctb[i] & CFC_CT_DONE) || A.ver[i] == DROP_NO_SERVICE);
-        home = khash(d, s, z, w) & A.mask;
+        home = khome(d, s, z, w) & A.mask;
     }
     const uint32_t r = block_count(&A.cnt[CTA_NSVC], want);
     if (want)
@@ -674,8 +674,8 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                 const uint32_t sl = rev ? find(A, o.da, o.sa, o.z1, o.w1)
                                         : find(A, o.sa, o.da, o.z2, o.w2);
                 if (sl == NONE) {
-                    const uint32_t h = rev ? khash(o.da, o.sa, o.z1, o.w1)
-                                           : khash(o.sa, o.da, o.z2, o.w2);
+                    const uint32_t h = rev ? khome(o.da, o.sa, o.z1, o.w1)
+                                           : khome(o.sa, o.da, o.z2, o.w2);
                     rq[ncr++] = pack(A, h & A.mask, ord_of(i, st, SEC_FHIT));
                     nfh++;
                     continue;
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                     order_mark(A, sl, MARK_ORDERED);
                 }
             } else if (o.kind == OP_CREATE) {
-                rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP));
+                rq[ncr++] = pack(A, khome(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP));
                 nkx += o.kx;
             }
         }
@@ -723,7 +723,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
                 if (o.reslave && A.lb)
                     order_mark(A, r.svc, MARK_ORDERED);
             } else if (o.kind == OP_CREATE) {
-                rq[ncr++] = pack(A, khash(o.sa, o.da, o.z2, o.w2) & A.mask,
+                rq[ncr++] = pack(A, khome(o.sa, o.da, o.z2, o.w2) & A.mask,
                                  ord_of(A.n + i, 0, SEC_OP));
             }
         }
@@ -1012,13 +1012,13 @@ __global__ __launch_bounds__(RQ_B) void k_cta_related(CtaArgs A, const uint64_t 
     if (rb) {
         if (b < A.req_cap) {
             const uint32_t h =
-                khash(o.sa, o.da, 0u, ct_word(icmp_proto<V6>(), fl, o.owner)) & A.mask;
+                khome(o.sa, o.da, 0u, ct_word(icmp_proto<V6>(), fl, o.owner)) & A.mask;
             A.reqB[b] = pack(A, h, ord | SEC_REL << 1);
         }
         b++;
     }
     if (kx && b < A.req_cap)
-        A.reqB[b] = pack(A, khash(o.kxa, o.kxs, o.z2, o.kxw) & A.mask, ord | SEC_KX << 1);
+        A.reqB[b] = pack(A, khome(o.kxa, o.kxs, o.z2, o.kxw) & A.mask, ord | SEC_KX << 1);
 }
 
 // ---- route: every op on an ordered slot -> the ordered list (the plain
@@ -1102,8 +1102,8 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
                 const uint64_t k = k0 + u;
                 if (k < n2 || slot[u] == HS_NONE)
                     continue;
-                unsigned long long *ac = reinterpret_cast<unsigned long long *>(A.T.ct_acct) +
-                                         4ull * (A.acct_base + slot[u]);
+                unsigned long long *ac =
+                    reinterpret_cast<unsigned long long *>(A.st[slot[u]].acct);
                 atomicAdd(ac, 1ull);
                 atomicAdd(ac + 1, (unsigned long long)(A.mt[(k >> 1) - A.n] >> 16));
             }
@@ -1196,9 +1196,9 @@ __device__ __forceinline__ St fresh(uint32_t now, bool is_tcp, uint32_t dir)
     upd_timeout(e, now, is_tcp, dir, is_tcp, 0);
     return e;
 }
-__device__ __forceinline__ St load_state(const CtTimer *tm, uint32_t slot)
+__device__ __forceinline__ St load_state(const CtState *st, uint32_t slot)
 {
-    const uint4 t = ld16(tm + slot);
+    const uint4 t = ld16(&st[slot].tm);
     St e;
     e.last_rx = t.x;
     e.last_tx = t.y;
@@ -1209,7 +1209,7 @@ __device__ __forceinline__ St load_state(const CtTimer *tm, uint32_t slot)
     e.lifetime = t.w;
     return e;
 }
-__device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St &e)
+__device__ __forceinline__ void store_state(CtState *st, uint32_t slot, const St &e)
 {
     uint4 t;
     t.x = e.last_rx;
@@ -1217,7 +1217,7 @@ __device__ __forceinline__ void store_state(CtTimer *tm, uint32_t slot, const St
     t.z = e.seen_rx | e.seen_tx << 8 | (e.bits & 3) << 16 |
           ((e.bits & SEEN_NON_SYN) ? CTT_NON_SYN : 0u) | ((e.bits & NAT46) ? CTT_NAT46 : 0u);
     t.w = e.lifetime;
-    *reinterpret_cast<uint4 *>(tm + slot) = t;
+    *reinterpret_cast<uint4 *>(&st[slot].tm) = t;
 }
 
 // ---- dedup: in the sorted ordered list, a plain hit identical to the op
@@ -1312,7 +1312,7 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
     const uint64_t omask = (1ull << A.ob) - 1;
     const bool was_fresh = (A.ms[slot].x & MARK_FRESH) != 0;
     bool live = !was_fresh, created = false, deleted = false, reslaved = false;
-    St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.tm, slot);
+    St e = was_fresh ? St{0, 0, 0, 0, 0, 0} : load_state(A.st, slot);
     uint64_t acct[4] = {0, 0, 0, 0};   // [tx pk, tx by, rx pk, rx by] added / set
     uint32_t sec = 0, rev = 0, lbx = 0, lby = 0;
     // the next op's header is loaded (branch-free) while this one is
@@ -1401,9 +1401,9 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
         A.lb[slot] = make_uint4(lbx, lby, 0, 0);
     else if (A.lb && live && reslaved)
         A.lb[slot].y = lby;
-    unsigned long long *ac =
-        reinterpret_cast<unsigned long long *>(A.T.ct_acct) + 4ull * (A.acct_base + slot);
-    CtInfo inf = A.info[slot];
+    // (the slot's report state, counters and record: one CtState line)
+    unsigned long long *ac = reinterpret_cast<unsigned long long *>(A.st[slot].acct);
+    CtInfo inf = A.st[slot].info;
     if (!live) {
         // ct_delete4/6: the entry and its counts go; the key stays readable
         // for the host (w | CT_TOMBSTONE) until it has synchronised
@@ -1412,7 +1412,7 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
         ac[0] = ac[1] = ac[2] = ac[3] = 0;
         inf.y |= CTI_DELETED;
     } else if (created) {
-        store_state(A.tm, slot, e);
+        store_state(A.st, slot, e);
         ac[0] = acct[0];
         ac[1] = acct[1];
         ac[2] = acct[2];
@@ -1421,14 +1421,14 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
         inf.y = (inf.y & ~0xFFFFu) | rev | CTI_CREATED | (deleted ? CTI_DELETED : 0u) |
                 (was_fresh ? CTI_FRESH : 0u) | (inf.y & CTI_FRESH);
     } else {
-        store_state(A.tm, slot, e);
+        store_state(A.st, slot, e);
         ac[0] += acct[0];
         ac[1] += acct[1];
         ac[2] += acct[2];
         ac[3] += acct[3];
         inf.y |= CTI_UPDATED;
     }
-    A.info[slot] = inf;
+    A.st[slot].info = inf;
     A.ms[slot] = make_uint2(0, 0);
     if (A.sum)   // (replayed here: the finish leaves the slot alone)
         A.sum[slot] = 0;
@@ -1630,7 +1630,7 @@ __global__ __launch_bounds__(256) void k_cta_fold_fin(CtaArgs A, const uint64_t 
             fold_run<V6, LB>(A, cx, ncx, r0);
             continue;
         }
-        St e = load_state(A.tm, slot);
+        St e = load_state(A.st, slot);
         const uint32_t now = A.now;
         for (int d = 0; d < 2; d++) {   // 0: rx (ingress), 1: tx
             if (!((w[RW_ANY] >> d) & 1))
@@ -1661,10 +1661,8 @@ __global__ __launch_bounds__(256) void k_cta_fold_fin(CtaArgs A, const uint64_t 
         const uint32_t life = !tcp ? CT_LIFETIME_NONTCP
                               : (e.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP : CT_SYN_TIMEOUT;
         e.lifetime = now + ((cb & 3u) == 3u ? CT_CLOSE_TIMEOUT : life);
-        store_state(A.tm, slot, e);
-        CtInfo inf = A.info[slot];
-        inf.y |= CTI_UPDATED;
-        A.info[slot] = inf;
+        store_state(A.st, slot, e);
+        A.st[slot].info.y |= CTI_UPDATED;
         A.ms[slot] = make_uint2(0, 0);
         if (A.sum)
             A.sum[slot] = 0;
@@ -1741,13 +1739,17 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
                 for (int q = 1; q < FU; q++)   // (m[u], without dynamic indexing)
                     m4[j] = u == q ? m[q] : m4[j];
             }
+            // the slot's report state and record: one CtState line.  (The
+            // entry's protocol is in the summary: every hit a finish sees
+            // is a plain hit without the close bit — closes and deletes
+            // are ordered — so a TCP entry's summary always carries bit 18,
+            // "a TCP hit without the close bit", and no other entry's does.)
             St x4[4];
-            uint32_t w4[4], iy[4];
+            uint32_t iy[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                x4[j] = load_state(A.tm, sl4[j]);
-                w4[j] = *slot_w<V6>(A, sl4[j]);
-                iy[j] = A.info[sl4[j]].y;
+                x4[j] = load_state(A.st, sl4[j]);
+                iy[j] = A.st[sl4[j]].info.y;
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -1755,19 +1757,16 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
                 continue;
             const uint32_t sl = sl4[j];
             St x = x4[j];
-            const uint32_t w = w4[j];
             const uint32_t mu = m4[j];
             if (A.sum)
                 A.sum[sl] = 0;
             else
                 A.ms[sl].x = 0;
             x.bits &= ~(RX_CLOSING | TX_CLOSING);
-            const bool is_tcp = (w & 0xFF) == 6;
-            if (is_tcp && (mu & (1u << 18)))
+            const bool is_tcp = (mu & (1u << 18)) != 0;
+            if (is_tcp)
                 x.bits |= SEEN_NON_SYN;
-            x.lifetime = A.now + (is_tcp ? ((x.bits & SEEN_NON_SYN) ? CT_LIFETIME_TCP
-                                                                    : CT_SYN_TIMEOUT)
-                                         : CT_LIFETIME_NONTCP);
+            x.lifetime = A.now + (is_tcp ? CT_LIFETIME_TCP : CT_LIFETIME_NONTCP);
             if (mu & (1u << 16)) {
                 const uint32_t seen = (x.seen_rx | (mu & 0xFF)) & 0xFF;
                 if (x.last_rx + CT_REPORT_INTERVAL < A.now || seen != x.seen_rx)
@@ -1780,8 +1779,8 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
                     x.last_tx = A.now;
                 x.seen_tx = seen;
             }
-            store_state(A.tm, sl, x);
-            A.info[sl].y = iy[j] | CTI_UPDATED;
+            store_state(A.st, sl, x);
+            A.st[sl].info.y = iy[j] | CTI_UPDATED;
             }
         }
     }
@@ -1854,7 +1853,7 @@ struct SyncOf<true> {
 };
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::Slot *ct,
-                                                     CtTimer *tm, CtInfo *info, const uint4 *lb,
+                                                     CtState *st, const uint4 *lb,
                                                      uint64_t slots,
                                                      typename SyncOf<V6>::Rec *out,
                                                      uint32_t cap, uint32_t *cnt)
@@ -1868,7 +1867,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::
 #pragma unroll
         for (int u = 0; u < CU; u++) {
             const uint64_t s = base + u * 256 + threadIdx.x;
-            in[u] = s < slots ? info[s] : CtInfo{0, 0};
+            in[u] = s < slots ? st[s].info : CtInfo{0, 0};
             nd += (in[u].y >> 16) != 0;
         }
         uint4 k[CU], t[CU], k2[CU], k3[CU], l[CU];
@@ -1883,7 +1882,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::
                 } else {
                     k[u] = ld16(ct + s);
                 }
-                t[u] = ld16(tm + s);
+                t[u] = ld16(&st[s].tm);
                 l[u] = lb ? ld16(lb + s) : make_uint4(0, 0, 0, 0);
             }
         }
@@ -1913,7 +1912,7 @@ __global__ __launch_bounds__(256) void k_cta_collect(const typename SyncOf<V6>::
                 o.flags = t[u].z;
                 o.lifetime = t[u].w;
                 o.pad = lb ? (l[u].y & 0xFFFF) | ((l[u].x >> 16) & 1) << 16 | 1u << 31 : 0u;
-                info[s].y = in[u].y & 0xFFFFu;
+                st[s].info.y = in[u].y & 0xFFFFu;
             }
             r++;
         }
@@ -1963,6 +1962,121 @@ __global__ __launch_bounds__(256) void k_ct_nonfree4(const Ct4Slot *ct4, uint64_
             c += w[u] != 0;
     }
     block_add(cnt, c);
+}
+
+// ---- device-side growth of a CT table (cfc_api.cpp ct_grow) ---------------
+// The reference's CT maps are fixed-size LRU hashes that never stop for an
+// insert (bpf_lxc.c:53-89); the device table is open-addressed and sized at
+// commit, so a batch that would take it past 3/4 load moves it into a table
+// with more slots here, on the device: every slot that holds a key — a live
+// entry, or one an apply deleted that the host has not taken yet (w |
+// CT_TOMBSTONE: its record goes to the host at the next ct_sync) — is
+// inserted at its home slot's probe sequence in the new table (a CAS on the
+// free word: the new table has no other writer), with its CtState line and
+// load-balancer word; plain tombstones and free slots are dropped.  map[old
+// slot] = its new slot (NONE: dropped): the host mirror and the pending GC
+// log follow it (ct_grow).  Four old slots per thread and step, each phase's
+// loads issued together.
+template <bool V6>
+__global__ __launch_bounds__(256) void k_ct_rehash(const typename SyncOf<V6>::Slot *ok,
+                                                   const CtState *ost, const uint4 *olb,
+                                                   uint64_t oslots,
+                                                   typename SyncOf<V6>::Slot *nk, CtState *nst,
+                                                   uint4 *nlb, uint32_t nmask, uint32_t *map,
+                                                   uint32_t *cnt)
+{
+    constexpr int RU = 4;
+    uint32_t moved = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * RU;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * RU; base < oslots; base += stride) {
+        uint32_t w[RU];
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const uint64_t sl = base + u * 256 + threadIdx.x;
+            w[u] = sl < oslots ? ok[sl].w : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < RU; u++) {
+            const uint64_t sl = base + u * 256 + threadIdx.x;
+            if (sl >= oslots)
+                continue;
+            if (w[u] == 0 || w[u] == CT_TOMBSTONE) {
+                map[sl] = NONE;
+                continue;
+            }
+            // (a deleted entry is placed by its key's own word)
+            const uint32_t w0 = (w[u] & CT_TOMBSTONE) == CT_TOMBSTONE ? w[u] & ~CT_TOMBSTONE : w[u];
+            uint32_t i;
+            if constexpr (V6) {
+                const uint4 d = ld16(ok[sl].d), sa = ld16(ok[sl].s);
+                const uint32_t z = ok[sl].z;
+                const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {sa.x, sa.y, sa.z, sa.w};
+                for (i = ct_home6(dw, sw, z, w0) & nmask;; i = (i + 1) & nmask)
+                    if (atomicCAS(&nk[i].w, 0u, w[u]) == 0u)
+                        break;
+                *reinterpret_cast<uint4 *>(nk[i].d) = d;
+                *reinterpret_cast<uint4 *>(nk[i].s) = sa;
+                nk[i].z = z;
+            } else {
+                const uint4 k = ld16(ok + sl);
+                for (i = ct_home4(k.x, k.y, k.z, w0) & nmask;; i = (i + 1) & nmask)
+                    if (atomicCAS(&nk[i].w, 0u, w[u]) == 0u)
+                        break;
+                nk[i].x = k.x;
+                nk[i].y = k.y;
+                nk[i].z = k.z;
+            }
+            const uint4 *src = reinterpret_cast<const uint4 *>(ost + sl);
+            uint4 *dst = reinterpret_cast<uint4 *>(nst + i);
+            const uint4 l0 = src[0], l1 = src[1], l2 = src[2], l3 = src[3];
+            dst[0] = l0;
+            dst[1] = l1;
+            dst[2] = l2;
+            dst[3] = l3;
+            if (olb)
+                nlb[i] = olb[sl];
+            map[sl] = i;
+            moved++;
+        }
+    }
+    block_add(cnt, moved);
+}
+// slots recorded against an older table, through its map (NONE: dropped)
+__global__ __launch_bounds__(256) void k_ct_remap(uint32_t *slot, uint64_t n, uint32_t stride,
+                                                  const uint32_t *map)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    uint32_t &v = slot[i * stride];
+    v = v == NONE ? NONE : map[v];
+}
+
+// ---- the CtState lines from and to the host ---------------------------------
+// a built table's report state (the flattened CtTimer array) into its lines
+// (the rest of each line zero: no counts, no record)
+__global__ __launch_bounds__(256) void k_ct_st_init(CtState *st, const CtTimer *tm, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    uint4 *l = reinterpret_cast<uint4 *>(st + i);
+    l[0] = ld16(tm + i);
+    l[1] = l[2] = l[3] = make_uint4(0, 0, 0, 0);
+}
+// the CONNTRACK_ACCOUNTING counts of every line into a dense [slot][4]
+// array for the host's fold, and the lines' counts cleared
+__global__ __launch_bounds__(256) void k_ct_acct_take(CtState *st, ulonglong2 *out, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n)
+        return;
+    ulonglong2 *a = reinterpret_cast<ulonglong2 *>(st[i].acct);
+    const ulonglong2 x = a[0], y = a[1];
+    out[2 * i] = x;
+    out[2 * i + 1] = y;
+    if (x.x | x.y | y.x | y.y)
+        a[0] = a[1] = make_ulonglong2(0, 0);
 }
 
 // ---- garbage collection (cfc_ct_gc, ctmap.go:303-325 doFiltering) ---------
@@ -2047,9 +2161,9 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
                        : -1;
         }
 #pragma unroll
-        for (int u = 0; u < GC_U; u++) {   // (every slot's: no branch between the loads)
+        for (int u = 0; u < GC_U; u++) {   // (an entry's line only: one per live slot)
             const uint64_t s = base + u * GC_B + threadIdx.x;
-            life[u] = A.tm[s < A.slots ? s : A.slots - 1].lifetime;
+            life[u] = j[u] >= 0 ? A.st[s].tm.lifetime : 0u;
         }
         bool del[GC_U], logit[GC_U];
 #pragma unroll
@@ -2057,7 +2171,7 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
             const uint64_t s = base + u * GC_B + threadIdx.x;
             del[u] = j[u] >= 0 && gc_delete(A, k[u].x, k[u].y, life[u]) &&
                      !(A.protect && ((A.protect[s >> 5] >> (s & 31)) & 1u));
-            infy[u] = del[u] ? A.info[s].y : 0u;
+            infy[u] = del[u] ? A.st[s].info.y : 0u;
         }
         uint32_t nl = 0;
 #pragma unroll
@@ -2082,10 +2196,10 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
                 atomicAdd(&scnt[j[u]], 1u);
             }
             *reinterpret_cast<uint4 *>(A.ct4 + s) = make_uint4(0, 0, 0, CT_TOMBSTONE);
-            A.info[s] = CtInfo{0, 0};
-            if (A.acct)
-                *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s) =
-                    *reinterpret_cast<ulonglong2 *>(A.acct + 4 * s + 2) = make_ulonglong2(0, 0);
+            // (the line's counters and record; its report state is dead)
+            ulonglong2 *a = reinterpret_cast<ulonglong2 *>(A.st[s].acct);
+            a[0] = a[1] = make_ulonglong2(0, 0);
+            A.st[s].info = CtInfo{0, 0};
         }
         // the tails of this step's clusters: a plain tombstone whose run of
         // tombstones ends at a free slot is freed (a live entry keeps the
@@ -2615,19 +2729,19 @@ int cta_newkeys(const CtaArgs &A, bool v6, uint32_t nreqA, uint64_t **sorted, ui
               : cta_newkeys_t<false>(A, nreqA, sorted, newk, s);
 }
 
-int cta_collect(const Ct4Slot *ct4, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+int cta_collect(const Ct4Slot *ct4, CtState *st, const uint4 *lb, uint64_t slots,
                 CtSyncRec *out, uint32_t cap, uint32_t *cnt, hipStream_t s)
 {
     hipLaunchKernelGGL(k_cta_collect<false>, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct4,
-                       tm, info, lb, slots, out, cap, cnt);
+                       st, lb, slots, out, cap, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
-int cta_collect6(const Ct6Slot *ct6, CtTimer *tm, CtInfo *info, const uint4 *lb, uint64_t slots,
+int cta_collect6(const Ct6Slot *ct6, CtState *st, const uint4 *lb, uint64_t slots,
                  CtSyncRec6 *out, uint32_t cap, uint32_t *cnt, hipStream_t s)
 {
     hipLaunchKernelGGL(k_cta_collect<true>, dim3(blocks_for(slots, 8192)), dim3(256), 0, s, ct6,
-                       tm, info, lb, slots, out, cap, cnt);
+                       st, lb, slots, out, cap, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -2657,6 +2771,45 @@ int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStre
     if (slots)
         hipLaunchKernelGGL(k_ct_nonfree4, dim3(blocks_for(slots, 2048)), dim3(256), 0, s, ct4,
                            slots, cnt);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_rehash(bool v6, const void *ok, const CtState *ost, const uint4 *olb, uint64_t oslots,
+              void *nk, CtState *nst, uint4 *nlb, uint32_t nmask, uint32_t *map, uint32_t *cnt,
+              hipStream_t s)
+{
+    if (v6)
+        hipLaunchKernelGGL(k_ct_rehash<true>, dim3(blocks_for(oslots, 8192)), dim3(256), 0, s,
+                           (const Ct6Slot *)ok, ost, olb, oslots, (Ct6Slot *)nk, nst, nlb, nmask,
+                           map, cnt);
+    else
+        hipLaunchKernelGGL(k_ct_rehash<false>, dim3(blocks_for(oslots, 8192)), dim3(256), 0, s,
+                           (const Ct4Slot *)ok, ost, olb, oslots, (Ct4Slot *)nk, nst, nlb, nmask,
+                           map, cnt);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_remap(uint32_t *slot, uint64_t n, uint32_t stride, const uint32_t *map, hipStream_t s)
+{
+    if (n)
+        hipLaunchKernelGGL(k_ct_remap, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slot, n,
+                           stride, map);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_state_init(CtState *st, const CtTimer *tm, uint64_t n, hipStream_t s)
+{
+    if (n)
+        hipLaunchKernelGGL(k_ct_st_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st,
+                           tm, n);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_acct_take(CtState *st, uint64_t *out, uint64_t n, hipStream_t s)
+{
+    if (n)
+        hipLaunchKernelGGL(k_ct_acct_take, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, st,
+                           reinterpret_cast<ulonglong2 *>(out), n);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

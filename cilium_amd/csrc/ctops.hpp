@@ -220,6 +220,17 @@ __device__ __forceinline__ uint32_t khash(uint4 d, uint4 s, uint32_t z, uint32_t
     const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {s.x, s.y, s.z, s.w};
     return ct_hash6(dw, sw, z, w);
 }
+// the key's home slot (placement, layout.h ct_home4 / ct_home6; khash is
+// the mixer the fingerprints use)
+__device__ __forceinline__ uint32_t khome(uint32_t d, uint32_t s, uint32_t z, uint32_t w)
+{
+    return ct_home4(d, s, z, w);
+}
+__device__ __forceinline__ uint32_t khome(uint4 d, uint4 s, uint32_t z, uint32_t w)
+{
+    const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {s.x, s.y, s.z, s.w};
+    return ct_home6(dw, sw, z, w);
+}
 template <bool V6>
 __device__ __forceinline__ Addr<V6> ld_addr(const uint32_t *p, uint64_t i)
 {
@@ -518,7 +529,7 @@ __device__ __forceinline__ uint32_t find(const CtaArgs &A, uint32_t x, uint32_t 
                                          uint32_t w)
 {
     const uint32_t mask = A.mask;
-    for (uint32_t i = ct_hash4(x, y, z, w) & mask;; i = (i + 1) & mask) {
+    for (uint32_t i = ct_home4(x, y, z, w) & mask;; i = (i + 1) & mask) {
         const uint4 s = ld16(A.ct4 + i);
         if (s.w == 0)
             return NONE;
@@ -530,7 +541,7 @@ __device__ __forceinline__ uint32_t find(const CtaArgs &A, uint4 d, uint4 s, uin
                                          uint32_t w)
 {
     const uint32_t mask = A.mask;
-    for (uint32_t i = khash(d, s, z, w) & mask;; i = (i + 1) & mask) {
+    for (uint32_t i = khome(d, s, z, w) & mask;; i = (i + 1) & mask) {
         const uint4 t = ld16(&A.ct6[i].z);   // {z, w, 0, 0}: compared first
         if (t.y == 0)
             return NONE;
@@ -573,7 +584,7 @@ __device__ uint32_t find_or_insert(const CtaArgs &A, Addr<V6> d, Addr<V6> s, uin
     if (f != NONE)
         return f;
     const uint32_t mask = A.mask;
-    for (uint32_t i = khash(d, s, z, w) & mask;; i = (i + 1) & mask) {
+    for (uint32_t i = khome(d, s, z, w) & mask;; i = (i + 1) & mask) {
         uint32_t *pw = slot_w<V6>(A, i);
         const uint32_t cur = __hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (cur != 0 && cur != CT_TOMBSTONE)

@@ -674,7 +674,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                 continue;
             const CtTimer tm = ct_timer_of(kv.second.val);
             if (!v6) {
-                uint32_t i = ct_hash4(e.x, e.y, e.z, e.w) & img->ct4_mask, p = 0;
+                uint32_t i = ct_home4(e.x, e.y, e.z, e.w) & img->ct4_mask, p = 0;
                 while (img->ct4[i].w) {
                     i = (i + 1) & img->ct4_mask;
                     p++;
@@ -688,7 +688,7 @@ static void build_ct(const std::vector<const Map *> &cts, HostImage *img)
                 img->n_nat46 += (tm.flags & CTT_NAT46) != 0;
             } else {
                 const Ct6Slot &e = e6;
-                uint32_t i = ct_hash6(e.d, e.s, e.z, e.w) & img->ct6_mask, p = 0;
+                uint32_t i = ct_home6(e.d, e.s, e.z, e.w) & img->ct6_mask, p = 0;
                 while (img->ct6[i].w) {
                     i = (i + 1) & img->ct6_mask;
                     p++;

@@ -324,7 +324,7 @@ __device__ __forceinline__ uint32_t ct4_find(const DevTables &T, uint32_t x,
 {
     if (!T.ct4)
         return NONE;
-    const uint32_t i = ct_hash4(x, y, z, w) & T.ct4_mask;
+    const uint32_t i = ct_home4(x, y, z, w) & T.ct4_mask;
     return ct4_walk(T, i, ld16(T.ct4 + i), x, y, z, w);
 }
 
@@ -335,7 +335,7 @@ __device__ __forceinline__ uint32_t ct6_find(const DevTables &T, const uint4 &d,
     if (!T.ct6)
         return NONE;
     const uint32_t dw[4] = {d.x, d.y, d.z, d.w}, sw[4] = {sa.x, sa.y, sa.z, sa.w};
-    uint32_t i = ct_hash6(dw, sw, z, w) & T.ct6_mask;
+    uint32_t i = ct_home6(dw, sw, z, w) & T.ct6_mask;
     for (uint32_t p = 0; p <= T.ct6_probe; p++) {
         const Ct6Slot *e = T.ct6 + i;
         const uint4 t = ld16(&e->z);
@@ -370,19 +370,30 @@ __device__ __forceinline__ CtResult ct_stage4(const DevTables &T, uint32_t sa,
         r.dport = k.ts;
         return r;
     }
-    // both home slots in flight together: an ESTABLISHED or NEW packet (k1
-    // misses) then costs one HBM round trip instead of two
-    const uint32_t i1 = ct_hash4(da, sa, k.z1, k.w1) & T.ct4_mask;
-    const uint32_t i2 = ct_hash4(sa, da, k.z2, k.w2) & T.ct4_mask;
-    const uint4 s1 = ld16(T.ct4 + i1), s2 = ld16(T.ct4 + i2);
-    r.slot = ct4_walk(T, i1, s1, da, sa, k.z1, k.w1);
-    if (r.slot != NONE) {
-        r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
-        r.dport = k.td;
-        return r;
+    // k1 and k2 share their home slot (ct_home4): one walk from it to the
+    // first free slot answers both lookups — k1 wins wherever it sits
+    // (__ct_lookup tries the reply direction first), else the slot where k2
+    // was passed.  An ESTABLISHED or NEW packet then costs one probe chain,
+    // not two.
+    uint32_t i = ct_home4(da, sa, k.z1, k.w1) & T.ct4_mask;
+    uint4 s = ld16(T.ct4 + i);
+    uint32_t s2 = NONE;
+    for (uint32_t p = 0; p <= T.ct4_probe; p++) {
+        if (s.w == 0)
+            break;
+        if (s.x == da && s.y == sa && s.z == k.z1 && s.w == k.w1) {
+            r.slot = i;
+            r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
+            r.dport = k.td;
+            return r;
+        }
+        if (s2 == NONE && s.x == sa && s.y == da && s.z == k.z2 && s.w == k.w2)
+            s2 = i;
+        i = (i + 1) & T.ct4_mask;
+        s = ld16(T.ct4 + i);
     }
-    r.slot = ct4_walk(T, i2, s2, sa, da, k.z2, k.w2);
-    r.res = r.slot != NONE ? CT_ESTABLISHED : CT_NEW;
+    r.slot = s2;
+    r.res = s2 != NONE ? CT_ESTABLISHED : CT_NEW;
     r.dport = k.ts;
     return r;
 }
@@ -393,15 +404,39 @@ __device__ __forceinline__ CtResult ct_stage6(const DevTables &T, const uint4 &s
 {
     const CtProbe k = ct_probe<true>(proto, pt, dir, owner);
     CtResult r;
-    r.slot = ct6_find(T, da, sa, k.z1, k.w1);
-    if (r.slot != NONE) {
-        r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
-        r.dport = k.td;
-        return r;
-    }
-    r.slot = ct6_find(T, sa, da, k.z2, k.w2);
-    r.res = r.slot != NONE ? CT_ESTABLISHED : CT_NEW;
+    r.slot = NONE;
+    r.res = CT_NEW;
     r.dport = k.ts;
+    if (!T.ct6)
+        return r;
+    // one walk for k1 and k2 from their shared home slot (ct_home6), as
+    // ct_stage4; a slot's {z, w} words are compared first
+    const uint32_t dw[4] = {da.x, da.y, da.z, da.w}, sw[4] = {sa.x, sa.y, sa.z, sa.w};
+    uint32_t i = ct_home6(dw, sw, k.z1, k.w1) & T.ct6_mask;
+    uint32_t s2 = NONE;
+    for (uint32_t p = 0; p <= T.ct6_probe; p++) {
+        const Ct6Slot *e = T.ct6 + i;
+        const uint4 t = ld16(&e->z);
+        if (t.y == 0)
+            break;
+        const bool m1 = t.x == k.z1 && t.y == k.w1, m2 = s2 == NONE && t.x == k.z2 && t.y == k.w2;
+        if (m1 || m2) {
+            const uint4 a = ld16(e->d), b = ld16(e->s);
+            if (m1 && a.x == da.x && a.y == da.y && a.z == da.z && a.w == da.w &&
+                b.x == sa.x && b.y == sa.y && b.z == sa.z && b.w == sa.w) {
+                r.slot = i;
+                r.res = (k.w1 & 0x200u) ? CT_RELATED : CT_REPLY;
+                r.dport = k.td;
+                return r;
+            }
+            if (m2 && a.x == sa.x && a.y == sa.y && a.z == sa.z && a.w == sa.w &&
+                b.x == da.x && b.y == da.y && b.z == da.z && b.w == da.w)
+                s2 = i;
+        }
+        i = (i + 1) & T.ct6_mask;
+    }
+    r.slot = s2;
+    r.res = s2 != NONE ? CT_ESTABLISHED : CT_NEW;
     return r;
 }
 
@@ -456,13 +491,15 @@ __device__ __forceinline__ uint32_t ct_monitor_of(const DevTables &T, uint4 t, i
     }
     return m;
 }
-__device__ __forceinline__ uint32_t ct_monitor(const DevTables &T, const CtTimer *tm,
+// (st: the family's CtState lines, T.ct_st or T.ct_st + T.ct6_acct_base;
+// null: no CT table)
+__device__ __forceinline__ uint32_t ct_monitor(const DevTables &T, const CtState *st,
                                                uint32_t slot, int dir, uint32_t action,
                                                uint32_t fl, uint32_t dport)
 {
     uint32_t m = TRACE_PAYLOAD_LEN;
-    if (slot != NONE && tm) {
-        const uint4 t = ld16(tm + slot);
+    if (slot != NONE && st) {
+        const uint4 t = ld16(&st[slot].tm);
         const bool in = dir == CT_INGRESS;
         uint32_t last = in ? t.x : t.y;
         uint32_t acc = in ? (t.z & 0xFF) : ((t.z >> 8) & 0xFF);
@@ -676,10 +713,16 @@ __device__ __forceinline__ bool icmp6_punt(const DevTables &T, uint32_t proto,
                            da.z == T.router6[2] && da.w == T.router6[3]);
 }
 
-// key of ct_acct[slot][dir] (k_ct_count), NONE for a miss
+// key of CtState[slot].acct[dir] (k_ct_count), NONE for a miss
 __device__ __forceinline__ uint32_t ct_acct_key(uint32_t slot, int dir)
 {
     return slot == NONE ? NONE : slot * 2 + (uint32_t)dir;
+}
+// the {packets, bytes} pair of accounting key k (slot * 2 + dir, slot
+// counted from the first IPv4 slot)
+__device__ __forceinline__ unsigned long long *ct_acct_at(CtState *st, uint64_t k)
+{
+    return reinterpret_cast<unsigned long long *>(st[k >> 1].acct) + 2 * (k & 1);
 }
 // A CT_NEW stage leaves in the same key array a tag instead: CK_MISS | a
 // hash of its k2 (owner word included) | 1 when k2 carries TUPLE_F_RELATED
@@ -745,8 +788,7 @@ __device__ __forceinline__ void ct_account(const DevTables &T, uint32_t slot,
 {
     if (slot == NONE)
         return;
-    unsigned long long *a =
-        reinterpret_cast<unsigned long long *>(T.ct_acct) + 4ull * slot + 2 * dir;
+    unsigned long long *a = ct_acct_at(T.ct_st, slot * 2 + (uint32_t)dir);
     atomicAdd(a, 1ull);
     atomicAdd(a + 1, (unsigned long long)len);
 }

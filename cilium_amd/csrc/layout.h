@@ -262,7 +262,8 @@ constexpr uint32_t LXC6_LDS_MAX_SLOTS = 256;      // 8 KiB
 //   v6 slot (48 B): daddr[4], saddr[4], {z, w, 0, 0}
 // owner: 0 = the global maps, else 1 << 11 | lxc_id << 16 (local maps).
 // Per-slot accounting (CONNTRACK_ACCOUNTING, conntrack.h:247-257) lives in
-// ct_acct[slot][dir][packets, bytes] (dir: CT_EGRESS 0 / CT_INGRESS 1).
+// the slot's CtState line (acct[dir][packets, bytes], dir: CT_EGRESS 0 /
+// CT_INGRESS 1).
 __host__ __device__ inline uint32_t ct_word(uint32_t nexthdr, uint32_t flags,
                                             uint32_t owner)
 {
@@ -293,6 +294,29 @@ __host__ __device__ inline uint32_t ct_hash6(const uint32_t d[4], const uint32_t
     h = fmix32(h ^ s[3]);
     return ct_hash4(h, z, w, 0x7f4a7c15u);
 }
+// The home slot of a CT key (the placement hash; ct_hash4 / ct_hash6 stay
+// the plain mixers the fingerprints use).  It is symmetric in the tuple's
+// direction: the two addresses and the two ports are taken as unordered
+// pairs and the direction flag (TUPLE_F_IN, bit 8 of w) is left out, so a
+// packet's two lookups — k1 = (daddr, saddr, ports as loaded, flags) for
+// REPLY / RELATED and k2 = (saddr, daddr, ports swapped, flags ^ IN) for
+// ESTABLISHED (__ct_lookup via ct_lookup4/6, conntrack.h:467-590) — start
+// their probe at the same slot, and one walk from it answers both.
+__host__ __device__ inline uint32_t ct_home4(uint32_t x, uint32_t y, uint32_t z, uint32_t w)
+{
+    const uint32_t lo = x < y ? x : y, hi = x < y ? y : x;
+    const uint32_t pa = z & 0xFFFFu, pb = z >> 16;
+    const uint32_t zs = (pa < pb ? pa : pb) | (pa < pb ? pb : pa) << 16;
+    return ct_hash4(lo, hi, zs, w & ~0x100u);
+}
+__host__ __device__ inline uint32_t ct_home6(const uint32_t d[4], const uint32_t s[4],
+                                             uint32_t z, uint32_t w)
+{
+    const uint32_t hd = ct_hash4(d[0], d[1], d[2], d[3]), hs = ct_hash4(s[0], s[1], s[2], s[3]);
+    const uint32_t pa = z & 0xFFFFu, pb = z >> 16;
+    const uint32_t zs = (pa < pb ? pa : pb) | (pa < pb ? pb : pa) << 16;
+    return ct_hash4(hd < hs ? hd : hs, hd < hs ? hs : hd, zs, (w & ~0x100u) ^ 0x7f4a7c15u);
+}
 struct alignas(16) Ct4Slot {
     uint32_t x, y, z, w;
 };
@@ -300,7 +324,7 @@ struct alignas(16) Ct4Slot {
 // what decides whether a hit is traced (__ct_update_timeout,
 // conntrack.h:125-185) and what the device CT apply (ctapply.hip) updates:
 // last_{rx,tx}_report, rx/tx_flags_seen, the rx/tx_closing and seen_non_syn
-// bits, lifetime.  The packet/byte counts live in ct_acct.
+// bits, lifetime.  The packet/byte counts sit beside it in CtState.
 struct alignas(16) CtTimer {
     uint32_t last_rx, last_tx;
     uint32_t flags;      // rx_flags_seen | tx_flags_seen << 8 | closing << 16
@@ -326,6 +350,26 @@ constexpr uint32_t CT_CLAIM = 0xE000u;
 struct alignas(16) Ct6Slot {
     uint32_t d[4], s[4], z, w, pad[2];
 };
+// Everything a CT slot's entry holds besides its key, in ONE 64-byte line
+// (struct ct_entry, common.h:380-406, as __ct_lookup / ct_create4/6 touch
+// it, conntrack.h:221-285, 615-772): the report state, the
+// CONNTRACK_ACCOUNTING counters and the device apply's per-slot record.  A
+// hit's fold, the finish, the GC and the accounting reduce each touch one
+// line per slot here (three to four separate arrays before).  The keys stay
+// a dense array of their own (Ct4Slot / Ct6Slot): the lookups probe only
+// keys, and a dense key array keeps a Zipf batch's hot keys in L2.
+//   tm     CtTimer
+//   acct   [dir][packets, bytes], dir CT_EGRESS 0 (tx) / CT_INGRESS 1 (rx)
+//   info   CtInfo
+// One array for both families: IPv4 slots, then IPv6 slots from
+// DevTables.ct6_acct_base (the accounting key slot * 2 + dir indexes it).
+struct alignas(64) CtState {
+    CtTimer tm;
+    uint64_t acct[4];
+    CtInfo info;
+    uint32_t pad[2];
+};
+static_assert(sizeof(CtState) == 64, "one line per CT slot");
 
 // ---- service load balancing (cilium_lb4_services, cilium_lb4_reverse_nat)
 // Services: open-addressed 32-byte slots keyed by struct lb4_key {address,
@@ -383,7 +427,7 @@ struct DevTables {
     // conntrack (null: every map empty -> every lookup is CT_NEW)
     const Ct4Slot *ct4;
     const Ct6Slot *ct6;
-    uint64_t *ct_acct;             // [slot][dir][packets, bytes], v4 then v6
+    CtState *ct_st;                // per slot, v4 then v6 (from ct6_acct_base)
     // per slot (as ct_acct) the plain-hit summary of the launch's hits
     // (ctapply.hip k_cta_finish's bits: flags per direction, hit per
     // direction, a TCP hit without the close bit), written by the
@@ -392,9 +436,7 @@ struct DevTables {
     uint32_t *ct_sum;
     uint32_t ct4_mask, ct4_probe;
     uint32_t ct6_mask, ct6_probe;
-    uint32_t ct6_acct_base;        // first v6 slot in ct_acct
-    const CtTimer *ct4_tm;         // report state per slot (parallel to ct4 / ct6)
-    const CtTimer *ct6_tm;
+    uint32_t ct6_acct_base;        // first v6 slot in ct_st
     // the launch: bpf_ktime_get_sec() (cfc_set_clock), HOST_IFINDEX
     uint32_t now;
     uint32_t host_ifindex;

@@ -604,7 +604,10 @@ typedef struct {
     uint32_t ct_apply_host;     /* ... and on the host */
     /* CT slots of the device tables (both families) */
     uint32_t ct_slots;
-    uint32_t pad0;
+    /* times a device CT table grew on the device (cfc_ct_apply_*: a batch
+     * that would take it past 3/4 load moves it into a table of more slots,
+     * no host rebuild), since the context opened (was pad0) */
+    uint32_t ct_grown;
     /* CT stages whose result the packet order changed from the batch-start
      * lookup (cfc_ct_apply: a later packet of a flow the batch created,
      * a packet after a delete), since the context opened (ABI 12: 64-bit,
