@@ -183,7 +183,18 @@ def reference_bpf_baseline():
     fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "cpu_reference_bpf_*.json")))
     if not fs:
         return None
+    fs.sort(key=lambda f: os.path.basename(os.path.dirname(f)))
     r = json.load(open(fs[-1]))
+    if "mpps_node" in r:   # (round 6 on: one pinned process per core, all at once)
+        return {"value": r["mpps_node"], "unit": "Mpps (node)",
+                "cores": r["cores"], "kind": "reference",
+                "mpps_per_core": r["mpps_per_core"],
+                "where": f"build container ({r['cpu']}, kernel {r['kernel']}), not the GPU box",
+                "sample": f"{r['headers']} distinct C2 headers over {r['cores']} pinned "
+                          f"processes (one per core, side by side), FULL mode (bpf_xdp -> "
+                          f"bpf_netdev -> bpf_lxc tail calls), in-program time summed per "
+                          f"process, one header per BPF_PROG_TEST_RUN",
+                "source": os.path.relpath(fs[-1], ROOT)}
     return {"value": r["mpps_per_core"], "unit": "Mpps per core",
             "cores": 1, "kind": "reference",
             "where": f"build container ({r['cpu']}, kernel {r['kernel']}), not the GPU box",
@@ -657,6 +668,16 @@ def main():
             "gc_runs": clock["gcs"],
             "gc_deleted": clock["gc_deleted"],
             "ct_entries_after_last_gc": clock["alive"],
+            # every timed step's call time (HIP events around classify +
+            # apply + GC), and the device table's growths inside the run
+            # (cfc_stats.ct_grown: the table moved into one of more slots on
+            # the device, no host rebuild) and its slots at the end
+            "step_ms": [round(a.elapsed_time(b), 3) for a, b in evs],
+            "step_ms_max_over_median": round(max(a.elapsed_time(b) for a, b in evs) /
+                                             float(np.median([a.elapsed_time(b)
+                                                              for a, b in evs])), 3),
+            "ct_grown": st2["ct_grown"],
+            "ct_slots_end": st2["ct_slots"],
         }
         if pe:   # the apply's and GC's kernels from the same PMC record
             ck = []

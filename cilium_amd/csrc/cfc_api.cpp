@@ -42,16 +42,16 @@ struct GIpc {          // ipcache, IPv4
     uint64_t bytes = 0;
 };
 struct GIpc6 {         // ipcache, IPv6 (host copy kept for in-place label patches)
-    DevBuf l6[3];
+    DevBuf l6[4];   // Lpm6: slots, bloom, lens, slots64
     Lpm6 ipc6{};
     Lpm6Host host;
     uint32_t lpm6_kib = 0, n_prefix6 = 0, lpm6_lengths = 0, lpm6_groups = 0;
     uint64_t bytes = 0;
 };
 struct GPf {           // prefilter
-    DevBuf pf24, pf8, pffix, pfbloom, l6fix[3], l6dyn[3];
+    DevBuf pf24, pf8, pffix, pfbloom, pf6bloom, l6fix[4], l6dyn[4];
     Lpm6 fix{}, dyn{};
-    uint32_t fix_mask = 0, fix_zero = 0, bloom_words = 0;
+    uint32_t fix_mask = 0, fix_zero = 0, bloom_words = 0, bloom6_words = 0;
     uint32_t n_fix4 = 0, n_dyn4 = 0, n_fix6 = 0, n_dyn6 = 0;
     uint64_t bytes = 0;
 };
@@ -161,6 +161,12 @@ struct cfc_ctx {
     // deletes of the device GC (cfc_ct_gc) the host mirror has not taken
     DevBuf gc_log, gc_tmp, gc_sets, gc_cnt;
     uint64_t gc_log_used = 0;
+    // the same for the IPv6 table (doGC6), and its exact occupancy after a
+    // GC or a growth (as ct_used for IPv4)
+    DevBuf gc_log6;
+    uint64_t gc_log6_used = 0;
+    uint64_t ct_used6 = 0;
+    bool ct_used6_valid = false;
     uint32_t cta_seq = 0;
     uint32_t n_apply_dev = 0, n_apply_host = 0;
     // the CT table's version: bumped by every commit that changes tables
@@ -468,6 +474,39 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
         }
     }
     std::string key;
+    // the device GC's deletes first (they precede every dirty record of
+    // their slots), as ct_sync does for IPv4
+    if (c->gc_log6_used) {
+        std::vector<CtGcRec6> gl(c->gc_log6_used);
+        if (hipMemcpyAsync(gl.data(), c->gc_log6.p, sizeof(CtGcRec6) * gl.size(),
+                           hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        for (const CtGcRec6 &r : gl) {
+            uint32_t d[4], sa[4];
+            memcpy(d, &r.d, 16);
+            memcpy(sa, &r.s, 16);
+            if (Map *m = ct_slot_key(E, 6, d, sa, r.z, r.w, &key))
+                m->erase_raw(key);
+            if (r.slot == 0xFFFFFFFFu) {   // (a growth since dropped its tombstone)
+                G.n_ct6--;
+                continue;
+            }
+            Ct6Slot &h = G.ct6_host[r.slot];
+            if (h.z == r.z && h.w == r.w && !memcmp(h.d, d, 16) && !memcmp(h.s, sa, 16)) {
+                G.n_ct6--;
+                G.tomb6++;
+            } else if (h.w == 0) {
+                G.tomb6++;
+            }
+            h = Ct6Slot{};
+            h.w = CT_TOMBSTONE;
+        }
+        c->gc_log6_used = 0;
+        for (auto &kv : c->maps)
+            if (kv.second->role == ROLE_CT6)
+                kv.second->gc_pending = 0;
+    }
     // deletes first (an entry deleted and created again lives in another
     // slot), then creates and updates
     for (int pass = 0; pass < 2; pass++) {
@@ -570,6 +609,16 @@ int ct_sync6(cfc_ctx *c, Epoch &E, hipStream_t s)
     c->cta_claims6 = 0;
     c->cta_ins6 = 0;
     c->ct6_dirty = false;
+    c->ct_used6_valid = false;
+    if (slots) {   // the device's exact load (a GC's trim freed tombstones the mirror holds)
+        uint32_t nonfree = 0;
+        if (hipMemsetAsync(cnt, 0, 4, s) != hipSuccess ||
+            ct_count_nonfree6((const Ct6Slot *)G.ct6.p, slots, cnt, s) ||
+            hipMemcpyAsync(&nonfree, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        G.tomb6 = nonfree >= G.n_ct6 ? (uint32_t)(nonfree - G.n_ct6) : 0u;
+    }
     E.st.ct6_entries = G.n_ct6;
     return 0;
 }
@@ -647,7 +696,8 @@ int ct_sync(cfc_ctx *c, hipStream_t s)
         }
         c->gc_log_used = 0;
         for (auto &kv : c->maps)
-            kv.second->gc_pending = 0;
+            if (kv.second->role == ROLE_CT4)
+                kv.second->gc_pending = 0;
     }
     for (int pass = 0; pass < 2; pass++) {
         for (const CtSyncRec &r : rec) {
@@ -861,9 +911,11 @@ int upload_lpm6(DevBuf *b, const Lpm6Host &h, Lpm6 *d, hipStream_t s)
 {
     int rc;
     if ((rc = upload_vec(b[0], h.slots, s)) || (rc = upload_vec(b[1], h.bloom, s)) ||
-        (rc = upload_vec(b[2], h.lens, s)))
+        (rc = upload_vec(b[2], h.lens, s)) || (rc = upload_vec(b[3], h.slots64, s)))
         return rc;
     d->slots = (const L6Slot *)b[0].p;
+    d->slots64 = (const uint4 *)b[3].p;
+    d->mask64 = h.slots64.empty() ? 0 : (uint32_t)h.slots64.size() - 1;
     d->bloom = (const uint64_t *)b[1].p;
     d->lens = (const uint32_t *)b[2].p;
     d->mask = h.slots.empty() ? 0 : (uint32_t)h.slots.size() - 1;
@@ -975,18 +1027,21 @@ std::shared_ptr<GPf> build_pf(const HostImage &img, hipStream_t s, int *rc)
     if ((*rc = upload_vec(g->pf24, img.pf_tbl24, s)) || (*rc = upload_vec(g->pf8, img.pf_tbl8, s)) ||
         (*rc = upload_vec(g->pffix, img.pf_fix, s)) ||
         (*rc = upload_vec(g->pfbloom, img.pf_bloom, s)) ||
+        (*rc = upload_vec(g->pf6bloom, img.pf6_bloom, s)) ||
         (*rc = upload_lpm6(g->l6fix, img.pf6_fix, &g->fix, s)) ||
         (*rc = upload_lpm6(g->l6dyn, img.pf6_dyn, &g->dyn, s)))
         return nullptr;
     g->fix_mask = img.pf_fix_mask;
     g->fix_zero = img.pf_fix_zero;
     g->bloom_words = (uint32_t)img.pf_bloom.size();
+    g->bloom6_words = (uint32_t)img.pf6_bloom.size();
     g->n_fix4 = img.n_pf_fix;
     g->n_dyn4 = img.n_pf_dyn;
     g->n_fix6 = img.pf6_fix.n;
     g->n_dyn6 = img.pf6_dyn.n;
     g->bytes = 4ull * (img.pf_tbl24.size() + img.pf_tbl8.size() + img.pf_fix.size() +
-                       img.pf_bloom.size()) + img.pf6_fix.bytes() + img.pf6_dyn.bytes();
+                       img.pf_bloom.size() + img.pf6_bloom.size()) + img.pf6_fix.bytes() +
+               img.pf6_dyn.bytes();
     return g;
 }
 
@@ -1141,6 +1196,8 @@ void assemble(Epoch &E)
     T.pf_bloom = (const uint32_t *)P.pfbloom.p;
     T.pf_bloom_words = P.bloom_words;
     T.pf6_fix = P.fix;
+    T.pf6_bloom = (const uint32_t *)P.pf6bloom.p;
+    T.pf6_bloom_words = P.bloom6_words;
     T.pf6_dyn = P.dyn;
     T.lxc4 = (const LxcSlot *)D.lxc4.p;
     T.lxc4_mask = D.lxc4_mask;
@@ -1231,11 +1288,20 @@ unsigned patch_touched(cfc_ctx *c, unsigned groups, hipStream_t s)
                     groups |= GROUP_IPCACHE6;
                     continue;
                 }
-                L6Slot &d = E.ipc6->host.slots[slot];
-                d.label = p.label;
-                char *dev = (char *)E.ipc6->l6[0].p + sizeof(L6Slot) * slot +
-                            offsetof(L6Slot, label);
-                if (hipMemcpyAsync(dev, &d.label, 4, hipMemcpyHostToDevice, s) != hipSuccess)
+                uint32_t *lab;
+                char *dev;
+                if (slot & L6_S64) {   // (a /1-/64 prefix: its 16-byte slot's z)
+                    uint4 &d = E.ipc6->host.slots64[slot & ~L6_S64];
+                    lab = &d.z;
+                    dev = (char *)E.ipc6->l6[3].p + 16 * (slot & ~L6_S64) + 8;
+                } else {
+                    L6Slot &d = E.ipc6->host.slots[slot];
+                    lab = &d.label;
+                    dev = (char *)E.ipc6->l6[0].p + sizeof(L6Slot) * slot +
+                          offsetof(L6Slot, label);
+                }
+                *lab = p.label;
+                if (hipMemcpyAsync(dev, lab, 4, hipMemcpyHostToDevice, s) != hipSuccess)
                     groups |= GROUP_IPCACHE6;
             }
         } else if (m->role == ROLE_POLICY && !(groups & GROUP_ENDPOINTS)) {
@@ -2142,32 +2208,6 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         ea.nat_idx = (uint32_t *)c->nat_list.p;
         ea.nat_cnt = (uint32_t *)c->nat_cnt.p;
     }
-    // an egress batch with services: the CT_SERVICE entry each header finds
-    // in packet order (the creates and re-selections of the headers before
-    // it), handed to the launch's service step
-    uint32_t nsvo = 0;
-    if (mode == CFC_MODE_EGRESS && in->n &&
-        (std::is_same<Hdr, cfc_hdr_v6>::value ? E.T.lb6 != nullptr : E.T.lb4 != nullptr)) {
-        const uint64_t n = in->n;
-        const size_t tb = svc_order_tmp_bytes(n);
-        if (c->svo_keys.bytes < 8 * n || c->svo.bytes < 4 * n || c->svo_tmp.bytes < tb) {
-            (void)hipStreamSynchronize(s);
-            if (c->svo_keys.ensure(8 * n) || c->svo_keys2.ensure(8 * n) || c->svo_tmp.ensure(tb) ||
-                c->svo.zeros(4 * n, s))
-                return -ENOMEM;
-        }
-        if (c->svo_cnt.ensure(16))
-            return -ENOMEM;
-        SvoArgs sa{(const uint32_t *)in->saddr, (const uint32_t *)in->daddr, in->ports, in->meta,
-                   in->hash, n, ep_lxc, ea.ct_owner,
-                   (uint64_t *)c->svo_keys.p, (uint64_t *)c->svo_keys2.p, (uint32_t *)c->svo.p,
-                   (uint32_t *)c->svo_cnt.p, c->svo_tmp.p, c->svo_tmp.bytes};
-        if ((rc = svc_order(T, sa, std::is_same<Hdr, cfc_hdr_v6>::value, &nsvo, s)))
-            return rc;
-        if (nsvo)
-            ea.svo = (const uint32_t *)c->svo.p;
-        c->n_svo += nsvo;
-    }
     const WsLayout wl = ws_layout(in->n, E.T, mode,
                                   E.T.ct4 || E.T.ct6 || out->ct || E.T.lb4 || E.T.rnat4 ||
                                       E.T.lb6 || E.T.rnat6);
@@ -2187,6 +2227,39 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
     // the workspace is shared: order this launch after the previous one
     if (c->ctr_pending && c->last_stream != s)
         (void)hipStreamWaitEvent(s, c->last_done, 0);
+    order_after_launches(c, s);
+    // an egress batch with services: the CT_SERVICE entry each header finds
+    // in packet order (the creates and re-selections of the headers before
+    // it), handed to the launch's service step.  (After the waits above:
+    // its per-context words and keys are shared with the previous launch,
+    // which may still read them on another stream, and it reads the CT
+    // table that launch's apply may still write.)
+    uint32_t nsvo = 0;
+    if (mode == CFC_MODE_EGRESS && in->n &&
+        (std::is_same<Hdr, cfc_hdr_v6>::value ? E.T.lb6 != nullptr : E.T.lb4 != nullptr)) {
+        const uint64_t n = in->n;
+        const size_t tb = svc_order_tmp_bytes(n);
+        if (c->svo_keys.bytes < 8 * n || c->svo.bytes < 4 * n || c->svo_tmp.bytes < tb) {
+            (void)hipStreamSynchronize(s);
+            if (c->svo_keys.ensure(8 * n) || c->svo_keys2.ensure(8 * n) || c->svo_tmp.ensure(tb) ||
+                c->svo.zeros(4 * n, s))
+                return -ENOMEM;
+        }
+        if (c->svo_cnt.ensure(16))
+            return -ENOMEM;
+        SvoArgs sa{(const uint32_t *)in->saddr, (const uint32_t *)in->daddr, in->ports, in->meta,
+                   in->hash, n, ep_lxc, ea.ct_owner,
+                   (uint64_t *)c->svo_keys.p, (uint64_t *)c->svo_keys2.p, (uint32_t *)c->svo.p,
+                   (uint32_t *)c->svo_cnt.p, c->svo_tmp.p, c->svo_tmp.bytes};
+        if ((rc = svc_order(T, sa, std::is_same<Hdr, cfc_hdr_v6>::value, &nsvo, s))) {
+            // (words it may have set before failing: zero for the next launch)
+            (void)hipMemsetAsync(c->svo.p, 0, 4 * n, s);
+            return rc;
+        }
+        if (nsvo)
+            ea.svo = (const uint32_t *)c->svo.p;
+        c->n_svo += nsvo;
+    }
     // plain-hit summaries: only of this launch (a batch with NAT hops keeps
     // none: its apply takes the scan's)
     if (c->sum_pending)   // (the last launch's went unused)
@@ -2224,8 +2297,8 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
                 in->n ? next_timing(c, std::is_same<Hdr, cfc_hdr_v6>::value) : nullptr);
     c->sum_dirty |= sums;
     c->sum_pending = sums;
-    if (!rc && nsvo &&   // (the entry words zero again for the next launch)
-        hipMemsetAsync(c->svo.p, 0, 4 * in->n, s) != hipSuccess)
+    if (nsvo &&   // (the entry words zero again for the next launch, on every exit)
+        hipMemsetAsync(c->svo.p, 0, 4 * in->n, s) != hipSuccess && !rc)
         rc = -EIO;
     if (rc)
         return rc;
@@ -3025,7 +3098,8 @@ int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter 
 // bytes.  Chosen on the host mirror (synced before), deleted there and
 // patched into the device table (patch_ct).  Every overflowing map is
 // checked before any is touched: 0 done, 1 a map has too few candidates
-// (nothing deleted: the host path), < 0 error.
+// (nothing deleted: the host path), 2 deleted but the table could not be
+// patched (the host path; the next commit rebuilds), < 0 error.
 int ct_evict_maps(cfc_ctx *c, bool v6, const std::vector<Map *> &fmaps,
                   const std::vector<uint64_t> &want, const uint32_t *hs, uint64_t nk,
                   hipStream_t s)
@@ -3098,7 +3172,25 @@ int ct_evict_maps(cfc_ctx *c, bool v6, const std::vector<Map *> &fmaps,
             n++;
         }
     c->n_evicted += n;
-    return n ? commit_locked(c, s) : 0;
+    if (!n)
+        return 0;
+    // the deletes into the live CT table only (patch_ct), not a commit: the
+    // other groups' pending changes stay pending and the epoch — whose
+    // tables the rest of this apply reads — stays
+    if (!patch_ct(c, s)) {
+        c->built_sig[3] = ~0ull;   // (the next commit rebuilds the CT group)
+        return 2;                  // the batch to the host path
+    }
+    uint64_t sig[NGROUPS];
+    group_sigs(c, sig);
+    c->built_sig[3] = sig[3];
+    for (auto &kv : c->maps)
+        if (kv.second->ct())
+            kv.second->touched.clear();
+    E.st.ct4_entries = G.n_ct4;
+    E.st.ct6_entries = G.n_ct6;
+    c->ct_gen++;
+    return hipStreamSynchronize(s) == hipSuccess ? 0 : -EIO;
 }
 
 // Device-side growth of family v6's CT table to `want` slots (a power of
@@ -3124,12 +3216,13 @@ int ct_grow(cfc_ctx *c, bool v6, uint64_t want, hipStream_t s)
          nsum = std::make_unique<DevBuf>(), nms = std::make_unique<DevBuf>(),
          nlb = std::make_unique<DevBuf>();
     DevBuf map;
-    if (nk->zeros(ksz * want, s) || nst->ensure(sizeof(CtState) * (m4 + m6)) ||
+    // (every new line zero: the rehash writes only the moved slots', and a
+    // free slot's record must read as no entry, no dirty bits)
+    if (nk->zeros(ksz * want, s) || nst->zeros(sizeof(CtState) * (m4 + m6), s) ||
         nsum->zeros(4 * (m4 + m6), s) || nms->zeros(8 * want, s) ||
         (lb.p && nlb->zeros(16 * want, s)) || map.ensure(4 * o) ||
         c->cta_cnt.ensure(4 * CTA_NCNT))
         return -ENOMEM;
-    nst->bytes = sizeof(CtState) * (m4 + m6);
     CtState *ost = (CtState *)G.ct_st.p, *ns = (CtState *)nst->p;
     uint32_t *cnt = (uint32_t *)c->cta_cnt.p, moved = 0;
     const uint64_t other = v6 ? n4 : n6;
@@ -3140,9 +3233,13 @@ int ct_grow(cfc_ctx *c, bool v6, uint64_t want, hipStream_t s)
                   ns + (v6 ? m4 : 0), (uint4 *)nlb->p, (uint32_t)(want - 1), (uint32_t *)map.p,
                   cnt, s))
         return -EIO;
-    // the GC log's slots (IPv4: its deletes the host has not taken)
+    // the GC log's slots (its deletes the host has not taken)
     if (!v6 && c->gc_log_used &&
         ct_remap(&((CtGcRec *)c->gc_log.p)->slot, c->gc_log_used, sizeof(CtGcRec) / 4,
+                 (const uint32_t *)map.p, s))
+        return -EIO;
+    if (v6 && c->gc_log6_used &&
+        ct_remap(&((CtGcRec6 *)c->gc_log6.p)->slot, c->gc_log6_used, sizeof(CtGcRec6) / 4,
                  (const uint32_t *)map.p, s))
         return -EIO;
     // the host mirror's remap: this one, or composed with one still pending
@@ -3197,9 +3294,10 @@ int ct_grow(cfc_ctx *c, bool v6, uint64_t want, hipStream_t s)
         G.slots6 = want;
         G.ct6_mask = (uint32_t)(want - 1);
         G.ct6_probe = G.ct6_mask;
-        // (the load check's count: live, plus the inserts since the sync)
-        G.tomb6 = moved > (uint64_t)G.n_ct6 + c->cta_ins6
-                      ? (uint32_t)(moved - G.n_ct6 - c->cta_ins6) : 0u;
+        G.tomb6 = moved > G.n_ct6 ? (uint32_t)(moved - G.n_ct6) : 0u;
+        c->ct_used6 = moved;
+        c->ct_used6_valid = true;
+        c->cta_ins6 = 0;
         c->ct_min6 = std::max<uint64_t>(c->ct_min6, want);
     } else {
         G.slots4 = want;
@@ -3473,7 +3571,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
     DevBuf &logbuf = V6 ? c->cta_log6 : c->cta_log;
     const size_t log_rec = V6 ? sizeof(CtLog6) : sizeof(CtLog);
     auto used_now = [&]() -> uint64_t {
-        return V6 ? (uint64_t)G.n_ct6 + G.tomb6
+        return V6 ? (c->ct_used6_valid ? c->ct_used6 : (uint64_t)G.n_ct6 + G.tomb6)
                   : (c->ct_used_valid ? c->ct_used : (uint64_t)G.n_ct4 + G.tomb4);
     };
     uint64_t used = used_now();
@@ -3567,7 +3665,28 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             A.n_emaps = 0;
         }
     }
-    if (ok && !fits(newk) && may_grow && maps_fit()) {
+    static const bool grow_host = getenv("CFC_CT_GROW_HOST") != nullptr;
+    if (ok && !fits(newk) && may_grow && maps_fit() && grow_host) {
+        // (A/B and debugging only: the old growth — the device state synced
+        // into the maps, the CT group rebuilt larger through a commit —
+        // unless other groups wait for a commit)
+        bool others = false;
+        uint64_t sg[NGROUPS];
+        group_sigs(c, sg);
+        for (int g = 0; g < NGROUPS; g++)
+            others |= g != 3 && sg[g] != c->built_sig[g];
+        if (!others) {
+            uint64_t &mn = V6 ? c->ct_min6 : c->ct_min4;
+            mn = std::max<uint64_t>(mn, 2 * (used + ins + newk));
+            if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess)
+                return -EIO;
+            c->built_sig[3] = ~0ull;
+            if (int rc = commit_locked(c, s))
+                return rc;
+            return ct_apply_dev(c, in, out, mode, ep_lxc, s, false, false);
+        }
+    }
+    if (ok && !fits(newk) && may_grow && maps_fit() && !grow_host) {
         // the batch outgrows the table but not its maps: the table grows on
         // the device (ct_grow: at least twice the slots, room for this
         // batch at under half load) and the batch is applied again on it —
@@ -3630,6 +3749,8 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
             const int rc = ct_evict_maps(c, V6, fmaps, want, A.hs, nk, s);
             if (rc < 0)
                 return rc;
+            if (rc == 2)   // (evicted on the host, not patched in: the host path)
+                ok = false;
         }
         used = used_now();
     }
@@ -4265,6 +4386,139 @@ int ct_gc_dev(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter 
     return 0;
 }
 
+// the IPv6 part on the device (doGC6, ctmap.go:239): the CT6 table and the
+// pending CtLog6 — the same passes as ct_gc_dev (k_ct_gc<true>), a slot's
+// addresses read only for the selected maps' entries
+int ct_gc_dev6(cfc_ctx *c, const std::vector<Map *> &sel, const cfc_ct_gc_filter &f,
+               cfc_ct_gc_stats &st, hipStream_t s)
+{
+    settle(c);
+    Epoch &E = *c->epoch;
+    GCt &G = *E.ct;
+    const uint64_t slots = G.slots6;
+    std::vector<uint32_t> mw;
+    std::vector<Map *> mm;
+    for (Map *m : sel)
+        if (m->role == ROLE_CT6) {
+            mw.push_back(ct_owner_word((uint32_t)std::max(m->policy_lxc, 0), m->policy_lxc >= 0) |
+                         (m->ct_any ? 2u : 0u));
+            mm.push_back(m);
+        }
+    if (mw.empty() || !slots)
+        return 0;
+    auto v6set = [](const cfc_ip *set, uint32_t n) {
+        std::vector<uint4> v;
+        for (uint32_t i = 0; i < n; i++)
+            if (set[i].family == 6) {
+                uint4 a;
+                memcpy(&a, set[i].addr, 16);
+                v.push_back(a);
+            }
+        std::sort(v.begin(), v.end(), [](const uint4 &a, const uint4 &b) {
+            return a.x != b.x ? a.x < b.x : a.y != b.y ? a.y < b.y : a.z != b.z ? a.z < b.z
+                                                                                : a.w < b.w;
+        });
+        return v;
+    };
+    const std::vector<uint4> va = (f.flags & CFC_GC_VALID_IPS) ? v6set(f.valid_ips, f.n_valid)
+                                                                : std::vector<uint4>();
+    const std::vector<uint4> ma = (f.flags & CFC_GC_MATCH_IPS) ? v6set(f.match_ips, f.n_match)
+                                                                : std::vector<uint4>();
+    const uint64_t need = c->gc_log6_used + G.n_ct6 + 1;
+    if (c->gc_log6.bytes < sizeof(CtGcRec6) * need) {
+        DevBuf nl;
+        if (nl.ensure(sizeof(CtGcRec6) * need))
+            return -ENOMEM;
+        if (c->gc_log6_used &&
+            (hipMemcpyAsync(nl.p, c->gc_log6.p, sizeof(CtGcRec6) * c->gc_log6_used,
+                            hipMemcpyDeviceToDevice, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess))
+            return -EIO;
+        std::swap(nl.p, c->gc_log6.p);
+        std::swap(nl.bytes, c->gc_log6.bytes);
+    }
+    // sets: the maps' words (2 * CTG_MAX_MAPS u32), then the addresses (uint4)
+    const size_t set_bytes = 8 * CTG_MAX_MAPS + 16 * (va.size() + ma.size() + 1);
+    if (c->gc_sets.ensure(set_bytes) || c->gc_cnt.ensure(4 * CTG_NCNT) ||
+        (c->log6_used && c->gc_tmp.ensure(sizeof(CtLog6) * c->log6_used)))
+        return -ENOMEM;
+    uint32_t *sets = (uint32_t *)c->gc_sets.p, *cnt = (uint32_t *)c->gc_cnt.p;
+    uint64_t deleted = 0, fresh = 0, live = 0, nonfree = 0, freed = 0, last_freed = 0;
+    uint32_t logkept = (uint32_t)c->log6_used, logn = (uint32_t)c->log6_used;
+    for (size_t a = 0; a < mw.size(); a += CTG_MAX_MAPS) {
+        const uint32_t nm = (uint32_t)std::min<size_t>(CTG_MAX_MAPS, mw.size() - a);
+        std::vector<uint32_t> hs(CTG_MAX_MAPS * 2, 0);
+        std::copy(mw.begin() + (long)a, mw.begin() + (long)a + nm, hs.begin());
+        std::vector<uint4> addrs(va);
+        addrs.insert(addrs.end(), ma.begin(), ma.end());
+        CtGcArgs A{};
+        A.ct6 = (Ct6Slot *)G.ct6.p;
+        A.st = (CtState *)G.ct_st.p + G.slots4;
+        A.slots = slots;
+        A.mask = (uint32_t)(slots - 1);
+        A.maps = sets;
+        A.n_maps = nm;
+        A.mcnt = sets + CTG_MAX_MAPS;
+        A.flags = ((f.flags & CFC_GC_REMOVE_EXPIRED) ? CTG_REMOVE_EXPIRED : 0u) |
+                  ((f.flags & CFC_GC_VALID_IPS) ? CTG_VALID : 0u) |
+                  ((f.flags & CFC_GC_MATCH_IPS) ? CTG_MATCH : 0u);
+        A.time = f.time;
+        A.valid6 = (const uint4 *)(sets + 2 * CTG_MAX_MAPS);
+        A.n_valid = (uint32_t)va.size();
+        A.match6 = A.valid6 + va.size();
+        A.n_match = (uint32_t)ma.size();
+        A.log6 = (CtGcRec6 *)c->gc_log6.p + c->gc_log6_used + deleted;
+        A.log_cap = (uint32_t)(c->gc_log6.bytes / sizeof(CtGcRec6) - c->gc_log6_used - deleted);
+        A.cnt = cnt;
+        uint32_t hc[CTG_NCNT], hm[CTG_MAX_MAPS];
+        if (hipMemcpyAsync(sets, hs.data(), 4 * hs.size(), hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            (!addrs.empty() &&
+             hipMemcpyAsync(sets + 2 * CTG_MAX_MAPS, addrs.data(), 16 * addrs.size(),
+                            hipMemcpyHostToDevice, s) != hipSuccess) ||
+            hipMemsetAsync(cnt, 0, 4 * CTG_NCNT, s) != hipSuccess || ct_gc4(A, s))
+            return -EIO;
+        if (logn && (ct_gc_log6(A, (const CtLog6 *)c->cta_log6.p, logn, (CtLog6 *)c->gc_tmp.p, s) ||
+                     hipMemcpyAsync(c->cta_log6.p, c->gc_tmp.p, sizeof(CtLog6) * logn,
+                                    hipMemcpyDeviceToDevice, s) != hipSuccess))
+            return -EIO;
+        if (hipMemcpyAsync(hc, cnt, 4 * CTG_NCNT, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(hm, A.mcnt, 4 * nm, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return -EIO;
+        if (hc[CTG_DELETED] > A.log_cap)
+            return -EIO;
+        for (uint32_t j = 0; j < nm; j++)
+            mm[a + j]->gc_pending += hm[j];
+        deleted += hc[CTG_DELETED];
+        fresh += hc[CTG_FRESH];
+        live += hc[CTG_LIVE];
+        nonfree = hc[CTG_NONFREE];
+        freed += hc[CTG_FREED];
+        last_freed = hc[CTG_FREED];
+        if (logn) {
+            logkept = hc[CTG_LOGKEPT];
+            logn = logkept;
+        }
+    }
+    c->gc_log6_used += deleted;
+    c->cta_claims6 -= std::min(c->cta_claims6, fresh);
+    c->ct_used6 = nonfree >= last_freed ? nonfree - last_freed : 0;
+    c->cta_ins6 = 0;
+    c->ct_used6_valid = true;
+    if (deleted || fresh) {
+        c->ct_dirty = true;
+        c->ct6_dirty = true;
+    }
+    c->ct_gen++;
+    st.device_deleted += deleted + fresh;
+    st.log_deleted += c->log6_used - logkept;
+    st.alive += live + logkept;
+    st.slots_freed += freed;
+    c->log6_used = logkept;
+    return 0;
+}
+
 int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, hipStream_t s)
 {
     if (f->flags & ~(CFC_GC_REMOVE_EXPIRED | CFC_GC_VALID_IPS | CFC_GC_MATCH_IPS))
@@ -4291,25 +4545,27 @@ int ct_gc(cfc_ctx *c, int fd, const cfc_ct_gc_filter *f, cfc_ct_gc_stats *out, h
     order_after_launches(c, s);
     cfc_ct_gc_stats st{};
     Epoch &E = *c->epoch;
-    const bool dev4 = E.ct->slots4 && E.ct->ct_st.p;
-    // IPv6 maps are collected on the host, after their device applies are
-    // synchronised — before the device pass, whose pending-log entries the
-    // sync would otherwise replay into the host maps after the pass counted
-    // them (and the host loop below count them again)
-    bool v6sel = false;
+    const bool dev4 = E.ct->slots4 && E.ct->ct_st.p, dev6 = E.ct->slots6 && E.ct->ct_st.p;
+    // both families on the device (doGC4 / doGC6); an IPv6 map without a
+    // device table is collected on the host after its device applies are
+    // synchronised (their pending-log entries first)
+    bool v6host = false;
     for (Map *m : sel)
-        v6sel |= m->role == ROLE_CT6 && !m->kv.empty();
-    if (v6sel && c->ct6_dirty)
+        v6host |= m->role == ROLE_CT6 && !m->kv.empty() && !dev6;
+    if (v6host && c->ct6_dirty)
         if (int rc = ct_sync(c, s))
             return rc;
     if (dev4)
         if (int rc = ct_gc_dev(c, sel, *f, st, s, nullptr))
             return rc;
-    // what only the host holds: IPv6 maps, IPv4 maps without a device
-    // table, IPv4 TCP maps' ICMP entries
+    if (dev6)
+        if (int rc = ct_gc_dev6(c, sel, *f, st, s))
+            return rc;
+    // what only the host holds: maps without a device table, the TCP maps'
+    // ICMP entries (no lookup reaches them: not in the device table)
     const GcFilterHost H{*f};
     for (Map *m : sel) {
-        const bool v6 = m->role == ROLE_CT6, all = v6 || !dev4;
+        const bool v6 = m->role == ROLE_CT6, all = v6 ? !dev6 : !dev4;
         if (!all && !m->n_aux)
             continue;
         uint64_t kept = 0, gone = 0;

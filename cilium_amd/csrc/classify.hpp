@@ -419,6 +419,7 @@ int cta_tomb(Ct4Slot *ct4, const CtSyncRec *rec, uint32_t n, hipStream_t s);
 // added into *cnt (the exact load: the GC's trim frees tombstones the host
 // mirror still counts)
 int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStream_t s);
+int ct_count_nonfree6(const Ct6Slot *ct6, uint64_t slots, uint32_t *cnt, hipStream_t s);
 int cta_tomb6(Ct6Slot *ct6, const CtSyncRec6 *rec, uint32_t n, hipStream_t s);
 // device-side growth (ct_grow): every key-holding slot of the old table
 // (ok: Ct4Slot / Ct6Slot, oslots) into the new one (nk, nmask + 1 slots,
@@ -450,9 +451,15 @@ constexpr uint32_t CTG_REMOVE_EXPIRED = 1, CTG_VALID = 2, CTG_MATCH = 4;
 struct CtGcRec {
     uint32_t slot, x, y, z, w;
 };
+struct CtGcRec6 {
+    uint32_t slot;
+    uint4 d, s;
+    uint32_t z, w;
+};
 struct CtGcArgs {
-    Ct4Slot *ct4;
-    CtState *st;                  // the IPv4 slots' lines
+    Ct4Slot *ct4;                 // the IPv4 table, or
+    Ct6Slot *ct6;                 // the IPv6 one (doGC6)
+    CtState *st;                  // the family's slots' lines
     uint64_t slots;
     uint32_t mask;
     // the CT maps selected (owner word | kind << 1: 0 TCP map, 1 ANY map);
@@ -462,8 +469,10 @@ struct CtGcArgs {
     uint32_t *mcnt;
     uint32_t flags, time;
     const uint32_t *valid, *match; // sorted raw be32 addresses
+    const uint4 *valid6, *match6;  // (IPv6) sorted raw addresses
     uint32_t n_valid, n_match;
     CtGcRec *log;
+    CtGcRec6 *log6;               // (IPv6)
     uint32_t log_cap;
     uint32_t *cnt;                // CTG_* counters
     const uint32_t *protect;      // slots never deleted (one bit each), or null
@@ -477,6 +486,7 @@ int ct_protect_hits(const uint32_t *hs, uint64_t nk, uint32_t *bm, hipStream_t s
 // same way, kept in order of appearance: in[0, n) -> out; the kept count
 // into A.cnt[CTG_LOGKEPT]
 int ct_gc_log(const CtGcArgs &A, const CtLog *in, uint32_t n, CtLog *out, hipStream_t s);
+int ct_gc_log6(const CtGcArgs &A, const CtLog6 *in, uint32_t n, CtLog6 *out, hipStream_t s);
 
 // ---- service load balancing of an egress batch (lb.hip)
 struct LbArgs {

@@ -7,7 +7,8 @@
 //   * the ipcache is a 1M-prefix IPv6 LPM (layout.h Lpm6): lengths are
 //     probed longest first, each group of lengths screened by one 8-byte
 //     Bloom word (L2-resident), so a lookup is usually one Bloom load plus
-//     one 32-byte slot (Infinity Cache);
+//     one slot (Infinity Cache): 16 bytes, one load, for the /32-/64 mass,
+//     32 bytes, two loads, beyond /64;
 //   * endpoints are 32-byte slots keyed by the full address, copied to LDS
 //     when the table is small;
 //   * the prefilter's exact /128 set and its LPM deny list are Lpm6 tables.
@@ -111,6 +112,16 @@ __device__ __forceinline__ uint32_t lpm6_lookup(const Lpm6 &P, uint32_t loff, ui
         const uint64_t b = l6_bloom_bits(h);
         if ((bw & b) != b)
             continue;
+        if (len <= 64) {   // (uniform) one 16-byte load per probe: {w0, w1, label, len}
+            for (uint32_t s = h & P.mask64;; s = (s + 1) & P.mask64) {
+                const uint4 k = ld16(P.slots64 + s);
+                if (k.w == len && k.x == m0 && k.y == m1)
+                    return k.z;
+                if (!k.w)
+                    break;
+            }
+            continue;
+        }
         for (uint32_t s = h & P.mask;; s = (s + 1) & P.mask) {
             const uint4 k = ld16(&P.slots[s].w[0]);
             const uint4 v = ld16(&P.slots[s].label);   // {label, len, 0, 0}
@@ -169,10 +180,11 @@ __device__ __forceinline__ bool ct6_new_dport(uint32_t proto, uint32_t ports,
 // length lists of the three Lpm6 tables (ipcache, prefilter fix, dyn): a
 // lookup reads its next length from LDS, not by a dependent global load
 struct LdsPlan6 {
-    uint32_t lxc_slots, pol_words, nlens;
+    uint32_t lxc_slots, pol_words, pf_words, nlens;
     __host__ __device__ size_t bytes() const
     {
-        return 8ull * LDS_MET6_U64 + 32ull * lxc_slots + 4ull * pol_words + 4ull * nlens;
+        return 8ull * LDS_MET6_U64 + 32ull * lxc_slots + 4ull * pol_words + 4ull * pf_words +
+               4ull * nlens;
     }
 };
 
@@ -181,7 +193,10 @@ __host__ LdsPlan6 lds_plan6(const DevTables &T)
     LdsPlan6 p;
     p.lxc_slots = (T.lxc6 && T.lxc6_lds) ? T.lxc6_mask + 1 : 0;
     p.pol_words = T.pol_bloom ? T.pol_bloom_words : 0;
+    p.pf_words = T.pf6_bloom ? T.pf6_bloom_words : 0;
     p.nlens = T.ipc6.nlen + T.pf6_fix.nlen + T.pf6_dyn.nlen;
+    if (p.bytes() > LDS_PER_WG)   // (the prefilter's filter is an optimisation: drop it first)
+        p.pf_words = 0;
     return p;
 }
 
@@ -255,14 +270,18 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
 {
     constexpr bool XDP = MODE == CFC_MODE_XDP || MODE == CFC_MODE_FULL;
     constexpr bool EGR = MODE == CFC_MODE_EGRESS;
-    // LDS image (uint4 units): metrics | endpoint slots | pol Bloom
+    // LDS image (uint4 units): metrics | endpoint slots | pol Bloom |
+    // prefilter Bloom | the length lists
     unsigned long long *s_met = lds_met();
     const uint32_t lxc_off = LDS_MET6_U64 / 2;
     const uint32_t pol4 = lxc_off + 2 * L.lxc_slots;
     const bool lxc_lds = L.lxc_slots != 0;
     Lds S;
+    const uint32_t pf4 = pol4 + L.pol_words / 4;
     S.lxc = false;
-    S.pfb = false;
+    S.pfb = L.pf_words != 0;
+    S.pfb_off = 4 * pf4;
+    S.pfb_mask = L.pf_words - 1;
     S.polb = L.pol_words != 0;
     S.polb_off = 4 * pol4;
     S.polb_mask = L.pol_words - 1;
@@ -274,8 +293,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
              2 * L.lxc_slots);
     lds_copy(cfc_smem + pol4, reinterpret_cast<const uint4 *>(T.pol_bloom),
              L.pol_words / 4);
+    lds_copy(cfc_smem + pf4, reinterpret_cast<const uint4 *>(T.pf6_bloom), L.pf_words / 4);
     // the length lists (dword offsets)
-    const uint32_t lo_ipc = 4 * pol4 + L.pol_words;
+    const uint32_t lo_ipc = 4 * pf4 + L.pf_words;
     const uint32_t lo_fix = lo_ipc + T.ipc6.nlen, lo_dyn = lo_fix + T.pf6_fix.nlen;
     {
         uint32_t *lw = reinterpret_cast<uint32_t *>(cfc_smem);
@@ -321,7 +341,10 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         // the Bloom words of the prefilter's and the ipcache's lookups of
         // this header's address, loaded together (egress with a load
         // balancer looks up the address after its service step instead)
-        const uint64_t bwf = XDP ? lpm6_bloom0(T.pf6_fix, lo_fix, sa) : 0ull;
+        // (the prefilter's exact set: its LDS filter first, when it has one)
+        const bool pf_maybe = XDP && (!S.pfb || bloom_maybe(S.pfb_off, S.pfb_mask,
+                                                            pf6_bloom_hash(sa.x, sa.y, sa.z, sa.w)));
+        const uint64_t bwf = (XDP && !S.pfb) ? lpm6_bloom0(T.pf6_fix, lo_fix, sa) : 0ull;
         const uint64_t bwi = MODE == CFC_MODE_XDP ? 0ull
                            : !EGR ? lpm6_bloom0(T.ipc6, lo_ipc, sa)
                            : !LB  ? lpm6_bloom0(T.ipc6, lo_ipc, da) : 0ull;
@@ -333,8 +356,9 @@ __global__ __launch_bounds__(BLOCK, WAVES_PER_SIMD) void k_classify_v6(
         bool done = false;
         if (XDP) {
             bool deny = lpm6_lookup(T.pf6_dyn, lo_dyn, sa) != 0;
-            if (!deny)
-                deny = lpm6_lookup(T.pf6_fix, lo_fix, sa, bwf) != 0;
+            if (!deny && pf_maybe)
+                deny = (S.pfb ? lpm6_lookup(T.pf6_fix, lo_fix, sa)
+                              : lpm6_lookup(T.pf6_fix, lo_fix, sa, bwf)) != 0;
             const bool drop = deny || !local;
             if (MODE == CFC_MODE_XDP || drop) {
                 act = drop ? XDP_DROP : XDP_PASS;

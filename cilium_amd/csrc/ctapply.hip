@@ -1945,8 +1945,9 @@ __global__ __launch_bounds__(256) void k_cta_tomb6(Ct6Slot *ct6, const CtSyncRec
     }
 }
 // slots whose word is not 0, four per thread and step
-__global__ __launch_bounds__(256) void k_ct_nonfree4(const Ct4Slot *ct4, uint64_t slots,
-                                                     uint32_t *cnt)
+template <class Slot>
+__global__ __launch_bounds__(256) void k_ct_nonfree(const Slot *ct4, uint64_t slots,
+                                                    uint32_t *cnt)
 {
     uint32_t c = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
@@ -2092,6 +2093,24 @@ __device__ __forceinline__ bool gc_in_set(const uint32_t *set, uint32_t n, uint3
     }
     return lo < n && set[lo] == a;
 }
+// IPv6 addresses: raw words, sorted lexicographically (x, y, z, w) by the
+// host (ct_gc_dev)
+__device__ __forceinline__ bool a6_lt(uint4 a, uint4 b)
+{
+    return a.x != b.x ? a.x < b.x : a.y != b.y ? a.y < b.y : a.z != b.z ? a.z < b.z : a.w < b.w;
+}
+__device__ __forceinline__ bool gc_in_set(const uint4 *set, uint32_t n, uint4 a)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a6_lt(set[mid], a))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo < n && aeq(set[lo], a);
+}
 // doFiltering on the entry's two addresses and lifetime
 __device__ __forceinline__ bool gc_delete(const CtGcArgs &A, uint32_t x, uint32_t y,
                                           uint32_t lifetime)
@@ -2103,6 +2122,16 @@ __device__ __forceinline__ bool gc_delete(const CtGcArgs &A, uint32_t x, uint32_
         return true;
     return (A.flags & CTG_MATCH) &&
            (gc_in_set(A.match, A.n_match, x) || gc_in_set(A.match, A.n_match, y));
+}
+__device__ __forceinline__ bool gc_delete(const CtGcArgs &A, uint4 x, uint4 y, uint32_t lifetime)
+{
+    if ((A.flags & CTG_REMOVE_EXPIRED) && lifetime < A.time)
+        return true;
+    if ((A.flags & CTG_VALID) && !gc_in_set(A.valid6, A.n_valid, x) &&
+        !gc_in_set(A.valid6, A.n_valid, y))
+        return true;
+    return (A.flags & CTG_MATCH) &&
+           (gc_in_set(A.match6, A.n_match, x) || gc_in_set(A.match6, A.n_match, y));
 }
 // the selected map an entry belongs to (its CT map: owner word, TCP or ANY
 // kind), or -1
@@ -2124,7 +2153,11 @@ __device__ __forceinline__ int gc_map(const uint32_t *smaps, uint32_t n, uint32_
 constexpr int GC_U = 8;
 // (1024-thread blocks, one per CU: one list atomic per 8192 slots)
 constexpr int GC_B = 1024;
-__global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
+// V6: the IPv6 table (doGC6, ctmap.go:239, next to doGC4 :272): a slot's
+// {z, w} words first (its map and state), its addresses only for an entry
+// of a selected map
+template <bool V6>
+__global__ __launch_bounds__(GC_B) void k_ct_gc(CtGcArgs A)
 {
     __shared__ uint32_t smaps[CTG_MAX_MAPS], scnt[CTG_MAX_MAPS];
     __shared__ uint32_t sw[GC_B * GC_U];   // (a step's w words after its deletes)
@@ -2138,18 +2171,27 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
     // (every thread runs the same number of steps: block_count_n needs the
     // whole block)
     for (uint64_t base = (uint64_t)blockIdx.x * GC_B * GC_U; base < A.slots; base += stride) {
+        // k: IPv4 the key {daddr, saddr, ports, w}; IPv6 {z, w, 0, 0}, then
+        // the addresses (kd, ks) of the selected maps' entries
         uint4 k[GC_U];
         int j[GC_U];
         uint32_t life[GC_U], infy[GC_U];
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {   // (no branches: the loads issue together)
             const uint64_t s = base + u * GC_B + threadIdx.x;
-            k[u] = ld16(A.ct4 + (s < A.slots ? s : A.slots - 1));
+            const uint64_t sc = s < A.slots ? s : A.slots - 1;
+            if constexpr (V6) {
+                const uint4 t = ld16(&A.ct6[sc].z);
+                k[u] = make_uint4(0, 0, t.x, t.y);   // (z, w where the v4 key has them)
+            } else {
+                k[u] = ld16(A.ct4 + sc);
+            }
         }
 #pragma unroll
         for (int u = 0; u < GC_U; u++)
             if (base + u * GC_B + threadIdx.x >= A.slots)
                 k[u] = make_uint4(0, 0, 0, 0);
+
         // a tombstone, a claim, or an apply's delete the host has not taken
         // is no entry of a map
 #pragma unroll
@@ -2166,11 +2208,24 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
             life[u] = j[u] >= 0 ? A.st[s].tm.lifetime : 0u;
         }
         bool del[GC_U], logit[GC_U];
+        uint4 kd[GC_U], ks[GC_U];
+        if constexpr (V6) {
+#pragma unroll
+            for (int u = 0; u < GC_U; u++) {
+                const uint64_t s = base + u * GC_B + threadIdx.x;
+                kd[u] = j[u] >= 0 ? ld16(A.ct6[s].d) : make_uint4(0, 0, 0, 0);
+                ks[u] = j[u] >= 0 ? ld16(A.ct6[s].s) : make_uint4(0, 0, 0, 0);
+            }
+        }
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {
             const uint64_t s = base + u * GC_B + threadIdx.x;
-            del[u] = j[u] >= 0 && gc_delete(A, k[u].x, k[u].y, life[u]) &&
-                     !(A.protect && ((A.protect[s >> 5] >> (s & 31)) & 1u));
+            bool d;
+            if constexpr (V6)
+                d = gc_delete(A, kd[u], ks[u], life[u]);
+            else
+                d = gc_delete(A, k[u].x, k[u].y, life[u]);
+            del[u] = j[u] >= 0 && d && !(A.protect && ((A.protect[s >> 5] >> (s & 31)) & 1u));
             infy[u] = del[u] ? A.st[s].info.y : 0u;
         }
         uint32_t nl = 0;
@@ -2190,12 +2245,23 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
                 continue;
             const uint64_t s = base + u * GC_B + threadIdx.x;
             if (logit[u]) {
-                if (r < A.log_cap)
-                    A.log[r] = CtGcRec{(uint32_t)s, k[u].x, k[u].y, k[u].z, k[u].w};
+                if (r < A.log_cap) {
+                    if constexpr (V6)
+                        A.log6[r] = CtGcRec6{(uint32_t)s, kd[u], ks[u], k[u].z, k[u].w};
+                    else
+                        A.log[r] = CtGcRec{(uint32_t)s, k[u].x, k[u].y, k[u].z, k[u].w};
+                }
                 r++;
                 atomicAdd(&scnt[j[u]], 1u);
             }
-            *reinterpret_cast<uint4 *>(A.ct4 + s) = make_uint4(0, 0, 0, CT_TOMBSTONE);
+            if constexpr (V6) {
+                const uint4 z = make_uint4(0, 0, 0, 0);
+                *reinterpret_cast<uint4 *>(A.ct6[s].d) = z;
+                *reinterpret_cast<uint4 *>(A.ct6[s].s) = z;
+                *reinterpret_cast<uint4 *>(&A.ct6[s].z) = make_uint4(0, CT_TOMBSTONE, 0, 0);
+            } else {
+                *reinterpret_cast<uint4 *>(A.ct4 + s) = make_uint4(0, 0, 0, CT_TOMBSTONE);
+            }
             // (the line's counters and record; its report state is dead)
             ulonglong2 *a = reinterpret_cast<ulonglong2 *>(A.st[s].acct);
             a[0] = a[1] = make_ulonglong2(0, 0);
@@ -2214,9 +2280,10 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
 #pragma unroll
         for (int u = 0; u < GC_U; u++)
             sw[u * GC_B + threadIdx.x] = del[u] ? CT_TOMBSTONE : k[u].w;
+        const uint32_t *pnext = V6 ? &A.ct6[(base + lim) & A.mask].w : &A.ct4[(base + lim) & A.mask].w;
         const uint32_t wnext = whole ? 1u
-                                     : __hip_atomic_load(&A.ct4[(base + lim) & A.mask].w,
-                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                     : __hip_atomic_load(pnext, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < GC_U; u++) {
@@ -2238,7 +2305,10 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
                 }
             }
             if (after == 0) {
-                A.ct4[base + c].w = 0u;
+                if constexpr (V6)
+                    A.ct6[base + c].w = 0u;
+                else
+                    A.ct4[base + c].w = 0u;
                 freed++;
             }
         }
@@ -2256,15 +2326,16 @@ __global__ __launch_bounds__(GC_B) void k_ct_gc4(CtGcArgs A)
 // the pending TCP-map ICMP entries (CtLog): lifetime as ct_create4 wrote it
 // (now + CT_LIFETIME_NONTCP, conntrack.h:741-760; no lookup ever updates
 // one), the TCP map of its owner
-__global__ __launch_bounds__(256) void k_ct_gc_log(CtGcArgs A, const CtLog *in, uint32_t n,
-                                                   CtLog *out)
+template <class Log>
+__global__ __launch_bounds__(256) void k_ct_gc_log(CtGcArgs A, const Log *in, uint32_t n,
+                                                   Log *out)
 {
     __shared__ uint32_t smaps[CTG_MAX_MAPS];
     for (uint32_t j = threadIdx.x; j < A.n_maps; j += 256)
         smaps[j] = A.maps[j];
     __syncthreads();
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    CtLog g{};
+    Log g{};
     bool keep = false;
     if (i < n) {
         g = in[i];
@@ -2749,11 +2820,12 @@ int ct_gc4(const CtGcArgs &A, hipStream_t s)
 {
     if (!A.slots || A.n_maps > CTG_MAX_MAPS)
         return -EINVAL;
-    hipLaunchKernelGGL(k_ct_gc4, dim3((unsigned)std::max<uint64_t>(
-                                     1, std::min<uint64_t>((A.slots + GC_B * GC_U - 1) /
-                                                               (GC_B * GC_U),
-                                                           256))),
-                       dim3(GC_B), 0, s, A);
+    const dim3 g((unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>((A.slots + GC_B * GC_U - 1) / (GC_B * GC_U), 256)));
+    if (A.ct6)
+        hipLaunchKernelGGL(k_ct_gc<true>, g, dim3(GC_B), 0, s, A);
+    else
+        hipLaunchKernelGGL(k_ct_gc<false>, g, dim3(GC_B), 0, s, A);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
@@ -2762,14 +2834,33 @@ int ct_gc_log(const CtGcArgs &A, const CtLog *in, uint32_t n, CtLog *out, hipStr
     if (A.n_maps > CTG_MAX_MAPS)
         return -EINVAL;
     if (n)
-        hipLaunchKernelGGL(k_ct_gc_log, dim3((n + 255) / 256), dim3(256), 0, s, A, in, n, out);
+        hipLaunchKernelGGL(k_ct_gc_log<CtLog>, dim3((n + 255) / 256), dim3(256), 0, s, A, in, n,
+                           out);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_gc_log6(const CtGcArgs &A, const CtLog6 *in, uint32_t n, CtLog6 *out, hipStream_t s)
+{
+    if (A.n_maps > CTG_MAX_MAPS)
+        return -EINVAL;
+    if (n)
+        hipLaunchKernelGGL(k_ct_gc_log<CtLog6>, dim3((n + 255) / 256), dim3(256), 0, s, A, in, n,
+                           out);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int ct_count_nonfree6(const Ct6Slot *ct6, uint64_t slots, uint32_t *cnt, hipStream_t s)
+{
+    if (slots)
+        hipLaunchKernelGGL(k_ct_nonfree<Ct6Slot>, dim3(blocks_for(slots, 2048)), dim3(256), 0, s,
+                           ct6, slots, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
 int ct_count_nonfree4(const Ct4Slot *ct4, uint64_t slots, uint32_t *cnt, hipStream_t s)
 {
     if (slots)
-        hipLaunchKernelGGL(k_ct_nonfree4, dim3(blocks_for(slots, 2048)), dim3(256), 0, s, ct4,
+        hipLaunchKernelGGL(k_ct_nonfree<Ct4Slot>, dim3(blocks_for(slots, 2048)), dim3(256), 0, s, ct4,
                            slots, cnt);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }

@@ -1179,10 +1179,29 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         // tags they take (a create's, its related entry's, an ICMP error's),
         // and the participants' list sized by the last batch; mark, probe and
         // collect back to back, one wait for all their counts
+        // the work list first: room for every header
+        if (B.wl.ensure(4 * 64 * O.W.words))
+            return -ENOMEM;
+        O.wl = (uint32_t *)B.wl.p;
+        hipLaunchKernelGGL(k_ord_list_w, dim3((unsigned)((O.W.words + LISTW - 1) / LISTW)),
+                           dim3(256), 0, s, O);
+        // a context's first apply has no last batch to size its sets by: its
+        // own work count (at least its creates) sizes them — one host wait,
+        // on that apply only (sized from nothing, its sets overflowed and
+        // the mark ran twice: 4.3 ms where a steady one takes 0.14)
+        uint32_t hint = B.creates_hint;
+        if (!hint) {
+            uint32_t nwl = 0;
+            if (hipMemcpyAsync(&nwl, O.cnt + ORD_NWL, 4, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return -EIO;
+            hint = nwl;
+        }
         uint32_t words = 1u << 16, fwords = 1u << 12;
-        while (words < 4ull * B.creates_hint + 4096 && words < (1u << 28))
+        while (words < 4ull * hint + 4096 && words < (1u << 28))
             words *= 2;
-        while (fwords < B.creates_hint / 2 && fwords < (1u << 26))
+        while (fwords < hint / 2 && fwords < (1u << 26))
             fwords *= 2;
         const uint64_t cap0 = std::max<uint64_t>(B.part.bytes / 4, 2ull * B.part_hint + 65536);
         if (B.fpset.ensure(8ull * words + 4ull * fwords) ||
@@ -1195,12 +1214,6 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         O.pf_mask = fwords - 1;
         O.part = (uint32_t *)B.part.p;
         O.part_cap = (uint32_t)std::min<uint64_t>(B.part.bytes / 4, 0x3FFFFFFFull);
-        // the work list: room for every header
-        if (B.wl.ensure(4 * 64 * O.W.words))
-            return -ENOMEM;
-        O.wl = (uint32_t *)B.wl.p;
-        hipLaunchKernelGGL(k_ord_list_w, dim3((unsigned)((O.W.words + LISTW - 1) / LISTW)),
-                           dim3(256), 0, s, O);
         mark();
         ORD_LAUNCH(k_ord_rel_w, 1024, A, O);
         ORD_LAUNCH(k_ord_probe_v, gp, A, O);

@@ -248,12 +248,25 @@ void build_lpm6(const std::vector<Pfx6> &pfx, Lpm6Host *out)
     }
     out->bloom.assign(pow2_at_least(std::max<size_t>(64, nkeys / 4)), 0);
     const uint32_t bmask = (uint32_t)out->bloom.size() - 1;
-    const uint32_t ns = pow2_at_least(std::max<size_t>(16, 2 * nkeys));
-    out->slots.assign(ns, L6Slot{});
+    size_t n64 = 0;
+    for (uint32_t len : L)
+        n64 += len <= 64 ? by_len[len].size() : 0;
+    if (nkeys > n64)
+        out->slots.assign(pow2_at_least(std::max<size_t>(16, 2 * (nkeys - n64))), L6Slot{});
+    if (n64)
+        out->slots64.assign(pow2_at_least(std::max<size_t>(16, 2 * n64)), make_uint4(0, 0, 0, 0));
+    const uint32_t ns = (uint32_t)out->slots.size(), ns64 = (uint32_t)out->slots64.size();
     for (uint32_t len : L)
         for (const Pfx6 *p : by_len[len]) {
             const uint32_t h = l6_hash(p->w[0], p->w[1], p->w[2], p->w[3], len);
             out->bloom[l6_group_hash(p->w, sel_of[len]) & bmask] |= l6_bloom_bits(h);
+            if (len <= 64) {
+                uint32_t s = h & (ns64 - 1);
+                while (out->slots64[s].w)
+                    s = (s + 1) & (ns64 - 1);
+                out->slots64[s] = make_uint4(p->w[0], p->w[1], p->label, len);
+                continue;
+            }
             uint32_t s = h & (ns - 1);
             while (out->slots[s].len)
                 s = (s + 1) & (ns - 1);
@@ -280,6 +293,17 @@ uint32_t lpm6_lookup_host(const Lpm6Host &t, const uint32_t w[4])
         const uint64_t b = l6_bloom_bits(h);
         if ((bw & b) != b)
             continue;
+        if (len <= 64) {
+            const uint32_t mask64 = (uint32_t)t.slots64.size() - 1;
+            for (uint32_t s = h & mask64;; s = (s + 1) & mask64) {
+                const uint4 &d = t.slots64[s];
+                if (!d.w)
+                    break;
+                if (d.w == len && d.x == m[0] && d.y == m[1])
+                    return d.z;
+            }
+            continue;
+        }
         for (uint32_t s = h & mask;; s = (s + 1) & mask) {
             const L6Slot &d = t.slots[s];
             if (!d.len)
@@ -380,6 +404,20 @@ bool ipcache_v6_entry(const std::string &nk, const std::string &val, Pfx6 *p)
 
 int64_t lpm6_find_slot(const Lpm6Host &t, const Pfx6 &p)
 {
+    if (p.plen && p.plen <= 64) {
+        if (t.slots64.empty())
+            return -1;
+        const uint32_t mask = (uint32_t)t.slots64.size() - 1;
+        uint32_t s = l6_hash(p.w[0], p.w[1], p.w[2], p.w[3], p.plen) & mask;
+        for (uint32_t n = 0; n <= mask; n++, s = (s + 1) & mask) {
+            const uint4 &d = t.slots64[s];
+            if (!d.w)
+                return -1;
+            if (d.w == p.plen && d.x == p.w[0] && d.y == p.w[1])
+                return L6_S64 | s;
+        }
+        return -1;
+    }
     if (t.slots.empty() || !p.plen)
         return -1;
     const uint32_t mask = (uint32_t)t.slots.size() - 1;
@@ -807,6 +845,16 @@ void build_image(const std::vector<Map *> &maps, const BuildOpts &opt,
         std::vector<Pfx6> pfx;
         prefilter_v6(pf6fix, true, &pfx);
         build_lpm6(pfx, &img->pf6_fix);
+        // (check_v6 looks up {prefixlen 128, saddr} exactly: a filter over
+        // the addresses screens it, as pf_bloom does for IPv4)
+        bool all128 = !pfx.empty();
+        for (const Pfx6 &p : pfx)
+            all128 &= p.plen == 128;
+        if (all128) {
+            bloom_size(&img->pf6_bloom, 2 * pfx.size(), PF_BLOOM_MAX_WORDS);
+            for (const Pfx6 &p : pfx)
+                bloom_add(&img->pf6_bloom, pf6_bloom_hash(p.w[0], p.w[1], p.w[2], p.w[3]));
+        }
     }
     if (pf6dyn && pf6dyn->ksz == 20) {
         std::vector<Pfx6> pfx;

@@ -30,7 +30,8 @@ struct Pfx6 {
     uint32_t label;
 };
 struct Lpm6Host {
-    std::vector<L6Slot> slots;
+    std::vector<L6Slot> slots;     // prefixes longer than /64
+    std::vector<uint4> slots64;    // /1-/64: {w0, w1, label, len}
     std::vector<uint64_t> bloom;
     std::vector<uint32_t> lens;
     uint32_t def_label = 0;
@@ -38,9 +39,12 @@ struct Lpm6Host {
     uint32_t groups = 0;   // Bloom groups
     uint64_t bytes() const
     {
-        return sizeof(L6Slot) * slots.size() + 8ull * bloom.size() + 4ull * lens.size();
+        return sizeof(L6Slot) * slots.size() + 16ull * slots64.size() + 8ull * bloom.size() +
+               4ull * lens.size();
     }
 };
+// lpm6_find_slot's answer for a prefix in slots64: L6_S64 | its slot
+constexpr int64_t L6_S64 = (int64_t)1 << 40;
 void build_lpm6(const std::vector<Pfx6> &pfx, Lpm6Host *out);
 // one ipcache entry (normalised key, value) as an IPv6 prefix; false when it
 // is not one the IPv6 table holds on its own (prefix within the static part)
@@ -67,6 +71,7 @@ struct HostImage {
     std::vector<uint32_t> pf_fix;
     uint32_t pf_fix_mask = 0, pf_fix_zero = 0, n_pf_fix = 0;
     std::vector<uint32_t> pf_bloom;                 // words (pow2) or empty
+    std::vector<uint32_t> pf6_bloom;                // over pf6_fix (all /128), or empty
     // endpoints
     std::vector<LxcSlot> lxc4;
     uint32_t lxc4_mask = 0, n_eps = 0;

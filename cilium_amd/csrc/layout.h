@@ -189,7 +189,9 @@ constexpr uint32_t LXC_LDS_MAX_SLOTS = 512;       // 8 KiB of endpoint slots
 // of keys), so the layout minimises Infinity-Cache accesses: the slots are
 // touched about once per lookup and everything before that is L2-resident.
 //   slots   32 bytes: masked address as host-order words (w[0] = bits 0-31),
-//           label, length (0 = free slot); linear probing, load <= 50%
+//           label, length (0 = free slot); linear probing, load <= 50%;
+//           prefixes of at most /64 in slots64 (16 bytes: w[0], w[1], label,
+//           length), probed with the same hash
 //   lens    the lengths present (> 0), longest first:
 //           len | sel << 8 | L6_GROUP_FIRST; consecutive lengths form a
 //           group sharing one Bloom word, chosen by the address masked to
@@ -208,11 +210,17 @@ struct alignas(16) L6Slot {
     uint32_t len;
     uint32_t pad[2];
 };
+// Prefixes of at most 64 bits (the /32-/64 mass of an ipcache) sit in a
+// table of their own with 16-byte slots {w0, w1, label, len} (len 0: free;
+// their masked address has w2 = w3 = 0): a probe is one load.  Longer ones
+// keep the 32-byte slots (two loads: key, then {label, len}).
 struct Lpm6 {
-    const L6Slot *slots;           // null: empty
+    const L6Slot *slots;           // prefixes longer than /64 (null: none)
+    const uint4 *slots64;          // prefixes of /1-/64 (null: none)
     const uint64_t *bloom;
     const uint32_t *lens;
     uint32_t mask;                 // slots - 1
+    uint32_t mask64;               // slots64 - 1
     uint32_t bloom_mask;           // words - 1
     uint32_t nlen;                 // entries of lens
     uint32_t def_label;            // label of ::/0 (0: none)
@@ -238,6 +246,14 @@ __host__ __device__ inline uint32_t l6_group_hash(const uint32_t w[4], uint32_t 
 __host__ __device__ inline uint64_t l6_bloom_bits(uint32_t h)
 {
     return (1ull << ((h >> 20) & 63)) | (1ull << (h >> 26));
+}
+// the IPv6 prefilter's exact /128 set (v6_fix, bpf_xdp.c:132-156): its
+// addresses (host-order words) in an LDS Bloom filter of the same kind, so
+// that a header whose source is not in the set costs no global load
+__host__ __device__ inline uint32_t pf6_bloom_hash(uint32_t w0, uint32_t w1, uint32_t w2,
+                                                   uint32_t w3)
+{
+    return fmix32(l6_hash(w0, w1, w2, w3, 0x300u) ^ 0x5bd1e995u);
 }
 
 // ---- IPv6 endpoints: 32-byte slots {raw address words, pol_base, pol_mask,
@@ -421,6 +437,8 @@ struct DevTables {
     Lpm6 ipc6;                     // ipcache
     Lpm6 pf6_fix;                  // prefilter exact /128 set (one length)
     Lpm6 pf6_dyn;                  // prefilter LPM deny list
+    const uint32_t *pf6_bloom;     // Bloom filter over pf6_fix (all /128), or null
+    uint32_t pf6_bloom_words;      // power of two, 0 = no filter
     const Lxc6Slot *lxc6;          // null when no IPv6 endpoints
     uint32_t lxc6_mask;
     uint32_t lxc6_lds;             // 1: copied to LDS

@@ -56,14 +56,15 @@ struct Map {
     // a commit patches into the device CT table in place
     std::map<std::string, int> touched;
     bool ct() const { return role == ROLE_CT4 || role == ROLE_CT6; }
-    // entries of an IPv4 TCP CT map that no lookup reaches (ct_create4's
-    // ICMP "related" entry, nexthdr != TCP at key byte 12): they live only
+    // entries of a TCP CT map that no lookup reaches (ct_create4/6's ICMP
+    // "related" entry, nexthdr != TCP at key byte 12 / 36): they live only
     // here, not in the device CT table (flatten.cpp build_ct), so the CT GC
     // filters them on the host; counted so a GC skips maps without any
     uint64_t n_aux = 0;
     bool aux_key(const std::string &k) const
     {
-        return role == ROLE_CT4 && !ct_any && k.size() >= 13 && (uint8_t)k[12] != 6;
+        return !ct_any && ((role == ROLE_CT4 && k.size() >= 13 && (uint8_t)k[12] != 6) ||
+                           (role == ROLE_CT6 && k.size() >= 37 && (uint8_t)k[36] != 6));
     }
     // CT entries the device GC deleted that the host mirror still holds
     // (erased at the next ct_sync)

@@ -99,7 +99,9 @@ def load_ct(dp: Datapath, t):
     if any(x >= 0 for x in lxcs):
         lxcs |= set(int(x) for x in t.policy)
     lxcs = sorted(lxcs | {-1})
-    n = max(1 << 16, 2 * len(ct))
+    # (t.ct_max_entries: the maps' capacity, when a test wants more room than
+    # the entries it loads — the device table is sized by the entries)
+    n = getattr(t, "ct_max_entries", None) or max(1 << 16, 2 * len(ct))
     fds = open_ct_maps(dp, lxcs, max_entries=n)
     import numpy as np
     for (fam, lxc, any_map), fd in fds.items():

@@ -5,8 +5,11 @@ section prescribes (FETCH_SIZE reads 1/2 of wide coalesced streaming reads
 on gfx950; the random 4-64 B lookups are reported as measured).
 
 usage: python3 scripts/pmc_summary.py OUTDIR [kernel-substring]
-           [--save PROFILE_DIR]
+           [--skip N] [--save PROFILE_DIR]
            [--record WORKLOAD MODE LPM4_LAYOUT [variant=V] KERNEL:HEADERS:STREAM_BYTES ...]
+
+--skip N leaves out each kernel's first N launches (the steady state: a
+context's first apply sizes its sets from nothing).
 
 --save copies the kernel statistics, the engine's rows of every counter pass
 (cfc:: kernels only) and this summary into PROFILE_DIR (the committed
@@ -39,22 +42,37 @@ def kernel_name(full):
     return m.group(1) if m else full.split("(")[0]
 
 
-def collect(out):
-    res = {"kernels": {}, "counters": {}}
+def collect(out, skip=0):
+    """skip: leave out each kernel's first `skip` launches (a context's first
+    apply sizes its sets cold; the steady state is what the bench line
+    describes), in the kernel trace's durations and in every counter pass"""
+    res = {"kernels": {}, "counters": {}, "skipped_first_launches": skip}
+    kt = glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))
     ks = glob.glob(os.path.join(out, "kt", "*kernel_stats.csv"))
-    if ks:
+    if kt:
+        durs = defaultdict(list)
+        for r in sorted(csv.DictReader(open(kt[0])), key=lambda r: int(r["Start_Timestamp"])):
+            if "cfc::" in r["Kernel_Name"]:
+                durs[kernel_name(r["Kernel_Name"])].append(
+                    (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        for k, v in durs.items():
+            v = v[skip:] if len(v) > skip else v
+            res["kernels"][k] = {"calls": len(v), "avg_ms": sum(v) / len(v)}
+    elif ks:
         for r in csv.DictReader(open(ks[0])):
             if "cfc::" in r["Name"]:
                 res["kernels"][kernel_name(r["Name"])] = {
                     "calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6}
     vals = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(out, "pmc*", "*counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
-            if "cfc::" in r["Kernel_Name"]:
-                vals[kernel_name(r["Kernel_Name"])][r["Counter_Name"]].append(
-                    float(r["Counter_Value"]))
+        rows = [r for r in csv.DictReader(open(f)) if "cfc::" in r["Kernel_Name"]]
+        rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
+        for r in rows:
+            vals[kernel_name(r["Kernel_Name"])][r["Counter_Name"]].append(
+                float(r["Counter_Value"]))
     for k, cs in vals.items():
-        res["counters"][k] = {c: sum(v) / len(v) for c, v in cs.items()}
+        res["counters"][k] = {c: sum(v[skip:] if len(v) > skip else v) /
+                              len(v[skip:] if len(v) > skip else v) for c, v in cs.items()}
     return res
 
 
@@ -144,9 +162,14 @@ def main(argv):
         i = a.index("--save")
         dst = a[i + 1]
         a = a[:i] + a[i + 2:]
+    skip = 0
+    if "--skip" in a:
+        i = a.index("--skip")
+        skip = int(a[i + 1])
+        a = a[:i] + a[i + 2:]
     out = a[0]
     kname = a[1] if len(a) > 1 else "k_classify_v4"
-    res = collect(out)
+    res = collect(out, skip)
     for k, c in res["counters"].items():
         res.setdefault("derived", {})[k] = derived(c)
     res["focus"] = kname

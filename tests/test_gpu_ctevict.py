@@ -145,3 +145,55 @@ def test_full_endpoint_maps_stay_on_device(torch, fam):
                 assert excess == 0       # the batch writes no global map
             total += excess
     assert total == st["ct_evicted"], (total, st)
+
+
+def test_evict_mid_apply_keeps_epoch_and_pending_work(torch):
+    """The eviction inside an apply patches only the CT table (patch_ct), it
+    does not commit: an earlier device apply's creates and TCP-map log
+    entries are still pending (no host sync between the batches), and a
+    policy entry added after the evicting batch was classified waits for a
+    commit.  The apply stays on the device, keeps the epoch its kernels read,
+    leaves the policy change pending for the next classify, and every
+    verdict, CT byte and surviving entry matches the oracle's sequential run
+    of both batches."""
+    from cilium_amd.datapath import Datapath, pack
+    from cilium_amd.loader import ct_rows
+    t, flows = full_tables(4)
+    # (new flows only: a live flow's packet could delete its entry, freeing
+    # room the second batch then would not need to evict)
+    h1 = S.headers_c5(t, flows, 100, seed=8, new_frac=1.0)
+    h2 = S.headers_c5(t, flows, 8000, seed=9, new_frac=0.1)
+    dp = Datapath(0)
+    pms = load_capped(dp, t)
+    dp.set_clock(1003)
+    b1, b2 = pack(h1), pack(h2)
+    o1 = dp.classify(b1, MODE_INGRESS, 0, want_ct=True)
+    dp.ct_apply(b1, o1, MODE_INGRESS, 0)
+    o2 = dp.classify(b2, MODE_INGRESS, 0, want_ct=True)
+    e0 = dp.stats()["epoch"]
+    pms[S.EP_LXC_ID].Allow(4_000_000, 0, 0, 0)   # (an identity no header has)
+    dp.ct_apply(b2, o2, MODE_INGRESS, 0)
+    torch.cuda.synchronize()
+    st = dp.stats()
+    assert st["epoch"] == e0, (st["epoch"], e0)
+    assert st["ct_evicted"] > 0 and st["ct_apply_host"] == 0, st
+    assert st["ct_apply_device"] == 2, st
+    ver = np.concatenate([o1.verdict.cpu().numpy(), o2.verdict.cpu().numpy()])
+    ctb = np.concatenate([o1.ct.cpu().numpy(), o2.ct.cpu().numpy()])
+    dp.counters_sync()
+    rows = ct_rows(dp, dp.ct_fds)
+    o3 = dp.classify(b1, MODE_INGRESS, 0, want_ct=True)   # commits the policy entry
+    torch.cuda.synchronize()
+    assert dp.stats()["epoch"] != e0
+    assert pms[S.EP_LXC_ID].Exists(4_000_000, 0, 0, 0)
+    del o3
+    dp.close()
+    o = O.Oracle(t)
+    o.set_clock(1003)
+    _, over, _, _, oct_ = o.run_sequential(S.concat([h1, h2]), MODE_INGRESS, 0, want_ct=True)
+    np.testing.assert_array_equal(ver, over)
+    np.testing.assert_array_equal(ctb, oct_)
+    wmap = {r[:44].tobytes(): r for r in o.ct_dump()}
+    for r in rows:
+        assert r[:44].tobytes() in wmap
+        np.testing.assert_array_equal(r, wmap[r[:44].tobytes()])

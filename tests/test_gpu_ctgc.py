@@ -1,8 +1,9 @@
 """Conntrack garbage collection (cfc_ct_gc: ctmap.GC with doFiltering,
 pkg/maps/ctmap/ctmap.go:303-350) against the oracle's restatement
-(cfo_ct_gc).  IPv4 entries are collected on the device CT table (tombstones,
-trimmed cluster tails, a delete log the host mirror replays lazily); IPv6
-maps and the ICMP entries of IPv4 TCP maps on the host.  After every GC the
+(cfo_ct_gc).  IPv4 and IPv6 entries are collected on the device CT tables
+(doGC4 / doGC6: tombstones, trimmed cluster tails, a delete log the host
+mirror replays lazily); the ICMP entries of TCP maps, which no lookup
+reaches and the device table does not hold, on the host.  After every GC the
 CT maps — keys, values, accounting — equal the oracle's byte for byte, and
 applies after a GC (reusing the freed slots) stay exact.
 Run on an MI355X: pytest -m gpu."""
@@ -132,8 +133,8 @@ def test_gc_steady_state_cycles(torch):
 
 @pytest.mark.parametrize("name", [n for n in G.names() if n.startswith("ct_")])
 def test_gc_golden_tables(torch, name):
-    """The reference's own CT state (IPv4 on the device with its TCP maps'
-    ICMP entries on the host; IPv6 on the host), one map at a time and all
+    """The reference's own CT state (both families on the device, their TCP
+    maps' ICMP entries on the host), one map at a time and all
     at once, at a time inside the spread of lifetimes."""
     g = G.Golden(name)
     dp = Datapath(0)
@@ -149,5 +150,82 @@ def test_gc_golden_tables(torch, name):
     same_ct(dp, o)
     st = dp.ct_gc(-1, mid + 7)
     assert st["deleted"] == o.ct_gc(time=mid + 7)   # nothing pending: exact
+    same_ct(dp, o)
+    dp.close()
+
+
+def step6(torch, dp, o, h, now, mode=0):
+    dp.set_clock(now)
+    o.set_clock(now)
+    b = pack(h)
+    out = dp.classify(b, mode, 0, want_ct=True)
+    dp.ct_apply(b, out, mode, 0)
+    _, ov, _, oct_ = o.classify(h, mode, 0, nthreads=16, want_ct=True, apply_ct=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.verdict.cpu().numpy(), ov)
+    assert np.array_equal(out.ct.cpu().numpy(), oct_)
+
+
+def test_gc6_on_device_vs_oracle(torch):
+    """doGC6 (ctmap.go:239) on the device CT6 table (k_ct_gc<true>): expiry,
+    then MatchIPs and ValidIPs over 16-byte addresses, each against the
+    oracle's maps byte for byte, with device applies before and after (the
+    freed slots reused) and the IPv6 TCP maps' ICMPv6 entries filtered on the
+    host."""
+    t, flows = S.config_c5_v6(6, n_flows=100_000, n_prefixes=20_000, now=1000)
+    dp = Datapath(0)
+    load_tables(dp, t)
+    o = O.Oracle(t)
+    h = S.headers_c5_v6(t, flows, 400_000, seed=6)
+    step6(torch, dp, o, h.slice(0, 200_000), 1000)
+    step6(torch, dp, o, h.slice(200_000, 400_000), 1030)
+    f = ctmap.GCFilter(remove_expired=True)
+    ctmap.GC(dp, -1, f, now=1065)
+    n = o.ct_gc(time=1065)
+    same_ct(dp, o)
+    assert n > 0 and f.stats["device_deleted"] > 0, f.stats
+    same_count(f.stats, n)
+    h2 = S.headers_c5_v6(t, flows, 200_000, seed=7)
+    step6(torch, dp, o, h2, 1070)
+    remote = np.unique(np.asarray(flows.saddr, np.uint8).reshape(-1, 16), axis=0)[:300]
+    rb = [bytes(r) for r in remote]
+    st = dp.ct_gc(-1, 0, False, match_ips=rb[:150])
+    n = o.ct_gc(remove_expired=False, match=[(6, b) for b in rb[:150]])
+    same_ct(dp, o)
+    assert n > 0 and st["device_deleted"] > 0, st
+    same_count(st, n)
+    valid = rb + [bytes(np.asarray(S.local_v6_addrs(t)[0], np.uint8))]
+    st = dp.ct_gc(-1, 0, False, valid_ips=valid[:200])
+    n = o.ct_gc(remove_expired=False, valid=[(6, b) for b in valid[:200]])
+    same_ct(dp, o)
+    same_count(st, n)
+    step6(torch, dp, o, h.slice(0, 100_000), 1080)
+    same_ct(dp, o)
+    assert dp.stats()["ct_apply_host"] == 0
+    dp.close()
+
+
+def test_gc6_steady_state_cycles(torch):
+    """IPv6 apply + GC cycles at the reference's cadence, every GC on the
+    device: no host walk, the table keeps its size, the maps the oracle's."""
+    t, flows = S.config_c5_v6(6, n_flows=60_000, n_prefixes=20_000, now=1000)
+    dp = Datapath(0)
+    load_tables(dp, t)
+    o = O.Oracle(t)
+    now, sizes, slots = 1000, [], []
+    for k in range(6):
+        h = S.headers_c5_v6(t, flows, 150_000, seed=30 + k)
+        step6(torch, dp, o, h, now)
+        now += ctmap.GC_INTERVAL_DEFAULT + 1
+        dp.set_clock(now)
+        f = ctmap.GCFilter(remove_expired=True)
+        ctmap.GC(dp, -1, f)
+        same_count(f.stats, o.ct_gc(time=now))
+        assert f.stats["device_deleted"] > 0, f.stats
+        dp.counters_sync()
+        sizes.append(len(o.ct_dump()))
+        slots.append(dp.stats()["ct_slots"])
+    assert dp.stats()["ct_apply_host"] == 0
+    assert len(set(slots[1:])) == 1, slots
     same_ct(dp, o)
     dp.close()

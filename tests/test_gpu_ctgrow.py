@@ -41,12 +41,13 @@ def slots_at_load(t):
 
 @pytest.mark.parametrize("mode", [0, 3])
 def test_ct_table_grows_inside_a_batch(torch, mode):
-    """20k live flows (a 64k-slot table), then a 600k-header packet-order
+    """5k live flows (10k entries: a 32k-slot table), then a 600k-header packet-order
     stream with 30% new-flow headers in two batches: the first batch alone
     adds more keys than 3/4 of the table holds, so its apply grows the table
     on the device (with the batch's ordering already resolved) and folds it
     there; the second batch runs on the grown table."""
-    t, flows = S.config_c5(5, n_flows=20_000, n_prefixes=20_000, n_policy=4000, now=1000)
+    t, flows = S.config_c5(5, n_flows=5_000, n_prefixes=20_000, n_policy=4000, now=1000)
+    t.ct_max_entries = 1 << 20   # (the maps have room: only the device table is small)
     h = S.headers_c5_seq(t, flows, 600_000, seed=21, new_frac=0.3)
     before = slots_at_load(t)
     g, want = run_both(torch, t, h, mode, clock=1003, chunks=2, notify=True)
@@ -61,7 +62,8 @@ def test_ct_table_grows_twice_before_a_sync(torch):
     """Three batches that each outgrow the table: the growths stack their
     slot maps before anything reads the host mirror (one remap, composed on
     the device, taken at the final dump)."""
-    t, flows = S.config_c5(5, n_flows=10_000, n_prefixes=20_000, n_policy=4000, now=1000)
+    t, flows = S.config_c5(5, n_flows=2_000, n_prefixes=20_000, n_policy=4000, now=1000)
+    t.ct_max_entries = 1 << 20
     h = S.headers_c5_seq(t, flows, 900_000, seed=22, new_frac=0.4)
     g, want = run_both(torch, t, h, 3, clock=1003, chunks=3, notify=False)
     check(g, want)
@@ -69,9 +71,10 @@ def test_ct_table_grows_twice_before_a_sync(torch):
 
 
 def test_ct6_table_grows_inside_a_batch(torch):
-    """IPv6: 20k live flows, 40% new-flow headers, three batches folded on
+    """IPv6: 5k live flows, 40% new-flow headers, three batches folded on
     the device; every CT6 entry and counter against the oracle."""
-    t, flows = S.config_c5_v6(6, n_flows=20_000, n_prefixes=20_000)
+    t, flows = S.config_c5_v6(6, n_flows=5_000, n_prefixes=20_000)
+    t.ct_max_entries = 1 << 20
     h = S.headers_c5_v6(t, flows, 300_000, seed=43, new_frac=0.4)
     before = slots_at_load(t)
     compare_with_oracle(torch, t, h, 0, chunks=3, ct_apply=L.CT_APPLY_DEVICE)
