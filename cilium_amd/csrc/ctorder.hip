@@ -974,9 +974,15 @@ __global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t
     }
     put_rk<V6>(O, r, o.sa, o.da, z, w);
     // the sort key: a 32-bit key fingerprint, then the header order (a
-    // create's related write right after its own lookup)
+    // create's related write right after its own lookup).  The fingerprint
+    // is fp64's second hash, independent of ct_hash4(sa, da, z, w): the
+    // participants were picked by tags (ck_miss4 / ck_miss6) that are that
+    // first hash, so two keys whose tags collided would share 29 of its 32
+    // bits — a collision in resolve's walk one time in eight, and a key
+    // behind a hot flow's thousands of records walks them all, one
+    // dependent load at a time (3-15 ms launches in round 6's first traces)
     const uint32_t ord = (uint32_t)(((2 * i + (uint64_t)st) << 1) | (rel ? 1u : 0u));
-    O.rh[r] = (fp64(o.sa, o.da, z, w) & 0xFFFFFFFF00000000ull) | ord;
+    O.rh[r] = (fp64(o.sa, o.da, z, w) << 32) | ord;
     O.ridx[r] = r;
     if (rel) {
         O.pinfo[r] = PI_REL | PI_POST;
@@ -1020,15 +1026,18 @@ __global__ __launch_bounds__(256) void k_ord_resolve(OrdArgs O, const uint64_t *
         return;
     uint8_t state = (f & PI_START) ? 1 : 0;
     const uint32_t fk = (uint32_t)(h[k] >> 32);
+    uint32_t coll = 0;
     for (uint32_t j = k; j > 0 && (uint32_t)(h[j - 1] >> 32) == fk; j--) {
         const uint32_t q = idx[j - 1];
         if (rk_eq<V6>(O, q, r)) {
             state = (O.pinfo[q] & PI_POST) ? 1 : 0;
             break;
         }
-        atomicAdd(&O.cnt[ORD_COLL], 1u);   // (a fingerprint collision: walk on)
+        coll++;   // (a fingerprint collision: walk on)
     }
     O.nres[r] = state;
+    if (coll)
+        atomicAdd(&O.cnt[ORD_COLL], coll);
 }
 
 // the related-entry writes of the creates round 1 resolved (CT_NEW and
@@ -1334,6 +1343,12 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         if (int rc = sort_records<V6>(O, npi, s, &h, &idx))
             return rc;
         hipLaunchKernelGGL(k_ord_resolve<V6>, dim3(gp), dim3(256), 0, s, O, h, idx, npi);
+        if (dbg) {
+            if (!rd())
+                return -EIO;
+            fprintf(stderr, "ord: resolve %u records, %u fingerprint-collision steps\n", npi,
+                    hc[ORD_COLL]);
+        }
         // round 2 only with an ICMP error among the participants: with the
         // launch's tags and no deleted slot, mark and collect counted them
         const bool relkeys = !O.tagged || O.ndel || hc[ORD_RELBOUND];
