@@ -238,6 +238,10 @@ def main():
                          "table) + the CT garbage collector when its interval has "
                          "passed; the new flows' source ports are re-drawn on the "
                          "device at the start of each step, so every step creates")
+    ap.add_argument("--family", type=int, default=4, choices=[4, 6],
+                    help="c5: the IPv4 (default) or the IPv6 shape — config_c5_v6's C3 "
+                         "tables (100k IPv6 prefixes) and --flows live CT6 flows, every "
+                         "header IPv6 (cfc_classify_v6 + cfc_ct_apply_v6)")
     ap.add_argument("--stream", default="spec", choices=["spec", "seq"],
                     help="c5: spec = SURVEY.md §8d's C5 stream (new flows whose "
                          "reverse is not in the batch); seq = synth.headers_c5_seq, "
@@ -253,8 +257,10 @@ def main():
     args = ap.parse_args()
     if args.ct_apply and args.workload != "c5":
         ap.error("--ct-apply needs --workload c5")
-    if args.notify and args.workload == "c3":
+    if args.notify and (args.workload == "c3" or args.family == 6):
         ap.error("--notify covers IPv4 batches (c2, c5)")
+    if args.family == 6 and (args.workload != "c5" or args.stream != "spec"):
+        ap.error("--family 6: the c5 workload's spec stream")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: start the ranks before anything touches the
         # GPU (torchrun on 127.0.0.1), wait for them, exit with their status
@@ -284,7 +290,13 @@ def main():
     ep_lxc = S.EP_LXC_ID if mode == 1 else 0
 
     t0 = time.time()
-    if args.workload == "c5":
+    v6c5 = args.workload == "c5" and args.family == 6
+    if v6c5:
+        assert world == 1, "--family 6: one GPU"
+        tables, flows = S.config_c5_v6(args.seed, n_flows=args.flows)
+        log(f"[rank {rank}] C5 IPv6 tables: {len(tables.ct)} CT6 entries for "
+            f"{len(flows)} flows ({time.time() - t0:.1f}s)")
+    elif args.workload == "c5":
         tables, flows = S.config_c5(args.seed, n_flows=args.flows)
         # several GPUs: flow affinity — each rank holds the CT
         # entries and draws the traffic of the address pairs it owns; no CT
@@ -312,6 +324,18 @@ def main():
         batch6 = pack_v6(h6, dev)
         n = n - n // 2
         s, d, p, m = S.gen_batch_v4_torch(tables, n, args.seed * 1000 + rank, dev)
+    elif v6c5:   # every header IPv6: the v4 batch is empty
+        from cilium_amd.datapath import pack_v6
+        h6, new6 = S.headers_c5_v6(tables, flows, n, seed=args.seed * 1000 + rank,
+                                   return_new=True)
+        new6 &= (h6.proto == S.IPPROTO_TCP) | (h6.proto == S.IPPROTO_UDP)
+        batch6 = pack_v6(h6, dev)
+        n = 0
+        s, d, p, m = (torch.empty(0, dtype=torch.int32, device=dev) for _ in range(4))
+        tf = torch.empty(0, dtype=torch.uint8, device=dev)
+        new_idx = torch.from_numpy(np.flatnonzero(new6)).to(dev)
+        new_ports = batch6.ports[new_idx].clone()
+        h6 = S.take(h6, slice(0, min(len(h6), args.cpu_sample)))   # (the CPU sample)
     elif args.workload == "c5":
         from cilium_amd.datapath import pack_v4
         if args.stream == "seq":
@@ -343,7 +367,11 @@ def main():
     clock = {"now": 0, "last_gc": 0, "gcs": 0, "gc_deleted": 0, "alive": None}
     n6 = len(batch6) if batch6 is not None else 0
     out6 = Verdicts(torch.empty(n6, dtype=torch.int32, device=dev),
-                    torch.empty(n6, dtype=torch.int32, device=dev), None)
+                    torch.empty(n6, dtype=torch.int32, device=dev), None,
+                    torch.empty(n6, dtype=torch.uint8, device=dev) if v6c5 and args.ct_apply
+                    else None)
+    # the batch the CT apply folds (IPv6 with --family 6)
+    ct_batch, ct_out = (batch6, out6) if v6c5 else (batch, out)
 
     nt_rec = nt_idx = nt_cnt = None
     if args.notify:
@@ -370,13 +398,16 @@ def main():
     def step(timed=False):
         if args.ct_apply:   # fresh new flows: their source ports re-drawn
             salt[0] += 1
-            p[new_idx] = new_ports ^ ((salt[0] * 0x9E37) & 0xFFFF)
+            ct_batch.ports[new_idx] = new_ports ^ ((salt[0] * 0x9E37) & 0xFFFF)
             clock["now"] += args.step_seconds
             dp.set_clock(clock["now"])
-        dp.classify_v4(batch, mode, ep_lxc, out=out)
+        if n:
+            dp.classify_v4(batch, mode, ep_lxc, out=out)
+        if v6c5:
+            dp.classify_v6(batch6, mode, ep_lxc, out=out6)
         if args.ct_apply:
             e0 = ev() if timed else None
-            dp.ct_apply(batch, out, mode, ep_lxc)
+            dp.ct_apply(ct_batch, ct_out, mode, ep_lxc)
             e1 = ev() if timed else None
             e2 = None
             # EnableConntrackGC's loop (pkg/endpointmanager/conntrack.go:96-125)
@@ -394,7 +425,7 @@ def main():
                 dp.h, ctypes.byref(nt_hdr), ctypes.byref(nt_out), mode, ep_lxc,
                 _ptr(nt_rec), _ptr(nt_idx), n, _ptr(nt_cnt), nt_stream),
                 "monitor events")
-        if n6:
+        if n6 and not v6c5:
             dp.classify_v6(batch6, mode, ep_lxc, out=out6)
     torch.cuda.synchronize()
     log(f"[rank {rank}] batch of {n} headers generated ({(n * S_IN) >> 20} MiB)")
@@ -436,7 +467,7 @@ def main():
     wall = time.perf_counter() - w0
     call_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     tm = dp.timing_collect()
-    assert tm["launches"] == args.steps * (2 if n6 else 1), tm
+    assert tm["launches"] == args.steps * ((1 if n else 0) + (1 if n6 else 0)), tm
     kern_ms = tm["classify_ms"] / args.steps        # classify kernel(s) per step
     count_ms = tm["count_ms"] / args.steps          # counter kernels per step
     kern6_ms = tm["classify_v6_ms"] / args.steps    # the IPv6 kernel's share
@@ -464,6 +495,7 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     samp = args.cpu_sample if (world == 1 and not args.no_cpu) else 200_000
+    samp6 = samp
     samp = min(samp, n)
     hs = S.unpack_v4(s[:samp].cpu().numpy(), d[:samp].cpu().numpy(),
                      p[:samp].cpu().numpy(), m[:samp].cpu().numpy())
@@ -477,14 +509,21 @@ def main():
     # the timed run computes what the engine computes (no lookup counting);
     # the lookup counts for the §8d bytes come from a second, untimed run
     c0 = time.perf_counter()
-    oa, ov, oi = orc.classify(hs, mode, ep_lxc, nthreads=cores)
+    if n:
+        oa, ov, oi = orc.classify(hs, mode, ep_lxc, nthreads=cores)
     cpu_s = time.perf_counter() - c0
-    lk = orc.classify(hs, mode, ep_lxc, nthreads=cores, want_lookups=True)[3]
+    lk = orc.classify(hs, mode, ep_lxc, nthreads=cores, want_lookups=True)[3] if n \
+        else np.zeros(1)
     # the timed region's last launch wrote `out` for this same batch
     # (with --ct-apply the tables moved on during the timed steps: the CT
     # parity of classify + apply is tests/test_gpu_fullsize.py's)
-    parity = None if args.ct_apply else bool(np.array_equal(out.verdict[:samp].cpu().numpy(), ov) and
+    parity = None if (args.ct_apply or not n) else bool(np.array_equal(out.verdict[:samp].cpu().numpy(), ov) and
                   np.array_equal(out.identity[:samp].cpu().numpy().view(np.uint32), oi))
+    if v6c5:
+        # the IPv6 sample's tuples as the last step classified them (its new
+        # flows' ports re-drawn per step)
+        pp = batch6.ports[:len(h6)].cpu().numpy().view(np.uint32)
+        h6.sport, h6.dport = (pp & 0xFFFF).astype(np.uint16), (pp >> 16).astype(np.uint16)
     if args.notify:   # the sample's monitor records, every field
         _, ov2, oi2, ow = orc.classify(hs, mode, ep_lxc, nthreads=cores,
                                        want_notify=True)
@@ -499,7 +538,7 @@ def main():
     b_hdr = S_IN + S_OUT + 64.0 * mean_l
     algo_bytes = n * b_hdr
     if n6:   # the IPv6 half: 40 B in per header, its own lookup counts
-        s6 = min(samp, n6)
+        s6 = min(samp6, n6, len(h6))
         hs6 = S.take(h6, slice(0, s6))
         c1 = time.perf_counter()
         o6a, o6v, o6i = orc.classify(hs6, mode, ep_lxc, nthreads=cores)
@@ -524,7 +563,7 @@ def main():
     ws_ct6 = 96 * (1 << max(0, 2 * st["ct6_entries"] - 1).bit_length()) if st["ct6_entries"] else 0
     ws4 = st["device_bytes"] - 1024 * st["lpm6_kib"] + ws_ct4
     ws6 = st["device_bytes"] - 1024 * st["lpm4_kib"] + ws_ct6
-    kernels = [("k_classify_v4", n, kern_ms - kern6_ms, ws4)]
+    kernels = [("k_classify_v4", n, kern_ms - kern6_ms, ws4)] if n else []
     if n6:
         kernels.append(("k_classify_v6", n6, kern6_ms, ws6))
     rows = ubench_ceilings()
@@ -533,8 +572,8 @@ def main():
     # serves them: the Infinity-Cache row of a kernel whose tables outgrow
     # L2, else the HBM row (the largest table measured)
     variant = "ct_apply" if args.ct_apply else "notify" if args.notify else "lookup"
-    pe = pmc_entry(args.workload, args.mode, layout, [(k, hn) for k, hn, _, _ in kernels],
-                   variant)
+    pe = pmc_entry("c5v6" if v6c5 else args.workload, args.mode, layout,
+                   [(k, hn) for k, hn, _, _ in kernels], variant)
     per_kernel = []
     req_tot = ideal_s = ideal_u = traffic = 0.0
     for k, hn, ms, ws in kernels:
@@ -573,6 +612,11 @@ def main():
                          f"{st['prefilter_v4_fix'] + st['prefilter_v6_fix']}-entry "
                          f"prefilter, {n6} IPv6 + {n} IPv4 headers per step, "
                          if args.workload == "c3" else
+                         f"C5 IPv6: C3 tables ({st['ipcache_v6_prefixes']} IPv6 prefixes) + "
+                         f"{st['ct6_entries']} reachable CT6 entries ({args.flows} live "
+                         f"flows, global CT6 maps), 95% Zipf(1.1) packets of live flows + "
+                         f"5% new (synth.headers_c5_v6), "
+                         if v6c5 else
                          f"C5: C2 tables + {st['ct4_entries']} reachable CT4 "
                          f"entries ({args.flows} live flows, global CT maps), "
                          + ("95% Zipf(1.1) packets of live flows + 5% new, "
@@ -593,9 +637,10 @@ def main():
                             f"header-stream shards x{world}, tables replicated"),
             "drop_notify": bool(args.notify),
             "ct_apply": bool(args.ct_apply),
+            "family": 6 if v6c5 else 4,
         },
         "roofline": {
-            "kernel": "k_classify_v4" + (" + k_classify_v6" if n6 else ""),
+            "kernel": " + ".join(k for k, _, _, _ in kernels),
             # random L2 (or Infinity-Cache) requests: the measured request-rate
             # ceiling for the tables' size is the bound
             "bound": bound,

@@ -1144,9 +1144,9 @@ std::shared_ptr<GCt> build_ctg(HostImage &img, const std::vector<Map *> &ms, hip
             }
         }
     }
-    if (n4 && (*rc = g->ct4_ms.zeros(8 * n4, s)))
+    if (n4 && (*rc = g->ct4_ms.zeros(12 * n4, s)))   // (ms, then lh)
         return nullptr;
-    if (n6 && (*rc = g->ct6_ms.zeros(8 * n6, s)))
+    if (n6 && (*rc = g->ct6_ms.zeros(12 * n6, s)))
         return nullptr;
     for (Map *m : ms)
         if (m->role == ROLE_CT4 || m->role == ROLE_CT6)
@@ -3219,7 +3219,7 @@ int ct_grow(cfc_ctx *c, bool v6, uint64_t want, hipStream_t s)
     // (every new line zero: the rehash writes only the moved slots', and a
     // free slot's record must read as no entry, no dirty bits)
     if (nk->zeros(ksz * want, s) || nst->zeros(sizeof(CtState) * (m4 + m6), s) ||
-        nsum->zeros(4 * (m4 + m6), s) || nms->zeros(8 * want, s) ||
+        nsum->zeros(4 * (m4 + m6), s) || nms->zeros(12 * want, s) ||
         (lb.p && nlb->zeros(16 * want, s)) || map.ensure(4 * o) ||
         c->cta_cnt.ensure(4 * CTA_NCNT))
         return -ENOMEM;
@@ -3418,12 +3418,14 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         A.acct_base = E.T.ct6_acct_base;
         A.st = (CtState *)G.ct_st.p + A.acct_base;
         A.ms = (uint2 *)G.ct6_ms.p;
+        A.lh = (uint32_t *)(A.ms + slots);
     } else {
         A.ct4 = (Ct4Slot *)G.ct4.p;
         A.mask = G.ct4_mask;
         A.acct_base = 0;
         A.st = (CtState *)G.ct_st.p;
         A.ms = (uint2 *)G.ct4_ms.p;
+        A.lh = (uint32_t *)(A.ms + slots);
     }
     A.hs = (uint32_t *)c->cta_hs.p;
     A.reqA = (uint64_t *)c->cta_req.p;
@@ -3678,7 +3680,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         if (!others) {
             uint64_t &mn = V6 ? c->ct_min6 : c->ct_min4;
             mn = std::max<uint64_t>(mn, 2 * (used + ins + newk));
-            if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess)
+            if (hipMemsetAsync(A.ms, 0, 12 * slots, s) != hipSuccess)
                 return -EIO;
             c->built_sig[3] = ~0ull;
             if (int rc = commit_locked(c, s))
@@ -3761,7 +3763,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
                 (unsigned long long)newk, (unsigned long long)(used + ins),
                 (unsigned long long)slots);
     if (!ok) {   // the scan's marks (and delete orders) go
-        if (hipMemsetAsync(A.ms, 0, 8 * slots, s) != hipSuccess ||
+        if (hipMemsetAsync(A.ms, 0, 12 * slots, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess)
             return -EIO;
         return 1;
@@ -3802,7 +3804,7 @@ int ct_apply_dev(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode, uint16
         // or summary may leak into the next apply, the claims made count,
         // and the next commit rebuilds the CT group from the synced maps
         (void)hipStreamSynchronize(s);
-        (void)hipMemsetAsync(A.ms, 0, 8 * slots, s);
+        (void)hipMemsetAsync(A.ms, 0, 12 * slots, s);
         uint32_t cl = 0;
         (void)hipMemcpyAsync(&cl, A.cnt + CTA_CLAIMS, 4, hipMemcpyDeviceToHost, s);
         (void)hipStreamSynchronize(s);

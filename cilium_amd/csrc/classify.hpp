@@ -212,6 +212,10 @@ struct CtaArgs {
     // per slot {mark, summary} of this apply (one 8-byte word: route reads
     // both with one random load)
     uint2 *ms;
+    // per slot the order + 1 of the last plain hit route kept out of the
+    // ordered list (0: none; k_cta_route), cleared by the fold; null: every
+    // hit of an ordered slot is listed
+    uint32_t *lh;
     // the classify launch's plain-hit summaries of this family's slots
     // (DevTables.ct_sum + acct_base) when the apply follows that launch:
     // the scan then leaves the summaries alone, the fold clears an ordered

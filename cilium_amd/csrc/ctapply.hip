@@ -1026,9 +1026,44 @@ __global__ __launch_bounds__(RQ_B) void k_cta_related(CtaArgs A, const uint64_t 
 // accounting).  RU consecutive header stages per thread and step: their
 // hit slots in four 16-byte loads, then the ordered-slot bitmap words, the
 // slot's words only for the ordered ones.  (Family-free.)
+//
+// A slot ordered by its closes alone (no create, related write or delete
+// among its ops; no monitor lengths wanted) keeps its plain hits out of the
+// list too — the TCP / UDP hits of headers without a work bit (wl_want):
+// every one of them is ACTION_CREATE on a live entry, so with one clock per
+// batch the run of them between two closes acts as its last one, and all of
+// them as one hit at the last one's order with the slot's summary (the
+// fold's sum_hit; the closes before it only add their flags, which the
+// summary's OR already holds).  Route keeps that order per slot (A.lh, a
+// max): a hot flow's hits, millions at C5 --stream seq, are one word, not
+// millions of sorted ops.  The maxima are taken per workgroup in an LDS
+// table first (a hot slot's atomics on one word would serialise).
 constexpr int RU = 16;
+constexpr uint32_t LH_N = 1024, LH_EMPTY = 0xFFFFFFFFu;
 __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
 {
+    __shared__ uint32_t s_lk[LH_N], s_lv[LH_N];
+    const bool summ = A.lh && A.W.bits && !A.nt;
+    if (summ) {
+        for (uint32_t q = threadIdx.x; q < LH_N; q += 256) {
+            s_lk[q] = LH_EMPTY;
+            s_lv[q] = 0;
+        }
+        __syncthreads();
+    }
+    auto lh_put = [&](uint32_t sl, uint32_t v) {
+        uint32_t h = (sl * 0x9E3779B1u) >> 22;
+        for (int p = 0; p < 8; p++, h = (h + 1) & (LH_N - 1)) {
+            uint32_t k = s_lk[h];
+            if (k == LH_EMPTY)
+                k = atomicCAS(&s_lk[h], LH_EMPTY, sl);
+            if (k == LH_EMPTY || k == sl) {
+                atomicMax(&s_lv[h], v);
+                return;
+            }
+        }
+        atomicMax(&A.lh[sl], v);   // (a full run of the table)
+    };
     // item k is header stage j = k (egress: two CT stages per header) or
     // j = 2k (one stage: the odd stages never hold a hit); with a load
     // balancer (egress) j in [2n, 4n) are the CT_SERVICE ops (virtual
@@ -1118,11 +1153,21 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
             const uint64_t j = two ? k0 + u : 2 * (k0 + u);
             const uint2 v = A.ms[slot[u]];
             bool o;
-            if ((v.x & (MARK_DEL | MARK_PUTC)) == MARK_DEL && !A.nt)
+            if ((v.x & (MARK_DEL | MARK_PUTC)) == MARK_DEL && !A.nt) {
                 // a deleted entry: its first delete stands for all its ops
                 o = ord_of(j >> 1, (int)(j & 1), SEC_OP) == 0xFFFFFFFFu - v.y;
-            else
+            } else {
                 o = (v.x & MARK_ORDERED) != 0;
+                const uint64_t i = j >> 1;
+                if (o && summ && !(v.x & (MARK_DEL | MARK_PUTC)) && i < A.n &&
+                    !((A.W.bits[i >> 6] >> (i & 63)) & 1)) {
+                    const uint32_t proto = A.mt[i] & 0xFF;
+                    if (proto == 6 || proto == 17) {   // (a plain hit: summarised)
+                        lh_put(slot[u], ord_of(i, (int)(j & 1), SEC_OP) + 1);
+                        o = false;
+                    }
+                }
+            }
             if (!o)
                 om &= ~(1u << u);
         }
@@ -1134,6 +1179,12 @@ __global__ __launch_bounds__(256) void k_cta_route(CtaArgs A)
                 A.cx[c] = pack(A, slot[u], ord_of(j >> 1, (int)(j & 1), SEC_OP));
             c++;
         }
+    }
+    if (summ) {   // (the workgroup's maxima)
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < LH_N; q += 256)
+            if (s_lk[q] != LH_EMPTY && A.lh[s_lk[q]] < s_lv[q])
+                atomicMax(&A.lh[s_lk[q]], s_lv[q]);
     }
 }
 
@@ -1188,6 +1239,32 @@ __device__ __forceinline__ uint32_t hit(St &e, uint32_t now, const Op<V6> &o)
             upd(e, now, CT_CLOSE_TIMEOUT, o.dir, o.tfl);
     }
     return m;
+}
+// a slot summary's plain hits (sum_bits: bit 16 / 17 a hit per direction
+// with its flags in bits 0-7 / 8-15, bit 18 a TCP hit without the close bit)
+// as one ACTION_CREATE hit on a live entry: the closing bits cleared, the
+// timeout re-armed, per direction with hits flags_seen |= theirs and
+// last_report = now iff the interval had passed or the flags grew (see
+// k_cta_finish)
+__device__ __forceinline__ void sum_hit(St &x, uint32_t now, uint32_t mu)
+{
+    x.bits &= ~(RX_CLOSING | TX_CLOSING);
+    const bool is_tcp = (mu & (1u << 18)) != 0;
+    if (is_tcp)
+        x.bits |= SEEN_NON_SYN;
+    x.lifetime = now + (is_tcp ? CT_LIFETIME_TCP : CT_LIFETIME_NONTCP);
+    if (mu & (1u << 16)) {
+        const uint32_t seen = (x.seen_rx | (mu & 0xFF)) & 0xFF;
+        if (x.last_rx + CT_REPORT_INTERVAL < now || seen != x.seen_rx)
+            x.last_rx = now;
+        x.seen_rx = seen;
+    }
+    if (mu & (1u << 17)) {
+        const uint32_t seen = (x.seen_tx | ((mu >> 8) & 0xFF)) & 0xFF;
+        if (x.last_tx + CT_REPORT_INTERVAL < now || seen != x.seen_tx)
+            x.last_tx = now;
+        x.seen_tx = seen;
+    }
 }
 // ct_create4/6's entry (seen_flags.syn = is_tcp: seen_non_syn stays clear)
 __device__ __forceinline__ St fresh(uint32_t now, bool is_tcp, uint32_t dir)
@@ -1258,8 +1335,12 @@ __global__ __launch_bounds__(256) void k_cta_dedup(CtaArgs A, const uint64_t *cx
     const uint64_t v = r < ncx ? cx[r] : ~0ull, vp = (r > 0 && r <= ncx) ? cx[r - 1] : ~0ull;
     const uint64_t sl = v >> A.ob;
     // a plain hit on a slot this batch does not write: its signature (a
-    // written slot keeps every hit: after the write each one counts)
-    const bool cand = sl <= A.mask && (vp >> A.ob) == sl && !(A.ms[(uint32_t)sl].x & MARK_PUTC);
+    // written slot keeps every hit: after the write each one counts; and an
+    // op with route's summarised hits between it and the one before, order
+    // lh - 1, is not a repeat: those hits may have changed the state)
+    const uint32_t lh = (sl <= A.mask && A.lh) ? A.lh[(uint32_t)sl] : 0u;
+    const bool cand = sl <= A.mask && (vp >> A.ob) == sl && !(A.ms[(uint32_t)sl].x & MARK_PUTC) &&
+                      !(lh && (uint32_t)(vp & omask) < lh - 1 && (uint32_t)(v & omask) >= lh);
     const uint32_t mine = sl <= A.mask ? hit_sig<V6>(A, (uint32_t)(v & omask)) : 0u;
     ssig[threadIdx.x + 1] = mine;
     if (threadIdx.x == 0)
@@ -1318,10 +1399,19 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
     // the next op's header is loaded (branch-free) while this one is
     // replayed; the owner word does not matter here (the slot is the key),
     // so no endpoint lookup
+    // (the plain hits route summarised: one hit at the last one's order)
+    const uint32_t lh = A.lh ? A.lh[slot] : 0u;
+    const uint32_t mu = lh ? (A.sum ? A.sum[slot] : A.ms[slot].x >> SUM_SH) : 0u;
+    bool summed = lh == 0;
     ScanIn<V6> cur;
     load_in<V6, LB, false>(A, ord_hdr((uint32_t)(cx[r0] & omask)), cur);
     for (uint32_t r = r0; r < ncx && (uint32_t)(cx[r] >> A.ob) == slot; r++) {
         const uint32_t ord = (uint32_t)(cx[r] & omask);
+        if (!summed && ord >= lh) {   // (past the last summarised hit, ord lh - 1)
+            if (live)
+                sum_hit(e, A.now, mu);
+            summed = true;
+        }
         ScanIn<V6> nxt;
         load_in<V6, LB, false>(A, ord_hdr((uint32_t)(cx[r + 1 < ncx ? r + 1 : r] & omask)), nxt);
         const Op<V6> o = decode_from<V6, LB>(A, cur, ord_st(ord), 0u);
@@ -1396,6 +1486,8 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
             }
         }
     }
+    if (!summed && live)
+        sum_hit(e, A.now, mu);
     // the load balancer's per-slot ct_state of what this batch wrote
     if (A.lb && live && created)
         A.lb[slot] = make_uint4(lbx, lby, 0, 0);
@@ -1432,6 +1524,8 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
     A.ms[slot] = make_uint2(0, 0);
     if (A.sum)   // (replayed here: the finish leaves the slot alone)
         A.sum[slot] = 0;
+    if (lh)
+        A.lh[slot] = 0;
 }
 
 // ---- the long runs (k_cta_fold's list).  When every op of a run is a
@@ -1459,8 +1553,11 @@ __device__ void fold_run(const CtaArgs &A, const uint64_t *cx, uint32_t ncx, uin
 // then per chunk its run, the OR of its closes, the OR of its closes after
 // its last ACTION_CREATE.
 constexpr uint32_t FOLD_CH = 4096;
+// A slot whose plain hits route summarised (A.lh) has them as one
+// ACTION_CREATE hit at the last one's place: RW_LH, the index + 1 of the
+// run's first op after it.
 enum { RW_R0, RW_END, RW_CBASE, RW_NCH, RW_BAD, RW_F0, RW_F1, RW_ANY, RW_NONSYN, RW_LASTC,
-       RW_LAST, RUN_W };
+       RW_LAST, RW_LH, RUN_W };
 struct LongScratch {
     uint32_t *start, *run, *crun, *call, *cafter;
     __device__ LongScratch(uint32_t *lng, uint32_t ncx)
@@ -1532,6 +1629,18 @@ __global__ __launch_bounds__(256) void k_cta_fold_plan(CtaArgs A, const uint64_t
         w[RW_NCH] = nch;
         for (int j = RW_BAD; j < RUN_W; j++)
             w[j] = 0;
+        const uint32_t lh = A.lh ? A.lh[slot] : 0u;
+        if (lh) {   // the first op past order lh - 1
+            uint32_t a = r0, b = lo;
+            while (a < b) {
+                const uint32_t mid = a + (b - a) / 2;
+                if ((uint32_t)(cx[mid] & ((1ull << A.ob) - 1)) < lh)
+                    a = mid + 1;
+                else
+                    b = mid;
+            }
+            w[RW_LH] = a + 1;
+        }
         for (uint32_t j = 0; j < nch; j++)
             L.crun[cb + j] = k;
     }
@@ -1586,8 +1695,11 @@ __global__ __launch_bounds__(256) void k_cta_fold_agg(CtaArgs A, const uint64_t 
         if (last)
             atomicMax(&s_last, last);
         __syncthreads();
-        // the chunk's closes after its last ACTION_CREATE hit
-        const uint32_t from = s_lastc;
+        // the chunk's closes after its last ACTION_CREATE hit (the
+        // summarised hits' one among them)
+        const uint32_t lhI = w[RW_LH];
+        const uint32_t from =
+            (lhI && lhI - 1 >= a && lhI - 1 < b) ? max(s_lastc, lhI - 1) : s_lastc;
         uint32_t after = 0;
         if (!s_bad)
             for (uint32_t r = max(a, from) + threadIdx.x; r < b; r += 256) {
@@ -1632,21 +1744,32 @@ __global__ __launch_bounds__(256) void k_cta_fold_fin(CtaArgs A, const uint64_t 
         }
         St e = load_state(A.st, slot);
         const uint32_t now = A.now;
+        const uint32_t lhI = w[RW_LH];
+        const uint32_t mu = lhI ? (A.sum ? A.sum[slot] : A.ms[slot].x >> SUM_SH) : 0u;
         for (int d = 0; d < 2; d++) {   // 0: rx (ingress), 1: tx
-            if (!((w[RW_ANY] >> d) & 1))
+            if (!(((w[RW_ANY] | mu >> 16) >> d) & 1))
                 continue;
-            const uint32_t fl = d == 0 ? w[RW_F0] : w[RW_F1];
+            const uint32_t fl = (d == 0 ? w[RW_F0] : w[RW_F1]) | ((mu >> (8 * d)) & 0xFFu);
             uint32_t &acc = d == 0 ? e.seen_rx : e.seen_tx;
             uint32_t &lr = d == 0 ? e.last_rx : e.last_tx;
             if (lr + CT_REPORT_INTERVAL < now || (fl & ~acc & 0xFFu))
                 lr = now;
             acc = (acc | fl) & 0xFF;
         }
-        if (w[RW_NONSYN])
+        if (w[RW_NONSYN] || (mu & (1u << 18)))
             e.bits |= SEEN_NON_SYN;
         const uint32_t cbase = w[RW_CBASE], nch = w[RW_NCH], lastc = w[RW_LASTC];
         uint32_t cb = 0, j0 = 0;
-        if (lastc) {   // the closes after the last ACTION_CREATE hit
+        if (lhI && lhI - 1 >= lastc) {   // the summarised hits are the last ACTION_CREATE
+            const uint32_t x = lhI - 1;
+            if (x >= w[RW_END]) {
+                j0 = nch;
+            } else {
+                j0 = (x - r0) / FOLD_CH;
+                cb = L.cafter[cbase + j0];
+                j0++;
+            }
+        } else if (lastc) {   // the closes after the last ACTION_CREATE hit
             j0 = (lastc - 1 - r0) / FOLD_CH;
             cb = L.cafter[cbase + j0];
             j0++;
@@ -1666,6 +1789,8 @@ __global__ __launch_bounds__(256) void k_cta_fold_fin(CtaArgs A, const uint64_t 
         A.ms[slot] = make_uint2(0, 0);
         if (A.sum)
             A.sum[slot] = 0;
+        if (lhI)
+            A.lh[slot] = 0;
     }
 }
 
@@ -1762,23 +1887,7 @@ __global__ __launch_bounds__(256) void k_cta_finish(CtaArgs A)
                 A.sum[sl] = 0;
             else
                 A.ms[sl].x = 0;
-            x.bits &= ~(RX_CLOSING | TX_CLOSING);
-            const bool is_tcp = (mu & (1u << 18)) != 0;
-            if (is_tcp)
-                x.bits |= SEEN_NON_SYN;
-            x.lifetime = A.now + (is_tcp ? CT_LIFETIME_TCP : CT_LIFETIME_NONTCP);
-            if (mu & (1u << 16)) {
-                const uint32_t seen = (x.seen_rx | (mu & 0xFF)) & 0xFF;
-                if (x.last_rx + CT_REPORT_INTERVAL < A.now || seen != x.seen_rx)
-                    x.last_rx = A.now;
-                x.seen_rx = seen;
-            }
-            if (mu & (1u << 17)) {
-                const uint32_t seen = (x.seen_tx | ((mu >> 8) & 0xFF)) & 0xFF;
-                if (x.last_tx + CT_REPORT_INTERVAL < A.now || seen != x.seen_tx)
-                    x.last_tx = A.now;
-                x.seen_tx = seen;
-            }
+            sum_hit(x, A.now, mu);
             store_state(A.st, sl, x);
             A.st[sl].info.y = iy[j] | CTI_UPDATED;
             }

@@ -901,9 +901,11 @@ def config_c5_v6(seed=6, n_flows=300_000, n_prefixes=100_000, n_policy=16384, no
     return t, flows
 
 
-def headers_c5_v6(t: Tables, flows: Headers, n, seed=6, new_frac=0.05, s=1.1):
+def headers_c5_v6(t: Tables, flows: Headers, n, seed=6, new_frac=0.05, s=1.1,
+                  return_new=False):
     """IPv6 C5 stream: Zipf packets of live flows plus new flows (C3
-    generator, every one to the endpoint)."""
+    generator, every one to the endpoint).  return_new: also the mask of
+    the new flows' headers."""
     rng = np.random.default_rng(seed + 777)
     m = int(n * (1 - new_frac))
     old = take(flows, _zipf_ranks(rng, len(flows), m, s))
@@ -912,7 +914,10 @@ def headers_c5_v6(t: Tables, flows: Headers, n, seed=6, new_frac=0.05, s=1.1):
     new = gen_headers_v6(rng, n - m, ipc6, local_v6_addrs(t)[:1], local_frac=1.0,
                          proxy_ident=proxy_identities(t))
     h = concat([old, new])
-    return take(h, rng.permutation(n))
+    perm = rng.permutation(n)
+    if return_new:
+        return take(h, perm), perm >= m
+    return take(h, perm)
 
 
 def headers_c5(t: Tables, flows: Headers, n, seed=5, new_frac=0.05, s=1.1,

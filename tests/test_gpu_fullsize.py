@@ -5,7 +5,8 @@ output of every header and every counter compared with the oracle:
   C3  configs[2]: 1M IPv6 + 100k IPv4 prefixes, 50k-entry prefilter;
   C5  configs[4]: C2 + 10M live flows (16M CT entries, a 32M-slot device
       table) with Zipf traffic, two batches folded into CT in between — the
-      CT accounting pass overflows its LDS table here.
+      CT accounting pass overflows its LDS table here; and its IPv6 shape
+      (10M live CT6 flows, two batches, the GC's expiry on the device).
 Run on an MI355X: pytest -m gpu."""
 import time
 
@@ -140,6 +141,57 @@ def test_c5_full_flows(torch):
     assert got.shape == want.shape
     np.testing.assert_array_equal(got, want)
     log(f"C5: CT maps compared ({len(got)} entries) {time.time() - t0:.1f}s")
+    dp.close()
+
+
+def test_c5_v6_full_flows(torch):
+    """The C5 shape in IPv6 at full size: C3-shaped tables (100k IPv6
+    prefixes) + 10M live flows in the global CT6 maps (a 32M-slot device
+    table of 48-byte keys), two Zipf batches classified, applied on the
+    device in packet order, then the CT GC's expiry on the device
+    (k_ct_gc<true>): verdicts, CT bytes, counters, the GC's deletes and every
+    CT6 entry against the oracle."""
+    from cilium_amd import ctmap
+    t0 = time.time()
+    t, flows = S.config_c5_v6(6, n_flows=10_000_000, n_prefixes=100_000, now=1000)
+    log(f"C5v6: {len(t.ct)} CT entries generated {time.time() - t0:.1f}s")
+    dp = Datapath(0)
+    pms = load_tables(dp, t)
+    st = dp.stats()
+    assert st["ct6_entries"] >= 10_000_000 and st["ct_slots"] >= 32 << 20, st
+    log(f"C5v6: engine tables {time.time() - t0:.1f}s")
+    o = O.Oracle(t)
+    h = S.headers_c5_v6(t, flows, 4_000_000, seed=66)
+    rng = np.random.default_rng(66)
+    h.tcpflags = np.where(h.proto == 6, rng.choice(np.array([0x10, 0x18, 0x02], np.uint8),
+                                                   size=len(h)), 0).astype(np.uint8)
+    b = pack(h)
+    for k, clock in enumerate((1003, 1010)):
+        dp.set_clock(clock)
+        o.set_clock(clock)
+        a, e = k * len(h) // 2, (k + 1) * len(h) // 2
+        sub = b.slice(a, e)
+        out = dp.classify(sub, 0, want_ct=True)
+        dp.ct_apply(sub, out, 0)
+        oa, ov, oi, oct_ = o.classify(h.slice(a, e), 0, 0, nthreads=16, want_ct=True,
+                                      apply_ct=True)
+        compare_outputs(out, oa, ov, oi)
+        np.testing.assert_array_equal(out.ct.cpu().numpy(), oct_)
+        log(f"C5v6: batch {k} compared {time.time() - t0:.1f}s")
+    st = dp.stats()
+    assert (st["ct_apply_device"], st["ct_apply_host"]) == (2, 0), st
+    # the GC at a clock past the UDP lifetime of the flows the batches missed
+    f = ctmap.GCFilter(remove_expired=True)
+    ctmap.GC(dp, -1, f, now=1070)
+    n = o.ct_gc(time=1070)
+    st = f.stats   # (test_gpu_ctgc.same_count: a twice-written pending entry counts twice)
+    assert st["device_deleted"] + st["host_deleted"] <= n <= st["deleted"], (st, n)
+    assert st["device_deleted"] > 0, st
+    compare_counters(dp, pms, o)
+    got, want = ct_rows(dp, dp.ct_fds), o.ct_dump()
+    assert got.shape == want.shape
+    np.testing.assert_array_equal(got, want)
+    log(f"C5v6: CT maps compared ({len(got)} entries) {time.time() - t0:.1f}s")
     dp.close()
 
 
