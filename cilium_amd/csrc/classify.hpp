@@ -357,8 +357,10 @@ struct OrdArgs {
     void *tmp;
     size_t tmp_bytes;
     // the launch's work list (EgressArgs.wl): with `sparse` the mark and
-    // collect passes read it rather than the whole batch; ord_resolve clears
-    // `sparse` when the batch deletes (the dense passes then run)
+    // collect passes read it rather than the whole batch (a deleting batch's
+    // mixed slots by two passes over it, k_ord_mixed / k_ord_collect_mix);
+    // ord_resolve clears `sparse` for an untagged create or full key sets
+    // (the dense passes then run)
     WList W;
     bool sparse;
     // (sparse) the batch's key set (cbloom as an open-addressing table of

@@ -44,6 +44,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "ctops.hpp"
 
@@ -339,7 +340,7 @@ __global__ __launch_bounds__(256) void k_ord_mixed(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= A.n)
+    if (i >= A.n || !O.cnt[ORD_NDEL])   // (the sparse passes launch it before their count)
         return;
     const uint32_t cb = A.ctb[i];
     const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
@@ -491,8 +492,10 @@ __global__ __launch_bounds__(256) void k_ord_collect(CtaArgs A, OrdArgs O)
 // of 64 headers.  Every create, every deleting stage and every ICMP error's
 // stage is a work bit; a dropped CT_NEW stage of another kind is a probe
 // bit.  An ESTABLISHED stage outside them is a plain hit, which takes part
-// only on a mixed slot — a batch with deletes goes back to the dense passes
-// (ord_resolve_t), so ORD_NEST counts the work bits' stages alone.
+// only on a mixed slot: a batch with deletes finds those by two passes over
+// the batch (k_ord_mixed, k_ord_collect_mix), and k_ord_write adds a plain
+// hit it changes to the work bits and list (the apply's sparse scan then
+// sees its create).  ORD_NEST counts the work bits' stages alone.
 
 // a dropped CT_NEW stage that is a probe (its header's probe bit): a key
 // tag that is not an ICMP error's
@@ -833,9 +836,13 @@ __global__ __launch_bounds__(256) void k_ord_probe_v(CtaArgs A, OrdArgs O)
 #pragma unroll
             for (int st = 0; st < NST; st++) {
                 const uint32_t tg = st ? k2[k] : k1[k];
-                // (a probe bit's stages: dropped CT_NEW, the header's last)
+                // (a probe bit's stage: dropped CT_NEW, the header's last —
+                // an egress header's first stage may be an allowed create,
+                // collect_w's participant, not a probe)
                 const uint32_t cs = (cb[k] >> (4 * st)) & 0xF;
-                if (!probe_tag(tg) || !(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_NEW)
+                const int last = (cb[k] & (CFC_CT_DONE << 4)) ? 1 : 0;
+                if (st != last || !probe_tag(tg) || !(cs & CFC_CT_DONE) ||
+                    (cs & CFC_CT_RES_MASK) != CT_NEW)
                     continue;
                 const uint32_t fb = bloom_bits(fmix32(tg));
                 if ((*pf_word(O, tg) & fb) != fb)
@@ -886,6 +893,37 @@ __global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
             }
             if (take)
                 part_put(S, O, (uint32_t)(i << 1) | (uint32_t)st);
+        }
+    }
+    part_flush(S, O);
+}
+
+// the sparse passes' mixed slots (a deleted slot with an allowed
+// CT_ESTABLISHED stage, k_ord_mixed): every CT_ESTABLISHED stage on one takes
+// part — plain hits outside the work bits among them, so a pass over the
+// batch (the launch's keys give the slots).  Nothing to do, and no load past
+// the counter, in a batch without deletes.
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_collect_mix(CtaArgs A, OrdArgs O)
+{
+    constexpr int NST = TWO ? 2 : 1;
+    __shared__ PartStage S;
+    if (threadIdx.x == 0)
+        S.n = 0;
+    __syncthreads();
+    if (O.cnt[ORD_NDEL]) {
+        for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < A.n;
+             i += (uint64_t)gridDim.x * 256) {
+            const uint32_t cb = A.ctb[i];
+#pragma unroll
+            for (int st = 0; st < NST; st++) {
+                const uint32_t cs = (cb >> (4 * st)) & 0xF;
+                if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED)
+                    continue;
+                const uint32_t sl = start_slot<V6>(A, O, i, st);
+                if (sl != NONE && ((O.mixbm[sl >> 5] >> (sl & 31)) & 1))
+                    part_put(S, O, (uint32_t)(i << 1) | (uint32_t)st);
+            }
         }
     }
     part_flush(S, O);
@@ -1080,6 +1118,16 @@ __global__ __launch_bounds__(256) void k_ord_write(CtaArgs A, OrdArgs O, uint32_
             uint32_t *ck = st ? O.ck2 : O.ck1;
             if (ck)
                 ck[i] = NONE;
+            // (sparse passes: a mixed slot's plain hit, outside the work
+            // bits, that changed joins them — and the work list the apply's
+            // scan runs over — once)
+            if (O.sparse && O.wl) {
+                unsigned long long *wb = reinterpret_cast<unsigned long long *>(
+                    const_cast<uint64_t *>(O.W.bits) + (i >> 6));
+                const unsigned long long bit = 1ull << (i & 63);
+                if (!(*wb & bit) && !(atomicOr(wb, bit) & bit))
+                    O.wl[atomicAdd(&O.cnt[ORD_NWL], 1u)] = (uint32_t)i;
+            }
         }
     }
     block_add(&O.cnt[ORD_CHANGED], chg ? 1u : 0u);
@@ -1227,14 +1275,16 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         ORD_LAUNCH(k_ord_rel_w, 1024, A, O);
         ORD_LAUNCH(k_ord_probe_v, gp, A, O);
         ORD_LAUNCH(k_ord_collect_w, gw, A, O);
+        // a batch that deletes: its mixed slots and their stages (two passes
+        // over the batch, each gone at its first load without a delete)
+        ORD_LAUNCH(k_ord_mixed, gn, A, O);
+        ORD_LAUNCH(k_ord_collect_mix, gw, A, O);
         if (!rd())
             return -EIO;
-        if (hc[ORD_NDEL] || hc[ORD_UNTAGGED] || hc[ORD_SETFULL]) {
-            // a batch that deletes (an allowed ESTABLISHED stage of a
-            // deleted slot, a plain hit outside the bits, takes part), with
-            // an untagged create, or whose keys the sets cannot hold: the
-            // dense passes on the filter (the delete marks made are
-            // idempotent)
+        if (hc[ORD_UNTAGGED] || hc[ORD_SETFULL]) {
+            // a batch with an untagged create, or whose keys the sets cannot
+            // hold: the dense passes on the filter (the delete and mixed
+            // marks made are idempotent)
             O.sparse = false;
             if (!filter(std::max(B.creates_hint, hc[ORD_NCREATE])) ||
                 hipMemsetAsync(O.cnt, 0, 4 * ORD_CHANGED, s) != hipSuccess)
@@ -1251,6 +1301,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
                 O.part_cap = hc[ORD_NPART];
                 ORD_LAUNCH(k_ord_probe_v, gp, A, O);
                 ORD_LAUNCH(k_ord_collect_w, gw, A, O);
+                ORD_LAUNCH(k_ord_collect_mix, gw, A, O);
                 if (!rd())
                     return -EIO;
             }
@@ -1376,6 +1427,30 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     if (np)
         hipLaunchKernelGGL(k_ord_write, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, A, O,
                            (uint32_t)np);
+    // (debugging: CFC_DEBUG_HDR=i,j,... prints those headers' participant
+    // records — result at the batch start, after, and the pass's)
+    static const char *dbg_hdr = getenv("CFC_DEBUG_HDR");
+    if (dbg_hdr && np && np < (1u << 24)) {
+        std::vector<uint32_t> part(np);
+        std::vector<uint8_t> pi(np), nr(np);
+        if (hipStreamSynchronize(s) == hipSuccess &&
+            hipMemcpy(part.data(), O.part, 4 * np, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(pi.data(), O.pinfo, np, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(nr.data(), O.nres, np, hipMemcpyDeviceToHost) == hipSuccess) {
+            std::vector<uint64_t> want;
+            for (const char *q = dbg_hdr; *q;) {
+                want.push_back(strtoull(q, (char **)&q, 10));
+                while (*q == ',')
+                    q++;
+            }
+            for (uint64_t p = 0; p < np; p++)
+                for (uint64_t w : want)
+                    if ((part[p] >> 1) == w)
+                        fprintf(stderr, "ord: part %llu hdr %llu st %u pinfo %02x nres %u\n",
+                                (unsigned long long)p, (unsigned long long)w, part[p] & 1,
+                                pi[p], nr[p]);
+        }
+    }
 #undef ORD_LAUNCH
     // (the per-slot state is cleared for the next batch as `clear` goes)
     return hipGetLastError() == hipSuccess ? 0 : -EIO;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 profile passes of the bench configurations (run via gpurun; one
 # call per group so each stays inside gpurun's limit):
-#   scripts/profile_r06.sh OUT c2|c3|c5ct|c5look|c5seq
+#   scripts/profile_r06.sh OUT c2|c3|c5ct|c5look|c5seq|c5v6 [ktonly]
 # kernel trace + stats, then one PMC pass per counter group (gfx950 block
 # limits), each under its own time limit; the first failure ends the script.
 set -o pipefail
@@ -14,6 +14,7 @@ c3)     ARGS="--workload c3 --steps 3 --warmup 1 --no-cpu" ;;
 c5ct)   ARGS="--workload c5 --ct-apply --steps 6 --warmup 2 --no-cpu" ;;
 c5look) ARGS="--workload c5 --steps 3 --warmup 1 --no-cpu" ;;
 c5seq)  ARGS="--workload c5 --ct-apply --stream seq --steps 6 --warmup 2 --no-cpu" ;;
+c5v6)   ARGS="--workload c5 --family 6 --ct-apply --steps 6 --warmup 2 --no-cpu" ;;
 *) echo "unknown group $G"; exit 2 ;;
 esac
 D="$OUT/$G"
