@@ -330,7 +330,7 @@ struct DevBuf {
 // ---- packet-order CT results (ctorder.hip), run by cfc_ct_apply before
 // the apply proper
 enum { ORD_NPART, ORD_NCREATE, ORD_NDEL, ORD_NNEWDROP, ORD_NEST, ORD_NESTDROP, ORD_UNTAGGED,
-       ORD_RELBOUND, ORD_NRELKEY, ORD_NREL,
+       ORD_RELBOUND, ORD_NRELKEY, ORD_NREL, ORD_NRK2, ORD_NMIX,
        ORD_COLL, ORD_SETFULL, ORD_NWL, ORD_NUL, ORD_CHANGED, ORD_NCNT };
 struct OrdArgs {
     uint8_t *ctb;                 // the batch's CT bytes (rewritten in place)

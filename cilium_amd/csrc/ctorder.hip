@@ -352,8 +352,9 @@ __global__ __launch_bounds__(256) void k_ord_mixed(CtaArgs A, OrdArgs O)
             continue;
         const uint32_t sl = start_slot<V6>(A, O, i, st);
         const uint32_t b = 1u << (sl & 31);
-        if (sl != NONE && (O.delbm[sl >> 5] & b) && !(O.mixbm[sl >> 5] & b))
-            atomicOr(&O.mixbm[sl >> 5], b);
+        if (sl != NONE && (O.delbm[sl >> 5] & b) && !(O.mixbm[sl >> 5] & b) &&
+            !(atomicOr(&O.mixbm[sl >> 5], b) & b))
+            atomicAdd(&O.cnt[ORD_NMIX], 1u);   // (rare: a slot's first)
     }
 }
 
@@ -902,7 +903,7 @@ __global__ __launch_bounds__(256) void k_ord_collect_w(CtaArgs A, OrdArgs O)
 // CT_ESTABLISHED stage, k_ord_mixed): every CT_ESTABLISHED stage on one takes
 // part — plain hits outside the work bits among them, so a pass over the
 // batch (the launch's keys give the slots).  Nothing to do, and no load past
-// the counter, in a batch without deletes.
+// the counters, in a batch without deletes or without a mixed slot.
 template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_ord_collect_mix(CtaArgs A, OrdArgs O)
 {
@@ -911,7 +912,7 @@ __global__ __launch_bounds__(256) void k_ord_collect_mix(CtaArgs A, OrdArgs O)
     if (threadIdx.x == 0)
         S.n = 0;
     __syncthreads();
-    if (O.cnt[ORD_NDEL]) {
+    if (O.cnt[ORD_NDEL] && O.cnt[ORD_NMIX]) {
         for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < A.n;
              i += (uint64_t)gridDim.x * 256) {
             const uint32_t cb = A.ctb[i];
@@ -993,14 +994,12 @@ __device__ __forceinline__ bool rk_eq(const OrdArgs &O, uint32_t a, uint32_t b)
     return true;
 }
 
+// record r: participant p's lookup, or (rel) the related-entry write of
+// the creating participant p
 template <bool V6>
-__global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t np, uint32_t nrel)
+__device__ __forceinline__ void ord_record(const CtaArgs &A, const OrdArgs &O, uint32_t r,
+                                           uint32_t p, bool rel)
 {
-    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
-    if (r >= np + nrel)
-        return;
-    const bool rel = r >= np;
-    const uint32_t p = rel ? O.rel_src[r - np] : r;
     const uint32_t pw = O.part[p];
     const uint64_t i = pw >> 1;
     const int st = (int)(pw & 1);
@@ -1042,8 +1041,39 @@ __global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t
     if (w & 0x200u)
         f |= PI_RELKEY;
     O.pinfo[r] = f;
-    if (f & PI_RELKEY)
+    if (f & PI_RELKEY && r == p)   // (round 1)
         atomicAdd(&O.cnt[ORD_NRELKEY], 1u);
+}
+// round 1: one thread per participant
+template <bool V6>
+__global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t np)
+{
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r < np)
+        ord_record<V6>(A, O, r, r, false);
+}
+// round 2: only the keys with TUPLE_F_RELATED take part — the ICMP errors'
+// lookups (nrk, copies of their participants: records np..) and the related
+// entries the creates write (nrel) — no other key has that flag, so every
+// other participant keeps round 1's result
+template <bool V6>
+__global__ __launch_bounds__(256) void k_ord_keys2(CtaArgs A, OrdArgs O, uint32_t np,
+                                                   uint32_t nrk, uint32_t nrel)
+{
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= nrk + nrel)
+        return;
+    if (j < nrk)
+        ord_record<V6>(A, O, np + j, O.rel_src[np + j], false);
+    else
+        ord_record<V6>(A, O, np + j, O.rel_src[j - nrk], true);
+}
+// round 2's results of the ICMP errors' copies back to their participants
+__global__ __launch_bounds__(256) void k_ord_rk2_back(OrdArgs O, uint32_t np, uint32_t nrk)
+{
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    if (j < nrk)
+        O.nres[O.rel_src[np + j]] = O.nres[np + j];
 }
 
 // ---- resolve: per record in (key, order) order, a lookup's result is the
@@ -1087,6 +1117,11 @@ __global__ __launch_bounds__(256) void k_ord_relsrc(OrdArgs O, uint32_t np)
     const uint32_t r = block_count(&O.cnt[ORD_NREL], want);
     if (want)
         O.rel_src[r] = p;
+    // (and the ICMP errors' participants, listed after np)
+    const bool rk = p < np && (O.pinfo[p] & PI_RELKEY);
+    const uint32_t q = block_count(&O.cnt[ORD_NRK2], rk);
+    if (rk)
+        O.rel_src[np + q] = p;
 }
 
 // ---- write: the changed stages' CT bytes (result and create bit) and hit
@@ -1362,7 +1397,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         // records: up to twice as many as participants
         const uint64_t nr = 2 * np;
         const size_t kw = V6 ? 48 : 16;
-        if (B.rel_src.ensure(4 * np) || B.rk.ensure(kw * nr) ||
+        if (B.rel_src.ensure(8 * np) || B.rk.ensure(kw * nr) ||
             B.rh.ensure(8 * nr) || B.rh2.ensure(8 * nr) || B.ridx.ensure(4 * nr) ||
             B.ridx2.ensure(4 * nr) || B.pinfo.ensure(nr) || B.nres.ensure(nr))
             return -ENOMEM;
@@ -1388,7 +1423,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         O.tmp_bytes = B.tmp.bytes;
         const uint32_t npi = (uint32_t)np;
         const unsigned gp = (unsigned)((npi + 255) / 256);
-        hipLaunchKernelGGL(k_ord_keys<V6>, dim3(gp), dim3(256), 0, s, A, O, npi, 0u);
+        hipLaunchKernelGGL(k_ord_keys<V6>, dim3(gp), dim3(256), 0, s, A, O, npi);
         const uint64_t *h;
         const uint32_t *idx;
         if (int rc = sort_records<V6>(O, npi, s, &h, &idx))
@@ -1410,14 +1445,22 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
             hipLaunchKernelGGL(k_ord_relsrc, dim3(gp), dim3(256), 0, s, O, npi);
             if (!rd())
                 return -EIO;
-            const uint32_t nrel = hc[ORD_NREL];
-            if (nrel) {
-                hipLaunchKernelGGL(k_ord_keys<V6>, dim3((npi + nrel + 255) / 256), dim3(256), 0, s,
-                                   A, O, npi, nrel);
-                if (int rc = sort_records<V6>(O, npi + nrel, s, &h, &idx))
+            const uint32_t nrel = hc[ORD_NREL], nrk = hc[ORD_NRK2], n2 = nrk + nrel;
+            if (nrel) {   // (records np.. : np + n2 <= 2 np, the buffers' room)
+                hipLaunchKernelGGL(k_ord_keys2<V6>, dim3((n2 + 255) / 256), dim3(256), 0, s, A, O,
+                                   npi, nrk, nrel);
+                OrdArgs O2 = O;
+                O2.rh += npi;
+                O2.rh2 += npi;
+                O2.ridx += npi;
+                O2.ridx2 += npi;
+                if (int rc = sort_records<V6>(O2, n2, s, &h, &idx))
                     return rc;
-                hipLaunchKernelGGL(k_ord_resolve<V6>, dim3((npi + nrel + 255) / 256), dim3(256), 0,
-                                   s, O, h, idx, npi + nrel);
+                hipLaunchKernelGGL(k_ord_resolve<V6>, dim3((n2 + 255) / 256), dim3(256), 0, s, O,
+                                   h, idx, n2);
+                if (nrk)
+                    hipLaunchKernelGGL(k_ord_rk2_back, dim3((nrk + 255) / 256), dim3(256), 0, s, O,
+                                       npi, nrk);
             }
         }
     }
