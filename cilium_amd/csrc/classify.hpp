@@ -184,9 +184,10 @@ struct CtSyncRec6 {
     uint32_t last_rx, last_tx, flags, lifetime;
     uint32_t pad;
 };
-// (NFHIT: requests that are counted hits; NKX: creates with a reverse-NAT entry)
+// (NFHIT: requests that are counted hits; NKX: creates with a reverse-NAT
+// entry; NRELB: creates that may write a related entry — not TCP, k2 not one)
 enum { CTA_NREQA, CTA_NHIT, CTA_NREQB, CTA_NCX, CTA_CLAIMS, CTA_NLOG, CTA_NDEDUP, CTA_NSVC,
-       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NEWKT, CTA_NLONG, CTA_NLCH, CTA_NCNT };
+       CTA_NFHIT, CTA_NKX, CTA_NEWK, CTA_NEWKT, CTA_NLONG, CTA_NLCH, CTA_NRELB, CTA_NCNT };
 struct CtaArgs {
     DevTables T;
     // addresses: one word per header (IPv4), four (IPv6, raw network order)

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
         s_nreq = 0;
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * 256 * SCAN_U;
-    uint32_t nhit = 0, nfh = 0;
+    uint32_t nhit = 0, nfh = 0, nrb = 0;
     for (uint64_t base = (uint64_t)blockIdx.x * 256 * SCAN_U; base < A.n; base += stride) {
         // SCAN_U consecutive headers per thread: with the batch's arrays
         // 16-byte aligned (A.vec) their words in one 16-byte load per array
@@ -218,6 +218,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
                 } else if (o.kind == OP_CREATE) {
                     home[u][st] = khome(o.sa, o.da, o.z2, o.w2) & A.mask;
                     ncr++;
+                    nrb += !o.is_tcp && !o.ki_form;
                 }
             }
         }
@@ -293,6 +294,7 @@ __global__ __launch_bounds__(256) void k_cta_scan(CtaArgs A)
     block_flush(s_req, &s_nreq, &A.cnt[CTA_NREQA], A.reqA, A.req_cap);
     block_add(&A.cnt[CTA_NHIT], nhit);
     block_add(&A.cnt[CTA_NFHIT], nfh);
+    block_add(&A.cnt[CTA_NRELB], nrb);
 }
 
 // ---- the scan over the classify launch's work bits (A.sparse: A.W, the
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
         s_n = 0;
     __syncthreads();
     const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t nfh = 0;
+    uint32_t nfh = 0, nrb = 0;
     auto put = [&](uint64_t v) {
         const uint32_t q = atomicAdd(&s_n, 1u);
         if (q < SCANW_STAGE) {
@@ -378,6 +380,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
                 }
             } else if (o.kind == OP_CREATE) {
                 put(pack(A, khome(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP)));
+                nrb += !o.is_tcp && !o.ki_form;
                 if constexpr (!V6)
                     if (A.rk4)
                         A.rk4[TWO ? 2 * i + st : i] = make_uint4(o.sa, o.da, o.z2, o.w2);
@@ -413,6 +416,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_w(CtaArgs A)
         if (s_base + q < A.req_cap)
             A.reqA[s_base + q] = s_req[q];
     block_add(&A.cnt[CTA_NFHIT], nfh);
+    block_add(&A.cnt[CTA_NRELB], nrb);
 }
 
 // the hit slots of a sparse scan's batch for the eviction's protect pass
@@ -653,7 +657,7 @@ __global__ __launch_bounds__(256) void k_cta_svc(CtaArgs A, uint64_t *req, uint3
 template <bool V6>
 __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
 {
-    uint32_t nhit = 0, nfh = 0, nkx = 0;
+    uint32_t nhit = 0, nfh = 0, nkx = 0, nrb = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < A.n; base += stride) {
         const uint64_t i = base + threadIdx.x;
@@ -701,6 +705,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
             } else if (o.kind == OP_CREATE) {
                 rq[ncr++] = pack(A, khome(o.sa, o.da, o.z2, o.w2) & A.mask, ord_of(i, st, SEC_OP));
                 nkx += o.kx;
+                nrb += !o.is_tcp && !o.ki_form;
             }
         }
         if (in && ((r.cb & CFC_CT_DONE) || (int32_t)r.ver == DROP_NO_SERVICE)) {
@@ -725,6 +730,8 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
             } else if (o.kind == OP_CREATE) {
                 rq[ncr++] = pack(A, khome(o.sa, o.da, o.z2, o.w2) & A.mask,
                                  ord_of(A.n + i, 0, SEC_OP));
+                nkx += o.kx;   // (k_cta_related's bound: whatever this op writes)
+                nrb += !o.is_tcp && !o.ki_form;
             }
         }
         if (in) {
@@ -739,6 +746,7 @@ __global__ __launch_bounds__(256) void k_cta_scan_lb(CtaArgs A)
     wave_add(&A.cnt[CTA_NHIT], nhit);
     wave_add(&A.cnt[CTA_NFHIT], nfh);
     wave_add(&A.cnt[CTA_NKX], nkx);
+    wave_add(&A.cnt[CTA_NRELB], nrb);
 }
 
 // key of a request, by its write: k2 of its op (a create), the ICMP entry
@@ -2773,10 +2781,13 @@ int cta_rest_t(const CtaArgs &A, uint32_t nreqA, const uint64_t *presorted, uint
     if (!sorted && (rc = sort_keys(A, A.reqA, A.reqA2, nreqA, bits, s, &sorted, false)))
         return rc;
     // the second round's requests (a create's related and reverse-NAT
-    // entries, at most two per create) and their ops' places in the list
-    // are laid out for that bound, the unused ones all-ones (sorted last,
-    // skipped by the insert, dropped by dedup): no wait for their count
-    const uint32_t nbB = (uint32_t)std::min<uint64_t>(2ull * nreqA, A.req_cap);
+    // entries) and their ops' places in the list are laid out for the
+    // scan's bound — its creates that are not TCP and whose k2 is not a
+    // related entry, and those with a reverse-NAT entry — the unused ones
+    // all-ones (sorted last, skipped by the insert, dropped by dedup): no
+    // wait for their count
+    const uint32_t nbB = (uint32_t)std::min<uint64_t>(
+        host_cnt ? (uint64_t)host_cnt[CTA_NRELB] + host_cnt[CTA_NKX] : 2ull * nreqA, A.req_cap);
     if (nbB && (hipMemsetAsync(A.reqB, 0xFF, 8ull * nbB, s) != hipSuccess ||
                 (uint64_t)nreqA + nbB > A.cx_cap ||
                 hipMemsetAsync(A.cx + nreqA, 0xFF, 8ull * nbB, s) != hipSuccess))

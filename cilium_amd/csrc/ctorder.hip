@@ -922,8 +922,13 @@ __global__ __launch_bounds__(256) void k_ord_collect_mix(CtaArgs A, OrdArgs O)
                 if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED)
                     continue;
                 const uint32_t sl = start_slot<V6>(A, O, i, st);
-                if (sl != NONE && ((O.mixbm[sl >> 5] >> (sl & 31)) & 1))
+                if (sl != NONE && ((O.mixbm[sl >> 5] >> (sl & 31)) & 1)) {
                     part_put(S, O, (uint32_t)(i << 1) | (uint32_t)st);
+                    // (round 2's bounds: an entry with TUPLE_F_RELATED is an
+                    // ICMP error's lookup; any other may be re-created after
+                    // its delete, with a related entry)
+                    atomicAdd(&O.cnt[(*slot_w<V6>(A, sl) & 0x200u) ? ORD_RELBOUND : ORD_NUL], 1u);
+                }
             }
         }
     }
@@ -1053,26 +1058,33 @@ __global__ __launch_bounds__(256) void k_ord_keys(CtaArgs A, OrdArgs O, uint32_t
         ord_record<V6>(A, O, r, r, false);
 }
 // round 2: only the keys with TUPLE_F_RELATED take part — the ICMP errors'
-// lookups (nrk, copies of their participants: records np..) and the related
-// entries the creates write (nrel) — no other key has that flag, so every
-// other participant keeps round 1's result
+// lookups (ORD_NRK2 of them, copies of their participants: records np..)
+// and the related entries the creates write (ORD_NREL) — no other key has
+// that flag, so every other participant keeps round 1's result.  Laid out
+// for a bound known on the host (n2), the counts read here: the places past
+// them are records that sort last and resolve skips — no wait for the counts
 template <bool V6>
-__global__ __launch_bounds__(256) void k_ord_keys2(CtaArgs A, OrdArgs O, uint32_t np,
-                                                   uint32_t nrk, uint32_t nrel)
+__global__ __launch_bounds__(256) void k_ord_keys2(CtaArgs A, OrdArgs O, uint32_t np, uint32_t n2)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j >= nrk + nrel)
+    if (j >= n2)
         return;
-    if (j < nrk)
+    const uint32_t nrk = O.cnt[ORD_NRK2], nrel = O.cnt[ORD_NREL];
+    if (j < nrk) {
         ord_record<V6>(A, O, np + j, O.rel_src[np + j], false);
-    else
+    } else if (j < nrk + nrel) {
         ord_record<V6>(A, O, np + j, O.rel_src[j - nrk], true);
+    } else {
+        O.rh[np + j] = ~0ull;
+        O.ridx[np + j] = np + j;
+        O.pinfo[np + j] = PI_REL;
+    }
 }
 // round 2's results of the ICMP errors' copies back to their participants
-__global__ __launch_bounds__(256) void k_ord_rk2_back(OrdArgs O, uint32_t np, uint32_t nrk)
+__global__ __launch_bounds__(256) void k_ord_rk2_back(OrdArgs O, uint32_t np, uint32_t n2)
 {
     const uint32_t j = blockIdx.x * 256 + threadIdx.x;
-    if (j < nrk)
+    if (j < n2 && j < O.cnt[ORD_NRK2])
         O.nres[O.rel_src[np + j]] = O.nres[np + j];
 }
 
@@ -1435,33 +1447,31 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
             fprintf(stderr, "ord: resolve %u records, %u fingerprint-collision steps\n", npi,
                     hc[ORD_COLL]);
         }
-        // round 2 only with an ICMP error among the participants: with the
-        // launch's tags and no deleted slot, mark and collect counted them
-        const bool relkeys = !O.tagged || O.ndel || hc[ORD_RELBOUND];
-        if (relkeys && !rd())
-            return -EIO;
-        if (relkeys && hc[ORD_NRELKEY]) {
-            // round 2: the related entries of the creates round 1 resolved
+        // round 2 only with an ICMP error among the participants (the
+        // sparse passes counted a bound of them, and of the creates that may
+        // write a related entry; the dense passes' bound is every participant:
+        // an untagged or a mixed stage is not counted there)
+        const bool relkeys = !done ? (!O.tagged || O.ndel || hc[ORD_RELBOUND])
+                                   : hc[ORD_RELBOUND] != 0;
+        if (relkeys) {
+            const uint32_t n2 = done ? (uint32_t)std::min<uint64_t>(
+                                           np, (uint64_t)hc[ORD_RELBOUND] + hc[ORD_NUL])
+                                     : npi;
+            // (records np.. : np + n2 <= 2 np, the buffers' room)
             hipLaunchKernelGGL(k_ord_relsrc, dim3(gp), dim3(256), 0, s, O, npi);
-            if (!rd())
-                return -EIO;
-            const uint32_t nrel = hc[ORD_NREL], nrk = hc[ORD_NRK2], n2 = nrk + nrel;
-            if (nrel) {   // (records np.. : np + n2 <= 2 np, the buffers' room)
-                hipLaunchKernelGGL(k_ord_keys2<V6>, dim3((n2 + 255) / 256), dim3(256), 0, s, A, O,
-                                   npi, nrk, nrel);
-                OrdArgs O2 = O;
-                O2.rh += npi;
-                O2.rh2 += npi;
-                O2.ridx += npi;
-                O2.ridx2 += npi;
-                if (int rc = sort_records<V6>(O2, n2, s, &h, &idx))
-                    return rc;
-                hipLaunchKernelGGL(k_ord_resolve<V6>, dim3((n2 + 255) / 256), dim3(256), 0, s, O,
-                                   h, idx, n2);
-                if (nrk)
-                    hipLaunchKernelGGL(k_ord_rk2_back, dim3((nrk + 255) / 256), dim3(256), 0, s, O,
-                                       npi, nrk);
-            }
+            hipLaunchKernelGGL(k_ord_keys2<V6>, dim3((n2 + 255) / 256), dim3(256), 0, s, A, O,
+                               npi, n2);
+            OrdArgs O2 = O;
+            O2.rh += npi;
+            O2.rh2 += npi;
+            O2.ridx += npi;
+            O2.ridx2 += npi;
+            if (int rc = sort_records<V6>(O2, n2, s, &h, &idx))
+                return rc;
+            hipLaunchKernelGGL(k_ord_resolve<V6>, dim3((n2 + 255) / 256), dim3(256), 0, s, O, h,
+                               idx, n2);
+            hipLaunchKernelGGL(k_ord_rk2_back, dim3((n2 + 255) / 256), dim3(256), 0, s, O, npi,
+                               n2);
         }
     }
     // (before k_ord_write: the launch's bytes of the deleting stages)
