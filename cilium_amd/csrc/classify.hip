@@ -1074,17 +1074,19 @@ __global__ __launch_bounds__(BLOCK) void k_ct_count(const uint32_t *ct_idx,
 //   F k_acc_reduce one workgroup per fine bucket (CTP_BUCKET keys): gathers
 //                  its run of every chunk of its coarse region, LDS sums per
 //                  key, then its counters, which no other workgroup touches
-// Records: key (26 bits) << 38 | kind << 37 | payload; kind 0: packets (16)
-// << 21 | bytes (21) of an LDS entry; kind 1: one << 25 | hit flags (9) << 16
+// Records: key (27 bits) << 37 | kind << 36 | payload; kind 0: packets (16)
+// << 20 | bytes (20) of an LDS entry; kind 1: one << 25 | hit flags (9) << 16
 // | low (16): one = 1, a single packet of length low (the overflow), else an
-// LDS entry's high part (bytes >> 21, which can pass 0) and its flags.
+// LDS entry's high part (bytes >> 20, which can pass 0) and its flags.
 // Hit flags (acc_flags): the TCP flags, and 1 << 8 for a TCP packet without
 // the close bit — per key (slot, direction) the plain-hit summary the device
 // CT apply needs (k_acc_reduce writes it into DevTables.ct_sum).
 constexpr uint32_t CTP_BUCKET_BITS = 12, CTP_BUCKET = 1u << CTP_BUCKET_BITS;
-constexpr uint32_t CTP_MAX_BUCKETS = 16384;    // keys < 2^26 (32M CT slots)
+constexpr uint32_t CTP_MAX_BUCKETS = 32768;    // keys < 2^27 (64M CT slots)
 constexpr uint32_t ACC_FINE_BITS = 7, ACC_FINE = 1u << ACC_FINE_BITS;
-constexpr uint32_t ACC_MAX_COARSE = CTP_MAX_BUCKETS / ACC_FINE;      // 128
+constexpr uint32_t ACC_MAX_COARSE = CTP_MAX_BUCKETS / ACC_FINE;      // 256
+constexpr int ACC_KEY_SHIFT = 37, ACC_KIND_BIT = 36, ACC_BY_BITS = 20;
+constexpr uint32_t ACC_BY_MASK = (1u << ACC_BY_BITS) - 1;
 constexpr uint32_t ACC_CHUNK_BITS = 14, ACC_CHUNK = 1u << ACC_CHUNK_BITS;
 constexpr uint32_t ACC_PER_THREAD = ACC_CHUNK / BLOCK;                // 16
 // records per slice: <= COUNT_PER_BLOCK overflow packets, <= CT_LDS_SLOTS
@@ -1093,8 +1095,9 @@ constexpr uint32_t ACC_SLICE_CHUNKS = 5;
 constexpr uint32_t ACC_RCAP = ACC_SLICE_CHUNKS * ACC_CHUNK;
 static_assert(COUNT_PER_BLOCK + 2 * CT_LDS_SLOTS <= ACC_RCAP, "slice records");
 static_assert(CTP_BUCKET % BLOCK == 0, "reduce flush");
-constexpr int ACC_COARSE_SHIFT = 38 + CTP_BUCKET_BITS + ACC_FINE_BITS;   // 57
-constexpr int ACC_BUCKET_SHIFT = 38 + CTP_BUCKET_BITS;                   // 50
+constexpr int ACC_COARSE_SHIFT = ACC_KEY_SHIFT + CTP_BUCKET_BITS + ACC_FINE_BITS;   // 56
+constexpr int ACC_BUCKET_SHIFT = ACC_KEY_SHIFT + CTP_BUCKET_BITS;                   // 49
+static_assert(ACC_COARSE_SHIFT + 8 == 64, "coarse bucket: the key's top 8 bits");
 constexpr uint32_t ACC_AGG_LDS =
     CT_LDS_SLOTS * 16 + ACC_SLICE_CHUNKS * ACC_MAX_COARSE * 4 + 16;
 constexpr uint32_t ACC_SORT_LDS = ACC_CHUNK * 8 + 3 * ACC_MAX_COARSE * 4 + 16;
@@ -1115,12 +1118,13 @@ uint64_t acc_slice(uint64_t n)
 
 __device__ __forceinline__ uint64_t acc_rec(uint32_t k, uint32_t pk, uint32_t by)
 {
-    return (uint64_t)k << 38 | (uint64_t)pk << 21 | by;
+    return (uint64_t)k << ACC_KEY_SHIFT | (uint64_t)pk << ACC_BY_BITS | by;
 }
 // kind 1: a single packet (one) or an LDS entry's high bytes, with flags
 __device__ __forceinline__ uint64_t acc_rec1(uint32_t k, bool one, uint32_t fl, uint32_t low)
 {
-    return (uint64_t)k << 38 | 1ull << 37 | (one ? 1ull << 25 : 0ull) | (uint64_t)fl << 16 | low;
+    return (uint64_t)k << ACC_KEY_SHIFT | 1ull << ACC_KIND_BIT | (one ? 1ull << 25 : 0ull) |
+           (uint64_t)fl << 16 | low;
 }
 // a header's hit flags (sum_bits in ctops.hpp, per direction)
 __device__ __forceinline__ uint32_t acc_flags(uint32_t meta, uint32_t tf)
@@ -1261,11 +1265,11 @@ __global__ __launch_bounds__(BLOCK) void k_acc_agg(const uint32_t *ct_idx,
         const uint32_t by = (uint32_t)v, fl = fls[j];
         const uint32_t r = wave_append(nrec, k != NONE);
         if (k != NONE)
-            put(r, acc_rec(k, (uint32_t)(v >> 32), by & 0x1FFFFFu));
-        const bool hi = k != NONE && (by >= (1u << 21) || fl);
+            put(r, acc_rec(k, (uint32_t)(v >> 32), by & ACC_BY_MASK));
+        const bool hi = k != NONE && (by > ACC_BY_MASK || fl);
         const uint32_t r2 = wave_append(nrec, hi);
         if (hi)
-            put(r2, acc_rec1(k, false, fl, by >> 21));
+            put(r2, acc_rec1(k, false, fl, by >> ACC_BY_BITS));
     }
     __syncthreads();
     const uint32_t nch = nv * ACC_SLICE_CHUNKS;
@@ -1296,21 +1300,29 @@ __device__ __forceinline__ void acc_local_sort(const uint64_t (&r)[ACC_PER_THREA
             rank[i] = atomicAdd(&cnt[(uint32_t)(r[i] >> shift) & mask], 1u);
     }
     __syncthreads();
-    if (threadIdx.x < 64) {   // exclusive scan of <= 128 counts by one wave
+    static_assert(ACC_MAX_COARSE <= 256, "one wave scans four counts per lane");
+    if (threadIdx.x < 64) {   // exclusive scan of <= 256 counts by one wave
         const uint32_t l = threadIdx.x;
-        const uint32_t a = 2 * l < nd ? cnt[2 * l] : 0u, b = 2 * l + 1 < nd ? cnt[2 * l + 1] : 0u;
-        uint32_t x = a + b;
+        uint32_t v[4], x = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            v[q] = 4 * l + q < nd ? cnt[4 * l + q] : 0u;
+            x += v[q];
+        }
+        const uint32_t own = x;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(x, d, 64);
             if (l >= (uint32_t)d)
                 x += y;
         }
-        const uint32_t e = x - a - b;
-        if (2 * l < nd)
-            base[2 * l] = e;
-        if (2 * l + 1 < nd)
-            base[2 * l + 1] = e + a;
+        uint32_t e = x - own;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (4 * l + q < nd)
+                base[4 * l + q] = e;
+            e += v[q];
+        }
         if (l == 63)
             base[nd] = x;
     }
@@ -1368,31 +1380,33 @@ __global__ __launch_bounds__(64) void k_acc_plan(const uint32_t *off, uint32_t n
 {
     const uint32_t l = threadIdx.x;
     const uint32_t total = off[(uint64_t)nco * nch];
-    uint32_t nc[2], a[2];
+    uint32_t nc[4], a[4], own = 0;
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t c = 2 * l + j;
+    for (int j = 0; j < 4; j++) {   // (four coarse buckets per lane: nco <= 256)
+        const uint32_t c = 4 * l + j;
         a[j] = c < nco ? off[(uint64_t)c * nch] : total;
         const uint32_t b = c + 1 < nco ? off[(uint64_t)(c + 1) * nch] : total;
         nc[j] = c < nco ? (b - a[j] + ACC_CHUNK - 1) >> ACC_CHUNK_BITS : 0u;
+        own += nc[j];
     }
-    uint32_t x = nc[0] + nc[1];
+    uint32_t x = own;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(x, d, 64);
         if (l >= (uint32_t)d)
             x += y;
     }
-    const uint32_t e = x - nc[0] - nc[1];
+    uint32_t e = x - own;
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint32_t c = 2 * l + j;
+    for (int j = 0; j < 4; j++) {
+        const uint32_t c = 4 * l + j;
         if (c < nco) {
             plan[c] = a[j];
-            plan[nco + 1 + c] = j ? e + nc[0] : e;
+            plan[nco + 1 + c] = e;
         }
+        e += nc[j];
     }
-    if (l == 63) {   // the ends (nco may be 128: no lane's own bucket)
+    if (l == 63) {   // the ends (nco may be 256: no lane's own bucket)
         plan[nco] = total;
         plan[2 * nco + 1] = x;
     }
@@ -1472,20 +1486,20 @@ __global__ __launch_bounds__(BLOCK) void k_acc_reduce(const uint64_t *recs, cons
         for (uint32_t r = r0 + t; r < r1; r += 128) {
             const uint64_t v = nv;
             nv = r + 128 < r1 ? ld_nt(recs + r + 128) : 0ull;
-            const uint32_t j = (uint32_t)(v >> 38) & (CTP_BUCKET - 1);
-            if ((v >> 37) & 1) {
+            const uint32_t j = (uint32_t)(v >> ACC_KEY_SHIFT) & (CTP_BUCKET - 1);
+            if ((v >> ACC_KIND_BIT) & 1) {
                 const uint32_t low = (uint32_t)v & 0xFFFFu, f = (uint32_t)(v >> 16) & 0x1FFu;
                 if ((v >> 25) & 1) {   // a single packet
                     atomicAdd(&pk[j], 1u);
                     atomicAdd(&by[j], (unsigned long long)low);
                 } else {
-                    atomicAdd(&by[j], (unsigned long long)low << 21);
+                    atomicAdd(&by[j], (unsigned long long)low << ACC_BY_BITS);
                 }
                 if (f && (fl[j] & f) != f)
                     atomicOr(&fl[j], f);
             } else {
-                atomicAdd(&pk[j], (uint32_t)(v >> 21) & 0xFFFFu);
-                atomicAdd(&by[j], v & 0x1FFFFFull);
+                atomicAdd(&pk[j], (uint32_t)(v >> ACC_BY_BITS) & 0xFFFFu);
+                atomicAdd(&by[j], v & ACC_BY_MASK);
             }
         }
     }

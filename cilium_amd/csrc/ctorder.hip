@@ -939,36 +939,49 @@ __global__ __launch_bounds__(256) void k_ord_collect_mix(CtaArgs A, OrdArgs O)
 // the entry gone (CT_NEW, no create: they are dropped).  Runs before
 // k_ord_write (its stages' bytes are the launch's).
 template <bool V6, bool TWO>
-__global__ __launch_bounds__(256) void k_ord_deltail(CtaArgs A, OrdArgs O)
+__device__ __forceinline__ bool deltail_one(const CtaArgs &A, const OrdArgs &O, uint64_t i)
 {
     constexpr int NST = TWO ? 2 : 1;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     bool chg = false;
-    if (i < A.n) {
-        const uint32_t cb = A.ctb[i];
-        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    const uint32_t cb = A.ctb[i];
+    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
 #pragma unroll
-        for (int st = 0; st < NST; st++) {
-            const uint32_t cs = (cb >> (4 * st)) & 0xF;
-            if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
-                !(st == last && A.ver[i] == DROP_POLICY))
-                continue;
-            const uint32_t sl = start_slot<V6>(A, O, i, st);
-            if (sl == NONE || ((O.mixbm[sl >> 5] >> (sl & 31)) & 1) ||
-                O.dfirst[sl] == ((uint32_t)(i << 1) | (uint32_t)st))
-                continue;
-            const uintptr_t ba = reinterpret_cast<uintptr_t>(O.ctb + i);
-            uint32_t *wp = reinterpret_cast<uint32_t *>(ba & ~(uintptr_t)3);
-            const uint32_t bs = 8 * (uint32_t)(ba & 3) + 4 * st;
-            atomicAnd(wp, ~(0xFu << bs));
-            atomicOr(wp, ((uint32_t)CT_NEW | CFC_CT_DONE) << bs);
-            uint32_t *ck = st ? O.ck2 : O.ck1;
-            if (ck)
-                ck[i] = NONE;
-            chg = true;
-        }
+    for (int st = 0; st < NST; st++) {
+        const uint32_t cs = (cb >> (4 * st)) & 0xF;
+        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
+            !(st == last && A.ver[i] == DROP_POLICY))
+            continue;
+        const uint32_t sl = start_slot<V6>(A, O, i, st);
+        if (sl == NONE || ((O.mixbm[sl >> 5] >> (sl & 31)) & 1) ||
+            O.dfirst[sl] == ((uint32_t)(i << 1) | (uint32_t)st))
+            continue;
+        const uintptr_t ba = reinterpret_cast<uintptr_t>(O.ctb + i);
+        uint32_t *wp = reinterpret_cast<uint32_t *>(ba & ~(uintptr_t)3);
+        const uint32_t bs = 8 * (uint32_t)(ba & 3) + 4 * st;
+        atomicAnd(wp, ~(0xFu << bs));
+        atomicOr(wp, ((uint32_t)CT_NEW | CFC_CT_DONE) << bs);
+        uint32_t *ck = st ? O.ck2 : O.ck1;
+        if (ck)
+            ck[i] = NONE;
+        chg = true;
     }
-    block_add(&O.cnt[ORD_CHANGED], chg ? 1u : 0u);
+    return chg;
+}
+// (every deleting stage is a work bit: the sparse passes' list holds them)
+template <bool V6, bool TWO>
+__global__ __launch_bounds__(256) void k_ord_deltail(CtaArgs A, OrdArgs O)
+{
+    uint32_t nchg = 0;
+    if (O.sparse && O.wl) {
+        const uint32_t nl = O.cnt[ORD_NWL];
+        for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < nl; x += gridDim.x * 256)
+            nchg += deltail_one<V6, TWO>(A, O, O.wl[x]) ? 1u : 0u;
+    } else {
+        for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < A.n;
+             i += (uint64_t)gridDim.x * 256)
+            nchg += deltail_one<V6, TWO>(A, O, i) ? 1u : 0u;
+    }
+    block_add(&O.cnt[ORD_CHANGED], nchg);
 }
 
 // ---- keys: one thread per record r.  r < np: participant r; else the
@@ -1476,7 +1489,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
     }
     // (before k_ord_write: the launch's bytes of the deleting stages)
     if (O.ndel)
-        ORD_LAUNCH(k_ord_deltail, gn, A, O);
+        ORD_LAUNCH(k_ord_deltail, done ? gw : gn, A, O);
     if (np)
         hipLaunchKernelGGL(k_ord_write, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, s, A, O,
                            (uint32_t)np);
