@@ -339,22 +339,24 @@ template <bool V6, bool TWO>
 __global__ __launch_bounds__(256) void k_ord_mixed(CtaArgs A, OrdArgs O)
 {
     constexpr int NST = TWO ? 2 : 1;
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= A.n || !O.cnt[ORD_NDEL])   // (the sparse passes launch it before their count)
+    if (!O.cnt[ORD_NDEL])   // (the sparse passes launch it before their count)
         return;
-    const uint32_t cb = A.ctb[i];
-    const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < A.n;
+         i += (uint64_t)gridDim.x * 256) {
+        const uint32_t cb = A.ctb[i];
+        const int last = (cb & (CFC_CT_DONE << 4)) ? 1 : 0;
 #pragma unroll
-    for (int st = 0; st < NST; st++) {
-        const uint32_t cs = (cb >> (4 * st)) & 0xF;
-        if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
-            (st == last && A.ver[i] == DROP_POLICY))
-            continue;
-        const uint32_t sl = start_slot<V6>(A, O, i, st);
-        const uint32_t b = 1u << (sl & 31);
-        if (sl != NONE && (O.delbm[sl >> 5] & b) && !(O.mixbm[sl >> 5] & b) &&
-            !(atomicOr(&O.mixbm[sl >> 5], b) & b))
-            atomicAdd(&O.cnt[ORD_NMIX], 1u);   // (rare: a slot's first)
+        for (int st = 0; st < NST; st++) {
+            const uint32_t cs = (cb >> (4 * st)) & 0xF;
+            if (!(cs & CFC_CT_DONE) || (cs & CFC_CT_RES_MASK) != CT_ESTABLISHED ||
+                (st == last && A.ver[i] == DROP_POLICY))
+                continue;
+            const uint32_t sl = start_slot<V6>(A, O, i, st);
+            const uint32_t b = 1u << (sl & 31);
+            if (sl != NONE && (O.delbm[sl >> 5] & b) && !(O.mixbm[sl >> 5] & b) &&
+                !(atomicOr(&O.mixbm[sl >> 5], b) & b))
+                atomicAdd(&O.cnt[ORD_NMIX], 1u);   // (rare: a slot's first)
+        }
     }
 }
 
@@ -1337,7 +1339,7 @@ int ord_resolve_t(const CtaArgs &A, OrdArgs &O, OrdBufs &B, uint32_t *changed, h
         ORD_LAUNCH(k_ord_collect_w, gw, A, O);
         // a batch that deletes: its mixed slots and their stages (two passes
         // over the batch, each gone at its first load without a delete)
-        ORD_LAUNCH(k_ord_mixed, gn, A, O);
+        ORD_LAUNCH(k_ord_mixed, gp, A, O);
         ORD_LAUNCH(k_ord_collect_mix, gw, A, O);
         if (!rd())
             return -EIO;
