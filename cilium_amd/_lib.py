@@ -114,7 +114,8 @@ class Stats(ctypes.Structure):
                 ("nat_hops", ctypes.c_uint64),
                 ("ct_evicted", ctypes.c_uint64),
                 ("svc_ordered", ctypes.c_uint64),
-                ("ct_apply_sparse", ctypes.c_uint64)]
+                ("ct_apply_sparse", ctypes.c_uint64),
+                ("ct_self_segments", ctypes.c_uint64)]
 
 
 class NodeConfig(ctypes.Structure):

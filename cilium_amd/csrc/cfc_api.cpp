@@ -228,7 +228,6 @@ struct cfc_ctx {
     // per-header CT_SERVICE entry words (zero between launches), count
     DevBuf svo_keys, svo_keys2, svo, svo_cnt, svo_tmp;
     uint64_t n_apply_sparse = 0;   // device applies that took the work list
-    uint64_t n_svo = 0;   // headers handed an entry an earlier header left
     bool nat46_seen = false, hop_nat46 = false;
     uint64_t n_nat_hops = 0;
     // eviction at a CT map's capacity (ct_evict; CFC_OPT_CT_EVICT)
@@ -236,6 +235,18 @@ struct cfc_ctx {
     DevBuf evict_bm, evict_maps, evict_rel;
     uint64_t n_evicted = 0;
     uint64_t n_ct_grow = 0;   // device-side CT table growths (ct_grow)
+    // traffic to itself (selfseg.hip, self_cuts): the candidate addresses,
+    // the listed headers and their count; segments run before the last; the
+    // last segment of the last cut batch, which its cfc_ct_apply folds
+    DevBuf self_addr, self_rows, self_cnt;
+    uint64_t n_self_segs = 0;
+    struct {
+        bool valid = false;
+        const void *ct = nullptr, *saddr = nullptr;
+        uint64_t n = 0, off = 0;
+        int mode = 0, family = 0;
+        uint16_t ep = 0;
+    } seg;
     // the IPv6 table's device applies: creates the host lacks, inserts
     // since the last sync, CtLog6 entries
     uint64_t cta_claims6 = 0, cta_ins6 = 0, log6_used = 0;
@@ -2139,19 +2150,9 @@ int nat_hop(cfc_ctx *c, const DevTables &T, const EgressArgs &ea, const Hdr &in,
 
 // cfc_classify_v4 / _v6: validation, auto-commit, workspace, launch
 template <class Hdr, class Launch>
-int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
-             uint16_t ep_lxc, void *stream, Launch launch)
+int classify_one(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
+                 uint16_t ep_lxc, void *stream, Launch launch)
 {
-    if (!c || !in || !out || !out->verdict || !out->identity)
-        return -EINVAL;
-    if (in->n && (!in->saddr || !in->daddr || !in->ports || !in->meta))
-        return -EINVAL;
-    if (mode < CFC_MODE_INGRESS || mode > CFC_MODE_FULL)
-        return -EINVAL;
-    std::lock_guard<std::recursive_mutex> g(c->mu);
-    if (c->device == CFC_DEVICE_NONE)
-        return -ENODEV;
-    (void)hipSetDevice(c->device);
     hipStream_t s = (hipStream_t)stream;
     int rc = commit_locked(c, s);
     if (rc)
@@ -2245,7 +2246,7 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
                 c->svo.zeros(4 * n, s))
                 return -ENOMEM;
         }
-        if (c->svo_cnt.ensure(16))
+        if (!c->svo_cnt.p && c->svo_cnt.zeros(16, s))   // (words 2-3: svc_ordered)
             return -ENOMEM;
         SvoArgs sa{(const uint32_t *)in->saddr, (const uint32_t *)in->daddr, in->ports, in->meta,
                    in->hash, n, ep_lxc, ea.ct_owner,
@@ -2258,7 +2259,6 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         }
         if (nsvo)
             ea.svo = (const uint32_t *)c->svo.p;
-        c->n_svo += nsvo;
     }
     // plain-hit summaries: only of this launch (a batch with NAT hops keeps
     // none: its apply takes the scan's)
@@ -2329,6 +2329,274 @@ int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
         L.sum = sums;
         L.wl = ea.wbits && sums;
     }
+    return 0;
+}
+
+// a batch's headers [a, a + m) as a batch of their own (same arrays)
+cfc_hdr_v4 sub_batch(const cfc_hdr_v4 &h, uint64_t a, uint64_t m)
+{
+    cfc_hdr_v4 r = h;
+    r.saddr += a;
+    r.daddr += a;
+    r.ports += a;
+    r.meta += a;
+    if (r.mark)
+        r.mark += a;
+    if (r.tcp_flags)
+        r.tcp_flags += a;
+    if (r.hash)
+        r.hash += a;
+    r.n = m;
+    return r;
+}
+
+cfc_hdr_v6 sub_batch(const cfc_hdr_v6 &h, uint64_t a, uint64_t m)
+{
+    cfc_hdr_v6 r = h;
+    r.saddr += 16 * a;
+    r.daddr += 16 * a;
+    r.ports += a;
+    r.meta += a;
+    if (r.mark)
+        r.mark += a;
+    if (r.tcp_flags)
+        r.tcp_flags += a;
+    if (r.hash)
+        r.hash += a;
+    r.n = m;
+    return r;
+}
+
+cfc_out sub_out(const cfc_out &o, uint64_t a, bool v6)
+{
+    cfc_out r = o;
+    r.verdict += a;
+    r.identity += a;
+    if (r.action)
+        r.action += a;
+    if (r.ct)
+        r.ct += a;
+    if (r.notify)
+        r.notify += a;
+    const uint64_t pw = v6 ? 4 * a : a;   // (IPv6: 16-byte address rows)
+    if (r.pkt_saddr)
+        r.pkt_saddr += pw;
+    if (r.pkt_daddr)
+        r.pkt_daddr += pw;
+    if (r.pkt_ports)
+        r.pkt_ports += a;
+    return r;
+}
+
+template <class Hdr>
+int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode,
+             uint16_t ep_lxc, void *stream);
+
+// Traffic to itself (selfseg.hip): where an egress batch of `ep` must be
+// cut so that no header's k1 is a key an earlier header of its own segment
+// may have written.  Such keys have both addresses the sender's own
+// (conntrack.h:487-494) or are a looped-back service flow's TUPLE_F_IN entry
+// (:725-748), so only headers to one of these destinations take part: the
+// endpoint's own addresses (cilium_lxc), and with services IPV4_LOOPBACK and
+// the services that have the endpoint as a backend (lb4_local's loopback;
+// an IPv6 service simply delivers back to it).  Header j is cut from an
+// earlier listed header i of its segment when i's writes may hold one of
+// j's lookup keys: any pair that involves a service or IPV4_LOOPBACK (the
+// translated ports are not in the header); an ICMP error (its RELATED keys
+// are every create's ICMP entry); an ICMP echo / other ICMP after an ICMP
+// one; TCP / UDP after the same protocol on the same two ports, in either
+// order (the answer finds the opening packet's entry).  cuts: segment
+// starts after 0, ascending (empty: one launch).  One host wait, on egress
+// batches with CT outputs only.
+template <class Hdr>
+int self_cuts(cfc_ctx *c, const Hdr &in, const cfc_out &out, int mode, uint16_t ep,
+              hipStream_t s, std::vector<uint64_t> *cuts)
+{
+    constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
+    cuts->clear();
+    if (mode != CFC_MODE_EGRESS || !out.ct || in.n < 2 || getenv("CFC_NO_SELF_CUTS"))
+        return 0;
+    int rc = commit_locked(c, s);
+    if (rc)
+        return rc;
+    const Epoch &E = *c->epoch;
+    if (V6 ? !E.T.ct6 : !E.T.ct4)
+        return 0;
+    const uint32_t al = V6 ? 16 : 4;
+    std::vector<uint8_t> own;   // the endpoint's addresses, then the loopback ones
+    auto add = [&](const uint8_t *a) {
+        for (size_t o = 0; o < own.size(); o += al)
+            if (!memcmp(&own[o], a, al))
+                return;
+        own.insert(own.end(), a, a + al);
+    };
+    for (auto &kv : c->maps) {
+        if (kv.second->role != ROLE_LXC)
+            continue;
+        for (auto &e : kv.second->kv) {
+            const uint8_t *k = (const uint8_t *)e.first.data();
+            const uint8_t *v = (const uint8_t *)e.second.val.data();
+            if (e.first.size() < 20 || e.second.val.size() < 12 || k[16] != (V6 ? 2 : 1))
+                continue;
+            uint16_t id;
+            uint32_t fl;
+            memcpy(&id, v + 6, 2);
+            memcpy(&fl, v + 8, 4);
+            if (id == ep && !(fl & 1))   // (not the host's own entry)
+                add(k);
+        }
+    }
+    const uint32_t n_own = (uint32_t)(own.size() / al);
+    if (!n_own)
+        return 0;
+    // services with the endpoint as a backend (a slave slot whose target is
+    // one of its addresses), and IPV4_LOOPBACK
+    for (auto &kv : c->maps) {
+        if (kv.second->role != (V6 ? ROLE_LB6_SVC : ROLE_LB4_SVC))
+            continue;
+        for (auto &e : kv.second->kv) {
+            const uint8_t *k = (const uint8_t *)e.first.data();
+            const uint8_t *v = (const uint8_t *)e.second.val.data();
+            if (e.first.size() < al + 4 || e.second.val.size() < al)
+                continue;
+            uint16_t slave;
+            memcpy(&slave, k + al + 2, 2);
+            if (!slave)
+                continue;
+            for (uint32_t j = 0; j < n_own; j++)
+                if (!memcmp(v, &own[j * al], al)) {
+                    add(k);
+                    break;
+                }
+        }
+        if (!V6) {
+            const uint32_t lo = IPV4_LOOPBACK;
+            add((const uint8_t *)&lo);
+        }
+    }
+    const uint32_t na = (uint32_t)(own.size() / al);
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(in.n, 1u << 24);
+    if (c->self_addr.bytes < own.size() || c->self_rows.bytes < 16ull * cap) {
+        (void)hipStreamSynchronize(s);
+        if (c->self_addr.ensure(own.size()) || c->self_rows.ensure(16ull * cap))
+            return -ENOMEM;
+    }
+    if (c->self_cnt.ensure(16))
+        return -ENOMEM;
+    // (the previous launch may still read these: order after it)
+    if (c->ctr_pending && c->last_stream != s)
+        (void)hipStreamWaitEvent(s, c->last_done, 0);
+    if (hipMemcpyAsync(c->self_addr.p, own.data(), own.size(), hipMemcpyHostToDevice, s) !=
+            hipSuccess ||
+        hipMemsetAsync(c->self_cnt.p, 0, 4, s) != hipSuccess)
+        return -EIO;
+    SelfArgs A{(const void *)in.daddr, in.ports, in.meta, in.n, (const uint32_t *)c->self_addr.p,
+               na, (uint4 *)c->self_rows.p, (uint32_t *)c->self_cnt.p, cap};
+    if ((rc = self_mark(A, V6, s)))
+        return rc;
+    uint32_t m = 0;
+    if (hipMemcpyAsync(&m, c->self_cnt.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    if (m < 2)
+        return 0;
+    if (m > cap)
+        return -E2BIG;
+    std::vector<uint4> rows(m);
+    if (hipMemcpyAsync(rows.data(), c->self_rows.p, 16ull * m, hipMemcpyDeviceToHost, s) !=
+            hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -EIO;
+    std::sort(rows.begin(), rows.end(), [](const uint4 &a, const uint4 &b) { return a.x < b.x; });
+    const uint32_t icmp = V6 ? 58 : 1;
+    std::set<uint64_t> l4;           // (proto, unordered ports) in the segment
+    bool any = false, svc = false, icmp_plain = false;
+    for (const uint4 &r : rows) {
+        const uint32_t proto = r.z & 0xFF, pt = r.y;
+        const bool lo = r.w >= n_own;   // a service or IPV4_LOOPBACK
+        const uint32_t type = pt & 0xFF;
+        const bool is_icmp = proto == icmp;
+        const bool err = is_icmp && (V6 ? (type >= 1 && type <= 4)
+                                        : (type == 3 || type == 11 || type == 12));
+        const uint64_t a = pt & 0xFFFF, b = pt >> 16;
+        const uint64_t key = (uint64_t)proto << 32 | std::min(a, b) << 16 | std::max(a, b);
+        const bool l4p = proto == 6 || proto == 17;
+        bool dep = false;
+        if (any) {
+            if (lo || svc || err)
+                dep = true;
+            else if (is_icmp)
+                dep = icmp_plain;
+            else if (l4p)
+                dep = l4.count(key) != 0;
+        }
+        if (dep) {
+            cuts->push_back(r.x);
+            l4.clear();
+            svc = icmp_plain = false;
+        }
+        any = true;
+        svc |= lo;
+        icmp_plain |= is_icmp && !err;
+        if (l4p)
+            l4.insert(key);
+    }
+    return 0;
+}
+
+template <class Hdr, class Launch>
+int classify(cfc_ctx *c, const Hdr *in, const cfc_out *out, int mode,
+             uint16_t ep_lxc, void *stream, Launch launch)
+{
+    if (!c || !in || !out || !out->verdict || !out->identity)
+        return -EINVAL;
+    if (in->n && (!in->saddr || !in->daddr || !in->ports || !in->meta))
+        return -EINVAL;
+    if (mode < CFC_MODE_INGRESS || mode > CFC_MODE_FULL)
+        return -EINVAL;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->device == CFC_DEVICE_NONE)
+        return -ENODEV;
+    (void)hipSetDevice(c->device);
+    hipStream_t s = (hipStream_t)stream;
+    constexpr bool V6 = std::is_same<Hdr, cfc_hdr_v6>::value;
+    c->seg.valid = false;
+    std::vector<uint64_t> cuts;
+    int rc = self_cuts(c, *in, *out, mode, ep_lxc, s, &cuts);
+    if (rc)
+        return rc;
+    if (cuts.empty())
+        return classify_one(c, in, out, mode, ep_lxc, stream, launch);
+    // the segments in order: each classified against the maps the ones
+    // before it left, and folded into them before the next (the caller's
+    // cfc_ct_apply folds the last)
+    cuts.push_back(in->n);
+    uint64_t a = 0;
+    for (size_t k = 0; k < cuts.size(); k++) {
+        const uint64_t b = cuts[k];
+        const Hdr si = sub_batch(*in, a, b - a);
+        const cfc_out so = sub_out(*out, a, V6);
+        if ((rc = classify_one(c, &si, &so, mode, ep_lxc, stream, launch)))
+            return rc;
+        if (k + 1 < cuts.size()) {
+            // (cfc_stats counts the caller's applies: these are the segments')
+            const uint32_t nd = c->n_apply_dev, nh = c->n_apply_host;
+            if ((rc = ct_apply(c, V6 ? 6 : 4, &si, &so, mode, ep_lxc, stream)))
+                return rc;
+            c->n_apply_dev = nd;
+            c->n_apply_host = nh;
+            c->n_self_segs++;
+        }
+        a = b;
+    }
+    c->seg.valid = true;
+    c->seg.ct = out->ct;
+    c->seg.saddr = in->saddr;
+    c->seg.n = in->n;
+    c->seg.off = cuts[cuts.size() - 2];
+    c->seg.mode = mode;
+    c->seg.family = V6 ? 6 : 4;
+    c->seg.ep = ep_lxc;
     return 0;
 }
 
@@ -2599,7 +2867,13 @@ int cfc_get_stats(cfc_ctx *c, cfc_stats *st)
     st->ct_order_changed = c->n_ord_changed;
     st->nat_hops = c->n_nat_hops;
     st->ct_evicted = c->n_evicted;
-    st->svc_ordered = c->n_svo;
+    // (the replay's running total of entry words it handed on)
+    uint64_t svo_total = 0;
+    if (c->svo_cnt.p && c->device != CFC_DEVICE_NONE &&
+        hipMemcpy(&svo_total, (char *)c->svo_cnt.p + 8, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        svo_total = 0;
+    st->svc_ordered = svo_total;
+    st->ct_self_segments = c->n_self_segs;
     st->ct_apply_sparse = c->n_apply_sparse;
     st->ct_grown = (uint32_t)c->n_ct_grow;
     st->ct_slots = (c->epoch && c->epoch->ct) ? (uint32_t)(c->epoch->ct->slots4 + c->epoch->ct->slots6)
@@ -4208,6 +4482,17 @@ int ct_apply(cfc_ctx *c, int family, const Hdr *in, const cfc_out *out, int mode
     if (!c || !in || !out || !out->ct || !out->verdict || !out->identity)
         return -EINVAL;
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (c->seg.valid && c->seg.ct == (const void *)out->ct && c->seg.saddr == in->saddr &&
+        c->seg.n == in->n && c->seg.mode == mode && c->seg.ep == ep_lxc &&
+        c->seg.family == family) {
+        // a batch cut for traffic to itself: its segments before the last
+        // were folded by cfc_classify; fold the last
+        c->seg.valid = false;
+        const uint64_t a = c->seg.off;
+        const Hdr si = sub_batch(*in, a, in->n - a);
+        const cfc_out so = sub_out(*out, a, family == 6);
+        return ct_apply(c, family, &si, &so, mode, ep_lxc, stream);
+    }
     auto it = c->nat.find((const void *)out->ct);
     if (it == c->nat.end() || it->second.family != family || it->second.saddr != in->saddr ||
         it->second.n != in->n || it->second.mode != mode || it->second.ep != ep_lxc)

@@ -521,6 +521,21 @@ struct SvoArgs {
 };
 size_t svc_order_tmp_bytes(uint64_t n);
 int svc_order(const DevTables &T, const SvoArgs &A, bool v6, uint32_t *count, hipStream_t s);
+// traffic to itself (selfseg.hip): the egress headers whose destination is
+// one of `addrs` (IPv4: na words; IPv6: na 16-byte rows) — per such header
+// a row {index, L4 word, meta, which address}, at most cap rows (cnt counts
+// them all; the caller zeroes it)
+struct SelfArgs {
+    const void *daddr;
+    const uint32_t *pt, *mt;
+    uint64_t n;
+    const uint32_t *addrs;
+    uint32_t na;
+    uint4 *rows;
+    uint32_t *cnt;
+    uint32_t cap;
+};
+int self_mark(const SelfArgs &A, bool v6, hipStream_t s);
 // the service step's results a classify launch reads (EGRESS), and the
 // packet outputs; all null when the launch has no load balancer
 struct LbIn {

@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256) void k_svo_replay(DevTables T, SvoArgs A, cons
     const uint32_t fp = (uint32_t)(keys[r0] >> 32);
     if (r0 > 0 && (uint32_t)(keys[r0 - 1] >> 32) == fp)
         return;
+    uint32_t wrote = 0;   // entry words handed to later headers (cfc_stats.svc_ordered)
     for (uint32_t r = r0; r < m && (uint32_t)(keys[r] >> 32) == fp; r++) {
         if (done[r])
             continue;
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(256) void k_svo_replay(DevTables T, SvoArgs A, cons
                 continue;   // (a fingerprint collision: another key)
             done[q] = 1;
             A.svo[j] = svo_word(e);
+            wrote++;
             const uint32_t hj = A.hash ? A.hash[j] : fhash(sj, dj, ptj, protoj);
             if constexpr (V6)
                 svc_next6(T, dj, ptj, protoj, hj, e);
@@ -152,6 +154,8 @@ __global__ __launch_bounds__(256) void k_svo_replay(DevTables T, SvoArgs A, cons
                 svc_next4(T, dj, ptj, protoj, hj, e);
         }
     }
+    if (wrote)   // (cnt words 2-3: a running total the host reads for its stats)
+        atomicAdd(reinterpret_cast<unsigned long long *>(A.cnt + 2), (unsigned long long)wrote);
 }
 
 }  // namespace

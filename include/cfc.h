@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CFC_ABI_VERSION 12
+#define CFC_ABI_VERSION 13
 
 typedef struct cfc_ctx cfc_ctx;
 
@@ -355,7 +355,14 @@ typedef struct {
 } cfc_out;
 
 /* Classify a batch (asynchronous on `stream`).  Policy-entry and metrics
- * counters accumulate on the device until cfc_counters_sync(). */
+ * counters accumulate on the device until cfc_counters_sync().
+ * An EGRESS batch with out->ct whose headers talk to the sending endpoint's
+ * own address (or to a service that loops back into it) is cut where a
+ * header's lookup key may have been written by an earlier header of the
+ * batch (conntrack.h:487-494, 725-748): the segments before the last are
+ * classified and folded into CT here, in order (synchronising `stream`),
+ * and the cfc_ct_apply_* of the same batch folds the last
+ * (cfc_stats.ct_self_segments). */
 int cfc_classify_v4(cfc_ctx *ctx, const cfc_hdr_v4 *in, const cfc_out *out,
                     int mode, uint16_t ep_lxc, void *stream);
 /* The IPv6 chain: bpf_netdev.c handle_ipv6 (:172-275) -> bpf_lxc.c
@@ -626,6 +633,13 @@ typedef struct {
      * launch's work list (the headers with a CT stage that is not a plain
      * hit) rather than the whole batch */
     uint64_t ct_apply_sparse;
+    /* (ABI 13) segments an egress batch with traffic to itself was cut into
+     * beyond its first, each classified after the ones before it were
+     * folded into CT (cfc_classify_*: a header whose lookup key an earlier
+     * header of the batch may have written — an endpoint talking to its own
+     * address, a service flow looped back into it; conntrack.h:487-494,
+     * 725-748), since the context opened */
+    uint64_t ct_self_segments;
 } cfc_stats;
 int cfc_get_stats(cfc_ctx *ctx, cfc_stats *st);
 const char *cfc_strerror(int err);

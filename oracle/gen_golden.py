@@ -1734,6 +1734,301 @@ def sc_nat64_local_v6(n=2400, seed=65):
     return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
 
 
+def _hdrs4(sa, da, sp, dp, proto, tcpf, length):
+    n = len(sp)
+    tcpf = np.asarray(tcpf, np.uint8)
+    h = S.Headers(4, np.full(n, sa, np.uint32), np.full(n, da, np.uint32),
+                  S.htons(sp), S.htons(dp), np.asarray(proto, np.uint8),
+                  np.zeros(n, np.uint8), np.asarray(length, np.uint16),
+                  np.zeros(n, np.uint32), tcpf)
+    h.flags[(h.proto == S.IPPROTO_TCP) & ((tcpf & 0x05) != 0)] = S.HF_TCP_CLOSE
+    return h
+
+
+def sc_self_egress(n=2600, seed=45):
+    """Traffic to itself inside one egress stream (the keys whose two
+    addresses are the sender's own, conntrack.h:487-494, and a looped-back
+    service flow's TUPLE_F_IN entry, :725-748): the endpoint opens TCP and
+    UDP flows to its own address and answers them (the answer's egress
+    lookup finds, as k1, the entry the opening packet's ingress stage
+    created: CT_REPLY), pings itself and sends ICMP errors about those
+    flows, and opens flows to the service whose backend is itself and
+    answers them to IPV4_LOOPBACK — all in the stream that creates the
+    entries.  Its own ingress admits its SECLABEL on TCP 80 and UDP 53 only,
+    so some opening packets are dropped at their second stage."""
+    t, rng, vips, ports, protos = _lb_setup(seed)
+    sec = int(t.seclabel[S.EP_LXC_ID])
+    pol = t.policy[S.EP_LXC_ID]
+    pol = pol[~((pol["egress"] == 0) & (pol["identity"] == sec))]
+    ing = np.zeros(2, S.POLICY_DT)
+    ing["identity"] = sec
+    ing["dport"] = S.htons(np.array([80, 53]))
+    ing["proto"] = [S.IPPROTO_TCP, S.IPPROTO_UDP]
+    t.policy[S.EP_LXC_ID] = np.concatenate([pol, ing])
+    A = int(S.LXC_IPV4)
+    lb = t.lb4
+    k6 = int(np.flatnonzero((lb["target"] == A))[0])
+    vip, vport = int(lb["addr"][k6]), int(lb["dport"][k6])
+
+    def svc_flows(x, f):
+        m = len(x)
+        return S.Headers(4, np.full(m, A, np.uint32), np.full(m, vip, np.uint32),
+                         S.htons(x), np.full(m, vport, np.uint16),
+                         np.full(m, S.IPPROTO_TCP, np.uint8), np.zeros(m, np.uint8),
+                         rng.integers(60, 1500, size=m).astype(np.uint16),
+                         np.zeros(m, np.uint32), np.full(m, f, np.uint8))
+    # a history: self flows opened and answered, service flows opened
+    hx = 29000 + np.arange(20)
+    hy = rng.choice(np.array([80, 8080]), size=20)
+    hist = S.concat([_hdrs4(A, A, hx, hy, np.full(20, S.IPPROTO_TCP), np.full(20, 0x02),
+                            np.full(20, 100)),
+                     _hdrs4(A, A, hy, hx, np.full(20, S.IPPROTO_TCP), np.full(20, 0x12),
+                            np.full(20, 100)),
+                     svc_flows(44000 + np.arange(40), 0x02),
+                     # (plain traffic too: the other endpoint's local CT maps
+                     # hold entries before the stream)
+                     S.gen_headers_v4(rng, 200, t.ipcache[t.ipcache["family"] == 1],
+                                      S.local_v4_addrs(t), local_frac=0.3, mark_host=0,
+                                      mark_proxy=0, src_fixed=S.LXC_IPV4, frag=0)])
+    hist.hash = None
+    dp = RefDatapath(t)
+    run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    parts, pos = [], []
+
+    def add_(h, p):
+        parts.append(h)
+        pos.append(np.asarray(p, np.float64))
+    # the history's flows: later packets, some closing
+    est = S.take(hist, rng.integers(0, len(hist), size=300))
+    est.tcpflags = np.where(rng.random(300) < 0.1, 0x11, 0x10).astype(np.uint8)
+    est.flags = np.where(est.tcpflags == 0x11, S.HF_TCP_CLOSE, 0).astype(np.uint8)
+    add_(est, rng.random(300))
+    # TCP to itself: SYN, SYN-ACK back, ACK, data back, some FIN, a re-open
+    m = 60
+    x = 30000 + np.arange(m)
+    y = rng.choice(np.array([80, 8080, 80, 443]), size=m)
+    p0 = rng.random(m) * 0.7
+    seq = [(x, y, 0x02), (y, x, 0x12), (x, y, 0x10), (y, x, 0x18), (x, y, 0x11),
+           (x, y, 0x02)]
+    keep = np.ones(m, bool)
+    for j, (a, b, f) in enumerate(seq):
+        if j == 4:
+            keep = rng.random(m) < 0.4
+        elif j == 5:
+            keep &= rng.random(m) < 0.5
+        sel = np.flatnonzero(keep)
+        add_(_hdrs4(A, A, a[sel], b[sel], np.full(len(sel), S.IPPROTO_TCP),
+                    np.full(len(sel), f), rng.integers(60, 1500, size=len(sel))),
+             p0[sel] + 0.04 * j + rng.random(len(sel)) * 0.01)
+    # UDP to itself (53 allowed at its own ingress, 5353 not), answers
+    m = 40
+    x = 33000 + np.arange(m)
+    y = rng.choice(np.array([53, 5353]), size=m)
+    p0 = rng.random(m) * 0.7
+    for j, (a, b) in enumerate([(x, y), (y, x), (x, y), (y, x)]):
+        sel = np.flatnonzero(rng.random(m) < (1.0 if j < 2 else 0.6))
+        add_(_hdrs4(A, A, a[sel], b[sel], np.full(len(sel), S.IPPROTO_UDP),
+                    np.zeros(len(sel)), rng.integers(60, 1500, size=len(sel))),
+             p0[sel] + 0.05 * j + rng.random(len(sel)) * 0.01)
+    # pings to itself and their replies; ICMP errors about its own flows
+    m = 30
+    p0 = rng.random(m) * 0.8
+    for j, ty in enumerate([8, 0, 8, 0]):
+        add_(_hdrs4(A, A, np.full(m, ty), np.zeros(m), np.full(m, S.IPPROTO_ICMP),
+                    np.zeros(m), rng.integers(60, 200, size=m)),
+             p0 + 0.03 * j + rng.random(m) * 0.01)
+    m = 40
+    add_(_hdrs4(A, A, rng.choice(np.array([3, 11]), size=m), np.zeros(m),
+                np.full(m, S.IPPROTO_ICMP), np.zeros(m), rng.integers(60, 200, size=m)),
+         0.2 + rng.random(m) * 0.8)
+    # flows to the service whose backend is the endpoint itself
+    m = 150
+    p0 = rng.random(m) * 0.6
+    svc = svc_flows(45000 + np.arange(m), 0x02)
+    add_(svc, p0)
+    later = S.take(svc, np.arange(m))
+    later.tcpflags = np.full(m, 0x10, np.uint8)
+    add_(later, p0 + 0.1)
+    # plain traffic beside it
+    plain = S.gen_headers_v4(rng, int(n * 0.35), t.ipcache[t.ipcache["family"] == 1],
+                             S.local_v4_addrs(t), local_frac=0.3, mark_host=0,
+                             mark_proxy=0, src_fixed=S.LXC_IPV4, frag=0)
+    add_(plain, rng.random(len(plain)))
+    h = S.concat(parts)
+    order = np.argsort(np.concatenate(pos), kind="stable")
+    h = S.take(h, order)
+    h.hash = None
+    # the looped-back flows' answers (the history's and the stream's): the endpoint, as the backend, replies
+    # to the address it saw (IPV4_LOOPBACK) from its translated port, after
+    # the flow's first packet (a dry run of the reference tells which flows
+    # looped back and their ports)
+    dry = RefDatapath(t)
+    try:
+        res = run(dry, h, MODE_EGRESS, S.EP_LXC_ID)
+    finally:
+        dry.close()
+    pk = res[8]
+    lo = np.flatnonzero((pk[:, 0] == S.IPV4_LOOPBACK) & (h.proto == S.IPPROTO_TCP) &
+                        (res[0] != 2))
+    _, first = np.unique(h.sport[lo], return_index=True)
+    lo = lo[first]
+    if len(lo):
+        rp = _hdrs4(A, S.IPV4_LOOPBACK, np.zeros(len(lo), np.uint16),
+                    np.zeros(len(lo), np.uint16), np.full(len(lo), S.IPPROTO_TCP),
+                    np.full(len(lo), 0x12), rng.integers(60, 1500, size=len(lo)))
+        rp.sport = (pk[lo, 2] >> 16).astype(np.uint16)   # be16 raw, as the packet left
+        rp.dport = (pk[lo, 2] & 0xFFFF).astype(np.uint16)
+        at = np.concatenate([np.arange(len(h)), lo + 0.5 + rng.random(len(lo)) * 40])
+        h = S.concat([h, rp])
+        h = S.take(h, np.argsort(at, kind="stable"))
+        h.hash = None
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
+def _hdrs6(sa, da, sp, dp, proto, tcpf, length):
+    n = len(sp)
+    tcpf = np.asarray(tcpf, np.uint8)
+    h = S.Headers(6, np.tile(sa, (n, 1)), np.tile(da, (n, 1)),
+                  S.htons(sp), S.htons(dp), np.asarray(proto, np.uint8),
+                  np.zeros(n, np.uint8), np.asarray(length, np.uint16),
+                  np.zeros(n, np.uint32), tcpf)
+    h.flags[(h.proto == S.IPPROTO_TCP) & ((tcpf & 0x05) != 0)] = S.HF_TCP_CLOSE
+    return h
+
+
+def sc_self_egress_v6(n=2400, seed=47):
+    """The IPv6 counterpart of self_egress_v4: an endpoint's TCP / UDP flows
+    to its own address and their answers, pings (ICMPv6 echo) and ICMPv6
+    errors to itself, and flows to the IPv6 service whose backend is the
+    endpoint (lb6_local translates the destination back to the sender; no
+    loopback address in IPv6) answered from the backend port — all in the
+    stream that creates the entries.  Its own ingress admits its SECLABEL
+    on TCP 80 and UDP 53 only."""
+    t, rng, vips, ports, protos = _lb_setup6(seed)
+    sec = int(t.seclabel[S.EP_LXC_ID])
+    pol = t.policy[S.EP_LXC_ID]
+    pol = pol[~((pol["egress"] == 0) & (pol["identity"] == sec))]
+    ing = np.zeros(2, S.POLICY_DT)
+    ing["identity"] = sec
+    ing["dport"] = S.htons(np.array([80, 53]))
+    ing["proto"] = [S.IPPROTO_TCP, S.IPPROTO_UDP]
+    t.policy[S.EP_LXC_ID] = np.concatenate([pol, ing])
+    A = np.asarray(S.LXC_IPV6, np.uint8)
+    lb = t.lb6
+    own = np.flatnonzero((np.asarray(lb["target"]).reshape(len(lb), -1) == A).all(1) &
+                         (lb["slave"] != 0))
+    k6 = int(own[0])
+    vip, vport = np.asarray(lb["addr"][k6], np.uint8), int(lb["dport"][k6])
+
+    def svc_flows(x, f):
+        m = len(x)
+        return S.Headers(6, np.tile(A, (m, 1)), np.tile(vip, (m, 1)), S.htons(x),
+                         np.full(m, vport, np.uint16), np.full(m, S.IPPROTO_TCP, np.uint8),
+                         np.zeros(m, np.uint8),
+                         rng.integers(100, 1500, size=m).astype(np.uint16),
+                         np.zeros(m, np.uint32), np.full(m, f, np.uint8))
+    ipc = t.ipcache[t.ipcache["family"] == 2]
+    hx = 29000 + np.arange(20)
+    hy = rng.choice(np.array([80, 8080]), size=20)
+    hist = S.concat([_hdrs6(A, A, hx, hy, np.full(20, S.IPPROTO_TCP), np.full(20, 0x02),
+                            np.full(20, 100)),
+                     _hdrs6(A, A, hy, hx, np.full(20, S.IPPROTO_TCP), np.full(20, 0x12),
+                            np.full(20, 100)),
+                     svc_flows(44000 + np.arange(40), 0x02),
+                     S.gen_headers_v6(rng, 200, ipc, S.local_v6_addrs(t), local_frac=0.3,
+                                      mark_host=0, mark_proxy=0, src_fixed=S.LXC_IPV6,
+                                      ext=0, exthdr_drop=0)])
+    hist.hash = None
+    dp = RefDatapath(t)
+    run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    parts, pos = [], []
+
+    def add_(h, p):
+        parts.append(h)
+        pos.append(np.asarray(p, np.float64))
+    est = S.take(hist, rng.integers(0, len(hist), size=300))
+    est.tcpflags = np.where(rng.random(300) < 0.1, 0x11, 0x10).astype(np.uint8)
+    est.flags = np.where((est.tcpflags == 0x11) & (est.proto == S.IPPROTO_TCP),
+                         S.HF_TCP_CLOSE, 0).astype(np.uint8)
+    add_(est, rng.random(300))
+    m = 60
+    x = 30000 + np.arange(m)
+    y = rng.choice(np.array([80, 8080, 80, 443]), size=m)
+    p0 = rng.random(m) * 0.7
+    keep = np.ones(m, bool)
+    for j, (a, b, f) in enumerate([(x, y, 0x02), (y, x, 0x12), (x, y, 0x10), (y, x, 0x18),
+                                   (x, y, 0x11), (x, y, 0x02)]):
+        if j == 4:
+            keep = rng.random(m) < 0.4
+        elif j == 5:
+            keep &= rng.random(m) < 0.5
+        sel = np.flatnonzero(keep)
+        add_(_hdrs6(A, A, a[sel], b[sel], np.full(len(sel), S.IPPROTO_TCP),
+                    np.full(len(sel), f), rng.integers(100, 1500, size=len(sel))),
+             p0[sel] + 0.04 * j + rng.random(len(sel)) * 0.01)
+    m = 40
+    x = 33000 + np.arange(m)
+    y = rng.choice(np.array([53, 5353]), size=m)
+    p0 = rng.random(m) * 0.7
+    for j, (a, b) in enumerate([(x, y), (y, x), (x, y), (y, x)]):
+        sel = np.flatnonzero(rng.random(m) < (1.0 if j < 2 else 0.6))
+        add_(_hdrs6(A, A, a[sel], b[sel], np.full(len(sel), S.IPPROTO_UDP),
+                    np.zeros(len(sel)), rng.integers(100, 1500, size=len(sel))),
+             p0[sel] + 0.05 * j + rng.random(len(sel)) * 0.01)
+    m = 30
+    p0 = rng.random(m) * 0.8
+    for j, ty in enumerate([128, 129, 128, 129]):
+        add_(_hdrs6(A, A, np.full(m, ty), np.zeros(m), np.full(m, S.IPPROTO_ICMPV6),
+                    np.zeros(m), rng.integers(100, 200, size=m)),
+             p0 + 0.03 * j + rng.random(m) * 0.01)
+    m = 40
+    add_(_hdrs6(A, A, rng.choice(np.array([1, 3]), size=m), np.zeros(m),
+                np.full(m, S.IPPROTO_ICMPV6), np.zeros(m), rng.integers(100, 200, size=m)),
+         0.2 + rng.random(m) * 0.8)
+    m = 150
+    p0 = rng.random(m) * 0.6
+    svc = svc_flows(45000 + np.arange(m), 0x02)
+    add_(svc, p0)
+    later = S.take(svc, np.arange(m))
+    later.tcpflags = np.full(m, 0x10, np.uint8)
+    add_(later, p0 + 0.1)
+    plain = S.gen_headers_v6(rng, int(n * 0.3), ipc, S.local_v6_addrs(t), local_frac=0.3,
+                             mark_host=0, mark_proxy=0, src_fixed=S.LXC_IPV6, ext=0,
+                             exthdr_drop=0)
+    add_(plain, rng.random(len(plain)))
+    h = S.concat(parts)
+    h = S.take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    h.hash = None
+    # the service flows the endpoint itself serves: it answers from the
+    # backend port (a dry run of the reference gives the translated port)
+    dry = RefDatapath(t)
+    try:
+        res = run(dry, h, MODE_EGRESS, S.EP_LXC_ID)
+    finally:
+        dry.close()
+    pk = res[8]
+    dst = np.ascontiguousarray(pk[:, 4:8]).view(np.uint8).reshape(-1, 16)
+    vis = (np.asarray(h.daddr) == vip).all(1)
+    lo = np.flatnonzero(vis & (dst == A).all(1) & (h.proto == S.IPPROTO_TCP) & (res[0] != 2))
+    _, first = np.unique(h.sport[lo], return_index=True)
+    lo = lo[first]
+    if len(lo):
+        rp = _hdrs6(A, A, np.zeros(len(lo)), np.zeros(len(lo)),
+                    np.full(len(lo), S.IPPROTO_TCP), np.full(len(lo), 0x12),
+                    rng.integers(100, 1500, size=len(lo)))
+        rp.sport = (pk[lo, 8] >> 16).astype(np.uint16)
+        rp.dport = (pk[lo, 8] & 0xFFFF).astype(np.uint16)
+        at = np.concatenate([np.arange(len(h)), lo + 0.5 + rng.random(len(lo)) * 40])
+        h = S.concat([h, rp])
+        h = S.take(h, np.argsort(at, kind="stable"))
+        h.hash = None
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
 SCENARIOS = {
     "edge_ingress_v4": sc_edge_ingress,
     "small_ingress_v4": sc_small_ingress,
@@ -1763,6 +2058,8 @@ SCENARIOS = {
     "lb_reply_v4": sc_lb_reply,
     "lb_egress_v6": sc_lb_egress_v6,
     "lb_reply_v6": sc_lb_reply_v6,
+    "self_egress_v4": sc_self_egress,
+    "self_egress_v6": sc_self_egress_v6,
 }
 
 

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(_lib.EXPORTS) == fns
-    assert L.cfc_abi_version() == 12
+    assert L.cfc_abi_version() == 13
     assert L.cfc_num_possible_cpus() == 1
 
 

@@ -38,8 +38,10 @@ def test_recorded_kernels_below_ceiling(e):
             # bench line's ct_apply section, not on the request roofline)
             assert pk["hbm_bytes_per_launch"] > 0 and pk["avg_ms"] > 0, (k, pk)
             continue
+        # (the requests and the hit / miss split come from separate counter
+        # passes over the same bench run: equal to a few in 10^4)
         assert pk["l2_hits_per_launch"] + pk["l2_misses_per_launch"] == pytest.approx(
-            pk["l2_requests_per_launch"], rel=1e-6)
+            pk["l2_requests_per_launch"], rel=1e-3)
         # a small working set prices misses at the HBM row, the slowest
         d, t_ideal, _ = bench.kernel_roofline(k, pk["headers"], pk["avg_ms"], 1 << 20, pk, rows)
         assert 0 < d["frac"] <= 1.0, (e["workload"], k, d["frac"])
