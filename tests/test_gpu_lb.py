@@ -274,3 +274,6 @@ def test_lb_stream_vs_oracle(torch, fam, mode):
     assert dev.sum() > 0
     if mode == 1:
         assert (r["ver"] == -158).any()
+        # later packets of the batch's new service flows were handed the
+        # CT_SERVICE entry their flow's first packet created
+        assert 0 < r["stats"]["svc_ordered"] < len(h)
