@@ -475,11 +475,12 @@ def main():
         tw = torch.tensor([wall], device=dev, dtype=torch.float64)
         dist.all_reduce(tw, op=dist.ReduceOp.MAX)
         wall = float(tw.item())
-    if world == 1:
-        if args.ct_apply:   # (the host mirror takes the device's CT changes)
-            log(f"[rank {rank}] timed steps done in {wall:.2f} s; folding counters "
-                f"and the CT maps into the host mirror")
+    if world == 1 and not args.ct_apply:
         dp.counters_sync()
+    # (with --ct-apply the counters stay on the device: folding them brings
+    # the host mirror of the CT maps up to date first, untimed host work in
+    # proportion to the run's CT changes — minutes after a long dependency
+    # stream — that no figure of this line reads)
     total = (n + n6) * world * args.steps
     mpps = total / wall / 1e6
     log(f"[rank {rank}] {args.steps} steps in {wall * 1e3:.2f} ms; per call "

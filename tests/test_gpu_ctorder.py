@@ -146,8 +146,8 @@ def test_c5_packet_order_hot_flows(torch, clock):
 def test_sparse_apply_packet_order(torch, mode, monkeypatch):
     """The apply's sparse passes — ordering and scan over the classify
     launch's work list (kern_common.hpp wl_want) instead of the whole batch —
-    on a stream without deletes (the headers of denied live flows taken out:
-    a batch that deletes takes the dense passes): multi-packet new flows,
+    on a stream without deletes (the headers of denied live flows taken out;
+    test_sparse_apply_with_deletes keeps them): multi-packet new flows,
     closes, ICMP errors, hot flows.  Every output, CT entry and counter
     against the sequential oracle, and the dense passes (CFC_DENSE_APPLY)
     give the same."""
@@ -170,3 +170,30 @@ def test_sparse_apply_packet_order(torch, mode, monkeypatch):
     for k in ("act", "ver", "ide", "ct"):
         np.testing.assert_array_equal(g[k], gd[k])
     np.testing.assert_array_equal(g["rows"], gd["rows"])
+
+
+@pytest.mark.parametrize("mode", [0, 3])
+def test_sparse_apply_with_deletes(torch, mode, monkeypatch):
+    """Batches that delete stay on the sparse passes (round 6: the deleted
+    slots' mixed hits join the work list, ctorder.hip k_ord_mixed /
+    k_ord_collect_mix / k_ord_write): the dependency stream with its denied
+    live flows (each loses its entry to its first packet, the later packets
+    of the batch find none), closes, multi-packet new flows, ICMP errors.
+    Every output, CT entry and counter against the sequential oracle, every
+    batch sparse, and the dense passes give the same."""
+    t, flows = S.config_c5(5, n_flows=100_000, n_prefixes=50_000, n_policy=8000, now=1000)
+    h = S.headers_c5_seq(t, flows, 600_000, seed=19)
+    o = O.Oracle(t)
+    o.set_clock(1003)
+    _, ov, _, oct_ = o.classify(h, mode, 0, nthreads=16, want_ct=True)
+    est_drop = ((oct_ & 0xF) == (1 | 4)) & (ov == -133)   # ESTABLISHED, DROP_POLICY
+    assert est_drop.sum() > 1000
+    g, want = run_both(torch, t, h, mode, chunks=3, notify=False)
+    check(g, want)
+    monkeypatch.setenv("CFC_DENSE_APPLY", "1")
+    gd, _ = run_both(torch, t, h, mode, chunks=3, notify=False)
+    assert gd["stats"]["ct_apply_sparse"] == 0, gd["stats"]
+    for k in ("act", "ver", "ide", "ct"):
+        np.testing.assert_array_equal(g[k], gd[k])
+    np.testing.assert_array_equal(g["rows"], gd["rows"])
+    assert g["stats"]["ct_apply_sparse"] == 3, g["stats"]
