@@ -18,13 +18,19 @@ Restated (file:line in /root/reference):
   * entities -> reserved-label selectors        pkg/policy/api/entity.go:45-70
   * CIDR selectors, CIDRSet except expansion,   pkg/policy/api/cidr.go:70-132,
     CIDR identity labels                        pkg/labels/cidr.go, pkg/labels/cidr/cidr.go:33-70
+  * an L7 port's filter also takes the peers    pkg/policy/repository.go:127-234
+    of L3-only and L3/L4 rules (wildcardL3L4Rules)
 
 Not restated (they need services the reference's agent talks to): toFQDNs
-(DNS proxy), toServices (Kubernetes endpoints), L7 rules / proxy redirects.
-Such rules contribute no keys here.  The reference resolver is Go, and this
-image has no Go toolchain, so the MapState itself is "parity unpinned"; the
-datapath verdicts over it are pinned by the reference BPF programs
-(oracle/gen_golden.py scenario c1_ingress_v4).
+(DNS proxy), toServices (Kubernetes endpoints), the L7 rules' contents and
+the proxy redirect (an L7 port's keys carry proxy port 0 here).  The
+reference resolver is Go and this image has no Go toolchain: rule selection,
+label access and L4 resolution are pinned to the reference's own
+known-answer tests (pkg/policy/repository_test.go, restated as data in
+tests/test_policy_repository_ref.py); the MapState step (policy.go), which
+no reference test covers, is pinned to hand-derived MapStates of the
+example policies; the datapath verdicts over it are pinned by the reference
+BPF programs (oracle/gen_golden.py scenario c1_ingress_v4).
 """
 from __future__ import annotations
 
@@ -140,6 +146,14 @@ def peer_selectors(r: dict, ingress: bool) -> list:
     return sel
 
 
+def label_based(r: dict, ingress: bool) -> bool:
+    """IngressRule / EgressRule IsLabelBased (api/ingress.go:120-122,
+    api/egress.go:148-150): no requirements, CIDRs (or services)."""
+    keys = ("fromRequires", "fromCIDR", "fromCIDRSet") if ingress else \
+        ("toRequires", "toCIDR", "toCIDRSet", "toServices")
+    return not any(r.get(k) for k in keys)
+
+
 def rule_cidrs(r: dict, ingress: bool) -> list:
     p = "from" if ingress else "to"
     return list(r.get(f"{p}CIDR", []) or []) + cidr_rule_set(r.get(f"{p}CIDRSet", []) or [])
@@ -235,7 +249,22 @@ class Repository:
             if r.selector.matches(subject):
                 for x in (r.ingress if ingress else r.egress):
                     reqs += [Selector.parse(s) for s in x.get(req_key, []) or []]
-        res = {}
+        res, l7 = {}, set()
+
+        def add(k, sel, wild):
+            cur = res.get(k, [])
+            if wild or cur == WILDCARD:
+                res[k] = WILDCARD
+            else:
+                res[k] = cur + [s for s in sel if s not in cur]
+
+        def keys_of(pr):
+            for p in pr.get("ports", []) or []:
+                protos = [p.get("protocol", "ANY").upper()]
+                if protos[0] == "ANY":
+                    protos = ["TCP", "UDP"]
+                for proto in protos:
+                    yield (int(p["port"]), PROTO[proto])
         for r in self.rules:
             if not r.selector.matches(subject):
                 continue
@@ -249,17 +278,33 @@ class Repository:
                            for i, s in enumerate(sel)]
                 wild = not sel or any(s.selects_all() for s in sel)
                 for pr in x["toPorts"]:
-                    for p in pr.get("ports", []) or []:
-                        protos = [p.get("protocol", "ANY").upper()]
-                        if protos[0] == "ANY":
-                            protos = ["TCP", "UDP"]
-                        for proto in protos:
-                            k = (int(p["port"]), PROTO[proto])
-                            cur = res.get(k, [])
-                            if wild or cur == WILDCARD:
-                                res[k] = WILDCARD
-                            else:
-                                res[k] = cur + [s for s in sel if s not in cur]
+                    for k in keys_of(pr):
+                        add(k, sel, wild)
+                        if pr.get("rules"):   # (an L7 parser on the port)
+                            l7.add(k)
+        # wildcardL3L4Rules (repository.go:166-234, wildcardL3L4Rule :127-164):
+        # a port with L7 rules also takes, with allow-all L7 rules, the peers
+        # of the label-based L3-only rules (every such port of TCP and UDP)
+        # and of the L3/L4 rules without L7 rules on the same port — they
+        # become L4 keys (the reference redirects them to its proxy)
+        if l7:
+            for r in self.rules:
+                if not r.selector.matches(subject):
+                    continue
+                for x in (r.ingress if ingress else r.egress):
+                    if not label_based(x, ingress):
+                        continue
+                    sel = peer_selectors(x, ingress)
+                    wild = any(s.selects_all() for s in sel)
+                    tps = x.get("toPorts") or []
+                    if not tps:
+                        targets = [k for k in l7 if k[1] in (6, 17)]
+                    else:
+                        targets = [k for pr in tps if not pr.get("rules")
+                                   for k in keys_of(pr) if k in l7]
+                    for k in targets:
+                        if sel:
+                            add(k, sel, wild)
         return res
 
     def map_state(self, subject: frozenset, identities: dict) -> dict:

@@ -1,0 +1,187 @@
+"""The C1 resolver (cilium_amd/policy_resolver.py) against the reference
+resolver's own known-answer tests, pkg/policy/repository_test.go: the same
+rules, the same label contexts, the answers the Go tests assert.  The Go
+code cannot run here (no Go toolchain); these cases are its expected values,
+restated as data.
+
+Mapping: a Go label "foo" / "id=foo" (labels.ParseSelectLabel: source any)
+is the resolver's "foo=" / "id=foo"; api.Rule is the CiliumNetworkPolicy
+JSON shape the resolver reads.  AllowsIngress/EgressRLocked without ports is
+the label verdict (CanReach), `Repository._can_reach`; ResolveL4*Policy is
+`Repository._l4` (port/proto -> peer selectors; the Go L4Filter's
+Endpoints as a set — the Go list repeats selectors that several rules add,
+which its test comments call an artifact — and without the L7 rule
+contents, which the resolver does not restate).  One difference is the
+API's, not the datapath's: the Go call answers Denied for an endpoint no
+rule selects, while that endpoint's policymap allows every identity
+(pkg/endpoint/policy.go: policy enforcement off), which is what the resolver
+computes; those cases check `enabled`."""
+from cilium_amd import policy_resolver as R
+
+
+def lab(s):
+    k, _, v = s.partition("=")
+    return f"{k}={v}"
+
+
+def lbls(*xs):
+    return frozenset(lab(x) for x in xs)
+
+
+def es(*xs):
+    return {"matchLabels": {lab(x).split("=", 1)[0]: lab(x).split("=", 1)[1] for x in xs}}
+
+
+def sel(*xs):
+    return R.Selector(lbls(*xs))
+
+
+def repo(*rules):
+    return R.Repository(R.parse_rules(list(rules)))
+
+
+def tcp(port, rules=None):
+    pr = {"ports": [{"port": str(port), "protocol": "TCP"}]}
+    if rules:
+        pr["rules"] = rules
+    return [pr]
+
+
+def ingress_allowed(rp, frm, to):
+    """AllowsIngressRLocked (label verdict); None: no rule selects `to`"""
+    if not rp.enabled(to)[0]:
+        return None
+    return rp._can_reach(to, frm, True)
+
+
+def egress_allowed(rp, frm, to):
+    if not rp.enabled(frm)[1]:
+        return None
+    return rp._can_reach(frm, to, False)
+
+
+def l4_sets(d):
+    return {k: (v if v == R.WILDCARD else frozenset(v)) for k, v in d.items()}
+
+
+def test_can_reach_ingress():
+    # repository_test.go:193-285
+    assert ingress_allowed(repo(), lbls("foo"), lbls("bar")) is None   # no rules: Denied
+    rp = repo({"endpointSelector": es("bar"), "ingress": [{"fromEndpoints": [es("foo")]}]},
+              {"endpointSelector": es("groupA"), "ingress": [{"fromRequires": [es("groupA")]}]},
+              {"endpointSelector": es("bar2"), "ingress": [{"fromEndpoints": [es("foo")]}]})
+    assert ingress_allowed(rp, lbls("foo"), lbls("bar")) is True
+    assert ingress_allowed(rp, lbls("foo"), lbls("bar2")) is True
+    assert ingress_allowed(rp, lbls("foo", "groupA"), lbls("bar", "groupA")) is True
+    assert ingress_allowed(rp, lbls("foo", "groupB"), lbls("bar", "groupA")) is False
+    assert ingress_allowed(rp, lbls("foo", "groupB"), lbls("bar", "groupB")) is True
+    # foo => bar3, no rule: Denied by the API; bar3's map allows all
+    assert ingress_allowed(rp, lbls("foo"), lbls("bar3")) is None
+
+
+def test_can_reach_egress():
+    # repository_test.go:287-383
+    assert egress_allowed(repo(), lbls("foo"), lbls("bar")) is None
+    rp = repo({"endpointSelector": es("foo"), "egress": [{"toEndpoints": [es("bar")]}]},
+              {"endpointSelector": es("groupA"), "egress": [{"toRequires": [es("groupA")]}]},
+              {"endpointSelector": es("foo"), "egress": [{"toEndpoints": [es("bar2")]}]})
+    assert egress_allowed(rp, lbls("foo"), lbls("bar")) is True
+    assert egress_allowed(rp, lbls("foo"), lbls("bar2")) is True
+    assert egress_allowed(rp, lbls("foo", "groupA"), lbls("bar", "groupA")) is True
+    assert egress_allowed(rp, lbls("bar", "groupA"), lbls("foo", "groupB")) is False
+    assert egress_allowed(rp, lbls("foo", "groupB"), lbls("bar", "groupB")) is True
+    assert egress_allowed(rp, lbls("foo"), lbls("bar3")) is False
+
+
+def test_minikube_getting_started():
+    # repository_test.go:1313-1453: app1 admits app2 on 80/TCP (three rules,
+    # two with HTTP rules); app3 has no L4 access, neither has L3 access
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    rp = repo(*[{"endpointSelector": es("id=app1"),
+                 "ingress": [{"fromEndpoints": [es("id=app2")], "toPorts": tcp(80, r)}]}
+                for r in (None, http, http)])
+    assert l4_sets(rp._l4(lbls("id=app1"), True)) == {(80, 6): frozenset({sel("id=app2")})}
+    assert ingress_allowed(rp, lbls("id=app2"), lbls("id=app1")) is False
+    assert ingress_allowed(rp, lbls("id=app3"), lbls("id=app1")) is False
+    ms = rp.map_state(lbls("id=app1"), {1000: lbls("id=app2"), 1001: lbls("id=app3")})
+    assert (1000, 80, 6, R.INGRESS) in ms and (1001, 80, 6, R.INGRESS) not in ms
+    assert (1000, 0, 0, R.INGRESS) not in ms and (1001, 0, 0, R.INGRESS) not in ms
+
+
+def test_l3_dependent_l4_from_requires():
+    # repository_test.go:685-808: FromRequires / ToRequires joins each
+    # From/ToEndpoints selector of the endpoint's L4 rules
+    for ingress in (True, False):
+        d, peers, req = (("ingress", "fromEndpoints", "fromRequires") if ingress else
+                         ("egress", "toEndpoints", "toRequires"))
+        rp = repo({"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar1")], "toPorts": tcp(80)}, {req: [es("id=bar2")]}]})
+        want = R.Selector(lbls("id=bar1"), (sel("id=bar2"),))
+        assert rp._l4(lbls("id=foo"), ingress) == {(80, 6): [want]}
+        # (no identity has both id=bar1 and id=bar2: the port admits none)
+        ms = rp.map_state(lbls("id=foo"), {1000: lbls("id=bar1"), 1001: lbls("id=bar2")})
+        dr = R.INGRESS if ingress else R.EGRESS
+        assert not any(k[1] == 80 and k[3] == dr for k in ms)
+
+
+def _wildcard_l3_rules(ingress):
+    d, peers = ("ingress", "fromEndpoints") if ingress else ("egress", "toEndpoints")
+    kafka = {"kafka": [{"apiKey": "produce"}]}
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    rules = [{"endpointSelector": es("id=foo"), d: [{peers: [es("id=bar1")]}]},
+             {"endpointSelector": es("id=foo"),
+              d: [{peers: [es("id=bar2")], "toPorts": tcp(9092, kafka)}]},
+             {"endpointSelector": es("id=foo"),
+              d: [{peers: [es("id=bar2")], "toPorts": tcp(80, http)}]}]
+    if ingress:   # (the ingress test also has a generic L7 parser on 9090)
+        rules.append({"endpointSelector": es("id=foo"),
+                      d: [{peers: [es("id=bar2")],
+                           "toPorts": tcp(9090, {"l7proto": "tester",
+                                                 "l7": [{"method": "GET", "path": "/"}]})}]})
+    return repo(*rules)
+
+
+def test_wildcard_l3_rules():
+    # repository_test.go:385-542 (ingress), :810-926 (egress): the L3-only
+    # rule's peer joins every L7 port's filter (wildcardL3L4Rules)
+    for ingress, ports in ((True, (9092, 80, 9090)), (False, (9092, 80))):
+        got = l4_sets(_wildcard_l3_rules(ingress)._l4(lbls("id=foo"), ingress))
+        assert got == {(p, 6): frozenset({sel("id=bar2"), sel("id=bar1")}) for p in ports}
+
+
+def test_wildcard_l4_rules():
+    # repository_test.go:544-683 (ingress), :928-1067 (egress): L3/L4 rules
+    # without L7 join the L7 filter of their own port
+    kafka = {"kafka": [{"apiKey": "produce"}]}
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    for ingress in (True, False):
+        d, peers = ("ingress", "fromEndpoints") if ingress else ("egress", "toEndpoints")
+        rp = repo({"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar1")], "toPorts": tcp(9092)}]},
+                  {"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar2")], "toPorts": tcp(9092, kafka)}]},
+                  {"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar1")], "toPorts": tcp(80)}]},
+                  {"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar2")], "toPorts": tcp(80, http)}]})
+        got = l4_sets(rp._l4(lbls("id=foo"), ingress))
+        assert got == {(p, 6): frozenset({sel("id=bar1"), sel("id=bar2")}) for p in (80, 9092)}
+
+
+def test_wildcard_l3_rules_entities():
+    # repository_test.go:1069-1189 (ingress), :1191-1311 (egress): an
+    # L3-only entity rule (world) joins the L7 filters as the entity's
+    # selector (api.EntitySelectorMapping[world] = reserved:world)
+    kafka = {"kafka": [{"apiKey": "produce"}]}
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    for ingress in (True, False):
+        d, peers, ent = (("ingress", "fromEndpoints", "fromEntities") if ingress else
+                         ("egress", "toEndpoints", "toEntities"))
+        rp = repo({"endpointSelector": es("id=foo"), d: [{ent: ["world"]}]},
+                  {"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar2")], "toPorts": tcp(9092, kafka)}]},
+                  {"endpointSelector": es("id=foo"),
+                   d: [{peers: [es("id=bar2")], "toPorts": tcp(80, http)}]})
+        world = R.Selector(frozenset({"reserved:world="}))
+        got = l4_sets(rp._l4(lbls("id=foo"), ingress))
+        assert got == {(p, 6): frozenset({sel("id=bar2"), world}) for p in (9092, 80)}
