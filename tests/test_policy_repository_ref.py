@@ -1,6 +1,7 @@
 """The C1 resolver (cilium_amd/policy_resolver.py) against the reference
-resolver's own known-answer tests, pkg/policy/repository_test.go: the same
-rules, the same label contexts, the answers the Go tests assert.  The Go
+resolver's own known-answer tests, pkg/policy/repository_test.go and
+rule_test.go: the same rules, the same label contexts, the answers the Go
+tests assert.  The Go
 code cannot run here (no Go toolchain); these cases are its expected values,
 restated as data.
 
@@ -20,6 +21,11 @@ from cilium_amd import policy_resolver as R
 
 
 def lab(s):
+    """a Go label string -> the resolver's: the k8s / any sources dropped
+    (selectors without a source match any), reserved: kept"""
+    for src in ("k8s:", "any:"):
+        if s.startswith(src):
+            s = s[len(src):]
     k, _, v = s.partition("=")
     return f"{k}={v}"
 
@@ -185,3 +191,78 @@ def test_wildcard_l3_rules_entities():
         world = R.Selector(frozenset({"reserved:world="}))
         got = l4_sets(rp._l4(lbls("id=foo"), ingress))
         assert got == {(p, 6): frozenset({sel("id=bar2"), world}) for p in (9092, 80)}
+
+
+# rule_test.go:1438-1460: the shared contexts
+A, B, C = lbls("id=a"), lbls("id1=b", "id2=c"), lbls("id=c")
+WORLD, FOO = lbls("reserved:world"), lbls("k8s:app=foo")
+WILD = {"matchLabels": {}}   # api.WildcardEndpointSelector
+
+
+def allows(rp, subject, peer, ingress, port=None):
+    """AllowsIngress/EgressRLocked on the datapath's terms: the subject's
+    policymap (map_state) admits the peer — at L3, or at L4 on `port`/TCP
+    when the context carries one; None: no rule selects the subject"""
+    if not rp.enabled(subject)[0 if ingress else 1]:
+        return None
+    d = R.INGRESS if ingress else R.EGRESS
+    ms = rp.map_state(subject, {1000: peer})
+    return (1000, 0, 0, d) in ms or (port is not None and (1000, port, 6, d) in ms)
+
+
+def test_rule_can_reach():
+    # rule_test.go:31-108 (one rule in the repository: Undecided is Denied)
+    rp = repo({"endpointSelector": es("bar"),
+               "ingress": [{"fromEndpoints": [es("foo", "foo2")]}]})
+    assert allows(rp, lbls("bar"), lbls("foo", "foo2"), True) is True
+    assert allows(rp, lbls("bar"), lbls("foo"), True) is False
+    rp = repo({"endpointSelector": es("bar"),
+               "ingress": [{"fromEndpoints": [es("foo")], "fromRequires": [es("baz")]}]})
+    assert allows(rp, lbls("bar"), lbls("foo"), True) is False
+    assert allows(rp, lbls("bar"), lbls("baz"), True) is False
+    assert allows(rp, lbls("bar"), lbls("foo", "baz"), True) is True
+
+
+def test_ingress_allow_all():
+    # rule_test.go:1495-1520, 1522-1554, 1556-1590
+    rp = repo({"endpointSelector": es("id=c"), "ingress": [{"fromEndpoints": [WILD]}]})
+    assert allows(rp, B, A, True) is None          # (the API: Denied)
+    assert allows(rp, C, A, True) is True
+    assert allows(rp, C, A, True, 80) and allows(rp, C, A, True, 90)
+    rp = repo({"endpointSelector": es("id=c"),
+               "ingress": [{"fromEndpoints": [WILD]}, {"toPorts": tcp(80)}]})
+    assert allows(rp, C, A, True, 80) and allows(rp, C, A, True, 90)
+    rp = repo({"endpointSelector": es("id=c"), "ingress": [{"toPorts": tcp(80)}]})
+    assert allows(rp, C, A, True, 80) is True
+    assert allows(rp, C, A, True, 90) is False
+    assert rp._l4(C, True) == {(80, 6): R.WILDCARD}
+
+
+def test_egress_allow_all():
+    # rule_test.go:1592-1616, 1618-1658
+    rp = repo({"endpointSelector": es("id=a"), "egress": [{"toEndpoints": [WILD]}]})
+    assert allows(rp, A, B, False) is True and allows(rp, A, C, False) is True
+    assert allows(rp, A, C, False, 80) and allows(rp, A, C, False, 90)
+    rp = repo({"endpointSelector": es("id=a"), "egress": [{"toPorts": tcp(80)}]})
+    assert allows(rp, A, C, False, 80) is True
+    assert allows(rp, A, C, False, 90) is False
+
+
+def test_egress_world_and_all_entities():
+    # rule_test.go:1660-1719 (L4 to world), 1721-1780 (L4 to all),
+    # 1782-1824 (L3 to world), 1826-1868 (L3 to all)
+    cases = (({"toEntities": ["world"], "toPorts": tcp(80)},
+              {(WORLD, 80): True, (WORLD, 90): False, (FOO, 80): False, (FOO, 90): False}),
+             ({"toEntities": ["all"], "toPorts": tcp(80)},
+              {(WORLD, 80): True, (WORLD, 90): False, (FOO, 80): True, (FOO, 90): False}),
+             ({"toEntities": ["world"]},
+              {(WORLD, 80): True, (WORLD, 90): True, (FOO, 80): False, (FOO, 90): False}),
+             ({"toEntities": ["all"]},
+              {(WORLD, 80): True, (WORLD, 90): True, (FOO, 80): True, (FOO, 90): True}))
+    for rule, want in cases:
+        rp = repo({"endpointSelector": es("id=a"), "egress": [rule]})
+        for (peer, port), ok in want.items():
+            assert allows(rp, A, peer, False, port) is ok, (rule, sorted(peer), port)
+        if "toPorts" in rule:   # one selector on 80/TCP (world, or all)
+            f = rp._l4(A, False)[(80, 6)]
+            assert f == R.WILDCARD or len(f) == 1
