@@ -266,3 +266,50 @@ def test_egress_world_and_all_entities():
         if "toPorts" in rule:   # one selector on 80/TCP (world, or all)
             f = rp._l4(A, False)[(80, 6)]
             assert f == R.WILDCARD or len(f) == 1
+
+
+def test_l4_policy():
+    # rule_test.go:110-315: L4 rules without peers select every identity;
+    # ProtoAny gives TCP and UDP; a rule that does not select the endpoint
+    # resolves to nothing
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    rule1 = {"endpointSelector": es("bar"),
+             "ingress": [{"toPorts": [{"ports": [{"port": "80", "protocol": "TCP"},
+                                                 {"port": "8080", "protocol": "TCP"}],
+                                       "rules": http}]}],
+             "egress": [{"toPorts": [{"ports": [{"port": "3000", "protocol": "ANY"}]}]}]}
+    rp = repo(rule1)
+    assert rp._l4(lbls("bar"), True) == {(80, 6): R.WILDCARD, (8080, 6): R.WILDCARD}
+    assert rp._l4(lbls("bar"), False) == {(3000, 6): R.WILDCARD, (3000, 17): R.WILDCARD}
+    assert rp._l4(lbls("foo"), True) == {} and rp._l4(lbls("foo"), False) == {}
+    rule2 = {"endpointSelector": es("bar"),
+             "ingress": [{"toPorts": tcp(80)}, {"toPorts": tcp(80, http)}],
+             "egress": [{"toPorts": [{"ports": [{"port": "3000", "protocol": "ANY"}]}]}]}
+    rp = repo(rule2)
+    assert rp._l4(lbls("bar"), True) == {(80, 6): R.WILDCARD}
+    assert rp._l4(lbls("bar"), False) == {(3000, 6): R.WILDCARD, (3000, 17): R.WILDCARD}
+
+
+def test_merge_l4_policy():
+    # rule_test.go:317-362 (ingress), 364-416 (egress): two rules' peers on
+    # one port merge, in rule order
+    for ingress in (True, False):
+        d, peers = ("ingress", "fromEndpoints") if ingress else ("egress", "toEndpoints")
+        rp = repo({"endpointSelector": es("bar"),
+                   d: [{peers: [es("foo")], "toPorts": tcp(80)},
+                       {peers: [es("baz")], "toPorts": tcp(80)}]})
+        assert rp._l4(lbls("bar"), ingress) == {(80, 6): [sel("foo"), sel("baz")]}
+
+
+def test_l4_wildcard_merge():
+    # rule_test.go:1870-2068: an L4-only rule (no peers, or the wildcard
+    # selector) on the port of an L3-dependent L7 rule, in either order,
+    # leaves the port open to every identity
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    l7 = {"fromEndpoints": [es("id=c")], "toPorts": tcp(80, http)}
+    for l4 in ({"toPorts": tcp(80)}, {"fromEndpoints": [WILD], "toPorts": tcp(80)}):
+        for pair in ((l7, l4), (l4, l7)):
+            rp = repo({"endpointSelector": es("id=a"), "ingress": list(pair)})
+            assert rp._l4(A, True) == {(80, 6): R.WILDCARD}
+            assert allows(rp, A, FOO, True, 80) is True
+            assert allows(rp, A, FOO, True, 90) is False
