@@ -313,3 +313,33 @@ def test_l4_wildcard_merge():
             assert rp._l4(A, True) == {(80, 6): R.WILDCARD}
             assert allows(rp, A, FOO, True, 80) is True
             assert allows(rp, A, FOO, True, 90) is False
+
+
+def test_prefixes_from_cidr():
+    # cidr_test.go:27-47 (getPrefixesFromCIDR: ip.ParseCIDRs, a bare address
+    # is a host prefix) — what the CIDR selectors' labels carry
+    # (labels.IPStringToLabel, pkg/labels/cidr.go:58-73)
+    for inp, want in (("0.0.0.0/0", "0.0.0.0/0"), ("192.0.2.3", "192.0.2.3/32"),
+                      ("192.0.2.3/32", "192.0.2.3/32"), ("192.0.2.3/24", "192.0.2.0/24"),
+                      ("192.0.2.0/24", "192.0.2.0/24"), ("::/0", "::/0"),
+                      ("fdff::ff", "fdff::ff/128")):
+        got = R.cidr_selectors([inp])
+        assert got[-1] == R.Selector(frozenset({f"cidr:{want}="})), inp
+        # (a /0 also selects reserved:world, once: api/cidr.go:70-86)
+        assert len(got) == (2 if want.endswith("/0") else 1)
+
+
+def test_get_cidr_prefixes():
+    # cidr_test.go:49-132 (GetCIDRPrefixes; the resolver keeps the set, the
+    # Go call lists every occurrence)
+    rp = repo({"endpointSelector": es("bar"),
+               "ingress": [{"fromCIDR": ["192.0.2.0/24"]}],
+               "egress": [{"toCIDR": ["192.0.2.0/24", "192.0.3.0/24"]}]})
+    assert set(rp.cidrs()) == {"192.0.2.0/24", "192.0.3.0/24"}
+    rp = repo({"endpointSelector": es("bar"),
+               "ingress": [{"fromCIDRSet": [{"cidr": "192.0.2.0/24",
+                                             "except": ["192.0.2.128/25"]}]}],
+               "egress": [{"toCIDRSet": [{"cidr": "10.0.0.0/8", "except": ["10.0.0.0/16"]}]}]})
+    assert set(rp.cidrs()) == {"192.0.2.0/25", "10.128.0.0/9", "10.64.0.0/10", "10.32.0.0/11",
+                               "10.16.0.0/12", "10.8.0.0/13", "10.4.0.0/14", "10.2.0.0/15",
+                               "10.1.0.0/16"}
