@@ -1,6 +1,6 @@
 """The C1 resolver (cilium_amd/policy_resolver.py) against the reference
-resolver's own known-answer tests, pkg/policy/repository_test.go and
-rule_test.go: the same rules, the same label contexts, the answers the Go
+resolver's own known-answer tests, pkg/policy/repository_test.go,
+rule_test.go, cidr_test.go and api/{entity,cidr}_test.go: the same rules, the same label contexts, the answers the Go
 tests assert.  The Go
 code cannot run here (no Go toolchain); these cases are its expected values,
 restated as data.
@@ -343,3 +343,31 @@ def test_get_cidr_prefixes():
     assert set(rp.cidrs()) == {"192.0.2.0/25", "10.128.0.0/9", "10.64.0.0/10", "10.32.0.0/11",
                                "10.16.0.0/12", "10.8.0.0/13", "10.4.0.0/14", "10.2.0.0/15",
                                "10.1.0.0/16"}
+
+
+def test_entities():
+    # api/entity_test.go:23-62 (EntityCluster does not select the host:
+    # an EndpointSelector cannot express OR)
+    host, cl, world, foo = (lbls("reserved:host"), lbls("reserved:cluster"),
+                            lbls("reserved:world"), lbls("id=foo"))
+    want = {"host": (True, False, False, False), "all": (True, True, True, True),
+            "cluster": (False, True, False, False), "world": (False, False, True, False)}
+    for e, w in want.items():
+        s = R.entity_selector(e)
+        assert tuple(s.matches(x) for x in (host, cl, world, foo)) == w, e
+    assert R.entity_selector("host").matches(lbls("reserved:host", "id=foo"))
+    sl = [R.entity_selector("host"), R.entity_selector("world")]
+    assert [any(s.matches(x) for s in sl) for x in (host, world, foo)] == [True, True, False]
+
+
+def test_cidr_endpoint_selectors():
+    # api/cidr_test.go:24-88: /0 matches all and brings reserved:world (once)
+    world = R.Selector(frozenset({"reserved:world="}))
+    v4, v6 = (R.Selector(frozenset({"cidr:0.0.0.0/0="})),
+              R.Selector(frozenset({"cidr:::/0="})))
+    assert R.cidr_selectors(["0.0.0.0/0"]) == [world, v4]
+    assert R.cidr_selectors(["::/0"]) == [world, v6]
+    assert R.cidr_selectors(["0.0.0.0/0", "::/0", "192.168.128.10/24"]) == \
+        [world, v4, v6, R.Selector(frozenset({"cidr:192.168.128.0/24="}))]
+    assert any(s.matches(lbls("reserved:world")) for s in R.cidr_selectors(["0.0.0.0/0"]))
+    assert R.cidr_selectors(["192.0.2.0/24"]) == [R.Selector(frozenset({"cidr:192.0.2.0/24="}))]
