@@ -19,6 +19,7 @@
 
 #include "../../include/cfc.h"
 #include "classify.hpp"
+#include "selfcut.hpp"
 #include "flatten.hpp"
 #include "maps.hpp"
 
@@ -2508,39 +2509,7 @@ int self_cuts(cfc_ctx *c, const Hdr &in, const cfc_out &out, int mode, uint16_t 
         hipStreamSynchronize(s) != hipSuccess)
         return -EIO;
     std::sort(rows.begin(), rows.end(), [](const uint4 &a, const uint4 &b) { return a.x < b.x; });
-    const uint32_t icmp = V6 ? 58 : 1;
-    std::set<uint64_t> l4;           // (proto, unordered ports) in the segment
-    bool any = false, svc = false, icmp_plain = false;
-    for (const uint4 &r : rows) {
-        const uint32_t proto = r.z & 0xFF, pt = r.y;
-        const bool lo = r.w >= n_own;   // a service or IPV4_LOOPBACK
-        const uint32_t type = pt & 0xFF;
-        const bool is_icmp = proto == icmp;
-        const bool err = is_icmp && (V6 ? (type >= 1 && type <= 4)
-                                        : (type == 3 || type == 11 || type == 12));
-        const uint64_t a = pt & 0xFFFF, b = pt >> 16;
-        const uint64_t key = (uint64_t)proto << 32 | std::min(a, b) << 16 | std::max(a, b);
-        const bool l4p = proto == 6 || proto == 17;
-        bool dep = false;
-        if (any) {
-            if (lo || svc || err)
-                dep = true;
-            else if (is_icmp)
-                dep = icmp_plain;
-            else if (l4p)
-                dep = l4.count(key) != 0;
-        }
-        if (dep) {
-            cuts->push_back(r.x);
-            l4.clear();
-            svc = icmp_plain = false;
-        }
-        any = true;
-        svc |= lo;
-        icmp_plain |= is_icmp && !err;
-        if (l4p)
-            l4.insert(key);
-    }
+    self_cut_rule(rows, n_own, V6, cuts);   // (selfcut.hpp)
     return 0;
 }
 

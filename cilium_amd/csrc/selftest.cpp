@@ -10,8 +10,54 @@
 #include <vector>
 
 #include "flatten.hpp"
+#include "selfcut.hpp"
 
 using namespace cfc;
+
+// the cut rule of an egress batch with traffic to itself (selfcut.hpp)
+struct Row {
+    uint32_t x, y, z, w;   // header index, L4 word, meta, address matched
+};
+static uint32_t ports(uint32_t sp, uint32_t dp) { return sp | dp << 16; }
+static int cuts_case(const char *name, const std::vector<Row> &rows, bool v6,
+                     const std::vector<uint64_t> &want)
+{
+    std::vector<uint64_t> got;
+    self_cut_rule(rows, 1, v6, &got);   // (address 0 the endpoint's own, 1 a loopback one)
+    const bool ok = got == want;
+    printf("selfcut %-24s %s (%zu cuts)\n", name, ok ? "ok" : "FAIL", got.size());
+    return ok ? 0 : 1;
+}
+static int selfcut_tests()
+{
+    const uint32_t TCP = 6, UDP = 17, ICMP = 1, ICMP6 = 58;
+    int fail = 0;
+    // an opening packet and its answer (ports swapped): cut at the answer
+    fail |= cuts_case("tcp-answer", {{3, ports(1000, 80), TCP, 0}, {9, ports(80, 1000), TCP, 0}},
+                      false, {9});
+    // a second packet of the same direction: also cut (conservative)
+    fail |= cuts_case("tcp-same-dir", {{3, ports(1000, 80), TCP, 0}, {5, ports(1000, 80), TCP, 0}},
+                      false, {5});
+    // two flows on other ports, or another protocol: one segment
+    fail |= cuts_case("tcp-unrelated", {{3, ports(1000, 80), TCP, 0}, {4, ports(1001, 80), TCP, 0},
+                                        {6, ports(80, 1000), UDP, 0}}, false, {});
+    // an ICMP error after anything: cut; echo after echo: cut; TCP after echo: none
+    fail |= cuts_case("icmp-error", {{1, ports(1000, 80), TCP, 0}, {2, 3, ICMP, 0}}, false, {2});
+    fail |= cuts_case("icmp-echo", {{1, 8, ICMP, 0}, {2, ports(1000, 80), TCP, 0}, {7, 0, ICMP, 0}},
+                      false, {7});
+    fail |= cuts_case("icmp6-error", {{1, ports(1000, 80), UDP, 0}, {2, 1, ICMP6, 0}}, true, {2});
+    // (IPv4 type 1 is no error: an ICMPv4 "other" after a TCP flow, none)
+    fail |= cuts_case("icmp4-type1", {{1, ports(1000, 80), TCP, 0}, {2, 1, ICMP, 0}}, false, {});
+    // a loopback address on either side: cut
+    fail |= cuts_case("loopback", {{1, ports(1000, 80), TCP, 1}, {2, ports(2000, 90), TCP, 0},
+                                   {3, ports(3000, 90), TCP, 1}}, false, {2, 3});
+    // a cut starts a new segment: a key of the segment before no longer counts
+    fail |= cuts_case("reset", {{1, ports(1000, 80), TCP, 0}, {2, ports(80, 1000), TCP, 0},
+                                {3, ports(2000, 80), TCP, 0}, {4, ports(1000, 80), TCP, 0}},
+                      false, {2, 4});
+    fail |= cuts_case("one-header", {{5, ports(1000, 80), TCP, 0}}, false, {});
+    return fail;
+}
 
 static uint32_t brute(const std::vector<Pfx6> &pfx, const uint32_t w[4])
 {
@@ -119,5 +165,6 @@ int main()
         fail |= run("exact128", v, rng, 20000);
         fail |= run("empty", std::vector<Pfx6>(), rng, 1000);
     }
+    fail |= selfcut_tests();
     return fail;
 }
