@@ -281,10 +281,11 @@ def main():
 
     rank, local_rank, world = env_rank()
     assert world == args.gpus, f"WORLD_SIZE {world} != --gpus {args.gpus}"
+    # (the rank's GPU first: RCCL's communicator binds to the current device)
+    torch.cuda.set_device(local_rank)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     mode = {"ingress": 0, "egress": 1, "xdp": 2, "full": 3}[args.mode]
     ep_lxc = S.EP_LXC_ID if mode == 1 else 0
