@@ -2333,17 +2333,65 @@ static void ct_create(cfo_t *o, const uint8_t k2[CTK], int alen, int dir,
  * the IPv4 egress lookup after NAT64, ipv6_policy's after NAT46), as
  * ct_apply does for a header's own stages; a NAT64 create carries nat46
  * (conntrack.h:714-716), an IPv6 ingress create its rev_nat_index
- * (bpf_lxc.c:787-788).  No load balancer on the hop. */
+ * (bpf_lxc.c:787-788). */
 static void apply_hop(cfo_t *o, int pass, size_t i, const struct hop *hp, uint8_t cs,
                       int32_t verdict, uint32_t len, int syn, uint8_t tfl, uint32_t sec,
-                      uint8_t *fresh)
+                      uint8_t *fresh, int svc_only)
 {
     (void)i;   /* fresh: this stage's "hit an entry the batch created" flag */
     const int alen = hp->alen, dir = hp->dir, is_tcp = hp->proto == 6;
     uint8_t k1[CTK], k2[CTK];
     int action;
     uint16_t td, ts;
-    if (ct_keys(alen, hp->owner, hp->sa, hp->da, hp->proto, hp->sport, hp->dport, syn, dir,
+    /* a NAT64 hop's IPv4 egress program runs its service step first
+     * (lb4_local, bpf_lxc.c:476-492, on the translated packet, tl_hash as the
+     * classify saw it): the hop's CT stage looks up (saddr, the service
+     * step's daddr), its create carries lb4_local's ct_state, and the
+     * CT_SERVICE entry is hit or created (ct_update4_slave) here too */
+    lbx_t x;
+    memset(&x, 0, sizeof(x));
+    uint8_t tda[16];
+    memcpy(tda, hp->da, 16);
+    uint16_t tsp = hp->sport, tdp = hp->dport;
+    int lbv = 0;
+    if (hp->kind == HOP_NAT64 && dir == CT_EGRESS && alen == 4 && o->lb4_n) {
+        uint32_t sa4, da4;
+        memcpy(&sa4, hp->sa, 4);
+        memcpy(&da4, hp->da, 4);
+        tl_pkt = (pkt4_t){sa4, da4, hp->sport, hp->dport};
+        lb4_egress(o, hp->owner, sa4, da4, hp->proto, syn, &x);
+        lbv = x.svc && !x.drop;
+        if (lbv) {
+            memcpy(tda, &x.t_da, 4);
+            tsp = tl_pkt.sport;
+            tdp = tl_pkt.dport;
+        }
+        if (pass == 2 && x.svc) {
+            uint8_t kk2[CTK];
+            int act;
+            uint16_t a_, b_;
+            (void)ct_keys(4, hp->owner, hp->sa, hp->da, hp->proto, hp->sport, hp->dport, syn,
+                          CT_SERVICE, x.k_svc, kk2, &act, &a_, &b_);
+            const uint8_t sfl = is_tcp ? tfl : 0;
+            if (x.svc_hit >= 0) {   /* __ct_lookup on the service entry */
+                ct_hit_update(o, &o->ct_ents[x.svc_hit], act, CT_SERVICE, is_tcp, syn, sfl,
+                              len);
+                if (x.reslave && !x.drop)   /* ct_update4_slave */
+                    o->ct_ents[x.svc_hit].slave = x.slave;
+            } else {
+                ctstate_t cs0 = {0, x.slave0, 0, 0, 0, 0};
+                ct_create(o, x.k_svc, 4, CT_SERVICE, len, 0, &cs0);
+                if (x.reslave && !x.drop) {
+                    int64_t ne = ct_find(o, x.k_svc);
+                    if (ne >= 0)
+                        o->ct_ents[ne].slave = x.slave;
+                }
+            }
+        }
+    }
+    if (svc_only)   /* (lb4_local found no backend: DROP_NO_SERVICE, no CT stage) */
+        return;
+    if (ct_keys(alen, hp->owner, hp->sa, tda, hp->proto, tsp, tdp, syn, dir,
                 k1, k2, &action, &td, &ts) < 0)
         return;
     const int b = cs & 3;
@@ -2384,6 +2432,8 @@ static void apply_hop(cfo_t *o, int pass, size_t i, const struct hop *hp, uint8_
             ctstate_t st = {alen == 16 && dir == CT_INGRESS
                                 ? (uint16_t)(hp->da[12] | hp->da[13] << 8) : 0,
                             0, 0, 0, 0, hp->kind == HOP_NAT64 && dir == CT_EGRESS};
+            if (lbv)   /* ct_state_new from lb4_local */
+                st = (ctstate_t){x.rev_nat, x.slave, x.loopback, x.addr, x.svc_addr, 1};
             ct_create(o, k2, alen, dir, len, sec, &st);
         }
     }
@@ -2533,6 +2583,16 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 dst = lxc_lookup(o, alen == 4 ? 1 : 2,
                                  alen == 4 ? (const uint8_t *)&pda4 : pda6);
             const uint8_t cs = (uint8_t)(c >> (4 * s));
+            if (s == 1 && !(cs & CTO_DONE1) && verdict[i] == DROP_NO_SERVICE && o->hop &&
+                i < o->hop_cap && o->hop[i].kind == HOP_NAT64) {
+                /* a NAT64 hop whose service step found no backend: its
+                 * CT_SERVICE entry was created (or hit) before the drop */
+                const struct hop *hp = &o->hop[i];
+                apply_hop(o, pass, i, hp, cs, verdict[i],
+                          (uint32_t)((int32_t)len[i] + hp->dlen),
+                          (flags[i] & HF_TCP_CLOSE) != 0, fl, 0, fresh + 2 * i + 1, 1);
+                continue;
+            }
             if (!(cs & CTO_DONE1))
                 continue;
             if (s == 1 && o->hop && i < o->hop_cap && o->hop[i].kind) {
@@ -2540,7 +2600,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                 const uint32_t hl = (uint32_t)((int32_t)len[i] + hp->dlen);
                 const uint32_t sec = mode == CFO_MODE_EGRESS ? o->seclabel[ep_lxc] : identity[i];
                 apply_hop(o, pass, i, hp, cs, verdict[i], hl, (flags[i] & HF_TCP_CLOSE) != 0,
-                          fl, sec, fresh + 2 * i + 1);
+                          fl, sec, fresh + 2 * i + 1, 0);
                 if (hp->has2 && (hp->ct2 & CTO_DONE1)) {
                     /* a NAT64 hop's local delivery: the destination's
                      * ipv4_policy lookup, after the hop's egress stage */
@@ -2552,7 +2612,7 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
                     memcpy(h2.sa, hp->sa2, 4);
                     memcpy(h2.da, hp->da2, 4);
                     apply_hop(o, pass, i, &h2, hp->ct2, verdict[i], hl,
-                              (flags[i] & HF_TCP_CLOSE) != 0, fl, sec, fresh3 + i);
+                              (flags[i] & HF_TCP_CLOSE) != 0, fl, sec, fresh3 + i, 0);
                 }
                 continue;
             }

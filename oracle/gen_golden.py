@@ -423,6 +423,11 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     # the first perf-ring record of the header reports it (get_hash_recalc,
     # what lb4_select_slave reduced), hash_ok = 0 where none was sent
     pktv = np.zeros((n, 3 if h.family == 4 else 9), np.uint32)
+    # IPv6 headers whose packet left as IPv4 (a NAT64 hop, bpf_lxc.c:1070-1083):
+    # (saddr, daddr, first L4 word) of that IPv4 packet — its daddr is what
+    # the IPv4 egress program's dstID derives from after a service step
+    pkt4 = np.zeros((n, 3), np.uint32)
+    pkt4_ok = np.zeros(n, np.uint8)
     hsh = np.zeros(n, np.uint32)
     hsh_ok = np.zeros(n, np.uint8)
     ev_hdr, ev_rec = [], []
@@ -468,6 +473,11 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
             pktv[i, 0], pktv[i, 1] = struct.unpack_from("<II", po, 14 + 12)
             if len(po) >= l4 + 4 and h.proto[i] in (6, 17):
                 pktv[i, 2] = struct.unpack_from("<I", po, l4)[0]
+        elif h.family == 6 and len(po) >= 14 + 20 and po[12:14] == b"\x08\x00":
+            pkt4[i, 0], pkt4[i, 1] = struct.unpack_from("<II", po, 14 + 12)
+            if len(po) >= 14 + 24 and h.proto[i] in (6, 17):
+                pkt4[i, 2] = struct.unpack_from("<I", po, 14 + 20)[0]
+            pkt4_ok[i] = 1
         elif h.family == 6 and len(po) >= 14 + 40:
             l4 = l4_offset(h, i)
             pktv[i, :8] = struct.unpack_from("<8I", po, 14 + 8)
@@ -483,7 +493,7 @@ def run(dp: RefDatapath, h: S.Headers, mode, ep_lxc=None):
     assert dp.ring.lost == 0, f"perf ring lost {dp.ring.lost} samples"
     ev = np.array(ev_rec, EV_DT) if ev_rec else np.zeros(0, EV_DT)
     return (action, verdict, ident, idmask, cbs, np.array(ev_hdr, np.uint32), ev,
-            clock, pktv, hsh, hsh_ok)
+            clock, pktv, hsh, hsh_ok, pkt4, pkt4_ok)
 
 
 def lpm_pin(ipc_map, h: S.Headers, pkt=None):
@@ -513,7 +523,7 @@ def lpm_pin(ipc_map, h: S.Headers, pkt=None):
 
 
 def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
-    action, verdict, ident, idmask, cbs, ev_hdr, ev, clock, pkt, hsh, hsh_ok = res
+    action, verdict, ident, idmask, cbs, ev_hdr, ev, clock, pkt, hsh, hsh_ok, pkt4, pkt4_ok = res
     extra = {}
     lb = getattr(t, "lb4", None) is not None or getattr(t, "lb6", None) is not None
     pk = None
@@ -527,6 +537,11 @@ def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
         # NAT64's IPv4 egress looks the v4-mapped destination's low 32 bits
         # up in the IPv4 ipcache (bpf_lxc.c:516-532 after :1070-1083)
         d4 = np.ascontiguousarray(np.asarray(h.daddr, np.uint8)[:, 12:16]).view("<u4").ravel()
+        if getattr(t, "lb4", None) is not None and pkt4_ok.any():
+            # (an IPv4 service step after the hop: the destination it left,
+            # the backend, bpf_lxc.c:476-501)
+            d4 = np.where(pkt4_ok != 0, pkt4[:, 1], d4).astype(np.uint32)
+            extra.update(x_pkt4=pkt4, x_pkt4_ok=pkt4_ok)
         h4 = S.Headers(4, d4, d4, h.sport, h.dport, h.proto, h.flags, h.length, h.mark)
         l4, k4 = lpm_pin(dp.L.maps["cilium_ipcache"], h4)
         extra.update(x_lpm_nat=l4[:, 1], x_lpm_nat_hit=k4[:, 1])
@@ -559,8 +574,9 @@ def save(name, t: S.Tables, h: S.Headers, mode, ep_lxc, res, dp):
         d[f"policy_{lxc}"] = pol
     for lxc, c in dp.policy_counters().items():
         d[f"x_counters_{lxc}"] = c
-    os.makedirs(GOLDEN, exist_ok=True)
-    path = os.path.join(GOLDEN, f"{name}.npz")
+    out_dir = GOLDEN + "_oracle" if name in ORACLE_ONLY else GOLDEN
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, f"{name}.npz")
     np.savez_compressed(path, **d)
     return path
 
@@ -1620,6 +1636,65 @@ def sc_nat46_egress_v6(n=3000, seed=61):
     return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
 
 
+def sc_nat64_lb_v6(n=2400, seed=67):
+    """Load-balanced NAT64 hops (an oracle-only fixture, tests/golden_oracle:
+    the engine was not run against it): IPv6 packets to v4-mapped IPv4
+    service VIPs leave through the IPv4 egress program (bpf_lxc.c:353-360 ->
+    tail_ipv6_to_ipv4 :1070-1083), whose service step (lb4_local,
+    :476-492) selects a backend, creates the CT_SERVICE entry and translates
+    the destination before ct_create4 writes the flow's entry (with nat46).
+    A history opens service flows; the test stream: their later packets, new
+    service flows of several packets, and plain NAT64 flows beside them."""
+    t, rng, ipc4 = _nat_setup(seed)
+    t.lb4, t.revnat4, vips, ports, protos = S.lb4_services(rng, t, loopback=False)
+
+    # (not the service whose backend slot lives only under the L3 key: every
+    # packet of its flows re-selects from its own skb->hash, which the
+    # reference's records do not carry for an untraced packet)
+    pick = np.flatnonzero(np.arange(len(vips)) != 5)
+
+    def svc64(k, base):
+        kk = pick[rng.integers(0, len(pick), size=k)]
+        h = _nat64_flows(rng, ipc4, k, base)
+        h.daddr = _mapped(vips[kk])
+        l4 = h.proto != S.IPPROTO_ICMPV6
+        h.proto[l4] = protos[kk][l4]
+        m = l4 & (ports[kk] != 0)
+        h.dport[m] = ports[kk][m]
+        h.tcpflags = np.where(h.proto == S.IPPROTO_TCP, 0x02, 0).astype(np.uint8)
+        return h
+    hist = S.concat([svc64(600, 20000), _nat64_flows(rng, ipc4, 200, 30000)])
+    dp = RefDatapath(t)
+    run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    parts, pos = [], []
+
+    def add(h, p):
+        parts.append(h)
+        pos.append(p)
+    est = S.take(hist, rng.integers(0, len(hist), size=int(n * 0.4)))
+    est.tcpflags = np.where(est.proto == S.IPPROTO_TCP,
+                            rng.choice(np.array([0x10, 0x18], np.uint8), size=len(est)), 0
+                            ).astype(np.uint8)
+    add(est, rng.random(len(est)))
+    new = svc64(int(n * 0.15), 40000)
+    at = rng.random(len(new)) * 0.9
+    add(new, at)
+    for f, p_ in ((0x10, 0.8), (0x18, 0.5)):
+        sel = np.flatnonzero(rng.random(len(new)) < p_)
+        h = S.take(new, sel)
+        h.tcpflags = np.where(h.proto == S.IPPROTO_TCP, f, 0).astype(np.uint8)
+        at = at + rng.random(len(new)) * 0.03
+        add(h, at[sel])
+    far = _nat64_flows(rng, ipc4, int(n * 0.1), 50000)
+    add(far, rng.random(len(far)))
+    h = S.concat(parts)
+    h = S.take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    h.hash = None
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
 def sc_nat46_reply_v4(n=3000, seed=63):
     """NAT46 in ipv4_policy (bpf_lxc.c:939-944, tail_ipv4_to_ipv6
     :1098-1110, nat46.h:236-328): IPv4 replies from the peers of NAT64'd
@@ -2060,7 +2135,11 @@ SCENARIOS = {
     "lb_reply_v6": sc_lb_reply_v6,
     "self_egress_v4": sc_self_egress,
     "self_egress_v6": sc_self_egress_v6,
+    "nat64_lb_v6": sc_nat64_lb_v6,
 }
+# fixtures that pin only the oracle (tests/golden_oracle): the engine has
+# not been run against them on the GPU
+ORACLE_ONLY = {"nat64_lb_v6"}
 
 
 def main(names):

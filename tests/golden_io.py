@@ -8,11 +8,19 @@ import oracle as O
 from cilium_amd import synth as S
 
 GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# fixtures that pin only the oracle: streams the engine has not been run
+# against on the GPU (the GPU tests take names(), golden/ alone)
+ORACLE_ONLY_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden_oracle")
 
 
 def names():
     return sorted(os.path.basename(p)[:-4]
                   for p in glob.glob(os.path.join(GOLDEN_DIR, "*.npz")))
+
+
+def oracle_only_names():
+    return sorted(os.path.basename(p)[:-4]
+                  for p in glob.glob(os.path.join(ORACLE_ONLY_DIR, "*.npz")))
 
 
 class Golden:
@@ -27,7 +35,10 @@ class Golden:
 
     def __init__(self, name):
         self.name = name
-        d = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+        path = os.path.join(GOLDEN_DIR, name + ".npz")
+        if not os.path.exists(path):
+            path = os.path.join(ORACLE_ONLY_DIR, name + ".npz")
+        d = np.load(path, allow_pickle=False)
         self.mode = int(d["mode"])
         self.ep_lxc = int(d["ep_lxc"])
         policy = {int(k.split("_")[1]): d[k] for k in d.files
@@ -84,6 +95,10 @@ class Golden:
         # IPv4 egress lookup of a v4-mapped destination
         self.lpm_nat = d["x_lpm_nat"] if "x_lpm_nat" in d.files else None
         self.lpm_nat_hit = d["x_lpm_nat_hit"] if "x_lpm_nat_hit" in d.files else None
+        # (IPv6 fixtures with IPv4 services) the IPv4 packet a NAT64 hop left:
+        # (saddr, daddr, L4 word) after the IPv4 program's service step
+        self.pkt4 = d["x_pkt4"] if "x_pkt4" in d.files else None
+        self.pkt4_ok = d["x_pkt4_ok"].astype(bool) if "x_pkt4_ok" in d.files else None
         # what the reference reported itself (perf-ring records, drop cb[],
         # proxy map); identity / idmask below add the identities derived
         # from the kernel's LPM for every other tc-path header
@@ -170,6 +185,8 @@ def lpm_identity(g: Golden):
         if nat.any() and g.lpm_nat is not None:
             d4 = np.ascontiguousarray(np.asarray(g.headers.daddr, np.uint8)[:, 12:16]
                                       ).view("<u4").ravel()
+            if g.pkt4 is not None:   # the service step's backend (bpf_lxc.c:476-501)
+                d4 = np.where(g.pkt4_ok, g.pkt4[:, 1], d4).astype(np.uint32)
             l4, h4 = g.lpm_nat.astype(np.uint32), g.lpm_nat_hit.astype(bool)
             e4 = np.where(h4 & (l4 != 0), l4,
                           np.where((d4 & 0xFF0000) == 0x100000, S.CLUSTER_ID, S.WORLD_ID))

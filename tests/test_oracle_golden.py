@@ -8,7 +8,8 @@ import golden_io as G
 import oracle as O
 from cilium_amd import synth as S
 
-NAMES = G.names()
+# (the oracle-only fixtures too: tests/golden_oracle, golden_io.ORACLE_ONLY_DIR)
+NAMES = G.names() + G.oracle_only_names()
 
 
 def test_have_goldens():
