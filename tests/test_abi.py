@@ -41,6 +41,23 @@ def test_no_gpu_means_no_datapath():
     assert e.value.errno == errno.ENODEV
 
 
+def test_stats_layout():
+    """cfc_stats as the binding lays it out: cfc.h's fields in order, the
+    ABI-13 field (ct_self_segments) last, the u64 totals 8-byte aligned;
+    before the first commit (a host-only context never has one) the call
+    returns -ENOENT"""
+    txt = open(os.path.join(ROOT, "include", "cfc.h")).read()
+    body = txt[txt.index("uint64_t epoch;"):txt.index("} cfc_stats;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"^\s*u?int\d+_t\s+(\w+);", body, flags=re.M)
+    assert [f for f, _ in _lib.Stats._fields_] == names
+    assert names[-1] == "ct_self_segments"
+    for f, t in _lib.Stats._fields_:
+        if t is ctypes.c_uint64:
+            assert getattr(_lib.Stats, f).offset % 8 == 0, f
+    assert errno_of(C.host_only().stats) == errno.ENOENT
+
+
 def test_options_on_host_only_context():
     """The ipcache layout is a table option (it applies at the next commit);
     timing needs a device."""
