@@ -1411,10 +1411,13 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
  * (:1098-1110) — ipv4_to_ipv6 (nat46.h:236-328): saddr NAT46_PREFIX/96 +
  * the IPv4 source, daddr the endpoint's LXC_IP, ICMP as ICMPv6 — then
  * tail_ipv6_policy on the translated packet with the source identity of
- * the IPv4 path (cb[CB_SRC_LABEL]); its CT lookup is stage 1 */
+ * the IPv4 path (cb[CB_SRC_LABEL]); its CT lookup is the stage after the
+ * IPv4 one: 1 behind from-netdev, 2 (tl_ct3, struct hop ct2, has2 = 2)
+ * behind an egress batch's local delivery (ipv4_local_delivery, l3.h:103-131,
+ * whose ipv4_policy lookup is stage 1) */
 static res_t nat46_ingress(cfo_t *o, const epinfo *ep, uint32_t src, uint32_t sa4,
                            uint8_t proto, uint16_t sport, uint16_t dport, int close,
-                           uint32_t len, int skip_proxy)
+                           uint32_t len, int skip_proxy, int stage)
 {
     uint16_t sp = sport;
     const uint8_t p6 = proto == IPPROTO_ICMP ? IPPROTO_ICMPV6 : proto;
@@ -1426,6 +1429,7 @@ static res_t nat46_ingress(cfo_t *o, const epinfo *ep, uint32_t src, uint32_t sa
     memcpy(da6, o->ep_v6[ep->lxc_id], 16);
     tl_hop = (struct hop){HOP_NAT46, 16, p6, CT_INGRESS, ct_owner(o, ep->lxc_id), sp, dport,
                           {0}, {0}, 20, 0, 0, 0, 0, 0, {0}, {0}};
+    tl_hop.has2 = stage == 2 ? 2 : 0;
     memcpy(tl_hop.sa, sa6, 16);
     memcpy(tl_hop.da, da6, 16);
     memcpy(tl_pkt6.sa, sa6, 16);
@@ -1433,7 +1437,7 @@ static res_t nat46_ingress(cfo_t *o, const epinfo *ep, uint32_t src, uint32_t sa
     tl_pkt6.sport = sp;
     tl_pkt6.dport = dport;
     return lxc_ingress(o, ep, src, 16, sa6, da6, p6, sp, dport, 0, close, len + 20,
-                       skip_proxy, METRIC_INGRESS, 1);
+                       skip_proxy, METRIC_INGRESS, stage);
 }
 
 static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
@@ -1477,7 +1481,8 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     if (alen == 4 && tl_nat == NAT46 && o->ep_has6[ep->lxc_id]) {
         uint32_t sa4;
         memcpy(&sa4, sa, 4);
-        return nat46_ingress(o, ep, src, sa4, proto, sport, dport, close, len, skip_proxy);
+        return nat46_ingress(o, ep, src, sa4, proto, sport, dport, close, len, skip_proxy,
+                             stage < 2 ? stage + 1 : 2);   /* (tl_mon[3]) */
     }
     /* (:808-815) any hit whose entry carries a rev_nat_index: the packet's
      * source from cilium_lb6_reverse_nat, when it holds the index */
@@ -1809,6 +1814,7 @@ void cfo_classify_v4(cfo_t *o, int mode, uint16_t ep_lxc, size_t n,
         }
         if (o->notify_mon)   /* both stages' monitor lengths (ct_apply) */
             o->notify_mon[i] = tl_mon[0] | tl_mon[1] << 16;
+        tl_hop.ct2 = tl_hop.has2 ? tl_ct3 : 0;
         o->hop[i] = tl_hop;
         if (o->pkt_out) {
             o->pkt_out[3 * i] = tl_pkt.sa;
@@ -2595,7 +2601,19 @@ static void ct_apply(cfo_t *o, int alen, int mode, uint16_t ep_lxc, size_t n,
             }
             if (!(cs & CTO_DONE1))
                 continue;
-            if (s == 1 && o->hop && i < o->hop_cap && o->hop[i].kind) {
+            if (s == 1 && o->hop && i < o->hop_cap && o->hop[i].kind == HOP_NAT46 &&
+                o->hop[i].has2 == 2) {
+                /* NAT46 behind an egress batch's local delivery: the hop's
+                 * IPv6 stage is a third one (its keys are IPv6, the
+                 * destination's ipv4_policy stage below IPv4, so their order
+                 * within the header does not matter) */
+                const struct hop *hp = &o->hop[i];
+                if (hp->ct2 & CTO_DONE1)
+                    apply_hop(o, pass, i, hp, hp->ct2, verdict[i],
+                              (uint32_t)((int32_t)len[i] + hp->dlen),
+                              (flags[i] & HF_TCP_CLOSE) != 0, fl, o->seclabel[ep_lxc],
+                              fresh3 + i, 0);
+            } else if (s == 1 && o->hop && i < o->hop_cap && o->hop[i].kind) {
                 const struct hop *hp = &o->hop[i];
                 const uint32_t hl = (uint32_t)((int32_t)len[i] + hp->dlen);
                 const uint32_t sec = mode == CFO_MODE_EGRESS ? o->seclabel[ep_lxc] : identity[i];

@@ -1809,6 +1809,60 @@ def sc_nat64_local_v6(n=2400, seed=65):
     return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
 
 
+def sc_nat46_self_v4(n=1600, seed=69):
+    """NAT46 behind an IPv4 egress batch's local delivery (an oracle-only
+    fixture, tests/golden_oracle: the engine was not run against it): the
+    endpoint's NAT64 flows to its own IPv4 address (::ffff:LXC_IPV4,
+    delivered to itself by the IPv4 egress program) are answered by IPv4
+    packets LXC_IPV4 -> LXC_IPV4; the egress program delivers them locally
+    (ipv4_local_delivery, l3.h:103-131), the destination's ipv4_policy finds
+    the flow's nat46 entry (conntrack.h:241-244) and tail_ipv4_to_ipv6
+    (bpf_lxc.c:939-944, :1098-1110) hands the translated packet to
+    ipv6_policy, whose ct_lookup6 / ct_create6 is a third CT stage.  The
+    test stream: replies of several packets per flow and plain IPv4 egress
+    traffic beside them."""
+    t, rng, ipc4 = _nat_setup(seed)
+    a4 = np.uint32(S.LXC_IPV4)
+    sec = int(t.seclabel[S.EP_LXC_ID])
+    # the endpoint admits its own identity on the flows' ports (ingress)
+    pol = t.policy[S.EP_LXC_ID]
+    add = np.zeros(4, S.POLICY_DT)
+    add["identity"] = sec
+    add["dport"] = S.htons(np.array([80, 53, 443, 0]))
+    add["proto"] = [S.IPPROTO_TCP, S.IPPROTO_UDP, S.IPPROTO_TCP, 0]
+    t.policy[S.EP_LXC_ID] = np.concatenate([pol, add])
+    hist = _nat64_flows(rng, ipc4, 500, 20000)
+    hist.daddr = _mapped(np.full(len(hist), a4))
+    hist.hash = None
+    dp = RefDatapath(t)
+    hres = run(dp, hist, MODE_EGRESS, S.EP_LXC_ID)
+    t.ct = S.ct_from_rows(dp.ct_dump())
+    dp.reset_counters()
+    ok = np.flatnonzero((hist.proto != S.IPPROTO_ICMPV6) & (hres[0] != 2))
+    parts, pos = [], []
+    at = rng.random(len(ok)) * 0.9
+    for f, p_ in ((0x12, 1.0), (0x10, 0.7), (0x18, 0.5)):
+        sel = np.flatnonzero(rng.random(len(ok)) < p_)
+        src = S.take(hist, ok[sel])
+        k = len(sel)
+        rep = S.Headers(4, np.full(k, a4, np.uint32), np.full(k, a4, np.uint32),
+                        src.dport.copy(), src.sport.copy(), src.proto.copy(),
+                        np.zeros(k, np.uint8), rng.integers(60, 1500, size=k).astype(np.uint16),
+                        np.zeros(k, np.uint32),
+                        np.where(src.proto == S.IPPROTO_TCP, f, 0).astype(np.uint8))
+        parts.append(rep)
+        pos.append(at[sel])
+        at = at + rng.random(len(ok)) * 0.03
+    plain = S.gen_headers_v4(rng, int(n * 0.2), ipc4, S.local_v4_addrs(t)[:1], local_frac=0.0,
+                             mark_host=0, mark_proxy=0, frag=0, src_fixed=S.LXC_IPV4)
+    parts.append(plain)
+    pos.append(rng.random(len(plain)))
+    h = S.concat(parts)
+    h = S.take(h, np.argsort(np.concatenate(pos), kind="stable"))
+    h.hash = None
+    return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
+
+
 def _hdrs4(sa, da, sp, dp, proto, tcpf, length):
     n = len(sp)
     tcpf = np.asarray(tcpf, np.uint8)
@@ -2136,10 +2190,11 @@ SCENARIOS = {
     "self_egress_v4": sc_self_egress,
     "self_egress_v6": sc_self_egress_v6,
     "nat64_lb_v6": sc_nat64_lb_v6,
+    "nat46_self_v4": sc_nat46_self_v4,
 }
 # fixtures that pin only the oracle (tests/golden_oracle): the engine has
 # not been run against them on the GPU
-ORACLE_ONLY = {"nat64_lb_v6"}
+ORACLE_ONLY = {"nat64_lb_v6", "nat46_self_v4"}
 
 
 def main(names):
