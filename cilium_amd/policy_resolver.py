@@ -20,6 +20,10 @@ Restated (file:line in /root/reference):
     CIDR identity labels                        pkg/labels/cidr.go, pkg/labels/cidr/cidr.go:33-70
   * an L7 port's filter also takes the peers    pkg/policy/repository.go:127-234
     of L3-only and L3/L4 rules (wildcardL3L4Rules)
+  * Rule.Sanitize (the errors a rule is         pkg/policy/api/rule_validation.go
+    refused with) and net.ParseCIDR / ParseIP
+  * the CIDR policy and its prefix-length       pkg/policy/rule.go:279-345,
+    counts (class masks for bare addresses)     l3.go:66-96, repository.go:340-353
 
 Not restated (they need services the reference's agent talks to): toFQDNs
 (DNS proxy), toServices (Kubernetes endpoints), the L7 rules' contents and
@@ -167,9 +171,13 @@ class Rule:
     name: str = ""
 
 
-def parse_rules(objs, origin="") -> list:
+def parse_rules(objs, origin="", sanitize=True) -> list:
+    """api.Rules -> the repository's rules, each checked by Rule.Sanitize
+    first (PolicyError), as the agent's policy import does."""
     rules = []
     for r in objs:
+        if sanitize:
+            sanitize_rule(r)
         name = ",".join(f"{x['key']}={x['value']}" for x in r.get("labels", []))
         rules.append(Rule(Selector.parse(r.get("endpointSelector")),
                           r.get("ingress", []) or [], r.get("egress", []) or [],
@@ -194,6 +202,218 @@ def load_fixture(path) -> list:
     return out
 
 
+# ------------------------------------------------------------- validation
+class PolicyError(ValueError):
+    """An error of Rule.Sanitize (pkg/policy/api/rule_validation.go): the
+    rule is refused before it reaches the repository."""
+
+
+MAX_PORTS = 40                  # rule_validation.go:27
+MAX_CIDR_PREFIX_LENGTHS = 40    # :29
+L4_PROTOS = ("TCP", "UDP", "ANY")
+
+
+def go_parse_ip(s: str):
+    """net.ParseIP: a dotted IPv4 address or an IPv6 address (no zone, no
+    mask) -> ipaddress object, or None."""
+    if not isinstance(s, str) or "%" in s or "/" in s:
+        return None
+    try:
+        return ipaddress.ip_address(s)
+    except ValueError:
+        return None
+
+
+def go_parse_cidr(s: str):
+    """net.ParseCIDR: <address>/<decimal prefix length within the family's
+    bits> -> the network (host bits cleared), or None.  (No netmask
+    notation: Go reads the part after '/' as a decimal length only.)"""
+    if not isinstance(s, str):
+        return None
+    addr, sep, plen = s.partition("/")
+    if not sep or not plen or not all("0" <= ch <= "9" for ch in plen):
+        return None
+    ip = go_parse_ip(addr)
+    if ip is None or int(plen) > (32 if ip.version == 4 else 128):
+        return None
+    return ipaddress.ip_network(f"{addr}/{int(plen)}", strict=False)
+
+
+def parse_port(port) -> int:
+    """PortProtocol.sanitize's port (rule_validation.go:309-321):
+    strconv.ParseUint(port, 0, 16) — decimal, 0x hex or 0 octal — not 0."""
+    t = str(port) if port is not None else ""
+    if t == "":
+        raise PolicyError("Port must be specified")
+    base, digits = 10, t
+    if t[:2] in ("0x", "0X"):
+        base, digits = 16, t[2:]
+    elif len(t) > 1 and t[0] == "0":
+        base, digits = 8, t[1:]
+    ok = "0123456789abcdef"[:base]
+    if not digits or any(ch.lower() not in ok for ch in digits) or int(digits, base) > 0xFFFF:
+        raise PolicyError(f"Unable to parse port: {t}")
+    v = int(digits, base)
+    if v == 0:
+        raise PolicyError("Port cannot be 0")
+    return v
+
+
+def parse_l4_proto(proto) -> str:
+    """ParseL4Proto (api/utils.go:103-110): upper-cased, empty is ANY."""
+    p = (proto or "").upper()
+    if p == "":
+        return "ANY"
+    if p not in L4_PROTOS:
+        raise PolicyError(f"invalid protocol {proto!r}, only {'/'.join(L4_PROTOS)} allowed")
+    return p
+
+
+def cidr_sanitize(c) -> int:
+    """CIDR.sanitize (rule_validation.go:333-356): a prefix, or a bare
+    address (prefix length 0 returned)."""
+    if not c:
+        raise PolicyError("IP must be specified")
+    n = go_parse_cidr(c)
+    if n is not None:
+        return n.prefixlen
+    if go_parse_ip(c) is None:
+        raise PolicyError(f"Unable to parse CIDR: {c}")
+    return 0
+
+
+def cidr_rule_sanitize(r: dict) -> int:
+    """CIDRRule.sanitize (rule_validation.go:361-395): <address>/<prefix>
+    only, every exception's address inside it (same family)."""
+    n = go_parse_cidr(r.get("cidr", ""))
+    if n is None:
+        raise PolicyError(f"Unable to parse CIDRRule {r.get('cidr', '')!r}")
+    for ex in r.get("except", []) or []:
+        e = go_parse_cidr(ex)
+        if e is None:
+            raise PolicyError(f"invalid CIDR address: {ex}")
+        if e.version != n.version or e.network_address not in n:
+            raise PolicyError(f"allow CIDR prefix {r['cidr']} does not contain "
+                              f"exclude CIDR prefix {ex}")
+    return n.prefixlen
+
+
+def _l7_sanitize(rules: dict):
+    """L7Rules.sanitize (rule_validation.go:248-285): HTTP method / path
+    regular expressions compile (Python's re stands in for Go's RE2), key
+    / value rules need a parser and no empty key (l7.go:27-33), one L7 type
+    per rule.  (Kafka: API key and role exclusive; the key / role tables
+    are not restated.)"""
+    import re
+    n = 0
+    if rules.get("http") is not None:
+        n += 1
+        for h in rules["http"]:
+            for f in ("path", "method"):
+                if h.get(f):
+                    try:
+                        re.compile(h[f])
+                    except re.error as e:
+                        raise PolicyError(str(e)) from None
+    if rules.get("kafka") is not None:
+        n += 1
+        for k in rules["kafka"]:
+            if k.get("apiKey") and k.get("role"):
+                raise PolicyError(f"Cannot set both Role:{k['role']!r} and "
+                                  f"APIKey :{k['apiKey']!r} together")
+    if rules.get("l7") is not None and not rules.get("l7proto"):
+        raise PolicyError("'l7' may only be specified when a 'l7proto' is also specified")
+    if rules.get("l7proto"):
+        n += 1
+        for kv in rules.get("l7") or []:
+            if any(k == "" for k in kv):
+                raise PolicyError("Empty key not allowed")
+    if n > 1:
+        raise PolicyError("multiple L7 protocol rule types specified in single rule")
+
+
+def _l7_empty(rules) -> bool:
+    """L7Rules.IsEmpty (api/l4.go:97-99)."""
+    return not rules or all(rules.get(k) is None for k in ("http", "kafka", "l7"))
+
+
+def _port_rule_sanitize(pr: dict):
+    """PortRule.sanitize (rule_validation.go:287-307)."""
+    ports = pr.get("ports", []) or []
+    if len(ports) > MAX_PORTS:
+        raise PolicyError(f"too many ports, the max is {MAX_PORTS}")
+    l7 = not _l7_empty(pr.get("rules"))
+    for p in ports:
+        parse_port(p.get("port"))
+        proto = parse_l4_proto(p.get("protocol"))
+        if l7 and proto != "TCP":
+            raise PolicyError(f"L7 rules can only apply exclusively to TCP, not {proto}")
+    if l7:
+        _l7_sanitize(pr["rules"])
+
+
+_L3_MEMBERS = {True: (("fromEndpoints", True), ("fromCIDR", False), ("fromCIDRSet", False),
+                      ("fromEntities", True)),
+               False: (("toCIDR", True), ("toCIDRSet", True), ("toEndpoints", True),
+                       ("toEntities", True), ("toServices", True), ("toFQDNs", True))}
+
+
+def _direction_sanitize(x: dict, ingress: bool):
+    """IngressRule / EgressRule .sanitize (rule_validation.go:67-198)."""
+    members = [(k, l4ok) for k, l4ok in _L3_MEMBERS[ingress] if x.get(k)]
+    if len(members) > 1:
+        raise PolicyError(f"Combining {members[0][0]} and {members[1][0]} is not supported yet")
+    tps = x.get("toPorts") or []
+    for k, l4ok in members:
+        if tps and not l4ok:
+            raise PolicyError(f"Combining {k} and ToPorts is not supported yet")
+    for pr in tps:
+        _port_rule_sanitize(pr)
+    p = "from" if ingress else "to"
+    lengths = {cidr_sanitize(c) for c in x.get(f"{p}CIDR", []) or []}
+    lengths |= {cidr_rule_sanitize(c) for c in x.get(f"{p}CIDRSet", []) or []}
+    for e in x.get(f"{p}Entities", []) or []:
+        if entity_selector(e) is None:
+            raise PolicyError(f"unsupported entity: {e}")
+    if len(lengths) > MAX_CIDR_PREFIX_LENGTHS:
+        raise PolicyError(f"too many {'ingress' if ingress else 'egress'} CIDR prefix lengths "
+                          f"{len(lengths)}/{MAX_CIDR_PREFIX_LENGTHS}")
+
+
+def sanitize_rule(r: dict):
+    """Rule.Sanitize (rule_validation.go:37-65): raises PolicyError."""
+    for lb in r.get("labels", []) or []:
+        if lb.get("source") == "cilium-generated":
+            raise PolicyError("rule labels cannot have cilium-generated source")
+    if r.get("endpointSelector") is None:
+        raise PolicyError("rule cannot have nil EndpointSelector")
+    for x in r.get("ingress", []) or []:
+        _direction_sanitize(x, True)
+    for x in r.get("egress", []) or []:
+        _direction_sanitize(x, False)
+
+
+def cidr_policy_key(c: str):
+    """CIDRPolicyMap.Insert's prefix (pkg/policy/l3.go:66-96): a prefix as
+    given, or a bare address with its class mask (/8, /16, /24) when the
+    bits after it are zero, else the full mask -> (key, family, length)."""
+    n = go_parse_cidr(c)
+    if n is None:
+        ip = go_parse_ip(c)
+        if ip is None:
+            raise PolicyError(f"Unable to parse CIDR: {c}")
+        if ip.version == 6 and ip.ipv4_mapped is not None:
+            ip = ip.ipv4_mapped   # (ip.To4())
+        if ip.version == 6:
+            n = ipaddress.ip_network(f"{ip}/128")
+        else:
+            b0 = int(ip) >> 24   # net.IP.DefaultMask
+            cls = 8 if b0 < 0x80 else 16 if b0 < 0xC0 else 24
+            m = ipaddress.ip_network(f"{ip}/{cls}", strict=False)
+            n = m if m.network_address == ip else ipaddress.ip_network(f"{ip}/32")
+    return f"{n.network_address}/{n.prefixlen}", n.version, n.prefixlen
+
+
 # ------------------------------------------------------------- repository
 class Repository:
     def __init__(self, rules, always_allow_localhost=True, host_allows_world=True):
@@ -214,6 +434,31 @@ class Repository:
                 out += rule_cidrs(x, False)
         return sorted(set(out), key=lambda c: (ipaddress.ip_network(c).network_address,
                                                ipaddress.ip_network(c).prefixlen))
+
+    def cidr_policy(self, subject) -> dict:
+        """ResolveCIDRPolicy (repository.go:340-353, rule.go:279-345): the
+        CIDR prefixes of the rules selecting `subject` — ingress L3-only
+        rules (CIDR + L4 is mergeL4Ingress's), egress every rule — with the
+        per-family prefix-length counts that size the datapath's prefix
+        list: {"ingress"|"egress": {"map": {key: (family, length)},
+        "v4": {length: n}, "v6": {length: n}}}."""
+        out = {}
+        for d, ingress in (("ingress", True), ("egress", False)):
+            m, cnt = {}, {4: {}, 6: {}}
+            for r in self.rules:
+                if not r.selector.matches(subject):
+                    continue
+                for x in (r.ingress if ingress else r.egress):
+                    cs = rule_cidrs(x, ingress)
+                    if ingress and cs and (x.get("toPorts") or []):
+                        continue
+                    for c in cs:
+                        key, fam, ln = cidr_policy_key(c)
+                        if key not in m:
+                            m[key] = (fam, ln)
+                            cnt[fam][ln] = cnt[fam].get(ln, 0) + 1
+            out[d] = {"map": m, "v4": cnt[4], "v6": cnt[6]}
+        return out
 
     def enabled(self, lbls):
         """GetRulesMatching (repository.go:624-643)."""
@@ -264,7 +509,7 @@ class Repository:
                 if protos[0] == "ANY":
                     protos = ["TCP", "UDP"]
                 for proto in protos:
-                    yield (int(p["port"]), PROTO[proto])
+                    yield (parse_port(p["port"]), PROTO[proto])
         for r in self.rules:
             if not r.selector.matches(subject):
                 continue

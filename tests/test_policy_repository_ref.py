@@ -1,7 +1,8 @@
 """The C1 resolver (cilium_amd/policy_resolver.py) against the reference
 resolver's own known-answer tests, pkg/policy/repository_test.go,
-rule_test.go, cidr_test.go and api/{entity,cidr}_test.go: the same rules, the same label contexts, the answers the Go
-tests assert.  The Go
+rule_test.go, cidr_test.go and api/{entity,cidr,rule_validation}_test.go:
+the same rules, the same label contexts, the answers the Go tests assert
+(a Go error is a PolicyError).  The Go
 code cannot run here (no Go toolchain); these cases are its expected values,
 restated as data.
 
@@ -17,6 +18,8 @@ API's, not the datapath's: the Go call answers Denied for an endpoint no
 rule selects, while that endpoint's policymap allows every identity
 (pkg/endpoint/policy.go: policy enforcement off), which is what the resolver
 computes; those cases check `enabled`."""
+import pytest
+
 from cilium_amd import policy_resolver as R
 
 
@@ -371,3 +374,128 @@ def test_cidr_endpoint_selectors():
         [world, v4, v6, R.Selector(frozenset({"cidr:192.168.128.0/24="}))]
     assert any(s.matches(lbls("reserved:world")) for s in R.cidr_selectors(["0.0.0.0/0"]))
     assert R.cidr_selectors(["192.0.2.0/24"]) == [R.Selector(frozenset({"cidr:192.0.2.0/24="}))]
+
+
+def test_rule_can_reach_entities():
+    # rule_test.go:1067-1111 (ingress from world / cluster), 1113-1157
+    # (egress to them): the entities allow, another peer is undecided
+    for ingress in (True, False):
+        d, ent = ("ingress", "fromEntities") if ingress else ("egress", "toEntities")
+        rp = repo({"endpointSelector": es("bar"), d: [{ent: ["world", "cluster"]}]})
+        for peer, ok in ((lbls("reserved:world"), True), (lbls("reserved:cluster"), True),
+                         (lbls("foo"), False)):
+            assert rp._can_reach(lbls("bar"), peer, ingress) is ok
+
+
+def test_l3_policy():
+    # rule_test.go:887-1018: the CIDR policy of the rule selecting bar — a
+    # bare IPv4 address takes its class mask when the bits after it are zero
+    # (192.168.2.0 -> /24), else /32; a bare IPv6 address /128; a CIDRSet
+    # its exceptions removed — and the prefix-length counts
+    rule = {"endpointSelector": es("bar"),
+            "ingress": [{"fromCIDR": ["10.0.1.0/24", "192.168.2.0", "10.0.3.1",
+                                      "2001:db8::1/48", "2001:db9::"]}],
+            "egress": [{"toCIDR": ["10.1.0.0/16", "2001:dbf::/64"]},
+                       {"toCIDRSet": [{"cidr": "10.0.0.0/8", "except": ["10.96.0.0/12"]}]}]}
+    cp = repo(rule).cidr_policy(lbls("bar"))
+    assert cp["ingress"]["map"] == {"10.0.1.0/24": (4, 24), "192.168.2.0/24": (4, 24),
+                                    "10.0.3.1/32": (4, 32), "2001:db8::/48": (6, 48),
+                                    "2001:db9::/128": (6, 128)}
+    assert cp["ingress"]["v4"] == {32: 1, 24: 2} and cp["ingress"]["v6"] == {128: 1, 48: 1}
+    assert cp["egress"]["map"] == {"10.1.0.0/16": (4, 16), "10.128.0.0/9": (4, 9),
+                                   "10.0.0.0/10": (4, 10), "10.64.0.0/11": (4, 11),
+                                   "10.112.0.0/12": (4, 12), "2001:dbf::/64": (6, 64)}
+    assert cp["egress"]["v4"] == {16: 1, 12: 1, 11: 1, 10: 1, 9: 1}
+    assert cp["egress"]["v6"] == {64: 1}
+    # a rule that does not select the endpoint contributes nothing
+    assert repo(rule).cidr_policy(lbls("foo"))["ingress"]["map"] == {}
+    # Sanitize refuses: an unparsable CIDR, a CIDRSet without a cidr or with a
+    # bare address, an exception outside the cidr, a netmask, a length
+    # beyond the family's bits
+    bad = [{"fromCIDR": ["10.0.1..0/24"]}, {"fromCIDRSet": [{"cidr": ""}]},
+           {"fromCIDRSet": [{"cidr": "10.0.1.32"}]},
+           {"fromCIDRSet": [{"cidr": "10.0.0.0/10", "except": ["10.64.0.0/11"]}]},
+           {"fromCIDR": ["10.0.1.0/128.0.0.128"]}, {"fromCIDR": ["10.0.1.0/34"]}]
+    for x in bad:
+        with pytest.raises(R.PolicyError):
+            R.sanitize_rule({"endpointSelector": es("bar"), "ingress": [x]})
+    R.sanitize_rule({"endpointSelector": es("bar"),
+                     "ingress": [{"fromCIDRSet": [{"cidr": "10.0.1.0/24"}]}]})
+
+
+def test_l3_policy_restrictions():
+    # rule_test.go:1020-1041: 41 prefix lengths are too many, either way;
+    # :1043-1065: ToCIDR and ToEndpoints cannot combine
+    cidrs = [f"{i}::/{i}" for i in range(1, 42)]
+    for d, k in (("ingress", "fromCIDR"), ("egress", "toCIDR")):
+        with pytest.raises(R.PolicyError, match="too many"):
+            R.sanitize_rule({"endpointSelector": es("bar"), d: [{k: cidrs}]})
+        R.sanitize_rule({"endpointSelector": es("bar"), d: [{k: cidrs[:40]}]})
+    with pytest.raises(R.PolicyError, match="Combining"):
+        R.sanitize_rule({"endpointSelector": es("bar"),
+                         "egress": [{"toCIDR": ["10.1.0.0/16", "2001:dbf::/64"],
+                                     "toEndpoints": [es("foo")]}]})
+
+
+def test_entity_validation():
+    # rule_test.go:1159-1216: world and host pass, an unknown entity fails
+    for d, k in (("ingress", "fromEntities"), ("egress", "toEntities")):
+        for ents, ok in ((["world"], True), (["host"], True), (["trololo"], False),
+                         (["world", "host"], True)):
+            r = {"endpointSelector": es("bar"), d: [{k: ents}]}
+            if ok:
+                R.sanitize_rule(r)
+            else:
+                with pytest.raises(R.PolicyError, match="unsupported entity"):
+                    R.sanitize_rule(r)
+
+
+def _l7_rule(ports, rules):
+    return {"endpointSelector": WILD,
+            "ingress": [{"fromEndpoints": [WILD],
+                         "toPorts": [{"ports": [{"port": p, "protocol": q} for p, q in ports],
+                                      "rules": rules}]}]}
+
+
+def test_l7_rules_with_non_tcp_protocols():
+    # api/rule_validation_test.go:24-147
+    http = {"http": [{"method": "GET", "path": "/"}]}
+    R.sanitize_rule(_l7_rule([("80", "TCP"), ("81", "TCP")], http))
+    for ports, proto in (([("80", "UDP")], "UDP"), ([("80", "ANY")], "ANY"),
+                         ([("80", "TCP"), ("12345", "UDP")], "UDP"),
+                         ([("80", "UDP"), ("12345", "TCP")], "UDP")):
+        with pytest.raises(R.PolicyError) as e:
+            R.sanitize_rule(_l7_rule(ports, http))
+        assert str(e.value) == f"L7 rules can only apply exclusively to TCP, not {proto}"
+
+
+def test_http_rule_regexes_and_l7_rules():
+    # api/rule_validation_test.go:151-198 (regexes), 274-347 (key/value rules)
+    tcp2 = [("80", "TCP"), ("81", "TCP")]
+    for h in ({"method": "GET", "path": "*"}, {"method": "*", "path": "/"}):
+        with pytest.raises(R.PolicyError):
+            R.sanitize_rule(_l7_rule(tcp2, {"http": [h]}))
+    R.sanitize_rule(_l7_rule(tcp2, {"l7proto": "test.lineparser",
+                                    "l7": [{"method": "PUT", "path": "/"},
+                                           {"method": "GET", "path": "/"}]}))
+    R.sanitize_rule(_l7_rule(tcp2, {"l7proto": "test.lineparser"}))
+    with pytest.raises(R.PolicyError, match="Empty key"):
+        R.sanitize_rule(_l7_rule(tcp2, {"l7proto": "test.lineparser",
+                                        "l7": [{"method": "PUT", "": "Foo"}]}))
+
+
+def test_cidr_rule_sanitize():
+    # api/rule_validation_test.go:201-238: the prefix length, or an error
+    for c, n in (("0.0.0.0/0", 0), ("10.0.0.0/24", 24), ("192.0.2.3/32", 32), ("::/0", 0),
+                 ("ff02::/64", 64), ("2001:0db8:85a3:0000:0000:8a2e:0370:7334/128", 128)):
+        assert R.cidr_rule_sanitize({"cidr": c}) == n
+    with pytest.raises(R.PolicyError):
+        R.cidr_rule_sanitize({"cidr": "10.0.0.0/254.0.0.255"})
+
+
+def test_to_services_sanitize():
+    # api/rule_validation_test.go:240-271: ToServices with ToPorts is allowed
+    R.sanitize_rule({"endpointSelector": WILD,
+                     "egress": [{"toServices": [{"k8sServiceSelector": {
+                         "selector": {"matchLabels": {"app": "tested-service"}}}}],
+                                 "toPorts": tcp(80) + tcp(81)}]})
