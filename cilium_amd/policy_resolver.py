@@ -25,9 +25,12 @@ Restated (file:line in /root/reference):
   * the CIDR policy and its prefix-length       pkg/policy/rule.go:279-345,
     counts (class masks for bare addresses)     l3.go:66-96, repository.go:340-353
 
+  * L4 filters with their L7 parser and L7     pkg/policy/l4.go:52-223,
+    rules per peer selector, merge conflicts    rule.go:36-141
+
 Not restated (they need services the reference's agent talks to): toFQDNs
-(DNS proxy), toServices (Kubernetes endpoints), the L7 rules' contents and
-the proxy redirect (an L7 port's keys carry proxy port 0 here).  The
+(DNS proxy), toServices (Kubernetes endpoints), the evaluation of L7 rules
+and the proxy redirect (an L7 port's keys carry proxy port 0 here).  The
 reference resolver is Go and this image has no Go toolchain: rule selection,
 label access and L4 resolution are pinned to the reference's own
 known-answer tests (pkg/policy/repository_test.go, restated as data in
@@ -414,6 +417,94 @@ def cidr_policy_key(c: str):
     return f"{n.network_address}/{n.prefixlen}", n.version, n.prefixlen
 
 
+# ------------------------------------------------------------- L4 filters
+WILDCARD_SELECTOR = Selector()   # api.WildcardEndpointSelector
+
+
+def _selects_all(sels) -> bool:
+    """EndpointSelectorSlice.SelectsAllEndpoints (api/selector.go:356-369)."""
+    return not sels or any(s.selects_all() for s in sels)
+
+
+def _l7_len(rules) -> int:
+    """L7Rules.Len."""
+    return sum(len(rules.get(k) or []) for k in ("http", "kafka", "l7"))
+
+
+def _l7_norm(rules) -> dict:
+    """An L7Rules value: {http, kafka, l7: list or None (Go nil), l7proto}."""
+    r = rules or {}
+    return {"http": list(r["http"]) if r.get("http") is not None else None,
+            "kafka": list(r["kafka"]) if r.get("kafka") is not None else None,
+            "l7proto": r.get("l7proto") or "",
+            "l7": list(r["l7"]) if r.get("l7") is not None else None}
+
+
+@dataclass
+class L4Filter:
+    """L4Filter (pkg/policy/l4.go:52-73) without its rule labels: the peers
+    (endpoints; the wildcard selector when it selects all), the L7 parser
+    ("" for ParserTypeNone) and the L7 rules per peer selector (L7DataMap,
+    keyed by selector value — the Go map's key is the selector struct, so
+    the reference's tests, which reuse one selector variable, key it the
+    same way)."""
+    port: int
+    proto: int
+    endpoints: list
+    parser: str = ""
+    l7: dict = field(default_factory=dict)
+
+    def allows_all(self) -> bool:
+        """AllowsAllAtL3 (l4.go:112-114)."""
+        return _selects_all(self.endpoints)
+
+    def merge(self, new: "L4Filter", peers):
+        """mergeL4Port (rule.go:36-108)."""
+        if self.allows_all() or new.allows_all():
+            self.endpoints = [WILDCARD_SELECTOR]
+        else:
+            self.endpoints = self.endpoints + list(peers)
+        if new.parser:
+            if not self.parser:
+                self.parser = new.parser
+            elif new.parser != self.parser:
+                raise PolicyError(f"Cannot merge conflicting L7 parsers "
+                                  f"({new.parser}/{self.parser})")
+        for sel, nr in new.l7.items():
+            ep = self.l7.get(sel)
+            if ep is None:
+                self.l7[sel] = _l7_norm(nr)
+                continue
+            if nr["http"]:
+                if ep["kafka"] or ep["l7proto"]:
+                    raise PolicyError("Cannot merge conflicting L7 rule types")
+                ep["http"] = (ep["http"] or []) + [x for x in nr["http"]
+                                                    if x not in (ep["http"] or [])]
+            elif nr["kafka"]:
+                if ep["http"] or ep["l7proto"]:
+                    raise PolicyError("Cannot merge conflicting L7 rule types")
+                ep["kafka"] = (ep["kafka"] or []) + [x for x in nr["kafka"]
+                                                      if x not in (ep["kafka"] or [])]
+            elif nr["l7proto"]:
+                if ep["kafka"] or ep["http"] or (ep["l7proto"] and ep["l7proto"] != nr["l7proto"]):
+                    raise PolicyError("Cannot merge conflicting L7 rule types")
+                ep["l7proto"] = ep["l7proto"] or nr["l7proto"]
+                ep["l7"] = (ep["l7"] or []) + [x for x in (nr["l7"] or [])
+                                                if x not in (ep["l7"] or [])]
+
+    def wildcard_l7(self, peers):
+        """wildcardL3L4Rule's body (repository.go:127-164): the peers allowed
+        at every L7 resource of the parser, and added to the filter."""
+        for sel in peers:
+            if self.parser == "http":
+                self.l7[sel] = _l7_norm({"http": [{}]})
+            elif self.parser == "kafka":
+                self.l7[sel] = _l7_norm({"kafka": [{}]})
+            else:
+                self.l7[sel] = _l7_norm({"l7proto": self.parser, "l7": []})
+        self.endpoints = self.endpoints + list(peers)
+
+
 # ------------------------------------------------------------- repository
 class Repository:
     def __init__(self, rules, always_allow_localhost=True, host_allows_world=True):
@@ -485,8 +576,17 @@ class Repository:
                     break
         return bool(decision)
 
-    def _l4(self, subject, ingress) -> dict:
-        """ResolveL4Ingress/EgressPolicy: {(port, proto): [selectors] | WILDCARD}."""
+    def l4_filters(self, subject, ingress, wildcard_l3l4=True) -> dict:
+        """ResolveL4IngressPolicy / ResolveL4EgressPolicy (repository.go:
+        245-330): {(port, proto): L4Filter}, every rule selecting `subject`
+        merged port by port (rule.go:36-141 mergeL4Port, :227-270; l4.go:
+        143-223 CreateL4Filter / CreateL4IngressFilter), FromRequires /
+        ToRequires joined into each From/ToEndpoints selector, then the L7
+        wildcarding of label-based L3-only and L3/L4 peers
+        (wildcardL3L4Rules, repository.go:127-234) unless `wildcard_l3l4`
+        is False (a single rule's resolveL4*Policy).  Conflicting L7 parsers
+        or rule types on one port raise PolicyError, as the Go call returns
+        its error."""
         req_key = "fromRequires" if ingress else "toRequires"
         ep_key = "fromEndpoints" if ingress else "toEndpoints"
         reqs = []
@@ -494,63 +594,81 @@ class Repository:
             if r.selector.matches(subject):
                 for x in (r.ingress if ingress else r.egress):
                     reqs += [Selector.parse(s) for s in x.get(req_key, []) or []]
-        res, l7 = {}, set()
-
-        def add(k, sel, wild):
-            cur = res.get(k, [])
-            if wild or cur == WILDCARD:
-                res[k] = WILDCARD
-            else:
-                res[k] = cur + [s for s in sel if s not in cur]
-
-        def keys_of(pr):
-            for p in pr.get("ports", []) or []:
-                protos = [p.get("protocol", "ANY").upper()]
-                if protos[0] == "ANY":
-                    protos = ["TCP", "UDP"]
-                for proto in protos:
-                    yield (parse_port(p["port"]), PROTO[proto])
+        res = {}
         for r in self.rules:
             if not r.selector.matches(subject):
                 continue
             for x in (r.ingress if ingress else r.egress):
                 if not (x.get("toPorts") or []):
                     continue
-                sel = peer_selectors(x, ingress)
+                peers = peer_selectors(x, ingress)
                 if reqs:   # requirements join each From/ToEndpoints selector
                     n_ep = len(x.get(ep_key, []) or [])
-                    sel = [Selector(s.labels, s.requires + tuple(reqs)) if i < n_ep else s
-                           for i, s in enumerate(sel)]
-                wild = not sel or any(s.selects_all() for s in sel)
+                    peers = [Selector(s.labels, s.requires + tuple(reqs)) if i < n_ep else s
+                             for i, s in enumerate(peers)]
                 for pr in x["toPorts"]:
-                    for k in keys_of(pr):
-                        add(k, sel, wild)
-                        if pr.get("rules"):   # (an L7 parser on the port)
-                            l7.add(k)
-        # wildcardL3L4Rules (repository.go:166-234, wildcardL3L4Rule :127-164):
-        # a port with L7 rules also takes, with allow-all L7 rules, the peers
-        # of the label-based L3-only rules (every such port of TCP and UDP)
-        # and of the L3/L4 rules without L7 rules on the same port — they
-        # become L4 keys (the reference redirects them to its proxy)
-        if l7:
+                    for p in pr.get("ports", []) or []:
+                        port = parse_port(p.get("port"))
+                        pn = parse_l4_proto(p.get("protocol"))
+                        for proto in (("TCP", "UDP") if pn == "ANY" else (pn,)):
+                            f = self._create_filter(peers, pr, port, proto, ingress)
+                            k = (port, PROTO[proto])
+                            if k in res:
+                                res[k].merge(f, peers)
+                            else:
+                                res[k] = f
+        if wildcard_l3l4 and any(f.parser for f in res.values()):
             for r in self.rules:
                 if not r.selector.matches(subject):
                     continue
                 for x in (r.ingress if ingress else r.egress):
                     if not label_based(x, ingress):
                         continue
-                    sel = peer_selectors(x, ingress)
-                    wild = any(s.selects_all() for s in sel)
+                    peers = peer_selectors(x, ingress)
                     tps = x.get("toPorts") or []
-                    if not tps:
-                        targets = [k for k in l7 if k[1] in (6, 17)]
-                    else:
-                        targets = [k for pr in tps if not pr.get("rules")
-                                   for k in keys_of(pr) if k in l7]
-                    for k in targets:
-                        if sel:
-                            add(k, sel, wild)
+                    if not tps:    # L3-only: every port of TCP and UDP
+                        targets = [("TCP", 0), ("UDP", 0)]
+                    else:          # L3/L4-only ports (an ANY port matches no filter)
+                        targets = [(parse_l4_proto(p.get("protocol")), parse_port(p.get("port")))
+                                   for pr in tps if _l7_empty(pr.get("rules"))
+                                   for p in pr.get("ports", []) or []]
+                    for proto, port in targets:
+                        for (fp, fpr), f in res.items():
+                            if PROTO.get(proto) == fpr and (port == 0 or port == fp) and f.parser:
+                                f.wildcard_l7(peers)
         return res
+
+    def _create_filter(self, peers, pr, port, proto, ingress) -> "L4Filter":
+        """CreateL4Filter (l4.go:162-200) and, ingress, CreateL4IngressFilter
+        (:209-223): the host (and world) selectors wildcarded at L7 when the
+        port rule has L7 rules and localhost is always allowed."""
+        f = L4Filter(port, PROTO[proto],
+                     [WILDCARD_SELECTOR] if _selects_all(peers) else list(peers))
+        rules = pr.get("rules")
+        if proto == "TCP" and rules is not None:
+            f.parser = ("http" if rules.get("http") else "kafka" if rules.get("kafka")
+                        else rules.get("l7proto") or "")
+            if not _l7_empty(rules) and _l7_len(rules) > 0:   # addRulesForEndpoints
+                for s in f.endpoints:
+                    f.l7[s] = _l7_norm(rules)
+        if ingress and not _l7_empty(rules) and self.always_allow_localhost:
+            f.l7[entity_selector("host")] = _l7_norm({})
+            if self.host_allows_world:
+                f.l7[entity_selector("world")] = _l7_norm({})
+        return f
+
+    def _l4(self, subject, ingress) -> dict:
+        """The L4 filters' peers: {(port, proto): [selectors] | WILDCARD}."""
+        out = {}
+        for k, f in self.l4_filters(subject, ingress).items():
+            if f.allows_all():
+                out[k] = WILDCARD
+            else:
+                out[k] = []
+                for s_ in f.endpoints:
+                    if s_ not in out[k]:
+                        out[k].append(s_)
+        return out
 
     def map_state(self, subject: frozenset, identities: dict) -> dict:
         """computeDesiredPolicyMapState (pkg/endpoint/policy.go:273-395):

@@ -499,3 +499,140 @@ def test_to_services_sanitize():
                      "egress": [{"toServices": [{"k8sServiceSelector": {
                          "selector": {"matchLabels": {"app": "tested-service"}}}}],
                                  "toPorts": tcp(80) + tcp(81)}]})
+
+
+# l4Filter_test.go: the L4 filters themselves (peers, parser, L7 rules per
+# peer selector).  The Go tests run with AllowLocalhost unset (no host / world
+# L7 override) but case 12; a single rule's resolveL4IngressPolicy has no
+# wildcardL3L4Rules step, ResolveL4IngressPolicy (cases 1, 2B) has.
+SA, SC, W = R.Selector(lbls("id=a")), R.Selector(lbls("id=c")), R.WILDCARD_SELECTOR
+GET = {"http": [{"method": "GET", "path": "/"}]}
+KFOO = {"kafka": [{"topic": "foo"}]}
+
+
+def _fr(*ingress_rules, localhost=False):
+    return R.Repository(R.parse_rules([{"endpointSelector": es("id=a"),
+                                        "ingress": list(ingress_rules)}]),
+                        always_allow_localhost=localhost, host_allows_world=False)
+
+
+def _ir(peers, rules=None, port="80"):
+    pr = {"ports": [{"port": port, "protocol": "TCP"}]}
+    if rules is not None:
+        pr["rules"] = rules
+    return {"fromEndpoints": peers, "toPorts": [pr]}
+
+
+def _one(rp, wildcard=False, subject=A):
+    fs = rp.l4_filters(subject, True, wildcard_l3l4=wildcard)
+    if not fs:
+        return None
+    (k, f), = fs.items()
+    return k, f
+
+
+def _l7(**kw):
+    return R._l7_norm(kw)
+
+
+def test_l4filter_allow_all_l3_and_l7():
+    # l4Filter_test.go:74-162 (case 1A explicit wildcard, 1B implicit)
+    for peers in ([WILD], []):
+        k, f = _one(_fr(_ir(peers), _ir(peers)), wildcard=True)
+        assert k == (80, 6) and f.allows_all() and f.parser == "" and f.l7 == {}
+
+
+def test_l4filter_allow_all_l3_and_shadowed_l7():
+    # :164-278 — 2A: the rule alone keeps the HTTP rule on the wildcard
+    # selector; 2B: the repository's wildcardL3L4Rules turns it allow-all
+    k, f = _one(_fr(_ir([WILD]), _ir([WILD], GET)))
+    assert f.allows_all() and f.parser == "http"
+    assert f.l7 == {W: _l7(http=[{"method": "GET", "path": "/"}])}
+    k, f = _one(_fr(_ir([WILD], GET), _ir([WILD])), wildcard=True)
+    assert f.allows_all() and f.parser == "http" and len(f.l7) == 1
+
+
+def test_l4filter_identical_restricted_l7():
+    # :280-350 (HTTP), :352-425 (Kafka): identical rules merge into one
+    for rules, port, parser in ((GET, "80", "http"), (KFOO, "9092", "kafka")):
+        k, f = _one(_fr(_ir([WILD], rules, port), _ir([WILD], rules, port)))
+        assert k == (int(port), 6) and f.allows_all() and f.parser == parser
+        assert f.l7 == {W: R._l7_norm(rules)}
+        # a rule that does not select the endpoint resolves to nothing
+        assert _one(_fr(_ir([WILD], rules, port)), subject=lbls("foo")) is None
+
+
+def test_l4filter_mismatching_parsers():
+    # :427-613: Kafka / HTTP in either order, HTTP then a generic parser,
+    # and (egress) a generic parser without rules then HTTP: an error
+    tester = {"l7proto": "testing", "l7": [{"method": "PUT", "path": "/Foo"}]}
+    for r1, r2 in ((KFOO, GET), (GET, KFOO), (GET, tester)):
+        with pytest.raises(R.PolicyError, match="conflicting L7"):
+            _fr(_ir([WILD], r1), _ir([WILD], r2)).l4_filters(A, True, wildcard_l3l4=False)
+    rp = R.Repository(R.parse_rules([{"endpointSelector": es("id=a"), "egress": [
+        {"toEndpoints": [es("id=c")], "toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}],
+                                                   "rules": {"l7proto": "testing"}}]},
+        {"toEndpoints": [es("id=c")], "toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}],
+                                                   "rules": GET}]}]}]),
+        always_allow_localhost=False)
+    with pytest.raises(R.PolicyError, match="conflicting L7"):
+        rp.l4_filters(A, False, wildcard_l3l4=False)
+
+
+def test_l4filter_l3_shadowed_by_allow_all():
+    # :615-730 (case 6): the wildcard rule shadows the id=a rule, either order
+    for pair in ((_ir([es("id=a")]), _ir([WILD])), (_ir([WILD]), _ir([es("id=a")]))):
+        k, f = _one(_fr(*pair))
+        assert f.endpoints == [W] and f.parser == "" and f.l7 == {}
+        assert _one(_fr(*pair), subject=lbls("foo")) is None
+
+
+def test_l4filter_l7_partially_and_fully_shadowed():
+    # :732-871 (case 7): id=a's HTTP rule stays on its selector, L3 is all;
+    # :873-1029 (case 8): both selectors keep the HTTP rule
+    http = _l7(http=[{"method": "GET", "path": "/"}])
+    for pair in ((_ir([es("id=a")], GET), _ir([WILD])), (_ir([WILD]), _ir([es("id=a")], GET))):
+        k, f = _one(_fr(*pair))
+        assert f.endpoints == [W] and f.parser == "http" and f.l7 == {SA: http}
+    for pair in ((_ir([es("id=a")], GET), _ir([WILD], GET)),
+                 (_ir([WILD], GET), _ir([es("id=a")], GET))):
+        k, f = _one(_fr(*pair))
+        assert f.endpoints == [W] and f.parser == "http" and f.l7 == {W: http, SA: http}
+
+
+def test_l4filter_conflicting_l7_with_endpoint():
+    # :1031-1136 (case 9): Kafka on id=a and HTTP on all, either order
+    for pair in ((_ir([es("id=a")], KFOO), _ir([WILD], GET)),
+                 (_ir([WILD], GET), _ir([es("id=a")], KFOO))):
+        with pytest.raises(R.PolicyError):
+            _fr(*pair).l4_filters(A, True, wildcard_l3l4=False)
+
+
+def test_l4filter_different_endpoints():
+    # :1138-1217 (case 10: the same L7 rule for id=a and id=c), :1219-1283
+    # (case 11: no L7 rules): both peers, in rule order
+    http = _l7(http=[{"method": "GET", "path": "/"}])
+    k, f = _one(_fr(_ir([es("id=a")], GET), _ir([es("id=c")], GET)))
+    assert f.endpoints == [SA, SC] and f.parser == "http" and f.l7 == {SC: http, SA: http}
+    k, f = _one(_fr(_ir([es("id=a")]), _ir([es("id=c")])))
+    assert f.endpoints == [SA, SC] and f.parser == "" and f.l7 == {}
+
+
+def test_l4filter_localhost_shadows_l7():
+    # :1285-1340 (case 12): AllowLocalhost=always puts the host selector at
+    # L7 allow-all (an empty L7Rules) beside the rule's own HTTP rule
+    k, f = _one(_fr(_ir([WILD], GET), localhost=True))
+    assert f.endpoints == [W] and f.parser == "http"
+    assert f.l7 == {W: _l7(http=[{"method": "GET", "path": "/"}]),
+                    R.entity_selector("host"): _l7()}
+
+
+def test_l3_l4_l7_merge():
+    # rule_test.go:2070-2168: an HTTP rule for every peer and an L4 rule for
+    # id=c on port 80, either order: the filter admits all, [wildcard, id=c],
+    # with the HTTP parser and L7 rules for both selectors
+    l7 = {"toPorts": [{"ports": [{"port": "80", "protocol": "TCP"}], "rules": GET}]}
+    for pair in ((l7, _ir([es("id=c")])), (_ir([es("id=c")]), l7)):
+        k, f = _one(_fr(*pair), wildcard=True)
+        assert f.endpoints == [W, SC] and f.parser == "http" and len(f.l7) == 2
+        assert f.l7[SC] == _l7(http=[{}])   # (id=c: allowed at every L7 resource)
