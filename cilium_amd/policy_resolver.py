@@ -267,8 +267,8 @@ def parse_l4_proto(proto) -> str:
     p = (proto or "").upper()
     if p == "":
         return "ANY"
-    if p not in L4_PROTOS:
-        raise PolicyError(f"invalid protocol {proto!r}, only {'/'.join(L4_PROTOS)} allowed")
+    if p not in L4_PROTOS:   # L4Proto.Validate (utils.go:92-100)
+        raise PolicyError(f'invalid protocol "{p}", must be {{ tcp | udp | any }}')
     return p
 
 

@@ -636,3 +636,15 @@ def test_l3_l4_l7_merge():
         k, f = _one(_fr(*pair), wildcard=True)
         assert f.endpoints == [W, SC] and f.parser == "http" and len(f.l7) == 2
         assert f.l7[SC] == _l7(http=[{}])   # (id=c: allowed at every L7 resource)
+
+
+def test_parse_l4_proto_and_selects_all():
+    # api/utils_test.go:93-117, api/selector_test.go:32-47
+    assert [R.parse_l4_proto(x) for x in ("TCP", "UDP", "ANY", "tcp", "Any", "")] == \
+        ["TCP", "UDP", "ANY", "TCP", "ANY", "ANY"]
+    for bad in ("TCP2", "t", "foo2"):
+        with pytest.raises(R.PolicyError, match="invalid protocol"):
+            R.parse_l4_proto(bad)
+    bar, foo = R.Selector(lbls("bar")), R.Selector(lbls("foo"))
+    assert R._selects_all([]) and R._selects_all([W]) and R._selects_all([W, bar])
+    assert not R._selects_all([bar, foo])
