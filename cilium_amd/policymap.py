@@ -57,10 +57,11 @@ class PolicyKey:
     def ToNetwork(self):                     # policymap.go:152
         return dataclasses.replace(self, DestPort=_htons(self.DestPort))
 
-    def String(self):
+    def String(self):                        # policymap.go:108-115
         d = "Egress" if self.TrafficDirection == Egress else "Ingress"
-        return (f"Identity={self.Identity},DestPort={self.GetPort()},"
-                f"Nexthdr={self.Nexthdr},TrafficDirection={d}")
+        if self.DestPort != 0:
+            return f"{d}: {self.Identity} {self.GetPort()}/{self.Nexthdr}"
+        return f"{d}: {self.Identity}"
 
 
 @dataclasses.dataclass
@@ -85,6 +86,20 @@ class PolicyEntry:
 class PolicyEntryDump:
     Key: PolicyKey
     PolicyEntry: PolicyEntry
+
+
+class PolicyEntriesDump(list):
+    """A dump sorted for display (policymap.go:88-106): by traffic
+    direction, then identity."""
+
+    def Less(self, i: int, j: int) -> bool:
+        a, b = self[i].Key, self[j].Key
+        if a.TrafficDirection < b.TrafficDirection:
+            return True
+        return a.TrafficDirection <= b.TrafficDirection and a.Identity < b.Identity
+
+    def Sort(self):
+        self.sort(key=lambda e: (e.Key.TrafficDirection, e.Key.Identity))
 
 
 class PolicyMap:

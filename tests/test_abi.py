@@ -157,6 +157,22 @@ def test_policymap_mirror():
     # raw layout: identity LE, port network order, proto, direction
     raw = policymap.PolicyKey(1000, 80, 6, 0).ToNetwork().pack()
     assert raw == struct.pack("<I", 1000) + b"\x00\x50" + b"\x06\x00"
+    # PolicyKey.String (policymap.go:108-115), on the stored (network) key
+    assert policymap.PolicyKey(1000, 0x5000, 6, 0).String() == "Ingress: 1000 80/6"
+    assert policymap.PolicyKey(2, 0, 0, 1).String() == "Egress: 2"
+    # the display order (policymap_test.go:31-108): direction, then identity
+    E = policymap.PolicyEntry()
+
+    def dump(*keys):
+        return policymap.PolicyEntriesDump(policymap.PolicyEntryDump(
+            policymap.PolicyKey(i, 0, 0, d), E) for i, d in keys)
+    assert not dump((0, 0)).Less(0, 0)
+    assert dump((0, 0), (1, 0)).Less(0, 1)
+    assert dump((0, 0), (1, 1)).Less(0, 1)
+    assert not dump((1, 1), (0, 1)).Less(0, 1)
+    ds = policymap.PolicyEntriesDump(pm.DumpToSlice())
+    ds.Sort()
+    assert [(e.Key.TrafficDirection, e.Key.Identity) for e in ds] == [(0, 1000), (0, 1000), (1, 0)]
     pm.Delete(1000, 80, 6, 0)
     assert not pm.Exists(1000, 80, 6, 0)
     pm.Flush()
