@@ -3,8 +3,9 @@ cilium_lb4_reverse_nat with the reference's key and value layouts
 (lbmap/ipv4.go: Service4Key {Address, Port, Slave}, Service4Value {Address,
 Port, Count, RevNat, Weight}, RevNat4Key, RevNat4Value) and byte order
 (ToNetwork: ports, rev-NAT ids and weights network order; count host order),
-and UpdateService's slot layout (lbmap.go:351-420): backends in slots
-1..n, the master slot 0 carrying the count.  IPv6 (lbmap/ipv6.go):
+and UpdateService's slot layout (lbmap.go:351-427, bpfservice.go): backends
+in slots 1..n kept stable across updates (a removed backend's slots become
+holes refilled by another backend), the master slot 0 carrying the count.  IPv6 (lbmap/ipv6.go):
 cilium_lb6_services {Service6Key: Service6Value} and cilium_lb6_reverse_nat,
 the same layouts with 16-byte addresses (LBMap6)."""
 from __future__ import annotations
@@ -44,6 +45,9 @@ class Service4Key:
     def pack(self):
         return self.address + struct.pack("<HH", _be16(self.port), self.slave)
 
+    def String(self):                                   # ipv4.go:95-97
+        return f"{socket.inet_ntoa(self.address)}:{self.port}"
+
 
 class Service4Value:
     """struct lb4_service (common.h:433-439)."""
@@ -56,6 +60,9 @@ class Service4Value:
         return self.target + struct.pack("<HHHH", _be16(self.port), self.count,
                                          _be16(self.rev_nat), _be16(self.weight))
 
+    def String(self):                                   # ipv4.go:196-198
+        return f"{socket.inet_ntoa(self.target)}:{self.port} ({self.rev_nat})"
+
 
 class RevNat4Value:
     def __init__(self, ip, port):
@@ -65,18 +72,99 @@ class RevNat4Value:
         return self.address + struct.pack("<H", _be16(self.port))
 
 
+class BpfBackend:
+    """bpfBackend (bpfservice.go): the backend a slot holds; a hole is a
+    slot whose backend was removed, filled with a copy of another one."""
+
+    def __init__(self, value, is_hole=False):
+        self.bpfValue, self.id, self.isHole = value, value.String(), is_hole
+
+
+class BpfService:
+    """bpfService (pkg/maps/lbmap/bpfservice.go): the slot layout of one
+    frontend.  A removed backend's slots become holes filled with the
+    remaining backend that fills the fewest slots, so every other backend
+    keeps its slot (CT entries hold slot numbers, lb4_local); a new backend
+    takes the oldest hole, else the next slot.  The reference breaks ties
+    (and orders the removed slots) in Go map order; here the backend first
+    seen in slot order wins and slots go in ascending order."""
+
+    def __init__(self, key):
+        self.frontendKey = key
+        self.holes = []
+        self.backendsByMapIndex = {}
+        self.uniqueBackends = {}
+
+    def addBackend(self, backend):
+        if self.holes:
+            index = self.holes.pop(0)
+            self.backendsByMapIndex[index] = BpfBackend(backend)
+        else:
+            self.backendsByMapIndex[len(self.uniqueBackends) + 1] = BpfBackend(backend)
+        self.uniqueBackends[backend.String()] = backend
+
+    def deleteBackend(self, backend):
+        rid = backend.String()
+        remove, count = [], {}
+        for index in sorted(self.backendsByMapIndex):
+            b = self.backendsByMapIndex[index]
+            if b.id == rid:
+                remove.append(index)
+            else:
+                count[b.id] = count.get(b.id, 0) + 1
+        fill = min(count, key=lambda k: count[k]) if count else ""
+        if not fill:
+            self.holes = []
+            self.backendsByMapIndex = {}
+        else:
+            for index in remove:
+                if not self.backendsByMapIndex[index].isHole:
+                    self.holes.append(index)
+                self.backendsByMapIndex[index] = BpfBackend(self.uniqueBackends[fill], True)
+        self.uniqueBackends.pop(rid, None)
+
+    def getBackends(self):
+        return [self.backendsByMapIndex[i].bpfValue
+                for i in range(1, len(self.backendsByMapIndex) + 1)]
+
+
+class LBMapCache:
+    """lbmapCache (bpfservice.go): one BpfService per frontend."""
+
+    def __init__(self):
+        self.entries = {}
+
+    def prepareUpdate(self, fe, backends) -> BpfService:
+        svc = self.entries.setdefault(fe.String(), BpfService(fe))
+        new = {b.String(): b for b in backends}
+        for key, b in list(svc.uniqueBackends.items()):
+            if key not in new:
+                svc.deleteBackend(b)
+        for b in backends:
+            if b.String() not in svc.uniqueBackends:
+                svc.addBackend(b)
+        return svc
+
+    def delete(self, fe):
+        self.entries.pop(fe.String(), None)
+
+
 class LBMap:
     def __init__(self, dp: Datapath):
         self.dp = dp
+        self.cache = LBMapCache()
         self.svc, _ = dp.open_or_create_map(Service4MapName, MAP_TYPE_HASH, 8, 12,
                                             MaxEntries)
         self.rnat, _ = dp.open_or_create_map(RevNat4MapName, MAP_TYPE_HASH, 2, 6,
                                              MaxEntries)
 
     def UpdateService(self, fe: Service4Key, backends, add_revnat=True, revnat_id=0):
-        """lbmap.go UpdateService: backends[i] into slot i + 1, the reverse
-        NAT entry revnat_id -> frontend, then the master slot (count,
-        non-zero weights), then stale slots past the new count removed."""
+        """lbmap.go:351-427 UpdateService: the frontend's slot layout from
+        the cache (prepareUpdate: holes keep the other backends' slots), slot
+        i + 1 for each, the reverse NAT entry revnat_id -> frontend, then
+        the master slot (count, non-zero weights), then stale slots past the
+        new count removed."""
+        backends = self.cache.prepareUpdate(fe, backends).getBackends()
         old = self.dp.lookup_element(self.svc, Service4Key(fe.address, fe.port, 0).pack())
         existing = struct.unpack_from("<H", old, 6)[0] if old else 0
         for i, be in enumerate(backends):
@@ -92,6 +180,9 @@ class LBMap:
             self.dp.delete_element(self.svc, Service4Key(fe.address, fe.port, i).pack())
 
     def DeleteService(self, fe: Service4Key):
+        """The frontend's master and backend slots (the daemon's loop over
+        lbmap.go:150-167 DeleteService), and its cache entry."""
+        self.cache.delete(fe)
         old = self.dp.lookup_element(self.svc, Service4Key(fe.address, fe.port, 0).pack())
         n = struct.unpack_from("<H", old, 6)[0] if old else 0
         for i in range(n, -1, -1):
@@ -116,6 +207,9 @@ class Service6Key(Service4Key):
     def __init__(self, ip, port, slave=0):
         self.address, self.port, self.slave = _ip6(ip), int(port), int(slave)
 
+    def String(self):                                   # ipv6.go:123-125
+        return f"[{socket.inet_ntop(socket.AF_INET6, self.address)}]:{self.port}"
+
 
 class Service6Value(Service4Value):
     """struct lb6_service (common.h:414-420)."""
@@ -123,6 +217,9 @@ class Service6Value(Service4Value):
     def __init__(self, count=0, target="::", port=0, rev_nat=0, weight=0):
         self.count, self.target, self.port = int(count), _ip6(target), int(port)
         self.rev_nat, self.weight = int(rev_nat), int(weight)
+
+    def String(self):                                   # ipv6.go:192-194
+        return f"[{socket.inet_ntop(socket.AF_INET6, self.target)}]:{self.port} ({self.rev_nat})"
 
 
 class RevNat6Value(RevNat4Value):
@@ -138,12 +235,14 @@ class LBMap6(LBMap):
 
     def __init__(self, dp: Datapath):
         self.dp = dp
+        self.cache = LBMapCache()
         self.svc, _ = dp.open_or_create_map(Service6MapName, MAP_TYPE_HASH, 20, 24,
                                             MaxEntries)
         self.rnat, _ = dp.open_or_create_map(RevNat6MapName, MAP_TYPE_HASH, 2, 18,
                                              MaxEntries)
 
     def UpdateService(self, fe: Service6Key, backends, add_revnat=True, revnat_id=0):
+        backends = self.cache.prepareUpdate(fe, backends).getBackends()
         old = self.dp.lookup_element(self.svc, Service6Key(fe.address, fe.port, 0).pack())
         existing = struct.unpack_from("<H", old, 18)[0] if old else 0
         for i, be in enumerate(backends):
@@ -159,6 +258,7 @@ class LBMap6(LBMap):
             self.dp.delete_element(self.svc, Service6Key(fe.address, fe.port, i).pack())
 
     def DeleteService(self, fe: Service6Key):
+        self.cache.delete(fe)
         old = self.dp.lookup_element(self.svc, Service6Key(fe.address, fe.port, 0).pack())
         n = struct.unpack_from("<H", old, 18)[0] if old else 0
         for i in range(n, -1, -1):

@@ -1,6 +1,7 @@
 """pkg/maps/lbmap mirror (cilium_amd/lbmap.py) on a host-only context: the
 reference's Service4Key / Service4Value / RevNat4 layouts and byte order, and
-UpdateService's slot layout (lbmap.go:351-420)."""
+UpdateService's slot layout (lbmap.go:351-427) with bpfservice.go's slot
+cache, pinned by bpfservice_test.go."""
 import struct
 
 import numpy as np
@@ -29,10 +30,19 @@ def test_update_service_slots_and_byte_order():
     k, v = dp.dump(m.rnat)
     assert bytes(k[0]) == struct.pack("<H", int(S.htons(7)))
     assert bytes(v[0]) == struct.pack("<IH", vip, int(S.htons(80)))
-    # shrinking the service removes the stale slot
+    # removing a backend keeps the slots: its slot becomes a hole holding
+    # the remaining backend (bpfservice.go deleteBackend), the count stays
     m.UpdateService(fe, bes[:1], add_revnat=False)
     k, v = dp.dump(m.svc)
-    assert len(k) == 2
+    rows = {bytes(a): bytes(b) for a, b in zip(k, v)}
+    assert len(rows) == 3
+    b2 = struct.pack("<IHH", vip, int(S.htons(80)), 2)
+    assert rows[b2][:4] == struct.pack("<I", S.ip4("10.1.0.1"))
+    assert struct.unpack("<IHHHH", rows[master])[2] == 2
+    # the last backend gone, the service has no slots: the stale ones go
+    m.UpdateService(fe, [], add_revnat=False)
+    k, v = dp.dump(m.svc)
+    assert len(k) == 1
     m.DeleteService(fe)
     k, v = dp.dump(m.svc)
     assert len(k) == 0
@@ -66,3 +76,55 @@ def test_lb_map_geometry_checked():
     with pytest.raises(OSError):
         dp.open_or_create_map("cilium_lb4_reverse_nat", 1, 4, 6, 65536)
     dp.close()
+
+
+def _be(ip):
+    return lbmap.Service4Value(target=ip, port=80, rev_nat=1)
+
+
+def test_scale_service():
+    # bpfservice_test.go:41-116 (TestScaleService)
+    svc = lbmap.BpfService(lbmap.Service4Key("1.1.1.1", 80))
+    b1, b2, b3, b4 = (_be(x) for x in ("2.2.2.2", "3.3.3.3", "4.4.4.4", "5.5.5.5"))
+
+    def slots():
+        return {i: (b.bpfValue.String(), b.isHole) for i, b in svc.backendsByMapIndex.items()}
+    svc.addBackend(b1)
+    assert slots() == {1: (b1.String(), False)} and svc.holes == []
+    svc.addBackend(b2)
+    assert slots() == {1: (b1.String(), False), 2: (b2.String(), False)}
+    svc.deleteBackend(b1)
+    assert slots() == {1: (b2.String(), True), 2: (b2.String(), False)} and len(svc.holes) == 1
+    svc.addBackend(b3)
+    assert slots() == {1: (b3.String(), False), 2: (b2.String(), False)} and svc.holes == []
+    svc.addBackend(b4)
+    assert slots() == {1: (b3.String(), False), 2: (b2.String(), False),
+                       3: (b4.String(), False)}
+    svc.deleteBackend(b4)
+    assert len(svc.backendsByMapIndex) == 3 and len(svc.holes) == 1
+    assert slots()[1][0] == b3.String() and slots()[2][0] == b2.String()
+    assert slots()[3][1] and slots()[3][0] in (b3.String(), b2.String())   # either fills
+    svc.deleteBackend(b3)
+    assert slots() == {1: (b2.String(), True), 2: (b2.String(), False),
+                       3: (b2.String(), True)} and len(svc.holes) == 2
+    svc.deleteBackend(b2)   # the last backend: every slot goes
+    assert svc.backendsByMapIndex == {} and svc.holes == []
+    svc.addBackend(b4)
+    assert slots() == {1: (b4.String(), False)} and svc.holes == []
+
+
+def test_prepare_update():
+    # bpfservice_test.go:118-181 (TestPrepareUpdate)
+    cache = lbmap.LBMapCache()
+    fe = lbmap.Service4Key("1.1.1.1", 80)
+    b1, b2, b3 = (_be(x) for x in ("2.2.2.2", "3.3.3.3", "4.4.4.4"))
+
+    def ids(svc):
+        return [b.String() for b in svc.getBackends()]
+    assert ids(cache.prepareUpdate(fe, [b1, b2])) == [b1.String(), b2.String()]
+    assert ids(cache.prepareUpdate(fe, [b1, b2, b3])) == [b1.String(), b2.String(), b3.String()]
+    got = ids(cache.prepareUpdate(fe, [b2, b3]))
+    assert len(got) == 3 and got[0] != b1.String() and got[1:] == [b2.String(), b3.String()]
+    assert ids(cache.prepareUpdate(fe, [b1, b2, b3])) == [b1.String(), b2.String(), b3.String()]
+    svc = cache.prepareUpdate(fe, [])
+    assert svc.backendsByMapIndex == {} and svc.getBackends() == []
