@@ -1857,6 +1857,19 @@ def sc_nat46_self_v4(n=1600, seed=69):
         parts.append(rep)
         pos.append(at[sel])
         at = at + rng.random(len(ok)) * 0.03
+    # ICMP errors the endpoint sends itself about those flows: every
+    # translation case of icmp4_to_icmp6 (nat46.h)
+    k = int(n * 0.1)
+    err = S.take(parts[0], rng.integers(0, len(parts[0]), size=k))
+    tc = np.array([[3, 0], [3, 1], [3, 3], [3, 4], [3, 9], [3, 13], [11, 0], [12, 0], [5, 0]],
+                  np.uint16)
+    pick = tc[rng.integers(0, len(tc), size=k)]
+    err.proto[:] = S.IPPROTO_ICMP
+    err.sport[:] = (pick[:, 0] | pick[:, 1] << 8).astype(np.uint16)
+    err.dport[:] = 0
+    err.tcpflags = np.zeros(k, np.uint8)
+    parts.append(err)
+    pos.append(rng.random(k))
     plain = S.gen_headers_v4(rng, int(n * 0.2), ipc4, S.local_v4_addrs(t)[:1], local_frac=0.0,
                              mark_host=0, mark_proxy=0, frag=0, src_fixed=S.LXC_IPV4)
     parts.append(plain)
