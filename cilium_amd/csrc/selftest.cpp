@@ -115,6 +115,26 @@ static int run(const char *name, const std::vector<Pfx6> &pfx, R &rng,
     return bad != 0;
 }
 
+// test/bpf/unit-test.c test_ipv6_addr_clear_suffix: the words an all-ones
+// address keeps under a prefix length (ipv6_addr_clear_suffix, ipv6.h:136-150),
+// here as l6_word_mask (layout.h), which builds and probes the IPv6 LPM
+static int clear_suffix_kats()
+{
+    struct { uint32_t len, w[4]; } k[] = {
+        {128, {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu}},
+        {127, {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xfffffffeu}},
+        {95, {0xffffffffu, 0xffffffffu, 0xfffffffeu, 0}},
+        {1, {0x80000000u, 0, 0, 0}},
+        {0, {0, 0, 0, 0}},   // (the reference's -1 case: no prefix bits)
+    };
+    int bad = 0;
+    for (const auto &c : k)
+        for (int i = 0; i < 4; i++)
+            bad += l6_word_mask(c.len, i) != c.w[i];
+    printf("clear_suffix kats: %s\n", bad ? "FAIL" : "ok");
+    return bad != 0;
+}
+
 int main()
 {
     std::mt19937 gen(12345);
@@ -166,5 +186,6 @@ int main()
         fail |= run("empty", std::vector<Pfx6>(), rng, 1000);
     }
     fail |= selfcut_tests();
+    fail |= clear_suffix_kats();
     return fail;
 }
