@@ -1636,7 +1636,7 @@ def sc_nat46_egress_v6(n=3000, seed=61):
     return t, h.slice(0, n), MODE_EGRESS, S.EP_LXC_ID, dp
 
 
-def sc_nat64_lb_v6(n=2400, seed=67):
+def sc_nat64_lb_v6(n=2400, seed=67, loopback=False):
     """Load-balanced NAT64 hops (an oracle-only fixture, tests/golden_oracle:
     the engine was not run against it): IPv6 packets to v4-mapped IPv4
     service VIPs leave through the IPv4 egress program (bpf_lxc.c:353-360 ->
@@ -1646,7 +1646,17 @@ def sc_nat64_lb_v6(n=2400, seed=67):
     A history opens service flows; the test stream: their later packets, new
     service flows of several packets, and plain NAT64 flows beside them."""
     t, rng, ipc4 = _nat_setup(seed)
-    t.lb4, t.revnat4, vips, ports, protos = S.lb4_services(rng, t, loopback=False)
+    t.lb4, t.revnat4, vips, ports, protos = S.lb4_services(rng, t, loopback=loopback)
+    if loopback:
+        # (loopback: a service whose backend is the endpoint itself — lb4_local
+        # SNATs to IPV4_LOOPBACK and the endpoint's ingress admits its own
+        # identity on the services' ports)
+        pol = t.policy[S.EP_LXC_ID]
+        add = np.zeros(len(ports), S.POLICY_DT)
+        add["identity"] = int(t.seclabel[S.EP_LXC_ID])
+        add["dport"] = ports
+        add["proto"] = protos
+        t.policy[S.EP_LXC_ID] = np.concatenate([pol, add])
 
     # (not the service whose backend slot lives only under the L3 key: every
     # packet of its flows re-selects from its own skb->hash, which the
@@ -2208,10 +2218,11 @@ SCENARIOS = {
     "self_egress_v6": sc_self_egress_v6,
     "nat64_lb_v6": sc_nat64_lb_v6,
     "nat46_self_v4": sc_nat46_self_v4,
+    "nat64_lb_lo_v6": lambda: sc_nat64_lb_v6(seed=68, loopback=True),
 }
 # fixtures that pin only the oracle (tests/golden_oracle): the engine has
 # not been run against them on the GPU
-ORACLE_ONLY = {"nat64_lb_v6", "nat46_self_v4"}
+ORACLE_ONLY = {"nat64_lb_v6", "nat46_self_v4", "nat64_lb_lo_v6"}
 
 
 def main(names):
