@@ -5,11 +5,14 @@
 // sets, prefixes piled under one /48 or /64 (groups must split), a ::/0,
 // and label-0 prefixes that shadow shorter ones.  No GPU needed.
 #include <cstdio>
+#include <cerrno>
 #include <cstring>
+#include <map>
 #include <random>
 #include <vector>
 
 #include "flatten.hpp"
+#include "maps.hpp"
 #include "selfcut.hpp"
 
 using namespace cfc;
@@ -135,6 +138,83 @@ static int clear_suffix_kats()
     return bad != 0;
 }
 
+// the host map store (maps.cpp) against a plain model under random
+// operations: a HASH (hashtab.c: -EEXIST / -ENOENT by flag, -E2BIG when
+// full, get_next_key visits every key once) and an LPM_TRIE (lpm_trie.c:
+// longest stored prefix no longer than the key's, data past the prefix
+// ignored, -ENOSPC when full, -EINVAL past 32 bits)
+static int map_fuzz(std::mt19937 &gen)
+{
+    int bad = 0;
+    {
+        Map m;
+        m.type = MT_HASH, m.ksz = 8, m.vsz = 8, m.max_entries = 64;
+        std::map<uint64_t, uint64_t> model;
+        for (int it = 0; it < 200000; it++) {
+            const uint64_t k = gen() % 96, v = gen();
+            const int op = gen() % 4;
+            if (op <= 1) {
+                const uint64_t fl = gen() % 3;
+                const bool has = model.count(k) != 0;
+                const int want = fl == 1 && has ? -EEXIST : fl == 2 && !has ? -ENOENT
+                                 : !has && model.size() >= 64 ? -E2BIG : 0;
+                bad += m.update(&k, &v, fl) != want;
+                if (!want)
+                    model[k] = v;
+            } else if (op == 2) {
+                uint64_t got = 0;
+                const int rc = m.lookup(&k, &got);
+                bad += model.count(k) ? (rc != 0 || got != model[k]) : rc != -ENOENT;
+            } else {
+                bad += m.erase(&k) != (model.erase(k) ? 0 : -ENOENT);
+            }
+        }
+        std::map<uint64_t, int> seen;   // a get_next_key walk from no key
+        uint64_t cur = 0, nxt = 0;
+        for (int rc = m.next_key(nullptr, &nxt); !rc; rc = m.next_key(&cur, &nxt))
+            seen[cur = nxt]++;
+        bad += seen.size() != model.size();
+        for (auto &kv : seen)
+            bad += kv.second != 1 || !model.count(kv.first);
+    }
+    {
+        Map m;
+        m.type = MT_LPM_TRIE, m.ksz = 8, m.vsz = 4, m.max_entries = 48;
+        std::map<std::pair<uint32_t, uint32_t>, uint32_t> model;   // (plen, masked) -> v
+        auto msk = [](uint32_t a, uint32_t p) { return p ? a & (0xFFFFFFFFu << (32 - p)) : 0u; };
+        for (int it = 0; it < 100000; it++) {
+            const uint32_t plen = gen() % 34, a = gen() & 0xFF0F00FFu, v = gen();
+            uint8_t key[8];
+            const uint32_t be = __builtin_bswap32(a);   // data in network order
+            memcpy(key, &plen, 4);
+            memcpy(key + 4, &be, 4);
+            const int op = gen() % 3;
+            if (op == 0) {
+                const auto mk = std::make_pair(plen, msk(a, plen));
+                const int want = plen > 32 ? -EINVAL
+                                 : !model.count(mk) && model.size() >= 48 ? -ENOSPC : 0;
+                bad += m.update(key, &v, 0) != want;
+                if (!want)
+                    model[mk] = v;
+            } else if (op == 1) {
+                uint32_t got = 0, want = 0;
+                int best = -1;
+                for (auto &e : model)
+                    if ((int)e.first.first > best && e.first.first <= std::min(plen, 32u) &&
+                        msk(a, e.first.first) == e.first.second)
+                        best = (int)e.first.first, want = e.second;
+                const int rc = m.lookup(key, &got);
+                bad += best < 0 ? rc != -ENOENT : (rc != 0 || got != want);
+            } else if (plen <= 32) {
+                bad += m.erase(key) != (model.erase(std::make_pair(plen, msk(a, plen))) ? 0
+                                                                                         : -ENOENT);
+            }
+        }
+    }
+    printf("map fuzz (hash, lpm): %s\n", bad ? "FAIL" : "ok");
+    return bad != 0;
+}
+
 int main()
 {
     std::mt19937 gen(12345);
@@ -187,5 +267,6 @@ int main()
     }
     fail |= selfcut_tests();
     fail |= clear_suffix_kats();
+    fail |= map_fuzz(gen);
     return fail;
 }
