@@ -238,8 +238,8 @@ def test_flattener_selftest():
     import subprocess
     csrc = os.path.join(ROOT, "cilium_amd", "csrc")
     exe = os.path.join(csrc, "build", "selftest")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-C", csrc, "-s", "selftest"], check=True)
+    # (make is incremental: a binary older than its sources is rebuilt)
+    subprocess.run(["make", "-C", csrc, "-s", "selftest"], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count(": ok") == 7 and "FAIL" not in r.stdout, r.stdout
