@@ -1,4 +1,4 @@
-"""Consumer side of the drop notifications and the metrics map (no GPU):
+"""Consumer side of the monitor records and the metrics map (no GPU):
 pkg/monitor's DropNotify decoding of the oracle's records, and the
 Prometheus labels SyncMetricsMap derives from cilium_metrics."""
 import numpy as np
@@ -43,3 +43,31 @@ def test_prometheus_labels_from_metrics_map():
                    ("drop", "Missed tail call", "INGRESS"): 2,
                    ("drop", "CT: Unknown L4 protocol", "UNKNOWN"): 4}
     assert L.CFC_DEVICE_NONE == -1
+
+
+def test_decode_reference_events():
+    """The reference's own perf-ring records (read from cilium_events when
+    the fixture was made) through the TraceNotify / DropNotify decoders
+    (datapath_trace.go:28-40, 96-150, 175-195): fields, observation points,
+    connection states, the text and JSON forms."""
+    g = G.Golden("ct_seq_egress_v4")
+    ev = monitor.decode_events(g.ev.tobytes())
+    assert len(ev) == len(g.ev)
+    tr = [e for e in ev if isinstance(e, monitor.TraceNotify)]
+    dr = [e for e in ev if isinstance(e, monitor.DropNotify)]
+    assert len(tr) == int((g.ev["type"] == 4).sum()) > 0 and len(dr) > 0
+    for e, r in zip(ev, g.ev):
+        assert (e.type, e.hash, e.orig_len, e.src_label, e.dst_label, e.ifindex) == \
+            (r["type"], r["hash"], r["len_orig"], r["src_label"], r["dst_label"], r["ifindex"])
+        if r["type"] == 4:
+            assert (e.obs_point, e.dst_id, e.reason) == \
+                (r["subtype"], r["w6"] & 0xFFFF, (r["w6"] >> 16) & 0xFF)
+    states = {monitor.conn_state(e.reason) for e in tr}
+    assert {"new", "established", "reply"} <= states
+    t = next(e for e in tr if e.obs_point == 0)   # TRACE_TO_LXC
+    assert t.dump_info().startswith(f"-> endpoint {t.dst_id} flow {t.hash:#x} identity ")
+    assert f"to-endpoint: {t.orig_len} bytes ({t.cap_len} captured)" in t.dump_verbose()
+    v = t.to_verbose()
+    assert v["type"] == "trace" and v["observationPoint"] == "to-endpoint"
+    assert v["traceSummary"] == f"-> endpoint {t.dst_id}" and "cpu" not in v
+    assert monitor.obs_point(42) == "42" and monitor.conn_state(9) == "9"
