@@ -90,6 +90,16 @@ class DropNotify:
             s += f", to endpoint {self.dst_id}"
         return s
 
+    def to_verbose(self, cpu_prefix: str = "", ifname: str | None = None) -> dict:
+        """DropNotifyToVerbose (datapath_drop.go:135-166): the JSON object
+        `cilium monitor -o json` prints (empty strings left out)."""
+        d = {"cpu": cpu_prefix, "type": "drop", "mark": f"{self.hash:#x}",
+             "ifindex": ifname if ifname is not None else str(self.ifindex),
+             "reason": drop_reason(self.sub_type), "source": self.source,
+             "bytes": self.orig_len, "srcLabel": self.src_label,
+             "dstLabel": self.dst_label, "dstID": self.dst_id}
+        return {k: v for k, v in d.items() if v != ""}
+
 
 def decode_records(buf) -> list[DropNotify]:
     """A packed array of records (bytes, numpy or a host copy of the tensor

@@ -71,3 +71,6 @@ def test_decode_reference_events():
     assert v["type"] == "trace" and v["observationPoint"] == "to-endpoint"
     assert v["traceSummary"] == f"-> endpoint {t.dst_id}" and "cpu" not in v
     assert monitor.obs_point(42) == "42" and monitor.conn_state(9) == "9"
+    d = dr[0].to_verbose(cpu_prefix="CPU 01: ")
+    assert d["type"] == "drop" and d["reason"] == monitor.drop_reason(dr[0].sub_type)
+    assert d["cpu"] == "CPU 01: " and d["mark"] == f"{dr[0].hash:#x}"
