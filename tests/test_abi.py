@@ -297,3 +297,21 @@ def test_drop_notify_abi_on_host_only_context():
     assert dt.itemsize == 32
     assert [dt.fields[k][1] for k in dt.names] == [0, 1, 2, 4, 8, 12, 16, 20, 24, 28]
     assert np.zeros(1, dt).view(np.uint8).size == 32
+
+
+def test_c_abi_from_c(tmp_path):
+    """include/cfc.h under a C11 compiler (-Werror) and the pkg/bpf call
+    sequence from C on a host-only context (tests/c/abi_host.c): what a cgo
+    shim (INTEGRATION.md) compiles and calls."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no C compiler")
+    exe = str(tmp_path / "abi_host")
+    lib = os.path.join(ROOT, "cilium_amd")
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror",
+                    "-I", os.path.join(ROOT, "include"), "-o", exe,
+                    os.path.join(ROOT, "tests", "c", "abi_host.c"), "-L", lib, "-lcfc",
+                    f"-Wl,-rpath,{lib}"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "abi_host: ok" in r.stdout, r.stdout + r.stderr
