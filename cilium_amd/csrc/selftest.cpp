@@ -138,6 +138,125 @@ static int clear_suffix_kats()
     return bad != 0;
 }
 
+// the IPv4 LPM builders (flatten.cpp build_dir24_8, build_l4trie) through
+// host restatements of the device lookups (classify.hip's DIR-24-8 probe,
+// kern_common.hpp l4_lookup) against a brute-force longest-prefix match:
+// random lengths, prefixes piled under one /16 (lists, then chunk splits),
+// a /0, labels past a list entry's 26 bits (lbl_ovf)
+static uint32_t dir24_lookup_host(const std::vector<uint32_t> &t24,
+                                  const std::vector<uint32_t> &t8, uint32_t a)
+{
+    uint32_t e = t24[a >> 8];
+    if (e & LPM_GROUP)
+        e = t8[((size_t)(e & ~LPM_GROUP) << 8) | (a & 255)];
+    return e;
+}
+static uint32_t l4_lookup_host(const std::vector<uint32_t> &d, const std::vector<uint32_t> &c,
+                               const std::vector<uint64_t> &l, const std::vector<uint32_t> &ovf,
+                               uint32_t a)
+{
+    auto list_leaf = [&](uint32_t hi) {
+        const uint32_t x = hi & (LL_INDIRECT | LL_PAYLOAD);
+        return (x & LL_INDIRECT) ? ovf[x & LL_PAYLOAD] : x;
+    };
+    const uint32_t *D = &d[4 * (a >> 16)];
+    const uint32_t e1 = (D[2] >> 16) | (D[3] << 16);
+    if (l4_inline_match(a, D[1]))
+        return list_leaf((D[1] >> 21) | (D[2] << 11));
+    if (l4_inline_match(a, e1))
+        return list_leaf(D[3] >> 5);
+    uint32_t e = D[0], shift = 16;
+    while (e & L4_PTR) {
+        const uint32_t cnt = (e >> 24) & 127, off = e & L4_OFF;
+        if (cnt == 0) {
+            shift -= 8;
+            e = c[off + ((a >> shift) & 255)];
+            continue;
+        }
+        for (uint32_t i = 0; i < cnt; i += 2) {
+            const uint64_t u = l[off + i], v = l[off + i + 1];
+            const bool m0 = l4_match(a, (uint32_t)u, (uint32_t)(u >> 32));
+            if (m0 || l4_match(a, (uint32_t)v, (uint32_t)(v >> 32)))
+                return list_leaf(m0 ? (uint32_t)(u >> 32) : (uint32_t)(v >> 32));
+        }
+        return 0;
+    }
+    return (e & LPM_INDIRECT) ? ovf[e & LPM_PAYLOAD] : e;
+}
+static int lpm4_case(const char *name, std::vector<Pfx4> pfx, std::mt19937 &gen, int nq)
+{
+    {   // one prefix per (masked address, length), as the ipcache map holds
+        std::map<std::pair<uint32_t, int>, Pfx4> u;
+        for (Pfx4 p : pfx) {
+            p.addr &= p.plen ? 0xFFFFFFFFu << (32 - p.plen) : 0u;
+            u.emplace(std::make_pair(p.addr, (int)p.plen), p);
+        }
+        pfx.clear();
+        for (auto &kv : u)
+            pfx.push_back(kv.second);
+    }
+    std::vector<uint32_t> t24, t8, ovf, d, c;
+    std::vector<uint64_t> l;
+    build_dir24_8(pfx, &t24, &t8);
+    const bool ok = build_l4trie(pfx, &ovf, &d, &c, &l);
+    int bad = !ok;
+    for (int q = 0; q < nq; q++) {
+        uint32_t a = gen();
+        if (!pfx.empty() && (q & 3)) {   // mostly inside some prefix
+            const Pfx4 &p = pfx[gen() % pfx.size()];
+            const uint32_t m = p.plen ? 0xFFFFFFFFu << (32 - p.plen) : 0u;
+            a = p.addr | (a & ~m);
+        }
+        uint32_t want = 0;
+        int best = -1;
+        for (const Pfx4 &p : pfx) {
+            const uint32_t m = p.plen ? 0xFFFFFFFFu << (32 - p.plen) : 0u;
+            if ((int)p.plen > best && (a & m) == p.addr)
+                best = p.plen, want = p.leaf;
+        }
+        const uint32_t x = dir24_lookup_host(t24, t8, a), y = l4_lookup_host(d, c, l, ovf, a);
+        if ((x != want || y != want) && bad++ < 5)
+            printf("%s: %08x -> dir24 %u, trie %u, want %u\n", name, a, x, y, want);
+    }
+    printf("lpm4 %-14s prefixes %5zu chunks %5zu list %6zu: %s\n", name, pfx.size(),
+           c.size() / 256, l.size(), bad ? "FAIL" : "ok");
+    return bad != 0;
+}
+static int lpm4_tests(std::mt19937 &gen)
+{
+    int fail = 0;
+    std::vector<Pfx4> v;
+    for (int i = 0; i < 4000; i++)   // random lengths, some wide labels
+        v.push_back({(uint32_t)gen(), (uint8_t)(gen() % 33),
+                     (i % 9) ? 1 + (uint32_t)(gen() % 100000) : (1u << 27) + i});
+    fail |= lpm4_case("random", v, gen, 40000);
+    v.clear();   // piled under 10.20.0.0/16: lists, then chunks, then deeper
+    for (int i = 0; i < 3000; i++)
+        v.push_back({0x0A140000u | (uint32_t)(gen() & 0xFFFF), (uint8_t)(17 + gen() % 16),
+                     1 + (uint32_t)i});
+    v.push_back({0x0A140000u, 16, 77});
+    v.push_back({0, 0, 5});
+    fail |= lpm4_case("piled", v, gen, 40000);
+    v.clear();   // piled under one /24 too: a second chunk level
+    for (int i = 0; i < 600; i++)
+        v.push_back({0x0A141E00u | (uint32_t)(gen() & 0xFF), (uint8_t)(25 + gen() % 8),
+                     1 + (uint32_t)i});
+    for (int i = 0; i < 40; i++)
+        v.push_back({0x0A140000u | (uint32_t)(gen() & 0xFFFF), (uint8_t)(17 + gen() % 16),
+                     (1u << 26) + (uint32_t)i});
+    fail |= lpm4_case("deep", v, gen, 40000);
+    for (int n : {1, 2, 3, 15, 16, 17}) {   // around the inline and list limits
+        v.clear();
+        for (int i = 0; i < n; i++)
+            v.push_back({0xC0A80000u | (uint32_t)(gen() & 0xFFFF), (uint8_t)(17 + gen() % 16),
+                         100 + (uint32_t)i});
+        char nm[32];
+        snprintf(nm, sizeof nm, "small-%d", n);
+        fail |= lpm4_case(nm, v, gen, 5000);
+    }
+    return fail;
+}
+
 // the host map store (maps.cpp) against a plain model under random
 // operations: a HASH (hashtab.c: -EEXIST / -ENOENT by flag, -E2BIG when
 // full, get_next_key visits every key once) and an LPM_TRIE (lpm_trie.c:
@@ -190,7 +309,7 @@ static int map_fuzz(std::mt19937 &gen)
             memcpy(key + 4, &be, 4);
             const int op = gen() % 3;
             if (op == 0) {
-                const auto mk = std::make_pair(plen, msk(a, plen));
+                const auto mk = std::make_pair(plen, plen <= 32 ? msk(a, plen) : 0u);
                 const int want = plen > 32 ? -EINVAL
                                  : !model.count(mk) && model.size() >= 48 ? -ENOSPC : 0;
                 bad += m.update(key, &v, 0) != want;
@@ -268,5 +387,6 @@ int main()
     fail |= selfcut_tests();
     fail |= clear_suffix_kats();
     fail |= map_fuzz(gen);
+    fail |= lpm4_tests(gen);
     return fail;
 }

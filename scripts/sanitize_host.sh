@@ -16,7 +16,7 @@ O.LIB = "/tmp/cfc_san/liboracle.so"   # (the oracle loads its library lazily)
 import pytest
 sys.exit(pytest.main(["-x", "-q", "-p", "no:cacheprovider", "tests/test_oracle_golden.py"]))
 PY
-/opt/rocm/bin/hipcc -O1 -g -std=c++17 -fsanitize=address,undefined -fno-gpu-sanitize \
+/opt/rocm/bin/hipcc -O1 -g -std=c++17 -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-gpu-sanitize \
     -o /tmp/cfc_san/selftest cilium_amd/csrc/selftest.cpp cilium_amd/csrc/flatten.cpp \
     cilium_amd/csrc/maps.cpp
 /tmp/cfc_san/selftest

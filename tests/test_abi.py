@@ -234,7 +234,10 @@ def test_flattener_selftest():
     longest-prefix match, the self-traffic cut rule, and the prefix masks
     against test/bpf/unit-test.c's ipv6_addr_clear_suffix known answers, and
     the host map store (HASH, LPM_TRIE) against a model under random
-    operations (cilium_amd/csrc/selftest.cpp, host only)."""
+    operations, and both IPv4 LPM layouts (DIR-24-8, the compact multibit
+    trie) through host restatements of the device lookups against a
+    brute-force longest-prefix match (cilium_amd/csrc/selftest.cpp, host
+    only)."""
     import subprocess
     csrc = os.path.join(ROOT, "cilium_amd", "csrc")
     exe = os.path.join(csrc, "build", "selftest")
@@ -242,7 +245,7 @@ def test_flattener_selftest():
     subprocess.run(["make", "-C", csrc, "-s", "selftest"], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(": ok") == 7 and "FAIL" not in r.stdout, r.stdout
+    assert r.stdout.count(": ok") == 16 and "FAIL" not in r.stdout, r.stdout
 
 
 def test_ct_maps_host_only():
