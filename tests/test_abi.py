@@ -312,9 +312,17 @@ def test_c_abi_from_c(tmp_path):
         pytest.skip("no C compiler")
     exe = str(tmp_path / "abi_host")
     lib = os.path.join(ROOT, "cilium_amd")
-    subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror",
+    subprocess.run(["gcc", "-std=c11", "-pedantic", "-Wall", "-Wextra", "-Werror",
                     "-I", os.path.join(ROOT, "include"), "-o", exe,
                     os.path.join(ROOT, "tests", "c", "abi_host.c"), "-L", lib, "-lcfc",
                     f"-Wl,-rpath,{lib}"], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "abi_host: ok" in r.stdout, r.stdout + r.stderr
+    # the header alone under a C++11 compiler too (a C++ host binds it as is)
+    if shutil.which("g++"):
+        src = tmp_path / "h.cpp"
+        src.write_text('#include "cfc.h"\nint main() { return cfc_abi_version() != '
+                       'CFC_ABI_VERSION; }\n')
+        subprocess.run(["g++", "-std=c++11", "-pedantic", "-Wall", "-Wextra", "-Werror",
+                        "-I", os.path.join(ROOT, "include"), "-fsyntax-only", str(src)],
+                       check=True)
