@@ -25,6 +25,10 @@ Restated (file:line in /root/reference):
   * the CIDR policy and its prefix-length       pkg/policy/rule.go:279-345,
     counts (class masks for bare addresses)     l3.go:66-96, repository.go:340-353
 
+  * endpoint selectors: matchLabels and        pkg/policy/api/selector.go:
+    matchExpressions (In, NotIn, Exists,        162-175, 277-300
+    DoesNotExist); unconvertible ones match
+    nothing
   * L4 filters with their L7 parser and L7     pkg/policy/l4.go:52-223,
     rules per peer selector, merge conflicts    rule.go:36-141
 
@@ -80,24 +84,55 @@ def pod_labels(d: dict) -> frozenset:
 
 
 # ------------------------------------------------------------- selectors
+_SEL_OPS = ("In", "NotIn", "Exists", "DoesNotExist")
+
+
 @dataclass(frozen=True)
 class Selector:
-    """EndpointSelector: every matchLabels pair present (keys without a
-    source match any source), plus extra 'requires' selectors (FromRequires
-    folded in as match expressions)."""
+    """EndpointSelector (pkg/policy/api/selector.go): every matchLabels pair
+    present (keys without a source match any source), every
+    matchExpressions requirement (k8s In / NotIn / Exists / DoesNotExist),
+    plus extra 'requires' selectors (FromRequires folded in as match
+    expressions).  A selector k8s refuses to convert (an unknown operator,
+    In / NotIn without values, Exists / DoesNotExist with values) matches
+    nothing, as EndpointSelector.Matches does when its requirements are nil
+    (selector.go:162-175, 277-288)."""
     labels: frozenset = frozenset()
     requires: tuple = ()
+    exprs: tuple = ()          # ((key, operator, frozenset(values)), ...)
+    invalid: bool = False
 
     @staticmethod
     def parse(obj) -> "Selector":
         ml = (obj or {}).get("matchLabels", {}) or {}
-        return Selector(frozenset(f"{k}={v}" for k, v in ml.items()))
+        exprs, invalid = [], False
+        for e in (obj or {}).get("matchExpressions", []) or []:
+            op, vals = e.get("operator"), tuple(e.get("values") or ())
+            if op not in _SEL_OPS or (op in ("In", "NotIn")) != bool(vals):
+                invalid = True
+            exprs.append((e.get("key", ""), op, frozenset(vals)))
+        return Selector(frozenset(f"{k}={v}" for k, v in ml.items()), (),
+                        tuple(sorted(exprs, key=lambda x: (x[0], str(x[1]), sorted(x[2])))),
+                        invalid)
+
+    @staticmethod
+    def _expr(lbls: frozenset, key: str, op: str, vals: frozenset) -> bool:
+        present = {lb.split("=", 1)[1] for lb in lbls if lb.split("=", 1)[0] == key}
+        if op == "In":
+            return bool(present & vals)
+        if op == "NotIn":
+            return not (present & vals)
+        if op == "Exists":
+            return bool(present)
+        return not present   # DoesNotExist
 
     def matches(self, lbls: frozenset) -> bool:
-        return self.labels <= lbls and all(r.matches(lbls) for r in self.requires)
+        return (not self.invalid and self.labels <= lbls and
+                all(self._expr(lbls, *e) for e in self.exprs) and
+                all(r.matches(lbls) for r in self.requires))
 
     def selects_all(self) -> bool:
-        return not self.labels and not self.requires
+        return not self.labels and not self.requires and not self.exprs and not self.invalid
 
 
 def entity_selector(e: str):
@@ -604,7 +639,8 @@ class Repository:
                 peers = peer_selectors(x, ingress)
                 if reqs:   # requirements join each From/ToEndpoints selector
                     n_ep = len(x.get(ep_key, []) or [])
-                    peers = [Selector(s.labels, s.requires + tuple(reqs)) if i < n_ep else s
+                    peers = [Selector(s.labels, s.requires + tuple(reqs), s.exprs, s.invalid)
+                             if i < n_ep else s
                              for i, s in enumerate(peers)]
                 for pr in x["toPorts"]:
                     for p in pr.get("ports", []) or []:

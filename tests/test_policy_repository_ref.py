@@ -648,3 +648,37 @@ def test_parse_l4_proto_and_selects_all():
     bar, foo = R.Selector(lbls("bar")), R.Selector(lbls("foo"))
     assert R._selects_all([]) and R._selects_all([W]) and R._selects_all([W, bar])
     assert not R._selects_all([bar, foo])
+
+
+def test_label_selector_requirements():
+    # api/selector_test.go:49-75: matchLabels become Equals requirements and
+    # matchExpressions join them (k8s LabelSelectorAsSelector); a selector
+    # that does not convert matches nothing (selector.go:162-175, 277-288)
+    s = R.Selector.parse({"matchLabels": {"foo": "bar", "baz": "alice"},
+                          "matchExpressions": [{"key": "foo", "operator": "NotIn",
+                                                "values": ["default"]}]})
+    assert s.matches(lbls("foo=bar", "baz=alice", "x=y"))
+    assert not s.matches(lbls("foo=bar")) and not s.matches(lbls("foo=default", "baz=alice"))
+    e = {"matchExpressions": [{"key": "env", "operator": "In", "values": ["prod", "qa"]},
+                              {"key": "tier", "operator": "Exists"},
+                              {"key": "debug", "operator": "DoesNotExist"},
+                              {"key": "zone", "operator": "NotIn", "values": ["b"]}]}
+    s = R.Selector.parse(e)
+    assert s.matches(lbls("env=qa", "tier=web")) and s.matches(lbls("env=prod", "tier=", "zone=a"))
+    for bad in (lbls("env=dev", "tier=web"), lbls("env=qa"), lbls("env=qa", "tier=web", "debug=1"),
+                lbls("env=qa", "tier=web", "zone=b")):
+        assert not s.matches(bad)
+    assert not s.selects_all()
+    for inval in ({"key": "a", "operator": "Equals", "values": ["x"]},
+                  {"key": "a", "operator": "In", "values": []},
+                  {"key": "a", "operator": "Exists", "values": ["x"]}):
+        s = R.Selector.parse({"matchExpressions": [inval]})
+        assert not s.matches(lbls("a=x")) and not s.matches(lbls()) and not s.selects_all()
+    # in a rule: the endpoint selector and a peer selector with expressions
+    rp = repo({"endpointSelector": {"matchExpressions": [{"key": "role", "operator": "In",
+                                                          "values": ["db", "cache"]}]},
+               "ingress": [{"fromEndpoints": [{"matchExpressions": [
+                   {"key": "role", "operator": "NotIn", "values": ["public"]}]}]}]})
+    assert ingress_allowed(rp, lbls("role=web"), lbls("role=db")) is True
+    assert ingress_allowed(rp, lbls("role=public"), lbls("role=cache")) is False
+    assert ingress_allowed(rp, lbls("role=web"), lbls("role=web")) is None   # not selected
