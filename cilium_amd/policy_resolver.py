@@ -127,7 +127,11 @@ class Selector:
         return not present   # DoesNotExist
 
     def matches(self, lbls: frozenset) -> bool:
-        return (not self.invalid and self.labels <= lbls and
+        if self.invalid:
+            return False
+        if "reserved:all=" in self.labels:   # (selector.go:290-294: matches all,
+            return True                       # yet is no wildcard selector)
+        return (self.labels <= lbls and
                 all(self._expr(lbls, *e) for e in self.exprs) and
                 all(r.matches(lbls) for r in self.requires))
 

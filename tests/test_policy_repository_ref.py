@@ -674,6 +674,9 @@ def test_label_selector_requirements():
                   {"key": "a", "operator": "Exists", "values": ["x"]}):
         s = R.Selector.parse({"matchExpressions": [inval]})
         assert not s.matches(lbls("a=x")) and not s.matches(lbls()) and not s.selects_all()
+    # a reserved:all key matches every label set, yet is no wildcard
+    s = R.Selector.parse({"matchLabels": {"reserved:all": ""}})
+    assert s.matches(lbls("foo")) and s.matches(lbls()) and not s.selects_all()
     # in a rule: the endpoint selector and a peer selector with expressions
     rp = repo({"endpointSelector": {"matchExpressions": [{"key": "role", "operator": "In",
                                                           "values": ["db", "cache"]}]},
