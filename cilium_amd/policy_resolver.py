@@ -103,6 +103,16 @@ class Selector:
     invalid: bool = False
 
     @staticmethod
+    def _key(k: str) -> str:
+        """A selector key's source: pod labels here are the k8s source's,
+        so `k8s:` and `any:` keys match them plainly (labels.ParseSelectLabel:
+        no source is `any`); `reserved:` and other sources stay."""
+        for src in ("k8s:", "any:"):
+            if k.startswith(src):
+                return k[len(src):]
+        return k
+
+    @staticmethod
     def parse(obj) -> "Selector":
         ml = (obj or {}).get("matchLabels", {}) or {}
         exprs, invalid = [], False
@@ -110,8 +120,8 @@ class Selector:
             op, vals = e.get("operator"), tuple(e.get("values") or ())
             if op not in _SEL_OPS or (op in ("In", "NotIn")) != bool(vals):
                 invalid = True
-            exprs.append((e.get("key", ""), op, frozenset(vals)))
-        return Selector(frozenset(f"{k}={v}" for k, v in ml.items()), (),
+            exprs.append((Selector._key(e.get("key", "")), op, frozenset(vals)))
+        return Selector(frozenset(f"{Selector._key(k)}={v}" for k, v in ml.items()), (),
                         tuple(sorted(exprs, key=lambda x: (x[0], str(x[1]), sorted(x[2])))),
                         invalid)
 

@@ -674,6 +674,10 @@ def test_label_selector_requirements():
                   {"key": "a", "operator": "Exists", "values": ["x"]}):
         s = R.Selector.parse({"matchExpressions": [inval]})
         assert not s.matches(lbls("a=x")) and not s.matches(lbls()) and not s.selects_all()
+    # source prefixes: k8s: / any: keys match the (k8s-sourced) pod labels
+    assert R.Selector.parse({"matchLabels": {"k8s:app": "x", "any:env": "p"}}) == \
+        R.Selector.parse({"matchLabels": {"app": "x", "env": "p"}})
+    assert R.Selector.parse({"matchLabels": {"reserved:host": ""}}).matches(lbls("reserved:host"))
     # a reserved:all key matches every label set, yet is no wildcard
     s = R.Selector.parse({"matchLabels": {"reserved:all": ""}})
     assert s.matches(lbls("foo")) and s.matches(lbls()) and not s.selects_all()
