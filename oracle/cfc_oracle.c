@@ -1411,10 +1411,10 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
  * (:1098-1110) — ipv4_to_ipv6 (nat46.h:236-328): saddr NAT46_PREFIX/96 +
  * the IPv4 source, daddr the endpoint's LXC_IP, ICMP as ICMPv6 — then
  * tail_ipv6_policy on the translated packet with the source identity of
- * the IPv4 path (cb[CB_SRC_LABEL]); its CT lookup is the stage after the
- * IPv4 one: 1 behind from-netdev, 2 (tl_ct3, struct hop ct2, has2 = 2)
- * behind an egress batch's local delivery (ipv4_local_delivery, l3.h:103-131,
- * whose ipv4_policy lookup is stage 1) */
+ * the IPv4 path (cb[CB_SRC_LABEL]); its CT lookup is stage 1 behind
+ * from-netdev, stage 2 (tl_ct3, struct hop ct2, has2 = 2) behind an IPv4
+ * egress batch's local delivery (ipv4_local_delivery, l3.h:103-131, whose
+ * ipv4_policy lookup is stage 1) */
 static res_t nat46_ingress(cfo_t *o, const epinfo *ep, uint32_t src, uint32_t sa4,
                            uint8_t proto, uint16_t sport, uint16_t dport, int close,
                            uint32_t len, int skip_proxy, int stage)
@@ -1481,8 +1481,11 @@ static res_t lxc_ingress(cfo_t *o, const epinfo *ep, uint32_t src, int alen,
     if (alen == 4 && tl_nat == NAT46 && o->ep_has6[ep->lxc_id]) {
         uint32_t sa4;
         memcpy(&sa4, sa, 4);
+        /* (stage 1 is an IPv4 egress batch's local delivery: the hop is a
+         * third stage; behind from-netdev, and behind a NAT64 hop's local
+         * delivery as before, it takes stage 1) */
         return nat46_ingress(o, ep, src, sa4, proto, sport, dport, close, len, skip_proxy,
-                             stage < 2 ? stage + 1 : 2);   /* (tl_mon[3]) */
+                             stage == 1 ? 2 : 1);
     }
     /* (:808-815) any hit whose entry carries a rev_nat_index: the packet's
      * source from cilium_lb6_reverse_nat, when it holds the index */
