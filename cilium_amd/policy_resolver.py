@@ -25,6 +25,9 @@ Restated (file:line in /root/reference):
   * the CIDR policy and its prefix-length       pkg/policy/rule.go:279-345,
     counts (class masks for bare addresses)     l3.go:66-96, repository.go:340-353
 
+  * rule management: Add (sanitized),          pkg/policy/repository.go:
+    SearchRLocked, DeleteByLabels,              495-586
+    ContainsAllRLocked, the revision
   * endpoint selectors: matchLabels and        pkg/policy/api/selector.go:
     matchExpressions (In, NotIn, Exists,        162-175, 277-300
     DoesNotExist); unconvertible ones match
@@ -221,6 +224,13 @@ class Rule:
     ingress: list = field(default_factory=list)
     egress: list = field(default_factory=list)
     name: str = ""
+    labels: frozenset = frozenset()   # the rule's LabelArray: (source, key, value)
+
+
+def rule_labels(r: dict) -> frozenset:
+    """api.Rule.Labels as a set of (source, key, value)."""
+    return frozenset((x.get("source", ""), x.get("key", ""), x.get("value", ""))
+                     for x in r.get("labels", []) or [])
 
 
 def parse_rules(objs, origin="", sanitize=True) -> list:
@@ -233,7 +243,7 @@ def parse_rules(objs, origin="", sanitize=True) -> list:
         name = ",".join(f"{x['key']}={x['value']}" for x in r.get("labels", []))
         rules.append(Rule(Selector.parse(r.get("endpointSelector")),
                           r.get("ingress", []) or [], r.get("egress", []) or [],
-                          name or origin))
+                          name or origin, rule_labels(r)))
     return rules
 
 
@@ -562,6 +572,37 @@ class Repository:
         self.rules = list(rules)
         self.always_allow_localhost = always_allow_localhost
         self.host_allows_world = host_allows_world
+        self.revision = 1   # NewPolicyRepository (repository.go)
+
+    # ---- the repository's rule management (repository.go:495-586)
+    def add(self, r: dict) -> int:
+        """Add: Rule.Sanitize, then AddListLocked -> the new revision;
+        PolicyError (the revision unchanged) for a refused rule."""
+        self.rules += parse_rules([r])
+        self.revision += 1
+        return self.revision
+
+    def search(self, lbls) -> list:
+        """SearchRLocked: the rules whose labels contain all of `lbls`."""
+        need = frozenset(lbls)
+        return [r for r in self.rules if need <= r.labels]
+
+    def delete_by_labels(self, lbls) -> tuple:
+        """DeleteByLabelsLocked -> (revision, deleted): the revision moves
+        only when a rule went."""
+        need = frozenset(lbls)
+        keep = [r for r in self.rules if not need <= r.labels]
+        n = len(self.rules) - len(keep)
+        if n:
+            self.rules = keep
+            self.revision += 1
+        return self.revision, n
+
+    def contains_all(self, needed) -> bool:
+        """ContainsAllRLocked: every label array of `needed` holds all the
+        labels of some rule that has labels."""
+        return all(any(r.labels and r.labels <= frozenset(n) for r in self.rules)
+                   for n in needed)
 
     def cidrs(self) -> list:
         """Every CIDR the rules name (the prefixes the agent allocates CIDR

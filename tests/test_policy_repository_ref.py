@@ -689,3 +689,56 @@ def test_label_selector_requirements():
     assert ingress_allowed(rp, lbls("role=web"), lbls("role=db")) is True
     assert ingress_allowed(rp, lbls("role=public"), lbls("role=cache")) is False
     assert ingress_allowed(rp, lbls("role=web"), lbls("role=web")) is None   # not selected
+
+
+def _L(*kv, src="unspec"):
+    return [{"source": src, "key": k, "value": v} for k, v in kv]
+
+
+def _T(*kv, src="unspec"):
+    return {(src, k, v) for k, v in kv}
+
+
+def test_add_search_delete():
+    # repository_test.go:29-112
+    rp = R.Repository([])
+    with pytest.raises(R.PolicyError):
+        rp.add({})                      # cannot add an empty rule
+    assert rp.revision == 1
+    l1, l2 = _L(("tag1", ""), ("tag2", "")), _L(("tag3", ""), src="any")
+    r1 = {"endpointSelector": es("foo"), "labels": l1}
+    r2 = {"endpointSelector": es("bar"), "labels": l1}
+    r3 = {"endpointSelector": es("bar"), "labels": l2}
+    assert rp.add(r1) == 2 and rp.add(r2) == 3
+    assert rp.search(_T(("tag3", ""), src="any")) == []
+    assert rp.add(r3) == 4
+    got = rp.search(_T(("tag1", ""), ("tag2", "")))
+    assert [r.selector for r in got] == [sel("foo"), sel("bar")]
+    assert len(rp.search(_T(("tag3", ""), src="any"))) == 1
+    assert rp.delete_by_labels(_T(("tag1", ""), ("tag2", ""))) == (5, 2)
+    assert rp.delete_by_labels(_T(("tag1", ""), ("tag2", ""))) == (5, 0)
+    assert len(rp.search(_T(("tag3", ""), src="any"))) == 1
+    assert rp.delete_by_labels(_T(("tag3", ""), src="any")) == (6, 1)
+    assert rp.search(_T(("tag3", ""), src="any")) == []
+
+
+def test_contains_all():
+    # repository_test.go:114-191
+    a = [_T(("1", "1"), ("2", "2"), ("3", "3"), src="1"),
+         _T(("4", "4"), ("5", "5"), ("6", "6"), src="1"),
+         _T(("7", "7"), ("8", "8"), ("9", "9"), src="1")]
+    b = a[:2]
+
+    def mk(sel_key, lab):
+        return {"endpointSelector": es(sel_key),
+                "labels": [{"source": s_, "key": k, "value": v} for s_, k, v in sorted(lab)]}
+    rpa = R.Repository([])
+    for lab, k in zip(a, ("foo", "bar", "bar")):
+        rpa.add(mk(k, lab))
+    rpb = R.Repository([])
+    for lab, k in zip(b, ("foo", "bar")):
+        rpb.add(mk(k, lab))
+    rpe = R.Repository([])
+    rpe.add({"endpointSelector": es("bar")})
+    assert rpa.contains_all(b) and not rpb.contains_all(a)
+    assert rpa.contains_all([]) and rpe.contains_all([]) and not rpe.contains_all(a)
