@@ -512,6 +512,7 @@ class L4Filter:
     endpoints: list
     parser: str = ""
     l7: dict = field(default_factory=dict)
+    derived: list = field(default_factory=list)   # DerivedFromRules: rule labels
 
     def allows_all(self) -> bool:
         """AllowsAllAtL3 (l4.go:112-114)."""
@@ -551,7 +552,7 @@ class L4Filter:
                 ep["l7"] = (ep["l7"] or []) + [x for x in (nr["l7"] or [])
                                                 if x not in (ep["l7"] or [])]
 
-    def wildcard_l7(self, peers):
+    def wildcard_l7(self, peers, rlabels=frozenset()):
         """wildcardL3L4Rule's body (repository.go:127-164): the peers allowed
         at every L7 resource of the parser, and added to the filter."""
         for sel in peers:
@@ -562,6 +563,7 @@ class L4Filter:
             else:
                 self.l7[sel] = _l7_norm({"l7proto": self.parser, "l7": []})
         self.endpoints = self.endpoints + list(peers)
+        self.derived.append(rlabels)
 
 
 # ------------------------------------------------------------- repository
@@ -703,9 +705,11 @@ class Repository:
                         pn = parse_l4_proto(p.get("protocol"))
                         for proto in (("TCP", "UDP") if pn == "ANY" else (pn,)):
                             f = self._create_filter(peers, pr, port, proto, ingress)
+                            f.derived = [r.labels]
                             k = (port, PROTO[proto])
                             if k in res:
                                 res[k].merge(f, peers)
+                                res[k].derived.append(r.labels)
                             else:
                                 res[k] = f
         if wildcard_l3l4 and any(f.parser for f in res.values()):
@@ -726,7 +730,7 @@ class Repository:
                     for proto, port in targets:
                         for (fp, fpr), f in res.items():
                             if PROTO.get(proto) == fpr and (port == 0 or port == fp) and f.parser:
-                                f.wildcard_l7(peers)
+                                f.wildcard_l7(peers, r.labels)
         return res
 
     def _create_filter(self, peers, pr, port, proto, ingress) -> "L4Filter":

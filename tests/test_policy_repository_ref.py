@@ -548,6 +548,7 @@ def test_l4filter_allow_all_l3_and_shadowed_l7():
     k, f = _one(_fr(_ir([WILD]), _ir([WILD], GET)))
     assert f.allows_all() and f.parser == "http"
     assert f.l7 == {W: _l7(http=[{"method": "GET", "path": "/"}])}
+    assert f.derived == [frozenset(), frozenset()]   # (DerivedFromRules {nil, nil})
     k, f = _one(_fr(_ir([WILD], GET), _ir([WILD])), wildcard=True)
     assert f.allows_all() and f.parser == "http" and len(f.l7) == 1
 
@@ -742,3 +743,28 @@ def test_contains_all():
     rpe.add({"endpointSelector": es("bar")})
     assert rpa.contains_all(b) and not rpb.contains_all(a)
     assert rpa.contains_all([]) and rpe.contains_all([]) and not rpe.contains_all(a)
+
+
+def test_l4_rule_labels():
+    # rule_test.go:1322-1436: each filter's DerivedFromRules lists the labels
+    # of the rules it came from; a rule without ports adds none
+    def rule(name, ing=None, eg=None):
+        r = {"endpointSelector": es("bar"), "labels": _L(("name", name))}
+        if ing:
+            r["ingress"] = [{"toPorts": tcp(ing)}]
+        if eg:
+            r["egress"] = [{"toPorts": tcp(eg)}]
+        return r
+    rules = {"rule0": rule("apiRule0"), "rule1": rule("apiRule1", 1010, 1100),
+             "rule2": rule("apiRule2", 1020, 1200)}
+    lab = {k: frozenset(_T(("name", "apiRule" + k[-1]))) for k in rules}
+    for apply, want_in, want_eg in (
+            (["rule0"], {}, {}),
+            (["rule1"], {1010: ["rule1"]}, {1100: ["rule1"]}),
+            (["rule0", "rule1", "rule2"], {1010: ["rule1"], 1020: ["rule2"]},
+             {1100: ["rule1"], 1200: ["rule2"]})):
+        rp = R.Repository(R.parse_rules([rules[k] for k in apply]))
+        for ingress, want in ((True, want_in), (False, want_eg)):
+            fs = rp.l4_filters(lbls("bar"), ingress, wildcard_l3l4=False)
+            assert {k[0]: [x for x in f.derived] for k, f in fs.items()} == \
+                {p: [lab[n] for n in ns] for p, ns in want.items()}
