@@ -624,10 +624,11 @@ class Repository:
         rules (CIDR + L4 is mergeL4Ingress's), egress every rule — with the
         per-family prefix-length counts that size the datapath's prefix
         list: {"ingress"|"egress": {"map": {key: (family, length)},
-        "v4": {length: n}, "v6": {length: n}}}."""
+        "v4": {length: n}, "v6": {length: n}, "derived": {key: [the labels
+        of each rule that named it]}}}."""
         out = {}
         for d, ingress in (("ingress", True), ("egress", False)):
-            m, cnt = {}, {4: {}, 6: {}}
+            m, cnt, derived = {}, {4: {}, 6: {}}, {}
             for r in self.rules:
                 if not r.selector.matches(subject):
                     continue
@@ -640,7 +641,8 @@ class Repository:
                         if key not in m:
                             m[key] = (fam, ln)
                             cnt[fam][ln] = cnt[fam].get(ln, 0) + 1
-            out[d] = {"map": m, "v4": cnt[4], "v6": cnt[6]}
+                        derived.setdefault(key, []).append(r.labels)   # (DerivedFromRules)
+            out[d] = {"map": m, "v4": cnt[4], "v6": cnt[6], "derived": derived}
         return out
 
     def enabled(self, lbls):

@@ -768,3 +768,25 @@ def test_l4_rule_labels():
             fs = rp.l4_filters(lbls("bar"), ingress, wildcard_l3l4=False)
             assert {k[0]: [x for x in f.derived] for k, f in fs.items()} == \
                 {p: [lab[n] for n in ns] for p, ns in want.items()}
+
+
+def test_l3_rule_labels():
+    # rule_test.go:1218-1320: each CIDR prefix's DerivedFromRules
+    def rule(name, i=None, e=None):
+        r = {"endpointSelector": es("bar"), "labels": _L(("name", name))}
+        if i:
+            r["ingress"] = [{"fromCIDR": [i]}]
+        if e:
+            r["egress"] = [{"toCIDR": [e]}]
+        return r
+    rules = {"rule0": rule("apiRule0"), "rule1": rule("apiRule1", "10.0.1.0/32", "10.1.0.0/32"),
+             "rule2": rule("apiRule2", "10.0.2.0/32", "10.2.0.0/32")}
+    lab = {k: frozenset(_T(("name", "apiRule" + k[-1]))) for k in rules}
+    for apply, want_in, want_eg in (
+            (["rule0"], {}, {}),
+            (["rule1"], {"10.0.1.0/32": ["rule1"]}, {"10.1.0.0/32": ["rule1"]}),
+            (["rule0", "rule1", "rule2"], {"10.0.1.0/32": ["rule1"], "10.0.2.0/32": ["rule2"]},
+             {"10.1.0.0/32": ["rule1"], "10.2.0.0/32": ["rule2"]})):
+        cp = R.Repository(R.parse_rules([rules[k] for k in apply])).cidr_policy(lbls("bar"))
+        for d, want in (("ingress", want_in), ("egress", want_eg)):
+            assert cp[d]["derived"] == {p: [lab[n] for n in ns] for p, ns in want.items()}
